@@ -1,0 +1,139 @@
+"""In-tree build of the native libraries (gfx950 only).
+
+``build()`` compiles
+
+* ``csrc/*.hip``  with ``hipcc --offload-arch=gfx950`` (pure HIP, no torch headers),
+* ``csrc/binding.cpp`` with ``g++`` against the installed PyTorch-ROCm headers,
+
+and links them into ``wellflow/_C.so`` (a pybind11 module).  It also builds the native
+runtime library ``wellflow/_runtime.so`` (C++ CSV reader / window batcher / prefetcher,
+``csrc/runtime/*.cpp``, ctypes ABI) when its sources exist.
+
+Builds are incremental (mtime-based) and parallel; the artefacts live inside the package
+so they travel with the repository snapshot to the GPU box (a JIT cache under ~/.cache
+would not).  There is no hipify step, no CUDA path and no fallback: on a GPU box the ops
+import ``_C`` and fail loudly if it is missing.
+"""
+from __future__ import annotations
+
+import concurrent.futures as cf
+import glob
+import os
+import subprocess
+import sys
+import sysconfig
+
+PKG_DIR = os.path.dirname(os.path.abspath(__file__))
+CSRC = os.path.join(PKG_DIR, "csrc")
+BUILD_DIR = os.path.join(PKG_DIR, "build")
+EXT_PATH = os.path.join(PKG_DIR, "_C.so")
+RUNTIME_PATH = os.path.join(PKG_DIR, "_runtime.so")
+ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
+ARCH = "gfx950"
+
+HIPCC_FLAGS = [
+    f"--offload-arch={ARCH}",
+    "-O3",
+    "-std=c++17",
+    "-fPIC",
+    "-munsafe-fp-atomics",  # float atomicAdd -> global_atomic_add_f32 (no CAS loop)
+    "-Wno-unused-result",
+]
+
+
+def _torch_flags():
+    import torch
+    from torch.utils import cpp_extension as ce
+
+    inc = ce.include_paths("cuda")
+    flags = [f"-I{p}" for p in inc]
+    flags += [
+        "-D__HIP_PLATFORM_AMD__=1",
+        "-DUSE_ROCM=1",
+        "-DTORCH_EXTENSION_NAME=_C",
+        "-DTORCH_API_INCLUDE_EXTENSION_H",
+        f"-D_GLIBCXX_USE_CXX11_ABI={int(torch.compiled_with_cxx11_abi())}",
+        f"-I{sysconfig.get_paths()['include']}",
+    ]
+    except Exception:  # pragma: no cover - older torch
+        pass
+    libdir = os.path.join(os.path.dirname(torch.__file__), "lib")
+    ldflags = [
+        f"-L{libdir}",
+        "-lc10",
+        "-ltorch",
+        "-ltorch_cpu",
+        "-ltorch_python",
+        "-lc10_hip",
+        "-ltorch_hip",
+        "-lamdhip64",  # torch's bundled HIP runtime (same soname as /opt/rocm's)
+        f"-Wl,-rpath,{libdir}",
+    ]
+    return flags, ldflags
+
+
+def _stale(target: str, deps) -> bool:
+    if not os.path.exists(target):
+        return True
+    t = os.path.getmtime(target)
+    return any(os.path.getmtime(d) > t for d in deps)
+
+
+def _run(cmd, verbose):
+    if verbose:
+        print(" ".join(cmd), flush=True)
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"build failed: {' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
+    return r
+
+
+def build(verbose: bool = False, jobs: int | None = None) -> str:
+    """Compile every HIP source for gfx950 and link ``_C.so``; returns its path."""
+    os.makedirs(BUILD_DIR, exist_ok=True)
+    headers = glob.glob(os.path.join(CSRC, "*.h"))
+    hip_srcs = sorted(glob.glob(os.path.join(CSRC, "*.hip")))
+    tflags, ldflags = _torch_flags()
+    hipcc = os.path.join(ROCM, "bin", "hipcc")
+    jobs = jobs or min(8, os.cpu_count() or 4)
+
+    tasks = []
+    objs = []
+    for src in hip_srcs:
+        obj = os.path.join(BUILD_DIR, os.path.basename(src) + ".o")
+        objs.append(obj)
+        if _stale(obj, [src] + headers):
+            tasks.append([hipcc, *HIPCC_FLAGS, f"-I{CSRC}", "-c", src, "-o", obj])
+    bsrc = os.path.join(CSRC, "binding.cpp")
+    bobj = os.path.join(BUILD_DIR, "binding.cpp.o")
+    objs.append(bobj)
+    if _stale(bobj, [bsrc] + headers):
+        tasks.append(["g++", "-O2", "-std=c++17", "-fPIC", f"-I{CSRC}", *tflags, "-c", bsrc, "-o", bobj])
+
+    with cf.ThreadPoolExecutor(max_workers=jobs) as ex:
+        for f in [ex.submit(_run, t, verbose) for t in tasks]:
+            f.result()
+
+    if _stale(EXT_PATH, objs):
+        tmp = EXT_PATH + ".tmp"
+        _run(["g++", "-shared", "-o", tmp, *objs, *ldflags], verbose)
+        os.replace(tmp, EXT_PATH)
+    build_runtime(verbose)
+    return EXT_PATH
+
+
+def build_runtime(verbose: bool = False) -> str | None:
+    """Native host runtime (C++17, no GPU code): CSV parsing, windowing, prefetch."""
+    srcs = sorted(glob.glob(os.path.join(CSRC, "runtime", "*.cpp")))
+    if not srcs:
+        return None
+    hdrs = glob.glob(os.path.join(CSRC, "runtime", "*.h"))
+    if _stale(RUNTIME_PATH, srcs + hdrs):
+        tmp = RUNTIME_PATH + ".tmp"
+        _run(["g++", "-O3", "-std=c++17", "-fPIC", "-shared", "-pthread", *srcs, "-o", tmp], verbose)
+        os.replace(tmp, RUNTIME_PATH)
+    return RUNTIME_PATH
+
+
+if __name__ == "__main__":
+    print(build(verbose="-v" in sys.argv))

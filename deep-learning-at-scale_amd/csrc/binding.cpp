@@ -1,0 +1,316 @@
+// wellflow — Python bindings for the HIP kernel library (pybind11 via torch/extension.h).
+//
+// Every entry point validates device, dtype, contiguity, alignment and the extents the
+// kernel and its grid will touch BEFORE launching: a hand-written kernel indexing out of
+// bounds can take the whole GPU node down, so shape errors must be caught on the host.
+#include <torch/extension.h>
+#include <ATen/hip/impl/HIPStreamMasqueradingAsCUDA.h>
+#include <ATen/hip/impl/HIPGuardImplMasqueradingAsCUDA.h>
+
+#include "kernels.h"
+
+namespace {
+
+using wf::bf16_t;
+
+hipStream_t cur_stream() { return c10::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream(); }
+
+void check_t(const at::Tensor& t, at::ScalarType dt, const char* name) {
+  TORCH_CHECK(t.defined(), name, ": undefined tensor");
+  TORCH_CHECK(t.is_cuda(), name, ": must be a GPU tensor");
+  TORCH_CHECK(t.scalar_type() == dt, name, ": expected dtype ", dt, " got ", t.scalar_type());
+  TORCH_CHECK(t.is_contiguous(), name, ": must be contiguous");
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(t.data_ptr()) % 16 == 0, name,
+              ": data pointer must be 16-byte aligned");
+}
+
+void check_extent(const at::Tensor& t, int64_t need, const char* name) {
+  TORCH_CHECK(t.numel() >= need, name, ": needs at least ", need, " elements, has ", t.numel());
+}
+
+bf16_t* bfp(const at::Tensor& t) { return reinterpret_cast<bf16_t*>(t.data_ptr()); }
+float* fp(const at::Tensor& t) { return t.data_ptr<float>(); }
+
+template <class T>
+T* opt_ptr(const c10::optional<at::Tensor>& t, at::ScalarType dt, const char* name,
+           int64_t need) {
+  if (!t.has_value() || !t->defined()) return nullptr;
+  check_t(*t, dt, name);
+  check_extent(*t, need, name);
+  return reinterpret_cast<T*>(t->data_ptr());
+}
+
+// Extent of a logical [rows][K] operand stored K-contiguous or MN-contiguous.
+int64_t operand_extent(bool mn, int64_t rows, int64_t K, int64_t ld) {
+  if (rows == 0 || K == 0) return 0;
+  return mn ? (K - 1) * ld + rows : (rows - 1) * ld + K;
+}
+
+void gemm(const at::Tensor& A, bool a_mn, int64_t lda, const at::Tensor& B, bool b_mn, int64_t ldb,
+          int64_t M, int64_t N, int64_t K, int64_t ksplit, c10::optional<at::Tensor> outF,
+          c10::optional<at::Tensor> outH, int64_t ldo, c10::optional<at::Tensor> bias,
+          c10::optional<at::Tensor> mask, int64_t ldm, double mask_scale,
+          c10::optional<at::Tensor> colsum, double alpha, double beta, int64_t act, bool atomic,
+          double drop_p, int64_t seed) {
+  check_t(A, at::kBFloat16, "A");
+  check_t(B, at::kBFloat16, "B");
+  TORCH_CHECK(M > 0 && N > 0 && K > 0, "gemm: empty problem");
+  TORCH_CHECK(lda % 8 == 0 && ldb % 8 == 0, "gemm: lda/ldb must be multiples of 8");
+  TORCH_CHECK(a_mn ? (M % 8 == 0) : (K % 8 == 0), "gemm: A contiguous extent must be a multiple of 8");
+  TORCH_CHECK(b_mn ? (N % 8 == 0) : (K % 8 == 0), "gemm: B contiguous extent must be a multiple of 8");
+  TORCH_CHECK(a_mn ? lda >= M : lda >= K, "gemm: lda too small");
+  TORCH_CHECK(b_mn ? ldb >= N : ldb >= K, "gemm: ldb too small");
+  check_extent(A, operand_extent(a_mn, M, K, lda), "A");
+  check_extent(B, operand_extent(b_mn, N, K, ldb), "B");
+  TORCH_CHECK(ldo >= N, "gemm: ldo < N");
+  const int64_t out_need = (M - 1) * ldo + N;
+  wf::GemmEpilogue e;
+  e.outF = opt_ptr<float>(outF, at::kFloat, "outF", out_need);
+  e.outH = opt_ptr<bf16_t>(outH, at::kBFloat16, "outH", out_need);
+  TORCH_CHECK(e.outF || e.outH, "gemm: need an output");
+  TORCH_CHECK(!atomic || (e.outF && !e.outH && beta == 0.0), "gemm: atomic needs outF only, beta 0");
+  TORCH_CHECK(beta == 0.0 || e.outF, "gemm: beta needs outF");
+  e.ldo = ldo;
+  e.bias = opt_ptr<float>(bias, at::kFloat, "bias", N);
+  if (mask.has_value() && mask->defined()) TORCH_CHECK(ldm >= N, "gemm: ldm < N");
+  e.mask = opt_ptr<bf16_t>(mask, at::kBFloat16, "mask", (M - 1) * ldm + N);
+  e.ldm = ldm;
+  e.mask_scale = (float)mask_scale;
+  e.colsum = opt_ptr<float>(colsum, at::kFloat, "colsum", N);
+  e.alpha = (float)alpha;
+  e.beta = (float)beta;
+  e.act = (int)act;
+  e.atomic = atomic ? 1 : 0;
+  e.drop_p = (float)drop_p;
+  e.seed = (unsigned long long)seed;
+  TORCH_CHECK(ksplit == 1 || atomic, "gemm: split-K needs atomic accumulation");
+  const c10::hip::OptionalHIPGuardMasqueradingAsCUDA guard(A.device());
+  wf::launch_gemm(bfp(A), lda, a_mn, bfp(B), ldb, b_mn, (int)M, (int)N, (int)K, (int)ksplit, e,
+                  cur_stream());
+}
+
+wf::LstmDims lstm_dims(int64_t B, int64_t T, int64_t F, int64_t KX, int64_t H) {
+  TORCH_CHECK(B > 0 && T > 0 && H > 0, "lstm: bad dims");
+  TORCH_CHECK(H % 128 == 0, "lstm: hidden size must be a multiple of 128");
+  TORCH_CHECK(KX % 64 == 0 && F + 1 <= KX, "lstm: KX must be a multiple of 64 and > F");
+  return wf::LstmDims{(int)B, (int)T, (int)F, (int)KX, (int)H};
+}
+
+void check_lstm_state(const at::Tensor& XH, const at::Tensor& Cst, const at::Tensor& S,
+                      const wf::LstmDims& d) {
+  const int64_t KA = d.KX + d.H, G = 4 * d.H;
+  check_t(XH, at::kBFloat16, "XH");
+  check_t(Cst, at::kFloat, "Cst");
+  check_t(S, at::kBFloat16, "S");
+  check_extent(XH, (int64_t)(d.T + 1) * d.B * KA, "XH");
+  check_extent(Cst, (int64_t)(d.T + 1) * d.B * d.H, "Cst");
+  check_extent(S, (int64_t)d.T * d.B * G, "S");
+}
+
+void lstm_pack_x(const at::Tensor& x, const at::Tensor& XH, int64_t B, int64_t T, int64_t F,
+                 int64_t KX, int64_t H) {
+  auto d = lstm_dims(B, T, F, KX, H);
+  check_t(x, at::kFloat, "x");
+  check_extent(x, B * T * F, "x");
+  check_t(XH, at::kBFloat16, "XH");
+  check_extent(XH, (T + 1) * B * (KX + H), "XH");
+  const c10::hip::OptionalHIPGuardMasqueradingAsCUDA guard(x.device());
+  wf::launch_lstm_pack_x(fp(x), bfp(XH), d, cur_stream());
+}
+
+void lstm_forward(const at::Tensor& XH, const at::Tensor& Wp, const at::Tensor& Cst,
+                  const at::Tensor& S, int64_t B, int64_t T, int64_t F, int64_t KX, int64_t H) {
+  auto d = lstm_dims(B, T, F, KX, H);
+  check_lstm_state(XH, Cst, S, d);
+  check_t(Wp, at::kBFloat16, "Wp");
+  check_extent(Wp, 4 * H * (KX + H), "Wp");
+  const c10::hip::OptionalHIPGuardMasqueradingAsCUDA guard(XH.device());
+  auto s = cur_stream();
+  for (int t = 0; t < d.T; ++t) wf::launch_lstm_fwd_step(t, bfp(XH), bfp(Wp), fp(Cst), bfp(S), d, s);
+}
+
+void lstm_backward(const at::Tensor& WhhT, const at::Tensor& XH, const at::Tensor& Cst,
+                   const at::Tensor& S, const at::Tensor& DG, const at::Tensor& dcarry,
+                   const at::Tensor& dy, const at::Tensor& w_out, int64_t B, int64_t T, int64_t F,
+                   int64_t KX, int64_t H) {
+  auto d = lstm_dims(B, T, F, KX, H);
+  check_lstm_state(XH, Cst, S, d);
+  check_t(WhhT, at::kBFloat16, "WhhT");
+  check_extent(WhhT, H * 4 * H, "WhhT");
+  check_t(DG, at::kBFloat16, "DG");
+  check_extent(DG, T * B * 4 * H, "DG");
+  check_t(dcarry, at::kFloat, "dcarry");
+  check_extent(dcarry, B * H, "dcarry");
+  check_t(dy, at::kFloat, "dy");
+  check_extent(dy, B, "dy");
+  check_t(w_out, at::kFloat, "w_out");
+  check_extent(w_out, H, "w_out");
+  const c10::hip::OptionalHIPGuardMasqueradingAsCUDA guard(XH.device());
+  auto s = cur_stream();
+  for (int t = d.T - 1; t >= 0; --t)
+    wf::launch_lstm_bwd_step(t, bfp(WhhT), fp(Cst), bfp(S), bfp(DG), fp(dcarry), fp(dy),
+                             fp(w_out), d, s);
+}
+
+void lstm_pack_weights(const at::Tensor& W, const at::Tensor& Wp, const at::Tensor& WhhT,
+                       int64_t H, int64_t KX) {
+  auto d = lstm_dims(1, 1, 0, KX, H);
+  check_t(W, at::kFloat, "W");
+  check_t(Wp, at::kBFloat16, "Wp");
+  check_t(WhhT, at::kBFloat16, "WhhT");
+  check_extent(W, 4 * H * (KX + H), "W");
+  check_extent(Wp, 4 * H * (KX + H), "Wp");
+  check_extent(WhhT, H * 4 * H, "WhhT");
+  const c10::hip::OptionalHIPGuardMasqueradingAsCUDA guard(W.device());
+  wf::launch_lstm_pack_weights(fp(W), bfp(Wp), bfp(WhhT), d, cur_stream());
+}
+
+// Regression-head input H may be a strided view of a larger bf16 buffer (e.g. the last
+// timestep of XH): the raw pointer is taken from the given tensor (its storage offset).
+void check_head_h(const at::Tensor& Hm, int64_t ldh, int64_t B, int64_t Hd) {
+  TORCH_CHECK(Hm.is_cuda() && Hm.scalar_type() == at::kBFloat16, "H: bf16 GPU tensor");
+  TORCH_CHECK(ldh >= Hd, "head: ldh < Hd");
+  TORCH_CHECK(Hm.storage().nbytes() - Hm.storage_offset() * 2 >= (size_t)(((B - 1) * ldh + Hd) * 2),
+              "head: H too small");
+}
+
+void head_fwd(const at::Tensor& Hm, int64_t ldh, int64_t B, int64_t Hd, const at::Tensor& w,
+              const at::Tensor& b0, c10::optional<at::Tensor> target, const at::Tensor& pred,
+              c10::optional<at::Tensor> dy, c10::optional<at::Tensor> loss_sum, double dy_scale) {
+  check_head_h(Hm, ldh, B, Hd);
+  TORCH_CHECK(Hd % 8 == 0 && ldh % 8 == 0, "head: Hd and ldh must be multiples of 8");
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(Hm.data_ptr()) % 16 == 0, "head: H must be 16-B aligned");
+  check_t(w, at::kFloat, "w");
+  check_extent(w, Hd, "w");
+  check_t(b0, at::kFloat, "b0");
+  check_t(pred, at::kFloat, "pred");
+  check_extent(pred, B, "pred");
+  const c10::hip::OptionalHIPGuardMasqueradingAsCUDA guard(Hm.device());
+  wf::launch_head_fwd(bfp(Hm), ldh, (int)B, (int)Hd, fp(w), fp(b0),
+                      opt_ptr<float>(target, at::kFloat, "target", B), fp(pred),
+                      opt_ptr<float>(dy, at::kFloat, "dy", B),
+                      opt_ptr<float>(loss_sum, at::kFloat, "loss_sum", 1), (float)dy_scale,
+                      cur_stream());
+}
+
+void head_bwd_w(const at::Tensor& Hm, int64_t ldh, int64_t B, int64_t Hd, const at::Tensor& dy,
+                const at::Tensor& dw, c10::optional<at::Tensor> db) {
+  check_head_h(Hm, ldh, B, Hd);
+  check_t(dy, at::kFloat, "dy");
+  check_extent(dy, B, "dy");
+  check_t(dw, at::kFloat, "dw");
+  check_extent(dw, Hd, "dw");
+  const c10::hip::OptionalHIPGuardMasqueradingAsCUDA guard(Hm.device());
+  wf::launch_head_bwd_w(bfp(Hm), ldh, (int)B, (int)Hd, fp(dy), fp(dw),
+                        opt_ptr<float>(db, at::kFloat, "db", 1), cur_stream());
+}
+
+void head_bwd_x(const at::Tensor& Hm, int64_t ldh, int64_t B, int64_t Hd, const at::Tensor& dy,
+                const at::Tensor& w, bool relu_mask, const at::Tensor& dz, int64_t ldz,
+                c10::optional<at::Tensor> colsum) {
+  check_head_h(Hm, ldh, B, Hd);
+  check_t(dy, at::kFloat, "dy");
+  check_extent(dy, B, "dy");
+  check_t(w, at::kFloat, "w");
+  check_extent(w, Hd, "w");
+  check_t(dz, at::kBFloat16, "dz");
+  check_extent(dz, (B - 1) * ldz + Hd, "dz");
+  const c10::hip::OptionalHIPGuardMasqueradingAsCUDA guard(Hm.device());
+  wf::launch_head_bwd_x(bfp(Hm), ldh, (int)B, (int)Hd, fp(dy), fp(w), relu_mask ? 1 : 0, bfp(dz),
+                        ldz, opt_ptr<float>(colsum, at::kFloat, "colsum", Hd), cur_stream());
+}
+
+void loss(int64_t kind, const at::Tensor& pred, const at::Tensor& y, int64_t B, int64_t O,
+          double clip, double scale, c10::optional<at::Tensor> loss_sum,
+          c10::optional<at::Tensor> dpred, c10::optional<at::Tensor> colsum) {
+  TORCH_CHECK(kind == 0 || kind == 1, "loss: kind 0 (mse) or 1 (mae_clip)");
+  check_t(pred, at::kFloat, "pred");
+  check_t(y, at::kFloat, "y");
+  check_extent(pred, B * O, "pred");
+  check_extent(y, B * O, "y");
+  const c10::hip::OptionalHIPGuardMasqueradingAsCUDA guard(pred.device());
+  wf::launch_loss((int)kind, fp(pred), fp(y), (int)B, (int)O, (float)clip, (float)scale,
+                  opt_ptr<float>(loss_sum, at::kFloat, "loss_sum", 1),
+                  opt_ptr<bf16_t>(dpred, at::kBFloat16, "dpred", B * O),
+                  opt_ptr<float>(colsum, at::kFloat, "colsum", O), cur_stream());
+}
+
+void adam(const at::Tensor& p, const at::Tensor& g, const at::Tensor& m, const at::Tensor& v,
+          double lr, double b1, double b2, double eps, double wd, double bc1, double bc2,
+          double gscale) {
+  check_t(p, at::kFloat, "p");
+  check_t(g, at::kFloat, "g");
+  check_t(m, at::kFloat, "m");
+  check_t(v, at::kFloat, "v");
+  const int64_t n = p.numel();
+  TORCH_CHECK(g.numel() == n && m.numel() == n && v.numel() == n, "adam: size mismatch");
+  const c10::hip::OptionalHIPGuardMasqueradingAsCUDA guard(p.device());
+  wf::launch_adam(fp(p), fp(g), fp(m), fp(v), n, (float)lr, (float)b1, (float)b2, (float)eps,
+                  (float)wd, (float)bc1, (float)bc2, (float)gscale, cur_stream());
+}
+
+void sgd(const at::Tensor& p, const at::Tensor& g, const at::Tensor& vel, double lr,
+         double momentum, bool nesterov, double gscale) {
+  check_t(p, at::kFloat, "p");
+  check_t(g, at::kFloat, "g");
+  check_t(vel, at::kFloat, "vel");
+  const int64_t n = p.numel();
+  TORCH_CHECK(g.numel() == n && vel.numel() == n, "sgd: size mismatch");
+  const c10::hip::OptionalHIPGuardMasqueradingAsCUDA guard(p.device());
+  wf::launch_sgd(fp(p), fp(g), fp(vel), n, (float)lr, (float)momentum, nesterov ? 1 : 0,
+                 (float)gscale, cur_stream());
+}
+
+void cast_bf16(const at::Tensor& src, const at::Tensor& dst) {
+  check_t(src, at::kFloat, "src");
+  check_t(dst, at::kBFloat16, "dst");
+  TORCH_CHECK(dst.numel() >= src.numel(), "cast: dst too small");
+  const c10::hip::OptionalHIPGuardMasqueradingAsCUDA guard(src.device());
+  wf::launch_cast_bf16(fp(src), bfp(dst), src.numel(), cur_stream());
+}
+
+void transpose_cast_bf16(const at::Tensor& src, int64_t lds, int64_t rows, int64_t cols,
+                         const at::Tensor& dst, int64_t ldd) {
+  TORCH_CHECK(src.is_cuda() && src.scalar_type() == at::kFloat, "src: fp32 GPU tensor");
+  check_t(dst, at::kBFloat16, "dst");
+  TORCH_CHECK(lds >= cols && ldd >= rows, "transpose_cast: bad leading dims");
+  TORCH_CHECK(src.storage().nbytes() - src.storage_offset() * 4 >= (size_t)(((rows - 1) * lds + cols) * 4),
+              "transpose_cast: src too small");
+  check_extent(dst, (cols - 1) * ldd + rows, "dst");
+  const c10::hip::OptionalHIPGuardMasqueradingAsCUDA guard(src.device());
+  wf::launch_transpose_cast_bf16(src.data_ptr<float>(), lds, (int)rows, (int)cols, bfp(dst), ldd,
+                                 cur_stream());
+}
+
+void im2col1d(const at::Tensor& x, int64_t B, int64_t L, int64_t Cin, int64_t ksz, int64_t Kp,
+              const at::Tensor& col) {
+  check_t(x, at::kFloat, "x");
+  check_t(col, at::kBFloat16, "col");
+  const int64_t Lout = L - ksz + 1;
+  TORCH_CHECK(Lout > 0 && Kp >= ksz * Cin + 1, "im2col1d: bad shape");
+  check_extent(x, B * L * Cin, "x");
+  check_extent(col, B * Lout * Kp, "col");
+  const c10::hip::OptionalHIPGuardMasqueradingAsCUDA guard(x.device());
+  wf::launch_im2col1d(fp(x), (int)B, (int)L, (int)Cin, (int)ksz, (int)Lout, (int)Kp, bfp(col),
+                      cur_stream());
+}
+
+}  // namespace
+
+PYBIND11_MODULE(_C, m) {
+  m.doc() = "wellflow HIP kernel library (gfx950)";
+  m.def("gemm", &gemm);
+  m.def("lstm_pack_x", &lstm_pack_x);
+  m.def("lstm_forward", &lstm_forward);
+  m.def("lstm_backward", &lstm_backward);
+  m.def("lstm_pack_weights", &lstm_pack_weights);
+  m.def("head_fwd", &head_fwd);
+  m.def("head_bwd_w", &head_bwd_w);
+  m.def("head_bwd_x", &head_bwd_x);
+  m.def("loss", &loss);
+  m.def("adam", &adam);
+  m.def("sgd", &sgd);
+  m.def("cast_bf16", &cast_bf16);
+  m.def("transpose_cast_bf16", &transpose_cast_bf16);
+  m.def("im2col1d", &im2col1d);
+}

@@ -1,0 +1,84 @@
+// wellflow native kernel library — shared device helpers (gfx950 / CDNA4 only).
+//
+// Storage conventions used by every kernel in this library:
+//   * bf16 tensors are raw 16-bit words (`bf16_t` = unsigned short); arithmetic is
+//     always done in fp32 and converted with the helpers below.
+//   * fp32 master weights / gradients / optimizer state live in flat buffers that
+//     the Python side views as parameters (wellflow/optim/flat.py).
+//   * wave64: every cross-lane idiom assumes 64 lanes (never 32).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <hip/hip_bf16.h>
+#include <stdint.h>
+
+namespace wf {
+
+typedef unsigned short bf16_t;
+typedef short bf16x8 __attribute__((ext_vector_type(8)));
+typedef short bf16x4 __attribute__((ext_vector_type(4)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int kWave = 64;
+
+__device__ __forceinline__ float bf2f(bf16_t x) {
+  return __uint_as_float(static_cast<unsigned>(x) << 16);
+}
+
+// Round-to-nearest-even; a plain cast lowers to v_cvt_pk_bf16_f32 on gfx950 which
+// keeps NaNs NaN (MI355X_MICROARCH.md, correctness boundaries).
+__device__ __forceinline__ bf16_t f2bf(float x) {
+  __hip_bfloat16 h = __float2bfloat16(x);
+  return *reinterpret_cast<bf16_t*>(&h);
+}
+
+__device__ __forceinline__ float sigmoidf_(float x) { return 1.0f / (1.0f + __expf(-x)); }
+
+__device__ __forceinline__ float tanhf_(float x) {
+  // tanh(x) = 1 - 2/(exp(2x)+1); saturates cleanly for |x| large.
+  float e = __expf(2.0f * x);
+  return 1.0f - 2.0f / (e + 1.0f);
+}
+
+// Counter-based uniform in [0,1) (splitmix64 finaliser). Dropout masks are regenerated
+// from (seed, flat index) in the backward pass instead of being stored; the same
+// function is mirrored in wellflow/ops/reference.py for CPU tests.
+__device__ __forceinline__ float uniform_hash(unsigned long long seed, unsigned long long idx) {
+  unsigned long long z = seed + idx * 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  z ^= z >> 31;
+  return (float)(z >> 40) * (1.0f / 16777216.0f);
+}
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+// Block-wide sum for blockDim.x == NT (multiple of 64). `red` must hold NT/64 floats.
+template <int NT>
+__device__ __forceinline__ float block_sum(float v, float* red) {
+  v = wave_sum(v);
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  if (lane == 0) red[wid] = v;
+  __syncthreads();
+  float s = 0.f;
+  if (threadIdx.x < NT / 64) s = red[threadIdx.x];
+  if (wid == 0) s = wave_sum(s);
+  __syncthreads();
+  return s;  // valid in wave 0 lanes
+}
+
+// Bijective XCD-aware remap of a linear workgroup id (cdna_hip_programming.md §5 "XCD
+// swizzle must be bijective"): blocks b, b+8, b+16... are dealt to the same XCD, so give
+// each XCD a contiguous run of logical tiles so neighbouring tiles share its L2.
+__device__ __forceinline__ int xcd_remap(int orig, int nwg) {
+  constexpr int NX = 8;
+  if (nwg < NX) return orig;
+  const int q = nwg / NX, r = nwg % NX;
+  const int x = orig % NX, i = orig / NX;
+  return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + i;
+}
+
+}  // namespace wf

@@ -1,0 +1,305 @@
+// wellflow — regression head, losses, fused optimizers, casts (gfx950).
+//
+// K6 (mae_clip fwd+bwd in one kernel), K8 (SGD-Nesterov with Keras-0.x
+// time decay, one launch over the flat buffer), K15 (regression head), K16 (MSE fwd+bwd,
+// wave64 shuffle reduction + one atomic per workgroup), K17 (fused Adam over the flat
+// fp32 master buffer, float4-vectorised), K18 (casts).
+#include "common.h"
+#include "kernels.h"
+
+namespace wf {
+
+// ---------------------------------------------------------------- regression head (N=1)
+// One wave per row: pred = <h[b], w> + b0; with a target also loss and dy = scale*(pred-y).
+__global__ __launch_bounds__(256) void head_fwd_kernel(const bf16_t* __restrict__ Hm, long ldh,
+                                                       int B, int Hd, const float* __restrict__ w,
+                                                       const float* __restrict__ b0,
+                                                       const float* __restrict__ target,
+                                                       float* __restrict__ pred,
+                                                       float* __restrict__ dy,
+                                                       float* __restrict__ loss_sum,
+                                                       float dy_scale) {
+  __shared__ float red[4];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int b = blockIdx.x * 4 + wid;
+  float lsum = 0.f;
+  if (b < B) {
+    const bf16_t* row = Hm + (size_t)b * ldh;
+    float acc = 0.f;
+    for (int k = lane * 8; k < Hd; k += 512) {
+      const bf16x8 v = *reinterpret_cast<const bf16x8*>(row + k);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) acc += bf2f((bf16_t)v[e]) * w[k + e];
+    }
+    acc = wave_sum(acc) + b0[0];
+    if (lane == 0) {
+      pred[b] = acc;
+      if (target != nullptr) {
+        const float diff = acc - target[b];
+        lsum = diff * diff;
+        if (dy != nullptr) dy[b] = dy_scale * diff;
+      }
+    }
+  }
+  if (loss_sum != nullptr) {
+    if (lane == 0) red[wid] = lsum;
+    __syncthreads();
+    if (threadIdx.x == 0) atomicAdd(loss_sum, red[0] + red[1] + red[2] + red[3]);
+  }
+}
+
+void launch_head_fwd(const bf16_t* Hm, long ldh, int B, int Hd, const float* w, const float* b0,
+                     const float* target, float* pred, float* dy, float* loss_sum, float dy_scale,
+                     hipStream_t s) {
+  hipLaunchKernelGGL(head_fwd_kernel, dim3((B + 3) / 4), dim3(256), 0, s, Hm, ldh, B, Hd, w, b0,
+                     target, pred, dy, loss_sum, dy_scale);
+}
+
+// dw[u] += sum_b dy[b] h[b][u]; db += sum_b dy[b]. grid = (ceil(Hd/256), splits over b).
+__global__ __launch_bounds__(256) void head_bwd_w_kernel(const bf16_t* __restrict__ Hm, long ldh,
+                                                         int B, int Hd, const float* __restrict__ dy,
+                                                         float* __restrict__ dw,
+                                                         float* __restrict__ db, int rows_per) {
+  __shared__ float red[4];
+  const int u = blockIdx.x * 256 + threadIdx.x;
+  const int b0 = blockIdx.y * rows_per;
+  const int b1 = min(B, b0 + rows_per);
+  float acc = 0.f, dsum = 0.f;
+  for (int b = b0; b < b1; ++b) {
+    const float g = dy[b];
+    dsum += g;
+    if (u < Hd) acc += g * bf2f(Hm[(size_t)b * ldh + u]);
+  }
+  if (u < Hd) atomicAdd(dw + u, acc);
+  if (blockIdx.x == 0 && threadIdx.x == 0 && db != nullptr) atomicAdd(db, dsum);
+  (void)red;
+}
+
+void launch_head_bwd_w(const bf16_t* Hm, long ldh, int B, int Hd, const float* dy, float* dw,
+                       float* db, hipStream_t s) {
+  const int gx = (Hd + 255) / 256;
+  int splits = (512 + gx - 1) / gx;
+  if (splits > B) splits = B > 0 ? B : 1;
+  const int rows_per = (B + splits - 1) / splits;
+  splits = (B + rows_per - 1) / rows_per;
+  hipLaunchKernelGGL(head_bwd_w_kernel, dim3(gx, splits), dim3(256), 0, s, Hm, ldh, B, Hd, dy, dw,
+                     db, rows_per);
+}
+
+// dz[b][u] = dy[b] * w[u] (* [h>0]); colsum[u] += sum_b dz. One block per 8 rows x 256 units.
+__global__ __launch_bounds__(256) void head_bwd_x_kernel(const bf16_t* __restrict__ Hm, long ldh,
+                                                         int B, int Hd, const float* __restrict__ dy,
+                                                         const float* __restrict__ w, int relu_mask,
+                                                         bf16_t* __restrict__ dz, long ldz,
+                                                         float* __restrict__ colsum, int rows_per) {
+  const int u = blockIdx.x * 256 + threadIdx.x;
+  if (u >= Hd) return;
+  const int b0 = blockIdx.y * rows_per, b1 = min(B, b0 + rows_per);
+  const float wu = w[u];
+  float cs = 0.f;
+  for (int b = b0; b < b1; ++b) {
+    float v = dy[b] * wu;
+    if (relu_mask && bf2f(Hm[(size_t)b * ldh + u]) <= 0.f) v = 0.f;
+    const bf16_t vb = f2bf(v);
+    dz[(size_t)b * ldz + u] = vb;
+    cs += bf2f(vb);
+  }
+  if (colsum != nullptr) atomicAdd(colsum + u, cs);
+}
+
+void launch_head_bwd_x(const bf16_t* Hm, long ldh, int B, int Hd, const float* dy, const float* w,
+                       int relu_mask, bf16_t* dz, long ldz, float* colsum, hipStream_t s) {
+  const int gx = (Hd + 255) / 256;
+  int splits = (1024 + gx - 1) / gx;
+  if (splits > B) splits = B > 0 ? B : 1;
+  const int rows_per = (B + splits - 1) / splits;
+  splits = (B + rows_per - 1) / rows_per;
+  hipLaunchKernelGGL(head_bwd_x_kernel, dim3(gx, splits), dim3(256), 0, s, Hm, ldh, B, Hd, dy, w,
+                     relu_mask, dz, ldz, colsum, rows_per);
+}
+
+// ---------------------------------------------------------------- multi-output losses
+// kind 0: L = sum (p-y)^2,            d = scale * 2 (p-y)
+// kind 1: L = sum clip(|y-p|, 0, c),  d = scale * (-sign(y-p)) * [|y-p| <= c]   (Theano grads)
+// loss_sum accumulates the raw sum (host divides); dpred (bf16) feeds the backward GEMMs;
+// colsum[o] += sum_b d (bias gradient of the producing layer).
+__global__ __launch_bounds__(256) void loss_kernel(int kind, const float* __restrict__ pred,
+                                                   const float* __restrict__ y, int B, int O,
+                                                   float clip, float scale,
+                                                   float* __restrict__ loss_sum,
+                                                   bf16_t* __restrict__ dpred,
+                                                   float* __restrict__ colsum) {
+  __shared__ float red[4];
+  const long total = (long)B * O;
+  float ls = 0.f;
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
+    const float p = pred[i], t = y[i];
+    float l, d;
+    if (kind == 0) {
+      const float e = p - t;
+      l = e * e;
+      d = 2.f * e;
+    } else {
+      const float e = t - p, a = fabsf(e);
+      l = fminf(a, clip);
+      const float sg = e > 0.f ? 1.f : (e < 0.f ? -1.f : 0.f);
+      d = a <= clip ? -sg : 0.f;
+    }
+    ls += l;
+    d *= scale;
+    if (dpred != nullptr) dpred[i] = f2bf(d);
+    if (colsum != nullptr) atomicAdd(colsum + (i % O), d);
+  }
+  const float s = block_sum<256>(ls, red);
+  if (threadIdx.x == 0 && loss_sum != nullptr) atomicAdd(loss_sum, s);
+}
+
+void launch_loss(int kind, const float* pred, const float* y, int B, int O, float clip, float scale,
+                 float* loss_sum, bf16_t* dpred, float* colsum, hipStream_t s) {
+  const long total = (long)B * O;
+  int blocks = (int)((total + 255) / 256);
+  if (blocks > 1024) blocks = 1024;
+  if (blocks < 1) blocks = 1;
+  hipLaunchKernelGGL(loss_kernel, dim3(blocks), dim3(256), 0, s, kind, pred, y, B, O, clip, scale,
+                     loss_sum, dpred, colsum);
+}
+
+// ---------------------------------------------------------------- optimizers
+// Adam (PyTorch semantics, decoupled weight decay when wd != 0 — AdamW form).
+// bc1 = 1 - b1^t, bc2 = 1 - b2^t are computed on the host per step.
+__device__ __forceinline__ void adam_one(float& p, float g, float& m, float& v, float lr, float b1,
+                                         float b2, float eps, float wd, float bc1, float bc2) {
+  m = b1 * m + (1.f - b1) * g;
+  v = b2 * v + (1.f - b2) * g * g;
+  const float mh = m / bc1, vh = v / bc2;
+  p -= lr * (mh / (sqrtf(vh) + eps) + wd * p);
+}
+
+__global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p, const float* __restrict__ g,
+                                                   float* __restrict__ m, float* __restrict__ v, long n,
+                                                   float lr, float b1, float b2, float eps, float wd,
+                                                   float bc1, float bc2, float gscale) {
+  const long n4 = n / 4;
+  const long stride = (long)gridDim.x * blockDim.x;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n4; i += stride) {
+    float4 pp = reinterpret_cast<float4*>(p)[i];
+    float4 gg = reinterpret_cast<const float4*>(g)[i];
+    float4 mm = reinterpret_cast<float4*>(m)[i];
+    float4 vv = reinterpret_cast<float4*>(v)[i];
+    adam_one(pp.x, gg.x * gscale, mm.x, vv.x, lr, b1, b2, eps, wd, bc1, bc2);
+    adam_one(pp.y, gg.y * gscale, mm.y, vv.y, lr, b1, b2, eps, wd, bc1, bc2);
+    adam_one(pp.z, gg.z * gscale, mm.z, vv.z, lr, b1, b2, eps, wd, bc1, bc2);
+    adam_one(pp.w, gg.w * gscale, mm.w, vv.w, lr, b1, b2, eps, wd, bc1, bc2);
+    reinterpret_cast<float4*>(p)[i] = pp;
+    reinterpret_cast<float4*>(m)[i] = mm;
+    reinterpret_cast<float4*>(v)[i] = vv;
+  }
+  for (long i = n4 * 4 + blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += stride)
+    adam_one(p[i], g[i] * gscale, m[i], v[i], lr, b1, b2, eps, wd, bc1, bc2);
+}
+
+static int ew_blocks(long n) {
+  long b = (n / 4 + 255) / 256;
+  if (b > 2048) b = 2048;
+  if (b < 1) b = 1;
+  return (int)b;
+}
+
+void launch_adam(float* p, const float* g, float* m, float* v, long n, float lr, float b1, float b2,
+                 float eps, float wd, float bc1, float bc2, float gscale, hipStream_t s) {
+  hipLaunchKernelGGL(adam_kernel, dim3(ew_blocks(n)), dim3(256), 0, s, p, g, m, v, n, lr, b1, b2,
+                     eps, wd, bc1, bc2, gscale);
+}
+
+// Keras-0.x SGD: v = mu v - lr_t g; p += mu v - lr_t g (Nesterov) or p += v.
+// lr_t = lr / (1 + decay * iterations) is computed on the host.
+__global__ __launch_bounds__(256) void sgd_kernel(float* __restrict__ p, const float* __restrict__ g,
+                                                  float* __restrict__ vel, long n, float lr,
+                                                  float momentum, int nesterov, float gscale) {
+  const long stride = (long)gridDim.x * blockDim.x;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += stride) {
+    const float gi = g[i] * gscale;
+    const float v = momentum * vel[i] - lr * gi;
+    vel[i] = v;
+    p[i] += nesterov ? (momentum * v - lr * gi) : v;
+  }
+}
+
+void launch_sgd(float* p, const float* g, float* vel, long n, float lr, float momentum,
+                int nesterov, float gscale, hipStream_t s) {
+  long b = (n + 255) / 256;
+  if (b > 2048) b = 2048;
+  if (b < 1) b = 1;
+  hipLaunchKernelGGL(sgd_kernel, dim3((int)b), dim3(256), 0, s, p, g, vel, n, lr, momentum,
+                     nesterov, gscale);
+}
+
+// ---------------------------------------------------------------- casts
+__global__ void cast_bf16_kernel(const float* __restrict__ src, bf16_t* __restrict__ dst, long n) {
+  const long stride = (long)gridDim.x * blockDim.x;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += stride) dst[i] = f2bf(src[i]);
+}
+
+void launch_cast_bf16(const float* src, bf16_t* dst, long n, hipStream_t s) {
+  long b = (n + 255) / 256;
+  if (b > 4096) b = 4096;
+  if (b < 1) b = 1;
+  hipLaunchKernelGGL(cast_bf16_kernel, dim3((int)b), dim3(256), 0, s, src, dst, n);
+}
+
+// dst[c][r] = bf16(src[r*lds + c]) for r < rows, c < cols; 32x32 tiles through LDS.
+__global__ void transpose_cast_kernel(const float* __restrict__ src, long lds, int rows, int cols,
+                                      bf16_t* __restrict__ dst, long ldd) {
+  __shared__ float tile[32][33];
+  const int r0 = blockIdx.y * 32, c0 = blockIdx.x * 32;
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;  // 256 threads: 32 x 8
+  for (int k = ty; k < 32; k += 8) {
+    const int r = r0 + k, c = c0 + tx;
+    tile[k][tx] = (r < rows && c < cols) ? src[(size_t)r * lds + c] : 0.f;
+  }
+  __syncthreads();
+  for (int k = ty; k < 32; k += 8) {
+    const int c = c0 + k, r = r0 + tx;
+    if (c < cols && r < rows) dst[(size_t)c * ldd + r] = f2bf(tile[tx][k]);
+  }
+}
+
+void launch_transpose_cast_bf16(const float* src, long lds, int rows, int cols, bf16_t* dst,
+                                long ldd, hipStream_t s) {
+  dim3 grid((cols + 31) / 32, (rows + 31) / 32);
+  hipLaunchKernelGGL(transpose_cast_kernel, grid, dim3(256), 0, s, src, lds, rows, cols, dst, ldd);
+}
+
+// 1-D im2col for a stride-1 valid convolution, channels-last input x[B][L][Cin]:
+// col[b*Lout + t][k*Cin + c] = x[b][t+k][c] for k < ksz; column ksz*Cin is the constant 1
+// (bias folded into the weight); remaining columns up to Kp are zero.
+__global__ void im2col1d_kernel(const float* __restrict__ x, int B, int L, int Cin, int ksz, int Lout,
+                                int Kp, bf16_t* __restrict__ col) {
+  const long total = (long)B * Lout * Kp;
+  const long stride = (long)gridDim.x * blockDim.x;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += stride) {
+    const int kc = i % Kp;
+    const long bt = i / Kp;
+    const int t = bt % Lout, b = bt / Lout;
+    float v = 0.f;
+    if (kc < ksz * Cin) {
+      const int k = kc / Cin, c = kc % Cin;
+      v = x[((long)b * L + t + k) * Cin + c];
+    } else if (kc == ksz * Cin) {
+      v = 1.f;
+    }
+    col[i] = f2bf(v);
+  }
+}
+
+void launch_im2col1d(const float* x, int B, int L, int Cin, int ksz, int Lout, int Kp, bf16_t* col,
+                     hipStream_t s) {
+  const long total = (long)B * Lout * Kp;
+  long b = (total + 255) / 256;
+  if (b > 4096) b = 4096;
+  if (b < 1) b = 1;
+  hipLaunchKernelGGL(im2col1d_kernel, dim3((int)b), dim3(256), 0, s, x, B, L, Cin, ksz, Lout, Kp,
+                     col);
+}
+
+}  // namespace wf

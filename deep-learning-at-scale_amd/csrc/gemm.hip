@@ -1,0 +1,99 @@
+// wellflow — general MFMA GEMM with fused epilogues (gfx950).
+//
+//   out[m, n] = act(alpha * sum_k A(m,k) B(n,k) + beta * out[m, n] + bias[n]) (* mask)
+//
+// Used by the static / dynamic MLP (GEMM + bias + ReLU forward,
+// dX with the ReLU-mask epilogue, dW = dZ^T X with MN-contiguous operands), the CNN
+// (K1/K5/K7) and the LSTM weight gradient (K14). Split-K reduces through fp32 atomics
+// into the (pre-zeroed) fp32 output: the weight-gradient GEMMs here have tiny M x N
+// (<= 2048 x 576) and a huge K (batch x time), so the atomic bytes are <1% of the
+// MFMA time (cdna_hip_programming.md Guideline 12 sizing rule).
+#include "gemm_core.h"
+#include "kernels.h"
+
+namespace wf {
+
+template <int BM, int BN, int LA, int LB>
+__global__ __launch_bounds__(256) void gemm_kernel(const bf16_t* __restrict__ A, long lda,
+                                                   const bf16_t* __restrict__ B, long ldb,
+                                                   int M, int N, int K, int kchunk,
+                                                   GemmEpilogue e) {
+  using C = GemmCfg<BM, BN, LA, LB>;
+  __shared__ __attribute__((aligned(16))) char smem[C::LDS_BYTES];
+  const int tiles_n = (N + BN - 1) / BN;
+  const int tiles = ((M + BM - 1) / BM) * tiles_n;
+  const int L = xcd_remap(blockIdx.x, gridDim.x);
+  const int split = L / tiles, t = L % tiles;
+  const int m0 = (t / tiles_n) * BM, n0 = (t % tiles_n) * BN;
+  const int kbeg = split * kchunk;
+  const int kend = min(K, kbeg + kchunk);
+
+  f32x4 acc[C::TM][C::TN];
+  gemm_mainloop<C>(A, lda, M, B, ldb, N, kbeg, kend, m0, n0, smem, acc);
+
+  const AccCoord<C> cc(m0, n0);
+#pragma unroll
+  for (int j = 0; j < C::TN; ++j) {
+    const int n = cc.col(j);
+    const bool nok = n < N;
+    const float bn = (e.bias != nullptr && nok) ? e.bias[n] : 0.f;
+    float csum = 0.f;
+#pragma unroll
+    for (int i = 0; i < C::TM; ++i) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = cc.row(i, r);
+        if (!nok || m >= M) continue;
+        float v = e.alpha * acc[i][j][r];
+        const size_t o = (size_t)m * e.ldo + n;
+        if (e.atomic) {
+          atomicAdd(e.outF + o, v);
+          continue;
+        }
+        if (e.beta != 0.f) v += e.beta * e.outF[o];
+        v += bn;
+        if (e.act == 1) v = fmaxf(v, 0.f);
+        if (e.drop_p > 0.f)
+          v = uniform_hash(e.seed, (unsigned long long)m * N + n) >= e.drop_p
+                  ? v * (1.f / (1.f - e.drop_p)) : 0.f;
+        if (e.mask != nullptr)
+          v = bf2f(e.mask[(size_t)m * e.ldm + n]) > 0.f ? v * e.mask_scale : 0.f;
+        csum += v;
+        if (e.outF != nullptr) e.outF[o] = v;
+        if (e.outH != nullptr) e.outH[o] = f2bf(v);
+      }
+    }
+    if (e.colsum != nullptr) {
+      csum += __shfl_xor(csum, 16, 64);
+      csum += __shfl_xor(csum, 32, 64);
+      if ((threadIdx.x & 63) < 16 && nok) atomicAdd(e.colsum + n, csum);
+    }
+  }
+}
+
+template <int BM, int BN, int LA, int LB>
+static void launch_cfg(const bf16_t* A, long lda, const bf16_t* B, long ldb, int M, int N, int K,
+                       int ksplit, const GemmEpilogue& e, hipStream_t s) {
+  const int tiles = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
+  if (ksplit < 1) ksplit = 1;
+  int kchunk = (K + ksplit - 1) / ksplit;
+  kchunk = (kchunk + 63) / 64 * 64;
+  if (kchunk < 64) kchunk = 64;
+  const int nsplit = (K + kchunk - 1) / kchunk;
+  hipLaunchKernelGGL((gemm_kernel<BM, BN, LA, LB>), dim3(tiles * (nsplit > 0 ? nsplit : 1)),
+                     dim3(256), 0, s, A, lda, B, ldb, M, N, K, kchunk, e);
+}
+
+void launch_gemm(const bf16_t* A, long lda, int a_mn, const bf16_t* B, long ldb, int b_mn, int M,
+                 int N, int K, int ksplit, const GemmEpilogue& e, hipStream_t s) {
+  if (!a_mn && !b_mn)
+    launch_cfg<128, 128, K_CONTIG, K_CONTIG>(A, lda, B, ldb, M, N, K, ksplit, e, s);
+  else if (!a_mn && b_mn)
+    launch_cfg<128, 128, K_CONTIG, MN_CONTIG>(A, lda, B, ldb, M, N, K, ksplit, e, s);
+  else if (a_mn && !b_mn)
+    launch_cfg<128, 128, MN_CONTIG, K_CONTIG>(A, lda, B, ldb, M, N, K, ksplit, e, s);
+  else
+    launch_cfg<128, 128, MN_CONTIG, MN_CONTIG>(A, lda, B, ldb, M, N, K, ksplit, e, s);
+}
+
+}  // namespace wf

@@ -1,0 +1,192 @@
+// wellflow — MFMA GEMM mainloop shared by every matmul-shaped kernel (gfx950).
+//
+// One workgroup = 256 threads = 4 waves laid out 2(M) x 2(N); each wave owns a
+// (BM/2) x (BN/2) output tile built from v_mfma_f32_16x16x32_bf16 tiles
+// (cdna_hip_programming.md §3). K advances in BK = 64 steps through a double-buffered
+// LDS image filled by register staging (issue the next tile's global loads before the
+// MFMAs, write them to the other LDS buffer after — §5.5 T14), one barrier per K-step.
+//
+// Operand layouts (logical operand X is [rows][K]):
+//   K_CONTIG : X(r,k) = p[r*ld + k]     (activations, torch Linear weights [out][in])
+//   MN_CONTIG: X(r,k) = p[k*ld + r]     (the "transposed" operand of a weight-gradient
+//                                         GEMM, e.g. dW = dZ^T X reduces over the batch)
+// K_CONTIG tiles are stored [rows][64] (128-B rows) with the 16-B chunk index XORed by
+// (row>>1)&7, which makes the ds_read_b128 fragment reads conflict-free. MN_CONTIG tiles
+// are stored [64 k][rows] with the 32-B chunk index XORed by (k&3)|((k>>1)&4); fragments
+// come out with two ds_read_b64_tr_b16 hardware-transposed reads (T10), conflict-free
+// for 128- and 256-row tiles.
+#pragma once
+#include "common.h"
+
+namespace wf {
+
+enum : int { K_CONTIG = 0, MN_CONTIG = 1 };
+
+typedef __attribute__((address_space(3))) bf16x4 lds_bf16x4;
+
+template <int R, int L>
+struct OpTile {
+  static constexpr int NT = 256;
+  static constexpr int BK = 64;
+  static constexpr int CHUNKS = R * BK / 8 / NT;  // 16-B chunks staged per thread
+  static constexpr int BYTES = R * BK * 2;
+  static_assert(CHUNKS >= 1, "tile too small for 256 threads");
+  static_assert(L == K_CONTIG || R >= 64, "MN_CONTIG tile needs >= 64 rows");
+
+  __device__ static __forceinline__ int hk(int k) {
+    return ((k & 3) | ((k >> 1) & 4)) & (R / 16 - 1);
+  }
+
+  // Global -> registers for the tile whose first row is row0 and first k is k0.
+  // Rows >= rows or k >= kmax read as zero (the address is clamped, the value masked,
+  // so the load itself is unconditional).
+  __device__ static __forceinline__ void gload(const bf16_t* __restrict__ p, long ld, int rows,
+                                               int kmax, int row0, int k0, uint4 (&r)[CHUNKS]) {
+#pragma unroll
+    for (int i = 0; i < CHUNKS; ++i) {
+      const int q = threadIdx.x + i * NT;
+      int gr, gk;
+      if constexpr (L == K_CONTIG) {
+        gr = row0 + (q >> 3);
+        gk = k0 + (q & 7) * 8;
+      } else {
+        constexpr int CPR = R / 8;
+        gk = k0 + q / CPR;
+        gr = row0 + (q % CPR) * 8;
+      }
+      const bool ok = (gr < rows) && (gk < kmax);
+      const size_t off = ok ? (L == K_CONTIG ? (size_t)gr * ld + gk : (size_t)gk * ld + gr) : 0;
+      uint4 v = *reinterpret_cast<const uint4*>(p + off);
+      if (!ok) v = make_uint4(0u, 0u, 0u, 0u);
+      r[i] = v;
+    }
+  }
+
+  __device__ static __forceinline__ void swrite(char* lds, const uint4 (&r)[CHUNKS]) {
+#pragma unroll
+    for (int i = 0; i < CHUNKS; ++i) {
+      const int q = threadIdx.x + i * NT;
+      int off;
+      if constexpr (L == K_CONTIG) {
+        const int row = q >> 3, c = q & 7;
+        off = row * 128 + ((c ^ ((row >> 1) & 7)) << 4);
+      } else {
+        constexpr int CPR = R / 8;
+        const int k = q / CPR, c8 = q % CPR;
+        off = k * (R * 2) + ((((c8 >> 1) ^ hk(k))) << 5) + ((c8 & 1) << 4);
+      }
+      *reinterpret_cast<uint4*>(lds + off) = r[i];
+    }
+  }
+
+  // Lane's A/B fragment for mfma_f32_16x16x32_bf16: rows rs..rs+15 (tile-local),
+  // k sub-step kk in {0,1}: lane l holds X[rs + (l&15)][32kk + 8(l>>4) + 0..7].
+  __device__ static __forceinline__ bf16x8 frag(const char* lds, int rs, int kk, int lane) {
+    if constexpr (L == K_CONTIG) {
+      const int row = rs + (lane & 15);
+      const int c = kk * 4 + (lane >> 4);
+      const int off = row * 128 + ((c ^ ((row >> 1) & 7)) << 4);
+      return *reinterpret_cast<const bf16x8*>(lds + off);
+    } else {
+      const int g = lane >> 4, q = (lane & 15) >> 2, p = lane & 3;
+      const int j = rs >> 4;
+      bf16x8 out;
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int k = kk * 32 + 8 * g + 4 * h + q;
+        const int off = k * (R * 2) + ((j ^ hk(k)) << 5) + p * 8;
+        bf16x4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_bf16x4*)(lds + off));
+        out[4 * h + 0] = v[0];
+        out[4 * h + 1] = v[1];
+        out[4 * h + 2] = v[2];
+        out[4 * h + 3] = v[3];
+      }
+      return out;
+    }
+  }
+};
+
+template <int BM_, int BN_, int LA, int LB>
+struct GemmCfg {
+  static constexpr int BM = BM_, BN = BN_, BK = 64, NT = 256;
+  static constexpr int WM = 2, WN = 2;
+  static constexpr int WTM = BM / WM, WTN = BN / WN;
+  static constexpr int TM = WTM / 16, TN = WTN / 16;
+  using TA = OpTile<BM, LA>;
+  using TB = OpTile<BN, LB>;
+  static constexpr int STAGE = TA::BYTES + TB::BYTES;
+  static constexpr int LDS_BYTES = 2 * STAGE;
+};
+
+// acc += A[m0:m0+BM, kbeg:kend] * B[n0:n0+BN, kbeg:kend]^T (operands in the layouts LA/LB).
+// kbeg must be a multiple of 64; k >= kend reads as zero.
+template <class C>
+__device__ __forceinline__ void gemm_mainloop(const bf16_t* __restrict__ A, long lda, int M,
+                                              const bf16_t* __restrict__ B, long ldb, int N,
+                                              int kbeg, int kend, int m0, int n0, char* smem,
+                                              f32x4 (&acc)[C::TM][C::TN]) {
+  using TA = typename C::TA;
+  using TB = typename C::TB;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int wm = wid / C::WN, wn = wid % C::WN;
+#pragma unroll
+  for (int i = 0; i < C::TM; ++i)
+#pragma unroll
+    for (int j = 0; j < C::TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nk = (kend - kbeg + C::BK - 1) / C::BK;
+  if (nk <= 0) return;
+  uint4 ra[TA::CHUNKS], rb[TB::CHUNKS];
+  TA::gload(A, lda, M, kend, m0, kbeg, ra);
+  TB::gload(B, ldb, N, kend, n0, kbeg, rb);
+  TA::swrite(smem, ra);
+  TB::swrite(smem + TA::BYTES, rb);
+  __syncthreads();
+
+  for (int kt = 0; kt < nk; ++kt) {
+    char* cur = smem + (kt & 1) * C::STAGE;
+    char* nxt = smem + ((kt & 1) ^ 1) * C::STAGE;
+    const bool more = (kt + 1) < nk;
+    if (more) {
+      const int k0 = kbeg + (kt + 1) * C::BK;
+      TA::gload(A, lda, M, kend, m0, k0, ra);
+      TB::gload(B, ldb, N, kend, n0, k0, rb);
+    }
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      bf16x8 a[C::TM], b[C::TN];
+#pragma unroll
+      for (int i = 0; i < C::TM; ++i) a[i] = TA::frag(cur, wm * C::WTM + i * 16, kk, lane);
+#pragma unroll
+      for (int j = 0; j < C::TN; ++j) b[j] = TB::frag(cur + TA::BYTES, wn * C::WTN + j * 16, kk, lane);
+#pragma unroll
+      for (int i = 0; i < C::TM; ++i)
+#pragma unroll
+        for (int j = 0; j < C::TN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
+    }
+    if (more) {
+      TA::swrite(nxt, ra);
+      TB::swrite(nxt + TA::BYTES, rb);
+    }
+    __syncthreads();
+  }
+}
+
+// Output coordinates of accumulator element acc[i][j][r] (16x16 C/D map: col = lane&15,
+// row = 4*(lane>>4) + r).
+template <class C>
+struct AccCoord {
+  int mb, nb;  // wave tile origin (absolute)
+  __device__ __forceinline__ AccCoord(int m0, int n0) {
+    const int wid = threadIdx.x >> 6;
+    mb = m0 + (wid / C::WN) * C::WTM;
+    nb = n0 + (wid % C::WN) * C::WTN;
+  }
+  __device__ __forceinline__ int row(int i, int r) const {
+    return mb + i * 16 + 4 * ((threadIdx.x & 63) >> 4) + r;
+  }
+  __device__ __forceinline__ int col(int j) const { return nb + j * 16 + (threadIdx.x & 15); }
+};
+
+}  // namespace wf

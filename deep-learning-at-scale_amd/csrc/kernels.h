@@ -1,0 +1,66 @@
+// wellflow — host-side launcher declarations for the HIP kernel library.
+// Pure HIP/C++ (no torch headers): binding.cpp validates tensors and calls these.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace wf {
+
+typedef unsigned short bf16_t;
+
+struct GemmEpilogue {
+  float* outF = nullptr;         // fp32 output (also the beta / atomic target)
+  bf16_t* outH = nullptr;        // bf16 output
+  long ldo = 0;
+  const float* bias = nullptr;   // [N]
+  const bf16_t* mask = nullptr;  // zero the output where mask <= 0 (ReLU backward)
+  long ldm = 0;
+  float mask_scale = 1.f;        // multiply kept values (inverted-dropout backward)
+  float* colsum = nullptr;       // [N] += column sums of the final output (bias grads)
+  float alpha = 1.f, beta = 0.f;
+  int act = 0;                   // 0 linear, 1 relu
+  int atomic = 0;                // split-K: atomicAdd alpha*acc into outF
+  float drop_p = 0.f;            // inverted dropout after the activation
+  unsigned long long seed = 0;
+};
+
+void launch_gemm(const bf16_t* A, long lda, int a_mn, const bf16_t* B, long ldb, int b_mn, int M,
+                 int N, int K, int ksplit, const GemmEpilogue& e, hipStream_t s);
+
+// ---- LSTM (single layer, batch-first input, seq-to-one regression) ----
+struct LstmDims {
+  int B, T, F, KX, H;  // G = 4H, KA = KX + H
+};
+void launch_lstm_pack_x(const float* x, bf16_t* XH, LstmDims d, hipStream_t s);
+void launch_lstm_fwd_step(int t, bf16_t* XH, const bf16_t* Wp, float* Cst, bf16_t* S,
+                          LstmDims d, hipStream_t s);
+void launch_lstm_bwd_step(int t, const bf16_t* WhhT, const float* Cst, const bf16_t* S,
+                          bf16_t* DG, float* dcarry, const float* dy, const float* w_out,
+                          LstmDims d, hipStream_t s);
+void launch_lstm_pack_weights(const float* W, bf16_t* Wp, bf16_t* WhhT, LstmDims d,
+                              hipStream_t s);
+
+// ---- regression head (N = 1) and losses ----
+void launch_head_fwd(const bf16_t* Hm, long ldh, int B, int Hd, const float* w, const float* b0,
+                     const float* target, float* pred, float* dy, float* loss_sum, float dy_scale,
+                     hipStream_t s);
+void launch_head_bwd_w(const bf16_t* Hm, long ldh, int B, int Hd, const float* dy, float* dw,
+                       float* db, hipStream_t s);
+void launch_head_bwd_x(const bf16_t* Hm, long ldh, int B, int Hd, const float* dy, const float* w,
+                       int relu_mask, bf16_t* dz, long ldz, float* colsum, hipStream_t s);
+// kind 0 = MSE, 1 = clipped MAE (reference mae_clip)
+void launch_loss(int kind, const float* pred, const float* y, int B, int O, float clip, float scale,
+                 float* loss_sum, bf16_t* dpred, float* colsum, hipStream_t s);
+
+// ---- optimizers and casts over flat fp32 buffers ----
+void launch_adam(float* p, const float* g, float* m, float* v, long n, float lr, float b1,
+                 float b2, float eps, float wd, float bc1, float bc2, float gscale, hipStream_t s);
+void launch_sgd(float* p, const float* g, float* vel, long n, float lr, float momentum,
+                int nesterov, float gscale, hipStream_t s);
+void launch_cast_bf16(const float* src, bf16_t* dst, long n, hipStream_t s);
+void launch_transpose_cast_bf16(const float* src, long lds, int rows, int cols, bf16_t* dst,
+                                long ldd, hipStream_t s);
+void launch_im2col1d(const float* x, int B, int L, int Cin, int ksz, int Lout, int Kp,
+                     bf16_t* col, hipStream_t s);
+
+}  // namespace wf

@@ -1,0 +1,212 @@
+// wellflow — LSTM kernels (BASELINE.json config 5:
+// seq-len 64, hidden 512, seq-to-one regression, bf16 on MFMA).
+//
+// Design (MI355X-first, not a cuDNN translation):
+//  * The input projection is not hoisted into a [T,B,4H] tensor (2 GB at B=8192):
+//    every step multiplies the concatenated row [x_t | 1 | 0.. | h_{t-1}] (KA = KX + H
+//    columns, KX = 64) by one weight matrix Wp [4H][KA] whose "1" column carries the
+//    bias. The whole cell is one GEMM + fused epilogue per timestep; the weight gradient
+//    for W_ih, W_hh and the bias becomes ONE big GEMM over all (t, b) at the end.
+//  * Gate columns are permuted so that a wave's 64-column N tile holds gates i,f,g,o of
+//    the same 16 hidden units: with the 16x16 MFMA C map each lane then owns all four
+//    gate pre-activations of its (row, unit) pairs and the cell update needs no LDS
+//    exchange.  column p <-> (gate, unit):  unit = (p>>6)*16 + (p&15),  gate = (p>>4)&3.
+//  * XH[t] (bf16 [B][KA]) is both the GEMM A operand of step t and the saved input of
+//    the weight-gradient GEMM; step t writes h_t straight into XH[t+1][:, KX:].
+//  * Backward step t is the GEMM dh_t = dG_{t+1} * W_hh (B operand WhhT = W_hh^T kept as
+//    a bf16 shadow, K-contiguous) whose epilogue runs the cell backward for step t and
+//    writes dG_t, so the time recurrence costs T-1 GEMM launches and no extra passes.
+#include "gemm_core.h"
+#include "kernels.h"
+
+namespace wf {
+
+__device__ __forceinline__ int gate_col(int gate, int u) { return (u >> 4) * 64 + gate * 16 + (u & 15); }
+
+// XH[t][b][0:KX] = [x[b][t][0:F], 1, 0, ...]; one thread per (t, b, k).
+__global__ void lstm_pack_x_kernel(const float* __restrict__ x, bf16_t* __restrict__ XH,
+                                   LstmDims d) {
+  const int KA = d.KX + d.H;
+  const long total = (long)d.T * d.B * d.KX;
+  for (long idx = blockIdx.x * (long)blockDim.x + threadIdx.x; idx < total;
+       idx += (long)gridDim.x * blockDim.x) {
+    const int k = idx % d.KX;
+    const long tb = idx / d.KX;
+    const int b = tb % d.B, t = tb / d.B;
+    float v = 0.f;
+    if (k < d.F) v = x[((long)b * d.T + t) * d.F + k];
+    else if (k == d.F) v = 1.f;
+    XH[((long)t * d.B + b) * KA + k] = f2bf(v);
+  }
+}
+
+void launch_lstm_pack_x(const float* x, bf16_t* XH, LstmDims d, hipStream_t s) {
+  const long total = (long)d.T * d.B * d.KX;
+  int blocks = (int)((total + 255) / 256);
+  if (blocks > 8192) blocks = 8192;
+  hipLaunchKernelGGL(lstm_pack_x_kernel, dim3(blocks), dim3(256), 0, s, x, XH, d);
+}
+
+using LstmCfg = GemmCfg<128, 128, K_CONTIG, K_CONTIG>;
+
+__global__ __launch_bounds__(256) void lstm_fwd_step_kernel(int t, bf16_t* __restrict__ XH,
+                                                            const bf16_t* __restrict__ Wp,
+                                                            float* __restrict__ Cst,
+                                                            bf16_t* __restrict__ S, LstmDims d) {
+  using C = LstmCfg;
+  __shared__ __attribute__((aligned(16))) char smem[C::LDS_BYTES];
+  const int KA = d.KX + d.H, G = 4 * d.H;
+  const int tiles_n = G / C::BN;
+  const int L = xcd_remap(blockIdx.x, gridDim.x);
+  const int m0 = (L / tiles_n) * C::BM, n0 = (L % tiles_n) * C::BN;
+  const bf16_t* A = XH + (size_t)t * d.B * KA;
+
+  f32x4 acc[C::TM][C::TN];
+  gemm_mainloop<C>(A, KA, d.B, Wp, KA, G, 0, KA, m0, n0, smem, acc);
+
+  const AccCoord<C> cc(m0, n0);
+  const int u = (cc.nb >> 6) * 16 + (threadIdx.x & 15);
+  const float* cprev = Cst + (size_t)t * d.B * d.H;
+  float* cnext = Cst + (size_t)(t + 1) * d.B * d.H;
+  bf16_t* hnext = XH + (size_t)(t + 1) * d.B * KA + d.KX;
+  bf16_t* St = S + (size_t)t * d.B * G;
+#pragma unroll
+  for (int i = 0; i < C::TM; ++i) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int m = cc.row(i, r);
+      if (m >= d.B) continue;
+      const float ig = sigmoidf_(acc[i][0][r]);
+      const float fg = sigmoidf_(acc[i][1][r]);
+      const float gg = tanhf_(acc[i][2][r]);
+      const float og = sigmoidf_(acc[i][3][r]);
+      const size_t mu = (size_t)m * d.H + u;
+      const float c = fg * cprev[mu] + ig * gg;
+      const float h = og * tanhf_(c);
+      cnext[mu] = c;
+      hnext[(size_t)m * KA + u] = f2bf(h);
+      bf16_t* srow = St + (size_t)m * G;
+      srow[gate_col(0, u)] = f2bf(ig);
+      srow[gate_col(1, u)] = f2bf(fg);
+      srow[gate_col(2, u)] = f2bf(gg);
+      srow[gate_col(3, u)] = f2bf(og);
+    }
+  }
+}
+
+void launch_lstm_fwd_step(int t, bf16_t* XH, const bf16_t* Wp, float* Cst, bf16_t* S,
+                          LstmDims d, hipStream_t s) {
+  const int G = 4 * d.H;
+  const int tiles = ((d.B + LstmCfg::BM - 1) / LstmCfg::BM) * (G / LstmCfg::BN);
+  hipLaunchKernelGGL(lstm_fwd_step_kernel, dim3(tiles), dim3(256), 0, s, t, XH, Wp, Cst, S, d);
+}
+
+// Cell backward for one (row m, unit u) of step t given dh_t; updates the dc carry and
+// writes the four gate-gradients of step t into DG[t] (permuted column order).
+__device__ __forceinline__ void cell_bwd(int t, int m, int u, float dh, const float* __restrict__ Cst,
+                                         const bf16_t* __restrict__ S, bf16_t* __restrict__ DG,
+                                         float* __restrict__ dcarry, const LstmDims& d) {
+  const int G = 4 * d.H;
+  const size_t rowg = ((size_t)t * d.B + m) * G;
+  const float ig = bf2f(S[rowg + gate_col(0, u)]);
+  const float fg = bf2f(S[rowg + gate_col(1, u)]);
+  const float gg = bf2f(S[rowg + gate_col(2, u)]);
+  const float og = bf2f(S[rowg + gate_col(3, u)]);
+  const size_t mu = (size_t)m * d.H + u;
+  const float c = Cst[(size_t)(t + 1) * d.B * d.H + mu];
+  const float cp = Cst[(size_t)t * d.B * d.H + mu];
+  const float tc = tanhf_(c);
+  const float dc = dcarry[mu] + dh * og * (1.f - tc * tc);
+  const float d_o = dh * tc * og * (1.f - og);
+  const float d_i = dc * gg * ig * (1.f - ig);
+  const float d_f = dc * cp * fg * (1.f - fg);
+  const float d_g = dc * ig * (1.f - gg * gg);
+  dcarry[mu] = dc * fg;
+  DG[rowg + gate_col(0, u)] = f2bf(d_i);
+  DG[rowg + gate_col(1, u)] = f2bf(d_f);
+  DG[rowg + gate_col(2, u)] = f2bf(d_g);
+  DG[rowg + gate_col(3, u)] = f2bf(d_o);
+}
+
+// t = T-1: dh comes from the regression head, dh[m][u] = dy[m] * w_out[u]; dcarry starts at 0.
+__global__ void lstm_bwd_last_kernel(const float* __restrict__ Cst, const bf16_t* __restrict__ S,
+                                     bf16_t* __restrict__ DG, float* __restrict__ dcarry,
+                                     const float* __restrict__ dy, const float* __restrict__ w_out,
+                                     LstmDims d) {
+  const long total = (long)d.B * d.H;
+  for (long idx = blockIdx.x * (long)blockDim.x + threadIdx.x; idx < total;
+       idx += (long)gridDim.x * blockDim.x) {
+    const int u = idx % d.H, m = idx / d.H;
+    dcarry[idx] = 0.f;
+    cell_bwd(d.T - 1, m, u, dy[m] * w_out[u], Cst, S, DG, dcarry, d);
+  }
+}
+
+__global__ __launch_bounds__(256) void lstm_bwd_step_kernel(int t, const bf16_t* __restrict__ WhhT,
+                                                            const float* __restrict__ Cst,
+                                                            const bf16_t* __restrict__ S,
+                                                            bf16_t* __restrict__ DG,
+                                                            float* __restrict__ dcarry, LstmDims d) {
+  using C = LstmCfg;
+  __shared__ __attribute__((aligned(16))) char smem[C::LDS_BYTES];
+  const int G = 4 * d.H;
+  const int tiles_n = d.H / C::BN;
+  const int L = xcd_remap(blockIdx.x, gridDim.x);
+  const int m0 = (L / tiles_n) * C::BM, n0 = (L % tiles_n) * C::BN;
+  const bf16_t* A = DG + (size_t)(t + 1) * d.B * G;
+
+  f32x4 acc[C::TM][C::TN];
+  gemm_mainloop<C>(A, G, d.B, WhhT, G, d.H, 0, G, m0, n0, smem, acc);
+
+  const AccCoord<C> cc(m0, n0);
+#pragma unroll
+  for (int j = 0; j < C::TN; ++j) {
+    const int u = cc.col(j);
+#pragma unroll
+    for (int i = 0; i < C::TM; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = cc.row(i, r);
+        if (m < d.B) cell_bwd(t, m, u, acc[i][j][r], Cst, S, DG, dcarry, d);
+      }
+  }
+}
+
+void launch_lstm_bwd_step(int t, const bf16_t* WhhT, const float* Cst, const bf16_t* S,
+                          bf16_t* DG, float* dcarry, const float* dy, const float* w_out,
+                          LstmDims d, hipStream_t s) {
+  if (t == d.T - 1) {
+    const long total = (long)d.B * d.H;
+    int blocks = (int)((total + 255) / 256);
+    if (blocks > 8192) blocks = 8192;
+    hipLaunchKernelGGL(lstm_bwd_last_kernel, dim3(blocks), dim3(256), 0, s, Cst, S, DG, dcarry,
+                       dy, w_out, d);
+    return;
+  }
+  const int tiles = ((d.B + LstmCfg::BM - 1) / LstmCfg::BM) * (d.H / LstmCfg::BN);
+  hipLaunchKernelGGL(lstm_bwd_step_kernel, dim3(tiles), dim3(256), 0, s, t, WhhT, Cst, S, DG,
+                     dcarry, d);
+}
+
+// fp32 master W [G][KA] (permuted rows) -> bf16 Wp [G][KA] and WhhT [H][G].
+__global__ void lstm_pack_weights_kernel(const float* __restrict__ W, bf16_t* __restrict__ Wp,
+                                         bf16_t* __restrict__ WhhT, LstmDims d) {
+  const int KA = d.KX + d.H, G = 4 * d.H;
+  const long total = (long)G * KA;
+  for (long idx = blockIdx.x * (long)blockDim.x + threadIdx.x; idx < total;
+       idx += (long)gridDim.x * blockDim.x) {
+    const int k = idx % KA, p = idx / KA;
+    const bf16_t v = f2bf(W[idx]);
+    Wp[idx] = v;
+    if (k >= d.KX) WhhT[(size_t)(k - d.KX) * G + p] = v;
+  }
+}
+
+void launch_lstm_pack_weights(const float* W, bf16_t* Wp, bf16_t* WhhT, LstmDims d, hipStream_t s) {
+  const long total = (long)4 * d.H * (d.KX + d.H);
+  int blocks = (int)((total + 255) / 256);
+  if (blocks > 4096) blocks = 4096;
+  hipLaunchKernelGGL(lstm_pack_weights_kernel, dim3(blocks), dim3(256), 0, s, W, Wp, WhhT, d);
+}
+
+}  // namespace wf

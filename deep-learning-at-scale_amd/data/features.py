@@ -1,0 +1,194 @@
+"""Feature engineering that replaces the reference's Spark ML pipeline (cnn.py:68-107).
+
+Reference stages and their semantics kept here:
+
+* ``randomSplit([0.64, 0.16, 0.2])`` (cnn.py:68) — per-row uniform draw against the
+  normalised cumulative weights; now SEEDED (defect A.1#10).
+* ``StringIndexer`` per categorical column (cnn.py:75) — labels ordered by frequency,
+  descending, ties alphabetical (Spark >= 3 ``frequencyDesc``).
+* multi-column ``OneHotEncoder`` (cnn.py:77-80) — ``dropLast=True``: the last category
+  index encodes to the all-zero vector.
+* ``VectorAssembler`` (cnn.py:82-85, 96-103) — ``[one-hot blocks in indexer order,
+  continuous columns in schema order]``.
+
+Fixes of reference defects: the pipeline is fitted on the
+TRAINING split only and applied to all three (#3 — the reference refits per split, so
+category indices disagree between splits); the target is excluded from the features
+(#4); unseen labels at transform time map to an extra "unknown" index (handleInvalid
+``keep``) instead of aborting the job. Continuous columns are standardised with train
+statistics (the reference fed raw magnitudes; standardisation is optional).
+"""
+from __future__ import annotations
+
+import dataclasses
+from collections import Counter
+
+import numpy as np
+
+from .schema import Schema
+
+
+def random_split(n: int, weights=(0.64, 0.16, 0.2), seed: int = 42):
+    """Row indices of each split (Spark randomSplit semantics, seeded)."""
+    w = np.asarray(weights, dtype=np.float64)
+    if np.any(w < 0) or w.sum() <= 0:
+        raise ValueError("split weights must be non-negative with a positive sum")
+    bounds = np.cumsum(w / w.sum())
+    u = np.random.default_rng(seed).random(n)
+    which = np.searchsorted(bounds, u, side="right")
+    which = np.minimum(which, len(w) - 1)
+    return [np.nonzero(which == k)[0] for k in range(len(w))]
+
+
+@dataclasses.dataclass
+class StringIndexer:
+    column: str
+    labels: list = dataclasses.field(default_factory=list)
+    handle_invalid: str = "keep"  # 'keep' | 'error' | 'skip'(treated as keep for arrays)
+
+    def fit(self, values) -> "StringIndexer":
+        cnt = Counter(str(v) for v in values)
+        self.labels = [k for k, _ in sorted(cnt.items(), key=lambda kv: (-kv[1], kv[0]))]
+        return self
+
+    def transform(self, values) -> np.ndarray:
+        lut = {k: i for i, k in enumerate(self.labels)}
+        out = np.empty(len(values), dtype=np.int64)
+        unk = len(self.labels)
+        for i, v in enumerate(values):
+            j = lut.get(str(v))
+            if j is None:
+                if self.handle_invalid == "error":
+                    raise ValueError(f"unseen label {v!r} in column {self.column!r}")
+                j = unk
+            out[i] = j
+        return out
+
+    @property
+    def num_categories(self) -> int:
+        return len(self.labels) + (1 if self.handle_invalid != "error" else 0)
+
+
+def one_hot(idx: np.ndarray, num_categories: int, drop_last: bool = True) -> np.ndarray:
+    size = num_categories - 1 if drop_last else num_categories
+    out = np.zeros((len(idx), max(size, 0)), dtype=np.float32)
+    ok = idx < size
+    out[np.nonzero(ok)[0], idx[ok]] = 1.0
+    return out
+
+
+@dataclasses.dataclass
+class FeaturePipeline:
+    """Fit on train, transform any split: table (dict of columns) -> (X [n, F], y [n])."""
+
+    schema: Schema
+    target: str
+    standardize: bool = True
+    drop_last: bool = True
+    indexers: list = dataclasses.field(default_factory=list)
+    mean: np.ndarray | None = None
+    std: np.ndarray | None = None
+    y_mean: float = 0.0
+    y_std: float = 1.0
+    standardize_target: bool = False
+
+    @property
+    def categorical(self):
+        return self.schema.categorical(exclude=(self.target,))
+
+    @property
+    def continuous(self):
+        return self.schema.continuous(exclude=(self.target,))
+
+    def fit(self, table: dict) -> "FeaturePipeline":
+        if self.target not in self.schema.names:
+            raise ValueError(f"target column {self.target!r} not in schema {self.schema.names}")
+        self.indexers = [StringIndexer(c).fit(table[c]) for c in self.categorical]
+        X = self._assemble(table)
+        if self.standardize and X.shape[1]:
+            self.mean = X.mean(axis=0)
+            self.std = X.std(axis=0)
+            self.std[self.std < 1e-8] = 1.0
+        y = self.target_values(table, raw=True)
+        if self.standardize_target and len(y):
+            self.y_mean, self.y_std = float(y.mean()), float(y.std() or 1.0)
+        return self
+
+    def _assemble(self, table: dict) -> np.ndarray:
+        n = len(table[self.schema.names[0]])
+        blocks = [one_hot(ix.transform(table[ix.column]), ix.num_categories, self.drop_last)
+                  for ix in self.indexers]
+        for c in self.continuous:
+            blocks.append(np.asarray(table[c], dtype=np.float32).reshape(n, 1))
+        return np.concatenate(blocks, axis=1) if blocks else np.zeros((n, 0), np.float32)
+
+    def target_values(self, table: dict, raw: bool = False) -> np.ndarray:
+        f = self.schema[self.target]
+        if not f.is_numeric:
+            # regression target must be numeric (defect A.1#5: the reference built a
+            # StringIndexer for it and never used it); try a float parse.
+            y = np.asarray([float(v) for v in table[self.target]], dtype=np.float32)
+        else:
+            y = np.asarray(table[self.target], dtype=np.float32)
+        if raw or not self.standardize_target:
+            return y
+        return ((y - self.y_mean) / self.y_std).astype(np.float32)
+
+    def transform(self, table: dict):
+        X = self._assemble(table)
+        if self.standardize and self.mean is not None:
+            nc = len(self.continuous)
+            # one-hot blocks are left as 0/1; only continuous columns are scaled
+            if nc:
+                X[:, -nc:] = (X[:, -nc:] - self.mean[-nc:]) / self.std[-nc:]
+        return X.astype(np.float32), self.target_values(table)
+
+    def inverse_target(self, y):
+        return y * self.y_std + self.y_mean if self.standardize_target else y
+
+    @property
+    def n_features(self) -> int:
+        return sum(max(ix.num_categories - (1 if self.drop_last else 0), 0) for ix in self.indexers) + len(
+            self.continuous)
+
+    def state(self) -> dict:
+        return {
+            "target": self.target,
+            "categorical": {ix.column: ix.labels for ix in self.indexers},
+            "mean": None if self.mean is None else self.mean.tolist(),
+            "std": None if self.std is None else self.std.tolist(),
+            "y_mean": self.y_mean,
+            "y_std": self.y_std,
+            "standardize_target": self.standardize_target,
+            "drop_last": self.drop_last,
+        }
+
+
+def take(table: dict, idx) -> dict:
+    return {k: np.asarray(v)[idx] for k, v in table.items()}
+
+
+def make_windows(X: np.ndarray, y: np.ndarray, T: int, groups=None, stride: int = 1):
+    """Sliding windows for sequence models: (X_w [n, T, F], y_w [n]) with y at the last step.
+
+    ``groups`` (per-row series id, rows already in time order inside a group) keeps
+    windows from crossing series boundaries.
+    """
+    n = len(X)
+    if groups is None:
+        groups = np.zeros(n, dtype=np.int64)
+    starts = []
+    g = np.asarray(groups)
+    i = 0
+    while i < n:
+        j = i
+        while j < n and g[j] == g[i]:
+            j += 1
+        for s in range(i, j - T + 1, stride):
+            starts.append(s)
+        i = j
+    starts = np.asarray(starts, dtype=np.int64)
+    if len(starts) == 0:
+        return np.zeros((0, T, X.shape[1]), np.float32), np.zeros((0,), np.float32)
+    idx = starts[:, None] + np.arange(T)[None, :]
+    return X[idx].astype(np.float32), y[starts + T - 1].astype(np.float32)

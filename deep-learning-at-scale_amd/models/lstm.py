@@ -1,0 +1,229 @@
+"""LSTM time-series regression (README "LSTM model", Readme.md:21; BASELINE.json:11 —
+seq-len 64, hidden 512, DP, bf16).
+
+Two implementations with one parameter layout:
+
+* :class:`LSTMRegressor` — plain PyTorch fp32 module (``nn.LSTM`` + linear head). It is
+  the CPU oracle for val-MSE parity and the reference for the kernel tests.
+* :class:`NativeLSTM` — the MI355X engine: one fused MFMA GEMM + cell kernel per
+  timestep forward, one fused GEMM + cell-backward kernel per timestep backward, and a
+  single split-K weight-gradient GEMM over all (t, b) (csrc/lstm.hip, csrc/gemm.hip).
+  Parameters live in a flat fp32 master buffer (so the optimizer and the DP all-reduce
+  are one launch / one collective each); bf16 shadows are repacked after every update.
+
+Flat layout (``LstmLayout``): ``[Wcat (4H x KA, gate-permuted rows) | w_out (H) | b_out (1)]``
+with ``Wcat = [W_ih | b_ih + b_hh | 0 ... | W_hh]`` (KA = KX + H, KX = 64-aligned, the
+bias rides on a constant-1 input column).
+"""
+from __future__ import annotations
+
+import dataclasses
+import math
+
+import torch
+from torch import nn
+
+
+def _round_up(x: int, m: int) -> int:
+    return (x + m - 1) // m * m
+
+
+@dataclasses.dataclass(frozen=True)
+class LstmLayout:
+    n_features: int
+    hidden: int
+
+    @property
+    def KX(self) -> int:
+        return _round_up(self.n_features + 1, 64)
+
+    @property
+    def KA(self) -> int:
+        return self.KX + self.hidden
+
+    @property
+    def G(self) -> int:
+        return 4 * self.hidden
+
+    @property
+    def w_size(self) -> int:
+        return self.G * self.KA
+
+    @property
+    def numel(self) -> int:
+        return _round_up(self.w_size + self.hidden + 1, 4)
+
+    def views(self, flat: torch.Tensor):
+        W = flat[: self.w_size].view(self.G, self.KA)
+        w_out = flat[self.w_size : self.w_size + self.hidden]
+        b_out = flat[self.w_size + self.hidden : self.w_size + self.hidden + 1]
+        return W, w_out, b_out
+
+    def perm(self) -> torch.Tensor:
+        """perm[p] = natural gate-row (gate*H + unit) stored at permuted row p."""
+        p = torch.arange(self.G)
+        unit = (p >> 6) * 16 + (p & 15)
+        gate = (p >> 4) & 3
+        return gate * self.hidden + unit
+
+
+class LSTMRegressor(nn.Module):
+    """fp32 reference: x [B, T, F] -> y [B] from the last hidden state."""
+
+    def __init__(self, n_features: int, hidden: int = 512):
+        super().__init__()
+        self.n_features = n_features
+        self.hidden = hidden
+        self.lstm = nn.LSTM(n_features, hidden, batch_first=True)
+        self.head = nn.Linear(hidden, 1)
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        out, _ = self.lstm(x)
+        return self.head(out[:, -1]).squeeze(-1)
+
+    # ---- flat-layout conversion (shared with NativeLSTM / checkpoints) ----
+    def to_flat(self) -> torch.Tensor:
+        lay = LstmLayout(self.n_features, self.hidden)
+        flat = torch.zeros(lay.numel, dtype=torch.float32)
+        W, w_out, b_out = lay.views(flat)
+        nat = torch.zeros(lay.G, lay.KA)
+        F, H = self.n_features, self.hidden
+        with torch.no_grad():
+            nat[:, :F] = self.lstm.weight_ih_l0.float().cpu()
+            nat[:, F] = (self.lstm.bias_ih_l0 + self.lstm.bias_hh_l0).float().cpu()
+            nat[:, lay.KX :] = self.lstm.weight_hh_l0.float().cpu()
+            W.copy_(nat[lay.perm()])
+            w_out.copy_(self.head.weight.view(-1).float().cpu())
+            b_out.copy_(self.head.bias.view(-1).float().cpu())
+        return flat
+
+    def load_flat(self, flat: torch.Tensor) -> None:
+        lay = LstmLayout(self.n_features, self.hidden)
+        W, w_out, b_out = lay.views(flat.detach().float().cpu())
+        nat = torch.empty_like(W)
+        nat[lay.perm()] = W
+        F = self.n_features
+        with torch.no_grad():
+            self.lstm.weight_ih_l0.copy_(nat[:, :F])
+            self.lstm.bias_ih_l0.copy_(nat[:, F])
+            self.lstm.bias_hh_l0.zero_()
+            self.lstm.weight_hh_l0.copy_(nat[:, lay.KX :])
+            self.head.weight.copy_(w_out.view(1, -1))
+            self.head.bias.copy_(b_out)
+
+
+def init_lstm_flat(n_features: int, hidden: int, seed: int = 0) -> torch.Tensor:
+    """PyTorch-default init (U(-1/sqrt(H), 1/sqrt(H))) in the flat layout."""
+    g = torch.Generator().manual_seed(seed)
+    lay = LstmLayout(n_features, hidden)
+    k = 1.0 / math.sqrt(hidden)
+    flat = torch.zeros(lay.numel)
+    W, w_out, b_out = lay.views(flat)
+    W[:, :n_features].uniform_(-k, k, generator=g)
+    W[:, n_features].uniform_(-2 * k, 2 * k, generator=g)  # b_ih + b_hh
+    W[:, lay.KX :].uniform_(-k, k, generator=g)
+    w_out.uniform_(-k, k, generator=g)
+    b_out.uniform_(-k, k, generator=g)
+    return flat
+
+
+class NativeLSTM:
+    """HIP/MFMA LSTM regression engine for a fixed (max) batch size.
+
+    ``params``/``grads`` are flat fp32 device buffers in :class:`LstmLayout` order;
+    call :meth:`sync_weights` after every change to ``params``.
+    """
+
+    def __init__(self, n_features: int, hidden: int, seq_len: int, batch: int,
+                 device="cuda", params: torch.Tensor | None = None,
+                 grads: torch.Tensor | None = None):
+        from ..ops.native import lib
+
+        self._C = lib()
+        self.lay = LstmLayout(n_features, hidden)
+        self.F, self.H, self.T, self.B = n_features, hidden, seq_len, batch
+        lay = self.lay
+        dev = torch.device(device)
+        self.device = dev
+        self.params = params if params is not None else torch.zeros(lay.numel, device=dev)
+        self.grads = grads if grads is not None else torch.zeros(lay.numel, device=dev)
+        bf = torch.bfloat16
+        T, B, H = seq_len, batch, hidden
+        self.XH = torch.zeros((T + 1) * B * lay.KA, dtype=bf, device=dev)
+        self.Cst = torch.zeros((T + 1) * B * H, dtype=torch.float32, device=dev)
+        self.S = torch.empty(T * B * lay.G, dtype=bf, device=dev)
+        self.DG = torch.empty(T * B * lay.G, dtype=bf, device=dev)
+        self.dcarry = torch.empty(B * H, dtype=torch.float32, device=dev)
+        self.Wp = torch.empty(lay.G * lay.KA, dtype=bf, device=dev)
+        self.WhhT = torch.empty(H * lay.G, dtype=bf, device=dev)
+        self.pred = torch.empty(B, dtype=torch.float32, device=dev)
+        self.dy = torch.empty(B, dtype=torch.float32, device=dev)
+        self.loss_sum = torch.zeros(1, dtype=torch.float32, device=dev)
+        self.sync_weights()
+
+    # ------------------------------------------------------------------ weights
+    def sync_weights(self) -> None:
+        W, _, _ = self.lay.views(self.params)
+        self._C.lstm_pack_weights(W, self.Wp, self.WhhT, self.H, self.lay.KX)
+
+    def _dims(self, B):
+        return (B, self.T, self.F, self.lay.KX, self.H)
+
+    def _hT(self, B):
+        lay = self.lay
+        base = self.T * self.B * lay.KA  # XH[T] starts here (row stride KA)
+        return self.XH[base + lay.KX : base + lay.KX + (B - 1) * lay.KA + self.H]
+
+    # ------------------------------------------------------------------ passes
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        """x: [B, T, F] fp32 (B <= max batch) -> predictions [B] (view of an internal buffer)."""
+        B = x.shape[0]
+        assert x.shape[1] == self.T and x.shape[2] == self.F and B <= self.B
+        x = x.contiguous().float()
+        # XH is laid out for the max batch B; a smaller batch uses the leading rows of
+        # every timestep slab only if B == self.B, so smaller batches run padded.
+        if B != self.B:
+            xp = torch.zeros(self.B, self.T, self.F, device=x.device)
+            xp[:B] = x
+            x = xp
+        C = self._C
+        C.lstm_pack_x(x, self.XH, *self._dims(self.B))
+        C.lstm_forward(self.XH, self.Wp, self.Cst, self.S, *self._dims(self.B))
+        _, w_out, b_out = self.lay.views(self.params)
+        C.head_fwd(self._hT(self.B), self.lay.KA, self.B, self.H, w_out, b_out, None, self.pred,
+                   None, None, 0.0)
+        return self.pred[:B]
+
+    def forward_backward(self, x: torch.Tensor, y: torch.Tensor, dy_scale: float,
+                         zero_grads: bool = True) -> torch.Tensor:
+        """One training forward + backward on a full batch; grads land in ``self.grads``.
+
+        ``dy_scale`` multiplies (pred - y): use 2 / global_batch for the mean-squared error
+        averaged over all data-parallel ranks. Returns the device scalar sum of squared
+        errors of this batch (no host sync).
+        """
+        B = self.B
+        assert x.shape == (B, self.T, self.F) and y.shape == (B,)
+        C = self._C
+        lay = self.lay
+        W, w_out, b_out = lay.views(self.params)
+        gW, gw_out, gb_out = lay.views(self.grads)
+        if zero_grads:
+            self.grads.zero_()
+        self.loss_sum.zero_()
+        C.lstm_pack_x(x.contiguous(), self.XH, *self._dims(B))
+        C.lstm_forward(self.XH, self.Wp, self.Cst, self.S, *self._dims(B))
+        hT = self._hT(B)
+        C.head_fwd(hT, lay.KA, B, self.H, w_out, b_out, y.contiguous(), self.pred, self.dy,
+                   self.loss_sum, float(dy_scale))
+        C.head_bwd_w(hT, lay.KA, B, self.H, self.dy, gw_out, gb_out)
+        C.lstm_backward(self.WhhT, self.XH, self.Cst, self.S, self.DG, self.dcarry, self.dy,
+                        w_out, *self._dims(B))
+        # dWcat = sum_{t,b} dG_t[b]^T [x_t | 1 | h_{t-1}][b]   (one split-K GEMM, K = T*B)
+        K = self.T * B
+        ksplit = max(1, min(64, K // 4096))
+        from ..ops.native import gemm
+
+        gemm(self.DG, self.XH, lay.G, lay.KA, K, a_mn=True, lda=lay.G, b_mn=True, ldb=lay.KA,
+             outF=gW, ldo=lay.KA, atomic=True, ksplit=ksplit)
+        return self.loss_sum

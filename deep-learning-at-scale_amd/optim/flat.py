@@ -1,0 +1,103 @@
+"""Optimizers over ONE flat fp32 master buffer.
+
+All parameters of a model are views into a single contiguous fp32 tensor and all
+gradients into a second one, so an update is one kernel launch (``adam`` / ``sgd`` in
+csrc/elementwise.hip) and the data-parallel reduction is one collective on one bucket.
+On CPU tensors the same math runs in PyTorch (this is the fp32 oracle path used by the
+CPU tests and the parity report — never a silent stand-in for a GPU op).
+"""
+from __future__ import annotations
+
+import torch
+
+
+class FlatAdam:
+    """Adam / AdamW (decoupled weight decay) with PyTorch's bias-correction semantics."""
+
+    def __init__(self, params: torch.Tensor, grads: torch.Tensor, lr: float = 1e-3,
+                 betas=(0.9, 0.999), eps: float = 1e-8, weight_decay: float = 0.0):
+        assert params.dtype == torch.float32 and params.shape == grads.shape
+        self.params, self.grads = params, grads
+        self.lr, self.betas, self.eps, self.weight_decay = lr, tuple(betas), eps, weight_decay
+        self.m = torch.zeros_like(params)
+        self.v = torch.zeros_like(params)
+        self.t = 0
+
+    def step(self, grad_scale: float = 1.0) -> None:
+        self.t += 1
+        b1, b2 = self.betas
+        bc1, bc2 = 1.0 - b1**self.t, 1.0 - b2**self.t
+        if self.params.is_cuda:
+            from ..ops.native import lib
+
+            lib().adam(self.params, self.grads, self.m, self.v, self.lr, b1, b2, self.eps,
+                       self.weight_decay, bc1, bc2, grad_scale)
+            return
+        g = self.grads * grad_scale
+        self.m.mul_(b1).add_(g, alpha=1 - b1)
+        self.v.mul_(b2).addcmul_(g, g, value=1 - b2)
+        upd = (self.m / bc1) / ((self.v / bc2).sqrt() + self.eps)
+        if self.weight_decay:
+            upd = upd + self.weight_decay * self.params
+        self.params.sub_(self.lr * upd)
+
+    def state_dict(self) -> dict:
+        return {"kind": "adam", "t": self.t, "m": self.m.detach().cpu(), "v": self.v.detach().cpu(),
+                "lr": self.lr, "betas": list(self.betas), "eps": self.eps,
+                "weight_decay": self.weight_decay}
+
+    def load_state_dict(self, sd: dict) -> None:
+        self.t = int(sd["t"])
+        self.m.copy_(sd["m"])
+        self.v.copy_(sd["v"])
+        self.lr, self.betas, self.eps = sd["lr"], tuple(sd["betas"]), sd["eps"]
+        self.weight_decay = sd["weight_decay"]
+
+
+class FlatSGD:
+    """Keras-0.x SGD (cnn.py:117: lr=0.001, momentum=0.99, decay=1e-6, nesterov=True).
+
+    lr_t = lr / (1 + decay * iterations); v = mu*v - lr_t*g;
+    p += mu*v - lr_t*g (Nesterov) else p += v.
+    """
+
+    def __init__(self, params: torch.Tensor, grads: torch.Tensor, lr: float = 0.001,
+                 momentum: float = 0.99, decay: float = 1e-6, nesterov: bool = True):
+        self.params, self.grads = params, grads
+        self.lr, self.momentum, self.decay, self.nesterov = lr, momentum, decay, nesterov
+        self.vel = torch.zeros_like(params)
+        self.iterations = 0
+
+    def step(self, grad_scale: float = 1.0) -> None:
+        lr_t = self.lr / (1.0 + self.decay * self.iterations)
+        self.iterations += 1
+        if self.params.is_cuda:
+            from ..ops.native import lib
+
+            lib().sgd(self.params, self.grads, self.vel, lr_t, self.momentum, self.nesterov, grad_scale)
+            return
+        g = self.grads * grad_scale
+        self.vel.mul_(self.momentum).sub_(lr_t * g)
+        if self.nesterov:
+            self.params.add_(self.momentum * self.vel - lr_t * g)
+        else:
+            self.params.add_(self.vel)
+
+    def state_dict(self) -> dict:
+        return {"kind": "sgd", "iterations": self.iterations, "vel": self.vel.detach().cpu(),
+                "lr": self.lr, "momentum": self.momentum, "decay": self.decay,
+                "nesterov": self.nesterov}
+
+    def load_state_dict(self, sd: dict) -> None:
+        self.iterations = int(sd["iterations"])
+        self.vel.copy_(sd["vel"])
+        self.lr, self.momentum, self.decay, self.nesterov = sd["lr"], sd["momentum"], sd["decay"], sd["nesterov"]
+
+
+def make_optimizer(name: str, params, grads, **kw):
+    name = name.lower()
+    if name in ("adam", "adamw"):
+        return FlatAdam(params, grads, **kw)
+    if name in ("sgd", "sgd_nesterov"):
+        return FlatSGD(params, grads, **kw)
+    raise ValueError(f"unknown optimizer {name!r}")

@@ -1,0 +1,132 @@
+"""Data-parallel runtime: one process per GPU, RCCL over xGMI (gloo on CPU).
+
+Replaces the reference's Spark/Hadoop layer (cnn.py:49 SparkSession; Readme.md:3) — the
+reference has NO gradient communication at all. Call sites (§2.5 [design]):
+
+  C1 ``broadcast_``      parameters from rank 0 once at start (identical init)
+  C2 ``all_reduce_sum_`` the flat gradient bucket, once per step
+  C3 ``all_reduce_sum_`` [loss_sum, count] per eval so early stopping agrees on all ranks
+  C4 ``barrier``         around rank-0 checkpoint writes
+  C5 ``broadcast_object`` feature vocabularies fitted on rank 0
+
+Bucket policy for MI355X: every model here is <= ~1.2 M parameters (4.7 MB fp32), far
+below the size where splitting the bucket to overlap with backward pays on a 7-link
+xGMI mesh (a 4.7 MB ring all-reduce at 8 ranks is ~7-50 us, versus a ~10-30 us RCCL
+launch/protocol floor): ONE flat bucket per step is the latency-optimal choice. Larger
+models can set ``bucket_bytes`` to split the flat buffer into equal chunks that are
+reduced back-to-back on a side stream (see :meth:`all_reduce_sum_`).
+"""
+from __future__ import annotations
+
+import datetime
+import os
+
+import torch
+import torch.distributed as dist
+
+
+class DistContext:
+    def __init__(self, rank: int = 0, world_size: int = 1, local_rank: int = 0,
+                 device: torch.device | None = None, backend: str | None = None,
+                 bucket_bytes: int = 0):
+        self.rank, self.world_size, self.local_rank = rank, world_size, local_rank
+        self.device = device or torch.device("cpu")
+        self.backend = backend
+        self.bucket_bytes = bucket_bytes
+
+    # ---------------------------------------------------------------- bootstrap
+    @classmethod
+    def from_env(cls, backend: str | None = None, timeout_s: float = 600.0,
+                 bucket_bytes: int = 0, device: str | None = None) -> "DistContext":
+        """Read torchrun's RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* and init the group.
+
+        Device selection happens BEFORE any CUDA call so each rank pins its own GPU.
+        """
+        world = int(os.environ.get("WORLD_SIZE", "1"))
+        rank = int(os.environ.get("RANK", "0"))
+        local = int(os.environ.get("LOCAL_RANK", "0"))
+        if device is None:
+            use_gpu = torch.cuda.is_available()
+        else:
+            use_gpu = device.startswith("cuda")
+        if use_gpu:
+            torch.cuda.set_device(local)
+            dev = torch.device("cuda", local)
+        else:
+            dev = torch.device("cpu")
+        if world > 1 and not dist.is_initialized():
+            backend = backend or ("nccl" if use_gpu else "gloo")
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            kw = dict(backend=backend, rank=rank, world_size=world,
+                      timeout=datetime.timedelta(seconds=timeout_s))
+            if backend == "nccl":
+                kw["device_id"] = dev
+            dist.init_process_group(**kw)
+        return cls(rank, world, local, dev, backend, bucket_bytes)
+
+    @property
+    def is_main(self) -> bool:
+        return self.rank == 0
+
+    @property
+    def distributed(self) -> bool:
+        return self.world_size > 1 and dist.is_initialized()
+
+    # ---------------------------------------------------------------- collectives
+    def broadcast_(self, t: torch.Tensor, src: int = 0) -> torch.Tensor:
+        if self.distributed:
+            dist.broadcast(t, src=src)
+        return t
+
+    def all_reduce_sum_(self, t: torch.Tensor) -> torch.Tensor:
+        if not self.distributed:
+            return t
+        if self.bucket_bytes and t.numel() * t.element_size() > self.bucket_bytes:
+            n = max(1, self.bucket_bytes // t.element_size())
+            works = [dist.all_reduce(t[i : i + n], async_op=True) for i in range(0, t.numel(), n)]
+            for w in works:
+                w.wait()
+        else:
+            dist.all_reduce(t)
+        return t
+
+    def all_reduce_avg_(self, t: torch.Tensor) -> torch.Tensor:
+        self.all_reduce_sum_(t)
+        if self.distributed:
+            t.div_(self.world_size)
+        return t
+
+    def max_scalar(self, x: float) -> float:
+        if not self.distributed:
+            return float(x)
+        t = torch.tensor([float(x)], dtype=torch.float64, device=self._coll_device())
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item())
+
+    def sum_scalars(self, *xs: float) -> list:
+        if not self.distributed:
+            return [float(x) for x in xs]
+        t = torch.tensor([float(x) for x in xs], dtype=torch.float64, device=self._coll_device())
+        dist.all_reduce(t)
+        return [float(v) for v in t.tolist()]
+
+    def broadcast_object(self, obj, src: int = 0):
+        if not self.distributed:
+            return obj
+        box = [obj]
+        dist.broadcast_object_list(box, src=src)
+        return box[0]
+
+    def barrier(self) -> None:
+        if self.distributed:
+            if self.backend == "nccl":
+                dist.barrier(device_ids=[self.local_rank])
+            else:
+                dist.barrier()
+
+    def shutdown(self) -> None:
+        if dist.is_initialized():
+            dist.destroy_process_group()
+
+    def _coll_device(self):
+        return self.device if self.backend == "nccl" else torch.device("cpu")

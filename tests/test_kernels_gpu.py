@@ -1,0 +1,186 @@
+"""Kernel numerics on a real MI355X: every HIP op against a plain PyTorch fp32 reference.
+
+GEMM checks use ASYMMETRIC operands and odd shapes (cdna_hip_programming.md §3: an
+A = I / symmetric-B check hides a transposed C write).
+"""
+import math
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+
+
+def _bf(x):
+    return x.to(torch.bfloat16)
+
+
+def _ref_gemm(A, B):  # A [M,K], B [N,K] logical, bf16 values in fp32 math
+    return A.float() @ B.float().t()
+
+
+@pytest.mark.parametrize("a_mn", [False, True])
+@pytest.mark.parametrize("b_mn", [False, True])
+@pytest.mark.parametrize("shape", [(128, 128, 64), (200, 72, 136), (256, 384, 512), (64, 8, 1000)])
+def test_gemm_layouts(a_mn, b_mn, shape):
+    from wellflow.ops.native import gemm
+
+    M, N, K = shape
+    if a_mn and M % 8:
+        pytest.skip("MN-contiguous needs M % 8 == 0")
+    torch.manual_seed(0)
+    A = _bf(torch.randn(M, K, device=DEV) + 0.1 * torch.arange(K, device=DEV) / K)
+    B = _bf(torch.randn(N, K, device=DEV) * torch.linspace(0.5, 2.0, N, device=DEV)[:, None])
+    Ast = A.t().contiguous() if a_mn else A
+    Bst = B.t().contiguous() if b_mn else B
+    out = torch.empty(M, N, device=DEV)
+    gemm(Ast, Bst, M, N, K, a_mn=a_mn, b_mn=b_mn, outF=out)
+    torch.cuda.synchronize()
+    ref = _ref_gemm(A, B)
+    err = (out - ref).abs().max().item()
+    assert err <= 1e-3 * ref.abs().max().item() + 1e-3, err
+
+
+def test_gemm_identity_asymmetric():
+    from wellflow.ops.native import gemm
+
+    M = N = K = 128
+    A = _bf(torch.eye(M, device=DEV))
+    Bm = _bf(torch.arange(N * K, device=DEV, dtype=torch.float32).view(N, K) % 97 - 48)
+    out = torch.empty(M, N, device=DEV)
+    gemm(A, Bm, M, N, K, outF=out)
+    torch.cuda.synchronize()
+    assert torch.equal(out, Bm.float().t())
+
+
+def test_gemm_epilogue_bias_relu_colsum_bf16():
+    from wellflow.ops.native import gemm
+
+    M, N, K = 300, 256, 40
+    torch.manual_seed(1)
+    A, B = _bf(torch.randn(M, K, device=DEV)), _bf(torch.randn(N, K, device=DEV))
+    bias = torch.randn(N, device=DEV)
+    outH = torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
+    cs = torch.zeros(N, device=DEV)
+    gemm(A, B, M, N, K, outH=outH, bias=bias, act=1, colsum=cs)
+    torch.cuda.synchronize()
+    ref = torch.relu(_ref_gemm(A, B) + bias)
+    assert (outH.float() - ref).abs().max().item() < 0.05 * ref.abs().max().item()
+    assert torch.allclose(cs, ref.sum(0), rtol=2e-2, atol=1e-1)
+
+
+def test_gemm_mask_and_splitk_atomic():
+    from wellflow.ops.native import gemm
+
+    M, N, K = 256, 256, 4096
+    torch.manual_seed(2)
+    A, B = _bf(torch.randn(M, K, device=DEV)), _bf(torch.randn(N, K, device=DEV))
+    out = torch.zeros(M, N, device=DEV)
+    gemm(A.t().contiguous(), B.t().contiguous(), M, N, K, a_mn=True, b_mn=True, outF=out,
+         atomic=True, ksplit=8, alpha=0.5)
+    mask = _bf(torch.randn(M, N, device=DEV))
+    outm = torch.empty(M, N, device=DEV)
+    gemm(A, B, M, N, K, outF=outm, mask=mask, mask_scale=2.0)
+    torch.cuda.synchronize()
+    ref = _ref_gemm(A, B)
+    assert torch.allclose(out, 0.5 * ref, rtol=1e-3, atol=5e-2)
+    refm = torch.where(mask.float() > 0, 2.0 * ref, torch.zeros_like(ref))
+    assert torch.allclose(outm, refm, rtol=1e-3, atol=5e-2)
+
+
+def test_lstm_forward_backward_matches_torch():
+    from wellflow.models.lstm import LSTMRegressor, LstmLayout, NativeLSTM
+
+    torch.manual_seed(3)
+    F, H, T, B = 9, 128, 12, 96
+    ref = LSTMRegressor(F, H).to(DEV)
+    x = torch.randn(B, T, F, device=DEV)
+    y = torch.randn(B, device=DEV)
+    eng = NativeLSTM(F, H, T, B, device=DEV)
+    eng.params.copy_(ref.to_flat().to(DEV))
+    eng.sync_weights()
+
+    pred = eng.forward(x).clone()
+    rp = ref(x)
+    assert (pred - rp).abs().max().item() < 3e-2, (pred - rp).abs().max().item()
+
+    loss_sum = eng.forward_backward(x, y, dy_scale=2.0 / B)
+    torch.cuda.synchronize()
+    loss = ((rp - y) ** 2).mean()
+    assert abs(loss_sum.item() / B - loss.item()) < 2e-2 * loss.item() + 1e-3
+    ref.zero_grad()
+    loss.backward()
+    # reference grads in flat layout
+    lay = LstmLayout(F, H)
+    gref = torch.zeros(lay.numel, device=DEV)
+    W, w_out, b_out = lay.views(gref)
+    nat = torch.zeros(lay.G, lay.KA, device=DEV)
+    nat[:, :F] = ref.lstm.weight_ih_l0.grad
+    nat[:, F] = ref.lstm.bias_ih_l0.grad
+    nat[:, lay.KX:] = ref.lstm.weight_hh_l0.grad
+    W.copy_(nat[lay.perm().to(DEV)])
+    w_out.copy_(ref.head.weight.grad.view(-1))
+    b_out.copy_(ref.head.bias.grad)
+    g = eng.grads
+    rel = (g - gref).norm() / gref.norm()
+    assert rel.item() < 3e-2, rel.item()
+    cos = torch.nn.functional.cosine_similarity(g, gref, dim=0)
+    assert cos.item() > 0.999
+
+
+def test_adam_and_sgd_match_reference():
+    from wellflow.ops.native import lib
+
+    C = lib()
+    n = 1001
+    torch.manual_seed(4)
+    p = torch.randn(n, device=DEV)
+    g = torch.randn(n, device=DEV)
+    m = torch.zeros(n, device=DEV)
+    v = torch.zeros(n, device=DEV)
+    pr = p.clone().requires_grad_(True)
+    opt = torch.optim.Adam([pr], lr=1e-3)
+    for step in range(1, 4):
+        C.adam(p, g, m, v, 1e-3, 0.9, 0.999, 1e-8, 0.0, 1 - 0.9 ** step, 1 - 0.999 ** step, 1.0)
+        pr.grad = g.clone()
+        opt.step()
+    torch.cuda.synchronize()
+    assert torch.allclose(p, pr.detach(), atol=1e-6)
+    # Keras-0.x Nesterov SGD
+    p2, vel = torch.randn(n, device=DEV), torch.zeros(n, device=DEV)
+    pc, vc = p2.clone(), vel.clone()
+    for it in range(3):
+        lr_t = 0.01 / (1 + 1e-6 * it)
+        C.sgd(p2, g, vel, lr_t, 0.99, True, 1.0)
+        vc = 0.99 * vc - lr_t * g
+        pc = pc + 0.99 * vc - lr_t * g
+    torch.cuda.synchronize()
+    assert torch.allclose(p2, pc, atol=1e-6)
+
+
+def test_losses():
+    from wellflow.ops.native import lib
+
+    C = lib()
+    B, O = 37, 12
+    torch.manual_seed(5)
+    pred = torch.randn(B, O, device=DEV) * 5
+    y = torch.randn(B, O, device=DEV) * 5
+    for kind in (0, 1):
+        ls = torch.zeros(1, device=DEV)
+        d = torch.empty(B, O, dtype=torch.bfloat16, device=DEV)
+        cs = torch.zeros(O, device=DEV)
+        scale = 1.0 / (B * O)
+        C.loss(kind, pred, y, B, O, 6.0, scale, ls, d, cs)
+        pr = pred.clone().requires_grad_(True)
+        if kind == 0:
+            L = ((pr - y) ** 2).sum()
+        else:
+            L = torch.clamp((y - pr).abs(), 0, 6).sum()
+        L.backward()
+        torch.cuda.synchronize()
+        assert abs(ls.item() - L.item()) < 1e-3 * abs(L.item()) + 1e-3
+        assert torch.allclose(d.float(), pr.grad * scale, rtol=1e-2, atol=1e-4)
+        assert torch.allclose(cs, (pr.grad * scale).sum(0), rtol=1e-2, atol=1e-4)
