@@ -55,8 +55,6 @@ def _torch_flags():
         f"-D_GLIBCXX_USE_CXX11_ABI={int(torch.compiled_with_cxx11_abi())}",
         f"-I{sysconfig.get_paths()['include']}",
     ]
-    except Exception:  # pragma: no cover - older torch
-        pass
     libdir = os.path.join(os.path.dirname(torch.__file__), "lib")
     ldflags = [
         f"-L{libdir}",
