@@ -60,10 +60,10 @@ def main() -> int:
     # synthetic well-log windows (Gilbert-consistent targets), resident on the GPU
     x, y = synth_lstm_batch(B, T, F, seed=rank)
     x, y = x.to(dev), y.to(dev)
-    dy_scale = 2.0 / (B * world)
+    grad_scale = 1.0 / (B * world)
 
     def step():
-        eng.forward_backward(x, y, dy_scale)
+        eng.forward_backward(x, y, grad_scale)
         ctx.all_reduce_sum_(eng.grads)  # C2: one flat bucket over RCCL / xGMI
         opt.step()
         eng.sync_weights()

@@ -93,7 +93,9 @@ wf::LstmDims lstm_dims(int64_t B, int64_t T, int64_t F, int64_t KX, int64_t H) {
   TORCH_CHECK(B > 0 && T > 0 && H > 0, "lstm: bad dims");
   TORCH_CHECK(H % 128 == 0, "lstm: hidden size must be a multiple of 128");
   TORCH_CHECK(KX % 64 == 0 && F + 1 <= KX, "lstm: KX must be a multiple of 64 and > F");
-  return wf::LstmDims{(int)B, (int)T, (int)F, (int)KX, (int)H};
+  wf::LstmDims d;
+  d.B = (int)B; d.T = (int)T; d.F = (int)F; d.KX = (int)KX; d.H = (int)H;
+  return d;
 }
 
 void check_lstm_state(const at::Tensor& XH, const at::Tensor& Cst, const at::Tensor& S,
@@ -119,8 +121,10 @@ void lstm_pack_x(const at::Tensor& x, const at::Tensor& XH, int64_t B, int64_t T
 }
 
 void lstm_forward(const at::Tensor& XH, const at::Tensor& Wp, const at::Tensor& Cst,
-                  const at::Tensor& S, int64_t B, int64_t T, int64_t F, int64_t KX, int64_t H) {
+                  const at::Tensor& S, int64_t B, int64_t T, int64_t F, int64_t KX, int64_t H,
+                  int64_t variant) {
   auto d = lstm_dims(B, T, F, KX, H);
+  d.fwd_variant = (int)variant;
   check_lstm_state(XH, Cst, S, d);
   check_t(Wp, at::kBFloat16, "Wp");
   check_extent(Wp, 4 * H * (KX + H), "Wp");
@@ -132,8 +136,9 @@ void lstm_forward(const at::Tensor& XH, const at::Tensor& Wp, const at::Tensor& 
 void lstm_backward(const at::Tensor& WhhT, const at::Tensor& XH, const at::Tensor& Cst,
                    const at::Tensor& S, const at::Tensor& DG, const at::Tensor& dcarry,
                    const at::Tensor& dy, const at::Tensor& w_out, int64_t B, int64_t T, int64_t F,
-                   int64_t KX, int64_t H) {
+                   int64_t KX, int64_t H, int64_t variant) {
   auto d = lstm_dims(B, T, F, KX, H);
+  d.bwd_variant = (int)variant;
   check_lstm_state(XH, Cst, S, d);
   check_t(WhhT, at::kBFloat16, "WhhT");
   check_extent(WhhT, H * 4 * H, "WhhT");
@@ -222,7 +227,8 @@ void head_bwd_x(const at::Tensor& Hm, int64_t ldh, int64_t B, int64_t Hd, const 
 
 void loss(int64_t kind, const at::Tensor& pred, const at::Tensor& y, int64_t B, int64_t O,
           double clip, double scale, c10::optional<at::Tensor> loss_sum,
-          c10::optional<at::Tensor> dpred, c10::optional<at::Tensor> colsum) {
+          c10::optional<at::Tensor> dpred, c10::optional<at::Tensor> dpredF,
+          c10::optional<at::Tensor> colsum) {
   TORCH_CHECK(kind == 0 || kind == 1, "loss: kind 0 (mse) or 1 (mae_clip)");
   check_t(pred, at::kFloat, "pred");
   check_t(y, at::kFloat, "y");
@@ -232,6 +238,7 @@ void loss(int64_t kind, const at::Tensor& pred, const at::Tensor& y, int64_t B, 
   wf::launch_loss((int)kind, fp(pred), fp(y), (int)B, (int)O, (float)clip, (float)scale,
                   opt_ptr<float>(loss_sum, at::kFloat, "loss_sum", 1),
                   opt_ptr<bf16_t>(dpred, at::kBFloat16, "dpred", B * O),
+                  opt_ptr<float>(dpredF, at::kFloat, "dpredF", B * O),
                   opt_ptr<float>(colsum, at::kFloat, "colsum", O), cur_stream());
 }
 

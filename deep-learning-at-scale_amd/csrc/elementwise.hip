@@ -128,6 +128,7 @@ __global__ __launch_bounds__(256) void loss_kernel(int kind, const float* __rest
                                                    float clip, float scale,
                                                    float* __restrict__ loss_sum,
                                                    bf16_t* __restrict__ dpred,
+                                                   float* __restrict__ dpredF,
                                                    float* __restrict__ colsum) {
   __shared__ float red[4];
   const long total = (long)B * O;
@@ -148,6 +149,7 @@ __global__ __launch_bounds__(256) void loss_kernel(int kind, const float* __rest
     ls += l;
     d *= scale;
     if (dpred != nullptr) dpred[i] = f2bf(d);
+    if (dpredF != nullptr) dpredF[i] = d;
     if (colsum != nullptr) atomicAdd(colsum + (i % O), d);
   }
   const float s = block_sum<256>(ls, red);
@@ -155,13 +157,13 @@ __global__ __launch_bounds__(256) void loss_kernel(int kind, const float* __rest
 }
 
 void launch_loss(int kind, const float* pred, const float* y, int B, int O, float clip, float scale,
-                 float* loss_sum, bf16_t* dpred, float* colsum, hipStream_t s) {
+                 float* loss_sum, bf16_t* dpred, float* dpredF, float* colsum, hipStream_t s) {
   const long total = (long)B * O;
   int blocks = (int)((total + 255) / 256);
   if (blocks > 1024) blocks = 1024;
   if (blocks < 1) blocks = 1;
   hipLaunchKernelGGL(loss_kernel, dim3(blocks), dim3(256), 0, s, kind, pred, y, B, O, clip, scale,
-                     loss_sum, dpred, colsum);
+                     loss_sum, dpred, dpredF, colsum);
 }
 
 // ---------------------------------------------------------------- optimizers

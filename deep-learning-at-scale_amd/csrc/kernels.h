@@ -30,6 +30,8 @@ void launch_gemm(const bf16_t* A, long lda, int a_mn, const bf16_t* B, long ldb,
 // ---- LSTM (single layer, batch-first input, seq-to-one regression) ----
 struct LstmDims {
   int B, T, F, KX, H;  // G = 4H, KA = KX + H
+  int fwd_variant = 0;  // tile shape of the forward step GEMM (0: 128x128, 1: 64x128, 2: 256x128)
+  int bwd_variant = 0;  // backward step GEMM (0: 128x128, 1: 64x128, 2: 128x64, 3: 64x64)
 };
 void launch_lstm_pack_x(const float* x, bf16_t* XH, LstmDims d, hipStream_t s);
 void launch_lstm_fwd_step(int t, bf16_t* XH, const bf16_t* Wp, float* Cst, bf16_t* S,
@@ -50,7 +52,7 @@ void launch_head_bwd_x(const bf16_t* Hm, long ldh, int B, int Hd, const float* d
                        int relu_mask, bf16_t* dz, long ldz, float* colsum, hipStream_t s);
 // kind 0 = MSE, 1 = clipped MAE (reference mae_clip)
 void launch_loss(int kind, const float* pred, const float* y, int B, int O, float clip, float scale,
-                 float* loss_sum, bf16_t* dpred, float* colsum, hipStream_t s);
+                 float* loss_sum, bf16_t* dpred, float* dpredF, float* colsum, hipStream_t s);
 
 // ---- optimizers and casts over flat fp32 buffers ----
 void launch_adam(float* p, const float* g, float* m, float* v, long n, float lr, float b1,

@@ -47,13 +47,12 @@ void launch_lstm_pack_x(const float* x, bf16_t* XH, LstmDims d, hipStream_t s) {
   hipLaunchKernelGGL(lstm_pack_x_kernel, dim3(blocks), dim3(256), 0, s, x, XH, d);
 }
 
-using LstmCfg = GemmCfg<128, 128, K_CONTIG, K_CONTIG>;
-
+template <int BM>
 __global__ __launch_bounds__(256) void lstm_fwd_step_kernel(int t, bf16_t* __restrict__ XH,
                                                             const bf16_t* __restrict__ Wp,
                                                             float* __restrict__ Cst,
                                                             bf16_t* __restrict__ S, LstmDims d) {
-  using C = LstmCfg;
+  using C = GemmCfg<BM, 128, K_CONTIG, K_CONTIG>;  // wave N tile = 64 = 4 gates x 16 units
   __shared__ __attribute__((aligned(16))) char smem[C::LDS_BYTES];
   const int KA = d.KX + d.H, G = 4 * d.H;
   const int tiles_n = G / C::BN;
@@ -94,11 +93,20 @@ __global__ __launch_bounds__(256) void lstm_fwd_step_kernel(int t, bf16_t* __res
   }
 }
 
+template <int BM>
+static void fwd_cfg(int t, bf16_t* XH, const bf16_t* Wp, float* Cst, bf16_t* S, LstmDims d,
+                    hipStream_t s) {
+  const int tiles = ((d.B + BM - 1) / BM) * (4 * d.H / 128);
+  hipLaunchKernelGGL((lstm_fwd_step_kernel<BM>), dim3(tiles), dim3(256), 0, s, t, XH, Wp, Cst, S, d);
+}
+
 void launch_lstm_fwd_step(int t, bf16_t* XH, const bf16_t* Wp, float* Cst, bf16_t* S,
                           LstmDims d, hipStream_t s) {
-  const int G = 4 * d.H;
-  const int tiles = ((d.B + LstmCfg::BM - 1) / LstmCfg::BM) * (G / LstmCfg::BN);
-  hipLaunchKernelGGL(lstm_fwd_step_kernel, dim3(tiles), dim3(256), 0, s, t, XH, Wp, Cst, S, d);
+  switch (d.fwd_variant) {
+    case 1: fwd_cfg<64>(t, XH, Wp, Cst, S, d, s); break;
+    case 2: fwd_cfg<256>(t, XH, Wp, Cst, S, d, s); break;
+    default: fwd_cfg<128>(t, XH, Wp, Cst, S, d, s); break;
+  }
 }
 
 // Cell backward for one (row m, unit u) of step t given dh_t; updates the dc carry and
@@ -142,12 +150,13 @@ __global__ void lstm_bwd_last_kernel(const float* __restrict__ Cst, const bf16_t
   }
 }
 
+template <int BM, int BN>
 __global__ __launch_bounds__(256) void lstm_bwd_step_kernel(int t, const bf16_t* __restrict__ WhhT,
                                                             const float* __restrict__ Cst,
                                                             const bf16_t* __restrict__ S,
                                                             bf16_t* __restrict__ DG,
                                                             float* __restrict__ dcarry, LstmDims d) {
-  using C = LstmCfg;
+  using C = GemmCfg<BM, BN, K_CONTIG, K_CONTIG>;
   __shared__ __attribute__((aligned(16))) char smem[C::LDS_BYTES];
   const int G = 4 * d.H;
   const int tiles_n = d.H / C::BN;
@@ -172,6 +181,14 @@ __global__ __launch_bounds__(256) void lstm_bwd_step_kernel(int t, const bf16_t*
   }
 }
 
+template <int BM, int BN>
+static void bwd_cfg(int t, const bf16_t* WhhT, const float* Cst, const bf16_t* S, bf16_t* DG,
+                    float* dcarry, LstmDims d, hipStream_t s) {
+  const int tiles = ((d.B + BM - 1) / BM) * (d.H / BN);
+  hipLaunchKernelGGL((lstm_bwd_step_kernel<BM, BN>), dim3(tiles), dim3(256), 0, s, t, WhhT, Cst, S,
+                     DG, dcarry, d);
+}
+
 void launch_lstm_bwd_step(int t, const bf16_t* WhhT, const float* Cst, const bf16_t* S,
                           bf16_t* DG, float* dcarry, const float* dy, const float* w_out,
                           LstmDims d, hipStream_t s) {
@@ -183,9 +200,12 @@ void launch_lstm_bwd_step(int t, const bf16_t* WhhT, const float* Cst, const bf1
                        dy, w_out, d);
     return;
   }
-  const int tiles = ((d.B + LstmCfg::BM - 1) / LstmCfg::BM) * (d.H / LstmCfg::BN);
-  hipLaunchKernelGGL(lstm_bwd_step_kernel, dim3(tiles), dim3(256), 0, s, t, WhhT, Cst, S, DG,
-                     dcarry, d);
+  switch (d.bwd_variant) {
+    case 1: bwd_cfg<64, 128>(t, WhhT, Cst, S, DG, dcarry, d, s); break;
+    case 2: bwd_cfg<128, 64>(t, WhhT, Cst, S, DG, dcarry, d, s); break;
+    case 3: bwd_cfg<64, 64>(t, WhhT, Cst, S, DG, dcarry, d, s); break;
+    default: bwd_cfg<128, 128>(t, WhhT, Cst, S, DG, dcarry, d, s); break;
+  }
 }
 
 // fp32 master W [G][KA] (permuted rows) -> bf16 Wp [G][KA] and WhhT [H][G].

@@ -1,0 +1,78 @@
+"""Engine interface shared by every trainable model.
+
+An *engine* owns ONE flat fp32 parameter buffer and ONE flat fp32 gradient buffer (so the
+optimizer is a single launch and the data-parallel reduction a single collective) and
+exposes:
+
+    forward(x) -> pred                         (device tensor, no host sync)
+    forward_backward(x, y, grad_scale) -> loss_sum
+        computes d/dθ [grad_scale * Σ_i loss_i] into ``grads`` and returns Σ_i loss_i as a
+        device scalar; loss_i = (pred_i - y_i)^2 ("mse") or clip(|y_i - pred_i|, 0, c)
+        ("mae_clip", cnn.py:29-32).
+    sync_weights()                              refresh derived copies after an update
+    to_reference() / from_reference()           the model-family reference layout (.mdl)
+
+Native engines (NativeLSTM / NativeMLP / NativeCNN) run the hand-written HIP kernels;
+:class:`TorchEngine` wraps the fp32 PyTorch reference modules (the CPU oracle) with their
+parameters and gradients re-seated as views into flat buffers, so trainer, optimizer and
+DP all-reduce code paths are identical for both.
+"""
+from __future__ import annotations
+
+import torch
+from torch import nn
+
+
+def per_element_loss(kind: str, pred: torch.Tensor, y: torch.Tensor, clip: float = 6.0):
+    if kind == "mse":
+        return (pred - y) ** 2
+    if kind == "mae_clip":
+        return torch.clamp((y - pred).abs(), 0.0, clip)
+    raise ValueError(f"unknown loss {kind!r}")
+
+
+class TorchEngine:
+    """fp32 PyTorch engine over a reference nn.Module (CPU oracle / GPU eager)."""
+
+    native = False
+
+    def __init__(self, module: nn.Module, loss: str = "mse", clip: float = 6.0, device="cpu"):
+        self.module = module.to(device)
+        self.loss_kind, self.clip = loss, clip
+        self.device = torch.device(device)
+        ps = [p for p in self.module.parameters()]
+        n = sum(p.numel() for p in ps)
+        self.params = torch.zeros(n, device=self.device)
+        self.grads = torch.zeros(n, device=self.device)
+        o = 0
+        for p in ps:
+            k = p.numel()
+            self.params[o : o + k].copy_(p.detach().reshape(-1))
+            p.data = self.params[o : o + k].view_as(p)
+            p.grad = self.grads[o : o + k].view_as(p)
+            o += k
+
+    def sync_weights(self) -> None:  # parameters ARE views of the flat buffer
+        pass
+
+    def train(self, mode: bool = True):
+        self.module.train(mode)
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        self.module.eval()
+        with torch.no_grad():
+            return self.module(x.to(self.device))
+
+    def forward_backward(self, x, y, grad_scale: float, zero_grads: bool = True, step: int = 0):
+        self.module.train()
+        if zero_grads:
+            self.grads.zero_()
+        pred = self.module(x.to(self.device))
+        li = per_element_loss(self.loss_kind, pred, y.to(self.device).view_as(pred), self.clip)
+        total = li.sum()
+        (total * grad_scale).backward()
+        return total.detach().view(1)
+
+
+def native_loss_kind(kind: str) -> int:
+    return {"mse": 0, "mae_clip": 1}[kind]

@@ -1,0 +1,217 @@
+"""The reference's only implemented model: 1-D CNN regression (cnn.py:110-114).
+
+Keras-0.x ``Sequential``: ``Convolution1D(1, 100, 13, activation="relu")`` ->
+``Dropout(0.5)`` -> ``Flatten()`` -> ``Dense(3600, 12)`` on input (B, 48, 1): 100 filters of
+width 13 (valid), 36 output steps, flatten in (step, filter) order, 12 linear outputs,
+44,612 parameters. Loss ``mae_clip`` (cnn.py:29-32), optimizer Keras SGD
+lr 1e-3 / momentum 0.99 / decay 1e-6 / Nesterov (cnn.py:117), batch 20 (cnn.py:128).
+
+* :class:`CNN1DRegressor` — PyTorch fp32 reference (CPU oracle, channels-last input).
+* :class:`NativeCNN` — MI355X engine: im2col (bias folded as a constant-1 tap) ->
+  conv-as-GEMM with fused ReLU + inverted-dropout epilogue (mask regenerated from a
+  counter hash, never stored) -> dense GEMM + bias -> fused loss/grad kernel; backward
+  reuses the stored post-dropout activation as the combined ReLU/dropout mask.
+  Internally filters are padded 100 -> 104 and outputs 12 -> 16 (zero rows) so every
+  MN-contiguous GEMM operand has a multiple-of-8 extent; the padding stays exactly zero.
+
+Theano's conv is a true convolution (kernel flipped); the exported reference layout
+(``to_reference``) therefore flips the taps, so a Keras-0.x consumer of the .mdl sees the
+same function.
+"""
+from __future__ import annotations
+
+import dataclasses
+import math
+
+import torch
+from torch import nn
+
+
+def _r8(x: int) -> int:
+    return (x + 7) // 8 * 8
+
+
+class CNN1DRegressor(nn.Module):
+    def __init__(self, input_len: int = 48, in_ch: int = 1, filters: int = 100, kernel: int = 13,
+                 outputs: int = 12, dropout: float = 0.5):
+        super().__init__()
+        self.input_len, self.in_ch, self.filters = input_len, in_ch, filters
+        self.kernel, self.outputs, self.p = kernel, outputs, dropout
+        self.lout = input_len - kernel + 1
+        self.conv = nn.Conv1d(in_ch, filters, kernel)
+        self.drop = nn.Dropout(dropout)
+        self.dense = nn.Linear(filters * self.lout, outputs)
+
+    def forward(self, x):  # x [B, L, C] (Keras channels-last)
+        if x.dim() == 2:
+            x = x.unsqueeze(-1)
+        h = torch.relu(self.conv(x.transpose(1, 2)))  # [B, F, Lout]
+        h = self.drop(h.transpose(1, 2).reshape(x.shape[0], -1))  # (step, filter) order
+        out = self.dense(h)
+        return out.squeeze(-1) if self.outputs == 1 else out
+
+    def init_keras(self, seed: int = 0):
+        """Keras-0.x defaults: conv 'uniform' (+-0.05), dense glorot_uniform, zero biases."""
+        g = torch.Generator().manual_seed(seed)
+        with torch.no_grad():
+            self.conv.weight.uniform_(-0.05, 0.05, generator=g)
+            self.conv.bias.zero_()
+            lim = math.sqrt(6.0 / (self.dense.in_features + self.dense.out_features))
+            self.dense.weight.uniform_(-lim, lim, generator=g)
+            self.dense.bias.zero_()
+        return self
+
+    @property
+    def layout(self) -> "CnnLayout":
+        return CnnLayout(self.input_len, self.in_ch, self.filters, self.kernel, self.outputs)
+
+    def to_flat(self) -> torch.Tensor:
+        lay = self.layout
+        flat = torch.zeros(lay.numel)
+        Wc, Wd, bd = lay.views(flat)
+        with torch.no_grad():
+            w = self.conv.weight.float().cpu()  # [F, C, k]
+            # column index of tap (k, c) = k*C + c (im2col order); bias column = k*C
+            Wc[: self.filters, : lay.taps] = w.permute(0, 2, 1).reshape(self.filters, -1)
+            Wc[: self.filters, lay.taps] = self.conv.bias.float().cpu()
+            d = self.dense.weight.float().cpu().view(self.outputs, self.lout, self.filters)
+            Wd.view(lay.Op, self.lout, lay.Fp)[: self.outputs, :, : self.filters] = d
+            bd[: self.outputs] = self.dense.bias.float().cpu()
+        return flat
+
+    def load_flat(self, flat: torch.Tensor) -> None:
+        lay = self.layout
+        Wc, Wd, bd = lay.views(flat.detach().float().cpu())
+        with torch.no_grad():
+            w = Wc[: self.filters, : lay.taps].reshape(self.filters, self.kernel, self.in_ch)
+            self.conv.weight.copy_(w.permute(0, 2, 1))
+            self.conv.bias.copy_(Wc[: self.filters, lay.taps])
+            d = Wd.view(lay.Op, self.lout, lay.Fp)[: self.outputs, :, : self.filters]
+            self.dense.weight.copy_(d.reshape(self.outputs, -1))
+            self.dense.bias.copy_(bd[: self.outputs])
+
+
+@dataclasses.dataclass(frozen=True)
+class CnnLayout:
+    input_len: int = 48
+    in_ch: int = 1
+    filters: int = 100
+    kernel: int = 13
+    outputs: int = 12
+
+    @property
+    def lout(self):
+        return self.input_len - self.kernel + 1
+
+    @property
+    def taps(self):
+        return self.kernel * self.in_ch
+
+    @property
+    def Kc(self):  # im2col width: taps + bias column, padded to 8
+        return _r8(self.taps + 1)
+
+    @property
+    def Fp(self):
+        return _r8(self.filters)
+
+    @property
+    def Op(self):
+        return _r8(self.outputs)
+
+    @property
+    def flat_width(self):
+        return self.lout * self.Fp
+
+    @property
+    def numel(self):
+        return self.Fp * self.Kc + self.Op * self.flat_width + self.Op
+
+    def views(self, flat):
+        a = self.Fp * self.Kc
+        b = a + self.Op * self.flat_width
+        return (flat[:a].view(self.Fp, self.Kc), flat[a:b].view(self.Op, self.flat_width),
+                flat[b : b + self.Op])
+
+
+class NativeCNN:
+    """HIP/MFMA engine for the reference CNN (any batch up to ``batch``)."""
+
+    native = True
+
+    def __init__(self, layout: CnnLayout = CnnLayout(), batch: int = 1024, device="cuda",
+                 dropout: float = 0.5, loss: str = "mae_clip", clip: float = 6.0, seed: int = 0,
+                 params: torch.Tensor | None = None, grads: torch.Tensor | None = None):
+        from ..ops.native import lib
+
+        self._C = lib()
+        self.lay, self.B, self.p = layout, batch, dropout
+        self.loss_kind, self.clip, self.seed = loss, clip, seed
+        dev = torch.device(device)
+        self.device = dev
+        n = layout.numel
+        self.params = params if params is not None else torch.zeros(n, device=dev)
+        self.grads = grads if grads is not None else torch.zeros(n, device=dev)
+        self.shadow = torch.empty(n, dtype=torch.bfloat16, device=dev)
+        bf = torch.bfloat16
+        L = layout
+        self.Xcol = torch.empty(batch * L.lout * L.Kc, dtype=bf, device=dev)
+        self.Hc = torch.empty(batch * L.flat_width, dtype=bf, device=dev)
+        self.dZc = torch.empty(batch * L.flat_width, dtype=bf, device=dev)
+        self.pred = torch.empty(batch * L.Op, device=dev)
+        self.ypad = torch.zeros(batch * L.Op, device=dev)
+        self.dpred = torch.zeros(batch * L.Op, dtype=bf, device=dev)
+        self.loss_sum = torch.zeros(1, device=dev)
+        self.sync_weights()
+
+    def sync_weights(self):
+        self._C.cast_bf16(self.params, self.shadow)
+
+    def _fwd(self, x, B, drop_p, seed):
+        from ..ops.native import gemm
+
+        L = self.lay
+        if x.dim() == 2:
+            x = x.unsqueeze(-1)
+        assert x.shape[1] == L.input_len and x.shape[2] == L.in_ch and B <= self.B
+        self._C.im2col1d(x.contiguous().float(), B, L.input_len, L.in_ch, L.kernel, L.Kc, self.Xcol)
+        Wc, Wd, _ = L.views(self.shadow)
+        _, _, bd = L.views(self.params)
+        gemm(self.Xcol, Wc, B * L.lout, L.Fp, L.Kc, outH=self.Hc, act=1, drop_p=drop_p, seed=seed)
+        gemm(self.Hc, Wd, B, L.Op, L.flat_width, outF=self.pred, bias=bd)
+
+    def forward(self, x):
+        B = x.shape[0]
+        self._fwd(x, B, 0.0, 0)
+        out = self.pred[: B * self.lay.Op].view(B, self.lay.Op)[:, : self.lay.outputs]
+        return out.squeeze(-1) if self.lay.outputs == 1 else out
+
+    def forward_backward(self, x, y, grad_scale: float, zero_grads: bool = True, step: int = 0):
+        from ..ops.native import gemm
+
+        L = self.lay
+        B = x.shape[0]
+        seed = (self.seed * 1000003 + step) & 0x7FFFFFFF
+        if zero_grads:
+            self.grads.zero_()
+        self.loss_sum.zero_()
+        self._fwd(x, B, self.p, seed)
+        yv = self.ypad[: B * L.Op].view(B, L.Op)
+        yv[:, : L.outputs].copy_(y.view(B, -1))
+        gWc, gWd, gbd = L.views(self.grads)
+        _, Wd, _ = L.views(self.shadow)
+        kind = 0 if self.loss_kind == "mse" else 1
+        self._C.loss(kind, self.pred, self.ypad, B, L.Op, self.clip, float(grad_scale),
+                     self.loss_sum, self.dpred, None, gbd)
+        # dWd = dpred^T Hc   (reduce over batch)
+        ks = max(1, min(16, B // 256))
+        gemm(self.dpred, self.Hc, L.Op, L.flat_width, B, a_mn=True, lda=L.Op, b_mn=True,
+             ldb=L.flat_width, outF=gWd, atomic=True, ksplit=ks)
+        # dHc = dpred Wd, masked by the stored post-dropout activation, x 1/(1-p)
+        gemm(self.dpred, Wd, B, L.flat_width, L.Op, b_mn=True, ldb=L.flat_width, outH=self.dZc,
+             mask=self.Hc, mask_scale=1.0 / (1.0 - self.p) if self.p > 0 else 1.0)
+        # dWc = dZc^T Xcol   (reduce over batch x steps)
+        ks2 = max(1, min(32, (B * L.lout) // 2048))
+        gemm(self.dZc, self.Xcol, L.Fp, L.Kc, B * L.lout, a_mn=True, lda=L.Fp, b_mn=True,
+             ldb=L.Kc, outF=gWc, atomic=True, ksplit=ks2)
+        return self.loss_sum

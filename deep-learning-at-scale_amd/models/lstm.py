@@ -134,12 +134,15 @@ class NativeLSTM:
     call :meth:`sync_weights` after every change to ``params``.
     """
 
+    native = True
+
     def __init__(self, n_features: int, hidden: int, seq_len: int, batch: int,
                  device="cuda", params: torch.Tensor | None = None,
-                 grads: torch.Tensor | None = None):
+                 grads: torch.Tensor | None = None, loss: str = "mse", clip: float = 6.0):
         from ..ops.native import lib
 
         self._C = lib()
+        self.loss_kind, self.clip = loss, clip
         self.lay = LstmLayout(n_features, hidden)
         self.F, self.H, self.T, self.B = n_features, hidden, seq_len, batch
         lay = self.lay
@@ -159,6 +162,10 @@ class NativeLSTM:
         self.pred = torch.empty(B, dtype=torch.float32, device=dev)
         self.dy = torch.empty(B, dtype=torch.float32, device=dev)
         self.loss_sum = torch.zeros(1, dtype=torch.float32, device=dev)
+        # tile shapes (csrc/kernels.h LstmDims), A/B-tuned on MI355X with tools/tune_lstm.py
+        # (profiles/r1_*): bwd 64x64 tiles 1.5x faster than 128x128 at B=8192; dW split-K 32.
+        self.fwd_variant, self.bwd_variant = 0, 3
+        self.dw_ksplit = 0  # 0 = heuristic
         self.sync_weights()
 
     # ------------------------------------------------------------------ weights
@@ -188,19 +195,19 @@ class NativeLSTM:
             x = xp
         C = self._C
         C.lstm_pack_x(x, self.XH, *self._dims(self.B))
-        C.lstm_forward(self.XH, self.Wp, self.Cst, self.S, *self._dims(self.B))
+        C.lstm_forward(self.XH, self.Wp, self.Cst, self.S, *self._dims(self.B), self.fwd_variant)
         _, w_out, b_out = self.lay.views(self.params)
         C.head_fwd(self._hT(self.B), self.lay.KA, self.B, self.H, w_out, b_out, None, self.pred,
                    None, None, 0.0)
         return self.pred[:B]
 
-    def forward_backward(self, x: torch.Tensor, y: torch.Tensor, dy_scale: float,
-                         zero_grads: bool = True) -> torch.Tensor:
+    def forward_backward(self, x: torch.Tensor, y: torch.Tensor, grad_scale: float,
+                         zero_grads: bool = True, step: int = 0) -> torch.Tensor:
         """One training forward + backward on a full batch; grads land in ``self.grads``.
 
-        ``dy_scale`` multiplies (pred - y): use 2 / global_batch for the mean-squared error
-        averaged over all data-parallel ranks. Returns the device scalar sum of squared
-        errors of this batch (no host sync).
+        Gradient of ``grad_scale * sum_i loss_i`` (models/base.py contract; use
+        1 / global_batch for the mean over all data-parallel ranks). Returns the device
+        scalar sum of per-sample losses of this batch (no host sync).
         """
         B = self.B
         assert x.shape == (B, self.T, self.F) and y.shape == (B,)
@@ -212,16 +219,22 @@ class NativeLSTM:
             self.grads.zero_()
         self.loss_sum.zero_()
         C.lstm_pack_x(x.contiguous(), self.XH, *self._dims(B))
-        C.lstm_forward(self.XH, self.Wp, self.Cst, self.S, *self._dims(B))
+        C.lstm_forward(self.XH, self.Wp, self.Cst, self.S, *self._dims(B), self.fwd_variant)
         hT = self._hT(B)
-        C.head_fwd(hT, lay.KA, B, self.H, w_out, b_out, y.contiguous(), self.pred, self.dy,
-                   self.loss_sum, float(dy_scale))
+        y = y.contiguous().float()
+        if self.loss_kind == "mse":  # head + MSE + dy fused in one kernel
+            C.head_fwd(hT, lay.KA, B, self.H, w_out, b_out, y, self.pred, self.dy,
+                       self.loss_sum, 2.0 * float(grad_scale))
+        else:
+            C.head_fwd(hT, lay.KA, B, self.H, w_out, b_out, None, self.pred, None, None, 0.0)
+            C.loss(1, self.pred, y, B, 1, self.clip, float(grad_scale), self.loss_sum, None,
+                   self.dy, None)
         C.head_bwd_w(hT, lay.KA, B, self.H, self.dy, gw_out, gb_out)
         C.lstm_backward(self.WhhT, self.XH, self.Cst, self.S, self.DG, self.dcarry, self.dy,
-                        w_out, *self._dims(B))
+                        w_out, *self._dims(B), self.bwd_variant)
         # dWcat = sum_{t,b} dG_t[b]^T [x_t | 1 | h_{t-1}][b]   (one split-K GEMM, K = T*B)
         K = self.T * B
-        ksplit = max(1, min(64, K // 4096))
+        ksplit = self.dw_ksplit or max(1, min(32, K // 16384))
         from ..ops.native import gemm
 
         gemm(self.DG, self.XH, lay.G, lay.KA, K, a_mn=True, lda=lay.G, b_mn=True, ldb=lay.KA,

@@ -1,0 +1,214 @@
+"""ANN static / dynamic regression models (README "ANN model", Readme.md:13-19;
+BASELINE.json:8-10 — "Static 3-layer MLP regression bf16", "Dynamic (online) MLP").
+
+* :class:`MLPRegressor` — PyTorch fp32 reference (CPU oracle).
+* :class:`NativeMLP` — MI355X engine. Per training step:
+  forward = one MFMA GEMM per layer with a fused bias + ReLU + bf16-cast epilogue, the
+  N=1 head fused with the MSE loss; backward = head kernel producing dZ_L (ReLU mask and
+  bias-grad column sums fused), then per layer one split-K GEMM for dW (MN-contiguous
+  operands, fp32 atomics straight into the flat gradient bucket) and one GEMM for
+  dZ_{l-1} = (dZ_l W_l) * [H_{l-1} > 0] whose epilogue also emits db_{l-1}.
+  W_l^T is never materialised: the dX GEMM reads W_l as an MN-contiguous operand.
+
+Flat layout (``MlpLayout``): per layer ``[W_l (out x in_pad) | b_l (out)]`` then
+``[w_head (H_L) | b_head (1)]``; every block starts 8-element aligned so the bf16 shadow
+(one cast of the whole flat buffer) yields 16-B aligned GEMM operands. The first layer's
+input width is padded to a multiple of 8 (zero columns).
+"""
+from __future__ import annotations
+
+import dataclasses
+import math
+
+import torch
+from torch import nn
+
+
+def _r8(x: int) -> int:
+    return (x + 7) // 8 * 8
+
+
+@dataclasses.dataclass(frozen=True)
+class MlpLayout:
+    n_features: int
+    hidden: tuple
+
+    @property
+    def dims(self):
+        """[(out, in_pad)] per hidden layer."""
+        out, prev = [], _r8(self.n_features)
+        for h in self.hidden:
+            out.append((h, prev))
+            prev = h
+        return out
+
+    def offsets(self):
+        offs, o = [], 0
+        for (h, k) in self.dims:
+            w = o
+            o = _r8(o + h * k)
+            b = o
+            o = _r8(o + h)
+            offs.append((w, b))
+        hw = o
+        o = _r8(o + self.hidden[-1])
+        hb = o
+        o = _r8(o + 1)
+        return offs, hw, hb, o
+
+    @property
+    def numel(self) -> int:
+        return self.offsets()[3]
+
+    def views(self, flat: torch.Tensor):
+        offs, hw, hb, _ = self.offsets()
+        layers = []
+        for (w, b), (h, k) in zip(offs, self.dims):
+            layers.append((flat[w : w + h * k].view(h, k), flat[b : b + h]))
+        H = self.hidden[-1]
+        return layers, flat[hw : hw + H], flat[hb : hb + 1]
+
+
+class MLPRegressor(nn.Module):
+    def __init__(self, n_features: int, hidden=(256, 256)):
+        super().__init__()
+        self.n_features, self.hidden = n_features, tuple(hidden)
+        layers, prev = [], n_features
+        for h in hidden:
+            layers += [nn.Linear(prev, h), nn.ReLU()]
+            prev = h
+        self.body = nn.Sequential(*layers)
+        self.head = nn.Linear(prev, 1)
+
+    def forward(self, x):
+        return self.head(self.body(x)).squeeze(-1)
+
+    def linears(self):
+        return [m for m in self.body if isinstance(m, nn.Linear)]
+
+    def to_flat(self) -> torch.Tensor:
+        lay = MlpLayout(self.n_features, self.hidden)
+        flat = torch.zeros(lay.numel)
+        layers, hw, hb = lay.views(flat)
+        with torch.no_grad():
+            for (W, b), lin in zip(layers, self.linears()):
+                W[:, : lin.in_features].copy_(lin.weight.float().cpu())
+                b.copy_(lin.bias.float().cpu())
+            hw.copy_(self.head.weight.view(-1).float().cpu())
+            hb.copy_(self.head.bias.float().cpu())
+        return flat
+
+    def load_flat(self, flat: torch.Tensor) -> None:
+        lay = MlpLayout(self.n_features, self.hidden)
+        layers, hw, hb = lay.views(flat.detach().float().cpu())
+        with torch.no_grad():
+            for (W, b), lin in zip(layers, self.linears()):
+                lin.weight.copy_(W[:, : lin.in_features])
+                lin.bias.copy_(b)
+            self.head.weight.copy_(hw.view(1, -1))
+            self.head.bias.copy_(hb)
+
+
+def init_mlp_flat(n_features: int, hidden=(256, 256), seed: int = 0) -> torch.Tensor:
+    torch.manual_seed(seed)
+    return MLPRegressor(n_features, hidden).to_flat()
+
+
+class NativeMLP:
+    """HIP/MFMA MLP regression engine for batches of up to ``batch`` rows."""
+
+    native = True
+
+    def __init__(self, n_features: int, hidden=(256, 256), batch: int = 4096, device="cuda",
+                 params: torch.Tensor | None = None, grads: torch.Tensor | None = None,
+                 loss: str = "mse", clip: float = 6.0):
+        from ..ops.native import lib
+
+        self._C = lib()
+        self.loss_kind, self.clip = loss, clip
+        self.lay = MlpLayout(n_features, tuple(hidden))
+        self.F, self.hidden, self.B = n_features, tuple(hidden), batch
+        dev = torch.device(device)
+        self.device = dev
+        n = self.lay.numel
+        self.params = params if params is not None else torch.zeros(n, device=dev)
+        self.grads = grads if grads is not None else torch.zeros(n, device=dev)
+        self.shadow = torch.empty(n, dtype=torch.bfloat16, device=dev)
+        bf = torch.bfloat16
+        self.Fp = _r8(n_features)
+        self.X = torch.zeros(batch * self.Fp, dtype=bf, device=dev)
+        self.Hs = [torch.empty(batch * h, dtype=bf, device=dev) for h in self.hidden]
+        self.dZ = [torch.empty(batch * h, dtype=bf, device=dev) for h in self.hidden]
+        self.pred = torch.empty(batch, device=dev)
+        self.dy = torch.empty(batch, device=dev)
+        self.loss_sum = torch.zeros(1, device=dev)
+        self.sync_weights()
+
+    def sync_weights(self) -> None:
+        self._C.cast_bf16(self.params, self.shadow)
+
+    def _load_x(self, x: torch.Tensor) -> int:
+        B = x.shape[0]
+        assert B <= self.B and x.shape[1] == self.F
+        Xv = self.X[: B * self.Fp].view(B, self.Fp)
+        if self.Fp == self.F:
+            self._C.cast_bf16(x.contiguous().float(), Xv)
+        else:
+            self._C.transpose_cast_bf16(x.t().contiguous().float(), B, self.F, B, Xv, self.Fp)
+        return B
+
+    def _forward_body(self, B: int) -> None:
+        from ..ops.native import gemm
+
+        wl, _, _ = self.lay.views(self.shadow)
+        pl, _, _ = self.lay.views(self.params)
+        A, K = self.X, self.Fp
+        for (W, _), (_, b), Hout, (h, k) in zip(wl, pl, self.Hs, self.lay.dims):
+            gemm(A, W, B, h, k, outH=Hout, bias=b, act=1)
+            A, K = Hout, h
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        B = self._load_x(x)
+        self._forward_body(B)
+        _, hw, hb = self.lay.views(self.params)
+        H = self.hidden[-1]
+        self._C.head_fwd(self.Hs[-1], H, B, H, hw, hb, None, self.pred, None, None, 0.0)
+        return self.pred[:B]
+
+    def forward_backward(self, x: torch.Tensor, y: torch.Tensor, grad_scale: float,
+                         zero_grads: bool = True, step: int = 0) -> torch.Tensor:
+        from ..ops.native import gemm
+
+        C = self._C
+        B = self._load_x(x)
+        if zero_grads:
+            self.grads.zero_()
+        self.loss_sum.zero_()
+        self._forward_body(B)
+        pl, hw, hb = self.lay.views(self.params)
+        gl, ghw, ghb = self.lay.views(self.grads)
+        wl, _, _ = self.lay.views(self.shadow)
+        L = len(self.hidden)
+        H = self.hidden[-1]
+        y = y.contiguous().float()
+        if self.loss_kind == "mse":
+            C.head_fwd(self.Hs[-1], H, B, H, hw, hb, y, self.pred, self.dy, self.loss_sum,
+                       2.0 * float(grad_scale))
+        else:
+            C.head_fwd(self.Hs[-1], H, B, H, hw, hb, None, self.pred, None, None, 0.0)
+            C.loss(1, self.pred, y, B, 1, self.clip, float(grad_scale), self.loss_sum, None,
+                   self.dy, None)
+        C.head_bwd_w(self.Hs[-1], H, B, H, self.dy, ghw, ghb)
+        C.head_bwd_x(self.Hs[-1], H, B, H, self.dy, hw, True, self.dZ[-1], H, gl[-1][1])
+        ksplit = max(1, min(32, B // 1024))
+        for l in range(L - 1, -1, -1):
+            h, k = self.lay.dims[l]
+            prevH = self.Hs[l - 1] if l > 0 else self.X
+            # dW_l = dZ_l^T H_{l-1}   (reduce over the batch; MN-contiguous operands)
+            gemm(self.dZ[l], prevH, h, k, B, a_mn=True, lda=h, b_mn=True, ldb=k,
+                 outF=gl[l][0], atomic=True, ksplit=ksplit)
+            if l > 0:
+                # dZ_{l-1} = (dZ_l W_l) * [H_{l-1} > 0];  db_{l-1} = colsum
+                gemm(self.dZ[l], wl[l][0], B, k, h, b_mn=True, ldb=k, outH=self.dZ[l - 1],
+                     mask=self.Hs[l - 1], colsum=gl[l - 1][1])
+        return self.loss_sum

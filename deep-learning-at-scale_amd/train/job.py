@@ -1,0 +1,137 @@
+"""One submitted learning job, end to end (the body of cnn.py, fixed and generalised).
+
+    python3 <script>.py columnNames columnTypes targetColumn storagePath [dataPath] [--opts]
+
+Flow: argv -> RunConfig -> DistContext (torchrun env; one process per
+GPU; RCCL or gloo) -> table (CSV or synthetic) -> features (fit on train) -> engine
+(native HIP engine on GPU in bf16, fp32 PyTorch oracle on CPU or with --precision fp32)
+-> param broadcast (C1) -> fit (early stopping, best .mdl, resumable .ckpt) -> test
+evaluation -> the reference's two stdout lines.
+"""
+from __future__ import annotations
+
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+from ..config import RunConfig, parse_argv
+from ..data.pipeline import prepare
+from ..data.schema import parse_schema
+from ..models import registry
+from ..models.gilbert import GilbertModel
+from ..optim.flat import make_optimizer
+from ..parallel.dist import DistContext
+from ..utils import checkpoint as ckpt
+from .trainer import Trainer
+
+
+def _optimizer(cfg: RunConfig, eng):
+    if cfg.optimizer == "sgd":
+        return make_optimizer("sgd", eng.params, eng.grads, lr=cfg.lr, momentum=cfg.momentum,
+                              decay=cfg.decay, nesterov=cfg.nesterov)
+    return make_optimizer("adam", eng.params, eng.grads, lr=cfg.lr, weight_decay=cfg.weight_decay)
+
+
+def _save_best(cfg, name, ref, prepared):
+    def cb(trainer):
+        registry.engine_to_reference(trainer.eng, ref)
+        extra = {"epoch": trainer.epoch, "val_loss": trainer.history.val_loss[-1],
+                 "features": prepared.pipeline.state() if prepared.pipeline else None}
+        ckpt.save_mdl(cfg.mdl_path(name), name, registry.keras_layers(name, ref), extra)
+    return cb
+
+
+def run_gilbert(cfg: RunConfig, ctx: DistContext, prepared, log):
+    t0 = time.time()
+    model = GilbertModel()
+    feats, y = prepared.test
+    test_mse = model.mse(feats, y)
+    elapsed = time.time() - t0
+    if ctx.is_main:
+        A, B, C, unit = model.constants()
+        ckpt.save_mdl(cfg.mdl_path("gilbert"), "gilbert",
+                      [("Gilbert", [torch.tensor([A, B, C], dtype=torch.float64)])],
+                      {"correlation": model.correlation, "glr_unit": unit})
+        log("\nTime elapsed: %f s" % elapsed)
+        log("Testing set loss: %f" % test_mse)
+    return {"test_loss": test_mse, "test_mse": test_mse, "elapsed": elapsed}
+
+
+def run_job(model: str, argv, log=print) -> dict:
+    cfg = parse_argv(model, argv)
+    return run_config(cfg, log=log)
+
+
+def run_config(cfg: RunConfig, log=print) -> dict:
+    device = None if cfg.device == "auto" else cfg.device
+    ctx = DistContext.from_env(device=device)
+    say = log if ctx.is_main else (lambda *a, **k: None)
+    schema = parse_schema(cfg.column_names, cfg.column_types)
+    say(schema)  # cnn.py:62
+    say("Categorical variables: " + ", ".join(schema.categorical(exclude=(cfg.target,))))  # cnn.py:73
+    prepared = prepare(cfg)
+    if cfg.model == "gilbert":
+        out = run_gilbert(cfg, ctx, prepared, say)
+        ctx.shutdown()
+        return out
+
+    dev = ctx.device
+    native = dev.type == "cuda" and cfg.precision == "bf16"
+    n_train = len(prepared.train[0])
+    b = max(1, min(cfg.batch_size, n_train // max(ctx.world_size, 1)))
+    eng, ref = registry.build_engine(cfg.model, cfg, prepared.n_features, prepared.n_outputs, b,
+                                     dev, native, seed=cfg.seed)
+    ctx.broadcast_(eng.params)  # C1
+    eng.sync_weights()
+    opt = _optimizer(cfg, eng)
+    trainer = Trainer(cfg, eng, opt, ctx, cfg.model, on_best=_save_best(cfg, cfg.model, ref, prepared),
+                      n_outputs=prepared.n_outputs, log=log)
+    resumed = trainer.try_resume()
+    if cfg.model == "mlp_online":
+        from .online import fit_online
+
+        if not resumed:
+            _warm_start(cfg, eng, ref, say)
+        t0 = time.time()
+        fit_online(trainer, prepared.train, prepared.val)
+    else:
+        t0 = time.time()
+        trainer.fit(prepared.train, prepared.val)
+    elapsed = time.time() - t0
+    test_loss, test_mse = trainer.evaluate(*prepared.test)
+    say("\nTime elapsed: %f s" % elapsed)  # cnn.py:133 (py3-correct)
+    say("Testing set loss: %f" % test_loss)  # cnn.py:134
+    result = {
+        "model": cfg.model, "native": native, "world_size": ctx.world_size,
+        "epochs": trainer.epoch, "steps": trainer.global_step, "elapsed": elapsed,
+        "test_loss": test_loss, "test_mse": test_mse,
+        "best_val_loss": trainer.stopper.best, "history": trainer.history.__dict__,
+    }
+    if ctx.is_main and os.environ.get("WELLFLOW_RESULT_JSON"):
+        with open(os.environ["WELLFLOW_RESULT_JSON"], "w") as f:
+            json.dump(result, f)
+    ctx.shutdown()
+    return result
+
+
+def _warm_start(cfg, eng, ref, say):
+    """Dynamic model: continue from the last saved .mdl of this storage path if present."""
+    path = cfg.mdl_path(cfg.model)
+    if not os.path.exists(path):
+        return
+    try:
+        name, layers, _ = ckpt.load_mdl(path)
+        registry.load_keras_layers(cfg.model, ref, layers)
+        registry.reference_to_engine(ref, eng)
+        say(f"Warm start from {path}")
+    except Exception as e:  # incompatible shapes (features changed between submissions)
+        say(f"Warm start skipped ({e})")
+
+
+def main(model: str) -> int:
+    run_job(model, sys.argv[1:])
+    return 0

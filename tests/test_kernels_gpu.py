@@ -106,7 +106,7 @@ def test_lstm_forward_backward_matches_torch():
     rp = ref(x)
     assert (pred - rp).abs().max().item() < 3e-2, (pred - rp).abs().max().item()
 
-    loss_sum = eng.forward_backward(x, y, dy_scale=2.0 / B)
+    loss_sum = eng.forward_backward(x, y, grad_scale=1.0 / B)
     torch.cuda.synchronize()
     loss = ((rp - y) ** 2).mean()
     assert abs(loss_sum.item() / B - loss.item()) < 2e-2 * loss.item() + 1e-3
@@ -173,7 +173,7 @@ def test_losses():
         d = torch.empty(B, O, dtype=torch.bfloat16, device=DEV)
         cs = torch.zeros(O, device=DEV)
         scale = 1.0 / (B * O)
-        C.loss(kind, pred, y, B, O, 6.0, scale, ls, d, cs)
+        C.loss(kind, pred, y, B, O, 6.0, scale, ls, d, None, cs)
         pr = pred.clone().requires_grad_(True)
         if kind == 0:
             L = ((pr - y) ** 2).sum()
