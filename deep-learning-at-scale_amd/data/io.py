@@ -28,12 +28,29 @@ def read_csv(path: str, schema: Schema, header: bool = False, block_size: int = 
     conv = pacsv.ConvertOptions(column_types=types, include_columns=schema.names,
                                 strings_can_be_null=False, quoted_strings_can_be_null=False)
     parse = pacsv.ParseOptions(invalid_row_handler=lambda row: "skip")
-    tbl = pacsv.read_csv(path, read_options=read_opts, parse_options=parse, convert_options=conv)
+    try:  # fast path: typed columnar parse
+        tbl = pacsv.read_csv(path, read_options=read_opts, parse_options=parse, convert_options=conv)
+        tolerant = False
+    except pa.ArrowInvalid:  # a cell failed its type: parse as text, coerce per column
+        conv = pacsv.ConvertOptions(column_types={n: pa.string() for n in schema.names},
+                                    include_columns=schema.names, strings_can_be_null=False)
+        tbl = pacsv.read_csv(path, read_options=read_opts, parse_options=parse, convert_options=conv)
+        tolerant = True
     out = {}
     valid = np.ones(tbl.num_rows, dtype=bool)
     for f in schema.fields:
         col = tbl.column(f.name)
         if f.is_numeric:
+            if tolerant:
+                import pandas as pd
+
+                num = pd.to_numeric(pd.Series(col.to_pylist()), errors="coerce").to_numpy()
+                if f.kind == INT:
+                    num = np.where(np.floor(num) == num, num, np.nan)
+                bad = np.isnan(num)
+                valid &= ~bad
+                out[f.name] = np.where(bad, 0, num).astype(np.int64 if f.kind == INT else np.float32)
+                continue
             valid &= ~np.asarray(col.is_null().to_numpy(zero_copy_only=False))
             arr = col.to_numpy(zero_copy_only=False)
             out[f.name] = np.asarray(arr, dtype=np.int64 if f.kind == INT else np.float32)

@@ -1,0 +1,110 @@
+"""Schema / feature pipeline / split / windows / CSV ingest (SURVEY.md §4 unit tier)."""
+import numpy as np
+import pytest
+from hypothesis import given, settings
+from hypothesis import strategies as st
+
+from wellflow.data.features import (FeaturePipeline, StringIndexer, make_windows, one_hot,
+                                    random_split, take)
+from wellflow.data.io import load_table, read_csv, write_csv
+from wellflow.data.schema import FLOAT, INT, STRING, map_type, parse_schema
+from wellflow.data.synth import TABLE_COLUMNS, TABLE_TYPES, synth_lstm_batch, well_log_table
+
+NAMES = ",".join(TABLE_COLUMNS)
+TYPES = ",".join(TABLE_TYPES)
+
+
+def test_type_mapping_keeps_reference_catch_all():
+    # cnn.py:55-59: only "int" and "float" are numeric; "double" becomes a string column
+    assert map_type("int") == INT and map_type("float") == FLOAT
+    for t in ("double", "string", "bool", "Float", ""):
+        assert map_type(t) == STRING
+
+
+def test_parse_schema_and_repr():
+    s = parse_schema("a,b,c", "int,float,double")
+    assert s.names == ["a", "b", "c"]
+    assert [f.kind for f in s.fields] == [INT, FLOAT, STRING]
+    assert str(s).startswith("StructType([StructField('a', IntegerType(), True)")
+    assert s.categorical() == ["c"] and s.continuous() == ["a", "b"]
+    assert s.continuous(exclude=("b",)) == ["a"]
+    with pytest.raises(ValueError):
+        parse_schema("a,b", "int")
+
+
+def test_string_indexer_frequency_desc_ties_alphabetical():
+    ix = StringIndexer("c").fit(["b", "a", "c", "b", "a", "d", "b"])
+    assert ix.labels == ["b", "a", "c", "d"]
+    assert ix.transform(["d", "b", "zz"]).tolist() == [3, 0, 4]  # unseen -> extra index
+    with pytest.raises(ValueError):
+        StringIndexer("c", handle_invalid="error").fit(["a"]).transform(["b"])
+
+
+def test_one_hot_drop_last():
+    out = one_hot(np.array([0, 1, 2]), 3, drop_last=True)
+    assert out.tolist() == [[1, 0], [0, 1], [0, 0]]
+    assert one_hot(np.array([2]), 3, drop_last=False).tolist() == [[0, 0, 1]]
+
+
+@settings(max_examples=25, deadline=None)
+@given(st.integers(50, 3000), st.integers(0, 10_000))
+def test_random_split_partition_and_ratio(n, seed):
+    parts = random_split(n, (0.64, 0.16, 0.2), seed)
+    allidx = np.sort(np.concatenate(parts))
+    assert np.array_equal(allidx, np.arange(n))
+    assert [p.tolist() for p in parts] == [p.tolist() for p in random_split(n, (0.64, 0.16, 0.2), seed)]
+    if n >= 1000:
+        assert abs(len(parts[0]) / n - 0.64) < 0.06
+
+
+def test_pipeline_fit_on_train_excludes_target_and_standardises():
+    tbl = well_log_table(4, 50, seed=1)
+    schema = parse_schema(NAMES, TYPES)
+    idx = random_split(200, seed=3)
+    pipe = FeaturePipeline(schema, "flow", standardize_target=True).fit(take(tbl, idx[0]))
+    assert "flow" not in pipe.continuous
+    X, y = pipe.transform(take(tbl, idx[0]))
+    # one-hot(well: 4 labels + unknown - dropLast = 4) + one-hot(field) + 7 continuous
+    assert X.shape[1] == pipe.n_features
+    nc = len(pipe.continuous)
+    assert np.allclose(X[:, -nc:].mean(0), 0, atol=1e-4)
+    assert abs(float(y.mean())) < 1e-4
+    Xv, _ = pipe.transform(take(tbl, idx[1]))  # same vocabulary on other splits
+    assert Xv.shape[1] == X.shape[1]
+
+
+def test_make_windows_respects_groups():
+    X = np.arange(10, dtype=np.float32).reshape(10, 1)
+    y = np.arange(10, dtype=np.float32)
+    g = np.array([0] * 4 + [1] * 6)
+    Xw, yw = make_windows(X, y, 3, g)
+    assert Xw.shape == (2 + 4, 3, 1)
+    assert yw.tolist() == [2, 3, 6, 7, 8, 9]
+    assert Xw[2, :, 0].tolist() == [4, 5, 6]
+
+
+def test_csv_roundtrip_headerless(tmp_path):
+    tbl = well_log_table(2, 20, seed=0)
+    p = tmp_path / "d.csv"
+    write_csv(tbl, str(p), columns=TABLE_COLUMNS, header=False)
+    schema = parse_schema(NAMES, TYPES)
+    back = read_csv(str(p), schema)
+    assert back["well"].tolist() == [str(v) for v in tbl["well"]]
+    assert np.allclose(back["whp"], tbl["whp"], rtol=1e-6)
+    assert back["t"].dtype == np.int64
+    same = load_table(str(p), schema)
+    assert len(same["flow"]) == 40
+
+
+def test_csv_drops_unparseable_numeric_rows(tmp_path):
+    p = tmp_path / "bad.csv"
+    p.write_text("1,2.5,a\nx,3.0,b\n4,5.0,c\n")
+    back = read_csv(str(p), parse_schema("i,f,s", "int,float,string"))
+    assert back["i"].tolist() == [1, 4] and back["s"].tolist() == ["a", "c"]
+
+
+def test_synthetic_batches_are_finite_and_learnable_scale():
+    x, y = synth_lstm_batch(64, 32, 16, seed=0)
+    assert x.shape == (64, 32, 16) and y.shape == (64,)
+    assert np.isfinite(x.numpy()).all() and np.isfinite(y.numpy()).all()
+    assert 0.2 < float(y.std()) < 3.0

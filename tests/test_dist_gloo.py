@@ -1,0 +1,93 @@
+"""Data-parallel correctness on CPU: gloo, world_size 2 and 4, launched through torchrun on
+127.0.0.1 (SURVEY.md §4 distributed tier). The same code path runs RCCL on GPUs."""
+import json
+import os
+import socket
+import subprocess
+import sys
+import textwrap
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _torchrun(tmp_path, body: str, nproc: int, timeout=300):
+    script = tmp_path / "worker.py"
+    script.write_text(textwrap.dedent(f"""
+        import json, os, sys
+        sys.path.insert(0, {ROOT!r})
+        import torch
+        from wellflow.parallel.dist import DistContext
+        OUT = {str(tmp_path)!r}
+    """) + textwrap.dedent(body))
+    env = dict(os.environ)
+    env["CUDA_VISIBLE_DEVICES"] = ""
+    env["OMP_NUM_THREADS"] = "1"
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), str(script)]
+    r = subprocess.run(cmd, capture_output=True, text=True, env=env, timeout=timeout, cwd=str(tmp_path))
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    return [json.load(open(tmp_path / f"rank{i}.json")) for i in range(nproc)]
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_dp_step_equals_single_process_step(tmp_path, world):
+    res = _torchrun(tmp_path, """
+        from wellflow.models.base import TorchEngine
+        from wellflow.models.mlp import MLPRegressor
+        from wellflow.optim.flat import FlatAdam
+        ctx = DistContext.from_env(device="cpu")
+        W, r = ctx.world_size, ctx.rank
+        torch.manual_seed(100 + r)               # different init on purpose ...
+        eng = TorchEngine(MLPRegressor(6, (16, 8)), loss="mse")
+        ctx.broadcast_(eng.params)               # ... C1 makes them identical
+        opt = FlatAdam(eng.params, eng.grads, lr=1e-2)
+        g = torch.Generator().manual_seed(0)
+        X, Y = torch.randn(32, 6, generator=g), torch.randn(32, generator=g)
+        B = 32 // W
+        for step in range(3):
+            xb, yb = X[r * B:(r + 1) * B], Y[r * B:(r + 1) * B]
+            eng.forward_backward(xb, yb, grad_scale=1.0 / 32)
+            ctx.all_reduce_sum_(eng.grads)       # C2
+            opt.step()
+        # single-process reference on the full batch, from the broadcast init
+        torch.manual_seed(100)
+        ref = TorchEngine(MLPRegressor(6, (16, 8)), loss="mse")
+        ropt = FlatAdam(ref.params, ref.grads, lr=1e-2)
+        for step in range(3):
+            ref.forward_backward(X, Y, grad_scale=1.0 / 32)
+            ropt.step()
+        err = (eng.params - ref.params).abs().max().item()
+        json.dump({"err": err, "p0": eng.params[:5].tolist()}, open(f"{OUT}/rank{r}.json", "w"))
+        ctx.shutdown()
+    """, world)
+    for rr in res:
+        assert rr["err"] < 1e-5
+    assert all(rr["p0"] == res[0]["p0"] for rr in res)
+
+
+def test_dp_training_job_agrees_on_early_stop_and_rank0_writes(tmp_path):
+    res = _torchrun(tmp_path, """
+        from wellflow.train.job import run_job
+        names = "well,field,t,whp,choke,glr,temp,water_cut,dsp,flow"
+        types = "string,string,int,float,float,float,float,float,float,float"
+        out = run_job("mlp", [names, types, "flow", OUT + "/store", "--epochs", "30", "--patience", "1",
+                              "--synth-wells", "3", "--synth-steps", "120", "--batch-size", "16",
+                              "--device", "cpu", "--lr", "0.05"], log=lambda *a, **k: None)
+        r = int(os.environ["RANK"])
+        json.dump({"epochs": out["epochs"], "test": out["test_loss"], "val": out["history"]["val_loss"]},
+                  open(f"{OUT}/rank{r}.json", "w"))
+    """, 2)
+    assert res[0]["epochs"] == res[1]["epochs"]
+    assert res[0]["val"] == res[1]["val"]
+    assert abs(res[0]["test"] - res[1]["test"]) < 1e-9
+    assert (tmp_path / "store" / "models" / "mlp.mdl").exists()

@@ -1,0 +1,104 @@
+"""Native MLP / CNN engines vs the fp32 PyTorch reference modules, and end-to-end native
+training jobs on the MI355X (forward values, flat gradients, learning curves)."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _rel(a, b):
+    return ((a - b).norm() / (b.norm() + 1e-12)).item()
+
+
+def _flat_grads_ref(ref):
+    return torch.cat([p.grad.reshape(-1) for p in ref.parameters()])
+
+
+@pytest.mark.parametrize("loss", ["mse", "mae_clip"])
+def test_native_mlp_matches_reference(loss):
+    from wellflow.models.base import per_element_loss
+    from wellflow.models.mlp import MLPRegressor, NativeMLP
+
+    torch.manual_seed(0)
+    F, Hs, B = 13, (256, 128), 300
+    ref = MLPRegressor(F, Hs).to(DEV)
+    eng = NativeMLP(F, Hs, batch=512, device=DEV, loss=loss)
+    eng.params.copy_(ref.to_flat().to(DEV))
+    eng.sync_weights()
+    x, y = torch.randn(B, F, device=DEV), torch.randn(B, device=DEV)
+    p = eng.forward(x).clone()
+    r = ref(x)
+    assert _rel(p, r) < 2e-2
+    eng.forward_backward(x, y, grad_scale=1.0 / B)
+    per_element_loss(loss, ref(x), y).sum().mul(1.0 / B).backward()
+    gref = MLPRegressor(F, Hs)
+    for pr, pg in zip(gref.parameters(), ref.parameters()):
+        pr.data.copy_(pg.grad.cpu())
+    gflat = gref.to_flat().to(DEV)
+    assert _rel(eng.grads, gflat) < 3e-2, _rel(eng.grads, gflat)
+
+
+@pytest.mark.parametrize("loss", ["mae_clip", "mse"])
+def test_native_cnn_matches_reference(loss):
+    from wellflow.models.base import per_element_loss
+    from wellflow.models.cnn import CNN1DRegressor, NativeCNN
+
+    torch.manual_seed(1)
+    ref = CNN1DRegressor(dropout=0.0).init_keras(3).to(DEV)
+    eng = NativeCNN(ref.layout, batch=64, device=DEV, dropout=0.0, loss=loss)
+    eng.params.copy_(ref.to_flat().to(DEV))
+    eng.sync_weights()
+    B = 40
+    x, y = torch.randn(B, 48, 1, device=DEV), torch.randn(B, 12, device=DEV)
+    assert _rel(eng.forward(x), ref(x)) < 2e-2
+    ls = eng.forward_backward(x, y, grad_scale=1.0 / (B * 12))
+    L = per_element_loss(loss, ref(x), y).sum()
+    (L / (B * 12)).backward()
+    assert abs(ls.item() - L.item()) < 2e-2 * L.item()
+    gref = CNN1DRegressor(dropout=0.0)
+    for pr, pg in zip(gref.parameters(), ref.parameters()):
+        pr.data.copy_(pg.grad.cpu())
+    assert _rel(eng.grads, gref.to_flat().to(DEV)) < 3e-2
+
+
+def test_native_cnn_dropout_mask_consistent():
+    """With dropout the backward must use exactly the forward's mask: check dL/dW_dense
+    against the stored post-dropout activation (dWd = dpred^T Hc)."""
+    from wellflow.models.cnn import CNN1DRegressor, NativeCNN
+
+    ref = CNN1DRegressor(dropout=0.5).init_keras(0)
+    eng = NativeCNN(ref.layout, batch=32, device=DEV, dropout=0.5, loss="mse")
+    eng.params.copy_(ref.to_flat().to(DEV))
+    eng.sync_weights()
+    x, y = torch.randn(32, 48, 1, device=DEV), torch.randn(32, 12, device=DEV)
+    eng.forward_backward(x, y, grad_scale=1.0, step=5)
+    L = eng.lay
+    Hc = eng.Hc[: 32 * L.flat_width].view(32, L.flat_width).float()
+    kept = (Hc > 0).float().mean().item()
+    assert 0.15 < kept < 0.45  # ~half of the ReLU-positive units survive
+    dpred = eng.dpred[: 32 * L.Op].view(32, L.Op).float()
+    _, gWd, _ = L.views(eng.grads)
+    assert _rel(gWd, dpred.t() @ Hc) < 2e-2
+
+
+@pytest.mark.parametrize("model", ["mlp", "lstm", "cnn", "mlp_online"])
+def test_native_training_job_learns(model, tmp_path):
+    from wellflow.train.job import run_job
+
+    names = "well,field,t,whp,choke,glr,temp,water_cut,dsp,flow"
+    types = "string,string,int,float,float,float,float,float,float,float"
+    args = [names, types, "flow", str(tmp_path), "--epochs", "8", "--synth-wells", "8",
+            "--synth-steps", "300", "--device", "cuda"]
+    if model == "lstm":
+        args += ["--seq-len", "32", "--batch-size", "256"]
+    if model == "cnn":
+        args += ["--batch-size", "64", "--lr", "0.01"]
+    if model == "mlp_online":
+        args += ["--online-chunk", "256", "--epochs", "3"]
+    out = run_job(model, args, log=lambda *a, **k: None)
+    assert out["native"] is True
+    h = out["history"]
+    assert min(h["val_loss"]) < h["val_loss"][0] or h["val_loss"][-1] < 1.0
+    assert out["test_loss"] == out["test_loss"]
+    assert (tmp_path / "models" / f"{model}.mdl").exists()

@@ -1,0 +1,102 @@
+"""Trainer semantics, checkpoint/resume, submission contract (CPU, fp32 oracle path)."""
+import os
+import subprocess
+import sys
+
+import pytest
+import torch
+
+from wellflow.config import parse_argv
+from wellflow.train.trainer import EarlyStopping
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+NAMES = "well,field,t,whp,choke,glr,temp,water_cut,dsp,flow"
+TYPES = "string,string,int,float,float,float,float,float,float,float"
+
+
+def test_early_stopping_keras01_rule():
+    es = EarlyStopping(patience=2)
+    seq = [1.0, 0.9, 0.95, 0.96, 0.97]
+    stops = [es.update(v) for v in seq]
+    # after the best (0.9): wait 0 -> 1 -> 2, stop when wait >= patience is checked
+    assert stops == [False, False, False, False, True]
+    assert es.best == 0.9
+
+
+def test_argv_contract_and_storage_path():
+    cfg = parse_argv("cnn", ["a,b", "int,float", "b", "/data/out/"])
+    assert cfg.data == "synth" and cfg.mdl_path() == "/data/out/models/cnn.mdl"
+    assert (cfg.lr, cfg.momentum, cfg.decay, cfg.nesterov) == (0.001, 0.99, 1e-6, True)
+    assert (cfg.batch_size, cfg.epochs, cfg.patience, cfg.loss) == (20, 1000, 10, "mae_clip")
+    cfg = parse_argv("lstm", ["a,b", "int,float", "b", "/data/out", "/x.csv", "--epochs", "3"])
+    assert cfg.data == "/x.csv" and cfg.epochs == 3 and cfg.mdl_path() == "/data/out/models/lstm.mdl"
+    assert (cfg.seq_len, cfg.hidden) == (64, 512)
+
+
+def _run_script(rel, args, env=None, cwd=None):
+    e = dict(os.environ)
+    e.update(env or {})
+    return subprocess.run([sys.executable, os.path.join(ROOT, rel), *args], capture_output=True,
+                          text=True, env=e, cwd=cwd, timeout=300)
+
+
+def test_cnn_script_stdout_contract_and_mdl(tmp_path):
+    r = _run_script("Artificial intelligence models/Static neural network models/cnn.py",
+                    [NAMES, TYPES, "flow", str(tmp_path) + "/", "--epochs", "2", "--synth-wells", "3",
+                     "--synth-steps", "150", "--device", "cpu"])
+    assert r.returncode == 0, r.stderr
+    lines = r.stdout.strip().splitlines()
+    assert lines[0].startswith("StructType([")
+    assert lines[1] == "Categorical variables: well, field"
+    assert lines[-2].startswith("Time elapsed: ") and lines[-2].endswith(" s")
+    assert lines[-1].startswith("Testing set loss: ")
+    assert (tmp_path / "models" / "cnn.mdl").exists()
+
+
+def test_resume_after_injected_fault(tmp_path):
+    args = [NAMES, TYPES, "flow", str(tmp_path), "--epochs", "4", "--synth-wells", "3",
+            "--synth-steps", "120", "--device", "cpu", "--batch-size", "32"]
+    rel = "Artificial intelligence models/Static neural network models/mlp.py"
+    # count steps per epoch from a clean run
+    ok = _run_script(rel, args)
+    assert ok.returncode == 0, ok.stderr
+    for p in (tmp_path / "models").iterdir():
+        p.unlink()
+    r = _run_script(rel, args, env={"WELLFLOW_FAIL_AT_STEP": "9"})
+    assert r.returncode != 0 and "injected fault" in r.stderr
+    assert (tmp_path / "models" / "mlp.ckpt").exists()
+    r2 = _run_script(rel, args + ["--resume"])
+    assert r2.returncode == 0, r2.stderr
+    assert "Resumed from" in r2.stdout
+    # both runs end with the same number of epochs in history
+    from wellflow.utils.checkpoint import load_state
+
+    st = load_state(str(tmp_path / "models" / "mlp.ckpt"))
+    assert st["epoch"] == 4
+
+
+def test_online_and_gilbert_jobs(tmp_path):
+    from wellflow.train.job import run_job
+
+    out = run_job("mlp_online", [NAMES, TYPES, "flow", str(tmp_path), "--epochs", "1", "--synth-wells",
+                                 "4", "--synth-steps", "200", "--online-chunk", "128", "--device", "cpu",
+                                 "--mlp-hidden", "32,16"], log=lambda *a, **k: None)
+    assert out["epochs"] >= 3 and out["test_loss"] == out["test_loss"]
+    # second submission warm-starts from the saved dynamic model
+    msgs = []
+    run_job("mlp_online", [NAMES, TYPES, "flow", str(tmp_path), "--epochs", "1", "--synth-wells", "4",
+                           "--synth-steps", "200", "--online-chunk", "128", "--device", "cpu",
+                           "--mlp-hidden", "32,16"], log=lambda *a, **k: msgs.append(str(a[0]) if a else ""))
+    assert any(m.startswith("Warm start from") for m in msgs)
+    g = run_job("gilbert", [NAMES, TYPES, "flow", str(tmp_path)], log=lambda *a, **k: None)
+    assert g["test_mse"] > 0 and (tmp_path / "models" / "gilbert.mdl").exists()
+
+
+def test_lstm_job_learns_on_cpu(tmp_path):
+    from wellflow.train.job import run_job
+
+    out = run_job("lstm", [NAMES, TYPES, "flow", str(tmp_path), "--epochs", "6", "--synth-wells", "4",
+                           "--synth-steps", "160", "--hidden", "128", "--seq-len", "16",
+                           "--batch-size", "64", "--device", "cpu"], log=lambda *a, **k: None)
+    h = out["history"]
+    assert h["val_loss"][-1] < h["val_loss"][0]
