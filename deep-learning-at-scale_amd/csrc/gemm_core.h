@@ -24,13 +24,13 @@ enum : int { K_CONTIG = 0, MN_CONTIG = 1 };
 
 typedef __attribute__((address_space(3))) bf16x4 lds_bf16x4;
 
-template <int R, int L>
+template <int R, int L, int NT_ = 256>
 struct OpTile {
-  static constexpr int NT = 256;
+  static constexpr int NT = NT_;
   static constexpr int BK = 64;
   static constexpr int CHUNKS = R * BK / 8 / NT;  // 16-B chunks staged per thread
   static constexpr int BYTES = R * BK * 2;
-  static_assert(CHUNKS >= 1, "tile too small for 256 threads");
+  static_assert(CHUNKS >= 1 && R * BK / 8 == CHUNKS * NT, "tile / thread-count mismatch");
   static_assert(L == K_CONTIG || R >= 64, "MN_CONTIG tile needs >= 64 rows");
 
   __device__ static __forceinline__ int hk(int k) {
@@ -106,14 +106,17 @@ struct OpTile {
   }
 };
 
-template <int BM_, int BN_, int LA, int LB>
+// WM x WN waves (NT = 64 * WM * WN threads); 8-wave (512-thread) configurations keep two
+// waves per SIMD on a 1-workgroup-per-CU grid, which the large-K LSTM GEMMs need.
+template <int BM_, int BN_, int LA, int LB, int WM_ = 2, int WN_ = 2>
 struct GemmCfg {
-  static constexpr int BM = BM_, BN = BN_, BK = 64, NT = 256;
-  static constexpr int WM = 2, WN = 2;
+  static constexpr int BM = BM_, BN = BN_, BK = 64;
+  static constexpr int WM = WM_, WN = WN_, NT = 64 * WM_ * WN_;
   static constexpr int WTM = BM / WM, WTN = BN / WN;
   static constexpr int TM = WTM / 16, TN = WTN / 16;
-  using TA = OpTile<BM, LA>;
-  using TB = OpTile<BN, LB>;
+  static_assert(TM >= 1 && TN >= 1, "wave tile must be >= 16x16");
+  using TA = OpTile<BM, LA, NT>;
+  using TB = OpTile<BN, LB, NT>;
   static constexpr int STAGE = TA::BYTES + TB::BYTES;
   static constexpr int LDS_BYTES = 2 * STAGE;
 };

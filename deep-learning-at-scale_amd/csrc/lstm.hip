@@ -47,12 +47,13 @@ void launch_lstm_pack_x(const float* x, bf16_t* XH, LstmDims d, hipStream_t s) {
   hipLaunchKernelGGL(lstm_pack_x_kernel, dim3(blocks), dim3(256), 0, s, x, XH, d);
 }
 
-template <int BM>
-__global__ __launch_bounds__(256) void lstm_fwd_step_kernel(int t, bf16_t* __restrict__ XH,
+template <int BM, int WM, int WN>
+__global__ __launch_bounds__(64 * WM * WN) void lstm_fwd_step_kernel(int t, bf16_t* __restrict__ XH,
                                                             const bf16_t* __restrict__ Wp,
                                                             float* __restrict__ Cst,
                                                             bf16_t* __restrict__ S, LstmDims d) {
-  using C = GemmCfg<BM, 128, K_CONTIG, K_CONTIG>;  // wave N tile = 64 = 4 gates x 16 units
+  // wave N tile must be 64 = 4 gates x 16 units
+  using C = GemmCfg<BM, 64 * WN, K_CONTIG, K_CONTIG, WM, WN>;
   __shared__ __attribute__((aligned(16))) char smem[C::LDS_BYTES];
   const int KA = d.KX + d.H, G = 4 * d.H;
   const int tiles_n = G / C::BN;
@@ -93,19 +94,23 @@ __global__ __launch_bounds__(256) void lstm_fwd_step_kernel(int t, bf16_t* __res
   }
 }
 
-template <int BM>
+template <int BM, int WM, int WN>
 static void fwd_cfg(int t, bf16_t* XH, const bf16_t* Wp, float* Cst, bf16_t* S, LstmDims d,
                     hipStream_t s) {
-  const int tiles = ((d.B + BM - 1) / BM) * (4 * d.H / 128);
-  hipLaunchKernelGGL((lstm_fwd_step_kernel<BM>), dim3(tiles), dim3(256), 0, s, t, XH, Wp, Cst, S, d);
+  const int tiles = ((d.B + BM - 1) / BM) * (4 * d.H / (64 * WN));
+  hipLaunchKernelGGL((lstm_fwd_step_kernel<BM, WM, WN>), dim3(tiles), dim3(64 * WM * WN), 0, s, t,
+                     XH, Wp, Cst, S, d);
 }
 
 void launch_lstm_fwd_step(int t, bf16_t* XH, const bf16_t* Wp, float* Cst, bf16_t* S,
                           LstmDims d, hipStream_t s) {
   switch (d.fwd_variant) {
-    case 1: fwd_cfg<64>(t, XH, Wp, Cst, S, d, s); break;
-    case 2: fwd_cfg<256>(t, XH, Wp, Cst, S, d, s); break;
-    default: fwd_cfg<128>(t, XH, Wp, Cst, S, d, s); break;
+    case 1: fwd_cfg<64, 2, 2>(t, XH, Wp, Cst, S, d, s); break;
+    case 2: fwd_cfg<256, 2, 2>(t, XH, Wp, Cst, S, d, s); break;
+    case 3: fwd_cfg<256, 4, 2>(t, XH, Wp, Cst, S, d, s); break;   // 256x128, 8 waves
+    case 4: fwd_cfg<128, 2, 4>(t, XH, Wp, Cst, S, d, s); break;   // 128x256, 8 waves
+    case 5: fwd_cfg<256, 2, 4>(t, XH, Wp, Cst, S, d, s); break;   // 256x256, 8 waves
+    default: fwd_cfg<128, 2, 2>(t, XH, Wp, Cst, S, d, s); break;
   }
 }
 
@@ -150,13 +155,13 @@ __global__ void lstm_bwd_last_kernel(const float* __restrict__ Cst, const bf16_t
   }
 }
 
-template <int BM, int BN>
-__global__ __launch_bounds__(256) void lstm_bwd_step_kernel(int t, const bf16_t* __restrict__ WhhT,
+template <int BM, int BN, int WM, int WN>
+__global__ __launch_bounds__(64 * WM * WN) void lstm_bwd_step_kernel(int t, const bf16_t* __restrict__ WhhT,
                                                             const float* __restrict__ Cst,
                                                             const bf16_t* __restrict__ S,
                                                             bf16_t* __restrict__ DG,
                                                             float* __restrict__ dcarry, LstmDims d) {
-  using C = GemmCfg<BM, BN, K_CONTIG, K_CONTIG>;
+  using C = GemmCfg<BM, BN, K_CONTIG, K_CONTIG, WM, WN>;
   __shared__ __attribute__((aligned(16))) char smem[C::LDS_BYTES];
   const int G = 4 * d.H;
   const int tiles_n = d.H / C::BN;
@@ -181,12 +186,12 @@ __global__ __launch_bounds__(256) void lstm_bwd_step_kernel(int t, const bf16_t*
   }
 }
 
-template <int BM, int BN>
+template <int BM, int BN, int WM = 2, int WN = 2>
 static void bwd_cfg(int t, const bf16_t* WhhT, const float* Cst, const bf16_t* S, bf16_t* DG,
                     float* dcarry, LstmDims d, hipStream_t s) {
   const int tiles = ((d.B + BM - 1) / BM) * (d.H / BN);
-  hipLaunchKernelGGL((lstm_bwd_step_kernel<BM, BN>), dim3(tiles), dim3(256), 0, s, t, WhhT, Cst, S,
-                     DG, dcarry, d);
+  hipLaunchKernelGGL((lstm_bwd_step_kernel<BM, BN, WM, WN>), dim3(tiles), dim3(64 * WM * WN), 0, s,
+                     t, WhhT, Cst, S, DG, dcarry, d);
 }
 
 void launch_lstm_bwd_step(int t, const bf16_t* WhhT, const float* Cst, const bf16_t* S,
@@ -204,6 +209,9 @@ void launch_lstm_bwd_step(int t, const bf16_t* WhhT, const float* Cst, const bf1
     case 1: bwd_cfg<64, 128>(t, WhhT, Cst, S, DG, dcarry, d, s); break;
     case 2: bwd_cfg<128, 64>(t, WhhT, Cst, S, DG, dcarry, d, s); break;
     case 3: bwd_cfg<64, 64>(t, WhhT, Cst, S, DG, dcarry, d, s); break;
+    case 4: bwd_cfg<128, 128, 2, 4>(t, WhhT, Cst, S, DG, dcarry, d, s); break;  // 8 waves
+    case 5: bwd_cfg<128, 128, 4, 2>(t, WhhT, Cst, S, DG, dcarry, d, s); break;  // 8 waves
+    case 6: bwd_cfg<128, 64, 2, 2>(t, WhhT, Cst, S, DG, dcarry, d, s); break;
     default: bwd_cfg<128, 128>(t, WhhT, Cst, S, DG, dcarry, d, s); break;
   }
 }
