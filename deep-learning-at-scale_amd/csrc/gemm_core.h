@@ -115,6 +115,7 @@ struct GemmCfg {
   static constexpr int WTM = BM / WM, WTN = BN / WN;
   static constexpr int TM = WTM / 16, TN = WTN / 16;
   static_assert(TM >= 1 && TN >= 1, "wave tile must be >= 16x16");
+  static constexpr int LA_ = LA, LB_ = LB;
   using TA = OpTile<BM, LA, NT>;
   using TB = OpTile<BN, LB, NT>;
   static constexpr int STAGE = TA::BYTES + TB::BYTES;
@@ -174,6 +175,128 @@ __device__ __forceinline__ void gemm_mainloop(const bf16_t* __restrict__ A, long
     }
     __syncthreads();
   }
+}
+
+// ----------------------------------------------------------------------------------------
+// Direct-to-LDS staging (global_load_lds_dwordx4): a wave-instruction writes 1 KiB of LDS
+// lane-linearly (base + 16*lane), so the XOR swizzles above move onto the per-lane SOURCE
+// address (cdna_hip_programming.md §5.4 rule 21) and the LDS images — hence frag() — stay
+// exactly the ones the register-staged path writes. No VGPRs, no ds_write instructions.
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+typedef __attribute__((address_space(3))) void lds_void;
+
+template <int R, int L, int NT>
+struct GldsTile {
+  static constexpr int BYTES = R * 64 * 2;
+  static constexpr int PIECES = BYTES / 1024;  // 1-KiB wave-instructions per tile
+  static constexpr int NW = NT / 64;
+  static constexpr int PER_WAVE = PIECES / NW;
+  static_assert(PIECES % NW == 0 && PER_WAVE >= 1, "tile pieces must split evenly over waves");
+
+  __device__ static __forceinline__ int hk(int k) {
+    return ((k & 3) | ((k >> 1) & 4)) & (R / 16 - 1);
+  }
+
+  // Issue this wave's glds for the tile (row0, k0) -> lds_tile. All rows/k in range.
+  __device__ static __forceinline__ void issue(const bf16_t* __restrict__ p, long ld, int row0,
+                                               int k0, char* lds_tile, int wid, int lane) {
+#pragma unroll
+    for (int i = 0; i < PER_WAVE; ++i) {
+      const int piece = i * NW + wid;
+      const bf16_t* src;
+      if constexpr (L == K_CONTIG) {
+        const int row = piece * 8 + (lane >> 3);
+        const int lc = (lane & 7) ^ ((row >> 1) & 7);
+        src = p + (size_t)(row0 + row) * ld + k0 + lc * 8;
+      } else {
+        constexpr int SPR = R / 8;  // 16-B slots per k-row
+        const int k = piece * (512 / R) + lane / SPR;
+        const int slot = lane % SPR;
+        const int col = (((slot >> 1) ^ hk(k)) << 4) + ((slot & 1) << 3);
+        src = p + (size_t)(k0 + k) * ld + row0 + col;
+      }
+      __builtin_amdgcn_global_load_lds((const void*)src, (lds_void*)(lds_tile + piece * 1024), 16, 0, 0);
+    }
+  }
+};
+
+// Same contract as gemm_mainloop but for FULL tiles only (m0+BM <= M, n0+BN <= N,
+// kbeg + 64*nk <= K): STAGES-deep LDS ring filled by glds, one barrier per K-step,
+// counted vmcnt so STAGES-2 tiles stay in flight across it (guide §5 "Pipelining across
+// barriers": raw s_barrier, never __syncthreads() while a glds is outstanding).
+template <class C, int STAGES>
+__device__ __forceinline__ void gemm_mainloop_glds(const bf16_t* __restrict__ A, long lda,
+                                                   const bf16_t* __restrict__ B, long ldb, int kbeg,
+                                                   int nk, int m0, int n0, char* smem,
+                                                   f32x4 (&acc)[C::TM][C::TN]) {
+  using TA = typename C::TA;
+  using TB = typename C::TB;
+  static_assert(STAGES >= 2 && STAGES <= 4, "2..4 stages");
+  constexpr int LA_ = C::LA_, LB_ = C::LB_;
+  using QA = GldsTile<C::BM, LA_, C::NT>;
+  using QB = GldsTile<C::BN, LB_, C::NT>;
+  constexpr int STAGE = QA::BYTES + QB::BYTES;
+  constexpr int LPT = QA::PER_WAVE + QB::PER_WAVE;  // glds per wave per K-tile
+  const int lane = threadIdx.x & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wm = wid / C::WN, wn = wid % C::WN;
+#pragma unroll
+  for (int i = 0; i < C::TM; ++i)
+#pragma unroll
+    for (int j = 0; j < C::TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  if (nk <= 0) return;
+
+#pragma unroll
+  for (int s = 0; s < STAGES - 1; ++s) {
+    if (s < nk) {
+      char* st = smem + s * STAGE;
+      QA::issue(A, lda, m0, kbeg + s * 64, st, wid, lane);
+      QB::issue(B, ldb, n0, kbeg + s * 64, st + QA::BYTES, wid, lane);
+    }
+  }
+  for (int t = 0; t < nk; ++t) {
+    // tiles issued after t that may stay in flight: min(nk-1, t+STAGES-2) - t
+    const int ahead = min(nk - 1, t + STAGES - 2) - t;
+    if constexpr (STAGES >= 4) {
+      if (ahead >= 2) wait_vmcnt<2 * LPT>();
+      else if (ahead == 1) wait_vmcnt<LPT>();
+      else wait_vmcnt<0>();
+    } else if constexpr (STAGES == 3) {
+      if (ahead >= 1) wait_vmcnt<LPT>();
+      else wait_vmcnt<0>();
+    } else {
+      wait_vmcnt<0>();
+    }
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    const int tn = t + STAGES - 1;
+    if (tn < nk) {  // refill the stage every wave finished reading in iteration t-1
+      char* st = smem + (tn % STAGES) * STAGE;
+      QA::issue(A, lda, m0, kbeg + tn * 64, st, wid, lane);
+      QB::issue(B, ldb, n0, kbeg + tn * 64, st + QA::BYTES, wid, lane);
+    }
+    const char* cur = smem + (t % STAGES) * STAGE;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      bf16x8 a[C::TM], b[C::TN];
+#pragma unroll
+      for (int i = 0; i < C::TM; ++i) a[i] = TA::frag(cur, wm * C::WTM + i * 16, kk, lane);
+#pragma unroll
+      for (int j = 0; j < C::TN; ++j) b[j] = TB::frag(cur + QA::BYTES, wn * C::WTN + j * 16, kk, lane);
+#pragma unroll
+      for (int i = 0; i < C::TM; ++i)
+#pragma unroll
+        for (int j = 0; j < C::TN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
+    }
+  }
+  // leave LDS reusable by the caller's epilogue
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
 }
 
 // Output coordinates of accumulator element acc[i][j][r] (16x16 C/D map: col = lane&15,

@@ -47,14 +47,17 @@ void launch_lstm_pack_x(const float* x, bf16_t* XH, LstmDims d, hipStream_t s) {
   hipLaunchKernelGGL(lstm_pack_x_kernel, dim3(blocks), dim3(256), 0, s, x, XH, d);
 }
 
-template <int BM, int WM, int WN>
+// STAGES == 0: register-staged mainloop (any batch); STAGES >= 2: direct-to-LDS ring
+// (requires B % BM == 0, checked by the launcher).
+template <int BM, int WM, int WN, int STAGES>
 __global__ __launch_bounds__(64 * WM * WN) void lstm_fwd_step_kernel(int t, bf16_t* __restrict__ XH,
                                                             const bf16_t* __restrict__ Wp,
                                                             float* __restrict__ Cst,
                                                             bf16_t* __restrict__ S, LstmDims d) {
   // wave N tile must be 64 = 4 gates x 16 units
   using C = GemmCfg<BM, 64 * WN, K_CONTIG, K_CONTIG, WM, WN>;
-  __shared__ __attribute__((aligned(16))) char smem[C::LDS_BYTES];
+  constexpr int LDSB = STAGES * C::STAGE > C::LDS_BYTES ? STAGES * C::STAGE : C::LDS_BYTES;
+  __shared__ __attribute__((aligned(16))) char smem[LDSB];
   const int KA = d.KX + d.H, G = 4 * d.H;
   const int tiles_n = G / C::BN;
   const int L = xcd_remap(blockIdx.x, gridDim.x);
@@ -62,7 +65,10 @@ __global__ __launch_bounds__(64 * WM * WN) void lstm_fwd_step_kernel(int t, bf16
   const bf16_t* A = XH + (size_t)t * d.B * KA;
 
   f32x4 acc[C::TM][C::TN];
-  gemm_mainloop<C>(A, KA, d.B, Wp, KA, G, 0, KA, m0, n0, smem, acc);
+  if constexpr (STAGES >= 2)
+    gemm_mainloop_glds<C, STAGES>(A, KA, Wp, KA, 0, KA / 64, m0, n0, smem, acc);
+  else
+    gemm_mainloop<C>(A, KA, d.B, Wp, KA, G, 0, KA, m0, n0, smem, acc);
 
   const AccCoord<C> cc(m0, n0);
   const int u = (cc.nb >> 6) * 16 + (threadIdx.x & 15);
@@ -94,12 +100,16 @@ __global__ __launch_bounds__(64 * WM * WN) void lstm_fwd_step_kernel(int t, bf16
   }
 }
 
-template <int BM, int WM, int WN>
+template <int BM, int WM, int WN, int STAGES = 0>
 static void fwd_cfg(int t, bf16_t* XH, const bf16_t* Wp, float* Cst, bf16_t* S, LstmDims d,
                     hipStream_t s) {
+  if (STAGES >= 2 && (d.B % BM != 0 || (4 * d.H) % (64 * WN) != 0)) {  // partial tiles
+    fwd_cfg<BM, WM, WN, 0>(t, XH, Wp, Cst, S, d, s);
+    return;
+  }
   const int tiles = ((d.B + BM - 1) / BM) * (4 * d.H / (64 * WN));
-  hipLaunchKernelGGL((lstm_fwd_step_kernel<BM, WM, WN>), dim3(tiles), dim3(64 * WM * WN), 0, s, t,
-                     XH, Wp, Cst, S, d);
+  hipLaunchKernelGGL((lstm_fwd_step_kernel<BM, WM, WN, STAGES>), dim3(tiles), dim3(64 * WM * WN), 0,
+                     s, t, XH, Wp, Cst, S, d);
 }
 
 void launch_lstm_fwd_step(int t, bf16_t* XH, const bf16_t* Wp, float* Cst, bf16_t* S,
@@ -110,6 +120,11 @@ void launch_lstm_fwd_step(int t, bf16_t* XH, const bf16_t* Wp, float* Cst, bf16_
     case 3: fwd_cfg<256, 4, 2>(t, XH, Wp, Cst, S, d, s); break;   // 256x128, 8 waves
     case 4: fwd_cfg<128, 2, 4>(t, XH, Wp, Cst, S, d, s); break;   // 128x256, 8 waves
     case 5: fwd_cfg<256, 2, 4>(t, XH, Wp, Cst, S, d, s); break;   // 256x256, 8 waves
+    case 6: fwd_cfg<256, 2, 4, 2>(t, XH, Wp, Cst, S, d, s); break;  // glds, 2 stages (128 KiB)
+    case 7: fwd_cfg<128, 2, 4, 3>(t, XH, Wp, Cst, S, d, s); break;  // glds, 3 stages (144 KiB)
+    case 8: fwd_cfg<128, 2, 2, 3>(t, XH, Wp, Cst, S, d, s); break;  // glds, 3 stages (96 KiB)
+    case 9: fwd_cfg<256, 4, 2, 3>(t, XH, Wp, Cst, S, d, s); break;  // glds, 3 stages (144 KiB)
+    case 10: fwd_cfg<128, 2, 2, 2>(t, XH, Wp, Cst, S, d, s); break; // glds, 2 stages (64 KiB)
     default: fwd_cfg<128, 2, 2>(t, XH, Wp, Cst, S, d, s); break;
   }
 }
@@ -155,14 +170,15 @@ __global__ void lstm_bwd_last_kernel(const float* __restrict__ Cst, const bf16_t
   }
 }
 
-template <int BM, int BN, int WM, int WN>
+template <int BM, int BN, int WM, int WN, int STAGES>
 __global__ __launch_bounds__(64 * WM * WN) void lstm_bwd_step_kernel(int t, const bf16_t* __restrict__ WhhT,
                                                             const float* __restrict__ Cst,
                                                             const bf16_t* __restrict__ S,
                                                             bf16_t* __restrict__ DG,
                                                             float* __restrict__ dcarry, LstmDims d) {
   using C = GemmCfg<BM, BN, K_CONTIG, K_CONTIG, WM, WN>;
-  __shared__ __attribute__((aligned(16))) char smem[C::LDS_BYTES];
+  constexpr int LDSB = STAGES * C::STAGE > C::LDS_BYTES ? STAGES * C::STAGE : C::LDS_BYTES;
+  __shared__ __attribute__((aligned(16))) char smem[LDSB];
   const int G = 4 * d.H;
   const int tiles_n = d.H / C::BN;
   const int L = xcd_remap(blockIdx.x, gridDim.x);
@@ -170,7 +186,10 @@ __global__ __launch_bounds__(64 * WM * WN) void lstm_bwd_step_kernel(int t, cons
   const bf16_t* A = DG + (size_t)(t + 1) * d.B * G;
 
   f32x4 acc[C::TM][C::TN];
-  gemm_mainloop<C>(A, G, d.B, WhhT, G, d.H, 0, G, m0, n0, smem, acc);
+  if constexpr (STAGES >= 2)
+    gemm_mainloop_glds<C, STAGES>(A, G, WhhT, G, 0, G / 64, m0, n0, smem, acc);
+  else
+    gemm_mainloop<C>(A, G, d.B, WhhT, G, d.H, 0, G, m0, n0, smem, acc);
 
   const AccCoord<C> cc(m0, n0);
 #pragma unroll
@@ -186,12 +205,16 @@ __global__ __launch_bounds__(64 * WM * WN) void lstm_bwd_step_kernel(int t, cons
   }
 }
 
-template <int BM, int BN, int WM = 2, int WN = 2>
+template <int BM, int BN, int WM = 2, int WN = 2, int STAGES = 0>
 static void bwd_cfg(int t, const bf16_t* WhhT, const float* Cst, const bf16_t* S, bf16_t* DG,
                     float* dcarry, LstmDims d, hipStream_t s) {
+  if (STAGES >= 2 && d.B % BM != 0) {
+    bwd_cfg<BM, BN, WM, WN, 0>(t, WhhT, Cst, S, DG, dcarry, d, s);
+    return;
+  }
   const int tiles = ((d.B + BM - 1) / BM) * (d.H / BN);
-  hipLaunchKernelGGL((lstm_bwd_step_kernel<BM, BN, WM, WN>), dim3(tiles), dim3(64 * WM * WN), 0, s,
-                     t, WhhT, Cst, S, DG, dcarry, d);
+  hipLaunchKernelGGL((lstm_bwd_step_kernel<BM, BN, WM, WN, STAGES>), dim3(tiles), dim3(64 * WM * WN),
+                     0, s, t, WhhT, Cst, S, DG, dcarry, d);
 }
 
 void launch_lstm_bwd_step(int t, const bf16_t* WhhT, const float* Cst, const bf16_t* S,
@@ -212,6 +235,12 @@ void launch_lstm_bwd_step(int t, const bf16_t* WhhT, const float* Cst, const bf1
     case 4: bwd_cfg<128, 128, 2, 4>(t, WhhT, Cst, S, DG, dcarry, d, s); break;  // 8 waves
     case 5: bwd_cfg<128, 128, 4, 2>(t, WhhT, Cst, S, DG, dcarry, d, s); break;  // 8 waves
     case 6: bwd_cfg<128, 64, 2, 2>(t, WhhT, Cst, S, DG, dcarry, d, s); break;
+    case 7: bwd_cfg<64, 64, 2, 2, 3>(t, WhhT, Cst, S, DG, dcarry, d, s); break;    // glds
+    case 8: bwd_cfg<128, 128, 2, 4, 3>(t, WhhT, Cst, S, DG, dcarry, d, s); break;  // glds 8w
+    case 9: bwd_cfg<64, 128, 2, 2, 3>(t, WhhT, Cst, S, DG, dcarry, d, s); break;   // glds
+    case 10: bwd_cfg<128, 64, 2, 2, 3>(t, WhhT, Cst, S, DG, dcarry, d, s); break;  // glds
+    case 11: bwd_cfg<128, 128, 2, 2, 3>(t, WhhT, Cst, S, DG, dcarry, d, s); break; // glds 4w
+    case 12: bwd_cfg<64, 64, 2, 2, 4>(t, WhhT, Cst, S, DG, dcarry, d, s); break;   // glds 4st
     default: bwd_cfg<128, 128>(t, WhhT, Cst, S, DG, dcarry, d, s); break;
   }
 }

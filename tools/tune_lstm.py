@@ -44,6 +44,23 @@ def main():
     dims = eng._dims(B)
     lay = eng.lay
     gW, _, _ = lay.views(eng.grads)
+    # correctness: every variant must reproduce the v0 (register-staged) outputs exactly
+    C.lstm_forward(eng.XH, eng.Wp, eng.Cst, eng.S, *dims, 0)
+    ref_fwd = (eng.XH.clone(), eng.Cst.clone(), eng.S.clone())
+    for v in map(int, a.fwd.split(",")):
+        eng.XH[(B * lay.KA):].zero_(); eng.Cst[B * H:].zero_(); eng.S.zero_()
+        C.lstm_forward(eng.XH, eng.Wp, eng.Cst, eng.S, *dims, v)
+        torch.cuda.synchronize()
+        errs = [(x.float() - y.float()).abs().max().item() for x, y in zip((eng.XH, eng.Cst, eng.S), ref_fwd)]
+        print(f"check fwd v{v}: max|diff| XH {errs[0]:.3g} C {errs[1]:.3g} S {errs[2]:.3g}", flush=True)
+    w_out = lay.views(eng.params)[1]
+    C.lstm_backward(eng.WhhT, eng.XH, eng.Cst, eng.S, eng.DG, eng.dcarry, eng.dy, w_out, *dims, 0)
+    ref_dg = eng.DG.clone()
+    for v in map(int, a.bwd.split(",")):
+        eng.DG.zero_()
+        C.lstm_backward(eng.WhhT, eng.XH, eng.Cst, eng.S, eng.DG, eng.dcarry, eng.dy, w_out, *dims, v)
+        torch.cuda.synchronize()
+        print(f"check bwd v{v}: max|diff| DG {(eng.DG.float() - ref_dg.float()).abs().max().item():.3g}", flush=True)
     res = {}
     for r in range(a.rounds):
         for v in map(int, a.fwd.split(",")):
