@@ -101,12 +101,13 @@ wf::LstmDims lstm_dims(int64_t B, int64_t T, int64_t F, int64_t KX, int64_t H) {
 void check_lstm_state(const at::Tensor& XH, const at::Tensor& Cst, const at::Tensor& S,
                       const wf::LstmDims& d) {
   const int64_t KA = d.KX + d.H, G = 4 * d.H;
+  const int64_t Bp = (d.B + 15) / 16 * 16;  // fragment-native state is padded to 16 rows
   check_t(XH, at::kBFloat16, "XH");
   check_t(Cst, at::kFloat, "Cst");
   check_t(S, at::kBFloat16, "S");
   check_extent(XH, (int64_t)(d.T + 1) * d.B * KA, "XH");
-  check_extent(Cst, (int64_t)(d.T + 1) * d.B * d.H, "Cst");
-  check_extent(S, (int64_t)d.T * d.B * G, "S");
+  check_extent(Cst, (int64_t)(d.T + 1) * Bp * d.H, "Cst");
+  check_extent(S, (int64_t)d.T * Bp * G, "S");
 }
 
 void lstm_pack_x(const at::Tensor& x, const at::Tensor& XH, int64_t B, int64_t T, int64_t F,
@@ -145,7 +146,7 @@ void lstm_backward(const at::Tensor& WhhT, const at::Tensor& XH, const at::Tenso
   check_t(DG, at::kBFloat16, "DG");
   check_extent(DG, T * B * 4 * H, "DG");
   check_t(dcarry, at::kFloat, "dcarry");
-  check_extent(dcarry, B * H, "dcarry");
+  check_extent(dcarry, (B + 15) / 16 * 16 * H, "dcarry");
   check_t(dy, at::kFloat, "dy");
   check_extent(dy, B, "dy");
   check_t(w_out, at::kFloat, "w_out");

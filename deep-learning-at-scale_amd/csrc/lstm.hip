@@ -23,6 +23,16 @@ namespace wf {
 
 __device__ __forceinline__ int gate_col(int gate, int u) { return (u >> 4) * 64 + gate * 16 + (u & 15); }
 
+// Fragment-native (FN) layout of the per-(row, unit) state the backward pass re-reads
+// (C, S, dc carry): 16x16 blocks, block (m>>4, u>>4) row-major over H/16 unit blocks;
+// inside a block element (m, u) sits at lane ((m&15)>>2)*16 + (u&15), slot m&3 — exactly
+// where the 16x16 MFMA C map puts it, so every lane moves 16-32 contiguous bytes.
+// Batch rows are padded to a multiple of 16 (fn_rows).
+__host__ __device__ __forceinline__ int fn_rows(int B) { return (B + 15) & ~15; }
+__device__ __forceinline__ size_t fn_block(int mrow0, int u, int H) {
+  return (size_t)(mrow0 >> 4) * (H >> 4) + (u >> 4);
+}
+
 // XH[t][b][0:KX] = [x[b][t][0:F], 1, 0, ...]; one thread per (t, b, k).
 __global__ void lstm_pack_x_kernel(const float* __restrict__ x, bf16_t* __restrict__ XH,
                                    LstmDims d) {
@@ -71,32 +81,39 @@ __global__ __launch_bounds__(64 * WM * WN) void lstm_fwd_step_kernel(int t, bf16
     gemm_mainloop<C>(A, KA, d.B, Wp, KA, G, 0, KA, m0, n0, smem, acc);
 
   const AccCoord<C> cc(m0, n0);
-  const int u = (cc.nb >> 6) * 16 + (threadIdx.x & 15);
-  const float* cprev = Cst + (size_t)t * d.B * d.H;
-  float* cnext = Cst + (size_t)(t + 1) * d.B * d.H;
+  const int lane = threadIdx.x & 63;
+  const int u = (cc.nb >> 6) * 16 + (lane & 15);
+  const int Bp = fn_rows(d.B);
+  const float* cprev = Cst + (size_t)t * Bp * d.H;
+  float* cnext = Cst + (size_t)(t + 1) * Bp * d.H;
   bf16_t* hnext = XH + (size_t)(t + 1) * d.B * KA + d.KX;
-  bf16_t* St = S + (size_t)t * d.B * G;
+  bf16_t* St = S + (size_t)t * Bp * G;
 #pragma unroll
   for (int i = 0; i < C::TM; ++i) {
+    const int mrow0 = cc.mb + i * 16;
+    if (mrow0 >= d.B) continue;
+    const size_t blk = fn_block(mrow0, u, d.H);
+    const float4 cp = *reinterpret_cast<const float4*>(cprev + blk * 256 + lane * 4);
+    const float cpv[4] = {cp.x, cp.y, cp.z, cp.w};
+    float cv[4];
+    unsigned pk[8];
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      const int m = cc.row(i, r);
-      if (m >= d.B) continue;
       const float ig = sigmoidf_(acc[i][0][r]);
       const float fg = sigmoidf_(acc[i][1][r]);
       const float gg = tanhf_(acc[i][2][r]);
       const float og = sigmoidf_(acc[i][3][r]);
-      const size_t mu = (size_t)m * d.H + u;
-      const float c = fg * cprev[mu] + ig * gg;
-      const float h = og * tanhf_(c);
-      cnext[mu] = c;
-      hnext[(size_t)m * KA + u] = f2bf(h);
-      bf16_t* srow = St + (size_t)m * G;
-      srow[gate_col(0, u)] = f2bf(ig);
-      srow[gate_col(1, u)] = f2bf(fg);
-      srow[gate_col(2, u)] = f2bf(gg);
-      srow[gate_col(3, u)] = f2bf(og);
+      const float c = fg * cpv[r] + ig * gg;
+      cv[r] = c;
+      pk[2 * r] = (unsigned)f2bf(ig) | ((unsigned)f2bf(fg) << 16);
+      pk[2 * r + 1] = (unsigned)f2bf(gg) | ((unsigned)f2bf(og) << 16);
+      const int m = mrow0 + 4 * (lane >> 4) + r;
+      if (m < d.B) hnext[(size_t)m * KA + u] = f2bf(og * tanhf_(c));
     }
+    *reinterpret_cast<float4*>(cnext + blk * 256 + lane * 4) = make_float4(cv[0], cv[1], cv[2], cv[3]);
+    uint4* sp = reinterpret_cast<uint4*>(St + blk * 1024 + lane * 16);
+    sp[0] = make_uint4(pk[0], pk[1], pk[2], pk[3]);
+    sp[1] = make_uint4(pk[4], pk[5], pk[6], pk[7]);
   }
 }
 
@@ -129,44 +146,67 @@ void launch_lstm_fwd_step(int t, bf16_t* XH, const bf16_t* Wp, float* Cst, bf16_
   }
 }
 
-// Cell backward for one (row m, unit u) of step t given dh_t; updates the dc carry and
-// writes the four gate-gradients of step t into DG[t] (permuted column order).
-__device__ __forceinline__ void cell_bwd(int t, int m, int u, float dh, const float* __restrict__ Cst,
-                                         const bf16_t* __restrict__ S, bf16_t* __restrict__ DG,
-                                         float* __restrict__ dcarry, const LstmDims& d) {
-  const int G = 4 * d.H;
-  const size_t rowg = ((size_t)t * d.B + m) * G;
-  const float ig = bf2f(S[rowg + gate_col(0, u)]);
-  const float fg = bf2f(S[rowg + gate_col(1, u)]);
-  const float gg = bf2f(S[rowg + gate_col(2, u)]);
-  const float og = bf2f(S[rowg + gate_col(3, u)]);
-  const size_t mu = (size_t)m * d.H + u;
-  const float c = Cst[(size_t)(t + 1) * d.B * d.H + mu];
-  const float cp = Cst[(size_t)t * d.B * d.H + mu];
-  const float tc = tanhf_(c);
-  const float dc = dcarry[mu] + dh * og * (1.f - tc * tc);
-  const float d_o = dh * tc * og * (1.f - og);
-  const float d_i = dc * gg * ig * (1.f - ig);
-  const float d_f = dc * cp * fg * (1.f - fg);
-  const float d_g = dc * ig * (1.f - gg * gg);
-  dcarry[mu] = dc * fg;
-  DG[rowg + gate_col(0, u)] = f2bf(d_i);
-  DG[rowg + gate_col(1, u)] = f2bf(d_f);
-  DG[rowg + gate_col(2, u)] = f2bf(d_g);
-  DG[rowg + gate_col(3, u)] = f2bf(d_o);
+// Cell backward for the 4 rows (mrow0 + 4*(lane>>4) + r) x unit u of step t held by this
+// lane, given dh for them: reads the lane's fragment-native S / C / dc-carry slots with
+// 16-B vector accesses, updates the carry and writes the gate gradients into DG[t]
+// (row-major, permuted columns: it is the next GEMM's A operand).
+__device__ __forceinline__ void cell_bwd4(int t, int mrow0, int u, int lane, const float (&dh)[4],
+                                          const float* __restrict__ Cst,
+                                          const bf16_t* __restrict__ S, bf16_t* __restrict__ DG,
+                                          float* __restrict__ dcarry, const LstmDims& d) {
+  const int G = 4 * d.H, Bp = fn_rows(d.B);
+  const size_t blk = fn_block(mrow0, u, d.H);
+  const uint4* sp = reinterpret_cast<const uint4*>(S + (size_t)t * Bp * G + blk * 1024 + lane * 16);
+  const uint4 s0 = sp[0], s1 = sp[1];
+  const unsigned pk[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
+  const float4 c4 = *reinterpret_cast<const float4*>(Cst + (size_t)(t + 1) * Bp * d.H + blk * 256 + lane * 4);
+  const float4 p4 = *reinterpret_cast<const float4*>(Cst + (size_t)t * Bp * d.H + blk * 256 + lane * 4);
+  float4* dcp = reinterpret_cast<float4*>(dcarry + blk * 256 + lane * 4);
+  const float4 k4 = *dcp;
+  const float cv[4] = {c4.x, c4.y, c4.z, c4.w}, pv[4] = {p4.x, p4.y, p4.z, p4.w};
+  const float kv[4] = {k4.x, k4.y, k4.z, k4.w};
+  float nk[4];
+  bf16_t* dgt = DG + (size_t)t * d.B * G;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const float ig = bf2f((bf16_t)(pk[2 * r] & 0xffff)), fg = bf2f((bf16_t)(pk[2 * r] >> 16));
+    const float gg = bf2f((bf16_t)(pk[2 * r + 1] & 0xffff)), og = bf2f((bf16_t)(pk[2 * r + 1] >> 16));
+    const float tc = tanhf_(cv[r]);
+    const float dc = kv[r] + dh[r] * og * (1.f - tc * tc);
+    nk[r] = dc * fg;
+    const int m = mrow0 + 4 * (lane >> 4) + r;
+    if (m < d.B) {
+      bf16_t* row = dgt + (size_t)m * G;
+      row[gate_col(0, u)] = f2bf(dc * gg * ig * (1.f - ig));
+      row[gate_col(1, u)] = f2bf(dc * pv[r] * fg * (1.f - fg));
+      row[gate_col(2, u)] = f2bf(dc * ig * (1.f - gg * gg));
+      row[gate_col(3, u)] = f2bf(dh[r] * tc * og * (1.f - og));
+    }
+  }
+  *dcp = make_float4(nk[0], nk[1], nk[2], nk[3]);
 }
 
-// t = T-1: dh comes from the regression head, dh[m][u] = dy[m] * w_out[u]; dcarry starts at 0.
+// t = T-1: dh comes from the regression head, dh[m][u] = dy[m] * w_out[u]; the carry
+// starts at 0. One thread per (fragment-native block, lane) = 4 rows of one unit.
 __global__ void lstm_bwd_last_kernel(const float* __restrict__ Cst, const bf16_t* __restrict__ S,
                                      bf16_t* __restrict__ DG, float* __restrict__ dcarry,
                                      const float* __restrict__ dy, const float* __restrict__ w_out,
                                      LstmDims d) {
-  const long total = (long)d.B * d.H;
+  const int ub = d.H >> 4;
+  const long total = (long)(fn_rows(d.B) >> 4) * ub * 64;
   for (long idx = blockIdx.x * (long)blockDim.x + threadIdx.x; idx < total;
        idx += (long)gridDim.x * blockDim.x) {
-    const int u = idx % d.H, m = idx / d.H;
-    dcarry[idx] = 0.f;
-    cell_bwd(d.T - 1, m, u, dy[m] * w_out[u], Cst, S, DG, dcarry, d);
+    const int lane = idx & 63;
+    const long blk = idx >> 6;
+    const int mrow0 = (int)(blk / ub) * 16, u = (int)(blk % ub) * 16 + (lane & 15);
+    *reinterpret_cast<float4*>(dcarry + blk * 256 + lane * 4) = make_float4(0.f, 0.f, 0.f, 0.f);
+    float dh[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int m = mrow0 + 4 * (lane >> 4) + r;
+      dh[r] = m < d.B ? dy[m] * w_out[u] : 0.f;
+    }
+    cell_bwd4(d.T - 1, mrow0, u, lane, dh, Cst, S, DG, dcarry, d);
   }
 }
 
@@ -192,16 +232,17 @@ __global__ __launch_bounds__(64 * WM * WN) void lstm_bwd_step_kernel(int t, cons
     gemm_mainloop<C>(A, G, d.B, WhhT, G, d.H, 0, G, m0, n0, smem, acc);
 
   const AccCoord<C> cc(m0, n0);
+  const int lane = threadIdx.x & 63;
 #pragma unroll
   for (int j = 0; j < C::TN; ++j) {
     const int u = cc.col(j);
 #pragma unroll
-    for (int i = 0; i < C::TM; ++i)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int m = cc.row(i, r);
-        if (m < d.B) cell_bwd(t, m, u, acc[i][j][r], Cst, S, DG, dcarry, d);
-      }
+    for (int i = 0; i < C::TM; ++i) {
+      const int mrow0 = cc.mb + i * 16;
+      if (mrow0 >= d.B) continue;
+      const float dh[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
+      cell_bwd4(t, mrow0, u, lane, dh, Cst, S, DG, dcarry, d);
+    }
   }
 }
 
@@ -221,7 +262,7 @@ void launch_lstm_bwd_step(int t, const bf16_t* WhhT, const float* Cst, const bf1
                           bf16_t* DG, float* dcarry, const float* dy, const float* w_out,
                           LstmDims d, hipStream_t s) {
   if (t == d.T - 1) {
-    const long total = (long)d.B * d.H;
+    const long total = (long)(fn_rows(d.B) >> 4) * (d.H >> 4) * 64;
     int blocks = (int)((total + 255) / 256);
     if (blocks > 8192) blocks = 8192;
     hipLaunchKernelGGL(lstm_bwd_last_kernel, dim3(blocks), dim3(256), 0, s, Cst, S, DG, dcarry,

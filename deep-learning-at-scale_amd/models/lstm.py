@@ -152,11 +152,12 @@ class NativeLSTM:
         self.grads = grads if grads is not None else torch.zeros(lay.numel, device=dev)
         bf = torch.bfloat16
         T, B, H = seq_len, batch, hidden
+        Bp = _round_up(B, 16)  # fragment-native state (C, S, dc carry) is 16-row padded
         self.XH = torch.zeros((T + 1) * B * lay.KA, dtype=bf, device=dev)
-        self.Cst = torch.zeros((T + 1) * B * H, dtype=torch.float32, device=dev)
-        self.S = torch.empty(T * B * lay.G, dtype=bf, device=dev)
+        self.Cst = torch.zeros((T + 1) * Bp * H, dtype=torch.float32, device=dev)
+        self.S = torch.empty(T * Bp * lay.G, dtype=bf, device=dev)
         self.DG = torch.empty(T * B * lay.G, dtype=bf, device=dev)
-        self.dcarry = torch.empty(B * H, dtype=torch.float32, device=dev)
+        self.dcarry = torch.empty(Bp * H, dtype=torch.float32, device=dev)
         self.Wp = torch.empty(lay.G * lay.KA, dtype=bf, device=dev)
         self.WhhT = torch.empty(H * lay.G, dtype=bf, device=dev)
         self.pred = torch.empty(B, dtype=torch.float32, device=dev)

@@ -48,7 +48,7 @@ def main():
     C.lstm_forward(eng.XH, eng.Wp, eng.Cst, eng.S, *dims, 0)
     ref_fwd = (eng.XH.clone(), eng.Cst.clone(), eng.S.clone())
     for v in map(int, a.fwd.split(",")):
-        eng.XH[(B * lay.KA):].zero_(); eng.Cst[B * H:].zero_(); eng.S.zero_()
+        eng.Cst[B * H:].zero_(); eng.S.zero_()  # (XH keeps x_t; its h part is rewritten)
         C.lstm_forward(eng.XH, eng.Wp, eng.Cst, eng.S, *dims, v)
         torch.cuda.synchronize()
         errs = [(x.float() - y.float()).abs().max().item() for x, y in zip((eng.XH, eng.Cst, eng.S), ref_fwd)]
