@@ -7,11 +7,21 @@
 #include <ATen/hip/impl/HIPStreamMasqueradingAsCUDA.h>
 #include <ATen/hip/impl/HIPGuardImplMasqueradingAsCUDA.h>
 
+#include <cstdlib>
+
 #include "kernels.h"
 
 namespace {
 
 using wf::bf16_t;
+
+bool disable_glds() {
+  static const bool off = [] {
+    const char* v = std::getenv("WELLFLOW_NO_GLDS");
+    return v != nullptr && v[0] == '1';
+  }();
+  return off;
+}
 
 hipStream_t cur_stream() { return c10::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream(); }
 
@@ -84,9 +94,18 @@ void gemm(const at::Tensor& A, bool a_mn, int64_t lda, const at::Tensor& B, bool
   e.drop_p = (float)drop_p;
   e.seed = (unsigned long long)seed;
   TORCH_CHECK(ksplit == 1 || atomic, "gemm: split-K needs atomic accumulation");
+  // glds (whole-tile) path: the 128x128 tiles may over-read rows/cols past M / N; allow it
+  // only when that stays inside both allocations (and every K chunk is 64-aligned).
+  const int64_t Mc = (M + 127) / 128 * 128, Nc = (N + 127) / 128 * 128;
+  int64_t kchunk = (K + std::max<int64_t>(ksplit, 1) - 1) / std::max<int64_t>(ksplit, 1);
+  kchunk = (kchunk + 63) / 64 * 64;
+  const bool glds_ok = (K % 64 == 0) && (kchunk % 64 == 0) &&
+                       A.numel() >= operand_extent(a_mn, Mc, K, lda) + (a_mn ? 0 : 0) &&
+                       B.numel() >= operand_extent(b_mn, Nc, K, ldb) &&
+                       (a_mn || Mc == M || lda >= K) && (b_mn || Nc == N || ldb >= K);
   const c10::hip::OptionalHIPGuardMasqueradingAsCUDA guard(A.device());
   wf::launch_gemm(bfp(A), lda, a_mn, bfp(B), ldb, b_mn, (int)M, (int)N, (int)K, (int)ksplit, e,
-                  cur_stream());
+                  cur_stream(), glds_ok && !disable_glds());
 }
 
 wf::LstmDims lstm_dims(int64_t B, int64_t T, int64_t F, int64_t KX, int64_t H) {

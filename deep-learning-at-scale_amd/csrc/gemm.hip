@@ -13,13 +13,18 @@
 
 namespace wf {
 
-template <int BM, int BN, int LA, int LB>
+// STAGES >= 2: direct-to-LDS ring; the host only selects it when every K chunk is a
+// multiple of 64 and the whole-tile over-read past M / N stays inside the operand
+// allocations (binding.cpp computes that from the tensor sizes); results outside M x N
+// are discarded by the epilogue as in the register path.
+template <int BM, int BN, int LA, int LB, int STAGES>
 __global__ __launch_bounds__(256) void gemm_kernel(const bf16_t* __restrict__ A, long lda,
                                                    const bf16_t* __restrict__ B, long ldb,
                                                    int M, int N, int K, int kchunk,
                                                    GemmEpilogue e) {
   using C = GemmCfg<BM, BN, LA, LB>;
-  __shared__ __attribute__((aligned(16))) char smem[C::LDS_BYTES];
+  constexpr int LDSB = STAGES * C::STAGE > C::LDS_BYTES ? STAGES * C::STAGE : C::LDS_BYTES;
+  __shared__ __attribute__((aligned(16))) char smem[LDSB];
   const int tiles_n = (N + BN - 1) / BN;
   const int tiles = ((M + BM - 1) / BM) * tiles_n;
   const int L = xcd_remap(blockIdx.x, gridDim.x);
@@ -29,7 +34,10 @@ __global__ __launch_bounds__(256) void gemm_kernel(const bf16_t* __restrict__ A,
   const int kend = min(K, kbeg + kchunk);
 
   f32x4 acc[C::TM][C::TN];
-  gemm_mainloop<C>(A, lda, M, B, ldb, N, kbeg, kend, m0, n0, smem, acc);
+  if constexpr (STAGES >= 2)
+    gemm_mainloop_glds<C, STAGES>(A, lda, B, ldb, kbeg, (kend - kbeg) / 64, m0, n0, smem, acc);
+  else
+    gemm_mainloop<C>(A, lda, M, B, ldb, N, kbeg, kend, m0, n0, smem, acc);
 
   const AccCoord<C> cc(m0, n0);
 #pragma unroll
@@ -73,27 +81,32 @@ __global__ __launch_bounds__(256) void gemm_kernel(const bf16_t* __restrict__ A,
 
 template <int BM, int BN, int LA, int LB>
 static void launch_cfg(const bf16_t* A, long lda, const bf16_t* B, long ldb, int M, int N, int K,
-                       int ksplit, const GemmEpilogue& e, hipStream_t s) {
+                       int ksplit, const GemmEpilogue& e, hipStream_t s, bool glds_ok) {
   const int tiles = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
   if (ksplit < 1) ksplit = 1;
   int kchunk = (K + ksplit - 1) / ksplit;
   kchunk = (kchunk + 63) / 64 * 64;
   if (kchunk < 64) kchunk = 64;
   const int nsplit = (K + kchunk - 1) / kchunk;
-  hipLaunchKernelGGL((gemm_kernel<BM, BN, LA, LB>), dim3(tiles * (nsplit > 0 ? nsplit : 1)),
-                     dim3(256), 0, s, A, lda, B, ldb, M, N, K, kchunk, e);
+  const dim3 grid(tiles * (nsplit > 0 ? nsplit : 1));
+  if (glds_ok && K % 64 == 0)
+    hipLaunchKernelGGL((gemm_kernel<BM, BN, LA, LB, 3>), grid, dim3(256), 0, s, A, lda, B, ldb, M,
+                       N, K, kchunk, e);
+  else
+    hipLaunchKernelGGL((gemm_kernel<BM, BN, LA, LB, 0>), grid, dim3(256), 0, s, A, lda, B, ldb, M,
+                       N, K, kchunk, e);
 }
 
 void launch_gemm(const bf16_t* A, long lda, int a_mn, const bf16_t* B, long ldb, int b_mn, int M,
-                 int N, int K, int ksplit, const GemmEpilogue& e, hipStream_t s) {
+                 int N, int K, int ksplit, const GemmEpilogue& e, hipStream_t s, bool glds_ok) {
   if (!a_mn && !b_mn)
-    launch_cfg<128, 128, K_CONTIG, K_CONTIG>(A, lda, B, ldb, M, N, K, ksplit, e, s);
+    launch_cfg<128, 128, K_CONTIG, K_CONTIG>(A, lda, B, ldb, M, N, K, ksplit, e, s, glds_ok);
   else if (!a_mn && b_mn)
-    launch_cfg<128, 128, K_CONTIG, MN_CONTIG>(A, lda, B, ldb, M, N, K, ksplit, e, s);
+    launch_cfg<128, 128, K_CONTIG, MN_CONTIG>(A, lda, B, ldb, M, N, K, ksplit, e, s, glds_ok);
   else if (a_mn && !b_mn)
-    launch_cfg<128, 128, MN_CONTIG, K_CONTIG>(A, lda, B, ldb, M, N, K, ksplit, e, s);
+    launch_cfg<128, 128, MN_CONTIG, K_CONTIG>(A, lda, B, ldb, M, N, K, ksplit, e, s, glds_ok);
   else
-    launch_cfg<128, 128, MN_CONTIG, MN_CONTIG>(A, lda, B, ldb, M, N, K, ksplit, e, s);
+    launch_cfg<128, 128, MN_CONTIG, MN_CONTIG>(A, lda, B, ldb, M, N, K, ksplit, e, s, glds_ok);
 }
 
 }  // namespace wf

@@ -25,7 +25,8 @@ struct GemmEpilogue {
 };
 
 void launch_gemm(const bf16_t* A, long lda, int a_mn, const bf16_t* B, long ldb, int b_mn, int M,
-                 int N, int K, int ksplit, const GemmEpilogue& e, hipStream_t s);
+                 int N, int K, int ksplit, const GemmEpilogue& e, hipStream_t s,
+                 bool glds_ok = false);
 
 // ---- LSTM (single layer, batch-first input, seq-to-one regression) ----
 struct LstmDims {

@@ -164,8 +164,8 @@ class NativeLSTM:
         self.dy = torch.empty(B, dtype=torch.float32, device=dev)
         self.loss_sum = torch.zeros(1, dtype=torch.float32, device=dev)
         # tile shapes (csrc/kernels.h LstmDims), A/B-tuned on MI355X with tools/tune_lstm.py
-        # (profiles/r1_*): bwd 64x64 tiles 1.5x faster than 128x128 at B=8192; dW split-K 32.
-        self.fwd_variant, self.bwd_variant = 0, 3
+        # (profiles/r1_*): fwd 256x256 glds ring (v6), bwd 64x128 glds ring (v9); dW split-K 32.
+        self.fwd_variant, self.bwd_variant = 6, 9
         self.dw_ksplit = 0  # 0 = heuristic
         self.sync_weights()
 
