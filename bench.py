@@ -33,6 +33,9 @@ def main() -> int:
     ap.add_argument("--hidden", type=int, default=512)
     ap.add_argument("--features", type=int, default=16)
     ap.add_argument("--lr", type=float, default=1e-3)
+    ap.add_argument("--dw-chunk", type=int, default=None, help="timesteps per overlapped dW chunk (0 = serial)")
+    ap.add_argument("--fwd-variant", type=int, default=None)
+    ap.add_argument("--bwd-variant", type=int, default=None)
     args = ap.parse_args()
 
     import torch
@@ -52,6 +55,12 @@ def main() -> int:
 
     B, T, F, H = args.batch, args.seq, args.features, args.hidden
     eng = NativeLSTM(F, H, T, B, device=dev)
+    if args.dw_chunk is not None:
+        eng.dw_chunk = args.dw_chunk
+    if args.fwd_variant is not None:
+        eng.fwd_variant = args.fwd_variant
+    if args.bwd_variant is not None:
+        eng.bwd_variant = args.bwd_variant
     eng.params.copy_(init_lstm_flat(F, H, seed=0).to(dev))
     ctx.broadcast_(eng.params)  # C1: identical init on every rank
     eng.sync_weights()

@@ -8,6 +8,9 @@
 #include <ATen/hip/impl/HIPGuardImplMasqueradingAsCUDA.h>
 
 #include <cstdlib>
+#include <map>
+#include <mutex>
+#include <vector>
 
 #include "kernels.h"
 
@@ -177,6 +180,109 @@ void lstm_backward(const at::Tensor& WhhT, const at::Tensor& XH, const at::Tenso
                              fp(w_out), d, s);
 }
 
+// Two persistent side streams per device for the backward pass: the serial BPTT chain
+// runs on a HIGH-priority stream, the weight-gradient GEMM chunks on a LOW-priority one,
+// fork/joined to the caller's stream with events (capturable in a hipGraph).
+struct SideStreams {
+  hipStream_t hi = nullptr, lo = nullptr;
+  std::vector<hipEvent_t> ev;
+};
+
+SideStreams& side_streams(int dev, size_t nev) {
+  static std::mutex mu;
+  static std::map<int, SideStreams> all;
+  std::lock_guard<std::mutex> g(mu);
+  SideStreams& ss = all[dev];
+  if (ss.hi == nullptr) {
+    int least = 0, greatest = 0;
+    TORCH_CHECK(hipDeviceGetStreamPriorityRange(&least, &greatest) == hipSuccess, "stream priorities");
+    TORCH_CHECK(hipStreamCreateWithPriority(&ss.hi, hipStreamNonBlocking, greatest) == hipSuccess,
+                "hi stream");
+    TORCH_CHECK(hipStreamCreateWithPriority(&ss.lo, hipStreamNonBlocking, least) == hipSuccess,
+                "lo stream");
+  }
+  while (ss.ev.size() < nev) {
+    hipEvent_t e;
+    TORCH_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming) == hipSuccess, "event");
+    ss.ev.push_back(e);
+  }
+  return ss;
+}
+
+// Full LSTM backward: BPTT chain + dWcat = sum_t DG[t]^T XH[t] into gW (fp32 [G][KA],
+// accumulated with atomics, so it must be zeroed by the caller). With chunk > 0 the dW
+// GEMM is cut into chunks of `chunk` timesteps, each launched on the low-priority stream
+// as soon as the chain has produced its DG slabs: compute-bound dW work fills the gaps of
+// the memory/latency-bound chain instead of running after it.
+void lstm_backward_dw(const at::Tensor& WhhT, const at::Tensor& XH, const at::Tensor& Cst,
+                      const at::Tensor& S, const at::Tensor& DG, const at::Tensor& dcarry,
+                      const at::Tensor& dy, const at::Tensor& w_out, const at::Tensor& gW,
+                      int64_t B, int64_t T, int64_t F, int64_t KX, int64_t H, int64_t variant,
+                      int64_t chunk, int64_t ksplit) {
+  auto d = lstm_dims(B, T, F, KX, H);
+  d.bwd_variant = (int)variant;
+  check_lstm_state(XH, Cst, S, d);
+  check_t(WhhT, at::kBFloat16, "WhhT");
+  check_extent(WhhT, H * 4 * H, "WhhT");
+  check_t(DG, at::kBFloat16, "DG");
+  check_extent(DG, T * B * 4 * H, "DG");
+  check_t(dcarry, at::kFloat, "dcarry");
+  check_extent(dcarry, (B + 15) / 16 * 16 * H, "dcarry");
+  check_t(dy, at::kFloat, "dy");
+  check_extent(dy, B, "dy");
+  check_t(w_out, at::kFloat, "w_out");
+  check_extent(w_out, H, "w_out");
+  check_t(gW, at::kFloat, "gW");
+  const int64_t G = 4 * H, KA = KX + H;
+  check_extent(gW, G * KA, "gW");
+  const c10::hip::OptionalHIPGuardMasqueradingAsCUDA guard(XH.device());
+  hipStream_t main = cur_stream();
+
+  auto dw = [&](int t0, int t1, hipStream_t s) {
+    const int64_t K = (int64_t)(t1 - t0) * B;
+    wf::GemmEpilogue e;
+    e.outF = fp(gW);
+    e.ldo = KA;
+    e.atomic = 1;
+    const bf16_t* A = bfp(DG) + (size_t)t0 * B * G;
+    const bf16_t* Bm = bfp(XH) + (size_t)t0 * B * KA;
+    // whole-tile over-read of XH columns 576..639 stays inside XH (its slab T follows)
+    int64_t ks = std::max<int64_t>(1, ksplit);
+    int64_t kchunk = ((K + ks - 1) / ks + 63) / 64 * 64;
+    const bool glds_ok = (K % 64 == 0) && (kchunk % 64 == 0) && !disable_glds();
+    wf::launch_gemm(A, G, 1, Bm, KA, 1, (int)G, (int)KA, (int)K, (int)ks, e, s, glds_ok);
+  };
+
+  if (chunk <= 0) {
+    for (int t = d.T - 1; t >= 0; --t)
+      wf::launch_lstm_bwd_step(t, bfp(WhhT), fp(Cst), bfp(S), bfp(DG), fp(dcarry), fp(dy),
+                               fp(w_out), d, main);
+    dw(0, d.T, main);
+    return;
+  }
+  const int nchunks = (int)((T + chunk - 1) / chunk);
+  SideStreams& ss = side_streams(XH.device().index(), nchunks + 3);
+  TORCH_CHECK(hipEventRecord(ss.ev[0], main) == hipSuccess, "event record");
+  TORCH_CHECK(hipStreamWaitEvent(ss.hi, ss.ev[0], 0) == hipSuccess, "wait");
+  TORCH_CHECK(hipStreamWaitEvent(ss.lo, ss.ev[0], 0) == hipSuccess, "wait");
+  int t_end = d.T, k = 0;
+  for (int t = d.T - 1; t >= 0; --t) {
+    wf::launch_lstm_bwd_step(t, bfp(WhhT), fp(Cst), bfp(S), bfp(DG), fp(dcarry), fp(dy),
+                             fp(w_out), d, ss.hi);
+    if (t % chunk == 0) {  // DG[t .. t_end) complete
+      hipEvent_t e = ss.ev[3 + k++];
+      TORCH_CHECK(hipEventRecord(e, ss.hi) == hipSuccess, "event record");
+      TORCH_CHECK(hipStreamWaitEvent(ss.lo, e, 0) == hipSuccess, "wait");
+      dw(t, t_end, ss.lo);
+      t_end = t;
+    }
+  }
+  TORCH_CHECK(hipEventRecord(ss.ev[1], ss.hi) == hipSuccess, "event record");
+  TORCH_CHECK(hipEventRecord(ss.ev[2], ss.lo) == hipSuccess, "event record");
+  TORCH_CHECK(hipStreamWaitEvent(main, ss.ev[1], 0) == hipSuccess, "join");
+  TORCH_CHECK(hipStreamWaitEvent(main, ss.ev[2], 0) == hipSuccess, "join");
+}
+
 void lstm_pack_weights(const at::Tensor& W, const at::Tensor& Wp, const at::Tensor& WhhT,
                        int64_t H, int64_t KX) {
   auto d = lstm_dims(1, 1, 0, KX, H);
@@ -330,6 +436,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("lstm_pack_x", &lstm_pack_x);
   m.def("lstm_forward", &lstm_forward);
   m.def("lstm_backward", &lstm_backward);
+  m.def("lstm_backward_dw", &lstm_backward_dw);
   m.def("lstm_pack_weights", &lstm_pack_weights);
   m.def("head_fwd", &head_fwd);
   m.def("head_bwd_w", &head_bwd_w);

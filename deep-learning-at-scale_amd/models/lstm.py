@@ -167,6 +167,7 @@ class NativeLSTM:
         # (profiles/r1_*): fwd 256x256 glds ring (v6), bwd 64x128 glds ring (v9); dW split-K 32.
         self.fwd_variant, self.bwd_variant = 6, 9
         self.dw_ksplit = 0  # 0 = heuristic
+        self.dw_chunk = 8   # timesteps per overlapped dW GEMM chunk (0 = serial dW at the end)
         self.sync_weights()
 
     # ------------------------------------------------------------------ weights
@@ -231,13 +232,12 @@ class NativeLSTM:
             C.loss(1, self.pred, y, B, 1, self.clip, float(grad_scale), self.loss_sum, None,
                    self.dy, None)
         C.head_bwd_w(hT, lay.KA, B, self.H, self.dy, gw_out, gb_out)
-        C.lstm_backward(self.WhhT, self.XH, self.Cst, self.S, self.DG, self.dcarry, self.dy,
-                        w_out, *self._dims(B), self.bwd_variant)
-        # dWcat = sum_{t,b} dG_t[b]^T [x_t | 1 | h_{t-1}][b]   (one split-K GEMM, K = T*B)
+        # BPTT chain (high-priority stream) + dWcat = sum_{t,b} dG_t[b]^T [x_t | 1 | h_{t-1}][b]
+        # as split-K GEMM chunks on a low-priority stream, overlapped with the chain.
         K = self.T * B
         ksplit = self.dw_ksplit or max(1, min(32, K // 16384))
-        from ..ops.native import gemm
-
-        gemm(self.DG, self.XH, lay.G, lay.KA, K, a_mn=True, lda=lay.G, b_mn=True, ldb=lay.KA,
-             outF=gW, ldo=lay.KA, atomic=True, ksplit=ksplit)
+        if self.dw_chunk > 0:
+            ksplit = max(1, ksplit * self.dw_chunk // self.T)
+        C.lstm_backward_dw(self.WhhT, self.XH, self.Cst, self.S, self.DG, self.dcarry, self.dy,
+                           w_out, gW, *self._dims(B), self.bwd_variant, self.dw_chunk, ksplit)
         return self.loss_sum
