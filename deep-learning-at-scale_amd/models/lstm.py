@@ -167,7 +167,9 @@ class NativeLSTM:
         # (profiles/r1_*): fwd 256x256 glds ring (v6), bwd 64x128 glds ring (v9); dW split-K 32.
         self.fwd_variant, self.bwd_variant = 6, 9
         self.dw_ksplit = 0  # 0 = heuristic
-        self.dw_chunk = 8   # timesteps per overlapped dW GEMM chunk (0 = serial dW at the end)
+        # timesteps per overlapped dW GEMM chunk; 0 = serial dW at the end (measured faster:
+        # the BPTT chain already fills every CU, overlapping only adds contention)
+        self.dw_chunk = 0
         self.sync_weights()
 
     # ------------------------------------------------------------------ weights
