@@ -31,12 +31,15 @@ __device__ __forceinline__ bf16_t f2bf(float x) {
   return *reinterpret_cast<bf16_t*>(&h);
 }
 
-__device__ __forceinline__ float sigmoidf_(float x) { return 1.0f / (1.0f + __expf(-x)); }
+// Gate activations on the transcendental unit: v_exp_f32 + v_rcp_f32 (1 ulp), no IEEE
+// division sequence (the precise 1/x costs ~10 VALU and dominated the LSTM epilogues).
+__device__ __forceinline__ float sigmoidf_(float x) {
+  return __builtin_amdgcn_rcpf(1.0f + __expf(-x));
+}
 
 __device__ __forceinline__ float tanhf_(float x) {
-  // tanh(x) = 1 - 2/(exp(2x)+1); saturates cleanly for |x| large.
-  float e = __expf(2.0f * x);
-  return 1.0f - 2.0f / (e + 1.0f);
+  // tanh(x) = 1 - 2/(exp(2x)+1); saturates cleanly for |x| large (exp -> inf or 0).
+  return 1.0f - 2.0f * __builtin_amdgcn_rcpf(__expf(2.0f * x) + 1.0f);
 }
 
 // Counter-based uniform in [0,1) (splitmix64 finaliser). Dropout masks are regenerated

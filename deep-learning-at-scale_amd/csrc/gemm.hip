@@ -35,7 +35,7 @@ __global__ __launch_bounds__(256) void gemm_kernel(const bf16_t* __restrict__ A,
 
   f32x4 acc[C::TM][C::TN];
   if constexpr (STAGES >= 2)
-    gemm_mainloop_glds<C, STAGES>(A, lda, B, ldb, kbeg, (kend - kbeg) / 64, m0, n0, smem, acc);
+    gemm_mainloop_glds2<C, STAGES>(A, lda, B, ldb, kbeg, (kend - kbeg) / 64, m0, n0, smem, acc);
   else
     gemm_mainloop<C>(A, lda, M, B, ldb, N, kbeg, kend, m0, n0, smem, acc);
 

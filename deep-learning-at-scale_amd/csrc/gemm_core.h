@@ -16,6 +16,8 @@
 // come out with two ds_read_b64_tr_b16 hardware-transposed reads (T10), conflict-free
 // for 128- and 256-row tiles.
 #pragma once
+#include <type_traits>
+
 #include "common.h"
 
 namespace wf {
@@ -295,6 +297,187 @@ __device__ __forceinline__ void gemm_mainloop_glds(const bf16_t* __restrict__ A,
     }
   }
   // leave LDS reusable by the caller's epilogue
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+// ----------------------------------------------------------------------------------------
+// glds mainloop v2 — same pipeline/contract as gemm_mainloop_glds, built to keep the VALU
+// out of the MFMA stream (rocprofv3 showed VALU:MFMA = 5-7:1 in v1):
+//  * every per-lane address is computed ONCE: glds sources are (scalar tile base) +
+//    (32-bit per-lane byte offset), the scalar base advancing by one K-step per tile;
+//  * fragment reads use per-lane LDS base offsets; the K-loop is unrolled by STAGES so
+//    the stage, K-substep and subtile offsets are compile-time immediates of ds_read.
+template <int U, int N, class F>
+__device__ __forceinline__ void static_for(F&& f) {
+  if constexpr (U < N) {
+    f(std::integral_constant<int, U>{});
+    static_for<U + 1, N>(f);
+  }
+}
+
+template <int R, int L, int NT>
+struct GldsOperand {
+  using Q = GldsTile<R, L, NT>;
+  static constexpr int TILE_BYTES = Q::BYTES;
+  unsigned src[Q::PER_WAVE];  // per-lane source byte offsets from the tile base
+  const char* base;           // scalar: tile (row0, kbeg) base address
+  long kstep_bytes;           // scalar: base advance per 64-deep K-step
+
+  __device__ __forceinline__ void init(const bf16_t* p, long ld, int row0, int kbeg, int wid, int lane) {
+#pragma unroll
+    for (int i = 0; i < Q::PER_WAVE; ++i) {
+      const int piece = i * Q::NW + wid;
+      long off;
+      if constexpr (L == K_CONTIG) {
+        const int row = piece * 8 + (lane >> 3);
+        const int lc = (lane & 7) ^ ((row >> 1) & 7);
+        off = (long)row * ld + lc * 8;
+      } else {
+        constexpr int SPR = R / 8;
+        const int k = piece * (512 / R) + lane / SPR;
+        const int slot = lane % SPR;
+        off = (long)k * ld + (((slot >> 1) ^ Q::hk(k)) << 4) + ((slot & 1) << 3);
+      }
+      src[i] = (unsigned)(off * 2);
+    }
+    if constexpr (L == K_CONTIG) {
+      base = reinterpret_cast<const char*>(p + (size_t)row0 * ld + kbeg);
+      kstep_bytes = 64 * 2;
+    } else {
+      base = reinterpret_cast<const char*>(p + (size_t)kbeg * ld + row0);
+      kstep_bytes = 64L * ld * 2;
+    }
+  }
+
+  __device__ __forceinline__ void issue(int tile, char* lds_tile, int wid) const {
+    const char* b = base + (long)tile * kstep_bytes;
+#pragma unroll
+    for (int i = 0; i < Q::PER_WAVE; ++i)
+      __builtin_amdgcn_global_load_lds((const void*)(b + src[i]),
+                                       (lds_void*)(lds_tile + (i * Q::NW + wid) * 1024), 16, 0, 0);
+  }
+};
+
+template <int R, int L, int WT>
+struct FragReader {
+  // K_CONTIG: fb[kk]; MN_CONTIG: fb[i] (one per 16-row subtile of the wave)
+  static constexpr int NB = (L == K_CONTIG) ? 2 : WT / 16;
+  int fb[NB];
+
+  __device__ __forceinline__ void init(int rw, int lane) {
+    const int l15 = lane & 15, g = lane >> 4;
+    if constexpr (L == K_CONTIG) {
+      const int s = (l15 >> 1) & 7;  // rw is a multiple of 16: the swizzle only sees l15
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) fb[kk] = (rw + l15) * 128 + (((kk * 4 + g) ^ s) << 4);
+    } else {
+      const int q = l15 >> 2, p = lane & 3;
+      const int hk = (q | ((g & 1) << 2)) & (R / 16 - 1);
+#pragma unroll
+      for (int i = 0; i < NB; ++i)
+        fb[i] = (8 * g + q) * (R * 2) + ((((rw >> 4) + i) ^ hk) << 5) + p * 8;
+    }
+  }
+
+  // fragment of subtile i, k-substep KK, from the tile at byte offset TOFF of smem
+  template <int KK, int TOFF>
+  __device__ __forceinline__ bf16x8 frag(const char* smem, int i) const {
+    if constexpr (L == K_CONTIG) {
+      return *reinterpret_cast<const bf16x8*>(smem + fb[KK] + TOFF + i * 16 * 128);
+    } else {
+      bf16x8 out;
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const char* a = smem + fb[i] + TOFF + (KK * 32 + 4 * h) * (R * 2);
+        bf16x4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_bf16x4*)a);
+        out[4 * h + 0] = v[0];
+        out[4 * h + 1] = v[1];
+        out[4 * h + 2] = v[2];
+        out[4 * h + 3] = v[3];
+      }
+      return out;
+    }
+  }
+};
+
+template <class C, int STAGES>
+__device__ __forceinline__ void gemm_mainloop_glds2(const bf16_t* __restrict__ A, long lda,
+                                                    const bf16_t* __restrict__ B, long ldb, int kbeg,
+                                                    int nk, int m0, int n0, char* smem,
+                                                    f32x4 (&acc)[C::TM][C::TN]) {
+  static_assert(STAGES >= 2 && STAGES <= 4, "2..4 stages");
+  using OA = GldsOperand<C::BM, C::LA_, C::NT>;
+  using OB = GldsOperand<C::BN, C::LB_, C::NT>;
+  constexpr int STAGE = OA::TILE_BYTES + OB::TILE_BYTES;
+  constexpr int LPT = OA::Q::PER_WAVE + OB::Q::PER_WAVE;
+  const int lane = threadIdx.x & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wm = wid / C::WN, wn = wid % C::WN;
+#pragma unroll
+  for (int i = 0; i < C::TM; ++i)
+#pragma unroll
+    for (int j = 0; j < C::TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  if (nk <= 0) return;
+  OA oa;
+  OB ob;
+  oa.init(A, lda, m0, kbeg, wid, lane);
+  ob.init(B, ldb, n0, kbeg, wid, lane);
+  FragReader<C::BM, C::LA_, C::WTM> fa;
+  FragReader<C::BN, C::LB_, C::WTN> fbr;
+  fa.init(wm * C::WTM, lane);
+  fbr.init(wn * C::WTN, lane);
+
+#pragma unroll
+  for (int s = 0; s < STAGES - 1; ++s) {
+    if (s < nk) {
+      oa.issue(s, smem + s * STAGE, wid);
+      ob.issue(s, smem + s * STAGE + OA::TILE_BYTES, wid);
+    }
+  }
+
+  auto body = [&](int tt, auto uc) {
+    constexpr int u = decltype(uc)::value;  // == tt % STAGES
+    const int ahead = min(nk - 1, tt + STAGES - 2) - tt;
+    if constexpr (STAGES >= 4) {
+      if (ahead >= 2) wait_vmcnt<2 * LPT>();
+      else if (ahead == 1) wait_vmcnt<LPT>();
+      else wait_vmcnt<0>();
+    } else if constexpr (STAGES == 3) {
+      if (ahead >= 1) wait_vmcnt<LPT>();
+      else wait_vmcnt<0>();
+    } else {
+      wait_vmcnt<0>();
+    }
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    const int tn = tt + STAGES - 1;
+    if (tn < nk) {
+      constexpr int sn = (u + STAGES - 1) % STAGES;
+      oa.issue(tn, smem + sn * STAGE, wid);
+      ob.issue(tn, smem + sn * STAGE + OA::TILE_BYTES, wid);
+    }
+    static_for<0, 2>([&](auto kc) {
+      constexpr int KK = decltype(kc)::value;
+      bf16x8 a[C::TM], b[C::TN];
+#pragma unroll
+      for (int i = 0; i < C::TM; ++i) a[i] = fa.template frag<KK, u * STAGE>(smem, i);
+#pragma unroll
+      for (int j = 0; j < C::TN; ++j) b[j] = fbr.template frag<KK, u * STAGE + OA::TILE_BYTES>(smem, j);
+#pragma unroll
+      for (int i = 0; i < C::TM; ++i)
+#pragma unroll
+        for (int j = 0; j < C::TN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
+    });
+  };
+
+  int t = 0;
+  for (; t + STAGES <= nk; t += STAGES)
+    static_for<0, STAGES>([&](auto uc) { body(t + decltype(uc)::value, uc); });
+  static_for<0, STAGES>([&](auto uc) {
+    if (t + decltype(uc)::value < nk) body(t + decltype(uc)::value, uc);
+  });
   __builtin_amdgcn_s_barrier();
   asm volatile("" ::: "memory");
 }

@@ -74,25 +74,15 @@ __global__ __launch_bounds__(64 * WM * WN) void lstm_fwd_step_kernel(int t, bf16
   const int m0 = (L / tiles_n) * C::BM, n0 = (L % tiles_n) * C::BN;
   const bf16_t* A = XH + (size_t)t * d.B * KA;
 
-  // c_{t-1} for this lane's fragment-native slots is fetched BEFORE the mainloop so its
-  // latency hides under the GEMM (16 B per lane per 16-row subtile).
   const AccCoord<C> cc(m0, n0);
   const int lane = threadIdx.x & 63;
   const int u = (cc.nb >> 6) * 16 + (lane & 15);
   const int Bp = fn_rows(d.B);
   const float* cprev = Cst + (size_t)t * Bp * d.H;
-  float4 cpre[C::TM];
-#pragma unroll
-  for (int i = 0; i < C::TM; ++i) {
-    const int mrow0 = cc.mb + i * 16;
-    cpre[i] = mrow0 < d.B ? *reinterpret_cast<const float4*>(cprev + fn_block(mrow0, u, d.H) * 256 + lane * 4)
-                          : make_float4(0.f, 0.f, 0.f, 0.f);
-  }
-  // (no wait here: the mainloop's first counted vmcnt retires these older loads too)
 
   f32x4 acc[C::TM][C::TN];
   if constexpr (STAGES >= 2)
-    gemm_mainloop_glds<C, STAGES>(A, KA, Wp, KA, 0, KA / 64, m0, n0, smem, acc);
+    gemm_mainloop_glds2<C, STAGES>(A, KA, Wp, KA, 0, KA / 64, m0, n0, smem, acc);
   else
     gemm_mainloop<C>(A, KA, d.B, Wp, KA, G, 0, KA, m0, n0, smem, acc);
 
@@ -104,7 +94,7 @@ __global__ __launch_bounds__(64 * WM * WN) void lstm_fwd_step_kernel(int t, bf16
     const int mrow0 = cc.mb + i * 16;
     if (mrow0 >= d.B) continue;
     const size_t blk = fn_block(mrow0, u, d.H);
-    const float4 cp = cpre[i];
+    const float4 cp = *reinterpret_cast<const float4*>(cprev + blk * 256 + lane * 4);
     const float cpv[4] = {cp.x, cp.y, cp.z, cp.w};
     float cv[4];
     unsigned pk[8];
@@ -238,7 +228,7 @@ __global__ __launch_bounds__(64 * WM * WN) void lstm_bwd_step_kernel(int t, cons
 
   f32x4 acc[C::TM][C::TN];
   if constexpr (STAGES >= 2)
-    gemm_mainloop_glds<C, STAGES>(A, G, WhhT, G, 0, G / 64, m0, n0, smem, acc);
+    gemm_mainloop_glds2<C, STAGES>(A, G, WhhT, G, 0, G / 64, m0, n0, smem, acc);
   else
     gemm_mainloop<C>(A, G, d.B, WhhT, G, d.H, 0, G, m0, n0, smem, acc);
 
