@@ -120,20 +120,16 @@ wf::LstmDims lstm_dims(int64_t B, int64_t T, int64_t F, int64_t KX, int64_t H) {
   return d;
 }
 
-// XH [T+1][B][KA] bf16; S [T][Bp*H][6] bf16 backward coefficients (fragment-native,
-// Bp = B padded to 16); Cst: 2-slot fp32 cell-state ping-pong [2][Bp*H].
-void check_lstm_state(const at::Tensor& XH, const at::Tensor* Cst, const at::Tensor& S,
+void check_lstm_state(const at::Tensor& XH, const at::Tensor& Cst, const at::Tensor& S,
                       const wf::LstmDims& d) {
-  const int64_t KA = d.KX + d.H;
-  const int64_t Bp = (d.B + 15) / 16 * 16;
+  const int64_t KA = d.KX + d.H, G = 4 * d.H;
+  const int64_t Bp = (d.B + 15) / 16 * 16;  // fragment-native state is padded to 16 rows
   check_t(XH, at::kBFloat16, "XH");
+  check_t(Cst, at::kFloat, "Cst");
   check_t(S, at::kBFloat16, "S");
   check_extent(XH, (int64_t)(d.T + 1) * d.B * KA, "XH");
-  check_extent(S, (int64_t)d.T * Bp * d.H * 6, "S");
-  if (Cst != nullptr) {
-    check_t(*Cst, at::kFloat, "Cst");
-    check_extent(*Cst, 2 * Bp * d.H, "Cst");
-  }
+  check_extent(Cst, (int64_t)(d.T + 1) * Bp * d.H, "Cst");
+  check_extent(S, (int64_t)d.T * Bp * G, "S");
 }
 
 void lstm_pack_x(const at::Tensor& x, const at::Tensor& XH, int64_t B, int64_t T, int64_t F,
@@ -152,24 +148,21 @@ void lstm_forward(const at::Tensor& XH, const at::Tensor& Wp, const at::Tensor& 
                   int64_t variant) {
   auto d = lstm_dims(B, T, F, KX, H);
   d.fwd_variant = (int)variant;
-  check_lstm_state(XH, &Cst, S, d);
+  check_lstm_state(XH, Cst, S, d);
   check_t(Wp, at::kBFloat16, "Wp");
   check_extent(Wp, 4 * H * (KX + H), "Wp");
   const c10::hip::OptionalHIPGuardMasqueradingAsCUDA guard(XH.device());
   auto s = cur_stream();
-  // c_0 = 0 in ping-pong slot 0 (slot 1 is fully written by step 0)
-  const int64_t Bp = (B + 15) / 16 * 16;
-  TORCH_CHECK(hipMemsetAsync(Cst.data_ptr(), 0, Bp * H * sizeof(float), s) == hipSuccess, "memset");
   for (int t = 0; t < d.T; ++t) wf::launch_lstm_fwd_step(t, bfp(XH), bfp(Wp), fp(Cst), bfp(S), d, s);
 }
 
-void lstm_backward(const at::Tensor& WhhT, const at::Tensor& XH,
+void lstm_backward(const at::Tensor& WhhT, const at::Tensor& XH, const at::Tensor& Cst,
                    const at::Tensor& S, const at::Tensor& DG, const at::Tensor& dcarry,
                    const at::Tensor& dy, const at::Tensor& w_out, int64_t B, int64_t T, int64_t F,
                    int64_t KX, int64_t H, int64_t variant) {
   auto d = lstm_dims(B, T, F, KX, H);
   d.bwd_variant = (int)variant;
-  check_lstm_state(XH, nullptr, S, d);
+  check_lstm_state(XH, Cst, S, d);
   check_t(WhhT, at::kBFloat16, "WhhT");
   check_extent(WhhT, H * 4 * H, "WhhT");
   check_t(DG, at::kBFloat16, "DG");
@@ -183,7 +176,7 @@ void lstm_backward(const at::Tensor& WhhT, const at::Tensor& XH,
   const c10::hip::OptionalHIPGuardMasqueradingAsCUDA guard(XH.device());
   auto s = cur_stream();
   for (int t = d.T - 1; t >= 0; --t)
-    wf::launch_lstm_bwd_step(t, bfp(WhhT), bfp(S), bfp(DG), fp(dcarry), fp(dy),
+    wf::launch_lstm_bwd_step(t, bfp(WhhT), fp(Cst), bfp(S), bfp(DG), fp(dcarry), fp(dy),
                              fp(w_out), d, s);
 }
 
@@ -221,14 +214,14 @@ SideStreams& side_streams(int dev, size_t nev) {
 // GEMM is cut into chunks of `chunk` timesteps, each launched on the low-priority stream
 // as soon as the chain has produced its DG slabs: compute-bound dW work fills the gaps of
 // the memory/latency-bound chain instead of running after it.
-void lstm_backward_dw(const at::Tensor& WhhT, const at::Tensor& XH,
+void lstm_backward_dw(const at::Tensor& WhhT, const at::Tensor& XH, const at::Tensor& Cst,
                       const at::Tensor& S, const at::Tensor& DG, const at::Tensor& dcarry,
                       const at::Tensor& dy, const at::Tensor& w_out, const at::Tensor& gW,
                       int64_t B, int64_t T, int64_t F, int64_t KX, int64_t H, int64_t variant,
                       int64_t chunk, int64_t ksplit) {
   auto d = lstm_dims(B, T, F, KX, H);
   d.bwd_variant = (int)variant;
-  check_lstm_state(XH, nullptr, S, d);
+  check_lstm_state(XH, Cst, S, d);
   check_t(WhhT, at::kBFloat16, "WhhT");
   check_extent(WhhT, H * 4 * H, "WhhT");
   check_t(DG, at::kBFloat16, "DG");
@@ -262,7 +255,7 @@ void lstm_backward_dw(const at::Tensor& WhhT, const at::Tensor& XH,
 
   if (chunk <= 0) {
     for (int t = d.T - 1; t >= 0; --t)
-      wf::launch_lstm_bwd_step(t, bfp(WhhT), bfp(S), bfp(DG), fp(dcarry), fp(dy),
+      wf::launch_lstm_bwd_step(t, bfp(WhhT), fp(Cst), bfp(S), bfp(DG), fp(dcarry), fp(dy),
                                fp(w_out), d, main);
     dw(0, d.T, main);
     return;
@@ -274,7 +267,7 @@ void lstm_backward_dw(const at::Tensor& WhhT, const at::Tensor& XH,
   TORCH_CHECK(hipStreamWaitEvent(ss.lo, ss.ev[0], 0) == hipSuccess, "wait");
   int t_end = d.T, k = 0;
   for (int t = d.T - 1; t >= 0; --t) {
-    wf::launch_lstm_bwd_step(t, bfp(WhhT), bfp(S), bfp(DG), fp(dcarry), fp(dy),
+    wf::launch_lstm_bwd_step(t, bfp(WhhT), fp(Cst), bfp(S), bfp(DG), fp(dcarry), fp(dy),
                              fp(w_out), d, ss.hi);
     if (t % chunk == 0) {  // DG[t .. t_end) complete
       hipEvent_t e = ss.ev[3 + k++];

@@ -37,7 +37,7 @@ struct LstmDims {
 void launch_lstm_pack_x(const float* x, bf16_t* XH, LstmDims d, hipStream_t s);
 void launch_lstm_fwd_step(int t, bf16_t* XH, const bf16_t* Wp, float* Cst, bf16_t* S,
                           LstmDims d, hipStream_t s);
-void launch_lstm_bwd_step(int t, const bf16_t* WhhT, const bf16_t* S,
+void launch_lstm_bwd_step(int t, const bf16_t* WhhT, const float* Cst, const bf16_t* S,
                           bf16_t* DG, float* dcarry, const float* dy, const float* w_out,
                           LstmDims d, hipStream_t s);
 void launch_lstm_pack_weights(const float* W, bf16_t* Wp, bf16_t* WhhT, LstmDims d,

@@ -29,7 +29,6 @@ __device__ __forceinline__ int gate_col(int gate, int u) { return (u >> 4) * 64 
 // where the 16x16 MFMA C map puts it, so every lane moves 16-32 contiguous bytes.
 // Batch rows are padded to a multiple of 16 (fn_rows).
 __host__ __device__ __forceinline__ int fn_rows(int B) { return (B + 15) & ~15; }
-constexpr int kCoef = 6;  // backward coefficients saved per (row, unit)
 __device__ __forceinline__ size_t fn_block(int mrow0, int u, int H) {
   return (size_t)(mrow0 >> 4) * (H >> 4) + (u >> 4);
 }
@@ -79,7 +78,7 @@ __global__ __launch_bounds__(64 * WM * WN) void lstm_fwd_step_kernel(int t, bf16
   const int lane = threadIdx.x & 63;
   const int u = (cc.nb >> 6) * 16 + (lane & 15);
   const int Bp = fn_rows(d.B);
-  const float* cprev = Cst + (size_t)(t & 1) * Bp * d.H;  // 2-slot ping-pong (MALL-resident)
+  const float* cprev = Cst + (size_t)t * Bp * d.H;
 
   f32x4 acc[C::TM][C::TN];
   if constexpr (STAGES >= 2)
@@ -87,9 +86,9 @@ __global__ __launch_bounds__(64 * WM * WN) void lstm_fwd_step_kernel(int t, bf16
   else
     gemm_mainloop<C>(A, KA, d.B, Wp, KA, G, 0, KA, m0, n0, smem, acc);
 
-  float* cnext = Cst + (size_t)((t + 1) & 1) * Bp * d.H;
+  float* cnext = Cst + (size_t)(t + 1) * Bp * d.H;
   bf16_t* hnext = XH + (size_t)(t + 1) * d.B * KA + d.KX;
-  bf16_t* St = S + (size_t)t * Bp * d.H * kCoef;
+  bf16_t* St = S + (size_t)t * Bp * G;
 #pragma unroll
   for (int i = 0; i < C::TM; ++i) {
     const int mrow0 = cc.mb + i * 16;
@@ -98,7 +97,7 @@ __global__ __launch_bounds__(64 * WM * WN) void lstm_fwd_step_kernel(int t, bf16
     const float4 cp = *reinterpret_cast<const float4*>(cprev + blk * 256 + lane * 4);
     const float cpv[4] = {cp.x, cp.y, cp.z, cp.w};
     float cv[4];
-    unsigned pk[12];
+    unsigned pk[8];
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const float ig = sigmoidf_(acc[i][0][r]);
@@ -106,23 +105,16 @@ __global__ __launch_bounds__(64 * WM * WN) void lstm_fwd_step_kernel(int t, bf16
       const float gg = tanhf_(acc[i][2][r]);
       const float og = sigmoidf_(acc[i][3][r]);
       const float c = fg * cpv[r] + ig * gg;
-      const float tc = tanhf_(c);
       cv[r] = c;
-      // the six backward coefficients of this (row, unit), see cell_bwd4
-      const float kA = og * (1.f - tc * tc), kO = tc * og * (1.f - og);
-      const float kI = gg * ig * (1.f - ig), kF = cpv[r] * fg * (1.f - fg);
-      const float kG = ig * (1.f - gg * gg);
-      pk[3 * r] = (unsigned)f2bf(kA) | ((unsigned)f2bf(kO) << 16);
-      pk[3 * r + 1] = (unsigned)f2bf(kI) | ((unsigned)f2bf(kF) << 16);
-      pk[3 * r + 2] = (unsigned)f2bf(kG) | ((unsigned)f2bf(fg) << 16);
+      pk[2 * r] = (unsigned)f2bf(ig) | ((unsigned)f2bf(fg) << 16);
+      pk[2 * r + 1] = (unsigned)f2bf(gg) | ((unsigned)f2bf(og) << 16);
       const int m = mrow0 + 4 * (lane >> 4) + r;
-      if (m < d.B) hnext[(size_t)m * KA + u] = f2bf(og * tc);
+      if (m < d.B) hnext[(size_t)m * KA + u] = f2bf(og * tanhf_(c));
     }
     *reinterpret_cast<float4*>(cnext + blk * 256 + lane * 4) = make_float4(cv[0], cv[1], cv[2], cv[3]);
-    uint4* sp = reinterpret_cast<uint4*>(St + blk * (256 * kCoef) + lane * (4 * kCoef));
+    uint4* sp = reinterpret_cast<uint4*>(St + blk * 1024 + lane * 16);
     sp[0] = make_uint4(pk[0], pk[1], pk[2], pk[3]);
     sp[1] = make_uint4(pk[4], pk[5], pk[6], pk[7]);
-    sp[2] = make_uint4(pk[8], pk[9], pk[10], pk[11]);
   }
 }
 
@@ -156,41 +148,40 @@ void launch_lstm_fwd_step(int t, bf16_t* XH, const bf16_t* Wp, float* Cst, bf16_
 }
 
 // Cell backward for the 4 rows (mrow0 + 4*(lane>>4) + r) x unit u of step t held by this
-// lane, given dh for them. The forward stored, per (row, unit), the six coefficients
-//   kA = o(1-tanh^2 c), kO = tanh(c) o(1-o), kI = g i(1-i), kF = c_{t-1} f(1-f),
-//   kG = i(1-g^2), f
-// so  dc = carry + dh kA;  d_o = dh kO;  d_i = dc kI;  d_f = dc kF;  d_g = dc kG;
-//     carry' = dc f  — no cell-state history is re-read. One lane moves 48 B of
-// coefficients + 16 B of carry (fragment-native) and writes the gate gradients into
-// DG[t] (row-major, permuted columns: the next GEMM's A operand).
+// lane, given dh for them: reads the lane's fragment-native S / C / dc-carry slots with
+// 16-B vector accesses, updates the carry and writes the gate gradients into DG[t]
+// (row-major, permuted columns: it is the next GEMM's A operand).
 __device__ __forceinline__ void cell_bwd4(int t, int mrow0, int u, int lane, const float (&dh)[4],
+                                          const float* __restrict__ Cst,
                                           const bf16_t* __restrict__ S, bf16_t* __restrict__ DG,
                                           float* __restrict__ dcarry, const LstmDims& d) {
   const int G = 4 * d.H, Bp = fn_rows(d.B);
   const size_t blk = fn_block(mrow0, u, d.H);
-  const uint4* sp = reinterpret_cast<const uint4*>(S + (size_t)t * Bp * d.H * kCoef +
-                                                   blk * (256 * kCoef) + lane * (4 * kCoef));
-  const uint4 s0 = sp[0], s1 = sp[1], s2 = sp[2];
-  const unsigned pk[12] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w, s2.x, s2.y, s2.z, s2.w};
+  const uint4* sp = reinterpret_cast<const uint4*>(S + (size_t)t * Bp * G + blk * 1024 + lane * 16);
+  const uint4 s0 = sp[0], s1 = sp[1];
+  const unsigned pk[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
+  const float4 c4 = *reinterpret_cast<const float4*>(Cst + (size_t)(t + 1) * Bp * d.H + blk * 256 + lane * 4);
+  const float4 p4 = *reinterpret_cast<const float4*>(Cst + (size_t)t * Bp * d.H + blk * 256 + lane * 4);
   float4* dcp = reinterpret_cast<float4*>(dcarry + blk * 256 + lane * 4);
   const float4 k4 = *dcp;
+  const float cv[4] = {c4.x, c4.y, c4.z, c4.w}, pv[4] = {p4.x, p4.y, p4.z, p4.w};
   const float kv[4] = {k4.x, k4.y, k4.z, k4.w};
   float nk[4];
   bf16_t* dgt = DG + (size_t)t * d.B * G;
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
-    const float kA = bf2f((bf16_t)(pk[3 * r] & 0xffff)), kO = bf2f((bf16_t)(pk[3 * r] >> 16));
-    const float kI = bf2f((bf16_t)(pk[3 * r + 1] & 0xffff)), kF = bf2f((bf16_t)(pk[3 * r + 1] >> 16));
-    const float kG = bf2f((bf16_t)(pk[3 * r + 2] & 0xffff)), fg = bf2f((bf16_t)(pk[3 * r + 2] >> 16));
-    const float dc = kv[r] + dh[r] * kA;
+    const float ig = bf2f((bf16_t)(pk[2 * r] & 0xffff)), fg = bf2f((bf16_t)(pk[2 * r] >> 16));
+    const float gg = bf2f((bf16_t)(pk[2 * r + 1] & 0xffff)), og = bf2f((bf16_t)(pk[2 * r + 1] >> 16));
+    const float tc = tanhf_(cv[r]);
+    const float dc = kv[r] + dh[r] * og * (1.f - tc * tc);
     nk[r] = dc * fg;
     const int m = mrow0 + 4 * (lane >> 4) + r;
     if (m < d.B) {
       bf16_t* row = dgt + (size_t)m * G;
-      row[gate_col(0, u)] = f2bf(dc * kI);
-      row[gate_col(1, u)] = f2bf(dc * kF);
-      row[gate_col(2, u)] = f2bf(dc * kG);
-      row[gate_col(3, u)] = f2bf(dh[r] * kO);
+      row[gate_col(0, u)] = f2bf(dc * gg * ig * (1.f - ig));
+      row[gate_col(1, u)] = f2bf(dc * pv[r] * fg * (1.f - fg));
+      row[gate_col(2, u)] = f2bf(dc * ig * (1.f - gg * gg));
+      row[gate_col(3, u)] = f2bf(dh[r] * tc * og * (1.f - og));
     }
   }
   *dcp = make_float4(nk[0], nk[1], nk[2], nk[3]);
@@ -198,7 +189,7 @@ __device__ __forceinline__ void cell_bwd4(int t, int mrow0, int u, int lane, con
 
 // t = T-1: dh comes from the regression head, dh[m][u] = dy[m] * w_out[u]; the carry
 // starts at 0. One thread per (fragment-native block, lane) = 4 rows of one unit.
-__global__ void lstm_bwd_last_kernel(const bf16_t* __restrict__ S,
+__global__ void lstm_bwd_last_kernel(const float* __restrict__ Cst, const bf16_t* __restrict__ S,
                                      bf16_t* __restrict__ DG, float* __restrict__ dcarry,
                                      const float* __restrict__ dy, const float* __restrict__ w_out,
                                      LstmDims d) {
@@ -216,12 +207,13 @@ __global__ void lstm_bwd_last_kernel(const bf16_t* __restrict__ S,
       const int m = mrow0 + 4 * (lane >> 4) + r;
       dh[r] = m < d.B ? dy[m] * w_out[u] : 0.f;
     }
-    cell_bwd4(d.T - 1, mrow0, u, lane, dh, S, DG, dcarry, d);
+    cell_bwd4(d.T - 1, mrow0, u, lane, dh, Cst, S, DG, dcarry, d);
   }
 }
 
 template <int BM, int BN, int WM, int WN, int STAGES>
 __global__ __launch_bounds__(64 * WM * WN) void lstm_bwd_step_kernel(int t, const bf16_t* __restrict__ WhhT,
+                                                            const float* __restrict__ Cst,
                                                             const bf16_t* __restrict__ S,
                                                             bf16_t* __restrict__ DG,
                                                             float* __restrict__ dcarry, LstmDims d) {
@@ -250,48 +242,48 @@ __global__ __launch_bounds__(64 * WM * WN) void lstm_bwd_step_kernel(int t, cons
       const int mrow0 = cc.mb + i * 16;
       if (mrow0 >= d.B) continue;
       const float dh[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
-      cell_bwd4(t, mrow0, u, lane, dh, S, DG, dcarry, d);
+      cell_bwd4(t, mrow0, u, lane, dh, Cst, S, DG, dcarry, d);
     }
   }
 }
 
 template <int BM, int BN, int WM = 2, int WN = 2, int STAGES = 0>
-static void bwd_cfg(int t, const bf16_t* WhhT, const bf16_t* S, bf16_t* DG,
+static void bwd_cfg(int t, const bf16_t* WhhT, const float* Cst, const bf16_t* S, bf16_t* DG,
                     float* dcarry, LstmDims d, hipStream_t s) {
   if (STAGES >= 2 && d.B % BM != 0) {
-    bwd_cfg<BM, BN, WM, WN, 0>(t, WhhT, S, DG, dcarry, d, s);
+    bwd_cfg<BM, BN, WM, WN, 0>(t, WhhT, Cst, S, DG, dcarry, d, s);
     return;
   }
   const int tiles = ((d.B + BM - 1) / BM) * (d.H / BN);
   hipLaunchKernelGGL((lstm_bwd_step_kernel<BM, BN, WM, WN, STAGES>), dim3(tiles), dim3(64 * WM * WN),
-                     0, s, t, WhhT, S, DG, dcarry, d);
+                     0, s, t, WhhT, Cst, S, DG, dcarry, d);
 }
 
-void launch_lstm_bwd_step(int t, const bf16_t* WhhT, const bf16_t* S,
+void launch_lstm_bwd_step(int t, const bf16_t* WhhT, const float* Cst, const bf16_t* S,
                           bf16_t* DG, float* dcarry, const float* dy, const float* w_out,
                           LstmDims d, hipStream_t s) {
   if (t == d.T - 1) {
     const long total = (long)(fn_rows(d.B) >> 4) * (d.H >> 4) * 64;
     int blocks = (int)((total + 255) / 256);
     if (blocks > 8192) blocks = 8192;
-    hipLaunchKernelGGL(lstm_bwd_last_kernel, dim3(blocks), dim3(256), 0, s, S, DG, dcarry,
+    hipLaunchKernelGGL(lstm_bwd_last_kernel, dim3(blocks), dim3(256), 0, s, Cst, S, DG, dcarry,
                        dy, w_out, d);
     return;
   }
   switch (d.bwd_variant) {
-    case 1: bwd_cfg<64, 128>(t, WhhT, S, DG, dcarry, d, s); break;
-    case 2: bwd_cfg<128, 64>(t, WhhT, S, DG, dcarry, d, s); break;
-    case 3: bwd_cfg<64, 64>(t, WhhT, S, DG, dcarry, d, s); break;
-    case 4: bwd_cfg<128, 128, 2, 4>(t, WhhT, S, DG, dcarry, d, s); break;  // 8 waves
-    case 5: bwd_cfg<128, 128, 4, 2>(t, WhhT, S, DG, dcarry, d, s); break;  // 8 waves
-    case 6: bwd_cfg<128, 64, 2, 2>(t, WhhT, S, DG, dcarry, d, s); break;
-    case 7: bwd_cfg<64, 64, 2, 2, 3>(t, WhhT, S, DG, dcarry, d, s); break;    // glds
-    case 8: bwd_cfg<128, 128, 2, 4, 3>(t, WhhT, S, DG, dcarry, d, s); break;  // glds 8w
-    case 9: bwd_cfg<64, 128, 2, 2, 3>(t, WhhT, S, DG, dcarry, d, s); break;   // glds
-    case 10: bwd_cfg<128, 64, 2, 2, 3>(t, WhhT, S, DG, dcarry, d, s); break;  // glds
-    case 11: bwd_cfg<128, 128, 2, 2, 3>(t, WhhT, S, DG, dcarry, d, s); break; // glds 4w
-    case 12: bwd_cfg<64, 64, 2, 2, 4>(t, WhhT, S, DG, dcarry, d, s); break;   // glds 4st
-    default: bwd_cfg<128, 128>(t, WhhT, S, DG, dcarry, d, s); break;
+    case 1: bwd_cfg<64, 128>(t, WhhT, Cst, S, DG, dcarry, d, s); break;
+    case 2: bwd_cfg<128, 64>(t, WhhT, Cst, S, DG, dcarry, d, s); break;
+    case 3: bwd_cfg<64, 64>(t, WhhT, Cst, S, DG, dcarry, d, s); break;
+    case 4: bwd_cfg<128, 128, 2, 4>(t, WhhT, Cst, S, DG, dcarry, d, s); break;  // 8 waves
+    case 5: bwd_cfg<128, 128, 4, 2>(t, WhhT, Cst, S, DG, dcarry, d, s); break;  // 8 waves
+    case 6: bwd_cfg<128, 64, 2, 2>(t, WhhT, Cst, S, DG, dcarry, d, s); break;
+    case 7: bwd_cfg<64, 64, 2, 2, 3>(t, WhhT, Cst, S, DG, dcarry, d, s); break;    // glds
+    case 8: bwd_cfg<128, 128, 2, 4, 3>(t, WhhT, Cst, S, DG, dcarry, d, s); break;  // glds 8w
+    case 9: bwd_cfg<64, 128, 2, 2, 3>(t, WhhT, Cst, S, DG, dcarry, d, s); break;   // glds
+    case 10: bwd_cfg<128, 64, 2, 2, 3>(t, WhhT, Cst, S, DG, dcarry, d, s); break;  // glds
+    case 11: bwd_cfg<128, 128, 2, 2, 3>(t, WhhT, Cst, S, DG, dcarry, d, s); break; // glds 4w
+    case 12: bwd_cfg<64, 64, 2, 2, 4>(t, WhhT, Cst, S, DG, dcarry, d, s); break;   // glds 4st
+    default: bwd_cfg<128, 128>(t, WhhT, Cst, S, DG, dcarry, d, s); break;
   }
 }
 

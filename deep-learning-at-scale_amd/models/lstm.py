@@ -154,10 +154,8 @@ class NativeLSTM:
         T, B, H = seq_len, batch, hidden
         Bp = _round_up(B, 16)  # fragment-native state (C, S, dc carry) is 16-row padded
         self.XH = torch.zeros((T + 1) * B * lay.KA, dtype=bf, device=dev)
-        # cell state: 2-slot ping-pong (the backward never re-reads it); S: the six
-        # backward coefficients per (row, unit) and step, fragment-native, bf16
-        self.Cst = torch.zeros(2 * Bp * H, dtype=torch.float32, device=dev)
-        self.S = torch.empty(T * Bp * H * 6, dtype=bf, device=dev)
+        self.Cst = torch.zeros((T + 1) * Bp * H, dtype=torch.float32, device=dev)
+        self.S = torch.empty(T * Bp * lay.G, dtype=bf, device=dev)
         self.DG = torch.empty(T * B * lay.G, dtype=bf, device=dev)
         self.dcarry = torch.empty(Bp * H, dtype=torch.float32, device=dev)
         self.Wp = torch.empty(lay.G * lay.KA, dtype=bf, device=dev)
@@ -239,9 +237,9 @@ class NativeLSTM:
         # BPTT chain (high-priority stream) + dWcat = sum_{t,b} dG_t[b]^T [x_t | 1 | h_{t-1}][b]
         # as split-K GEMM chunks on a low-priority stream, overlapped with the chain.
         K = self.T * B
-        ksplit = self.dw_ksplit or max(1, min(16, K // 32768))
+        ksplit = self.dw_ksplit or max(1, min(32, K // 16384))
         if self.dw_chunk > 0:
             ksplit = max(1, ksplit * self.dw_chunk // self.T)
-        C.lstm_backward_dw(self.WhhT, self.XH, self.S, self.DG, self.dcarry, self.dy,
+        C.lstm_backward_dw(self.WhhT, self.XH, self.Cst, self.S, self.DG, self.dcarry, self.dy,
                            w_out, gW, *self._dims(B), self.bwd_variant, self.dw_chunk, ksplit)
         return self.loss_sum

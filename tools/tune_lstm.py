@@ -48,17 +48,17 @@ def main():
     C.lstm_forward(eng.XH, eng.Wp, eng.Cst, eng.S, *dims, 0)
     ref_fwd = (eng.XH.clone(), eng.Cst.clone(), eng.S.clone())
     for v in map(int, a.fwd.split(",")):
-        eng.S.zero_()  # (XH keeps x_t; its h part is rewritten)
+        eng.Cst[B * H:].zero_(); eng.S.zero_()  # (XH keeps x_t; its h part is rewritten)
         C.lstm_forward(eng.XH, eng.Wp, eng.Cst, eng.S, *dims, v)
         torch.cuda.synchronize()
         errs = [(x.float() - y.float()).abs().max().item() for x, y in zip((eng.XH, eng.Cst, eng.S), ref_fwd)]
         print(f"check fwd v{v}: max|diff| XH {errs[0]:.3g} C {errs[1]:.3g} S {errs[2]:.3g}", flush=True)
     w_out = lay.views(eng.params)[1]
-    C.lstm_backward(eng.WhhT, eng.XH, eng.S, eng.DG, eng.dcarry, eng.dy, w_out, *dims, 0)
+    C.lstm_backward(eng.WhhT, eng.XH, eng.Cst, eng.S, eng.DG, eng.dcarry, eng.dy, w_out, *dims, 0)
     ref_dg = eng.DG.clone()
     for v in map(int, a.bwd.split(",")):
         eng.DG.zero_()
-        C.lstm_backward(eng.WhhT, eng.XH, eng.S, eng.DG, eng.dcarry, eng.dy, w_out, *dims, v)
+        C.lstm_backward(eng.WhhT, eng.XH, eng.Cst, eng.S, eng.DG, eng.dcarry, eng.dy, w_out, *dims, v)
         torch.cuda.synchronize()
         print(f"check bwd v{v}: max|diff| DG {(eng.DG.float() - ref_dg.float()).abs().max().item():.3g}", flush=True)
     res = {}
@@ -67,7 +67,7 @@ def main():
             ms = timeit(lambda: C.lstm_forward(eng.XH, eng.Wp, eng.Cst, eng.S, *dims, v))
             res.setdefault(f"fwd v{v}", []).append(ms)
         for v in map(int, a.bwd.split(",")):
-            ms = timeit(lambda: C.lstm_backward(eng.WhhT, eng.XH, eng.S, eng.DG, eng.dcarry,
+            ms = timeit(lambda: C.lstm_backward(eng.WhhT, eng.XH, eng.Cst, eng.S, eng.DG, eng.dcarry,
                                                 eng.dy, lay.views(eng.params)[1], *dims, v))
             res.setdefault(f"bwd v{v}", []).append(ms)
         for ks in map(int, a.ksplit.split(",")):
