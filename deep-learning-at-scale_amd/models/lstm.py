@@ -165,7 +165,7 @@ class NativeLSTM:
         self.loss_sum = torch.zeros(1, dtype=torch.float32, device=dev)
         # tile shapes (csrc/kernels.h LstmDims), A/B-tuned on MI355X with tools/tune_lstm.py
         # (profiles/r1_*): fwd 256x256 glds ring (v6), bwd 64x128 glds ring (v9); dW split-K 32.
-        self.fwd_variant, self.bwd_variant = 6, 9
+        self.fwd_variant, self.bwd_variant = 6, 8
         self.dw_ksplit = 0  # 0 = heuristic
         # timesteps per overlapped dW GEMM chunk; 0 = serial dW at the end (measured faster:
         # the BPTT chain already fills every CU, overlapping only adds contention)
@@ -237,7 +237,7 @@ class NativeLSTM:
         # BPTT chain (high-priority stream) + dWcat = sum_{t,b} dG_t[b]^T [x_t | 1 | h_{t-1}][b]
         # as split-K GEMM chunks on a low-priority stream, overlapped with the chain.
         K = self.T * B
-        ksplit = self.dw_ksplit or max(1, min(32, K // 16384))
+        ksplit = self.dw_ksplit or max(1, min(16, K // 32768))
         if self.dw_chunk > 0:
             ksplit = max(1, ksplit * self.dw_chunk // self.T)
         C.lstm_backward_dw(self.WhhT, self.XH, self.Cst, self.S, self.DG, self.dcarry, self.dy,

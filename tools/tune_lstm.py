@@ -76,6 +76,16 @@ def main():
                 gemm(eng.DG, eng.XH, lay.G, lay.KA, T * B, a_mn=True, lda=lay.G, b_mn=True, ldb=lay.KA,
                      outF=gW, ldo=lay.KA, atomic=True, ksplit=ks)
             res.setdefault(f"dW ksplit {ks}", []).append(timeit(dw))
+        # decomposition of one backward step: same-shape GEMM alone, cell epilogue alone
+        tmp = torch.empty(B * H, dtype=torch.bfloat16, device="cuda")
+        A1 = eng.DG[B * lay.G : 2 * B * lay.G]
+        res.setdefault("bwd-shape GEMM x63", []).append(
+            63 * timeit(lambda: gemm(A1, eng.WhhT, B, H, lay.G, outH=tmp)))
+        d1 = (B, 1, F, lay.KX, H)
+        res.setdefault("bwd epilogue-only x63", []).append(63 * timeit(lambda: C.lstm_backward(
+            eng.WhhT, eng.XH, eng.Cst, eng.S, eng.DG, eng.dcarry, eng.dy, lay.views(eng.params)[1], *d1, 0)))
+        res.setdefault("fwd-shape GEMM x64", []).append(
+            64 * timeit(lambda: gemm(eng.XH[: B * lay.KA], eng.Wp, B, lay.G, lay.KA, outH=eng.DG[: B * lay.G])))
     fl_fwd = 2.0 * B * lay.G * lay.KA * T
     fl_bwd = 2.0 * B * H * lay.G * (T - 1)
     fl_dw = 2.0 * B * T * lay.G * lay.KA
