@@ -143,6 +143,7 @@ void launch_lstm_fwd_step(int t, bf16_t* XH, const bf16_t* Wp, float* Cst, bf16_
     case 8: fwd_cfg<128, 2, 2, 3>(t, XH, Wp, Cst, S, d, s); break;  // glds, 3 stages (96 KiB)
     case 9: fwd_cfg<256, 4, 2, 3>(t, XH, Wp, Cst, S, d, s); break;  // glds, 3 stages (144 KiB)
     case 10: fwd_cfg<128, 2, 2, 2>(t, XH, Wp, Cst, S, d, s); break; // glds, 2 stages (64 KiB)
+    case 11: fwd_cfg<128, 2, 2, 4>(t, XH, Wp, Cst, S, d, s); break; // glds, 4 stages (128 KiB)
     default: fwd_cfg<128, 2, 2>(t, XH, Wp, Cst, S, d, s); break;
   }
 }
@@ -283,6 +284,9 @@ void launch_lstm_bwd_step(int t, const bf16_t* WhhT, const float* Cst, const bf1
     case 10: bwd_cfg<128, 64, 2, 2, 3>(t, WhhT, Cst, S, DG, dcarry, d, s); break;  // glds
     case 11: bwd_cfg<128, 128, 2, 2, 3>(t, WhhT, Cst, S, DG, dcarry, d, s); break; // glds 4w
     case 12: bwd_cfg<64, 64, 2, 2, 4>(t, WhhT, Cst, S, DG, dcarry, d, s); break;   // glds 4st
+    case 13: bwd_cfg<128, 128, 2, 4, 4>(t, WhhT, Cst, S, DG, dcarry, d, s); break; // 8w 4st 128K
+    case 14: bwd_cfg<64, 128, 2, 2, 4>(t, WhhT, Cst, S, DG, dcarry, d, s); break;  // 4st 96K
+    case 15: bwd_cfg<128, 64, 2, 2, 4>(t, WhhT, Cst, S, DG, dcarry, d, s); break;  // 4st 96K
     default: bwd_cfg<128, 128>(t, WhhT, Cst, S, DG, dcarry, d, s); break;
   }
 }
