@@ -1,13 +1,17 @@
 #!/usr/bin/env python3
-"""Headline benchmark: rows/sec (whole node) of LSTM seq-64 hidden-512 regression training.
+"""Headline benchmark (BASELINE.json): rows/sec (whole node) of LSTM seq-64 hidden-512
+time-series regression training, DP over 1/2/4/8 MI355X, bf16.
 
-BASELINE.json:2 / :11 — "LSTM seq-len=64 hidden=512 time-series regression, DP=8 bf16".
-One row = one training sample (a 64-step window of well-log features and its flow
-target). Each timed step is a FULL training step: forward over all 64 timesteps, MSE
-loss, backward through time, RCCL gradient all-reduce (world > 1), fused Adam update and
-the bf16 weight repack. Weak scaling: the per-GPU batch is fixed, global = per-GPU x N.
+One row = one training sample (a 64-step window of well-log features and its flow target).
+Every timed step is a FULL training step: forward over all 64 timesteps, MSE loss,
+backward through time, weight gradients, RCCL gradient all-reduce (world > 1), fused Adam
+update and the bf16 weight repack. Weak scaling: per-GPU batch fixed, global = per-GPU x N.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B_per_gpu]
+Secondary configs (BASELINE.json:8-10), same JSON contract:
+  --model mlp         static 3-layer MLP (F -> 256 -> 256 -> 1), resident batch, hipGraph step
+  --model mlp_online  dynamic MLP: every step trains on a NEW mini-batch streamed host -> HBM
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B_per_gpu] [--model ...]
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
 """
 from __future__ import annotations
@@ -22,13 +26,136 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
 
+METRIC = "rows/sec (whole node), LSTM seq64 regression at 1/2/4/8 MI355X; val MSE parity"
+DEFAULT_BATCH = {"lstm": 8192, "mlp": 65536, "mlp_online": 65536}
+
+
+def _timed(ctx, step, steps, warmup):
+    import torch
+
+    for _ in range(warmup):
+        step()
+    ctx.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    torch.cuda.synchronize()
+    ctx.barrier()
+    return ctx.max_scalar(time.perf_counter() - t0)
+
+
+def bench_lstm(args, ctx):
+    from wellflow.data.synth import synth_lstm_batch
+    from wellflow.models.lstm import NativeLSTM, init_lstm_flat
+    from wellflow.optim.flat import FlatAdam
+
+    B, T, F, H = args.batch, args.seq, args.features, args.hidden
+    eng = NativeLSTM(F, H, T, B, device=ctx.device)
+    if args.dw_chunk is not None:
+        eng.dw_chunk = args.dw_chunk
+    if args.fwd_variant is not None:
+        eng.fwd_variant = args.fwd_variant
+    if args.bwd_variant is not None:
+        eng.bwd_variant = args.bwd_variant
+    eng.params.copy_(init_lstm_flat(F, H, seed=0).to(ctx.device))
+    ctx.broadcast_(eng.params)  # C1: identical init on every rank
+    eng.sync_weights()
+    opt = FlatAdam(eng.params, eng.grads, lr=args.lr)
+    x, y = synth_lstm_batch(B, T, F, seed=ctx.rank)  # Gilbert-consistent windows, GPU-resident
+    x, y = x.to(ctx.device), y.to(ctx.device)
+    gscale = 1.0 / (B * ctx.world_size)
+
+    def step():
+        eng.forward_backward(x, y, gscale)
+        ctx.all_reduce_sum_(eng.grads)  # C2: one flat bucket over RCCL / xGMI
+        opt.step()
+        eng.sync_weights()
+
+    el = _timed(ctx, step, args.steps, args.warmup)
+    model = f"LSTM seq-len={T} hidden={H} time-series regression (features={F}, linear head, MSE, Adam)"
+    return el, B, model, eng.loss_sum.item() / B
+
+
+def bench_mlp(args, ctx, online: bool):
+    import torch
+
+    from wellflow.data.stream import DeviceStreamer, HostPool
+    from wellflow.data.synth import synth_tabular_batch
+    from wellflow.models.mlp import NativeMLP, init_mlp_flat
+    from wellflow.optim.flat import FlatAdam
+
+    B, F, hid = args.batch, args.features, (256, 256)
+    eng = NativeMLP(F, hid, B, device=ctx.device)
+    eng.params.copy_(init_mlp_flat(F, hid, seed=0).to(ctx.device))
+    ctx.broadcast_(eng.params)
+    eng.sync_weights()
+    opt = FlatAdam(eng.params, eng.grads, lr=args.lr)
+    gscale = 1.0 / (B * ctx.world_size)
+
+    if online:
+        pool = HostPool(lambda k: synth_tabular_batch(B, F, seed=1000 * ctx.rank + k), n=8)
+        streamer = DeviceStreamer(pool, ctx.device, depth=3)
+
+        def step():
+            xb, yb = streamer.next()
+            eng.forward_backward(xb, yb, gscale)
+            ctx.all_reduce_sum_(eng.grads)
+            opt.step()
+            eng.sync_weights()
+    else:
+        x, y = synth_tabular_batch(B, F, seed=ctx.rank)
+        x, y = x.to(ctx.device), y.to(ctx.device)
+
+        def compute():
+            eng.forward_backward(x, y, gscale)
+
+        def update():
+            opt.step()
+            eng.sync_weights()
+
+        graphs = None
+        if not args.no_graph:
+            # the whole step is a few tiny launches: capture it so the CPU launch path is
+            # out of the loop (Adam's step counter is device-side, so replay is exact)
+            s = torch.cuda.Stream(device=ctx.device)
+            s.wait_stream(torch.cuda.current_stream(ctx.device))
+            with torch.cuda.stream(s):
+                for _ in range(3):
+                    compute()
+                    ctx.all_reduce_sum_(eng.grads)
+                    update()
+            torch.cuda.current_stream(ctx.device).wait_stream(s)
+            g1, g2 = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g1):
+                compute()
+            with torch.cuda.graph(g2):
+                update()
+            graphs = (g1, g2)
+
+        def step():
+            if graphs is None:
+                compute()
+                ctx.all_reduce_sum_(eng.grads)
+                update()
+            else:
+                graphs[0].replay()
+                ctx.all_reduce_sum_(eng.grads)
+                graphs[1].replay()
+
+    el = _timed(ctx, step, args.steps, args.warmup)
+    kind = "dynamic (online, host->HBM streamed mini-batches)" if online else "static (resident batch)"
+    model = f"{kind} 3-layer MLP regression F={F} -> 256 -> 256 -> 1, MSE, Adam"
+    return el, B, model, eng.loss_sum.item() / B
+
 
 def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--batch", type=int, default=8192, help="per-GPU batch (rows)")
+    ap.add_argument("--model", choices=["lstm", "mlp", "mlp_online"], default="lstm")
+    ap.add_argument("--batch", type=int, default=None, help="per-GPU batch (rows)")
     ap.add_argument("--seq", type=int, default=64)
     ap.add_argument("--hidden", type=int, default=512)
     ap.add_argument("--features", type=int, default=16)
@@ -36,84 +163,47 @@ def main() -> int:
     ap.add_argument("--dw-chunk", type=int, default=None, help="timesteps per overlapped dW chunk (0 = serial)")
     ap.add_argument("--fwd-variant", type=int, default=None)
     ap.add_argument("--bwd-variant", type=int, default=None)
+    ap.add_argument("--no-graph", action="store_true")
     args = ap.parse_args()
+    if args.batch is None:
+        args.batch = DEFAULT_BATCH[args.model]
 
     import torch
-    import torch.distributed as dist
 
-    from wellflow.data.synth import synth_lstm_batch
-    from wellflow.models.lstm import NativeLSTM, init_lstm_flat
-    from wellflow.optim.flat import FlatAdam
     from wellflow.parallel.dist import DistContext
 
     ctx = DistContext.from_env()
-    world, rank = ctx.world_size, ctx.rank
-    if world != args.gpus and rank == 0:
-        print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
-    dev = ctx.device
-    torch.manual_seed(1234 + rank)
+    if ctx.world_size != args.gpus and ctx.is_main:
+        print(f"warning: --gpus {args.gpus} but WORLD_SIZE={ctx.world_size}", file=sys.stderr)
+    torch.manual_seed(1234 + ctx.rank)
+    if args.model == "lstm":
+        elapsed, B, model, loss = bench_lstm(args, ctx)
+    else:
+        elapsed, B, model, loss = bench_mlp(args, ctx, online=args.model == "mlp_online")
 
-    B, T, F, H = args.batch, args.seq, args.features, args.hidden
-    eng = NativeLSTM(F, H, T, B, device=dev)
-    if args.dw_chunk is not None:
-        eng.dw_chunk = args.dw_chunk
-    if args.fwd_variant is not None:
-        eng.fwd_variant = args.fwd_variant
-    if args.bwd_variant is not None:
-        eng.bwd_variant = args.bwd_variant
-    eng.params.copy_(init_lstm_flat(F, H, seed=0).to(dev))
-    ctx.broadcast_(eng.params)  # C1: identical init on every rank
-    eng.sync_weights()
-    opt = FlatAdam(eng.params, eng.grads, lr=args.lr)
-
-    # synthetic well-log windows (Gilbert-consistent targets), resident on the GPU
-    x, y = synth_lstm_batch(B, T, F, seed=rank)
-    x, y = x.to(dev), y.to(dev)
-    grad_scale = 1.0 / (B * world)
-
-    def step():
-        eng.forward_backward(x, y, grad_scale)
-        ctx.all_reduce_sum_(eng.grads)  # C2: one flat bucket over RCCL / xGMI
-        opt.step()
-        eng.sync_weights()
-
-    for _ in range(args.warmup):
-        step()
-    ctx.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-    torch.cuda.synchronize()
-    ctx.barrier()
-    elapsed = time.perf_counter() - t0
-    elapsed = ctx.max_scalar(elapsed)
-    loss = eng.loss_sum.item() / B
-
-    ms = 1000.0 * elapsed / max(args.steps, 1)
-    rows_per_s = B * world * args.steps / elapsed
-    if rank == 0:
+    W = ctx.world_size
+    if ctx.is_main:
         rec = {
-            "metric": "rows/sec (whole node), LSTM seq64 regression training",
-            "value": round(rows_per_s, 1),
+            "metric": METRIC if args.model == "lstm" else f"rows/sec (whole node), {args.model} regression training",
+            "value": round(B * W * args.steps / elapsed, 1),
             "unit": "rows/s",
-            "n_gpus": world,
+            "n_gpus": W,
             "steps": args.steps,
             "warmup": args.warmup,
-            "ms_per_step": round(ms, 4),
+            "ms_per_step": round(1000.0 * elapsed / max(args.steps, 1), 4),
             "higher_is_better": True,
             "scaling": "weak",
-            "vs_baseline": None,
+            "vs_baseline": None,  # the reference publishes no numbers (BASELINE.json "published": {})
             "dtype": "bf16",
-            "data": "synthetic (Gilbert-equation well-log windows, random-init weights)",
+            "data": "synthetic (Gilbert-equation well-log data), random-init weights",
             "config": {
-                "model": f"LSTM seq_len={T} hidden={H} features={F} -> linear head, MSE, Adam",
-                "global_batch": B * world,
+                "model": model,
+                "global_batch": B * W,
                 "per_gpu_batch": B,
-                "seq_len": T,
-                "parallelism": f"dp{world}",
+                "seq_len": args.seq if args.model == "lstm" else 1,
+                "parallelism": f"dp{W}",
             },
-            "final_train_mse": round(loss, 6),
+            "final_train_loss": round(loss, 6),
         }
         print(json.dumps(rec), flush=True)
     ctx.shutdown()

@@ -382,6 +382,21 @@ void adam(const at::Tensor& p, const at::Tensor& g, const at::Tensor& m, const a
                   (float)wd, (float)bc1, (float)bc2, (float)gscale, cur_stream());
 }
 
+void adam_dev(const at::Tensor& p, const at::Tensor& g, const at::Tensor& m, const at::Tensor& v,
+              const at::Tensor& step, double lr, double b1, double b2, double eps, double wd,
+              double gscale) {
+  check_t(p, at::kFloat, "p");
+  check_t(g, at::kFloat, "g");
+  check_t(m, at::kFloat, "m");
+  check_t(v, at::kFloat, "v");
+  check_t(step, at::kFloat, "step");
+  const int64_t n = p.numel();
+  TORCH_CHECK(g.numel() == n && m.numel() == n && v.numel() == n, "adam: size mismatch");
+  const c10::hip::OptionalHIPGuardMasqueradingAsCUDA guard(p.device());
+  wf::launch_adam_dev(fp(p), fp(g), fp(m), fp(v), n, fp(step), (float)lr, (float)b1, (float)b2,
+                      (float)eps, (float)wd, (float)gscale, cur_stream());
+}
+
 void sgd(const at::Tensor& p, const at::Tensor& g, const at::Tensor& vel, double lr,
          double momentum, bool nesterov, double gscale) {
   check_t(p, at::kFloat, "p");
@@ -443,6 +458,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("head_bwd_x", &head_bwd_x);
   m.def("loss", &loss);
   m.def("adam", &adam);
+  m.def("adam_dev", &adam_dev);
   m.def("sgd", &sgd);
   m.def("cast_bf16", &cast_bf16);
   m.def("transpose_cast_bf16", &transpose_cast_bf16);

@@ -213,6 +213,45 @@ void launch_adam(float* p, const float* g, float* m, float* v, long n, float lr,
                      eps, wd, bc1, bc2, gscale);
 }
 
+// Graph-capturable Adam: the step counter lives on the device (incremented by a 1-thread
+// kernel in the same stream), so a captured hipGraph replays with correct bias corrections.
+__global__ void inc_counter_kernel(float* step) {
+  if (blockIdx.x == 0 && threadIdx.x == 0) step[0] += 1.f;
+}
+
+__global__ __launch_bounds__(256) void adam_dev_kernel(float* __restrict__ p, const float* __restrict__ g,
+                                                       float* __restrict__ m, float* __restrict__ v,
+                                                       long n, const float* __restrict__ step, float lr,
+                                                       float b1, float b2, float eps, float wd,
+                                                       float gscale) {
+  const float t = step[0];
+  const float bc1 = 1.f - __powf(b1, t), bc2 = 1.f - __powf(b2, t);
+  const long n4 = n / 4;
+  const long stride = (long)gridDim.x * blockDim.x;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n4; i += stride) {
+    float4 pp = reinterpret_cast<float4*>(p)[i];
+    float4 gg = reinterpret_cast<const float4*>(g)[i];
+    float4 mm = reinterpret_cast<float4*>(m)[i];
+    float4 vv = reinterpret_cast<float4*>(v)[i];
+    adam_one(pp.x, gg.x * gscale, mm.x, vv.x, lr, b1, b2, eps, wd, bc1, bc2);
+    adam_one(pp.y, gg.y * gscale, mm.y, vv.y, lr, b1, b2, eps, wd, bc1, bc2);
+    adam_one(pp.z, gg.z * gscale, mm.z, vv.z, lr, b1, b2, eps, wd, bc1, bc2);
+    adam_one(pp.w, gg.w * gscale, mm.w, vv.w, lr, b1, b2, eps, wd, bc1, bc2);
+    reinterpret_cast<float4*>(p)[i] = pp;
+    reinterpret_cast<float4*>(m)[i] = mm;
+    reinterpret_cast<float4*>(v)[i] = vv;
+  }
+  for (long i = n4 * 4 + blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += stride)
+    adam_one(p[i], g[i] * gscale, m[i], v[i], lr, b1, b2, eps, wd, bc1, bc2);
+}
+
+void launch_adam_dev(float* p, const float* g, float* m, float* v, long n, float* step, float lr,
+                     float b1, float b2, float eps, float wd, float gscale, hipStream_t s) {
+  hipLaunchKernelGGL(inc_counter_kernel, dim3(1), dim3(64), 0, s, step);
+  hipLaunchKernelGGL(adam_dev_kernel, dim3(ew_blocks(n)), dim3(256), 0, s, p, g, m, v, n, step, lr,
+                     b1, b2, eps, wd, gscale);
+}
+
 // Keras-0.x SGD: v = mu v - lr_t g; p += mu v - lr_t g (Nesterov) or p += v.
 // lr_t = lr / (1 + decay * iterations) is computed on the host.
 __global__ __launch_bounds__(256) void sgd_kernel(float* __restrict__ p, const float* __restrict__ g,

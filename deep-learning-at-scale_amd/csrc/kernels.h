@@ -58,6 +58,8 @@ void launch_loss(int kind, const float* pred, const float* y, int B, int O, floa
 // ---- optimizers and casts over flat fp32 buffers ----
 void launch_adam(float* p, const float* g, float* m, float* v, long n, float lr, float b1,
                  float b2, float eps, float wd, float bc1, float bc2, float gscale, hipStream_t s);
+void launch_adam_dev(float* p, const float* g, float* m, float* v, long n, float* step, float lr,
+                     float b1, float b2, float eps, float wd, float gscale, hipStream_t s);
 void launch_sgd(float* p, const float* g, float* vel, long n, float lr, float momentum,
                 int nesterov, float gscale, hipStream_t s);
 void launch_cast_bf16(const float* src, bf16_t* dst, long n, hipStream_t s);

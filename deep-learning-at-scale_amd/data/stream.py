@@ -1,0 +1,69 @@
+"""Streaming mini-batches host -> HBM for the dynamic (online) model (BASELINE.json:10).
+
+``DeviceStreamer`` keeps a ring of ``depth`` device buffers fed from pinned host memory on
+a dedicated copy stream: batch k+1 (and k+2 ...) is in flight over PCIe while the compute
+stream trains on batch k; compute waits only on the event of the batch it consumes. The
+source is any iterator of (x, y) numpy/torch arrays (CSV chunks, a message queue, the
+synthetic generator); ``HostPool`` pre-stages a set of batches in pinned memory and
+cycles through them, which is how the benchmark isolates the transfer + train pipeline
+from Python-side generation cost. Inputs can be streamed as bf16 (the MFMA engines
+consume bf16 directly), halving PCIe bytes.
+"""
+from __future__ import annotations
+
+import itertools
+
+import torch
+
+
+class HostPool:
+    """``n`` distinct (x, y) batches resident in pinned host memory, cycled forever."""
+
+    def __init__(self, make_batch, n: int, x_dtype=torch.float32):
+        self.batches = []
+        for k in range(n):
+            x, y = make_batch(k)
+            x = torch.as_tensor(x).to(x_dtype).pin_memory()
+            y = torch.as_tensor(y).float().pin_memory()
+            self.batches.append((x, y))
+
+    def __iter__(self):
+        return itertools.cycle(self.batches)
+
+
+class DeviceStreamer:
+    def __init__(self, source, device, depth: int = 3):
+        assert depth >= 2
+        self.src = iter(source)
+        self.device = torch.device(device)
+        self.copy_stream = torch.cuda.Stream(device=self.device)
+        self.depth = depth
+        self.slots = []  # (x_dev, y_dev, event)
+        self.k = 0
+        self._primed = False
+
+    def _issue(self):
+        x, y = next(self.src)
+        slot = self.k % self.depth
+        if len(self.slots) < self.depth:
+            xd = torch.empty(x.shape, dtype=x.dtype, device=self.device)
+            yd = torch.empty(y.shape, dtype=y.dtype, device=self.device)
+            self.slots.append([xd, yd, torch.cuda.Event()])
+        xd, yd, ev = self.slots[slot]
+        # the slot's previous consumer must be done before it is overwritten
+        self.copy_stream.wait_stream(torch.cuda.current_stream(self.device))
+        with torch.cuda.stream(self.copy_stream):
+            xd.copy_(x, non_blocking=True)
+            yd.copy_(y, non_blocking=True)
+            ev.record(self.copy_stream)
+        self.k += 1
+
+    def next(self):
+        if not self._primed:
+            for _ in range(self.depth - 1):
+                self._issue()
+            self._primed = True
+        self._issue()  # keep depth-1 batches in flight
+        xd, yd, ev = self.slots[(self.k - self.depth) % self.depth]
+        torch.cuda.current_stream(self.device).wait_event(ev)
+        return xd, yd

@@ -22,17 +22,20 @@ class FlatAdam:
         self.m = torch.zeros_like(params)
         self.v = torch.zeros_like(params)
         self.t = 0
+        # device-side step counter: the GPU update is graph-capturable (bias corrections
+        # are computed in-kernel from it, never baked in as launch constants)
+        self.step_dev = torch.zeros(4, device=params.device) if params.is_cuda else None
 
     def step(self, grad_scale: float = 1.0) -> None:
         self.t += 1
         b1, b2 = self.betas
-        bc1, bc2 = 1.0 - b1**self.t, 1.0 - b2**self.t
         if self.params.is_cuda:
             from ..ops.native import lib
 
-            lib().adam(self.params, self.grads, self.m, self.v, self.lr, b1, b2, self.eps,
-                       self.weight_decay, bc1, bc2, grad_scale)
+            lib().adam_dev(self.params, self.grads, self.m, self.v, self.step_dev, self.lr, b1, b2,
+                           self.eps, self.weight_decay, grad_scale)
             return
+        bc1, bc2 = 1.0 - b1**self.t, 1.0 - b2**self.t
         g = self.grads * grad_scale
         self.m.mul_(b1).add_(g, alpha=1 - b1)
         self.v.mul_(b2).addcmul_(g, g, value=1 - b2)
@@ -48,6 +51,8 @@ class FlatAdam:
 
     def load_state_dict(self, sd: dict) -> None:
         self.t = int(sd["t"])
+        if self.step_dev is not None:
+            self.step_dev.fill_(float(self.t))
         self.m.copy_(sd["m"])
         self.v.copy_(sd["v"])
         self.lr, self.betas, self.eps = sd["lr"], tuple(sd["betas"]), sd["eps"]
