@@ -97,6 +97,9 @@ void gemm(const at::Tensor& A, bool a_mn, int64_t lda, const at::Tensor& B, bool
   e.drop_p = (float)drop_p;
   e.seed = (unsigned long long)seed;
   TORCH_CHECK(ksplit == 1 || atomic, "gemm: split-K needs atomic accumulation");
+  e.stage_ok = (e.outH != nullptr && e.outF == nullptr && !atomic && beta == 0.0 && N % 8 == 0 &&
+                ldo % 8 == 0 && (e.mask == nullptr || ldm % 8 == 0))
+                   ? 1 : 0;
   // glds (whole-tile) path: the 128x128 tiles may over-read rows/cols past M / N; allow it
   // only when that stays inside both allocations (and every K chunk is 64-aligned).
   const int64_t Mc = (M + 127) / 128 * 128, Nc = (N + 127) / 128 * 128;
@@ -300,6 +303,8 @@ void lstm_pack_weights(const at::Tensor& W, const at::Tensor& Wp, const at::Tens
 // timestep of XH): the raw pointer is taken from the given tensor (its storage offset).
 void check_head_h(const at::Tensor& Hm, int64_t ldh, int64_t B, int64_t Hd) {
   TORCH_CHECK(Hm.is_cuda() && Hm.scalar_type() == at::kBFloat16, "H: bf16 GPU tensor");
+  TORCH_CHECK(Hd % 8 == 0 && ldh % 8 == 0 && Hd <= 2048, "head: Hd, ldh multiples of 8, Hd <= 2048");
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(Hm.data_ptr()) % 16 == 0, "head: H must be 16-B aligned");
   TORCH_CHECK(ldh >= Hd, "head: ldh < Hd");
   TORCH_CHECK(Hm.storage().nbytes() - Hm.storage_offset() * 2 >= (size_t)(((B - 1) * ldh + Hd) * 2),
               "head: H too small");
@@ -346,6 +351,7 @@ void head_bwd_x(const at::Tensor& Hm, int64_t ldh, int64_t B, int64_t Hd, const 
   check_extent(w, Hd, "w");
   check_t(dz, at::kBFloat16, "dz");
   check_extent(dz, (B - 1) * ldz + Hd, "dz");
+  TORCH_CHECK(ldz % 8 == 0, "head_bwd_x: ldz must be a multiple of 8");
   const c10::hip::OptionalHIPGuardMasqueradingAsCUDA guard(Hm.device());
   wf::launch_head_bwd_x(bfp(Hm), ldh, (int)B, (int)Hd, fp(dy), fp(w), relu_mask ? 1 : 0, bfp(dz),
                         ldz, opt_ptr<float>(colsum, at::kFloat, "colsum", Hd), cur_stream());

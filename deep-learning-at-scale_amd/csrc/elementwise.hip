@@ -10,7 +10,11 @@
 namespace wf {
 
 // ---------------------------------------------------------------- regression head (N=1)
-// One wave per row: pred = <h[b], w> + b0; with a target also loss and dy = scale*(pred-y).
+// Row groups of LPR lanes (LPR = Hd/8 rounded up to a power of two, <= 64) each own one
+// row: a lane loads 16 B (8 bf16) of it, the group reduces with xor-shuffles. The loss is
+// block-reduced and added with ONE atomic per workgroup (same-address atomics from every
+// workgroup were 33% of the MLP step before).
+template <int LPR>
 __global__ __launch_bounds__(256) void head_fwd_kernel(const bf16_t* __restrict__ Hm, long ldh,
                                                        int B, int Hd, const float* __restrict__ w,
                                                        const float* __restrict__ b0,
@@ -20,102 +24,176 @@ __global__ __launch_bounds__(256) void head_fwd_kernel(const bf16_t* __restrict_
                                                        float* __restrict__ loss_sum,
                                                        float dy_scale) {
   __shared__ float red[4];
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  const int b = blockIdx.x * 4 + wid;
+  constexpr int RPB = 256 / LPR;  // rows per block pass
+  const int sub = threadIdx.x % LPR, grp = threadIdx.x / LPR;
+  const float bias = b0[0];
   float lsum = 0.f;
-  if (b < B) {
-    const bf16_t* row = Hm + (size_t)b * ldh;
+  for (int rb = blockIdx.x * RPB; rb < B; rb += gridDim.x * RPB) {
+    const int b = rb + grp;
     float acc = 0.f;
-    for (int k = lane * 8; k < Hd; k += 512) {
-      const bf16x8 v = *reinterpret_cast<const bf16x8*>(row + k);
-#pragma unroll
-      for (int e = 0; e < 8; ++e) acc += bf2f((bf16_t)v[e]) * w[k + e];
+    if (b < B) {
+      const bf16_t* row = Hm + (size_t)b * ldh;
+      for (int k = sub * 8; k < Hd; k += LPR * 8) {
+        const bf16x8 v = *reinterpret_cast<const bf16x8*>(row + k);
+        const float4 w0 = *reinterpret_cast<const float4*>(w + k);
+        const float4 w1 = *reinterpret_cast<const float4*>(w + k + 4);
+        acc += bf2f((bf16_t)v[0]) * w0.x + bf2f((bf16_t)v[1]) * w0.y + bf2f((bf16_t)v[2]) * w0.z +
+               bf2f((bf16_t)v[3]) * w0.w + bf2f((bf16_t)v[4]) * w1.x + bf2f((bf16_t)v[5]) * w1.y +
+               bf2f((bf16_t)v[6]) * w1.z + bf2f((bf16_t)v[7]) * w1.w;
+      }
     }
-    acc = wave_sum(acc) + b0[0];
-    if (lane == 0) {
+#pragma unroll
+    for (int o = LPR / 2; o > 0; o >>= 1) acc += __shfl_xor(acc, o, 64);
+    if (sub == 0 && b < B) {
+      acc += bias;
       pred[b] = acc;
       if (target != nullptr) {
         const float diff = acc - target[b];
-        lsum = diff * diff;
+        lsum += diff * diff;
         if (dy != nullptr) dy[b] = dy_scale * diff;
       }
     }
   }
   if (loss_sum != nullptr) {
-    if (lane == 0) red[wid] = lsum;
-    __syncthreads();
-    if (threadIdx.x == 0) atomicAdd(loss_sum, red[0] + red[1] + red[2] + red[3]);
+    const float t = block_sum<256>(lsum, red);
+    if (threadIdx.x == 0) atomicAdd(loss_sum, t);
   }
+}
+
+static int lanes_per_row(int Hd) {
+  int l = 1;
+  while (l < 64 && l * 8 < Hd) l <<= 1;
+  return l;
 }
 
 void launch_head_fwd(const bf16_t* Hm, long ldh, int B, int Hd, const float* w, const float* b0,
                      const float* target, float* pred, float* dy, float* loss_sum, float dy_scale,
                      hipStream_t s) {
-  hipLaunchKernelGGL(head_fwd_kernel, dim3((B + 3) / 4), dim3(256), 0, s, Hm, ldh, B, Hd, w, b0,
-                     target, pred, dy, loss_sum, dy_scale);
+  const int lpr = lanes_per_row(Hd);
+  const int rpb = 256 / lpr;
+  int grid = (B + rpb - 1) / rpb;
+  if (grid > 1024) grid = 1024;
+#define HEAD_FWD(L)                                                                              \
+  hipLaunchKernelGGL(head_fwd_kernel<L>, dim3(grid), dim3(256), 0, s, Hm, ldh, B, Hd, w, b0, target, \
+                     pred, dy, loss_sum, dy_scale)
+  switch (lpr) {
+    case 1: HEAD_FWD(1); break;
+    case 2: HEAD_FWD(2); break;
+    case 4: HEAD_FWD(4); break;
+    case 8: HEAD_FWD(8); break;
+    case 16: HEAD_FWD(16); break;
+    case 32: HEAD_FWD(32); break;
+    default: HEAD_FWD(64); break;
+  }
+#undef HEAD_FWD
 }
 
-// dw[u] += sum_b dy[b] h[b][u]; db += sum_b dy[b]. grid = (ceil(Hd/256), splits over b).
+// Column-chunk x row-group layout shared by the two head backward kernels: a thread owns
+// 8 consecutive units (16-B loads/stores) of rows rg, rg + RG, ...; partial column sums
+// are combined through LDS and leave the block with one atomic per column.
+struct HeadBwdGeom {
+  int cth;  // column threads = ceil(Hd / 8)
+  int rg;   // row groups per block = 256 / cth
+};
+
+__device__ __forceinline__ void colsum_block_atomic(float (&acc)[8], int cth, int c, int r, int RG,
+                                                    int Hd, float* __restrict__ out, float* lds) {
+  // lds: [RG][cth*8] floats; threads beyond the RG x cth grid own no slot
+  if (r < RG) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) lds[r * cth * 8 + c * 8 + e] = acc[e];
+  }
+  __syncthreads();
+  for (int col = threadIdx.x; col < cth * 8; col += 256) {
+    float t = 0.f;
+    for (int q = 0; q < RG; ++q) t += lds[q * cth * 8 + col];
+    if (col < Hd) atomicAdd(out + col, t);
+  }
+}
+
+// dw[u] += sum_b dy[b] h[b][u]; db += sum_b dy[b]
 __global__ __launch_bounds__(256) void head_bwd_w_kernel(const bf16_t* __restrict__ Hm, long ldh,
                                                          int B, int Hd, const float* __restrict__ dy,
                                                          float* __restrict__ dw,
-                                                         float* __restrict__ db, int rows_per) {
+                                                         float* __restrict__ db, HeadBwdGeom g) {
+  __shared__ float lds[256 * 8];
   __shared__ float red[4];
-  const int u = blockIdx.x * 256 + threadIdx.x;
-  const int b0 = blockIdx.y * rows_per;
-  const int b1 = min(B, b0 + rows_per);
-  float acc = 0.f, dsum = 0.f;
-  for (int b = b0; b < b1; ++b) {
-    const float g = dy[b];
-    dsum += g;
-    if (u < Hd) acc += g * bf2f(Hm[(size_t)b * ldh + u]);
+  const int c = threadIdx.x % g.cth, r = threadIdx.x / g.cth;
+  const bool active = r < g.rg && c * 8 < Hd;
+  float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  float dsum = 0.f;
+  if (active) {
+    for (int b = blockIdx.x * g.rg + r; b < B; b += gridDim.x * g.rg) {
+      const float gy = dy[b];
+      if (c == 0) dsum += gy;
+      const bf16x8 v = *reinterpret_cast<const bf16x8*>(Hm + (size_t)b * ldh + c * 8);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) acc[e] += gy * bf2f((bf16_t)v[e]);
+    }
   }
-  if (u < Hd) atomicAdd(dw + u, acc);
-  if (blockIdx.x == 0 && threadIdx.x == 0 && db != nullptr) atomicAdd(db, dsum);
-  (void)red;
+  colsum_block_atomic(acc, g.cth, c, r, g.rg, Hd, dw, lds);
+  if (db != nullptr) {
+    const float t = block_sum<256>(dsum, red);
+    if (threadIdx.x == 0) atomicAdd(db, t);
+  }
+}
+
+static HeadBwdGeom head_geom(int Hd) {
+  HeadBwdGeom g;
+  g.cth = (Hd + 7) / 8;
+  if (g.cth > 256) g.cth = 256;  // Hd <= 2048 supported
+  g.rg = 256 / g.cth;
+  return g;
 }
 
 void launch_head_bwd_w(const bf16_t* Hm, long ldh, int B, int Hd, const float* dy, float* dw,
                        float* db, hipStream_t s) {
-  const int gx = (Hd + 255) / 256;
-  int splits = (512 + gx - 1) / gx;
-  if (splits > B) splits = B > 0 ? B : 1;
-  const int rows_per = (B + splits - 1) / splits;
-  splits = (B + rows_per - 1) / rows_per;
-  hipLaunchKernelGGL(head_bwd_w_kernel, dim3(gx, splits), dim3(256), 0, s, Hm, ldh, B, Hd, dy, dw,
-                     db, rows_per);
+  const HeadBwdGeom g = head_geom(Hd);
+  int grid = (B + g.rg - 1) / g.rg;
+  if (grid > 512) grid = 512;
+  hipLaunchKernelGGL(head_bwd_w_kernel, dim3(grid), dim3(256), 0, s, Hm, ldh, B, Hd, dy, dw, db, g);
 }
 
-// dz[b][u] = dy[b] * w[u] (* [h>0]); colsum[u] += sum_b dz. One block per 8 rows x 256 units.
+// dz[b][u] = dy[b] * w[u] (* [h>0]); colsum[u] += sum_b dz   (16-B vector rows)
 __global__ __launch_bounds__(256) void head_bwd_x_kernel(const bf16_t* __restrict__ Hm, long ldh,
                                                          int B, int Hd, const float* __restrict__ dy,
                                                          const float* __restrict__ w, int relu_mask,
                                                          bf16_t* __restrict__ dz, long ldz,
-                                                         float* __restrict__ colsum, int rows_per) {
-  const int u = blockIdx.x * 256 + threadIdx.x;
-  if (u >= Hd) return;
-  const int b0 = blockIdx.y * rows_per, b1 = min(B, b0 + rows_per);
-  const float wu = w[u];
-  float cs = 0.f;
-  for (int b = b0; b < b1; ++b) {
-    float v = dy[b] * wu;
-    if (relu_mask && bf2f(Hm[(size_t)b * ldh + u]) <= 0.f) v = 0.f;
-    const bf16_t vb = f2bf(v);
-    dz[(size_t)b * ldz + u] = vb;
-    cs += bf2f(vb);
+                                                         float* __restrict__ colsum, HeadBwdGeom g) {
+  __shared__ float lds[256 * 8];
+  const int c = threadIdx.x % g.cth, r = threadIdx.x / g.cth;
+  const bool active = r < g.rg && c * 8 < Hd;
+  float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  if (active) {
+    float wv[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) wv[e] = w[c * 8 + e];
+    for (int b = blockIdx.x * g.rg + r; b < B; b += gridDim.x * g.rg) {
+      const float gy = dy[b];
+      bf16x8 hv;
+      if (relu_mask) hv = *reinterpret_cast<const bf16x8*>(Hm + (size_t)b * ldh + c * 8);
+      bf16x8 out;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        float v = gy * wv[e];
+        if (relu_mask && bf2f((bf16_t)hv[e]) <= 0.f) v = 0.f;
+        const bf16_t vb = f2bf(v);
+        out[e] = (short)vb;
+        acc[e] += bf2f(vb);
+      }
+      *reinterpret_cast<bf16x8*>(dz + (size_t)b * ldz + c * 8) = out;
+    }
   }
-  if (colsum != nullptr) atomicAdd(colsum + u, cs);
+  if (colsum != nullptr) colsum_block_atomic(acc, g.cth, c, r, g.rg, Hd, colsum, lds);
 }
 
 void launch_head_bwd_x(const bf16_t* Hm, long ldh, int B, int Hd, const float* dy, const float* w,
                        int relu_mask, bf16_t* dz, long ldz, float* colsum, hipStream_t s) {
-  const int gx = (Hd + 255) / 256;
-  int splits = (1024 + gx - 1) / gx;
-  if (splits > B) splits = B > 0 ? B : 1;
-  const int rows_per = (B + splits - 1) / splits;
-  splits = (B + rows_per - 1) / rows_per;
-  hipLaunchKernelGGL(head_bwd_x_kernel, dim3(gx, splits), dim3(256), 0, s, Hm, ldh, B, Hd, dy, w,
-                     relu_mask, dz, ldz, colsum, rows_per);
+  const HeadBwdGeom g = head_geom(Hd);
+  int grid = (B + g.rg - 1) / g.rg;
+  if (grid > 1024) grid = 1024;
+  hipLaunchKernelGGL(head_bwd_x_kernel, dim3(grid), dim3(256), 0, s, Hm, ldh, B, Hd, dy, w,
+                     relu_mask, dz, ldz, colsum, g);
 }
 
 // ---------------------------------------------------------------- multi-output losses

@@ -40,6 +40,69 @@ __global__ __launch_bounds__(256) void gemm_kernel(const bf16_t* __restrict__ A,
     gemm_mainloop<C>(A, lda, M, B, ldb, N, kbeg, kend, m0, n0, smem, acc);
 
   const AccCoord<C> cc(m0, n0);
+
+  // Staged bf16 epilogue: the ReLU-mask tile is read and the bf16 output tile written
+  // through LDS ([BM][BN] bf16 each, 16-B chunks XOR-swizzled by row) so global traffic is
+  // whole 16-B-per-lane row segments instead of 2-B scattered accesses.
+  static_assert(2 * BM * BN * 2 <= LDSB, "staging tiles must fit the mainloop LDS");
+  const bool staged = e.stage_ok && e.outH != nullptr && e.outF == nullptr && !e.atomic;
+  if (staged) {
+    constexpr int CPR = BN / 8;  // 16-B chunks per tile row
+    bf16_t* mt = reinterpret_cast<bf16_t*>(smem);
+    bf16_t* ot = reinterpret_cast<bf16_t*>(smem + BM * BN * 2);
+    auto chunk_off = [&](int row, int c8) { return row * BN + ((c8 ^ (row & (CPR - 1))) << 3); };
+    if (e.mask != nullptr) {
+      for (int q = threadIdx.x; q < BM * CPR; q += C::NT) {
+        const int row = q / CPR, c8 = q % CPR;
+        const int m = m0 + row, n = n0 + c8 * 8;
+        uint4 v = make_uint4(0u, 0u, 0u, 0u);
+        if (m < M && n < N) v = *reinterpret_cast<const uint4*>(e.mask + (size_t)m * e.ldm + n);
+        *reinterpret_cast<uint4*>(mt + chunk_off(row, c8)) = v;
+      }
+      __syncthreads();
+    }
+#pragma unroll
+    for (int j = 0; j < C::TN; ++j) {
+      const int n = cc.col(j);
+      const int col = n - n0;
+      const bool nok = n < N;
+      const float bn = (e.bias != nullptr && nok) ? e.bias[n] : 0.f;
+      float csum = 0.f;
+#pragma unroll
+      for (int i = 0; i < C::TM; ++i) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int m = cc.row(i, r);
+          const int row = m - m0;
+          const int lo = chunk_off(row, col >> 3) + (col & 7);
+          float v = e.alpha * acc[i][j][r] + bn;
+          if (e.act == 1) v = fmaxf(v, 0.f);
+          if (e.drop_p > 0.f)
+            v = uniform_hash(e.seed, (unsigned long long)m * N + n) >= e.drop_p
+                    ? v * (1.f / (1.f - e.drop_p)) : 0.f;
+          if (e.mask != nullptr) v = bf2f(mt[lo]) > 0.f ? v * e.mask_scale : 0.f;
+          const bf16_t vb = f2bf(v);
+          ot[lo] = vb;
+          if (nok && m < M) csum += bf2f(vb);
+        }
+      }
+      if (e.colsum != nullptr) {
+        csum += __shfl_xor(csum, 16, 64);
+        csum += __shfl_xor(csum, 32, 64);
+        if ((threadIdx.x & 63) < 16 && nok) atomicAdd(e.colsum + n, csum);
+      }
+    }
+    __syncthreads();
+    for (int q = threadIdx.x; q < BM * CPR; q += C::NT) {
+      const int row = q / CPR, c8 = q % CPR;
+      const int m = m0 + row, n = n0 + c8 * 8;
+      if (m < M && n < N)
+        *reinterpret_cast<uint4*>(e.outH + (size_t)m * e.ldo + n) =
+            *reinterpret_cast<const uint4*>(ot + chunk_off(row, c8));
+    }
+    return;
+  }
+
 #pragma unroll
   for (int j = 0; j < C::TN; ++j) {
     const int n = cc.col(j);

@@ -22,6 +22,7 @@ struct GemmEpilogue {
   int atomic = 0;                // split-K: atomicAdd alpha*acc into outF
   float drop_p = 0.f;            // inverted dropout after the activation
   unsigned long long seed = 0;
+  int stage_ok = 0;              // host-verified: bf16 output/mask tiles may go through LDS
 };
 
 void launch_gemm(const bf16_t* A, long lda, int a_mn, const bf16_t* B, long ldb, int b_mn, int M,

@@ -33,25 +33,35 @@ __device__ __forceinline__ size_t fn_block(int mrow0, int u, int H) {
   return (size_t)(mrow0 >> 4) * (H >> 4) + (u >> 4);
 }
 
-// XH[t][b][0:KX] = [x[b][t][0:F], 1, 0, ...]; one thread per (t, b, k).
+// XH[t][b][0:KX] = [x[b][t][0:F], 1, 0, ...]. One thread per (b, t) row with t fastest:
+// the F-float reads of neighbouring threads are contiguous and each thread writes whole
+// 16-B chunks (KX*2 bytes = full 128-B lines for KX = 64).
 __global__ void lstm_pack_x_kernel(const float* __restrict__ x, bf16_t* __restrict__ XH,
                                    LstmDims d) {
   const int KA = d.KX + d.H;
-  const long total = (long)d.T * d.B * d.KX;
+  const long total = (long)d.T * d.B;
   for (long idx = blockIdx.x * (long)blockDim.x + threadIdx.x; idx < total;
        idx += (long)gridDim.x * blockDim.x) {
-    const int k = idx % d.KX;
-    const long tb = idx / d.KX;
-    const int b = tb % d.B, t = tb / d.B;
-    float v = 0.f;
-    if (k < d.F) v = x[((long)b * d.T + t) * d.F + k];
-    else if (k == d.F) v = 1.f;
-    XH[((long)t * d.B + b) * KA + k] = f2bf(v);
+    const int t = idx % d.T;
+    const long b = idx / d.T;
+    const float* src = x + (b * d.T + t) * d.F;
+    bf16_t* dst = XH + ((long)t * d.B + b) * KA;
+    for (int c = 0; c < d.KX; c += 8) {
+      unsigned pk[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int k0 = c + 2 * e, k1 = k0 + 1;
+        const float v0 = k0 < d.F ? src[k0] : (k0 == d.F ? 1.f : 0.f);
+        const float v1 = k1 < d.F ? src[k1] : (k1 == d.F ? 1.f : 0.f);
+        pk[e] = (unsigned)f2bf(v0) | ((unsigned)f2bf(v1) << 16);
+      }
+      *reinterpret_cast<uint4*>(dst + c) = make_uint4(pk[0], pk[1], pk[2], pk[3]);
+    }
   }
 }
 
 void launch_lstm_pack_x(const float* x, bf16_t* XH, LstmDims d, hipStream_t s) {
-  const long total = (long)d.T * d.B * d.KX;
+  const long total = (long)d.T * d.B;
   int blocks = (int)((total + 255) / 256);
   if (blocks > 8192) blocks = 8192;
   hipLaunchKernelGGL(lstm_pack_x_kernel, dim3(blocks), dim3(256), 0, s, x, XH, d);
