@@ -95,14 +95,42 @@ def bench_mlp(args, ctx, online: bool):
 
     if online:
         pool = HostPool(lambda k: synth_tabular_batch(B, F, seed=1000 * ctx.rank + k), n=8)
-        streamer = DeviceStreamer(pool, ctx.device, depth=3)
+        depth = 3
+        streamer = DeviceStreamer(pool, ctx.device, depth=depth)
+        for _ in range(depth):  # allocate every ring slot
+            streamer.next()
+        torch.cuda.synchronize()
+        graphs = {}
+        if not args.no_graph:
+            # one captured compute graph per ring slot (it reads that slot's buffers)
+            s = torch.cuda.Stream(device=ctx.device)
+            s.wait_stream(torch.cuda.current_stream(ctx.device))
+            with torch.cuda.stream(s):
+                for _ in range(2):
+                    eng.forward_backward(streamer.slots[0][0], streamer.slots[0][1], gscale)
+            torch.cuda.current_stream(ctx.device).wait_stream(s)
+            for k in range(depth):
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g):
+                    eng.forward_backward(streamer.slots[k][0], streamer.slots[k][1], gscale)
+                graphs[k] = g
+            gu = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(gu):
+                opt.step()
+                eng.sync_weights()
+            graphs["update"] = gu
 
         def step():
             xb, yb = streamer.next()
-            eng.forward_backward(xb, yb, gscale)
-            ctx.all_reduce_sum_(eng.grads)
-            opt.step()
-            eng.sync_weights()
+            if graphs:
+                graphs[streamer.last_slot].replay()
+                ctx.all_reduce_sum_(eng.grads)
+                graphs["update"].replay()
+            else:
+                eng.forward_backward(xb, yb, gscale)
+                ctx.all_reduce_sum_(eng.grads)
+                opt.step()
+                eng.sync_weights()
     else:
         x, y = synth_tabular_batch(B, F, seed=ctx.rank)
         x, y = x.to(ctx.device), y.to(ctx.device)

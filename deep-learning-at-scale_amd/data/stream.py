@@ -64,6 +64,7 @@ class DeviceStreamer:
                 self._issue()
             self._primed = True
         self._issue()  # keep depth-1 batches in flight
-        xd, yd, ev = self.slots[(self.k - self.depth) % self.depth]
+        self.last_slot = (self.k - self.depth) % self.depth
+        xd, yd, ev = self.slots[self.last_slot]
         torch.cuda.current_stream(self.device).wait_event(ev)
         return xd, yd

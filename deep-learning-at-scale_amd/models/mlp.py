@@ -200,11 +200,14 @@ class NativeMLP:
                    self.dy, None)
         C.head_bwd_w(self.Hs[-1], H, B, H, self.dy, ghw, ghb)
         C.head_bwd_x(self.Hs[-1], H, B, H, self.dy, hw, True, self.dZ[-1], H, gl[-1][1])
-        ksplit = max(1, min(32, B // 1024))
+        # dW GEMMs have tiny M x N (a few 128x128 tiles) and K = batch: split K so the
+        # grid has ~512 workgroups, each reducing >= 256 rows
+        tiles = lambda h, k: ((h + 127) // 128) * ((k + 127) // 128)  # noqa: E731
         for l in range(L - 1, -1, -1):
             h, k = self.lay.dims[l]
             prevH = self.Hs[l - 1] if l > 0 else self.X
             # dW_l = dZ_l^T H_{l-1}   (reduce over the batch; MN-contiguous operands)
+            ksplit = max(1, min(512 // tiles(h, k), B // 256))
             gemm(self.dZ[l], prevH, h, k, B, a_mn=True, lda=h, b_mn=True, ldb=k,
                  outF=gl[l][0], atomic=True, ksplit=ksplit)
             if l > 0:
