@@ -72,7 +72,7 @@ void launch_head_fwd(const bf16_t* Hm, long ldh, int B, int Hd, const float* w, 
   const int lpr = lanes_per_row(Hd);
   const int rpb = 256 / lpr;
   int grid = (B + rpb - 1) / rpb;
-  if (grid > 16384) grid = 16384;
+  if (grid > 2048) grid = 2048;  // one same-address loss atomic per block
 #define HEAD_FWD(L)                                                                              \
   hipLaunchKernelGGL(head_fwd_kernel<L>, dim3(grid), dim3(256), 0, s, Hm, ldh, B, Hd, w, b0, target, \
                      pred, dy, loss_sum, dy_scale)
