@@ -191,7 +191,7 @@ void launch_head_bwd_x(const bf16_t* Hm, long ldh, int B, int Hd, const float* d
                        int relu_mask, bf16_t* dz, long ldz, float* colsum, hipStream_t s) {
   const HeadBwdGeom g = head_geom(Hd);
   int grid = (B + g.rg - 1) / g.rg;
-  if (grid > 8192) grid = 8192;
+  if (grid > 1024) grid = 1024;  // bounds same-column atomic contention (colsum)
   hipLaunchKernelGGL(head_bwd_x_kernel, dim3(grid), dim3(256), 0, s, Hm, ldh, B, Hd, dy, w,
                      relu_mask, dz, ldz, colsum, g);
 }

@@ -208,7 +208,7 @@ class NativeMLP:
             prevH = self.Hs[l - 1] if l > 0 else self.X
             # dW_l = dZ_l^T H_{l-1}   (reduce over the batch; MN-contiguous operands)
             # ... but keep the fp32 atomic traffic (ksplit x h x k x 4 B) <= ~8 MB
-            ksplit = max(1, min(512 // tiles(h, k), B // 256, (8 << 20) // (4 * h * k)))
+            ksplit = max(1, min(512 // tiles(h, k), B // 256, 64, (8 << 20) // (4 * h * k)))
             gemm(self.dZ[l], prevH, h, k, B, a_mn=True, lda=h, b_mn=True, ldb=k,
                  outF=gl[l][0], atomic=True, ksplit=ksplit)
             if l > 0:
