@@ -120,6 +120,8 @@ wf::LstmDims lstm_dims(int64_t B, int64_t T, int64_t F, int64_t KX, int64_t H) {
   TORCH_CHECK(KX % 64 == 0 && F + 1 <= KX, "lstm: KX must be a multiple of 64 and > F");
   wf::LstmDims d;
   d.B = (int)B; d.T = (int)T; d.F = (int)F; d.KX = (int)KX; d.H = (int)H;
+  const char* xm = std::getenv("WELLFLOW_XCD_MAP");  // diagnostics: 0 = identity tile order
+  d.xcd_map = (xm != nullptr && xm[0] == '0') ? 0 : 1;
   return d;
 }
 

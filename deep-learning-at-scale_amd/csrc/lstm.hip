@@ -80,7 +80,7 @@ __global__ __launch_bounds__(64 * WM * WN) void lstm_fwd_step_kernel(int t, bf16
   __shared__ __attribute__((aligned(16))) char smem[LDSB];
   const int KA = d.KX + d.H, G = 4 * d.H;
   const int tiles_n = G / C::BN;
-  const int L = xcd_remap(blockIdx.x, gridDim.x);
+  const int L = d.xcd_map ? xcd_remap(blockIdx.x, gridDim.x) : (int)blockIdx.x;
   const int m0 = (L / tiles_n) * C::BM, n0 = (L % tiles_n) * C::BN;
   const bf16_t* A = XH + (size_t)t * d.B * KA;
 
@@ -233,7 +233,7 @@ __global__ __launch_bounds__(64 * WM * WN) void lstm_bwd_step_kernel(int t, cons
   __shared__ __attribute__((aligned(16))) char smem[LDSB];
   const int G = 4 * d.H;
   const int tiles_n = d.H / C::BN;
-  const int L = xcd_remap(blockIdx.x, gridDim.x);
+  const int L = d.xcd_map ? xcd_remap(blockIdx.x, gridDim.x) : (int)blockIdx.x;
   const int m0 = (L / tiles_n) * C::BM, n0 = (L % tiles_n) * C::BN;
   const bf16_t* A = DG + (size_t)(t + 1) * d.B * G;
 
