@@ -122,6 +122,8 @@ wf::LstmDims lstm_dims(int64_t B, int64_t T, int64_t F, int64_t KX, int64_t H) {
   d.B = (int)B; d.T = (int)T; d.F = (int)F; d.KX = (int)KX; d.H = (int)H;
   const char* xm = std::getenv("WELLFLOW_XCD_MAP");  // diagnostics: 0 = identity tile order
   d.xcd_map = (xm != nullptr && xm[0] == '0') ? 0 : 1;
+  const char* nt = std::getenv("WELLFLOW_NT");
+  d.nt = (nt != nullptr && nt[0] == '0') ? 0 : 1;
   return d;
 }
 

@@ -35,6 +35,7 @@ struct LstmDims {
   int fwd_variant = 0;  // tile shape of the forward step GEMM (0: 128x128, 1: 64x128, 2: 256x128)
   int bwd_variant = 0;  // backward step GEMM (0: 128x128, 1: 64x128, 2: 128x64, 3: 64x64)
   int xcd_map = 1;      // 1: XCD-aware tile remap (default), 0: identity (diagnostics)
+  int nt = 1;           // non-temporal hints on the read-once/write-once state streams
 };
 void launch_lstm_pack_x(const float* x, bf16_t* XH, LstmDims d, hipStream_t s);
 void launch_lstm_fwd_step(int t, bf16_t* XH, const bf16_t* Wp, float* Cst, bf16_t* S,

@@ -29,6 +29,21 @@ __device__ __forceinline__ int gate_col(int gate, int u) { return (u >> 4) * 64 
 // where the 16x16 MFMA C map puts it, so every lane moves 16-32 contiguous bytes.
 // Batch rows are padded to a multiple of 16 (fn_rows).
 __host__ __device__ __forceinline__ int fn_rows(int B) { return (B + 15) & ~15; }
+
+// Non-temporal 16-B accesses for the read-once / write-once streams (saved gates S, the
+// cell-state history as read by the backward): they should not evict the operands the
+// step GEMMs reuse through L2 (recurrent weights, the previous step's activations).
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ uint4 ld16(const void* p, int nt) {
+  u32x4 v = nt ? __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p))
+               : *reinterpret_cast<const u32x4*>(p);
+  return make_uint4(v[0], v[1], v[2], v[3]);
+}
+__device__ __forceinline__ void st16(void* p, uint4 v, int nt) {
+  const u32x4 w = {v.x, v.y, v.z, v.w};
+  if (nt) __builtin_nontemporal_store(w, reinterpret_cast<u32x4*>(p));
+  else *reinterpret_cast<u32x4*>(p) = w;
+}
 __device__ __forceinline__ size_t fn_block(int mrow0, int u, int H) {
   return (size_t)(mrow0 >> 4) * (H >> 4) + (u >> 4);
 }
@@ -123,8 +138,8 @@ __global__ __launch_bounds__(64 * WM * WN) void lstm_fwd_step_kernel(int t, bf16
     }
     *reinterpret_cast<float4*>(cnext + blk * 256 + lane * 4) = make_float4(cv[0], cv[1], cv[2], cv[3]);
     uint4* sp = reinterpret_cast<uint4*>(St + blk * 1024 + lane * 16);
-    sp[0] = make_uint4(pk[0], pk[1], pk[2], pk[3]);
-    sp[1] = make_uint4(pk[4], pk[5], pk[6], pk[7]);
+    st16(sp, make_uint4(pk[0], pk[1], pk[2], pk[3]), d.nt);
+    st16(sp + 1, make_uint4(pk[4], pk[5], pk[6], pk[7]), d.nt);
   }
 }
 
@@ -169,10 +184,14 @@ __device__ __forceinline__ void cell_bwd4(int t, int mrow0, int u, int lane, con
   const int G = 4 * d.H, Bp = fn_rows(d.B);
   const size_t blk = fn_block(mrow0, u, d.H);
   const uint4* sp = reinterpret_cast<const uint4*>(S + (size_t)t * Bp * G + blk * 1024 + lane * 16);
-  const uint4 s0 = sp[0], s1 = sp[1];
+  const uint4 s0 = ld16(sp, d.nt), s1 = ld16(sp + 1, d.nt);
   const unsigned pk[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
-  const float4 c4 = *reinterpret_cast<const float4*>(Cst + (size_t)(t + 1) * Bp * d.H + blk * 256 + lane * 4);
-  const float4 p4 = *reinterpret_cast<const float4*>(Cst + (size_t)t * Bp * d.H + blk * 256 + lane * 4);
+  const uint4 c4u = ld16(Cst + (size_t)(t + 1) * Bp * d.H + blk * 256 + lane * 4, d.nt);
+  const uint4 p4u = ld16(Cst + (size_t)t * Bp * d.H + blk * 256 + lane * 4, d.nt);
+  const float4 c4 = make_float4(__uint_as_float(c4u.x), __uint_as_float(c4u.y), __uint_as_float(c4u.z),
+                                __uint_as_float(c4u.w));
+  const float4 p4 = make_float4(__uint_as_float(p4u.x), __uint_as_float(p4u.y), __uint_as_float(p4u.z),
+                                __uint_as_float(p4u.w));
   float4* dcp = reinterpret_cast<float4*>(dcarry + blk * 256 + lane * 4);
   const float4 k4 = *dcp;
   const float cv[4] = {c4.x, c4.y, c4.z, c4.w}, pv[4] = {p4.x, p4.y, p4.z, p4.w};
