@@ -251,6 +251,11 @@ void lstm_backward_dw(const at::Tensor& WhhT, const at::Tensor& XH, const at::Te
     e.outF = fp(gW);
     e.ldo = KA;
     e.atomic = 1;
+    static const bool big = [] {
+      const char* v = std::getenv("WELLFLOW_DW_BIG");
+      return v == nullptr || v[0] != '0';
+    }();
+    e.big_tile = big ? 1 : 0;
     const bf16_t* A = bfp(DG) + (size_t)t0 * B * G;
     const bf16_t* Bm = bfp(XH) + (size_t)t0 * B * KA;
     // whole-tile over-read of XH columns 576..639 stays inside XH (its slab T follows)

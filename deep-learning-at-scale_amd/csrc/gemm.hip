@@ -17,12 +17,12 @@ namespace wf {
 // multiple of 64 and the whole-tile over-read past M / N stays inside the operand
 // allocations (binding.cpp computes that from the tensor sizes); results outside M x N
 // are discarded by the epilogue as in the register path.
-template <int BM, int BN, int LA, int LB, int STAGES>
-__global__ __launch_bounds__(256) void gemm_kernel(const bf16_t* __restrict__ A, long lda,
+template <int BM, int BN, int LA, int LB, int STAGES, int WM = 2, int WN = 2>
+__global__ __launch_bounds__(64 * WM * WN) void gemm_kernel(const bf16_t* __restrict__ A, long lda,
                                                    const bf16_t* __restrict__ B, long ldb,
                                                    int M, int N, int K, int kchunk,
                                                    GemmEpilogue e) {
-  using C = GemmCfg<BM, BN, LA, LB>;
+  using C = GemmCfg<BM, BN, LA, LB, WM, WN>;
   constexpr int LDSB = STAGES * C::STAGE > C::LDS_BYTES ? STAGES * C::STAGE : C::LDS_BYTES;
   __shared__ __attribute__((aligned(16))) char smem[LDSB];
   const int tiles_n = (N + BN - 1) / BN;
@@ -160,8 +160,25 @@ static void launch_cfg(const bf16_t* A, long lda, const bf16_t* B, long ldb, int
                        N, K, kchunk, e);
 }
 
+// Big-tile configuration for the MN x MN weight-gradient GEMMs (dW = dZ^T X over a huge
+// batch/time K): 256x128 tile, 8 waves, 3-stage glds ring (144 KiB): 87 FLOP per staged
+// byte instead of 64 for 128x128.
+static void launch_dw_big(const bf16_t* A, long lda, const bf16_t* B, long ldb, int M, int N, int K,
+                          int ksplit, const GemmEpilogue& e, hipStream_t s) {
+  constexpr int BM = 256, BN = 128;
+  const int tiles = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
+  int kchunk = ((K + ksplit - 1) / ksplit + 63) / 64 * 64;
+  const int nsplit = (K + kchunk - 1) / kchunk;
+  hipLaunchKernelGGL((gemm_kernel<BM, BN, MN_CONTIG, MN_CONTIG, 3, 4, 2>), dim3(tiles * nsplit),
+                     dim3(512), 0, s, A, lda, B, ldb, M, N, K, kchunk, e);
+}
+
 void launch_gemm(const bf16_t* A, long lda, int a_mn, const bf16_t* B, long ldb, int b_mn, int M,
                  int N, int K, int ksplit, const GemmEpilogue& e, hipStream_t s, bool glds_ok) {
+  if (a_mn && b_mn && glds_ok && e.atomic && e.big_tile && M % 256 == 0 && K % 64 == 0) {
+    launch_dw_big(A, lda, B, ldb, M, N, K, ksplit < 1 ? 1 : ksplit, e, s);
+    return;
+  }
   if (!a_mn && !b_mn)
     launch_cfg<128, 128, K_CONTIG, K_CONTIG>(A, lda, B, ldb, M, N, K, ksplit, e, s, glds_ok);
   else if (!a_mn && b_mn)

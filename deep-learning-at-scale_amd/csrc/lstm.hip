@@ -316,6 +316,8 @@ void launch_lstm_bwd_step(int t, const bf16_t* WhhT, const float* Cst, const bf1
     case 13: bwd_cfg<128, 128, 2, 4, 4>(t, WhhT, Cst, S, DG, dcarry, d, s); break; // 8w 4st 128K
     case 14: bwd_cfg<64, 128, 2, 2, 4>(t, WhhT, Cst, S, DG, dcarry, d, s); break;  // 4st 96K
     case 15: bwd_cfg<128, 64, 2, 2, 4>(t, WhhT, Cst, S, DG, dcarry, d, s); break;  // 4st 96K
+    case 16: bwd_cfg<128, 128, 4, 4, 3>(t, WhhT, Cst, S, DG, dcarry, d, s); break; // 16 waves
+    case 17: bwd_cfg<128, 128, 4, 4, 4>(t, WhhT, Cst, S, DG, dcarry, d, s); break; // 16w 4st
     default: bwd_cfg<128, 128>(t, WhhT, Cst, S, DG, dcarry, d, s); break;
   }
 }
