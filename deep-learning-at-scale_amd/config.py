@@ -73,6 +73,7 @@ class RunConfig:
     max_steps: int = 0           # 0 = no cap (tests / smoke)
     resume: bool = False
     verbose: int = 2             # Keras verbose=2: one line per epoch (cnn.py:128)
+    metrics_path: str = ""       # JSONL: one record per epoch / chunk (rank 0)
     fail_at_step: int = -1       # fault injection for resume tests (env WELLFLOW_FAIL_AT_STEP)
 
     @property
@@ -135,6 +136,7 @@ def build_parser(model: str) -> argparse.ArgumentParser:
     ap.add_argument("--max-steps", type=int, dest="max_steps")
     ap.add_argument("--resume", action="store_true", default=None)
     ap.add_argument("--verbose", type=int)
+    ap.add_argument("--metrics", dest="metrics_path", help="append per-epoch JSON lines here")
     return ap
 
 
@@ -155,4 +157,7 @@ def parse_argv(model: str, argv) -> RunConfig:
     env_fail = os.environ.get("WELLFLOW_FAIL_AT_STEP")
     if env_fail is not None:
         cfg.fail_at_step = int(env_fail)
+    # elastic restarts (torchrun --max-restarts): a restarted worker resumes from .ckpt
+    if int(os.environ.get("TORCHELASTIC_RESTART_COUNT", "0")) > 0:
+        cfg.resume = True
     return cfg

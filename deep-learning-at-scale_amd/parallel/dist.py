@@ -25,6 +25,13 @@ import torch
 import torch.distributed as dist
 
 
+def _base_store(rank: int, world: int, timeout_s: float):
+    """Client (or, outside the elastic agent, rank-0 server) of the MASTER_* TCP store."""
+    from torch.distributed.rendezvous import _create_c10d_store
+    return _create_c10d_store(os.environ["MASTER_ADDR"], int(os.environ["MASTER_PORT"]), rank, world,
+                              datetime.timedelta(seconds=timeout_s))
+
+
 class DistContext:
     def __init__(self, rank: int = 0, world_size: int = 1, local_rank: int = 0,
                  device: torch.device | None = None, backend: str | None = None,
@@ -61,6 +68,12 @@ class DistContext:
                       timeout=datetime.timedelta(seconds=timeout_s))
             if backend == "nccl":
                 kw["device_id"] = dev
+            restart = os.environ.get("TORCHELASTIC_RESTART_COUNT")
+            if restart is not None and "MASTER_PORT" in os.environ:
+                # static rendezvous (--master-addr/--master-port) keeps ONE agent store across
+                # torchrun restarts, so a restarted group would read the dead attempt's
+                # transport addresses. Namespace every attempt's keys.
+                kw["store"] = dist.PrefixStore(f"wellflow/attempt_{restart}", _base_store(rank, world, timeout_s))
             dist.init_process_group(**kw)
         return cls(rank, world, local, dev, backend, bucket_bytes)
 

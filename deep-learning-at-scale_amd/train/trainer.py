@@ -20,6 +20,7 @@ early-stop decision (C3), rank-0 checkpoint writes fenced by barriers (C4), a re
 from __future__ import annotations
 
 import dataclasses
+import json
 import math
 import os
 import time
@@ -29,6 +30,7 @@ import torch
 
 from ..models.base import per_element_loss
 from ..utils import checkpoint as ckpt
+from ..utils.profiling import trace_range
 
 
 class InjectedFault(RuntimeError):
@@ -150,6 +152,31 @@ class Trainer:
             ckpt.save_state(self.cfg.ckpt_path(self.name), self.state_dict())
         self.ctx.barrier()
 
+    # ------------------------------------------------------------------ faults / metrics
+    def _inject_fault(self) -> None:
+        """Fail ONCE per (storage path, model, rank): a marker file makes the restarted
+        process (torchrun --max-restarts, or a manual --resume) run through."""
+        d = self.cfg.model_dir
+        os.makedirs(d, exist_ok=True)
+        marker = os.path.join(d, f".fault_injected_{self.name}_r{self.ctx.rank}")
+        if os.path.exists(marker):
+            return
+        with open(marker, "w") as f:
+            f.write(str(self.global_step))
+        raise InjectedFault(f"injected fault at step {self.global_step}")
+
+    def _log_metrics(self) -> None:
+        path = getattr(self.cfg, "metrics_path", "")
+        if not path or not self.ctx.is_main:
+            return
+        h = self.history
+        rec = {"epoch": self.epoch, "global_step": self.global_step, "loss": h.loss[-1],
+               "val_loss": h.val_loss[-1], "val_mse": h.val_mse[-1], "rows_per_s": h.rows_per_s[-1],
+               "epoch_time_s": h.epoch_time[-1], "world_size": self.ctx.world_size,
+               "time": time.time()}
+        with open(path, "a") as f:
+            f.write(json.dumps(rec) + "\n")
+
     # ------------------------------------------------------------------ fit
     def train_steps(self, Xd, Yd, order: torch.Tensor, b: int):
         """One pass over ``order`` (device index tensor of this rank) in batches of ``b``."""
@@ -169,7 +196,7 @@ class Trainer:
             eng.sync_weights()
             self.global_step += 1
             if cfg.fail_at_step >= 0 and self.global_step == cfg.fail_at_step:
-                raise InjectedFault(f"injected fault at step {self.global_step}")
+                self._inject_fault()
             if cfg.max_steps and self.global_step >= cfg.max_steps:
                 break
         if eng.device.type == "cuda":
@@ -193,8 +220,10 @@ class Trainer:
             perm = np.random.default_rng(cfg.seed + 7919 * self.epoch).permutation(n)
             mine = perm[ctx.rank * per_rank : (ctx.rank + 1) * per_rank]
             order = torch.as_tensor(mine, device=dev)
-            tr_loss, rows, dt = self.train_steps(Xd, Yd, order, b)
-            v_loss, v_mse = self.evaluate(*val)
+            with trace_range("train_epoch", dev):
+                tr_loss, rows, dt = self.train_steps(Xd, Yd, order, b)
+            with trace_range("evaluate", dev):
+                v_loss, v_mse = self.evaluate(*val)
             self.epoch += 1
             h = self.history
             h.loss.append(tr_loss)
@@ -206,14 +235,16 @@ class Trainer:
                 self.log(f"Epoch {self.epoch}/{cfg.epochs} - {h.epoch_time[-1]:.2f}s - loss: {tr_loss:.6f}"
                          f" - val_loss: {v_loss:.6f} - val_mse: {v_mse:.6f} - rows/s: {h.rows_per_s[-1]:.0f}",
                          flush=True)
+            self._log_metrics()
             improved = v_loss < self.stopper.best
             self.stopper.update(v_loss)
-            if improved and self.on_best is not None:
-                ctx.barrier()
-                if ctx.is_main:
-                    self.on_best(self)
-                ctx.barrier()
-            self.save_state()
+            with trace_range("checkpoint", dev):
+                if improved and self.on_best is not None:
+                    ctx.barrier()
+                    if ctx.is_main:
+                        self.on_best(self)
+                    ctx.barrier()
+                self.save_state()
             if cfg.max_steps and self.global_step >= cfg.max_steps:
                 break
         return self.history

@@ -20,7 +20,7 @@ def _free_port():
     return p
 
 
-def _torchrun(tmp_path, body: str, nproc: int, timeout=300):
+def _torchrun(tmp_path, body: str, nproc: int, timeout=300, extra_env=None, max_restarts=0):
     script = tmp_path / "worker.py"
     script.write_text(textwrap.dedent(f"""
         import json, os, sys
@@ -32,8 +32,10 @@ def _torchrun(tmp_path, body: str, nproc: int, timeout=300):
     env = dict(os.environ)
     env["CUDA_VISIBLE_DEVICES"] = ""
     env["OMP_NUM_THREADS"] = "1"
+    env.update(extra_env or {})
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
-           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), str(script)]
+           f"--max-restarts={max_restarts}", "--master-addr", "127.0.0.1", "--master-port",
+           str(_free_port()), str(script)]
     r = subprocess.run(cmd, capture_output=True, text=True, env=env, timeout=timeout, cwd=str(tmp_path))
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     return [json.load(open(tmp_path / f"rank{i}.json")) for i in range(nproc)]
@@ -91,3 +93,27 @@ def test_dp_training_job_agrees_on_early_stop_and_rank0_writes(tmp_path):
     assert res[0]["val"] == res[1]["val"]
     assert abs(res[0]["test"] - res[1]["test"]) < 1e-9
     assert (tmp_path / "store" / "models" / "mlp.mdl").exists()
+
+
+def test_elastic_restart_resumes_from_checkpoint(tmp_path):
+    """torchrun --max-restarts=1: both ranks hit an injected fault once, the group is
+    restarted, the workers see TORCHELASTIC_RESTART_COUNT=1, resume from the .ckpt and
+    finish all epochs; the metrics JSONL holds one record per epoch."""
+    res = _torchrun(tmp_path, """
+        from wellflow.train.job import run_job
+        names = "well,field,t,whp,choke,glr,temp,water_cut,dsp,flow"
+        types = "string,string,int,float,float,float,float,float,float,float"
+        out = run_job("mlp", [names, types, "flow", OUT + "/store", "--epochs", "4",
+                              "--synth-wells", "3", "--synth-steps", "120", "--batch-size", "16",
+                              "--device", "cpu", "--metrics", OUT + "/metrics.jsonl"],
+                      log=lambda *a, **k: None)
+        r = int(os.environ["RANK"])
+        json.dump({"epochs": out["epochs"], "restart": os.environ.get("TORCHELASTIC_RESTART_COUNT")},
+                  open(f"{OUT}/rank{r}.json", "w"))
+    """, 2, extra_env={"WELLFLOW_FAIL_AT_STEP": "10"}, max_restarts=1)
+    assert all(r["epochs"] == 4 for r in res)
+    assert all(r["restart"] == "1" for r in res)
+    assert (tmp_path / "store" / "models" / ".fault_injected_mlp_r0").exists()
+    # 7 steps/epoch: the fault hits epoch 2, the restart resumes after epoch 1 (no replay)
+    recs = [json.loads(l) for l in open(tmp_path / "metrics.jsonl")]
+    assert [r["epoch"] for r in recs] == [1, 2, 3, 4]
