@@ -45,6 +45,40 @@ def _timed(ctx, step, steps, warmup):
     return ctx.max_scalar(time.perf_counter() - t0)
 
 
+def _graph_step(ctx, eng, compute, update, no_graph: bool):
+    """Capture compute (fwd+bwd) and update (Adam + bf16 repack) as two hipGraphs; the RCCL
+    all-reduce between them stays eager. Adam's step counter lives on the device, so a
+    replay is exactly the eager step. Three eager warm-up steps on a side stream first
+    (allocator + lazy init), as torch.cuda.graph requires."""
+    import torch
+
+    if no_graph:
+        def step():
+            compute()
+            ctx.all_reduce_sum_(eng.grads)
+            update()
+        return step
+    s = torch.cuda.Stream(device=ctx.device)
+    s.wait_stream(torch.cuda.current_stream(ctx.device))
+    with torch.cuda.stream(s):
+        for _ in range(3):
+            compute()
+            ctx.all_reduce_sum_(eng.grads)
+            update()
+    torch.cuda.current_stream(ctx.device).wait_stream(s)
+    g1, g2 = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g1):
+        compute()
+    with torch.cuda.graph(g2):
+        update()
+
+    def step():
+        g1.replay()
+        ctx.all_reduce_sum_(eng.grads)
+        g2.replay()
+    return step
+
+
 def bench_lstm(args, ctx):
     from wellflow.data.synth import synth_lstm_batch
     from wellflow.models.lstm import NativeLSTM, init_lstm_flat
@@ -66,11 +100,16 @@ def bench_lstm(args, ctx):
     x, y = x.to(ctx.device), y.to(ctx.device)
     gscale = 1.0 / (B * ctx.world_size)
 
-    def step():
+    def compute():
         eng.forward_backward(x, y, gscale)
-        ctx.all_reduce_sum_(eng.grads)  # C2: one flat bucket over RCCL / xGMI
+
+    def update():
         opt.step()
         eng.sync_weights()
+
+    # the ~135 launches of a step (64 fwd + 64 bwd + dW + head/loss/Adam) replay as one
+    # hipGraph; C2 (one flat RCCL bucket over xGMI) runs between the two graphs
+    step = _graph_step(ctx, eng, compute, update, args.no_graph or eng.dw_chunk > 0)
 
     el = _timed(ctx, step, args.steps, args.warmup)
     model = f"LSTM seq-len={T} hidden={H} time-series regression (features={F}, linear head, MSE, Adam)"
@@ -142,34 +181,7 @@ def bench_mlp(args, ctx, online: bool):
             opt.step()
             eng.sync_weights()
 
-        graphs = None
-        if not args.no_graph:
-            # the whole step is a few tiny launches: capture it so the CPU launch path is
-            # out of the loop (Adam's step counter is device-side, so replay is exact)
-            s = torch.cuda.Stream(device=ctx.device)
-            s.wait_stream(torch.cuda.current_stream(ctx.device))
-            with torch.cuda.stream(s):
-                for _ in range(3):
-                    compute()
-                    ctx.all_reduce_sum_(eng.grads)
-                    update()
-            torch.cuda.current_stream(ctx.device).wait_stream(s)
-            g1, g2 = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g1):
-                compute()
-            with torch.cuda.graph(g2):
-                update()
-            graphs = (g1, g2)
-
-        def step():
-            if graphs is None:
-                compute()
-                ctx.all_reduce_sum_(eng.grads)
-                update()
-            else:
-                graphs[0].replay()
-                ctx.all_reduce_sum_(eng.grads)
-                graphs[1].replay()
+        step = _graph_step(ctx, eng, compute, update, args.no_graph)
 
     el = _timed(ctx, step, args.steps, args.warmup)
     kind = "dynamic (online, host->HBM streamed mini-batches)" if online else "static (resident batch)"
