@@ -124,6 +124,8 @@ wf::LstmDims lstm_dims(int64_t B, int64_t T, int64_t F, int64_t KX, int64_t H) {
   d.xcd_map = (xm != nullptr && xm[0] == '0') ? 0 : 1;
   const char* nt = std::getenv("WELLFLOW_NT");
   d.nt = (nt != nullptr && nt[0] == '0') ? 0 : 1;
+  const char* pd = std::getenv("WELLFLOW_PF_DBG");
+  d.dbg = pd != nullptr ? std::atoi(pd) : 0;
   return d;
 }
 
@@ -161,6 +163,23 @@ void lstm_forward(const at::Tensor& XH, const at::Tensor& Wp, const at::Tensor& 
   const c10::hip::OptionalHIPGuardMasqueradingAsCUDA guard(XH.device());
   auto s = cur_stream();
   for (int t = 0; t < d.T; ++t) wf::launch_lstm_fwd_step(t, bfp(XH), bfp(Wp), fp(Cst), bfp(S), d, s);
+}
+
+// All T steps in one cooperative launch (lstm_persistent.hip). Returns false (nothing
+// launched) when the shape or device cannot host it; `sync` (int32) word 0 reports a
+// spin timeout after the launch completes.
+bool lstm_forward_persistent(const at::Tensor& XH, const at::Tensor& Wp, const at::Tensor& Cst,
+                             const at::Tensor& S, const at::Tensor& sync, int64_t B, int64_t T, int64_t F,
+                             int64_t KX, int64_t H) {
+  auto d = lstm_dims(B, T, F, KX, H);
+  check_lstm_state(XH, Cst, S, d);
+  check_t(Wp, at::kBFloat16, "Wp");
+  check_extent(Wp, 4 * H * (KX + H), "Wp");
+  check_t(sync, at::kInt, "sync");
+  const c10::hip::OptionalHIPGuardMasqueradingAsCUDA guard(XH.device());
+  return wf::launch_lstm_fwd_persistent(bfp(XH), bfp(Wp), fp(Cst), bfp(S),
+                                        reinterpret_cast<unsigned*>(sync.data_ptr<int>()), sync.numel(), d,
+                                        cur_stream());
 }
 
 void lstm_backward(const at::Tensor& WhhT, const at::Tensor& XH, const at::Tensor& Cst,
@@ -465,6 +484,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("gemm", &gemm);
   m.def("lstm_pack_x", &lstm_pack_x);
   m.def("lstm_forward", &lstm_forward);
+  m.def("lstm_forward_persistent", &lstm_forward_persistent);
   m.def("lstm_backward", &lstm_backward);
   m.def("lstm_backward_dw", &lstm_backward_dw);
   m.def("lstm_pack_weights", &lstm_pack_weights);

@@ -37,10 +37,18 @@ struct LstmDims {
   int bwd_variant = 0;  // backward step GEMM (0: 128x128, 1: 64x128, 2: 128x64, 3: 64x64)
   int xcd_map = 1;      // 1: XCD-aware tile remap (default), 0: identity (diagnostics)
   int nt = 1;           // non-temporal hints on the read-once/write-once state streams
+  int dbg = 0;          // persistent-forward diagnostics (WELLFLOW_PF_DBG): 1 = skip the
+                        // hand-off wait (timing only: results are wrong)
 };
 void launch_lstm_pack_x(const float* x, bf16_t* XH, LstmDims d, hipStream_t s);
 void launch_lstm_fwd_step(int t, bf16_t* XH, const bf16_t* Wp, float* Cst, bf16_t* S,
                           LstmDims d, hipStream_t s);
+// All T forward steps in ONE cooperative launch (lstm_persistent.hip). `sync` must hold
+// lstm_persistent_sync_words(B / (64 * NC)) words (<= 16 + 16 * B / 64 always suffices);
+// word 0 reports a spin timeout. Returns false when the shape / device cannot host it.
+int lstm_persistent_sync_words(int row_blocks);
+bool launch_lstm_fwd_persistent(bf16_t* XH, const bf16_t* Wp, float* Cst, bf16_t* S, unsigned* sync,
+                                long sync_words, LstmDims d, hipStream_t s);
 void launch_lstm_bwd_step(int t, const bf16_t* WhhT, const float* Cst, const bf16_t* S,
                           bf16_t* DG, float* dcarry, const float* dy, const float* w_out,
                           LstmDims d, hipStream_t s);

@@ -1,0 +1,334 @@
+// wellflow — persistent LSTM forward: ONE launch runs all T timesteps
+// (SURVEY.md §2.4 K13 "persistent kernel over T, W sliced across CUs, per-step agent-scope
+// hand-off of h_t"; §7.4 hard part 2).
+//
+// Why: the per-step kernel (lstm.hip) re-streams its whole 256x256 weight tile from L2 /
+// Infinity Cache every step (576 KB per CU per step with the activations) and pays a grid
+// fill/drain per step. Here the weights never move after the prologue:
+//  * grid = (B / (64*NC)) row blocks x (4H / 256) gate-column blocks, one 256-thread
+//    workgroup (4 waves, one per SIMD) per CU, all co-resident (cooperative launch).
+//  * wave w of column block n keeps Wp[gate cols n*256 + 64w .. +63][0:KA] — the four
+//    gates of 16 hidden units (see the permutation in lstm.hip) — as MFMA B fragments in
+//    registers for the whole sequence: KA/32 x 4 bf16x8 = 288 VGPRs at KA = 576.
+//  * per step the workgroup streams its rows of [x_t | 1 | h_{t-1}] through a 2-deep LDS
+//    ring of 64-row chunks (global_load_lds, 72 KB per chunk), so only activations move:
+//    half the bytes of the per-step kernel.
+//  * the fused cell epilogue is the per-step kernel's (same FN layouts for C / S, so the
+//    backward pass is unchanged); h_t is staged through LDS and published with 8-B
+//    write-through (sc1) stores.
+//  * hand-off (cdna_hip_programming.md Guideline 16, recipe R1): every wave drains its
+//    stores (vmcnt(0)), workgroup barrier, ONE lane adds to the row block's arrival counter
+//    (agent-scope atomic); the consumer polls that counter relaxed with s_sleep, then ONE
+//    agent-scope acquire, then plain / LDS-DMA loads. Only the NB workgroups of one row
+//    block depend on each other, so row blocks drift freely (no grid barrier), and the
+//    XCD-aware block map puts a row block's NB workgroups on one XCD (speed only).
+//  * every spin is bounded: on timeout the error word is set and all workgroups drain.
+#include "gemm_core.h"
+#include "kernels.h"
+#include "lstm_layout.h"
+
+namespace wf {
+
+namespace {
+constexpr int PF_ROWS = 32;               // rows per ring chunk
+constexpr unsigned PF_SPIN_LIMIT = 1u << 21;
+typedef __attribute__((address_space(1))) unsigned gu32;
+typedef __attribute__((address_space(1))) unsigned long long gu64;
+}  // namespace
+
+// sync words (uint32): [0] error code (0 ok, 1 spin timeout), [16 + 16*m] arrivals of row block m.
+int lstm_persistent_sync_words(int row_blocks) { return 16 + 16 * row_blocks; }
+
+// KT = KA / 32 k-tiles; NC = 32-row chunks per workgroup per step (compile-time, so every
+// ring slot, LDS offset and vmcnt count below is an immediate).
+template <int KT, int NC, int DBG = 0>  // DBG: timing-only builds (2 no MFMA, 4 no C/S stores, 8 no c loads)
+__global__ __launch_bounds__(256, 1) void lstm_fwd_persistent_kernel(
+    bf16_t* __restrict__ XH, const bf16_t* __restrict__ Wp, float* __restrict__ Cst,
+    bf16_t* __restrict__ S, unsigned* __restrict__ sync, LstmDims d) {
+  constexpr int KA = 32 * KT;
+  constexpr int KS = KA / 64;                // 64-deep k-steps = A pieces per wave per chunk
+  constexpr int ABYTES = PF_ROWS * KA * 2;   // chunk of [x_t | 1 | h_t-1] rows: KS [32][64] images
+  constexpr int CBYTES = PF_ROWS * 64 * 4;   // chunk of c_t-1 (FN blocks of the workgroup's units)
+  constexpr int LPT = KS + ((DBG & 8) ? 0 : 2);  // LDS-DMA instructions per wave per chunk
+  constexpr int NSTORE = (DBG & 4) ? 1 : 7;  // stores per wave per chunk: 2 C, 4 S, 1 h
+  // Distinct static LDS objects per ring slot: the compiler then proves the slot being
+  // filled by LDS-DMA disjoint from the slots being read, and inserts no vmcnt(0) of its own.
+  // EXACTLY ONE static LDS variable, compile-time offsets for every ring slot, the h staging
+  // area and the flag word (slot k at k*SLOT: [A chunk | c_{t-1} chunk]). With several LDS
+  // variables the LDS lowering gives each its own alias scope, the waitcnt pass then tracks
+  // the LDS-DMA into the ring and guards the first read of every slot with vmcnt(0) — which
+  // drained the whole prefetch ring every chunk (measured: loads no longer overlapped MFMA).
+  constexpr int SLOT = ABYTES + CBYTES;
+  constexpr int HOFF = 3 * SLOT, FOFF = HOFF + PF_ROWS * 64 * 2;
+  __shared__ __attribute__((aligned(16))) char smem[FOFF + 16];
+  // h_t staging [32][64] bf16, accessed only through inline asm (32-bit LDS address)
+  const unsigned hb_lds = (unsigned)(uintptr_t)((__attribute__((address_space(3))) char*)(smem + HOFF));
+  int* const lflag_s = reinterpret_cast<int*>(smem + FOFF);
+  volatile int* lflag = lflag_s;
+
+  constexpr int H = KA - 64, G = 4 * H, NB = G / 256, HB = H / 16;  // KX = 64 (host-checked)
+  const int Bp = fn_rows(d.B);
+  const int lane = threadIdx.x & 63, l15 = lane & 15, g = lane >> 4;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int L = xcd_remap(blockIdx.x, gridDim.x);
+  const int m = L / NB, n = L % NB;
+  const int row0 = m * PF_ROWS * NC;
+  const int ub = n * 4 + wid;                // 16-unit block of this wave
+  const int u = ub * 16 + l15;               // hidden unit of this lane
+  const int loff_c = ub * 256 + lane * 4;    // float offset of this lane's C slot in a FN row block
+  const int loff_s = ub * 1024 + lane * 16;  // bf16 offset of this lane's S slot in a FN row block
+  const int loff_h = (((int)threadIdx.x >> 3) * KA + ((int)threadIdx.x & 7) * 8) * 2;  // h publish
+  gu32* err = (gu32*)(sync);
+  gu32* cnt = (gu32*)(sync + 16 + 16 * m);
+  // XH as a buffer resource for the 16-B sc1 h stores (byte offsets < 2^31: checked on the host)
+  const __amdgpu_buffer_rsrc_t xh_rsrc = __builtin_amdgcn_make_buffer_rsrc(XH, 0, 0x7FFFFFFF, 0x00020000);
+
+  // ---- prologue: stationary weight fragments (B operand: lane holds col l15, k 8g..8g+7)
+  bf16x8 w[KT][4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const bf16_t* wr = Wp + (size_t)(n * 256 + wid * 64 + j * 16 + l15) * KA + 8 * g;
+#pragma unroll
+    for (int kt = 0; kt < KT; ++kt) w[kt][j] = *reinterpret_cast<const bf16x8*>(wr + 32 * kt);
+  }
+  // drain them with a wait the compiler's counter model sees (the memory clobber keeps the
+  // loads above it), so it does not re-wait for them at the top of every step
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_waitcnt(0xF70);  // vmcnt(0) expcnt(7) lgkmcnt(15)
+  __builtin_amdgcn_sched_barrier(0);
+
+  // A piece s of this wave: k-step s, rows wid*8 + (lane>>3); the K_CONTIG 16-B chunk
+  // swizzle (row>>1)&7 = 4(wid&1) + g is lane-constant, so it moves onto the source offset.
+  const unsigned aoff = (unsigned)((wid * 8 + (lane >> 3)) * KA * 2 + (((lane & 7) ^ (4 * (wid & 1) + g)) << 4));
+  int fa[2];  // A fragment offsets in a [32][64] image (rows l15 of a 16-row tile)
+#pragma unroll
+  for (int kk = 0; kk < 2; ++kk) fa[kk] = l15 * 128 + (((kk * 4 + g) ^ ((l15 >> 1) & 7)) << 4);
+
+  for (int t = 0; t < d.T; ++t) {
+    if (t > 0) {
+      // ---- publish step t-1 (every wave drained its sc1 h stores) and wait for the row block
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      if (threadIdx.x == 0) {
+        __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const unsigned target = (unsigned)(NB * t);
+        int ok = 1;
+        unsigned spins = 0;
+        while (!(d.dbg & 1) && __hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+          if (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) {
+            ok = 0;
+            break;
+          }
+          if (++spins > PF_SPIN_LIMIT) {
+            __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            ok = 0;
+            break;
+          }
+          __builtin_amdgcn_s_sleep(2);
+        }
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        *lflag = ok;
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      if (*lflag == 0) return;  // uniform: every wave reads the same word
+    }
+    // opaque per-step copy of the row origin: stops the compiler hoisting every chunk's
+    // lane addresses out of the time loop (NC x 64-bit offsets live across the whole
+    // kernel pushed the H = 512, NC = 8 build into spills)
+    int rb = row0;
+    asm volatile("" : "+s"(rb));
+    // per-step uniform bases (row block origin folded in) + per-lane constant offsets
+    // (loff_c / loff_s / loff_h), so every chunk address is base + compile-time stride
+    const float* cprev = Cst + (size_t)t * Bp * H + (size_t)(rb >> 4) * HB * 256;
+    float* cnext = Cst + (size_t)(t + 1) * Bp * H + (size_t)(rb >> 4) * HB * 256;
+    bf16_t* St = S + (size_t)t * Bp * G + (size_t)(rb >> 4) * HB * 1024;
+    const char* abase = reinterpret_cast<const char*>(XH + ((size_t)t * d.B + rb) * KA) + aoff;
+    const int hsoff = (int)((((size_t)(t + 1) * d.B + rb) * KA + 64 + n * 64) * 2);
+
+    // chunk c -> ring slot c % 3: KS A pieces + this wave's 2 FN blocks of c_{t-1}
+    auto issue = [&](int c, auto sc) {  // chunk c into ring slot SL (= c % 3)
+      constexpr int SL = decltype(sc)::value;
+      char* ra = smem + SL * SLOT;
+      char* rcb = ra + ABYTES;
+      const char* src = abase + (size_t)c * ABYTES;
+#pragma unroll
+      for (int s = 0; s < KS; ++s)
+        __builtin_amdgcn_global_load_lds((const void*)(src + s * 128), (lds_void*)(ra + s * 4096 + wid * 1024),
+                                         16, 0, 0);
+#pragma unroll
+      for (int j = 0; j < ((DBG & 8) ? 0 : 2); ++j) {
+        __builtin_amdgcn_global_load_lds((const void*)(cprev + (2 * c + j) * HB * 256 + loff_c),
+                                         (lds_void*)(rcb + (wid * 2 + j) * 1024), 16, 0, 0);
+      }
+    };
+    issue(0, std::integral_constant<int, 0>{});
+    if constexpr (NC > 1) issue(1, std::integral_constant<int, 1>{});
+
+    // chunk body, ring slot P = c % 3 compile-time (3 bodies in a runtime loop keep the
+    // register pressure of a 3-chunk kernel; a fully unrolled NC = 8 spilled)
+    auto chunk = [&](int c, auto pc) {
+      constexpr int P = decltype(pc)::value;
+      // vector-memory ops issued after chunk c's LDS-DMA (top of c issues c+2, then stores)
+      if (c == 0) {
+        if (NC > 1) wait_vmcnt<LPT>(); else wait_vmcnt<0>();
+      } else if (c == 1) {
+        if (NC > 2) wait_vmcnt<LPT + NSTORE>(); else wait_vmcnt<NSTORE>();
+      } else if (c + 1 < NC) {
+        wait_vmcnt<2 * NSTORE + LPT>();
+      } else {
+        wait_vmcnt<2 * NSTORE>();
+      }
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);  // keep each chunk's code (and live ranges) to itself
+      if (c + 2 < NC) issue(c + 2, std::integral_constant<int, (P + 2) % 3>{});
+      const char* cur = smem + P * SLOT;
+      const char* cpl = cur + ABYTES;
+
+      f32x4 acc[2][4];
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int kt = 0; kt < KT; ++kt) {
+        bf16x8 a[2];
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+          a[i] = *reinterpret_cast<const bf16x8*>(cur + (kt >> 1) * 4096 + i * 2048 + fa[kt & 1]);
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            if constexpr (!(DBG & 2))
+              acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], w[kt][j], acc[i][j], 0, 0, 0);
+      }
+
+      // ---- fused cell epilogue (lane: chunk rows 16i + 4g + r, unit u; gates acc[i][0..3])
+      // both c_{t-1} tiles into registers BEFORE the first h_t write to LDS: read lazily
+      // after it, the compiler guarded the read with a vmcnt(0) (waiting for the ring's
+      // in-flight LDS-DMA); the empty asm pins the loads here
+      f32x4 cpr[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) cpr[i] = *reinterpret_cast<const f32x4*>(cpl + (wid * 2 + i) * 1024 + lane * 16);
+      asm volatile("" : "+v"(cpr[0]), "+v"(cpr[1]));
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const float cpv[4] = {cpr[i][0], cpr[i][1], cpr[i][2], cpr[i][3]};
+        float cv[4];
+        unsigned pk[8];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float ig = sigmoidf_(acc[i][0][r]);
+          const float fg = sigmoidf_(acc[i][1][r]);
+          const float gg = tanhf_(acc[i][2][r]);
+          const float og = sigmoidf_(acc[i][3][r]);
+          const float cn = fg * cpv[r] + ig * gg;
+          cv[r] = cn;
+          pk[2 * r] = (unsigned)f2bf(ig) | ((unsigned)f2bf(fg) << 16);
+          pk[2 * r + 1] = (unsigned)f2bf(gg) | ((unsigned)f2bf(og) << 16);
+          // h staging store in asm: a compiler-visible LDS write here is guarded by a
+          // vmcnt(0) (the waitcnt pass orders every LDS access after in-flight LDS-DMA)
+          const unsigned hv = f2bf(og * tanhf_(cn));
+          asm volatile("ds_write_b16 %0, %1" ::"v"(hb_lds + 2u * ((i * 16 + 4 * g + r) * 64 + wid * 16 + l15)),
+                       "v"(hv)
+                       : "memory");
+        }
+        if constexpr (!(DBG & 4)) {
+          *reinterpret_cast<float4*>(cnext + (2 * c + i) * HB * 256 + loff_c) = make_float4(cv[0], cv[1], cv[2], cv[3]);
+          uint4* sp = reinterpret_cast<uint4*>(St + (2 * c + i) * HB * 1024 + loff_s);
+          sp[0] = make_uint4(pk[0], pk[1], pk[2], pk[3]);
+          sp[1] = make_uint4(pk[4], pk[5], pk[6], pk[7]);
+        }
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      // ---- publish the chunk's h rows: 32 rows x 128 B, one 16-B write-through (sc1)
+      // buffer store per thread (Guideline 16 R1: no release fence; 8-B sc1 stores cost
+      // 0.4 ms per forward more, measured)
+      {
+        u32x4 vv;  // row threadIdx>>3, 16-B column threadIdx&7 of the [32][64] bf16 tile
+        asm volatile("ds_read_b128 %0, %1\n\ts_waitcnt lgkmcnt(0)"
+                     : "=&v"(vv)
+                     : "v"(hb_lds + 16u * threadIdx.x)
+                     : "memory");
+        __builtin_amdgcn_raw_buffer_store_b128(vv, xh_rsrc, loff_h, hsoff + c * PF_ROWS * KA * 2, 16 /* sc1 */);
+      }
+    };
+    using S0 = std::integral_constant<int, 0>;
+    using S1 = std::integral_constant<int, 1>;
+    using S2 = std::integral_constant<int, 2>;
+    for (int c = 0; c < NC; c += 3) {
+      chunk(c, S0{});
+      if (c + 1 < NC) chunk(c + 1, S1{});
+      if (c + 2 < NC) chunk(c + 2, S2{});
+    }
+  }
+}
+
+template <int KT, int NC>
+static bool launch_pf(bf16_t* XH, const bf16_t* Wp, float* Cst, bf16_t* S, unsigned* sync, int grid,
+                      LstmDims d, hipStream_t s) {
+  const void* f = reinterpret_cast<const void*>(&lstm_fwd_persistent_kernel<KT, NC>);
+  if constexpr (KT == 18 && NC == 8) {  // timing-only diagnostic builds (WELLFLOW_PF_DBG >= 2)
+    if (d.dbg == 2) f = reinterpret_cast<const void*>(&lstm_fwd_persistent_kernel<KT, NC, 2>);
+    if (d.dbg == 4) f = reinterpret_cast<const void*>(&lstm_fwd_persistent_kernel<KT, NC, 4>);
+    if (d.dbg == 8) f = reinterpret_cast<const void*>(&lstm_fwd_persistent_kernel<KT, NC, 8>);
+    if (d.dbg == 14) f = reinterpret_cast<const void*>(&lstm_fwd_persistent_kernel<KT, NC, 14>);
+  }
+  void* args[] = {&XH, &Wp, &Cst, &S, &sync, &d};
+  return hipLaunchCooperativeKernel(f, dim3(grid), dim3(256), args, 0u, s) == hipSuccess;
+}
+
+template <int KT>
+static bool launch_pf_nc(int NC, bf16_t* XH, const bf16_t* Wp, float* Cst, bf16_t* S, unsigned* sync,
+                         int grid, LstmDims d, hipStream_t s) {
+  switch (NC) {
+    case 1: return launch_pf<KT, 1>(XH, Wp, Cst, S, sync, grid, d, s);
+    case 2: return launch_pf<KT, 2>(XH, Wp, Cst, S, sync, grid, d, s);
+    case 4: return launch_pf<KT, 4>(XH, Wp, Cst, S, sync, grid, d, s);
+    case 8: return launch_pf<KT, 8>(XH, Wp, Cst, S, sync, grid, d, s);
+    default: return false;
+  }
+}
+
+// Returns false (and launches nothing) when the shape or the device cannot host the
+// persistent schedule; the caller then runs the per-step kernels.
+bool launch_lstm_fwd_persistent(bf16_t* XH, const bf16_t* Wp, float* Cst, bf16_t* S, unsigned* sync,
+                                long sync_words, LstmDims d, hipStream_t s) {
+  const int KA = d.KX + d.H, G = 4 * d.H;
+  if ((double)(d.T + 1) * d.B * KA * 2 >= 2147483647.0) return false;  // 32-bit buffer offsets
+  if (d.KX % 64 != 0 || KA % 64 != 0 || G % 256 != 0 || d.B % PF_ROWS != 0 || d.KX != 64) return false;
+  int dev = 0, cus = 0;
+  if (hipGetDevice(&dev) != hipSuccess ||
+      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+    return false;
+  const int NB = G / 256;
+  // fewest 32-row chunks per workgroup whose grid fits one workgroup per CU
+  int NC = 0;
+  for (int nc = 1; nc <= 8; nc *= 2) {
+    if (d.B % (PF_ROWS * nc) == 0 && (d.B / (PF_ROWS * nc)) * NB <= cus) {
+      NC = nc;
+      break;
+    }
+  }
+  if (NC == 0) return false;
+  const int MB = d.B / (PF_ROWS * NC);
+  if (sync_words < lstm_persistent_sync_words(MB)) return false;
+  if (hipMemsetAsync(sync, 0, sizeof(unsigned) * (size_t)lstm_persistent_sync_words(MB), s) != hipSuccess)
+    return false;
+  const int grid = MB * NB;
+  switch (KA / 32) {
+    case 6: return launch_pf_nc<6>(NC, XH, Wp, Cst, S, sync, grid, d, s);    // H = 128
+    case 10: return launch_pf_nc<10>(NC, XH, Wp, Cst, S, sync, grid, d, s);  // H = 256
+    case 18: return launch_pf_nc<18>(NC, XH, Wp, Cst, S, sync, grid, d, s);  // H = 512
+    default: return false;
+  }
+}
+
+}  // namespace wf

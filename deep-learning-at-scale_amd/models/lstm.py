@@ -19,6 +19,7 @@ from __future__ import annotations
 
 import dataclasses
 import math
+import os
 
 import torch
 from torch import nn
@@ -166,6 +167,12 @@ class NativeLSTM:
         # tile shapes (csrc/kernels.h LstmDims), A/B-tuned on MI355X with tools/tune_lstm.py
         # (profiles/r1_*): fwd 256x256 glds ring (v6), bwd 64x128 glds ring (v9); dW split-K 32.
         self.fwd_variant, self.bwd_variant = 6, 8
+        # persistent forward (csrc/lstm_persistent.hip): all T steps in ONE cooperative
+        # launch with the gate weights resident in registers; falls back to the per-step
+        # kernels (fwd_variant) when the shape / device cannot host it
+        self.persistent = os.environ.get("WELLFLOW_PERSISTENT", "1") != "0"
+        self.sync = torch.zeros(16 + 16 * (B // 32 + 1), dtype=torch.int32, device=dev)
+        self.last_forward_persistent = False
         self.dw_ksplit = 0  # 0 = heuristic
         # timesteps per overlapped dW GEMM chunk; 0 = serial dW at the end (measured faster:
         # the BPTT chain already fills every CU, overlapping only adds contention)
@@ -185,6 +192,18 @@ class NativeLSTM:
         base = self.T * self.B * lay.KA  # XH[T] starts here (row stride KA)
         return self.XH[base + lay.KX : base + lay.KX + (B - 1) * lay.KA + self.H]
 
+    def _forward_steps(self, B):
+        C = self._C
+        ok = self.persistent and C.lstm_forward_persistent(self.XH, self.Wp, self.Cst, self.S, self.sync,
+                                                          *self._dims(B))
+        if not ok:
+            C.lstm_forward(self.XH, self.Wp, self.Cst, self.S, *self._dims(B), self.fwd_variant)
+        self.last_forward_persistent = bool(ok)
+
+    def persistent_error(self) -> int:
+        """Non-zero if the last persistent forward hit its spin bound (host sync)."""
+        return int(self.sync[0].item()) if self.last_forward_persistent else 0
+
     # ------------------------------------------------------------------ passes
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         """x: [B, T, F] fp32 (B <= max batch) -> predictions [B] (view of an internal buffer)."""
@@ -199,7 +218,7 @@ class NativeLSTM:
             x = xp
         C = self._C
         C.lstm_pack_x(x, self.XH, *self._dims(self.B))
-        C.lstm_forward(self.XH, self.Wp, self.Cst, self.S, *self._dims(self.B), self.fwd_variant)
+        self._forward_steps(self.B)
         _, w_out, b_out = self.lay.views(self.params)
         C.head_fwd(self._hT(self.B), self.lay.KA, self.B, self.H, w_out, b_out, None, self.pred,
                    None, None, 0.0)
@@ -223,7 +242,7 @@ class NativeLSTM:
             self.grads.zero_()
         self.loss_sum.zero_()
         C.lstm_pack_x(x.contiguous(), self.XH, *self._dims(B))
-        C.lstm_forward(self.XH, self.Wp, self.Cst, self.S, *self._dims(B), self.fwd_variant)
+        self._forward_steps(B)
         hT = self._hT(B)
         y = y.contiguous().float()
         if self.loss_kind == "mse":  # head + MSE + dy fused in one kernel

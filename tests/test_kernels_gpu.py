@@ -184,3 +184,35 @@ def test_losses():
         assert abs(ls.item() - L.item()) < 1e-3 * abs(L.item()) + 1e-3
         assert torch.allclose(d.float(), pr.grad * scale, rtol=1e-2, atol=1e-4)
         assert torch.allclose(cs, (pr.grad * scale).sum(0), rtol=1e-2, atol=1e-4)
+
+
+@pytest.mark.parametrize("B,H,T", [(8192, 512, 8), (512, 256, 6), (256, 128, 5), (2048, 512, 64)])
+def test_lstm_persistent_forward_matches_per_step(B, H, T):
+    """The one-launch persistent forward (csrc/lstm_persistent.hip) must reproduce the
+    per-step kernels: same MFMA k-order per output, so h/C/S agree to the last bf16 ulp
+    apart from transcendental rounding (tolerance), and its spin bound must not trip."""
+    from wellflow.data.synth import synth_lstm_batch
+    from wellflow.models.lstm import NativeLSTM, init_lstm_flat
+
+    F = 16
+    eng = NativeLSTM(F, H, T, B, device=DEV)
+    eng.params.copy_(init_lstm_flat(F, H, seed=1).to(DEV))
+    eng.sync_weights()
+    x, _ = synth_lstm_batch(B, T, F, seed=2)
+    x = x.to(DEV)
+    C = eng._C
+    dims = eng._dims(B)
+    C.lstm_pack_x(x, eng.XH, *dims)
+    C.lstm_forward(eng.XH, eng.Wp, eng.Cst, eng.S, *dims, 6)
+    ref = (eng.XH.clone(), eng.Cst.clone(), eng.S.clone())
+    eng.XH[B * eng.lay.KA:].zero_()
+    C.lstm_pack_x(x, eng.XH, *dims)
+    eng.Cst[B * H:].zero_()
+    eng.S.zero_()
+    ok = C.lstm_forward_persistent(eng.XH, eng.Wp, eng.Cst, eng.S, eng.sync, *dims)
+    torch.cuda.synchronize()
+    assert ok, "persistent launch refused"
+    assert int(eng.sync[0].item()) == 0, "spin bound tripped"
+    for name, a, b in zip(("XH", "C", "S"), (eng.XH, eng.Cst, eng.S), ref):
+        d = (a.float() - b.float()).abs().max().item()
+        assert d <= 2e-2, (name, d)
