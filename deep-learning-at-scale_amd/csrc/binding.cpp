@@ -64,7 +64,7 @@ void gemm(const at::Tensor& A, bool a_mn, int64_t lda, const at::Tensor& B, bool
           c10::optional<at::Tensor> outH, int64_t ldo, c10::optional<at::Tensor> bias,
           c10::optional<at::Tensor> mask, int64_t ldm, double mask_scale,
           c10::optional<at::Tensor> colsum, double alpha, double beta, int64_t act, bool atomic,
-          double drop_p, int64_t seed) {
+          double drop_p, int64_t seed, int64_t big_tile) {
   check_t(A, at::kBFloat16, "A");
   check_t(B, at::kBFloat16, "B");
   TORCH_CHECK(M > 0 && N > 0 && K > 0, "gemm: empty problem");
@@ -96,6 +96,7 @@ void gemm(const at::Tensor& A, bool a_mn, int64_t lda, const at::Tensor& B, bool
   e.atomic = atomic ? 1 : 0;
   e.drop_p = (float)drop_p;
   e.seed = (unsigned long long)seed;
+  e.big_tile = (int)big_tile;
   TORCH_CHECK(ksplit == 1 || atomic, "gemm: split-K needs atomic accumulation");
   e.stage_ok = (e.outH != nullptr && e.outF == nullptr && !atomic && beta == 0.0 && N % 8 == 0 &&
                 ldo % 8 == 0 && (e.mask == nullptr || ldm % 8 == 0))
@@ -270,11 +271,13 @@ void lstm_backward_dw(const at::Tensor& WhhT, const at::Tensor& XH, const at::Te
     e.outF = fp(gW);
     e.ldo = KA;
     e.atomic = 1;
-    static const bool big = [] {
+    // WELLFLOW_DW_BIG: 0 = 128x128 tile, 1 (default) = 256x128 8-wave, 2 = 128x288 4-wave
+    // (tools/tune_lstm.py, B = 8192: 1.33 / 1.60 ms at split-K 32)
+    static const int big = [] {
       const char* v = std::getenv("WELLFLOW_DW_BIG");
-      return v == nullptr || v[0] != '0';
+      return v == nullptr ? 1 : std::atoi(v);
     }();
-    e.big_tile = big ? 1 : 0;
+    e.big_tile = big;
     const bf16_t* A = bfp(DG) + (size_t)t0 * B * G;
     const bf16_t* Bm = bfp(XH) + (size_t)t0 * B * KA;
     // whole-tile over-read of XH columns 576..639 stays inside XH (its slab T follows)

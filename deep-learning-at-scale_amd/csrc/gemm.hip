@@ -173,8 +173,56 @@ static void launch_dw_big(const bf16_t* A, long lda, const bf16_t* B, long ldb, 
                      dim3(512), 0, s, A, lda, B, ldb, M, N, K, kchunk, e);
 }
 
+// LSTM weight gradient (M = 4H = 2048, N = KA = 576, K = T*B), alternative tile: 128x288,
+// 4 waves of 64x144, 3-stage ring (156 KiB). N = 2 x 288 exactly (the 256x128 tile wastes
+// half of its 5th column tile) and 16 x 2 = 32 tiles per K split = one XCD's 32 CUs. Measured
+// slower than the 256x128 8-wave tile (1.60 vs 1.33 ms at split-K 32: one wave per SIMD
+// cannot hide the fragment reads), so it is opt-in (WELLFLOW_DW_BIG=2).
+// Split-K weight-gradient kernel: MN x MN operands, full tiles only (M % BM == N % BN == 0,
+// host-checked), epilogue = fp32 atomic add of alpha * acc (nothing else, so the 144
+// accumulator registers stay in registers).
+template <int BM, int BN, int STAGES, int WM, int WN>
+__global__ __launch_bounds__(64 * WM * WN) void gemm_dw_kernel(const bf16_t* __restrict__ A, long lda,
+                                                      const bf16_t* __restrict__ B, long ldb, int N,
+                                                      int kchunk, int tiles, float* __restrict__ out,
+                                                      long ldo, float alpha) {
+  using C = GemmCfg<BM, BN, MN_CONTIG, MN_CONTIG, WM, WN>;
+  __shared__ __attribute__((aligned(16))) char smem[STAGES * C::STAGE];
+  const int tiles_n = N / BN;
+  const int L = xcd_remap(blockIdx.x, gridDim.x);
+  const int split = L / tiles, t = L % tiles;
+  const int m0 = (t / tiles_n) * BM, n0 = (t % tiles_n) * BN;
+  f32x4 acc[C::TM][C::TN];
+  gemm_mainloop_glds2<C, STAGES>(A, lda, B, ldb, split * kchunk, kchunk / 64, m0, n0, smem, acc);
+  const AccCoord<C> cc(m0, n0);
+#pragma unroll
+  for (int j = 0; j < C::TN; ++j)
+#pragma unroll
+    for (int i = 0; i < C::TM; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        atomicAdd(out + (size_t)cc.row(i, r) * ldo + cc.col(j), alpha * acc[i][j][r]);
+}
+
+static void launch_dw_288(const bf16_t* A, long lda, const bf16_t* B, long ldb, int M, int N, int K,
+                          int ksplit, const GemmEpilogue& e, hipStream_t s) {
+  constexpr int BM = 128, BN = 288;
+  const int tiles = (M / BM) * (N / BN);
+  // equal 64-aligned K chunks (K % (64 * nsplit) == 0 is required: partial chunks would need
+  // the masked mainloop)
+  int nsplit = ksplit;
+  while (nsplit > 1 && K % (64 * nsplit) != 0) --nsplit;
+  const int kchunk = K / nsplit;
+  hipLaunchKernelGGL((gemm_dw_kernel<BM, BN, 3, 2, 2>), dim3(tiles * nsplit), dim3(256), 0, s, A, lda, B, ldb,
+                     N, kchunk, tiles, e.outF, e.ldo, e.alpha);
+}
+
 void launch_gemm(const bf16_t* A, long lda, int a_mn, const bf16_t* B, long ldb, int b_mn, int M,
                  int N, int K, int ksplit, const GemmEpilogue& e, hipStream_t s, bool glds_ok) {
+  if (a_mn && b_mn && glds_ok && e.atomic && e.big_tile == 2 && M % 128 == 0 && N % 288 == 0 && K % 64 == 0) {
+    launch_dw_288(A, lda, B, ldb, M, N, K, ksplit < 1 ? 1 : ksplit, e, s);
+    return;
+  }
   if (a_mn && b_mn && glds_ok && e.atomic && e.big_tile && M % 256 == 0 && K % 64 == 0) {
     launch_dw_big(A, lda, B, ldb, M, N, K, ksplit < 1 ? 1 : ksplit, e, s);
     return;

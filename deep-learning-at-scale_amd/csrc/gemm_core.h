@@ -26,6 +26,19 @@ enum : int { K_CONTIG = 0, MN_CONTIG = 1 };
 
 typedef __attribute__((address_space(3))) bf16x4 lds_bf16x4;
 
+// MN_CONTIG image swizzle for an R-row tile ([64 k][R] bf16, C = R/16 32-B chunks per k-row):
+// data chunk j of k-row k sits in slot pos(j, hk(k)). Power-of-two C: XOR (as before);
+// other C (the 288-wide weight-gradient tile): rotation mod C, still a bijection per row.
+template <int R>
+struct MnSwz {
+  static constexpr int C = R / 16;
+  static constexpr bool POW2 = (C & (C - 1)) == 0;
+  __host__ __device__ static constexpr int hmask() { return POW2 ? C - 1 : 7; }
+  __device__ static __forceinline__ int hk(int k) { return ((k & 3) | ((k >> 1) & 4)) & hmask(); }
+  __device__ static __forceinline__ int pos(int j, int h) { return POW2 ? (j ^ h) : (j + h) % C; }
+  __device__ static __forceinline__ int data(int p, int h) { return POW2 ? (p ^ h) : (p + C - h) % C; }
+};
+
 template <int R, int L, int NT_ = 256>
 struct OpTile {
   static constexpr int NT = NT_;
@@ -34,10 +47,10 @@ struct OpTile {
   static constexpr int BYTES = R * BK * 2;
   static_assert(CHUNKS >= 1 && R * BK / 8 == CHUNKS * NT, "tile / thread-count mismatch");
   static_assert(L == K_CONTIG || R >= 64, "MN_CONTIG tile needs >= 64 rows");
+  static_assert(L == K_CONTIG || R % 16 == 0, "MN_CONTIG tile rows must be a multiple of 16");
+  using SW = MnSwz<R>;
 
-  __device__ static __forceinline__ int hk(int k) {
-    return ((k & 3) | ((k >> 1) & 4)) & (R / 16 - 1);
-  }
+  __device__ static __forceinline__ int hk(int k) { return SW::hk(k); }
 
   // Global -> registers for the tile whose first row is row0 and first k is k0.
   // Rows >= rows or k >= kmax read as zero (the address is clamped, the value masked,
@@ -75,7 +88,7 @@ struct OpTile {
       } else {
         constexpr int CPR = R / 8;
         const int k = q / CPR, c8 = q % CPR;
-        off = k * (R * 2) + ((((c8 >> 1) ^ hk(k))) << 5) + ((c8 & 1) << 4);
+        off = k * (R * 2) + (SW::pos(c8 >> 1, hk(k)) << 5) + ((c8 & 1) << 4);
       }
       *reinterpret_cast<uint4*>(lds + off) = r[i];
     }
@@ -96,7 +109,7 @@ struct OpTile {
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
         const int k = kk * 32 + 8 * g + 4 * h + q;
-        const int off = k * (R * 2) + ((j ^ hk(k)) << 5) + p * 8;
+        const int off = k * (R * 2) + (SW::pos(j, hk(k)) << 5) + p * 8;
         bf16x4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_bf16x4*)(lds + off));
         out[4 * h + 0] = v[0];
         out[4 * h + 1] = v[1];
@@ -198,9 +211,16 @@ struct GldsTile {
   static constexpr int NW = NT / 64;
   static constexpr int PER_WAVE = PIECES / NW;
   static_assert(PIECES % NW == 0 && PER_WAVE >= 1, "tile pieces must split evenly over waves");
+  using SW = MnSwz<R>;
 
-  __device__ static __forceinline__ int hk(int k) {
-    return ((k & 3) | ((k >> 1) & 4)) & (R / 16 - 1);
+  __device__ static __forceinline__ int hk(int k) { return SW::hk(k); }
+
+  // MN_CONTIG: the (k, column) whose 16 B land at LDS byte o of the tile image (pieces may
+  // straddle k-rows when 2R does not divide 1 KiB)
+  __device__ static __forceinline__ void mn_src(int o, int& k, int& col) {
+    k = o / (R * 2);
+    const int b = o % (R * 2);
+    col = (SW::data(b >> 5, hk(k)) << 4) + (((b >> 4) & 1) << 3);
   }
 
   // Issue this wave's glds for the tile (row0, k0) -> lds_tile. All rows/k in range.
@@ -215,10 +235,8 @@ struct GldsTile {
         const int lc = (lane & 7) ^ ((row >> 1) & 7);
         src = p + (size_t)(row0 + row) * ld + k0 + lc * 8;
       } else {
-        constexpr int SPR = R / 8;  // 16-B slots per k-row
-        const int k = piece * (512 / R) + lane / SPR;
-        const int slot = lane % SPR;
-        const int col = (((slot >> 1) ^ hk(k)) << 4) + ((slot & 1) << 3);
+        int k, col;
+        mn_src(piece * 1024 + lane * 16, k, col);
         src = p + (size_t)(k0 + k) * ld + row0 + col;
       }
       __builtin_amdgcn_global_load_lds((const void*)src, (lds_void*)(lds_tile + piece * 1024), 16, 0, 0);
@@ -334,10 +352,9 @@ struct GldsOperand {
         const int lc = (lane & 7) ^ ((row >> 1) & 7);
         off = (long)row * ld + lc * 8;
       } else {
-        constexpr int SPR = R / 8;
-        const int k = piece * (512 / R) + lane / SPR;
-        const int slot = lane % SPR;
-        off = (long)k * ld + (((slot >> 1) ^ Q::hk(k)) << 4) + ((slot & 1) << 3);
+        int k, col;
+        Q::mn_src(piece * 1024 + lane * 16, k, col);
+        off = (long)k * ld + col;
       }
       src[i] = (unsigned)(off * 2);
     }
@@ -373,10 +390,11 @@ struct FragReader {
       for (int kk = 0; kk < 2; ++kk) fb[kk] = (rw + l15) * 128 + (((kk * 4 + g) ^ s) << 4);
     } else {
       const int q = l15 >> 2, p = lane & 3;
-      const int hk = (q | ((g & 1) << 2)) & (R / 16 - 1);
+      // hk(k) for k = 32kk + 8g + 4h + q does not depend on kk or h
+      const int hk = (q | ((g & 1) << 2)) & MnSwz<R>::hmask();
 #pragma unroll
       for (int i = 0; i < NB; ++i)
-        fb[i] = (8 * g + q) * (R * 2) + ((((rw >> 4) + i) ^ hk) << 5) + p * 8;
+        fb[i] = (8 * g + q) * (R * 2) + (MnSwz<R>::pos((rw >> 4) + i, hk) << 5) + p * 8;
     }
   }
 

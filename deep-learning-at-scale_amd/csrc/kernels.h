@@ -23,7 +23,7 @@ struct GemmEpilogue {
   float drop_p = 0.f;            // inverted dropout after the activation
   unsigned long long seed = 0;
   int stage_ok = 0;              // host-verified: bf16 output/mask tiles may go through LDS
-  int big_tile = 0;              // MN x MN split-K weight gradient: use the 256x128 8-wave tile
+  int big_tile = 0;              // MN x MN split-K weight gradient: 1 = 256x128 8-wave tile, 2 = 128x288
 };
 
 void launch_gemm(const bf16_t* A, long lda, int a_mn, const bf16_t* B, long ldb, int b_mn, int M,

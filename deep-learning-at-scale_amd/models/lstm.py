@@ -256,7 +256,7 @@ class NativeLSTM:
         # BPTT chain (high-priority stream) + dWcat = sum_{t,b} dG_t[b]^T [x_t | 1 | h_{t-1}][b]
         # as split-K GEMM chunks on a low-priority stream, overlapped with the chain.
         K = self.T * B
-        ksplit = self.dw_ksplit or max(1, min(16, K // 32768))
+        ksplit = self.dw_ksplit or max(1, min(32, K // 16384))
         if self.dw_chunk > 0:
             ksplit = max(1, ksplit * self.dw_chunk // self.T)
         C.lstm_backward_dw(self.WhhT, self.XH, self.Cst, self.S, self.DG, self.dcarry, self.dy,

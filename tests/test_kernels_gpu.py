@@ -90,15 +90,17 @@ def test_gemm_mask_and_splitk_atomic():
     assert torch.allclose(outm, refm, rtol=1e-3, atol=5e-2)
 
 
-def test_lstm_forward_backward_matches_torch():
+@pytest.mark.parametrize("F,H,T,B,ksplit", [(9, 128, 12, 96, 0), (16, 512, 4, 64, 0), (16, 512, 3, 256, 3)])
+def test_lstm_forward_backward_matches_torch(F, H, T, B, ksplit):
+    """(16, 512, ...) exercises the persistent forward and the 128x288 split-K dW tile."""
     from wellflow.models.lstm import LSTMRegressor, LstmLayout, NativeLSTM
 
     torch.manual_seed(3)
-    F, H, T, B = 9, 128, 12, 96
     ref = LSTMRegressor(F, H).to(DEV)
     x = torch.randn(B, T, F, device=DEV)
     y = torch.randn(B, device=DEV)
     eng = NativeLSTM(F, H, T, B, device=DEV)
+    eng.dw_ksplit = ksplit
     eng.params.copy_(ref.to_flat().to(DEV))
     eng.sync_weights()
 

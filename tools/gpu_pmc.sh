@@ -9,6 +9,6 @@ grep -oE "^\s*(SQ|TCC|TCP|GRBM|TA|TD)[A-Za-z0-9_]*" gpurun_out/pmc/counters_list
 i=0
 for set in "$@"; do
   i=$((i+1))
-  timeout -k 10 300 rocprofv3 --pmc $set --output-format csv -d gpurun_out/pmc/set$i -o run -- python3 bench.py --steps 2 --warmup 1 > gpurun_out/pmc/set$i.log 2>&1 || { echo "set $i failed"; tail -5 gpurun_out/pmc/set$i.log; exit 1; }
+  timeout -k 10 150 rocprofv3 --pmc $set --output-format csv -d gpurun_out/pmc/set$i -o run -- python3 bench.py --steps 2 --warmup 1 --no-graph > gpurun_out/pmc/set$i.log 2>&1 || { echo "set $i failed"; tail -5 gpurun_out/pmc/set$i.log; exit 1; }
 done
 ls -R gpurun_out/pmc | head -40

@@ -32,6 +32,7 @@ def main():
     ap.add_argument("--fwd", default="0,1,2")
     ap.add_argument("--bwd", default="0,1,2,3")
     ap.add_argument("--ksplit", default="8,16,32,64")
+    ap.add_argument("--tiles", default="1,2", help="dW GEMM tiles (1: 256x128, 2: 128x288)")
     a = ap.parse_args()
     B, T, F, H = a.batch, 64, 16, 512
     eng = NativeLSTM(F, H, T, B)
@@ -71,11 +72,12 @@ def main():
                                                 eng.dy, lay.views(eng.params)[1], *dims, v))
             res.setdefault(f"bwd v{v}", []).append(ms)
         for ks in map(int, a.ksplit.split(",")):
-            def dw():
-                gW.zero_()
-                gemm(eng.DG, eng.XH, lay.G, lay.KA, T * B, a_mn=True, lda=lay.G, b_mn=True, ldb=lay.KA,
-                     outF=gW, ldo=lay.KA, atomic=True, ksplit=ks)
-            res.setdefault(f"dW ksplit {ks}", []).append(timeit(dw))
+            for tile in map(int, a.tiles.split(",")):
+                def dw():
+                    gW.zero_()
+                    gemm(eng.DG, eng.XH, lay.G, lay.KA, T * B, a_mn=True, lda=lay.G, b_mn=True, ldb=lay.KA,
+                         outF=gW, ldo=lay.KA, atomic=True, ksplit=ks, tile=tile)
+                res.setdefault(f"dW tile{tile} ks{ks}", []).append(timeit(dw))
         # decomposition of one backward step: same-shape GEMM alone, cell epilogue alone
         tmp = torch.empty(B * H, dtype=torch.bfloat16, device="cuda")
         A1 = eng.DG[B * lay.G : 2 * B * lay.G]
