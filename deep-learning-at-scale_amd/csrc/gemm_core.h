@@ -424,7 +424,7 @@ __device__ __forceinline__ void gemm_mainloop_glds2(const bf16_t* __restrict__ A
                                                     const bf16_t* __restrict__ B, long ldb, int kbeg,
                                                     int nk, int m0, int n0, char* smem,
                                                     f32x4 (&acc)[C::TM][C::TN]) {
-  static_assert(STAGES >= 2 && STAGES <= 4, "2..4 stages");
+  static_assert(STAGES >= 2 && STAGES <= 6, "2..6 stages");
   using OA = GldsOperand<C::BM, C::LA_, C::NT>;
   using OB = GldsOperand<C::BN, C::LB_, C::NT>;
   constexpr int STAGE = OA::TILE_BYTES + OB::TILE_BYTES;
@@ -457,7 +457,13 @@ __device__ __forceinline__ void gemm_mainloop_glds2(const bf16_t* __restrict__ A
   auto body = [&](int tt, auto uc) {
     constexpr int u = decltype(uc)::value;  // == tt % STAGES
     const int ahead = min(nk - 1, tt + STAGES - 2) - tt;
-    if constexpr (STAGES >= 4) {
+    if constexpr (STAGES >= 5) {
+      if (ahead >= STAGES - 2) wait_vmcnt<(STAGES - 2) * LPT>();
+      else if (ahead == 3) wait_vmcnt<3 * LPT>();
+      else if (ahead == 2) wait_vmcnt<2 * LPT>();
+      else if (ahead == 1) wait_vmcnt<LPT>();
+      else wait_vmcnt<0>();
+    } else if constexpr (STAGES >= 4) {
       if (ahead >= 2) wait_vmcnt<2 * LPT>();
       else if (ahead == 1) wait_vmcnt<LPT>();
       else wait_vmcnt<0>();

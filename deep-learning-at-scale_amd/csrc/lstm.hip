@@ -294,6 +294,9 @@ void launch_lstm_bwd_step(int t, const bf16_t* WhhT, const float* Cst, const bf1
     case 15: bwd_cfg<128, 64, 2, 2, 4>(t, WhhT, Cst, S, DG, dcarry, d, s); break;  // 4st 96K
     case 16: bwd_cfg<128, 128, 4, 4, 3>(t, WhhT, Cst, S, DG, dcarry, d, s); break; // 16 waves
     case 17: bwd_cfg<128, 128, 4, 4, 4>(t, WhhT, Cst, S, DG, dcarry, d, s); break; // 16w 4st
+    case 19: bwd_cfg<128, 128, 2, 4, 4>(t, WhhT, Cst, S, DG, dcarry, d, s); break;  // 8w 4st (128 KiB)
+    case 20: bwd_cfg<128, 128, 2, 4, 5>(t, WhhT, Cst, S, DG, dcarry, d, s); break;  // 8w 5st (160 KiB)
+    case 21: bwd_cfg<64, 128, 2, 2, 6>(t, WhhT, Cst, S, DG, dcarry, d, s); break;   // 4w 6st (144 KiB)
     case 98: bwd_cfg<128, 128, 2, 4, 3, true>(t, WhhT, Cst, S, DG, dcarry, d, s); break;  // timing only
     default: bwd_cfg<128, 128>(t, WhhT, Cst, S, DG, dcarry, d, s); break;
   }

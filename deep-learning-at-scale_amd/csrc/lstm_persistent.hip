@@ -23,6 +23,8 @@
 //    block depend on each other, so row blocks drift freely (no grid barrier), and the
 //    XCD-aware block map puts a row block's NB workgroups on one XCD (speed only).
 //  * every spin is bounded: on timeout the error word is set and all workgroups drain.
+#include <cstdlib>
+
 #include "gemm_core.h"
 #include "kernels.h"
 #include "lstm_layout.h"
@@ -282,7 +284,19 @@ static bool launch_pf(bf16_t* XH, const bf16_t* Wp, float* Cst, bf16_t* S, unsig
     if (d.dbg == 14) f = reinterpret_cast<const void*>(&lstm_fwd_persistent_kernel<KT, NC, 14>);
   }
   void* args[] = {&XH, &Wp, &Cst, &S, &sync, &d};
-  return hipLaunchCooperativeKernel(f, dim3(grid), dim3(256), args, 0u, s) == hipSuccess;
+  // Cooperative launch: the runtime rejects a grid that cannot be co-resident. rocprofv3
+  // (ROCm 7.2) crashes at exit after tracing a cooperative dispatch, so WELLFLOW_COOP=0
+  // (profiling runs) uses a plain launch guarded by the same residency check done here.
+  static const bool coop = [] {
+    const char* v = std::getenv("WELLFLOW_COOP");
+    return v == nullptr || v[0] != '0';
+  }();
+  if (coop) return hipLaunchCooperativeKernel(f, dim3(grid), dim3(256), args, 0u, s) == hipSuccess;
+  int per_cu = 0, dev = 0, cus = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, f, 256, 0) != hipSuccess || hipGetDevice(&dev) != hipSuccess ||
+      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || per_cu * cus < grid)
+    return false;
+  return hipLaunchKernel(f, dim3(grid), dim3(256), args, 0u, s) == hipSuccess;
 }
 
 template <int KT>
