@@ -40,14 +40,18 @@ class DistContext:
         self.device = device or torch.device("cpu")
         self.backend = backend
         self.bucket_bytes = bucket_bytes
+        self.forced = False
 
     # ---------------------------------------------------------------- bootstrap
     @classmethod
     def from_env(cls, backend: str | None = None, timeout_s: float = 600.0,
-                 bucket_bytes: int = 0, device: str | None = None) -> "DistContext":
+                 bucket_bytes: int = 0, device: str | None = None,
+                 force_group: bool = False) -> "DistContext":
         """Read torchrun's RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* and init the group.
 
         Device selection happens BEFORE any CUDA call so each rank pins its own GPU.
+        ``force_group`` creates the process group even at world size 1 (tests of the
+        RCCL path on a one-GPU box); otherwise a single process runs without one.
         """
         world = int(os.environ.get("WORLD_SIZE", "1"))
         rank = int(os.environ.get("RANK", "0"))
@@ -61,7 +65,7 @@ class DistContext:
             dev = torch.device("cuda", local)
         else:
             dev = torch.device("cpu")
-        if world > 1 and not dist.is_initialized():
+        if (world > 1 or force_group) and not dist.is_initialized():
             backend = backend or ("nccl" if use_gpu else "gloo")
             os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
             kw = dict(backend=backend, rank=rank, world_size=world,
@@ -75,7 +79,9 @@ class DistContext:
                 # transport addresses. Namespace every attempt's keys.
                 kw["store"] = dist.PrefixStore(f"wellflow/attempt_{restart}", _base_store(rank, world, timeout_s))
             dist.init_process_group(**kw)
-        return cls(rank, world, local, dev, backend, bucket_bytes)
+        ctx = cls(rank, world, local, dev, backend, bucket_bytes)
+        ctx.forced = bool(force_group)
+        return ctx
 
     @property
     def is_main(self) -> bool:
@@ -83,7 +89,7 @@ class DistContext:
 
     @property
     def distributed(self) -> bool:
-        return self.world_size > 1 and dist.is_initialized()
+        return dist.is_initialized() and (self.world_size > 1 or self.forced)
 
     # ---------------------------------------------------------------- collectives
     def broadcast_(self, t: torch.Tensor, src: int = 0) -> torch.Tensor:
