@@ -168,26 +168,37 @@ def take(table: dict, idx) -> dict:
     return {k: np.asarray(v)[idx] for k, v in table.items()}
 
 
-def make_windows(X: np.ndarray, y: np.ndarray, T: int, groups=None, stride: int = 1):
-    """Sliding windows for sequence models: (X_w [n, T, F], y_w [n]) with y at the last step.
-
-    ``groups`` (per-row series id, rows already in time order inside a group) keeps
-    windows from crossing series boundaries.
-    """
-    n = len(X)
-    if groups is None:
-        groups = np.zeros(n, dtype=np.int64)
+def window_starts(n: int, T: int, groups=None, stride: int = 1) -> np.ndarray:
+    """First row of every length-``T`` window that stays inside one series (``groups`` =
+    per-row series id, rows in time order inside a group)."""
+    g = np.zeros(n, dtype=np.int64) if groups is None else np.asarray(groups)
     starts = []
-    g = np.asarray(groups)
     i = 0
     while i < n:
         j = i
         while j < n and g[j] == g[i]:
             j += 1
-        for s in range(i, j - T + 1, stride):
-            starts.append(s)
+        starts.extend(range(i, j - T + 1, stride))
         i = j
-    starts = np.asarray(starts, dtype=np.int64)
+    return np.asarray(starts, dtype=np.int64)
+
+
+def window_rows(starts: np.ndarray, T: int) -> np.ndarray:
+    """Sorted unique row indices covered by the windows starting at ``starts``."""
+    if len(starts) == 0:
+        return np.zeros((0,), np.int64)
+    return np.unique((starts[:, None] + np.arange(T)[None, :]).ravel())
+
+
+def make_windows(X: np.ndarray, y: np.ndarray, T: int, groups=None, stride: int = 1, starts=None):
+    """Sliding windows for sequence models: (X_w [n, T, F], y_w [n]) with y at the last step.
+
+    ``groups`` (per-row series id, rows already in time order inside a group) keeps
+    windows from crossing series boundaries; ``starts`` (from :func:`window_starts`)
+    overrides the enumeration.
+    """
+    if starts is None:
+        starts = window_starts(len(X), T, groups, stride)
     if len(starts) == 0:
         return np.zeros((0, T, X.shape[1]), np.float32), np.zeros((0,), np.float32)
     idx = starts[:, None] + np.arange(T)[None, :]

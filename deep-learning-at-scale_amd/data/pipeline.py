@@ -18,7 +18,7 @@ import dataclasses
 
 import numpy as np
 
-from .features import FeaturePipeline, make_windows, random_split, take
+from .features import FeaturePipeline, make_windows, random_split, take, window_rows, window_starts
 from .io import load_table
 from .schema import parse_schema
 
@@ -74,24 +74,28 @@ def prepare(cfg) -> Prepared:
     ids, gcol = _group_ids(table, schema, cfg.group_col)
     table, ids = _sort_by_group(table, ids, schema)
     if cfg.model == "lstm":
-        # fit the feature pipeline on the rows that belong to training windows' series
+        # windows are split at random (as the reference split rows); the feature pipeline
+        # is fitted ONLY on the rows that training windows cover
+        T = cfg.seq_len
+        starts = window_starts(n, T, ids)
+        idx = random_split(len(starts), cfg.split, cfg.seed)
         pipe = FeaturePipeline(schema, cfg.target, standardize_target=True)
-        pipe.fit(table)  # vocab/scales over all rows of the file; windows are split below
+        pipe.fit(take(table, window_rows(starts[idx[0]], T)))
         X, y = pipe.transform(table)
-        Xw, yw = make_windows(X, y, cfg.seq_len, ids)
-        idx = random_split(len(Xw), cfg.split, cfg.seed)
+        Xw, yw = make_windows(X, y, T, starts=starts)
         parts = [(Xw[ix], yw[ix]) for ix in idx]
         return Prepared(*parts, n_features=pipe.n_features, pipeline=pipe,
                         info={"group_col": gcol, "windows": len(Xw)})
     if cfg.model == "cnn":
         L, O = cfg.cnn_input_len, cfg.cnn_outputs
+        starts = window_starts(n, L + O, ids)
+        idx = random_split(len(starts), cfg.split, cfg.seed)
         pipe = FeaturePipeline(schema, cfg.target, standardize_target=True)
-        pipe.fit(table)
+        pipe.fit(take(table, window_rows(starts[idx[0]], L + O)))
         y = pipe.target_values(table)
-        seq = np.concatenate([y[:, None]], axis=1)  # univariate (reference input_dim=1)
-        Xw, _ = make_windows(seq, y, L + O, ids)
+        seq = y[:, None]  # univariate (reference input_dim=1)
+        Xw, _ = make_windows(seq, y, L + O, starts=starts)
         X, Y = Xw[:, :L, :], Xw[:, L:, 0]
-        idx = random_split(len(X), cfg.split, cfg.seed)
         parts = [(X[ix], Y[ix]) for ix in idx]
         return Prepared(*parts, n_features=1, pipeline=pipe, n_outputs=O,
                         info={"group_col": gcol, "windows": len(X)})

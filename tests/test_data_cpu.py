@@ -108,3 +108,31 @@ def test_synthetic_batches_are_finite_and_learnable_scale():
     assert x.shape == (64, 32, 16) and y.shape == (64,)
     assert np.isfinite(x.numpy()).all() and np.isfinite(y.numpy()).all()
     assert 0.2 < float(y.std()) < 3.0
+
+
+def test_sequence_pipeline_fits_on_training_windows_only():
+    """LSTM/CNN windows are split at random; scaling statistics and vocabularies must come
+    from the rows the TRAINING windows cover (SURVEY.md A.1 #3), not from the whole file."""
+    import numpy as np
+
+    from wellflow.config import parse_argv
+    from wellflow.data.features import take, window_rows, window_starts, random_split
+    from wellflow.data.pipeline import _group_ids, _sort_by_group, prepare
+    from wellflow.data.io import load_table
+    from wellflow.data.schema import parse_schema
+
+    names = "well,field,t,whp,choke,glr,temp,water_cut,dsp,flow"
+    types = "string,string,int,float,float,float,float,float,float,float"
+    cfg = parse_argv("lstm", [names, types, "flow", "/tmp/x/", "--synth-wells", "4", "--synth-steps", "90",
+                              "--seq-len", "16"])
+    prep = prepare(cfg)
+    schema = parse_schema(names, types)
+    table = load_table("synth", schema, synth_wells=4, synth_steps=90, seed=cfg.seed)
+    ids, _ = _group_ids(table, schema, "")
+    table, ids = _sort_by_group(table, ids, schema)
+    starts = window_starts(len(ids), 16, ids)
+    train_rows = window_rows(starts[random_split(len(starts), cfg.split, cfg.seed)[0]], 16)
+    assert len(train_rows) < len(ids)  # some rows are only in val/test windows
+    y_train = np.asarray(take(table, train_rows)["flow"], np.float32)
+    assert abs(prep.pipeline.y_mean - float(y_train.mean())) < 1e-4
+    assert len(prep.train[0]) + len(prep.val[0]) + len(prep.test[0]) == len(starts)
