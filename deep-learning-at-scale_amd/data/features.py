@@ -203,3 +203,48 @@ def make_windows(X: np.ndarray, y: np.ndarray, T: int, groups=None, stride: int 
         return np.zeros((0, T, X.shape[1]), np.float32), np.zeros((0,), np.float32)
     idx = starts[:, None] + np.arange(T)[None, :]
     return X[idx].astype(np.float32), y[starts + T - 1].astype(np.float32)
+
+
+class SeriesWindows:
+    """Length-``T`` windows over a per-row feature matrix WITHOUT materialising them.
+
+    ``rows`` [n_rows, F] (numpy or a device tensor) + ``starts`` [n_windows]. Indexing
+    returns the gathered batch [len(idx), T, F] (numpy for numpy storage; a device tensor
+    gathered on the GPU for tensor storage), so a dataset costs n_rows x F instead of
+    n_windows x T x F (64x less for the LSTM config) — in host RAM and, after :meth:`to`,
+    resident in HBM.
+    """
+
+    def __init__(self, rows, starts, T: int):
+        self.rows, self.starts, self.T = rows, starts, int(T)
+
+    def __len__(self) -> int:
+        return len(self.starts)
+
+    @property
+    def shape(self):
+        return (len(self.starts), self.T, self.rows.shape[1])
+
+    @property
+    def device(self):
+        return getattr(self.rows, "device", None)
+
+    def __getitem__(self, idx):
+        st = self.starts[idx]
+        if hasattr(st, "unsqueeze"):  # torch
+            import torch
+
+            ar = torch.arange(self.T, device=st.device)
+            return self.rows[st.reshape(-1, 1) + ar]
+        st = np.asarray(st).reshape(-1)
+        return self.rows[st[:, None] + np.arange(self.T)[None, :]]
+
+    def to(self, device):
+        import torch
+
+        rows = torch.as_tensor(self.rows, dtype=torch.float32).to(device)
+        starts = torch.as_tensor(np.asarray(self.starts, np.int64) if not hasattr(self.starts, "to") else self.starts)
+        return SeriesWindows(rows, starts.to(device), self.T)
+
+    def materialize(self):
+        return self[np.arange(len(self.starts))] if not hasattr(self.starts, "to") else self[:]

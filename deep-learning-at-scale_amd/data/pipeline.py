@@ -18,7 +18,7 @@ import dataclasses
 
 import numpy as np
 
-from .features import FeaturePipeline, make_windows, random_split, take, window_rows, window_starts
+from .features import FeaturePipeline, SeriesWindows, make_windows, random_split, take, window_rows, window_starts
 from .io import load_table
 from .schema import parse_schema
 
@@ -82,10 +82,11 @@ def prepare(cfg) -> Prepared:
         pipe = FeaturePipeline(schema, cfg.target, standardize_target=True)
         pipe.fit(take(table, window_rows(starts[idx[0]], T)))
         X, y = pipe.transform(table)
-        Xw, yw = make_windows(X, y, T, starts=starts)
-        parts = [(Xw[ix], yw[ix]) for ix in idx]
+        # lazy windows: rows + start indices, gathered per batch (on the GPU once resident)
+        yw = y[starts + T - 1].astype(np.float32)
+        parts = [(SeriesWindows(X, starts[ix], T), yw[ix]) for ix in idx]
         return Prepared(*parts, n_features=pipe.n_features, pipeline=pipe,
-                        info={"group_col": gcol, "windows": len(Xw)})
+                        info={"group_col": gcol, "windows": len(starts)})
     if cfg.model == "cnn":
         L, O = cfg.cnn_input_len, cfg.cnn_outputs
         starts = window_starts(n, L + O, ids)

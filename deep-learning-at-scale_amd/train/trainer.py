@@ -66,6 +66,8 @@ class History:
 
 
 def _to_dev(a, device):
+    if hasattr(a, "to") and hasattr(a, "starts"):  # data.features.SeriesWindows: rows + starts
+        return a.to(device)
     t = torch.as_tensor(a)
     if t.dtype == torch.float64:
         t = t.float()
@@ -98,7 +100,8 @@ class Trainer:
         idx = np.arange(r, n, w)
         chunk = chunk or getattr(self.eng, "B", 4096) or 4096
         s_loss, s_mse, cnt = 0.0, 0.0, 0
-        Xd = X if torch.is_tensor(X) and X.device == self.eng.device else None
+        Xd = X if (torch.is_tensor(X) or hasattr(X, "starts")) and getattr(X, "device", None) == self.eng.device \
+            else None
         for i in range(0, len(idx), chunk):
             sel = idx[i : i + chunk]
             xb = (Xd[torch.as_tensor(sel, device=Xd.device)] if Xd is not None

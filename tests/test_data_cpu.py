@@ -136,3 +136,24 @@ def test_sequence_pipeline_fits_on_training_windows_only():
     y_train = np.asarray(take(table, train_rows)["flow"], np.float32)
     assert abs(prep.pipeline.y_mean - float(y_train.mean())) < 1e-4
     assert len(prep.train[0]) + len(prep.val[0]) + len(prep.test[0]) == len(starts)
+
+
+def test_series_windows_match_materialised_windows():
+    import numpy as np
+    import torch
+
+    from wellflow.data.features import SeriesWindows, make_windows, window_starts
+
+    rng = np.random.default_rng(0)
+    X = rng.standard_normal((50, 3)).astype(np.float32)
+    y = rng.standard_normal(50).astype(np.float32)
+    g = np.repeat([0, 1, 2], [20, 12, 18])
+    st = window_starts(50, 7, g)
+    Xw, yw = make_windows(X, y, 7, g)
+    sw = SeriesWindows(X, st, 7)
+    assert sw.shape == Xw.shape and len(sw) == len(Xw)
+    sel = np.array([5, 0, 17, 3])
+    assert np.array_equal(sw[sel], Xw[sel])
+    dev = sw.to("cpu")
+    assert torch.equal(dev[torch.as_tensor(sel)], torch.as_tensor(Xw[sel]))
+    assert np.array_equal(sw.materialize(), Xw)
