@@ -22,37 +22,37 @@
 
 namespace wf {
 
-// XH[t][b][0:KX] = [x[b][t][0:F], 1, 0, ...]. One thread per (b, t) row with t fastest:
-// the F-float reads of neighbouring threads are contiguous and each thread writes whole
-// 16-B chunks (KX*2 bytes = full 128-B lines for KX = 64).
+// XH[t][b][0:KX] = [x[b][t][0:F], 1, 0, ...]. One lane per 16-B chunk of a destination
+// row (KX/8 lanes per row, rows of one timestep consecutive): every store instruction
+// writes whole 128-B lines of 8 rows instead of 64 partial lines (the thread-per-row
+// version ran at 1.6 TB/s).
 __global__ void lstm_pack_x_kernel(const float* __restrict__ x, bf16_t* __restrict__ XH,
                                    LstmDims d) {
-  const int KA = d.KX + d.H;
-  const long total = (long)d.T * d.B;
+  const int KA = d.KX + d.H, CPR = d.KX >> 3;  // 16-B chunks per row
+  const long total = (long)d.T * d.B * CPR;
   for (long idx = blockIdx.x * (long)blockDim.x + threadIdx.x; idx < total;
        idx += (long)gridDim.x * blockDim.x) {
-    const int t = idx % d.T;
-    const long b = idx / d.T;
+    const int c = (int)(idx % CPR) * 8;
+    const long row = idx / CPR;  // = t * B + b
+    const long b = row % d.B;
+    const int t = (int)(row / d.B);
     const float* src = x + (b * d.T + t) * d.F;
-    bf16_t* dst = XH + ((long)t * d.B + b) * KA;
-    for (int c = 0; c < d.KX; c += 8) {
-      unsigned pk[4];
+    unsigned pk[4];
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const int k0 = c + 2 * e, k1 = k0 + 1;
-        const float v0 = k0 < d.F ? src[k0] : (k0 == d.F ? 1.f : 0.f);
-        const float v1 = k1 < d.F ? src[k1] : (k1 == d.F ? 1.f : 0.f);
-        pk[e] = (unsigned)f2bf(v0) | ((unsigned)f2bf(v1) << 16);
-      }
-      *reinterpret_cast<uint4*>(dst + c) = make_uint4(pk[0], pk[1], pk[2], pk[3]);
+    for (int e = 0; e < 4; ++e) {
+      const int k0 = c + 2 * e, k1 = k0 + 1;
+      const float v0 = k0 < d.F ? src[k0] : (k0 == d.F ? 1.f : 0.f);
+      const float v1 = k1 < d.F ? src[k1] : (k1 == d.F ? 1.f : 0.f);
+      pk[e] = (unsigned)f2bf(v0) | ((unsigned)f2bf(v1) << 16);
     }
+    *reinterpret_cast<uint4*>(XH + row * KA + c) = make_uint4(pk[0], pk[1], pk[2], pk[3]);
   }
 }
 
 void launch_lstm_pack_x(const float* x, bf16_t* XH, LstmDims d, hipStream_t s) {
-  const long total = (long)d.T * d.B;
+  const long total = (long)d.T * d.B * (d.KX >> 3);
   int blocks = (int)((total + 255) / 256);
-  if (blocks > 8192) blocks = 8192;
+  if (blocks > 16384) blocks = 16384;
   hipLaunchKernelGGL(lstm_pack_x_kernel, dim3(blocks), dim3(256), 0, s, x, XH, d);
 }
 
