@@ -98,5 +98,8 @@ def test_lstm_graph_replay_equals_eager():
         step_e()
         g.replay()
     torch.cuda.synchronize()
+    # split-K fp32 atomics make the summation order (not the math) vary between runs, and
+    # Adam divides by sqrt(v): near-zero gradients turn 1e-7 grad noise into ~1e-6 param
+    # noise. A broken capture (stale buffer, missing launch) moves params by >= lr = 1e-3.
     d = (eng_e.params - eng_g.params).abs().max().item()
-    assert d <= 1e-5 * eng_e.params.abs().max().item(), d
+    assert d <= 5e-5, d
