@@ -271,11 +271,12 @@ void lstm_backward_dw(const at::Tensor& WhhT, const at::Tensor& XH, const at::Te
     e.outF = fp(gW);
     e.ldo = KA;
     e.atomic = 1;
-    // WELLFLOW_DW_BIG: 0 = 128x128 tile, 1 (default) = 256x128 8-wave, 2 = 128x288 4-wave
-    // (tools/tune_lstm.py, B = 8192: 1.33 / 1.60 ms at split-K 32)
+    // WELLFLOW_DW_BIG: 0 = 128x128 tile, 1 = 256x128 8-wave, 2 = 128x288 4-wave,
+    // 3 (default) = 256x192 8-wave (tools/tune_lstm.py, B = 8192, split-K 32:
+    // 1.35 / 1.60 / 1.28 ms for 1 / 2 / 3); shapes a tile cannot take fall back to 256x128
     static const int big = [] {
       const char* v = std::getenv("WELLFLOW_DW_BIG");
-      return v == nullptr ? 1 : std::atoi(v);
+      return v == nullptr ? 3 : std::atoi(v);
     }();
     e.big_tile = big;
     const bf16_t* A = bfp(DG) + (size_t)t0 * B * G;

@@ -217,10 +217,27 @@ static void launch_dw_288(const bf16_t* A, long lda, const bf16_t* B, long ldb, 
                      N, kchunk, tiles, e.outF, e.ldo, e.alpha);
 }
 
+// 256x192, 8 waves of 64x96, 2-stage ring (112 KiB): N = 576 = 3 x 192 exactly, and 22 % fewer
+// operand bytes per MFMA than 256x128 (rotation-swizzled 192-wide MN image).
+static void launch_dw_192(const bf16_t* A, long lda, const bf16_t* B, long ldb, int M, int N, int K,
+                          int ksplit, const GemmEpilogue& e, hipStream_t s) {
+  constexpr int BM = 256, BN = 192;
+  const int tiles = (M / BM) * (N / BN);
+  int nsplit = ksplit;
+  while (nsplit > 1 && K % (64 * nsplit) != 0) --nsplit;
+  const int kchunk = K / nsplit;
+  hipLaunchKernelGGL((gemm_dw_kernel<BM, BN, 2, 4, 2>), dim3(tiles * nsplit), dim3(512), 0, s, A, lda, B, ldb,
+                     N, kchunk, tiles, e.outF, e.ldo, e.alpha);
+}
+
 void launch_gemm(const bf16_t* A, long lda, int a_mn, const bf16_t* B, long ldb, int b_mn, int M,
                  int N, int K, int ksplit, const GemmEpilogue& e, hipStream_t s, bool glds_ok) {
   if (a_mn && b_mn && glds_ok && e.atomic && e.big_tile == 2 && M % 128 == 0 && N % 288 == 0 && K % 64 == 0) {
     launch_dw_288(A, lda, B, ldb, M, N, K, ksplit < 1 ? 1 : ksplit, e, s);
+    return;
+  }
+  if (a_mn && b_mn && glds_ok && e.atomic && e.big_tile == 3 && M % 256 == 0 && N % 192 == 0 && K % 64 == 0) {
+    launch_dw_192(A, lda, B, ldb, M, N, K, ksplit < 1 ? 1 : ksplit, e, s);
     return;
   }
   if (a_mn && b_mn && glds_ok && e.atomic && e.big_tile && M % 256 == 0 && K % 64 == 0) {

@@ -42,7 +42,7 @@ def gemm(A, B, M, N, K, *, a_mn=False, lda=None, b_mn=False, ldb=None, outF=None
     """out = act(alpha * A(M,K) B(N,K)^T + beta*out + bias) (* mask), on MFMA.
 
     ``a_mn``/``b_mn`` select the MN-contiguous layout (X(r,k) = p[k*ld + r]).
-    ``tile`` (MN x MN split-K atomic only): 1 = 256x128 8-wave tile, 2 = 128x288 tile.
+    ``tile`` (MN x MN split-K atomic only): 1 = 256x128 8-wave tile, 2 = 128x288, 3 = 256x192.
     """
     if lda is None:
         lda = M if a_mn else K

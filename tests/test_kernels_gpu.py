@@ -218,3 +218,22 @@ def test_lstm_persistent_forward_matches_per_step(B, H, T):
     for name, a, b in zip(("XH", "C", "S"), (eng.XH, eng.Cst, eng.S), ref):
         d = (a.float() - b.float()).abs().max().item()
         assert d <= 2e-2, (name, d)
+
+
+@pytest.mark.parametrize("tile", [0, 1, 2, 3])
+@pytest.mark.parametrize("ksplit", [1, 4])
+def test_weight_gradient_tiles_match_reference(tile, ksplit):
+    """Every split-K MN x MN weight-gradient tile (128x128, 256x128, 128x288 and the
+    rotation-swizzled 256x192) against fp32 torch, on the LSTM dW shape family."""
+    from wellflow.ops.native import gemm
+
+    torch.manual_seed(7)
+    M, N, K = 512, 576, 2048
+    Amn = _bf(torch.randn(K, M, device=DEV))                     # A(m, k) = Amn[k, m]
+    Bmn = _bf(torch.randn(K, N, device=DEV) * torch.linspace(0.5, 2, N, device=DEV))
+    out = torch.zeros(M, N, device=DEV)
+    gemm(Amn, Bmn, M, N, K, a_mn=True, b_mn=True, outF=out, atomic=True, ksplit=ksplit, tile=tile)
+    torch.cuda.synchronize()
+    ref = Amn.float().t() @ Bmn.float()
+    err = (out - ref).abs().max().item()
+    assert err < 2e-3 * ref.abs().max().item(), (tile, err)
