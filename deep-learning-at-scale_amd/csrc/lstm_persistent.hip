@@ -50,17 +50,19 @@ __global__ __launch_bounds__(256, 1) void lstm_fwd_persistent_kernel(
   constexpr int KA = 32 * KT;
   constexpr int KS = KA / 64;                // 64-deep k-steps = A pieces per wave per chunk
   constexpr int ABYTES = PF_ROWS * KA * 2;   // chunk of [x_t | 1 | h_t-1] rows: KS [32][64] images
-  constexpr int CBYTES = PF_ROWS * 64 * 4;   // chunk of c_t-1 (FN blocks of the workgroup's units)
-  constexpr int LPT = KS + ((DBG & 8) ? 0 : 2);  // LDS-DMA instructions per wave per chunk
+  constexpr int LPT = KS;                    // LDS-DMA instructions per wave per chunk
+  // k-tiles whose weight fragments live in AGPRs (the rest in VGPRs): 256 AGPRs minus the
+  // 32 accumulator registers = 14 k-tiles x 4 column tiles x 4 registers
+  constexpr int KTA = KT < 14 ? KT : 14;
   constexpr int NSTORE = (DBG & 4) ? 1 : 7;  // stores per wave per chunk: 2 C, 4 S, 1 h
   // Distinct static LDS objects per ring slot: the compiler then proves the slot being
   // filled by LDS-DMA disjoint from the slots being read, and inserts no vmcnt(0) of its own.
   // EXACTLY ONE static LDS variable, compile-time offsets for every ring slot, the h staging
-  // area and the flag word (slot k at k*SLOT: [A chunk | c_{t-1} chunk]). With several LDS
+  // area and the flag word (slot k at k*SLOT: one A chunk). With several LDS
   // variables the LDS lowering gives each its own alias scope, the waitcnt pass then tracks
   // the LDS-DMA into the ring and guards the first read of every slot with vmcnt(0) — which
   // drained the whole prefetch ring every chunk (measured: loads no longer overlapped MFMA).
-  constexpr int SLOT = ABYTES + CBYTES;
+  constexpr int SLOT = ABYTES;
   constexpr int HOFF = 3 * SLOT, FOFF = HOFF + PF_ROWS * 64 * 2;
   __shared__ __attribute__((aligned(16))) char smem[FOFF + 16];
   // h_t staging [32][64] bf16, accessed only through inline asm (32-bit LDS address)
@@ -84,6 +86,15 @@ __global__ __launch_bounds__(256, 1) void lstm_fwd_persistent_kernel(
   gu32* cnt = (gu32*)(sync + 16 + 16 * m);
   // XH as a buffer resource for the 16-B sc1 h stores (byte offsets < 2^31: checked on the host)
   const __amdgpu_buffer_rsrc_t xh_rsrc = __builtin_amdgcn_make_buffer_rsrc(XH, 0, 0x7FFFFFFF, 0x00020000);
+  // DBG & 16: timeline stamps (s_memrealtime, 100 MHz) of step PF_STAMP_T, wave 0 lane 0 of
+  // every workgroup, into sync + 4096 words (64 slots per workgroup; diagnostics only)
+  constexpr int PF_STAMP_T = 10;
+  unsigned long long* stamps = reinterpret_cast<unsigned long long*>(sync + 4096) + blockIdx.x * 64;
+  auto stamp = [&](int t, int slot) {
+    if constexpr ((DBG & 16) != 0) {
+      if (t == PF_STAMP_T && threadIdx.x == 0) stamps[slot] = __builtin_amdgcn_s_memrealtime();
+    }
+  };
 
   // ---- prologue: stationary weight fragments (B operand: lane holds col l15, k 8g..8g+7)
   bf16x8 w[KT][4];
@@ -106,7 +117,18 @@ __global__ __launch_bounds__(256, 1) void lstm_fwd_persistent_kernel(
 #pragma unroll
   for (int kk = 0; kk < 2; ++kk) fa[kk] = l15 * 128 + (((kk * 4 + g) ^ ((l15 >> 1) & 7)) << 4);
 
+  // c_{t-1} of the workgroup's 8 chunks stays in registers for the whole sequence (a queue
+  // the chunk loop rotates: chunk c reads cq[0] and appends its c_t), so the forward never
+  // re-reads the cell state it wrote (16.8 MB per step at B = 8192); C is still stored for
+  // the backward. c_{-1} = 0.
+  f32x4 cq[NC][2];
+#pragma unroll
+  for (int q = 0; q < NC; ++q)
+#pragma unroll
+    for (int i = 0; i < 2; ++i) cq[q][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+
   for (int t = 0; t < d.T; ++t) {
+    stamp(t, 0);
     if (t > 0) {
       // ---- publish step t-1 (every wave drained its sc1 h stores) and wait for the row block
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -138,6 +160,7 @@ __global__ __launch_bounds__(256, 1) void lstm_fwd_persistent_kernel(
       asm volatile("" ::: "memory");
       if (*lflag == 0) return;  // uniform: every wave reads the same word
     }
+    stamp(t, 1);
     // opaque per-step copy of the row origin: stops the compiler hoisting every chunk's
     // lane addresses out of the time loop (NC x 64-bit offsets live across the whole
     // kernel pushed the H = 512, NC = 8 build into spills)
@@ -145,7 +168,6 @@ __global__ __launch_bounds__(256, 1) void lstm_fwd_persistent_kernel(
     asm volatile("" : "+s"(rb));
     // per-step uniform bases (row block origin folded in) + per-lane constant offsets
     // (loff_c / loff_s / loff_h), so every chunk address is base + compile-time stride
-    const float* cprev = Cst + (size_t)t * Bp * H + (size_t)(rb >> 4) * HB * 256;
     float* cnext = Cst + (size_t)(t + 1) * Bp * H + (size_t)(rb >> 4) * HB * 256;
     bf16_t* St = S + (size_t)t * Bp * G + (size_t)(rb >> 4) * HB * 1024;
     const char* abase = reinterpret_cast<const char*>(XH + ((size_t)t * d.B + rb) * KA) + aoff;
@@ -155,17 +177,11 @@ __global__ __launch_bounds__(256, 1) void lstm_fwd_persistent_kernel(
     auto issue = [&](int c, auto sc) {  // chunk c into ring slot SL (= c % 3)
       constexpr int SL = decltype(sc)::value;
       char* ra = smem + SL * SLOT;
-      char* rcb = ra + ABYTES;
       const char* src = abase + (size_t)c * ABYTES;
 #pragma unroll
       for (int s = 0; s < KS; ++s)
         __builtin_amdgcn_global_load_lds((const void*)(src + s * 128), (lds_void*)(ra + s * 4096 + wid * 1024),
                                          16, 0, 0);
-#pragma unroll
-      for (int j = 0; j < ((DBG & 8) ? 0 : 2); ++j) {
-        __builtin_amdgcn_global_load_lds((const void*)(cprev + (2 * c + j) * HB * 256 + loff_c),
-                                         (lds_void*)(rcb + (wid * 2 + j) * 1024), 16, 0, 0);
-      }
     };
     issue(0, std::integral_constant<int, 0>{});
     if constexpr (NC > 1) issue(1, std::integral_constant<int, 1>{});
@@ -174,6 +190,7 @@ __global__ __launch_bounds__(256, 1) void lstm_fwd_persistent_kernel(
     // register pressure of a 3-chunk kernel; a fully unrolled NC = 8 spilled)
     auto chunk = [&](int c, auto pc) {
       constexpr int P = decltype(pc)::value;
+      stamp(t, 2 + 5 * c);
       // vector-memory ops issued after chunk c's LDS-DMA (top of c issues c+2, then stores)
       if (c == 0) {
         if (NC > 1) wait_vmcnt<LPT>(); else wait_vmcnt<0>();
@@ -187,40 +204,67 @@ __global__ __launch_bounds__(256, 1) void lstm_fwd_persistent_kernel(
       __builtin_amdgcn_s_barrier();
       asm volatile("" ::: "memory");
       __builtin_amdgcn_sched_barrier(0);  // keep each chunk's code (and live ranges) to itself
+      stamp(t, 3 + 5 * c);
       if (c + 2 < NC) issue(c + 2, std::integral_constant<int, (P + 2) % 3>{});
       const char* cur = smem + P * SLOT;
-      const char* cpl = cur + ABYTES;
 
       f32x4 acc[2][4];
 #pragma unroll
       for (int i = 0; i < 2; ++i)
 #pragma unroll
         for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+      // MFMAs in inline asm with explicit register classes: weights of k-tiles < KTA as AGPR
+      // operands, the rest as VGPR operands, accumulators in AGPRs. With the builtin the
+      // register allocator shuffled the 288 weight registers through v_accvgpr_read/mov copies
+      // before every use and single-buffered the A fragments (timeline: 2.5 us per chunk of
+      // MFMA work that issues in ~1 us). A fragments of k-tile kt+1 are read during kt.
+      bf16x8 a[2][2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) a[0][i] = *reinterpret_cast<const bf16x8*>(cur + i * 2048 + fa[0]);
+      if constexpr ((DBG & 32) != 0) {
+        a[1][0] = a[0][0];
+        a[1][1] = a[0][1];
+      }
 #pragma unroll
       for (int kt = 0; kt < KT; ++kt) {
-        bf16x8 a[2];
+        if (kt + 1 < KT && !(DBG & 32)) {  // DBG & 32: timing only, no fragment reads
+#pragma unroll
+          for (int i = 0; i < 2; ++i)
+            a[(kt + 1) & 1][i] =
+                *reinterpret_cast<const bf16x8*>(cur + ((kt + 1) >> 1) * 4096 + i * 2048 + fa[(kt + 1) & 1]);
+        }
 #pragma unroll
         for (int i = 0; i < 2; ++i)
-          a[i] = *reinterpret_cast<const bf16x8*>(cur + (kt >> 1) * 4096 + i * 2048 + fa[kt & 1]);
 #pragma unroll
-        for (int i = 0; i < 2; ++i)
-#pragma unroll
-          for (int j = 0; j < 4; ++j)
-            if constexpr (!(DBG & 2))
-              acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], w[kt][j], acc[i][j], 0, 0, 0);
+          for (int j = 0; j < 4; ++j) {
+            if constexpr (!(DBG & 2)) {
+              if (kt == 0)  // the accumulators were just zeroed by v_accvgpr_write: wait states
+                asm volatile("s_nop 2\n\tv_mfma_f32_16x16x32_bf16 %0, %1, %2, %0"
+                             : "+a"(acc[i][j]) : "v"(a[kt & 1][i]), "a"(w[kt][j]));
+              else if (kt < KTA)
+                asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc[i][j]) : "v"(a[kt & 1][i]), "a"(w[kt][j]));
+              else
+                asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc[i][j]) : "v"(a[kt & 1][i]), "v"(w[kt][j]));
+            }
+          }
       }
+      // the epilogue reads the accumulators with VALU: cover the last MFMAs' pipeline
+      // (the compiler pads nothing after inline asm)
+      asm volatile("s_nop 7\n\ts_nop 7" ::: "memory");
 
+      if constexpr ((DBG & 16) != 0) {  // MFMA completion: consume a result before stamping
+        float sink = acc[1][3][3];
+        asm volatile("" ::"v"(sink));
+        stamp(t, 4 + 5 * c);
+      }
       // ---- fused cell epilogue (lane: chunk rows 16i + 4g + r, unit u; gates acc[i][0..3])
       // both c_{t-1} tiles into registers BEFORE the first h_t write to LDS: read lazily
       // after it, the compiler guarded the read with a vmcnt(0) (waiting for the ring's
       // in-flight LDS-DMA); the empty asm pins the loads here
-      f32x4 cpr[2];
-#pragma unroll
-      for (int i = 0; i < 2; ++i) cpr[i] = *reinterpret_cast<const f32x4*>(cpl + (wid * 2 + i) * 1024 + lane * 16);
-      asm volatile("" : "+v"(cpr[0]), "+v"(cpr[1]));
+      f32x4 cnew[2];
 #pragma unroll
       for (int i = 0; i < 2; ++i) {
-        const float cpv[4] = {cpr[i][0], cpr[i][1], cpr[i][2], cpr[i][3]};
+        const float cpv[4] = {cq[0][i][0], cq[0][i][1], cq[0][i][2], cq[0][i][3]};
         float cv[4];
         unsigned pk[8];
 #pragma unroll
@@ -231,6 +275,7 @@ __global__ __launch_bounds__(256, 1) void lstm_fwd_persistent_kernel(
           const float og = sigmoidf_(acc[i][3][r]);
           const float cn = fg * cpv[r] + ig * gg;
           cv[r] = cn;
+          cnew[i][r] = cn;
           pk[2 * r] = (unsigned)f2bf(ig) | ((unsigned)f2bf(fg) << 16);
           pk[2 * r + 1] = (unsigned)f2bf(gg) | ((unsigned)f2bf(og) << 16);
           // h staging store in asm: a compiler-visible LDS write here is guarded by a
@@ -247,6 +292,13 @@ __global__ __launch_bounds__(256, 1) void lstm_fwd_persistent_kernel(
           sp[1] = make_uint4(pk[4], pk[5], pk[6], pk[7]);
         }
       }
+      stamp(t, 5 + 5 * c);
+#pragma unroll
+      for (int q = 0; q + 1 < NC; ++q)
+#pragma unroll
+        for (int i = 0; i < 2; ++i) cq[q][i] = cq[q + 1][i];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) cq[NC - 1][i] = cnew[i];
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();
       asm volatile("" ::: "memory");
@@ -261,6 +313,7 @@ __global__ __launch_bounds__(256, 1) void lstm_fwd_persistent_kernel(
                      : "memory");
         __builtin_amdgcn_raw_buffer_store_b128(vv, xh_rsrc, loff_h, hsoff + c * PF_ROWS * KA * 2, 16 /* sc1 */);
       }
+      stamp(t, 6 + 5 * c);
     };
     using S0 = std::integral_constant<int, 0>;
     using S1 = std::integral_constant<int, 1>;
@@ -280,8 +333,9 @@ static bool launch_pf(bf16_t* XH, const bf16_t* Wp, float* Cst, bf16_t* S, unsig
   if constexpr (KT == 18 && NC == 8) {  // timing-only diagnostic builds (WELLFLOW_PF_DBG >= 2)
     if (d.dbg == 2) f = reinterpret_cast<const void*>(&lstm_fwd_persistent_kernel<KT, NC, 2>);
     if (d.dbg == 4) f = reinterpret_cast<const void*>(&lstm_fwd_persistent_kernel<KT, NC, 4>);
-    if (d.dbg == 8) f = reinterpret_cast<const void*>(&lstm_fwd_persistent_kernel<KT, NC, 8>);
     if (d.dbg == 14) f = reinterpret_cast<const void*>(&lstm_fwd_persistent_kernel<KT, NC, 14>);
+    if (d.dbg == 16) f = reinterpret_cast<const void*>(&lstm_fwd_persistent_kernel<KT, NC, 16>);
+    if (d.dbg == 48) f = reinterpret_cast<const void*>(&lstm_fwd_persistent_kernel<KT, NC, 48>);
   }
   void* args[] = {&XH, &Wp, &Cst, &S, &sync, &d};
   // Cooperative launch: the runtime rejects a grid that cannot be co-resident. rocprofv3
