@@ -51,9 +51,9 @@ __global__ __launch_bounds__(256, 1) void lstm_fwd_persistent_kernel(
   constexpr int KS = KA / 64;                // 64-deep k-steps = A pieces per wave per chunk
   constexpr int ABYTES = PF_ROWS * KA * 2;   // chunk of [x_t | 1 | h_t-1] rows: KS [32][64] images
   constexpr int LPT = KS;                    // LDS-DMA instructions per wave per chunk
-  // k-tiles whose weight fragments live in AGPRs (the rest in VGPRs): 256 AGPRs minus the
-  // 32 accumulator registers = 14 k-tiles x 4 column tiles x 4 registers
-  constexpr int KTA = KT < 14 ? KT : 14;
+  // k-tiles whose weight fragments live in AGPRs (the rest in VGPRs): 256 AGPRs minus 2 x 32
+  // accumulator registers (this chunk + the pipelined previous one) = 12 k-tiles x 4 x 4
+  constexpr int KTA = KT < 12 ? KT : 12;
   constexpr int NSTORE = (DBG & 4) ? 1 : 7;  // stores per wave per chunk: 2 C, 4 S, 1 h
   // Distinct static LDS objects per ring slot: the compiler then proves the slot being
   // filled by LDS-DMA disjoint from the slots being read, and inserts no vmcnt(0) of its own.
@@ -127,6 +127,12 @@ __global__ __launch_bounds__(256, 1) void lstm_fwd_persistent_kernel(
 #pragma unroll
     for (int i = 0; i < 2; ++i) cq[q][i] = f32x4{0.f, 0.f, 0.f, 0.f};
 
+  f32x4 accp[2][4];  // gate pre-activations of the previous chunk (software pipeline)
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) accp[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
   for (int t = 0; t < d.T; ++t) {
     stamp(t, 0);
     if (t > 0) {
@@ -173,6 +179,58 @@ __global__ __launch_bounds__(256, 1) void lstm_fwd_persistent_kernel(
     const char* abase = reinterpret_cast<const char*>(XH + ((size_t)t * d.B + rb) * KA) + aoff;
     const int hsoff = (int)((((size_t)(t + 1) * d.B + rb) * KA + 64 + n * 64) * 2);
 
+    // cell epilogue element (row-tile i, row r) of the carried chunk: accp + c_{t-1} = cq[0]
+    auto epi_elem = [&](int i, int r, float (&cv)[2][4], unsigned (&pk)[2][8], unsigned (&hv)[2][4]) {
+      const float ig = sigmoidf_(accp[i][0][r]);
+      const float fg = sigmoidf_(accp[i][1][r]);
+      const float gg = tanhf_(accp[i][2][r]);
+      const float og = sigmoidf_(accp[i][3][r]);
+      const float cn = fg * cq[0][i][r] + ig * gg;
+      cv[i][r] = cn;
+      pk[i][2 * r] = (unsigned)f2bf(ig) | ((unsigned)f2bf(fg) << 16);
+      pk[i][2 * r + 1] = (unsigned)f2bf(gg) | ((unsigned)f2bf(og) << 16);
+      hv[i][r] = f2bf(og * tanhf_(cn));
+    };
+    // stores of chunk e (C, S: NSTORE - 1 per wave), h staged in LDS, c-queue rotation
+    auto epi_store = [&](int e, const float (&cv)[2][4], const unsigned (&pk)[2][8], const unsigned (&hv)[2][4]) {
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          // LDS staging writes in asm: compiler-visible LDS writes are guarded by a vmcnt(0)
+          // (the waitcnt pass orders every LDS access after in-flight LDS-DMA)
+          asm volatile("ds_write_b16 %0, %1" ::"v"(hb_lds + 2u * ((i * 16 + 4 * g + r) * 64 + wid * 16 + l15)),
+                       "v"(hv[i][r])
+                       : "memory");
+        if constexpr (!(DBG & 4)) {
+          *reinterpret_cast<float4*>(cnext + (2 * e + i) * HB * 256 + loff_c) =
+              make_float4(cv[i][0], cv[i][1], cv[i][2], cv[i][3]);
+          uint4* sp = reinterpret_cast<uint4*>(St + (2 * e + i) * HB * 1024 + loff_s);
+          sp[0] = make_uint4(pk[i][0], pk[i][1], pk[i][2], pk[i][3]);
+          sp[1] = make_uint4(pk[i][4], pk[i][5], pk[i][6], pk[i][7]);
+        }
+      }
+#pragma unroll
+      for (int q = 0; q + 1 < NC; ++q)
+#pragma unroll
+        for (int i = 0; i < 2; ++i) cq[q][i] = cq[q + 1][i];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) cq[NC - 1][i] = f32x4{cv[i][0], cv[i][1], cv[i][2], cv[i][3]};
+    };
+    // publish chunk e's h rows: 32 rows x 128 B, one 16-B write-through (sc1) buffer store per
+    // thread (Guideline 16 R1: no release fence; 8-B sc1 stores cost 0.4 ms more, measured)
+    auto publish = [&](int e) {
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      u32x4 vv;  // row threadIdx>>3, 16-B column threadIdx&7 of the [32][64] bf16 tile
+      asm volatile("ds_read_b128 %0, %1\n\ts_waitcnt lgkmcnt(0)"
+                   : "=&v"(vv)
+                   : "v"(hb_lds + 16u * threadIdx.x)
+                   : "memory");
+      __builtin_amdgcn_raw_buffer_store_b128(vv, xh_rsrc, loff_h, hsoff + e * PF_ROWS * KA * 2, 16 /* sc1 */);
+    };
+
     // chunk c -> ring slot c % 3: KS A pieces + this wave's 2 FN blocks of c_{t-1}
     auto issue = [&](int c, auto sc) {  // chunk c into ring slot SL (= c % 3)
       constexpr int SL = decltype(sc)::value;
@@ -192,10 +250,14 @@ __global__ __launch_bounds__(256, 1) void lstm_fwd_persistent_kernel(
       constexpr int P = decltype(pc)::value;
       stamp(t, 2 + 5 * c);
       // vector-memory ops issued after chunk c's LDS-DMA (top of c issues c+2, then stores)
+      // (issue order: prologue glds 0, 1; chunk k: glds k+2, then the stores of chunk k-1,
+      // NSTORE per wave, none in chunk 0)
       if (c == 0) {
         if (NC > 1) wait_vmcnt<LPT>(); else wait_vmcnt<0>();
       } else if (c == 1) {
-        if (NC > 2) wait_vmcnt<LPT + NSTORE>(); else wait_vmcnt<NSTORE>();
+        if (NC > 2) wait_vmcnt<LPT>(); else wait_vmcnt<0>();
+      } else if (c == 2) {
+        if (NC > 3) wait_vmcnt<LPT + NSTORE>(); else wait_vmcnt<NSTORE>();
       } else if (c + 1 < NC) {
         wait_vmcnt<2 * NSTORE + LPT>();
       } else {
@@ -218,16 +280,21 @@ __global__ __launch_bounds__(256, 1) void lstm_fwd_persistent_kernel(
       // register allocator shuffled the 288 weight registers through v_accvgpr_read/mov copies
       // before every use and single-buffered the A fragments (timeline: 2.5 us per chunk of
       // MFMA work that issues in ~1 us). A fragments of k-tile kt+1 are read during kt.
+      // Software pipeline: the cell epilogue of chunk c-1 (accp, cq[0]) is computed INSIDE
+      // this loop, one (row-tile, row) element per k-tile, so its VALU / transcendental work
+      // issues between the MFMAs (chunk 0 computes on leftovers and discards the result).
       bf16x8 a[2][2];
+      float cv[2][4];
+      unsigned pk[2][8], hv[2][4];
 #pragma unroll
       for (int i = 0; i < 2; ++i) a[0][i] = *reinterpret_cast<const bf16x8*>(cur + i * 2048 + fa[0]);
       if constexpr ((DBG & 32) != 0) {
         a[1][0] = a[0][0];
         a[1][1] = a[0][1];
       }
-#pragma unroll
-      for (int kt = 0; kt < KT; ++kt) {
-        if (kt + 1 < KT && !(DBG & 32)) {  // DBG & 32: timing only, no fragment reads
+      static_for<0, KT>([&](auto kc) {
+        constexpr int kt = decltype(kc)::value;
+        if constexpr (kt + 1 < KT && !(DBG & 32)) {  // DBG & 32: timing only, no fragment reads
 #pragma unroll
           for (int i = 0; i < 2; ++i)
             a[(kt + 1) & 1][i] =
@@ -238,81 +305,34 @@ __global__ __launch_bounds__(256, 1) void lstm_fwd_persistent_kernel(
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
             if constexpr (!(DBG & 2)) {
-              if (kt == 0)  // the accumulators were just zeroed by v_accvgpr_write: wait states
+              if constexpr (kt == 0)  // the accumulators were just zeroed by v_accvgpr_write
                 asm volatile("s_nop 2\n\tv_mfma_f32_16x16x32_bf16 %0, %1, %2, %0"
                              : "+a"(acc[i][j]) : "v"(a[kt & 1][i]), "a"(w[kt][j]));
-              else if (kt < KTA)
+              else if constexpr (kt < KTA)
                 asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc[i][j]) : "v"(a[kt & 1][i]), "a"(w[kt][j]));
               else
                 asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc[i][j]) : "v"(a[kt & 1][i]), "v"(w[kt][j]));
             }
           }
-      }
+        if constexpr (kt < 8) epi_elem(kt >> 2, kt & 3, cv, pk, hv);
+      });
       // the epilogue reads the accumulators with VALU: cover the last MFMAs' pipeline
       // (the compiler pads nothing after inline asm)
       asm volatile("s_nop 7\n\ts_nop 7" ::: "memory");
-
       if constexpr ((DBG & 16) != 0) {  // MFMA completion: consume a result before stamping
         float sink = acc[1][3][3];
         asm volatile("" ::"v"(sink));
         stamp(t, 4 + 5 * c);
       }
-      // ---- fused cell epilogue (lane: chunk rows 16i + 4g + r, unit u; gates acc[i][0..3])
-      // both c_{t-1} tiles into registers BEFORE the first h_t write to LDS: read lazily
-      // after it, the compiler guarded the read with a vmcnt(0) (waiting for the ring's
-      // in-flight LDS-DMA); the empty asm pins the loads here
-      f32x4 cnew[2];
-#pragma unroll
-      for (int i = 0; i < 2; ++i) {
-        const float cpv[4] = {cq[0][i][0], cq[0][i][1], cq[0][i][2], cq[0][i][3]};
-        float cv[4];
-        unsigned pk[8];
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const float ig = sigmoidf_(acc[i][0][r]);
-          const float fg = sigmoidf_(acc[i][1][r]);
-          const float gg = tanhf_(acc[i][2][r]);
-          const float og = sigmoidf_(acc[i][3][r]);
-          const float cn = fg * cpv[r] + ig * gg;
-          cv[r] = cn;
-          cnew[i][r] = cn;
-          pk[2 * r] = (unsigned)f2bf(ig) | ((unsigned)f2bf(fg) << 16);
-          pk[2 * r + 1] = (unsigned)f2bf(gg) | ((unsigned)f2bf(og) << 16);
-          // h staging store in asm: a compiler-visible LDS write here is guarded by a
-          // vmcnt(0) (the waitcnt pass orders every LDS access after in-flight LDS-DMA)
-          const unsigned hv = f2bf(og * tanhf_(cn));
-          asm volatile("ds_write_b16 %0, %1" ::"v"(hb_lds + 2u * ((i * 16 + 4 * g + r) * 64 + wid * 16 + l15)),
-                       "v"(hv)
-                       : "memory");
-        }
-        if constexpr (!(DBG & 4)) {
-          *reinterpret_cast<float4*>(cnext + (2 * c + i) * HB * 256 + loff_c) = make_float4(cv[0], cv[1], cv[2], cv[3]);
-          uint4* sp = reinterpret_cast<uint4*>(St + (2 * c + i) * HB * 1024 + loff_s);
-          sp[0] = make_uint4(pk[0], pk[1], pk[2], pk[3]);
-          sp[1] = make_uint4(pk[4], pk[5], pk[6], pk[7]);
-        }
+      if (c > 0) {
+        epi_store(c - 1, cv, pk, hv);
+        stamp(t, 5 + 5 * c);
+        publish(c - 1);
       }
-      stamp(t, 5 + 5 * c);
 #pragma unroll
-      for (int q = 0; q + 1 < NC; ++q)
+      for (int i = 0; i < 2; ++i)
 #pragma unroll
-        for (int i = 0; i < 2; ++i) cq[q][i] = cq[q + 1][i];
-#pragma unroll
-      for (int i = 0; i < 2; ++i) cq[NC - 1][i] = cnew[i];
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();
-      asm volatile("" ::: "memory");
-      // ---- publish the chunk's h rows: 32 rows x 128 B, one 16-B write-through (sc1)
-      // buffer store per thread (Guideline 16 R1: no release fence; 8-B sc1 stores cost
-      // 0.4 ms per forward more, measured)
-      {
-        u32x4 vv;  // row threadIdx>>3, 16-B column threadIdx&7 of the [32][64] bf16 tile
-        asm volatile("ds_read_b128 %0, %1\n\ts_waitcnt lgkmcnt(0)"
-                     : "=&v"(vv)
-                     : "v"(hb_lds + 16u * threadIdx.x)
-                     : "memory");
-        __builtin_amdgcn_raw_buffer_store_b128(vv, xh_rsrc, loff_h, hsoff + c * PF_ROWS * KA * 2, 16 /* sc1 */);
-      }
+        for (int j = 0; j < 4; ++j) accp[i][j] = acc[i][j];
       stamp(t, 6 + 5 * c);
     };
     using S0 = std::integral_constant<int, 0>;
@@ -322,6 +342,14 @@ __global__ __launch_bounds__(256, 1) void lstm_fwd_persistent_kernel(
       chunk(c, S0{});
       if (c + 1 < NC) chunk(c + 1, S1{});
       if (c + 2 < NC) chunk(c + 2, S2{});
+    }
+    {  // drain: the last chunk's epilogue
+      float cv[2][4];
+      unsigned pk[2][8], hv[2][4];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) epi_elem(e >> 2, e & 3, cv, pk, hv);
+      epi_store(NC - 1, cv, pk, hv);
+      publish(NC - 1);
     }
   }
 }

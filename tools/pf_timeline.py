@@ -28,7 +28,7 @@ names = ["sync_end"] + [f"c{c}_{k}" for c in range(8) for k in ("top", "after_wa
 print("step 10, us since step start (mean / max over 256 workgroups)")
 for i, nm in enumerate(names, start=1):
     print(f"{nm:16s} {rel[:, i].mean():8.2f} {rel[:, i].max():8.2f}")
-d = np.diff(rel[:, 2:42].reshape(256, 8, 5), axis=2).mean(axis=(0, 1))
-print("per chunk mean: wait %.2f  mfma %.2f  epilogue %.2f  publish %.2f us" % tuple(d))
+d = np.diff(rel[:, 2:42].reshape(256, 8, 5)[:, 1:, :], axis=2).mean(axis=(0, 1))  # chunks >= 1
+print("per chunk mean (c >= 1): wait %.2f  mfma %.2f  store %.2f  publish %.2f us" % tuple(d))
 top = rel[:, 2:42:5]
 print("chunk-to-chunk mean %.2f us" % np.diff(top, axis=1).mean())
