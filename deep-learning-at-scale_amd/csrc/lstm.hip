@@ -150,7 +150,7 @@ void launch_lstm_fwd_step(int t, bf16_t* XH, const bf16_t* Wp, float* Cst, bf16_
 // Cell backward for the 4 rows (mrow0 + 4*(lane>>4) + r) x unit u of step t held by this
 // lane, given dh for them: reads the lane's fragment-native S / C / dc-carry slots with
 // 16-B vector accesses, updates the carry and writes the gate gradients into DG[t]
-// (row-major, permuted columns: it is the next GEMM's A operand).
+// (row-major, dg_col order: it is the next GEMM's A operand and the dW GEMM's M side).
 template <bool LITE = false>  // LITE: timing-only (no c_t / dc-carry traffic; wrong results)
 __device__ __forceinline__ void cell_bwd4(int t, int mrow0, int u, int lane, const float (&dh)[4],
                                           const float* __restrict__ Cst,
@@ -182,11 +182,10 @@ __device__ __forceinline__ void cell_bwd4(int t, int mrow0, int u, int lane, con
     nk[r] = dc * fg;
     const int m = mrow0 + 4 * (lane >> 4) + r;
     if (m < d.B) {
-      bf16_t* row = dgt + (size_t)m * G;
-      row[gate_col(0, u)] = f2bf(dc * gg * ig * (1.f - ig));
-      row[gate_col(1, u)] = f2bf(dc * pv[r] * fg * (1.f - fg));
-      row[gate_col(2, u)] = f2bf(dc * ig * (1.f - gg * gg));
-      row[gate_col(3, u)] = f2bf(dh[r] * tc * og * (1.f - og));
+      uint2 v;
+      v.x = (unsigned)f2bf(dc * gg * ig * (1.f - ig)) | ((unsigned)f2bf(dc * pv[r] * fg * (1.f - fg)) << 16);
+      v.y = (unsigned)f2bf(dc * ig * (1.f - gg * gg)) | ((unsigned)f2bf(dh[r] * tc * og * (1.f - og)) << 16);
+      *reinterpret_cast<uint2*>(dgt + (size_t)m * G + dg_col(0, u)) = v;
     }
   }
   if (!LITE) *dcp = make_float4(nk[0], nk[1], nk[2], nk[3]);
@@ -302,7 +301,8 @@ void launch_lstm_bwd_step(int t, const bf16_t* WhhT, const float* Cst, const bf1
   }
 }
 
-// fp32 master W [G][KA] (permuted rows) -> bf16 Wp [G][KA] and WhhT [H][G].
+// fp32 master W [G][KA] (rows in dg_col order) -> bf16 Wp [G][KA] (rows in gate_col order,
+// the forward's) and WhhT [H][G] (columns in dg_col order, the backward's).
 __global__ void lstm_pack_weights_kernel(const float* __restrict__ W, bf16_t* __restrict__ Wp,
                                          bf16_t* __restrict__ WhhT, LstmDims d) {
   const int KA = d.KX + d.H, G = 4 * d.H;
@@ -311,7 +311,7 @@ __global__ void lstm_pack_weights_kernel(const float* __restrict__ W, bf16_t* __
        idx += (long)gridDim.x * blockDim.x) {
     const int k = idx % KA, p = idx / KA;
     const bf16_t v = f2bf(W[idx]);
-    Wp[idx] = v;
+    Wp[(size_t)gate_col(p & 3, p >> 2) * KA + k] = v;
     if (k >= d.KX) WhhT[(size_t)(k - d.KX) * G + p] = v;
   }
 }

@@ -4,7 +4,14 @@
 
 namespace wf {
 
+// Forward gate-column order (rows of the packed bf16 weights Wp, columns of the forward
+// GEMM): a 64-column tile holds gates i,f,g,o of 16 consecutive units, so one lane's four
+// 16x16 MFMA fragments carry all four gates of its unit.
 __device__ __forceinline__ int gate_col(int gate, int u) { return (u >> 4) * 64 + gate * 16 + (u & 15); }
+// Backward gate-column order (columns of DG, rows of the fp32 master W / its gradient,
+// columns of WhhT): unit-major, gate-minor. A lane's four gate gradients of one (row,
+// unit) are ONE 8-B store (16 lanes = a full 128-B line) instead of four 2-B stores.
+__host__ __device__ __forceinline__ int dg_col(int gate, int u) { return 4 * u + gate; }
 
 // Fragment-native (FN) layout of the per-(row, unit) state the backward pass re-reads
 // (C, S, dc carry): 16x16 blocks, block (m>>4, u>>4) row-major over H/16 unit blocks;

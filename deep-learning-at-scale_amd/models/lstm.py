@@ -11,7 +11,7 @@ Two implementations with one parameter layout:
   Parameters live in a flat fp32 master buffer (so the optimizer and the DP all-reduce
   are one launch / one collective each); bf16 shadows are repacked after every update.
 
-Flat layout (``LstmLayout``): ``[Wcat (4H x KA, gate-permuted rows) | w_out (H) | b_out (1)]``
+Flat layout (``LstmLayout``): ``[Wcat (4H x KA, unit-major rows 4u+g) | w_out (H) | b_out (1)]``
 with ``Wcat = [W_ih | b_ih + b_hh | 0 ... | W_hh]`` (KA = KX + H, KX = 64-aligned, the
 bias rides on a constant-1 input column).
 """
@@ -61,11 +61,11 @@ class LstmLayout:
         return W, w_out, b_out
 
     def perm(self) -> torch.Tensor:
-        """perm[p] = natural gate-row (gate*H + unit) stored at permuted row p."""
+        """perm[p] = natural gate-row (gate*H + unit) stored at master row p = 4*unit + gate
+        (csrc/lstm_layout.h dg_col: the backward's gate-gradient column order; the
+        forward's bf16 weights are re-permuted by the pack kernel)."""
         p = torch.arange(self.G)
-        unit = (p >> 6) * 16 + (p & 15)
-        gate = (p >> 4) & 3
-        return gate * self.hidden + unit
+        return (p & 3) * self.hidden + (p >> 2)
 
 
 class LSTMRegressor(nn.Module):

@@ -52,10 +52,10 @@ def test_lstm_perm_is_bijection_and_groups_gates():
     lay = LstmLayout(16, 512)
     p = lay.perm()
     assert sorted(p.tolist()) == list(range(2048))
-    # a wave's 64-column tile = gates i,f,g,o of the same 16 units
-    tile = p[:64].view(4, 16)
-    assert (tile // 512).tolist() == [[g] * 16 for g in range(4)]
-    assert ((tile % 512) == torch.arange(16)).all()
+    # unit-major: master rows 4u..4u+3 = gates i,f,g,o of unit u
+    tile = p[:64].view(16, 4)
+    assert (tile // 512).tolist() == [list(range(4))] * 16
+    assert ((tile % 512) == torch.arange(16).view(16, 1)).all()
     flat = init_lstm_flat(16, 512)
     W, _, _ = lay.views(flat)
     assert torch.count_nonzero(W[:, 17:64]) == 0  # padding columns stay zero
