@@ -186,7 +186,7 @@ bool lstm_forward_persistent(const at::Tensor& XH, const at::Tensor& Wp, const a
 void lstm_backward(const at::Tensor& WhhT, const at::Tensor& XH, const at::Tensor& Cst,
                    const at::Tensor& S, const at::Tensor& DG, const at::Tensor& dcarry,
                    const at::Tensor& dy, const at::Tensor& w_out, int64_t B, int64_t T, int64_t F,
-                   int64_t KX, int64_t H, int64_t variant) {
+                   int64_t KX, int64_t H, int64_t variant, const c10::optional<at::Tensor>& sync) {
   auto d = lstm_dims(B, T, F, KX, H);
   d.bwd_variant = (int)variant;
   check_lstm_state(XH, Cst, S, d);
@@ -202,6 +202,16 @@ void lstm_backward(const at::Tensor& WhhT, const at::Tensor& XH, const at::Tenso
   check_extent(w_out, H, "w_out");
   const c10::hip::OptionalHIPGuardMasqueradingAsCUDA guard(XH.device());
   auto s = cur_stream();
+  if (sync.has_value()) {  // step T-1, then the persistent chain (tools/pb_time.py)
+    check_t(*sync, at::kInt, "sync");
+    wf::launch_lstm_bwd_step(d.T - 1, bfp(WhhT), fp(Cst), bfp(S), bfp(DG), fp(dcarry), fp(dy),
+                             fp(w_out), d, s);
+    TORCH_CHECK(wf::launch_lstm_bwd_persistent(bfp(WhhT), fp(Cst), bfp(S), bfp(DG), fp(dcarry),
+                                               reinterpret_cast<unsigned*>(sync->data_ptr<int>()),
+                                               sync->numel(), d, s),
+                "persistent backward refused this shape");
+    return;
+  }
   for (int t = d.T - 1; t >= 0; --t)
     wf::launch_lstm_bwd_step(t, bfp(WhhT), fp(Cst), bfp(S), bfp(DG), fp(dcarry), fp(dy),
                              fp(w_out), d, s);
@@ -245,7 +255,7 @@ void lstm_backward_dw(const at::Tensor& WhhT, const at::Tensor& XH, const at::Te
                       const at::Tensor& S, const at::Tensor& DG, const at::Tensor& dcarry,
                       const at::Tensor& dy, const at::Tensor& w_out, const at::Tensor& gW,
                       int64_t B, int64_t T, int64_t F, int64_t KX, int64_t H, int64_t variant,
-                      int64_t chunk, int64_t ksplit) {
+                      int64_t chunk, int64_t ksplit, const c10::optional<at::Tensor>& sync) {
   auto d = lstm_dims(B, T, F, KX, H);
   d.bwd_variant = (int)variant;
   check_lstm_state(XH, Cst, S, d);
@@ -289,9 +299,21 @@ void lstm_backward_dw(const at::Tensor& WhhT, const at::Tensor& XH, const at::Te
   };
 
   if (chunk <= 0) {
-    for (int t = d.T - 1; t >= 0; --t)
-      wf::launch_lstm_bwd_step(t, bfp(WhhT), fp(Cst), bfp(S), bfp(DG), fp(dcarry), fp(dy),
-                               fp(w_out), d, main);
+    // step T-1 (dh from the head), then steps T-2 .. 0 in one persistent launch when a sync
+    // buffer is given and the shape fits (lstm_persistent_bwd.hip), else per-step kernels
+    wf::launch_lstm_bwd_step(d.T - 1, bfp(WhhT), fp(Cst), bfp(S), bfp(DG), fp(dcarry), fp(dy),
+                             fp(w_out), d, main);
+    bool done = false;
+    if (sync.has_value()) {
+      check_t(*sync, at::kInt, "sync");
+      done = wf::launch_lstm_bwd_persistent(bfp(WhhT), fp(Cst), bfp(S), bfp(DG), fp(dcarry),
+                                            reinterpret_cast<unsigned*>(sync->data_ptr<int>()),
+                                            sync->numel(), d, main);
+    }
+    if (!done)
+      for (int t = d.T - 2; t >= 0; --t)
+        wf::launch_lstm_bwd_step(t, bfp(WhhT), fp(Cst), bfp(S), bfp(DG), fp(dcarry), fp(dy),
+                                 fp(w_out), d, main);
     dw(0, d.T, main);
     return;
   }

@@ -49,6 +49,12 @@ void launch_lstm_fwd_step(int t, bf16_t* XH, const bf16_t* Wp, float* Cst, bf16_
 int lstm_persistent_sync_words(int row_blocks);
 bool launch_lstm_fwd_persistent(bf16_t* XH, const bf16_t* Wp, float* Cst, bf16_t* S, unsigned* sync,
                                 long sync_words, LstmDims d, hipStream_t s);
+// Backward steps T-2 .. 0 in ONE cooperative launch (lstm_persistent_bwd.hip), after step
+// T-1 ran (launch_lstm_bwd_step(T-1, ...)). Same `sync` contract as the forward (word 0 =
+// spin timeout). Returns false (nothing launched) when the shape / device cannot host it.
+bool launch_lstm_bwd_persistent(const bf16_t* WhhT, const float* Cst, const bf16_t* S, bf16_t* DG,
+                                const float* dcarry, unsigned* sync, long sync_words, LstmDims d,
+                                hipStream_t s);
 void launch_lstm_bwd_step(int t, const bf16_t* WhhT, const float* Cst, const bf16_t* S,
                           bf16_t* DG, float* dcarry, const float* dy, const float* w_out,
                           LstmDims d, hipStream_t s);

@@ -1,0 +1,392 @@
+// wellflow — persistent LSTM backward (BPTT): ONE launch runs steps T-2 .. 0
+// (SURVEY.md §2.4 K14 "lstm_seq_bwd (persistent)"; the forward twin is lstm_persistent.hip).
+//
+// Why: the per-step backward (lstm.hip, 63 launches) re-streams its W_hh tile from L2 every
+// step (512 KB per 128x128 tile, 134 MB per step over the grid), and round-trips the fp32
+// dc carry through HBM (2 x 16.8 MB per step at B = 8192). Here
+//  * grid = (B / (16 * NRT)) row blocks x (H / 64) unit blocks, one 256-thread workgroup
+//    (4 waves, one per SIMD) per CU, co-resident (cooperative launch). Workgroup (m, n)
+//    owns rows [16*NRT*m, +16*NRT) x units [64n, 64n + 64) for the whole sequence, i.e.
+//    the 256 contiguous DG columns 4u + gate of those units (dg_col order).
+//  * dh_t = DG_{t+1} W_hh is split over K by wave: wave w multiplies DG columns
+//    [w*H, (w+1)*H) by the matching rows of W_hh, for all 64 units. Its W_hh^T slice
+//    (64 units x H k's) stays in AGPRs for the whole sequence (H/2 = 256 registers at
+//    H = 512), and its A fragments come straight from L2 into VGPRs (no LDS staging: no
+//    other wave reads them). The 4 partial 16x64 dh tiles are summed through LDS, each
+//    wave then owning one 16-unit tile for the cell backward.
+//  * the dc carry of the workgroup's rows x units lives in LDS for the whole sequence
+//    (it never touches HBM); c_{t-1} and the saved gates S_t are read once (non-temporal,
+//    prefetched two row tiles ahead), DG_t is written once with 16-B write-through (sc1)
+//    stores (lane pairs exchange halves so each store is a whole 16-B (row, 2 units) run).
+//  * hand-off (cdna_hip_programming.md Guideline 16, recipe R1, as in the forward): every
+//    wave drains its stores (vmcnt(0)), workgroup barrier, ONE lane adds to the row
+//    block's arrival counter (agent scope); consumers poll relaxed with s_sleep, then ONE
+//    agent-scope acquire, then plain loads of DG_{t+1}. Only the H/64 workgroups of one
+//    row block depend on each other; every spin is bounded (error word 0, all drain).
+// Step T-1 (dh from the regression head) is lstm_bwd_last_kernel in lstm.hip.
+#include <cstdlib>
+
+#include "gemm_core.h"
+#include "kernels.h"
+#include "lstm_layout.h"
+
+namespace wf {
+
+namespace {
+constexpr unsigned PB_SPIN_LIMIT = 1u << 21;
+constexpr int PB_MAX_RT = 16;  // row tiles per workgroup (dc carry in registers: 4 VGPRs each)
+typedef __attribute__((address_space(1))) unsigned gu32;
+}  // namespace
+
+// KT = H / 32 k-tiles per wave (each wave's K quarter of G = 4H is H wide); NRT row tiles
+// of 16 rows per workgroup (compile-time: the row-tile loop is fully unrolled so the dc
+// carry, the prefetch rings and every vmcnt below are static).
+// DBG (timing-only builds, results wrong; WELLFLOW_PF_DBG at H = 512, NRT = 16):
+// 1 no hand-off wait, 2 no MFMA, 4 no DG stores, 8 no S / c loads, 16 no A loads.
+template <int KT, int NRT, int DBG = 0>
+__global__ __launch_bounds__(256, 1) void lstm_bwd_persistent_kernel(
+    const bf16_t* __restrict__ WhhT, const float* __restrict__ Cst, const bf16_t* __restrict__ S,
+    bf16_t* __restrict__ DG, const float* __restrict__ dcarry, unsigned* __restrict__ sync, LstmDims d) {
+  constexpr int H = 32 * KT, G = 4 * H, NB = H / 64, HB = H / 16;
+  constexpr int KS = KT / 2;             // 64-wide k-steps per wave per row tile
+  constexpr int WSLOT = 16 * KT * 64;    // bytes of one wave's A tile: 16 rows x H k (bf16)
+  constexpr int RING = 4 * 2 * WSLOT;    // [wave][2 slots]
+  constexpr int RED = RING;              // partial sums [parity][src wave][unit tile][lane] x 16 B
+  constexpr int FLAG = RED + (1 * 16 + 0 * 4 + 0) * 1024;  // slot [1][0][0]: never written (own tile)
+  // ONE static LDS object (see lstm_persistent.hip: with several, the waitcnt pass guards LDS
+  // accesses behind the LDS-DMA with vmcnt(0)); LDS writes go through inline asm.
+  __shared__ __attribute__((aligned(16))) char smem[RED + 2 * 16 * 1024];
+  typedef __attribute__((address_space(3))) char lds_char;
+  const unsigned lds0 = (unsigned)(uintptr_t)((lds_char*)smem);
+
+  const int Bp = fn_rows(d.B);
+  const int lane = threadIdx.x & 63, l15 = lane & 15, g = lane >> 4;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int L = xcd_remap(blockIdx.x, gridDim.x);
+  const int m = L / NB, n = L % NB;
+  const int row0 = m * 16 * NRT;
+  const int ue = n * 64 + wid * 16 + l15;  // unit of this lane's cell backward
+  const bool even = (l15 & 1) == 0;
+  gu32* err = (gu32*)(sync);
+  gu32* cnt = (gu32*)(sync + 16 + 16 * m);
+
+  // ---- prologue: stationary W_hh^T fragments (B operand: lane = unit col l15, k 8g..8g+7)
+  bf16x8 w[KT][4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const bf16_t* wr = WhhT + (size_t)(n * 64 + j * 16 + l15) * G + wid * H + 8 * g;
+#pragma unroll
+    for (int kt = 0; kt < KT; ++kt) w[kt][j] = *reinterpret_cast<const bf16x8*>(wr + 32 * kt);
+  }
+  // dc carry of step T-1 (lstm_bwd_last_kernel): registers for the whole sequence
+  f32x4 dcr[NRT];
+#pragma unroll
+  for (int rt = 0; rt < NRT; ++rt)
+    dcr[rt] = *reinterpret_cast<const f32x4*>(dcarry + fn_block(row0 + rt * 16, ue, H) * 256 + lane * 4);
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_waitcnt(0xF70);  // vmcnt(0)
+  __builtin_amdgcn_sched_barrier(0);
+
+  // ---- per-lane constant offsets
+  // A (DG_{t+1}) staging: one LDS-DMA instruction = 8 rows x 128 B (full lines) of the wave's
+  // K quarter; LDS image per 64-k step: [16 rows][8 x 16-B chunks], chunk c of row r in slot
+  // c ^ ((r >> 1) & 7), so the fragment reads below are conflict-free (gemm_core.h K_CONTIG);
+  // the swizzle moves onto the per-lane SOURCE address (the DMA writes LDS lane-linearly).
+  const int dr = lane >> 3;  // row within the 8-row half written by this lane
+  const int a_src = dr * G + wid * H + 8 * ((lane & 7) ^ ((dr >> 1) & 7));          // h = 0 (rows 0-7)
+  const int a_src1 = (8 + dr) * G + wid * H + 8 * ((lane & 7) ^ (((8 + dr) >> 1) & 7));  // h = 1
+  const int a_vo = a_src * 2, a_vo1 = a_src1 * 2;
+  const unsigned a_lds = lds0 + wid * 2 * WSLOT;  // this wave's ring
+  int fa[2];  // fragment byte offsets inside a 64-k step image, k-tile half 0 / 1
+#pragma unroll
+  for (int hf = 0; hf < 2; ++hf) fa[hf] = l15 * 128 + (((4 * hf + g) ^ ((l15 >> 1) & 7)) << 4);
+  const int s_lane = ue / 16 * 1024 + lane * 16;                    // FN S slot (block column ue>>4)
+  const int c_lane = ue / 16 * 256 + lane * 4;                      // FN C slot
+  const int ue2 = even ? ue : ue - 1;                               // first unit of this lane's 16-B run
+  const int st_lane = ((4 * g + (even ? 0 : 1)) * G + 4 * ue2) * 2;  // byte offset (row 4g + r0, col 4*ue2)
+  const size_t s_row = (size_t)(row0 >> 4) * HB * 1024 + s_lane, c_row = (size_t)(row0 >> 4) * HB * 256 + c_lane;
+
+  // saved gates + c_{t-1} (HBM): 3-slot register ring, row tile rt in slot rt % 3, issued two
+  // tiles ahead; tiles 0 and 1 of a step are issued before its hand-off wait (they do not
+  // depend on it). No register of an in-flight load is ever moved.
+  // Every address below is buffer-resource based: a 32-bit per-lane constant (s_vo / c_vo /
+  // a_src) plus scalar (per step / per tile) parts, so the fully unrolled tile loop keeps no
+  // per-tile 64-bit addresses live in VGPRs.
+  const int s_vo = (int)(s_row * 2), c_vo = (int)(c_row * 4);
+  u32x4 sq0[3], sq1[3], cq[3];
+  auto load_sc = [&](int t, auto rc, auto slot) {
+    constexpr int RT = decltype(rc)::value, Q = decltype(slot)::value;
+    if constexpr ((DBG & 8) != 0) {
+      if (t < d.T - 2 || RT > 1) return;
+    }
+    const __amdgpu_buffer_rsrc_t sr = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<bf16_t*>(S) + (size_t)t * Bp * G, 0, 0x7FFFFFFF, 0x00020000);
+    const __amdgpu_buffer_rsrc_t cr = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<float*>(Cst) + (size_t)t * Bp * H, 0, 0x7FFFFFFF, 0x00020000);
+    constexpr int SO = RT * HB * 1024 * 2, CO = RT * HB * 256 * 4;
+    sq0[Q] = __builtin_amdgcn_raw_buffer_load_b128(sr, s_vo, SO, 2 /* nt */);
+    sq1[Q] = __builtin_amdgcn_raw_buffer_load_b128(sr, s_vo + 16, SO, 2 /* nt */);
+    cq[Q] = __builtin_amdgcn_raw_buffer_load_b128(cr, c_vo, CO, 2 /* nt */);
+  };
+
+  for (int s = 0; s < d.T - 1; ++s) {
+    const int t = d.T - 2 - s;
+    if (s > 0) {
+      // ---- publish step s-1 (every wave drained its DG stores) and wait for the row block
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      load_sc(t, std::integral_constant<int, 0>{}, std::integral_constant<int, 0>{});
+      if constexpr (NRT > 1) load_sc(t, std::integral_constant<int, 1>{}, std::integral_constant<int, 1>{});
+      __builtin_amdgcn_sched_barrier(0);
+      if (threadIdx.x == 0) {
+        __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const unsigned target = (unsigned)(NB * s);
+        int ok = 1;
+        unsigned spins = 0;
+        while (!(DBG & 1) && __hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+          if (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) {
+            ok = 0;
+            break;
+          }
+          if (++spins > PB_SPIN_LIMIT) {
+            __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            ok = 0;
+            break;
+          }
+          __builtin_amdgcn_s_sleep(2);
+        }
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        asm volatile("ds_write_b32 %0, %1" ::"v"(lds0 + FLAG), "v"(ok) : "memory");
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      int okv;
+      asm volatile("ds_read_b32 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(okv) : "v"(lds0 + FLAG) : "memory");
+      if (__builtin_amdgcn_readfirstlane(okv) == 0) return;  // uniform
+    } else {
+      load_sc(t, std::integral_constant<int, 0>{}, std::integral_constant<int, 0>{});
+      if constexpr (NRT > 1) load_sc(t, std::integral_constant<int, 1>{}, std::integral_constant<int, 1>{});
+    }
+
+    const __amdgpu_buffer_rsrc_t a_rsrc =
+        __builtin_amdgcn_make_buffer_rsrc(DG + ((size_t)(t + 1) * d.B + row0) * G, 0, 0x7FFFFFFF, 0x00020000);
+    const __amdgpu_buffer_rsrc_t dg_rsrc =
+        __builtin_amdgcn_make_buffer_rsrc(DG + (size_t)t * d.B * G, 0, 0x7FFFFFFF, 0x00020000);
+    const int st_base = row0 * G * 2 + st_lane;
+    // A tile rt of this wave -> ring slot rt & 1: KS k-steps x 2 row halves, 1 KB each
+    auto issue_a = [&](auto rc) {
+      constexpr int RT = decltype(rc)::value;
+      if constexpr ((DBG & 16) != 0) {
+        if (RT > 1) return;
+      }
+      const unsigned dst = a_lds + (RT & 1) * WSLOT;
+      static_for<0, KS>([&](auto kc) {
+        constexpr int ks = decltype(kc)::value;
+        (void)a_rsrc;
+        // (the instruction offset would also move the LDS address: the k-step goes into soffset)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(a_rsrc, (lds_void*)(uintptr_t)(dst + ks * 2048), 16, a_vo,
+                                                 RT * 16 * G * 2 + ks * 128, 0, 0);
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(a_rsrc, (lds_void*)(uintptr_t)(dst + ks * 2048 + 1024), 16,
+                                                 a_vo1, RT * 16 * G * 2 + ks * 128, 0, 0);
+      });
+    };
+    constexpr int NA = ((DBG & 16) != 0) ? 0 : 2 * KS;  // DMA instructions per A tile
+    constexpr int NSC = ((DBG & 8) != 0) ? 0 : 3;       // S / c loads per tile
+    constexpr int NST = ((DBG & 4) != 0) ? 0 : 2;       // DG stores per tile
+    issue_a(std::integral_constant<int, 0>{});
+
+    static_for<0, NRT>([&](auto rc) {
+      constexpr int RT = decltype(rc)::value, K = RT % 3, P = RT & 1;
+      // ---- issue: A of RT + 1 (LDS-DMA), then S / c of RT + 2 (or of the next step)
+      if constexpr (RT + 1 < NRT) issue_a(std::integral_constant<int, RT + 1>{});
+      __builtin_amdgcn_sched_barrier(0);
+      if constexpr (RT + 2 < NRT) load_sc(t, std::integral_constant<int, RT + 2>{}, std::integral_constant<int, (K + 2) % 3>{});
+      __builtin_amdgcn_sched_barrier(0);
+      // ---- wait for A(RT): everything issued after it may stay in flight
+      // (tile RT issues: DMA(RT + 1) if RT + 1 < NRT, S / c(RT + 2) if RT + 2 < NRT, 2 stores)
+      constexpr int AFTER_PREV = (RT >= 1 && RT + 1 < NRT ? NSC : 0) + NST;  // rest of tile RT-1
+      constexpr int AFTER_CUR = (RT + 1 < NRT ? NA : 0) + (RT + 2 < NRT ? NSC : 0);
+      if constexpr (RT == 0)
+        wait_vmcnt<AFTER_CUR>();
+      else
+        wait_vmcnt<AFTER_PREV + AFTER_CUR>();
+      const unsigned cur = a_lds + P * WSLOT;
+
+      f32x4 acc[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+      bf16x8 a[2];
+      asm volatile("ds_read_b128 %0, %1" : "=v"(a[0]) : "v"(cur + fa[0]) : "memory");
+      static_for<0, KT>([&](auto kc) {
+        constexpr int kt = decltype(kc)::value;
+        (void)acc;  // odr-use outside the asm operands: clang does not capture them implicitly
+        (void)w;
+        if constexpr (kt + 1 < KT)
+          asm volatile("ds_read_b128 %0, %1 offset:%2"
+                       : "=v"(a[(kt + 1) & 1])
+                       : "v"(cur + fa[(kt + 1) & 1]), "i"(((kt + 1) >> 1) * 2048)
+                       : "memory");
+        if constexpr (kt + 1 < KT)
+          asm volatile("s_waitcnt lgkmcnt(1)" ::: "memory");
+        else
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          if constexpr (!(DBG & 2)) {
+            asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+v"(acc[j]) : "v"(a[kt & 1]), "a"(w[kt][j]));
+          }
+        }
+      });
+      // VALU / LDS reads of MFMA results: cover the pipeline (nothing is padded after asm)
+      asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 3" ::: "memory");
+
+      // ---- K-split partials -> LDS (own tile stays in registers); wave w sums unit tile w
+      const unsigned rbase = lds0 + RED + (P * 4 + wid) * 4 * 1024 + lane * 16;  // red[P][wid][.][lane]
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        if (j != wid) asm volatile("ds_write_b128 %0, %1 offset:%2" ::"v"(rbase), "v"(acc[j]), "i"(j * 1024) : "memory");
+      __builtin_amdgcn_sched_barrier(0);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      const unsigned rd_base = lds0 + RED + wid * 1024 + lane * 16;  // red[.][.][wid][lane]
+      f32x4 dh4 = wid == 0 ? acc[0] : wid == 1 ? acc[1] : wid == 2 ? acc[2] : acc[3];
+static_for<0, 4>([&](auto wc) {
+        constexpr int w2 = decltype(wc)::value;
+        (void)dh4;
+        if (w2 != wid) {
+          f32x4 pv;
+          asm volatile("ds_read_b128 %0, %1 offset:%2\n\ts_waitcnt lgkmcnt(0)"
+                       : "=v"(pv)
+                       : "v"(rd_base), "i"((P * 4 + w2) * 4 * 1024)
+                       : "memory");
+          dh4 += pv;
+        }
+      });
+
+      // ---- cell backward of rows 4g + r (r = 0..3) x unit ue (as cell_bwd4 in lstm.hip)
+      const u32x4 s0 = sq0[K], s1 = sq1[K], c4 = cq[K];
+      const unsigned pk[8] = {s0[0], s0[1], s0[2], s0[3], s1[0], s1[1], s1[2], s1[3]};
+      const float pv[4] = {__uint_as_float(c4[0]), __uint_as_float(c4[1]), __uint_as_float(c4[2]),
+                           __uint_as_float(c4[3])};
+      const f32x4 kv = dcr[RT];
+      f32x4 nk;
+      unsigned v[4][2];  // gate gradients of row r: (di | df), (dg | do)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float ig = bf2f((bf16_t)(pk[2 * r] & 0xffff)), fg = bf2f((bf16_t)(pk[2 * r] >> 16));
+        const float gg = bf2f((bf16_t)(pk[2 * r + 1] & 0xffff)), og = bf2f((bf16_t)(pk[2 * r + 1] >> 16));
+        const float tc = tanhf_(fg * pv[r] + ig * gg);
+        const float dh = dh4[r];
+        const float dc = kv[r] + dh * og * (1.f - tc * tc);
+        nk[r] = dc * fg;
+        v[r][0] = (unsigned)f2bf(dc * gg * ig * (1.f - ig)) | ((unsigned)f2bf(dc * pv[r] * fg * (1.f - fg)) << 16);
+        v[r][1] = (unsigned)f2bf(dc * ig * (1.f - gg * gg)) | ((unsigned)f2bf(dh * tc * og * (1.f - og)) << 16);
+      }
+      dcr[RT] = nk;
+      // lane pair (2i, 2i+1) = units (u, u+1): the even lane stores rows 0, 2 and the odd lane
+      // rows 1, 3 of both units, each a 16-B run [4 gates of u | 4 gates of u+1]
+      unsigned o[4];
+      {
+        const unsigned snd[4] = {even ? v[1][0] : v[0][0], even ? v[1][1] : v[0][1], even ? v[3][0] : v[2][0],
+                                 even ? v[3][1] : v[2][1]};
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          o[i] = (unsigned)__builtin_amdgcn_mov_dpp((int)snd[i], 0xB1, 0xF, 0xF, false);  // quad_perm [1,0,3,2]
+      }
+      u32x4 lo, hi;
+      if (even) {
+        lo = u32x4{v[0][0], v[0][1], o[0], o[1]};  // row 4g + 0: units u, u+1
+        hi = u32x4{v[2][0], v[2][1], o[2], o[3]};  // row 4g + 2
+      } else {
+        lo = u32x4{o[0], o[1], v[1][0], v[1][1]};  // row 4g + 1: units u-1, u
+        hi = u32x4{o[2], o[3], v[3][0], v[3][1]};  // row 4g + 3
+      }
+      constexpr int SOFF = RT * 16 * G * 2;
+      if constexpr ((DBG & 4) != 0) {
+        if (lo[0] == 0x7fc07fc1u && hi[1] == 0x7fc07fc1u) dcr[RT][0] = 1.f;  // keep the values live
+      } else {
+        __builtin_amdgcn_raw_buffer_store_b128(lo, dg_rsrc, st_base, SOFF, 16 /* sc1 */);
+        __builtin_amdgcn_raw_buffer_store_b128(hi, dg_rsrc, st_base, SOFF + 2 * G * 2, 16 /* sc1 */);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    });
+  }
+}
+
+template <int KT, int NRT>
+static bool launch_pb(const bf16_t* WhhT, const float* Cst, const bf16_t* S, bf16_t* DG, const float* dcarry,
+                      unsigned* sync, int grid, LstmDims d, hipStream_t s) {
+  const void* f = reinterpret_cast<const void*>(&lstm_bwd_persistent_kernel<KT, NRT>);
+  if constexpr (KT == 16 && NRT == 16) {  // timing-only diagnostic builds (WELLFLOW_PF_DBG)
+    switch (d.dbg) {
+      case 1: f = reinterpret_cast<const void*>(&lstm_bwd_persistent_kernel<KT, NRT, 1>); break;
+      case 2: f = reinterpret_cast<const void*>(&lstm_bwd_persistent_kernel<KT, NRT, 2>); break;
+      case 4: f = reinterpret_cast<const void*>(&lstm_bwd_persistent_kernel<KT, NRT, 4>); break;
+      case 8: f = reinterpret_cast<const void*>(&lstm_bwd_persistent_kernel<KT, NRT, 8>); break;
+      case 16: f = reinterpret_cast<const void*>(&lstm_bwd_persistent_kernel<KT, NRT, 16>); break;
+      default: break;
+    }
+  }
+  void* args[] = {&WhhT, &Cst, &S, &DG, &dcarry, &sync, &d};
+  static const bool coop = [] {
+    const char* v = std::getenv("WELLFLOW_COOP");
+    return v == nullptr || v[0] != '0';
+  }();
+  if (coop) return hipLaunchCooperativeKernel(f, dim3(grid), dim3(256), args, 0u, s) == hipSuccess;
+  int per_cu = 0, dev = 0, cus = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, f, 256, 0) != hipSuccess || hipGetDevice(&dev) != hipSuccess ||
+      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || per_cu * cus < grid)
+    return false;
+  return hipLaunchKernel(f, dim3(grid), dim3(256), args, 0u, s) == hipSuccess;
+}
+
+template <int KT>
+static bool launch_pb_nrt(int NRT, const bf16_t* WhhT, const float* Cst, const bf16_t* S, bf16_t* DG,
+                          const float* dcarry, unsigned* sync, int grid, LstmDims d, hipStream_t s) {
+  switch (NRT) {
+    case 4: return launch_pb<KT, 4>(WhhT, Cst, S, DG, dcarry, sync, grid, d, s);
+    case 8: return launch_pb<KT, 8>(WhhT, Cst, S, DG, dcarry, sync, grid, d, s);
+    case 16: return launch_pb<KT, 16>(WhhT, Cst, S, DG, dcarry, sync, grid, d, s);
+    default: return false;
+  }
+}
+
+// Steps T-2 .. 0 of the backward in one launch (step T-1 must already be done: DG[T-1] and
+// the dc carry written by lstm_bwd_last_kernel). Returns false (nothing launched) when the
+// shape / device cannot host the persistent schedule; the caller runs the per-step kernels.
+bool launch_lstm_bwd_persistent(const bf16_t* WhhT, const float* Cst, const bf16_t* S, bf16_t* DG,
+                                const float* dcarry, unsigned* sync, long sync_words, LstmDims d,
+                                hipStream_t s) {
+  if (d.T < 2) return true;  // nothing after the last step
+  const int G = 4 * d.H;
+  if (d.H % 64 != 0 || d.B % 16 != 0) return false;
+  if ((double)d.B * G * 2 >= 2147483647.0) return false;  // 32-bit buffer offsets per step
+  int dev = 0, cus = 0;
+  if (hipGetDevice(&dev) != hipSuccess ||
+      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+    return false;
+  const int NB = d.H / 64, tiles = d.B / 16;
+  int NRT = 0;  // fewest row tiles per workgroup whose grid fits one workgroup per CU
+  for (int nrt = 4; nrt <= PB_MAX_RT; nrt *= 2) {  // multiple of 4: the row-tile loop is unrolled by 4
+    if (tiles % nrt == 0 && (tiles / nrt) * NB <= cus) {
+      NRT = nrt;
+      break;
+    }
+  }
+  if (NRT == 0) return false;
+  const int MB = tiles / NRT;
+  if (sync_words < lstm_persistent_sync_words(MB)) return false;
+  if (hipMemsetAsync(sync, 0, sizeof(unsigned) * (size_t)lstm_persistent_sync_words(MB), s) != hipSuccess)
+    return false;
+  const int grid = MB * NB;
+  switch (d.H) {
+    case 128: return launch_pb_nrt<4>(NRT, WhhT, Cst, S, DG, dcarry, sync, grid, d, s);
+    case 256: return launch_pb_nrt<8>(NRT, WhhT, Cst, S, DG, dcarry, sync, grid, d, s);
+    case 512: return launch_pb_nrt<16>(NRT, WhhT, Cst, S, DG, dcarry, sync, grid, d, s);
+    default: return false;
+  }
+}
+
+}  // namespace wf

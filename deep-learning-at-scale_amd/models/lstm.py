@@ -173,6 +173,10 @@ class NativeLSTM:
         self.persistent = os.environ.get("WELLFLOW_PERSISTENT", "1") != "0"
         self.sync = torch.zeros(16 + 16 * (B // 32 + 1), dtype=torch.int32, device=dev)
         self.last_forward_persistent = False
+        # persistent backward (csrc/lstm_persistent_bwd.hip): steps T-2..0 in ONE launch,
+        # W_hh^T in registers, dc carry in LDS; per-step kernels (bwd_variant) otherwise
+        self.persistent_bwd = os.environ.get("WELLFLOW_PERSISTENT_BWD", "1") != "0"
+        self.sync_bwd = torch.zeros(16 + 16 * (B // 64 + 1), dtype=torch.int32, device=dev)
         self.dw_ksplit = 0  # 0 = heuristic
         # timesteps per overlapped dW GEMM chunk; 0 = serial dW at the end (measured faster:
         # the BPTT chain already fills every CU, overlapping only adds contention)
@@ -201,8 +205,9 @@ class NativeLSTM:
         self.last_forward_persistent = bool(ok)
 
     def persistent_error(self) -> int:
-        """Non-zero if the last persistent forward hit its spin bound (host sync)."""
-        return int(self.sync[0].item()) if self.last_forward_persistent else 0
+        """Non-zero if the last persistent forward or backward hit its spin bound (host sync)."""
+        fwd = int(self.sync[0].item()) if self.last_forward_persistent else 0
+        return fwd or int(self.sync_bwd[0].item())
 
     # ------------------------------------------------------------------ passes
     def forward(self, x: torch.Tensor) -> torch.Tensor:
@@ -260,5 +265,6 @@ class NativeLSTM:
         if self.dw_chunk > 0:
             ksplit = max(1, ksplit * self.dw_chunk // self.T)
         C.lstm_backward_dw(self.WhhT, self.XH, self.Cst, self.S, self.DG, self.dcarry, self.dy,
-                           w_out, gW, *self._dims(B), self.bwd_variant, self.dw_chunk, ksplit)
+                           w_out, gW, *self._dims(B), self.bwd_variant, self.dw_chunk, ksplit,
+                           self.sync_bwd if self.persistent_bwd else None)
         return self.loss_sum

@@ -237,3 +237,35 @@ def test_weight_gradient_tiles_match_reference(tile, ksplit):
     ref = Amn.float().t() @ Bmn.float()
     err = (out - ref).abs().max().item()
     assert err < 2e-3 * ref.abs().max().item(), (tile, err)
+
+
+@pytest.mark.parametrize("B,H,T", [(8192, 512, 8), (512, 256, 6), (256, 128, 5), (2048, 512, 64)])
+def test_lstm_persistent_backward_matches_per_step(B, H, T):
+    """The one-launch persistent BPTT (csrc/lstm_persistent_bwd.hip) against the per-step
+    backward kernels on the same forward state: the K-split dh partials are summed in a
+    different fp32 order, so DG agrees to bf16 rounding and the weight gradient closely."""
+    from wellflow.data.synth import synth_lstm_batch
+    from wellflow.models.lstm import NativeLSTM, init_lstm_flat
+
+    F = 16
+    eng = NativeLSTM(F, H, T, B, device=DEV)
+    eng.params.copy_(init_lstm_flat(F, H, seed=4).to(DEV))
+    eng.sync_weights()
+    x, y = synth_lstm_batch(B, T, F, seed=5)
+    x, y = x.to(DEV), y.to(DEV)
+    res = {}
+    for pb in (False, True):
+        eng.persistent_bwd = pb
+        eng.sync_bwd.fill_(7)  # the launcher must reset it
+        eng.forward_backward(x, y, grad_scale=1.0 / B)
+        torch.cuda.synchronize()
+        if pb:
+            assert int(eng.sync_bwd[0].item()) == 0, "spin bound tripped"
+            assert int(eng.sync_bwd[16].item()) > 0, "persistent backward did not run"
+        res[pb] = (eng.DG.clone(), eng.grads.clone())
+    (dg0, g0), (dg1, g1) = res[False], res[True]
+    scale = dg0.float().abs().max().item()
+    d = (dg0.float() - dg1.float()).abs().max().item()
+    assert d <= 2e-2 * scale + 1e-6, (d, scale)
+    rel = ((g0 - g1).norm() / g0.norm()).item()
+    assert rel < 5e-3, rel

@@ -55,11 +55,11 @@ def main():
         errs = [(x.float() - y.float()).abs().max().item() for x, y in zip((eng.XH, eng.Cst, eng.S), ref_fwd)]
         print(f"check fwd v{v}: max|diff| XH {errs[0]:.3g} C {errs[1]:.3g} S {errs[2]:.3g}", flush=True)
     w_out = lay.views(eng.params)[1]
-    C.lstm_backward(eng.WhhT, eng.XH, eng.Cst, eng.S, eng.DG, eng.dcarry, eng.dy, w_out, *dims, 0)
+    C.lstm_backward(eng.WhhT, eng.XH, eng.Cst, eng.S, eng.DG, eng.dcarry, eng.dy, w_out, *dims, 0, None)
     ref_dg = eng.DG.clone()
     for v in map(int, a.bwd.split(",")):
         eng.DG.zero_()
-        C.lstm_backward(eng.WhhT, eng.XH, eng.Cst, eng.S, eng.DG, eng.dcarry, eng.dy, w_out, *dims, v)
+        C.lstm_backward(eng.WhhT, eng.XH, eng.Cst, eng.S, eng.DG, eng.dcarry, eng.dy, w_out, *dims, v, None)
         torch.cuda.synchronize()
         print(f"check bwd v{v}: max|diff| DG {(eng.DG.float() - ref_dg.float()).abs().max().item():.3g}", flush=True)
     res = {}
@@ -69,7 +69,7 @@ def main():
             res.setdefault(f"fwd v{v}", []).append(ms)
         for v in map(int, a.bwd.split(",")):
             ms = timeit(lambda: C.lstm_backward(eng.WhhT, eng.XH, eng.Cst, eng.S, eng.DG, eng.dcarry,
-                                                eng.dy, lay.views(eng.params)[1], *dims, v))
+                                                eng.dy, lay.views(eng.params)[1], *dims, v, None))
             res.setdefault(f"bwd v{v}", []).append(ms)
         for ks in map(int, a.ksplit.split(",")):
             for tile in map(int, a.tiles.split(",")):
@@ -85,7 +85,7 @@ def main():
             63 * timeit(lambda: gemm(A1, eng.WhhT, B, H, lay.G, outH=tmp)))
         d1 = (B, 1, F, lay.KX, H)
         res.setdefault("bwd epilogue-only x63", []).append(63 * timeit(lambda: C.lstm_backward(
-            eng.WhhT, eng.XH, eng.Cst, eng.S, eng.DG, eng.dcarry, eng.dy, lay.views(eng.params)[1], *d1, 0)))
+            eng.WhhT, eng.XH, eng.Cst, eng.S, eng.DG, eng.dcarry, eng.dy, lay.views(eng.params)[1], *d1, 0, None)))
         res.setdefault("fwd-shape GEMM x64", []).append(
             64 * timeit(lambda: gemm(eng.XH[: B * lay.KA], eng.Wp, B, lay.G, lay.KA, outH=eng.DG[: B * lay.G])))
     fl_fwd = 2.0 * B * lay.G * lay.KA * T
