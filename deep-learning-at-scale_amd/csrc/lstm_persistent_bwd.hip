@@ -42,7 +42,10 @@ typedef __attribute__((address_space(1))) unsigned gu32;
 // of 16 rows per workgroup (compile-time: the row-tile loop is fully unrolled so the dc
 // carry, the prefetch rings and every vmcnt below are static).
 // DBG (timing-only builds, results wrong; WELLFLOW_PF_DBG at H = 512, NRT = 16):
-// 1 no hand-off wait, 2 no MFMA, 4 no DG stores, 8 no S / c loads, 16 no A loads.
+// 1 no hand-off wait, 2 no MFMA, 4 no DG stores, 8 no S / c loads, 16 no A loads;
+// 64 = plain (L2-resident) DG stores + agent release before the arrival add (correct results);
+// 32 = timeline: s_memrealtime stamps of step PB_STAMP_S, wave 0 lane 0 of every workgroup,
+// into sync + 4096 words (128 per workgroup; tools/pb_timeline.py).
 template <int KT, int NRT, int DBG = 0>
 __global__ __launch_bounds__(256, 1) void lstm_bwd_persistent_kernel(
     const bf16_t* __restrict__ WhhT, const float* __restrict__ Cst, const bf16_t* __restrict__ S,
@@ -69,6 +72,13 @@ __global__ __launch_bounds__(256, 1) void lstm_bwd_persistent_kernel(
   const bool even = (l15 & 1) == 0;
   gu32* err = (gu32*)(sync);
   gu32* cnt = (gu32*)(sync + 16 + 16 * m);
+  constexpr int PB_STAMP_S = 10;
+  unsigned long long* stamps = reinterpret_cast<unsigned long long*>(sync + 4096) + blockIdx.x * 128;
+  auto stamp = [&](int s, int slot) {
+    if constexpr ((DBG & 32) != 0) {
+      if (s == PB_STAMP_S && threadIdx.x == 0) stamps[slot] = __builtin_amdgcn_s_memrealtime();
+    }
+  };
 
   // ---- prologue: stationary W_hh^T fragments (B operand: lane = unit col l15, k 8g..8g+7)
   bf16x8 w[KT][4];
@@ -131,6 +141,7 @@ __global__ __launch_bounds__(256, 1) void lstm_bwd_persistent_kernel(
 
   for (int s = 0; s < d.T - 1; ++s) {
     const int t = d.T - 2 - s;
+    stamp(s, 0);
     if (s > 0) {
       // ---- publish step s-1 (every wave drained its DG stores) and wait for the row block
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -140,6 +151,10 @@ __global__ __launch_bounds__(256, 1) void lstm_bwd_persistent_kernel(
       if constexpr (NRT > 1) load_sc(t, std::integral_constant<int, 1>{}, std::integral_constant<int, 1>{});
       __builtin_amdgcn_sched_barrier(0);
       if (threadIdx.x == 0) {
+        if constexpr ((DBG & 64) != 0) {  // plain DG stores: publish them with an agent release
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
         __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         const unsigned target = (unsigned)(NB * s);
         int ok = 1;
@@ -170,48 +185,117 @@ __global__ __launch_bounds__(256, 1) void lstm_bwd_persistent_kernel(
       if constexpr (NRT > 1) load_sc(t, std::integral_constant<int, 1>{}, std::integral_constant<int, 1>{});
     }
 
+    stamp(s, 1);
     const __amdgpu_buffer_rsrc_t a_rsrc =
         __builtin_amdgcn_make_buffer_rsrc(DG + ((size_t)(t + 1) * d.B + row0) * G, 0, 0x7FFFFFFF, 0x00020000);
     const __amdgpu_buffer_rsrc_t dg_rsrc =
         __builtin_amdgcn_make_buffer_rsrc(DG + (size_t)t * d.B * G, 0, 0x7FFFFFFF, 0x00020000);
     const int st_base = row0 * G * 2 + st_lane;
     // A tile rt of this wave -> ring slot rt & 1: KS k-steps x 2 row halves, 1 KB each
-    auto issue_a = [&](auto rc) {
-      constexpr int RT = decltype(rc)::value;
+    // piece i (k-step i / 2, rows 8 * (i % 2) ..) of A tile RT of this wave -> ring slot RT & 1
+    auto issue_a = [&](auto rc, auto ic) {
+      constexpr int RT = decltype(rc)::value, i = decltype(ic)::value, ks = i / 2, hf = i % 2;
       if constexpr ((DBG & 16) != 0) {
         if (RT > 1) return;
       }
-      const unsigned dst = a_lds + (RT & 1) * WSLOT;
-      static_for<0, KS>([&](auto kc) {
-        constexpr int ks = decltype(kc)::value;
-        (void)a_rsrc;
-        // (the instruction offset would also move the LDS address: the k-step goes into soffset)
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(a_rsrc, (lds_void*)(uintptr_t)(dst + ks * 2048), 16, a_vo,
-                                                 RT * 16 * G * 2 + ks * 128, 0, 0);
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(a_rsrc, (lds_void*)(uintptr_t)(dst + ks * 2048 + 1024), 16,
-                                                 a_vo1, RT * 16 * G * 2 + ks * 128, 0, 0);
-      });
+      const unsigned dst = a_lds + (RT & 1) * WSLOT + ks * 2048 + hf * 1024;
+      // (the instruction offset would also move the LDS address: the k-step goes into soffset)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(a_rsrc, (lds_void*)(uintptr_t)dst, 16, hf ? a_vo1 : a_vo,
+                                               RT * 16 * G * 2 + ks * 128, 0, 0);
     };
-    constexpr int NA = ((DBG & 16) != 0) ? 0 : 2 * KS;  // DMA instructions per A tile
+    constexpr int NA = ((DBG & 16) != 0) ? 0 : 2 * KS;  // DMA instructions per A tile (= KT)
     constexpr int NSC = ((DBG & 8) != 0) ? 0 : 3;       // S / c loads per tile
     constexpr int NST = ((DBG & 4) != 0) ? 0 : 2;       // DG stores per tile
-    issue_a(std::integral_constant<int, 0>{});
+    static_assert(2 * KS == KT, "two A pieces per k-tile over the first half of the loop");
+    (void)NA;
+    static_for<0, 2 * KS>([&](auto ic) { issue_a(std::integral_constant<int, 0>{}, ic); });
+
+    // Cell backward of row tile RTp (its dh in dhp, its saved gates / c_{t-1} in ring slot
+    // RTp % 3, its carry in dcr[RTp]) in parts 1..EPI_PARTS, two rows at a time in packed fp32
+    // (v_pk_fma / v_pk_mul: half the VALU issue of the scalar form), so that tile RTp + 1's
+    // MFMA loop can issue one part per k-tile in the MFMAs' shadow (software pipeline).
+    //   per row pair q: part 3q+1 gates, x = f c + i g, e = exp(2x); part 3q+2 tanh, dc, carry;
+    //   part 3q+3 the four gate gradients, packed to bf16; part 7 lane-pair exchange; 8 stores.
+    constexpr int EPI_PARTS = 8;
+    typedef float f32x2 __attribute__((ext_vector_type(2)));
+    f32x4 dhp = f32x4{0.f, 0.f, 0.f, 0.f};
+    unsigned ev[4][2];
+    f32x4 enk;
+    f32x2 eig[2], efg[2], egg[2], eog[2], ecp[2], eex[2], etc[2], edc[2], eq[2];
+    u32x4 elo, ehi;
+    auto epi = [&](auto rpc, auto partc) {
+      constexpr int RTp = decltype(rpc)::value, part = decltype(partc)::value, Kp = RTp % 3;
+      constexpr int q = (part - 1) / 3, sub = (part - 1) % 3;
+      if constexpr (part <= 6 && sub == 0) {
+        const u32x4 sv = q == 0 ? sq0[Kp] : sq1[Kp];  // rows 2q, 2q+1: (i|f), (g|o) per row
+        eig[q] = f32x2{__uint_as_float(sv[0] << 16), __uint_as_float(sv[2] << 16)};
+        efg[q] = f32x2{__uint_as_float(sv[0] & 0xffff0000u), __uint_as_float(sv[2] & 0xffff0000u)};
+        egg[q] = f32x2{__uint_as_float(sv[1] << 16), __uint_as_float(sv[3] << 16)};
+        eog[q] = f32x2{__uint_as_float(sv[1] & 0xffff0000u), __uint_as_float(sv[3] & 0xffff0000u)};
+        ecp[q] = f32x2{__uint_as_float(cq[Kp][2 * q]), __uint_as_float(cq[Kp][2 * q + 1])};
+        const f32x2 x2 = (efg[q] * ecp[q] + eig[q] * egg[q]) * 2.f;
+        eex[q] = f32x2{__expf(x2[0]), __expf(x2[1])};
+      } else if constexpr (part <= 6 && sub == 1) {
+        etc[q] = 1.f - 2.f * f32x2{__builtin_amdgcn_rcpf(eex[q][0] + 1.f), __builtin_amdgcn_rcpf(eex[q][1] + 1.f)};
+        const f32x2 dh = f32x2{dhp[2 * q], dhp[2 * q + 1]};
+        const f32x2 kv = f32x2{dcr[RTp][2 * q], dcr[RTp][2 * q + 1]};
+        eq[q] = dh * eog[q];
+        edc[q] = eq[q] * (1.f - etc[q] * etc[q]) + kv;
+        const f32x2 nk = edc[q] * efg[q];
+        enk[2 * q] = nk[0];
+        enk[2 * q + 1] = nk[1];
+      } else if constexpr (part <= 6 && sub == 2) {
+        const f32x2 a = edc[q] * eig[q], tq = a * egg[q];
+        const f32x2 di = tq - tq * eig[q];          // dc g i (1 - i)
+        const f32x2 dg = a - tq * egg[q];           // dc i (1 - g^2)
+        const f32x2 u = edc[q] * efg[q] * ecp[q];
+        const f32x2 df = u - u * efg[q];            // dc c_{t-1} f (1 - f)
+        const f32x2 e = eq[q] * etc[q];
+        const f32x2 dO = e - e * eog[q];            // dh tanh(c) o (1 - o)
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+          ev[2 * q + k][0] = (unsigned)f2bf(di[k]) | ((unsigned)f2bf(df[k]) << 16);
+          ev[2 * q + k][1] = (unsigned)f2bf(dg[k]) | ((unsigned)f2bf(dO[k]) << 16);
+        }
+      } else if constexpr (part == 7) {
+        dcr[RTp] = enk;
+        // lane pair (2i, 2i+1) = units (u, u+1): the even lane stores rows 0, 2 and the odd
+        // lane rows 1, 3 of both units, each a 16-B run [4 gates of u | 4 gates of u+1]
+        const unsigned snd[4] = {even ? ev[1][0] : ev[0][0], even ? ev[1][1] : ev[0][1],
+                                 even ? ev[3][0] : ev[2][0], even ? ev[3][1] : ev[2][1]};
+        unsigned o[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          o[i] = (unsigned)__builtin_amdgcn_mov_dpp((int)snd[i], 0xB1, 0xF, 0xF, false);  // quad_perm [1,0,3,2]
+        if (even) {
+          elo = u32x4{ev[0][0], ev[0][1], o[0], o[1]};  // row 4g + 0: units u, u+1
+          ehi = u32x4{ev[2][0], ev[2][1], o[2], o[3]};  // row 4g + 2
+        } else {
+          elo = u32x4{o[0], o[1], ev[1][0], ev[1][1]};  // row 4g + 1: units u-1, u
+          ehi = u32x4{o[2], o[3], ev[3][0], ev[3][1]};  // row 4g + 3
+        }
+      } else if constexpr (part == 8) {
+        constexpr int SOFF = RTp * 16 * G * 2;
+        if constexpr ((DBG & 4) != 0) {
+          if (elo[0] == 0x7fc07fc1u && ehi[1] == 0x7fc07fc1u) dcr[RTp][0] = 1.f;  // keep the values live
+        } else {
+          constexpr int AUX = (DBG & 64) ? 0 : 16;  // sc1 (write-through) unless released
+          __builtin_amdgcn_raw_buffer_store_b128(elo, dg_rsrc, st_base, SOFF, AUX);
+          __builtin_amdgcn_raw_buffer_store_b128(ehi, dg_rsrc, st_base, SOFF + 2 * G * 2, AUX);
+        }
+      }
+    };
 
     static_for<0, NRT>([&](auto rc) {
       constexpr int RT = decltype(rc)::value, K = RT % 3, P = RT & 1;
-      // ---- issue: A of RT + 1 (LDS-DMA), then S / c of RT + 2 (or of the next step)
-      if constexpr (RT + 1 < NRT) issue_a(std::integral_constant<int, RT + 1>{});
-      __builtin_amdgcn_sched_barrier(0);
-      if constexpr (RT + 2 < NRT) load_sc(t, std::integral_constant<int, RT + 2>{}, std::integral_constant<int, (K + 2) % 3>{});
-      __builtin_amdgcn_sched_barrier(0);
-      // ---- wait for A(RT): everything issued after it may stay in flight
-      // (tile RT issues: DMA(RT + 1) if RT + 1 < NRT, S / c(RT + 2) if RT + 2 < NRT, 2 stores)
-      constexpr int AFTER_PREV = (RT >= 1 && RT + 1 < NRT ? NSC : 0) + NST;  // rest of tile RT-1
-      constexpr int AFTER_CUR = (RT + 1 < NRT ? NA : 0) + (RT + 2 < NRT ? NSC : 0);
+      // ---- wait for A(RT): its pieces were issued in the first half of tile RT-1's MFMA loop;
+      // after the last one came tile RT-2's DG stores (epilogue part 8, if RT-1 > 0) and tile
+      // RT-1's S / c loads of tile RT+1, which may stay in flight
       if constexpr (RT == 0)
-        wait_vmcnt<AFTER_CUR>();
+        wait_vmcnt<0>();
       else
-        wait_vmcnt<AFTER_PREV + AFTER_CUR>();
+        wait_vmcnt<(RT >= 2 ? NST : 0) + (RT + 1 < NRT ? NSC : 0)>();
+      stamp(s, 2 + 5 * RT);
       const unsigned cur = a_lds + P * WSLOT;
 
       f32x4 acc[4];
@@ -238,9 +322,35 @@ __global__ __launch_bounds__(256, 1) void lstm_bwd_persistent_kernel(
             asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+v"(acc[j]) : "v"(a[kt & 1]), "a"(w[kt][j]));
           }
         }
+        // two A pieces of the next tile per k-tile over the first half of the loop: the vector-
+        // memory queue drains under the MFMAs instead of blocking the wave before them, and the
+        // last piece lands well before the next tile needs it
+        if constexpr (RT + 1 < NRT && 2 * kt < KT) {
+          issue_a(std::integral_constant<int, RT + 1>{}, std::integral_constant<int, 2 * kt>{});
+          issue_a(std::integral_constant<int, RT + 1>{}, std::integral_constant<int, 2 * kt + 1>{});
+        }
+        // parts of the previous tile's cell backward on every other k-tile (part p at 2p - 1)
+        if constexpr (RT > 0 && (kt & 1) == 1 && (kt + 1) / 2 <= EPI_PARTS)
+          epi(std::integral_constant<int, RT - 1>{}, std::integral_constant<int, (kt + 1) / 2>{});
+        // the MFMAs above are inline asm, so the compiler knows neither their latency nor that
+        // they still read this fragment: keep its registers allocated until here, so no VALU
+        // result of the interleaved epilogue can land in them while the MFMAs are in flight
+        asm volatile("" ::"v"(a[kt & 1]));
       });
+      // parts that did not fit a short loop (2p - 1 >= KT)
+      if constexpr (RT > 0 && 2 * EPI_PARTS - 1 >= KT)
+        static_for<KT / 2 + 1, EPI_PARTS + 1>([&](auto pc) { epi(std::integral_constant<int, RT - 1>{}, pc); });
       // VALU / LDS reads of MFMA results: cover the pipeline (nothing is padded after asm)
       asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 3" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+      // S / c of tile RT + 2 (HBM), after the A pieces: waiting for A(RT + 1) leaves them in flight
+      if constexpr (RT + 2 < NRT) load_sc(t, std::integral_constant<int, RT + 2>{}, std::integral_constant<int, (K + 2) % 3>{});
+      __builtin_amdgcn_sched_barrier(0);
+      if constexpr ((DBG & 32) != 0) {  // MFMA completion: consume a result before stamping
+        float sink = acc[3][3];
+        asm volatile("" ::"v"(sink));
+        stamp(s, 3 + 5 * RT);
+      }
 
       // ---- K-split partials -> LDS (own tile stays in registers); wave w sums unit tile w
       const unsigned rbase = lds0 + RED + (P * 4 + wid) * 4 * 1024 + lane * 16;  // red[P][wid][.][lane]
@@ -250,66 +360,26 @@ __global__ __launch_bounds__(256, 1) void lstm_bwd_persistent_kernel(
       __builtin_amdgcn_sched_barrier(0);
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();
+      stamp(s, 4 + 5 * RT);
       const unsigned rd_base = lds0 + RED + wid * 1024 + lane * 16;  // red[.][.][wid][lane]
-      f32x4 dh4 = wid == 0 ? acc[0] : wid == 1 ? acc[1] : wid == 2 ? acc[2] : acc[3];
-static_for<0, 4>([&](auto wc) {
+      // the partials of the other waves land in the accumulators just written out (their
+      // ds_writes completed before the barrier): acc[w2] <- red[P][w2][wid], own tile kept
+      static_for<0, 4>([&](auto wc) {
         constexpr int w2 = decltype(wc)::value;
-        (void)dh4;
-        if (w2 != wid) {
-          f32x4 pv;
-          asm volatile("ds_read_b128 %0, %1 offset:%2\n\ts_waitcnt lgkmcnt(0)"
-                       : "=v"(pv)
-                       : "v"(rd_base), "i"((P * 4 + w2) * 4 * 1024)
-                       : "memory");
-          dh4 += pv;
-        }
+        (void)acc;
+        (void)rd_base;
+        if (w2 != wid)
+          asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(acc[w2]) : "v"(rd_base), "i"((P * 4 + w2) * 4 * 1024) : "memory");
       });
-
-      // ---- cell backward of rows 4g + r (r = 0..3) x unit ue (as cell_bwd4 in lstm.hip)
-      const u32x4 s0 = sq0[K], s1 = sq1[K], c4 = cq[K];
-      const unsigned pk[8] = {s0[0], s0[1], s0[2], s0[3], s1[0], s1[1], s1[2], s1[3]};
-      const float pv[4] = {__uint_as_float(c4[0]), __uint_as_float(c4[1]), __uint_as_float(c4[2]),
-                           __uint_as_float(c4[3])};
-      const f32x4 kv = dcr[RT];
-      f32x4 nk;
-      unsigned v[4][2];  // gate gradients of row r: (di | df), (dg | do)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const float ig = bf2f((bf16_t)(pk[2 * r] & 0xffff)), fg = bf2f((bf16_t)(pk[2 * r] >> 16));
-        const float gg = bf2f((bf16_t)(pk[2 * r + 1] & 0xffff)), og = bf2f((bf16_t)(pk[2 * r + 1] >> 16));
-        const float tc = tanhf_(fg * pv[r] + ig * gg);
-        const float dh = dh4[r];
-        const float dc = kv[r] + dh * og * (1.f - tc * tc);
-        nk[r] = dc * fg;
-        v[r][0] = (unsigned)f2bf(dc * gg * ig * (1.f - ig)) | ((unsigned)f2bf(dc * pv[r] * fg * (1.f - fg)) << 16);
-        v[r][1] = (unsigned)f2bf(dc * ig * (1.f - gg * gg)) | ((unsigned)f2bf(dh * tc * og * (1.f - og)) << 16);
+      // the wait takes the accumulators as operands: the compiler sees inline-asm outputs as
+      // ready at once and would otherwise schedule the sum between the reads and the wait
+      asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(acc[0]), "+v"(acc[1]), "+v"(acc[2]), "+v"(acc[3]) :: "memory");
+      dhp = (acc[0] + acc[1]) + (acc[2] + acc[3]);
+      stamp(s, 5 + 5 * RT);
+      if constexpr (RT + 1 == NRT) {  // drain: the last tile's cell backward before the hand-off
+        static_for<1, EPI_PARTS + 1>([&](auto pc) { epi(std::integral_constant<int, RT>{}, pc); });
       }
-      dcr[RT] = nk;
-      // lane pair (2i, 2i+1) = units (u, u+1): the even lane stores rows 0, 2 and the odd lane
-      // rows 1, 3 of both units, each a 16-B run [4 gates of u | 4 gates of u+1]
-      unsigned o[4];
-      {
-        const unsigned snd[4] = {even ? v[1][0] : v[0][0], even ? v[1][1] : v[0][1], even ? v[3][0] : v[2][0],
-                                 even ? v[3][1] : v[2][1]};
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-          o[i] = (unsigned)__builtin_amdgcn_mov_dpp((int)snd[i], 0xB1, 0xF, 0xF, false);  // quad_perm [1,0,3,2]
-      }
-      u32x4 lo, hi;
-      if (even) {
-        lo = u32x4{v[0][0], v[0][1], o[0], o[1]};  // row 4g + 0: units u, u+1
-        hi = u32x4{v[2][0], v[2][1], o[2], o[3]};  // row 4g + 2
-      } else {
-        lo = u32x4{o[0], o[1], v[1][0], v[1][1]};  // row 4g + 1: units u-1, u
-        hi = u32x4{o[2], o[3], v[3][0], v[3][1]};  // row 4g + 3
-      }
-      constexpr int SOFF = RT * 16 * G * 2;
-      if constexpr ((DBG & 4) != 0) {
-        if (lo[0] == 0x7fc07fc1u && hi[1] == 0x7fc07fc1u) dcr[RT][0] = 1.f;  // keep the values live
-      } else {
-        __builtin_amdgcn_raw_buffer_store_b128(lo, dg_rsrc, st_base, SOFF, 16 /* sc1 */);
-        __builtin_amdgcn_raw_buffer_store_b128(hi, dg_rsrc, st_base, SOFF + 2 * G * 2, 16 /* sc1 */);
-      }
+      stamp(s, 6 + 5 * RT);
       __builtin_amdgcn_sched_barrier(0);
     });
   }
@@ -326,6 +396,9 @@ static bool launch_pb(const bf16_t* WhhT, const float* Cst, const bf16_t* S, bf1
       case 4: f = reinterpret_cast<const void*>(&lstm_bwd_persistent_kernel<KT, NRT, 4>); break;
       case 8: f = reinterpret_cast<const void*>(&lstm_bwd_persistent_kernel<KT, NRT, 8>); break;
       case 16: f = reinterpret_cast<const void*>(&lstm_bwd_persistent_kernel<KT, NRT, 16>); break;
+      case 32: f = reinterpret_cast<const void*>(&lstm_bwd_persistent_kernel<KT, NRT, 32>); break;
+      case 64: f = reinterpret_cast<const void*>(&lstm_bwd_persistent_kernel<KT, NRT, 64>); break;
+      case 96: f = reinterpret_cast<const void*>(&lstm_bwd_persistent_kernel<KT, NRT, 96>); break;
       default: break;
     }
   }
