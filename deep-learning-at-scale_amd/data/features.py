@@ -171,6 +171,14 @@ def take(table: dict, idx) -> dict:
 def window_starts(n: int, T: int, groups=None, stride: int = 1) -> np.ndarray:
     """First row of every length-``T`` window that stays inside one series (``groups`` =
     per-row series id, rows in time order inside a group)."""
+    from . import native
+
+    if native.wanted():  # C++ scan (csrc/runtime/windows.cpp); the loop below is its oracle
+        return native.window_starts(n, T, groups, stride)
+    return window_starts_py(n, T, groups, stride)
+
+
+def window_starts_py(n: int, T: int, groups=None, stride: int = 1) -> np.ndarray:
     g = np.zeros(n, dtype=np.int64) if groups is None else np.asarray(groups)
     starts = []
     i = 0
@@ -237,6 +245,11 @@ class SeriesWindows:
             ar = torch.arange(self.T, device=st.device)
             return self.rows[st.reshape(-1, 1) + ar]
         st = np.asarray(st).reshape(-1)
+        from . import native
+
+        if (isinstance(self.rows, np.ndarray) and self.rows.dtype == np.float32 and self.rows.flags.c_contiguous
+                and native.wanted()):  # one memcpy per window, threaded
+            return native.gather_windows(self.rows, st, self.T)
         return self.rows[st[:, None] + np.arange(self.T)[None, :]]
 
     def to(self, device):

@@ -1,8 +1,9 @@
 """Dataset ingest (replaces ``spark.read.csv(path, header=False, schema=schema)``, cnn.py:65).
 
 Headerless CSV by default (as the reference), explicit schema from the submission strings
-(data/schema.py). Parsing is done by Arrow's multithreaded C++ CSV reader (pyarrow):
-columns come back typed per the schema (int -> int32 = Spark IntegerType, float ->
+(data/schema.py). Parsing is done by the framework's own multithreaded C++ reader
+(csrc/runtime/csv.cpp via data/native.py), or by Arrow's (pyarrow) when the native runtime
+is not built: columns come back typed per the schema (int -> int32 = Spark IntegerType, float ->
 float32 = FloatType, string -> utf8). Rows whose numeric cells fail to parse become nulls
 in Spark; here they are dropped (and counted) because the regression models cannot use
 them. Multi-rank jobs read the file once per rank and take a deterministic shard of the
@@ -17,6 +18,15 @@ from .synth import TABLE_COLUMNS, TABLE_TYPES, well_log_table
 
 
 def read_csv(path: str, schema: Schema, header: bool = False, block_size: int = 1 << 24) -> dict:
+    """Native multithreaded C++ parser (csrc/runtime/csv.cpp) when built; Arrow otherwise."""
+    from . import native
+
+    if native.wanted():
+        return native.read_csv(path, schema, header=header)
+    return read_csv_arrow(path, schema, header=header, block_size=block_size)
+
+
+def read_csv_arrow(path: str, schema: Schema, header: bool = False, block_size: int = 1 << 24) -> dict:
     import pyarrow as pa
     import pyarrow.csv as pacsv
 
