@@ -42,7 +42,8 @@ typedef __attribute__((address_space(1))) unsigned gu32;
 // of 16 rows per workgroup (compile-time: the row-tile loop is fully unrolled so the dc
 // carry, the prefetch rings and every vmcnt below are static).
 // DBG (timing-only builds, results wrong; WELLFLOW_PF_DBG at H = 512, NRT = 16):
-// 1 no hand-off wait, 2 no MFMA, 4 no DG stores, 8 no S / c loads, 16 no A loads;
+// 1 no hand-off wait, 2 no MFMA, 4 no DG stores, 8 no S / c loads, 16 no A loads, 128 A
+// always from row tile 0 (same bytes, L2-hot);
 // 64 = plain (L2-resident) DG stores + agent release before the arrival add (correct results);
 // 32 = timeline: s_memrealtime stamps of step PB_STAMP_S, wave 0 lane 0 of every workgroup,
 // into sync + 4096 words (128 per workgroup; tools/pb_timeline.py).
@@ -116,14 +117,17 @@ __global__ __launch_bounds__(256, 1) void lstm_bwd_persistent_kernel(
   const int st_lane = ((4 * g + (even ? 0 : 1)) * G + 4 * ue2) * 2;  // byte offset (row 4g + r0, col 4*ue2)
   const size_t s_row = (size_t)(row0 >> 4) * HB * 1024 + s_lane, c_row = (size_t)(row0 >> 4) * HB * 256 + c_lane;
 
-  // saved gates + c_{t-1} (HBM): 3-slot register ring, row tile rt in slot rt % 3, issued two
-  // tiles ahead; tiles 0 and 1 of a step are issued before its hand-off wait (they do not
-  // depend on it). No register of an in-flight load is ever moved.
+  // saved gates + c_{t-1} (HBM): 4-slot register ring, row tile rt in slot rt % 4 (NRT % 4 == 0,
+  // so the slots line up across steps), issued two tiles ahead RIGHT AFTER the last A piece of
+  // the current tile's loop: vmcnt completes in issue order, so an HBM load issued before an
+  // A piece would hold that piece's wait for the whole HBM latency. The last two tiles of a
+  // step prefetch tiles 0 and 1 of the next step (they do not depend on the hand-off). No
+  // register of an in-flight load is ever moved.
   // Every address below is buffer-resource based: a 32-bit per-lane constant (s_vo / c_vo /
   // a_src) plus scalar (per step / per tile) parts, so the fully unrolled tile loop keeps no
   // per-tile 64-bit addresses live in VGPRs.
   const int s_vo = (int)(s_row * 2), c_vo = (int)(c_row * 4);
-  u32x4 sq0[3], sq1[3], cq[3];
+  u32x4 sq0[4], sq1[4], cq[4];
   auto load_sc = [&](int t, auto rc, auto slot) {
     constexpr int RT = decltype(rc)::value, Q = decltype(slot)::value;
     if constexpr ((DBG & 8) != 0) {
@@ -138,6 +142,8 @@ __global__ __launch_bounds__(256, 1) void lstm_bwd_persistent_kernel(
     sq1[Q] = __builtin_amdgcn_raw_buffer_load_b128(sr, s_vo + 16, SO, 2 /* nt */);
     cq[Q] = __builtin_amdgcn_raw_buffer_load_b128(cr, c_vo, CO, 2 /* nt */);
   };
+  load_sc(d.T - 2, std::integral_constant<int, 0>{}, std::integral_constant<int, 0>{});
+  load_sc(d.T - 2, std::integral_constant<int, 1>{}, std::integral_constant<int, 1>{});
 
   for (int s = 0; s < d.T - 1; ++s) {
     const int t = d.T - 2 - s;
@@ -147,9 +153,6 @@ __global__ __launch_bounds__(256, 1) void lstm_bwd_persistent_kernel(
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();
       asm volatile("" ::: "memory");
-      load_sc(t, std::integral_constant<int, 0>{}, std::integral_constant<int, 0>{});
-      if constexpr (NRT > 1) load_sc(t, std::integral_constant<int, 1>{}, std::integral_constant<int, 1>{});
-      __builtin_amdgcn_sched_barrier(0);
       if (threadIdx.x == 0) {
         if constexpr ((DBG & 64) != 0) {  // plain DG stores: publish them with an agent release
           __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
@@ -180,9 +183,6 @@ __global__ __launch_bounds__(256, 1) void lstm_bwd_persistent_kernel(
       int okv;
       asm volatile("ds_read_b32 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(okv) : "v"(lds0 + FLAG) : "memory");
       if (__builtin_amdgcn_readfirstlane(okv) == 0) return;  // uniform
-    } else {
-      load_sc(t, std::integral_constant<int, 0>{}, std::integral_constant<int, 0>{});
-      if constexpr (NRT > 1) load_sc(t, std::integral_constant<int, 1>{}, std::integral_constant<int, 1>{});
     }
 
     stamp(s, 1);
@@ -200,8 +200,9 @@ __global__ __launch_bounds__(256, 1) void lstm_bwd_persistent_kernel(
       }
       const unsigned dst = a_lds + (RT & 1) * WSLOT + ks * 2048 + hf * 1024;
       // (the instruction offset would also move the LDS address: the k-step goes into soffset)
+      constexpr int RTS = (DBG & 128) ? 0 : RT;  // timing build 128: always row tile 0 (L2-hot lines)
       __builtin_amdgcn_raw_ptr_buffer_load_lds(a_rsrc, (lds_void*)(uintptr_t)dst, 16, hf ? a_vo1 : a_vo,
-                                               RT * 16 * G * 2 + ks * 128, 0, 0);
+                                               RTS * 16 * G * 2 + ks * 128, 0, 0);
     };
     constexpr int NA = ((DBG & 16) != 0) ? 0 : 2 * KS;  // DMA instructions per A tile (= KT)
     constexpr int NSC = ((DBG & 8) != 0) ? 0 : 3;       // S / c loads per tile
@@ -224,7 +225,7 @@ __global__ __launch_bounds__(256, 1) void lstm_bwd_persistent_kernel(
     f32x2 eig[2], efg[2], egg[2], eog[2], ecp[2], eex[2], etc[2], edc[2], eq[2];
     u32x4 elo, ehi;
     auto epi = [&](auto rpc, auto partc) {
-      constexpr int RTp = decltype(rpc)::value, part = decltype(partc)::value, Kp = RTp % 3;
+      constexpr int RTp = decltype(rpc)::value, part = decltype(partc)::value, Kp = RTp % 4;
       constexpr int q = (part - 1) / 3, sub = (part - 1) % 3;
       if constexpr (part <= 6 && sub == 0) {
         const u32x4 sv = q == 0 ? sq0[Kp] : sq1[Kp];  // rows 2q, 2q+1: (i|f), (g|o) per row
@@ -286,27 +287,38 @@ __global__ __launch_bounds__(256, 1) void lstm_bwd_persistent_kernel(
       }
     };
 
+    // K-split partial exchange, deferred by one tile: tile r writes its 3 foreign partials to
+    // red[r & 1] at its end and runs on; tile r+1's loop passes a barrier after its first
+    // k-tile (the writes drained by that k-tile's lgkmcnt wait), issues the partial reads, and
+    // sums them at k-tile 1 (so their LDS latency hides under MFMAs). The last tile of a step
+    // exchanges at once (its cell backward drains before the hand-off).
+    f32x4 dho = f32x4{0.f, 0.f, 0.f, 0.f};  // own partial of the previous tile (its unit tile)
+    const unsigned rd_base = lds0 + RED + wid * 1024 + lane * 16;  // red[.][.][wid][lane]
+    auto kt_of_part = [](int p) { return 2 * p - 1 + (p == 1 ? 1 : 0); };  // parts at k-tiles 2,3,5,..,15
+
     static_for<0, NRT>([&](auto rc) {
-      constexpr int RT = decltype(rc)::value, K = RT % 3, P = RT & 1;
+      constexpr int RT = decltype(rc)::value, P = RT & 1;
       // ---- wait for A(RT): its pieces were issued in the first half of tile RT-1's MFMA loop;
-      // after the last one came tile RT-2's DG stores (epilogue part 8, if RT-1 > 0) and tile
-      // RT-1's S / c loads of tile RT+1, which may stay in flight
+      // after the last one came tile RT-1's S / c loads (of tile RT+1 or of the next step) and
+      // tile RT-2's DG stores (epilogue part 8, if RT-1 > 0), which may stay in flight
       if constexpr (RT == 0)
         wait_vmcnt<0>();
       else
-        wait_vmcnt<(RT >= 2 ? NST : 0) + (RT + 1 < NRT ? NSC : 0)>();
+        wait_vmcnt<NSC + (RT >= 2 ? NST : 0)>();
       stamp(s, 2 + 5 * RT);
       const unsigned cur = a_lds + P * WSLOT;
 
       f32x4 acc[4];
 #pragma unroll
       for (int j = 0; j < 4; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+      f32x4 pr[4];
       bf16x8 a[2];
       asm volatile("ds_read_b128 %0, %1" : "=v"(a[0]) : "v"(cur + fa[0]) : "memory");
       static_for<0, KT>([&](auto kc) {
         constexpr int kt = decltype(kc)::value;
         (void)acc;  // odr-use outside the asm operands: clang does not capture them implicitly
         (void)w;
+        (void)pr;
         if constexpr (kt + 1 < KT)
           asm volatile("ds_read_b128 %0, %1 offset:%2"
                        : "=v"(a[(kt + 1) & 1])
@@ -316,6 +328,12 @@ __global__ __launch_bounds__(256, 1) void lstm_bwd_persistent_kernel(
           asm volatile("s_waitcnt lgkmcnt(1)" ::: "memory");
         else
           asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        if constexpr (RT > 0 && kt == 1) {
+          // the wait above drained the partial reads issued at k-tile 0 (LDS returns in order):
+          // tie them to it, then the previous tile's dh
+          asm volatile("" : "+v"(pr[0]), "+v"(pr[1]), "+v"(pr[2]), "+v"(pr[3]));
+          dhp = dho + ((pr[0] + pr[1]) + (pr[2] + pr[3]));
+        }
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
           if constexpr (!(DBG & 2)) {
@@ -329,22 +347,48 @@ __global__ __launch_bounds__(256, 1) void lstm_bwd_persistent_kernel(
           issue_a(std::integral_constant<int, RT + 1>{}, std::integral_constant<int, 2 * kt>{});
           issue_a(std::integral_constant<int, RT + 1>{}, std::integral_constant<int, 2 * kt + 1>{});
         }
-        // parts of the previous tile's cell backward on every other k-tile (part p at 2p - 1)
-        if constexpr (RT > 0 && (kt & 1) == 1 && (kt + 1) / 2 <= EPI_PARTS)
-          epi(std::integral_constant<int, RT - 1>{}, std::integral_constant<int, (kt + 1) / 2>{});
+        if constexpr (kt == KT / 2 - 1) {  // S / c of tile RT + 2 right after the last A piece
+          __builtin_amdgcn_sched_barrier(0);
+          if constexpr (RT + 2 < NRT)
+            load_sc(t, std::integral_constant<int, RT + 2>{}, std::integral_constant<int, (RT + 2) % 4>{});
+          else  // tiles 0 / 1 of the next step (t - 1; past step 0: a harmless reload, same count)
+            load_sc(t > 0 ? t - 1 : t, std::integral_constant<int, RT + 2 - NRT>{},
+                    std::integral_constant<int, (RT + 2) % 4>{});
+          __builtin_amdgcn_sched_barrier(0);
+        }
+        if constexpr (RT > 0 && kt == 0) {
+          // every wave's partial writes of tile RT-1 were drained by its lgkmcnt wait above
+          __builtin_amdgcn_s_barrier();
+          static_for<0, 4>([&](auto wc) {
+            constexpr int w2 = decltype(wc)::value;
+            (void)pr;
+            (void)rd_base;
+            if (w2 != wid)
+              asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(pr[w2]) : "v"(rd_base),
+                           "i"((((RT - 1) & 1) * 4 + w2) * 4 * 1024) : "memory");
+            else
+              pr[w2] = f32x4{0.f, 0.f, 0.f, 0.f};
+          });
+        }
+        // parts of the previous tile's cell backward (part p at k-tile kt_of_part(p))
+        static_for<1, EPI_PARTS + 1>([&](auto pc) {
+          constexpr int p = decltype(pc)::value;
+          if constexpr (RT > 0 && 2 * p - 1 + (p == 1 ? 1 : 0) == kt)
+            epi(std::integral_constant<int, RT - 1>{}, pc);
+        });
         // the MFMAs above are inline asm, so the compiler knows neither their latency nor that
         // they still read this fragment: keep its registers allocated until here, so no VALU
         // result of the interleaved epilogue can land in them while the MFMAs are in flight
         asm volatile("" ::"v"(a[kt & 1]));
       });
-      // parts that did not fit a short loop (2p - 1 >= KT)
-      if constexpr (RT > 0 && 2 * EPI_PARTS - 1 >= KT)
-        static_for<KT / 2 + 1, EPI_PARTS + 1>([&](auto pc) { epi(std::integral_constant<int, RT - 1>{}, pc); });
+      (void)kt_of_part;
+      // parts that did not fit a short loop
+      static_for<1, EPI_PARTS + 1>([&](auto pc) {
+        constexpr int p = decltype(pc)::value;
+        if constexpr (RT > 0 && 2 * p - 1 + (p == 1 ? 1 : 0) >= KT) epi(std::integral_constant<int, RT - 1>{}, pc);
+      });
       // VALU / LDS reads of MFMA results: cover the pipeline (nothing is padded after asm)
       asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 3" ::: "memory");
-      __builtin_amdgcn_sched_barrier(0);
-      // S / c of tile RT + 2 (HBM), after the A pieces: waiting for A(RT + 1) leaves them in flight
-      if constexpr (RT + 2 < NRT) load_sc(t, std::integral_constant<int, RT + 2>{}, std::integral_constant<int, (K + 2) % 3>{});
       __builtin_amdgcn_sched_barrier(0);
       if constexpr ((DBG & 32) != 0) {  // MFMA completion: consume a result before stamping
         float sink = acc[3][3];
@@ -352,31 +396,29 @@ __global__ __launch_bounds__(256, 1) void lstm_bwd_persistent_kernel(
         stamp(s, 3 + 5 * RT);
       }
 
-      // ---- K-split partials -> LDS (own tile stays in registers); wave w sums unit tile w
+      // ---- K-split partials -> red[P] (the own unit tile stays in registers: dho)
+      dho = wid == 0 ? acc[0] : wid == 1 ? acc[1] : wid == 2 ? acc[2] : acc[3];
       const unsigned rbase = lds0 + RED + (P * 4 + wid) * 4 * 1024 + lane * 16;  // red[P][wid][.][lane]
 #pragma unroll
       for (int j = 0; j < 4; ++j)
         if (j != wid) asm volatile("ds_write_b128 %0, %1 offset:%2" ::"v"(rbase), "v"(acc[j]), "i"(j * 1024) : "memory");
       __builtin_amdgcn_sched_barrier(0);
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();
       stamp(s, 4 + 5 * RT);
-      const unsigned rd_base = lds0 + RED + wid * 1024 + lane * 16;  // red[.][.][wid][lane]
-      // the partials of the other waves land in the accumulators just written out (their
-      // ds_writes completed before the barrier): acc[w2] <- red[P][w2][wid], own tile kept
-      static_for<0, 4>([&](auto wc) {
-        constexpr int w2 = decltype(wc)::value;
-        (void)acc;
-        (void)rd_base;
-        if (w2 != wid)
-          asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(acc[w2]) : "v"(rd_base), "i"((P * 4 + w2) * 4 * 1024) : "memory");
-      });
-      // the wait takes the accumulators as operands: the compiler sees inline-asm outputs as
-      // ready at once and would otherwise schedule the sum between the reads and the wait
-      asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(acc[0]), "+v"(acc[1]), "+v"(acc[2]), "+v"(acc[3]) :: "memory");
-      dhp = (acc[0] + acc[1]) + (acc[2] + acc[3]);
-      stamp(s, 5 + 5 * RT);
-      if constexpr (RT + 1 == NRT) {  // drain: the last tile's cell backward before the hand-off
+      if constexpr (RT + 1 == NRT) {  // last tile: exchange now, drain its cell backward
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        static_for<0, 4>([&](auto wc) {
+          constexpr int w2 = decltype(wc)::value;
+          (void)acc;
+          (void)rd_base;
+          if (w2 != wid)
+            asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(acc[w2]) : "v"(rd_base), "i"((P * 4 + w2) * 4 * 1024) : "memory");
+        });
+        // the wait takes the accumulators as operands: the compiler sees inline-asm outputs as
+        // ready at once and would otherwise schedule the sum between the reads and the wait
+        asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(acc[0]), "+v"(acc[1]), "+v"(acc[2]), "+v"(acc[3]) :: "memory");
+        dhp = (acc[0] + acc[1]) + (acc[2] + acc[3]);
+        stamp(s, 5 + 5 * RT);
         static_for<1, EPI_PARTS + 1>([&](auto pc) { epi(std::integral_constant<int, RT>{}, pc); });
       }
       stamp(s, 6 + 5 * RT);
@@ -399,6 +441,7 @@ static bool launch_pb(const bf16_t* WhhT, const float* Cst, const bf16_t* S, bf1
       case 32: f = reinterpret_cast<const void*>(&lstm_bwd_persistent_kernel<KT, NRT, 32>); break;
       case 64: f = reinterpret_cast<const void*>(&lstm_bwd_persistent_kernel<KT, NRT, 64>); break;
       case 96: f = reinterpret_cast<const void*>(&lstm_bwd_persistent_kernel<KT, NRT, 96>); break;
+      case 128: f = reinterpret_cast<const void*>(&lstm_bwd_persistent_kernel<KT, NRT, 128>); break;
       default: break;
     }
   }
