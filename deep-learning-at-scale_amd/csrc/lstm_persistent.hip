@@ -43,7 +43,7 @@ int lstm_persistent_sync_words(int row_blocks) { return 16 + 16 * row_blocks; }
 
 // KT = KA / 32 k-tiles; NC = 32-row chunks per workgroup per step (compile-time, so every
 // ring slot, LDS offset and vmcnt count below is an immediate).
-template <int KT, int NC, int DBG = 0>  // DBG: timing-only builds (2 no MFMA, 4 no C/S stores, 8 no c loads)
+template <int KT, int NC, int DBG = 0>  // DBG: timing-only builds (2 no MFMA, 4 no C/S stores, 8 no c loads; 64 stores in the loop)
 __global__ __launch_bounds__(256, 1) void lstm_fwd_persistent_kernel(
     bf16_t* __restrict__ XH, const bf16_t* __restrict__ Wp, float* __restrict__ Cst,
     bf16_t* __restrict__ S, unsigned* __restrict__ sync, LstmDims d) {
@@ -191,6 +191,40 @@ __global__ __launch_bounds__(256, 1) void lstm_fwd_persistent_kernel(
       pk[i][2 * r + 1] = (unsigned)f2bf(gg) | ((unsigned)f2bf(og) << 16);
       hv[i][r] = f2bf(og * tanhf_(cn));
     };
+    // The same three pieces, issued one by one from inside the next chunk's MFMA loop
+    // (diagnostic build WELLFLOW_PF_DBG=64, KT >= 16): h staging, then one C / S store per
+    // k-tile (issue order unchanged, so the vmcnt counts below still hold). Measured 1.64 vs
+    // 1.60 ms for the stores after the loop (tools/pf_time.py 0,64): not the default.
+    auto epi_h = [&](const unsigned (&hv)[2][4]) {
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          asm volatile("ds_write_b16 %0, %1" ::"v"(hb_lds + 2u * ((i * 16 + 4 * g + r) * 64 + wid * 16 + l15)),
+                       "v"(hv[i][r])
+                       : "memory");
+    };
+    auto epi_cs = [&](int e, int k, const float (&cv)[2][4], const unsigned (&pk)[2][8]) {  // k = 0..5
+      if constexpr (!(DBG & 4)) {
+        const int i = k < 2 ? k : (k - 2) >> 1;
+        if (k < 2) {
+          *reinterpret_cast<float4*>(cnext + (2 * e + i) * HB * 256 + loff_c) =
+              make_float4(cv[i][0], cv[i][1], cv[i][2], cv[i][3]);
+        } else {
+          const int hf = (k - 2) & 1;
+          uint4* sp = reinterpret_cast<uint4*>(St + (2 * e + i) * HB * 1024 + loff_s);
+          sp[hf] = make_uint4(pk[i][4 * hf], pk[i][4 * hf + 1], pk[i][4 * hf + 2], pk[i][4 * hf + 3]);
+        }
+      }
+    };
+    auto rotate = [&](const float (&cv)[2][4]) {
+#pragma unroll
+      for (int q = 0; q + 1 < NC; ++q)
+#pragma unroll
+        for (int i = 0; i < 2; ++i) cq[q][i] = cq[q + 1][i];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) cq[NC - 1][i] = f32x4{cv[i][0], cv[i][1], cv[i][2], cv[i][3]};
+    };
     // stores of chunk e (C, S: NSTORE - 1 per wave), h staged in LDS, c-queue rotation
     auto epi_store = [&](int e, const float (&cv)[2][4], const unsigned (&pk)[2][8], const unsigned (&hv)[2][4]) {
 #pragma unroll
@@ -315,6 +349,17 @@ __global__ __launch_bounds__(256, 1) void lstm_fwd_persistent_kernel(
             }
           }
         if constexpr (kt < 8) epi_elem(kt >> 2, kt & 3, cv, pk, hv);
+        if constexpr (KT >= 16 && (DBG & 64)) {  // chunk c-1's stores and publish in this loop's shadow
+          if constexpr (kt == 8) {
+            if (c > 0) epi_h(hv);
+          }
+          if constexpr (kt >= 9 && kt <= 14) {
+            if (c > 0) epi_cs(c - 1, kt - 9, cv, pk);
+          }
+          if constexpr (kt == 16) {
+            if (c > 0) publish(c - 1);
+          }
+        }
       });
       // the epilogue reads the accumulators with VALU: cover the last MFMAs' pipeline
       // (the compiler pads nothing after inline asm)
@@ -324,7 +369,9 @@ __global__ __launch_bounds__(256, 1) void lstm_fwd_persistent_kernel(
         asm volatile("" ::"v"(sink));
         stamp(t, 4 + 5 * c);
       }
-      if (c > 0) {
+      if constexpr (KT >= 16 && (DBG & 64)) {
+        if (c > 0) rotate(cv);
+      } else if (c > 0) {
         epi_store(c - 1, cv, pk, hv);
         stamp(t, 5 + 5 * c);
         publish(c - 1);
@@ -364,6 +411,7 @@ static bool launch_pf(bf16_t* XH, const bf16_t* Wp, float* Cst, bf16_t* S, unsig
     if (d.dbg == 14) f = reinterpret_cast<const void*>(&lstm_fwd_persistent_kernel<KT, NC, 14>);
     if (d.dbg == 16) f = reinterpret_cast<const void*>(&lstm_fwd_persistent_kernel<KT, NC, 16>);
     if (d.dbg == 48) f = reinterpret_cast<const void*>(&lstm_fwd_persistent_kernel<KT, NC, 48>);
+    if (d.dbg == 64) f = reinterpret_cast<const void*>(&lstm_fwd_persistent_kernel<KT, NC, 64>);  // stores inside the loop
   }
   void* args[] = {&XH, &Wp, &Cst, &S, &sync, &d};
   // Cooperative launch: the runtime rejects a grid that cannot be co-resident. rocprofv3
