@@ -11,17 +11,19 @@
 //  * dh_t = DG_{t+1} W_hh is split over K by wave: wave w multiplies DG columns
 //    [w*H, (w+1)*H) by the matching rows of W_hh, for all 64 units. Its W_hh^T slice
 //    (64 units x H k's) stays in AGPRs for the whole sequence (H/2 = 256 registers at
-//    H = 512), and its A fragments come straight from L2 into VGPRs (no LDS staging: no
-//    other wave reads them). The 4 partial 16x64 dh tiles are summed through LDS, each
-//    wave then owning one 16-unit tile for the cell backward.
-//  * the dc carry of the workgroup's rows x units lives in LDS for the whole sequence
-//    (it never touches HBM); c_{t-1} and the saved gates S_t are read once (non-temporal,
-//    prefetched two row tiles ahead), DG_t is written once with 16-B write-through (sc1)
-//    stores (lane pairs exchange halves so each store is a whole 16-B (row, 2 units) run).
+//    H = 512). Its A operand streams through a private 2-slot LDS-DMA ring (buffer_load ...
+//    lds, every instruction 8 rows x 128 B: full lines; the pieces of tile r+1 are issued
+//    between tile r's MFMAs). The 4 partial 16x64 dh tiles are summed through LDS (deferred
+//    into the next tile's loop), each wave then owning one 16-unit tile for the cell backward.
+//  * the dc carry of the workgroup's rows x units lives in VGPRs for the whole sequence (it
+//    never touches HBM); c_{t-1} and the saved gates S_t are read once (register ring,
+//    two row tiles ahead); the cell backward of tile r-1 runs in packed fp32 inside tile r's
+//    MFMA loop; DG_t is written once with 16-B write-through (sc1) stores (lane pairs
+//    exchange halves by DPP so each store is a whole 16-B (row, 2 units) run).
 //  * hand-off (cdna_hip_programming.md Guideline 16, recipe R1, as in the forward): every
 //    wave drains its stores (vmcnt(0)), workgroup barrier, ONE lane adds to the row
 //    block's arrival counter (agent scope); consumers poll relaxed with s_sleep, then ONE
-//    agent-scope acquire, then plain loads of DG_{t+1}. Only the H/64 workgroups of one
+//    agent-scope acquire, then the LDS-DMA loads of DG_{t+1}. Only the H/64 workgroups of one
 //    row block depend on each other; every spin is bounded (error word 0, all drain).
 // Step T-1 (dh from the regression head) is lstm_bwd_last_kernel in lstm.hip.
 #include <cstdlib>
@@ -43,7 +45,7 @@ typedef __attribute__((address_space(1))) unsigned gu32;
 // carry, the prefetch rings and every vmcnt below are static).
 // DBG (timing-only builds, results wrong; WELLFLOW_PF_DBG at H = 512, NRT = 16):
 // 1 no hand-off wait, 2 no MFMA, 4 no DG stores, 8 no S / c loads, 16 no A loads, 128 A
-// always from row tile 0 (same bytes, L2-hot);
+// always from row tile 0 (same bytes, L2-hot), 256 default-policy (not nt) S / c loads;
 // 64 = plain (L2-resident) DG stores + agent release before the arrival add (correct results);
 // 32 = timeline: s_memrealtime stamps of step PB_STAMP_S, wave 0 lane 0 of every workgroup,
 // into sync + 4096 words (128 per workgroup; tools/pb_timeline.py).
@@ -138,9 +140,11 @@ __global__ __launch_bounds__(256, 1) void lstm_bwd_persistent_kernel(
     const __amdgpu_buffer_rsrc_t cr = __builtin_amdgcn_make_buffer_rsrc(
         const_cast<float*>(Cst) + (size_t)t * Bp * H, 0, 0x7FFFFFFF, 0x00020000);
     constexpr int SO = RT * HB * 1024 * 2, CO = RT * HB * 256 * 4;
-    sq0[Q] = __builtin_amdgcn_raw_buffer_load_b128(sr, s_vo, SO, 2 /* nt */);
-    sq1[Q] = __builtin_amdgcn_raw_buffer_load_b128(sr, s_vo + 16, SO, 2 /* nt */);
-    cq[Q] = __builtin_amdgcn_raw_buffer_load_b128(cr, c_vo, CO, 2 /* nt */);
+    // nt on the read-once streams (256: default policy; A/B within run-to-run noise)
+    constexpr int NTA = (DBG & 256) ? 0 : 2;
+    sq0[Q] = __builtin_amdgcn_raw_buffer_load_b128(sr, s_vo, SO, NTA);
+    sq1[Q] = __builtin_amdgcn_raw_buffer_load_b128(sr, s_vo + 16, SO, NTA);
+    cq[Q] = __builtin_amdgcn_raw_buffer_load_b128(cr, c_vo, CO, NTA);
   };
   load_sc(d.T - 2, std::integral_constant<int, 0>{}, std::integral_constant<int, 0>{});
   load_sc(d.T - 2, std::integral_constant<int, 1>{}, std::integral_constant<int, 1>{});
@@ -442,6 +446,7 @@ static bool launch_pb(const bf16_t* WhhT, const float* Cst, const bf16_t* S, bf1
       case 64: f = reinterpret_cast<const void*>(&lstm_bwd_persistent_kernel<KT, NRT, 64>); break;
       case 96: f = reinterpret_cast<const void*>(&lstm_bwd_persistent_kernel<KT, NRT, 96>); break;
       case 128: f = reinterpret_cast<const void*>(&lstm_bwd_persistent_kernel<KT, NRT, 128>); break;
+      case 256: f = reinterpret_cast<const void*>(&lstm_bwd_persistent_kernel<KT, NRT, 256>); break;
       default: break;
     }
   }

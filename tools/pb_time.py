@@ -47,8 +47,14 @@ for dbg in ("0", "64"):  # correct builds must match the per-step kernels
     print(f"check dbg{dbg}: max|dDG| {err:.3g} (scale {ref.float().abs().max().item():.3g}) "
           f"timeout word {int(eng.sync_bwd[0].item())}", flush=True)
 dbgs = sys.argv[1].split(",") if len(sys.argv) > 1 else ["0", "1", "2", "4", "8", "16"]
-for dbg in dbgs:
-    os.environ["WELLFLOW_PF_DBG"] = dbg
-    row[f"pb dbg{dbg}"] = timeit(lambda: C.lstm_backward(*args, 8, eng.sync_bwd))
+# variants interleaved over several rounds (a fixed order biases toward the later ones:
+# clocks and caches settle), median per variant
+ts = {}
+for rnd in range(int(os.environ.get("PB_ROUNDS", "3"))):
+    for dbg in (dbgs if rnd % 2 == 0 else dbgs[::-1]):
+        os.environ["WELLFLOW_PF_DBG"] = dbg
+        ts.setdefault(f"pb dbg{dbg}", []).append(timeit(lambda: C.lstm_backward(*args, 8, eng.sync_bwd)))
 os.environ["WELLFLOW_PF_DBG"] = "0"
+for k, v in ts.items():
+    row[k] = statistics.median(v)
 print("bwd chain T=64 B=8192: " + "  ".join(f"{k} {v:.3f}ms" for k, v in row.items()), flush=True)
