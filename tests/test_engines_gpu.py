@@ -1,5 +1,6 @@
 """Native MLP / CNN engines vs the fp32 PyTorch reference modules, and end-to-end native
 training jobs on the MI355X (forward values, flat gradients, learning curves)."""
+import os
 import pytest
 import torch
 
@@ -102,3 +103,31 @@ def test_native_training_job_learns(model, tmp_path):
     assert min(h["val_loss"]) < h["val_loss"][0] or h["val_loss"][-1] < 1.0
     assert out["test_loss"] == out["test_loss"]
     assert (tmp_path / "models" / f"{model}.mdl").exists()
+
+
+def test_lstm_submission_script_from_csv_on_gpu(tmp_path):
+    """The reference's submission contract end to end on the MI355X: the LSTM model script
+    with names / types / target / storagePath and a CSV data path -> native C++ CSV ingest
+    (wellflow/_runtime.so) -> features -> HIP LSTM engine (wellflow/_C.so) -> .mdl + the two
+    stdout lines (cnn.py:2, 41-44, 122, 133-134)."""
+    import subprocess
+    import sys
+
+    from wellflow.data.io import write_csv
+    from wellflow.data.synth import TABLE_COLUMNS, well_log_table
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    data = str(tmp_path / "logs.csv")
+    write_csv(well_log_table(6, 240, seed=9), data, columns=TABLE_COLUMNS)
+    names = ",".join(TABLE_COLUMNS)
+    types = "string,string,int,float,float,float,float,float,float,float"
+    env = dict(os.environ, WELLFLOW_NATIVE_IO="1")
+    r = subprocess.run([sys.executable, os.path.join(root, "Artificial intelligence models", "LSTM models", "lstm.py"),
+                        names, types, "flow", str(tmp_path) + "/", data, "--epochs", "3", "--seq-len", "16",
+                        "--batch-size", "128", "--device", "cuda"],
+                       capture_output=True, text=True, env=env, timeout=300, cwd=str(tmp_path))
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    lines = r.stdout.strip().splitlines()
+    assert lines[-2].startswith("Time elapsed: ") and lines[-1].startswith("Testing set loss: ")
+    assert float(lines[-1].split(":")[1]) == float(lines[-1].split(":")[1])  # finite, parseable
+    assert (tmp_path / "models" / "lstm.mdl").exists()
