@@ -383,6 +383,42 @@ void head_fwd(const at::Tensor& Hm, int64_t ldh, int64_t B, int64_t Hd, const at
                       cur_stream());
 }
 
+// Fused MLP forward (mlp_fused.hip): both 256-wide hidden layers + head (+ MSE) in one launch.
+// Returns false (nothing launched) when the shape is not covered; the caller then runs the
+// per-layer GEMMs + head kernel.
+bool mlp2_forward(const at::Tensor& X, int64_t Fp, const at::Tensor& W1, const at::Tensor& b1,
+                  const at::Tensor& W2, const at::Tensor& b2, const at::Tensor& w3, const at::Tensor& b3,
+                  c10::optional<at::Tensor> y, const at::Tensor& H1, const at::Tensor& H2,
+                  const at::Tensor& pred, c10::optional<at::Tensor> dy, c10::optional<at::Tensor> loss_sum,
+                  double dy_scale, int64_t B) {
+  constexpr int64_t H = 256;
+  check_t(X, at::kBFloat16, "X");
+  check_extent(X, B * Fp, "X");
+  check_t(W1, at::kBFloat16, "W1");
+  check_extent(W1, H * Fp, "W1");
+  check_t(W2, at::kBFloat16, "W2");
+  check_extent(W2, H * H, "W2");
+  for (const at::Tensor* t : {&b1, &b2, &w3}) {
+    check_t(*t, at::kFloat, "bias/w3");
+    check_extent(*t, H, "bias/w3");
+  }
+  check_t(b3, at::kFloat, "b3");
+  check_t(H1, at::kBFloat16, "H1");
+  check_extent(H1, B * H, "H1");
+  check_t(H2, at::kBFloat16, "H2");
+  check_extent(H2, B * H, "H2");
+  check_t(pred, at::kFloat, "pred");
+  check_extent(pred, B, "pred");
+  for (const at::Tensor* t : {&X, &W1, &W2, &H1, &H2})
+    TORCH_CHECK(reinterpret_cast<uintptr_t>(t->data_ptr()) % 16 == 0, "mlp2_forward: bf16 operands must be 16-B aligned");
+  const c10::hip::OptionalHIPGuardMasqueradingAsCUDA guard(X.device());
+  return wf::launch_mlp2_fwd(bfp(X), (int)Fp, bfp(W1), fp(b1), bfp(W2), fp(b2), fp(w3), fp(b3),
+                             opt_ptr<float>(y, at::kFloat, "y", B), bfp(H1), bfp(H2), fp(pred),
+                             opt_ptr<float>(dy, at::kFloat, "dy", B),
+                             opt_ptr<float>(loss_sum, at::kFloat, "loss_sum", 1), (float)dy_scale, (int)B,
+                             cur_stream());
+}
+
 void head_bwd_w(const at::Tensor& Hm, int64_t ldh, int64_t B, int64_t Hd, const at::Tensor& dy,
                 const at::Tensor& dw, c10::optional<at::Tensor> db) {
   check_head_h(Hm, ldh, B, Hd);
@@ -508,6 +544,7 @@ void im2col1d(const at::Tensor& x, int64_t B, int64_t L, int64_t Cin, int64_t ks
 PYBIND11_MODULE(_C, m) {
   m.doc() = "wellflow HIP kernel library (gfx950)";
   m.def("gemm", &gemm);
+  m.def("mlp2_forward", &mlp2_forward);
   m.def("lstm_pack_x", &lstm_pack_x);
   m.def("lstm_forward", &lstm_forward);
   m.def("lstm_forward_persistent", &lstm_forward_persistent);

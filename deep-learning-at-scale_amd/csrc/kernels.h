@@ -61,6 +61,14 @@ void launch_lstm_bwd_step(int t, const bf16_t* WhhT, const float* Cst, const bf1
 void launch_lstm_pack_weights(const float* W, bf16_t* Wp, bf16_t* WhhT, LstmDims d,
                               hipStream_t s);
 
+// ---- fused MLP forward (mlp_fused.hip): F (<= 32, padded to Fp % 8 == 0) -> 256 -> 256 -> 1,
+// ReLU, bias, linear head, optional MSE (y, dy = dy_scale * (pred - y), loss_sum += (pred - y)^2).
+// Writes H1, H2 ([B][256] bf16: the backward's saved activations) and pred. Returns false
+// (nothing launched) for shapes it does not cover.
+bool launch_mlp2_fwd(const bf16_t* X, int Fp, const bf16_t* W1, const float* b1, const bf16_t* W2, const float* b2,
+                     const float* w3, const float* b3, const float* y, bf16_t* H1, bf16_t* H2, float* pred, float* dy,
+                     float* loss_sum, float dy_scale, int B, hipStream_t s);
+
 // ---- regression head (N = 1) and losses ----
 void launch_head_fwd(const bf16_t* Hm, long ldh, int B, int Hd, const float* w, const float* b0,
                      const float* target, float* pred, float* dy, float* loss_sum, float dy_scale,

@@ -1,0 +1,214 @@
+// wellflow — fused, weight-stationary forward of the static / dynamic MLP regressor
+// (BASELINE.json:8-10: F -> 256 -> 256 -> 1, ReLU, linear head, MSE; SURVEY.md §2.4 K10, K15,
+// K16).
+//
+// Why: per layer, the generic GEMM path (gemm.hip) streams the activations through HBM
+// and re-reads the 256 x 256 weight tile in every one of its 1024 short-lived workgroups,
+// then a separate head kernel re-reads the last hidden layer: ~84 us of a 0.3 ms training
+// step at 65,536 rows for ~71 MB of compulsory traffic. Here ONE launch does
+//   Z1 = X W1^T + b1, H1 = relu(Z1); Z2 = H1 W2^T + b2, H2 = relu(Z2);
+//   pred = H2 w3 + b3; (MSE) dy = s (pred - y), loss += (pred - y)^2
+// with every weight resident in registers for the whole launch:
+//  * grid <= 256 workgroups of 256 threads (4 waves, one per SIMD), persistent over
+//    64-row chunks; wave w owns hidden units [64w, 64w + 64) of both layers.
+//  * transposed products: C = W (A operand: weights, lane = unit) x act^T (B operand:
+//    activations, lane = row), so each lane's MFMA result holds 4 CONSECUTIVE units of one
+//    row — packed to 8 bytes it lands in the LDS activation tile [row][unit] that the next
+//    layer reads as 16-byte B fragments (conflict-free XOR swizzle).
+//  * W1 slice 16 VGPRs, W2 slice 128 VGPRs per lane (loaded once); H1 / H2 leave the CU
+//    once each, as whole 16-byte row segments (they are the backward pass's saved
+//    activations); the head dot product is reduced across lanes (DPP) and waves (LDS).
+#include "common.h"
+#include "kernels.h"
+
+namespace wf {
+
+namespace {
+constexpr int MF_ROWS = 64;  // rows per chunk
+constexpr int MF_H = 256;    // hidden width (both layers)
+
+// [64 rows][256 units] bf16 tile, 16-B chunk c (units 8c..8c+7) of row r at chunk c ^ (r & 15)
+// (32 chunks per row, 512-B rows): the B-fragment reads (16 rows x one chunk) hit 16 distinct
+// 16-B bank groups, as do the row-wise copy-out reads.
+__device__ __forceinline__ int tile_off(int row, int unit) {
+  const int c = unit >> 3;
+  return row * (MF_H * 2) + ((c ^ (row & 15)) << 4) + ((unit & 7) << 1);
+}
+// [64 rows][32 features] bf16 input tile (4 chunks per row, 64-B rows: rows r, r+4, r+8, r+12
+// share a bank group, so the chunk is swizzled by (row >> 2) & 3)
+__device__ __forceinline__ int xtile_off(int row, int chunk) { return row * 64 + ((chunk ^ ((row >> 2) & 3)) << 4); }
+}  // namespace
+
+__global__ __launch_bounds__(256, 1) void mlp2_fwd_kernel(
+    const bf16_t* __restrict__ X, int Fp, const bf16_t* __restrict__ W1, const float* __restrict__ b1,
+    const bf16_t* __restrict__ W2, const float* __restrict__ b2, const float* __restrict__ w3,
+    const float* __restrict__ b3, const float* __restrict__ y, bf16_t* __restrict__ H1, bf16_t* __restrict__ H2,
+    float* __restrict__ pred, float* __restrict__ dy, float* __restrict__ loss_sum, float dy_scale, int B) {
+  __shared__ __attribute__((aligned(16))) char xs[MF_ROWS * 64];
+  __shared__ __attribute__((aligned(16))) char h1s[MF_ROWS * MF_H * 2];
+  __shared__ __attribute__((aligned(16))) char h2s[MF_ROWS * MF_H * 2];
+  __shared__ float red[4][MF_ROWS];
+  __shared__ float lred[4];
+
+  const int lane = threadIdx.x & 63, l15 = lane & 15, g = lane >> 4;
+  const int wid = threadIdx.x >> 6;
+  const int u0 = wid * 64;  // first unit of this wave
+
+  // ---- stationary weights (A operand: lane = unit l15 of M-tile m, k 8g..8g+7)
+  bf16x8 w1f[4], w2f[4][8];
+  float bias1[4][4], bias2[4][4], w3v[4][4];
+#pragma unroll
+  for (int m = 0; m < 4; ++m) {
+    const int u = u0 + 16 * m + l15;
+    if (8 * g + 8 <= Fp)
+      w1f[m] = *reinterpret_cast<const bf16x8*>(W1 + (size_t)u * Fp + 8 * g);
+    else
+      w1f[m] = bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+    for (int kt = 0; kt < 8; ++kt) w2f[m][kt] = *reinterpret_cast<const bf16x8*>(W2 + (size_t)u * MF_H + 32 * kt + 8 * g);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {  // C rows of this lane: units 16m + 4g + r
+      const int uc = u0 + 16 * m + 4 * g + r;
+      bias1[m][r] = b1[uc];
+      bias2[m][r] = b2[uc];
+      w3v[m][r] = w3[uc];
+    }
+  }
+  const float bias3 = b3[0];
+  float lsum = 0.f;
+
+  const int nchunks = (B + MF_ROWS - 1) / MF_ROWS;
+  for (int ch = blockIdx.x; ch < nchunks; ch += gridDim.x) {
+    const int row0 = ch * MF_ROWS;
+    // ---- X chunk -> LDS, zero-padded to 32 features (thread: row t >> 2, 16-B chunk t & 3)
+    {
+      const int r = threadIdx.x >> 2, c = threadIdx.x & 3, gr = row0 + r;
+      uint4 v = make_uint4(0, 0, 0, 0);
+      if (gr < B && 8 * c + 8 <= Fp) v = *reinterpret_cast<const uint4*>(X + (size_t)gr * Fp + 8 * c);
+      *reinterpret_cast<uint4*>(xs + xtile_off(r, c)) = v;
+    }
+    __syncthreads();
+
+    // ---- layer 1: Z1^T (64 units x 64 rows per wave) = W1 x X^T, K = 32
+    f32x4 acc[4][4];
+#pragma unroll
+    for (int n = 0; n < 4; ++n) {
+      const bf16x8 xb = *reinterpret_cast<const bf16x8*>(xs + xtile_off(16 * n + l15, g));
+#pragma unroll
+      for (int m = 0; m < 4; ++m)
+        acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w1f[m], xb, f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+    }
+    // epilogue 1: + b1, relu, 4 units -> 8 B into the H1 tile
+#pragma unroll
+    for (int m = 0; m < 4; ++m)
+#pragma unroll
+      for (int n = 0; n < 4; ++n) {
+        unsigned pk[2];
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+          const float v0 = fmaxf(acc[m][n][2 * q] + bias1[m][2 * q], 0.f);
+          const float v1 = fmaxf(acc[m][n][2 * q + 1] + bias1[m][2 * q + 1], 0.f);
+          pk[q] = (unsigned)f2bf(v0) | ((unsigned)f2bf(v1) << 16);
+        }
+        *reinterpret_cast<uint2*>(h1s + tile_off(16 * n + l15, u0 + 16 * m + 4 * g)) = make_uint2(pk[0], pk[1]);
+      }
+    __syncthreads();
+
+    // ---- H1 tile -> HBM (saved for the backward): 64 rows x 512 B, 16-B stores
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int idx = threadIdx.x + 256 * k, r = idx >> 5, c = idx & 31, gr = row0 + r;
+      if (gr < B)
+        *reinterpret_cast<uint4*>(H1 + (size_t)gr * MF_H + 8 * c) =
+            *reinterpret_cast<const uint4*>(h1s + tile_off(r, 8 * c));
+    }
+
+    // ---- layer 2: Z2^T = W2 x H1^T, K = 256 (8 k-tiles)
+#pragma unroll
+    for (int m = 0; m < 4; ++m)
+#pragma unroll
+      for (int n = 0; n < 4; ++n) acc[m][n] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int kt = 0; kt < 8; ++kt) {
+      bf16x8 hb[4];
+#pragma unroll
+      for (int n = 0; n < 4; ++n) hb[n] = *reinterpret_cast<const bf16x8*>(h1s + tile_off(16 * n + l15, 32 * kt + 8 * g));
+#pragma unroll
+      for (int m = 0; m < 4; ++m)
+#pragma unroll
+        for (int n = 0; n < 4; ++n)
+          acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w2f[m][kt], hb[n], acc[m][n], 0, 0, 0);
+    }
+    // epilogue 2: + b2, relu -> H2 tile; head partial sums per row
+    float hp[4] = {0.f, 0.f, 0.f, 0.f};  // rows 16n + l15, this lane's 16 units
+#pragma unroll
+    for (int m = 0; m < 4; ++m)
+#pragma unroll
+      for (int n = 0; n < 4; ++n) {
+        float v[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          // round to bf16 first: the head consumes exactly the H2 the backward will see
+          v[r] = bf2f(f2bf(fmaxf(acc[m][n][r] + bias2[m][r], 0.f)));
+          hp[n] += v[r] * w3v[m][r];
+        }
+        const unsigned p0 = (unsigned)f2bf(v[0]) | ((unsigned)f2bf(v[1]) << 16);
+        const unsigned p1 = (unsigned)f2bf(v[2]) | ((unsigned)f2bf(v[3]) << 16);
+        *reinterpret_cast<uint2*>(h2s + tile_off(16 * n + l15, u0 + 16 * m + 4 * g)) = make_uint2(p0, p1);
+      }
+    // sum the 4 lane groups g (same row l15): lanes l15, l15 + 16, + 32, + 48
+#pragma unroll
+    for (int n = 0; n < 4; ++n) {
+      hp[n] += __shfl_xor(hp[n], 16, 64);
+      hp[n] += __shfl_xor(hp[n], 32, 64);
+    }
+    if (g == 0) {
+#pragma unroll
+      for (int n = 0; n < 4; ++n) red[wid][16 * n + l15] = hp[n];
+    }
+    __syncthreads();
+
+    // ---- H2 tile -> HBM; head + loss for the chunk's rows (threads 0..63)
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int idx = threadIdx.x + 256 * k, r = idx >> 5, c = idx & 31, gr = row0 + r;
+      if (gr < B)
+        *reinterpret_cast<uint4*>(H2 + (size_t)gr * MF_H + 8 * c) =
+            *reinterpret_cast<const uint4*>(h2s + tile_off(r, 8 * c));
+    }
+    if (threadIdx.x < MF_ROWS) {
+      const int gr = row0 + threadIdx.x;
+      if (gr < B) {
+        const float p = red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] + red[3][threadIdx.x] + bias3;
+        pred[gr] = p;
+        if (y != nullptr) {
+          const float diff = p - y[gr];
+          lsum += diff * diff;
+          if (dy != nullptr) dy[gr] = dy_scale * diff;
+        }
+      }
+    }
+    __syncthreads();  // xs / h1s / h2s / red are rewritten by the next chunk
+  }
+  if (loss_sum != nullptr) {
+    const float t = block_sum<256>(lsum, lred);
+    if (threadIdx.x == 0 && t != 0.f) atomicAdd(loss_sum, t);
+  }
+}
+
+bool launch_mlp2_fwd(const bf16_t* X, int Fp, const bf16_t* W1, const float* b1, const bf16_t* W2, const float* b2,
+                     const float* w3, const float* b3, const float* y, bf16_t* H1, bf16_t* H2, float* pred, float* dy,
+                     float* loss_sum, float dy_scale, int B, hipStream_t s) {
+  if (Fp > 32 || Fp % 8 != 0 || B <= 0) return false;
+  const int nchunks = (B + MF_ROWS - 1) / MF_ROWS;
+  int dev = 0, cus = 0;
+  if (hipGetDevice(&dev) != hipSuccess ||
+      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+    cus = 256;
+  const int grid = nchunks < cus ? nchunks : cus;
+  hipLaunchKernelGGL(mlp2_fwd_kernel, dim3(grid), dim3(256), 0, s, X, Fp, W1, b1, W2, b2, w3, b3, y, H1, H2, pred,
+                     dy, loss_sum, dy_scale, B);
+  return true;
+}
+
+}  // namespace wf

@@ -20,6 +20,8 @@ from __future__ import annotations
 import dataclasses
 import math
 
+import os
+
 import torch
 from torch import nn
 
@@ -142,6 +144,8 @@ class NativeMLP:
         self.pred = torch.empty(batch, device=dev)
         self.dy = torch.empty(batch, device=dev)
         self.loss_sum = torch.zeros(1, device=dev)
+        # fused weight-stationary forward for the 256 x 256 BASELINE shape (WELLFLOW_MLP_FUSED=0: per-layer)
+        self.fused = os.environ.get("WELLFLOW_MLP_FUSED", "1") != "0"
         self.sync_weights()
 
     def sync_weights(self) -> None:
@@ -167,8 +171,20 @@ class NativeMLP:
             gemm(A, W, B, h, k, outH=Hout, bias=b, act=1)
             A, K = Hout, h
 
+    def _fused_forward(self, B: int, y=None, dy=None, loss_sum=None, dy_scale: float = 0.0) -> bool:
+        """Both hidden layers + head (+ MSE) in ONE weight-stationary launch
+        (csrc/mlp_fused.hip) for the BASELINE shape F -> 256 -> 256 -> 1; False = not covered."""
+        if not self.fused or self.hidden != (256, 256) or self.Fp > 32:
+            return False
+        wl, _, _ = self.lay.views(self.shadow)
+        pl, hw, hb = self.lay.views(self.params)
+        return bool(self._C.mlp2_forward(self.X, self.Fp, wl[0][0], pl[0][1], wl[1][0], pl[1][1], hw, hb, y,
+                                         self.Hs[0], self.Hs[1], self.pred, dy, loss_sum, float(dy_scale), B))
+
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         B = self._load_x(x)
+        if self._fused_forward(B):
+            return self.pred[:B]
         self._forward_body(B)
         _, hw, hb = self.lay.views(self.params)
         H = self.hidden[-1]
@@ -184,18 +200,22 @@ class NativeMLP:
         if zero_grads:
             self.grads.zero_()
         self.loss_sum.zero_()
-        self._forward_body(B)
         pl, hw, hb = self.lay.views(self.params)
         gl, ghw, ghb = self.lay.views(self.grads)
         wl, _, _ = self.lay.views(self.shadow)
         L = len(self.hidden)
         H = self.hidden[-1]
         y = y.contiguous().float()
-        if self.loss_kind == "mse":
+        if self.loss_kind == "mse" and self._fused_forward(B, y, self.dy, self.loss_sum, 2.0 * float(grad_scale)):
+            pass  # layers + head + MSE + dy in one launch
+        elif self.loss_kind == "mse":
+            self._forward_body(B)
             C.head_fwd(self.Hs[-1], H, B, H, hw, hb, y, self.pred, self.dy, self.loss_sum,
                        2.0 * float(grad_scale))
         else:
-            C.head_fwd(self.Hs[-1], H, B, H, hw, hb, None, self.pred, None, None, 0.0)
+            if not self._fused_forward(B):
+                self._forward_body(B)
+                C.head_fwd(self.Hs[-1], H, B, H, hw, hb, None, self.pred, None, None, 0.0)
             C.loss(1, self.pred, y, B, 1, self.clip, float(grad_scale), self.loss_sum, None,
                    self.dy, None)
         C.head_bwd_w(self.Hs[-1], H, B, H, self.dy, ghw, ghb)

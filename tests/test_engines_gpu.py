@@ -131,3 +131,32 @@ def test_lstm_submission_script_from_csv_on_gpu(tmp_path):
     assert lines[-2].startswith("Time elapsed: ") and lines[-1].startswith("Testing set loss: ")
     assert float(lines[-1].split(":")[1]) == float(lines[-1].split(":")[1])  # finite, parseable
     assert (tmp_path / "models" / "lstm.mdl").exists()
+
+
+@pytest.mark.parametrize("B,F", [(65536, 16), (1000, 9), (64, 32)])
+def test_fused_mlp_forward_matches_per_layer(B, F):
+    """The one-launch weight-stationary MLP forward (csrc/mlp_fused.hip) against the
+    per-layer GEMM + head path on the same weights: saved activations, predictions, loss and
+    the gradients the unchanged backward computes from them."""
+    from wellflow.data.synth import synth_tabular_batch
+    from wellflow.models.mlp import NativeMLP, init_mlp_flat
+
+    eng = NativeMLP(F, (256, 256), B, device=DEV)
+    eng.params.copy_(init_mlp_flat(F, (256, 256), seed=3).to(DEV))
+    eng.sync_weights()
+    x, y = synth_tabular_batch(B, F, seed=4)
+    x, y = x.to(DEV), y.to(DEV)
+    res = {}
+    for fused in (False, True):
+        eng.fused = fused
+        ls = eng.forward_backward(x, y, grad_scale=1.0 / B).item()
+        torch.cuda.synchronize()
+        res[fused] = (eng.Hs[0][: B * 256].float().clone(), eng.Hs[1][: B * 256].float().clone(),
+                      eng.pred[:B].clone(), eng.dy[:B].clone(), ls, eng.grads.clone())
+    (h1a, h2a, pa, da, la, ga), (h1b, h2b, pb, db, lb, gb) = res[False], res[True]
+    assert (h1a - h1b).abs().max().item() <= 1e-2 * max(1.0, h1a.abs().max().item())
+    assert (h2a - h2b).abs().max().item() <= 2e-2 * max(1.0, h2a.abs().max().item())
+    assert (pa - pb).abs().max().item() <= 1e-2 * max(1.0, pa.abs().max().item())
+    assert abs(la - lb) <= 1e-3 * abs(la) + 1e-6
+    assert ((ga - gb).norm() / ga.norm()).item() < 1e-2
+    assert torch.allclose(da, db, rtol=1e-2, atol=1e-6 * max(1.0, da.abs().max().item()))
