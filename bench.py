@@ -27,7 +27,9 @@ if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
 
 METRIC = "rows/sec (whole node), LSTM seq64 regression at 1/2/4/8 MI355X; val MSE parity"
-DEFAULT_BATCH = {"lstm": 8192, "mlp": 65536, "mlp_online": 65536}
+# per-GPU rows per step. MLP: 262144 rows (bf16 activations ~270 MB of 288 GB HBM) — at
+# 65536 the 0.24 ms step is launch/stream-overhead bound (216-272 M rows/s vs 382 M here)
+DEFAULT_BATCH = {"lstm": 8192, "mlp": 262144, "mlp_online": 262144}
 
 
 def _timed(ctx, step, steps, warmup):
@@ -133,7 +135,10 @@ def bench_mlp(args, ctx, online: bool):
     gscale = 1.0 / (B * ctx.world_size)
 
     if online:
-        pool = HostPool(lambda k: synth_tabular_batch(B, F, seed=1000 * ctx.rank + k), n=8)
+        # features cross PCIe as bf16 (the engine's MFMA input format: identical numerics to
+        # streaming fp32 and casting on the device, half the bytes); targets stay fp32
+        x_dtype = torch.float32 if args.stream_fp32 else torch.bfloat16
+        pool = HostPool(lambda k: synth_tabular_batch(B, F, seed=1000 * ctx.rank + k), n=8, x_dtype=x_dtype)
         depth = 3
         streamer = DeviceStreamer(pool, ctx.device, depth=depth)
         for _ in range(depth):  # allocate every ring slot
@@ -204,6 +209,7 @@ def main() -> int:
     ap.add_argument("--fwd-variant", type=int, default=None)
     ap.add_argument("--bwd-variant", type=int, default=None)
     ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--stream-fp32", action="store_true", help="mlp_online: stream fp32 features")
     args = ap.parse_args()
     if args.batch is None:
         args.batch = DEFAULT_BATCH[args.model]

@@ -155,7 +155,10 @@ class NativeMLP:
         B = x.shape[0]
         assert B <= self.B and x.shape[1] == self.F
         Xv = self.X[: B * self.Fp].view(B, self.Fp)
-        if self.Fp == self.F:
+        if x.dtype == torch.bfloat16 and self.Fp == self.F:
+            # already in the MFMA input format (bf16-streamed online batches): one D2D copy
+            Xv.copy_(x)
+        elif self.Fp == self.F:
             self._C.cast_bf16(x.contiguous().float(), Xv)
         else:
             self._C.transpose_cast_bf16(x.t().contiguous().float(), B, self.F, B, Xv, self.Fp)

@@ -160,3 +160,27 @@ def test_fused_mlp_forward_matches_per_layer(B, F):
     assert abs(la - lb) <= 1e-3 * abs(la) + 1e-6
     assert ((ga - gb).norm() / ga.norm()).item() < 1e-2
     assert torch.allclose(da, db, rtol=1e-2, atol=1e-6 * max(1.0, da.abs().max().item()))
+
+
+def test_mlp_bf16_input_matches_fp32_input():
+    """bf16-streamed features (online bench, data/stream.py) give the same step as fp32
+    features: the engine casts fp32 to bf16 itself, so predictions are bitwise equal."""
+    from wellflow.data.synth import synth_tabular_batch
+    from wellflow.models.mlp import NativeMLP, init_mlp_flat
+
+    B, F = 262144, 16
+    eng = NativeMLP(F, (256, 256), B, device=DEV)
+    eng.params.copy_(init_mlp_flat(F, (256, 256), seed=5).to(DEV))
+    eng.sync_weights()
+    x, y = synth_tabular_batch(B, F, seed=6)
+    x, y = x.to(DEV), y.to(DEV)
+    out = []
+    for xin in (x, x.to(torch.bfloat16)):
+        ls = eng.forward_backward(xin, y, grad_scale=1.0 / B).item()
+        torch.cuda.synchronize()
+        out.append((ls, eng.pred[:B].clone(), eng.grads.clone()))
+    (la, pa, ga), (lb, pb, gb) = out
+    assert torch.equal(pa, pb)
+    # fp32 atomics in the split-K dW reduce in a run-dependent order: compare with a tolerance
+    assert abs(la - lb) <= 1e-5 * abs(la) + 1e-6
+    assert ((ga - gb).norm() / ga.norm()).item() < 1e-5
