@@ -35,14 +35,18 @@ DEFAULT_BATCH = {"lstm": 8192, "mlp": 262144, "mlp_online": 262144}
 def _timed(ctx, step, steps, warmup):
     import torch
 
+    def sync():
+        if ctx.device.type == "cuda":
+            torch.cuda.synchronize()
+
     for _ in range(warmup):
         step()
     ctx.barrier()
-    torch.cuda.synchronize()
+    sync()
     t0 = time.perf_counter()
     for _ in range(steps):
         step()
-    torch.cuda.synchronize()
+    sync()
     ctx.barrier()
     return ctx.max_scalar(time.perf_counter() - t0)
 
@@ -87,6 +91,9 @@ def bench_lstm(args, ctx):
     from wellflow.optim.flat import FlatAdam
 
     B, T, F, H = args.batch, args.seq, args.features, args.hidden
+    model = f"LSTM seq-len={T} hidden={H} time-series regression (features={F}, linear head, MSE, Adam)"
+    if ctx.device.type == "cpu":
+        return _cpu_rehearsal(args, ctx, model)
     eng = NativeLSTM(F, H, T, B, device=ctx.device)
     if args.dw_chunk is not None:
         eng.dw_chunk = args.dw_chunk
@@ -114,8 +121,42 @@ def bench_lstm(args, ctx):
     step = _graph_step(ctx, eng, compute, update, args.no_graph or eng.dw_chunk > 0)
 
     el = _timed(ctx, step, args.steps, args.warmup)
-    model = f"LSTM seq-len={T} hidden={H} time-series regression (features={F}, linear head, MSE, Adam)"
     return el, B, model, eng.loss_sum.item() / B
+
+
+def _cpu_rehearsal(args, ctx, model):
+    """--device cpu: the same timed DP step (C1 broadcast, C2 flat all-reduce, flat Adam)
+    on the fp32 PyTorch reference model over gloo. It exists so the launch / timing / JSON
+    contract at world size > 1 is exercised without GPUs (tests/test_bench_cpu.py); its
+    numbers are NOT the benchmark (the line says dtype fp32 and data 'cpu rehearsal')."""
+    import torch
+
+    from wellflow.data.synth import synth_lstm_batch, synth_tabular_batch
+    from wellflow.models.base import TorchEngine
+    from wellflow.models.lstm import LSTMRegressor
+    from wellflow.models.mlp import MLPRegressor
+    from wellflow.optim.flat import FlatAdam
+
+    torch.manual_seed(0)
+    B, F = args.batch, args.features
+    if args.model == "lstm":
+        eng = TorchEngine(LSTMRegressor(F, args.hidden))
+        x, y = synth_lstm_batch(B, args.seq, F, seed=ctx.rank)
+    else:
+        eng = TorchEngine(MLPRegressor(F, (256, 256)))
+        x, y = synth_tabular_batch(B, F, seed=ctx.rank)
+    ctx.broadcast_(eng.params)
+    opt = FlatAdam(eng.params, eng.grads, lr=args.lr)
+    gscale = 1.0 / (B * ctx.world_size)
+    last = [0.0]
+
+    def step():
+        last[0] = float(eng.forward_backward(x, y, gscale))
+        ctx.all_reduce_sum_(eng.grads)
+        opt.step()
+
+    el = _timed(ctx, step, args.steps, args.warmup)
+    return el, B, model, last[0] / B
 
 
 def bench_mlp(args, ctx, online: bool):
@@ -127,6 +168,10 @@ def bench_mlp(args, ctx, online: bool):
     from wellflow.optim.flat import FlatAdam
 
     B, F, hid = args.batch, args.features, (256, 256)
+    kind = "dynamic (online, host->HBM streamed mini-batches)" if online else "static (resident batch)"
+    model = f"{kind} 3-layer MLP regression F={F} -> 256 -> 256 -> 1, MSE, Adam"
+    if ctx.device.type == "cpu":
+        return _cpu_rehearsal(args, ctx, model)
     eng = NativeMLP(F, hid, B, device=ctx.device)
     eng.params.copy_(init_mlp_flat(F, hid, seed=0).to(ctx.device))
     ctx.broadcast_(eng.params)
@@ -189,8 +234,6 @@ def bench_mlp(args, ctx, online: bool):
         step = _graph_step(ctx, eng, compute, update, args.no_graph)
 
     el = _timed(ctx, step, args.steps, args.warmup)
-    kind = "dynamic (online, host->HBM streamed mini-batches)" if online else "static (resident batch)"
-    model = f"{kind} 3-layer MLP regression F={F} -> 256 -> 256 -> 1, MSE, Adam"
     return el, B, model, eng.loss_sum.item() / B
 
 
@@ -210,6 +253,8 @@ def main() -> int:
     ap.add_argument("--bwd-variant", type=int, default=None)
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--stream-fp32", action="store_true", help="mlp_online: stream fp32 features")
+    ap.add_argument("--device", choices=["auto", "cpu"], default="auto",
+                    help="cpu: rehearse the launch/timing/JSON contract on the fp32 reference over gloo")
     args = ap.parse_args()
     if args.batch is None:
         args.batch = DEFAULT_BATCH[args.model]
@@ -218,7 +263,12 @@ def main() -> int:
 
     from wellflow.parallel.dist import DistContext
 
-    ctx = DistContext.from_env()
+    if args.device == "auto" and not torch.cuda.is_available():
+        # never fall back silently: a CPU number is not the benchmark
+        print("bench.py: no GPU visible (use --device cpu for the contract rehearsal)", file=sys.stderr)
+        return 2
+    ctx = DistContext.from_env(device="cpu" if args.device == "cpu" else None)
+    cpu = ctx.device.type == "cpu"
     if ctx.world_size != args.gpus and ctx.is_main:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE={ctx.world_size}", file=sys.stderr)
     torch.manual_seed(1234 + ctx.rank)
@@ -240,8 +290,9 @@ def main() -> int:
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,  # the reference publishes no numbers (BASELINE.json "published": {})
-            "dtype": "bf16",
-            "data": "synthetic (Gilbert-equation well-log data), random-init weights",
+            "dtype": "fp32" if cpu else "bf16",
+            "data": "synthetic (Gilbert-equation well-log data), random-init weights"
+                    + ("; CPU contract rehearsal, not a benchmark" if cpu else ""),
             "config": {
                 "model": model,
                 "global_batch": B * W,

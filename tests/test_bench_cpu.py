@@ -1,0 +1,67 @@
+"""bench.py contract at world size 1, 2 and 4 without GPUs (--device cpu: gloo + the fp32
+reference model). The driver launches bench.py under torch.distributed.run on 1/2/4/8
+MI355X once per round; this rehearses everything around the kernels: rendezvous on
+127.0.0.1, C1 broadcast, C2 all-reduce, the barrier-bracketed timing, max over ranks, and
+exactly ONE JSON line from rank 0 with the whole-job aggregate value."""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+KEYS = {"metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better",
+        "scaling", "vs_baseline", "dtype", "data", "config"}
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _run(world, model, extra):
+    env = dict(os.environ, CUDA_VISIBLE_DEVICES="", OMP_NUM_THREADS="1")
+    args = ["bench.py", "--gpus", str(world), "--steps", "3", "--warmup", "1", "--device", "cpu",
+            "--model", model] + extra
+    if world > 1:
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
+               "--master-addr", "127.0.0.1", "--master-port", str(_port())] + args
+    else:
+        cmd = [sys.executable] + args
+    r = subprocess.run(cmd, capture_output=True, text=True, env=env, cwd=ROOT, timeout=300)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    return json.loads(lines[0])
+
+
+@pytest.mark.parametrize("world", [1, 2, 4])
+def test_bench_json_contract_lstm(world):
+    B = 4
+    rec = _run(world, "lstm", ["--batch", str(B), "--seq", "6", "--hidden", "16"])
+    assert KEYS <= set(rec)
+    assert rec["n_gpus"] == world and rec["steps"] == 3 and rec["warmup"] == 1
+    assert rec["config"]["global_batch"] == B * world and rec["config"]["parallelism"] == f"dp{world}"
+    assert rec["config"]["seq_len"] == 6
+    assert rec["metric"].startswith("rows/sec (whole node), LSTM seq64")
+    # value is the whole-job aggregate: global rows per step / seconds per step
+    assert rec["value"] == pytest.approx(B * world / (rec["ms_per_step"] / 1000.0), rel=1e-3)
+    assert rec["dtype"] == "fp32" and "rehearsal" in rec["data"]  # never mistaken for the benchmark
+    assert rec["higher_is_better"] is True and rec["scaling"] == "weak"
+
+
+def test_bench_json_contract_mlp_dp2():
+    rec = _run(2, "mlp", ["--batch", "64"])
+    assert rec["config"]["global_batch"] == 128 and rec["n_gpus"] == 2
+
+
+def test_bench_refuses_without_gpu():
+    env = dict(os.environ, CUDA_VISIBLE_DEVICES="")
+    r = subprocess.run([sys.executable, "bench.py", "--steps", "1", "--warmup", "0"], capture_output=True,
+                       text=True, env=env, cwd=ROOT, timeout=300)
+    assert r.returncode == 2 and not r.stdout.strip()

@@ -41,20 +41,32 @@ def _torchrun(tmp_path, body: str, nproc: int, timeout=300, extra_env=None, max_
     return [json.load(open(tmp_path / f"rank{i}.json")) for i in range(nproc)]
 
 
-@pytest.mark.parametrize("world", [2, 4])
-def test_dp_step_equals_single_process_step(tmp_path, world):
+@pytest.mark.parametrize("world,kind", [(2, "mlp"), (4, "mlp"), (8, "mlp"), (2, "lstm"), (4, "cnn")])
+def test_dp_step_equals_single_process_step(tmp_path, world, kind):
     res = _torchrun(tmp_path, """
         from wellflow.models.base import TorchEngine
         from wellflow.models.mlp import MLPRegressor
+        from wellflow.models.lstm import LSTMRegressor
+        from wellflow.models.cnn import CNN1DRegressor
         from wellflow.optim.flat import FlatAdam
+        KIND = __KIND__
+        def make():
+            if KIND == "mlp":
+                return MLPRegressor(6, (16, 8))
+            if KIND == "lstm":
+                return LSTMRegressor(6, 8)
+            return CNN1DRegressor(input_len=10, in_ch=6, filters=4, kernel=3, outputs=1, dropout=0.0)
+        def data(g):
+            shape = (32, 6) if KIND == "mlp" else (32, 10, 6) if KIND == "cnn" else (32, 5, 6)
+            return torch.randn(*shape, generator=g), torch.randn(32, generator=g)
         ctx = DistContext.from_env(device="cpu")
         W, r = ctx.world_size, ctx.rank
         torch.manual_seed(100 + r)               # different init on purpose ...
-        eng = TorchEngine(MLPRegressor(6, (16, 8)), loss="mse")
+        eng = TorchEngine(make(), loss="mse")
         ctx.broadcast_(eng.params)               # ... C1 makes them identical
         opt = FlatAdam(eng.params, eng.grads, lr=1e-2)
         g = torch.Generator().manual_seed(0)
-        X, Y = torch.randn(32, 6, generator=g), torch.randn(32, generator=g)
+        X, Y = data(g)
         B = 32 // W
         for step in range(3):
             xb, yb = X[r * B:(r + 1) * B], Y[r * B:(r + 1) * B]
@@ -63,7 +75,7 @@ def test_dp_step_equals_single_process_step(tmp_path, world):
             opt.step()
         # single-process reference on the full batch, from the broadcast init
         torch.manual_seed(100)
-        ref = TorchEngine(MLPRegressor(6, (16, 8)), loss="mse")
+        ref = TorchEngine(make(), loss="mse")
         ropt = FlatAdam(ref.params, ref.grads, lr=1e-2)
         for step in range(3):
             ref.forward_backward(X, Y, grad_scale=1.0 / 32)
@@ -71,7 +83,7 @@ def test_dp_step_equals_single_process_step(tmp_path, world):
         err = (eng.params - ref.params).abs().max().item()
         json.dump({"err": err, "p0": eng.params[:5].tolist()}, open(f"{OUT}/rank{r}.json", "w"))
         ctx.shutdown()
-    """, world)
+    """.replace("__KIND__", repr(kind)), world)
     for rr in res:
         assert rr["err"] < 1e-5
     assert all(rr["p0"] == res[0]["p0"] for rr in res)
