@@ -383,6 +383,32 @@ void head_fwd(const at::Tensor& Hm, int64_t ldh, int64_t B, int64_t Hd, const at
                       cur_stream());
 }
 
+// Fused MLP backward (mlp_fused.hip) for the F -> 256 -> 256 -> 1 shape: dZ2, dZ1 and the
+// bias / head gradients in one launch (the dW GEMMs stay separate).
+bool mlp2_backward(const at::Tensor& H1, const at::Tensor& H2, const at::Tensor& dy, const at::Tensor& w3,
+                   const at::Tensor& W2, const at::Tensor& dZ1, const at::Tensor& dZ2, const at::Tensor& db1,
+                   const at::Tensor& db2, const at::Tensor& dw3, const at::Tensor& db3, int64_t B) {
+  constexpr int64_t H = 256;
+  for (const at::Tensor* t : {&H1, &H2, &dZ1, &dZ2}) {
+    check_t(*t, at::kBFloat16, "H/dZ");
+    check_extent(*t, B * H, "H/dZ");
+    TORCH_CHECK(reinterpret_cast<uintptr_t>(t->data_ptr()) % 16 == 0, "mlp2_backward: activations must be 16-B aligned");
+  }
+  check_t(W2, at::kBFloat16, "W2");
+  check_extent(W2, H * H, "W2");
+  check_t(dy, at::kFloat, "dy");
+  check_extent(dy, B, "dy");
+  for (const at::Tensor* t : {&w3, &db1, &db2, &dw3}) {
+    check_t(*t, at::kFloat, "w3/db");
+    check_extent(*t, H, "w3/db");
+  }
+  check_t(db3, at::kFloat, "db3");
+  check_extent(db3, 1, "db3");
+  const c10::hip::OptionalHIPGuardMasqueradingAsCUDA guard(H1.device());
+  return wf::launch_mlp2_bwd(bfp(H1), bfp(H2), fp(dy), fp(w3), bfp(W2), bfp(dZ1), bfp(dZ2), fp(db1), fp(db2),
+                             fp(dw3), fp(db3), (int)B, cur_stream());
+}
+
 // Fused MLP forward (mlp_fused.hip): both 256-wide hidden layers + head (+ MSE) in one launch.
 // Returns false (nothing launched) when the shape is not covered; the caller then runs the
 // per-layer GEMMs + head kernel.
@@ -545,6 +571,7 @@ PYBIND11_MODULE(_C, m) {
   m.doc() = "wellflow HIP kernel library (gfx950)";
   m.def("gemm", &gemm);
   m.def("mlp2_forward", &mlp2_forward);
+  m.def("mlp2_backward", &mlp2_backward);
   m.def("lstm_pack_x", &lstm_pack_x);
   m.def("lstm_forward", &lstm_forward);
   m.def("lstm_forward_persistent", &lstm_forward_persistent);

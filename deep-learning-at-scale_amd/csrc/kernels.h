@@ -68,6 +68,12 @@ void launch_lstm_pack_weights(const float* W, bf16_t* Wp, bf16_t* WhhT, LstmDims
 bool launch_mlp2_fwd(const bf16_t* X, int Fp, const bf16_t* W1, const float* b1, const bf16_t* W2, const float* b2,
                      const float* w3, const float* b3, const float* y, bf16_t* H1, bf16_t* H2, float* pred, float* dy,
                      float* loss_sum, float dy_scale, int B, hipStream_t s);
+// ---- fused MLP backward (mlp_fused.hip), everything but the dW1 / dW2 GEMMs: from H1, H2
+// ([B][256] bf16), dy and w3 / W2: dZ2, dZ1 ([B][256] bf16) and db1, db2, dw3, db3 (fp32,
+// accumulated with atomics).
+bool launch_mlp2_bwd(const bf16_t* H1, const bf16_t* H2, const float* dy, const float* w3, const bf16_t* W2,
+                     bf16_t* dZ1, bf16_t* dZ2, float* db1, float* db2, float* dw3, float* db3, int B,
+                     hipStream_t s);
 
 // ---- regression head (N = 1) and losses ----
 void launch_head_fwd(const bf16_t* Hm, long ldh, int B, int Hd, const float* w, const float* b0,

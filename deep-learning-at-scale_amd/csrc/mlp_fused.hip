@@ -1,4 +1,4 @@
-// wellflow — fused, weight-stationary forward of the static / dynamic MLP regressor
+// wellflow — fused, weight-stationary forward (and backward, below) of the static / dynamic MLP regressor
 // (BASELINE.json:8-10: F -> 256 -> 256 -> 1, ReLU, linear head, MSE; SURVEY.md §2.4 K10, K15,
 // K16).
 //
@@ -194,6 +194,205 @@ __global__ __launch_bounds__(256, 1) void mlp2_fwd_kernel(
     const float t = block_sum<256>(lsum, lred);
     if (threadIdx.x == 0 && t != 0.f) atomicAdd(loss_sum, t);
   }
+}
+
+// ----------------------------------------------------------------------------------------
+// Fused backward of the same MLP, everything except the two weight-gradient GEMMs (which
+// reduce over the whole batch and stay split-K GEMMs in gemm.hip):
+//   dw3 += H2^T dy, db3 += sum dy                           (head)
+//   dZ2 = (dy w3^T) * [H2 > 0]  -> HBM (bf16, dW2's operand), db2 += colsum dZ2
+//   dZ1 = (dZ2 W2)  * [H1 > 0]  -> HBM (bf16, dW1's operand), db1 += colsum dZ1
+// Replaces head_bwd_w + head_bwd_x + the dX GEMM (3 launches, dZ2 written then re-read, the
+// 256 x 256 W2 tile re-read by each of ~4000 short workgroups): here H1 / H2 / dy are read
+// once, dZ1 / dZ2 written once, and W2^T stays in registers.
+//  * grid <= 256 workgroups of 4 waves, persistent over 64-row chunks. Wave w owns input
+//    units k in [64w, 64w + 64) of dH1: A operand = W2^T rows (lane = k, K = u, gathered
+//    once: 128 VGPRs), B operand = the dZ2 tile rows from LDS, exactly the forward's
+//    transposed-product pattern, so each lane's result is 4 consecutive k of one row.
+//  * elementwise phase: thread t always handles the 8-unit chunk c = t & 31 (rows
+//    (t >> 5) + 8q), so its db2 / dw3 partials stay in registers across all chunks.
+//  * the H1 tile is staged in LDS for the ReLU mask and overwritten in place by dZ1 (each
+//    lane reads and writes the same 8 bytes), then copied out as 16-B row segments.
+__global__ __launch_bounds__(256, 1) void mlp2_bwd_kernel(
+    const bf16_t* __restrict__ H1, const bf16_t* __restrict__ H2, const float* __restrict__ dy,
+    const float* __restrict__ w3, const bf16_t* __restrict__ W2, bf16_t* __restrict__ dZ1,
+    bf16_t* __restrict__ dZ2, float* __restrict__ db1, float* __restrict__ db2, float* __restrict__ dw3,
+    float* __restrict__ db3, int B) {
+  __shared__ __attribute__((aligned(16))) char zs[MF_ROWS * MF_H * 2];  // dZ2 tile
+  __shared__ __attribute__((aligned(16))) char hs[MF_ROWS * MF_H * 2];  // H1 tile -> dZ1 in place
+  __shared__ float lred[4];
+
+  const int lane = threadIdx.x & 63, l15 = lane & 15, g = lane >> 4;
+  const int wid = threadIdx.x >> 6;
+  const int u0 = wid * 64;
+
+  // ---- stationary W2^T (A operand: lane = input unit k = u0 + 16m + l15, K = output unit u)
+  bf16x8 wt[4][8];
+#pragma unroll
+  for (int m = 0; m < 4; ++m) {
+    const int k = u0 + 16 * m + l15;
+#pragma unroll
+    for (int kt = 0; kt < 8; ++kt)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) wt[m][kt][j] = (short)W2[(size_t)(32 * kt + 8 * g + j) * MF_H + k];
+  }
+  // ---- elementwise-phase ownership: units 8c .. 8c + 7
+  const int c = threadIdx.x & 31, rq = threadIdx.x >> 5;
+  float w3c[8], db2a[8], dw3a[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    w3c[e] = w3[8 * c + e];
+    db2a[e] = 0.f;
+    dw3a[e] = 0.f;
+  }
+  float db3a = 0.f;
+  float db1a[4][4];
+#pragma unroll
+  for (int m = 0; m < 4; ++m)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) db1a[m][i] = 0.f;
+
+  const int nchunks = (B + MF_ROWS - 1) / MF_ROWS;
+  for (int ch = blockIdx.x; ch < nchunks; ch += gridDim.x) {
+    const int row0 = ch * MF_ROWS;
+    // ---- dZ2 (+ head / db2 partials) from H2 and dy; H1 -> LDS (2 rows in flight per
+    // thread: a full unroll keeps 8 x 2 row loads live and spills next to the 128-VGPR W2^T)
+#pragma unroll 2
+    for (int q = 0; q < 8; ++q) {
+      const int r = rq + 8 * q, gr = row0 + r;
+      uint4 h2v = make_uint4(0, 0, 0, 0), h1v = make_uint4(0, 0, 0, 0);
+      float gy = 0.f;
+      if (gr < B) {
+        h2v = *reinterpret_cast<const uint4*>(H2 + (size_t)gr * MF_H + 8 * c);
+        h1v = *reinterpret_cast<const uint4*>(H1 + (size_t)gr * MF_H + 8 * c);
+        gy = dy[gr];
+      }
+      if (c == 0) db3a += gy;
+      const unsigned hw[4] = {h2v.x, h2v.y, h2v.z, h2v.w};
+      unsigned zw[4];
+#pragma unroll
+      for (int p = 0; p < 4; ++p) {
+        unsigned pk = 0;
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const int e = 2 * p + h;
+          const float hv = bf2f((bf16_t)(hw[p] >> (16 * h)));
+          dw3a[e] += gy * hv;
+          const bf16_t zb = f2bf(hv > 0.f ? gy * w3c[e] : 0.f);
+          db2a[e] += bf2f(zb);
+          pk |= (unsigned)zb << (16 * h);
+        }
+        zw[p] = pk;
+      }
+      const uint4 zv = make_uint4(zw[0], zw[1], zw[2], zw[3]);
+      *reinterpret_cast<uint4*>(zs + tile_off(r, 8 * c)) = zv;
+      *reinterpret_cast<uint4*>(hs + tile_off(r, 8 * c)) = h1v;
+      if (gr < B) *reinterpret_cast<uint4*>(dZ2 + (size_t)gr * MF_H + 8 * c) = zv;
+    }
+    __syncthreads();
+
+    // ---- dH1^T (64 k x 64 rows per wave) = W2^T x dZ2^T, K = 256
+    f32x4 acc[4][4];
+#pragma unroll
+    for (int m = 0; m < 4; ++m)
+#pragma unroll
+      for (int n = 0; n < 4; ++n) acc[m][n] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int kt = 0; kt < 8; ++kt) {
+      bf16x8 zb[4];
+#pragma unroll
+      for (int n = 0; n < 4; ++n) zb[n] = *reinterpret_cast<const bf16x8*>(zs + tile_off(16 * n + l15, 32 * kt + 8 * g));
+#pragma unroll
+      for (int m = 0; m < 4; ++m)
+#pragma unroll
+        for (int n = 0; n < 4; ++n)
+          acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wt[m][kt], zb[n], acc[m][n], 0, 0, 0);
+    }
+    // ---- ReLU mask from the H1 tile, dZ1 back into the same 8 bytes, db1 partials
+#pragma unroll
+    for (int m = 0; m < 4; ++m)
+#pragma unroll
+      for (int n = 0; n < 4; ++n) {
+        const int r = 16 * n + l15;
+        uint2* p = reinterpret_cast<uint2*>(hs + tile_off(r, u0 + 16 * m + 4 * g));
+        const uint2 hv = *p;
+        const unsigned hw2[2] = {hv.x, hv.y};
+        unsigned ow[2];
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+          unsigned pk = 0;
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            const int i = 2 * q + h;
+            const bool on = bf2f((bf16_t)(hw2[q] >> (16 * h))) > 0.f && row0 + r < B;
+            const bf16_t vb = f2bf(on ? acc[m][n][i] : 0.f);
+            db1a[m][i] += bf2f(vb);
+            pk |= (unsigned)vb << (16 * h);
+          }
+          ow[q] = pk;
+        }
+        *p = make_uint2(ow[0], ow[1]);
+      }
+    __syncthreads();
+    // ---- dZ1 tile -> HBM
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int idx = threadIdx.x + 256 * k, r = idx >> 5, cc = idx & 31, gr = row0 + r;
+      if (gr < B)
+        *reinterpret_cast<uint4*>(dZ1 + (size_t)gr * MF_H + 8 * cc) =
+            *reinterpret_cast<const uint4*>(hs + tile_off(r, 8 * cc));
+    }
+    __syncthreads();  // zs / hs are rewritten by the next chunk
+  }
+
+  // ---- reductions. db1: lanes of one g share k = u0 + 16m + 4g + i -> sum over l15
+#pragma unroll
+  for (int m = 0; m < 4; ++m)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      float v = db1a[m][i];
+      v += __shfl_xor(v, 1, 64);
+      v += __shfl_xor(v, 2, 64);
+      v += __shfl_xor(v, 4, 64);
+      v += __shfl_xor(v, 8, 64);
+      if (l15 == 0 && v != 0.f) atomicAdd(db1 + u0 + 16 * m + 4 * g + i, v);
+    }
+  // db2 / dw3: the 8 threads of one chunk c (rq = 0..7) -> LDS [8][256] x 2, then one per unit
+  float* sd = reinterpret_cast<float*>(zs);
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    sd[rq * MF_H + 8 * c + e] = db2a[e];
+    sd[8 * MF_H + rq * MF_H + 8 * c + e] = dw3a[e];
+  }
+  __syncthreads();
+  {
+    const int u = threadIdx.x;
+    float s2 = 0.f, s3 = 0.f;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      s2 += sd[q * MF_H + u];
+      s3 += sd[8 * MF_H + q * MF_H + u];
+    }
+    if (s2 != 0.f) atomicAdd(db2 + u, s2);
+    if (s3 != 0.f) atomicAdd(dw3 + u, s3);
+  }
+  const float t3 = block_sum<256>(db3a, lred);
+  if (threadIdx.x == 0 && t3 != 0.f) atomicAdd(db3, t3);
+}
+
+bool launch_mlp2_bwd(const bf16_t* H1, const bf16_t* H2, const float* dy, const float* w3, const bf16_t* W2,
+                     bf16_t* dZ1, bf16_t* dZ2, float* db1, float* db2, float* dw3, float* db3, int B,
+                     hipStream_t s) {
+  if (B <= 0) return false;
+  const int nchunks = (B + MF_ROWS - 1) / MF_ROWS;
+  int dev = 0, cus = 0;
+  if (hipGetDevice(&dev) != hipSuccess ||
+      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+    cus = 256;
+  const int grid = nchunks < cus ? nchunks : cus;
+  hipLaunchKernelGGL(mlp2_bwd_kernel, dim3(grid), dim3(256), 0, s, H1, H2, dy, w3, W2, dZ1, dZ2, db1, db2, dw3,
+                     db3, B);
+  return true;
 }
 
 bool launch_mlp2_fwd(const bf16_t* X, int Fp, const bf16_t* W1, const float* b1, const bf16_t* W2, const float* b2,

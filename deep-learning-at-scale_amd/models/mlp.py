@@ -146,6 +146,7 @@ class NativeMLP:
         self.loss_sum = torch.zeros(1, device=dev)
         # fused weight-stationary forward for the 256 x 256 BASELINE shape (WELLFLOW_MLP_FUSED=0: per-layer)
         self.fused = os.environ.get("WELLFLOW_MLP_FUSED", "1") != "0"
+        self.fused_bwd = os.environ.get("WELLFLOW_MLP_FUSED_BWD", "1") != "0"
         self.sync_weights()
 
     def sync_weights(self) -> None:
@@ -221,8 +222,14 @@ class NativeMLP:
                 C.head_fwd(self.Hs[-1], H, B, H, hw, hb, None, self.pred, None, None, 0.0)
             C.loss(1, self.pred, y, B, 1, self.clip, float(grad_scale), self.loss_sum, None,
                    self.dy, None)
-        C.head_bwd_w(self.Hs[-1], H, B, H, self.dy, ghw, ghb)
-        C.head_bwd_x(self.Hs[-1], H, B, H, self.dy, hw, True, self.dZ[-1], H, gl[-1][1])
+        # fused backward (csrc/mlp_fused.hip) for the BASELINE shape: head + dZ2 + dZ1 + all
+        # bias gradients in one launch; only the two dW GEMMs remain
+        fused_bwd = (self.fused_bwd and self.hidden == (256, 256) and
+                     C.mlp2_backward(self.Hs[0], self.Hs[1], self.dy, hw, wl[1][0], self.dZ[0], self.dZ[1],
+                                     gl[0][1], gl[1][1], ghw, ghb, B))
+        if not fused_bwd:
+            C.head_bwd_w(self.Hs[-1], H, B, H, self.dy, ghw, ghb)
+            C.head_bwd_x(self.Hs[-1], H, B, H, self.dy, hw, True, self.dZ[-1], H, gl[-1][1])
         # dW GEMMs have tiny M x N (a few 128x128 tiles) and K = batch: split K so the
         # grid has ~512 workgroups, each reducing >= 256 rows
         tiles = lambda h, k: ((h + 127) // 128) * ((k + 127) // 128)  # noqa: E731
@@ -234,7 +241,7 @@ class NativeMLP:
             ksplit = max(1, min(512 // tiles(h, k), B // 256, 64, (8 << 20) // (4 * h * k)))
             gemm(self.dZ[l], prevH, h, k, B, a_mn=True, lda=h, b_mn=True, ldb=k,
                  outF=gl[l][0], atomic=True, ksplit=ksplit)
-            if l > 0:
+            if l > 0 and not fused_bwd:
                 # dZ_{l-1} = (dZ_l W_l) * [H_{l-1} > 0];  db_{l-1} = colsum
                 gemm(self.dZ[l], wl[l][0], B, k, h, b_mn=True, ldb=k, outH=self.dZ[l - 1],
                      mask=self.Hs[l - 1], colsum=gl[l - 1][1])

@@ -147,19 +147,34 @@ def test_fused_mlp_forward_matches_per_layer(B, F):
     x, y = synth_tabular_batch(B, F, seed=4)
     x, y = x.to(DEV), y.to(DEV)
     res = {}
-    for fused in (False, True):
-        eng.fused = fused
+    for fused, fused_bwd in ((False, False), (True, False), (True, True)):
+        eng.fused, eng.fused_bwd = fused, fused_bwd
         ls = eng.forward_backward(x, y, grad_scale=1.0 / B).item()
         torch.cuda.synchronize()
-        res[fused] = (eng.Hs[0][: B * 256].float().clone(), eng.Hs[1][: B * 256].float().clone(),
-                      eng.pred[:B].clone(), eng.dy[:B].clone(), ls, eng.grads.clone())
-    (h1a, h2a, pa, da, la, ga), (h1b, h2b, pb, db, lb, gb) = res[False], res[True]
-    assert (h1a - h1b).abs().max().item() <= 1e-2 * max(1.0, h1a.abs().max().item())
-    assert (h2a - h2b).abs().max().item() <= 2e-2 * max(1.0, h2a.abs().max().item())
-    assert (pa - pb).abs().max().item() <= 1e-2 * max(1.0, pa.abs().max().item())
-    assert abs(la - lb) <= 1e-3 * abs(la) + 1e-6
-    assert ((ga - gb).norm() / ga.norm()).item() < 1e-2
-    assert torch.allclose(da, db, rtol=1e-2, atol=1e-6 * max(1.0, da.abs().max().item()))
+        res[fused, fused_bwd] = (eng.Hs[0][: B * 256].float().clone(), eng.Hs[1][: B * 256].float().clone(),
+                                 eng.pred[:B].clone(), eng.dy[:B].clone(), ls, eng.grads.clone(),
+                                 eng.dZ[0][: B * 256].float().clone(), eng.dZ[1][: B * 256].float().clone())
+    h1a, h2a, pa, da, la, ga, z1a, z2a = res[False, False]
+    for key in ((True, False), (True, True)):
+        h1b, h2b, pb, db, lb, gb, z1b, z2b = res[key]
+        assert (h1a - h1b).abs().max().item() <= 1e-2 * max(1.0, h1a.abs().max().item()), key
+        assert (h2a - h2b).abs().max().item() <= 2e-2 * max(1.0, h2a.abs().max().item()), key
+        assert (pa - pb).abs().max().item() <= 1e-2 * max(1.0, pa.abs().max().item()), key
+        assert abs(la - lb) <= 1e-3 * abs(la) + 1e-6, key
+        assert ((ga - gb).norm() / ga.norm()).item() < 1e-2, key
+        assert torch.allclose(da, db, rtol=1e-2, atol=1e-6 * max(1.0, da.abs().max().item())), key
+        # saved gate gradients of the backward (fused kernel vs head kernels + dX GEMM)
+        assert ((z2a - z2b).norm() / z2a.norm()).item() < 2e-2, key
+        assert ((z1a - z1b).norm() / z1a.norm()).item() < 2e-2, key
+    # per-block gradient agreement of the fully fused step (bias / head blocks included)
+    from wellflow.models.mlp import MlpLayout
+    ga_l, ga_hw, ga_hb = MlpLayout(F, (256, 256)).views(ga)
+    gb_l, gb_hw, gb_hb = MlpLayout(F, (256, 256)).views(res[True, True][5])
+    for (Wa, ba), (Wb, bb) in zip(ga_l, gb_l):
+        assert ((Wa - Wb).norm() / Wa.norm()).item() < 2e-2
+        assert ((ba - bb).norm() / ba.norm()).item() < 2e-2
+    assert ((ga_hw - gb_hw).norm() / ga_hw.norm()).item() < 1e-2
+    assert torch.allclose(ga_hb, gb_hb, rtol=1e-3, atol=1e-6)
 
 
 def test_mlp_bf16_input_matches_fp32_input():
