@@ -386,7 +386,8 @@ void head_fwd(const at::Tensor& Hm, int64_t ldh, int64_t B, int64_t Hd, const at
 // Fused MLP backward (mlp_fused.hip) for the F -> 256 -> 256 -> 1 shape: dZ2, dZ1 and the
 // bias / head gradients in one launch (the dW GEMMs stay separate).
 bool mlp2_backward(const at::Tensor& H1, const at::Tensor& H2, const at::Tensor& dy, const at::Tensor& w3,
-                   const at::Tensor& W2, const at::Tensor& dZ1, const at::Tensor& dZ2, const at::Tensor& db1,
+                   const at::Tensor& W2, const at::Tensor& X, int64_t Fp, const at::Tensor& dZ1,
+                   const at::Tensor& dZ2, c10::optional<at::Tensor> dW1, const at::Tensor& db1,
                    const at::Tensor& db2, const at::Tensor& dw3, const at::Tensor& db3, int64_t B) {
   constexpr int64_t H = 256;
   for (const at::Tensor* t : {&H1, &H2, &dZ1, &dZ2}) {
@@ -404,9 +405,13 @@ bool mlp2_backward(const at::Tensor& H1, const at::Tensor& H2, const at::Tensor&
   }
   check_t(db3, at::kFloat, "db3");
   check_extent(db3, 1, "db3");
+  check_t(X, at::kBFloat16, "X");
+  check_extent(X, B * Fp, "X");
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(X.data_ptr()) % 16 == 0, "mlp2_backward: X must be 16-B aligned");
   const c10::hip::OptionalHIPGuardMasqueradingAsCUDA guard(H1.device());
-  return wf::launch_mlp2_bwd(bfp(H1), bfp(H2), fp(dy), fp(w3), bfp(W2), bfp(dZ1), bfp(dZ2), fp(db1), fp(db2),
-                             fp(dw3), fp(db3), (int)B, cur_stream());
+  return wf::launch_mlp2_bwd(bfp(H1), bfp(H2), fp(dy), fp(w3), bfp(W2), bfp(X), (int)Fp, bfp(dZ1), bfp(dZ2),
+                             opt_ptr<float>(dW1, at::kFloat, "dW1", H * Fp), fp(db1), fp(db2), fp(dw3), fp(db3),
+                             (int)B, cur_stream());
 }
 
 // Fused MLP forward (mlp_fused.hip): both 256-wide hidden layers + head (+ MSE) in one launch.

@@ -68,12 +68,13 @@ void launch_lstm_pack_weights(const float* W, bf16_t* Wp, bf16_t* WhhT, LstmDims
 bool launch_mlp2_fwd(const bf16_t* X, int Fp, const bf16_t* W1, const float* b1, const bf16_t* W2, const float* b2,
                      const float* w3, const float* b3, const float* y, bf16_t* H1, bf16_t* H2, float* pred, float* dy,
                      float* loss_sum, float dy_scale, int B, hipStream_t s);
-// ---- fused MLP backward (mlp_fused.hip), everything but the dW1 / dW2 GEMMs: from H1, H2
-// ([B][256] bf16), dy and w3 / W2: dZ2, dZ1 ([B][256] bf16) and db1, db2, dw3, db3 (fp32,
-// accumulated with atomics).
+// ---- fused MLP backward (mlp_fused.hip), everything but the dW2 GEMM: from H1, H2
+// ([B][256] bf16), dy, w3 / W2 and X: dZ2 ([B][256] bf16, dW2's operand), db1, db2, dw3, db3
+// and — when dW1 != nullptr — dW1 ([256][Fp], Fp <= 32) (fp32, accumulated with atomics);
+// with dW1 == nullptr dZ1 ([B][256] bf16) is written for a separate dW1 GEMM instead.
 bool launch_mlp2_bwd(const bf16_t* H1, const bf16_t* H2, const float* dy, const float* w3, const bf16_t* W2,
-                     bf16_t* dZ1, bf16_t* dZ2, float* db1, float* db2, float* dw3, float* db3, int B,
-                     hipStream_t s);
+                     const bf16_t* X, int Fp, bf16_t* dZ1, bf16_t* dZ2, float* dW1, float* db1, float* db2,
+                     float* dw3, float* db3, int B, hipStream_t s);
 
 // ---- regression head (N = 1) and losses ----
 void launch_head_fwd(const bf16_t* Hm, long ldh, int B, int Hd, const float* w, const float* b0,

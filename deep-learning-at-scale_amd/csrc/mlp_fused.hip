@@ -19,6 +19,7 @@
 //    once each, as whole 16-byte row segments (they are the backward pass's saved
 //    activations); the head dot product is reduced across lanes (DPP) and waves (LDS).
 #include "common.h"
+#include "gemm_core.h"
 #include "kernels.h"
 
 namespace wf {
@@ -213,13 +214,21 @@ __global__ __launch_bounds__(256, 1) void mlp2_fwd_kernel(
 //    (t >> 5) + 8q), so its db2 / dw3 partials stay in registers across all chunks.
 //  * the H1 tile is staged in LDS for the ReLU mask and overwritten in place by dZ1 (each
 //    lane reads and writes the same 8 bytes), then copied out as 16-B row segments.
+//  * dW1 = dZ1^T X (K = the batch) is accumulated here too when dW1 != nullptr: the dZ1 tile
+//    [row][unit] and the X tile [row][feature] are both "MN-contiguous" images of operands
+//    whose reduction index is the row, so their MFMA fragments come out of LDS with
+//    ds_read_b64_tr_b16 (gemm_core.h) at per-lane addresses that follow this file's
+//    swizzles; the 64 x Fp slice of dW1 per wave stays in registers across all chunks
+//    (2 x 4 x NFT MFMAs per chunk), and dZ1 is then not written to HBM at all.
+template <int NFT>  // 16-feature tiles of dW1 (1: Fp <= 16, 2: Fp <= 32): dW1 registers = 16 x NFT
 __global__ __launch_bounds__(256, 1) void mlp2_bwd_kernel(
     const bf16_t* __restrict__ H1, const bf16_t* __restrict__ H2, const float* __restrict__ dy,
-    const float* __restrict__ w3, const bf16_t* __restrict__ W2, bf16_t* __restrict__ dZ1,
-    bf16_t* __restrict__ dZ2, float* __restrict__ db1, float* __restrict__ db2, float* __restrict__ dw3,
-    float* __restrict__ db3, int B) {
+    const float* __restrict__ w3, const bf16_t* __restrict__ W2, const bf16_t* __restrict__ X, int Fp,
+    bf16_t* __restrict__ dZ1, bf16_t* __restrict__ dZ2, float* __restrict__ dW1, float* __restrict__ db1,
+    float* __restrict__ db2, float* __restrict__ dw3, float* __restrict__ db3, int B) {
   __shared__ __attribute__((aligned(16))) char zs[MF_ROWS * MF_H * 2];  // dZ2 tile
   __shared__ __attribute__((aligned(16))) char hs[MF_ROWS * MF_H * 2];  // H1 tile -> dZ1 in place
+  __shared__ __attribute__((aligned(16))) char xs[MF_ROWS * 64];        // X tile (dW1)
   __shared__ float lred[4];
 
   const int lane = threadIdx.x & 63, l15 = lane & 15, g = lane >> 4;
@@ -251,6 +260,15 @@ __global__ __launch_bounds__(256, 1) void mlp2_bwd_kernel(
   for (int m = 0; m < 4; ++m)
 #pragma unroll
     for (int i = 0; i < 4; ++i) db1a[m][i] = 0.f;
+  const bool fuse_dw1 = dW1 != nullptr;
+  f32x4 dw1a[4][NFT];
+#pragma unroll
+  for (int m = 0; m < 4; ++m)
+#pragma unroll
+    for (int f = 0; f < NFT; ++f) dw1a[m][f] = f32x4{0.f, 0.f, 0.f, 0.f};
+  // per-lane tr-read coordinates (gemm_core.h MN fragment): tile row 8g + 4h + q (+ 32 kk),
+  // 4 consecutive columns from 4p
+  const int tq = (lane & 15) >> 2, tp = lane & 3;
 
   const int nchunks = (B + MF_ROWS - 1) / MF_ROWS;
   for (int ch = blockIdx.x; ch < nchunks; ch += gridDim.x) {
@@ -288,6 +306,12 @@ __global__ __launch_bounds__(256, 1) void mlp2_bwd_kernel(
       *reinterpret_cast<uint4*>(zs + tile_off(r, 8 * c)) = zv;
       *reinterpret_cast<uint4*>(hs + tile_off(r, 8 * c)) = h1v;
       if (gr < B) *reinterpret_cast<uint4*>(dZ2 + (size_t)gr * MF_H + 8 * c) = zv;
+    }
+    if (fuse_dw1) {  // X chunk -> LDS, zero-padded to 32 features (as in the forward)
+      const int r = threadIdx.x >> 2, xc = threadIdx.x & 3, gr = row0 + r;
+      uint4 v = make_uint4(0, 0, 0, 0);
+      if (gr < B && 8 * xc + 8 <= Fp) v = *reinterpret_cast<const uint4*>(X + (size_t)gr * Fp + 8 * xc);
+      *reinterpret_cast<uint4*>(xs + xtile_off(r, xc)) = v;
     }
     __syncthreads();
 
@@ -334,6 +358,39 @@ __global__ __launch_bounds__(256, 1) void mlp2_bwd_kernel(
         *p = make_uint2(ow[0], ow[1]);
       }
     __syncthreads();
+    if (fuse_dw1) {
+      // ---- dW1^T slice (64 units x Fp per wave) += dZ1^T X over this chunk's 64 rows
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        bf16x8 af[4], bfr[NFT];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const int r = 32 * kk + 8 * g + 4 * h + tq;
+#pragma unroll
+          for (int m = 0; m < 4; ++m) {
+            const bf16x4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+                (lds_bf16x4*)(hs + tile_off(r, u0 + 16 * m + 4 * tp)));
+#pragma unroll
+            for (int e = 0; e < 4; ++e) af[m][4 * h + e] = v[e];
+          }
+#pragma unroll
+          for (int f = 0; f < NFT; ++f) {
+            const int f0 = 16 * f + 4 * tp;
+            const bf16x4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+                (lds_bf16x4*)(xs + xtile_off(r, f0 >> 3) + ((f0 & 7) << 1)));
+#pragma unroll
+            for (int e = 0; e < 4; ++e) bfr[f][4 * h + e] = v[e];
+          }
+        }
+#pragma unroll
+        for (int m = 0; m < 4; ++m)
+#pragma unroll
+          for (int f = 0; f < NFT; ++f)
+            dw1a[m][f] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[m], bfr[f], dw1a[m][f], 0, 0, 0);
+      }
+      __syncthreads();  // zs / hs / xs are rewritten by the next chunk
+      continue;        // dZ1 itself is not needed outside this kernel
+    }
     // ---- dZ1 tile -> HBM
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
@@ -357,6 +414,18 @@ __global__ __launch_bounds__(256, 1) void mlp2_bwd_kernel(
       v += __shfl_xor(v, 8, 64);
       if (l15 == 0 && v != 0.f) atomicAdd(db1 + u0 + 16 * m + 4 * g + i, v);
     }
+  // dW1 (C layout: lane holds units u0 + 16m + 4g + i, feature l15 + 16f)
+  if (fuse_dw1) {
+#pragma unroll
+    for (int m = 0; m < 4; ++m)
+#pragma unroll
+      for (int f = 0; f < NFT; ++f) {
+        const int ft = l15 + 16 * f;
+        if (ft < Fp)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) atomicAdd(dW1 + (size_t)(u0 + 16 * m + 4 * g + i) * Fp + ft, dw1a[m][f][i]);
+      }
+  }
   // db2 / dw3: the 8 threads of one chunk c (rq = 0..7) -> LDS [8][256] x 2, then one per unit
   float* sd = reinterpret_cast<float*>(zs);
 #pragma unroll
@@ -381,17 +450,21 @@ __global__ __launch_bounds__(256, 1) void mlp2_bwd_kernel(
 }
 
 bool launch_mlp2_bwd(const bf16_t* H1, const bf16_t* H2, const float* dy, const float* w3, const bf16_t* W2,
-                     bf16_t* dZ1, bf16_t* dZ2, float* db1, float* db2, float* dw3, float* db3, int B,
-                     hipStream_t s) {
-  if (B <= 0) return false;
+                     const bf16_t* X, int Fp, bf16_t* dZ1, bf16_t* dZ2, float* dW1, float* db1, float* db2,
+                     float* dw3, float* db3, int B, hipStream_t s) {
+  if (B <= 0 || (dW1 != nullptr && (X == nullptr || Fp > 32 || Fp % 8 != 0))) return false;
   const int nchunks = (B + MF_ROWS - 1) / MF_ROWS;
   int dev = 0, cus = 0;
   if (hipGetDevice(&dev) != hipSuccess ||
       hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
     cus = 256;
   const int grid = nchunks < cus ? nchunks : cus;
-  hipLaunchKernelGGL(mlp2_bwd_kernel, dim3(grid), dim3(256), 0, s, H1, H2, dy, w3, W2, dZ1, dZ2, db1, db2, dw3,
-                     db3, B);
+  if (Fp <= 16)
+    hipLaunchKernelGGL(mlp2_bwd_kernel<1>, dim3(grid), dim3(256), 0, s, H1, H2, dy, w3, W2, X, Fp, dZ1, dZ2, dW1,
+                       db1, db2, dw3, db3, B);
+  else
+    hipLaunchKernelGGL(mlp2_bwd_kernel<2>, dim3(grid), dim3(256), 0, s, H1, H2, dy, w3, W2, X, Fp, dZ1, dZ2, dW1,
+                       db1, db2, dw3, db3, B);
   return true;
 }
 

@@ -163,9 +163,11 @@ def test_fused_mlp_forward_matches_per_layer(B, F):
         assert abs(la - lb) <= 1e-3 * abs(la) + 1e-6, key
         assert ((ga - gb).norm() / ga.norm()).item() < 1e-2, key
         assert torch.allclose(da, db, rtol=1e-2, atol=1e-6 * max(1.0, da.abs().max().item())), key
-        # saved gate gradients of the backward (fused kernel vs head kernels + dX GEMM)
+        # saved gradients of the backward (fused kernel vs head kernels + dX GEMM); the fused
+        # backward keeps dZ1 on chip (dW1 is accumulated in the kernel), so only dZ2 is compared
         assert ((z2a - z2b).norm() / z2a.norm()).item() < 2e-2, key
-        assert ((z1a - z1b).norm() / z1a.norm()).item() < 2e-2, key
+        if not key[1]:
+            assert ((z1a - z1b).norm() / z1a.norm()).item() < 2e-2, key
     # per-block gradient agreement of the fully fused step (bias / head blocks included)
     from wellflow.models.mlp import MlpLayout
     ga_l, ga_hw, ga_hb = MlpLayout(F, (256, 256)).views(ga)
