@@ -61,7 +61,7 @@ void launch_lstm_bwd_step(int t, const bf16_t* WhhT, const float* Cst, const bf1
 void launch_lstm_pack_weights(const float* W, bf16_t* Wp, bf16_t* WhhT, LstmDims d,
                               hipStream_t s);
 
-// ---- fused MLP forward (mlp_fused.hip): F (<= 32, padded to Fp % 8 == 0) -> 256 -> 256 -> 1,
+// ---- fused MLP forward (mlp_fused.hip): F (<= 64, padded to Fp % 8 == 0) -> 256 -> 256 -> 1,
 // ReLU, bias, linear head, optional MSE (y, dy = dy_scale * (pred - y), loss_sum += (pred - y)^2).
 // Writes H1, H2 ([B][256] bf16: the backward's saved activations) and pred. Returns false
 // (nothing launched) for shapes it does not cover.

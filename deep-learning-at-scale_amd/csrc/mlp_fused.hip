@@ -35,17 +35,20 @@ __device__ __forceinline__ int tile_off(int row, int unit) {
   const int c = unit >> 3;
   return row * (MF_H * 2) + ((c ^ (row & 15)) << 4) + ((unit & 7) << 1);
 }
-// [64 rows][32 features] bf16 input tile (4 chunks per row, 64-B rows: rows r, r+4, r+8, r+12
-// share a bank group, so the chunk is swizzled by (row >> 2) & 3)
-__device__ __forceinline__ int xtile_off(int row, int chunk) { return row * 64 + ((chunk ^ ((row >> 2) & 3)) << 4); }
+// [64 rows][64 features] bf16 input tile (8 chunks per row, 128-B rows: rows r and r + 2
+// share banks, so the chunk is swizzled by (row >> 1) & 7 — 16-row fragment reads of one
+// chunk hit 16 distinct bank groups)
+constexpr int MF_XROW = 128;
+__device__ __forceinline__ int xtile_off(int row, int chunk) { return row * MF_XROW + ((chunk ^ ((row >> 1) & 7)) << 4); }
 }  // namespace
 
+template <int KT1>  // layer-1 K steps of 32 features: 1 (Fp <= 32) or 2 (Fp <= 64)
 __global__ __launch_bounds__(256, 1) void mlp2_fwd_kernel(
     const bf16_t* __restrict__ X, int Fp, const bf16_t* __restrict__ W1, const float* __restrict__ b1,
     const bf16_t* __restrict__ W2, const float* __restrict__ b2, const float* __restrict__ w3,
     const float* __restrict__ b3, const float* __restrict__ y, bf16_t* __restrict__ H1, bf16_t* __restrict__ H2,
     float* __restrict__ pred, float* __restrict__ dy, float* __restrict__ loss_sum, float dy_scale, int B) {
-  __shared__ __attribute__((aligned(16))) char xs[MF_ROWS * 64];
+  __shared__ __attribute__((aligned(16))) char xs[MF_ROWS * MF_XROW];
   __shared__ __attribute__((aligned(16))) char h1s[MF_ROWS * MF_H * 2];
   __shared__ __attribute__((aligned(16))) char h2s[MF_ROWS * MF_H * 2];
   __shared__ float red[4][MF_ROWS];
@@ -56,15 +59,19 @@ __global__ __launch_bounds__(256, 1) void mlp2_fwd_kernel(
   const int u0 = wid * 64;  // first unit of this wave
 
   // ---- stationary weights (A operand: lane = unit l15 of M-tile m, k 8g..8g+7)
-  bf16x8 w1f[4], w2f[4][8];
+  bf16x8 w1f[KT1][4], w2f[4][8];
   float bias1[4][4], bias2[4][4], w3v[4][4];
 #pragma unroll
   for (int m = 0; m < 4; ++m) {
     const int u = u0 + 16 * m + l15;
-    if (8 * g + 8 <= Fp)
-      w1f[m] = *reinterpret_cast<const bf16x8*>(W1 + (size_t)u * Fp + 8 * g);
-    else
-      w1f[m] = bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+    for (int k1 = 0; k1 < KT1; ++k1) {
+      const int f0 = 32 * k1 + 8 * g;
+      if (f0 + 8 <= Fp)
+        w1f[k1][m] = *reinterpret_cast<const bf16x8*>(W1 + (size_t)u * Fp + f0);
+      else
+        w1f[k1][m] = bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
+    }
 #pragma unroll
     for (int kt = 0; kt < 8; ++kt) w2f[m][kt] = *reinterpret_cast<const bf16x8*>(W2 + (size_t)u * MF_H + 32 * kt + 8 * g);
 #pragma unroll
@@ -81,24 +88,31 @@ __global__ __launch_bounds__(256, 1) void mlp2_fwd_kernel(
   const int nchunks = (B + MF_ROWS - 1) / MF_ROWS;
   for (int ch = blockIdx.x; ch < nchunks; ch += gridDim.x) {
     const int row0 = ch * MF_ROWS;
-    // ---- X chunk -> LDS, zero-padded to 32 features (thread: row t >> 2, 16-B chunk t & 3)
-    {
-      const int r = threadIdx.x >> 2, c = threadIdx.x & 3, gr = row0 + r;
+    // ---- X chunk -> LDS, zero-padded to 32 * KT1 features (thread: row t >> 2, chunk t & 3 (+4))
+#pragma unroll
+    for (int k1 = 0; k1 < KT1; ++k1) {
+      const int r = threadIdx.x >> 2, c = (threadIdx.x & 3) + 4 * k1, gr = row0 + r;
       uint4 v = make_uint4(0, 0, 0, 0);
       if (gr < B && 8 * c + 8 <= Fp) v = *reinterpret_cast<const uint4*>(X + (size_t)gr * Fp + 8 * c);
       *reinterpret_cast<uint4*>(xs + xtile_off(r, c)) = v;
     }
     __syncthreads();
 
-    // ---- layer 1: Z1^T (64 units x 64 rows per wave) = W1 x X^T, K = 32
+    // ---- layer 1: Z1^T (64 units x 64 rows per wave) = W1 x X^T, K = 32 * KT1
     f32x4 acc[4][4];
 #pragma unroll
-    for (int n = 0; n < 4; ++n) {
-      const bf16x8 xb = *reinterpret_cast<const bf16x8*>(xs + xtile_off(16 * n + l15, g));
+    for (int m = 0; m < 4; ++m)
 #pragma unroll
-      for (int m = 0; m < 4; ++m)
-        acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w1f[m], xb, f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
-    }
+      for (int n = 0; n < 4; ++n) acc[m][n] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int k1 = 0; k1 < KT1; ++k1)
+#pragma unroll
+      for (int n = 0; n < 4; ++n) {
+        const bf16x8 xb = *reinterpret_cast<const bf16x8*>(xs + xtile_off(16 * n + l15, 4 * k1 + g));
+#pragma unroll
+        for (int m = 0; m < 4; ++m)
+          acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w1f[k1][m], xb, acc[m][n], 0, 0, 0);
+      }
     // epilogue 1: + b1, relu, 4 units -> 8 B into the H1 tile
 #pragma unroll
     for (int m = 0; m < 4; ++m)
@@ -228,7 +242,7 @@ __global__ __launch_bounds__(256, 1) void mlp2_bwd_kernel(
     float* __restrict__ db2, float* __restrict__ dw3, float* __restrict__ db3, int B) {
   __shared__ __attribute__((aligned(16))) char zs[MF_ROWS * MF_H * 2];  // dZ2 tile
   __shared__ __attribute__((aligned(16))) char hs[MF_ROWS * MF_H * 2];  // H1 tile -> dZ1 in place
-  __shared__ __attribute__((aligned(16))) char xs[MF_ROWS * 64];        // X tile (dW1)
+  __shared__ __attribute__((aligned(16))) char xs[MF_ROWS * MF_XROW];   // X tile (dW1)
   __shared__ float lred[4];
 
   const int lane = threadIdx.x & 63, l15 = lane & 15, g = lane >> 4;
@@ -471,15 +485,19 @@ bool launch_mlp2_bwd(const bf16_t* H1, const bf16_t* H2, const float* dy, const 
 bool launch_mlp2_fwd(const bf16_t* X, int Fp, const bf16_t* W1, const float* b1, const bf16_t* W2, const float* b2,
                      const float* w3, const float* b3, const float* y, bf16_t* H1, bf16_t* H2, float* pred, float* dy,
                      float* loss_sum, float dy_scale, int B, hipStream_t s) {
-  if (Fp > 32 || Fp % 8 != 0 || B <= 0) return false;
+  if (Fp > 64 || Fp % 8 != 0 || B <= 0) return false;
   const int nchunks = (B + MF_ROWS - 1) / MF_ROWS;
   int dev = 0, cus = 0;
   if (hipGetDevice(&dev) != hipSuccess ||
       hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
     cus = 256;
   const int grid = nchunks < cus ? nchunks : cus;
-  hipLaunchKernelGGL(mlp2_fwd_kernel, dim3(grid), dim3(256), 0, s, X, Fp, W1, b1, W2, b2, w3, b3, y, H1, H2, pred,
-                     dy, loss_sum, dy_scale, B);
+  if (Fp <= 32)
+    hipLaunchKernelGGL(mlp2_fwd_kernel<1>, dim3(grid), dim3(256), 0, s, X, Fp, W1, b1, W2, b2, w3, b3, y, H1, H2,
+                       pred, dy, loss_sum, dy_scale, B);
+  else
+    hipLaunchKernelGGL(mlp2_fwd_kernel<2>, dim3(grid), dim3(256), 0, s, X, Fp, W1, b1, W2, b2, w3, b3, y, H1, H2,
+                       pred, dy, loss_sum, dy_scale, B);
   return true;
 }
 

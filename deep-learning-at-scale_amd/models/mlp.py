@@ -178,7 +178,7 @@ class NativeMLP:
     def _fused_forward(self, B: int, y=None, dy=None, loss_sum=None, dy_scale: float = 0.0) -> bool:
         """Both hidden layers + head (+ MSE) in ONE weight-stationary launch
         (csrc/mlp_fused.hip) for the BASELINE shape F -> 256 -> 256 -> 1; False = not covered."""
-        if not self.fused or self.hidden != (256, 256) or self.Fp > 32:
+        if not self.fused or self.hidden != (256, 256) or self.Fp > 64:
             return False
         wl, _, _ = self.lay.views(self.shadow)
         pl, hw, hb = self.lay.views(self.params)
@@ -222,11 +222,14 @@ class NativeMLP:
                 C.head_fwd(self.Hs[-1], H, B, H, hw, hb, None, self.pred, None, None, 0.0)
             C.loss(1, self.pred, y, B, 1, self.clip, float(grad_scale), self.loss_sum, None,
                    self.dy, None)
-        # fused backward (csrc/mlp_fused.hip) for the BASELINE shape: head + dZ2 + dZ1 + dW1 +
-        # every bias gradient in one launch; only the dW2 GEMM remains
-        fused_bwd = (self.fused_bwd and self.hidden == (256, 256) and self.Fp <= 32 and
+        # fused backward (csrc/mlp_fused.hip) for the BASELINE shape: head + dZ2 + dZ1 + every
+        # bias gradient in one launch, + dW1 on chip when Fp <= 32; then only dW2 (and, for
+        # wider inputs, dW1) run as split-K GEMMs
+        fused_dw1 = self.Fp <= 32
+        fused_bwd = (self.fused_bwd and self.hidden == (256, 256) and
                      C.mlp2_backward(self.Hs[0], self.Hs[1], self.dy, hw, wl[1][0], self.X, self.Fp,
-                                     self.dZ[0], self.dZ[1], gl[0][0], gl[0][1], gl[1][1], ghw, ghb, B))
+                                     self.dZ[0], self.dZ[1], gl[0][0] if fused_dw1 else None, gl[0][1],
+                                     gl[1][1], ghw, ghb, B))
         if not fused_bwd:
             C.head_bwd_w(self.Hs[-1], H, B, H, self.dy, ghw, ghb)
             C.head_bwd_x(self.Hs[-1], H, B, H, self.dy, hw, True, self.dZ[-1], H, gl[-1][1])
@@ -234,7 +237,7 @@ class NativeMLP:
         # grid has ~512 workgroups, each reducing >= 256 rows
         tiles = lambda h, k: ((h + 127) // 128) * ((k + 127) // 128)  # noqa: E731
         for l in range(L - 1, -1, -1):
-            if l == 0 and fused_bwd:
+            if l == 0 and fused_bwd and fused_dw1:
                 break  # dW1 accumulated inside the fused backward
             h, k = self.lay.dims[l]
             prevH = self.Hs[l - 1] if l > 0 else self.X

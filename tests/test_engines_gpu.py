@@ -133,7 +133,7 @@ def test_lstm_submission_script_from_csv_on_gpu(tmp_path):
     assert (tmp_path / "models" / "lstm.mdl").exists()
 
 
-@pytest.mark.parametrize("B,F", [(65536, 16), (1000, 9), (64, 32)])
+@pytest.mark.parametrize("B,F", [(65536, 16), (1000, 9), (64, 32), (3000, 40), (512, 64)])
 def test_fused_mlp_forward_matches_per_layer(B, F):
     """The one-launch weight-stationary MLP forward (csrc/mlp_fused.hip) against the
     per-layer GEMM + head path on the same weights: saved activations, predictions, loss and
