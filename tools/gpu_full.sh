@@ -13,6 +13,12 @@ timeout -k 10 300 python bench.py || exit $?
 timeout -k 10 300 python bench.py --model mlp || exit $?
 timeout -k 10 300 python bench.py --model mlp_online || exit $?
 if [ "$1" = "prof" ]; then
+  # rocprofv3 7.2 segfaults at exit after tracing a cooperative dispatch: plain launch
+  export WELLFLOW_COOP=0
   timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_full -o run -- python3 bench.py --steps 20 --warmup 5 > gpurun_out/prof_full.log 2>&1 || exit $?
   find gpurun_out/prof_full -name "*kernel_stats.csv"
+fi
+if [ "$1" = "prof" ]; then
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_mlp -o run -- python3 bench.py --model mlp --steps 20 --warmup 5 > gpurun_out/prof_mlp.log 2>&1 || exit $?
+  find gpurun_out/prof_mlp -name "*kernel_stats.csv"
 fi
