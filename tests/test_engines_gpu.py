@@ -147,16 +147,32 @@ def test_fused_mlp_forward_matches_per_layer(B, F):
     x, y = synth_tabular_batch(B, F, seed=4)
     x, y = x.to(DEV), y.to(DEV)
     res = {}
-    for fused, fused_bwd in ((False, False), (True, False), (True, True)):
-        eng.fused, eng.fused_bwd = fused, fused_bwd
+    masks = None
+    # (fused forward, fused backward, H2 as a ReLU bitmask + head gradients in the forward)
+    for fused, fused_bwd, mask in ((False, False, False), (True, False, False), (True, True, False),
+                                   (True, True, True)):
+        eng.fused, eng.fused_bwd, eng.mask_h2 = fused, fused_bwd, mask
+        if mask:
+            eng.Hs[1].zero_()  # not written in mask mode
         ls = eng.forward_backward(x, y, grad_scale=1.0 / B).item()
         torch.cuda.synchronize()
-        res[fused, fused_bwd] = (eng.Hs[0][: B * 256].float().clone(), eng.Hs[1][: B * 256].float().clone(),
-                                 eng.pred[:B].clone(), eng.dy[:B].clone(), ls, eng.grads.clone(),
-                                 eng.dZ[0][: B * 256].float().clone(), eng.dZ[1][: B * 256].float().clone())
-    h1a, h2a, pa, da, la, ga, z1a, z2a = res[False, False]
-    for key in ((True, False), (True, True)):
+        res[fused, fused_bwd, mask] = (eng.Hs[0][: B * 256].float().clone(), eng.Hs[1][: B * 256].float().clone(),
+                                       eng.pred[:B].clone(), eng.dy[:B].clone(), ls, eng.grads.clone(),
+                                       eng.dZ[0][: B * 256].float().clone(), eng.dZ[1][: B * 256].float().clone())
+        if mask:
+            masks = eng.M2[: B * 8].clone()
+    # the bitmask is exactly H2 > 0 of the same fused forward
+    h2f = res[True, True, False][1].view(B, 8, 32)
+    bits = torch.tensor([1 << i for i in range(31)] + [-(1 << 31)], dtype=torch.int64, device=DEV)
+    want = ((h2f > 0).long() * bits).sum(-1)
+    want = torch.where(want >= (1 << 31), want - (1 << 32), want).to(torch.int32).view(-1)
+    assert torch.equal(masks, want)
+    assert res[True, True, True][1].abs().max().item() == 0.0  # H2 never left the CU
+    h1a, h2a, pa, da, la, ga, z1a, z2a = res[False, False, False]
+    for key in ((True, False, False), (True, True, False), (True, True, True)):
         h1b, h2b, pb, db, lb, gb, z1b, z2b = res[key]
+        if key[2]:
+            h2b = res[True, True, False][1]
         assert (h1a - h1b).abs().max().item() <= 1e-2 * max(1.0, h1a.abs().max().item()), key
         assert (h2a - h2b).abs().max().item() <= 2e-2 * max(1.0, h2a.abs().max().item()), key
         assert (pa - pb).abs().max().item() <= 1e-2 * max(1.0, pa.abs().max().item()), key
@@ -171,12 +187,17 @@ def test_fused_mlp_forward_matches_per_layer(B, F):
     # per-block gradient agreement of the fully fused step (bias / head blocks included)
     from wellflow.models.mlp import MlpLayout
     ga_l, ga_hw, ga_hb = MlpLayout(F, (256, 256)).views(ga)
-    gb_l, gb_hw, gb_hb = MlpLayout(F, (256, 256)).views(res[True, True][5])
-    for (Wa, ba), (Wb, bb) in zip(ga_l, gb_l):
-        assert ((Wa - Wb).norm() / Wa.norm()).item() < 2e-2
-        assert ((ba - bb).norm() / ba.norm()).item() < 2e-2
-    assert ((ga_hw - gb_hw).norm() / ga_hw.norm()).item() < 1e-2
-    assert torch.allclose(ga_hb, gb_hb, rtol=1e-3, atol=1e-6)
+    for key in ((True, True, False), (True, True, True)):
+        gb_l, gb_hw, gb_hb = MlpLayout(F, (256, 256)).views(res[key][5])
+        for (Wa, ba), (Wb, bb) in zip(ga_l, gb_l):
+            assert ((Wa - Wb).norm() / Wa.norm()).item() < 2e-2, key
+            assert ((ba - bb).norm() / ba.norm()).item() < 2e-2, key
+        assert ((ga_hw - gb_hw).norm() / ga_hw.norm()).item() < 1e-2, key
+        assert torch.allclose(ga_hb, gb_hb, rtol=1e-3, atol=1e-6), key
+    # mask mode against the H2-reading fused backward: same forward, same gradients up to
+    # fp32 summation order
+    gm, gh = res[True, True, True][5], res[True, True, False][5]
+    assert ((gm - gh).norm() / gh.norm()).item() < 1e-4
 
 
 def test_mlp_bf16_input_matches_fp32_input():
