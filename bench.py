@@ -176,7 +176,8 @@ def bench_mlp(args, ctx, online: bool):
     eng.params.copy_(init_mlp_flat(F, hid, seed=0).to(ctx.device))
     ctx.broadcast_(eng.params)
     eng.sync_weights()
-    opt = FlatAdam(eng.params, eng.grads, lr=args.lr)
+    # Adam writes the bf16 compute copy and clears the gradient bucket in its own launch
+    opt = FlatAdam(eng.params, eng.grads, lr=args.lr, shadow=eng.shadow, zero_grads=True)
     gscale = 1.0 / (B * ctx.world_size)
 
     if online:
@@ -197,16 +198,16 @@ def bench_mlp(args, ctx, online: bool):
             with torch.cuda.stream(s):
                 for _ in range(2):
                     eng.forward_backward(streamer.slots[0][0], streamer.slots[0][1], gscale)
+                eng.grads.zero_()  # from here on Adam clears the bucket after each update
             torch.cuda.current_stream(ctx.device).wait_stream(s)
             for k in range(depth):
                 g = torch.cuda.CUDAGraph()
                 with torch.cuda.graph(g):
-                    eng.forward_backward(streamer.slots[k][0], streamer.slots[k][1], gscale)
+                    eng.forward_backward(streamer.slots[k][0], streamer.slots[k][1], gscale, zero_grads=False)
                 graphs[k] = g
             gu = torch.cuda.CUDAGraph()
             with torch.cuda.graph(gu):
-                opt.step()
-                eng.sync_weights()
+                opt.step()  # + bf16 shadow + grad clear
             graphs["update"] = gu
 
         def step():
@@ -216,20 +217,18 @@ def bench_mlp(args, ctx, online: bool):
                 ctx.all_reduce_sum_(eng.grads)
                 graphs["update"].replay()
             else:
-                eng.forward_backward(xb, yb, gscale)
+                eng.forward_backward(xb, yb, gscale, zero_grads=False)
                 ctx.all_reduce_sum_(eng.grads)
                 opt.step()
-                eng.sync_weights()
     else:
         x, y = synth_tabular_batch(B, F, seed=ctx.rank)
         x, y = x.to(ctx.device), y.to(ctx.device)
 
         def compute():
-            eng.forward_backward(x, y, gscale)
+            eng.forward_backward(x, y, gscale, zero_grads=False)
 
         def update():
-            opt.step()
-            eng.sync_weights()
+            opt.step()  # + bf16 shadow + grad clear
 
         step = _graph_step(ctx, eng, compute, update, args.no_graph)
 

@@ -162,6 +162,32 @@ def test_adam_and_sgd_match_reference():
     assert torch.allclose(p2, pc, atol=1e-6)
 
 
+@pytest.mark.parametrize("n", [1001, 70401, 3_000_001])
+def test_fused_device_adam(n):
+    """Graph-capturable Adam (device step counter advanced by the last workgroup, bf16 shadow
+    written and the gradient bucket cleared in the same launch) vs torch.optim.Adam fp32."""
+    from wellflow.optim.flat import FlatAdam
+
+    torch.manual_seed(5)
+    p = torch.randn(n, device=DEV)
+    g = torch.zeros(n, device=DEV)
+    shadow = torch.empty(n, dtype=torch.bfloat16, device=DEV)
+    opt = FlatAdam(p, g, lr=1e-3, shadow=shadow, zero_grads=True)
+    pr = p.clone().requires_grad_(True)
+    ref = torch.optim.Adam([pr], lr=1e-3)
+    for step in range(1, 6):
+        gs = torch.randn(n, device=DEV)
+        g.add_(gs)  # the bucket was cleared by the previous update
+        opt.step()
+        pr.grad = gs.clone()
+        ref.step()
+        torch.cuda.synchronize()
+        assert opt.step_dev[0].item() == float(step) and opt.step_dev[1].item() == 0.0
+        assert g.abs().max().item() == 0.0
+    assert torch.allclose(p, pr.detach(), atol=1e-6, rtol=1e-5)
+    assert torch.equal(shadow, p.to(torch.bfloat16))
+
+
 def test_losses():
     from wellflow.ops.native import lib
 
