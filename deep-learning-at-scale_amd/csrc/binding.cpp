@@ -385,10 +385,20 @@ void head_fwd(const at::Tensor& Hm, int64_t ldh, int64_t B, int64_t Hd, const at
 
 // Fused MLP backward (mlp_fused.hip) for the F -> 256 -> 256 -> 1 shape: dZ2, dZ1 and the
 // bias / head gradients in one launch (the dW GEMMs stay separate).
+// ReLU bitmask of the MLP's second hidden layer: int32 [B][8] (256 bits per row), 16-B aligned
+static unsigned* mask_ptr(const c10::optional<at::Tensor>& M2, int64_t B) {
+  if (!M2.has_value()) return nullptr;
+  check_t(*M2, at::kInt, "M2");
+  check_extent(*M2, B * 8, "M2");
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(M2->data_ptr()) % 16 == 0, "M2 must be 16-B aligned");
+  return reinterpret_cast<unsigned*>(M2->data_ptr<int>());
+}
+
 bool mlp2_backward(const at::Tensor& H1, const at::Tensor& H2, const at::Tensor& dy, const at::Tensor& w3,
                    const at::Tensor& W2, const at::Tensor& X, int64_t Fp, const at::Tensor& dZ1,
                    const at::Tensor& dZ2, c10::optional<at::Tensor> dW1, const at::Tensor& db1,
-                   const at::Tensor& db2, const at::Tensor& dw3, const at::Tensor& db3, int64_t B) {
+                   const at::Tensor& db2, const at::Tensor& dw3, const at::Tensor& db3, int64_t B,
+                   c10::optional<at::Tensor> M2) {
   constexpr int64_t H = 256;
   for (const at::Tensor* t : {&H1, &H2, &dZ1, &dZ2}) {
     check_t(*t, at::kBFloat16, "H/dZ");
@@ -409,7 +419,7 @@ bool mlp2_backward(const at::Tensor& H1, const at::Tensor& H2, const at::Tensor&
   check_extent(X, B * Fp, "X");
   TORCH_CHECK(reinterpret_cast<uintptr_t>(X.data_ptr()) % 16 == 0, "mlp2_backward: X must be 16-B aligned");
   const c10::hip::OptionalHIPGuardMasqueradingAsCUDA guard(H1.device());
-  return wf::launch_mlp2_bwd(bfp(H1), bfp(H2), fp(dy), fp(w3), bfp(W2), bfp(X), (int)Fp, bfp(dZ1), bfp(dZ2),
+  return wf::launch_mlp2_bwd(bfp(H1), bfp(H2), mask_ptr(M2, B), fp(dy), fp(w3), bfp(W2), bfp(X), (int)Fp, bfp(dZ1), bfp(dZ2),
                              opt_ptr<float>(dW1, at::kFloat, "dW1", H * Fp), fp(db1), fp(db2), fp(dw3), fp(db3),
                              (int)B, cur_stream());
 }
@@ -421,7 +431,8 @@ bool mlp2_forward(const at::Tensor& X, int64_t Fp, const at::Tensor& W1, const a
                   const at::Tensor& W2, const at::Tensor& b2, const at::Tensor& w3, const at::Tensor& b3,
                   c10::optional<at::Tensor> y, const at::Tensor& H1, const at::Tensor& H2,
                   const at::Tensor& pred, c10::optional<at::Tensor> dy, c10::optional<at::Tensor> loss_sum,
-                  double dy_scale, int64_t B) {
+                  double dy_scale, int64_t B, c10::optional<at::Tensor> M2,
+                  c10::optional<at::Tensor> dw3, c10::optional<at::Tensor> db3) {
   constexpr int64_t H = 256;
   check_t(X, at::kBFloat16, "X");
   check_extent(X, B * Fp, "X");
@@ -444,7 +455,9 @@ bool mlp2_forward(const at::Tensor& X, int64_t Fp, const at::Tensor& W1, const a
     TORCH_CHECK(reinterpret_cast<uintptr_t>(t->data_ptr()) % 16 == 0, "mlp2_forward: bf16 operands must be 16-B aligned");
   const c10::hip::OptionalHIPGuardMasqueradingAsCUDA guard(X.device());
   return wf::launch_mlp2_fwd(bfp(X), (int)Fp, bfp(W1), fp(b1), bfp(W2), fp(b2), fp(w3), fp(b3),
-                             opt_ptr<float>(y, at::kFloat, "y", B), bfp(H1), bfp(H2), fp(pred),
+                             opt_ptr<float>(y, at::kFloat, "y", B), bfp(H1), bfp(H2), mask_ptr(M2, B),
+                             opt_ptr<float>(dw3, at::kFloat, "dw3", H), opt_ptr<float>(db3, at::kFloat, "db3", 1),
+                             fp(pred),
                              opt_ptr<float>(dy, at::kFloat, "dy", B),
                              opt_ptr<float>(loss_sum, at::kFloat, "loss_sum", 1), (float)dy_scale, (int)B,
                              cur_stream());
@@ -511,17 +524,21 @@ void adam(const at::Tensor& p, const at::Tensor& g, const at::Tensor& m, const a
 
 void adam_dev(const at::Tensor& p, const at::Tensor& g, const at::Tensor& m, const at::Tensor& v,
               const at::Tensor& step, double lr, double b1, double b2, double eps, double wd,
-              double gscale) {
+              double gscale, c10::optional<at::Tensor> shadow, bool zero_g) {
   check_t(p, at::kFloat, "p");
   check_t(g, at::kFloat, "g");
   check_t(m, at::kFloat, "m");
   check_t(v, at::kFloat, "v");
   check_t(step, at::kFloat, "step");
+  check_extent(step, 2, "step");  // [0] = t, [1] = completion ticket
   const int64_t n = p.numel();
   TORCH_CHECK(g.numel() == n && m.numel() == n && v.numel() == n, "adam: size mismatch");
+  for (const at::Tensor* t : {&p, &g, &m, &v})
+    TORCH_CHECK(reinterpret_cast<uintptr_t>(t->data_ptr()) % 16 == 0, "adam: buffers must be 16-B aligned");
   const c10::hip::OptionalHIPGuardMasqueradingAsCUDA guard(p.device());
   wf::launch_adam_dev(fp(p), fp(g), fp(m), fp(v), n, fp(step), (float)lr, (float)b1, (float)b2,
-                      (float)eps, (float)wd, (float)gscale, cur_stream());
+                      (float)eps, (float)wd, (float)gscale, opt_ptr<bf16_t>(shadow, at::kBFloat16, "shadow", n),
+                      zero_g ? 1 : 0, cur_stream());
 }
 
 void sgd(const at::Tensor& p, const at::Tensor& g, const at::Tensor& vel, double lr,

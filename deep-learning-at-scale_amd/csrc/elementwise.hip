@@ -291,18 +291,18 @@ void launch_adam(float* p, const float* g, float* m, float* v, long n, float lr,
                      eps, wd, bc1, bc2, gscale);
 }
 
-// Graph-capturable Adam: the step counter lives on the device (incremented by a 1-thread
-// kernel in the same stream), so a captured hipGraph replays with correct bias corrections.
-__global__ void inc_counter_kernel(float* step) {
-  if (blockIdx.x == 0 && threadIdx.x == 0) step[0] += 1.f;
-}
-
-__global__ __launch_bounds__(256) void adam_dev_kernel(float* __restrict__ p, const float* __restrict__ g,
+// Graph-capturable Adam: the step counter lives on the device, so a captured hipGraph
+// replays with correct bias corrections. Every workgroup reads t = step[0] + 1 at entry; the
+// LAST workgroup to finish (ticket in step[1]) stores it back, so no second launch is needed
+// and no workgroup can see the new value early. Optional fusions: the bf16 shadow copy of
+// the updated master weights (shadow != nullptr; replaces a cast launch) and zeroing the
+// gradient bucket after it is consumed (zero_g; replaces the next step's fill launch).
+__global__ __launch_bounds__(256) void adam_dev_kernel(float* __restrict__ p, float* __restrict__ g,
                                                        float* __restrict__ m, float* __restrict__ v,
-                                                       long n, const float* __restrict__ step, float lr,
+                                                       long n, float* __restrict__ step, float lr,
                                                        float b1, float b2, float eps, float wd,
-                                                       float gscale) {
-  const float t = step[0];
+                                                       float gscale, bf16_t* __restrict__ shadow, int zero_g) {
+  const float t = step[0] + 1.f;
   const float bc1 = 1.f - __powf(b1, t), bc2 = 1.f - __powf(b2, t);
   const long n4 = n / 4;
   const long stride = (long)gridDim.x * blockDim.x;
@@ -318,16 +318,33 @@ __global__ __launch_bounds__(256) void adam_dev_kernel(float* __restrict__ p, co
     reinterpret_cast<float4*>(p)[i] = pp;
     reinterpret_cast<float4*>(m)[i] = mm;
     reinterpret_cast<float4*>(v)[i] = vv;
+    if (zero_g) reinterpret_cast<float4*>(g)[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (shadow != nullptr) {
+      const unsigned lo = (unsigned)f2bf(pp.x) | ((unsigned)f2bf(pp.y) << 16);
+      const unsigned hi = (unsigned)f2bf(pp.z) | ((unsigned)f2bf(pp.w) << 16);
+      reinterpret_cast<uint2*>(shadow)[i] = make_uint2(lo, hi);
+    }
   }
-  for (long i = n4 * 4 + blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += stride)
+  for (long i = n4 * 4 + blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += stride) {
     adam_one(p[i], g[i] * gscale, m[i], v[i], lr, b1, b2, eps, wd, bc1, bc2);
+    if (zero_g) g[i] = 0.f;
+    if (shadow != nullptr) shadow[i] = f2bf(p[i]);
+  }
+  __syncthreads();  // every thread of this workgroup has read step[0]
+  if (threadIdx.x == 0) {
+    unsigned* ticket = reinterpret_cast<unsigned*>(step + 1);
+    if (atomicAdd(ticket, 1u) == gridDim.x - 1) {  // all other workgroups are past their read
+      step[0] = t;
+      *ticket = 0u;
+    }
+  }
 }
 
-void launch_adam_dev(float* p, const float* g, float* m, float* v, long n, float* step, float lr,
-                     float b1, float b2, float eps, float wd, float gscale, hipStream_t s) {
-  hipLaunchKernelGGL(inc_counter_kernel, dim3(1), dim3(64), 0, s, step);
+void launch_adam_dev(float* p, float* g, float* m, float* v, long n, float* step, float lr,
+                     float b1, float b2, float eps, float wd, float gscale, bf16_t* shadow, int zero_g,
+                     hipStream_t s) {
   hipLaunchKernelGGL(adam_dev_kernel, dim3(ew_blocks(n)), dim3(256), 0, s, p, g, m, v, n, step, lr,
-                     b1, b2, eps, wd, gscale);
+                     b1, b2, eps, wd, gscale, shadow, zero_g);
 }
 
 // Keras-0.x SGD: v = mu v - lr_t g; p += mu v - lr_t g (Nesterov) or p += v.

@@ -66,13 +66,18 @@ void launch_lstm_pack_weights(const float* W, bf16_t* Wp, bf16_t* WhhT, LstmDims
 // Writes H1, H2 ([B][256] bf16: the backward's saved activations) and pred. Returns false
 // (nothing launched) for shapes it does not cover.
 bool launch_mlp2_fwd(const bf16_t* X, int Fp, const bf16_t* W1, const float* b1, const bf16_t* W2, const float* b2,
-                     const float* w3, const float* b3, const float* y, bf16_t* H1, bf16_t* H2, float* pred, float* dy,
-                     float* loss_sum, float dy_scale, int B, hipStream_t s);
+                     const float* w3, const float* b3, const float* y, bf16_t* H1, bf16_t* H2, unsigned* M2,
+                     float* dw3, float* db3, float* pred, float* dy, float* loss_sum, float dy_scale, int B,
+                     hipStream_t s);
+// Mask mode (M2 != nullptr; needs y, dw3, db3): H2 is NOT written — only its ReLU bitmask M2
+// ([B][8] u32, bit u of row r = word 8r + u / 32, bit u % 32) — and dw3 += H2^T dy,
+// db3 += sum dy are accumulated by the forward itself.
 // ---- fused MLP backward (mlp_fused.hip), everything but the dW2 GEMM: from H1, H2
 // ([B][256] bf16), dy, w3 / W2 and X: dZ2 ([B][256] bf16, dW2's operand), db1, db2, dw3, db3
 // and — when dW1 != nullptr — dW1 ([256][Fp], Fp <= 32) (fp32, accumulated with atomics);
 // with dW1 == nullptr dZ1 ([B][256] bf16) is written for a separate dW1 GEMM instead.
-bool launch_mlp2_bwd(const bf16_t* H1, const bf16_t* H2, const float* dy, const float* w3, const bf16_t* W2,
+// M2 != nullptr: ReLU mask of layer 2 from the forward's bitmask (H2 unused) and no dw3 / db3.
+bool launch_mlp2_bwd(const bf16_t* H1, const bf16_t* H2, const unsigned* M2, const float* dy, const float* w3, const bf16_t* W2,
                      const bf16_t* X, int Fp, bf16_t* dZ1, bf16_t* dZ2, float* dW1, float* db1, float* db2,
                      float* dw3, float* db3, int B, hipStream_t s);
 
@@ -91,8 +96,9 @@ void launch_loss(int kind, const float* pred, const float* y, int B, int O, floa
 // ---- optimizers and casts over flat fp32 buffers ----
 void launch_adam(float* p, const float* g, float* m, float* v, long n, float lr, float b1,
                  float b2, float eps, float wd, float bc1, float bc2, float gscale, hipStream_t s);
-void launch_adam_dev(float* p, const float* g, float* m, float* v, long n, float* step, float lr,
-                     float b1, float b2, float eps, float wd, float gscale, hipStream_t s);
+void launch_adam_dev(float* p, float* g, float* m, float* v, long n, float* step, float lr,
+                     float b1, float b2, float eps, float wd, float gscale, bf16_t* shadow, int zero_g,
+                     hipStream_t s);
 void launch_sgd(float* p, const float* g, float* vel, long n, float lr, float momentum,
                 int nesterov, float gscale, hipStream_t s);
 void launch_cast_bf16(const float* src, bf16_t* dst, long n, hipStream_t s);

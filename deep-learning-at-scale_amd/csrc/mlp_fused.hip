@@ -47,12 +47,21 @@ __global__ __launch_bounds__(256, 1) void mlp2_fwd_kernel(
     const bf16_t* __restrict__ X, int Fp, const bf16_t* __restrict__ W1, const float* __restrict__ b1,
     const bf16_t* __restrict__ W2, const float* __restrict__ b2, const float* __restrict__ w3,
     const float* __restrict__ b3, const float* __restrict__ y, bf16_t* __restrict__ H1, bf16_t* __restrict__ H2,
-    float* __restrict__ pred, float* __restrict__ dy, float* __restrict__ loss_sum, float dy_scale, int B) {
+    unsigned* __restrict__ M2, float* __restrict__ dw3, float* __restrict__ db3, float* __restrict__ pred,
+    float* __restrict__ dy, float* __restrict__ loss_sum, float dy_scale, int B) {
   __shared__ __attribute__((aligned(16))) char xs[MF_ROWS * MF_XROW];
   __shared__ __attribute__((aligned(16))) char h1s[MF_ROWS * MF_H * 2];
   __shared__ __attribute__((aligned(16))) char h2s[MF_ROWS * MF_H * 2];
   __shared__ float red[4][MF_ROWS];
+  __shared__ float dys[MF_ROWS];
   __shared__ float lred[4];
+  // mask mode (M2 != nullptr, training): H2 leaves the CU only as its ReLU bitmask (32 B per
+  // row instead of 512 B) and the head gradients dw3 = H2^T dy, db3 = sum dy are accumulated
+  // here, from the H2 tile still in LDS, so the backward never needs the H2 values
+  const bool mask_mode = M2 != nullptr;
+  const int ec = threadIdx.x & 31, erq = threadIdx.x >> 5;  // dw3 ownership: units 8ec .. 8ec + 7
+  float dw3a[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  float db3a = 0.f;
 
   const int lane = threadIdx.x & 63, l15 = lane & 15, g = lane >> 4;
   const int wid = threadIdx.x >> 6;
@@ -183,13 +192,30 @@ __global__ __launch_bounds__(256, 1) void mlp2_fwd_kernel(
     }
     __syncthreads();
 
-    // ---- H2 tile -> HBM; head + loss for the chunk's rows (threads 0..63)
+    // ---- H2 tile (or its ReLU bitmask) -> HBM; head + loss for the chunk's rows (threads 0..63)
+    if (!mask_mode) {
 #pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      const int idx = threadIdx.x + 256 * k, r = idx >> 5, c = idx & 31, gr = row0 + r;
-      if (gr < B)
-        *reinterpret_cast<uint4*>(H2 + (size_t)gr * MF_H + 8 * c) =
-            *reinterpret_cast<const uint4*>(h2s + tile_off(r, 8 * c));
+      for (int k = 0; k < 8; ++k) {
+        const int idx = threadIdx.x + 256 * k, r = idx >> 5, c = idx & 31, gr = row0 + r;
+        if (gr < B)
+          *reinterpret_cast<uint4*>(H2 + (size_t)gr * MF_H + 8 * c) =
+              *reinterpret_cast<const uint4*>(h2s + tile_off(r, 8 * c));
+      }
+    } else {
+      // thread -> row t >> 2, units 64q .. 64q + 63 (q = t & 3) = mask words 2q, 2q + 1
+      const int r = threadIdx.x >> 2, q = threadIdx.x & 3, gr = row0 + r;
+      unsigned mw[2] = {0u, 0u};
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const uint4 v = *reinterpret_cast<const uint4*>(h2s + tile_off(r, 64 * q + 8 * k));
+        const unsigned w4[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const int bit = 8 * k + e;
+          if (bf2f((bf16_t)(w4[e >> 1] >> (16 * (e & 1)))) > 0.f) mw[bit >> 5] |= 1u << (bit & 31);
+        }
+      }
+      if (gr < B) *reinterpret_cast<uint2*>(M2 + (size_t)gr * 8 + 2 * q) = make_uint2(mw[0], mw[1]);
     }
     if (threadIdx.x < MF_ROWS) {
       const int gr = row0 + threadIdx.x;
@@ -200,14 +226,45 @@ __global__ __launch_bounds__(256, 1) void mlp2_fwd_kernel(
           const float diff = p - y[gr];
           lsum += diff * diff;
           if (dy != nullptr) dy[gr] = dy_scale * diff;
+          if (mask_mode) {
+            dys[threadIdx.x] = dy_scale * diff;
+            db3a += dy_scale * diff;
+          }
         }
+      } else if (mask_mode) {
+        dys[threadIdx.x] = 0.f;
       }
     }
-    __syncthreads();  // xs / h1s / h2s / red are rewritten by the next chunk
+    if (mask_mode) {  // dw3 partials: H2 tile rows x dy
+      __syncthreads();
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const int r = erq + 8 * q;
+        const float gy = dys[r];
+        const uint4 v = *reinterpret_cast<const uint4*>(h2s + tile_off(r, 8 * ec));
+        const unsigned w4[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int e = 0; e < 8; ++e) dw3a[e] += gy * bf2f((bf16_t)(w4[e >> 1] >> (16 * (e & 1))));
+      }
+    }
+    __syncthreads();  // xs / h1s / h2s / red / dys are rewritten by the next chunk
   }
   if (loss_sum != nullptr) {
     const float t = block_sum<256>(lsum, lred);
     if (threadIdx.x == 0 && t != 0.f) atomicAdd(loss_sum, t);
+  }
+  if (mask_mode) {
+    // the 8 threads of one unit chunk (erq = 0..7) -> LDS [8][256], then one atomic per unit
+    float* sd = reinterpret_cast<float*>(h1s);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) sd[erq * MF_H + 8 * ec + e] = dw3a[e];
+    __syncthreads();
+    float s3 = 0.f;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) s3 += sd[q * MF_H + threadIdx.x];
+    if (s3 != 0.f) atomicAdd(dw3 + threadIdx.x, s3);
+    const float t3 = block_sum<256>(db3a, lred);
+    if (threadIdx.x == 0 && t3 != 0.f) atomicAdd(db3, t3);
   }
 }
 
@@ -236,7 +293,8 @@ __global__ __launch_bounds__(256, 1) void mlp2_fwd_kernel(
 //    (2 x 4 x NFT MFMAs per chunk), and dZ1 is then not written to HBM at all.
 template <int NFT>  // 16-feature tiles of dW1 (1: Fp <= 16, 2: Fp <= 32): dW1 registers = 16 x NFT
 __global__ __launch_bounds__(256, 1) void mlp2_bwd_kernel(
-    const bf16_t* __restrict__ H1, const bf16_t* __restrict__ H2, const float* __restrict__ dy,
+    const bf16_t* __restrict__ H1, const bf16_t* __restrict__ H2, const unsigned* __restrict__ M2,
+    const float* __restrict__ dy,
     const float* __restrict__ w3, const bf16_t* __restrict__ W2, const bf16_t* __restrict__ X, int Fp,
     bf16_t* __restrict__ dZ1, bf16_t* __restrict__ dZ2, float* __restrict__ dW1, float* __restrict__ db1,
     float* __restrict__ db2, float* __restrict__ dw3, float* __restrict__ db3, int B) {
@@ -293,13 +351,17 @@ __global__ __launch_bounds__(256, 1) void mlp2_bwd_kernel(
     for (int q = 0; q < 8; ++q) {
       const int r = rq + 8 * q, gr = row0 + r;
       uint4 h2v = make_uint4(0, 0, 0, 0), h1v = make_uint4(0, 0, 0, 0);
+      unsigned mb = 0u;  // mask mode: ReLU bits of units 8c .. 8c + 7
       float gy = 0.f;
       if (gr < B) {
-        h2v = *reinterpret_cast<const uint4*>(H2 + (size_t)gr * MF_H + 8 * c);
+        if (M2 == nullptr)
+          h2v = *reinterpret_cast<const uint4*>(H2 + (size_t)gr * MF_H + 8 * c);
+        else
+          mb = M2[(size_t)gr * 8 + (c >> 2)] >> (8 * (c & 3));
         h1v = *reinterpret_cast<const uint4*>(H1 + (size_t)gr * MF_H + 8 * c);
         gy = dy[gr];
       }
-      if (c == 0) db3a += gy;
+      if (c == 0 && M2 == nullptr) db3a += gy;  // mask mode: the forward did the head gradients
       const unsigned hw[4] = {h2v.x, h2v.y, h2v.z, h2v.w};
       unsigned zw[4];
 #pragma unroll
@@ -308,9 +370,15 @@ __global__ __launch_bounds__(256, 1) void mlp2_bwd_kernel(
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
           const int e = 2 * p + h;
-          const float hv = bf2f((bf16_t)(hw[p] >> (16 * h)));
-          dw3a[e] += gy * hv;
-          const bf16_t zb = f2bf(hv > 0.f ? gy * w3c[e] : 0.f);
+          bool on;
+          if (M2 == nullptr) {
+            const float hv = bf2f((bf16_t)(hw[p] >> (16 * h)));
+            dw3a[e] += gy * hv;
+            on = hv > 0.f;
+          } else {
+            on = (mb >> e) & 1u;
+          }
+          const bf16_t zb = f2bf(on ? gy * w3c[e] : 0.f);
           db2a[e] += bf2f(zb);
           pk |= (unsigned)zb << (16 * h);
         }
@@ -463,7 +531,7 @@ __global__ __launch_bounds__(256, 1) void mlp2_bwd_kernel(
   if (threadIdx.x == 0 && t3 != 0.f) atomicAdd(db3, t3);
 }
 
-bool launch_mlp2_bwd(const bf16_t* H1, const bf16_t* H2, const float* dy, const float* w3, const bf16_t* W2,
+bool launch_mlp2_bwd(const bf16_t* H1, const bf16_t* H2, const unsigned* M2, const float* dy, const float* w3, const bf16_t* W2,
                      const bf16_t* X, int Fp, bf16_t* dZ1, bf16_t* dZ2, float* dW1, float* db1, float* db2,
                      float* dw3, float* db3, int B, hipStream_t s) {
   if (B <= 0 || (dW1 != nullptr && (X == nullptr || Fp > 32 || Fp % 8 != 0))) return false;
@@ -474,18 +542,20 @@ bool launch_mlp2_bwd(const bf16_t* H1, const bf16_t* H2, const float* dy, const 
     cus = 256;
   const int grid = nchunks < cus ? nchunks : cus;
   if (Fp <= 16)
-    hipLaunchKernelGGL(mlp2_bwd_kernel<1>, dim3(grid), dim3(256), 0, s, H1, H2, dy, w3, W2, X, Fp, dZ1, dZ2, dW1,
+    hipLaunchKernelGGL(mlp2_bwd_kernel<1>, dim3(grid), dim3(256), 0, s, H1, H2, M2, dy, w3, W2, X, Fp, dZ1, dZ2, dW1,
                        db1, db2, dw3, db3, B);
   else
-    hipLaunchKernelGGL(mlp2_bwd_kernel<2>, dim3(grid), dim3(256), 0, s, H1, H2, dy, w3, W2, X, Fp, dZ1, dZ2, dW1,
+    hipLaunchKernelGGL(mlp2_bwd_kernel<2>, dim3(grid), dim3(256), 0, s, H1, H2, M2, dy, w3, W2, X, Fp, dZ1, dZ2, dW1,
                        db1, db2, dw3, db3, B);
   return true;
 }
 
 bool launch_mlp2_fwd(const bf16_t* X, int Fp, const bf16_t* W1, const float* b1, const bf16_t* W2, const float* b2,
-                     const float* w3, const float* b3, const float* y, bf16_t* H1, bf16_t* H2, float* pred, float* dy,
-                     float* loss_sum, float dy_scale, int B, hipStream_t s) {
+                     const float* w3, const float* b3, const float* y, bf16_t* H1, bf16_t* H2, unsigned* M2,
+                     float* dw3, float* db3, float* pred, float* dy, float* loss_sum, float dy_scale, int B,
+                     hipStream_t s) {
   if (Fp > 64 || Fp % 8 != 0 || B <= 0) return false;
+  if (M2 != nullptr && (y == nullptr || dw3 == nullptr || db3 == nullptr)) return false;
   const int nchunks = (B + MF_ROWS - 1) / MF_ROWS;
   int dev = 0, cus = 0;
   if (hipGetDevice(&dev) != hipSuccess ||
@@ -494,10 +564,10 @@ bool launch_mlp2_fwd(const bf16_t* X, int Fp, const bf16_t* W1, const float* b1,
   const int grid = nchunks < cus ? nchunks : cus;
   if (Fp <= 32)
     hipLaunchKernelGGL(mlp2_fwd_kernel<1>, dim3(grid), dim3(256), 0, s, X, Fp, W1, b1, W2, b2, w3, b3, y, H1, H2,
-                       pred, dy, loss_sum, dy_scale, B);
+                       M2, dw3, db3, pred, dy, loss_sum, dy_scale, B);
   else
     hipLaunchKernelGGL(mlp2_fwd_kernel<2>, dim3(grid), dim3(256), 0, s, X, Fp, W1, b1, W2, b2, w3, b3, y, H1, H2,
-                       pred, dy, loss_sum, dy_scale, B);
+                       M2, dw3, db3, pred, dy, loss_sum, dy_scale, B);
   return true;
 }
 

@@ -147,6 +147,13 @@ class NativeMLP:
         # fused weight-stationary forward for the 256 x 256 BASELINE shape (WELLFLOW_MLP_FUSED=0: per-layer)
         self.fused = os.environ.get("WELLFLOW_MLP_FUSED", "1") != "0"
         self.fused_bwd = os.environ.get("WELLFLOW_MLP_FUSED_BWD", "1") != "0"
+        # training step with both fused kernels: H2 leaves the forward only as a ReLU bitmask
+        # (32 B per row instead of 512 B) and the head gradients are taken in the forward
+        self.mask_h2 = os.environ.get("WELLFLOW_MLP_MASK", "1") != "0"
+        # weight-gradient GEMM overrides (tools/gpu_mlp_dw.sh sweep): split-K depth, tile (ops.native.gemm)
+        self.dw_ksplit = int(os.environ.get("WELLFLOW_MLP_DW_KSPLIT", "0"))
+        self.dw_tile = int(os.environ.get("WELLFLOW_MLP_DW_TILE", "0"))
+        self.M2 = torch.zeros(batch * 8, dtype=torch.int32, device=dev) if self.hidden == (256, 256) else None
         self.sync_weights()
 
     def sync_weights(self) -> None:
@@ -175,15 +182,18 @@ class NativeMLP:
             gemm(A, W, B, h, k, outH=Hout, bias=b, act=1)
             A, K = Hout, h
 
-    def _fused_forward(self, B: int, y=None, dy=None, loss_sum=None, dy_scale: float = 0.0) -> bool:
+    def _fused_forward(self, B: int, y=None, dy=None, loss_sum=None, dy_scale: float = 0.0,
+                       head_grads=None) -> bool:
         """Both hidden layers + head (+ MSE) in ONE weight-stationary launch
         (csrc/mlp_fused.hip) for the BASELINE shape F -> 256 -> 256 -> 1; False = not covered."""
         if not self.fused or self.hidden != (256, 256) or self.Fp > 64:
             return False
         wl, _, _ = self.lay.views(self.shadow)
         pl, hw, hb = self.lay.views(self.params)
+        m2, dw3, db3 = (self.M2, *head_grads) if head_grads is not None else (None, None, None)
         return bool(self._C.mlp2_forward(self.X, self.Fp, wl[0][0], pl[0][1], wl[1][0], pl[1][1], hw, hb, y,
-                                         self.Hs[0], self.Hs[1], self.pred, dy, loss_sum, float(dy_scale), B))
+                                         self.Hs[0], self.Hs[1], self.pred, dy, loss_sum, float(dy_scale), B,
+                                         m2, dw3, db3))
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         B = self._load_x(x)
@@ -210,9 +220,14 @@ class NativeMLP:
         L = len(self.hidden)
         H = self.hidden[-1]
         y = y.contiguous().float()
-        if self.loss_kind == "mse" and self._fused_forward(B, y, self.dy, self.loss_sum, 2.0 * float(grad_scale)):
-            pass  # layers + head + MSE + dy in one launch
+        # mask mode needs the fused backward to consume the bitmask (it always launches for
+        # the (256, 256) shape: dW1 moves to a GEMM when Fp > 32)
+        use_mask = self.mask_h2 and self.fused_bwd and self.hidden == (256, 256) and self.loss_kind == "mse"
+        if self.loss_kind == "mse" and self._fused_forward(B, y, self.dy, self.loss_sum, 2.0 * float(grad_scale),
+                                                           (ghw, ghb) if use_mask else None):
+            pass  # layers + head + MSE + dy (+ head gradients in mask mode) in one launch
         elif self.loss_kind == "mse":
+            use_mask = False
             self._forward_body(B)
             C.head_fwd(self.Hs[-1], H, B, H, hw, hb, y, self.pred, self.dy, self.loss_sum,
                        2.0 * float(grad_scale))
@@ -229,7 +244,9 @@ class NativeMLP:
         fused_bwd = (self.fused_bwd and self.hidden == (256, 256) and
                      C.mlp2_backward(self.Hs[0], self.Hs[1], self.dy, hw, wl[1][0], self.X, self.Fp,
                                      self.dZ[0], self.dZ[1], gl[0][0] if fused_dw1 else None, gl[0][1],
-                                     gl[1][1], ghw, ghb, B))
+                                     gl[1][1], ghw, ghb, B, self.M2 if use_mask else None))
+        if use_mask and not fused_bwd:
+            raise RuntimeError("NativeMLP: H2 bitmask written but the fused backward did not launch")
         if not fused_bwd:
             C.head_bwd_w(self.Hs[-1], H, B, H, self.dy, ghw, ghb)
             C.head_bwd_x(self.Hs[-1], H, B, H, self.dy, hw, True, self.dZ[-1], H, gl[-1][1])
@@ -242,10 +259,14 @@ class NativeMLP:
             h, k = self.lay.dims[l]
             prevH = self.Hs[l - 1] if l > 0 else self.X
             # dW_l = dZ_l^T H_{l-1}   (reduce over the batch; MN-contiguous operands)
-            # ... but keep the fp32 atomic traffic (ksplit x h x k x 4 B) <= ~8 MB
-            ksplit = max(1, min(512 // tiles(h, k), B // 256, 64, (8 << 20) // (4 * h * k)))
+            # ... but keep the fp32 atomic traffic (ksplit x h x k x 4 B) <= ~16 MB. 256 x 256 at
+            # B = 262144: split-K 64 = 256 workgroups, one per CU (tools/gpu_mlp_dw.sh sweep:
+            # 0.421 ms/step at split-K 32 -> 0.390 at 64, 0.404 at 128)
+            ksplit = max(1, min(512 // tiles(h, k), B // 256, 64, (16 << 20) // (4 * h * k)))
+            if self.dw_ksplit > 0:
+                ksplit = max(1, min(self.dw_ksplit, B // 256))
             gemm(self.dZ[l], prevH, h, k, B, a_mn=True, lda=h, b_mn=True, ldb=k,
-                 outF=gl[l][0], atomic=True, ksplit=ksplit)
+                 outF=gl[l][0], atomic=True, ksplit=ksplit, tile=self.dw_tile)
             if l > 0 and not fused_bwd:
                 # dZ_{l-1} = (dZ_l W_l) * [H_{l-1} > 0];  db_{l-1} = colsum
                 gemm(self.dZ[l], wl[l][0], B, k, h, b_mn=True, ldb=k, outH=self.dZ[l - 1],

@@ -15,9 +15,15 @@ class FlatAdam:
     """Adam / AdamW (decoupled weight decay) with PyTorch's bias-correction semantics."""
 
     def __init__(self, params: torch.Tensor, grads: torch.Tensor, lr: float = 1e-3,
-                 betas=(0.9, 0.999), eps: float = 1e-8, weight_decay: float = 0.0):
+                 betas=(0.9, 0.999), eps: float = 1e-8, weight_decay: float = 0.0,
+                 shadow: torch.Tensor | None = None, zero_grads: bool = False):
+        """GPU fusions: ``shadow`` (bf16, same numel) receives the updated weights in the same
+        launch (an engine whose compute copy is a plain cast, e.g. NativeMLP.shadow);
+        ``zero_grads`` clears the gradient bucket after the update (the next
+        forward_backward then runs with zero_grads=False)."""
         assert params.dtype == torch.float32 and params.shape == grads.shape
         self.params, self.grads = params, grads
+        self.shadow, self.zero_grads = shadow, zero_grads
         self.lr, self.betas, self.eps, self.weight_decay = lr, tuple(betas), eps, weight_decay
         self.m = torch.zeros_like(params)
         self.v = torch.zeros_like(params)
@@ -33,7 +39,7 @@ class FlatAdam:
             from ..ops.native import lib
 
             lib().adam_dev(self.params, self.grads, self.m, self.v, self.step_dev, self.lr, b1, b2,
-                           self.eps, self.weight_decay, grad_scale)
+                           self.eps, self.weight_decay, grad_scale, self.shadow, self.zero_grads)
             return
         bc1, bc2 = 1.0 - b1**self.t, 1.0 - b2**self.t
         g = self.grads * grad_scale
@@ -43,6 +49,10 @@ class FlatAdam:
         if self.weight_decay:
             upd = upd + self.weight_decay * self.params
         self.params.sub_(self.lr * upd)
+        if self.shadow is not None:
+            self.shadow.copy_(self.params)
+        if self.zero_grads:
+            self.grads.zero_()
 
     def state_dict(self) -> dict:
         return {"kind": "adam", "t": self.t, "m": self.m.detach().cpu(), "v": self.v.detach().cpu(),
@@ -52,7 +62,8 @@ class FlatAdam:
     def load_state_dict(self, sd: dict) -> None:
         self.t = int(sd["t"])
         if self.step_dev is not None:
-            self.step_dev.fill_(float(self.t))
+            self.step_dev.zero_()  # [1] is the kernel's completion ticket
+            self.step_dev[0] = float(self.t)
         self.m.copy_(sd["m"])
         self.v.copy_(sd["v"])
         self.lr, self.betas, self.eps = sd["lr"], tuple(sd["betas"]), sd["eps"]
