@@ -139,6 +139,10 @@ class NativeMLP:
         bf = torch.bfloat16
         self.Fp = _r8(n_features)
         self.X = torch.zeros(batch * self.Fp, dtype=bf, device=dev)
+        # read bf16 streamed batches in place instead of one D2D copy into self.X: A/B at 100
+        # steps x 3 was within run-to-run noise (558 vs 571 M rows/s), so off by default
+        self.x_inplace = os.environ.get("WELLFLOW_MLP_X_INPLACE", "0") != "0"
+        self._Xop = self.X  # the X operand of the current step (self.X or a bf16 batch read in place)
         self.Hs = [torch.empty(batch * h, dtype=bf, device=dev) for h in self.hidden]
         self.dZ = [torch.empty(batch * h, dtype=bf, device=dev) for h in self.hidden]
         self.pred = torch.empty(batch, device=dev)
@@ -162,9 +166,15 @@ class NativeMLP:
     def _load_x(self, x: torch.Tensor) -> int:
         B = x.shape[0]
         assert B <= self.B and x.shape[1] == self.F
+        self._Xop = self.X
         Xv = self.X[: B * self.Fp].view(B, self.Fp)
-        if x.dtype == torch.bfloat16 and self.Fp == self.F:
-            # already in the MFMA input format (bf16-streamed online batches): one D2D copy
+        if (self.x_inplace and x.dtype == torch.bfloat16 and self.Fp == self.F and x.is_contiguous()
+                and x.device == self.device
+                and x.data_ptr() % 16 == 0):
+            # already in the MFMA input format (bf16-streamed online batches, whose ring slot
+            # is not overwritten before this step's kernels ran): read it in place
+            self._Xop = x.view(-1)
+        elif x.dtype == torch.bfloat16 and self.Fp == self.F:
             Xv.copy_(x)
         elif self.Fp == self.F:
             self._C.cast_bf16(x.contiguous().float(), Xv)
@@ -177,7 +187,7 @@ class NativeMLP:
 
         wl, _, _ = self.lay.views(self.shadow)
         pl, _, _ = self.lay.views(self.params)
-        A, K = self.X, self.Fp
+        A, K = self._Xop, self.Fp
         for (W, _), (_, b), Hout, (h, k) in zip(wl, pl, self.Hs, self.lay.dims):
             gemm(A, W, B, h, k, outH=Hout, bias=b, act=1)
             A, K = Hout, h
@@ -191,7 +201,7 @@ class NativeMLP:
         wl, _, _ = self.lay.views(self.shadow)
         pl, hw, hb = self.lay.views(self.params)
         m2, dw3, db3 = (self.M2, *head_grads) if head_grads is not None else (None, None, None)
-        return bool(self._C.mlp2_forward(self.X, self.Fp, wl[0][0], pl[0][1], wl[1][0], pl[1][1], hw, hb, y,
+        return bool(self._C.mlp2_forward(self._Xop, self.Fp, wl[0][0], pl[0][1], wl[1][0], pl[1][1], hw, hb, y,
                                          self.Hs[0], self.Hs[1], self.pred, dy, loss_sum, float(dy_scale), B,
                                          m2, dw3, db3))
 
@@ -242,7 +252,7 @@ class NativeMLP:
         # wider inputs, dW1) run as split-K GEMMs
         fused_dw1 = self.Fp <= 32
         fused_bwd = (self.fused_bwd and self.hidden == (256, 256) and
-                     C.mlp2_backward(self.Hs[0], self.Hs[1], self.dy, hw, wl[1][0], self.X, self.Fp,
+                     C.mlp2_backward(self.Hs[0], self.Hs[1], self.dy, hw, wl[1][0], self._Xop, self.Fp,
                                      self.dZ[0], self.dZ[1], gl[0][0] if fused_dw1 else None, gl[0][1],
                                      gl[1][1], ghw, ghb, B, self.M2 if use_mask else None))
         if use_mask and not fused_bwd:
@@ -257,7 +267,7 @@ class NativeMLP:
             if l == 0 and fused_bwd and fused_dw1:
                 break  # dW1 accumulated inside the fused backward
             h, k = self.lay.dims[l]
-            prevH = self.Hs[l - 1] if l > 0 else self.X
+            prevH = self.Hs[l - 1] if l > 0 else self._Xop
             # dW_l = dZ_l^T H_{l-1}   (reduce over the batch; MN-contiguous operands)
             # ... but keep the fp32 atomic traffic (ksplit x h x k x 4 B) <= ~16 MB. 256 x 256 at
             # B = 262144: split-K 64 = 256 workgroups, one per CU (tools/gpu_mlp_dw.sh sweep:
