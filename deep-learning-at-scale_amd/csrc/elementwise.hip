@@ -4,6 +4,8 @@
 // time decay, one launch over the flat buffer), K15 (regression head), K16 (MSE fwd+bwd,
 // wave64 shuffle reduction + one atomic per workgroup), K17 (fused Adam over the flat
 // fp32 master buffer, float4-vectorised), K18 (casts).
+#include <cstdlib>
+
 #include "common.h"
 #include "kernels.h"
 
@@ -72,7 +74,15 @@ void launch_head_fwd(const bf16_t* Hm, long ldh, int B, int Hd, const float* w, 
   const int lpr = lanes_per_row(Hd);
   const int rpb = 256 / lpr;
   int grid = (B + rpb - 1) / rpb;
-  if (grid > 2048) grid = 2048;  // one same-address loss atomic per block
+  // one same-address loss atomic per block: cap the grid. LSTM head (B = 8192, Hd = 512,
+  // kernel trace, tools/gpu_head_sweep.sh): 30.8 us at 2048 blocks, 18.3 at 1024, 13.4 at 512,
+  // 14.0 at 256 — the atomics serialise, not the loads (WELLFLOW_HEAD_GRID overrides)
+  static const int cap = [] {
+    const char* e = std::getenv("WELLFLOW_HEAD_GRID");
+    const int v = e != nullptr ? std::atoi(e) : 0;
+    return v > 0 ? v : 512;
+  }();
+  if (grid > cap) grid = cap;
 #define HEAD_FWD(L)                                                                              \
   hipLaunchKernelGGL(head_fwd_kernel<L>, dim3(grid), dim3(256), 0, s, Hm, ldh, B, Hd, w, b0, target, \
                      pred, dy, loss_sum, dy_scale)
@@ -150,7 +160,15 @@ void launch_head_bwd_w(const bf16_t* Hm, long ldh, int B, int Hd, const float* d
                        float* db, hipStream_t s) {
   const HeadBwdGeom g = head_geom(Hd);
   int grid = (B + g.rg - 1) / g.rg;
-  if (grid > 512) grid = 512;
+  // per-column atomics per block: cap the grid. LSTM head (B = 8192, Hd = 512, kernel trace,
+  // tools/gpu_headw_sweep.sh): 16.2 us at 512 blocks, 11.0 at 256, 10.3 at 128, 13.6 at 64
+  // (WELLFLOW_HEADW_GRID overrides)
+  static const int cap = [] {
+    const char* e = std::getenv("WELLFLOW_HEADW_GRID");
+    const int v = e != nullptr ? std::atoi(e) : 0;
+    return v > 0 ? v : 128;
+  }();
+  if (grid > cap) grid = cap;
   hipLaunchKernelGGL(head_bwd_w_kernel, dim3(grid), dim3(256), 0, s, Hm, ldh, B, Hd, dy, dw, db, g);
 }
 
