@@ -104,13 +104,14 @@ def bench_lstm(args, ctx):
     eng.params.copy_(init_lstm_flat(F, H, seed=0).to(ctx.device))
     ctx.broadcast_(eng.params)  # C1: identical init on every rank
     eng.sync_weights()
-    opt = FlatAdam(eng.params, eng.grads, lr=args.lr)
+    # Adam clears the gradient bucket in its own launch (no fill kernel before the backward)
+    opt = FlatAdam(eng.params, eng.grads, lr=args.lr, zero_grads=True)
     x, y = synth_lstm_batch(B, T, F, seed=ctx.rank)  # Gilbert-consistent windows, GPU-resident
     x, y = x.to(ctx.device), y.to(ctx.device)
     gscale = 1.0 / (B * ctx.world_size)
 
     def compute():
-        eng.forward_backward(x, y, gscale)
+        eng.forward_backward(x, y, gscale, zero_grads=False)
 
     def update():
         opt.step()
