@@ -6,19 +6,27 @@ One row = one training sample (a 64-step window of well-log features and its flo
 Every timed step is a FULL training step: forward over all 64 timesteps, MSE loss,
 backward through time, weight gradients, RCCL gradient all-reduce (world > 1), fused Adam
 update and the bf16 weight repack. Weak scaling: per-GPU batch fixed, global = per-GPU x N.
+The step is the production one (wellflow/train/step.py StepRunner, also driven by the
+job's Trainer): after two eager steps it replays as ONE hipGraph per step, the RCCL
+all-reduce captured inside it.
 
 Secondary configs (BASELINE.json:8-10), same JSON contract:
-  --model mlp         static 3-layer MLP (F -> 256 -> 256 -> 1), resident batch, hipGraph step
+  --model mlp         static 3-layer MLP (F -> 256 -> 256 -> 1), resident batch
   --model mlp_online  dynamic MLP: every step trains on a NEW mini-batch streamed host -> HBM
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B_per_gpu] [--model ...]
-    python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
+
+With --gpus N > 1 and no torchrun environment, this process (which never touches the GPU)
+starts `torch.distributed.run --nproc-per-node N` on itself and exits with its status; under
+torchrun (WORLD_SIZE set) every rank runs the benchmark and rank 0 prints the JSON line.
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -30,6 +38,25 @@ METRIC = "rows/sec (whole node), LSTM seq64 regression at 1/2/4/8 MI355X; val MS
 # per-GPU rows per step. MLP: 262144 rows (bf16 activations ~270 MB of 288 GB HBM) — at
 # 65536 the 0.24 ms step is launch/stream-overhead bound (216-272 M rows/s vs 382 M here)
 DEFAULT_BATCH = {"lstm": 8192, "mlp": 262144, "mlp_online": 262144}
+
+
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _spawn_ranks(n: int, argv) -> int:
+    """Launcher mode: N ranks on this node via torch.distributed.run (127.0.0.1 rendezvous).
+    The parent imports nothing GPU-related; each child pins its own GPU (LOCAL_RANK)."""
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # dmabuf IPC (RCCL / tensor sharing)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+           os.path.abspath(__file__), *argv]
+    return subprocess.run(cmd, env=env, cwd=ROOT).returncode
 
 
 def _timed(ctx, step, steps, warmup):
@@ -51,44 +78,31 @@ def _timed(ctx, step, steps, warmup):
     return ctx.max_scalar(time.perf_counter() - t0)
 
 
-def _graph_step(ctx, eng, compute, update, no_graph: bool):
-    """Capture compute (fwd+bwd) and update (Adam + bf16 repack) as two hipGraphs; the RCCL
-    all-reduce between them stays eager. Adam's step counter lives on the device, so a
-    replay is exactly the eager step. Three eager warm-up steps on a side stream first
-    (allocator + lazy init), as torch.cuda.graph requires."""
+def _comm_ms(ctx, buf, iters: int = 20) -> float | None:
+    """Event-timed C2 (the flat gradient all-reduce) at this world size, outside the step
+    (inside the step it is one node of the captured graph). None at world size 1."""
     import torch
 
-    if no_graph:
-        def step():
-            compute()
-            ctx.all_reduce_sum_(eng.grads)
-            update()
-        return step
-    s = torch.cuda.Stream(device=ctx.device)
-    s.wait_stream(torch.cuda.current_stream(ctx.device))
-    with torch.cuda.stream(s):
-        for _ in range(3):
-            compute()
-            ctx.all_reduce_sum_(eng.grads)
-            update()
-    torch.cuda.current_stream(ctx.device).wait_stream(s)
-    g1, g2 = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
-    with torch.cuda.graph(g1):
-        compute()
-    with torch.cuda.graph(g2):
-        update()
-
-    def step():
-        g1.replay()
-        ctx.all_reduce_sum_(eng.grads)
-        g2.replay()
-    return step
+    if not ctx.distributed or ctx.world_size == 1 or ctx.device.type != "cuda":
+        return None
+    scratch = buf.clone()
+    for _ in range(3):
+        ctx.all_reduce_sum_(scratch)
+    ctx.barrier()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(iters):
+        ctx.all_reduce_sum_(scratch)
+    e1.record()
+    torch.cuda.synchronize()
+    return ctx.max_scalar(e0.elapsed_time(e1) / iters)
 
 
 def bench_lstm(args, ctx):
     from wellflow.data.synth import synth_lstm_batch
     from wellflow.models.lstm import NativeLSTM, init_lstm_flat
     from wellflow.optim.flat import FlatAdam
+    from wellflow.train.step import StepRunner
 
     B, T, F, H = args.batch, args.seq, args.features, args.hidden
     model = f"LSTM seq-len={T} hidden={H} time-series regression (features={F}, linear head, MSE, Adam)"
@@ -108,28 +122,20 @@ def bench_lstm(args, ctx):
     opt = FlatAdam(eng.params, eng.grads, lr=args.lr, zero_grads=True)
     x, y = synth_lstm_batch(B, T, F, seed=ctx.rank)  # Gilbert-consistent windows, GPU-resident
     x, y = x.to(ctx.device), y.to(ctx.device)
-    gscale = 1.0 / (B * ctx.world_size)
-
-    def compute():
-        eng.forward_backward(x, y, gscale, zero_grads=False)
-
-    def update():
-        opt.step()
-        eng.sync_weights()
-
-    # the ~135 launches of a step (64 fwd + 64 bwd + dW + head/loss/Adam) replay as one
-    # hipGraph; C2 (one flat RCCL bucket over xGMI) runs between the two graphs
-    step = _graph_step(ctx, eng, compute, update, args.no_graph or eng.dw_chunk > 0)
-
-    el = _timed(ctx, step, args.steps, args.warmup)
-    return el, B, model, eng.loss_sum.item() / B
+    run = StepRunner(eng, opt, ctx, 1.0 / (B * ctx.world_size), lambda k: (x, y),
+                     graph=not (args.no_graph or eng.dw_chunk > 0), comm_in_graph=not args.eager_comm)
+    el = _timed(ctx, run.run, args.steps, args.warmup)
+    eng.check_device_errors()  # a timed-out persistent hand-off anywhere in the run fails the bench
+    extra = {"persistent_fwd": eng.last_forward_persistent, "persistent_bwd": eng.last_backward_persistent}
+    return el, B, model, float(eng.loss_sum.item()) / B, run, eng, extra
 
 
 def _cpu_rehearsal(args, ctx, model):
     """--device cpu: the same timed DP step (C1 broadcast, C2 flat all-reduce, flat Adam)
-    on the fp32 PyTorch reference model over gloo. It exists so the launch / timing / JSON
-    contract at world size > 1 is exercised without GPUs (tests/test_bench_cpu.py); its
-    numbers are NOT the benchmark (the line says dtype fp32 and data 'cpu rehearsal')."""
+    on the fp32 PyTorch reference model over gloo, through the same StepRunner. It exists so
+    the launch / timing / JSON contract at world size > 1 is exercised without GPUs
+    (tests/test_bench_cpu.py); its numbers are NOT the benchmark (the line says dtype fp32
+    and data 'cpu rehearsal')."""
     import torch
 
     from wellflow.data.synth import synth_lstm_batch, synth_tabular_batch
@@ -137,6 +143,7 @@ def _cpu_rehearsal(args, ctx, model):
     from wellflow.models.lstm import LSTMRegressor
     from wellflow.models.mlp import MLPRegressor
     from wellflow.optim.flat import FlatAdam
+    from wellflow.train.step import StepRunner
 
     torch.manual_seed(0)
     B, F = args.batch, args.features
@@ -148,16 +155,9 @@ def _cpu_rehearsal(args, ctx, model):
         x, y = synth_tabular_batch(B, F, seed=ctx.rank)
     ctx.broadcast_(eng.params)
     opt = FlatAdam(eng.params, eng.grads, lr=args.lr)
-    gscale = 1.0 / (B * ctx.world_size)
-    last = [0.0]
-
-    def step():
-        last[0] = float(eng.forward_backward(x, y, gscale))
-        ctx.all_reduce_sum_(eng.grads)
-        opt.step()
-
-    el = _timed(ctx, step, args.steps, args.warmup)
-    return el, B, model, last[0] / B
+    run = StepRunner(eng, opt, ctx, 1.0 / (B * ctx.world_size), lambda k: (x, y))
+    el = _timed(ctx, run.run, args.steps, args.warmup)
+    return el, B, model, run.take_loss() / (B * (args.steps + args.warmup)), run, eng, {}
 
 
 def bench_mlp(args, ctx, online: bool):
@@ -167,6 +167,7 @@ def bench_mlp(args, ctx, online: bool):
     from wellflow.data.synth import synth_tabular_batch
     from wellflow.models.mlp import NativeMLP, init_mlp_flat
     from wellflow.optim.flat import FlatAdam
+    from wellflow.train.step import StepRunner
 
     B, F, hid = args.batch, args.features, (256, 256)
     kind = "dynamic (online, host->HBM streamed mini-batches)" if online else "static (resident batch)"
@@ -180,61 +181,27 @@ def bench_mlp(args, ctx, online: bool):
     # Adam writes the bf16 compute copy and clears the gradient bucket in its own launch
     opt = FlatAdam(eng.params, eng.grads, lr=args.lr, shadow=eng.shadow, zero_grads=True)
     gscale = 1.0 / (B * ctx.world_size)
-
+    graph = not args.no_graph
     if online:
         # features cross PCIe as bf16 (the engine's MFMA input format: identical numerics to
         # streaming fp32 and casting on the device, half the bytes); targets stay fp32
         x_dtype = torch.float32 if args.stream_fp32 else torch.bfloat16
         pool = HostPool(lambda k: synth_tabular_batch(B, F, seed=1000 * ctx.rank + k), n=8, x_dtype=x_dtype)
-        depth = 3
-        streamer = DeviceStreamer(pool, ctx.device, depth=depth)
-        for _ in range(depth):  # allocate every ring slot
-            streamer.next()
-        torch.cuda.synchronize()
-        graphs = {}
-        if not args.no_graph:
-            # one captured compute graph per ring slot (it reads that slot's buffers)
-            s = torch.cuda.Stream(device=ctx.device)
-            s.wait_stream(torch.cuda.current_stream(ctx.device))
-            with torch.cuda.stream(s):
-                for _ in range(2):
-                    eng.forward_backward(streamer.slots[0][0], streamer.slots[0][1], gscale)
-                eng.grads.zero_()  # from here on Adam clears the bucket after each update
-            torch.cuda.current_stream(ctx.device).wait_stream(s)
-            for k in range(depth):
-                g = torch.cuda.CUDAGraph()
-                with torch.cuda.graph(g):
-                    eng.forward_backward(streamer.slots[k][0], streamer.slots[k][1], gscale, zero_grads=False)
-                graphs[k] = g
-            gu = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(gu):
-                opt.step()  # + bf16 shadow + grad clear
-            graphs["update"] = gu
+        streamer = DeviceStreamer(pool, ctx.device, depth=3)
+        # one captured step per ring slot (the graph reads that slot's buffers)
+        run = StepRunner(eng, opt, ctx, gscale, lambda k: tuple(streamer.slots[k][:2]), graph=graph,
+                         comm_in_graph=not args.eager_comm)
 
         def step():
-            xb, yb = streamer.next()
-            if graphs:
-                graphs[streamer.last_slot].replay()
-                ctx.all_reduce_sum_(eng.grads)
-                graphs["update"].replay()
-            else:
-                eng.forward_backward(xb, yb, gscale, zero_grads=False)
-                ctx.all_reduce_sum_(eng.grads)
-                opt.step()
+            streamer.next()
+            run.run(streamer.last_slot)
     else:
         x, y = synth_tabular_batch(B, F, seed=ctx.rank)
         x, y = x.to(ctx.device), y.to(ctx.device)
-
-        def compute():
-            eng.forward_backward(x, y, gscale, zero_grads=False)
-
-        def update():
-            opt.step()  # + bf16 shadow + grad clear
-
-        step = _graph_step(ctx, eng, compute, update, args.no_graph)
-
+        run = StepRunner(eng, opt, ctx, gscale, lambda k: (x, y), graph=graph, comm_in_graph=not args.eager_comm)
+        step = run.run
     el = _timed(ctx, step, args.steps, args.warmup)
-    return el, B, model, eng.loss_sum.item() / B
+    return el, B, model, float(eng.loss_sum.item()) / B, run, eng, {}
 
 
 def main() -> int:
@@ -252,12 +219,16 @@ def main() -> int:
     ap.add_argument("--fwd-variant", type=int, default=None)
     ap.add_argument("--bwd-variant", type=int, default=None)
     ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--eager-comm", action="store_true", help="all-reduce between two graphs, not captured")
     ap.add_argument("--stream-fp32", action="store_true", help="mlp_online: stream fp32 features")
     ap.add_argument("--device", choices=["auto", "cpu"], default="auto",
                     help="cpu: rehearse the launch/timing/JSON contract on the fp32 reference over gloo")
     args = ap.parse_args()
     if args.batch is None:
         args.batch = DEFAULT_BATCH[args.model]
+
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        return _spawn_ranks(args.gpus, sys.argv[1:])
 
     import torch
 
@@ -269,16 +240,28 @@ def main() -> int:
         return 2
     ctx = DistContext.from_env(device="cpu" if args.device == "cpu" else None)
     cpu = ctx.device.type == "cpu"
-    if ctx.world_size != args.gpus and ctx.is_main:
-        print(f"warning: --gpus {args.gpus} but WORLD_SIZE={ctx.world_size}", file=sys.stderr)
+    if ctx.world_size != args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={ctx.world_size}", file=sys.stderr)
+        ctx.shutdown()
+        return 2
     torch.manual_seed(1234 + ctx.rank)
     if args.model == "lstm":
-        elapsed, B, model, loss = bench_lstm(args, ctx)
+        elapsed, B, model, loss, run, eng, extra = bench_lstm(args, ctx)
     else:
-        elapsed, B, model, loss = bench_mlp(args, ctx, online=args.model == "mlp_online")
+        elapsed, B, model, loss, run, eng, extra = bench_mlp(args, ctx, online=args.model == "mlp_online")
+    comm = _comm_ms(ctx, eng.grads)
 
     W = ctx.world_size
     if ctx.is_main:
+        import torch.distributed as dist
+
+        rccl = None
+        if not cpu:
+            try:
+                v = torch.cuda.nccl.version()
+                rccl = ".".join(map(str, v)) if isinstance(v, tuple) else str(v)
+            except Exception:  # noqa: BLE001 - version probe only
+                rccl = None
         rec = {
             "metric": METRIC if args.model == "lstm" else f"rows/sec (whole node), {args.model} regression training",
             "value": round(B * W * args.steps / elapsed, 1),
@@ -300,7 +283,15 @@ def main() -> int:
                 "seq_len": args.seq if args.model == "lstm" else 1,
                 "parallelism": f"dp{W}",
             },
+            "world_size": dist.get_world_size() if dist.is_initialized() else 1,
+            "backend": ctx.backend or ("none" if W == 1 else None),
+            "rccl_version": rccl,
+            "comm_ms": None if comm is None else round(comm, 4),
+            "grad_bucket_mb": round(eng.grads.numel() * 4 / 2**20, 3),
+            "step_graph": bool(run.graphs),
+            "comm_in_graph": bool(run.captured_comm),
             "final_train_loss": round(loss, 6),
+            **extra,
         }
         print(json.dumps(rec), flush=True)
     ctx.shutdown()

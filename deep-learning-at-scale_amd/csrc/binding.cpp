@@ -9,6 +9,7 @@
 
 #include <cstdlib>
 #include <map>
+#include <type_traits>
 #include <mutex>
 #include <vector>
 
@@ -64,7 +65,7 @@ void gemm(const at::Tensor& A, bool a_mn, int64_t lda, const at::Tensor& B, bool
           c10::optional<at::Tensor> outH, int64_t ldo, c10::optional<at::Tensor> bias,
           c10::optional<at::Tensor> mask, int64_t ldm, double mask_scale,
           c10::optional<at::Tensor> colsum, double alpha, double beta, int64_t act, bool atomic,
-          double drop_p, int64_t seed, int64_t big_tile) {
+          double drop_p, int64_t seed, int64_t big_tile, c10::optional<at::Tensor> seed_dev) {
   check_t(A, at::kBFloat16, "A");
   check_t(B, at::kBFloat16, "B");
   TORCH_CHECK(M > 0 && N > 0 && K > 0, "gemm: empty problem");
@@ -96,6 +97,11 @@ void gemm(const at::Tensor& A, bool a_mn, int64_t lda, const at::Tensor& B, bool
   e.atomic = atomic ? 1 : 0;
   e.drop_p = (float)drop_p;
   e.seed = (unsigned long long)seed;
+  if (seed_dev.has_value() && seed_dev->defined()) {
+    TORCH_CHECK(seed_dev->is_cuda() && seed_dev->scalar_type() == at::kLong && seed_dev->numel() >= 1,
+                "gemm: seed_dev must be a GPU int64 tensor");
+    e.seed_dev = reinterpret_cast<const long long*>(seed_dev->data_ptr<int64_t>());
+  }
   e.big_tile = (int)big_tile;
   TORCH_CHECK(ksplit == 1 || atomic, "gemm: split-K needs atomic accumulation");
   e.stage_ok = (e.outH != nullptr && e.outF == nullptr && !atomic && beta == 0.0 && N % 8 == 0 &&
@@ -127,6 +133,8 @@ wf::LstmDims lstm_dims(int64_t B, int64_t T, int64_t F, int64_t KX, int64_t H) {
   d.nt = (nt != nullptr && nt[0] == '0') ? 0 : 1;
   const char* pd = std::getenv("WELLFLOW_PF_DBG");
   d.dbg = pd != nullptr ? std::atoi(pd) : 0;
+  const char* sl = std::getenv("WELLFLOW_SPIN_LIMIT");  // tests: force the hand-off timeout path
+  d.spin_limit = sl != nullptr ? (unsigned)std::strtoul(sl, nullptr, 10) : 0u;
   return d;
 }
 
@@ -166,9 +174,15 @@ void lstm_forward(const at::Tensor& XH, const at::Tensor& Wp, const at::Tensor& 
   for (int t = 0; t < d.T; ++t) wf::launch_lstm_fwd_step(t, bfp(XH), bfp(Wp), fp(Cst), bfp(S), d, s);
 }
 
-// All T steps in one cooperative launch (lstm_persistent.hip). Returns false (nothing
-// launched) when the shape or device cannot host it; `sync` (int32) word 0 reports a
-// spin timeout after the launch completes.
+// Raise on a failed persistent launch (status < 0: -(hipError_t)); 0 = not supported.
+bool persistent_status(int st, const char* what) {
+  TORCH_CHECK(st >= 0, what, ": launch failed: ", hipGetErrorString((hipError_t)(-st)));
+  return st == 1;
+}
+
+// All T steps in one persistent launch per sub-batch (lstm_persistent.hip). Returns false
+// (nothing launched) when the shape or device cannot host it and raises when the launch
+// fails; `sync` (int32) word 0 is the sticky spin-timeout flag.
 bool lstm_forward_persistent(const at::Tensor& XH, const at::Tensor& Wp, const at::Tensor& Cst,
                              const at::Tensor& S, const at::Tensor& sync, int64_t B, int64_t T, int64_t F,
                              int64_t KX, int64_t H) {
@@ -178,9 +192,10 @@ bool lstm_forward_persistent(const at::Tensor& XH, const at::Tensor& Wp, const a
   check_extent(Wp, 4 * H * (KX + H), "Wp");
   check_t(sync, at::kInt, "sync");
   const c10::hip::OptionalHIPGuardMasqueradingAsCUDA guard(XH.device());
-  return wf::launch_lstm_fwd_persistent(bfp(XH), bfp(Wp), fp(Cst), bfp(S),
-                                        reinterpret_cast<unsigned*>(sync.data_ptr<int>()), sync.numel(), d,
-                                        cur_stream());
+  return persistent_status(wf::launch_lstm_fwd_persistent(bfp(XH), bfp(Wp), fp(Cst), bfp(S),
+                                                          reinterpret_cast<unsigned*>(sync.data_ptr<int>()),
+                                                          sync.numel(), d, cur_stream()),
+                           "persistent LSTM forward");
 }
 
 void lstm_backward(const at::Tensor& WhhT, const at::Tensor& XH, const at::Tensor& Cst,
@@ -206,9 +221,10 @@ void lstm_backward(const at::Tensor& WhhT, const at::Tensor& XH, const at::Tenso
     check_t(*sync, at::kInt, "sync");
     wf::launch_lstm_bwd_step(d.T - 1, bfp(WhhT), fp(Cst), bfp(S), bfp(DG), fp(dcarry), fp(dy),
                              fp(w_out), d, s);
-    TORCH_CHECK(wf::launch_lstm_bwd_persistent(bfp(WhhT), fp(Cst), bfp(S), bfp(DG), fp(dcarry),
-                                               reinterpret_cast<unsigned*>(sync->data_ptr<int>()),
-                                               sync->numel(), d, s),
+    TORCH_CHECK(persistent_status(wf::launch_lstm_bwd_persistent(bfp(WhhT), fp(Cst), bfp(S), bfp(DG), fp(dcarry),
+                                                                 reinterpret_cast<unsigned*>(sync->data_ptr<int>()),
+                                                                 sync->numel(), d, s),
+                                  "persistent LSTM backward"),
                 "persistent backward refused this shape");
     return;
   }
@@ -251,7 +267,8 @@ SideStreams& side_streams(int dev, size_t nev) {
 // GEMM is cut into chunks of `chunk` timesteps, each launched on the low-priority stream
 // as soon as the chain has produced its DG slabs: compute-bound dW work fills the gaps of
 // the memory/latency-bound chain instead of running after it.
-void lstm_backward_dw(const at::Tensor& WhhT, const at::Tensor& XH, const at::Tensor& Cst,
+// Returns true when the BPTT chain ran as the persistent kernel (false: per-step kernels).
+bool lstm_backward_dw(const at::Tensor& WhhT, const at::Tensor& XH, const at::Tensor& Cst,
                       const at::Tensor& S, const at::Tensor& DG, const at::Tensor& dcarry,
                       const at::Tensor& dy, const at::Tensor& w_out, const at::Tensor& gW,
                       int64_t B, int64_t T, int64_t F, int64_t KX, int64_t H, int64_t variant,
@@ -306,16 +323,17 @@ void lstm_backward_dw(const at::Tensor& WhhT, const at::Tensor& XH, const at::Te
     bool done = false;
     if (sync.has_value()) {
       check_t(*sync, at::kInt, "sync");
-      done = wf::launch_lstm_bwd_persistent(bfp(WhhT), fp(Cst), bfp(S), bfp(DG), fp(dcarry),
-                                            reinterpret_cast<unsigned*>(sync->data_ptr<int>()),
-                                            sync->numel(), d, main);
+      done = persistent_status(wf::launch_lstm_bwd_persistent(bfp(WhhT), fp(Cst), bfp(S), bfp(DG), fp(dcarry),
+                                                              reinterpret_cast<unsigned*>(sync->data_ptr<int>()),
+                                                              sync->numel(), d, main),
+                               "persistent LSTM backward");
     }
     if (!done)
       for (int t = d.T - 2; t >= 0; --t)
         wf::launch_lstm_bwd_step(t, bfp(WhhT), fp(Cst), bfp(S), bfp(DG), fp(dcarry), fp(dy),
                                  fp(w_out), d, main);
     dw(0, d.T, main);
-    return;
+    return done;
   }
   const int nchunks = (int)((T + chunk - 1) / chunk);
   SideStreams& ss = side_streams(XH.device().index(), nchunks + 3);
@@ -338,6 +356,7 @@ void lstm_backward_dw(const at::Tensor& WhhT, const at::Tensor& XH, const at::Te
   TORCH_CHECK(hipEventRecord(ss.ev[2], ss.lo) == hipSuccess, "event record");
   TORCH_CHECK(hipStreamWaitEvent(main, ss.ev[1], 0) == hipSuccess, "join");
   TORCH_CHECK(hipStreamWaitEvent(main, ss.ev[2], 0) == hipSuccess, "join");
+  return false;
 }
 
 void lstm_pack_weights(const at::Tensor& W, const at::Tensor& Wp, const at::Tensor& WhhT,
@@ -553,6 +572,20 @@ void sgd(const at::Tensor& p, const at::Tensor& g, const at::Tensor& vel, double
                  (float)gscale, cur_stream());
 }
 
+void sgd_dev(const at::Tensor& p, const at::Tensor& g, const at::Tensor& vel, const at::Tensor& step, double lr,
+             double decay, double momentum, bool nesterov, double gscale, bool zero_g) {
+  check_t(p, at::kFloat, "p");
+  check_t(g, at::kFloat, "g");
+  check_t(vel, at::kFloat, "vel");
+  check_t(step, at::kFloat, "step");
+  check_extent(step, 2, "step");  // [0] = iterations, [1] = completion ticket
+  const int64_t n = p.numel();
+  TORCH_CHECK(g.numel() == n && vel.numel() == n, "sgd: size mismatch");
+  const c10::hip::OptionalHIPGuardMasqueradingAsCUDA guard(p.device());
+  wf::launch_sgd_dev(fp(p), fp(g), fp(vel), n, fp(step), (float)lr, (float)decay, (float)momentum, nesterov ? 1 : 0,
+                     (float)gscale, zero_g ? 1 : 0, cur_stream());
+}
+
 void cast_bf16(const at::Tensor& src, const at::Tensor& dst) {
   check_t(src, at::kFloat, "src");
   check_t(dst, at::kBFloat16, "dst");
@@ -587,27 +620,53 @@ void im2col1d(const at::Tensor& x, int64_t B, int64_t L, int64_t Cin, int64_t ks
                       cur_stream());
 }
 
+// Every binding runs behind this wrapper: a kernel launch that the runtime rejected (bad grid,
+// missing code object, invalid resource) raises here instead of failing silently.
+template <auto F>
+struct Checked;
+template <class R, class... A, R (*F)(A...)>
+struct Checked<F> {
+  static R call(A... a) {
+    (void)hipGetLastError();  // errors of earlier, foreign launches are not ours to report
+    if constexpr (std::is_void_v<R>) {
+      F(a...);
+      check();
+    } else {
+      R r = F(a...);
+      check();
+      return r;
+    }
+  }
+  static void check() {
+    const hipError_t e = hipGetLastError();
+    TORCH_CHECK(e == hipSuccess, "wellflow kernel launch failed: ", hipGetErrorString(e));
+  }
+};
+
 }  // namespace
+
+#define WF_DEF(name) m.def(#name, &Checked<&name>::call)
 
 PYBIND11_MODULE(_C, m) {
   m.doc() = "wellflow HIP kernel library (gfx950)";
-  m.def("gemm", &gemm);
-  m.def("mlp2_forward", &mlp2_forward);
-  m.def("mlp2_backward", &mlp2_backward);
-  m.def("lstm_pack_x", &lstm_pack_x);
-  m.def("lstm_forward", &lstm_forward);
-  m.def("lstm_forward_persistent", &lstm_forward_persistent);
-  m.def("lstm_backward", &lstm_backward);
-  m.def("lstm_backward_dw", &lstm_backward_dw);
-  m.def("lstm_pack_weights", &lstm_pack_weights);
-  m.def("head_fwd", &head_fwd);
-  m.def("head_bwd_w", &head_bwd_w);
-  m.def("head_bwd_x", &head_bwd_x);
-  m.def("loss", &loss);
-  m.def("adam", &adam);
-  m.def("adam_dev", &adam_dev);
-  m.def("sgd", &sgd);
-  m.def("cast_bf16", &cast_bf16);
-  m.def("transpose_cast_bf16", &transpose_cast_bf16);
-  m.def("im2col1d", &im2col1d);
+  WF_DEF(gemm);
+  WF_DEF(mlp2_forward);
+  WF_DEF(mlp2_backward);
+  WF_DEF(lstm_pack_x);
+  WF_DEF(lstm_forward);
+  WF_DEF(lstm_forward_persistent);
+  WF_DEF(lstm_backward);
+  WF_DEF(lstm_backward_dw);
+  WF_DEF(lstm_pack_weights);
+  WF_DEF(head_fwd);
+  WF_DEF(head_bwd_w);
+  WF_DEF(head_bwd_x);
+  WF_DEF(loss);
+  WF_DEF(adam);
+  WF_DEF(adam_dev);
+  WF_DEF(sgd);
+  WF_DEF(sgd_dev);
+  WF_DEF(cast_bf16);
+  WF_DEF(transpose_cast_bf16);
+  WF_DEF(im2col1d);
 }

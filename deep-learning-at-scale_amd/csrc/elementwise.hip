@@ -388,6 +388,42 @@ void launch_sgd(float* p, const float* g, float* vel, long n, float lr, float mo
                      nesterov, gscale);
 }
 
+// Graph-capturable Keras-0.x SGD: the iteration counter lives on the device (step[0];
+// step[1] is the completion ticket, as in adam_dev_kernel), so lr_t = lr / (1 + decay * it)
+// advances on every hipGraph replay instead of being baked in at capture time.
+__global__ __launch_bounds__(256) void sgd_dev_kernel(float* __restrict__ p, float* __restrict__ g,
+                                                      float* __restrict__ vel, long n, float* __restrict__ step,
+                                                      float lr, float decay, float momentum, int nesterov,
+                                                      float gscale, int zero_g) {
+  const float it = step[0];
+  const float lr_t = lr / (1.f + decay * it);
+  const long stride = (long)gridDim.x * blockDim.x;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += stride) {
+    const float gi = g[i] * gscale;
+    const float v = momentum * vel[i] - lr_t * gi;
+    vel[i] = v;
+    p[i] += nesterov ? (momentum * v - lr_t * gi) : v;
+    if (zero_g) g[i] = 0.f;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    unsigned* ticket = reinterpret_cast<unsigned*>(step + 1);
+    if (atomicAdd(ticket, 1u) == gridDim.x - 1) {
+      step[0] = it + 1.f;
+      *ticket = 0u;
+    }
+  }
+}
+
+void launch_sgd_dev(float* p, float* g, float* vel, long n, float* step, float lr, float decay, float momentum,
+                    int nesterov, float gscale, int zero_g, hipStream_t s) {
+  long b = (n + 255) / 256;
+  if (b > 2048) b = 2048;
+  if (b < 1) b = 1;
+  hipLaunchKernelGGL(sgd_dev_kernel, dim3((int)b), dim3(256), 0, s, p, g, vel, n, step, lr, decay, momentum,
+                     nesterov, gscale, zero_g);
+}
+
 // ---------------------------------------------------------------- casts
 __global__ void cast_bf16_kernel(const float* __restrict__ src, bf16_t* __restrict__ dst, long n) {
   const long stride = (long)gridDim.x * blockDim.x;

@@ -13,6 +13,12 @@
 
 namespace wf {
 
+// dropout stream of this launch: the host seed, mixed with the device step counter when one
+// is given (so a hipGraph replay draws a fresh mask every step)
+__device__ __forceinline__ unsigned long long drop_seed(const GemmEpilogue& e) {
+  return e.seed_dev != nullptr ? e.seed ^ ((unsigned long long)e.seed_dev[0] * 0xD1B54A32D192ED03ull) : e.seed;
+}
+
 // STAGES >= 2: direct-to-LDS ring; the host only selects it when every K chunk is a
 // multiple of 64 and the whole-tile over-read past M / N stays inside the operand
 // allocations (binding.cpp computes that from the tensor sizes); results outside M x N
@@ -78,7 +84,7 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_kernel(const bf16_t* __rest
           float v = e.alpha * acc[i][j][r] + bn;
           if (e.act == 1) v = fmaxf(v, 0.f);
           if (e.drop_p > 0.f)
-            v = uniform_hash(e.seed, (unsigned long long)m * N + n) >= e.drop_p
+            v = uniform_hash(drop_seed(e), (unsigned long long)m * N + n) >= e.drop_p
                     ? v * (1.f / (1.f - e.drop_p)) : 0.f;
           if (e.mask != nullptr) v = bf2f(mt[lo]) > 0.f ? v * e.mask_scale : 0.f;
           const bf16_t vb = f2bf(v);
@@ -125,7 +131,7 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_kernel(const bf16_t* __rest
         v += bn;
         if (e.act == 1) v = fmaxf(v, 0.f);
         if (e.drop_p > 0.f)
-          v = uniform_hash(e.seed, (unsigned long long)m * N + n) >= e.drop_p
+          v = uniform_hash(drop_seed(e), (unsigned long long)m * N + n) >= e.drop_p
                   ? v * (1.f / (1.f - e.drop_p)) : 0.f;
         if (e.mask != nullptr)
           v = bf2f(e.mask[(size_t)m * e.ldm + n]) > 0.f ? v * e.mask_scale : 0.f;

@@ -22,6 +22,7 @@ struct GemmEpilogue {
   int atomic = 0;                // split-K: atomicAdd alpha*acc into outF
   float drop_p = 0.f;            // inverted dropout after the activation
   unsigned long long seed = 0;
+  const long long* seed_dev = nullptr;  // optional device step counter mixed into the seed (graph replays)
   int stage_ok = 0;              // host-verified: bf16 output/mask tiles may go through LDS
   int big_tile = 0;              // MN x MN split-K weight gradient: 1 = 256x128 8-wave tile, 2 = 128x288
 };
@@ -39,20 +40,24 @@ struct LstmDims {
   int nt = 1;           // non-temporal hints on the read-once/write-once state streams
   int dbg = 0;          // persistent-forward diagnostics (WELLFLOW_PF_DBG): 1 = skip the
                         // hand-off wait (timing only: results are wrong)
+  int row_off = 0;      // persistent kernels: first batch row of this sub-batch launch
+  unsigned spin_limit = 0;  // persistent hand-off spin bound (0 = built-in; tests shrink it)
 };
 void launch_lstm_pack_x(const float* x, bf16_t* XH, LstmDims d, hipStream_t s);
 void launch_lstm_fwd_step(int t, bf16_t* XH, const bf16_t* Wp, float* Cst, bf16_t* S,
                           LstmDims d, hipStream_t s);
-// All T forward steps in ONE cooperative launch (lstm_persistent.hip). `sync` must hold
-// lstm_persistent_sync_words(B / (64 * NC)) words (<= 16 + 16 * B / 64 always suffices);
-// word 0 reports a spin timeout. Returns false when the shape / device cannot host it.
+// All T forward steps in ONE persistent launch per sub-batch (lstm_persistent.hip). `sync`
+// must hold lstm_persistent_sync_words(row blocks) words (<= 16 + 16 * B / 32 always
+// suffices); word 0 is the STICKY spin-timeout flag (never cleared by a launch), word 1 the
+// current launch's. Returns 1 launched, 0 shape / device cannot host it (nothing launched),
+// < 0 = -(hipError_t) of a failed launch.
 int lstm_persistent_sync_words(int row_blocks);
-bool launch_lstm_fwd_persistent(bf16_t* XH, const bf16_t* Wp, float* Cst, bf16_t* S, unsigned* sync,
+int launch_lstm_fwd_persistent(bf16_t* XH, const bf16_t* Wp, float* Cst, bf16_t* S, unsigned* sync,
                                 long sync_words, LstmDims d, hipStream_t s);
-// Backward steps T-2 .. 0 in ONE cooperative launch (lstm_persistent_bwd.hip), after step
-// T-1 ran (launch_lstm_bwd_step(T-1, ...)). Same `sync` contract as the forward (word 0 =
-// spin timeout). Returns false (nothing launched) when the shape / device cannot host it.
-bool launch_lstm_bwd_persistent(const bf16_t* WhhT, const float* Cst, const bf16_t* S, bf16_t* DG,
+// Backward steps T-2 .. 0 in ONE persistent launch per sub-batch (lstm_persistent_bwd.hip),
+// after step T-1 ran (launch_lstm_bwd_step(T-1, ...)). Same `sync` contract and return
+// codes as the forward.
+int launch_lstm_bwd_persistent(const bf16_t* WhhT, const float* Cst, const bf16_t* S, bf16_t* DG,
                                 const float* dcarry, unsigned* sync, long sync_words, LstmDims d,
                                 hipStream_t s);
 void launch_lstm_bwd_step(int t, const bf16_t* WhhT, const float* Cst, const bf16_t* S,
@@ -101,6 +106,8 @@ void launch_adam_dev(float* p, float* g, float* m, float* v, long n, float* step
                      hipStream_t s);
 void launch_sgd(float* p, const float* g, float* vel, long n, float lr, float momentum,
                 int nesterov, float gscale, hipStream_t s);
+void launch_sgd_dev(float* p, float* g, float* vel, long n, float* step, float lr, float decay, float momentum,
+                    int nesterov, float gscale, int zero_g, hipStream_t s);
 void launch_cast_bf16(const float* src, bf16_t* dst, long n, hipStream_t s);
 void launch_transpose_cast_bf16(const float* src, long lds, int rows, int cols, bf16_t* dst,
                                 long ldd, hipStream_t s);

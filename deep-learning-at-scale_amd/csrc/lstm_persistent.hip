@@ -6,7 +6,7 @@
 // Infinity Cache every step (576 KB per CU per step with the activations) and pays a grid
 // fill/drain per step. Here the weights never move after the prologue:
 //  * grid = (B / (64*NC)) row blocks x (4H / 256) gate-column blocks, one 256-thread
-//    workgroup (4 waves, one per SIMD) per CU, all co-resident (cooperative launch).
+//    workgroup (4 waves, one per SIMD) per CU, all co-resident (persistent_launch.h).
 //  * wave w of column block n keeps Wp[gate cols n*256 + 64w .. +63][0:KA] — the four
 //    gates of 16 hidden units (see the permutation in lstm.hip) — as MFMA B fragments in
 //    registers for the whole sequence: KA/32 x 4 bf16x8 = 288 VGPRs at KA = 576.
@@ -28,6 +28,7 @@
 #include "gemm_core.h"
 #include "kernels.h"
 #include "lstm_layout.h"
+#include "persistent_launch.h"
 
 namespace wf {
 
@@ -38,7 +39,10 @@ typedef __attribute__((address_space(1))) unsigned gu32;
 typedef __attribute__((address_space(1))) unsigned long long gu64;
 }  // namespace
 
-// sync words (uint32): [0] error code (0 ok, 1 spin timeout), [16 + 16*m] arrivals of row block m.
+// sync words (uint32): [0] STICKY error (bit 0: a spin bound tripped in some launch; never
+// cleared by a launch, read and reset by the host), [1] error of the current launch (all
+// workgroups drain when it is set), [16 + 16*m] arrivals of row block m. A launch resets
+// words 1.. only, so a timeout in any earlier step stays visible (NativeLSTM.check_device_errors).
 int lstm_persistent_sync_words(int row_blocks) { return 16 + 16 * row_blocks; }
 
 // KT = KA / 32 k-tiles; NC = 32-row chunks per workgroup per step (compile-time, so every
@@ -76,14 +80,16 @@ __global__ __launch_bounds__(256, 1) void lstm_fwd_persistent_kernel(
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int L = xcd_remap(blockIdx.x, gridDim.x);
   const int m = L / NB, n = L % NB;
-  const int row0 = m * PF_ROWS * NC;
+  const int row0 = m * PF_ROWS * NC + d.row_off;  // row_off: sub-batch origin (launcher)
   const int ub = n * 4 + wid;                // 16-unit block of this wave
   const int u = ub * 16 + l15;               // hidden unit of this lane
   const int loff_c = ub * 256 + lane * 4;    // float offset of this lane's C slot in a FN row block
   const int loff_s = ub * 1024 + lane * 16;  // bf16 offset of this lane's S slot in a FN row block
   const int loff_h = (((int)threadIdx.x >> 3) * KA + ((int)threadIdx.x & 7) * 8) * 2;  // h publish
-  gu32* err = (gu32*)(sync);
+  gu32* err = (gu32*)(sync + 1);
+  gu32* sticky = (gu32*)(sync);
   gu32* cnt = (gu32*)(sync + 16 + 16 * m);
+  const unsigned spin_limit = d.spin_limit ? d.spin_limit : PF_SPIN_LIMIT;
   // XH as a buffer resource for the 16-B sc1 h stores (byte offsets < 2^31: checked on the host)
   const __amdgpu_buffer_rsrc_t xh_rsrc = __builtin_amdgcn_make_buffer_rsrc(XH, 0, 0x7FFFFFFF, 0x00020000);
   // DBG & 16: timeline stamps (s_memrealtime, 100 MHz) of step PF_STAMP_T, wave 0 lane 0 of
@@ -150,8 +156,9 @@ __global__ __launch_bounds__(256, 1) void lstm_fwd_persistent_kernel(
             ok = 0;
             break;
           }
-          if (++spins > PF_SPIN_LIMIT) {
+          if (++spins > spin_limit) {
             __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_fetch_or(sticky, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             ok = 0;
             break;
           }
@@ -402,8 +409,8 @@ __global__ __launch_bounds__(256, 1) void lstm_fwd_persistent_kernel(
 }
 
 template <int KT, int NC>
-static bool launch_pf(bf16_t* XH, const bf16_t* Wp, float* Cst, bf16_t* S, unsigned* sync, int grid,
-                      LstmDims d, hipStream_t s) {
+static int launch_pf(bf16_t* XH, const bf16_t* Wp, float* Cst, bf16_t* S, unsigned* sync, int grid,
+                     LstmDims d, hipStream_t s) {
   const void* f = reinterpret_cast<const void*>(&lstm_fwd_persistent_kernel<KT, NC>);
   if constexpr (KT == 18 && NC == 8) {  // timing-only diagnostic builds (WELLFLOW_PF_DBG >= 2)
     if (d.dbg == 2) f = reinterpret_cast<const void*>(&lstm_fwd_persistent_kernel<KT, NC, 2>);
@@ -414,65 +421,76 @@ static bool launch_pf(bf16_t* XH, const bf16_t* Wp, float* Cst, bf16_t* S, unsig
     if (d.dbg == 64) f = reinterpret_cast<const void*>(&lstm_fwd_persistent_kernel<KT, NC, 64>);  // stores inside the loop
   }
   void* args[] = {&XH, &Wp, &Cst, &S, &sync, &d};
-  // Cooperative launch: the runtime rejects a grid that cannot be co-resident. rocprofv3
-  // (ROCm 7.2) crashes at exit after tracing a cooperative dispatch, so WELLFLOW_COOP=0
-  // (profiling runs) uses a plain launch guarded by the same residency check done here.
-  static const bool coop = [] {
-    const char* v = std::getenv("WELLFLOW_COOP");
-    return v == nullptr || v[0] != '0';
-  }();
-  if (coop) return hipLaunchCooperativeKernel(f, dim3(grid), dim3(256), args, 0u, s) == hipSuccess;
-  int per_cu = 0, dev = 0, cus = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, f, 256, 0) != hipSuccess || hipGetDevice(&dev) != hipSuccess ||
-      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || per_cu * cus < grid)
-    return false;
-  return hipLaunchKernel(f, dim3(grid), dim3(256), args, 0u, s) == hipSuccess;
+  return persistent_launch(f, grid, args, s);  // persistent_launch.h: residency check + plain launch
 }
 
 template <int KT>
-static bool launch_pf_nc(int NC, bf16_t* XH, const bf16_t* Wp, float* Cst, bf16_t* S, unsigned* sync,
-                         int grid, LstmDims d, hipStream_t s) {
+static int launch_pf_nc(int NC, bf16_t* XH, const bf16_t* Wp, float* Cst, bf16_t* S, unsigned* sync,
+                        int grid, LstmDims d, hipStream_t s) {
   switch (NC) {
     case 1: return launch_pf<KT, 1>(XH, Wp, Cst, S, sync, grid, d, s);
     case 2: return launch_pf<KT, 2>(XH, Wp, Cst, S, sync, grid, d, s);
     case 4: return launch_pf<KT, 4>(XH, Wp, Cst, S, sync, grid, d, s);
     case 8: return launch_pf<KT, 8>(XH, Wp, Cst, S, sync, grid, d, s);
-    default: return false;
+    default: return 0;
   }
 }
 
-// Returns false (and launches nothing) when the shape or the device cannot host the
-// persistent schedule; the caller then runs the per-step kernels.
-bool launch_lstm_fwd_persistent(bf16_t* XH, const bf16_t* Wp, float* Cst, bf16_t* S, unsigned* sync,
-                                long sync_words, LstmDims d, hipStream_t s) {
+// Batch split for the persistent schedules: the fewest equal sub-batches (launched one after
+// the other on the stream, each a full persistent launch over its row range, d.row_off) whose
+// grid of `rows_per_unit * units` rows per workgroup fits one workgroup per CU. Returns the
+// number of sub-batches (0 = none fits) and the chosen units per workgroup.
+int persistent_split(int B, int row_quantum, int max_units, int cols, int cus, int* units_out) {
+  for (int nsub = 1; nsub <= 64; ++nsub) {
+    if (B % nsub != 0) continue;
+    const int Bs = B / nsub;
+    if (Bs % row_quantum != 0) continue;
+    for (int u = 1; u <= max_units; u *= 2) {
+      if (Bs % (row_quantum * u) == 0 && (Bs / (row_quantum * u)) * cols <= cus) {
+        *units_out = u;
+        return nsub;
+      }
+    }
+  }
+  return 0;
+}
+
+// 1 = launched, 0 = the shape or device cannot host the persistent schedule (nothing launched;
+// the caller runs the per-step kernels), < 0 = -(hipError_t) of a failed launch.
+// Batches larger than one co-resident grid run as consecutive sub-batch launches (no cap on B).
+int launch_lstm_fwd_persistent(bf16_t* XH, const bf16_t* Wp, float* Cst, bf16_t* S, unsigned* sync,
+                               long sync_words, LstmDims d, hipStream_t s) {
   const int KA = d.KX + d.H, G = 4 * d.H;
-  if ((double)(d.T + 1) * d.B * KA * 2 >= 2147483647.0) return false;  // 32-bit buffer offsets
-  if (d.KX % 64 != 0 || KA % 64 != 0 || G % 256 != 0 || d.B % PF_ROWS != 0 || d.KX != 64) return false;
+  if ((double)(d.T + 1) * d.B * KA * 2 >= 2147483647.0) return 0;  // 32-bit buffer offsets
+  if (d.KX % 64 != 0 || KA % 64 != 0 || G % 256 != 0 || d.B % PF_ROWS != 0 || d.KX != 64) return 0;
+  if (KA / 32 != 6 && KA / 32 != 10 && KA / 32 != 18) return 0;
   int dev = 0, cus = 0;
   if (hipGetDevice(&dev) != hipSuccess ||
       hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-    return false;
+    return -(int)hipErrorInvalidDevice;
   const int NB = G / 256;
-  // fewest 32-row chunks per workgroup whose grid fits one workgroup per CU
+  // fewest sub-batches, then the fewest 32-row chunks per workgroup, one workgroup per CU
   int NC = 0;
-  for (int nc = 1; nc <= 8; nc *= 2) {
-    if (d.B % (PF_ROWS * nc) == 0 && (d.B / (PF_ROWS * nc)) * NB <= cus) {
-      NC = nc;
-      break;
-    }
-  }
-  if (NC == 0) return false;
-  const int MB = d.B / (PF_ROWS * NC);
-  if (sync_words < lstm_persistent_sync_words(MB)) return false;
-  if (hipMemsetAsync(sync, 0, sizeof(unsigned) * (size_t)lstm_persistent_sync_words(MB), s) != hipSuccess)
-    return false;
+  const int nsub = persistent_split(d.B, PF_ROWS, 8, NB, cus, &NC);
+  if (nsub == 0) return 0;
+  const int Bs = d.B / nsub, MB = Bs / (PF_ROWS * NC);
+  if (sync_words < lstm_persistent_sync_words(MB)) return 0;
   const int grid = MB * NB;
-  switch (KA / 32) {
-    case 6: return launch_pf_nc<6>(NC, XH, Wp, Cst, S, sync, grid, d, s);    // H = 128
-    case 10: return launch_pf_nc<10>(NC, XH, Wp, Cst, S, sync, grid, d, s);  // H = 256
-    case 18: return launch_pf_nc<18>(NC, XH, Wp, Cst, S, sync, grid, d, s);  // H = 512
-    default: return false;
+  for (int k = 0; k < nsub; ++k) {
+    // reset this launch's error word and the arrival counters; word 0 (sticky) is kept
+    if (hipMemsetAsync(sync + 1, 0, sizeof(unsigned) * (size_t)(lstm_persistent_sync_words(MB) - 1), s) != hipSuccess)
+      return -(int)hipErrorLaunchFailure;
+    LstmDims dk = d;
+    dk.row_off = k * Bs;
+    int r = 0;
+    switch (KA / 32) {
+      case 6: r = launch_pf_nc<6>(NC, XH, Wp, Cst, S, sync, grid, dk, s); break;    // H = 128
+      case 10: r = launch_pf_nc<10>(NC, XH, Wp, Cst, S, sync, grid, dk, s); break;  // H = 256
+      case 18: r = launch_pf_nc<18>(NC, XH, Wp, Cst, S, sync, grid, dk, s); break;  // H = 512
+    }
+    if (r <= 0) return k == 0 ? r : (r < 0 ? r : -(int)hipErrorLaunchFailure);
   }
+  return 1;
 }
 
 }  // namespace wf

@@ -5,7 +5,7 @@
 // step (512 KB per 128x128 tile, 134 MB per step over the grid), and round-trips the fp32
 // dc carry through HBM (2 x 16.8 MB per step at B = 8192). Here
 //  * grid = (B / (16 * NRT)) row blocks x (H / 64) unit blocks, one 256-thread workgroup
-//    (4 waves, one per SIMD) per CU, co-resident (cooperative launch). Workgroup (m, n)
+//    (4 waves, one per SIMD) per CU, co-resident (persistent_launch.h). Workgroup (m, n)
 //    owns rows [16*NRT*m, +16*NRT) x units [64n, 64n + 64) for the whole sequence, i.e.
 //    the 256 contiguous DG columns 4u + gate of those units (dg_col order).
 //  * dh_t = DG_{t+1} W_hh is split over K by wave: wave w multiplies DG columns
@@ -24,13 +24,14 @@
 //    wave drains its stores (vmcnt(0)), workgroup barrier, ONE lane adds to the row
 //    block's arrival counter (agent scope); consumers poll relaxed with s_sleep, then ONE
 //    agent-scope acquire, then the LDS-DMA loads of DG_{t+1}. Only the H/64 workgroups of one
-//    row block depend on each other; every spin is bounded (error word 0, all drain).
+//    row block depend on each other; every spin is bounded (error words 1 and sticky 0, all drain).
 // Step T-1 (dh from the regression head) is lstm_bwd_last_kernel in lstm.hip.
 #include <cstdlib>
 
 #include "gemm_core.h"
 #include "kernels.h"
 #include "lstm_layout.h"
+#include "persistent_launch.h"
 
 namespace wf {
 
@@ -70,11 +71,13 @@ __global__ __launch_bounds__(256, 1) void lstm_bwd_persistent_kernel(
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int L = xcd_remap(blockIdx.x, gridDim.x);
   const int m = L / NB, n = L % NB;
-  const int row0 = m * 16 * NRT;
+  const int row0 = m * 16 * NRT + d.row_off;  // row_off: sub-batch origin (launcher)
   const int ue = n * 64 + wid * 16 + l15;  // unit of this lane's cell backward
   const bool even = (l15 & 1) == 0;
-  gu32* err = (gu32*)(sync);
+  gu32* err = (gu32*)(sync + 1);  // this launch's error; sync[0] is the sticky one (lstm_persistent.hip)
+  gu32* sticky = (gu32*)(sync);
   gu32* cnt = (gu32*)(sync + 16 + 16 * m);
+  const unsigned spin_limit = d.spin_limit ? d.spin_limit : PB_SPIN_LIMIT;
   constexpr int PB_STAMP_S = 10;
   unsigned long long* stamps = reinterpret_cast<unsigned long long*>(sync + 4096) + blockIdx.x * 128;
   auto stamp = [&](int s, int slot) {
@@ -171,8 +174,9 @@ __global__ __launch_bounds__(256, 1) void lstm_bwd_persistent_kernel(
             ok = 0;
             break;
           }
-          if (++spins > PB_SPIN_LIMIT) {
+          if (++spins > spin_limit) {
             __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_fetch_or(sticky, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             ok = 0;
             break;
           }
@@ -432,7 +436,7 @@ __global__ __launch_bounds__(256, 1) void lstm_bwd_persistent_kernel(
 }
 
 template <int KT, int NRT>
-static bool launch_pb(const bf16_t* WhhT, const float* Cst, const bf16_t* S, bf16_t* DG, const float* dcarry,
+static int launch_pb(const bf16_t* WhhT, const float* Cst, const bf16_t* S, bf16_t* DG, const float* dcarry,
                       unsigned* sync, int grid, LstmDims d, hipStream_t s) {
   const void* f = reinterpret_cast<const void*>(&lstm_bwd_persistent_kernel<KT, NRT>);
   if constexpr (KT == 16 && NRT == 16) {  // timing-only diagnostic builds (WELLFLOW_PF_DBG)
@@ -451,63 +455,61 @@ static bool launch_pb(const bf16_t* WhhT, const float* Cst, const bf16_t* S, bf1
     }
   }
   void* args[] = {&WhhT, &Cst, &S, &DG, &dcarry, &sync, &d};
-  static const bool coop = [] {
-    const char* v = std::getenv("WELLFLOW_COOP");
-    return v == nullptr || v[0] != '0';
-  }();
-  if (coop) return hipLaunchCooperativeKernel(f, dim3(grid), dim3(256), args, 0u, s) == hipSuccess;
-  int per_cu = 0, dev = 0, cus = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, f, 256, 0) != hipSuccess || hipGetDevice(&dev) != hipSuccess ||
-      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || per_cu * cus < grid)
-    return false;
-  return hipLaunchKernel(f, dim3(grid), dim3(256), args, 0u, s) == hipSuccess;
+  return persistent_launch(f, grid, args, s);  // persistent_launch.h
 }
 
 template <int KT>
-static bool launch_pb_nrt(int NRT, const bf16_t* WhhT, const float* Cst, const bf16_t* S, bf16_t* DG,
+static int launch_pb_nrt(int NRT, const bf16_t* WhhT, const float* Cst, const bf16_t* S, bf16_t* DG,
                           const float* dcarry, unsigned* sync, int grid, LstmDims d, hipStream_t s) {
   switch (NRT) {
     case 4: return launch_pb<KT, 4>(WhhT, Cst, S, DG, dcarry, sync, grid, d, s);
     case 8: return launch_pb<KT, 8>(WhhT, Cst, S, DG, dcarry, sync, grid, d, s);
     case 16: return launch_pb<KT, 16>(WhhT, Cst, S, DG, dcarry, sync, grid, d, s);
-    default: return false;
+    default: return 0;
   }
 }
 
-// Steps T-2 .. 0 of the backward in one launch (step T-1 must already be done: DG[T-1] and
-// the dc carry written by lstm_bwd_last_kernel). Returns false (nothing launched) when the
-// shape / device cannot host the persistent schedule; the caller runs the per-step kernels.
-bool launch_lstm_bwd_persistent(const bf16_t* WhhT, const float* Cst, const bf16_t* S, bf16_t* DG,
-                                const float* dcarry, unsigned* sync, long sync_words, LstmDims d,
-                                hipStream_t s) {
-  if (d.T < 2) return true;  // nothing after the last step
+int persistent_split(int B, int row_quantum, int max_units, int cols, int cus, int* units_out);  // lstm_persistent.hip
+
+// Steps T-2 .. 0 of the backward in one launch per sub-batch (step T-1 must already be done:
+// DG[T-1] and the dc carry written by lstm_bwd_last_kernel). 1 = launched, 0 = the shape /
+// device cannot host the persistent schedule (nothing launched; the caller runs the per-step
+// kernels), < 0 = -(hipError_t) of a failed launch.
+int launch_lstm_bwd_persistent(const bf16_t* WhhT, const float* Cst, const bf16_t* S, bf16_t* DG,
+                               const float* dcarry, unsigned* sync, long sync_words, LstmDims d,
+                               hipStream_t s) {
+  if (d.T < 2) return 1;  // nothing after the last step
   const int G = 4 * d.H;
-  if (d.H % 64 != 0 || d.B % 16 != 0) return false;
-  if ((double)d.B * G * 2 >= 2147483647.0) return false;  // 32-bit buffer offsets per step
+  if (d.H % 64 != 0 || d.B % 64 != 0) return 0;
+  if (d.H != 128 && d.H != 256 && d.H != 512) return 0;
+  if ((double)d.B * G * 2 >= 2147483647.0) return 0;  // 32-bit buffer offsets per step
   int dev = 0, cus = 0;
   if (hipGetDevice(&dev) != hipSuccess ||
       hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-    return false;
-  const int NB = d.H / 64, tiles = d.B / 16;
-  int NRT = 0;  // fewest row tiles per workgroup whose grid fits one workgroup per CU
-  for (int nrt = 4; nrt <= PB_MAX_RT; nrt *= 2) {  // multiple of 4: the row-tile loop is unrolled by 4
-    if (tiles % nrt == 0 && (tiles / nrt) * NB <= cus) {
-      NRT = nrt;
-      break;
-    }
-  }
-  if (NRT == 0) return false;
-  const int MB = tiles / NRT;
-  if (sync_words < lstm_persistent_sync_words(MB)) return false;
-  if (hipMemsetAsync(sync, 0, sizeof(unsigned) * (size_t)lstm_persistent_sync_words(MB), s) != hipSuccess)
-    return false;
+    return -(int)hipErrorInvalidDevice;
+  const int NB = d.H / 64;
+  // fewest sub-batches, then the fewest row tiles per workgroup (a multiple of 4: the row-tile
+  // loop is unrolled by 4; at most PB_MAX_RT: the dc carry lives in registers), one WG per CU
+  int u = 0;
+  const int nsub = persistent_split(d.B, 64, PB_MAX_RT / 4, NB, cus, &u);
+  if (nsub == 0) return 0;
+  const int NRT = 4 * u, Bs = d.B / nsub, MB = Bs / (16 * NRT);
+  if (sync_words < lstm_persistent_sync_words(MB)) return 0;
   const int grid = MB * NB;
-  switch (d.H) {
-    case 128: return launch_pb_nrt<4>(NRT, WhhT, Cst, S, DG, dcarry, sync, grid, d, s);
-    case 256: return launch_pb_nrt<8>(NRT, WhhT, Cst, S, DG, dcarry, sync, grid, d, s);
-    case 512: return launch_pb_nrt<16>(NRT, WhhT, Cst, S, DG, dcarry, sync, grid, d, s);
-    default: return false;
+  for (int k = 0; k < nsub; ++k) {
+    if (hipMemsetAsync(sync + 1, 0, sizeof(unsigned) * (size_t)(lstm_persistent_sync_words(MB) - 1), s) != hipSuccess)
+      return -(int)hipErrorLaunchFailure;  // word 0 (sticky error) is kept
+    LstmDims dk = d;
+    dk.row_off = k * Bs;
+    int r = 0;
+    switch (d.H) {
+      case 128: r = launch_pb_nrt<4>(NRT, WhhT, Cst, S, DG, dcarry, sync, grid, dk, s); break;
+      case 256: r = launch_pb_nrt<8>(NRT, WhhT, Cst, S, DG, dcarry, sync, grid, dk, s); break;
+      case 512: r = launch_pb_nrt<16>(NRT, WhhT, Cst, S, DG, dcarry, sync, grid, dk, s); break;
+    }
+    if (r <= 0) return k == 0 ? r : (r < 0 ? r : -(int)hipErrorLaunchFailure);
   }
+  return 1;
 }
 
 }  // namespace wf

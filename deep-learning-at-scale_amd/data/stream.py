@@ -4,10 +4,16 @@
 a dedicated copy stream: batch k+1 (and k+2 ...) is in flight over PCIe while the compute
 stream trains on batch k; compute waits only on the event of the batch it consumes. The
 source is any iterator of (x, y) numpy/torch arrays (CSV chunks, a message queue, the
-synthetic generator); ``HostPool`` pre-stages a set of batches in pinned memory and
-cycles through them, which is how the benchmark isolates the transfer + train pipeline
-from Python-side generation cost. Inputs can be streamed as bf16 (the MFMA engines
-consume bf16 directly), halving PCIe bytes.
+synthetic generator). Pinned sources (``HostPool``) are copied straight from their own
+pages; anything else is first staged into a pinned ring (one host memcpy, then an async
+DMA), so the H2D copy never runs synchronously from pageable memory.
+
+The device ring buffers keep their addresses for the streamer's lifetime — a hipGraph
+captured on slot k (train/step.py StepRunner: one graph per slot) stays valid — and a new
+source can be fed with :meth:`feed` (one per online chunk, train/online.py).
+``HostPool`` pre-stages a set of batches in pinned memory and cycles through them, which is
+how the benchmark isolates the transfer + train pipeline from Python-side generation cost.
+Inputs can be streamed as bf16 (the MFMA engines consume bf16 directly), halving PCIe bytes.
 """
 from __future__ import annotations
 
@@ -32,24 +38,70 @@ class HostPool:
 
 
 class DeviceStreamer:
-    def __init__(self, source, device, depth: int = 3):
+    def __init__(self, source, device, depth: int = 3, x_dtype=None):
+        """``x_dtype``: cast features on the host before the copy (e.g. torch.bfloat16)."""
         assert depth >= 2
-        self.src = iter(source)
         self.device = torch.device(device)
         self.copy_stream = torch.cuda.Stream(device=self.device)
         self.depth = depth
-        self.slots = []  # (x_dev, y_dev, event)
-        self.k = 0
+        self.x_dtype = x_dtype
+        self.slots = []    # [x_dev, y_dev, event] — fixed addresses
+        self.staging = []  # pinned host ring for pageable sources: [x_pin, y_pin]
+        self.k = 0         # batches issued
+        self.used = 0      # batches handed to the consumer
+        self.last_slot = 0
+        self.src = None
         self._primed = False
+        self._exhausted = False
+        if source is not None:
+            self.feed(source)
 
-    def _issue(self):
-        x, y = next(self.src)
+    def feed(self, source) -> None:
+        """Start streaming a new source; the ring and any captured graphs stay valid."""
+        self.src = iter(source)
+        self._primed = False
+        self._exhausted = False
+        self.k = self.used = 0
+
+    def _host(self, x, y, slot):
+        x = torch.as_tensor(x)
+        if x.dtype == torch.float64:
+            x = x.float()
+        if self.x_dtype is not None and x.dtype != self.x_dtype:
+            x = x.to(self.x_dtype)
+        y = torch.as_tensor(y).float()
+        if x.is_pinned() and y.is_pinned():
+            return x, y
+        while len(self.staging) <= slot:
+            self.staging.append([None, None])
+        st = self.staging[slot]
+        if st[0] is None or st[0].shape != x.shape or st[0].dtype != x.dtype:
+            st[0] = torch.empty(x.shape, dtype=x.dtype).pin_memory()
+        if st[1] is None or st[1].shape != y.shape:
+            st[1] = torch.empty(y.shape, dtype=y.dtype).pin_memory()
+        if slot < len(self.slots):
+            self.slots[slot][2].synchronize()  # the slot's previous DMA has read the staging pages
+        st[0].copy_(x)
+        st[1].copy_(y)
+        return st[0], st[1]
+
+    def _issue(self) -> bool:
+        if self._exhausted:
+            return False
+        try:
+            x, y = next(self.src)
+        except StopIteration:
+            self._exhausted = True
+            return False
         slot = self.k % self.depth
-        if len(self.slots) < self.depth:
+        x, y = self._host(x, y, slot)
+        if len(self.slots) <= slot:
             xd = torch.empty(x.shape, dtype=x.dtype, device=self.device)
             yd = torch.empty(y.shape, dtype=y.dtype, device=self.device)
             self.slots.append([xd, yd, torch.cuda.Event()])
         xd, yd, ev = self.slots[slot]
+        assert xd.shape == x.shape and xd.dtype == x.dtype and yd.shape == y.shape, \
+            "DeviceStreamer: every batch must have the ring's shape"
         # the slot's previous consumer must be done before it is overwritten
         self.copy_stream.wait_stream(torch.cuda.current_stream(self.device))
         with torch.cuda.stream(self.copy_stream):
@@ -57,14 +109,29 @@ class DeviceStreamer:
             yd.copy_(y, non_blocking=True)
             ev.record(self.copy_stream)
         self.k += 1
+        return True
 
     def next(self):
+        """The next batch on the device, ordered before the current stream's later work;
+        raises StopIteration when a finite source is drained."""
         if not self._primed:
             for _ in range(self.depth - 1):
                 self._issue()
             self._primed = True
         self._issue()  # keep depth-1 batches in flight
-        self.last_slot = (self.k - self.depth) % self.depth
+        if self.used >= self.k:
+            raise StopIteration
+        self.last_slot = self.used % self.depth
+        self.used += 1
         xd, yd, ev = self.slots[self.last_slot]
         torch.cuda.current_stream(self.device).wait_event(ev)
         return xd, yd
+
+    def __iter__(self):
+        """Yields the ring slot index of each batch (its tensors: ``slots[k][0:2]``)."""
+        while True:
+            try:
+                self.next()
+            except StopIteration:
+                return
+            yield self.last_slot

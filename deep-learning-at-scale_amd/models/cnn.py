@@ -162,12 +162,15 @@ class NativeCNN:
         self.ypad = torch.zeros(batch * L.Op, device=dev)
         self.dpred = torch.zeros(batch * L.Op, dtype=bf, device=dev)
         self.loss_sum = torch.zeros(1, device=dev)
+        # dropout step counter on the device: the mask differs every training step, eager or
+        # replayed from a captured hipGraph (a host-side step would be baked into the graph)
+        self.rng = torch.zeros(1, dtype=torch.int64, device=dev)
         self.sync_weights()
 
     def sync_weights(self):
         self._C.cast_bf16(self.params, self.shadow)
 
-    def _fwd(self, x, B, drop_p, seed):
+    def _fwd(self, x, B, drop_p, seed, seed_dev=None):
         from ..ops.native import gemm
 
         L = self.lay
@@ -177,7 +180,8 @@ class NativeCNN:
         self._C.im2col1d(x.contiguous().float(), B, L.input_len, L.in_ch, L.kernel, L.Kc, self.Xcol)
         Wc, Wd, _ = L.views(self.shadow)
         _, _, bd = L.views(self.params)
-        gemm(self.Xcol, Wc, B * L.lout, L.Fp, L.Kc, outH=self.Hc, act=1, drop_p=drop_p, seed=seed)
+        gemm(self.Xcol, Wc, B * L.lout, L.Fp, L.Kc, outH=self.Hc, act=1, drop_p=drop_p, seed=seed,
+             seed_dev=seed_dev)
         gemm(self.Hc, Wd, B, L.Op, L.flat_width, outF=self.pred, bias=bd)
 
     def forward(self, x):
@@ -191,11 +195,12 @@ class NativeCNN:
 
         L = self.lay
         B = x.shape[0]
-        seed = (self.seed * 1000003 + step) & 0x7FFFFFFF
+        seed = (self.seed * 1000003) & 0x7FFFFFFF  # + the device step counter self.rng
         if zero_grads:
             self.grads.zero_()
         self.loss_sum.zero_()
-        self._fwd(x, B, self.p, seed)
+        self._fwd(x, B, self.p, seed, self.rng)
+        self.rng += 1
         yv = self.ypad[: B * L.Op].view(B, L.Op)
         yv[:, : L.outputs].copy_(y.view(B, -1))
         gWc, gWd, gbd = L.views(self.grads)

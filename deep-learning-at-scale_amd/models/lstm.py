@@ -20,6 +20,7 @@ from __future__ import annotations
 import dataclasses
 import math
 import os
+import sys
 
 import torch
 from torch import nn
@@ -181,6 +182,8 @@ class NativeLSTM:
         # timesteps per overlapped dW GEMM chunk; 0 = serial dW at the end (measured faster:
         # the BPTT chain already fills every CU, overlapping only adds contention)
         self.dw_chunk = 0
+        self._fallback_noted = set()
+        self.last_backward_persistent = False
         self.sync_weights()
 
     # ------------------------------------------------------------------ weights
@@ -196,18 +199,46 @@ class NativeLSTM:
         base = self.T * self.B * lay.KA  # XH[T] starts here (row stride KA)
         return self.XH[base + lay.KX : base + lay.KX + (B - 1) * lay.KA + self.H]
 
+    def _note_fallback(self, which: str, enabled: bool) -> None:
+        """Say ONCE per engine that a pass runs as per-step kernels (a silent fallback costs
+        ~25 % of the step): either disabled by env or refused for this shape / device."""
+        if which in self._fallback_noted:
+            return
+        self._fallback_noted.add(which)
+        why = ("disabled (WELLFLOW_PERSISTENT%s=0)" % ("_BWD" if which == "backward" else "")
+               if not enabled else "shape/device not supported by the persistent schedule")
+        print(f"wellflow: LSTM {which} runs per-step kernels: {why} "
+              f"(B={self.B} T={self.T} F={self.F} H={self.H})", file=sys.stderr, flush=True)
+
     def _forward_steps(self, B):
         C = self._C
+        # raises if the launch itself fails; False = shape / device cannot host the schedule
         ok = self.persistent and C.lstm_forward_persistent(self.XH, self.Wp, self.Cst, self.S, self.sync,
                                                           *self._dims(B))
         if not ok:
+            self._note_fallback("forward", self.persistent)
             C.lstm_forward(self.XH, self.Wp, self.Cst, self.S, *self._dims(B), self.fwd_variant)
         self.last_forward_persistent = bool(ok)
 
     def persistent_error(self) -> int:
-        """Non-zero if the last persistent forward or backward hit its spin bound (host sync)."""
-        fwd = int(self.sync[0].item()) if self.last_forward_persistent else 0
-        return fwd or int(self.sync_bwd[0].item())
+        """Sticky spin-timeout flags of the persistent forward (bit 0) and backward (bit 1),
+        set by ANY launch since the last :meth:`reset_device_errors` (one host sync)."""
+        w = torch.stack([self.sync[0], self.sync_bwd[0]]).cpu()
+        return (1 if int(w[0]) else 0) | (2 if int(w[1]) else 0)
+
+    def reset_device_errors(self) -> None:
+        self.sync[0] = 0
+        self.sync_bwd[0] = 0
+
+    def check_device_errors(self) -> None:
+        """Raise if a persistent kernel's hand-off wait timed out in any step so far (its
+        workgroups drained early: the state of that step is garbage)."""
+        e = self.persistent_error()
+        if e:
+            parts = [n for b, n in ((1, "forward"), (2, "backward")) if e & b]
+            raise RuntimeError(f"persistent LSTM {' and '.join(parts)} hit the hand-off spin bound "
+                               "(a workgroup never arrived: non-resident grid or a hung wave); "
+                               "results of the affected steps are invalid")
 
     # ------------------------------------------------------------------ passes
     def forward(self, x: torch.Tensor) -> torch.Tensor:
@@ -264,7 +295,10 @@ class NativeLSTM:
         ksplit = self.dw_ksplit or max(1, min(32, K // 16384))
         if self.dw_chunk > 0:
             ksplit = max(1, ksplit * self.dw_chunk // self.T)
-        C.lstm_backward_dw(self.WhhT, self.XH, self.Cst, self.S, self.DG, self.dcarry, self.dy,
-                           w_out, gW, *self._dims(B), self.bwd_variant, self.dw_chunk, ksplit,
-                           self.sync_bwd if self.persistent_bwd else None)
+        pb = C.lstm_backward_dw(self.WhhT, self.XH, self.Cst, self.S, self.DG, self.dcarry, self.dy,
+                                w_out, gW, *self._dims(B), self.bwd_variant, self.dw_chunk, ksplit,
+                                self.sync_bwd if self.persistent_bwd and self.dw_chunk <= 0 else None)
+        self.last_backward_persistent = bool(pb)
+        if not pb and self.dw_chunk <= 0:
+            self._note_fallback("backward", self.persistent_bwd)
         return self.loss_sum

@@ -38,11 +38,12 @@ def available() -> bool:
 
 def gemm(A, B, M, N, K, *, a_mn=False, lda=None, b_mn=False, ldb=None, outF=None, outH=None,
          ldo=None, bias=None, mask=None, ldm=None, mask_scale=1.0, colsum=None, alpha=1.0,
-         beta=0.0, act=0, atomic=False, ksplit=1, drop_p=0.0, seed=0, tile=0):
+         beta=0.0, act=0, atomic=False, ksplit=1, drop_p=0.0, seed=0, tile=0, seed_dev=None):
     """out = act(alpha * A(M,K) B(N,K)^T + beta*out + bias) (* mask), on MFMA.
 
     ``a_mn``/``b_mn`` select the MN-contiguous layout (X(r,k) = p[k*ld + r]).
     ``tile`` (MN x MN split-K atomic only): 1 = 256x128 8-wave tile, 2 = 128x288, 3 = 256x192.
+    ``seed_dev`` (int64 GPU tensor): a device step counter mixed into the dropout seed.
     """
     if lda is None:
         lda = M if a_mn else K
@@ -54,4 +55,4 @@ def gemm(A, B, M, N, K, *, a_mn=False, lda=None, b_mn=False, ldb=None, outF=None
         ldm = ldo
     lib().gemm(A, bool(a_mn), int(lda), B, bool(b_mn), int(ldb), int(M), int(N), int(K),
                int(ksplit), outF, outH, int(ldo), bias, mask, int(ldm), float(mask_scale), colsum,
-               float(alpha), float(beta), int(act), bool(atomic), float(drop_p), int(seed), int(tile))
+               float(alpha), float(beta), int(act), bool(atomic), float(drop_p), int(seed), int(tile), seed_dev)

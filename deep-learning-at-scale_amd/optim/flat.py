@@ -54,7 +54,16 @@ class FlatAdam:
         if self.zero_grads:
             self.grads.zero_()
 
+    @property
+    def steps_taken(self) -> int:
+        """Updates applied so far. On the GPU the device counter is the truth: hipGraph
+        replays (train/step.py) advance it without calling :meth:`step` on the host."""
+        if self.step_dev is not None:
+            return int(self.step_dev[0].item())
+        return self.t
+
     def state_dict(self) -> dict:
+        self.t = self.steps_taken
         return {"kind": "adam", "t": self.t, "m": self.m.detach().cpu(), "v": self.v.detach().cpu(),
                 "lr": self.lr, "betas": list(self.betas), "eps": self.eps,
                 "weight_decay": self.weight_decay}
@@ -78,34 +87,53 @@ class FlatSGD:
     """
 
     def __init__(self, params: torch.Tensor, grads: torch.Tensor, lr: float = 0.001,
-                 momentum: float = 0.99, decay: float = 1e-6, nesterov: bool = True):
+                 momentum: float = 0.99, decay: float = 1e-6, nesterov: bool = True,
+                 zero_grads: bool = False):
         self.params, self.grads = params, grads
         self.lr, self.momentum, self.decay, self.nesterov = lr, momentum, decay, nesterov
+        self.zero_grads = zero_grads
         self.vel = torch.zeros_like(params)
         self.iterations = 0
+        # device iteration counter ([1] = completion ticket): lr_t is computed in-kernel, so a
+        # hipGraph-captured update decays the learning rate on every replay
+        self.step_dev = torch.zeros(4, device=params.device) if params.is_cuda else None
 
     def step(self, grad_scale: float = 1.0) -> None:
-        lr_t = self.lr / (1.0 + self.decay * self.iterations)
-        self.iterations += 1
         if self.params.is_cuda:
             from ..ops.native import lib
 
-            lib().sgd(self.params, self.grads, self.vel, lr_t, self.momentum, self.nesterov, grad_scale)
+            self.iterations += 1
+            lib().sgd_dev(self.params, self.grads, self.vel, self.step_dev, self.lr, self.decay, self.momentum,
+                          self.nesterov, grad_scale, self.zero_grads)
             return
+        lr_t = self.lr / (1.0 + self.decay * self.iterations)
+        self.iterations += 1
         g = self.grads * grad_scale
         self.vel.mul_(self.momentum).sub_(lr_t * g)
         if self.nesterov:
             self.params.add_(self.momentum * self.vel - lr_t * g)
         else:
             self.params.add_(self.vel)
+        if self.zero_grads:
+            self.grads.zero_()
+
+    @property
+    def steps_taken(self) -> int:
+        if self.step_dev is not None:
+            return int(self.step_dev[0].item())
+        return self.iterations
 
     def state_dict(self) -> dict:
+        self.iterations = self.steps_taken
         return {"kind": "sgd", "iterations": self.iterations, "vel": self.vel.detach().cpu(),
                 "lr": self.lr, "momentum": self.momentum, "decay": self.decay,
                 "nesterov": self.nesterov}
 
     def load_state_dict(self, sd: dict) -> None:
         self.iterations = int(sd["iterations"])
+        if self.step_dev is not None:
+            self.step_dev.zero_()
+            self.step_dev[0] = float(self.iterations)
         self.vel.copy_(sd["vel"])
         self.lr, self.momentum, self.decay, self.nesterov = sd["lr"], sd["momentum"], sd["decay"], sd["nesterov"]
 

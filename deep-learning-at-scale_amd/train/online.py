@@ -9,6 +9,11 @@ from the previous submission's ``.mdl`` (train/job.py) the model keeps adapting 
 well data arrives, which is what distinguishes it from the static model.
 ``cfg.epochs`` bounds the passes over the stream (default 1 for pure online learning
 when the stream is long).
+
+On a GPU the mini-batches really stream: a :class:`~wellflow.data.stream.DeviceStreamer`
+ring (pinned host staging, async H2D on a copy stream, ``depth`` batches in flight) feeds
+the same StepRunner step that bench.py times (train/step.py), one captured hipGraph per
+ring slot. Nothing of a chunk is resident on the device beyond the ring.
 """
 from __future__ import annotations
 
@@ -24,12 +29,52 @@ def stream_chunks(X, Y, chunk: int):
         yield X[s : s + chunk], Y[s : s + chunk]
 
 
+def rank_batches(Xc, Yc, b: int, rank: int, world: int):
+    """This rank's mini-batches of one chunk, in arrival order (full batches only)."""
+    per_rank = len(Xc) // world
+    lo = rank * per_rank
+    for s in range(per_rank // b):
+        i = lo + s * b
+        yield Xc[i : i + b], Yc[i : i + b]
+
+
+def _train_chunk_streamed(trainer, streamer, Xc, Yc, b):
+    from .step import StepRunner
+
+    ctx, eng = trainer.ctx, trainer.eng
+    streamer.feed(rank_batches(Xc, Yc, b, ctx.rank, ctx.world_size))
+    run = trainer._runners.get("stream")
+    if run is None or run.grad_scale != 1.0 / (b * ctx.world_size * trainer.n_out):
+        run = StepRunner(eng, trainer.opt, ctx, 1.0 / (b * ctx.world_size * trainer.n_out),
+                         lambda k: tuple(streamer.slots[k][:2]))
+        trainer._runners = {"stream": run}
+    run.take_loss()
+    t0 = time.perf_counter()
+    done = 0
+    for slot in streamer:
+        run.run(slot)
+        done += 1
+        if trainer._after_step():
+            break
+    torch.cuda.synchronize(eng.device)
+    dt = time.perf_counter() - t0
+    (tot,) = ctx.sum_scalars(run.take_loss())
+    rows = done * b * ctx.world_size
+    return tot / max(rows * trainer.n_out, 1), rows, dt
+
+
 def fit_online(trainer, train, val):
     cfg, ctx, eng = trainer.cfg, trainer.ctx, trainer.eng
     Xtr, Ytr = train
     chunk = max(cfg.online_chunk, ctx.world_size)
     passes = max(1, cfg.epochs)
     done_chunks = int(trainer.extra_state.get("chunks_done", 0))
+    streamed = eng.device.type == "cuda" and getattr(eng, "native", False)
+    streamer = None
+    if streamed:
+        from ..data.stream import DeviceStreamer
+
+        streamer = DeviceStreamer(None, eng.device, depth=3)
     k = 0
     for p in range(passes):
         for Xc, Yc in stream_chunks(Xtr, Ytr, chunk):
@@ -37,11 +82,16 @@ def fit_online(trainer, train, val):
                 k += 1
                 continue
             t0 = time.perf_counter()
-            Xd, Yd = _to_dev(Xc, eng.device), _to_dev(Yc, eng.device)
-            per_rank = len(Xd) // ctx.world_size
-            order = torch.arange(ctx.rank * per_rank, (ctx.rank + 1) * per_rank, device=eng.device)
-            b = max(1, min(cfg.batch_size, per_rank, getattr(eng, "B", cfg.batch_size)))
-            tr_loss, rows, dt = trainer.train_steps(Xd, Yd, order, b)
+            per_rank = len(Xc) // ctx.world_size
+            b_full = max(1, min(cfg.batch_size, getattr(eng, "B", cfg.batch_size)))
+            b = max(1, min(b_full, per_rank))
+            if streamed and per_rank >= b_full:  # the ring holds full batches of one shape
+                tr_loss, rows, dt = _train_chunk_streamed(trainer, streamer, Xc, Yc, b_full)
+            else:  # CPU oracle, or a short tail chunk: train on it from device memory
+                Xd, Yd = _to_dev(Xc, eng.device), _to_dev(Yc, eng.device)
+                order = torch.arange(ctx.rank * per_rank, (ctx.rank + 1) * per_rank, device=eng.device)
+                tr_loss, rows, dt = trainer.train_steps(Xd, Yd, order, b)
+            trainer.check_device()
             v_loss, v_mse = trainer.evaluate(*val)
             k += 1
             trainer.extra_state["chunks_done"] = k

@@ -1,0 +1,138 @@
+"""The training step, shared by the production loop (Trainer, fit_online) and bench.py.
+
+Replaces one iteration of Keras ``model.fit`` (cnn.py:127-128: forward, loss, backward,
+SGD update) with the MI355X step:
+
+    inputs() -> engine.forward_backward -> C2 flat all-reduce (RCCL over xGMI)
+             -> fused optimizer launch (Adam: update + bf16 shadow + gradient clear)
+             -> engine.sync_weights() (bf16 repack of the weights the kernels read)
+
+On a GPU the first ``eager_steps`` calls run eagerly (they are real training steps: the
+optimizer really updates) and the step is then captured as ONE hipGraph per input slot —
+the ~135 launches of an LSTM step, the RCCL all-reduce included (``comm_in_graph``), replay
+with one host call. The optimizer's step counter lives on the device (optim/flat.py), so a
+replay is exactly the eager step. ``inputs`` is called inside the captured region and must
+read only tensors whose storage stays put (static index buffers, a resident dataset, a
+streamer's ring slot): a replay re-reads the same addresses.
+
+Round-1 verdict item 6 ("one step implementation for bench and jobs"): bench.py times
+:meth:`StepRunner.run`, and Trainer.train_steps / fit_online drive the same object.
+"""
+from __future__ import annotations
+
+import os
+import sys
+
+import torch
+
+
+def _env_flag(name: str, default: bool) -> bool:
+    v = os.environ.get(name)
+    return default if v is None else v not in ("0", "", "false", "False")
+
+
+class StepRunner:
+    def __init__(self, eng, opt, ctx, grad_scale: float, inputs, *, graph: bool | None = None,
+                 comm_in_graph: bool | None = None, eager_steps: int = 2, accumulate_loss: bool = True):
+        """``inputs(key) -> (x, y)``: the step's batch on the engine's device for slot ``key``."""
+        self.eng, self.opt, self.ctx = eng, opt, ctx
+        self.grad_scale = float(grad_scale)
+        self.inputs = inputs
+        cuda = eng.device.type == "cuda"
+        self.graph = cuda and (graph if graph is not None else _env_flag("WELLFLOW_GRAPH", True))
+        self.comm_in_graph = comm_in_graph if comm_in_graph is not None else _env_flag("WELLFLOW_COMM_IN_GRAPH", True)
+        self.eager_steps = max(1, int(eager_steps))
+        self.fused_clear = bool(getattr(opt, "zero_grads", False))
+        # Adam writing the engine's bf16 compute copy in its own launch (NativeMLP.shadow)
+        # replaces the separate repack
+        sh = getattr(opt, "shadow", None)
+        self.fused_shadow = sh is not None and sh is getattr(eng, "shadow", None)
+        self.loss_acc = torch.zeros(1, device=eng.device) if accumulate_loss else None
+        self.graphs: dict = {}
+        self.update_graph = None  # comm outside the graph: [compute graph] all-reduce [update graph]
+        self.calls = 0
+        self.captured_comm = False
+
+    # ------------------------------------------------------------------ pieces
+    def _compute(self, key):
+        x, y = self.inputs(key)
+        ls = self.eng.forward_backward(x, y, self.grad_scale, zero_grads=not self.fused_clear)
+        if self.loss_acc is not None:
+            self.loss_acc += ls
+
+    def _comm(self):
+        self.ctx.all_reduce_sum_(self.eng.grads)
+
+    def _update(self):
+        self.opt.step()
+        if not self.fused_shadow:
+            self.eng.sync_weights()
+
+    def _eager(self, key):
+        self._compute(key)
+        self._comm()
+        self._update()
+
+    def _capture(self, key):
+        dev = self.eng.device
+        torch.cuda.synchronize(dev)
+        g = torch.cuda.CUDAGraph()
+        comm = self.comm_in_graph and self.ctx.distributed
+        if comm:
+            try:
+                with torch.cuda.graph(g):
+                    self._compute(key)
+                    self._comm()
+                    self._update()
+                self.captured_comm = True
+                self.graphs[key] = g
+                return
+            except Exception as e:  # RCCL build that cannot be captured: split graphs, comm eager
+                if self.ctx.is_main:
+                    print(f"StepRunner: all-reduce capture failed ({e!r}); comm runs between graphs",
+                          file=sys.stderr, flush=True)
+                torch.cuda.synchronize(dev)
+                self.comm_in_graph = False
+                g = torch.cuda.CUDAGraph()
+        if not self.ctx.distributed:
+            with torch.cuda.graph(g):
+                self._compute(key)
+                self._update()
+            self.graphs[key] = g
+            return
+        with torch.cuda.graph(g):
+            self._compute(key)
+        self.graphs[key] = g
+        if self.update_graph is None:
+            gu = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(gu):
+                self._update()
+            self.update_graph = gu
+
+    # ------------------------------------------------------------------ API
+    def run(self, key=0) -> None:
+        """One full training step on the batch ``inputs(key)`` (no host sync)."""
+        self.calls += 1
+        g = self.graphs.get(key)
+        if g is None and self.graph and self.calls > self.eager_steps:
+            self._capture(key)
+            g = self.graphs[key]
+        if g is None:
+            self._eager(key)
+        elif self.captured_comm or not self.ctx.distributed:
+            g.replay()
+        else:
+            g.replay()
+            self._comm()
+            self.update_graph.replay()
+        check = getattr(self.eng, "check_device_errors", None)
+        if check is not None and self.calls <= self.eager_steps + 1:
+            check()  # a broken hand-off in the first (eager / first replay) steps fails loudly
+
+    def take_loss(self) -> float:
+        """Sum of per-sample losses since the last call (one host sync)."""
+        if self.loss_acc is None:
+            return float("nan")
+        v = float(self.loss_acc.item())
+        self.loss_acc.zero_()
+        return v

@@ -85,6 +85,8 @@ class Trainer:
         self.epoch = 0
         self.global_step = 0
         self.extra_state = {}
+        self._runners = {}
+        self._idx = {}
 
     # ------------------------------------------------------------------ helpers
     def _local_batch(self, n_train: int) -> int:
@@ -122,6 +124,7 @@ class Trainer:
             "epoch": self.epoch,
             "global_step": self.global_step,
             "params": self.eng.params.detach().cpu().clone(),
+            # (optimizer.state_dict reads the device step counter: graph replays advance it)
             "optimizer": self.opt.state_dict(),
             "early_stopping": dataclasses.asdict(self.stopper),
             "history": dataclasses.asdict(self.history),
@@ -132,6 +135,8 @@ class Trainer:
     def load_state_dict(self, sd: dict) -> None:
         self.eng.params.copy_(sd["params"].to(self.eng.params.device))
         self.eng.sync_weights()
+        if getattr(self.eng, "rng", None) is not None:  # dropout stream continues where it stopped
+            self.eng.rng.fill_(int(sd["global_step"]))
         self.opt.load_state_dict(sd["optimizer"])
         self.epoch = int(sd["epoch"])
         self.global_step = int(sd["global_step"])
@@ -181,33 +186,67 @@ class Trainer:
             f.write(json.dumps(rec) + "\n")
 
     # ------------------------------------------------------------------ fit
+    def _runner(self, key, make_inputs, b: int):
+        """The StepRunner (train/step.py, the same step bench.py times) for batches of ``b``
+        rows, cached per data source: after two eager steps it replays as one hipGraph."""
+        from .step import StepRunner
+
+        rk = (key, b)
+        if self._runners.get("key") != rk:
+            gscale = 1.0 / (b * self.ctx.world_size * self.n_out)
+            native = getattr(self.eng, "native", False)
+            self._runners = {"key": rk, "run": StepRunner(self.eng, self.opt, self.ctx, gscale, make_inputs,
+                                                          graph=None if native else False)}
+        return self._runners["run"]
+
+    def _after_step(self) -> bool:
+        """Step bookkeeping; True = stop (max_steps)."""
+        self.global_step += 1
+        cfg = self.cfg
+        if cfg.fail_at_step >= 0 and self.global_step == cfg.fail_at_step:
+            self._inject_fault()
+        return bool(cfg.max_steps and self.global_step >= cfg.max_steps)
+
     def train_steps(self, Xd, Yd, order: torch.Tensor, b: int):
-        """One pass over ``order`` (device index tensor of this rank) in batches of ``b``."""
-        eng, ctx, cfg = self.eng, self.ctx, self.cfg
+        """One pass over ``order`` (device index tensor of this rank) in batches of ``b``.
+
+        Each step gathers its batch from the resident dataset through a STATIC index buffer
+        inside the captured step, so the whole step (gather, fwd, bwd, all-reduce, update)
+        is one graph replay; the remainder that does not fill a batch is dropped (the native
+        engines run fixed-shape batches)."""
+        eng, ctx = self.eng, self.ctx
         steps = len(order) // b
         if steps == 0 and len(order) > 0 and not getattr(eng, "native", False):
             steps, b = 1, len(order)
-        gscale = 1.0 / (b * ctx.world_size * self.n_out)
-        loss_acc = torch.zeros(1, device=eng.device)
+        idx = self._idx.get(b)
+        if idx is None:
+            idx = self._idx[b] = torch.zeros(b, dtype=torch.long, device=eng.device)
+
+        def inputs(_k):
+            return Xd[idx], Yd[idx]
+
+        run = self._runner(("resident", id(Xd), id(Yd)), inputs, b)
+        run.take_loss()
         t0 = time.perf_counter()
+        done = 0
         for s in range(steps):
-            sel = order[s * b : (s + 1) * b]
-            xb, yb = Xd[sel], Yd[sel]
-            loss_acc += eng.forward_backward(xb, yb, gscale, step=self.global_step)
-            ctx.all_reduce_sum_(eng.grads)
-            self.opt.step()
-            eng.sync_weights()
-            self.global_step += 1
-            if cfg.fail_at_step >= 0 and self.global_step == cfg.fail_at_step:
-                self._inject_fault()
-            if cfg.max_steps and self.global_step >= cfg.max_steps:
+            idx.copy_(order[s * b : (s + 1) * b])
+            run.run()
+            done += 1
+            if self._after_step():
                 break
         if eng.device.type == "cuda":
             torch.cuda.synchronize(eng.device)
         dt = time.perf_counter() - t0
-        (tot,) = ctx.sum_scalars(loss_acc.item())
-        rows = (s + 1 if steps else 0) * b * ctx.world_size
+        (tot,) = ctx.sum_scalars(run.take_loss())
+        rows = done * b * ctx.world_size
         return tot / max(rows * self.n_out, 1), rows, dt
+
+    def check_device(self) -> None:
+        """Once per epoch: raise if a persistent kernel's hand-off timed out in any step."""
+        check = getattr(self.eng, "check_device_errors", None)
+        if check is not None:
+            check()
 
     def fit(self, train, val):
         cfg, ctx = self.cfg, self.ctx
@@ -225,6 +264,7 @@ class Trainer:
             order = torch.as_tensor(mine, device=dev)
             with trace_range("train_epoch", dev):
                 tr_loss, rows, dt = self.train_steps(Xd, Yd, order, b)
+            self.check_device()
             with trace_range("evaluate", dev):
                 v_loss, v_mse = self.evaluate(*val)
             self.epoch += 1

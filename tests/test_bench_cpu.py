@@ -1,8 +1,9 @@
 """bench.py contract at world size 1, 2 and 4 without GPUs (--device cpu: gloo + the fp32
-reference model). The driver launches bench.py under torch.distributed.run on 1/2/4/8
-MI355X once per round; this rehearses everything around the kernels: rendezvous on
-127.0.0.1, C1 broadcast, C2 all-reduce, the barrier-bracketed timing, max over ranks, and
-exactly ONE JSON line from rank 0 with the whole-job aggregate value."""
+reference model). The driver runs bench.py either under torch.distributed.run or as
+`python bench.py --gpus N` (bench.py then spawns the N ranks itself); this rehearses
+everything around the kernels for both: rendezvous on 127.0.0.1, C1 broadcast, C2
+all-reduce, the barrier-bracketed timing, max over ranks, and exactly ONE JSON line from
+rank 0 with the whole-job aggregate value."""
 import json
 import os
 import socket
@@ -24,11 +25,13 @@ def _port():
     return p
 
 
-def _run(world, model, extra):
+def _run(world, model, extra, torchrun=True):
     env = dict(os.environ, CUDA_VISIBLE_DEVICES="", OMP_NUM_THREADS="1")
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
+        env.pop(k, None)
     args = ["bench.py", "--gpus", str(world), "--steps", "3", "--warmup", "1", "--device", "cpu",
             "--model", model] + extra
-    if world > 1:
+    if world > 1 and torchrun:
         cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
                "--master-addr", "127.0.0.1", "--master-port", str(_port())] + args
     else:
@@ -53,6 +56,22 @@ def test_bench_json_contract_lstm(world):
     assert rec["value"] == pytest.approx(B * world / (rec["ms_per_step"] / 1000.0), rel=1e-3)
     assert rec["dtype"] == "fp32" and "rehearsal" in rec["data"]  # never mistaken for the benchmark
     assert rec["higher_is_better"] is True and rec["scaling"] == "weak"
+
+
+def test_bench_self_spawns_ranks():
+    """`python bench.py --gpus 4` with no launcher: the parent starts 4 ranks itself
+    (torch.distributed.run on 127.0.0.1) and exactly one JSON line comes back, n_gpus 4."""
+    B = 4
+    rec = _run(4, "lstm", ["--batch", str(B), "--seq", "6", "--hidden", "16"], torchrun=False)
+    assert rec["n_gpus"] == 4 and rec["world_size"] == 4 and rec["config"]["parallelism"] == "dp4"
+    assert rec["config"]["global_batch"] == 4 * B and rec["backend"] == "gloo"
+
+
+def test_bench_refuses_world_mismatch():
+    env = dict(os.environ, CUDA_VISIBLE_DEVICES="", WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, "bench.py", "--gpus", "2", "--device", "cpu", "--steps", "1"],
+                       capture_output=True, text=True, env=env, cwd=ROOT, timeout=300)
+    assert r.returncode == 2 and not r.stdout.strip()
 
 
 def test_bench_json_contract_mlp_dp2():

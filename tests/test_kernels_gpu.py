@@ -214,11 +214,13 @@ def test_losses():
         assert torch.allclose(cs, (pr.grad * scale).sum(0), rtol=1e-2, atol=1e-4)
 
 
-@pytest.mark.parametrize("B,H,T", [(8192, 512, 8), (512, 256, 6), (256, 128, 5), (2048, 512, 64)])
+@pytest.mark.parametrize("B,H,T", [(8192, 512, 8), (512, 256, 6), (256, 128, 5), (2048, 512, 64),
+                                   (16384, 512, 4), (12288, 512, 3)])
 def test_lstm_persistent_forward_matches_per_step(B, H, T):
     """The one-launch persistent forward (csrc/lstm_persistent.hip) must reproduce the
     per-step kernels: same MFMA k-order per output, so h/C/S agree to the last bf16 ulp
-    apart from transcendental rounding (tolerance), and its spin bound must not trip."""
+    apart from transcendental rounding (tolerance), and its spin bound must not trip.
+    B > 8192 at H = 512 runs as consecutive sub-batch launches (no batch cap)."""
     from wellflow.data.synth import synth_lstm_batch
     from wellflow.models.lstm import NativeLSTM, init_lstm_flat
 
@@ -240,7 +242,7 @@ def test_lstm_persistent_forward_matches_per_step(B, H, T):
     ok = C.lstm_forward_persistent(eng.XH, eng.Wp, eng.Cst, eng.S, eng.sync, *dims)
     torch.cuda.synchronize()
     assert ok, "persistent launch refused"
-    assert int(eng.sync[0].item()) == 0, "spin bound tripped"
+    assert eng.persistent_error() == 0, "spin bound tripped"
     for name, a, b in zip(("XH", "C", "S"), (eng.XH, eng.Cst, eng.S), ref):
         d = (a.float() - b.float()).abs().max().item()
         assert d <= 2e-2, (name, d)
@@ -265,7 +267,8 @@ def test_weight_gradient_tiles_match_reference(tile, ksplit):
     assert err < 2e-3 * ref.abs().max().item(), (tile, err)
 
 
-@pytest.mark.parametrize("B,H,T", [(8192, 512, 8), (512, 256, 6), (256, 128, 5), (2048, 512, 64)])
+@pytest.mark.parametrize("B,H,T", [(8192, 512, 8), (512, 256, 6), (256, 128, 5), (2048, 512, 64),
+                                   (16384, 512, 4)])
 def test_lstm_persistent_backward_matches_per_step(B, H, T):
     """The one-launch persistent BPTT (csrc/lstm_persistent_bwd.hip) against the per-step
     backward kernels on the same forward state: the K-split dh partials are summed in a
@@ -282,11 +285,12 @@ def test_lstm_persistent_backward_matches_per_step(B, H, T):
     res = {}
     for pb in (False, True):
         eng.persistent_bwd = pb
-        eng.sync_bwd.fill_(7)  # the launcher must reset it
+        eng.sync_bwd[1:].fill_(7)  # the launcher must reset its launch words (word 0 is sticky)
         eng.forward_backward(x, y, grad_scale=1.0 / B)
         torch.cuda.synchronize()
         if pb:
-            assert int(eng.sync_bwd[0].item()) == 0, "spin bound tripped"
+            assert eng.last_backward_persistent, "persistent backward refused"
+            assert eng.persistent_error() == 0, "spin bound tripped"
             assert int(eng.sync_bwd[16].item()) > 0, "persistent backward did not run"
         res[pb] = (eng.DG.clone(), eng.grads.clone())
     (dg0, g0), (dg1, g1) = res[False], res[True]
@@ -295,3 +299,43 @@ def test_lstm_persistent_backward_matches_per_step(B, H, T):
     assert d <= 2e-2 * scale + 1e-6, (d, scale)
     rel = ((g0 - g1).norm() / g0.norm()).item()
     assert rel < 5e-3, rel
+
+
+def test_persistent_timeout_is_sticky_and_raises(monkeypatch):
+    """A hand-off wait that times out must not be silent (round-1 advice): with a diagnostic
+    spin bound of 1 poll the persistent kernels drain early, the STICKY word survives the
+    next launch's reset, check_device_errors() raises, and the StepRunner raises on its
+    first steps. After reset_device_errors() and the normal bound, steps are clean again."""
+    from wellflow.data.synth import synth_lstm_batch
+    from wellflow.models.lstm import NativeLSTM, init_lstm_flat
+    from wellflow.optim.flat import FlatAdam
+    from wellflow.parallel.dist import DistContext
+    from wellflow.train.step import StepRunner
+
+    B, T, F, H = 8192, 8, 16, 512
+    eng = NativeLSTM(F, H, T, B, device=DEV)
+    eng.params.copy_(init_lstm_flat(F, H, seed=0).to(DEV))
+    eng.sync_weights()
+    x, y = synth_lstm_batch(B, T, F, seed=0)
+    x, y = x.to(DEV), y.to(DEV)
+    monkeypatch.setenv("WELLFLOW_SPIN_LIMIT", "1")
+    eng.forward_backward(x, y, 1.0 / B)
+    torch.cuda.synchronize()
+    assert eng.persistent_error() != 0, "a 1-poll spin bound should trip on a 256-workgroup grid"
+    monkeypatch.delenv("WELLFLOW_SPIN_LIMIT")
+    eng.forward_backward(x, y, 1.0 / B)  # a clean launch: resets words 1.., keeps word 0
+    torch.cuda.synchronize()
+    with pytest.raises(RuntimeError, match="spin bound"):
+        eng.check_device_errors()
+    eng.reset_device_errors()
+    eng.forward_backward(x, y, 1.0 / B)
+    torch.cuda.synchronize()
+    eng.check_device_errors()
+    # the production step raises on its first steps
+    monkeypatch.setenv("WELLFLOW_SPIN_LIMIT", "1")
+    opt = FlatAdam(eng.params, eng.grads, lr=1e-3, zero_grads=True)
+    run = StepRunner(eng, opt, DistContext(device=torch.device(DEV)), 1.0 / B, lambda k: (x, y), graph=False)
+    with pytest.raises(RuntimeError, match="spin bound"):
+        run.run()
+    monkeypatch.delenv("WELLFLOW_SPIN_LIMIT")
+    eng.reset_device_errors()

@@ -1,0 +1,138 @@
+"""The production training step (wellflow/train/step.py StepRunner) on the MI355X: the
+hipGraph-captured step equals the eager step — with Adam clearing the gradient bucket in its
+own launch (the bench configuration) on the graph side and a zero-before-backward eager
+reference on the other — and the RCCL all-reduce captured INSIDE the step graph (forced
+process group at world size 1) gives the same parameters as the eager step. Also: the CNN's
+dropout mask changes on every replay (device step counter, not a baked constant)."""
+import os
+import socket
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _lstm(B=2048, T=16, F=16, H=512, seed=3):
+    from wellflow.data.synth import synth_lstm_batch
+    from wellflow.models.lstm import NativeLSTM, init_lstm_flat
+
+    eng = NativeLSTM(F, H, T, B, device=DEV)
+    eng.params.copy_(init_lstm_flat(F, H, seed=seed).to(DEV))
+    eng.sync_weights()
+    x, y = synth_lstm_batch(B, T, F, seed=seed)
+    return eng, x.to(DEV), y.to(DEV)
+
+
+def _mlp(B=65536, F=16, seed=2):
+    from wellflow.data.synth import synth_tabular_batch
+    from wellflow.models.mlp import NativeMLP, init_mlp_flat
+
+    eng = NativeMLP(F, (256, 256), B, device=DEV)
+    eng.params.copy_(init_mlp_flat(F, (256, 256), seed=seed).to(DEV))
+    eng.sync_weights()
+    x, y = synth_tabular_batch(B, F, seed=seed)
+    return eng, x.to(DEV), y.to(DEV)
+
+
+def _eager_reference(eng, x, y, steps, lr=1e-3):
+    """Plain eager loop: zero grads before every backward, Adam without fusions."""
+    from wellflow.optim.flat import FlatAdam
+
+    opt = FlatAdam(eng.params, eng.grads, lr=lr)
+    for _ in range(steps):
+        eng.forward_backward(x, y, 1.0 / len(y), zero_grads=True)
+        opt.step()
+        eng.sync_weights()
+    torch.cuda.synchronize()
+    return eng.params.clone()
+
+
+def _runner_params(eng, x, y, steps, ctx, comm_in_graph=True, lr=1e-3):
+    from wellflow.optim.flat import FlatAdam
+    from wellflow.train.step import StepRunner
+
+    kw = {"shadow": eng.shadow} if hasattr(eng, "shadow") else {}
+    opt = FlatAdam(eng.params, eng.grads, lr=lr, zero_grads=True, **kw)
+    run = StepRunner(eng, opt, ctx, 1.0 / len(y), lambda k: (x, y), graph=True, comm_in_graph=comm_in_graph)
+    for _ in range(steps):
+        run.run()
+    torch.cuda.synchronize()
+    assert run.graphs, "the step was never captured"
+    assert opt.steps_taken == steps  # device counter: replays advance it
+    return eng.params.clone(), run
+
+
+@pytest.mark.parametrize("model", ["lstm", "mlp"])
+def test_step_graph_with_fused_clear_equals_eager(model):
+    from wellflow.parallel.dist import DistContext
+
+    make = _lstm if model == "lstm" else _mlp
+    eng_e, x, y = make()
+    eng_g, _, _ = make()
+    steps = 6  # 2 eager + capture + 3 replays (capture does not execute)
+    pe = _eager_reference(eng_e, x, y, steps)
+    pg, _ = _runner_params(eng_g, x, y, steps, DistContext(device=torch.device(DEV)))
+    # split-K fp32 atomics reorder sums run to run; a missed gradient clear doubles the
+    # gradients and moves parameters by ~lr (1e-3)
+    d = (pe - pg).abs().max().item()
+    assert d <= 5e-5, d
+
+
+def test_rccl_allreduce_captured_in_step_graph(monkeypatch):
+    """One replay per step with the RCCL all-reduce inside the graph (forced group, world 1):
+    same parameters as the eager step for both native engines."""
+    from wellflow.parallel.dist import DistContext
+
+    for k, v in {"RANK": "0", "LOCAL_RANK": "0", "WORLD_SIZE": "1", "MASTER_ADDR": "127.0.0.1",
+                 "MASTER_PORT": str(_port())}.items():
+        monkeypatch.setenv(k, v)
+    monkeypatch.delenv("TORCHELASTIC_RESTART_COUNT", raising=False)
+    ctx = DistContext.from_env(force_group=True)
+    try:
+        assert ctx.distributed and ctx.backend == "nccl"
+        for make in (_lstm, _mlp):
+            eng_e, x, y = make()
+            eng_g, _, _ = make()
+            pe = _eager_reference(eng_e, x, y, 6)
+            pg, run = _runner_params(eng_g, x, y, 6, ctx, comm_in_graph=True)
+            assert run.captured_comm, "RCCL all-reduce was not captured in the step graph"
+            d = (pe - pg).abs().max().item()
+            assert d <= 5e-5, (make.__name__, d)
+    finally:
+        ctx.shutdown()
+
+
+def test_cnn_dropout_mask_differs_per_replay():
+    from wellflow.models.cnn import CNN1DRegressor, NativeCNN
+    from wellflow.optim.flat import FlatSGD
+    from wellflow.parallel.dist import DistContext
+    from wellflow.train.step import StepRunner
+
+    ref = CNN1DRegressor(dropout=0.5).init_keras(0)
+    eng = NativeCNN(ref.layout, batch=64, device=DEV, dropout=0.5, loss="mae_clip")
+    eng.params.copy_(ref.to_flat().to(DEV))
+    eng.sync_weights()
+    x, y = torch.randn(64, 48, 1, device=DEV), torch.randn(64, 12, device=DEV)
+    opt = FlatSGD(eng.params, eng.grads, lr=0.0, zero_grads=True)  # lr 0: weights stay put
+    run = StepRunner(eng, opt, DistContext(device=torch.device(DEV)), 1.0 / 64, lambda k: (x, y), graph=True)
+    masks = []
+    for _ in range(5):
+        run.run()
+        torch.cuda.synchronize()
+        masks.append((eng.Hc[: 64 * eng.lay.flat_width] != 0).clone())
+    assert run.graphs
+    for a, b in zip(masks[2:], masks[3:]):  # replays 1, 2, 3
+        frac = (a != b).float().mean().item()
+        assert frac > 0.05, "dropout mask repeated across graph replays"
+    assert int(eng.rng.item()) == 5
+    assert opt.steps_taken == 5
