@@ -67,6 +67,10 @@ class RunConfig:
     device: str = "auto"         # auto | cpu | cuda
     precision: str = "bf16"      # bf16 (native MFMA path) | fp32 (torch oracle)
     group_col: str = ""          # series id column for windowing (default: first string col)
+    # windowed models (lstm, cnn): "time" = contiguous per-series blocks in time order with a
+    # one-window gap between splits (no row of a val/test window inside any training window);
+    # "random" = windows drawn at random (overlapping windows then leak across splits)
+    window_split: str = "time"
     synth_wells: int = 16
     synth_steps: int = 600
     online_chunk: int = 4096     # dynamic model: rows per streamed chunk
@@ -130,6 +134,7 @@ def build_parser(model: str) -> argparse.ArgumentParser:
     ap.add_argument("--device", choices=["auto", "cpu", "cuda"])
     ap.add_argument("--precision", choices=["bf16", "fp32"])
     ap.add_argument("--group-col", dest="group_col")
+    ap.add_argument("--window-split", dest="window_split", choices=["time", "random"])
     ap.add_argument("--synth-wells", type=int, dest="synth_wells")
     ap.add_argument("--synth-steps", type=int, dest="synth_steps")
     ap.add_argument("--online-chunk", type=int, dest="online_chunk")

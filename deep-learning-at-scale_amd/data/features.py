@@ -164,6 +164,51 @@ class FeaturePipeline:
         }
 
 
+def time_block_split(starts: np.ndarray, span: int, groups=None, weights=(0.64, 0.16, 0.2), seed: int = 42):
+    """Leak-free split of overlapping windows (window k covers rows starts[k] .. +span-1).
+
+    Inside every series the windows are cut, in time order, into contiguous train / val /
+    test blocks of the given proportions, and the ``span - 1`` windows after each cut are
+    dropped, so no row that a val or test window reads (inputs or targets) lies inside any
+    training window, and none of a test window's rows inside a val window. Series too short
+    to be cut that way (fewer than 3 windows per block after the gaps) are assigned WHOLE,
+    seeded, in the same proportions (disjoint series cannot share rows). The reference split
+    ROWS at random (cnn.py:68); a random split of stride-1 windows would put 63 of a test
+    window's 64 rows into training windows. Returns index arrays into ``starts``.
+    """
+    w = np.asarray(weights, dtype=np.float64)
+    w = w / w.sum()
+    starts = np.asarray(starts, np.int64)
+    gid = np.zeros(len(starts), np.int64) if groups is None else np.asarray(groups)[starts]
+    out = [[] for _ in w]
+    gap = max(span - 1, 0)
+    short = []
+    # windows of one series are consecutive in `starts` (window_starts enumerates per series)
+    bounds = np.flatnonzero(np.diff(gid)) + 1
+    for seg in np.split(np.arange(len(starts)), bounds):
+        usable = len(seg) - gap * (len(w) - 1)
+        sizes = np.floor(w * max(usable, 0)).astype(np.int64)
+        if usable <= 0 or sizes.min() < 3:
+            short.append(seg)
+            continue
+        sizes[0] += usable - sizes.sum()
+        pos = 0
+        for k, sz in enumerate(sizes):
+            out[k].append(seg[pos: pos + sz])
+            pos += sz + gap
+    if short:
+        order = np.random.default_rng(seed).permutation(len(short))
+        cuts = np.round(np.cumsum(w) * len(short)).astype(np.int64)
+        if len(short) >= len(w):  # every split gets at least one whole series
+            for k in range(len(w) - 1):
+                cuts[k] = min(max(cuts[k], (cuts[k - 1] if k else 0) + 1), len(short) - (len(w) - 1 - k))
+        lo = 0
+        for k, hi in enumerate(cuts):
+            out[k].extend(short[j] for j in order[lo:hi])
+            lo = hi
+    return [np.concatenate(o) if o else np.zeros(0, np.int64) for o in out]
+
+
 def take(table: dict, idx) -> dict:
     return {k: np.asarray(v)[idx] for k, v in table.items()}
 

@@ -9,8 +9,11 @@
   past ``cnn_input_len`` target values of a series -> the next ``cnn_outputs`` values.
 * ``gilbert``: the raw physical columns (whp, choke, glr) and the raw target.
 
-The split (0.64/0.16/0.20, cnn.py:68) is drawn per sample with a fixed seed; the
-feature pipeline is fitted on the training split only.
+The split (0.64/0.16/0.20, cnn.py:68) is drawn per row with a fixed seed for the row
+models; the windowed models (lstm, cnn) split each series into contiguous time blocks with
+a one-window gap (``window_split="time"``, data/features.py time_block_split), so
+overlapping windows cannot leak val/test rows into training. The feature pipeline is
+fitted on the training split only.
 """
 from __future__ import annotations
 
@@ -18,7 +21,8 @@ import dataclasses
 
 import numpy as np
 
-from .features import FeaturePipeline, SeriesWindows, make_windows, random_split, take, window_rows, window_starts
+from .features import (FeaturePipeline, SeriesWindows, make_windows, random_split, take, time_block_split,
+                       window_rows, window_starts)
 from .io import load_table
 from .schema import parse_schema
 
@@ -73,12 +77,17 @@ def prepare(cfg) -> Prepared:
 
     ids, gcol = _group_ids(table, schema, cfg.group_col)
     table, ids = _sort_by_group(table, ids, schema)
+    def split_windows(starts, span):
+        if getattr(cfg, "window_split", "time") == "random":
+            return random_split(len(starts), cfg.split, cfg.seed)
+        return time_block_split(starts, span, ids, cfg.split, cfg.seed)
+
     if cfg.model == "lstm":
-        # windows are split at random (as the reference split rows); the feature pipeline
-        # is fitted ONLY on the rows that training windows cover
+        # leak-free time-block split of the windows; the feature pipeline is fitted ONLY on
+        # the rows that training windows cover
         T = cfg.seq_len
         starts = window_starts(n, T, ids)
-        idx = random_split(len(starts), cfg.split, cfg.seed)
+        idx = split_windows(starts, T)
         pipe = FeaturePipeline(schema, cfg.target, standardize_target=True)
         pipe.fit(take(table, window_rows(starts[idx[0]], T)))
         X, y = pipe.transform(table)
@@ -90,7 +99,7 @@ def prepare(cfg) -> Prepared:
     if cfg.model == "cnn":
         L, O = cfg.cnn_input_len, cfg.cnn_outputs
         starts = window_starts(n, L + O, ids)
-        idx = random_split(len(starts), cfg.split, cfg.seed)
+        idx = split_windows(starts, L + O)
         pipe = FeaturePipeline(schema, cfg.target, standardize_target=True)
         pipe.fit(take(table, window_rows(starts[idx[0]], L + O)))
         y = pipe.target_values(table)

@@ -111,12 +111,12 @@ def test_synthetic_batches_are_finite_and_learnable_scale():
 
 
 def test_sequence_pipeline_fits_on_training_windows_only():
-    """LSTM/CNN windows are split at random; scaling statistics and vocabularies must come
-    from the rows the TRAINING windows cover (SURVEY.md A.1 #3), not from the whole file."""
+    """LSTM/CNN windows are split in time blocks; scaling statistics and vocabularies must
+    come from the rows the TRAINING windows cover (SURVEY.md A.1 #3), not the whole file."""
     import numpy as np
 
     from wellflow.config import parse_argv
-    from wellflow.data.features import take, window_rows, window_starts, random_split
+    from wellflow.data.features import take, time_block_split, window_rows, window_starts
     from wellflow.data.pipeline import _group_ids, _sort_by_group, prepare
     from wellflow.data.io import load_table
     from wellflow.data.schema import parse_schema
@@ -131,11 +131,51 @@ def test_sequence_pipeline_fits_on_training_windows_only():
     ids, _ = _group_ids(table, schema, "")
     table, ids = _sort_by_group(table, ids, schema)
     starts = window_starts(len(ids), 16, ids)
-    train_rows = window_rows(starts[random_split(len(starts), cfg.split, cfg.seed)[0]], 16)
+    tr, va, te = time_block_split(starts, 16, ids, cfg.split, cfg.seed)
+    train_rows = window_rows(starts[tr], 16)
     assert len(train_rows) < len(ids)  # some rows are only in val/test windows
     y_train = np.asarray(take(table, train_rows)["flow"], np.float32)
     assert abs(prep.pipeline.y_mean - float(y_train.mean())) < 1e-4
-    assert len(prep.train[0]) + len(prep.val[0]) + len(prep.test[0]) == len(starts)
+    assert (len(prep.train[0]), len(prep.val[0]), len(prep.test[0])) == (len(tr), len(va), len(te))
+
+
+@pytest.mark.parametrize("span", [1, 7, 16, 64])
+def test_time_block_split_has_no_row_leak(span):
+    """Round-1 advice: overlapping stride-1 windows split at random leak test rows into
+    training. With the time-block split no row of a val/test window (inputs AND target) lies
+    inside any training window, and no test row inside a val window; proportions hold."""
+    import numpy as np
+
+    from wellflow.data.features import time_block_split, window_rows, window_starts
+
+    # 40 rows: too short to cut at every span -> assigned whole; the others are cut in time
+    g = np.repeat(np.arange(5), [400, 250, 900, 600, 40])
+    starts = window_starts(len(g), span, g)
+    tr, va, te = time_block_split(starts, span, g)
+    assert len(np.intersect1d(tr, va)) == len(np.intersect1d(tr, te)) == len(np.intersect1d(va, te)) == 0
+    rows_tr, rows_va, rows_te = (set(window_rows(starts[i], span).tolist()) for i in (tr, va, te))
+    assert not (rows_tr & rows_va) and not (rows_tr & rows_te) and not (rows_va & rows_te)
+    n = len(tr) + len(va) + len(te)
+    assert abs(len(tr) / n - 0.64) < 0.03 and abs(len(te) / n - 0.2) < 0.03
+    # three short series only: each split gets one whole series
+    g3 = np.repeat(np.arange(3), [30, 30, 30])
+    st3 = window_starts(len(g3), 20, g3)
+    parts = time_block_split(st3, 20, g3)
+    assert all(len(p) for p in parts) and len(set(g3[st3[np.concatenate(parts)]])) == 3
+    for k in range(5):  # time order inside every series: train < val < test
+        sel = lambda ix: ix[g[starts[ix]] == k]  # noqa: E731
+        a, b, c = sel(tr), sel(va), sel(te)
+        if len(b) and len(c):
+            assert a.max() < b.min() and b.max() < c.min()
+
+
+def test_random_window_split_still_available():
+    from wellflow.config import parse_argv
+
+    names = "well,field,t,whp,choke,glr,temp,water_cut,dsp,flow"
+    types = "string,string,int,float,float,float,float,float,float,float"
+    cfg = parse_argv("lstm", [names, types, "flow", "/tmp/x/", "--window-split", "random"])
+    assert cfg.window_split == "random"
 
 
 def test_series_windows_match_materialised_windows():
