@@ -139,9 +139,12 @@ class NativeMLP:
         bf = torch.bfloat16
         self.Fp = _r8(n_features)
         self.X = torch.zeros(batch * self.Fp, dtype=bf, device=dev)
-        # read bf16 streamed batches in place instead of one D2D copy into self.X: A/B at 100
-        # steps x 3 was within run-to-run noise (558 vs 571 M rows/s), so off by default
-        self.x_inplace = os.environ.get("WELLFLOW_MLP_X_INPLACE", "0") != "0"
+        # read bf16 batches (streamed ring slots, bf16 resident datasets gathered per step) in
+        # place instead of one D2D copy into self.X (WELLFLOW_MLP_X_INPLACE=0: always copy)
+        self.x_inplace = os.environ.get("WELLFLOW_MLP_X_INPLACE", "1") != "0"
+        # the MFMA input format: the Trainer keeps resident datasets in it (half the bytes of
+        # fp32, and the per-step gather IS the engine's input: no cast kernel)
+        self.input_dtype = torch.bfloat16 if self.Fp == n_features else torch.float32
         self._Xop = self.X  # the X operand of the current step (self.X or a bf16 batch read in place)
         self.Hs = [torch.empty(batch * h, dtype=bf, device=dev) for h in self.hidden]
         self.dZ = [torch.empty(batch * h, dtype=bf, device=dev) for h in self.hidden]

@@ -106,7 +106,7 @@ def run_config(cfg: RunConfig, log=print) -> dict:
     say("\nTime elapsed: %f s" % elapsed)  # cnn.py:133 (py3-correct)
     say("Testing set loss: %f" % test_loss)  # cnn.py:134
     result = {
-        "model": cfg.model, "native": native, "world_size": ctx.world_size,
+        "model": cfg.model, "native": native, "world_size": ctx.world_size, "n_features": prepared.n_features,
         "epochs": trainer.epoch, "steps": trainer.global_step, "elapsed": elapsed,
         "test_loss": test_loss, "test_mse": test_mse,
         "best_val_loss": trainer.stopper.best, "history": trainer.history.__dict__,

@@ -223,7 +223,9 @@ class Trainer:
             idx = self._idx[b] = torch.zeros(b, dtype=torch.long, device=eng.device)
 
         def inputs(_k):
-            return Xd[idx], Yd[idx]
+            if torch.is_tensor(Xd):  # row gather (index_select: one coalesced kernel per tensor)
+                return Xd.index_select(0, idx), Yd.index_select(0, idx)
+            return Xd[idx], Yd.index_select(0, idx)
 
         run = self._runner(("resident", id(Xd), id(Yd)), inputs, b)
         run.take_loss()
@@ -254,6 +256,9 @@ class Trainer:
         dev = self.eng.device
         # resident dataset in device memory (288 GB HBM: the small well-log sets fit whole)
         Xd, Yd = _to_dev(Xtr, dev), _to_dev(Ytr, dev)
+        in_dt = getattr(self.eng, "input_dtype", None)
+        if in_dt is not None and torch.is_tensor(Xd) and Xd.dtype != in_dt:
+            Xd = Xd.to(in_dt)  # engine input format (NativeMLP: bf16, read in place)
         n = len(Xd)
         b = self._local_batch(n)
         per_rank = n // max(ctx.world_size, 1)

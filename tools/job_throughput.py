@@ -1,0 +1,66 @@
+#!/usr/bin/env python3
+"""Steady-state training throughput of the PRODUCTION job path (train/job.py -> Trainer ->
+StepRunner) at the bench's per-GPU batch, next to bench.py's number for the same step.
+
+    python tools/job_throughput.py [--model lstm|mlp] [--out profiles/r2/job_vs_bench_lstm.json]
+
+The job trains on a synthetic well-log table (CSV-free: the generator stands in for the
+ingest) through feature engineering, the time-block split, the resident dataset with
+per-step index gathers, evaluation and checkpointing; rows/s is the Trainer's own per-epoch
+figure (train steps only, history.rows_per_s) from the epochs after the first (the first
+holds the two eager steps and the graph capture).
+"""
+import argparse
+import json
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+NAMES = "well,field,t,whp,choke,glr,temp,water_cut,dsp,flow"
+TYPES = "string,string,int,float,float,float,float,float,float,float"
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--model", default="lstm", choices=["lstm", "mlp"])
+    ap.add_argument("--epochs", type=int, default=4)
+    ap.add_argument("--out", default=None)
+    a = ap.parse_args()
+    from wellflow.config import parse_argv
+    from wellflow.train.job import run_config
+
+    if a.model == "lstm":
+        batch, extra, wells, steps = 8192, ["--seq-len", "64", "--hidden", "512"], 6, 40000
+    else:
+        batch, extra, wells, steps = 262144, [], 6, 640000
+    # 6 wells (3 fields): 5 + 2 one-hot columns + 9 continuous = 16 features, the bench's F
+    argv = [NAMES, TYPES, "flow", "/tmp/wellflow_jobtp/", "--epochs", str(a.epochs), "--patience", "100",
+            "--synth-wells", str(wells), "--synth-steps", str(steps), "--batch-size", str(batch),
+            "--device", "cuda", "--verbose", "0"] + extra
+    cfg = parse_argv(a.model, argv)
+    out = run_config(cfg, log=lambda *x, **k: None)
+    from wellflow.data.pipeline import prepare  # noqa: F401  (feature count reported below)
+    rps = out["history"]["rows_per_s"]
+    steady = rps[1:] if len(rps) > 1 else rps
+    job = max(steady)
+    bench = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--model", a.model, "--batch", str(batch),
+                            "--steps", "20", "--warmup", "5"], capture_output=True, text=True, cwd=ROOT)
+    line = [ln for ln in bench.stdout.splitlines() if ln.startswith("{")]
+    b = json.loads(line[-1])["value"] if line else None
+    rec = {"model": a.model, "per_gpu_batch": batch, "job_rows_per_s_per_epoch": rps,
+           "job_steady_rows_per_s": job, "bench_rows_per_s": b,
+           "job_over_bench": None if not b else job / b, "steps": out["steps"], "epochs": out["epochs"],
+           "native": out["native"], "n_features": out.get("n_features"),
+           "data": f"synthetic well-log table {wells} wells x {steps} steps"}
+    print(json.dumps(rec), flush=True)
+    if a.out:
+        os.makedirs(os.path.dirname(a.out) or ".", exist_ok=True)
+        with open(a.out, "w") as f:
+            json.dump(rec, f, indent=1)
+
+
+if __name__ == "__main__":
+    main()
