@@ -413,16 +413,40 @@ static unsigned* mask_ptr(const c10::optional<at::Tensor>& M2, int64_t B) {
   return reinterpret_cast<unsigned*>(M2->data_ptr<int>());
 }
 
-bool mlp2_backward(const at::Tensor& H1, const at::Tensor& H2, const at::Tensor& dy, const at::Tensor& w3,
+static const long long* rows_ptr(const c10::optional<at::Tensor>& rows, int64_t B) {
+  if (!rows.has_value() || !rows->defined()) return nullptr;
+  TORCH_CHECK(rows->is_cuda() && rows->scalar_type() == at::kLong && rows->is_contiguous(), "rows: contiguous int64 GPU tensor");
+  TORCH_CHECK(rows->numel() >= B, "rows: needs ", B, " indices");
+  return reinterpret_cast<const long long*>(rows->data_ptr<int64_t>());
+}
+
+// X rows read by a kernel: B rows directly, or dataset rows named by `rows`. Returns the
+// dataset row count; the kernels CLAMP every index into [0, nrows) (an out-of-range index
+// must never become an out-of-bounds device read, and checking here would need a host sync,
+// which a captured hipGraph step cannot do).
+static int64_t check_x_rows(const at::Tensor& X, int64_t Fp, int64_t B, const c10::optional<at::Tensor>& rows) {
+  if (!rows.has_value() || !rows->defined()) {
+    check_extent(X, B * Fp, "X");
+    return B;
+  }
+  const int64_t nrows = X.numel() / Fp;
+  TORCH_CHECK(nrows > 0, "X: empty dataset");
+  return nrows;
+}
+
+bool mlp2_backward(c10::optional<at::Tensor> H1, const at::Tensor& H2, const at::Tensor& dy, const at::Tensor& w3,
                    const at::Tensor& W2, const at::Tensor& X, int64_t Fp, const at::Tensor& dZ1,
                    const at::Tensor& dZ2, c10::optional<at::Tensor> dW1, const at::Tensor& db1,
                    const at::Tensor& db2, const at::Tensor& dw3, const at::Tensor& db3, int64_t B,
-                   c10::optional<at::Tensor> M2) {
+                   c10::optional<at::Tensor> M2, c10::optional<at::Tensor> W1, c10::optional<at::Tensor> b1,
+                   c10::optional<at::Tensor> rows) {
   constexpr int64_t H = 256;
-  for (const at::Tensor* t : {&H1, &H2, &dZ1, &dZ2}) {
+  const bool recompute = !H1.has_value() || !H1->defined();
+  std::vector<const at::Tensor*> acts = {&H2, &dZ1, &dZ2};
+  if (!recompute) acts.push_back(&*H1);
+  for (const at::Tensor* t : acts) {
     check_t(*t, at::kBFloat16, "H/dZ");
     check_extent(*t, B * H, "H/dZ");
-    TORCH_CHECK(reinterpret_cast<uintptr_t>(t->data_ptr()) % 16 == 0, "mlp2_backward: activations must be 16-B aligned");
   }
   check_t(W2, at::kBFloat16, "W2");
   check_extent(W2, H * H, "W2");
@@ -435,12 +459,33 @@ bool mlp2_backward(const at::Tensor& H1, const at::Tensor& H2, const at::Tensor&
   check_t(db3, at::kFloat, "db3");
   check_extent(db3, 1, "db3");
   check_t(X, at::kBFloat16, "X");
-  check_extent(X, B * Fp, "X");
-  TORCH_CHECK(reinterpret_cast<uintptr_t>(X.data_ptr()) % 16 == 0, "mlp2_backward: X must be 16-B aligned");
-  const c10::hip::OptionalHIPGuardMasqueradingAsCUDA guard(H1.device());
-  return wf::launch_mlp2_bwd(bfp(H1), bfp(H2), mask_ptr(M2, B), fp(dy), fp(w3), bfp(W2), bfp(X), (int)Fp, bfp(dZ1), bfp(dZ2),
-                             opt_ptr<float>(dW1, at::kFloat, "dW1", H * Fp), fp(db1), fp(db2), fp(dw3), fp(db3),
-                             (int)B, cur_stream());
+  const int64_t nrows = check_x_rows(X, Fp, B, rows);
+  const bf16_t* w1p = opt_ptr<bf16_t>(W1, at::kBFloat16, "W1", H * Fp);
+  const float* b1p = opt_ptr<float>(b1, at::kFloat, "b1", H);
+  TORCH_CHECK(!recompute || (w1p && b1p && dW1.has_value()), "mlp2_backward: H1 recompute needs W1, b1 and dW1");
+  const c10::hip::OptionalHIPGuardMasqueradingAsCUDA guard(H2.device());
+  return wf::launch_mlp2_bwd(recompute ? nullptr : bfp(*H1), bfp(H2), mask_ptr(M2, B), fp(dy), fp(w3), bfp(W2), bfp(X),
+                             (int)Fp, bfp(dZ1), bfp(dZ2), opt_ptr<float>(dW1, at::kFloat, "dW1", H * Fp), fp(db1),
+                             fp(db2), fp(dw3), fp(db3), (int)B, w1p, b1p, rows_ptr(rows, B), nrows, cur_stream());
+}
+
+// dW2 [256][256] += dZ2^T relu(X W1^T + b1), H1 recomputed (mlp_fused.hip mlp2_dw2_kernel).
+bool mlp2_dw2(const at::Tensor& dZ2, const at::Tensor& X, int64_t Fp, c10::optional<at::Tensor> rows,
+              const at::Tensor& W1, const at::Tensor& b1, int64_t B, int64_t nsplit, const at::Tensor& dW2) {
+  constexpr int64_t H = 256;
+  check_t(dZ2, at::kBFloat16, "dZ2");
+  check_extent(dZ2, B * H, "dZ2");
+  check_t(X, at::kBFloat16, "X");
+  const int64_t nrows = check_x_rows(X, Fp, B, rows);
+  check_t(W1, at::kBFloat16, "W1");
+  check_extent(W1, H * Fp, "W1");
+  check_t(b1, at::kFloat, "b1");
+  check_extent(b1, H, "b1");
+  check_t(dW2, at::kFloat, "dW2");
+  check_extent(dW2, H * H, "dW2");
+  const c10::hip::OptionalHIPGuardMasqueradingAsCUDA guard(dZ2.device());
+  return wf::launch_mlp2_dw2(bfp(dZ2), bfp(X), (int)Fp, rows_ptr(rows, B), nrows, bfp(W1), fp(b1), (int)B, (int)nsplit,
+                             fp(dW2), cur_stream());
 }
 
 // Fused MLP forward (mlp_fused.hip): both 256-wide hidden layers + head (+ MSE) in one launch.
@@ -448,13 +493,13 @@ bool mlp2_backward(const at::Tensor& H1, const at::Tensor& H2, const at::Tensor&
 // per-layer GEMMs + head kernel.
 bool mlp2_forward(const at::Tensor& X, int64_t Fp, const at::Tensor& W1, const at::Tensor& b1,
                   const at::Tensor& W2, const at::Tensor& b2, const at::Tensor& w3, const at::Tensor& b3,
-                  c10::optional<at::Tensor> y, const at::Tensor& H1, const at::Tensor& H2,
+                  c10::optional<at::Tensor> y, c10::optional<at::Tensor> H1, const at::Tensor& H2,
                   const at::Tensor& pred, c10::optional<at::Tensor> dy, c10::optional<at::Tensor> loss_sum,
                   double dy_scale, int64_t B, c10::optional<at::Tensor> M2,
-                  c10::optional<at::Tensor> dw3, c10::optional<at::Tensor> db3) {
+                  c10::optional<at::Tensor> dw3, c10::optional<at::Tensor> db3, c10::optional<at::Tensor> rows) {
   constexpr int64_t H = 256;
   check_t(X, at::kBFloat16, "X");
-  check_extent(X, B * Fp, "X");
+  const int64_t nrows = check_x_rows(X, Fp, B, rows);
   check_t(W1, at::kBFloat16, "W1");
   check_extent(W1, H * Fp, "W1");
   check_t(W2, at::kBFloat16, "W2");
@@ -464,22 +509,22 @@ bool mlp2_forward(const at::Tensor& X, int64_t Fp, const at::Tensor& W1, const a
     check_extent(*t, H, "bias/w3");
   }
   check_t(b3, at::kFloat, "b3");
-  check_t(H1, at::kBFloat16, "H1");
-  check_extent(H1, B * H, "H1");
+  bf16_t* h1p = opt_ptr<bf16_t>(H1, at::kBFloat16, "H1", B * H);
   check_t(H2, at::kBFloat16, "H2");
   check_extent(H2, B * H, "H2");
   check_t(pred, at::kFloat, "pred");
   check_extent(pred, B, "pred");
-  for (const at::Tensor* t : {&X, &W1, &W2, &H1, &H2})
+  for (const at::Tensor* t : {&X, &W1, &W2, &H2})
     TORCH_CHECK(reinterpret_cast<uintptr_t>(t->data_ptr()) % 16 == 0, "mlp2_forward: bf16 operands must be 16-B aligned");
+  const int64_t ny = nrows;  // y is indexed like X
   const c10::hip::OptionalHIPGuardMasqueradingAsCUDA guard(X.device());
   return wf::launch_mlp2_fwd(bfp(X), (int)Fp, bfp(W1), fp(b1), bfp(W2), fp(b2), fp(w3), fp(b3),
-                             opt_ptr<float>(y, at::kFloat, "y", B), bfp(H1), bfp(H2), mask_ptr(M2, B),
+                             opt_ptr<float>(y, at::kFloat, "y", ny), h1p, bfp(H2), mask_ptr(M2, B),
                              opt_ptr<float>(dw3, at::kFloat, "dw3", H), opt_ptr<float>(db3, at::kFloat, "db3", 1),
                              fp(pred),
                              opt_ptr<float>(dy, at::kFloat, "dy", B),
                              opt_ptr<float>(loss_sum, at::kFloat, "loss_sum", 1), (float)dy_scale, (int)B,
-                             cur_stream());
+                             rows_ptr(rows, B), nrows, cur_stream());
 }
 
 void head_bwd_w(const at::Tensor& Hm, int64_t ldh, int64_t B, int64_t Hd, const at::Tensor& dy,
@@ -652,6 +697,7 @@ PYBIND11_MODULE(_C, m) {
   WF_DEF(gemm);
   WF_DEF(mlp2_forward);
   WF_DEF(mlp2_backward);
+  WF_DEF(mlp2_dw2);
   WF_DEF(lstm_pack_x);
   WF_DEF(lstm_forward);
   WF_DEF(lstm_forward_persistent);

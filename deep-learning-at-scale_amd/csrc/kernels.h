@@ -73,7 +73,7 @@ void launch_lstm_pack_weights(const float* W, bf16_t* Wp, bf16_t* WhhT, LstmDims
 bool launch_mlp2_fwd(const bf16_t* X, int Fp, const bf16_t* W1, const float* b1, const bf16_t* W2, const float* b2,
                      const float* w3, const float* b3, const float* y, bf16_t* H1, bf16_t* H2, unsigned* M2,
                      float* dw3, float* db3, float* pred, float* dy, float* loss_sum, float dy_scale, int B,
-                     hipStream_t s);
+                     const long long* rows, long nrows, hipStream_t s);
 // Mask mode (M2 != nullptr; needs y, dw3, db3): H2 is NOT written — only its ReLU bitmask M2
 // ([B][8] u32, bit u of row r = word 8r + u / 32, bit u % 32) — and dw3 += H2^T dy,
 // db3 += sum dy are accumulated by the forward itself.
@@ -84,7 +84,13 @@ bool launch_mlp2_fwd(const bf16_t* X, int Fp, const bf16_t* W1, const float* b1,
 // M2 != nullptr: ReLU mask of layer 2 from the forward's bitmask (H2 unused) and no dw3 / db3.
 bool launch_mlp2_bwd(const bf16_t* H1, const bf16_t* H2, const unsigned* M2, const float* dy, const float* w3, const bf16_t* W2,
                      const bf16_t* X, int Fp, bf16_t* dZ1, bf16_t* dZ2, float* dW1, float* db1, float* db2,
-                     float* dw3, float* db3, int B, hipStream_t s);
+                     float* dw3, float* db3, int B, const bf16_t* W1, const float* b1, const long long* rows,
+                     long nrows, hipStream_t s);
+// H1 == nullptr: recompute H1 from X with W1 / b1 (needs dW1 != nullptr, i.e. Fp <= 32);
+// rows != nullptr: dataset row indices of X (and y in the forward) per batch row.
+// dW2 += dZ2^T relu(X W1^T + b1) with H1 recomputed per chunk (B % 64 == 0, Fp <= 32)
+bool launch_mlp2_dw2(const bf16_t* dZ2, const bf16_t* X, int Fp, const long long* rows, long nrows, const bf16_t* W1,
+                     const float* b1, int B, int nsplit, float* dW2, hipStream_t s);
 
 // ---- regression head (N = 1) and losses ----
 void launch_head_fwd(const bf16_t* Hm, long ldh, int B, int Hd, const float* w, const float* b0,

@@ -26,6 +26,13 @@ namespace wf {
 
 namespace {
 constexpr int MF_ROWS = 64;  // rows per chunk
+// dataset row of batch row gr (indices clamped into the dataset: never an out-of-bounds read)
+__device__ __forceinline__ size_t data_row(const long long* rows, int gr, long nrows) {
+  if (rows == nullptr) return (size_t)gr;
+  long long r = rows[gr];
+  r = r < 0 ? 0 : (r >= nrows ? nrows - 1 : r);
+  return (size_t)r;
+}
 constexpr int MF_H = 256;    // hidden width (both layers)
 
 // [64 rows][256 units] bf16 tile, 16-B chunk c (units 8c..8c+7) of row r at chunk c ^ (r & 15)
@@ -48,7 +55,11 @@ __global__ __launch_bounds__(256, 1) void mlp2_fwd_kernel(
     const bf16_t* __restrict__ W2, const float* __restrict__ b2, const float* __restrict__ w3,
     const float* __restrict__ b3, const float* __restrict__ y, bf16_t* __restrict__ H1, bf16_t* __restrict__ H2,
     unsigned* __restrict__ M2, float* __restrict__ dw3, float* __restrict__ db3, float* __restrict__ pred,
-    float* __restrict__ dy, float* __restrict__ loss_sum, float dy_scale, int B) {
+    float* __restrict__ dy, float* __restrict__ loss_sum, float dy_scale, int B, const long long* __restrict__ rows,
+    long nrows) {
+  // rows != nullptr: batch row r is dataset row rows[r] of X / y (the resident dataset is read
+  // in place, no gather kernel); H1 == nullptr: H1 is not stored (the training step's backward
+  // recomputes it from X, inference never needs it)
   __shared__ __attribute__((aligned(16))) char xs[MF_ROWS * MF_XROW];
   __shared__ __attribute__((aligned(16))) char h1s[MF_ROWS * MF_H * 2];
   __shared__ __attribute__((aligned(16))) char h2s[MF_ROWS * MF_H * 2];
@@ -95,17 +106,33 @@ __global__ __launch_bounds__(256, 1) void mlp2_fwd_kernel(
   float lsum = 0.f;
 
   const int nchunks = (B + MF_ROWS - 1) / MF_ROWS;
-  for (int ch = blockIdx.x; ch < nchunks; ch += gridDim.x) {
-    const int row0 = ch * MF_ROWS;
-    // ---- X chunk -> LDS, zero-padded to 32 * KT1 features (thread: row t >> 2, chunk t & 3 (+4))
+  // the NEXT chunk's X row segment (thread: row t >> 2, chunk t & 3 (+4)) and target are loaded
+  // right after this chunk's X tile is in LDS, so their latency hides behind this chunk's MFMAs
+  // (one wave per SIMD: a load at the top of the chunk stalled every wave for its round trip)
+  uint4 xv[KT1];
+  float yv = 0.f;
+  auto prefetch = [&](int ch) {
+    const int r = threadIdx.x >> 2, gr = ch * MF_ROWS + r;
+    const size_t dr = gr < B ? data_row(rows, gr, nrows) : 0;
 #pragma unroll
     for (int k1 = 0; k1 < KT1; ++k1) {
-      const int r = threadIdx.x >> 2, c = (threadIdx.x & 3) + 4 * k1, gr = row0 + r;
-      uint4 v = make_uint4(0, 0, 0, 0);
-      if (gr < B && 8 * c + 8 <= Fp) v = *reinterpret_cast<const uint4*>(X + (size_t)gr * Fp + 8 * c);
-      *reinterpret_cast<uint4*>(xs + xtile_off(r, c)) = v;
+      const int c = (threadIdx.x & 3) + 4 * k1;
+      xv[k1] = (gr < B && 8 * c + 8 <= Fp) ? *reinterpret_cast<const uint4*>(X + dr * Fp + 8 * c)
+                                           : make_uint4(0, 0, 0, 0);
     }
+    const int ty = ch * MF_ROWS + (int)threadIdx.x;
+    if (y != nullptr && threadIdx.x < MF_ROWS && ty < B) yv = y[data_row(rows, ty, nrows)];
+  };
+  if ((int)blockIdx.x < nchunks) prefetch(blockIdx.x);
+  for (int ch = blockIdx.x; ch < nchunks; ch += gridDim.x) {
+    const int row0 = ch * MF_ROWS;
+    // ---- X chunk -> LDS, zero-padded to 32 * KT1 features
+#pragma unroll
+    for (int k1 = 0; k1 < KT1; ++k1)
+      *reinterpret_cast<uint4*>(xs + xtile_off(threadIdx.x >> 2, (threadIdx.x & 3) + 4 * k1)) = xv[k1];
+    const float ycur = yv;
     __syncthreads();
+    if (ch + (int)gridDim.x < nchunks) prefetch(ch + gridDim.x);
 
     // ---- layer 1: Z1^T (64 units x 64 rows per wave) = W1 x X^T, K = 32 * KT1
     f32x4 acc[4][4];
@@ -139,12 +166,14 @@ __global__ __launch_bounds__(256, 1) void mlp2_fwd_kernel(
     __syncthreads();
 
     // ---- H1 tile -> HBM (saved for the backward): 64 rows x 512 B, 16-B stores
+    if (H1 != nullptr) {
 #pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      const int idx = threadIdx.x + 256 * k, r = idx >> 5, c = idx & 31, gr = row0 + r;
-      if (gr < B)
-        *reinterpret_cast<uint4*>(H1 + (size_t)gr * MF_H + 8 * c) =
-            *reinterpret_cast<const uint4*>(h1s + tile_off(r, 8 * c));
+      for (int k = 0; k < 8; ++k) {
+        const int idx = threadIdx.x + 256 * k, r = idx >> 5, c = idx & 31, gr = row0 + r;
+        if (gr < B)
+          *reinterpret_cast<uint4*>(H1 + (size_t)gr * MF_H + 8 * c) =
+              *reinterpret_cast<const uint4*>(h1s + tile_off(r, 8 * c));
+      }
     }
 
     // ---- layer 2: Z2^T = W2 x H1^T, K = 256 (8 k-tiles)
@@ -223,7 +252,7 @@ __global__ __launch_bounds__(256, 1) void mlp2_fwd_kernel(
         const float p = red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] + red[3][threadIdx.x] + bias3;
         pred[gr] = p;
         if (y != nullptr) {
-          const float diff = p - y[gr];
+          const float diff = p - ycur;
           lsum += diff * diff;
           if (dy != nullptr) dy[gr] = dy_scale * diff;
           if (mask_mode) {
@@ -297,7 +326,12 @@ __global__ __launch_bounds__(256, 1) void mlp2_bwd_kernel(
     const float* __restrict__ dy,
     const float* __restrict__ w3, const bf16_t* __restrict__ W2, const bf16_t* __restrict__ X, int Fp,
     bf16_t* __restrict__ dZ1, bf16_t* __restrict__ dZ2, float* __restrict__ dW1, float* __restrict__ db1,
-    float* __restrict__ db2, float* __restrict__ dw3, float* __restrict__ db3, int B) {
+    float* __restrict__ db2, float* __restrict__ dw3, float* __restrict__ db3, int B,
+    const bf16_t* __restrict__ W1, const float* __restrict__ b1, const long long* __restrict__ rows, long nrows) {
+  // H1 == nullptr (needs the fused dW1 path, Fp <= 32): H1 is RECOMPUTED from the X tile with
+  // W1 / b1 in registers (8 extra MFMAs per wave and chunk) instead of being read back:
+  // the forward no longer writes it (134 MB at B = 262144) and nothing reads it.
+  // rows: dataset rows of X (as in the forward).
   __shared__ __attribute__((aligned(16))) char zs[MF_ROWS * MF_H * 2];  // dZ2 tile
   __shared__ __attribute__((aligned(16))) char hs[MF_ROWS * MF_H * 2];  // H1 tile -> dZ1 in place
   __shared__ __attribute__((aligned(16))) char xs[MF_ROWS * MF_XROW];   // X tile (dW1)
@@ -333,6 +367,23 @@ __global__ __launch_bounds__(256, 1) void mlp2_bwd_kernel(
 #pragma unroll
     for (int i = 0; i < 4; ++i) db1a[m][i] = 0.f;
   const bool fuse_dw1 = dW1 != nullptr;
+  const bool recompute = H1 == nullptr;
+  // layer-1 weights for the recompute (lane = unit u0 + 16m + l15, features 8g..8g+7) and
+  // biases (C rows: units u0 + 16m + 4g + r)
+  bf16x8 w1f[4];
+  float bias1[4][4];
+#pragma unroll
+  for (int m = 0; m < 4; ++m) {
+    w1f[m] = bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+    for (int r = 0; r < 4; ++r) bias1[m][r] = 0.f;
+    if (recompute) {
+      const int u = u0 + 16 * m + l15;
+      if (8 * g + 8 <= Fp) w1f[m] = *reinterpret_cast<const bf16x8*>(W1 + (size_t)u * Fp + 8 * g);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) bias1[m][r] = b1[u0 + 16 * m + 4 * g + r];
+    }
+  }
   f32x4 dw1a[4][NFT];
 #pragma unroll
   for (int m = 0; m < 4; ++m)
@@ -358,7 +409,7 @@ __global__ __launch_bounds__(256, 1) void mlp2_bwd_kernel(
           h2v = *reinterpret_cast<const uint4*>(H2 + (size_t)gr * MF_H + 8 * c);
         else
           mb = M2[(size_t)gr * 8 + (c >> 2)] >> (8 * (c & 3));
-        h1v = *reinterpret_cast<const uint4*>(H1 + (size_t)gr * MF_H + 8 * c);
+        if (!recompute) h1v = *reinterpret_cast<const uint4*>(H1 + (size_t)gr * MF_H + 8 * c);
         gy = dy[gr];
       }
       if (c == 0 && M2 == nullptr) db3a += gy;  // mask mode: the forward did the head gradients
@@ -386,16 +437,46 @@ __global__ __launch_bounds__(256, 1) void mlp2_bwd_kernel(
       }
       const uint4 zv = make_uint4(zw[0], zw[1], zw[2], zw[3]);
       *reinterpret_cast<uint4*>(zs + tile_off(r, 8 * c)) = zv;
-      *reinterpret_cast<uint4*>(hs + tile_off(r, 8 * c)) = h1v;
+      if (!recompute) *reinterpret_cast<uint4*>(hs + tile_off(r, 8 * c)) = h1v;
       if (gr < B) *reinterpret_cast<uint4*>(dZ2 + (size_t)gr * MF_H + 8 * c) = zv;
     }
     if (fuse_dw1) {  // X chunk -> LDS, zero-padded to 32 features (as in the forward)
       const int r = threadIdx.x >> 2, xc = threadIdx.x & 3, gr = row0 + r;
       uint4 v = make_uint4(0, 0, 0, 0);
-      if (gr < B && 8 * xc + 8 <= Fp) v = *reinterpret_cast<const uint4*>(X + (size_t)gr * Fp + 8 * xc);
+      if (gr < B && 8 * xc + 8 <= Fp) {
+        v = *reinterpret_cast<const uint4*>(X + data_row(rows, gr, nrows) * Fp + 8 * xc);
+      }
       *reinterpret_cast<uint4*>(xs + xtile_off(r, xc)) = v;
     }
     __syncthreads();
+    if (recompute) {
+      // ---- H1 of this wave's 64 units (the forward's layer 1, bit-identical inputs): each lane
+      // writes the 8 bytes the ReLU-mask phase below reads back (same lane, no barrier needed)
+      f32x4 a1[4][4];
+#pragma unroll
+      for (int m = 0; m < 4; ++m)
+#pragma unroll
+        for (int n = 0; n < 4; ++n) a1[m][n] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int n = 0; n < 4; ++n) {
+        const bf16x8 xb = *reinterpret_cast<const bf16x8*>(xs + xtile_off(16 * n + l15, g));
+#pragma unroll
+        for (int m = 0; m < 4; ++m) a1[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w1f[m], xb, a1[m][n], 0, 0, 0);
+      }
+#pragma unroll
+      for (int m = 0; m < 4; ++m)
+#pragma unroll
+        for (int n = 0; n < 4; ++n) {
+          unsigned pk[2];
+#pragma unroll
+          for (int q = 0; q < 2; ++q) {
+            const float v0 = fmaxf(a1[m][n][2 * q] + bias1[m][2 * q], 0.f);
+            const float v1 = fmaxf(a1[m][n][2 * q + 1] + bias1[m][2 * q + 1], 0.f);
+            pk[q] = (unsigned)f2bf(v0) | ((unsigned)f2bf(v1) << 16);
+          }
+          *reinterpret_cast<uint2*>(hs + tile_off(16 * n + l15, u0 + 16 * m + 4 * g)) = make_uint2(pk[0], pk[1]);
+        }
+    }
 
     // ---- dH1^T (64 k x 64 rows per wave) = W2^T x dZ2^T, K = 256
     f32x4 acc[4][4];
@@ -531,29 +612,446 @@ __global__ __launch_bounds__(256, 1) void mlp2_bwd_kernel(
   if (threadIdx.x == 0 && t3 != 0.f) atomicAdd(db3, t3);
 }
 
+// ----------------------------------------------------------------------------------------
+// The training-step backward in its leanest form (mask mode + H1 recompute + fused dW1: the
+// bench / job configuration, Fp <= 32): per 64-row chunk it reads only the H2 ReLU bits, dy and
+// the X rows, and writes only dZ2. Same math as mlp2_bwd_kernel (that kernel's comments
+// apply), organised for one wave per SIMD: the next chunk's bits, dy and X row segments are
+// loaded right after the current chunk's tiles are in LDS, so their round trip hides behind
+// this chunk's 152 MFMAs per wave instead of stalling every wave at the top of the chunk.
+template <int NFT>
+__global__ __launch_bounds__(256, 1) void mlp2_bwd_rc_kernel(
+    const unsigned* __restrict__ M2, const float* __restrict__ dy, const float* __restrict__ w3,
+    const bf16_t* __restrict__ W2, const bf16_t* __restrict__ X, int Fp, bf16_t* __restrict__ dZ2,
+    float* __restrict__ dW1, float* __restrict__ db1, float* __restrict__ db2, int B,
+    const bf16_t* __restrict__ W1, const float* __restrict__ b1, const long long* __restrict__ rows, long nrows) {
+  __shared__ __attribute__((aligned(16))) char zs[MF_ROWS * MF_H * 2];  // dZ2 tile
+  __shared__ __attribute__((aligned(16))) char hs[MF_ROWS * MF_H * 2];  // H1 tile -> dZ1 in place
+  __shared__ __attribute__((aligned(16))) char xs[MF_ROWS * MF_XROW];   // X tile
+
+  const int lane = threadIdx.x & 63, l15 = lane & 15, g = lane >> 4;
+  const int wid = threadIdx.x >> 6;
+  const int u0 = wid * 64;
+  bf16x8 wt[4][8];  // W2^T (A operand: lane = input unit k = u0 + 16m + l15, K = output unit)
+  bf16x8 w1f[4];    // W1 rows of this wave's units (recompute)
+  float bias1[4][4];
+#pragma unroll
+  for (int m = 0; m < 4; ++m) {
+    const int k = u0 + 16 * m + l15;
+#pragma unroll
+    for (int kt = 0; kt < 8; ++kt)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) wt[m][kt][j] = (short)W2[(size_t)(32 * kt + 8 * g + j) * MF_H + k];
+    w1f[m] = 8 * g + 8 <= Fp ? *reinterpret_cast<const bf16x8*>(W1 + (size_t)k * Fp + 8 * g)
+                             : bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+    for (int r = 0; r < 4; ++r) bias1[m][r] = b1[u0 + 16 * m + 4 * g + r];
+  }
+  const int c = threadIdx.x & 31, rq = threadIdx.x >> 5;  // elementwise phase: units 8c.., rows rq + 8q
+  float w3c[8], db2a[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    w3c[e] = w3[8 * c + e];
+    db2a[e] = 0.f;
+  }
+  float db1a[4][4];
+#pragma unroll
+  for (int m = 0; m < 4; ++m)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) db1a[m][i] = 0.f;
+  f32x4 dw1a[4][NFT];
+#pragma unroll
+  for (int m = 0; m < 4; ++m)
+#pragma unroll
+    for (int f = 0; f < NFT; ++f) dw1a[m][f] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int tq = (lane & 15) >> 2, tp = lane & 3;
+
+  // prefetched inputs of one chunk: ReLU bits of units 8c..8c+7 and dy for rows rq + 8q, and
+  // this thread's X row segment (row t >> 2, feature chunk t & 3)
+  unsigned mb[8];
+  float gyv[8];
+  uint4 xv;
+  auto prefetch = [&](int ch) {
+    const int row0 = ch * MF_ROWS;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const int gr = row0 + rq + 8 * q;
+      mb[q] = gr < B ? M2[(size_t)gr * 8 + (c >> 2)] : 0u;
+      gyv[q] = gr < B ? dy[gr] : 0.f;
+    }
+    const int xr = threadIdx.x >> 2, xc = threadIdx.x & 3, gr = row0 + xr;
+    xv = (gr < B && 8 * xc + 8 <= Fp) ? *reinterpret_cast<const uint4*>(X + data_row(rows, gr, nrows) * Fp + 8 * xc)
+                                      : make_uint4(0, 0, 0, 0);
+  };
+  const int nchunks = (B + MF_ROWS - 1) / MF_ROWS;
+  if ((int)blockIdx.x < nchunks) prefetch(blockIdx.x);
+  for (int ch = blockIdx.x; ch < nchunks; ch += gridDim.x) {
+    const int row0 = ch * MF_ROWS;
+    // ---- dZ2 = (dy w3^T) * [H2 > 0] -> LDS + HBM (dW2's operand); db2 partials
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const int r = rq + 8 * q, gr = row0 + r;
+      const unsigned bits = mb[q] >> (8 * (c & 3));
+      unsigned zw[4];
+#pragma unroll
+      for (int p = 0; p < 4; ++p) {
+        unsigned pk = 0;
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const int e = 2 * p + h;
+          const bf16_t zb = f2bf(((bits >> e) & 1u) ? gyv[q] * w3c[e] : 0.f);
+          db2a[e] += bf2f(zb);
+          pk |= (unsigned)zb << (16 * h);
+        }
+        zw[p] = pk;
+      }
+      const uint4 zv = make_uint4(zw[0], zw[1], zw[2], zw[3]);
+      *reinterpret_cast<uint4*>(zs + tile_off(r, 8 * c)) = zv;
+      if (gr < B) *reinterpret_cast<uint4*>(dZ2 + (size_t)gr * MF_H + 8 * c) = zv;
+    }
+    *reinterpret_cast<uint4*>(xs + xtile_off(threadIdx.x >> 2, threadIdx.x & 3)) = xv;
+    __syncthreads();
+    if (ch + (int)gridDim.x < nchunks) prefetch(ch + gridDim.x);
+
+    // ---- H1 of this wave's units (bit-identical to the forward's layer 1) -> hs, own lanes only
+    {
+      f32x4 a1[4][4];
+#pragma unroll
+      for (int n = 0; n < 4; ++n) {
+        const bf16x8 xb = *reinterpret_cast<const bf16x8*>(xs + xtile_off(16 * n + l15, g));
+#pragma unroll
+        for (int m = 0; m < 4; ++m)
+          a1[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w1f[m], xb, f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+      }
+#pragma unroll
+      for (int m = 0; m < 4; ++m)
+#pragma unroll
+        for (int n = 0; n < 4; ++n) {
+          unsigned pk[2];
+#pragma unroll
+          for (int q = 0; q < 2; ++q) {
+            const float v0 = fmaxf(a1[m][n][2 * q] + bias1[m][2 * q], 0.f);
+            const float v1 = fmaxf(a1[m][n][2 * q + 1] + bias1[m][2 * q + 1], 0.f);
+            pk[q] = (unsigned)f2bf(v0) | ((unsigned)f2bf(v1) << 16);
+          }
+          *reinterpret_cast<uint2*>(hs + tile_off(16 * n + l15, u0 + 16 * m + 4 * g)) = make_uint2(pk[0], pk[1]);
+        }
+    }
+    // ---- dH1^T (64 k x 64 rows per wave) = W2^T x dZ2^T, K = 256
+    f32x4 acc[4][4];
+#pragma unroll
+    for (int m = 0; m < 4; ++m)
+#pragma unroll
+      for (int n = 0; n < 4; ++n) acc[m][n] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int kt = 0; kt < 8; ++kt) {
+      bf16x8 zb[4];
+#pragma unroll
+      for (int n = 0; n < 4; ++n) zb[n] = *reinterpret_cast<const bf16x8*>(zs + tile_off(16 * n + l15, 32 * kt + 8 * g));
+#pragma unroll
+      for (int m = 0; m < 4; ++m)
+#pragma unroll
+        for (int n = 0; n < 4; ++n)
+          acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wt[m][kt], zb[n], acc[m][n], 0, 0, 0);
+    }
+    // ---- dZ1 = dH1 * [H1 > 0] into the same 8 bytes of hs; db1 partials
+#pragma unroll
+    for (int m = 0; m < 4; ++m)
+#pragma unroll
+      for (int n = 0; n < 4; ++n) {
+        const int r = 16 * n + l15;
+        uint2* pp = reinterpret_cast<uint2*>(hs + tile_off(r, u0 + 16 * m + 4 * g));
+        const uint2 hv = *pp;
+        const unsigned hw2[2] = {hv.x, hv.y};
+        unsigned ow[2];
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+          unsigned pk = 0;
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            const int i = 2 * q + h;
+            const bool on = bf2f((bf16_t)(hw2[q] >> (16 * h))) > 0.f && row0 + r < B;
+            const bf16_t vb = f2bf(on ? acc[m][n][i] : 0.f);
+            db1a[m][i] += bf2f(vb);
+            pk |= (unsigned)vb << (16 * h);
+          }
+          ow[q] = pk;
+        }
+        *pp = make_uint2(ow[0], ow[1]);
+      }
+    __syncthreads();
+    // ---- dW1^T slice (64 units x Fp per wave) += dZ1^T X over the chunk's rows
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      bf16x8 af[4], bfr[NFT];
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int r = 32 * kk + 8 * g + 4 * h + tq;
+#pragma unroll
+        for (int m = 0; m < 4; ++m) {
+          const bf16x4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_bf16x4*)(hs + tile_off(r, u0 + 16 * m + 4 * tp)));
+#pragma unroll
+          for (int e = 0; e < 4; ++e) af[m][4 * h + e] = v[e];
+        }
+#pragma unroll
+        for (int f = 0; f < NFT; ++f) {
+          const int f0 = 16 * f + 4 * tp;
+          const bf16x4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+              (lds_bf16x4*)(xs + xtile_off(r, f0 >> 3) + ((f0 & 7) << 1)));
+#pragma unroll
+          for (int e = 0; e < 4; ++e) bfr[f][4 * h + e] = v[e];
+        }
+      }
+#pragma unroll
+      for (int m = 0; m < 4; ++m)
+#pragma unroll
+        for (int f = 0; f < NFT; ++f)
+          dw1a[m][f] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[m], bfr[f], dw1a[m][f], 0, 0, 0);
+    }
+    __syncthreads();  // zs / hs / xs are rewritten by the next chunk
+  }
+  // ---- reductions (as mlp2_bwd_kernel)
+#pragma unroll
+  for (int m = 0; m < 4; ++m)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      float v = db1a[m][i];
+      v += __shfl_xor(v, 1, 64);
+      v += __shfl_xor(v, 2, 64);
+      v += __shfl_xor(v, 4, 64);
+      v += __shfl_xor(v, 8, 64);
+      if (l15 == 0 && v != 0.f) atomicAdd(db1 + u0 + 16 * m + 4 * g + i, v);
+    }
+#pragma unroll
+  for (int m = 0; m < 4; ++m)
+#pragma unroll
+    for (int f = 0; f < NFT; ++f) {
+      const int ft = l15 + 16 * f;
+      if (ft < Fp)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) atomicAdd(dW1 + (size_t)(u0 + 16 * m + 4 * g + i) * Fp + ft, dw1a[m][f][i]);
+    }
+  float* sd = reinterpret_cast<float*>(zs);
+#pragma unroll
+  for (int e = 0; e < 8; ++e) sd[rq * MF_H + 8 * c + e] = db2a[e];
+  __syncthreads();
+  float s2 = 0.f;
+#pragma unroll
+  for (int q = 0; q < 8; ++q) s2 += sd[q * MF_H + threadIdx.x];
+  if (s2 != 0.f) atomicAdd(db2 + threadIdx.x, s2);
+}
+
+// ----------------------------------------------------------------------------------------
+// dW2 += dZ2^T H1 with H1 = relu(X W1^T + b1) RECOMPUTED per 64-row chunk instead of being
+// stored by the forward and re-read here (the generic split-K GEMM read H1 [B][256] twice:
+// 268 MB at B = 262144). Per chunk a workgroup streams its dZ2 columns (MN-contiguous image,
+// LDS-DMA) and the 64 X rows (LDS-DMA per-lane gather, so `rows` indirection costs nothing),
+// rebuilds its 128 H1 units from the X tile with W1 in registers (8 MFMAs per wave), writes
+// them straight into the MN-contiguous image the dW MFMAs read (gemm_core.h swizzle), and
+// accumulates the 128 x 128 output tile in registers (32 MFMAs per wave per chunk).
+//  * grid = 4 output tiles x nsplit row ranges (one workgroup per CU at nsplit = 64); the 4
+//    tiles of one row range are consecutive logical ids, so xcd_remap puts them on one XCD
+//    and the second reader of each dZ2 chunk hits L2.
+//  * 3-stage ring of {dZ2 16 KB, X 4 KB}, two barriers per chunk, counted vmcnt.
+//  * X padding: features >= Fp are multiplied by zero W1 columns; their lanes DMA a valid
+//    chunk of the same row (finite values), never out-of-bounds memory.
+constexpr int DW2_STAGES = 4;
+constexpr int DW2_MAX_ROWS = 8192;  // rows per workgroup (the LDS row-id table)
+__global__ __launch_bounds__(256, 1) void mlp2_dw2_kernel(const bf16_t* __restrict__ dZ2, const bf16_t* __restrict__ X,
+                                                          int Fp, const long long* __restrict__ rows, long nrows,
+                                                          const bf16_t* __restrict__ W1, const float* __restrict__ b1,
+                                                          int kchunk, float* __restrict__ dW2) {
+  constexpr int BM = 128, BN = 128;
+  using C = GemmCfg<BM, BN, MN_CONTIG, MN_CONTIG>;
+  using QA = GldsTile<BM, MN_CONTIG, 256>;
+  constexpr int ABYTES = QA::BYTES;           // 16 KB: [64 rows][128 units]
+  constexpr int XBYTES = MF_ROWS * 64;        // 4 KB: [64 rows][4 x 16-B feature chunks]
+  constexpr int SLOT = ABYTES + XBYTES;
+  constexpr int HIMG = BN * 64 * 2;           // one H1 image [64 rows][128 units], 16 KB
+  constexpr int HOFF = DW2_STAGES * SLOT;     // two H1 images (chunk c read while c + 1 is built)
+  constexpr int LPT = QA::PER_WAVE + 1;       // DMA instructions per wave per chunk
+  constexpr int ROFF = HOFF + 2 * HIMG;       // dataset row ids of the range (int32), read from
+                                              // LDS: a global index load would join the vmcnt
+                                              // queue and drain the DMA prefetch
+  __shared__ __attribute__((aligned(16))) char smem[ROFF + DW2_MAX_ROWS * 4];
+  const int lane = threadIdx.x & 63, l15 = lane & 15, g = lane >> 4;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wm = wid >> 1, wn = wid & 1;
+  const int L = xcd_remap(blockIdx.x, gridDim.x);
+  const int split = L >> 2, t = L & 3;
+  const int m0 = (t >> 1) * BM, n0 = (t & 1) * BN;
+  const int kbeg = split * kchunk;
+  const int nk = kchunk / MF_ROWS;
+  int* ridx = reinterpret_cast<int*>(smem + ROFF);
+  if (rows != nullptr) {
+    for (int i = threadIdx.x; i < kchunk; i += 256) ridx[i] = (int)data_row(rows, kbeg + i, nrows);
+    __syncthreads();
+  }
+
+  // recompute operands: this wave builds H1 units n0 + 32 wid .. + 31 (2 tiles of 16)
+  bf16x8 w1f[2];
+  float bias1[2][4];
+#pragma unroll
+  for (int mt = 0; mt < 2; ++mt) {
+    const int u = n0 + 32 * wid + 16 * mt + l15;
+    w1f[mt] = 8 * g + 8 <= Fp ? *reinterpret_cast<const bf16x8*>(W1 + (size_t)u * Fp + 8 * g)
+                              : bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+    for (int r = 0; r < 4; ++r) bias1[mt][r] = b1[n0 + 32 * wid + 16 * mt + 4 * g + r];
+  }
+  // X gather: lane -> tile row 16 wid + (lane >> 2), LDS chunk slot lane & 3 holding feature
+  // chunk (slot ^ ((row >> 2) & 3)) (conflict-free fragment reads below)
+  const int xrow = 16 * wid + (lane >> 2);
+  int xc = (lane & 3) ^ ((xrow >> 2) & 3);
+  if (8 * xc + 8 > Fp) xc = 0;  // padding: any finite chunk of the same row (W1 there is 0)
+  auto issue = [&](int c, int slot) {
+    char* st = smem + slot * SLOT;
+    QA::issue(dZ2, MF_H, m0, kbeg + c * MF_ROWS, st, wid, lane);
+    const size_t xr = rows != nullptr ? (size_t)ridx[c * MF_ROWS + xrow] : (size_t)(kbeg + c * MF_ROWS + xrow);
+    __builtin_amdgcn_global_load_lds((const void*)(X + xr * Fp + 8 * xc),
+                                     (lds_void*)(st + ABYTES + wid * 1024), 16, 0, 0);
+  };
+  using SW = MnSwz<BN>;
+  // H1 = relu(X W1^T + b1) of chunk c (X in ring slot) -> H1 image `img` (MN-contiguous operand:
+  // element (k = chunk row, n) of the dW GEMM's B operand)
+  auto recompute = [&](int slot, int img) {
+    const char* st = smem + slot * SLOT;
+    f32x4 a1[2][4];
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) {
+      const int r = 16 * nt + l15;
+      const bf16x8 xb = *reinterpret_cast<const bf16x8*>(st + ABYTES + r * 64 + ((g ^ ((r >> 2) & 3)) << 4));
+#pragma unroll
+      for (int mt = 0; mt < 2; ++mt)
+        a1[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w1f[mt], xb, f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+    }
+    const unsigned hbase = (unsigned)(uintptr_t)((__attribute__((address_space(3))) char*)(smem + HOFF + img * HIMG));
+#pragma unroll
+    for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt) {
+        const int r = 16 * nt + l15;
+        unsigned pk[2];
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+          const float v0 = fmaxf(a1[mt][nt][2 * q] + bias1[mt][2 * q], 0.f);
+          const float v1 = fmaxf(a1[mt][nt][2 * q + 1] + bias1[mt][2 * q + 1], 0.f);
+          pk[q] = (unsigned)f2bf(v0) | ((unsigned)f2bf(v1) << 16);
+        }
+        const unsigned off = r * (BN * 2) + (SW::pos(2 * wid + mt, SW::hk(r)) << 5) + 8 * g;
+        // LDS writes in asm: compiler-visible ones get a vmcnt(0) guard behind the LDS-DMA
+        asm volatile("ds_write_b64 %0, %1" ::"v"(hbase + off), "v"(make_uint2(pk[0], pk[1])) : "memory");
+      }
+  };
+  FragReader<BM, MN_CONTIG, 64> fa;
+  FragReader<BN, MN_CONTIG, 64> fb;
+  fa.init(wm * 64, lane);
+  fb.init(wn * 64, lane);
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // prologue: chunks 0..2 in flight, H1 of chunk 0 built
+  issue(0, 0);
+  if (nk > 1) issue(1, 1);
+  if (nk > 2) issue(2, 2);
+  if (nk > 2) wait_vmcnt<2 * LPT>(); else if (nk > 1) wait_vmcnt<LPT>(); else wait_vmcnt<0>();
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+  recompute(0, 0);
+
+  // chunk c: [wait chunk c+1's DMA, barrier] issue c+3 | build H1(c+1) | dW MFMAs of c
+  auto body = [&](int c, auto sc) {
+    constexpr int S = decltype(sc)::value;  // == c % 4 (ring slot of chunk c); H1 image c & 1
+    if (c + 2 < nk) wait_vmcnt<LPT>(); else wait_vmcnt<0>();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's H1 image writes
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (c + 3 < nk) issue(c + 3, (S + 3) % DW2_STAGES);
+    if (c + 1 < nk) recompute((S + 1) % DW2_STAGES, (S + 1) & 1);
+    static_for<0, 2>([&](auto kc) {
+      constexpr int KK = decltype(kc)::value;
+      bf16x8 a[4], b[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) a[i] = fa.template frag<KK, S * SLOT>(smem, i);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) b[j] = fb.template frag<KK, HOFF + (S & 1) * HIMG>(smem, j);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
+    });
+  };
+  int c = 0;
+  for (; c + 4 <= nk; c += 4) {
+    body(c, std::integral_constant<int, 0>{});
+    body(c + 1, std::integral_constant<int, 1>{});
+    body(c + 2, std::integral_constant<int, 2>{});
+    body(c + 3, std::integral_constant<int, 3>{});
+  }
+  if (c < nk) body(c, std::integral_constant<int, 0>{});
+  if (c + 1 < nk) body(c + 1, std::integral_constant<int, 1>{});
+  if (c + 2 < nk) body(c + 2, std::integral_constant<int, 2>{});
+  const AccCoord<C> cc(m0, n0);
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) atomicAdd(dW2 + (size_t)cc.row(i, r) * MF_H + cc.col(j), acc[i][j][r]);
+}
+
+// dW2 [256][256] fp32 (atomics: zeroed or accumulating) from dZ2 [B][256], X rows (rows), W1, b1.
+// Needs B % 64 == 0 and Fp <= 32 (one K = 32 layer-1 step); false = not covered.
+bool launch_mlp2_dw2(const bf16_t* dZ2, const bf16_t* X, int Fp, const long long* rows, long nrows, const bf16_t* W1,
+                     const float* b1, int B, int nsplit, float* dW2, hipStream_t s) {
+  if (B <= 0 || B % MF_ROWS != 0 || Fp > 32 || Fp % 8 != 0) return false;
+  const int chunks = B / MF_ROWS;
+  if (nsplit < 1) nsplit = 1;
+  while (nsplit > 1 && chunks % nsplit != 0) --nsplit;
+  const int kchunk = (chunks / nsplit) * MF_ROWS;
+  if (rows != nullptr && kchunk > DW2_MAX_ROWS) return false;
+  hipLaunchKernelGGL(mlp2_dw2_kernel, dim3(4 * nsplit), dim3(256), 0, s, dZ2, X, Fp, rows, nrows, W1, b1, kchunk, dW2);
+  return true;
+}
+
 bool launch_mlp2_bwd(const bf16_t* H1, const bf16_t* H2, const unsigned* M2, const float* dy, const float* w3, const bf16_t* W2,
                      const bf16_t* X, int Fp, bf16_t* dZ1, bf16_t* dZ2, float* dW1, float* db1, float* db2,
-                     float* dw3, float* db3, int B, hipStream_t s) {
+                     float* dw3, float* db3, int B, const bf16_t* W1, const float* b1, const long long* rows,
+                     long nrows, hipStream_t s) {
   if (B <= 0 || (dW1 != nullptr && (X == nullptr || Fp > 32 || Fp % 8 != 0))) return false;
+  if (H1 == nullptr && (dW1 == nullptr || W1 == nullptr || b1 == nullptr)) return false;  // recompute needs the X tile
+  if (rows != nullptr && dW1 == nullptr) return false;  // X is read only by the fused dW1 path
   const int nchunks = (B + MF_ROWS - 1) / MF_ROWS;
   int dev = 0, cus = 0;
   if (hipGetDevice(&dev) != hipSuccess ||
       hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
     cus = 256;
   const int grid = nchunks < cus ? nchunks : cus;
+  if (H1 == nullptr && M2 != nullptr && dW1 != nullptr) {  // the training step's configuration
+    if (Fp <= 16)
+      hipLaunchKernelGGL(mlp2_bwd_rc_kernel<1>, dim3(grid), dim3(256), 0, s, M2, dy, w3, W2, X, Fp, dZ2, dW1, db1, db2,
+                         B, W1, b1, rows, nrows);
+    else
+      hipLaunchKernelGGL(mlp2_bwd_rc_kernel<2>, dim3(grid), dim3(256), 0, s, M2, dy, w3, W2, X, Fp, dZ2, dW1, db1, db2,
+                         B, W1, b1, rows, nrows);
+    return true;
+  }
   if (Fp <= 16)
     hipLaunchKernelGGL(mlp2_bwd_kernel<1>, dim3(grid), dim3(256), 0, s, H1, H2, M2, dy, w3, W2, X, Fp, dZ1, dZ2, dW1,
-                       db1, db2, dw3, db3, B);
+                       db1, db2, dw3, db3, B, W1, b1, rows, nrows);
   else
     hipLaunchKernelGGL(mlp2_bwd_kernel<2>, dim3(grid), dim3(256), 0, s, H1, H2, M2, dy, w3, W2, X, Fp, dZ1, dZ2, dW1,
-                       db1, db2, dw3, db3, B);
+                       db1, db2, dw3, db3, B, W1, b1, rows, nrows);
   return true;
 }
 
 bool launch_mlp2_fwd(const bf16_t* X, int Fp, const bf16_t* W1, const float* b1, const bf16_t* W2, const float* b2,
                      const float* w3, const float* b3, const float* y, bf16_t* H1, bf16_t* H2, unsigned* M2,
                      float* dw3, float* db3, float* pred, float* dy, float* loss_sum, float dy_scale, int B,
-                     hipStream_t s) {
+                     const long long* rows, long nrows, hipStream_t s) {
   if (Fp > 64 || Fp % 8 != 0 || B <= 0) return false;
   if (M2 != nullptr && (y == nullptr || dw3 == nullptr || db3 == nullptr)) return false;
   const int nchunks = (B + MF_ROWS - 1) / MF_ROWS;
@@ -564,10 +1062,10 @@ bool launch_mlp2_fwd(const bf16_t* X, int Fp, const bf16_t* W1, const float* b1,
   const int grid = nchunks < cus ? nchunks : cus;
   if (Fp <= 32)
     hipLaunchKernelGGL(mlp2_fwd_kernel<1>, dim3(grid), dim3(256), 0, s, X, Fp, W1, b1, W2, b2, w3, b3, y, H1, H2,
-                       M2, dw3, db3, pred, dy, loss_sum, dy_scale, B);
+                       M2, dw3, db3, pred, dy, loss_sum, dy_scale, B, rows, nrows);
   else
     hipLaunchKernelGGL(mlp2_fwd_kernel<2>, dim3(grid), dim3(256), 0, s, X, Fp, W1, b1, W2, b2, w3, b3, y, H1, H2,
-                       M2, dw3, db3, pred, dy, loss_sum, dy_scale, B);
+                       M2, dw3, db3, pred, dy, loss_sum, dy_scale, B, rows, nrows);
   return true;
 }
 

@@ -120,6 +120,7 @@ class NativeMLP:
     """HIP/MFMA MLP regression engine for batches of up to ``batch`` rows."""
 
     native = True
+    row_indexed = True  # forward_backward(..., rows=) reads dataset rows in place
 
     def __init__(self, n_features: int, hidden=(256, 256), batch: int = 4096, device="cuda",
                  params: torch.Tensor | None = None, grads: torch.Tensor | None = None,
@@ -161,14 +162,50 @@ class NativeMLP:
         self.dw_ksplit = int(os.environ.get("WELLFLOW_MLP_DW_KSPLIT", "0"))
         self.dw_tile = int(os.environ.get("WELLFLOW_MLP_DW_TILE", "0"))
         self.M2 = torch.zeros(batch * 8, dtype=torch.int32, device=dev) if self.hidden == (256, 256) else None
+        # H1 never stored: recomputed from X in the backward and the dW2 kernel (WELLFLOW_MLP_RECOMPUTE=0: store)
+        self.recompute_h1 = os.environ.get("WELLFLOW_MLP_RECOMPUTE", "1") != "0"
+        self.dw2_split = int(os.environ.get("WELLFLOW_MLP_DW2_SPLIT", "64"))
+        # dW2 = dZ2^T H1 as the generic split-K GEMM over a STORED H1 (the forward writes it)
+        # instead of the H1-recomputing kernel (WELLFLOW_MLP_DW2=gemm)
+        self.dw2_gemm = os.environ.get("WELLFLOW_MLP_DW2", "recompute") == "gemm"
         self.sync_weights()
 
     def sync_weights(self) -> None:
         self._C.cast_bf16(self.params, self.shadow)
 
+    def _step_recompute(self, Xop, y, rows, grad_scale: float, zero_grads: bool) -> torch.Tensor:
+        """fused forward (H2 -> bitmask, head gradients) -> fused backward (dZ2, dZ1, dW1, biases;
+        H1 recomputed) -> dW2 with H1 recomputed: three launches, activations never in HBM
+        except dZ2."""
+        C = self._C
+        B = rows.shape[0] if rows is not None else self._Xop_rows
+        if zero_grads:
+            self.grads.zero_()
+        self.loss_sum.zero_()
+        wl, _, _ = self.lay.views(self.shadow)
+        pl, hw, hb = self.lay.views(self.params)
+        gl, ghw, ghb = self.lay.views(self.grads)
+        self._Xop = Xop
+        if not self._fused_forward(B, y, self.dy, self.loss_sum, 2.0 * float(grad_scale), (ghw, ghb),
+                                   store_h1=self.dw2_gemm, rows=rows):
+            raise RuntimeError("NativeMLP: fused forward refused the recompute step")
+        ok = C.mlp2_backward(None, self.Hs[1], self.dy, hw, wl[1][0], Xop, self.Fp, self.dZ[0], self.dZ[1],
+                             gl[0][0], gl[0][1], gl[1][1], ghw, ghb, B, self.M2, wl[0][0], pl[0][1], rows)
+        if self.dw2_gemm:
+            from ..ops.native import gemm
+
+            gemm(self.dZ[1], self.Hs[0], 256, 256, B, a_mn=True, lda=256, b_mn=True, ldb=256, outF=gl[1][0],
+                 atomic=True, ksplit=max(1, min(64, B // 256)))
+        else:
+            ok = ok and C.mlp2_dw2(self.dZ[1], Xop, self.Fp, rows, wl[0][0], pl[0][1], B, self.dw2_split, gl[1][0])
+        if not ok:
+            raise RuntimeError("NativeMLP: recompute backward refused (shape)")
+        return self.loss_sum
+
     def _load_x(self, x: torch.Tensor) -> int:
         B = x.shape[0]
         assert B <= self.B and x.shape[1] == self.F
+        self._Xop_rows = B
         self._Xop = self.X
         Xv = self.X[: B * self.Fp].view(B, self.Fp)
         if (self.x_inplace and x.dtype == torch.bfloat16 and self.Fp == self.F and x.is_contiguous()
@@ -196,21 +233,22 @@ class NativeMLP:
             A, K = Hout, h
 
     def _fused_forward(self, B: int, y=None, dy=None, loss_sum=None, dy_scale: float = 0.0,
-                       head_grads=None) -> bool:
+                       head_grads=None, store_h1: bool = True, rows=None) -> bool:
         """Both hidden layers + head (+ MSE) in ONE weight-stationary launch
-        (csrc/mlp_fused.hip) for the BASELINE shape F -> 256 -> 256 -> 1; False = not covered."""
+        (csrc/mlp_fused.hip) for the BASELINE shape F -> 256 -> 256 -> 1; False = not covered.
+        ``store_h1=False``: H1 is not written (inference, or a backward that recomputes it)."""
         if not self.fused or self.hidden != (256, 256) or self.Fp > 64:
             return False
         wl, _, _ = self.lay.views(self.shadow)
         pl, hw, hb = self.lay.views(self.params)
         m2, dw3, db3 = (self.M2, *head_grads) if head_grads is not None else (None, None, None)
         return bool(self._C.mlp2_forward(self._Xop, self.Fp, wl[0][0], pl[0][1], wl[1][0], pl[1][1], hw, hb, y,
-                                         self.Hs[0], self.Hs[1], self.pred, dy, loss_sum, float(dy_scale), B,
-                                         m2, dw3, db3))
+                                         self.Hs[0] if store_h1 else None, self.Hs[1], self.pred, dy, loss_sum,
+                                         float(dy_scale), B, m2, dw3, db3, rows))
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         B = self._load_x(x)
-        if self._fused_forward(B):
+        if self._fused_forward(B, store_h1=False):
             return self.pred[:B]
         self._forward_body(B)
         _, hw, hb = self.lay.views(self.params)
@@ -218,12 +256,29 @@ class NativeMLP:
         self._C.head_fwd(self.Hs[-1], H, B, H, hw, hb, None, self.pred, None, None, 0.0)
         return self.pred[:B]
 
+    def _recompute_ok(self, B: int) -> bool:
+        """The H1-free training step: fused forward writes only the H2 bitmask, the fused
+        backward and the dW2 kernel recompute H1 = relu(X W1^T + b1) from X (csrc/mlp_fused.hip)."""
+        return (self.recompute_h1 and self.fused and self.fused_bwd and self.mask_h2 and self.hidden == (256, 256)
+                and self.loss_kind == "mse" and self.Fp <= 32 and B % 64 == 0)
+
     def forward_backward(self, x: torch.Tensor, y: torch.Tensor, grad_scale: float,
-                         zero_grads: bool = True, step: int = 0) -> torch.Tensor:
+                         zero_grads: bool = True, step: int = 0, rows: torch.Tensor | None = None) -> torch.Tensor:
+        """``rows`` (int64, device): train on dataset rows ``x[rows]``, ``y[rows]`` — the fused
+        kernels read the resident dataset through the index (no gather launch); other paths
+        gather first."""
         from ..ops.native import gemm
 
         C = self._C
+        if rows is not None:
+            B = rows.shape[0]
+            if (self._recompute_ok(B) and x.dtype == torch.bfloat16 and x.is_contiguous() and x.shape[1] == self.Fp
+                    and x.data_ptr() % 16 == 0 and B <= self.B):
+                return self._step_recompute(x.view(-1), y.contiguous().float(), rows, grad_scale, zero_grads)
+            x, y = x.index_select(0, rows), y.index_select(0, rows)
         B = self._load_x(x)
+        if self._recompute_ok(B):
+            return self._step_recompute(self._Xop, y.contiguous().float(), None, grad_scale, zero_grads)
         if zero_grads:
             self.grads.zero_()
         self.loss_sum.zero_()
@@ -257,7 +312,7 @@ class NativeMLP:
         fused_bwd = (self.fused_bwd and self.hidden == (256, 256) and
                      C.mlp2_backward(self.Hs[0], self.Hs[1], self.dy, hw, wl[1][0], self._Xop, self.Fp,
                                      self.dZ[0], self.dZ[1], gl[0][0] if fused_dw1 else None, gl[0][1],
-                                     gl[1][1], ghw, ghb, B, self.M2 if use_mask else None))
+                                     gl[1][1], ghw, ghb, B, self.M2 if use_mask else None, None, None, None))
         if use_mask and not fused_bwd:
             raise RuntimeError("NativeMLP: H2 bitmask written but the fused backward did not launch")
         if not fused_bwd:

@@ -34,7 +34,9 @@ def _env_flag(name: str, default: bool) -> bool:
 class StepRunner:
     def __init__(self, eng, opt, ctx, grad_scale: float, inputs, *, graph: bool | None = None,
                  comm_in_graph: bool | None = None, eager_steps: int = 2, accumulate_loss: bool = True):
-        """``inputs(key) -> (x, y)``: the step's batch on the engine's device for slot ``key``."""
+        """``inputs(key) -> (x, y)``: the step's batch on the engine's device for slot ``key``;
+        or ``(X, Y, rows)``: a resident dataset and this step's row indices, for engines with
+        ``row_indexed = True`` (their kernels gather the rows themselves)."""
         self.eng, self.opt, self.ctx = eng, opt, ctx
         self.grad_scale = float(grad_scale)
         self.inputs = inputs
@@ -55,8 +57,13 @@ class StepRunner:
 
     # ------------------------------------------------------------------ pieces
     def _compute(self, key):
-        x, y = self.inputs(key)
-        ls = self.eng.forward_backward(x, y, self.grad_scale, zero_grads=not self.fused_clear)
+        inp = self.inputs(key)
+        if len(inp) == 3:  # (dataset X, dataset y, row indices): the engine reads rows in place
+            x, y, rows = inp
+            ls = self.eng.forward_backward(x, y, self.grad_scale, zero_grads=not self.fused_clear, rows=rows)
+        else:
+            x, y = inp
+            ls = self.eng.forward_backward(x, y, self.grad_scale, zero_grads=not self.fused_clear)
         if self.loss_acc is not None:
             self.loss_acc += ls
 

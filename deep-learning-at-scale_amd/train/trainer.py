@@ -222,7 +222,11 @@ class Trainer:
         if idx is None:
             idx = self._idx[b] = torch.zeros(b, dtype=torch.long, device=eng.device)
 
+        row_indexed = getattr(eng, "row_indexed", False) and torch.is_tensor(Xd)
+
         def inputs(_k):
+            if row_indexed:  # the engine's kernels read the rows through the index
+                return Xd, Yd, idx
             if torch.is_tensor(Xd):  # row gather (index_select: one coalesced kernel per tensor)
                 return Xd.index_select(0, idx), Yd.index_select(0, idx)
             return Xd[idx], Yd.index_select(0, idx)

@@ -222,3 +222,56 @@ def test_mlp_bf16_input_matches_fp32_input():
     # fp32 atomics in the split-K dW reduce in a run-dependent order: compare with a tolerance
     assert abs(la - lb) <= 1e-5 * abs(la) + 1e-6
     assert ((ga - gb).norm() / ga.norm()).item() < 1e-5
+
+
+@pytest.mark.parametrize("B,F", [(262144, 16), (4096, 32), (128, 8)])
+def test_mlp_recompute_step_matches_stored_h1(B, F):
+    """The H1-free training step (fused forward writes only the H2 bitmask; the fused backward
+    and the dW2 kernel recompute H1 from X, csrc/mlp_fused.hip) against the step that stores
+    and re-reads H1 with the generic split-K dW2 GEMM: same loss, same gradients up to the
+    fp32 summation order."""
+    from wellflow.data.synth import synth_tabular_batch
+    from wellflow.models.mlp import NativeMLP, init_mlp_flat
+
+    eng = NativeMLP(F, (256, 256), B, device=DEV)
+    eng.params.copy_(init_mlp_flat(F, (256, 256), seed=8).to(DEV))
+    eng.sync_weights()
+    x, y = synth_tabular_batch(B, F, seed=9)
+    x, y = x.to(DEV), y.to(DEV)
+    out = {}
+    for rec in (False, True):
+        eng.recompute_h1 = rec
+        eng.Hs[0].fill_(float("nan")) if rec else None  # recompute must not read a stored H1
+        ls = eng.forward_backward(x, y, grad_scale=1.0 / B).item()
+        torch.cuda.synchronize()
+        out[rec] = (ls, eng.pred[:B].clone(), eng.grads.clone())
+    assert eng._recompute_ok(B)
+    (la, pa, ga), (lb, pb, gb) = out[False], out[True]
+    assert torch.equal(pa, pb)
+    assert abs(la - lb) <= 1e-5 * abs(la) + 1e-7
+    assert torch.isfinite(gb).all()
+    assert ((ga - gb).norm() / ga.norm()).item() < 1e-4
+
+
+def test_mlp_row_indexed_step_matches_gathered_batch():
+    """forward_backward(dataset, targets, rows=idx) reads the resident dataset through the
+    index inside the fused kernels; it must equal the step on the explicitly gathered batch
+    (the Trainer's job path uses it, train/trainer.py)."""
+    from wellflow.data.synth import synth_tabular_batch
+    from wellflow.models.mlp import NativeMLP, init_mlp_flat
+
+    N, B, F = 100000, 16384, 16
+    eng = NativeMLP(F, (256, 256), B, device=DEV)
+    eng.params.copy_(init_mlp_flat(F, (256, 256), seed=10).to(DEV))
+    eng.sync_weights()
+    X, Y = synth_tabular_batch(N, F, seed=11)
+    X, Y = X.to(DEV).to(torch.bfloat16), Y.to(DEV)
+    idx = torch.randperm(N, device=DEV)[:B]
+    ls_a = eng.forward_backward(X.index_select(0, idx), Y.index_select(0, idx), 1.0 / B).item()
+    torch.cuda.synchronize()
+    pa, ga = eng.pred[:B].clone(), eng.grads.clone()
+    ls_b = eng.forward_backward(X, Y, 1.0 / B, rows=idx).item()
+    torch.cuda.synchronize()
+    assert torch.equal(pa, eng.pred[:B])
+    assert abs(ls_a - ls_b) <= 1e-5 * abs(ls_a)
+    assert ((ga - eng.grads).norm() / ga.norm()).item() < 1e-4
