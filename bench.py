@@ -182,7 +182,12 @@ def bench_mlp(args, ctx, online: bool):
     opt = FlatAdam(eng.params, eng.grads, lr=args.lr, shadow=eng.shadow, zero_grads=True)
     gscale = 1.0 / (B * ctx.world_size)
     graph = not args.no_graph
+    extra = {}
     if online:
+        from wellflow.utils.numa import bind_to_gpu_numa
+
+        # pinned ring pages on the GPU's NUMA node (utils/numa.py), before anything is pinned
+        extra["numa_bound_cpus"] = len(bind_to_gpu_numa(ctx.device.index or 0))
         # features cross PCIe as bf16 (the engine's MFMA input format: identical numerics to
         # streaming fp32 and casting on the device, half the bytes); targets stay fp32
         x_dtype = torch.float32 if args.stream_fp32 else torch.bfloat16
@@ -201,7 +206,7 @@ def bench_mlp(args, ctx, online: bool):
         run = StepRunner(eng, opt, ctx, gscale, lambda k: (x, y), graph=graph, comm_in_graph=not args.eager_comm)
         step = run.run
     el = _timed(ctx, step, args.steps, args.warmup)
-    return el, B, model, float(eng.loss_sum.item()) / B, run, eng, {}
+    return el, B, model, float(eng.loss_sum.item()) / B, run, eng, extra
 
 
 def main() -> int:

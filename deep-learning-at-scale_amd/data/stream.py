@@ -51,6 +51,7 @@ class DeviceStreamer:
         self.used = 0      # batches handed to the consumer
         self.last_slot = 0
         self.src = None
+        self._pinned = {}  # id(tensor) -> tensor, sources already known to be pinned (no per-step query)
         self._primed = False
         self._exhausted = False
         if source is not None:
@@ -64,6 +65,8 @@ class DeviceStreamer:
         self.k = self.used = 0
 
     def _host(self, x, y, slot):
+        if id(x) in self._pinned and id(y) in self._pinned and self.x_dtype in (None, x.dtype):
+            return x, y  # a pinned batch seen before (HostPool cycles a fixed set)
         x = torch.as_tensor(x)
         if x.dtype == torch.float64:
             x = x.float()
@@ -71,6 +74,8 @@ class DeviceStreamer:
             x = x.to(self.x_dtype)
         y = torch.as_tensor(y).float()
         if x.is_pinned() and y.is_pinned():
+            if len(self._pinned) < 256:
+                self._pinned[id(x)], self._pinned[id(y)] = x, y  # keeps them alive: ids stay unique
             return x, y
         while len(self.staging) <= slot:
             self.staging.append([None, None])

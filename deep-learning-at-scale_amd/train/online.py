@@ -73,7 +73,9 @@ def fit_online(trainer, train, val):
     streamer = None
     if streamed:
         from ..data.stream import DeviceStreamer
+        from ..utils.numa import bind_to_gpu_numa
 
+        bind_to_gpu_numa(eng.device.index or 0)  # pinned staging ring next to the GPU's PCIe root
         streamer = DeviceStreamer(None, eng.device, depth=3)
     k = 0
     for p in range(passes):
