@@ -75,7 +75,7 @@ void launch_head_fwd(const bf16_t* Hm, long ldh, int B, int Hd, const float* w, 
   const int rpb = 256 / lpr;
   int grid = (B + rpb - 1) / rpb;
   // one same-address loss atomic per block: cap the grid. LSTM head (B = 8192, Hd = 512,
-  // kernel trace, tools/gpu_head_sweep.sh): 30.8 us at 2048 blocks, 18.3 at 1024, 13.4 at 512,
+  // kernel trace, tools/gpu.sh ksweep WELLFLOW_HEAD_GRID): 30.8 us at 2048 blocks, 18.3 at 1024, 13.4 at 512,
   // 14.0 at 256 — the atomics serialise, not the loads (WELLFLOW_HEAD_GRID overrides)
   static const int cap = [] {
     const char* e = std::getenv("WELLFLOW_HEAD_GRID");
@@ -161,7 +161,7 @@ void launch_head_bwd_w(const bf16_t* Hm, long ldh, int B, int Hd, const float* d
   const HeadBwdGeom g = head_geom(Hd);
   int grid = (B + g.rg - 1) / g.rg;
   // per-column atomics per block: cap the grid. LSTM head (B = 8192, Hd = 512, kernel trace,
-  // tools/gpu_headw_sweep.sh): 16.2 us at 512 blocks, 11.0 at 256, 10.3 at 128, 13.6 at 64
+  // tools/gpu.sh ksweep WELLFLOW_HEADW_GRID): 16.2 us at 512 blocks, 11.0 at 256, 10.3 at 128, 13.6 at 64
   // (WELLFLOW_HEADW_GRID overrides)
   static const int cap = [] {
     const char* e = std::getenv("WELLFLOW_HEADW_GRID");

@@ -158,7 +158,7 @@ class NativeMLP:
         # training step with both fused kernels: H2 leaves the forward only as a ReLU bitmask
         # (32 B per row instead of 512 B) and the head gradients are taken in the forward
         self.mask_h2 = os.environ.get("WELLFLOW_MLP_MASK", "1") != "0"
-        # weight-gradient GEMM overrides (tools/gpu_mlp_dw.sh sweep): split-K depth, tile (ops.native.gemm)
+        # weight-gradient GEMM overrides (tools/gpu.sh sweep WELLFLOW_MLP_DW_KSPLIT ...): split-K depth, tile (ops.native.gemm)
         self.dw_ksplit = int(os.environ.get("WELLFLOW_MLP_DW_KSPLIT", "0"))
         self.dw_tile = int(os.environ.get("WELLFLOW_MLP_DW_TILE", "0"))
         self.M2 = torch.zeros(batch * 8, dtype=torch.int32, device=dev) if self.hidden == (256, 256) else None
@@ -328,7 +328,7 @@ class NativeMLP:
             prevH = self.Hs[l - 1] if l > 0 else self._Xop
             # dW_l = dZ_l^T H_{l-1}   (reduce over the batch; MN-contiguous operands)
             # ... but keep the fp32 atomic traffic (ksplit x h x k x 4 B) <= ~16 MB. 256 x 256 at
-            # B = 262144: split-K 64 = 256 workgroups, one per CU (tools/gpu_mlp_dw.sh sweep:
+            # B = 262144: split-K 64 = 256 workgroups, one per CU (tools/gpu.sh sweep:
             # 0.421 ms/step at split-K 32 -> 0.390 at 64, 0.404 at 128)
             ksplit = max(1, min(512 // tiles(h, k), B // 256, 64, (16 << 20) // (4 * h * k)))
             if self.dw_ksplit > 0:

@@ -8,7 +8,7 @@ wall clock around fit, cnn.py:126-133).
 * :class:`StepTimer` — device-event timing of named phases, aggregated per phase
   (used by tools and the trainer's ``--profile`` summaries).
 * kernel-level evidence comes from ``rocprofv3 --kernel-trace --stats`` and ``--pmc``
-  (tools/gpu_prof.sh, tools/gpu_pmc.sh), summarised into profiles/.
+  (tools/gpu.sh prof / pmc / pmcsets), summarised into profiles/.
 """
 from __future__ import annotations
 
