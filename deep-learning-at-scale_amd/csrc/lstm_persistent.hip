@@ -90,8 +90,6 @@ __global__ __launch_bounds__(256, 1) void lstm_fwd_persistent_kernel(
   gu32* sticky = (gu32*)(sync);
   gu32* cnt = (gu32*)(sync + 16 + 16 * m);
   const unsigned spin_limit = d.spin_limit ? d.spin_limit : PF_SPIN_LIMIT;
-  // XH as a buffer resource for the 16-B sc1 h stores (byte offsets < 2^31: checked on the host)
-  const __amdgpu_buffer_rsrc_t xh_rsrc = __builtin_amdgcn_make_buffer_rsrc(XH, 0, 0x7FFFFFFF, 0x00020000);
   // DBG & 16: timeline stamps (s_memrealtime, 100 MHz) of step PF_STAMP_T, wave 0 lane 0 of
   // every workgroup, into sync + 4096 words (64 slots per workgroup; diagnostics only)
   constexpr int PF_STAMP_T = 10;
@@ -184,7 +182,11 @@ __global__ __launch_bounds__(256, 1) void lstm_fwd_persistent_kernel(
     float* cnext = Cst + (size_t)(t + 1) * Bp * H + (size_t)(rb >> 4) * HB * 256;
     bf16_t* St = S + (size_t)t * Bp * G + (size_t)(rb >> 4) * HB * 1024;
     const char* abase = reinterpret_cast<const char*>(XH + ((size_t)t * d.B + rb) * KA) + aoff;
-    const int hsoff = (int)((((size_t)(t + 1) * d.B + rb) * KA + 64 + n * 64) * 2);
+    // slab t + 1 of XH as a buffer resource for the 16-B sc1 h stores: per-slab byte offsets
+    // (< B * KA * 2 < 2^31, host-checked) so any batch size fits the 32-bit offsets
+    const __amdgpu_buffer_rsrc_t xh_rsrc =
+        __builtin_amdgcn_make_buffer_rsrc(XH + (size_t)(t + 1) * d.B * KA, 0, 0x7FFFFFFF, 0x00020000);
+    const int hsoff = (int)(((size_t)rb * KA + 64 + n * 64) * 2);
 
     // cell epilogue element (row-tile i, row r) of the carried chunk: accp + c_{t-1} = cq[0]
     auto epi_elem = [&](int i, int r, float (&cv)[2][4], unsigned (&pk)[2][8], unsigned (&hv)[2][4]) {
@@ -461,7 +463,7 @@ int persistent_split(int B, int row_quantum, int max_units, int cols, int cus, i
 int launch_lstm_fwd_persistent(bf16_t* XH, const bf16_t* Wp, float* Cst, bf16_t* S, unsigned* sync,
                                long sync_words, LstmDims d, hipStream_t s) {
   const int KA = d.KX + d.H, G = 4 * d.H;
-  if ((double)(d.T + 1) * d.B * KA * 2 >= 2147483647.0) return 0;  // 32-bit buffer offsets
+  if ((double)d.B * KA * 2 >= 2147483647.0) return 0;  // 32-bit buffer offsets within one timestep slab
   if (d.KX % 64 != 0 || KA % 64 != 0 || G % 256 != 0 || d.B % PF_ROWS != 0 || d.KX != 64) return 0;
   if (KA / 32 != 6 && KA / 32 != 10 && KA / 32 != 18) return 0;
   int dev = 0, cus = 0;
