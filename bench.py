@@ -202,11 +202,13 @@ def bench_mlp(args, ctx, online: bool):
             run.run(streamer.last_slot)
     else:
         x, y = synth_tabular_batch(B, F, seed=ctx.rank)
-        x, y = x.to(ctx.device), y.to(ctx.device)
+        # resident in the engine's input format, as the job path keeps its datasets (Trainer)
+        x, y = x.to(ctx.device, eng.input_dtype), y.to(ctx.device)
         run = StepRunner(eng, opt, ctx, gscale, lambda k: (x, y), graph=graph, comm_in_graph=not args.eager_comm)
         step = run.run
     el = _timed(ctx, step, args.steps, args.warmup)
-    return el, B, model, float(eng.loss_sum.item()) / B, run, eng, extra
+    # the engine adds each step's loss straight into the runner's accumulator: mean over the run
+    return el, B, model, run.take_loss() / (B * (args.steps + args.warmup)), run, eng, extra
 
 
 def main() -> int:
@@ -295,7 +297,7 @@ def main() -> int:
             "grad_bucket_mb": round(eng.grads.numel() * 4 / 2**20, 3),
             "step_graph": bool(run.graphs),
             "comm_in_graph": bool(run.captured_comm),
-            "final_train_loss": round(loss, 6),
+            "train_loss": round(loss, 6),  # lstm: last step; mlp / cpu: mean over the run
             **extra,
         }
         print(json.dumps(rec), flush=True)

@@ -18,6 +18,8 @@
 //  * W1 slice 16 VGPRs, W2 slice 128 VGPRs per lane (loaded once); H1 / H2 leave the CU
 //    once each, as whole 16-byte row segments (they are the backward pass's saved
 //    activations); the head dot product is reduced across lanes (DPP) and waves (LDS).
+#include <cstdlib>
+
 #include "common.h"
 #include "gemm_core.h"
 #include "kernels.h"
@@ -295,6 +297,221 @@ __global__ __launch_bounds__(256, 1) void mlp2_fwd_kernel(
     const float t3 = block_sum<256>(db3a, lred);
     if (threadIdx.x == 0 && t3 != 0.f) atomicAdd(db3, t3);
   }
+}
+
+// ----------------------------------------------------------------------------------------
+// The training-step forward (mask mode, neither H1 nor H2 stored) with 8 waves, two per SIMD:
+// one wave's epilogue VALU / LDS traffic overlaps the other's MFMAs (the 4-wave kernel above
+// holds 64 units per wave and leaves its SIMD idle through every epilogue and barrier).
+//  * wave w owns hidden units [32w, 32w + 32) of both layers (W2 slice: 64 VGPRs).
+//  * the H2 ReLU bitmask, the head gradients and the loss come straight from the layer-2
+//    accumulators, with no H2 tile in LDS: a lane's bits (4 units x 2 M tiles of one row) are
+//    OR-reduced over the row's 4 lane groups and stored as the wave's 32-bit mask word; dy of
+//    the chunk's rows is rebuilt by every wave from the per-wave head partials, so
+//    dw3 += H2^T dy accumulates in registers.
+//  * three barriers per chunk (X staged, H1 tile complete, head partials complete); the
+//    targets are double-buffered so the next chunk's staging never races this chunk's reads.
+template <int KT1>
+__global__ __launch_bounds__(512, 1) void mlp2_fwd_train_kernel(
+    const bf16_t* __restrict__ X, int Fp, const bf16_t* __restrict__ W1, const float* __restrict__ b1,
+    const bf16_t* __restrict__ W2, const float* __restrict__ b2, const float* __restrict__ w3,
+    const float* __restrict__ b3, const float* __restrict__ y, unsigned* __restrict__ M2, float* __restrict__ dw3,
+    float* __restrict__ db3, float* __restrict__ pred, float* __restrict__ dy, float* __restrict__ loss_sum,
+    float dy_scale, int B, const long long* __restrict__ rows, long nrows) {
+  constexpr int NW = 8, MT = 2;  // waves; 16-unit M tiles per wave
+  __shared__ __attribute__((aligned(16))) char xs[MF_ROWS * MF_XROW];
+  __shared__ __attribute__((aligned(16))) char h1s[MF_ROWS * MF_H * 2];
+  __shared__ __attribute__((aligned(16))) float red[MF_ROWS][NW];
+  __shared__ float ys[2][MF_ROWS];
+  __shared__ float lred[NW];
+
+  const int lane = threadIdx.x & 63, l15 = lane & 15, g = lane >> 4;
+  const int wid = threadIdx.x >> 6;
+  const int u0 = wid * 16 * MT;
+  bf16x8 w1f[KT1][MT], w2f[MT][8];
+  float bias1[MT][4], bias2[MT][4], w3v[MT][4], dw3r[MT][4];
+#pragma unroll
+  for (int m = 0; m < MT; ++m) {
+    const int u = u0 + 16 * m + l15;
+#pragma unroll
+    for (int k1 = 0; k1 < KT1; ++k1) {
+      const int f0 = 32 * k1 + 8 * g;
+      w1f[k1][m] = f0 + 8 <= Fp ? *reinterpret_cast<const bf16x8*>(W1 + (size_t)u * Fp + f0)
+                                : bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
+    }
+#pragma unroll
+    for (int kt = 0; kt < 8; ++kt) w2f[m][kt] = *reinterpret_cast<const bf16x8*>(W2 + (size_t)u * MF_H + 32 * kt + 8 * g);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int uc = u0 + 16 * m + 4 * g + r;
+      bias1[m][r] = b1[uc];
+      bias2[m][r] = b2[uc];
+      w3v[m][r] = w3[uc];
+      dw3r[m][r] = 0.f;
+    }
+  }
+  const float bias3 = b3[0];
+  float lsum = 0.f, db3a = 0.f;
+
+  const int nchunks = (B + MF_ROWS - 1) / MF_ROWS;
+  // next chunk's inputs, loaded right after this chunk's are in LDS: threads 0..255 one X row
+  // segment each (row t >> 2, chunk t & 3 (+4)), threads 256..319 one target
+  uint4 xv[KT1];
+  float yv = 0.f;
+  auto prefetch = [&](int ch) {
+    if (threadIdx.x < 256) {
+      const int r = threadIdx.x >> 2, gr = ch * MF_ROWS + r;
+      const size_t dr = gr < B ? data_row(rows, gr, nrows) : 0;
+#pragma unroll
+      for (int k1 = 0; k1 < KT1; ++k1) {
+        const int c = (threadIdx.x & 3) + 4 * k1;
+        xv[k1] = (gr < B && 8 * c + 8 <= Fp) ? *reinterpret_cast<const uint4*>(X + dr * Fp + 8 * c)
+                                             : make_uint4(0, 0, 0, 0);
+      }
+    } else if (threadIdx.x < 256 + MF_ROWS) {
+      const int ty = ch * MF_ROWS + (int)threadIdx.x - 256;
+      yv = ty < B ? y[data_row(rows, ty, nrows)] : 0.f;
+    }
+  };
+  if ((int)blockIdx.x < nchunks) prefetch(blockIdx.x);
+  int par = 0;
+  for (int ch = blockIdx.x; ch < nchunks; ch += gridDim.x, par ^= 1) {
+    const int row0 = ch * MF_ROWS;
+    if (threadIdx.x < 256) {
+#pragma unroll
+      for (int k1 = 0; k1 < KT1; ++k1)
+        *reinterpret_cast<uint4*>(xs + xtile_off(threadIdx.x >> 2, (threadIdx.x & 3) + 4 * k1)) = xv[k1];
+    } else if (threadIdx.x < 256 + MF_ROWS) {
+      ys[par][threadIdx.x - 256] = yv;
+    }
+    __syncthreads();
+    if (ch + (int)gridDim.x < nchunks) prefetch(ch + gridDim.x);
+
+    // ---- layer 1: Z1^T (32 units x 64 rows per wave) = W1 x X^T
+    f32x4 acc[MT][4];
+#pragma unroll
+    for (int m = 0; m < MT; ++m)
+#pragma unroll
+      for (int n = 0; n < 4; ++n) acc[m][n] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int k1 = 0; k1 < KT1; ++k1)
+#pragma unroll
+      for (int n = 0; n < 4; ++n) {
+        const bf16x8 xb = *reinterpret_cast<const bf16x8*>(xs + xtile_off(16 * n + l15, 4 * k1 + g));
+#pragma unroll
+        for (int m = 0; m < MT; ++m)
+          acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w1f[k1][m], xb, acc[m][n], 0, 0, 0);
+      }
+#pragma unroll
+    for (int m = 0; m < MT; ++m)
+#pragma unroll
+      for (int n = 0; n < 4; ++n) {
+        unsigned pk[2];
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+          const float v0 = fmaxf(acc[m][n][2 * q] + bias1[m][2 * q], 0.f);
+          const float v1 = fmaxf(acc[m][n][2 * q + 1] + bias1[m][2 * q + 1], 0.f);
+          pk[q] = (unsigned)f2bf(v0) | ((unsigned)f2bf(v1) << 16);
+        }
+        *reinterpret_cast<uint2*>(h1s + tile_off(16 * n + l15, u0 + 16 * m + 4 * g)) = make_uint2(pk[0], pk[1]);
+      }
+    __syncthreads();
+
+    // ---- layer 2: Z2^T = W2 x H1^T, K = 256
+#pragma unroll
+    for (int m = 0; m < MT; ++m)
+#pragma unroll
+      for (int n = 0; n < 4; ++n) acc[m][n] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int kt = 0; kt < 8; ++kt) {
+      bf16x8 hb[4];
+#pragma unroll
+      for (int n = 0; n < 4; ++n) hb[n] = *reinterpret_cast<const bf16x8*>(h1s + tile_off(16 * n + l15, 32 * kt + 8 * g));
+#pragma unroll
+      for (int m = 0; m < MT; ++m)
+#pragma unroll
+        for (int n = 0; n < 4; ++n)
+          acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w2f[m][kt], hb[n], acc[m][n], 0, 0, 0);
+    }
+    // ---- H2 = relu(Z2 + b2) rounded to bf16 (the values the backward's mask describes), kept
+    // in acc; head partial sums and ReLU bits of rows 16n + l15
+    float hp[4] = {0.f, 0.f, 0.f, 0.f};
+    unsigned bits[4] = {0u, 0u, 0u, 0u};
+#pragma unroll
+    for (int m = 0; m < MT; ++m)
+#pragma unroll
+      for (int n = 0; n < 4; ++n)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float v = bf2f(f2bf(fmaxf(acc[m][n][r] + bias2[m][r], 0.f)));
+          acc[m][n][r] = v;
+          hp[n] += v * w3v[m][r];
+          if (v > 0.f) bits[n] |= 1u << (16 * m + 4 * g + r);
+        }
+#pragma unroll
+    for (int n = 0; n < 4; ++n) {
+      hp[n] += __shfl_xor(hp[n], 16, 64);
+      hp[n] += __shfl_xor(hp[n], 32, 64);
+      bits[n] |= (unsigned)__shfl_xor((int)bits[n], 16, 64);
+      bits[n] |= (unsigned)__shfl_xor((int)bits[n], 32, 64);
+    }
+    if (g == 0) {
+#pragma unroll
+      for (int n = 0; n < 4; ++n) red[16 * n + l15][wid] = hp[n];
+    }
+    {  // lane group g stores the mask word of row 16g + l15 (units 32 wid .. 32 wid + 31)
+      const unsigned bw = g == 0 ? bits[0] : g == 1 ? bits[1] : g == 2 ? bits[2] : bits[3];
+      const int gr = row0 + 16 * g + l15;
+      if (gr < B) M2[(size_t)gr * 8 + wid] = bw;
+    }
+    __syncthreads();
+
+    // ---- prediction, dy and loss of rows 16n + l15 (every wave: its dw3 needs dy); wave 0
+    // stores them, lane group g for row 16g + l15
+    float dyn[4];
+#pragma unroll
+    for (int n = 0; n < 4; ++n) {
+      const int r = 16 * n + l15, gr = row0 + r;
+      const float4 pa = *reinterpret_cast<const float4*>(&red[r][0]);
+      const float4 pb = *reinterpret_cast<const float4*>(&red[r][4]);
+      const float p = ((pa.x + pa.y) + (pa.z + pa.w)) + ((pb.x + pb.y) + (pb.z + pb.w)) + bias3;
+      dyn[n] = 0.f;
+      if (gr < B) {
+        const float diff = p - ys[par][r];
+        dyn[n] = dy_scale * diff;
+        if (wid == 0 && g == n) {
+          if (pred != nullptr) pred[gr] = p;
+          if (dy != nullptr) dy[gr] = dyn[n];
+          lsum += diff * diff;
+          db3a += dyn[n];
+        }
+      }
+    }
+#pragma unroll
+    for (int m = 0; m < MT; ++m)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int n = 0; n < 4; ++n) dw3r[m][r] += acc[m][n][r] * dyn[n];
+  }
+  if (loss_sum != nullptr) {
+    const float t = block_sum<512>(lsum, lred);
+    if (threadIdx.x == 0 && t != 0.f) atomicAdd(loss_sum, t);
+  }
+  // dw3: the 16 lanes l15 of a lane group hold the same 4 units (different rows)
+#pragma unroll
+  for (int m = 0; m < MT; ++m)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      float v = dw3r[m][r];
+      v += __shfl_xor(v, 1, 64);
+      v += __shfl_xor(v, 2, 64);
+      v += __shfl_xor(v, 4, 64);
+      v += __shfl_xor(v, 8, 64);
+      if (l15 == 0 && v != 0.f) atomicAdd(dw3 + u0 + 16 * m + 4 * g + r, v);
+    }
+  const float t3 = block_sum<512>(db3a, lred);
+  if (threadIdx.x == 0 && t3 != 0.f) atomicAdd(db3, t3);
 }
 
 // ----------------------------------------------------------------------------------------
@@ -842,6 +1059,241 @@ __global__ __launch_bounds__(256, 1) void mlp2_bwd_rc_kernel(
 }
 
 // ----------------------------------------------------------------------------------------
+// mlp2_bwd_rc_kernel with 8 waves, two per SIMD (wave w owns input units [32w, 32w + 32):
+// W2^T slice 64 VGPRs), so one wave's dZ2 / dZ1 elementwise work and LDS traffic overlaps the
+// other's MFMAs. The dZ2 and X tiles are double-buffered and the H1 / dZ1 tile is wave-private
+// (every wave reads back only its own units), so a chunk needs ONE workgroup barrier: the
+// next chunk's staging writes the other buffer, whose last readers passed this barrier.
+template <int NFT>
+__global__ __launch_bounds__(512, 1) void mlp2_bwd_rc8_kernel(
+    const unsigned* __restrict__ M2, const float* __restrict__ dy, const float* __restrict__ w3,
+    const bf16_t* __restrict__ W2, const bf16_t* __restrict__ X, int Fp, bf16_t* __restrict__ dZ2,
+    float* __restrict__ dW1, float* __restrict__ db1, float* __restrict__ db2, int B,
+    const bf16_t* __restrict__ W1, const float* __restrict__ b1, const long long* __restrict__ rows, long nrows) {
+  constexpr int MT = 2, ZB = MF_ROWS * MF_H * 2, XB = MF_ROWS * MF_XROW;
+  __shared__ __attribute__((aligned(16))) char zs[2 * ZB];  // dZ2 tiles (double-buffered)
+  __shared__ __attribute__((aligned(16))) char hs[ZB];      // H1 -> dZ1 in place (wave-private units)
+  __shared__ __attribute__((aligned(16))) char xs[2 * XB];  // X tiles (double-buffered)
+
+  const int lane = threadIdx.x & 63, l15 = lane & 15, g = lane >> 4;
+  const int wid = threadIdx.x >> 6;
+  const int u0 = wid * 16 * MT;
+  bf16x8 wt[MT][8];  // W2^T (A operand: lane = input unit k = u0 + 16m + l15, K = output unit)
+  bf16x8 w1f[MT];    // W1 rows of this wave's units (recompute)
+  float bias1[MT][4], db1a[MT][4];
+  f32x4 dw1a[MT][NFT];
+#pragma unroll
+  for (int m = 0; m < MT; ++m) {
+    const int k = u0 + 16 * m + l15;
+#pragma unroll
+    for (int kt = 0; kt < 8; ++kt)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) wt[m][kt][j] = (short)W2[(size_t)(32 * kt + 8 * g + j) * MF_H + k];
+    w1f[m] = 8 * g + 8 <= Fp ? *reinterpret_cast<const bf16x8*>(W1 + (size_t)k * Fp + 8 * g)
+                             : bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      bias1[m][r] = b1[u0 + 16 * m + 4 * g + r];
+      db1a[m][r] = 0.f;
+    }
+#pragma unroll
+    for (int f = 0; f < NFT; ++f) dw1a[m][f] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+  const int c = threadIdx.x & 31, rq = threadIdx.x >> 5;  // elementwise phase: units 8c.., rows rq + 16q
+  float w3c[8], db2a[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    w3c[e] = w3[8 * c + e];
+    db2a[e] = 0.f;
+  }
+  const int tq = (lane & 15) >> 2, tp = lane & 3;
+
+  unsigned mb[4];
+  float gyv[4];
+  uint4 xv = make_uint4(0, 0, 0, 0);
+  auto prefetch = [&](int ch) {
+    const int row0 = ch * MF_ROWS;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int gr = row0 + rq + 16 * q;
+      mb[q] = gr < B ? M2[(size_t)gr * 8 + (c >> 2)] : 0u;
+      gyv[q] = gr < B ? dy[gr] : 0.f;
+    }
+    if (threadIdx.x < 256) {
+      const int xr = threadIdx.x >> 2, xc = threadIdx.x & 3, gr = row0 + xr;
+      xv = (gr < B && 8 * xc + 8 <= Fp) ? *reinterpret_cast<const uint4*>(X + data_row(rows, gr, nrows) * Fp + 8 * xc)
+                                        : make_uint4(0, 0, 0, 0);
+    }
+  };
+  const int nchunks = (B + MF_ROWS - 1) / MF_ROWS;
+  if ((int)blockIdx.x < nchunks) prefetch(blockIdx.x);
+  int par = 0;
+  for (int ch = blockIdx.x; ch < nchunks; ch += gridDim.x, par ^= 1) {
+    const int row0 = ch * MF_ROWS;
+    char* zt = zs + par * ZB;
+    char* xt = xs + par * XB;
+    // ---- dZ2 = (dy w3^T) * [H2 > 0] -> LDS + HBM (dW2's operand); db2 partials
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int r = rq + 16 * q, gr = row0 + r;
+      const unsigned bits = mb[q] >> (8 * (c & 3));
+      unsigned zw[4];
+#pragma unroll
+      for (int p = 0; p < 4; ++p) {
+        unsigned pk = 0;
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const int e = 2 * p + h;
+          const bf16_t zb = f2bf(((bits >> e) & 1u) ? gyv[q] * w3c[e] : 0.f);
+          db2a[e] += bf2f(zb);
+          pk |= (unsigned)zb << (16 * h);
+        }
+        zw[p] = pk;
+      }
+      const uint4 zv = make_uint4(zw[0], zw[1], zw[2], zw[3]);
+      *reinterpret_cast<uint4*>(zt + tile_off(r, 8 * c)) = zv;
+      if (gr < B) *reinterpret_cast<uint4*>(dZ2 + (size_t)gr * MF_H + 8 * c) = zv;
+    }
+    if (threadIdx.x < 256) *reinterpret_cast<uint4*>(xt + xtile_off(threadIdx.x >> 2, threadIdx.x & 3)) = xv;
+    __syncthreads();
+    if (ch + (int)gridDim.x < nchunks) prefetch(ch + gridDim.x);
+
+    // ---- H1 of this wave's units (bit-identical to the forward's layer 1) -> hs
+    {
+      f32x4 a1[MT][4];
+#pragma unroll
+      for (int n = 0; n < 4; ++n) {
+        const bf16x8 xb = *reinterpret_cast<const bf16x8*>(xt + xtile_off(16 * n + l15, g));
+#pragma unroll
+        for (int m = 0; m < MT; ++m)
+          a1[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w1f[m], xb, f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+      }
+#pragma unroll
+      for (int m = 0; m < MT; ++m)
+#pragma unroll
+        for (int n = 0; n < 4; ++n) {
+          unsigned pk[2];
+#pragma unroll
+          for (int q = 0; q < 2; ++q) {
+            const float v0 = fmaxf(a1[m][n][2 * q] + bias1[m][2 * q], 0.f);
+            const float v1 = fmaxf(a1[m][n][2 * q + 1] + bias1[m][2 * q + 1], 0.f);
+            pk[q] = (unsigned)f2bf(v0) | ((unsigned)f2bf(v1) << 16);
+          }
+          *reinterpret_cast<uint2*>(hs + tile_off(16 * n + l15, u0 + 16 * m + 4 * g)) = make_uint2(pk[0], pk[1]);
+        }
+    }
+    // ---- dH1^T (32 k x 64 rows per wave) = W2^T x dZ2^T, K = 256
+    f32x4 acc[MT][4];
+#pragma unroll
+    for (int m = 0; m < MT; ++m)
+#pragma unroll
+      for (int n = 0; n < 4; ++n) acc[m][n] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int kt = 0; kt < 8; ++kt) {
+      bf16x8 zb[4];
+#pragma unroll
+      for (int n = 0; n < 4; ++n) zb[n] = *reinterpret_cast<const bf16x8*>(zt + tile_off(16 * n + l15, 32 * kt + 8 * g));
+#pragma unroll
+      for (int m = 0; m < MT; ++m)
+#pragma unroll
+        for (int n = 0; n < 4; ++n)
+          acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wt[m][kt], zb[n], acc[m][n], 0, 0, 0);
+    }
+    // ---- dZ1 = dH1 * [H1 > 0] into the same 8 bytes of hs; db1 partials
+#pragma unroll
+    for (int m = 0; m < MT; ++m)
+#pragma unroll
+      for (int n = 0; n < 4; ++n) {
+        const int r = 16 * n + l15;
+        uint2* pp = reinterpret_cast<uint2*>(hs + tile_off(r, u0 + 16 * m + 4 * g));
+        const uint2 hv = *pp;
+        const unsigned hw2[2] = {hv.x, hv.y};
+        unsigned ow[2];
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+          unsigned pk = 0;
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            const int i = 2 * q + h;
+            const bool on = bf2f((bf16_t)(hw2[q] >> (16 * h))) > 0.f && row0 + r < B;
+            const bf16_t vb = f2bf(on ? acc[m][n][i] : 0.f);
+            db1a[m][i] += bf2f(vb);
+            pk |= (unsigned)vb << (16 * h);
+          }
+          ow[q] = pk;
+        }
+        *pp = make_uint2(ow[0], ow[1]);
+      }
+    // the dW1 fragments below read other lanes' dZ1 (same wave): complete the writes first
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
+    // ---- dW1^T slice (32 units x Fp per wave) += dZ1^T X over the chunk's rows
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      bf16x8 af[MT], bfr[NFT];
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int r = 32 * kk + 8 * g + 4 * h + tq;
+#pragma unroll
+        for (int m = 0; m < MT; ++m) {
+          const bf16x4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_bf16x4*)(hs + tile_off(r, u0 + 16 * m + 4 * tp)));
+#pragma unroll
+          for (int e = 0; e < 4; ++e) af[m][4 * h + e] = v[e];
+        }
+#pragma unroll
+        for (int f = 0; f < NFT; ++f) {
+          const int f0 = 16 * f + 4 * tp;
+          const bf16x4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+              (lds_bf16x4*)(xt + xtile_off(r, f0 >> 3) + ((f0 & 7) << 1)));
+#pragma unroll
+          for (int e = 0; e < 4; ++e) bfr[f][4 * h + e] = v[e];
+        }
+      }
+#pragma unroll
+      for (int m = 0; m < MT; ++m)
+#pragma unroll
+        for (int f = 0; f < NFT; ++f)
+          dw1a[m][f] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[m], bfr[f], dw1a[m][f], 0, 0, 0);
+    }
+    // hs is rewritten by this wave's next H1 recompute: its dW1 reads must be complete
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
+  }
+  // ---- reductions
+#pragma unroll
+  for (int m = 0; m < MT; ++m)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      float v = db1a[m][i];
+      v += __shfl_xor(v, 1, 64);
+      v += __shfl_xor(v, 2, 64);
+      v += __shfl_xor(v, 4, 64);
+      v += __shfl_xor(v, 8, 64);
+      if (l15 == 0 && v != 0.f) atomicAdd(db1 + u0 + 16 * m + 4 * g + i, v);
+    }
+#pragma unroll
+  for (int m = 0; m < MT; ++m)
+#pragma unroll
+    for (int f = 0; f < NFT; ++f) {
+      const int ft = l15 + 16 * f;
+      if (ft < Fp)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) atomicAdd(dW1 + (size_t)(u0 + 16 * m + 4 * g + i) * Fp + ft, dw1a[m][f][i]);
+    }
+  __syncthreads();  // the last chunk's dZ2 tile reads are done before zs becomes the db2 scratch
+  float* sd = reinterpret_cast<float*>(zs);
+#pragma unroll
+  for (int e = 0; e < 8; ++e) sd[rq * MF_H + 8 * c + e] = db2a[e];
+  __syncthreads();
+  if (threadIdx.x < MF_H) {
+    float s2 = 0.f;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) s2 += sd[q * MF_H + threadIdx.x];
+    if (s2 != 0.f) atomicAdd(db2 + threadIdx.x, s2);
+  }
+}
+
+// ----------------------------------------------------------------------------------------
 // dW2 += dZ2^T H1 with H1 = relu(X W1^T + b1) RECOMPUTED per 64-row chunk instead of being
 // stored by the forward and re-read here (the generic split-K GEMM read H1 [B][256] twice:
 // 268 MB at B = 262144). Per chunk a workgroup streams its dZ2 columns (MN-contiguous image,
@@ -1031,6 +1483,19 @@ bool launch_mlp2_bwd(const bf16_t* H1, const bf16_t* H2, const unsigned* M2, con
     cus = 256;
   const int grid = nchunks < cus ? nchunks : cus;
   if (H1 == nullptr && M2 != nullptr && dW1 != nullptr) {  // the training step's configuration
+    static const bool bwd8 = [] {
+      const char* e = std::getenv("WELLFLOW_MLP_BWD8");
+      return e == nullptr || e[0] != '0';
+    }();
+    if (bwd8) {
+      if (Fp <= 16)
+        hipLaunchKernelGGL(mlp2_bwd_rc8_kernel<1>, dim3(grid), dim3(512), 0, s, M2, dy, w3, W2, X, Fp, dZ2, dW1, db1,
+                           db2, B, W1, b1, rows, nrows);
+      else
+        hipLaunchKernelGGL(mlp2_bwd_rc8_kernel<2>, dim3(grid), dim3(512), 0, s, M2, dy, w3, W2, X, Fp, dZ2, dW1, db1,
+                           db2, B, W1, b1, rows, nrows);
+      return true;
+    }
     if (Fp <= 16)
       hipLaunchKernelGGL(mlp2_bwd_rc_kernel<1>, dim3(grid), dim3(256), 0, s, M2, dy, w3, W2, X, Fp, dZ2, dW1, db1, db2,
                          B, W1, b1, rows, nrows);
@@ -1060,6 +1525,19 @@ bool launch_mlp2_fwd(const bf16_t* X, int Fp, const bf16_t* W1, const float* b1,
       hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
     cus = 256;
   const int grid = nchunks < cus ? nchunks : cus;
+  static const bool fwd8 = [] {
+    const char* e = std::getenv("WELLFLOW_MLP_FWD8");
+    return e == nullptr || e[0] != '0';
+  }();
+  if (fwd8 && M2 != nullptr && H1 == nullptr) {  // the training step (mask mode never writes H2)
+    if (Fp <= 32)
+      hipLaunchKernelGGL(mlp2_fwd_train_kernel<1>, dim3(grid), dim3(512), 0, s, X, Fp, W1, b1, W2, b2, w3, b3, y, M2,
+                         dw3, db3, pred, dy, loss_sum, dy_scale, B, rows, nrows);
+    else
+      hipLaunchKernelGGL(mlp2_fwd_train_kernel<2>, dim3(grid), dim3(512), 0, s, X, Fp, W1, b1, W2, b2, w3, b3, y, M2,
+                         dw3, db3, pred, dy, loss_sum, dy_scale, B, rows, nrows);
+    return true;
+  }
   if (Fp <= 32)
     hipLaunchKernelGGL(mlp2_fwd_kernel<1>, dim3(grid), dim3(256), 0, s, X, Fp, W1, b1, W2, b2, w3, b3, y, H1, H2,
                        M2, dw3, db3, pred, dy, loss_sum, dy_scale, B, rows, nrows);

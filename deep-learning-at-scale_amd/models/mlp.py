@@ -173,20 +173,23 @@ class NativeMLP:
     def sync_weights(self) -> None:
         self._C.cast_bf16(self.params, self.shadow)
 
-    def _step_recompute(self, Xop, y, rows, grad_scale: float, zero_grads: bool) -> torch.Tensor:
+    def _step_recompute(self, Xop, y, rows, grad_scale: float, zero_grads: bool, loss_into=None) -> torch.Tensor:
         """fused forward (H2 -> bitmask, head gradients) -> fused backward (dZ2, dZ1, dW1, biases;
         H1 recomputed) -> dW2 with H1 recomputed: three launches, activations never in HBM
-        except dZ2."""
+        except dZ2. ``loss_into``: the forward adds the batch loss to that accumulator directly
+        (no per-step zero fill and no separate accumulate launch)."""
         C = self._C
         B = rows.shape[0] if rows is not None else self._Xop_rows
         if zero_grads:
             self.grads.zero_()
-        self.loss_sum.zero_()
+        ls = loss_into if loss_into is not None else self.loss_sum
+        if loss_into is None:
+            self.loss_sum.zero_()
         wl, _, _ = self.lay.views(self.shadow)
         pl, hw, hb = self.lay.views(self.params)
         gl, ghw, ghb = self.lay.views(self.grads)
         self._Xop = Xop
-        if not self._fused_forward(B, y, self.dy, self.loss_sum, 2.0 * float(grad_scale), (ghw, ghb),
+        if not self._fused_forward(B, y, self.dy, ls, 2.0 * float(grad_scale), (ghw, ghb),
                                    store_h1=self.dw2_gemm, rows=rows):
             raise RuntimeError("NativeMLP: fused forward refused the recompute step")
         ok = C.mlp2_backward(None, self.Hs[1], self.dy, hw, wl[1][0], Xop, self.Fp, self.dZ[0], self.dZ[1],
@@ -200,7 +203,7 @@ class NativeMLP:
             ok = ok and C.mlp2_dw2(self.dZ[1], Xop, self.Fp, rows, wl[0][0], pl[0][1], B, self.dw2_split, gl[1][0])
         if not ok:
             raise RuntimeError("NativeMLP: recompute backward refused (shape)")
-        return self.loss_sum
+        return ls
 
     def _load_x(self, x: torch.Tensor) -> int:
         B = x.shape[0]
@@ -263,10 +266,12 @@ class NativeMLP:
                 and self.loss_kind == "mse" and self.Fp <= 32 and B % 64 == 0)
 
     def forward_backward(self, x: torch.Tensor, y: torch.Tensor, grad_scale: float,
-                         zero_grads: bool = True, step: int = 0, rows: torch.Tensor | None = None) -> torch.Tensor:
+                         zero_grads: bool = True, step: int = 0, rows: torch.Tensor | None = None,
+                         loss_into: torch.Tensor | None = None) -> torch.Tensor:
         """``rows`` (int64, device): train on dataset rows ``x[rows]``, ``y[rows]`` — the fused
         kernels read the resident dataset through the index (no gather launch); other paths
-        gather first."""
+        gather first. ``loss_into``: accumulate the batch loss there (returned) instead of
+        returning this step's ``loss_sum``."""
         from ..ops.native import gemm
 
         C = self._C
@@ -274,11 +279,12 @@ class NativeMLP:
             B = rows.shape[0]
             if (self._recompute_ok(B) and x.dtype == torch.bfloat16 and x.is_contiguous() and x.shape[1] == self.Fp
                     and x.data_ptr() % 16 == 0 and B <= self.B):
-                return self._step_recompute(x.view(-1), y.contiguous().float(), rows, grad_scale, zero_grads)
+                return self._step_recompute(x.view(-1), y.contiguous().float(), rows, grad_scale, zero_grads,
+                                            loss_into)
             x, y = x.index_select(0, rows), y.index_select(0, rows)
         B = self._load_x(x)
         if self._recompute_ok(B):
-            return self._step_recompute(self._Xop, y.contiguous().float(), None, grad_scale, zero_grads)
+            return self._step_recompute(self._Xop, y.contiguous().float(), None, grad_scale, zero_grads, loss_into)
         if zero_grads:
             self.grads.zero_()
         self.loss_sum.zero_()
@@ -339,4 +345,7 @@ class NativeMLP:
                 # dZ_{l-1} = (dZ_l W_l) * [H_{l-1} > 0];  db_{l-1} = colsum
                 gemm(self.dZ[l], wl[l][0], B, k, h, b_mn=True, ldb=k, outH=self.dZ[l - 1],
                      mask=self.Hs[l - 1], colsum=gl[l - 1][1])
+        if loss_into is not None:
+            loss_into += self.loss_sum
+            return loss_into
         return self.loss_sum

@@ -20,6 +20,7 @@ Round-1 verdict item 6 ("one step implementation for bench and jobs"): bench.py 
 """
 from __future__ import annotations
 
+import inspect
 import os
 import sys
 
@@ -50,6 +51,11 @@ class StepRunner:
         sh = getattr(opt, "shadow", None)
         self.fused_shadow = sh is not None and sh is getattr(eng, "shadow", None)
         self.loss_acc = torch.zeros(1, device=eng.device) if accumulate_loss else None
+        # engines that add the batch loss straight into the accumulator (no zero + add launches)
+        try:
+            self._loss_into = "loss_into" in inspect.signature(eng.forward_backward).parameters
+        except (TypeError, ValueError):
+            self._loss_into = False
         self.graphs: dict = {}
         self.update_graph = None  # comm outside the graph: [compute graph] all-reduce [update graph]
         self.calls = 0
@@ -58,13 +64,17 @@ class StepRunner:
     # ------------------------------------------------------------------ pieces
     def _compute(self, key):
         inp = self.inputs(key)
+        kw = {"zero_grads": not self.fused_clear}
+        direct = self._loss_into and self.loss_acc is not None
+        if direct:
+            kw["loss_into"] = self.loss_acc
         if len(inp) == 3:  # (dataset X, dataset y, row indices): the engine reads rows in place
             x, y, rows = inp
-            ls = self.eng.forward_backward(x, y, self.grad_scale, zero_grads=not self.fused_clear, rows=rows)
+            ls = self.eng.forward_backward(x, y, self.grad_scale, rows=rows, **kw)
         else:
             x, y = inp
-            ls = self.eng.forward_backward(x, y, self.grad_scale, zero_grads=not self.fused_clear)
-        if self.loss_acc is not None:
+            ls = self.eng.forward_backward(x, y, self.grad_scale, **kw)
+        if self.loss_acc is not None and not direct:
             self.loss_acc += ls
 
     def _comm(self):

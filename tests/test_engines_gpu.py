@@ -229,7 +229,8 @@ def test_mlp_recompute_step_matches_stored_h1(B, F):
     """The H1-free training step (fused forward writes only the H2 bitmask; the fused backward
     and the dW2 kernel recompute H1 from X, csrc/mlp_fused.hip) against the step that stores
     and re-reads H1 with the generic split-K dW2 GEMM: same loss, same gradients up to the
-    fp32 summation order."""
+    fp32 summation order (both the fused kernels and the GEMM path are checked against fp32
+    torch in test_numerics_gpu.py)."""
     from wellflow.data.synth import synth_tabular_batch
     from wellflow.models.mlp import NativeMLP, init_mlp_flat
 
@@ -247,7 +248,8 @@ def test_mlp_recompute_step_matches_stored_h1(B, F):
         out[rec] = (ls, eng.pred[:B].clone(), eng.grads.clone())
     assert eng._recompute_ok(B)
     (la, pa, ga), (lb, pb, gb) = out[False], out[True]
-    assert torch.equal(pa, pb)
+    # the training forward (8 waves, 32 units each) sums the head in a different fp32 order
+    torch.testing.assert_close(pa, pb, rtol=1e-5, atol=1e-6)
     assert abs(la - lb) <= 1e-5 * abs(la) + 1e-7
     assert torch.isfinite(gb).all()
     assert ((ga - gb).norm() / ga.norm()).item() < 1e-4
