@@ -191,8 +191,11 @@ def bench_mlp(args, ctx, online: bool):
         # features cross PCIe as bf16 (the engine's MFMA input format: identical numerics to
         # streaming fp32 and casting on the device, half the bytes); targets stay fp32
         x_dtype = torch.float32 if args.stream_fp32 else torch.bfloat16
-        pool = HostPool(lambda k: synth_tabular_batch(B, F, seed=1000 * ctx.rank + k), n=8, x_dtype=x_dtype)
-        streamer = DeviceStreamer(pool, ctx.device, depth=3)
+        pool = HostPool(lambda k: synth_tabular_batch(B, F, seed=1000 * ctx.rank + k), n=args.host_pool,
+                        x_dtype=x_dtype)
+        # copies bracketed by events: the JSON reports their device time (a shared host's PCIe
+        # load shows up here, not in the kernels)
+        streamer = DeviceStreamer(pool, ctx.device, depth=4, timing=True)
         # one captured step per ring slot (the graph reads that slot's buffers)
         run = StepRunner(eng, opt, ctx, gscale, lambda k: tuple(streamer.slots[k][:2]), graph=graph,
                          comm_in_graph=not args.eager_comm)
@@ -207,6 +210,10 @@ def bench_mlp(args, ctx, online: bool):
         run = StepRunner(eng, opt, ctx, gscale, lambda k: (x, y), graph=graph, comm_in_graph=not args.eager_comm)
         step = run.run
     el = _timed(ctx, step, args.steps, args.warmup)
+    if online:
+        extra.update(streamer.copy_stats(skip=args.warmup))
+        extra["h2d_mb_per_step"] = round((streamer.slots[0][0].numel() * streamer.slots[0][0].element_size()
+                                          + streamer.slots[0][1].numel() * 4) / 1e6, 3)
     # the engine adds each step's loss straight into the runner's accumulator: mean over the run
     return el, B, model, run.take_loss() / (B * (args.steps + args.warmup)), run, eng, extra
 
@@ -228,6 +235,7 @@ def main() -> int:
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--eager-comm", action="store_true", help="all-reduce between two graphs, not captured")
     ap.add_argument("--stream-fp32", action="store_true", help="mlp_online: stream fp32 features")
+    ap.add_argument("--host-pool", type=int, default=8, help="mlp_online: distinct pinned host batches cycled")
     ap.add_argument("--device", choices=["auto", "cpu"], default="auto",
                     help="cpu: rehearse the launch/timing/JSON contract on the fp32 reference over gloo")
     args = ap.parse_args()

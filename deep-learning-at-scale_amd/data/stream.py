@@ -8,6 +8,15 @@ synthetic generator). Pinned sources (``HostPool``) are copied straight from the
 pages; anything else is first staged into a pinned ring (one host memcpy, then an async
 DMA), so the H2D copy never runs synchronously from pageable memory.
 
+Issue order (measured on MI355X, tools/online_host.py): a copy-stream wait on compute work
+makes the host block inside the copy call until that compute has finished, so the ring is
+refilled with a lag of two: at batch k the slot of batch k-2 is refilled, waiting only on an
+event recorded right after batch k-2's compute, while batch k-1's compute is already queued.
+(A producer thread issuing the copies instead was slower: it contends for the GIL with the
+training loop.) On the shared MI355X host the copies themselves are the limit: median 0.21 ms
+per 9.4 MB batch (~45 GB/s, fully hidden under a 0.275 ms step) but 4-5 % of them stall for
+3-6 ms (bench.py reports h2d_ms_median / max / over_1ms for every online run).
+
 The device ring buffers keep their addresses for the streamer's lifetime — a hipGraph
 captured on slot k (train/step.py StepRunner: one graph per slot) stays valid — and a new
 source can be fed with :meth:`feed` (one per online chunk, train/online.py).
@@ -38,14 +47,18 @@ class HostPool:
 
 
 class DeviceStreamer:
-    def __init__(self, source, device, depth: int = 3, x_dtype=None):
-        """``x_dtype``: cast features on the host before the copy (e.g. torch.bfloat16)."""
-        assert depth >= 2
+    def __init__(self, source, device, depth: int = 4, x_dtype=None, timing: bool = False):
+        """``x_dtype``: cast features on the host before the copy (e.g. torch.bfloat16);
+        ``timing``: bracket every batch's copies with events (:meth:`copy_stats`)."""
+        assert depth >= 3, "the refill lags two batches behind the consumer (module docstring)"
         self.device = torch.device(device)
         self.copy_stream = torch.cuda.Stream(device=self.device)
         self.depth = depth
         self.x_dtype = x_dtype
-        self.slots = []    # [x_dev, y_dev, event] — fixed addresses
+        self.slots = []    # [x_dev, y_dev, ready event] — fixed addresses
+        self.consumed = [None] * depth  # per slot: event after the compute that read it
+        self.timing = timing
+        self._tev = []  # (start, end) events of timed batches
         self.staging = []  # pinned host ring for pageable sources: [x_pin, y_pin]
         self.k = 0         # batches issued
         self.used = 0      # batches handed to the consumer
@@ -59,10 +72,17 @@ class DeviceStreamer:
 
     def feed(self, source) -> None:
         """Start streaming a new source; the ring and any captured graphs stay valid."""
+        if self.used > 0:  # the old source's last batch: its slot is refilled only after its compute
+            ev = torch.cuda.Event()
+            ev.record(torch.cuda.current_stream(self.device))
+            self.consumed[(self.used - 1) % self.depth] = ev
         self.src = iter(source)
         self._primed = False
         self._exhausted = False
         self.k = self.used = 0
+
+    def close(self) -> None:
+        """Nothing to release (API symmetry with producer-style streamers)."""
 
     def _host(self, x, y, slot):
         if id(x) in self._pinned and id(y) in self._pinned and self.x_dtype in (None, x.dtype):
@@ -107,30 +127,56 @@ class DeviceStreamer:
         xd, yd, ev = self.slots[slot]
         assert xd.shape == x.shape and xd.dtype == x.dtype and yd.shape == y.shape, \
             "DeviceStreamer: every batch must have the ring's shape"
-        # the slot's previous consumer must be done before it is overwritten
-        self.copy_stream.wait_stream(torch.cuda.current_stream(self.device))
+        # the slot's previous consumer must be done before it is overwritten (its event, not
+        # the whole compute stream: see the module docstring)
+        done = self.consumed[slot]
+        if done is not None:
+            self.copy_stream.wait_event(done)
         with torch.cuda.stream(self.copy_stream):
+            if self.timing:
+                t0, t1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                t0.record(self.copy_stream)
             xd.copy_(x, non_blocking=True)
             yd.copy_(y, non_blocking=True)
             ev.record(self.copy_stream)
+            if self.timing:
+                t1.record(self.copy_stream)
+                self._tev.append((t0, t1))
         self.k += 1
         return True
 
     def next(self):
         """The next batch on the device, ordered before the current stream's later work;
         raises StopIteration when a finite source is drained."""
+        cur = torch.cuda.current_stream(self.device)
+        if self.used > 0:  # the previous batch's compute is queued: mark where it ends
+            ev = torch.cuda.Event()
+            ev.record(cur)
+            self.consumed[(self.used - 1) % self.depth] = ev
         if not self._primed:
-            for _ in range(self.depth - 1):
+            for _ in range(self.depth):
                 self._issue()
             self._primed = True
-        self._issue()  # keep depth-1 batches in flight
+        elif self.used >= 2:
+            self._issue()  # refill the slot of batch used - 2 (lag two: module docstring)
         if self.used >= self.k:
             raise StopIteration
         self.last_slot = self.used % self.depth
         self.used += 1
         xd, yd, ev = self.slots[self.last_slot]
-        torch.cuda.current_stream(self.device).wait_event(ev)
+        cur.wait_event(ev)
         return xd, yd
+
+    def copy_stats(self, skip: int = 0) -> dict:
+        """Device time of each timed batch's host->HBM copies (ms): mean / median / max (syncs)."""
+        torch.cuda.synchronize(self.device)
+        ms = [a.elapsed_time(b) for a, b in list(self._tev)[skip:]]
+        if not ms:
+            return {}
+        srt = sorted(ms)
+        return {"h2d_ms_mean": round(sum(ms) / len(ms), 4), "h2d_ms_median": round(srt[len(srt) // 2], 4),
+                "h2d_ms_max": round(srt[-1], 4), "h2d_batches": len(ms),
+                "h2d_over_1ms": sum(1 for v in ms if v > 1.0)}
 
     def __iter__(self):
         """Yields the ring slot index of each batch (its tensors: ``slots[k][0:2]``)."""

@@ -76,7 +76,7 @@ def fit_online(trainer, train, val):
         from ..utils.numa import bind_to_gpu_numa
 
         bind_to_gpu_numa(eng.device.index or 0)  # pinned staging ring next to the GPU's PCIe root
-        streamer = DeviceStreamer(None, eng.device, depth=3)
+        streamer = DeviceStreamer(None, eng.device, depth=4)
     k = 0
     for p in range(passes):
         for Xc, Yc in stream_chunks(Xtr, Ytr, chunk):
