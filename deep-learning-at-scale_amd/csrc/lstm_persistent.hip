@@ -313,11 +313,7 @@ __global__ __launch_bounds__(256, 1) void lstm_fwd_persistent_kernel(
       if (c + 2 < NC) issue(c + 2, std::integral_constant<int, (P + 2) % 3>{});
       const char* cur = smem + P * SLOT;
 
-      f32x4 acc[2][4];
-#pragma unroll
-      for (int i = 0; i < 2; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+      f32x4 acc[2][4];  // written first by k-tile 0's MFMAs (src C = 0: no zeroing writes)
       // MFMAs in inline asm with explicit register classes: weights of k-tiles < KTA as AGPR
       // operands, the rest as VGPR operands, accumulators in AGPRs. With the builtin the
       // register allocator shuffled the 288 weight registers through v_accvgpr_read/mov copies
@@ -348,9 +344,9 @@ __global__ __launch_bounds__(256, 1) void lstm_fwd_persistent_kernel(
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
             if constexpr (!(DBG & 2)) {
-              if constexpr (kt == 0)  // the accumulators were just zeroed by v_accvgpr_write
-                asm volatile("s_nop 2\n\tv_mfma_f32_16x16x32_bf16 %0, %1, %2, %0"
-                             : "+a"(acc[i][j]) : "v"(a[kt & 1][i]), "a"(w[kt][j]));
+              if constexpr (kt == 0)  // accumulator := A B (inline-constant 0 as src C)
+                asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, 0"
+                             : "=&a"(acc[i][j]) : "v"(a[kt & 1][i]), "a"(w[kt][j]));
               else if constexpr (kt < KTA)
                 asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc[i][j]) : "v"(a[kt & 1][i]), "a"(w[kt][j]));
               else

@@ -316,9 +316,7 @@ __global__ __launch_bounds__(256, 1) void lstm_bwd_persistent_kernel(
       stamp(s, 2 + 5 * RT);
       const unsigned cur = a_lds + P * WSLOT;
 
-      f32x4 acc[4];
-#pragma unroll
-      for (int j = 0; j < 4; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+      f32x4 acc[4];  // written first by k-tile 0's MFMAs (src C = 0)
       f32x4 pr[4];
       bf16x8 a[2];
       asm volatile("ds_read_b128 %0, %1" : "=v"(a[0]) : "v"(cur + fa[0]) : "memory");
@@ -345,7 +343,10 @@ __global__ __launch_bounds__(256, 1) void lstm_bwd_persistent_kernel(
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
           if constexpr (!(DBG & 2)) {
-            asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+v"(acc[j]) : "v"(a[kt & 1]), "a"(w[kt][j]));
+            if constexpr (kt == 0)
+              asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, 0" : "=&v"(acc[j]) : "v"(a[kt & 1]), "a"(w[kt][j]));
+            else
+              asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+v"(acc[j]) : "v"(a[kt & 1]), "a"(w[kt][j]));
           }
         }
         // two A pieces of the next tile per k-tile over the first half of the loop: the vector-
