@@ -1309,26 +1309,42 @@ __global__ __launch_bounds__(512, 1) void mlp2_bwd_rc8_kernel(
 //    chunk of the same row (finite values), never out-of-bounds memory.
 constexpr int DW2_STAGES = 4;
 constexpr int DW2_MAX_ROWS = 8192;  // rows per workgroup (the LDS row-id table)
-__global__ __launch_bounds__(256, 1) void mlp2_dw2_kernel(const bf16_t* __restrict__ dZ2, const bf16_t* __restrict__ X,
-                                                          int Fp, const long long* __restrict__ rows, long nrows,
-                                                          const bf16_t* __restrict__ W1, const float* __restrict__ b1,
-                                                          int kchunk, float* __restrict__ dW2) {
-  constexpr int BM = 128, BN = 128;
-  using C = GemmCfg<BM, BN, MN_CONTIG, MN_CONTIG>;
-  using QA = GldsTile<BM, MN_CONTIG, 256>;
+// NW = 4: waves 2(M) x 2(N) of 64x64, each rebuilding 32 H1 units; NW = 8 (default): two waves
+// per SIMD, 2(M) x 4(N) of 64x32, 16 H1 units each, so one wave's H1 rebuild (VALU) and
+// fragment reads overlap the other's MFMAs. The X tile is 4 one-KiB pieces, issued by waves
+// 0-3: with 8 waves the DMA count per chunk differs by wave (dma_wait below).
+template <int NW>
+__global__ __launch_bounds__(64 * NW, 1) void mlp2_dw2_kernel(const bf16_t* __restrict__ dZ2, const bf16_t* __restrict__ X,
+                                                              int Fp, const long long* __restrict__ rows, long nrows,
+                                                              const bf16_t* __restrict__ W1, const float* __restrict__ b1,
+                                                              int kchunk, float* __restrict__ dW2) {
+  static_assert(NW == 4 || NW == 8, "4 or 8 waves");
+  constexpr int NT = 64 * NW, BM = 128, BN = 128, MTR = 128 / (16 * NW);  // H1 unit tiles per wave
+  using C = GemmCfg<BM, BN, MN_CONTIG, MN_CONTIG, 2, NW / 2>;
+  using QA = GldsTile<BM, MN_CONTIG, NT>;
   constexpr int ABYTES = QA::BYTES;           // 16 KB: [64 rows][128 units]
   constexpr int XBYTES = MF_ROWS * 64;        // 4 KB: [64 rows][4 x 16-B feature chunks]
   constexpr int SLOT = ABYTES + XBYTES;
   constexpr int HIMG = BN * 64 * 2;           // one H1 image [64 rows][128 units], 16 KB
   constexpr int HOFF = DW2_STAGES * SLOT;     // two H1 images (chunk c read while c + 1 is built)
-  constexpr int LPT = QA::PER_WAVE + 1;       // DMA instructions per wave per chunk
+  constexpr int LPT_X = QA::PER_WAVE + 1;     // DMA instructions per chunk: waves 0-3 (A + X)
+  constexpr int LPT_A = QA::PER_WAVE;         //   waves 4-7 (A only)
   constexpr int ROFF = HOFF + 2 * HIMG;       // dataset row ids of the range (int32), read from
                                               // LDS: a global index load would join the vmcnt
                                               // queue and drain the DMA prefetch
   __shared__ __attribute__((aligned(16))) char smem[ROFF + DW2_MAX_ROWS * 4];
   const int lane = threadIdx.x & 63, l15 = lane & 15, g = lane >> 4;
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int wm = wid >> 1, wn = wid & 1;
+  const int wm = wid / (NW / 2), wn = wid % (NW / 2);
+  const bool xw = wid < 4;  // this wave DMAs one X piece per chunk
+  // wait until at most n chunks' DMA of this wave are in flight (counts differ by wave)
+  auto dma_wait = [&](auto nc) {
+    constexpr int n = decltype(nc)::value;
+    if (NW == 4 || xw)
+      wait_vmcnt<n * LPT_X>();
+    else
+      wait_vmcnt<n * LPT_A>();
+  };
   const int L = xcd_remap(blockIdx.x, gridDim.x);
   const int split = L >> 2, t = L & 3;
   const int m0 = (t >> 1) * BM, n0 = (t & 1) * BN;
@@ -1336,50 +1352,52 @@ __global__ __launch_bounds__(256, 1) void mlp2_dw2_kernel(const bf16_t* __restri
   const int nk = kchunk / MF_ROWS;
   int* ridx = reinterpret_cast<int*>(smem + ROFF);
   if (rows != nullptr) {
-    for (int i = threadIdx.x; i < kchunk; i += 256) ridx[i] = (int)data_row(rows, kbeg + i, nrows);
+    for (int i = threadIdx.x; i < kchunk; i += NT) ridx[i] = (int)data_row(rows, kbeg + i, nrows);
     __syncthreads();
   }
 
-  // recompute operands: this wave builds H1 units n0 + 32 wid .. + 31 (2 tiles of 16)
-  bf16x8 w1f[2];
-  float bias1[2][4];
+  // recompute operands: this wave builds H1 units n0 + 16 MTR wid .. (MTR tiles of 16)
+  bf16x8 w1f[MTR];
+  float bias1[MTR][4];
 #pragma unroll
-  for (int mt = 0; mt < 2; ++mt) {
-    const int u = n0 + 32 * wid + 16 * mt + l15;
+  for (int mt = 0; mt < MTR; ++mt) {
+    const int u = n0 + 16 * (MTR * wid + mt) + l15;
     w1f[mt] = 8 * g + 8 <= Fp ? *reinterpret_cast<const bf16x8*>(W1 + (size_t)u * Fp + 8 * g)
                               : bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
 #pragma unroll
-    for (int r = 0; r < 4; ++r) bias1[mt][r] = b1[n0 + 32 * wid + 16 * mt + 4 * g + r];
+    for (int r = 0; r < 4; ++r) bias1[mt][r] = b1[n0 + 16 * (MTR * wid + mt) + 4 * g + r];
   }
-  // X gather: lane -> tile row 16 wid + (lane >> 2), LDS chunk slot lane & 3 holding feature
-  // chunk (slot ^ ((row >> 2) & 3)) (conflict-free fragment reads below)
-  const int xrow = 16 * wid + (lane >> 2);
+  // X gather (waves 0-3): lane -> tile row 16 wid + (lane >> 2), LDS chunk slot lane & 3
+  // holding feature chunk (slot ^ ((row >> 2) & 3)) (conflict-free fragment reads below)
+  const int xrow = 16 * (wid & 3) + (lane >> 2);
   int xc = (lane & 3) ^ ((xrow >> 2) & 3);
   if (8 * xc + 8 > Fp) xc = 0;  // padding: any finite chunk of the same row (W1 there is 0)
   auto issue = [&](int c, int slot) {
     char* st = smem + slot * SLOT;
     QA::issue(dZ2, MF_H, m0, kbeg + c * MF_ROWS, st, wid, lane);
-    const size_t xr = rows != nullptr ? (size_t)ridx[c * MF_ROWS + xrow] : (size_t)(kbeg + c * MF_ROWS + xrow);
-    __builtin_amdgcn_global_load_lds((const void*)(X + xr * Fp + 8 * xc),
-                                     (lds_void*)(st + ABYTES + wid * 1024), 16, 0, 0);
+    if (NW == 4 || xw) {
+      const size_t xr = rows != nullptr ? (size_t)ridx[c * MF_ROWS + xrow] : (size_t)(kbeg + c * MF_ROWS + xrow);
+      __builtin_amdgcn_global_load_lds((const void*)(X + xr * Fp + 8 * xc),
+                                       (lds_void*)(st + ABYTES + (wid & 3) * 1024), 16, 0, 0);
+    }
   };
   using SW = MnSwz<BN>;
   // H1 = relu(X W1^T + b1) of chunk c (X in ring slot) -> H1 image `img` (MN-contiguous operand:
   // element (k = chunk row, n) of the dW GEMM's B operand)
   auto recompute = [&](int slot, int img) {
     const char* st = smem + slot * SLOT;
-    f32x4 a1[2][4];
+    f32x4 a1[MTR][4];
 #pragma unroll
     for (int nt = 0; nt < 4; ++nt) {
       const int r = 16 * nt + l15;
       const bf16x8 xb = *reinterpret_cast<const bf16x8*>(st + ABYTES + r * 64 + ((g ^ ((r >> 2) & 3)) << 4));
 #pragma unroll
-      for (int mt = 0; mt < 2; ++mt)
+      for (int mt = 0; mt < MTR; ++mt)
         a1[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w1f[mt], xb, f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
     }
     const unsigned hbase = (unsigned)(uintptr_t)((__attribute__((address_space(3))) char*)(smem + HOFF + img * HIMG));
 #pragma unroll
-    for (int mt = 0; mt < 2; ++mt)
+    for (int mt = 0; mt < MTR; ++mt)
 #pragma unroll
       for (int nt = 0; nt < 4; ++nt) {
         const int r = 16 * nt + l15;
@@ -1390,26 +1408,28 @@ __global__ __launch_bounds__(256, 1) void mlp2_dw2_kernel(const bf16_t* __restri
           const float v1 = fmaxf(a1[mt][nt][2 * q + 1] + bias1[mt][2 * q + 1], 0.f);
           pk[q] = (unsigned)f2bf(v0) | ((unsigned)f2bf(v1) << 16);
         }
-        const unsigned off = r * (BN * 2) + (SW::pos(2 * wid + mt, SW::hk(r)) << 5) + 8 * g;
+        const unsigned off = r * (BN * 2) + (SW::pos(MTR * wid + mt, SW::hk(r)) << 5) + 8 * g;
         // LDS writes in asm: compiler-visible ones get a vmcnt(0) guard behind the LDS-DMA
         asm volatile("ds_write_b64 %0, %1" ::"v"(hbase + off), "v"(make_uint2(pk[0], pk[1])) : "memory");
       }
   };
-  FragReader<BM, MN_CONTIG, 64> fa;
-  FragReader<BN, MN_CONTIG, 64> fb;
-  fa.init(wm * 64, lane);
-  fb.init(wn * 64, lane);
-  f32x4 acc[4][4];
+  FragReader<BM, MN_CONTIG, C::WTM> fa;
+  FragReader<BN, MN_CONTIG, C::WTN> fb;
+  fa.init(wm * C::WTM, lane);
+  fb.init(wn * C::WTN, lane);
+  f32x4 acc[C::TM][C::TN];
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+  for (int i = 0; i < C::TM; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < C::TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   // prologue: chunks 0..2 in flight, H1 of chunk 0 built
   issue(0, 0);
   if (nk > 1) issue(1, 1);
   if (nk > 2) issue(2, 2);
-  if (nk > 2) wait_vmcnt<2 * LPT>(); else if (nk > 1) wait_vmcnt<LPT>(); else wait_vmcnt<0>();
+  if (nk > 2) dma_wait(std::integral_constant<int, 2>{});
+  else if (nk > 1) dma_wait(std::integral_constant<int, 1>{});
+  else dma_wait(std::integral_constant<int, 0>{});
   __builtin_amdgcn_s_barrier();
   asm volatile("" ::: "memory");
   recompute(0, 0);
@@ -1417,7 +1437,8 @@ __global__ __launch_bounds__(256, 1) void mlp2_dw2_kernel(const bf16_t* __restri
   // chunk c: [wait chunk c+1's DMA, barrier] issue c+3 | build H1(c+1) | dW MFMAs of c
   auto body = [&](int c, auto sc) {
     constexpr int S = decltype(sc)::value;  // == c % 4 (ring slot of chunk c); H1 image c & 1
-    if (c + 2 < nk) wait_vmcnt<LPT>(); else wait_vmcnt<0>();
+    if (c + 2 < nk) dma_wait(std::integral_constant<int, 1>{});
+    else dma_wait(std::integral_constant<int, 0>{});
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's H1 image writes
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
@@ -1425,15 +1446,15 @@ __global__ __launch_bounds__(256, 1) void mlp2_dw2_kernel(const bf16_t* __restri
     if (c + 1 < nk) recompute((S + 1) % DW2_STAGES, (S + 1) & 1);
     static_for<0, 2>([&](auto kc) {
       constexpr int KK = decltype(kc)::value;
-      bf16x8 a[4], b[4];
+      bf16x8 a[C::TM], b[C::TN];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) a[i] = fa.template frag<KK, S * SLOT>(smem, i);
+      for (int i = 0; i < C::TM; ++i) a[i] = fa.template frag<KK, S * SLOT>(smem, i);
 #pragma unroll
-      for (int j = 0; j < 4; ++j) b[j] = fb.template frag<KK, HOFF + (S & 1) * HIMG>(smem, j);
+      for (int j = 0; j < C::TN; ++j) b[j] = fb.template frag<KK, HOFF + (S & 1) * HIMG>(smem, j);
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
+      for (int i = 0; i < C::TM; ++i)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
+        for (int j = 0; j < C::TN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
     });
   };
   int c = 0;
@@ -1448,9 +1469,9 @@ __global__ __launch_bounds__(256, 1) void mlp2_dw2_kernel(const bf16_t* __restri
   if (c + 2 < nk) body(c + 2, std::integral_constant<int, 2>{});
   const AccCoord<C> cc(m0, n0);
 #pragma unroll
-  for (int j = 0; j < 4; ++j)
+  for (int j = 0; j < C::TN; ++j)
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+    for (int i = 0; i < C::TM; ++i)
 #pragma unroll
       for (int r = 0; r < 4; ++r) atomicAdd(dW2 + (size_t)cc.row(i, r) * MF_H + cc.col(j), acc[i][j][r]);
 }
@@ -1465,7 +1486,16 @@ bool launch_mlp2_dw2(const bf16_t* dZ2, const bf16_t* X, int Fp, const long long
   while (nsplit > 1 && chunks % nsplit != 0) --nsplit;
   const int kchunk = (chunks / nsplit) * MF_ROWS;
   if (rows != nullptr && kchunk > DW2_MAX_ROWS) return false;
-  hipLaunchKernelGGL(mlp2_dw2_kernel, dim3(4 * nsplit), dim3(256), 0, s, dZ2, X, Fp, rows, nrows, W1, b1, kchunk, dW2);
+  static const bool dw2_8 = [] {
+    const char* e = std::getenv("WELLFLOW_MLP_DW2_8");
+    return e == nullptr || e[0] != '0';
+  }();
+  if (dw2_8)
+    hipLaunchKernelGGL(mlp2_dw2_kernel<8>, dim3(4 * nsplit), dim3(512), 0, s, dZ2, X, Fp, rows, nrows, W1, b1, kchunk,
+                       dW2);
+  else
+    hipLaunchKernelGGL(mlp2_dw2_kernel<4>, dim3(4 * nsplit), dim3(256), 0, s, dZ2, X, Fp, rows, nrows, W1, b1, kchunk,
+                       dW2);
   return true;
 }
 
