@@ -8,6 +8,8 @@
 // into the (pre-zeroed) fp32 output: the weight-gradient GEMMs here have tiny M x N
 // (<= 2048 x 576) and a huge K (batch x time), so the atomic bytes are <1% of the
 // MFMA time (cdna_hip_programming.md Guideline 12 sizing rule).
+#include <cstdlib>
+
 #include "gemm_core.h"
 #include "kernels.h"
 
@@ -187,7 +189,7 @@ static void launch_dw_big(const bf16_t* A, long lda, const bf16_t* B, long ldb, 
 // Split-K weight-gradient kernel: MN x MN operands, full tiles only (M % BM == N % BN == 0,
 // host-checked), epilogue = fp32 atomic add of alpha * acc (nothing else, so the 144
 // accumulator registers stay in registers).
-template <int BM, int BN, int STAGES, int WM, int WN>
+template <int BM, int BN, int STAGES, int WM, int WN, int PRIO = 0>
 __global__ __launch_bounds__(64 * WM * WN) void gemm_dw_kernel(const bf16_t* __restrict__ A, long lda,
                                                       const bf16_t* __restrict__ B, long ldb, int N,
                                                       int kchunk, int tiles, float* __restrict__ out,
@@ -199,7 +201,7 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_dw_kernel(const bf16_t* __r
   const int split = L / tiles, t = L % tiles;
   const int m0 = (t / tiles_n) * BM, n0 = (t % tiles_n) * BN;
   f32x4 acc[C::TM][C::TN];
-  gemm_mainloop_glds2<C, STAGES>(A, lda, B, ldb, split * kchunk, kchunk / 64, m0, n0, smem, acc);
+  gemm_mainloop_glds2<C, STAGES, PRIO>(A, lda, B, ldb, split * kchunk, kchunk / 64, m0, n0, smem, acc);
   const AccCoord<C> cc(m0, n0);
 #pragma unroll
   for (int j = 0; j < C::TN; ++j)
@@ -232,8 +234,22 @@ static void launch_dw_192(const bf16_t* A, long lda, const bf16_t* B, long ldb, 
   int nsplit = ksplit;
   while (nsplit > 1 && K % (64 * nsplit) != 0) --nsplit;
   const int kchunk = K / nsplit;
-  hipLaunchKernelGGL((gemm_dw_kernel<BM, BN, 2, 4, 2>), dim3(tiles * nsplit), dim3(512), 0, s, A, lda, B, ldb,
-                     N, kchunk, tiles, e.outF, e.ldo, e.alpha);
+  // s_setprio(1) around each MFMA cluster (cdna_hip_programming.md §5.5 T5: hipcc then keeps
+  // the clusters between the barriers): 1.24 -> 1.16 ms at B = 8192 (WELLFLOW_DW_PRIO=0/2: off /
+  // static priority for waves 4-7, no gain)
+  static const int prio = [] {
+    const char* v = std::getenv("WELLFLOW_DW_PRIO");
+    return v == nullptr ? 1 : std::atoi(v);
+  }();
+  if (prio == 1)
+    hipLaunchKernelGGL((gemm_dw_kernel<BM, BN, 2, 4, 2, 1>), dim3(tiles * nsplit), dim3(512), 0, s, A, lda, B, ldb,
+                       N, kchunk, tiles, e.outF, e.ldo, e.alpha);
+  else if (prio == 2)
+    hipLaunchKernelGGL((gemm_dw_kernel<BM, BN, 2, 4, 2, 2>), dim3(tiles * nsplit), dim3(512), 0, s, A, lda, B, ldb,
+                       N, kchunk, tiles, e.outF, e.ldo, e.alpha);
+  else
+    hipLaunchKernelGGL((gemm_dw_kernel<BM, BN, 2, 4, 2>), dim3(tiles * nsplit), dim3(512), 0, s, A, lda, B, ldb,
+                       N, kchunk, tiles, e.outF, e.ldo, e.alpha);
 }
 
 void launch_gemm(const bf16_t* A, long lda, int a_mn, const bf16_t* B, long ldb, int b_mn, int M,

@@ -419,7 +419,9 @@ struct FragReader {
   }
 };
 
-template <class C, int STAGES>
+// PRIO (A/B, cdna_hip_programming.md §5.5 T5): 1 = s_setprio(1) around each MFMA cluster;
+// 2 = the static form, waves 4-7 at priority 1 for the whole loop
+template <class C, int STAGES, int PRIO = 0>
 __device__ __forceinline__ void gemm_mainloop_glds2(const bf16_t* __restrict__ A, long lda,
                                                     const bf16_t* __restrict__ B, long ldb, int kbeg,
                                                     int nk, int m0, int n0, char* smem,
@@ -488,14 +490,19 @@ __device__ __forceinline__ void gemm_mainloop_glds2(const bf16_t* __restrict__ A
       for (int i = 0; i < C::TM; ++i) a[i] = fa.template frag<KK, u * STAGE>(smem, i);
 #pragma unroll
       for (int j = 0; j < C::TN; ++j) b[j] = fbr.template frag<KK, u * STAGE + OA::TILE_BYTES>(smem, j);
+      if constexpr (PRIO == 1) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
       for (int i = 0; i < C::TM; ++i)
 #pragma unroll
         for (int j = 0; j < C::TN; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
+      if constexpr (PRIO == 1) __builtin_amdgcn_s_setprio(0);
     });
   };
 
+  if constexpr (PRIO == 2) {
+    if (__builtin_amdgcn_readfirstlane(threadIdx.x) >= 256) __builtin_amdgcn_s_setprio(1);
+  }
   int t = 0;
   for (; t + STAGES <= nk; t += STAGES)
     static_for<0, STAGES>([&](auto uc) { body(t + decltype(uc)::value, uc); });

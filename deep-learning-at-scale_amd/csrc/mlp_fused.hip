@@ -27,6 +27,15 @@
 namespace wf {
 
 namespace {
+// WELLFLOW_MLP_PRIO bit mask: s_setprio(1) around the MFMA clusters of 1 forward, 2 backward,
+// 4 dW2 (8-wave kernels)
+int mlp_prio() {
+  static const int p = [] {
+    const char* e = std::getenv("WELLFLOW_MLP_PRIO");
+    return e == nullptr ? 0 : std::atoi(e);
+  }();
+  return p;
+}
 constexpr int MF_ROWS = 64;  // rows per chunk
 // dataset row of batch row gr (indices clamped into the dataset: never an out-of-bounds read)
 __device__ __forceinline__ size_t data_row(const long long* rows, int gr, long nrows) {
@@ -311,7 +320,7 @@ __global__ __launch_bounds__(256, 1) void mlp2_fwd_kernel(
 //    dw3 += H2^T dy accumulates in registers.
 //  * three barriers per chunk (X staged, H1 tile complete, head partials complete); the
 //    targets are double-buffered so the next chunk's staging never races this chunk's reads.
-template <int KT1>
+template <int KT1, int PR = 0>  // PR: s_setprio(1) around the layer-2 MFMA cluster (A/B)
 __global__ __launch_bounds__(512, 1) void mlp2_fwd_train_kernel(
     const bf16_t* __restrict__ X, int Fp, const bf16_t* __restrict__ W1, const float* __restrict__ b1,
     const bf16_t* __restrict__ W2, const float* __restrict__ b2, const float* __restrict__ w3,
@@ -422,6 +431,7 @@ __global__ __launch_bounds__(512, 1) void mlp2_fwd_train_kernel(
     for (int m = 0; m < MT; ++m)
 #pragma unroll
       for (int n = 0; n < 4; ++n) acc[m][n] = f32x4{0.f, 0.f, 0.f, 0.f};
+    if constexpr (PR) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int kt = 0; kt < 8; ++kt) {
       bf16x8 hb[4];
@@ -433,6 +443,7 @@ __global__ __launch_bounds__(512, 1) void mlp2_fwd_train_kernel(
         for (int n = 0; n < 4; ++n)
           acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w2f[m][kt], hb[n], acc[m][n], 0, 0, 0);
     }
+    if constexpr (PR) __builtin_amdgcn_s_setprio(0);
     // ---- H2 = relu(Z2 + b2) rounded to bf16 (the values the backward's mask describes), kept
     // in acc; head partial sums and ReLU bits of rows 16n + l15
     float hp[4] = {0.f, 0.f, 0.f, 0.f};
@@ -1064,7 +1075,7 @@ __global__ __launch_bounds__(256, 1) void mlp2_bwd_rc_kernel(
 // other's MFMAs. The dZ2 and X tiles are double-buffered and the H1 / dZ1 tile is wave-private
 // (every wave reads back only its own units), so a chunk needs ONE workgroup barrier: the
 // next chunk's staging writes the other buffer, whose last readers passed this barrier.
-template <int NFT>
+template <int NFT, int PR = 0>  // PR: s_setprio(1) around the dH1 MFMA cluster (A/B)
 __global__ __launch_bounds__(512, 1) void mlp2_bwd_rc8_kernel(
     const unsigned* __restrict__ M2, const float* __restrict__ dy, const float* __restrict__ w3,
     const bf16_t* __restrict__ W2, const bf16_t* __restrict__ X, int Fp, bf16_t* __restrict__ dZ2,
@@ -1188,6 +1199,7 @@ __global__ __launch_bounds__(512, 1) void mlp2_bwd_rc8_kernel(
     for (int m = 0; m < MT; ++m)
 #pragma unroll
       for (int n = 0; n < 4; ++n) acc[m][n] = f32x4{0.f, 0.f, 0.f, 0.f};
+    if constexpr (PR) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int kt = 0; kt < 8; ++kt) {
       bf16x8 zb[4];
@@ -1199,6 +1211,7 @@ __global__ __launch_bounds__(512, 1) void mlp2_bwd_rc8_kernel(
         for (int n = 0; n < 4; ++n)
           acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wt[m][kt], zb[n], acc[m][n], 0, 0, 0);
     }
+    if constexpr (PR) __builtin_amdgcn_s_setprio(0);
     // ---- dZ1 = dH1 * [H1 > 0] into the same 8 bytes of hs; db1 partials
 #pragma unroll
     for (int m = 0; m < MT; ++m)
@@ -1313,7 +1326,7 @@ constexpr int DW2_MAX_ROWS = 8192;  // rows per workgroup (the LDS row-id table)
 // per SIMD, 2(M) x 4(N) of 64x32, 16 H1 units each, so one wave's H1 rebuild (VALU) and
 // fragment reads overlap the other's MFMAs. The X tile is 4 one-KiB pieces, issued by waves
 // 0-3: with 8 waves the DMA count per chunk differs by wave (dma_wait below).
-template <int NW>
+template <int NW, int PR = 0>  // PR: s_setprio(1) around each MFMA cluster (A/B)
 __global__ __launch_bounds__(64 * NW, 1) void mlp2_dw2_kernel(const bf16_t* __restrict__ dZ2, const bf16_t* __restrict__ X,
                                                               int Fp, const long long* __restrict__ rows, long nrows,
                                                               const bf16_t* __restrict__ W1, const float* __restrict__ b1,
@@ -1451,10 +1464,12 @@ __global__ __launch_bounds__(64 * NW, 1) void mlp2_dw2_kernel(const bf16_t* __re
       for (int i = 0; i < C::TM; ++i) a[i] = fa.template frag<KK, S * SLOT>(smem, i);
 #pragma unroll
       for (int j = 0; j < C::TN; ++j) b[j] = fb.template frag<KK, HOFF + (S & 1) * HIMG>(smem, j);
+      if constexpr (PR) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
       for (int i = 0; i < C::TM; ++i)
 #pragma unroll
         for (int j = 0; j < C::TN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
+      if constexpr (PR) __builtin_amdgcn_s_setprio(0);
     });
   };
   int c = 0;
@@ -1490,7 +1505,10 @@ bool launch_mlp2_dw2(const bf16_t* dZ2, const bf16_t* X, int Fp, const long long
     const char* e = std::getenv("WELLFLOW_MLP_DW2_8");
     return e == nullptr || e[0] != '0';
   }();
-  if (dw2_8)
+  if (dw2_8 && (mlp_prio() & 4))
+    hipLaunchKernelGGL((mlp2_dw2_kernel<8, 1>), dim3(4 * nsplit), dim3(512), 0, s, dZ2, X, Fp, rows, nrows, W1, b1, kchunk,
+                       dW2);
+  else if (dw2_8)
     hipLaunchKernelGGL(mlp2_dw2_kernel<8>, dim3(4 * nsplit), dim3(512), 0, s, dZ2, X, Fp, rows, nrows, W1, b1, kchunk,
                        dW2);
   else
@@ -1518,7 +1536,10 @@ bool launch_mlp2_bwd(const bf16_t* H1, const bf16_t* H2, const unsigned* M2, con
       return e == nullptr || e[0] != '0';
     }();
     if (bwd8) {
-      if (Fp <= 16)
+      if (Fp <= 16 && (mlp_prio() & 2))
+        hipLaunchKernelGGL((mlp2_bwd_rc8_kernel<1, 1>), dim3(grid), dim3(512), 0, s, M2, dy, w3, W2, X, Fp, dZ2, dW1, db1,
+                           db2, B, W1, b1, rows, nrows);
+      else if (Fp <= 16)
         hipLaunchKernelGGL(mlp2_bwd_rc8_kernel<1>, dim3(grid), dim3(512), 0, s, M2, dy, w3, W2, X, Fp, dZ2, dW1, db1,
                            db2, B, W1, b1, rows, nrows);
       else
@@ -1560,7 +1581,10 @@ bool launch_mlp2_fwd(const bf16_t* X, int Fp, const bf16_t* W1, const float* b1,
     return e == nullptr || e[0] != '0';
   }();
   if (fwd8 && M2 != nullptr && H1 == nullptr) {  // the training step (mask mode never writes H2)
-    if (Fp <= 32)
+    if (Fp <= 32 && (mlp_prio() & 1))
+      hipLaunchKernelGGL((mlp2_fwd_train_kernel<1, 1>), dim3(grid), dim3(512), 0, s, X, Fp, W1, b1, W2, b2, w3, b3, y,
+                         M2, dw3, db3, pred, dy, loss_sum, dy_scale, B, rows, nrows);
+    else if (Fp <= 32)
       hipLaunchKernelGGL(mlp2_fwd_train_kernel<1>, dim3(grid), dim3(512), 0, s, X, Fp, W1, b1, W2, b2, w3, b3, y, M2,
                          dw3, db3, pred, dy, loss_sum, dy_scale, B, rows, nrows);
     else
