@@ -37,6 +37,17 @@ __device__ __forceinline__ float sigmoidf_(float x) {
   return __builtin_amdgcn_rcpf(1.0f + __expf(-x));
 }
 
+// LSTM gates from PRE-SCALED pre-activations: lstm_pack_weights folds -log2(e) (sigmoid
+// gates) and 2 log2(e) (the tanh gate) into the forward's bf16 weights Wp, so each gate is
+// one v_exp_f32 (2^x) + add + v_rcp_f32 with no scaling multiply (the persistent forward's
+// MFMA loop is vector-issue bound: cell math shares the SIMD's issue slots with the MFMAs)
+constexpr float kLstmSigScale = -1.4426950408889634f;  // -log2(e)
+constexpr float kLstmTanhScale = 2.8853900817779268f;  // 2 log2(e)
+__device__ __forceinline__ float sigmoid_pre(float zs) { return __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(zs)); }
+__device__ __forceinline__ float tanh_pre(float zs) {
+  return 1.0f - 2.0f * __builtin_amdgcn_rcpf(__builtin_amdgcn_exp2f(zs) + 1.0f);
+}
+
 __device__ __forceinline__ float tanhf_(float x) {
   // tanh(x) = 1 - 2/(exp(2x)+1); saturates cleanly for |x| large (exp -> inf or 0).
   return 1.0f - 2.0f * __builtin_amdgcn_rcpf(__expf(2.0f * x) + 1.0f);

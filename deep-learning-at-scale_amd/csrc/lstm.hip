@@ -99,10 +99,10 @@ __global__ __launch_bounds__(64 * WM * WN) void lstm_fwd_step_kernel(int t, bf16
     unsigned pk[8];
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      const float ig = sigmoidf_(acc[i][0][r]);
-      const float fg = sigmoidf_(acc[i][1][r]);
-      const float gg = tanhf_(acc[i][2][r]);
-      const float og = sigmoidf_(acc[i][3][r]);
+      const float ig = sigmoid_pre(acc[i][0][r]);  // Wp carries the gate scales (pack kernel)
+      const float fg = sigmoid_pre(acc[i][1][r]);
+      const float gg = tanh_pre(acc[i][2][r]);
+      const float og = sigmoid_pre(acc[i][3][r]);
       const float c = fg * cpv[r] + ig * gg;
       cv[r] = c;
       pk[2 * r] = (unsigned)f2bf(ig) | ((unsigned)f2bf(fg) << 16);
@@ -302,7 +302,8 @@ void launch_lstm_bwd_step(int t, const bf16_t* WhhT, const float* Cst, const bf1
 }
 
 // fp32 master W [G][KA] (rows in dg_col order) -> bf16 Wp [G][KA] (rows in gate_col order,
-// the forward's) and WhhT [H][G] (columns in dg_col order, the backward's).
+// the forward's, each gate row pre-scaled for sigmoid_pre / tanh_pre: common.h) and WhhT
+// [H][G] (columns in dg_col order, the backward's, unscaled).
 __global__ void lstm_pack_weights_kernel(const float* __restrict__ W, bf16_t* __restrict__ Wp,
                                          bf16_t* __restrict__ WhhT, LstmDims d) {
   const int KA = d.KX + d.H, G = 4 * d.H;
@@ -310,9 +311,10 @@ __global__ void lstm_pack_weights_kernel(const float* __restrict__ W, bf16_t* __
   for (long idx = blockIdx.x * (long)blockDim.x + threadIdx.x; idx < total;
        idx += (long)gridDim.x * blockDim.x) {
     const int k = idx % KA, p = idx / KA;
-    const bf16_t v = f2bf(W[idx]);
-    Wp[(size_t)gate_col(p & 3, p >> 2) * KA + k] = v;
-    if (k >= d.KX) WhhT[(size_t)(k - d.KX) * G + p] = v;
+    const float w = W[idx];
+    const float sc = (p & 3) == 2 ? kLstmTanhScale : kLstmSigScale;
+    Wp[(size_t)gate_col(p & 3, p >> 2) * KA + k] = f2bf(w * sc);
+    if (k >= d.KX) WhhT[(size_t)(k - d.KX) * G + p] = f2bf(w);
   }
 }
 

@@ -190,10 +190,10 @@ __global__ __launch_bounds__(256, 1) void lstm_fwd_persistent_kernel(
 
     // cell epilogue element (row-tile i, row r) of the carried chunk: accp + c_{t-1} = cq[0]
     auto epi_elem = [&](int i, int r, float (&cv)[2][4], unsigned (&pk)[2][8], unsigned (&hv)[2][4]) {
-      const float ig = sigmoidf_(accp[i][0][r]);
-      const float fg = sigmoidf_(accp[i][1][r]);
-      const float gg = tanhf_(accp[i][2][r]);
-      const float og = sigmoidf_(accp[i][3][r]);
+      const float ig = sigmoid_pre(accp[i][0][r]);  // Wp carries the gate scales (pack kernel)
+      const float fg = sigmoid_pre(accp[i][1][r]);
+      const float gg = tanh_pre(accp[i][2][r]);
+      const float og = sigmoid_pre(accp[i][3][r]);
       const float cn = fg * cq[0][i][r] + ig * gg;
       cv[i][r] = cn;
       pk[i][2 * r] = (unsigned)f2bf(ig) | ((unsigned)f2bf(fg) << 16);
