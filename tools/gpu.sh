@@ -10,7 +10,8 @@
 #   tools/gpu.sh ksweep VAR "v1 v2 .." KERNEL [bench args]  the same under rocprofv3 --kernel-trace,
 #                                 printing the stats line of kernels matching KERNEL per value
 #   tools/gpu.sh pmcsets "SET1" "SET2" ..   one rocprofv3 --pmc pass per counter set over a 2-step
-#                                 LSTM bench (--no-graph) -> gpurun_out/pmc/setN
+#                                 LSTM bench (--no-graph; PMC_ARGS overrides the bench args)
+#                                 -> gpurun_out/pmc/setN (tools/pmc_table.py summarises them)
 #   tools/gpu.sh tool SCRIPT [args]   a diagnostic script under tools/ (pf_time.py, pb_time.py,
 #                                 pf_timeline.py, pb_timeline.py, tune_lstm.py, dw_vs_blas.py, ...)
 # Every GPU step has its own time limit and the steps are chained: the first failure ends it.
@@ -65,12 +66,13 @@ case "$what" in
       echo "$var=$v $(grep -h "$kern" "gpurun_out/ks_$v/run_kernel_stats.csv" | cut -d, -f1-5)"
     done ;;
   pmcsets)
+    rm -rf gpurun_out/pmc
     mkdir -p gpurun_out/pmc
     i=0
     for set in "$@"; do
       i=$((i+1))
       timeout -s KILL 150 rocprofv3 --pmc $set --output-format csv -d gpurun_out/pmc/set$i -o run \
-        -- python3 bench.py --steps 2 --warmup 1 --no-graph > gpurun_out/pmc/set$i.log 2>&1 || { tail -5 gpurun_out/pmc/set$i.log; exit 1; }
+        -- python3 bench.py ${PMC_ARGS:---steps 2 --warmup 1 --no-graph} > gpurun_out/pmc/set$i.log 2>&1 || { tail -5 gpurun_out/pmc/set$i.log; exit 1; }
     done ;;
   tool)
     script="$1"; shift
