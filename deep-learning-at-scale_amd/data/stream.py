@@ -8,14 +8,15 @@ synthetic generator). Pinned sources (``HostPool``) are copied straight from the
 pages; anything else is first staged into a pinned ring (one host memcpy, then an async
 DMA), so the H2D copy never runs synchronously from pageable memory.
 
-Issue order (measured on MI355X, tools/online_host.py): a copy-stream wait on compute work
-makes the host block inside the copy call until that compute has finished, so the ring is
-refilled with a lag of two: at batch k the slot of batch k-2 is refilled, waiting only on an
-event recorded right after batch k-2's compute, while batch k-1's compute is already queued.
-(A producer thread issuing the copies instead was slower: it contends for the GIL with the
-training loop.) On the shared MI355X host the copies themselves are the limit: median 0.21 ms
-per 9.4 MB batch (~45 GB/s, fully hidden under a 0.275 ms step) but 4-5 % of them stall for
-3-6 ms (bench.py reports h2d_ms_median / max / over_1ms for every online run).
+Ordering (measured on MI355X, tools/online_host.py, bench.py h2d_* fields): a copy-stream
+wait on an event of the compute stream (a cross-queue dependency, compute queue -> SDMA) made
+4-5 % of the 9.4 MB batch copies stall for 3-6 ms (0.38-0.47 ms per step instead of 0.275).
+The slot's reuse is therefore ordered on the HOST: before refilling the slot of batch k-2 the
+producer synchronizes on an event recorded right after batch k-2's compute (batch k-1's compute
+is already queued, so the GPU never runs dry), and the copy itself has no queue dependency.
+With that the streamed step runs at the static step's speed (952 vs 950 M rows/s; copies
+median 0.22 ms, max 0.24 ms). A producer thread issuing the copies was slower (GIL
+contention), and so were extra copy streams.
 
 The device ring buffers keep their addresses for the streamer's lifetime — a hipGraph
 captured on slot k (train/step.py StepRunner: one graph per slot) stays valid — and a new
@@ -27,6 +28,7 @@ Inputs can be streamed as bf16 (the MFMA engines consume bf16 directly), halving
 from __future__ import annotations
 
 import itertools
+import os
 
 import torch
 
@@ -57,6 +59,9 @@ class DeviceStreamer:
         self.x_dtype = x_dtype
         self.slots = []    # [x_dev, y_dev, ready event] — fixed addresses
         self.consumed = [None] * depth  # per slot: event after the compute that read it
+        # slot reuse is ordered on the host (event.synchronize) instead of by a copy-queue wait
+        # on the compute stream: module docstring (WELLFLOW_H2D_HOSTWAIT=0: queue wait)
+        self.host_wait = os.environ.get("WELLFLOW_H2D_HOSTWAIT", "1") != "0"
         self.timing = timing
         self._tev = []  # (start, end) events of timed batches
         self.staging = []  # pinned host ring for pageable sources: [x_pin, y_pin]
@@ -131,7 +136,10 @@ class DeviceStreamer:
         # the whole compute stream: see the module docstring)
         done = self.consumed[slot]
         if done is not None:
-            self.copy_stream.wait_event(done)
+            if self.host_wait:  # the host waits, the copy queue gets no cross-queue dependency
+                done.synchronize()
+            else:
+                self.copy_stream.wait_event(done)
         with torch.cuda.stream(self.copy_stream):
             if self.timing:
                 t0, t1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)

@@ -2,7 +2,7 @@
 """Steady-state training throughput of the PRODUCTION job path (train/job.py -> Trainer ->
 StepRunner) at the bench's per-GPU batch, next to bench.py's number for the same step.
 
-    python tools/job_throughput.py [--model lstm|mlp] [--out profiles/r2/job_vs_bench_lstm.json]
+    python tools/job_throughput.py [--model lstm|mlp|mlp_online] [--out profiles/r2/job_vs_bench_lstm.json]
 
 The job trains on a synthetic well-log table (CSV-free: the generator stands in for the
 ingest) through feature engineering, the time-block split, the resident dataset with
@@ -25,7 +25,7 @@ TYPES = "string,string,int,float,float,float,float,float,float,float"
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--model", default="lstm", choices=["lstm", "mlp"])
+    ap.add_argument("--model", default="lstm", choices=["lstm", "mlp", "mlp_online"])
     ap.add_argument("--epochs", type=int, default=4)
     ap.add_argument("--out", default=None)
     a = ap.parse_args()
@@ -34,8 +34,10 @@ def main():
 
     if a.model == "lstm":
         batch, extra, wells, steps = 8192, ["--seq-len", "64", "--hidden", "512"], 6, 40000
-    else:
+    elif a.model == "mlp":
         batch, extra, wells, steps = 262144, [], 6, 640000
+    else:  # the stream: chunks of 8 mini-batches, each consumed once (train/online.py)
+        batch, extra, wells, steps = 262144, ["--online-chunk", str(8 * 262144)], 6, 640000
     # 6 wells (3 fields): 5 + 2 one-hot columns + 9 continuous = 16 features, the bench's F
     argv = [NAMES, TYPES, "flow", "/tmp/wellflow_jobtp/", "--epochs", str(a.epochs), "--patience", "100",
             "--synth-wells", str(wells), "--synth-steps", str(steps), "--batch-size", str(batch),
