@@ -29,14 +29,20 @@ typedef __attribute__((address_space(3))) bf16x4 lds_bf16x4;
 // MN_CONTIG image swizzle for an R-row tile ([64 k][R] bf16, C = R/16 32-B chunks per k-row):
 // data chunk j of k-row k sits in slot pos(j, hk(k)). Power-of-two C: XOR (as before);
 // other C (the 288-wide weight-gradient tile): rotation mod C, still a bijection per row.
+// 192-wide (C = 12) images rotate by h >> 1, not h: a 384-B k-row is 128 B mod the 256-B bank
+// line, so row parity already shifts a 32-lane ds_read_b64_tr_b16 group by half a line; rotating
+// by h as well put lanes (q, g) and (q, g + 1) on one bank pair for j >= 5 (PMC: 7.7 % of the
+// dW kernel's cycles in bank conflicts). Rotation by h >> 1 is conflict-free for every j
+// (exhaustive check over the fragment-read lane pattern); C = 18 keeps rotation by h.
 template <int R>
 struct MnSwz {
   static constexpr int C = R / 16;
   static constexpr bool POW2 = (C & (C - 1)) == 0;
+  static constexpr int RSH = C == 12 ? 1 : 0;
   __host__ __device__ static constexpr int hmask() { return POW2 ? C - 1 : 7; }
   __device__ static __forceinline__ int hk(int k) { return ((k & 3) | ((k >> 1) & 4)) & hmask(); }
-  __device__ static __forceinline__ int pos(int j, int h) { return POW2 ? (j ^ h) : (j + h) % C; }
-  __device__ static __forceinline__ int data(int p, int h) { return POW2 ? (p ^ h) : (p + C - h) % C; }
+  __device__ static __forceinline__ int pos(int j, int h) { return POW2 ? (j ^ h) : (j + (h >> RSH)) % C; }
+  __device__ static __forceinline__ int data(int p, int h) { return POW2 ? (p ^ h) : (p + C - (h >> RSH)) % C; }
 };
 
 template <int R, int L, int NT_ = 256>
