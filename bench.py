@@ -241,6 +241,8 @@ def main() -> int:
     args = ap.parse_args()
     if args.batch is None:
         args.batch = DEFAULT_BATCH[args.model]
+        if args.device == "cpu":  # the fp32 CPU rehearsal: N ranks share one host's memory
+            args.batch = {"lstm": 256, "mlp": 8192, "mlp_online": 8192}[args.model]
 
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
         return _spawn_ranks(args.gpus, sys.argv[1:])
