@@ -150,15 +150,17 @@ void check_lstm_state(const at::Tensor& XH, const at::Tensor& Cst, const at::Ten
   check_extent(S, (int64_t)d.T * Bp * G, "S");
 }
 
+// full = false: only the feature chunks (the buffer's constant 1 column / zero padding were
+// written by an earlier full pack of the same B)
 void lstm_pack_x(const at::Tensor& x, const at::Tensor& XH, int64_t B, int64_t T, int64_t F,
-                 int64_t KX, int64_t H) {
+                 int64_t KX, int64_t H, bool full) {
   auto d = lstm_dims(B, T, F, KX, H);
   check_t(x, at::kFloat, "x");
   check_extent(x, B * T * F, "x");
   check_t(XH, at::kBFloat16, "XH");
   check_extent(XH, (T + 1) * B * (KX + H), "XH");
   const c10::hip::OptionalHIPGuardMasqueradingAsCUDA guard(x.device());
-  wf::launch_lstm_pack_x(fp(x), bfp(XH), d, cur_stream());
+  wf::launch_lstm_pack_x(fp(x), bfp(XH), d, cur_stream(), full);
 }
 
 void lstm_forward(const at::Tensor& XH, const at::Tensor& Wp, const at::Tensor& Cst,

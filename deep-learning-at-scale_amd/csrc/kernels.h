@@ -43,7 +43,7 @@ struct LstmDims {
   int row_off = 0;      // persistent kernels: first batch row of this sub-batch launch
   unsigned spin_limit = 0;  // persistent hand-off spin bound (0 = built-in; tests shrink it)
 };
-void launch_lstm_pack_x(const float* x, bf16_t* XH, LstmDims d, hipStream_t s);
+void launch_lstm_pack_x(const float* x, bf16_t* XH, LstmDims d, hipStream_t s, bool full = true);
 void launch_lstm_fwd_step(int t, bf16_t* XH, const bf16_t* Wp, float* Cst, bf16_t* S,
                           LstmDims d, hipStream_t s);
 // All T forward steps in ONE persistent launch per sub-batch (lstm_persistent.hip). `sync`

@@ -26,9 +26,12 @@ namespace wf {
 // row (KX/8 lanes per row, rows of one timestep consecutive): every store instruction
 // writes whole 128-B lines of 8 rows instead of 64 partial lines (the thread-per-row
 // version ran at 1.6 TB/s).
+// cpr = 16-B chunks written per row: all KX/8 (full: the constant 1 column and the zero
+// padding too) or only the ones holding features and the 1 column (the rest of the x block is
+// constant, so after one full pack of a buffer the per-step pack writes 3 of 8 chunks at F = 16)
 __global__ void lstm_pack_x_kernel(const float* __restrict__ x, bf16_t* __restrict__ XH,
-                                   LstmDims d) {
-  const int KA = d.KX + d.H, CPR = d.KX >> 3;  // 16-B chunks per row
+                                   LstmDims d, int cpr) {
+  const int KA = d.KX + d.H, CPR = cpr;
   const long total = (long)d.T * d.B * CPR;
   for (long idx = blockIdx.x * (long)blockDim.x + threadIdx.x; idx < total;
        idx += (long)gridDim.x * blockDim.x) {
@@ -49,11 +52,12 @@ __global__ void lstm_pack_x_kernel(const float* __restrict__ x, bf16_t* __restri
   }
 }
 
-void launch_lstm_pack_x(const float* x, bf16_t* XH, LstmDims d, hipStream_t s) {
-  const long total = (long)d.T * d.B * (d.KX >> 3);
+void launch_lstm_pack_x(const float* x, bf16_t* XH, LstmDims d, hipStream_t s, bool full) {
+  const int cpr = full ? (d.KX >> 3) : (d.F + 1 + 7) / 8;
+  const long total = (long)d.T * d.B * cpr;
   int blocks = (int)((total + 255) / 256);
   if (blocks > 16384) blocks = 16384;
-  hipLaunchKernelGGL(lstm_pack_x_kernel, dim3(blocks), dim3(256), 0, s, x, XH, d);
+  hipLaunchKernelGGL(lstm_pack_x_kernel, dim3(blocks), dim3(256), 0, s, x, XH, d, cpr);
 }
 
 // STAGES == 0: register-staged mainloop (any batch); STAGES >= 2: direct-to-LDS ring

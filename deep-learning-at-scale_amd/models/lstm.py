@@ -161,6 +161,7 @@ class NativeLSTM:
         self.DG = torch.empty(T * B * lay.G, dtype=bf, device=dev)
         self.dcarry = torch.empty(Bp * H, dtype=torch.float32, device=dev)
         self.Wp = torch.empty(lay.G * lay.KA, dtype=bf, device=dev)
+        self._xh_const = False  # XH's constant x-block columns written (_pack_x)
         self.WhhT = torch.empty(H * lay.G, dtype=bf, device=dev)
         self.pred = torch.empty(B, dtype=torch.float32, device=dev)
         self.dy = torch.empty(B, dtype=torch.float32, device=dev)
@@ -193,6 +194,13 @@ class NativeLSTM:
 
     def _dims(self, B):
         return (B, self.T, self.F, self.lay.KX, self.H)
+
+    def _pack_x(self, x, B):
+        """x -> the bf16 x block of XH. The block's constant part (the 1 column of the bias,
+        the zero padding up to KX) is written by the first pack only: later packs write the
+        feature chunks alone (csrc/lstm.hip lstm_pack_x_kernel)."""
+        self._C.lstm_pack_x(x, self.XH, *self._dims(B), not self._xh_const)
+        self._xh_const = True
 
     def _hT(self, B):
         lay = self.lay
@@ -253,7 +261,7 @@ class NativeLSTM:
             xp[:B] = x
             x = xp
         C = self._C
-        C.lstm_pack_x(x, self.XH, *self._dims(self.B))
+        self._pack_x(x, self.B)
         self._forward_steps(self.B)
         _, w_out, b_out = self.lay.views(self.params)
         C.head_fwd(self._hT(self.B), self.lay.KA, self.B, self.H, w_out, b_out, None, self.pred,
@@ -277,7 +285,7 @@ class NativeLSTM:
         if zero_grads:
             self.grads.zero_()
         self.loss_sum.zero_()
-        C.lstm_pack_x(x.contiguous(), self.XH, *self._dims(B))
+        self._pack_x(x.contiguous(), B)
         self._forward_steps(B)
         hT = self._hT(B)
         y = y.contiguous().float()

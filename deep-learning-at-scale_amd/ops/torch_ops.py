@@ -163,7 +163,7 @@ def _lstm_fwd(x: torch.Tensor, flat: torch.Tensor, H: int, KX: int) -> tuple[tor
     W, w_out, b_out = lay.views(flat)
     C.lstm_pack_weights(W.contiguous(), Wp[: lay.G * lay.KA], Wp[lay.G * lay.KA:], H, KX)
     dims = _lstm_dims(B, T, F, KX, H)
-    C.lstm_pack_x(x.float().contiguous(), XH, *dims)
+    C.lstm_pack_x(x.float().contiguous(), XH, *dims, True)
     sync = torch.zeros(16 + 16 * (B // 32 + 1), dtype=torch.int32, device=dev)
     if not C.lstm_forward_persistent(XH, Wp[: lay.G * lay.KA], Cst, S, sync, *dims):
         C.lstm_forward(XH, Wp[: lay.G * lay.KA], Cst, S, *dims, 6)

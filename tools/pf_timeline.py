@@ -15,7 +15,7 @@ eng.params.copy_(init_lstm_flat(F, H, seed=1).cuda())
 eng.sync_weights()
 x = torch.randn(B, T, F, device="cuda")
 C, dims = eng._C, eng._dims(B)
-C.lstm_pack_x(x, eng.XH, *dims)
+C.lstm_pack_x(x, eng.XH, *dims, True)
 sync = torch.zeros(4096 + 2 * 64 * 256, dtype=torch.int32, device="cuda")
 os.environ["WELLFLOW_PF_DBG"] = sys.argv[1] if len(sys.argv) > 1 else "16"
 for _ in range(3):
