@@ -13,6 +13,7 @@ all-reduce captured inside it.
 Secondary configs (BASELINE.json:8-10), same JSON contract:
   --model mlp         static 3-layer MLP (F -> 256 -> 256 -> 1), resident batch
   --model mlp_online  dynamic MLP: every step trains on a NEW mini-batch streamed host -> HBM
+  --model cnn         the reference's own 1-D CNN (cnn.py:110-118), SGD-Nesterov, 65,536 windows
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B_per_gpu] [--model ...]
 
@@ -37,7 +38,7 @@ if ROOT not in sys.path:
 METRIC = "rows/sec (whole node), LSTM seq64 regression at 1/2/4/8 MI355X; val MSE parity"
 # per-GPU rows per step. MLP: 262144 rows (bf16 activations ~270 MB of 288 GB HBM) — at
 # 65536 the 0.24 ms step is launch/stream-overhead bound (216-272 M rows/s vs 382 M here)
-DEFAULT_BATCH = {"lstm": 8192, "mlp": 262144, "mlp_online": 262144}
+DEFAULT_BATCH = {"lstm": 8192, "mlp": 262144, "mlp_online": 262144, "cnn": 65536}
 
 
 def _free_port() -> int:
@@ -150,6 +151,12 @@ def _cpu_rehearsal(args, ctx, model):
     if args.model == "lstm":
         eng = TorchEngine(LSTMRegressor(F, args.hidden))
         x, y = synth_lstm_batch(B, args.seq, F, seed=ctx.rank)
+    elif args.model == "cnn":
+        from wellflow.models.cnn import CNN1DRegressor
+
+        eng = TorchEngine(CNN1DRegressor(), loss="mae_clip", clip=6.0)
+        series = torch.randn(B, 60).cumsum(1) * 0.1
+        x, y = series[:, :48].contiguous(), series[:, 48:].contiguous()
     else:
         eng = TorchEngine(MLPRegressor(F, (256, 256)))
         x, y = synth_tabular_batch(B, F, seed=ctx.rank)
@@ -158,6 +165,38 @@ def _cpu_rehearsal(args, ctx, model):
     run = StepRunner(eng, opt, ctx, 1.0 / (B * ctx.world_size), lambda k: (x, y))
     el = _timed(ctx, run.run, args.steps, args.warmup)
     return el, B, model, run.take_loss() / (B * (args.steps + args.warmup)), run, eng, {}
+
+
+def bench_cnn(args, ctx):
+    """The reference's own model (cnn.py:110-118): Conv1D(1->100, k=13, ReLU) -> Dropout 0.5 ->
+    Dense 3600->12, clipped-MAE loss, Keras SGD-Nesterov (lr .001, momentum .99, decay 1e-6),
+    on 48-step windows; the step is NativeCNN (im2col + MFMA GEMMs with fused bias / ReLU /
+    dropout epilogues, split-K weight gradients) through the same StepRunner."""
+    import torch
+
+    from wellflow.models.cnn import CNN1DRegressor, CnnLayout, NativeCNN
+    from wellflow.optim.flat import FlatSGD
+    from wellflow.train.step import StepRunner
+
+    lay = CnnLayout()
+    B = args.batch
+    model = "1-D CNN (reference cnn.py): 48-step window, Conv1D 100x13 + ReLU, dropout 0.5, Dense 3600->12, clipped MAE, SGD-Nesterov"
+    ref = CNN1DRegressor(lay.input_len, lay.in_ch, lay.filters, lay.kernel, lay.outputs)
+    if ctx.device.type == "cpu":
+        return _cpu_rehearsal(args, ctx, model)
+    eng = NativeCNN(lay, B, ctx.device)
+    eng.params.copy_(ref.to_flat().to(ctx.device))
+    ctx.broadcast_(eng.params)
+    eng.sync_weights()
+    opt = FlatSGD(eng.params, eng.grads, zero_grads=True)
+    g = torch.Generator(device="cpu").manual_seed(ctx.rank)
+    series = torch.randn(B, lay.input_len + lay.outputs, generator=g).cumsum(1) * 0.1  # random-walk windows
+    x = series[:, : lay.input_len].contiguous().to(ctx.device)
+    y = series[:, lay.input_len :].contiguous().to(ctx.device)
+    run = StepRunner(eng, opt, ctx, 1.0 / (B * ctx.world_size * lay.outputs), lambda k: (x, y),
+                     graph=not args.no_graph, comm_in_graph=not args.eager_comm)
+    el = _timed(ctx, run.run, args.steps, args.warmup)
+    return el, B, model, run.take_loss() / (B * lay.outputs * (args.steps + args.warmup)), run, eng, {}
 
 
 def bench_mlp(args, ctx, online: bool):
@@ -223,7 +262,7 @@ def main() -> int:
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--model", choices=["lstm", "mlp", "mlp_online"], default="lstm")
+    ap.add_argument("--model", choices=["lstm", "mlp", "mlp_online", "cnn"], default="lstm")
     ap.add_argument("--batch", type=int, default=None, help="per-GPU batch (rows)")
     ap.add_argument("--seq", type=int, default=64)
     ap.add_argument("--hidden", type=int, default=512)
@@ -242,7 +281,7 @@ def main() -> int:
     if args.batch is None:
         args.batch = DEFAULT_BATCH[args.model]
         if args.device == "cpu":  # the fp32 CPU rehearsal: N ranks share one host's memory
-            args.batch = {"lstm": 256, "mlp": 8192, "mlp_online": 8192}[args.model]
+            args.batch = {"lstm": 256, "mlp": 8192, "mlp_online": 8192, "cnn": 1024}[args.model]
 
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
         return _spawn_ranks(args.gpus, sys.argv[1:])
@@ -264,6 +303,8 @@ def main() -> int:
     torch.manual_seed(1234 + ctx.rank)
     if args.model == "lstm":
         elapsed, B, model, loss, run, eng, extra = bench_lstm(args, ctx)
+    elif args.model == "cnn":
+        elapsed, B, model, loss, run, eng, extra = bench_cnn(args, ctx)
     else:
         elapsed, B, model, loss, run, eng, extra = bench_mlp(args, ctx, online=args.model == "mlp_online")
     comm = _comm_ms(ctx, eng.grads)
@@ -291,7 +332,8 @@ def main() -> int:
             "scaling": "weak",
             "vs_baseline": None,  # the reference publishes no numbers (BASELINE.json "published": {})
             "dtype": "fp32" if cpu else "bf16",
-            "data": "synthetic (Gilbert-equation well-log data), random-init weights"
+            "data": ("synthetic random-walk windows" if args.model == "cnn"
+                     else "synthetic (Gilbert-equation well-log data)") + ", random-init weights"
                     + ("; CPU contract rehearsal, not a benchmark" if cpu else ""),
             "config": {
                 "model": model,
@@ -307,7 +349,7 @@ def main() -> int:
             "grad_bucket_mb": round(eng.grads.numel() * 4 / 2**20, 3),
             "step_graph": bool(run.graphs),
             "comm_in_graph": bool(run.captured_comm),
-            "train_loss": round(loss, 6),  # lstm: last step; mlp / cpu: mean over the run
+            "train_loss": round(loss, 6),  # lstm: last step; mlp / cnn / cpu: mean over the run
             **extra,
         }
         print(json.dumps(rec), flush=True)
