@@ -22,6 +22,7 @@ from __future__ import annotations
 
 import dataclasses
 import math
+import os
 
 import torch
 from torch import nn
@@ -209,14 +210,17 @@ class NativeCNN:
         self._C.loss(kind, self.pred, self.ypad, B, L.Op, self.clip, float(grad_scale),
                      self.loss_sum, self.dpred, None, gbd)
         # dWd = dpred^T Hc   (reduce over batch)
-        ks = max(1, min(16, B // 256))
+        ks = int(os.environ.get("WELLFLOW_CNN_KS1", "0")) or max(1, min(16, B // 256))
         gemm(self.dpred, self.Hc, L.Op, L.flat_width, B, a_mn=True, lda=L.Op, b_mn=True,
              ldb=L.flat_width, outF=gWd, atomic=True, ksplit=ks)
         # dHc = dpred Wd, masked by the stored post-dropout activation, x 1/(1-p)
         gemm(self.dpred, Wd, B, L.flat_width, L.Op, b_mn=True, ldb=L.flat_width, outH=self.dZc,
              mask=self.Hc, mask_scale=1.0 / (1.0 - self.p) if self.p > 0 else 1.0)
         # dWc = dZc^T Xcol   (reduce over batch x steps)
-        ks2 = max(1, min(32, (B * L.lout) // 2048))
+        # K = B x steps is huge and M x N = filters x taps tiny: split K deep (one 128x128 tile,
+        # ~4.6k rows per workgroup). bench.py --model cnn at B = 65536: split 32 / 128 / 512 /
+        # 2048 = 20.4 / 34.2 / 40.0 / 39.1 M windows/s (WELLFLOW_CNN_KS2 overrides)
+        ks2 = int(os.environ.get("WELLFLOW_CNN_KS2", "0")) or max(1, min(512, (B * L.lout) // 4096))
         gemm(self.dZc, self.Xcol, L.Fp, L.Kc, B * L.lout, a_mn=True, lda=L.Fp, b_mn=True,
              ldb=L.Kc, outF=gWc, atomic=True, ksplit=ks2)
         return self.loss_sum
