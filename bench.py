@@ -128,7 +128,8 @@ def bench_lstm(args, ctx):
     el = _timed(ctx, run.run, args.steps, args.warmup)
     eng.check_device_errors()  # a timed-out persistent hand-off anywhere in the run fails the bench
     extra = {"persistent_fwd": eng.last_forward_persistent, "persistent_bwd": eng.last_backward_persistent}
-    return el, B, model, float(eng.loss_sum.item()) / B, run, eng, extra
+    # the engine adds each step's loss straight into the runner's accumulator: mean over the run
+    return el, B, model, run.take_loss() / (B * (args.steps + args.warmup)), run, eng, extra
 
 
 def _cpu_rehearsal(args, ctx, model):
@@ -349,7 +350,7 @@ def main() -> int:
             "grad_bucket_mb": round(eng.grads.numel() * 4 / 2**20, 3),
             "step_graph": bool(run.graphs),
             "comm_in_graph": bool(run.captured_comm),
-            "train_loss": round(loss, 6),  # lstm: last step; mlp / cnn / cpu: mean over the run
+            "train_loss": round(loss, 6),  # mean over the run
             **extra,
         }
         print(json.dumps(rec), flush=True)

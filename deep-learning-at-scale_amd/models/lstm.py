@@ -269,7 +269,8 @@ class NativeLSTM:
         return self.pred[:B]
 
     def forward_backward(self, x: torch.Tensor, y: torch.Tensor, grad_scale: float,
-                         zero_grads: bool = True, step: int = 0) -> torch.Tensor:
+                         zero_grads: bool = True, step: int = 0,
+                         loss_into: torch.Tensor | None = None) -> torch.Tensor:
         """One training forward + backward on a full batch; grads land in ``self.grads``.
 
         Gradient of ``grad_scale * sum_i loss_i`` (models/base.py contract; use
@@ -284,17 +285,21 @@ class NativeLSTM:
         gW, gw_out, gb_out = lay.views(self.grads)
         if zero_grads:
             self.grads.zero_()
-        self.loss_sum.zero_()
+        # loss_into: the head kernel adds this batch's loss straight into the caller's
+        # accumulator (train/step.py StepRunner: no per-step zero fill and accumulate launch)
+        ls = loss_into if loss_into is not None else self.loss_sum
+        if loss_into is None:
+            self.loss_sum.zero_()
         self._pack_x(x.contiguous(), B)
         self._forward_steps(B)
         hT = self._hT(B)
         y = y.contiguous().float()
         if self.loss_kind == "mse":  # head + MSE + dy fused in one kernel
             C.head_fwd(hT, lay.KA, B, self.H, w_out, b_out, y, self.pred, self.dy,
-                       self.loss_sum, 2.0 * float(grad_scale))
+                       ls, 2.0 * float(grad_scale))
         else:
             C.head_fwd(hT, lay.KA, B, self.H, w_out, b_out, None, self.pred, None, None, 0.0)
-            C.loss(1, self.pred, y, B, 1, self.clip, float(grad_scale), self.loss_sum, None,
+            C.loss(1, self.pred, y, B, 1, self.clip, float(grad_scale), ls, None,
                    self.dy, None)
         C.head_bwd_w(hT, lay.KA, B, self.H, self.dy, gw_out, gb_out)
         # BPTT chain (high-priority stream) + dWcat = sum_{t,b} dG_t[b]^T [x_t | 1 | h_{t-1}][b]
@@ -309,4 +314,4 @@ class NativeLSTM:
         self.last_backward_persistent = bool(pb)
         if not pb and self.dw_chunk <= 0:
             self._note_fallback("backward", self.persistent_bwd)
-        return self.loss_sum
+        return ls
