@@ -31,6 +31,14 @@ __device__ __forceinline__ bf16_t f2bf(float x) {
   return *reinterpret_cast<bf16_t*>(&h);
 }
 
+// Two floats -> one packed bf16 pair (lo in bits 0-15): a single v_cvt_pk_bf16_f32 (RNE),
+// where f2bf(a) | f2bf(b) << 16 costs two conversions plus the and / shift / or to merge.
+typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+typedef float f32x2_t __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ unsigned pk_bf16(float lo, float hi) {
+  return __builtin_bit_cast(unsigned, __builtin_convertvector((f32x2_t{lo, hi}), bf16x2_t));
+}
+
 // Gate activations on the transcendental unit: v_exp_f32 + v_rcp_f32 (1 ulp), no IEEE
 // division sequence (the precise 1/x costs ~10 VALU and dominated the LSTM epilogues).
 __device__ __forceinline__ float sigmoidf_(float x) {

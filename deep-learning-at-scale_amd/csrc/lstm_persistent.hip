@@ -37,6 +37,20 @@ constexpr int PF_ROWS = 32;               // rows per ring chunk
 constexpr unsigned PF_SPIN_LIMIT = 1u << 21;
 typedef __attribute__((address_space(1))) unsigned gu32;
 typedef __attribute__((address_space(1))) unsigned long long gu64;
+
+// one cell element in flight through the forward's micro-staged epilogue
+struct EpiMicro {
+  float zi, zf, zg, zo, ei, ef, eg, eo, ig, fg, gg, og, cn, ec;
+  unsigned p0, p1;
+};
+// empty volatile asm: the value must exist in a VGPR at this point of the instruction stream
+// The value is redefined there ("+v"), so its consumers stay after this point too. (Input-
+// only pins avoid the hazard recognizer's s_nop after every such asm, but let the compiler
+// regroup the stages and shuffle values through AGPRs: 2.21 vs 1.50 ms per forward.)
+__device__ __forceinline__ void pin(float& a) { asm volatile("" : "+v"(a)); }
+template <typename A, typename B> __device__ __forceinline__ void pin(A& a, B& b) {
+  asm volatile("" : "+v"(a), "+v"(b));
+}
 }  // namespace
 
 // sync words (uint32): [0] STICKY error (bit 0: a spin bound tripped in some launch; never
@@ -59,6 +73,9 @@ __global__ __launch_bounds__(256, 1) void lstm_fwd_persistent_kernel(
   // accumulator registers (this chunk + the pipelined previous one) = 12 k-tiles x 4 x 4
   constexpr int KTA = KT < 12 ? KT : 12;
   constexpr int NSTORE = (DBG & 4) ? 1 : 7;  // stores per wave per chunk: 2 C, 4 S, 1 h
+  // one asm statement per MFMA + cell-math micro-stage (H = 512; WELLFLOW_PF_DBG=512: pinned
+  // C++ micro-stages instead, for A/B)
+  constexpr bool FUSED = KT == 18 && (DBG & (2 | 128 | 512)) == 0;
   // Distinct static LDS objects per ring slot: the compiler then proves the slot being
   // filled by LDS-DMA disjoint from the slots being read, and inserts no vmcnt(0) of its own.
   // EXACTLY ONE static LDS variable, compile-time offsets for every ring slot, the h staging
@@ -196,9 +213,98 @@ __global__ __launch_bounds__(256, 1) void lstm_fwd_persistent_kernel(
       const float og = sigmoid_pre(accp[i][3][r]);
       const float cn = fg * cq[0][i][r] + ig * gg;
       cv[i][r] = cn;
-      pk[i][2 * r] = (unsigned)f2bf(ig) | ((unsigned)f2bf(fg) << 16);
-      pk[i][2 * r + 1] = (unsigned)f2bf(gg) | ((unsigned)f2bf(og) << 16);
+      pk[i][2 * r] = pk_bf16(ig, fg);
+      pk[i][2 * r + 1] = pk_bf16(gg, og);
       hv[i][r] = f2bf(og * tanhf_(cn));
+    };
+    // The same element in two halves pinned to k-tile positions of the next chunk's MFMA
+    // loop. Empty asm statements take the inputs and produce the outputs at that point:
+    // the MFMAs are volatile asm too, so the compiler can neither hoist the cell math above
+    // the loop nor sink it below (it sank all of it: 144 MFMAs back to back, then ~280 VALU
+    // with the matrix core idle). Half 0: i, f, g gates and c_t; half 1: o gate, tanh(c_t),
+    // h_t and the packed gate words.
+    auto epi_half = [&](int hh, int i, int r, float (&cv)[2][4], float (&gs)[2][4], unsigned (&pk)[2][8],
+                        unsigned (&hv)[2][4]) {
+      if (hh == 0) {
+        float zi = accp[i][0][r], zf = accp[i][1][r], zg = accp[i][2][r], cp = cq[0][i][r];
+        asm volatile("" : "+v"(zi), "+v"(zf), "+v"(zg), "+v"(cp));
+        const float ig = sigmoid_pre(zi), fg = sigmoid_pre(zf), gg = tanh_pre(zg);
+        float cn = fg * cp + ig * gg;
+        unsigned p0 = pk_bf16(ig, fg);
+        float g2 = gg;
+        asm volatile("" : "+v"(cn), "+v"(p0), "+v"(g2));
+        cv[i][r] = cn;
+        pk[i][2 * r] = p0;
+        gs[i][r] = g2;
+      } else {
+        float zo = accp[i][3][r];
+        asm volatile("" : "+v"(zo));
+        const float og = sigmoid_pre(zo);
+        unsigned p1 = pk_bf16(gs[i][r], og);
+        unsigned h = f2bf(og * tanhf_(cv[i][r]));
+        asm volatile("" : "+v"(p1), "+v"(h));
+        pk[i][2 * r + 1] = p1;
+        hv[i][r] = h;
+      }
+    };
+    // The element as 18 micro-stages, each at most one issue slot's worth of VALU (one
+    // transcendental or two plain ops, <= 8 cycles: what a 16x16x32 MFMA leaves free of its
+    // 16), placed one per MFMA of the next chunk's loop (8 x 18 = 144 = the MFMA count at
+    // H = 512). Every stage pins its inputs and outputs with empty volatile asm, so it
+    // stays between its two MFMAs.
+    auto epi_micro = [&](auto sc, int i, int r, EpiMicro& e, float (&cv)[2][4], unsigned (&pk)[2][8],
+                         unsigned (&hv)[2][4]) {
+      constexpr int s = decltype(sc)::value;
+      if constexpr (s == 0) {
+        e.zi = accp[i][0][r];
+        e.zf = accp[i][1][r];
+        e.zg = accp[i][2][r];
+        e.zo = accp[i][3][r];
+        pin(e.zi, e.zf);
+        pin(e.zg, e.zo);
+      } else if constexpr (s == 1) {
+        pin(e.zi); e.ei = __builtin_amdgcn_exp2f(e.zi); pin(e.ei);
+      } else if constexpr (s == 2) {
+        pin(e.zf); e.ef = __builtin_amdgcn_exp2f(e.zf); pin(e.ef);
+      } else if constexpr (s == 3) {
+        pin(e.zg); e.eg = __builtin_amdgcn_exp2f(e.zg); pin(e.eg);
+      } else if constexpr (s == 4) {
+        pin(e.zo); e.eo = __builtin_amdgcn_exp2f(e.zo); pin(e.eo);
+      } else if constexpr (s == 5) {
+        pin(e.ei, e.ef); e.ei += 1.0f; e.ef += 1.0f; pin(e.ei, e.ef);
+      } else if constexpr (s == 6) {
+        pin(e.ei); e.ig = __builtin_amdgcn_rcpf(e.ei); pin(e.ig);
+      } else if constexpr (s == 7) {
+        pin(e.ef); e.fg = __builtin_amdgcn_rcpf(e.ef); pin(e.fg);
+      } else if constexpr (s == 8) {
+        pin(e.eg, e.eo); e.eg += 1.0f; e.eo += 1.0f; pin(e.eg, e.eo);
+      } else if constexpr (s == 9) {
+        pin(e.eg); e.gg = __builtin_amdgcn_rcpf(e.eg); pin(e.gg);
+      } else if constexpr (s == 10) {
+        pin(e.eo); e.og = __builtin_amdgcn_rcpf(e.eo); pin(e.og);
+      } else if constexpr (s == 11) {
+        // c_t = fma(f, c_{t-1}, i * g): the contraction the per-step kernel's
+        // f * c + i * g compiles to, so both paths round alike
+        pin(e.gg, e.ig); e.gg = 1.0f - 2.0f * e.gg; e.cn = e.ig * e.gg; pin(e.gg, e.cn);
+      } else if constexpr (s == 12) {
+        pin(e.cn, e.fg); e.cn = __builtin_fmaf(e.fg, cq[0][i][r], e.cn); e.p0 = pk_bf16(e.ig, e.fg); pin(e.cn, e.p0);
+      } else if constexpr (s == 13) {
+        pin(e.og); e.p1 = pk_bf16(e.gg, e.og); e.ec = e.cn * 2.8853900817779268f; pin(e.p1, e.ec);
+      } else if constexpr (s == 14) {
+        pin(e.ec); e.ec = __builtin_amdgcn_exp2f(e.ec); pin(e.ec);
+      } else if constexpr (s == 15) {
+        pin(e.ec); e.ec = __builtin_amdgcn_rcpf(e.ec + 1.0f); pin(e.ec);
+      } else if constexpr (s == 16) {
+        pin(e.ec); e.ec = e.og * (1.0f - 2.0f * e.ec); pin(e.ec);
+      } else {
+        pin(e.ec);
+        unsigned h = f2bf(e.ec);
+        pin(h, e.cn);
+        cv[i][r] = e.cn;
+        pk[i][2 * r] = e.p0;
+        pk[i][2 * r + 1] = e.p1;
+        hv[i][r] = h;
+      }
     };
     // The same three pieces, issued one by one from inside the next chunk's MFMA loop
     // (diagnostic build WELLFLOW_PF_DBG=64, KT >= 16): h staging, then one C / S store per
@@ -323,8 +429,82 @@ __global__ __launch_bounds__(256, 1) void lstm_fwd_persistent_kernel(
       // this loop, one (row-tile, row) element per k-tile, so its VALU / transcendental work
       // issues between the MFMAs (chunk 0 computes on leftovers and discards the result).
       bf16x8 a[2][2];
-      float cv[2][4];
+      float cv[2][4], gs[2][4];
       unsigned pk[2][8], hv[2][4];
+      EpiMicro ms;
+      // H = 512 (KT = 18, 144 MFMAs per chunk): each MFMA and one micro-stage of the carried
+      // chunk's cell math are ONE asm statement. No pin asm between them, so the hazard
+      // recognizer has nothing to pad: it pads (s_nop) only where an asm reads a VGPR that
+      // the asm right before it wrote, and two elements are in flight with their stages
+      // alternating, so a stage's producer is always >= 2 statements back. Slot m: pair
+      // m / 36 (elements 2p, 2p+1), stage (m % 36) / 2 of element 2p + (m & 1). Outputs are
+      // early-clobber: no stage result can share a register with the MFMA's operands.
+      EpiMicro e2[2];
+      auto fused_slot = [&](auto kc, auto mc) {
+        constexpr int kt = decltype(kc)::value, mm = decltype(mc)::value;
+        constexpr int i = mm >> 2, j = mm & 3, m = kt * 8 + mm;
+        constexpr int el = 2 * (m / 36) + (m & 1), st = (m % 36) / 2, ei_ = el >> 2, er = el & 3;
+        EpiMicro& E = e2[m & 1];
+        const bf16x8& A = a[kt & 1][i];
+#define WF_UNP(...) __VA_ARGS__
+#define WF_MF(TXT, OUTS, INS)                                                                          \
+  if constexpr (kt == 0)                                                                               \
+    asm volatile("v_mfma_f32_16x16x32_bf16 %[c], %[a], %[b], 0\n\t" TXT                                \
+                 : [c] "=&a"(acc[i][j]), WF_UNP OUTS : [a] "v"(A), [b] "a"(w[kt][j]) WF_UNP INS);    \
+  else if constexpr (kt < KTA)                                                                         \
+    asm volatile("v_mfma_f32_16x16x32_bf16 %[c], %[a], %[b], %[c]\n\t" TXT                             \
+                 : [c] "+a"(acc[i][j]), WF_UNP OUTS : [a] "v"(A), [b] "a"(w[kt][j]) WF_UNP INS);     \
+  else                                                                                                 \
+    asm volatile("v_mfma_f32_16x16x32_bf16 %[c], %[a], %[b], %[c]\n\t" TXT                             \
+                 : [c] "+a"(acc[i][j]), WF_UNP OUTS : [a] "v"(A), [b] "v"(w[kt][j]) WF_UNP INS);
+        if constexpr (st == 0) {
+          WF_MF("v_exp_f32 %[o], %[x]", ([o] "=&v"(E.ei)), (, [x] "v"(accp[ei_][0][er])))
+        } else if constexpr (st == 1) {
+          WF_MF("v_exp_f32 %[o], %[x]", ([o] "=&v"(E.ef)), (, [x] "v"(accp[ei_][1][er])))
+        } else if constexpr (st == 2) {
+          WF_MF("v_exp_f32 %[o], %[x]", ([o] "=&v"(E.eg)), (, [x] "v"(accp[ei_][2][er])))
+        } else if constexpr (st == 3) {
+          WF_MF("v_exp_f32 %[o], %[x]", ([o] "=&v"(E.eo)), (, [x] "v"(accp[ei_][3][er])))
+        } else if constexpr (st == 4) {
+          WF_MF("v_add_f32 %[p], 1.0, %[p]\n\tv_add_f32 %[q], 1.0, %[q]", ([p] "+v"(E.ei), [q] "+v"(E.ef)), ())
+        } else if constexpr (st == 5) {
+          WF_MF("v_rcp_f32 %[o], %[x]", ([o] "=&v"(E.ig)), (, [x] "v"(E.ei)))
+        } else if constexpr (st == 6) {
+          WF_MF("v_rcp_f32 %[o], %[x]", ([o] "=&v"(E.fg)), (, [x] "v"(E.ef)))
+        } else if constexpr (st == 7) {
+          WF_MF("v_add_f32 %[p], 1.0, %[p]\n\tv_add_f32 %[q], 1.0, %[q]", ([p] "+v"(E.eg), [q] "+v"(E.eo)), ())
+        } else if constexpr (st == 8) {
+          WF_MF("v_rcp_f32 %[o], %[x]", ([o] "=&v"(E.gg)), (, [x] "v"(E.eg)))
+        } else if constexpr (st == 9) {
+          WF_MF("v_rcp_f32 %[o], %[x]", ([o] "=&v"(E.og)), (, [x] "v"(E.eo)))
+        } else if constexpr (st == 10) {  // g = 1 - 2 r (tanh), then i * g into cn
+          WF_MF("v_fma_f32 %[g], %[g], -2.0, 1.0\n\tv_mul_f32 %[c2], %[x], %[g]", ([g] "+v"(E.gg), [c2] "=&v"(E.cn)),
+                (, [x] "v"(E.ig)))
+        } else if constexpr (st == 11) {  // c_t = fma(f, c_{t-1}, i g); packed (i, f)
+          WF_MF("v_fma_f32 %[c2], %[f], %[cp], %[c2]\n\tv_cvt_pk_bf16_f32 %[o], %[x], %[f]",
+                ([c2] "+v"(E.cn), [o] "=&v"(E.p0)), (, [f] "v"(E.fg), [cp] "v"(cq[0][ei_][er]), [x] "v"(E.ig)))
+        } else if constexpr (st == 12) {  // packed (g, o); 2 log2(e) c_t
+          WF_MF("v_cvt_pk_bf16_f32 %[o], %[g], %[x]\n\tv_mul_f32 %[y], 0x4038aa3b, %[c2]", ([o] "=&v"(E.p1), [y] "=&v"(E.ec)),
+                (, [g] "v"(E.gg), [x] "v"(E.og), [c2] "v"(E.cn)))
+        } else if constexpr (st == 13) {
+          WF_MF("v_exp_f32 %[p], %[p]", ([p] "+v"(E.ec)), ())
+        } else if constexpr (st == 14) {
+          WF_MF("v_add_f32 %[p], 1.0, %[p]", ([p] "+v"(E.ec)), ())
+        } else if constexpr (st == 15) {
+          WF_MF("v_rcp_f32 %[p], %[p]", ([p] "+v"(E.ec)), ())
+        } else if constexpr (st == 16) {  // h = o (1 - 2 r)
+          WF_MF("v_fma_f32 %[p], %[p], -2.0, 1.0\n\tv_mul_f32 %[p], %[x], %[p]", ([p] "+v"(E.ec)), (, [x] "v"(E.og)))
+        } else {  // bf16(h) in the low half
+          unsigned h;
+          WF_MF("v_cvt_pk_bf16_f32 %[o], %[x], 0", ([o] "=&v"(h)), (, [x] "v"(E.ec)))
+          cv[ei_][er] = E.cn;
+          pk[ei_][2 * er] = E.p0;
+          pk[ei_][2 * er + 1] = E.p1;
+          hv[ei_][er] = h;
+        }
+#undef WF_MF
+#undef WF_UNP
+      };
 #pragma unroll
       for (int i = 0; i < 2; ++i) a[0][i] = *reinterpret_cast<const bf16x8*>(cur + i * 2048 + fa[0]);
       if constexpr ((DBG & 32) != 0) {
@@ -339,21 +519,40 @@ __global__ __launch_bounds__(256, 1) void lstm_fwd_persistent_kernel(
             a[(kt + 1) & 1][i] =
                 *reinterpret_cast<const bf16x8*>(cur + ((kt + 1) >> 1) * 4096 + i * 2048 + fa[(kt + 1) & 1]);
         }
-#pragma unroll
-        for (int i = 0; i < 2; ++i)
-#pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            if constexpr (!(DBG & 2)) {
-              if constexpr (kt == 0)  // accumulator := A B (inline-constant 0 as src C)
-                asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, 0"
-                             : "=&a"(acc[i][j]) : "v"(a[kt & 1][i]), "a"(w[kt][j]));
-              else if constexpr (kt < KTA)
-                asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc[i][j]) : "v"(a[kt & 1][i]), "a"(w[kt][j]));
-              else
-                asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc[i][j]) : "v"(a[kt & 1][i]), "v"(w[kt][j]));
-            }
+        static_for<0, 8>([&](auto mc) {
+          constexpr int i = decltype(mc)::value >> 2, j = decltype(mc)::value & 3;
+          if constexpr (FUSED) {
+            fused_slot(kc, mc);
+            return;
           }
-        if constexpr (kt < 8) epi_elem(kt >> 2, kt & 3, cv, pk, hv);
+          if constexpr (!(DBG & 2)) {
+            if constexpr (kt == 0)  // accumulator := A B (inline-constant 0 as src C)
+              asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, 0"
+                           : "=&a"(acc[i][j]) : "v"(a[kt & 1][i]), "a"(w[kt][j]));
+            else if constexpr (kt < KTA)
+              asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc[i][j]) : "v"(a[kt & 1][i]), "a"(w[kt][j]));
+            else
+              asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc[i][j]) : "v"(a[kt & 1][i]), "v"(w[kt][j]));
+          }
+          if constexpr (!(DBG & 128)) {
+            // micro-stages of the carried chunk's cell math, one issue-slot's worth (<= 8
+            // cycles: one transcendental or two plain VALU) in each MFMA's shadow:
+            // stage q of 144 (8 elements x 18) goes after MFMA slot q * 8KT / 144
+            constexpr int S = 8 * KT, m = kt * 8 + decltype(mc)::value;
+            constexpr int qlo = (m * 144 + S - 1) / S, qhi = ((m + 1) * 144 + S - 1) / S;
+            static_for<qlo, qhi>([&](auto qc) {
+              constexpr int q = decltype(qc)::value;
+              epi_micro(std::integral_constant<int, q % 18>{}, q / 18 >> 2, (q / 18) & 3, ms, cv, pk, hv);
+            });
+          }
+        });
+        if constexpr ((DBG & 128) != 0) {
+          // 16 half-elements spread evenly over the KT k-tiles (half q at k-tile q * KT / 16)
+          static_for<0, 16>([&](auto qc) {
+            constexpr int q = decltype(qc)::value;
+            if constexpr (q * KT / 16 == kt) epi_half(q & 1, q >> 3, (q >> 1) & 3, cv, gs, pk, hv);
+          });
+        }
         if constexpr (KT >= 16 && (DBG & 64)) {  // chunk c-1's stores and publish in this loop's shadow
           if constexpr (kt == 8) {
             if (c > 0) epi_h(hv);
@@ -365,10 +564,23 @@ __global__ __launch_bounds__(256, 1) void lstm_fwd_persistent_kernel(
             if (c > 0) publish(c - 1);
           }
         }
+        // The MFMAs are inline asm, so the compiler knows neither their latency nor that they
+        // still read this k-tile's A fragments after issue: keep those registers allocated to
+        // the end of the k-tile, so no micro-stage result lands in them under an MFMA in
+        // flight (it did: a v_accvgpr_read into SrcA one instruction after the MFMA, wrong h
+        // at H = 128 / 256).
+        asm volatile("" ::"v"(a[kt & 1][0]), "v"(a[kt & 1][1]));
       });
       // the epilogue reads the accumulators with VALU: cover the last MFMAs' pipeline
-      // (the compiler pads nothing after inline asm)
-      asm volatile("s_nop 7\n\ts_nop 7" ::: "memory");
+      // (the compiler pads nothing after inline asm). The accumulators are operands of the
+      // padding, so no read of them (the accp copy, or the drain's cell math at NC = 1) can
+      // be scheduled above it: the compiler sees an inline-asm MFMA's result as ready at
+      // once and had put v_accvgpr_reads 2 instructions behind the last MFMAs (tools/mfma_war.py).
+      asm volatile("s_nop 7\n\ts_nop 7"
+                   : "+a"(acc[0][0]), "+a"(acc[0][1]), "+a"(acc[0][2]), "+a"(acc[0][3]), "+a"(acc[1][0]),
+                     "+a"(acc[1][1]), "+a"(acc[1][2]), "+a"(acc[1][3])
+                   :
+                   : "memory");
       if constexpr ((DBG & 16) != 0) {  // MFMA completion: consume a result before stamping
         float sink = acc[1][3][3];
         asm volatile("" ::"v"(sink));
@@ -417,6 +629,8 @@ static int launch_pf(bf16_t* XH, const bf16_t* Wp, float* Cst, bf16_t* S, unsign
     if (d.dbg == 16) f = reinterpret_cast<const void*>(&lstm_fwd_persistent_kernel<KT, NC, 16>);
     if (d.dbg == 48) f = reinterpret_cast<const void*>(&lstm_fwd_persistent_kernel<KT, NC, 48>);
     if (d.dbg == 64) f = reinterpret_cast<const void*>(&lstm_fwd_persistent_kernel<KT, NC, 64>);  // stores inside the loop
+    if (d.dbg == 512) f = reinterpret_cast<const void*>(&lstm_fwd_persistent_kernel<KT, NC, 512>);  // pinned micro-stages
+    if (d.dbg == 128) f = reinterpret_cast<const void*>(&lstm_fwd_persistent_kernel<KT, NC, 128>);  // half-element epilogue
   }
   void* args[] = {&XH, &Wp, &Cst, &S, &sync, &d};
   return persistent_launch(f, grid, args, s);  // persistent_launch.h: residency check + plain launch

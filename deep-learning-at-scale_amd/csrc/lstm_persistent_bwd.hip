@@ -263,8 +263,8 @@ __global__ __launch_bounds__(256, 1) void lstm_bwd_persistent_kernel(
         const f32x2 dO = e - e * eog[q];            // dh tanh(c) o (1 - o)
 #pragma unroll
         for (int k = 0; k < 2; ++k) {
-          ev[2 * q + k][0] = (unsigned)f2bf(di[k]) | ((unsigned)f2bf(df[k]) << 16);
-          ev[2 * q + k][1] = (unsigned)f2bf(dg[k]) | ((unsigned)f2bf(dO[k]) << 16);
+          ev[2 * q + k][0] = pk_bf16(di[k], df[k]);  // one v_cvt_pk_bf16_f32 per pair
+          ev[2 * q + k][1] = pk_bf16(dg[k], dO[k]);
         }
       } else if constexpr (part == 7) {
         dcr[RTp] = enk;
