@@ -88,8 +88,7 @@ __global__ __launch_bounds__(256, 1) void lstm_fwd_persistent_kernel(
   __shared__ __attribute__((aligned(16))) char smem[FOFF + 16];
   // h_t staging [32][64] bf16, accessed only through inline asm (32-bit LDS address)
   const unsigned hb_lds = (unsigned)(uintptr_t)((__attribute__((address_space(3))) char*)(smem + HOFF));
-  int* const lflag_s = reinterpret_cast<int*>(smem + FOFF);
-  volatile int* lflag = lflag_s;
+  const unsigned flag_lds = (unsigned)(uintptr_t)((__attribute__((address_space(3))) char*)(smem + FOFF));
 
   constexpr int H = KA - 64, G = 4 * H, NB = G / 256, HB = H / 16;  // KX = 64 (host-checked)
   const int Bp = fn_rows(d.B);
@@ -181,12 +180,15 @@ __global__ __launch_bounds__(256, 1) void lstm_fwd_persistent_kernel(
         }
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        *lflag = ok;
+        asm volatile("ds_write_b32 %0, %1" ::"v"(flag_lds), "v"(ok) : "memory");
       }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();
-      asm volatile("" ::: "memory");
-      if (*lflag == 0) return;  // uniform: every wave reads the same word
+      // the flag word through ds_read in asm (a volatile C++ access became a flat load with
+      // sc0 sc1 and a vmcnt + lgkmcnt wait, every step)
+      int okv;
+      asm volatile("ds_read_b32 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(okv) : "v"(flag_lds) : "memory");
+      if (__builtin_amdgcn_readfirstlane(okv) == 0) return;  // uniform: every wave reads the same word
     }
     stamp(t, 1);
     // opaque per-step copy of the row origin: stops the compiler hoisting every chunk's
