@@ -39,6 +39,12 @@ namespace {
 constexpr unsigned PB_SPIN_LIMIT = 1u << 21;
 constexpr int PB_MAX_RT = 16;  // row tiles per workgroup (dc carry in registers: 4 VGPRs each)
 typedef __attribute__((address_space(1))) unsigned gu32;
+// empty volatile asm redefining the value ("+v"): its producer stays above this point and its
+// consumers below it (lstm_persistent.hip uses the same pins)
+template <typename A> __device__ __forceinline__ void pin(A& a) { asm volatile("" : "+v"(a)); }
+template <typename A, typename B> __device__ __forceinline__ void pin(A& a, B& b) {
+  asm volatile("" : "+v"(a), "+v"(b));
+}
 }  // namespace
 
 // KT = H / 32 k-tiles per wave (each wave's K quarter of G = 4H is H wide); NRT row tiles
@@ -56,6 +62,7 @@ __global__ __launch_bounds__(256, 1) void lstm_bwd_persistent_kernel(
     bf16_t* __restrict__ DG, const float* __restrict__ dcarry, unsigned* __restrict__ sync, LstmDims d) {
   constexpr int H = 32 * KT, G = 4 * H, NB = H / 64, HB = H / 16;
   constexpr int KS = KT / 2;             // 64-wide k-steps per wave per row tile
+  constexpr bool MICRO = (DBG & 512) == 0;  // cell backward as per-MFMA micro-stages (bstage)
   constexpr int WSLOT = 16 * KT * 64;    // bytes of one wave's A tile: 16 rows x H k (bf16)
   constexpr int RING = 4 * 2 * WSLOT;    // [wave][2 slots]
   constexpr int RED = RING;              // partial sums [parity][src wave][unit tile][lane] x 16 B
@@ -295,6 +302,94 @@ __global__ __launch_bounds__(256, 1) void lstm_bwd_persistent_kernel(
       }
     };
 
+    // The cell backward as 64 micro-stages in scalar fp32, one per MFMA of the next tile's loop
+    // (at most two plain ops or one transcendental: what a 16x16x32 MFMA leaves free of its
+    // 16 issue cycles; packed fp32 costs more issue beside MFMAs than two scalar ops).
+    // Stage q < 60: rows 2p, 2p+1 (p = q / 30) in flight together, stage (q % 30) / 2 of row
+    // 2p + (q & 1); q = 60: lane-pair exchange (part 7); q = 62: DG stores (part 8). Every
+    // stage pins its values with empty "+v" asm, so the compiler can neither sink the math
+    // below the MFMAs nor hoist it above them (it had gathered each part into one clump).
+    // WELLFLOW_PF_DBG=512: the 8-part schedule instead (A/B).
+    struct BRow {
+      unsigned sa, sb;
+      float i, f, g, o, x, tc, eq, dc, nk, a, tq, u, di, dg, df, e;
+      unsigned p0, p1;
+    };
+    BRow brow[2];
+    auto bstage = [&](auto rpc, auto qc) {
+      constexpr int RTp = decltype(rpc)::value, q = decltype(qc)::value, Kp = RTp % 4;
+      if constexpr (q < 60) {
+        constexpr int r = 2 * (q / 30) + (q & 1), st = (q % 30) / 2;
+        BRow& b = brow[q & 1];
+        if constexpr (st == 0) {
+          const u32x4 sv = r < 2 ? sq0[Kp] : sq1[Kp];  // row r: (i|f), (g|o)
+          b.sa = sv[2 * (r & 1)];
+          b.sb = sv[2 * (r & 1) + 1];
+          b.i = __uint_as_float(b.sa << 16);
+          b.f = __uint_as_float(b.sa & 0xffff0000u);
+          pin(b.i, b.f);
+          pin(b.sb);
+        } else if constexpr (st == 1) {
+          b.g = __uint_as_float(b.sb << 16);
+          b.o = __uint_as_float(b.sb & 0xffff0000u);
+          pin(b.g, b.o);
+        } else if constexpr (st == 2) {  // c_t = fma(f, c_{t-1}, i g) as the forward rounds it
+          b.x = b.i * b.g;
+          b.x = __builtin_fmaf(b.f, __uint_as_float(cq[Kp][r]), b.x);
+          pin(b.x);
+        } else if constexpr (st == 3) {
+          b.x = b.x * 2.8853900817779268f;  // exp(2 c) = 2^(2 log2(e) c)
+          pin(b.x);
+        } else if constexpr (st == 4) {
+          b.x = __builtin_amdgcn_exp2f(b.x);
+          pin(b.x);
+        } else if constexpr (st == 5) {
+          b.x = b.x + 1.f;
+          pin(b.x);
+        } else if constexpr (st == 6) {
+          b.x = __builtin_amdgcn_rcpf(b.x);
+          pin(b.x);
+        } else if constexpr (st == 7) {  // tanh(c_t); dh o
+          b.tc = 1.f - 2.f * b.x;
+          b.eq = dhp[r] * b.o;
+          pin(b.tc, b.eq);
+        } else if constexpr (st == 8) {  // dc = dh o (1 - tanh^2) + carry
+          b.dc = 1.f - b.tc * b.tc;
+          b.dc = __builtin_fmaf(b.eq, b.dc, dcr[RTp][r]);
+          pin(b.dc);
+        } else if constexpr (st == 9) {
+          b.nk = b.dc * b.f;  // carry to step t-1
+          b.a = b.dc * b.i;
+          pin(b.nk, b.a);
+        } else if constexpr (st == 10) {
+          b.tq = b.a * b.g;
+          b.u = b.nk * __uint_as_float(cq[Kp][r]);
+          pin(b.tq, b.u);
+        } else if constexpr (st == 11) {
+          b.di = b.tq - b.tq * b.i;  // dc g i (1 - i)
+          b.dg = b.a - b.tq * b.g;   // dc i (1 - g^2)
+          pin(b.di, b.dg);
+        } else if constexpr (st == 12) {
+          b.df = b.u - b.u * b.f;  // dc c_{t-1} f (1 - f)
+          b.e = b.eq * b.tc;
+          pin(b.df, b.e);
+        } else if constexpr (st == 13) {
+          const float dO = b.e - b.e * b.o;  // dh tanh(c) o (1 - o)
+          b.p0 = pk_bf16(b.di, b.df);
+          b.p1 = pk_bf16(b.dg, dO);
+          pin(b.p0, b.p1);
+        } else {
+          ev[r][0] = b.p0;
+          ev[r][1] = b.p1;
+          enk[r] = b.nk;
+        }
+      } else if constexpr (q == 60) {
+        epi(rpc, std::integral_constant<int, 7>{});
+      } else if constexpr (q == 62) {
+        epi(rpc, std::integral_constant<int, 8>{});
+      }
+    };
+
     // K-split partial exchange, deferred by one tile: tile r writes its 3 foreign partials to
     // red[r & 1] at its end and runs on; tile r+1's loop passes a barrier after its first
     // k-tile (the writes drained by that k-tile's lgkmcnt wait), issues the partial reads, and
@@ -340,15 +435,24 @@ __global__ __launch_bounds__(256, 1) void lstm_bwd_persistent_kernel(
           asm volatile("" : "+v"(pr[0]), "+v"(pr[1]), "+v"(pr[2]), "+v"(pr[3]));
           dhp = dho + ((pr[0] + pr[1]) + (pr[2] + pr[3]));
         }
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
+        static_for<0, 4>([&](auto jc) {
+          constexpr int j = decltype(jc)::value;
           if constexpr (!(DBG & 2)) {
             if constexpr (kt == 0)
               asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, 0" : "=&v"(acc[j]) : "v"(a[kt & 1]), "a"(w[kt][j]));
             else
               asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+v"(acc[j]) : "v"(a[kt & 1]), "a"(w[kt][j]));
           }
-        }
+          if constexpr (MICRO && RT > 0) {
+            // stage instances [qlo, qhi) after MFMA slot m, from k-tile 1 on (dh of the
+            // previous tile is summed at the top of k-tile 1)
+            constexpr int S = 4 * KT - 4, m = kt * 4 + j - 4;
+            if constexpr (m >= 0) {
+              constexpr int qlo = (m * 64 + S - 1) / S, qhi = ((m + 1) * 64 + S - 1) / S;
+              static_for<qlo, qhi>([&](auto qc) { bstage(std::integral_constant<int, RT - 1>{}, qc); });
+            }
+          }
+        });
         // two A pieces of the next tile per k-tile over the first half of the loop: the vector-
         // memory queue drains under the MFMAs instead of blocking the wave before them, and the
         // last piece lands well before the next tile needs it
@@ -382,7 +486,7 @@ __global__ __launch_bounds__(256, 1) void lstm_bwd_persistent_kernel(
         // parts of the previous tile's cell backward (part p at k-tile kt_of_part(p))
         static_for<1, EPI_PARTS + 1>([&](auto pc) {
           constexpr int p = decltype(pc)::value;
-          if constexpr (RT > 0 && 2 * p - 1 + (p == 1 ? 1 : 0) == kt)
+          if constexpr (!MICRO && RT > 0 && 2 * p - 1 + (p == 1 ? 1 : 0) == kt)
             epi(std::integral_constant<int, RT - 1>{}, pc);
         });
         // the MFMAs above are inline asm, so the compiler knows neither their latency nor that
@@ -394,7 +498,7 @@ __global__ __launch_bounds__(256, 1) void lstm_bwd_persistent_kernel(
       // parts that did not fit a short loop
       static_for<1, EPI_PARTS + 1>([&](auto pc) {
         constexpr int p = decltype(pc)::value;
-        if constexpr (RT > 0 && 2 * p - 1 + (p == 1 ? 1 : 0) >= KT) epi(std::integral_constant<int, RT - 1>{}, pc);
+        if constexpr (!MICRO && RT > 0 && 2 * p - 1 + (p == 1 ? 1 : 0) >= KT) epi(std::integral_constant<int, RT - 1>{}, pc);
       });
       // VALU / LDS reads of MFMA results: cover the pipeline (nothing is padded after asm)
       asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 3" ::: "memory");
@@ -428,7 +532,10 @@ __global__ __launch_bounds__(256, 1) void lstm_bwd_persistent_kernel(
         asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(acc[0]), "+v"(acc[1]), "+v"(acc[2]), "+v"(acc[3]) :: "memory");
         dhp = (acc[0] + acc[1]) + (acc[2] + acc[3]);
         stamp(s, 5 + 5 * RT);
-        static_for<1, EPI_PARTS + 1>([&](auto pc) { epi(std::integral_constant<int, RT>{}, pc); });
+        if constexpr (MICRO)
+          static_for<0, 64>([&](auto qc) { bstage(std::integral_constant<int, RT>{}, qc); });
+        else
+          static_for<1, EPI_PARTS + 1>([&](auto pc) { epi(std::integral_constant<int, RT>{}, pc); });
       }
       stamp(s, 6 + 5 * RT);
       __builtin_amdgcn_sched_barrier(0);
@@ -452,6 +559,7 @@ static int launch_pb(const bf16_t* WhhT, const float* Cst, const bf16_t* S, bf16
       case 96: f = reinterpret_cast<const void*>(&lstm_bwd_persistent_kernel<KT, NRT, 96>); break;
       case 128: f = reinterpret_cast<const void*>(&lstm_bwd_persistent_kernel<KT, NRT, 128>); break;
       case 256: f = reinterpret_cast<const void*>(&lstm_bwd_persistent_kernel<KT, NRT, 256>); break;
+      case 512: f = reinterpret_cast<const void*>(&lstm_bwd_persistent_kernel<KT, NRT, 512>); break;  // 8-part epilogue
       default: break;
     }
   }
