@@ -63,7 +63,7 @@ case "$what" in
     for v in $vals; do
       env "$var=$v" timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "gpurun_out/ks_$v" -o run \
         -- python3 bench.py "$@" > "gpurun_out/ks_$v.log" 2>&1 || exit $?
-      echo "$var=$v $(grep -h "$kern" "gpurun_out/ks_$v/run_kernel_stats.csv" | cut -d, -f1-5)"
+      echo "$var=$v $(python3 tools/kstats.py "gpurun_out/ks_$v/run_kernel_stats.csv" | grep "$kern")"
     done ;;
   pmcsets)
     rm -rf gpurun_out/pmc
