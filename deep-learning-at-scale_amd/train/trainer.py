@@ -104,18 +104,44 @@ class Trainer:
         s_loss, s_mse, cnt = 0.0, 0.0, 0
         Xd = X if (torch.is_tensor(X) or hasattr(X, "starts")) and getattr(X, "device", None) == self.eng.device \
             else None
-        for i in range(0, len(idx), chunk):
+        pf = self._eval_prefetcher(X, chunk) if Xd is None and len(idx) > chunk else None
+        if pf is not None:
+            pf.submit(0, idx[:chunk])
+        for k, i in enumerate(range(0, len(idx), chunk)):
             sel = idx[i : i + chunk]
-            xb = (Xd[torch.as_tensor(sel, device=Xd.device)] if Xd is not None
-                  else _to_dev(X[sel], self.eng.device))
+            if pf is not None:
+                # native background gather (csrc/runtime: wf_prefetch_*) of the next chunk's
+                # windows into the other slot while this chunk is copied and evaluated
+                if i + chunk < len(idx):
+                    pf.submit((k + 1) % 2, idx[i + chunk : i + 2 * chunk])
+                xh, _ = pf.wait(k % 2)
+                xb = xh.to(self.eng.device)  # synchronous: the slot is free again afterwards
+            else:
+                xb = (Xd[torch.as_tensor(sel, device=Xd.device)] if Xd is not None
+                      else _to_dev(X[sel], self.eng.device))
             yb = _to_dev(Y[sel] if not torch.is_tensor(Y) else Y[torch.as_tensor(sel, device=Y.device)],
                          self.eng.device)
             pred = self.eng.forward(xb).float().reshape(yb.shape)
             s_loss += per_element_loss(self.cfg.loss, pred, yb, self.cfg.clip).sum().item()
             s_mse += ((pred - yb) ** 2).sum().item()
             cnt += yb.numel()
+        if pf is not None:
+            pf.close()
         s_loss, s_mse, cnt = self.ctx.sum_scalars(s_loss, s_mse, cnt)
         return s_loss / max(cnt, 1), s_mse / max(cnt, 1)
+
+    def _eval_prefetcher(self, X, chunk: int):
+        """Two-slot native window prefetcher for a host-resident window set (float32
+        SeriesWindows rows), or None (tensor / other storage, native runtime not built)."""
+        from ..data import native
+
+        rows = getattr(X, "rows", None)
+        if not (hasattr(X, "starts") and isinstance(rows, np.ndarray) and rows.dtype == np.float32
+                and native.wanted()):
+            return None
+        # targets come from Y per window; the prefetcher's per-row target buffer is unused
+        return native.Prefetcher(rows, np.asarray(X.starts), np.zeros(len(rows), np.float32), X.T, chunk,
+                                 nslots=2, threads=2, pin=self.eng.device.type == "cuda")
 
     # ------------------------------------------------------------------ state
     def state_dict(self) -> dict:

@@ -100,3 +100,38 @@ def test_lstm_job_learns_on_cpu(tmp_path):
                            "--batch-size", "64", "--device", "cpu"], log=lambda *a, **k: None)
     h = out["history"]
     assert h["val_loss"][-1] < h["val_loss"][0]
+
+
+def test_evaluate_with_native_window_prefetcher_matches_plain_gather(monkeypatch):
+    """Trainer.evaluate on a host-resident window set gathers chunk k+1 in the native
+    background prefetcher (csrc/runtime, wf_prefetch_*) while chunk k is evaluated; the result
+    must equal the plain per-chunk gather (WELLFLOW_NATIVE_IO=0)."""
+    import numpy as np
+
+    from wellflow.data import native
+    from wellflow.data.features import SeriesWindows
+    from wellflow.models.base import TorchEngine
+    from wellflow.models.lstm import LSTMRegressor
+    from wellflow.parallel.dist import DistContext
+    from wellflow.train.trainer import Trainer
+
+    if not native.available():
+        pytest.skip("native runtime not built")
+    rng = np.random.default_rng(3)
+    T, F = 12, 5
+    rows = rng.standard_normal((700, F)).astype(np.float32)
+    starts = np.arange(0, 700 - T, 2, dtype=np.int64)
+    X = SeriesWindows(rows, starts, T)
+    Y = rng.standard_normal(len(starts)).astype(np.float32)
+    torch.manual_seed(0)
+    eng = TorchEngine(LSTMRegressor(F, hidden=16))
+    cfg = type("Cfg", (), {"loss": "mse", "clip": 6.0, "batch_size": 64, "patience": 3})()
+    tr = Trainer(cfg, eng, None, DistContext(), "t")
+    calls = []
+    orig = native.Prefetcher.wait
+    monkeypatch.setattr(native.Prefetcher, "wait", lambda self, s: calls.append(s) or orig(self, s))
+    with_pf = tr.evaluate(X, Y, chunk=50)
+    assert len(calls) == -(-len(starts) // 50)  # every chunk came through the prefetcher
+    monkeypatch.setenv("WELLFLOW_NATIVE_IO", "0")
+    plain = tr.evaluate(X, Y, chunk=50)
+    assert with_pf == pytest.approx(plain, rel=1e-6)
