@@ -76,6 +76,10 @@ __global__ __launch_bounds__(256, 1) void lstm_fwd_persistent_kernel(
   // one asm statement per MFMA + cell-math micro-stage (H = 512; WELLFLOW_PF_DBG=512: pinned
   // C++ micro-stages instead, for A/B)
   constexpr bool FUSED = KT == 18 && (DBG & (2 | 128 | 512)) == 0;
+  // the step top issues only chunk 0's pieces, so chunk 0 starts sooner after the hand-off
+  // (every workgroup of the grid fetches its first chunks at once there); chunk 0 issues
+  // chunks 1 and 2 from its MFMA loop (WELLFLOW_PF_DBG=1024: both at the step top, A/B)
+  constexpr bool PF01 = NC >= 3 && (DBG & (2 | 1024)) == 0;
   // Distinct static LDS objects per ring slot: the compiler then proves the slot being
   // filled by LDS-DMA disjoint from the slots being read, and inserts no vmcnt(0) of its own.
   // EXACTLY ONE static LDS variable, compile-time offsets for every ring slot, the h staging
@@ -392,19 +396,29 @@ __global__ __launch_bounds__(256, 1) void lstm_fwd_persistent_kernel(
         __builtin_amdgcn_global_load_lds((const void*)(src + s * 128), (lds_void*)(ra + s * 4096 + wid * 1024),
                                          16, 0, 0);
     };
+    // piece s of chunk c into ring slot SL
+    auto issue_piece = [&](int c, auto sc, int s) {
+      constexpr int SL = decltype(sc)::value;
+      const char* src = abase + (size_t)c * ABYTES;
+      __builtin_amdgcn_global_load_lds((const void*)(src + s * 128), (lds_void*)(smem + SL * SLOT + s * 4096 + wid * 1024),
+                                       16, 0, 0);
+    };
     issue(0, std::integral_constant<int, 0>{});
-    if constexpr (NC > 1) issue(1, std::integral_constant<int, 1>{});
+    if constexpr (NC > 1 && !PF01) issue(1, std::integral_constant<int, 1>{});
 
     // chunk body, ring slot P = c % 3 compile-time (3 bodies in a runtime loop keep the
     // register pressure of a 3-chunk kernel; a fully unrolled NC = 8 spilled)
-    auto chunk = [&](int c, auto pc) {
+    // FIRST: chunk 0 with PF01 (compile-time c = 0): only its own pieces were issued at the
+    // step top, and it issues chunks 1 and 2 one piece per k-tile from inside its MFMA loop
+    auto chunk = [&](int c, auto pc, auto fc) {
       constexpr int P = decltype(pc)::value;
+      constexpr bool FIRST = decltype(fc)::value;
       stamp(t, 2 + 5 * c);
       // vector-memory ops issued after chunk c's LDS-DMA (top of c issues c+2, then stores)
       // (issue order: prologue glds 0, 1; chunk k: glds k+2, then the stores of chunk k-1,
       // NSTORE per wave, none in chunk 0)
       if (c == 0) {
-        if (NC > 1) wait_vmcnt<LPT>(); else wait_vmcnt<0>();
+        if (NC > 1 && !FIRST) wait_vmcnt<LPT>(); else wait_vmcnt<0>();
       } else if (c == 1) {
         if (NC > 2) wait_vmcnt<LPT>(); else wait_vmcnt<0>();
       } else if (c == 2) {
@@ -418,7 +432,9 @@ __global__ __launch_bounds__(256, 1) void lstm_fwd_persistent_kernel(
       asm volatile("" ::: "memory");
       __builtin_amdgcn_sched_barrier(0);  // keep each chunk's code (and live ranges) to itself
       stamp(t, 3 + 5 * c);
-      if (c + 2 < NC) issue(c + 2, std::integral_constant<int, (P + 2) % 3>{});
+      if constexpr (!FIRST) {
+        if (c + 2 < NC) issue(c + 2, std::integral_constant<int, (P + 2) % 3>{});
+      }
       const char* cur = smem + P * SLOT;
 
       f32x4 acc[2][4];  // written first by k-tile 0's MFMAs (src C = 0: no zeroing writes)
@@ -523,6 +539,18 @@ __global__ __launch_bounds__(256, 1) void lstm_fwd_persistent_kernel(
         }
         static_for<0, 8>([&](auto mc) {
           constexpr int i = decltype(mc)::value >> 2, j = decltype(mc)::value & 3;
+          if constexpr (FIRST) {  // no carried chunk: plain MFMAs, next chunks' pieces in between
+            if constexpr (kt == 0)
+              asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, 0"
+                           : "=&a"(acc[i][j]) : "v"(a[kt & 1][i]), "a"(w[kt][j]));
+            else if constexpr (kt < KTA)
+              asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc[i][j]) : "v"(a[kt & 1][i]), "a"(w[kt][j]));
+            else
+              asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc[i][j]) : "v"(a[kt & 1][i]), "v"(w[kt][j]));
+            if constexpr (decltype(mc)::value == 0)  // piece kt of chunks 1, 2 (KS pieces each)
+              issue_piece(1 + kt / KS, std::integral_constant<int, 1 + kt / KS>{}, kt % KS);
+            return;
+          }
           if constexpr (FUSED) {
             fused_slot(kc, mc);
             return;
@@ -604,10 +632,20 @@ __global__ __launch_bounds__(256, 1) void lstm_fwd_persistent_kernel(
     using S0 = std::integral_constant<int, 0>;
     using S1 = std::integral_constant<int, 1>;
     using S2 = std::integral_constant<int, 2>;
-    for (int c = 0; c < NC; c += 3) {
-      chunk(c, S0{});
-      if (c + 1 < NC) chunk(c + 1, S1{});
-      if (c + 2 < NC) chunk(c + 2, S2{});
+    using NF = std::false_type;
+    if constexpr (PF01) {
+      chunk(0, S0{}, std::true_type{});
+      for (int c = 1; c < NC; c += 3) {
+        chunk(c, S1{}, NF{});
+        if (c + 1 < NC) chunk(c + 1, S2{}, NF{});
+        if (c + 2 < NC) chunk(c + 2, S0{}, NF{});
+      }
+    } else {
+      for (int c = 0; c < NC; c += 3) {
+        chunk(c, S0{}, NF{});
+        if (c + 1 < NC) chunk(c + 1, S1{}, NF{});
+        if (c + 2 < NC) chunk(c + 2, S2{}, NF{});
+      }
     }
     {  // drain: the last chunk's epilogue
       float cv[2][4];
@@ -631,6 +669,7 @@ static int launch_pf(bf16_t* XH, const bf16_t* Wp, float* Cst, bf16_t* S, unsign
     if (d.dbg == 16) f = reinterpret_cast<const void*>(&lstm_fwd_persistent_kernel<KT, NC, 16>);
     if (d.dbg == 48) f = reinterpret_cast<const void*>(&lstm_fwd_persistent_kernel<KT, NC, 48>);
     if (d.dbg == 64) f = reinterpret_cast<const void*>(&lstm_fwd_persistent_kernel<KT, NC, 64>);  // stores inside the loop
+    if (d.dbg == 1024) f = reinterpret_cast<const void*>(&lstm_fwd_persistent_kernel<KT, NC, 1024>);  // chunk 1 at the step top
     if (d.dbg == 512) f = reinterpret_cast<const void*>(&lstm_fwd_persistent_kernel<KT, NC, 512>);  // pinned micro-stages
     if (d.dbg == 128) f = reinterpret_cast<const void*>(&lstm_fwd_persistent_kernel<KT, NC, 128>);  // half-element epilogue
   }

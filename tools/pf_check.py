@@ -9,7 +9,7 @@ sys.path.insert(0, ".")
 from wellflow.data.synth import synth_lstm_batch  # noqa: E402
 from wellflow.models.lstm import NativeLSTM, init_lstm_flat  # noqa: E402
 
-variants = sys.argv[1].split(",") if len(sys.argv) > 1 else ["0"]
+variants = sys.argv[1].split(",") if len(sys.argv) > 1 else ["0"]  # WELLFLOW_PF_DBG values
 for B, H, T in ((8192, 512, 8), (512, 256, 6), (256, 128, 5), (2048, 512, 64)):
     F = 16
     eng = NativeLSTM(F, H, T, B, device="cuda")
