@@ -231,8 +231,12 @@ class NativeLSTM:
     def persistent_error(self) -> int:
         """Sticky spin-timeout flags of the persistent forward (bit 0) and backward (bit 1),
         set by ANY launch since the last :meth:`reset_device_errors` (one host sync)."""
-        w = torch.stack([self.sync[0], self.sync_bwd[0]]).cpu()
-        return (1 if int(w[0]) else 0) | (2 if int(w[1]) else 0)
+        w = torch.stack([self.sync[:4], self.sync_bwd[:4]]).cpu().tolist()
+        # bit 0 / 1: sticky spin timeout; bit 2 / 3: the LAST launch's workgroups completed fewer
+        # steps than launched (word 2 < word 3: an early exit that tripped no spin bound)
+        e = (1 if w[0][0] else 0) | (2 if w[1][0] else 0)
+        e |= (4 if w[0][3] and w[0][2] != w[0][3] else 0) | (8 if w[1][3] and w[1][2] != w[1][3] else 0)
+        return e
 
     def reset_device_errors(self) -> None:
         self.sync[0] = 0
@@ -244,9 +248,14 @@ class NativeLSTM:
         e = self.persistent_error()
         if e:
             parts = [n for b, n in ((1, "forward"), (2, "backward")) if e & b]
-            raise RuntimeError(f"persistent LSTM {' and '.join(parts)} hit the hand-off spin bound "
-                               "(a workgroup never arrived: non-resident grid or a hung wave); "
-                               "results of the affected steps are invalid")
+            short = [n for b, n in ((4, "forward"), (8, "backward")) if e & b]
+            what = []
+            if parts:
+                what.append(f"{' and '.join(parts)} hit the hand-off spin bound (a workgroup never arrived: "
+                            "non-resident grid or a hung wave)")
+            if short:
+                what.append(f"{' and '.join(short)} workgroups exited before completing every step")
+            raise RuntimeError(f"persistent LSTM {'; '.join(what)}; results of the affected steps are invalid")
 
     # ------------------------------------------------------------------ passes
     def forward(self, x: torch.Tensor) -> torch.Tensor:

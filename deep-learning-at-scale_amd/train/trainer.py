@@ -139,9 +139,13 @@ class Trainer:
         if not (hasattr(X, "starts") and isinstance(rows, np.ndarray) and rows.dtype == np.float32
                 and native.wanted()):
             return None
-        # targets come from Y per window; the prefetcher's per-row target buffer is unused
+        # targets come from Y per window; the prefetcher's per-row target buffer is unused.
+        # Pageable slots by default: with pinned slots (WELLFLOW_EVAL_PIN=1) allocated between
+        # the epochs of a graph-replayed LSTM job, later persistent launches completed only
+        # part of their steps (job bwd 0.11 vs 1.76 ms; caught by the completion counters,
+        # NativeLSTM.check_device_errors; profiles/r2_summary.md)
         return native.Prefetcher(rows, np.asarray(X.starts), np.zeros(len(rows), np.float32), X.T, chunk,
-                                 nslots=2, threads=2, pin=self.eng.device.type == "cuda")
+                                 nslots=2, threads=2, pin=os.environ.get("WELLFLOW_EVAL_PIN", "0") == "1")
 
     # ------------------------------------------------------------------ state
     def state_dict(self) -> dict:
