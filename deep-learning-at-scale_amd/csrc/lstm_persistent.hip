@@ -56,7 +56,7 @@ template <typename A, typename B> __device__ __forceinline__ void pin(A& a, B& b
 // sync words (uint32): [0] STICKY error (bit 0: a spin bound tripped in some launch; never
 // cleared by a launch, read and reset by the host), [1] error of the current launch (all
 // workgroups drain when it is set), [2] steps completed by the launch's workgroups, [3] the
-// launcher's expected count (grid x steps), [16 + 16*m] arrivals of row block m. A launch resets
+// expected count (grid x steps, stored by workgroup 0 before any exit path), [16 + 16*m] arrivals of row block m. A launch resets
 // words 1.. only, so a timeout in any earlier step stays visible (NativeLSTM.check_device_errors).
 int lstm_persistent_sync_words(int row_blocks) { return 16 + 16 * row_blocks; }
 
@@ -121,6 +121,8 @@ __global__ __launch_bounds__(256, 1) void lstm_fwd_persistent_kernel(
     }
   };
 
+  // expected completion count (word 3 = grid x T), stored before any exit path
+  if (blockIdx.x == 0 && threadIdx.x == 0) sync[3] = gridDim.x * (unsigned)d.T;
   // ---- prologue: stationary weight fragments (B operand: lane holds col l15, k 8g..8g+7)
   bf16x8 w[KT][4];
 #pragma unroll
@@ -657,7 +659,7 @@ __global__ __launch_bounds__(256, 1) void lstm_fwd_persistent_kernel(
       publish(NC - 1);
     }
   }
-  // completion count: every workgroup that ran all T steps adds T to word 2; the launcher
+  // completion count: every workgroup that ran all T steps adds T to word 2; workgroup 0
   // stored grid * T in word 3. Any early exit leaves word 2 short of word 3, which the host
   // check reports even when no spin bound tripped (NativeLSTM.persistent_error)
   if (threadIdx.x == 0) __hip_atomic_fetch_add(sync + 2, (unsigned)d.T, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -736,8 +738,7 @@ int launch_lstm_fwd_persistent(bf16_t* XH, const bf16_t* Wp, float* Cst, bf16_t*
   const int grid = MB * NB;
   for (int k = 0; k < nsub; ++k) {
     // reset this launch's error word and the arrival counters; word 0 (sticky) is kept
-    if (hipMemsetAsync(sync + 1, 0, sizeof(unsigned) * (size_t)(lstm_persistent_sync_words(MB) - 1), s) != hipSuccess ||
-        hipMemsetD32Async((hipDeviceptr_t)(sync + 3), grid * d.T, 1, s) != hipSuccess)  // expected completion count
+    if (hipMemsetAsync(sync + 1, 0, sizeof(unsigned) * (size_t)(lstm_persistent_sync_words(MB) - 1), s) != hipSuccess)
       return -(int)hipErrorLaunchFailure;
     LstmDims dk = d;
     dk.row_off = k * Bs;

@@ -93,6 +93,8 @@ __global__ __launch_bounds__(256, 1) void lstm_bwd_persistent_kernel(
     }
   };
 
+  // expected completion count (word 3 = grid x (T - 1)), stored before any exit path
+  if (blockIdx.x == 0 && threadIdx.x == 0) sync[3] = gridDim.x * (unsigned)(d.T - 1);
   // ---- prologue: stationary W_hh^T fragments (B operand: lane = unit col l15, k 8g..8g+7)
   bf16x8 w[KT][4];
 #pragma unroll
@@ -541,7 +543,7 @@ __global__ __launch_bounds__(256, 1) void lstm_bwd_persistent_kernel(
       __builtin_amdgcn_sched_barrier(0);
     });
   }
-  // completion count (word 2 vs the launcher's word 3; lstm_persistent.hip)
+  // completion count (word 2 vs word 3 from workgroup 0; lstm_persistent.hip)
   if (threadIdx.x == 0) __hip_atomic_fetch_add(sync + 2, (unsigned)(d.T - 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
@@ -608,9 +610,8 @@ int launch_lstm_bwd_persistent(const bf16_t* WhhT, const float* Cst, const bf16_
   if (sync_words < lstm_persistent_sync_words(MB)) return 0;
   const int grid = MB * NB;
   for (int k = 0; k < nsub; ++k) {
-    if (hipMemsetAsync(sync + 1, 0, sizeof(unsigned) * (size_t)(lstm_persistent_sync_words(MB) - 1), s) != hipSuccess ||
-        hipMemsetD32Async((hipDeviceptr_t)(sync + 3), grid * (d.T - 1), 1, s) != hipSuccess)
-      return -(int)hipErrorLaunchFailure;  // word 0 (sticky error) is kept; word 3 = expected completion count
+    if (hipMemsetAsync(sync + 1, 0, sizeof(unsigned) * (size_t)(lstm_persistent_sync_words(MB) - 1), s) != hipSuccess)
+      return -(int)hipErrorLaunchFailure;  // word 0 (sticky error) is kept
     LstmDims dk = d;
     dk.row_off = k * Bs;
     int r = 0;
