@@ -339,3 +339,27 @@ def test_persistent_timeout_is_sticky_and_raises(monkeypatch):
         run.run()
     monkeypatch.delenv("WELLFLOW_SPIN_LIMIT")
     eng.reset_device_errors()
+
+
+def test_persistent_completion_counters():
+    """Every persistent launch counts the steps its workgroups completed (sync word 2) against
+    the grid x steps workgroup 0 stores (word 3): equal after a clean forward + backward, and a
+    short count (an early exit that tripped no spin bound) makes check_device_errors raise."""
+    from wellflow.data.synth import synth_lstm_batch
+    from wellflow.models.lstm import NativeLSTM, init_lstm_flat
+
+    B, T, F, H = 8192, 8, 16, 512
+    eng = NativeLSTM(F, H, T, B, device=DEV)
+    eng.params.copy_(init_lstm_flat(F, H, seed=0).to(DEV))
+    eng.sync_weights()
+    x, y = synth_lstm_batch(B, T, F, seed=0)
+    eng.forward_backward(x.to(DEV), y.to(DEV), 1.0 / B)
+    torch.cuda.synchronize()
+    assert eng.last_forward_persistent and eng.last_backward_persistent
+    fw, bw = eng.sync[:4].tolist(), eng.sync_bwd[:4].tolist()
+    assert fw[3] > 0 and fw[2] == fw[3] and fw[3] % T == 0, fw
+    assert bw[3] > 0 and bw[2] == bw[3] and bw[3] % (T - 1) == 0, bw
+    eng.check_device_errors()
+    eng.sync_bwd[2] -= T - 1  # one workgroup "left early"
+    with pytest.raises(RuntimeError, match="backward workgroups exited before completing"):
+        eng.check_device_errors()
