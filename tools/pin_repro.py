@@ -1,0 +1,55 @@
+"""Does a pinned host allocation between persistent-LSTM launches make later launches exit
+early? (Round-2 finding: pinned eval prefetch slots allocated between the epochs of a
+graph-replayed job made the persistent kernels complete only part of their steps.)
+
+Prints the completion counters (sync words 2 / 3 of the forward and backward) for eager
+launches and for hipGraph replays, before and after pinning host memory."""
+import sys
+
+import torch
+
+sys.path.insert(0, ".")
+from wellflow.data.synth import synth_lstm_batch  # noqa: E402
+from wellflow.models.lstm import NativeLSTM, init_lstm_flat  # noqa: E402
+
+B, T, F, H = 8192, 64, 16, 512
+eng = NativeLSTM(F, H, T, B, device="cuda")
+eng.params.copy_(init_lstm_flat(F, H, seed=0).cuda())
+eng.sync_weights()
+x, y = synth_lstm_batch(B, T, F, seed=0)
+x, y = x.cuda(), y.cuda()
+
+
+def counters(tag):
+    torch.cuda.synchronize()
+    fw, bw = eng.sync[:4].tolist(), eng.sync_bwd[:4].tolist()
+    ok = fw[2] == fw[3] and bw[2] == bw[3]
+    print(f"{tag:40s} fwd {fw[2]}/{fw[3]} bwd {bw[2]}/{bw[3]} sticky {fw[0]},{bw[0]} -> {'ok' if ok else 'SHORT'}",
+          flush=True)
+
+
+eng.forward_backward(x, y, 1.0 / B)
+counters("eager")
+s = torch.cuda.Stream()
+s.wait_stream(torch.cuda.current_stream())
+with torch.cuda.stream(s):
+    eng.forward_backward(x, y, 1.0 / B)
+torch.cuda.current_stream().wait_stream(s)
+g = torch.cuda.CUDAGraph()
+with torch.cuda.graph(g):
+    eng.forward_backward(x, y, 1.0 / B)
+g.replay()
+counters("graph replay")
+pinned = [torch.empty(B * T * F, dtype=torch.float32).pin_memory() for _ in range(2)]
+counters("after pinning (no launch)")
+g.replay()
+counters("graph replay after pinning")
+eng.forward_backward(x, y, 1.0 / B)
+counters("eager after pinning")
+for p in pinned:
+    p.cuda()  # a copy from the pinned buffers
+g.replay()
+counters("graph replay after pinned copies")
+del pinned
+g.replay()
+counters("graph replay after freeing")
