@@ -53,3 +53,31 @@ counters("graph replay after pinned copies")
 del pinned
 g.replay()
 counters("graph replay after freeing")
+
+# the job's pattern: the native prefetcher filling pinned slots while the persistent forward
+# (evaluation) runs, then the graph-replayed training step
+import numpy as np  # noqa: E402
+
+from wellflow.data import native  # noqa: E402
+
+rows = np.random.default_rng(0).standard_normal((200000, F)).astype(np.float32)
+starts = np.arange(0, 200000 - T, dtype=np.int64)
+pf = native.Prefetcher(rows, starts, np.zeros(len(rows), np.float32), T, B, nslots=2, threads=2, pin=True)
+rng = np.random.default_rng(1)
+pf.submit(0, rng.integers(0, len(starts), B))
+for k in range(4):
+    pf.submit((k + 1) % 2, rng.integers(0, len(starts), B))
+    xh, _ = pf.wait(k % 2)
+    xb = xh.to("cuda")
+    eng.forward(xb)
+pf.wait(0)
+pf.wait(1)
+counters("eval forwards with the pinned prefetcher")
+pf.close()
+del pf
+g.replay()
+counters("graph replay after the pinned prefetcher")
+g.replay()
+counters("second replay")
+eng.forward_backward(x, y, 1.0 / B)
+counters("eager after the pinned prefetcher")
