@@ -77,6 +77,38 @@ def _stale(target: str, deps) -> bool:
     return any(os.path.getmtime(d) > t for d in deps)
 
 
+def _local_deps(src: str, seen=None) -> list:
+    """The quoted #include files of ``src`` (transitively, csrc-local only): a header edit
+    rebuilds only the sources that include it (the persistent LSTM kernels alone take
+    minutes to compile)."""
+    import re
+
+    seen = set() if seen is None else seen
+    d = os.path.dirname(src)
+    with open(src) as f:
+        for inc in re.findall(r'^\s*#\s*include\s+"([^"]+)"', f.read(), re.M):
+            p = os.path.normpath(os.path.join(d, inc))
+            if os.path.exists(p) and p not in seen:
+                seen.add(p)
+                _local_deps(p, seen)
+    return sorted(seen)
+
+
+def _variants(src: str) -> list:
+    """[(object tag, -D flags)]: one object per variant listed in the source's
+    ``// wf-build-variants: -DA=1 -DB=2 | -DA=3 ...`` lines (instantiation sources compile in
+    parallel, one slow template instantiation each), else one plain object."""
+    out = []
+    with open(src) as f:
+        for line in f:
+            if line.startswith("// wf-build-variants:"):
+                for v in line.split(":", 1)[1].split("|"):
+                    defs = v.split()
+                    tag = "." + "_".join(d[2:].replace("=", "") for d in defs)
+                    out.append((tag, defs))
+    return out or [("", [])]
+
+
 def _run(cmd, verbose):
     if verbose:
         print(" ".join(cmd), flush=True)
@@ -89,7 +121,6 @@ def _run(cmd, verbose):
 def build(verbose: bool = False, jobs: int | None = None) -> str:
     """Compile every HIP source for gfx950 and link ``_C.so``; returns its path."""
     os.makedirs(BUILD_DIR, exist_ok=True)
-    headers = glob.glob(os.path.join(CSRC, "*.h"))
     hip_srcs = sorted(glob.glob(os.path.join(CSRC, "*.hip")))
     tflags, ldflags = _torch_flags()
     hipcc = os.path.join(ROCM, "bin", "hipcc")
@@ -97,15 +128,21 @@ def build(verbose: bool = False, jobs: int | None = None) -> str:
 
     tasks = []
     objs = []
+    # WELLFLOW_DIAG_BUILD=1: also the timing-only diagnostic kernel variants (WELLFLOW_PF_DBG,
+    # tools/pf_time.py, pb_time.py, *_timeline.py); separate objects, so switching is a relink
+    diag = os.environ.get("WELLFLOW_DIAG_BUILD", "0") == "1"
     for src in hip_srcs:
-        obj = os.path.join(BUILD_DIR, os.path.basename(src) + ".o")
-        objs.append(obj)
-        if _stale(obj, [src] + headers):
-            tasks.append([hipcc, *HIPCC_FLAGS, f"-I{CSRC}", "-c", src, "-o", obj])
+        deps = [src] + _local_deps(src)
+        for tag, defs in _variants(src):
+            defs = defs + (["-DWF_DIAG"] if diag else [])
+            obj = os.path.join(BUILD_DIR, os.path.basename(src) + tag + (".diag" if diag else "") + ".o")
+            objs.append(obj)
+            if _stale(obj, deps):
+                tasks.append([hipcc, *HIPCC_FLAGS, *defs, f"-I{CSRC}", "-c", src, "-o", obj])
     bsrc = os.path.join(CSRC, "binding.cpp")
     bobj = os.path.join(BUILD_DIR, "binding.cpp.o")
     objs.append(bobj)
-    if _stale(bobj, [bsrc] + headers):
+    if _stale(bobj, [bsrc] + _local_deps(bsrc)):
         tasks.append(["g++", "-O2", "-std=c++17", "-fPIC", f"-I{CSRC}", *tflags, "-c", bsrc, "-o", bobj])
 
     with cf.ThreadPoolExecutor(max_workers=jobs) as ex:

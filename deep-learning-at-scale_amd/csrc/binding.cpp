@@ -176,6 +176,16 @@ void lstm_forward(const at::Tensor& XH, const at::Tensor& Wp, const at::Tensor& 
   for (int t = 0; t < d.T; ++t) wf::launch_lstm_fwd_step(t, bfp(XH), bfp(Wp), fp(Cst), bfp(S), d, s);
 }
 
+// A persistent kernel's sync buffer: int32, and the START of its own allocation. The launcher
+// zeroes its per-launch block with one memset from that start; a memset node whose region
+// starts inside an allocation (4 B past it in round 2) left 0x04040404 in its first word
+// under graph replay, which drained every workgroup (profiles/r3_early_exit.md).
+void check_sync(const at::Tensor& sync) {
+  check_t(sync, at::kInt, "sync");
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(sync.data_ptr()) % 512 == 0,
+              "persistent sync buffer must start its own allocation (models/lstm.py persistent_sync_buffer)");
+}
+
 // Raise on a failed persistent launch (status < 0: -(hipError_t)); 0 = not supported.
 bool persistent_status(int st, const char* what) {
   TORCH_CHECK(st >= 0, what, ": launch failed: ", hipGetErrorString((hipError_t)(-st)));
@@ -192,7 +202,7 @@ bool lstm_forward_persistent(const at::Tensor& XH, const at::Tensor& Wp, const a
   check_lstm_state(XH, Cst, S, d);
   check_t(Wp, at::kBFloat16, "Wp");
   check_extent(Wp, 4 * H * (KX + H), "Wp");
-  check_t(sync, at::kInt, "sync");
+  check_sync(sync);
   const c10::hip::OptionalHIPGuardMasqueradingAsCUDA guard(XH.device());
   return persistent_status(wf::launch_lstm_fwd_persistent(bfp(XH), bfp(Wp), fp(Cst), bfp(S),
                                                           reinterpret_cast<unsigned*>(sync.data_ptr<int>()),
@@ -220,7 +230,7 @@ void lstm_backward(const at::Tensor& WhhT, const at::Tensor& XH, const at::Tenso
   const c10::hip::OptionalHIPGuardMasqueradingAsCUDA guard(XH.device());
   auto s = cur_stream();
   if (sync.has_value()) {  // step T-1, then the persistent chain (tools/pb_time.py)
-    check_t(*sync, at::kInt, "sync");
+    check_sync(*sync);
     wf::launch_lstm_bwd_step(d.T - 1, bfp(WhhT), fp(Cst), bfp(S), bfp(DG), fp(dcarry), fp(dy),
                              fp(w_out), d, s);
     TORCH_CHECK(persistent_status(wf::launch_lstm_bwd_persistent(bfp(WhhT), fp(Cst), bfp(S), bfp(DG), fp(dcarry),
@@ -324,7 +334,7 @@ bool lstm_backward_dw(const at::Tensor& WhhT, const at::Tensor& XH, const at::Te
                              fp(w_out), d, main);
     bool done = false;
     if (sync.has_value()) {
-      check_t(*sync, at::kInt, "sync");
+      check_sync(*sync);
       done = persistent_status(wf::launch_lstm_bwd_persistent(bfp(WhhT), fp(Cst), bfp(S), bfp(DG), fp(dcarry),
                                                               reinterpret_cast<unsigned*>(sync->data_ptr<int>()),
                                                               sync->numel(), d, main),

@@ -47,11 +47,13 @@ void launch_lstm_pack_x(const float* x, bf16_t* XH, LstmDims d, hipStream_t s, b
 void launch_lstm_fwd_step(int t, bf16_t* XH, const bf16_t* Wp, float* Cst, bf16_t* S,
                           LstmDims d, hipStream_t s);
 // All T forward steps in ONE persistent launch per sub-batch (lstm_persistent.hip). `sync`
-// must hold lstm_persistent_sync_words(row blocks) words (<= 16 + 16 * B / 32 always
-// suffices); word 0 is the STICKY spin-timeout flag (never cleared by a launch), word 1 the
-// current launch's. Returns 1 launched, 0 shape / device cannot host it (nothing launched),
+// must hold lstm_persistent_sync_total(row blocks) words (16 + 16 * (B / 32 + 1) + 64 always
+// suffices): a per-launch block at the start (zeroed by the launcher) and the 64-word
+// completion STAT block at the end (persistent_guard.h; running totals, never cleared by a
+// launch). Returns 1 launched, 0 shape / device cannot host it (nothing launched),
 // < 0 = -(hipError_t) of a failed launch.
 int lstm_persistent_sync_words(int row_blocks);
+long lstm_persistent_sync_total(int row_blocks);
 int launch_lstm_fwd_persistent(bf16_t* XH, const bf16_t* Wp, float* Cst, bf16_t* S, unsigned* sync,
                                 long sync_words, LstmDims d, hipStream_t s);
 // Backward steps T-2 .. 0 in ONE persistent launch per sub-batch (lstm_persistent_bwd.hip),

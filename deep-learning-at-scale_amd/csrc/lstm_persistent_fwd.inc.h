@@ -1,0 +1,692 @@
+// wellflow — persistent LSTM forward: ONE launch runs all T timesteps (kernel template; the
+// instantiations are lstm_pf_parts.hip, the host launcher lstm_persistent.hip)
+// (SURVEY.md §2.4 K13 "persistent kernel over T, W sliced across CUs, per-step agent-scope
+// hand-off of h_t"; §7.4 hard part 2).
+//
+// Why: the per-step kernel (lstm.hip) re-streams its whole 256x256 weight tile from L2 /
+// Infinity Cache every step (576 KB per CU per step with the activations) and pays a grid
+// fill/drain per step. Here the weights never move after the prologue:
+//  * grid = (B / (64*NC)) row blocks x (4H / 256) gate-column blocks, one 256-thread
+//    workgroup (4 waves, one per SIMD) per CU, all co-resident (persistent_launch.h).
+//  * wave w of column block n keeps Wp[gate cols n*256 + 64w .. +63][0:KA] — the four
+//    gates of 16 hidden units (see the permutation in lstm.hip) — as MFMA B fragments in
+//    registers for the whole sequence: KA/32 x 4 bf16x8 = 288 VGPRs at KA = 576.
+//  * per step the workgroup streams its rows of [x_t | 1 | h_{t-1}] through a 2-deep LDS
+//    ring of 64-row chunks (global_load_lds, 72 KB per chunk), so only activations move:
+//    half the bytes of the per-step kernel.
+//  * the fused cell epilogue is the per-step kernel's (same FN layouts for C / S, so the
+//    backward pass is unchanged); h_t is staged through LDS and published with 8-B
+//    write-through (sc1) stores.
+//  * hand-off (cdna_hip_programming.md Guideline 16, recipe R1): every wave drains its
+//    stores (vmcnt(0)), workgroup barrier, ONE lane adds to the row block's arrival counter
+//    (agent-scope atomic); the consumer polls that counter relaxed with s_sleep, then ONE
+//    agent-scope acquire, then plain / LDS-DMA loads. Only the NB workgroups of one row
+//    block depend on each other, so row blocks drift freely (no grid barrier), and the
+//    XCD-aware block map puts a row block's NB workgroups on one XCD (speed only).
+//  * every spin is bounded: on timeout the error word is set and all workgroups drain.
+#pragma once
+#include <cstdlib>
+
+#include "gemm_core.h"
+#include "kernels.h"
+#include "lstm_layout.h"
+#include "persistent_guard.h"
+#include "persistent_launch.h"
+
+namespace wf {
+
+namespace {
+constexpr int PF_ROWS = 32;               // rows per ring chunk
+constexpr unsigned PF_SPIN_LIMIT = 1u << 21;
+typedef __attribute__((address_space(1))) unsigned gu32;
+typedef __attribute__((address_space(1))) unsigned long long gu64;
+
+// one cell element in flight through the forward's micro-staged epilogue
+struct EpiMicro {
+  float zi, zf, zg, zo, ei, ef, eg, eo, ig, fg, gg, og, cn, ec;
+  unsigned p0, p1;
+};
+// empty volatile asm: the value must exist in a VGPR at this point of the instruction stream
+// The value is redefined there ("+v"), so its consumers stay after this point too. (Input-
+// only pins avoid the hazard recognizer's s_nop after every such asm, but let the compiler
+// regroup the stages and shuffle values through AGPRs: 2.21 vs 1.50 ms per forward.)
+__device__ __forceinline__ void pin(float& a) { asm volatile("" : "+v"(a)); }
+template <typename A, typename B> __device__ __forceinline__ void pin(A& a, B& b) {
+  asm volatile("" : "+v"(a), "+v"(b));
+}
+}  // namespace
+
+// KT = KA / 32 k-tiles; NC = 32-row chunks per workgroup per step (compile-time, so every
+// ring slot, LDS offset and vmcnt count below is an immediate).
+template <int KT, int NC, int DBG = 0>  // DBG: timing-only builds (2 no MFMA, 4 no C/S stores, 8 no c loads; 64 stores in the loop)
+__global__ __launch_bounds__(256, 1) void lstm_fwd_persistent_kernel(
+    bf16_t* __restrict__ XH, const bf16_t* __restrict__ Wp, float* __restrict__ Cst,
+    bf16_t* __restrict__ S, unsigned* __restrict__ sync, unsigned* __restrict__ stat, LstmDims d) {
+  constexpr int KA = 32 * KT;
+  constexpr int KS = KA / 64;                // 64-deep k-steps = A pieces per wave per chunk
+  constexpr int ABYTES = PF_ROWS * KA * 2;   // chunk of [x_t | 1 | h_t-1] rows: KS [32][64] images
+  constexpr int LPT = KS;                    // LDS-DMA instructions per wave per chunk
+  // k-tiles whose weight fragments live in AGPRs (the rest in VGPRs): 256 AGPRs minus 2 x 32
+  // accumulator registers (this chunk + the pipelined previous one) = 12 k-tiles x 4 x 4
+  constexpr int KTA = KT < 12 ? KT : 12;
+  constexpr int NSTORE = (DBG & 4) ? 1 : 7;  // stores per wave per chunk: 2 C, 4 S, 1 h
+  // one asm statement per MFMA + cell-math micro-stage (H = 512; WELLFLOW_PF_DBG=512: pinned
+  // C++ micro-stages instead, for A/B)
+  constexpr bool FUSED = KT == 18 && (DBG & (2 | 128 | 512)) == 0;
+  // the step top issues only chunk 0's pieces, so chunk 0 starts sooner after the hand-off
+  // (every workgroup of the grid fetches its first chunks at once there); chunk 0 issues
+  // chunks 1 and 2 from its MFMA loop (WELLFLOW_PF_DBG=1024: both at the step top, A/B)
+  constexpr bool PF01 = NC >= 3 && (DBG & (2 | 1024)) == 0;
+  // Distinct static LDS objects per ring slot: the compiler then proves the slot being
+  // filled by LDS-DMA disjoint from the slots being read, and inserts no vmcnt(0) of its own.
+  // EXACTLY ONE static LDS variable, compile-time offsets for every ring slot, the h staging
+  // area and the flag word (slot k at k*SLOT: one A chunk). With several LDS
+  // variables the LDS lowering gives each its own alias scope, the waitcnt pass then tracks
+  // the LDS-DMA into the ring and guards the first read of every slot with vmcnt(0) — which
+  // drained the whole prefetch ring every chunk (measured: loads no longer overlapped MFMA).
+  constexpr int SLOT = ABYTES;
+  constexpr int HOFF = 3 * SLOT, FOFF = HOFF + PF_ROWS * 64 * 2;
+  __shared__ __attribute__((aligned(16))) char smem[FOFF + 16];
+  // h_t staging [32][64] bf16, accessed only through inline asm (32-bit LDS address)
+  const unsigned hb_lds = (unsigned)(uintptr_t)((__attribute__((address_space(3))) char*)(smem + HOFF));
+  const unsigned flag_lds = (unsigned)(uintptr_t)((__attribute__((address_space(3))) char*)(smem + FOFF));
+
+  constexpr int H = KA - 64, G = 4 * H, NB = G / 256, HB = H / 16;  // KX = 64 (host-checked)
+  const int Bp = fn_rows(d.B);
+  const int lane = threadIdx.x & 63, l15 = lane & 15, g = lane >> 4;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int L = xcd_remap(blockIdx.x, gridDim.x);
+  const int m = L / NB, n = L % NB;
+  const int row0 = m * PF_ROWS * NC + d.row_off;  // row_off: sub-batch origin (launcher)
+  const int ub = n * 4 + wid;                // 16-unit block of this wave
+  const int u = ub * 16 + l15;               // hidden unit of this lane
+  const int loff_c = ub * 256 + lane * 4;    // float offset of this lane's C slot in a FN row block
+  const int loff_s = ub * 1024 + lane * 16;  // bf16 offset of this lane's S slot in a FN row block
+  const int loff_h = (((int)threadIdx.x >> 3) * KA + ((int)threadIdx.x & 7) * 8) * 2;  // h publish
+  // error word: word 0 of the per-launch block (word 1 in the round-2 layout A/B, PF_DBG bit 20)
+  gu32* err = (gu32*)(sync + ((d.dbg >> 20) & 1));
+  gu32* cnt = (gu32*)(sync + 16 + 16 * m);
+  const unsigned spin_limit = d.spin_limit ? d.spin_limit : PF_SPIN_LIMIT;
+  // DBG & 16: timeline stamps (s_memrealtime, 100 MHz) of step PF_STAMP_T, wave 0 lane 0 of
+  // every workgroup, into sync + 4096 words (64 slots per workgroup; diagnostics only)
+  constexpr int PF_STAMP_T = 10;
+  unsigned long long* stamps = reinterpret_cast<unsigned long long*>(sync + 4096) + blockIdx.x * 64;
+  auto stamp = [&](int t, int slot) {
+    if constexpr ((DBG & 16) != 0) {
+      if (t == PF_STAMP_T && threadIdx.x == 0) stamps[slot] = __builtin_amdgcn_s_memrealtime();
+    }
+  };
+
+  // completion guard (persistent_guard.h): started / expected counts before any exit path
+  unsigned ord = 0;
+  if (threadIdx.x == 0) ord = pguard_start(stat, (unsigned)d.T);
+  // ---- prologue: stationary weight fragments (B operand: lane holds col l15, k 8g..8g+7)
+  bf16x8 w[KT][4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const bf16_t* wr = Wp + (size_t)(n * 256 + wid * 64 + j * 16 + l15) * KA + 8 * g;
+#pragma unroll
+    for (int kt = 0; kt < KT; ++kt) w[kt][j] = *reinterpret_cast<const bf16x8*>(wr + 32 * kt);
+  }
+  // drain them with a wait the compiler's counter model sees (the memory clobber keeps the
+  // loads above it), so it does not re-wait for them at the top of every step
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_waitcnt(0xF70);  // vmcnt(0) expcnt(7) lgkmcnt(15)
+  __builtin_amdgcn_sched_barrier(0);
+
+  // A piece s of this wave: k-step s, rows wid*8 + (lane>>3); the K_CONTIG 16-B chunk
+  // swizzle (row>>1)&7 = 4(wid&1) + g is lane-constant, so it moves onto the source offset.
+  const unsigned aoff = (unsigned)((wid * 8 + (lane >> 3)) * KA * 2 + (((lane & 7) ^ (4 * (wid & 1) + g)) << 4));
+  int fa[2];  // A fragment offsets in a [32][64] image (rows l15 of a 16-row tile)
+#pragma unroll
+  for (int kk = 0; kk < 2; ++kk) fa[kk] = l15 * 128 + (((kk * 4 + g) ^ ((l15 >> 1) & 7)) << 4);
+
+  // c_{t-1} of the workgroup's 8 chunks stays in registers for the whole sequence (a queue
+  // the chunk loop rotates: chunk c reads cq[0] and appends its c_t), so the forward never
+  // re-reads the cell state it wrote (16.8 MB per step at B = 8192); C is still stored for
+  // the backward. c_{-1} = 0.
+  f32x4 cq[NC][2];
+#pragma unroll
+  for (int q = 0; q < NC; ++q)
+#pragma unroll
+    for (int i = 0; i < 2; ++i) cq[q][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  f32x4 accp[2][4];  // gate pre-activations of the previous chunk (software pipeline)
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) accp[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  for (int t = 0; t < d.T; ++t) {
+    stamp(t, 0);
+    if (t > 0) {
+      // ---- publish step t-1 (every wave drained its sc1 h stores) and wait for the row block
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      // thread 0's view of the wait, kept for the exit record (persistent_guard.h)
+      unsigned why = 0, seen_err = 0, seen_cnt = 0;
+      const unsigned target = (unsigned)(NB * t);
+      if (threadIdx.x == 0) {
+        __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        unsigned spins = 0;
+        while (!(d.dbg & 1) && (seen_cnt = __hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) < target) {
+          if ((seen_err = __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) != 0u) {
+            why = 1;
+            break;
+          }
+          if (++spins > spin_limit) {
+            __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            pguard_sticky(stat);
+            why = 2;
+            break;
+          }
+          __builtin_amdgcn_s_sleep(2);
+        }
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const int ok = why == 0 ? 1 : 0;
+        asm volatile("ds_write_b32 %0, %1" ::"v"(flag_lds), "v"(ok) : "memory");
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      // the flag word through ds_read in asm (a volatile C++ access became a flat load with
+      // sc0 sc1 and a vmcnt + lgkmcnt wait, every step)
+      int okv;
+      asm volatile("ds_read_b32 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(okv) : "v"(flag_lds) : "memory");
+      if (__builtin_amdgcn_readfirstlane(okv) != 1) {  // uniform: every wave reads the same word
+        if (lane == 0)
+          pguard_exit(stat, (unsigned)t, wid != 0 ? 4u : (why != 0 ? why : 3u), seen_err, seen_cnt, target,
+                      (unsigned)okv, ord);
+        return;
+      }
+    }
+    stamp(t, 1);
+    // opaque per-step copy of the row origin: stops the compiler hoisting every chunk's
+    // lane addresses out of the time loop (NC x 64-bit offsets live across the whole
+    // kernel pushed the H = 512, NC = 8 build into spills)
+    int rb = row0;
+    asm volatile("" : "+s"(rb));
+    // per-step uniform bases (row block origin folded in) + per-lane constant offsets
+    // (loff_c / loff_s / loff_h), so every chunk address is base + compile-time stride
+    float* cnext = Cst + (size_t)(t + 1) * Bp * H + (size_t)(rb >> 4) * HB * 256;
+    bf16_t* St = S + (size_t)t * Bp * G + (size_t)(rb >> 4) * HB * 1024;
+    const char* abase = reinterpret_cast<const char*>(XH + ((size_t)t * d.B + rb) * KA) + aoff;
+    // slab t + 1 of XH as a buffer resource for the 16-B sc1 h stores: per-slab byte offsets
+    // (< B * KA * 2 < 2^31, host-checked) so any batch size fits the 32-bit offsets
+    const __amdgpu_buffer_rsrc_t xh_rsrc =
+        __builtin_amdgcn_make_buffer_rsrc(XH + (size_t)(t + 1) * d.B * KA, 0, 0x7FFFFFFF, 0x00020000);
+    const int hsoff = (int)(((size_t)rb * KA + 64 + n * 64) * 2);
+
+    // cell epilogue element (row-tile i, row r) of the carried chunk: accp + c_{t-1} = cq[0]
+    auto epi_elem = [&](int i, int r, float (&cv)[2][4], unsigned (&pk)[2][8], unsigned (&hv)[2][4]) {
+      const float ig = sigmoid_pre(accp[i][0][r]);  // Wp carries the gate scales (pack kernel)
+      const float fg = sigmoid_pre(accp[i][1][r]);
+      const float gg = tanh_pre(accp[i][2][r]);
+      const float og = sigmoid_pre(accp[i][3][r]);
+      const float cn = fg * cq[0][i][r] + ig * gg;
+      cv[i][r] = cn;
+      pk[i][2 * r] = pk_bf16(ig, fg);
+      pk[i][2 * r + 1] = pk_bf16(gg, og);
+      hv[i][r] = f2bf(og * tanhf_(cn));
+    };
+    // The same element in two halves pinned to k-tile positions of the next chunk's MFMA
+    // loop. Empty asm statements take the inputs and produce the outputs at that point:
+    // the MFMAs are volatile asm too, so the compiler can neither hoist the cell math above
+    // the loop nor sink it below (it sank all of it: 144 MFMAs back to back, then ~280 VALU
+    // with the matrix core idle). Half 0: i, f, g gates and c_t; half 1: o gate, tanh(c_t),
+    // h_t and the packed gate words.
+    auto epi_half = [&](int hh, int i, int r, float (&cv)[2][4], float (&gs)[2][4], unsigned (&pk)[2][8],
+                        unsigned (&hv)[2][4]) {
+      if (hh == 0) {
+        float zi = accp[i][0][r], zf = accp[i][1][r], zg = accp[i][2][r], cp = cq[0][i][r];
+        asm volatile("" : "+v"(zi), "+v"(zf), "+v"(zg), "+v"(cp));
+        const float ig = sigmoid_pre(zi), fg = sigmoid_pre(zf), gg = tanh_pre(zg);
+        float cn = fg * cp + ig * gg;
+        unsigned p0 = pk_bf16(ig, fg);
+        float g2 = gg;
+        asm volatile("" : "+v"(cn), "+v"(p0), "+v"(g2));
+        cv[i][r] = cn;
+        pk[i][2 * r] = p0;
+        gs[i][r] = g2;
+      } else {
+        float zo = accp[i][3][r];
+        asm volatile("" : "+v"(zo));
+        const float og = sigmoid_pre(zo);
+        unsigned p1 = pk_bf16(gs[i][r], og);
+        unsigned h = f2bf(og * tanhf_(cv[i][r]));
+        asm volatile("" : "+v"(p1), "+v"(h));
+        pk[i][2 * r + 1] = p1;
+        hv[i][r] = h;
+      }
+    };
+    // The element as 18 micro-stages, each at most one issue slot's worth of VALU (one
+    // transcendental or two plain ops, <= 8 cycles: what a 16x16x32 MFMA leaves free of its
+    // 16), placed one per MFMA of the next chunk's loop (8 x 18 = 144 = the MFMA count at
+    // H = 512). Every stage pins its inputs and outputs with empty volatile asm, so it
+    // stays between its two MFMAs.
+    auto epi_micro = [&](auto sc, int i, int r, EpiMicro& e, float (&cv)[2][4], unsigned (&pk)[2][8],
+                         unsigned (&hv)[2][4]) {
+      constexpr int s = decltype(sc)::value;
+      if constexpr (s == 0) {
+        e.zi = accp[i][0][r];
+        e.zf = accp[i][1][r];
+        e.zg = accp[i][2][r];
+        e.zo = accp[i][3][r];
+        pin(e.zi, e.zf);
+        pin(e.zg, e.zo);
+      } else if constexpr (s == 1) {
+        pin(e.zi); e.ei = __builtin_amdgcn_exp2f(e.zi); pin(e.ei);
+      } else if constexpr (s == 2) {
+        pin(e.zf); e.ef = __builtin_amdgcn_exp2f(e.zf); pin(e.ef);
+      } else if constexpr (s == 3) {
+        pin(e.zg); e.eg = __builtin_amdgcn_exp2f(e.zg); pin(e.eg);
+      } else if constexpr (s == 4) {
+        pin(e.zo); e.eo = __builtin_amdgcn_exp2f(e.zo); pin(e.eo);
+      } else if constexpr (s == 5) {
+        pin(e.ei, e.ef); e.ei += 1.0f; e.ef += 1.0f; pin(e.ei, e.ef);
+      } else if constexpr (s == 6) {
+        pin(e.ei); e.ig = __builtin_amdgcn_rcpf(e.ei); pin(e.ig);
+      } else if constexpr (s == 7) {
+        pin(e.ef); e.fg = __builtin_amdgcn_rcpf(e.ef); pin(e.fg);
+      } else if constexpr (s == 8) {
+        pin(e.eg, e.eo); e.eg += 1.0f; e.eo += 1.0f; pin(e.eg, e.eo);
+      } else if constexpr (s == 9) {
+        pin(e.eg); e.gg = __builtin_amdgcn_rcpf(e.eg); pin(e.gg);
+      } else if constexpr (s == 10) {
+        pin(e.eo); e.og = __builtin_amdgcn_rcpf(e.eo); pin(e.og);
+      } else if constexpr (s == 11) {
+        // c_t = fma(f, c_{t-1}, i * g): the contraction the per-step kernel's
+        // f * c + i * g compiles to, so both paths round alike
+        pin(e.gg, e.ig); e.gg = 1.0f - 2.0f * e.gg; e.cn = e.ig * e.gg; pin(e.gg, e.cn);
+      } else if constexpr (s == 12) {
+        pin(e.cn, e.fg); e.cn = __builtin_fmaf(e.fg, cq[0][i][r], e.cn); e.p0 = pk_bf16(e.ig, e.fg); pin(e.cn, e.p0);
+      } else if constexpr (s == 13) {
+        pin(e.og); e.p1 = pk_bf16(e.gg, e.og); e.ec = e.cn * 2.8853900817779268f; pin(e.p1, e.ec);
+      } else if constexpr (s == 14) {
+        pin(e.ec); e.ec = __builtin_amdgcn_exp2f(e.ec); pin(e.ec);
+      } else if constexpr (s == 15) {
+        pin(e.ec); e.ec = __builtin_amdgcn_rcpf(e.ec + 1.0f); pin(e.ec);
+      } else if constexpr (s == 16) {
+        pin(e.ec); e.ec = e.og * (1.0f - 2.0f * e.ec); pin(e.ec);
+      } else {
+        pin(e.ec);
+        unsigned h = f2bf(e.ec);
+        pin(h, e.cn);
+        cv[i][r] = e.cn;
+        pk[i][2 * r] = e.p0;
+        pk[i][2 * r + 1] = e.p1;
+        hv[i][r] = h;
+      }
+    };
+    // The same three pieces, issued one by one from inside the next chunk's MFMA loop
+    // (diagnostic build WELLFLOW_PF_DBG=64, KT >= 16): h staging, then one C / S store per
+    // k-tile (issue order unchanged, so the vmcnt counts below still hold). Measured 1.64 vs
+    // 1.60 ms for the stores after the loop (tools/pf_time.py 0,64): not the default.
+    auto epi_h = [&](const unsigned (&hv)[2][4]) {
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          asm volatile("ds_write_b16 %0, %1" ::"v"(hb_lds + 2u * ((i * 16 + 4 * g + r) * 64 + wid * 16 + l15)),
+                       "v"(hv[i][r])
+                       : "memory");
+    };
+    auto epi_cs = [&](int e, int k, const float (&cv)[2][4], const unsigned (&pk)[2][8]) {  // k = 0..5
+      if constexpr (!(DBG & 4)) {
+        const int i = k < 2 ? k : (k - 2) >> 1;
+        if (k < 2) {
+          *reinterpret_cast<float4*>(cnext + (2 * e + i) * HB * 256 + loff_c) =
+              make_float4(cv[i][0], cv[i][1], cv[i][2], cv[i][3]);
+        } else {
+          const int hf = (k - 2) & 1;
+          uint4* sp = reinterpret_cast<uint4*>(St + (2 * e + i) * HB * 1024 + loff_s);
+          sp[hf] = make_uint4(pk[i][4 * hf], pk[i][4 * hf + 1], pk[i][4 * hf + 2], pk[i][4 * hf + 3]);
+        }
+      }
+    };
+    auto rotate = [&](const float (&cv)[2][4]) {
+#pragma unroll
+      for (int q = 0; q + 1 < NC; ++q)
+#pragma unroll
+        for (int i = 0; i < 2; ++i) cq[q][i] = cq[q + 1][i];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) cq[NC - 1][i] = f32x4{cv[i][0], cv[i][1], cv[i][2], cv[i][3]};
+    };
+    // stores of chunk e (C, S: NSTORE - 1 per wave), h staged in LDS, c-queue rotation
+    auto epi_store = [&](int e, const float (&cv)[2][4], const unsigned (&pk)[2][8], const unsigned (&hv)[2][4]) {
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          // LDS staging writes in asm: compiler-visible LDS writes are guarded by a vmcnt(0)
+          // (the waitcnt pass orders every LDS access after in-flight LDS-DMA)
+          asm volatile("ds_write_b16 %0, %1" ::"v"(hb_lds + 2u * ((i * 16 + 4 * g + r) * 64 + wid * 16 + l15)),
+                       "v"(hv[i][r])
+                       : "memory");
+        if constexpr (!(DBG & 4)) {
+          *reinterpret_cast<float4*>(cnext + (2 * e + i) * HB * 256 + loff_c) =
+              make_float4(cv[i][0], cv[i][1], cv[i][2], cv[i][3]);
+          uint4* sp = reinterpret_cast<uint4*>(St + (2 * e + i) * HB * 1024 + loff_s);
+          sp[0] = make_uint4(pk[i][0], pk[i][1], pk[i][2], pk[i][3]);
+          sp[1] = make_uint4(pk[i][4], pk[i][5], pk[i][6], pk[i][7]);
+        }
+      }
+#pragma unroll
+      for (int q = 0; q + 1 < NC; ++q)
+#pragma unroll
+        for (int i = 0; i < 2; ++i) cq[q][i] = cq[q + 1][i];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) cq[NC - 1][i] = f32x4{cv[i][0], cv[i][1], cv[i][2], cv[i][3]};
+    };
+    // publish chunk e's h rows: 32 rows x 128 B, one 16-B write-through (sc1) buffer store per
+    // thread (Guideline 16 R1: no release fence; 8-B sc1 stores cost 0.4 ms more, measured)
+    auto publish = [&](int e) {
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      u32x4 vv;  // row threadIdx>>3, 16-B column threadIdx&7 of the [32][64] bf16 tile
+      asm volatile("ds_read_b128 %0, %1\n\ts_waitcnt lgkmcnt(0)"
+                   : "=&v"(vv)
+                   : "v"(hb_lds + 16u * threadIdx.x)
+                   : "memory");
+      __builtin_amdgcn_raw_buffer_store_b128(vv, xh_rsrc, loff_h, hsoff + e * PF_ROWS * KA * 2, 16 /* sc1 */);
+    };
+
+    // chunk c -> ring slot c % 3: KS A pieces + this wave's 2 FN blocks of c_{t-1}
+    auto issue = [&](int c, auto sc) {  // chunk c into ring slot SL (= c % 3)
+      constexpr int SL = decltype(sc)::value;
+      char* ra = smem + SL * SLOT;
+      const char* src = abase + (size_t)c * ABYTES;
+#pragma unroll
+      for (int s = 0; s < KS; ++s)
+        __builtin_amdgcn_global_load_lds((const void*)(src + s * 128), (lds_void*)(ra + s * 4096 + wid * 1024),
+                                         16, 0, 0);
+    };
+    // piece s of chunk c into ring slot SL
+    auto issue_piece = [&](int c, auto sc, int s) {
+      constexpr int SL = decltype(sc)::value;
+      const char* src = abase + (size_t)c * ABYTES;
+      __builtin_amdgcn_global_load_lds((const void*)(src + s * 128), (lds_void*)(smem + SL * SLOT + s * 4096 + wid * 1024),
+                                       16, 0, 0);
+    };
+    issue(0, std::integral_constant<int, 0>{});
+    if constexpr (NC > 1 && !PF01) issue(1, std::integral_constant<int, 1>{});
+
+    // chunk body, ring slot P = c % 3 compile-time (3 bodies in a runtime loop keep the
+    // register pressure of a 3-chunk kernel; a fully unrolled NC = 8 spilled)
+    // FIRST: chunk 0 with PF01 (compile-time c = 0): only its own pieces were issued at the
+    // step top, and it issues chunks 1 and 2 one piece per k-tile from inside its MFMA loop
+    auto chunk = [&](int c, auto pc, auto fc) {
+      constexpr int P = decltype(pc)::value;
+      constexpr bool FIRST = decltype(fc)::value;
+      stamp(t, 2 + 5 * c);
+      // vector-memory ops issued after chunk c's LDS-DMA (top of c issues c+2, then stores)
+      // (issue order: prologue glds 0, 1; chunk k: glds k+2, then the stores of chunk k-1,
+      // NSTORE per wave, none in chunk 0)
+      if (c == 0) {
+        if (NC > 1 && !FIRST) wait_vmcnt<LPT>(); else wait_vmcnt<0>();
+      } else if (c == 1) {
+        if (NC > 2) wait_vmcnt<LPT>(); else wait_vmcnt<0>();
+      } else if (c == 2) {
+        if (NC > 3) wait_vmcnt<LPT + NSTORE>(); else wait_vmcnt<NSTORE>();
+      } else if (c + 1 < NC) {
+        wait_vmcnt<2 * NSTORE + LPT>();
+      } else {
+        wait_vmcnt<2 * NSTORE>();
+      }
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);  // keep each chunk's code (and live ranges) to itself
+      stamp(t, 3 + 5 * c);
+      if constexpr (!FIRST) {
+        if (c + 2 < NC) issue(c + 2, std::integral_constant<int, (P + 2) % 3>{});
+      }
+      const char* cur = smem + P * SLOT;
+
+      f32x4 acc[2][4];  // written first by k-tile 0's MFMAs (src C = 0: no zeroing writes)
+      // MFMAs in inline asm with explicit register classes: weights of k-tiles < KTA as AGPR
+      // operands, the rest as VGPR operands, accumulators in AGPRs. With the builtin the
+      // register allocator shuffled the 288 weight registers through v_accvgpr_read/mov copies
+      // before every use and single-buffered the A fragments (timeline: 2.5 us per chunk of
+      // MFMA work that issues in ~1 us). A fragments of k-tile kt+1 are read during kt.
+      // Software pipeline: the cell epilogue of chunk c-1 (accp, cq[0]) is computed INSIDE
+      // this loop, one (row-tile, row) element per k-tile, so its VALU / transcendental work
+      // issues between the MFMAs (chunk 0 computes on leftovers and discards the result).
+      bf16x8 a[2][2];
+      float cv[2][4], gs[2][4];
+      unsigned pk[2][8], hv[2][4];
+      EpiMicro ms;
+      // H = 512 (KT = 18, 144 MFMAs per chunk): each MFMA and one micro-stage of the carried
+      // chunk's cell math are ONE asm statement. No pin asm between them, so the hazard
+      // recognizer has nothing to pad: it pads (s_nop) only where an asm reads a VGPR that
+      // the asm right before it wrote, and two elements are in flight with their stages
+      // alternating, so a stage's producer is always >= 2 statements back. Slot m: pair
+      // m / 36 (elements 2p, 2p+1), stage (m % 36) / 2 of element 2p + (m & 1). Outputs are
+      // early-clobber: no stage result can share a register with the MFMA's operands.
+      EpiMicro e2[2];
+      auto fused_slot = [&](auto kc, auto mc) {
+        constexpr int kt = decltype(kc)::value, mm = decltype(mc)::value;
+        constexpr int i = mm >> 2, j = mm & 3, m = kt * 8 + mm;
+        constexpr int el = 2 * (m / 36) + (m & 1), st = (m % 36) / 2, ei_ = el >> 2, er = el & 3;
+        EpiMicro& E = e2[m & 1];
+        const bf16x8& A = a[kt & 1][i];
+#define WF_UNP(...) __VA_ARGS__
+#define WF_MF(TXT, OUTS, INS)                                                                          \
+  if constexpr (kt == 0)                                                                               \
+    asm volatile("v_mfma_f32_16x16x32_bf16 %[c], %[a], %[b], 0\n\t" TXT                                \
+                 : [c] "=&a"(acc[i][j]), WF_UNP OUTS : [a] "v"(A), [b] "a"(w[kt][j]) WF_UNP INS);    \
+  else if constexpr (kt < KTA)                                                                         \
+    asm volatile("v_mfma_f32_16x16x32_bf16 %[c], %[a], %[b], %[c]\n\t" TXT                             \
+                 : [c] "+a"(acc[i][j]), WF_UNP OUTS : [a] "v"(A), [b] "a"(w[kt][j]) WF_UNP INS);     \
+  else                                                                                                 \
+    asm volatile("v_mfma_f32_16x16x32_bf16 %[c], %[a], %[b], %[c]\n\t" TXT                             \
+                 : [c] "+a"(acc[i][j]), WF_UNP OUTS : [a] "v"(A), [b] "v"(w[kt][j]) WF_UNP INS);
+        if constexpr (st == 0) {
+          WF_MF("v_exp_f32 %[o], %[x]", ([o] "=&v"(E.ei)), (, [x] "v"(accp[ei_][0][er])))
+        } else if constexpr (st == 1) {
+          WF_MF("v_exp_f32 %[o], %[x]", ([o] "=&v"(E.ef)), (, [x] "v"(accp[ei_][1][er])))
+        } else if constexpr (st == 2) {
+          WF_MF("v_exp_f32 %[o], %[x]", ([o] "=&v"(E.eg)), (, [x] "v"(accp[ei_][2][er])))
+        } else if constexpr (st == 3) {
+          WF_MF("v_exp_f32 %[o], %[x]", ([o] "=&v"(E.eo)), (, [x] "v"(accp[ei_][3][er])))
+        } else if constexpr (st == 4) {
+          WF_MF("v_add_f32 %[p], 1.0, %[p]\n\tv_add_f32 %[q], 1.0, %[q]", ([p] "+v"(E.ei), [q] "+v"(E.ef)), ())
+        } else if constexpr (st == 5) {
+          WF_MF("v_rcp_f32 %[o], %[x]", ([o] "=&v"(E.ig)), (, [x] "v"(E.ei)))
+        } else if constexpr (st == 6) {
+          WF_MF("v_rcp_f32 %[o], %[x]", ([o] "=&v"(E.fg)), (, [x] "v"(E.ef)))
+        } else if constexpr (st == 7) {
+          WF_MF("v_add_f32 %[p], 1.0, %[p]\n\tv_add_f32 %[q], 1.0, %[q]", ([p] "+v"(E.eg), [q] "+v"(E.eo)), ())
+        } else if constexpr (st == 8) {
+          WF_MF("v_rcp_f32 %[o], %[x]", ([o] "=&v"(E.gg)), (, [x] "v"(E.eg)))
+        } else if constexpr (st == 9) {
+          WF_MF("v_rcp_f32 %[o], %[x]", ([o] "=&v"(E.og)), (, [x] "v"(E.eo)))
+        } else if constexpr (st == 10) {  // g = 1 - 2 r (tanh), then i * g into cn
+          WF_MF("v_fma_f32 %[g], %[g], -2.0, 1.0\n\tv_mul_f32 %[c2], %[x], %[g]", ([g] "+v"(E.gg), [c2] "=&v"(E.cn)),
+                (, [x] "v"(E.ig)))
+        } else if constexpr (st == 11) {  // c_t = fma(f, c_{t-1}, i g); packed (i, f)
+          WF_MF("v_fma_f32 %[c2], %[f], %[cp], %[c2]\n\tv_cvt_pk_bf16_f32 %[o], %[x], %[f]",
+                ([c2] "+v"(E.cn), [o] "=&v"(E.p0)), (, [f] "v"(E.fg), [cp] "v"(cq[0][ei_][er]), [x] "v"(E.ig)))
+        } else if constexpr (st == 12) {  // packed (g, o); 2 log2(e) c_t
+          WF_MF("v_cvt_pk_bf16_f32 %[o], %[g], %[x]\n\tv_mul_f32 %[y], 0x4038aa3b, %[c2]", ([o] "=&v"(E.p1), [y] "=&v"(E.ec)),
+                (, [g] "v"(E.gg), [x] "v"(E.og), [c2] "v"(E.cn)))
+        } else if constexpr (st == 13) {
+          WF_MF("v_exp_f32 %[p], %[p]", ([p] "+v"(E.ec)), ())
+        } else if constexpr (st == 14) {
+          WF_MF("v_add_f32 %[p], 1.0, %[p]", ([p] "+v"(E.ec)), ())
+        } else if constexpr (st == 15) {
+          WF_MF("v_rcp_f32 %[p], %[p]", ([p] "+v"(E.ec)), ())
+        } else if constexpr (st == 16) {  // h = o (1 - 2 r)
+          WF_MF("v_fma_f32 %[p], %[p], -2.0, 1.0\n\tv_mul_f32 %[p], %[x], %[p]", ([p] "+v"(E.ec)), (, [x] "v"(E.og)))
+        } else {  // bf16(h) in the low half
+          unsigned h;
+          WF_MF("v_cvt_pk_bf16_f32 %[o], %[x], 0", ([o] "=&v"(h)), (, [x] "v"(E.ec)))
+          cv[ei_][er] = E.cn;
+          pk[ei_][2 * er] = E.p0;
+          pk[ei_][2 * er + 1] = E.p1;
+          hv[ei_][er] = h;
+        }
+#undef WF_MF
+#undef WF_UNP
+      };
+#pragma unroll
+      for (int i = 0; i < 2; ++i) a[0][i] = *reinterpret_cast<const bf16x8*>(cur + i * 2048 + fa[0]);
+      if constexpr ((DBG & 32) != 0) {
+        a[1][0] = a[0][0];
+        a[1][1] = a[0][1];
+      }
+      static_for<0, KT>([&](auto kc) {
+        constexpr int kt = decltype(kc)::value;
+        if constexpr (kt + 1 < KT && !(DBG & 32)) {  // DBG & 32: timing only, no fragment reads
+#pragma unroll
+          for (int i = 0; i < 2; ++i)
+            a[(kt + 1) & 1][i] =
+                *reinterpret_cast<const bf16x8*>(cur + ((kt + 1) >> 1) * 4096 + i * 2048 + fa[(kt + 1) & 1]);
+        }
+        static_for<0, 8>([&](auto mc) {
+          constexpr int i = decltype(mc)::value >> 2, j = decltype(mc)::value & 3;
+          if constexpr (FIRST) {  // no carried chunk: plain MFMAs, next chunks' pieces in between
+            if constexpr (kt == 0)
+              asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, 0"
+                           : "=&a"(acc[i][j]) : "v"(a[kt & 1][i]), "a"(w[kt][j]));
+            else if constexpr (kt < KTA)
+              asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc[i][j]) : "v"(a[kt & 1][i]), "a"(w[kt][j]));
+            else
+              asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc[i][j]) : "v"(a[kt & 1][i]), "v"(w[kt][j]));
+            if constexpr (decltype(mc)::value == 0)  // piece kt of chunks 1, 2 (KS pieces each)
+              issue_piece(1 + kt / KS, std::integral_constant<int, 1 + kt / KS>{}, kt % KS);
+            return;
+          }
+          if constexpr (FUSED) {
+            fused_slot(kc, mc);
+            return;
+          }
+          if constexpr (!(DBG & 2)) {
+            if constexpr (kt == 0)  // accumulator := A B (inline-constant 0 as src C)
+              asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, 0"
+                           : "=&a"(acc[i][j]) : "v"(a[kt & 1][i]), "a"(w[kt][j]));
+            else if constexpr (kt < KTA)
+              asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc[i][j]) : "v"(a[kt & 1][i]), "a"(w[kt][j]));
+            else
+              asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc[i][j]) : "v"(a[kt & 1][i]), "v"(w[kt][j]));
+          }
+          if constexpr (!(DBG & 128)) {
+            // micro-stages of the carried chunk's cell math, one issue-slot's worth (<= 8
+            // cycles: one transcendental or two plain VALU) in each MFMA's shadow:
+            // stage q of 144 (8 elements x 18) goes after MFMA slot q * 8KT / 144
+            constexpr int S = 8 * KT, m = kt * 8 + decltype(mc)::value;
+            constexpr int qlo = (m * 144 + S - 1) / S, qhi = ((m + 1) * 144 + S - 1) / S;
+            static_for<qlo, qhi>([&](auto qc) {
+              constexpr int q = decltype(qc)::value;
+              epi_micro(std::integral_constant<int, q % 18>{}, q / 18 >> 2, (q / 18) & 3, ms, cv, pk, hv);
+            });
+          }
+        });
+        if constexpr ((DBG & 128) != 0) {
+          // 16 half-elements spread evenly over the KT k-tiles (half q at k-tile q * KT / 16)
+          static_for<0, 16>([&](auto qc) {
+            constexpr int q = decltype(qc)::value;
+            if constexpr (q * KT / 16 == kt) epi_half(q & 1, q >> 3, (q >> 1) & 3, cv, gs, pk, hv);
+          });
+        }
+        if constexpr (KT >= 16 && (DBG & 64)) {  // chunk c-1's stores and publish in this loop's shadow
+          if constexpr (kt == 8) {
+            if (c > 0) epi_h(hv);
+          }
+          if constexpr (kt >= 9 && kt <= 14) {
+            if (c > 0) epi_cs(c - 1, kt - 9, cv, pk);
+          }
+          if constexpr (kt == 16) {
+            if (c > 0) publish(c - 1);
+          }
+        }
+        // The MFMAs are inline asm, so the compiler knows neither their latency nor that they
+        // still read this k-tile's A fragments after issue: keep those registers allocated to
+        // the end of the k-tile, so no micro-stage result lands in them under an MFMA in
+        // flight (it did: a v_accvgpr_read into SrcA one instruction after the MFMA, wrong h
+        // at H = 128 / 256).
+        asm volatile("" ::"v"(a[kt & 1][0]), "v"(a[kt & 1][1]));
+      });
+      // the epilogue reads the accumulators with VALU: cover the last MFMAs' pipeline
+      // (the compiler pads nothing after inline asm). The accumulators are operands of the
+      // padding, so no read of them (the accp copy, or the drain's cell math at NC = 1) can
+      // be scheduled above it: the compiler sees an inline-asm MFMA's result as ready at
+      // once and had put v_accvgpr_reads 2 instructions behind the last MFMAs (tools/mfma_war.py).
+      asm volatile("s_nop 7\n\ts_nop 7"
+                   : "+a"(acc[0][0]), "+a"(acc[0][1]), "+a"(acc[0][2]), "+a"(acc[0][3]), "+a"(acc[1][0]),
+                     "+a"(acc[1][1]), "+a"(acc[1][2]), "+a"(acc[1][3])
+                   :
+                   : "memory");
+      if constexpr ((DBG & 16) != 0) {  // MFMA completion: consume a result before stamping
+        float sink = acc[1][3][3];
+        asm volatile("" ::"v"(sink));
+        stamp(t, 4 + 5 * c);
+      }
+      if constexpr (KT >= 16 && (DBG & 64)) {
+        if (c > 0) rotate(cv);
+      } else if (c > 0) {
+        epi_store(c - 1, cv, pk, hv);
+        stamp(t, 5 + 5 * c);
+        publish(c - 1);
+      }
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) accp[i][j] = acc[i][j];
+      stamp(t, 6 + 5 * c);
+    };
+    using S0 = std::integral_constant<int, 0>;
+    using S1 = std::integral_constant<int, 1>;
+    using S2 = std::integral_constant<int, 2>;
+    using NF = std::false_type;
+    if constexpr (PF01) {
+      chunk(0, S0{}, std::true_type{});
+      for (int c = 1; c < NC; c += 3) {
+        chunk(c, S1{}, NF{});
+        if (c + 1 < NC) chunk(c + 1, S2{}, NF{});
+        if (c + 2 < NC) chunk(c + 2, S0{}, NF{});
+      }
+    } else {
+      for (int c = 0; c < NC; c += 3) {
+        chunk(c, S0{}, NF{});
+        if (c + 1 < NC) chunk(c + 1, S1{}, NF{});
+        if (c + 2 < NC) chunk(c + 2, S2{}, NF{});
+      }
+    }
+    {  // drain: the last chunk's epilogue
+      float cv[2][4];
+      unsigned pk[2][8], hv[2][4];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) epi_elem(e >> 2, e & 3, cv, pk, hv);
+      epi_store(NC - 1, cv, pk, hv);
+      publish(NC - 1);
+    }
+  }
+  // completion count: every workgroup that ran all T steps adds T to DONE; any early exit
+  // leaves DONE short of EXPECT, which the host check reports even when no spin bound tripped
+  if (threadIdx.x == 0) pguard_done(stat, (unsigned)d.T);
+}
+
+template <int KT, int NC>
+static int launch_pf(bf16_t* XH, const bf16_t* Wp, float* Cst, bf16_t* S, unsigned* sync, unsigned* stat, int grid,
+                     LstmDims d, hipStream_t s) {
+  const void* f = reinterpret_cast<const void*>(&lstm_fwd_persistent_kernel<KT, NC>);
+#ifdef WF_DIAG  // timing-only diagnostic builds (WELLFLOW_PF_DBG >= 2; WELLFLOW_DIAG_BUILD=1)
+  if constexpr (KT == 18 && NC == 8) {
+    if (d.dbg == 2) f = reinterpret_cast<const void*>(&lstm_fwd_persistent_kernel<KT, NC, 2>);
+    if (d.dbg == 4) f = reinterpret_cast<const void*>(&lstm_fwd_persistent_kernel<KT, NC, 4>);
+    if (d.dbg == 14) f = reinterpret_cast<const void*>(&lstm_fwd_persistent_kernel<KT, NC, 14>);
+    if (d.dbg == 16) f = reinterpret_cast<const void*>(&lstm_fwd_persistent_kernel<KT, NC, 16>);
+    if (d.dbg == 48) f = reinterpret_cast<const void*>(&lstm_fwd_persistent_kernel<KT, NC, 48>);
+    if (d.dbg == 64) f = reinterpret_cast<const void*>(&lstm_fwd_persistent_kernel<KT, NC, 64>);  // stores inside the loop
+    if (d.dbg == 1024) f = reinterpret_cast<const void*>(&lstm_fwd_persistent_kernel<KT, NC, 1024>);  // chunk 1 at the step top
+    if (d.dbg == 512) f = reinterpret_cast<const void*>(&lstm_fwd_persistent_kernel<KT, NC, 512>);  // pinned micro-stages
+    if (d.dbg == 128) f = reinterpret_cast<const void*>(&lstm_fwd_persistent_kernel<KT, NC, 128>);  // half-element epilogue
+  }
+#endif
+  void* args[] = {&XH, &Wp, &Cst, &S, &sync, &stat, &d};
+  return persistent_launch(f, grid, args, s);  // persistent_launch.h: residency check + plain launch
+}
+
+}  // namespace wf

@@ -114,6 +114,45 @@ class LSTMRegressor(nn.Module):
             self.head.bias.copy_(b_out)
 
 
+# completion STAT block at the end of every persistent sync buffer (csrc/persistent_guard.h)
+PSTAT_WORDS = 64
+_PST_STICKY, _PST_DONE, _PST_EXPECT, _PST_STARTED, _PST_EXPECT_WG, _PST_EXITS, _PST_LAUNCHES = range(7)
+_PST_REC = 8
+_EXIT_REASONS = {1: "the launch's error word was set while it polled (another workgroup's spin bound)",
+                 2: "its own hand-off spin bound tripped",
+                 3: "wave 0 read a hand-off flag != 1 from LDS although its own poll succeeded",
+                 4: "a wave read a hand-off flag != 1 from LDS"}
+
+
+def persistent_sync_buffer(B: int, row_quantum: int, device) -> torch.Tensor:
+    """int32 sync buffer of a persistent LSTM kernel for batches <= B: the per-launch block
+    (error word + one arrival counter per row block of ``row_quantum`` rows, zeroed by the
+    launcher) and the STAT block of running completion totals at its end."""
+    return torch.zeros(16 + 16 * (B // row_quantum + 1) + PSTAT_WORDS, dtype=torch.int32, device=device)
+
+
+def decode_pstat(words) -> dict:
+    """STAT block (list of 64 ints) -> named totals + the first early-exit record."""
+    w = [int(v) & 0xFFFFFFFF for v in words]
+    rec = None
+    if w[_PST_REC - 1]:
+        r = w[_PST_REC : _PST_REC + 8]
+        rec = {"block": r[0], "step": r[1], "reason": r[2], "why": _EXIT_REASONS.get(r[2], "?"),
+               "err_seen": r[3], "arrivals_seen": r[4], "target": r[5], "flag": r[6], "started_ordinal": r[7]}
+    return {"sticky": w[_PST_STICKY], "done": w[_PST_DONE], "expect": w[_PST_EXPECT], "started": w[_PST_STARTED],
+            "expect_wg": w[_PST_EXPECT_WG], "exits": w[_PST_EXITS], "launches": w[_PST_LAUNCHES], "first_exit": rec}
+
+
+def pstat_error(st: dict) -> int:
+    """0 = every launch since the reset completed; bit 0 spin bound tripped, bit 1 short
+    step count, bit 2 workgroups that never started, bit 3 early exits recorded."""
+    e = 1 if st["sticky"] else 0
+    e |= 2 if st["done"] != st["expect"] else 0
+    e |= 4 if st["started"] != st["expect_wg"] else 0
+    e |= 8 if st["exits"] else 0
+    return e
+
+
 def init_lstm_flat(n_features: int, hidden: int, seed: int = 0) -> torch.Tensor:
     """PyTorch-default init (U(-1/sqrt(H), 1/sqrt(H))) in the flat layout."""
     g = torch.Generator().manual_seed(seed)
@@ -173,12 +212,12 @@ class NativeLSTM:
         # launch with the gate weights resident in registers; falls back to the per-step
         # kernels (fwd_variant) when the shape / device cannot host it
         self.persistent = os.environ.get("WELLFLOW_PERSISTENT", "1") != "0"
-        self.sync = torch.zeros(16 + 16 * (B // 32 + 1), dtype=torch.int32, device=dev)
+        self.sync = persistent_sync_buffer(B, 32, dev)
         self.last_forward_persistent = False
         # persistent backward (csrc/lstm_persistent_bwd.hip): steps T-2..0 in ONE launch,
         # W_hh^T in registers, dc carry in LDS; per-step kernels (bwd_variant) otherwise
         self.persistent_bwd = os.environ.get("WELLFLOW_PERSISTENT_BWD", "1") != "0"
-        self.sync_bwd = torch.zeros(16 + 16 * (B // 64 + 1), dtype=torch.int32, device=dev)
+        self.sync_bwd = persistent_sync_buffer(B, 64, dev)
         self.dw_ksplit = 0  # 0 = heuristic
         # timesteps per overlapped dW GEMM chunk; 0 = serial dW at the end (measured faster:
         # the BPTT chain already fills every CU, overlapping only adds contention)
@@ -228,34 +267,46 @@ class NativeLSTM:
             C.lstm_forward(self.XH, self.Wp, self.Cst, self.S, *self._dims(B), self.fwd_variant)
         self.last_forward_persistent = bool(ok)
 
+    def persistent_stats(self) -> dict:
+        """Running completion totals of the persistent forward / backward since the last
+        :meth:`reset_device_errors` (csrc/persistent_guard.h; one host sync)."""
+        w = torch.stack([self.sync[-PSTAT_WORDS:], self.sync_bwd[-PSTAT_WORDS:]]).cpu().tolist()
+        return {"forward": decode_pstat(w[0]), "backward": decode_pstat(w[1])}
+
     def persistent_error(self) -> int:
-        """Sticky spin-timeout flags of the persistent forward (bit 0) and backward (bit 1),
-        set by ANY launch since the last :meth:`reset_device_errors` (one host sync)."""
-        w = torch.stack([self.sync[:4], self.sync_bwd[:4]]).cpu().tolist()
-        # bit 0 / 1: sticky spin timeout; bit 2 / 3: the LAST launch's workgroups completed fewer
-        # steps than launched (word 2 < word 3: an early exit that tripped no spin bound)
-        e = (1 if w[0][0] else 0) | (2 if w[1][0] else 0)
-        e |= (4 if w[0][3] and w[0][2] != w[0][3] else 0) | (8 if w[1][3] and w[1][2] != w[1][3] else 0)
-        return e
+        """Bits 0-3: forward, bits 4-7: backward (:func:`pstat_error`) — covers EVERY launch and
+        sub-batch since the last :meth:`reset_device_errors`, not only the last one."""
+        st = self.persistent_stats()
+        return pstat_error(st["forward"]) | (pstat_error(st["backward"]) << 4)
 
     def reset_device_errors(self) -> None:
-        self.sync[0] = 0
-        self.sync_bwd[0] = 0
+        self.sync[-PSTAT_WORDS:].zero_()
+        self.sync_bwd[-PSTAT_WORDS:].zero_()
 
     def check_device_errors(self) -> None:
-        """Raise if a persistent kernel's hand-off wait timed out in any step so far (its
-        workgroups drained early: the state of that step is garbage)."""
-        e = self.persistent_error()
-        if e:
-            parts = [n for b, n in ((1, "forward"), (2, "backward")) if e & b]
-            short = [n for b, n in ((4, "forward"), (8, "backward")) if e & b]
-            what = []
-            if parts:
-                what.append(f"{' and '.join(parts)} hit the hand-off spin bound (a workgroup never arrived: "
-                            "non-resident grid or a hung wave)")
-            if short:
-                what.append(f"{' and '.join(short)} workgroups exited before completing every step")
-            raise RuntimeError(f"persistent LSTM {'; '.join(what)}; results of the affected steps are invalid")
+        """Raise if any persistent launch since the last reset left work undone (a tripped
+        spin bound, an early exit, a short step count or workgroups that never started): the
+        state of the affected steps is garbage."""
+        st = self.persistent_stats()
+        bad = {k: v for k, v in st.items() if pstat_error(v)}
+        if not bad:
+            return
+        what = []
+        for k, v in bad.items():
+            e = pstat_error(v)
+            parts = []
+            if e & 1:
+                parts.append("hit the hand-off spin bound (a workgroup never arrived: non-resident grid or a hung wave)")
+            if e & 2:
+                parts.append(f"completed {v['done']} of {v['expect']} workgroup-steps")
+            if e & 4:
+                parts.append(f"started {v['started']} of {v['expect_wg']} workgroups")
+            if e & 8:
+                parts.append(f"{v['exits']} waves exited early")
+            if v["first_exit"]:
+                parts.append(f"first exit: {v['first_exit']}")
+            what.append(f"{k} ({v['launches']} launches): " + "; ".join(parts))
+        raise RuntimeError("persistent LSTM " + " | ".join(what) + "; results of the affected steps are invalid")
 
     # ------------------------------------------------------------------ passes
     def forward(self, x: torch.Tensor) -> torch.Tensor:

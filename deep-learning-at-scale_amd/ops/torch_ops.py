@@ -24,6 +24,7 @@ from __future__ import annotations
 import torch
 from torch import nn
 
+from ..models.lstm import PSTAT_WORDS, decode_pstat, persistent_sync_buffer, pstat_error
 from .native import gemm, lib
 
 _BF = torch.bfloat16
@@ -164,15 +165,16 @@ def _lstm_fwd(x: torch.Tensor, flat: torch.Tensor, H: int, KX: int) -> tuple[tor
     C.lstm_pack_weights(W.contiguous(), Wp[: lay.G * lay.KA], Wp[lay.G * lay.KA:], H, KX)
     dims = _lstm_dims(B, T, F, KX, H)
     C.lstm_pack_x(x.float().contiguous(), XH, *dims, True)
-    sync = torch.zeros(16 + 16 * (B // 32 + 1), dtype=torch.int32, device=dev)
+    sync = persistent_sync_buffer(B, 32, dev)
     if not C.lstm_forward_persistent(XH, Wp[: lay.G * lay.KA], Cst, S, sync, *dims):
         C.lstm_forward(XH, Wp[: lay.G * lay.KA], Cst, S, *dims, 6)
     pred = torch.empty(B, device=dev)
     base = T * B * lay.KA
     hT = XH[base + KX: base + KX + (B - 1) * lay.KA + H]
     C.head_fwd(hT, lay.KA, B, H, w_out.contiguous(), b_out.contiguous(), None, pred, None, None, 0.0)
-    if int(sync[0].item()):
-        raise RuntimeError("wellflow::lstm_regressor: persistent forward hit its spin bound")
+    if pstat_error(decode_pstat(sync[-PSTAT_WORDS:].tolist())):
+        raise RuntimeError("wellflow::lstm_regressor: persistent forward left work undone "
+                           f"{decode_pstat(sync[-PSTAT_WORDS:].tolist())}")
     return pred, XH, Cst, S, Wp
 
 
@@ -208,12 +210,13 @@ def _lstm_bwd(dpred: torch.Tensor, XH: torch.Tensor, Cst: torch.Tensor, S: torch
     Bp = (B + 15) // 16 * 16
     DG = torch.empty(T * B * lay.G, dtype=_BF, device=dev)
     dcarry = torch.empty(Bp * H, device=dev)
-    sync = torch.zeros(16 + 16 * (B // 64 + 1), dtype=torch.int32, device=dev)
+    sync = persistent_sync_buffer(B, 64, dev)
     ksplit = max(1, min(32, T * B // 16384))
     C.lstm_backward_dw(Wp[lay.G * lay.KA:], XH, Cst, S, DG, dcarry, dy, w_out.contiguous(), gW, *dims, 8, 0,
                        ksplit, sync)
-    if int(sync[0].item()):
-        raise RuntimeError("wellflow::lstm_regressor: persistent backward hit its spin bound")
+    if pstat_error(decode_pstat(sync[-PSTAT_WORDS:].tolist())):
+        raise RuntimeError("wellflow::lstm_regressor: persistent backward left work undone "
+                           f"{decode_pstat(sync[-PSTAT_WORDS:].tolist())}")
     return g
 
 

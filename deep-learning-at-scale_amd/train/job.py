@@ -103,6 +103,7 @@ def run_config(cfg: RunConfig, log=print) -> dict:
         trainer.fit(prepared.train, prepared.val)
     elapsed = time.time() - t0
     test_loss, test_mse = trainer.evaluate(*prepared.test)
+    trainer.check_device()  # running completion totals cover every persistent launch of the job
     say("\nTime elapsed: %f s" % elapsed)  # cnn.py:133 (py3-correct)
     say("Testing set loss: %f" % test_loss)  # cnn.py:134
     result = {
@@ -111,6 +112,9 @@ def run_config(cfg: RunConfig, log=print) -> dict:
         "test_loss": test_loss, "test_mse": test_mse,
         "best_val_loss": trainer.stopper.best, "history": trainer.history.__dict__,
     }
+    if hasattr(eng, "persistent_stats"):  # csrc/persistent_guard.h totals (checked just above)
+        result["persistent"] = {k: {kk: vv for kk, vv in v.items() if kk != "first_exit"}
+                                for k, v in eng.persistent_stats().items()}
     if ctx.is_main and os.environ.get("WELLFLOW_RESULT_JSON"):
         with open(os.environ["WELLFLOW_RESULT_JSON"], "w") as f:
             json.dump(result, f)

@@ -285,7 +285,7 @@ def test_lstm_persistent_backward_matches_per_step(B, H, T):
     res = {}
     for pb in (False, True):
         eng.persistent_bwd = pb
-        eng.sync_bwd[1:].fill_(7)  # the launcher must reset its launch words (word 0 is sticky)
+        eng.sync_bwd[:-64].fill_(7)  # the launcher must reset its per-launch block (the STAT block is kept)
         eng.forward_backward(x, y, grad_scale=1.0 / B)
         torch.cuda.synchronize()
         if pb:
@@ -323,7 +323,7 @@ def test_persistent_timeout_is_sticky_and_raises(monkeypatch):
     torch.cuda.synchronize()
     assert eng.persistent_error() != 0, "a 1-poll spin bound should trip on a 256-workgroup grid"
     monkeypatch.delenv("WELLFLOW_SPIN_LIMIT")
-    eng.forward_backward(x, y, 1.0 / B)  # a clean launch: resets words 1.., keeps word 0
+    eng.forward_backward(x, y, 1.0 / B)  # a clean launch: resets its per-launch block, keeps the STAT block
     torch.cuda.synchronize()
     with pytest.raises(RuntimeError, match="spin bound"):
         eng.check_device_errors()
@@ -342,9 +342,47 @@ def test_persistent_timeout_is_sticky_and_raises(monkeypatch):
 
 
 def test_persistent_completion_counters():
-    """Every persistent launch counts the steps its workgroups completed (sync word 2) against
-    the grid x steps workgroup 0 stores (word 3): equal after a clean forward + backward, and a
-    short count (an early exit that tripped no spin bound) makes check_device_errors raise."""
+    """The persistent kernels keep RUNNING completion totals (csrc/persistent_guard.h): steps
+    done vs grid x steps expected and workgroups started vs launched, over every launch and
+    sub-batch since the last reset. Equal after clean steps; a short count in an EARLIER
+    launch is still caught after later clean launches (round-2 advice: the old per-launch
+    count was erased by the next launch); reset clears it."""
+    from wellflow.data.synth import synth_lstm_batch
+    from wellflow.models.lstm import NativeLSTM, init_lstm_flat
+
+    B, T, F, H = 16384, 8, 16, 512  # two sub-batch launches per pass at H = 512
+    eng = NativeLSTM(F, H, T, B, device=DEV)
+    eng.params.copy_(init_lstm_flat(F, H, seed=0).to(DEV))
+    eng.sync_weights()
+    x, y = synth_lstm_batch(B, T, F, seed=0)
+    x, y = x.to(DEV), y.to(DEV)
+    eng.forward_backward(x, y, 1.0 / B)
+    torch.cuda.synchronize()
+    assert eng.last_forward_persistent and eng.last_backward_persistent
+    st = eng.persistent_stats()
+    fw, bw = st["forward"], st["backward"]
+    assert fw["launches"] == 2 and bw["launches"] == 2, st
+    assert fw["expect"] > 0 and fw["done"] == fw["expect"] and fw["expect"] % T == 0, fw
+    assert bw["expect"] > 0 and bw["done"] == bw["expect"] and bw["expect"] % (T - 1) == 0, bw
+    assert fw["started"] == fw["expect_wg"] and bw["started"] == bw["expect_wg"], st
+    eng.check_device_errors()
+    eng.sync_bwd[-64 + 1] -= T - 1  # one workgroup of this pass "left early"
+    for _ in range(2):  # later clean passes do not erase it
+        eng.forward_backward(x, y, 1.0 / B)
+    torch.cuda.synchronize()
+    assert eng.persistent_stats()["backward"]["launches"] == 6
+    with pytest.raises(RuntimeError, match="backward .*completed"):
+        eng.check_device_errors()
+    eng.reset_device_errors()
+    eng.forward_backward(x, y, 1.0 / B)
+    torch.cuda.synchronize()
+    eng.check_device_errors()
+
+
+def test_persistent_exit_record(monkeypatch):
+    """An early exit leaves a record (block, step, reason, words seen) in the STAT block: with
+    a 1-poll spin bound the first exiting wave says why (its own bound, or the error word
+    another workgroup's bound set)."""
     from wellflow.data.synth import synth_lstm_batch
     from wellflow.models.lstm import NativeLSTM, init_lstm_flat
 
@@ -353,13 +391,12 @@ def test_persistent_completion_counters():
     eng.params.copy_(init_lstm_flat(F, H, seed=0).to(DEV))
     eng.sync_weights()
     x, y = synth_lstm_batch(B, T, F, seed=0)
+    monkeypatch.setenv("WELLFLOW_SPIN_LIMIT", "1")
     eng.forward_backward(x.to(DEV), y.to(DEV), 1.0 / B)
     torch.cuda.synchronize()
-    assert eng.last_forward_persistent and eng.last_backward_persistent
-    fw, bw = eng.sync[:4].tolist(), eng.sync_bwd[:4].tolist()
-    assert fw[3] > 0 and fw[2] == fw[3] and fw[3] % T == 0, fw
-    assert bw[3] > 0 and bw[2] == bw[3] and bw[3] % (T - 1) == 0, bw
-    eng.check_device_errors()
-    eng.sync_bwd[2] -= T - 1  # one workgroup "left early"
-    with pytest.raises(RuntimeError, match="backward workgroups exited before completing"):
-        eng.check_device_errors()
+    monkeypatch.delenv("WELLFLOW_SPIN_LIMIT")
+    fw = eng.persistent_stats()["forward"]
+    assert fw["sticky"] == 1 and fw["exits"] > 0 and fw["done"] < fw["expect"], fw
+    rec = fw["first_exit"]
+    assert rec is not None and rec["reason"] in (1, 2, 4) and 1 <= rec["step"] < T, rec
+    eng.reset_device_errors()

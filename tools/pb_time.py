@@ -45,7 +45,7 @@ for dbg in ("0", "64", "512"):  # correct builds must match the per-step kernels
     torch.cuda.synchronize()
     err = (eng.DG.float() - ref.float()).abs().max().item()
     print(f"check dbg{dbg}: max|dDG| {err:.3g} (scale {ref.float().abs().max().item():.3g}) "
-          f"timeout word {int(eng.sync_bwd[0].item())}", flush=True)
+          f"sticky word {int(eng.sync_bwd[-64].item())}", flush=True)
 dbgs = sys.argv[1].split(",") if len(sys.argv) > 1 else ["0", "1", "2", "4", "8", "16"]
 # variants interleaved over several rounds (a fixed order biases toward the later ones:
 # clocks and caches settle), median per variant

@@ -19,12 +19,12 @@ eng.forward_backward(x.cuda(), y.cuda(), 1.0 / B)
 C, dims = eng._C, eng._dims(B)
 w_out = eng.lay.views(eng.params)[1]
 args = (eng.WhhT, eng.XH, eng.Cst, eng.S, eng.DG, eng.dcarry, eng.dy, w_out, *dims)
-sync = torch.zeros(4096 + 2 * 128 * 256, dtype=torch.int32, device="cuda")
+sync = torch.zeros(4096 + 2 * 128 * 256 + 64, dtype=torch.int32, device="cuda")  # + the STAT block
 os.environ["WELLFLOW_PF_DBG"] = sys.argv[1] if len(sys.argv) > 1 else "32"
 for _ in range(3):
     C.lstm_backward(*args, 8, sync)
 torch.cuda.synchronize()
-st = sync[4096:].view(torch.int64).view(256, 128).cpu().numpy().astype(np.float64) * 10.0  # ns
+st = sync[4096:-64].view(torch.int64).view(256, 128).cpu().numpy().astype(np.float64) * 10.0  # ns
 rel = (st - st[:, 0:1]) / 1000.0  # us from step start
 print("step 10, us since step start (mean / max over 256 workgroups)")
 print(f"{'handoff_done':16s} {rel[:, 1].mean():8.2f} {rel[:, 1].max():8.2f}")

@@ -16,12 +16,12 @@ eng.sync_weights()
 x = torch.randn(B, T, F, device="cuda")
 C, dims = eng._C, eng._dims(B)
 C.lstm_pack_x(x, eng.XH, *dims, True)
-sync = torch.zeros(4096 + 2 * 64 * 256, dtype=torch.int32, device="cuda")
+sync = torch.zeros(4096 + 2 * 64 * 256 + 64, dtype=torch.int32, device="cuda")  # + the STAT block
 os.environ["WELLFLOW_PF_DBG"] = sys.argv[1] if len(sys.argv) > 1 else "16"
 for _ in range(3):
     assert C.lstm_forward_persistent(eng.XH, eng.Wp, eng.Cst, eng.S, sync, *dims)
 torch.cuda.synchronize()
-st = sync[4096:].view(torch.int64).view(256, 64).cpu().numpy().astype(np.float64) * 10.0  # ns
+st = sync[4096:-64].view(torch.int64).view(256, 64).cpu().numpy().astype(np.float64) * 10.0  # ns
 base = st[:, 0:1]
 rel = (st - base) / 1000.0  # us from step start
 names = ["sync_end"] + [f"c{c}_{k}" for c in range(8) for k in ("top", "after_wait", "mfma_done", "epi_done", "published")]

@@ -2,7 +2,7 @@
 early? (Round-2 finding: pinned eval prefetch slots allocated between the epochs of a
 graph-replayed job made the persistent kernels complete only part of their steps.)
 
-Prints the completion counters (sync words 2 / 3 of the forward and backward) for eager
+Prints the running completion totals (csrc/persistent_guard.h) of the forward and backward for eager
 launches and for hipGraph replays, before and after pinning host memory."""
 import sys
 
@@ -22,9 +22,10 @@ x, y = x.cuda(), y.cuda()
 
 def counters(tag):
     torch.cuda.synchronize()
-    fw, bw = eng.sync[:4].tolist(), eng.sync_bwd[:4].tolist()
-    ok = fw[2] == fw[3] and bw[2] == bw[3]
-    print(f"{tag:40s} fwd {fw[2]}/{fw[3]} bwd {bw[2]}/{bw[3]} sticky {fw[0]},{bw[0]} -> {'ok' if ok else 'SHORT'}",
+    st = eng.persistent_stats(); fw, bw = st["forward"], st["backward"]
+    ok = fw["done"] == fw["expect"] and bw["done"] == bw["expect"]
+    print(f"{tag:40s} fwd {fw['done']}/{fw['expect']} bwd {bw['done']}/{bw['expect']} sticky {fw['sticky']},{bw['sticky']} "
+          f"-> {'ok' if ok else 'SHORT'} {fw['first_exit']} {bw['first_exit']}",
           flush=True)
 
 
