@@ -14,6 +14,9 @@ Secondary configs (BASELINE.json:8-10), same JSON contract:
   --model mlp         static 3-layer MLP (F -> 256 -> 256 -> 1), resident batch
   --model mlp_online  dynamic MLP: every step trains on a NEW mini-batch streamed host -> HBM
   --model cnn         the reference's own 1-D CNN (cnn.py:110-118), SGD-Nesterov, 65,536 windows
+The default invocation times all three AFTER the headline's timed region and reports them in
+a nested "secondary" object of the same JSON line (each with its own steps, ms/step, rows/s,
+timed seconds); the headline "value" is the LSTM alone.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B_per_gpu] [--model ...]
 
@@ -53,7 +56,11 @@ def _spawn_ranks(n: int, argv) -> int:
     """Launcher mode: N ranks on this node via torch.distributed.run (127.0.0.1 rendezvous).
     The parent imports nothing GPU-related; each child pins its own GPU (LOCAL_RANK)."""
     env = dict(os.environ)
-    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # dmabuf IPC (RCCL / tensor sharing)
+    # dmabuf IPC: the MI355X hosts of this pool support only dmabuf IPC, and without it RCCL's
+    # and torch's cross-process GPU memory sharing fails with hipIpcGetMemHandle: invalid
+    # argument. The pool exports it already (then setdefault changes nothing); the JSON line
+    # reports the value the ranks ran with.
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
            "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
            os.path.abspath(__file__), *argv]
@@ -97,6 +104,41 @@ def _comm_ms(ctx, buf, iters: int = 20) -> float | None:
     e1.record()
     torch.cuda.synchronize()
     return ctx.max_scalar(e0.elapsed_time(e1) / iters)
+
+
+def _rccl_debug_setup(ctx_rank: int) -> str | None:
+    """Ask RCCL for its INIT/GRAPH log in a per-rank file (before the process group exists;
+    RCCL reads the variables when the communicator is created), so the JSON line can say
+    what RCCL built at this world size: ranks, channels and the transport of each ring hop."""
+    if int(os.environ.get("WORLD_SIZE", "1")) <= 1 or "NCCL_DEBUG_FILE" in os.environ:
+        return None
+    path = f"/tmp/wellflow_rccl.{os.getpid()}.r{ctx_rank}.log"
+    os.environ.setdefault("NCCL_DEBUG", "INFO")
+    os.environ.setdefault("NCCL_DEBUG_SUBSYS", "INIT,GRAPH")
+    os.environ["NCCL_DEBUG_FILE"] = path
+    return path
+
+
+def _rccl_summary(path: str | None) -> dict | None:
+    import re
+    from collections import Counter
+
+    if not path or not os.path.exists(path):
+        return None
+    nranks, chans, via, version = None, set(), Counter(), None
+    with open(path, errors="replace") as f:
+        for line in f:
+            m = re.search(r"nRanks (\d+)", line)
+            if m:
+                nranks = int(m.group(1))
+            m = re.search(r"Channel (\d+)/\d+ :.* via (\S+(?: \S+)?)", line)
+            if m:
+                chans.add(int(m.group(1)))
+                via[m.group(2)] += 1
+            m = re.search(r"(RCCL version \S+)", line)
+            if m and version is None:
+                version = m.group(1)
+    return {"nranks": nranks, "channels": len(chans), "transport": dict(via), "version": version, "log": path}
 
 
 def bench_lstm(args, ctx):
@@ -258,6 +300,46 @@ def bench_mlp(args, ctx, online: bool):
     return el, B, model, run.take_loss() / (B * (args.steps + args.warmup)), run, eng, extra
 
 
+SECONDARY = ("mlp", "mlp_online", "cnn")
+CPU_BATCH = {"lstm": 256, "mlp": 8192, "mlp_online": 8192, "cnn": 1024}
+
+
+def _run_model(args, ctx):
+    if args.model == "lstm":
+        return bench_lstm(args, ctx)
+    if args.model == "cnn":
+        return bench_cnn(args, ctx)
+    return bench_mlp(args, ctx, online=args.model == "mlp_online")
+
+
+def _secondary(args, ctx, models) -> dict:
+    """BASELINE.json:8-10 in the same invocation, AFTER the headline's timed region: each
+    config's own full training step (same StepRunner, same timing bracket: barrier +
+    synchronize on both sides, max over ranks), default per-GPU batch, the headline's
+    steps / warmup. The headline's engine is freed first."""
+    import gc
+
+    import torch
+
+    out = {}
+    for m in models:
+        a = argparse.Namespace(**vars(args))
+        a.model = m
+        a.batch = (CPU_BATCH if ctx.device.type == "cpu" else DEFAULT_BATCH)[m]
+        gc.collect()
+        if ctx.device.type == "cuda":
+            torch.cuda.empty_cache()
+        el, B, desc, loss, run, eng, extra = _run_model(a, ctx)
+        W = ctx.world_size
+        out[m] = {"metric": f"rows/sec (whole node), {m} regression training", "value": round(B * W * a.steps / el, 1),
+                  "unit": "rows/s", "ms_per_step": round(1000.0 * el / max(a.steps, 1), 4), "steps": a.steps,
+                  "warmup": a.warmup, "timed_s": round(el, 4), "per_gpu_batch": B, "global_batch": B * W,
+                  "model": desc, "train_loss": round(loss, 6), "step_graph": bool(run.graphs),
+                  **{k: v for k, v in extra.items() if k.startswith("h2d") or k in ("persistent_fwd",)}}
+        del run, eng
+    return out
+
+
 def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -278,11 +360,23 @@ def main() -> int:
     ap.add_argument("--host-pool", type=int, default=8, help="mlp_online: distinct pinned host batches cycled")
     ap.add_argument("--device", choices=["auto", "cpu"], default="auto",
                     help="cpu: rehearse the launch/timing/JSON contract on the fp32 reference over gloo")
+    ap.add_argument("--secondary", default="auto",
+                    help="comma list of configs timed after the headline (mlp,mlp_online,cnn), 'none'; "
+                         "auto = all three after the default LSTM headline, none otherwise")
     args = ap.parse_args()
     if args.batch is None:
         args.batch = DEFAULT_BATCH[args.model]
         if args.device == "cpu":  # the fp32 CPU rehearsal: N ranks share one host's memory
-            args.batch = {"lstm": 256, "mlp": 8192, "mlp_online": 8192, "cnn": 1024}[args.model]
+            args.batch = CPU_BATCH[args.model]
+    if args.secondary == "auto":
+        default_headline = args.model == "lstm" and (args.batch, args.seq, args.hidden, args.features) == (
+            DEFAULT_BATCH["lstm"] if args.device != "cpu" else CPU_BATCH["lstm"], 64, 512, 16)
+        secondary = list(SECONDARY) if default_headline else []
+    else:
+        secondary = [m for m in args.secondary.split(",") if m and m != "none"]
+        bad = [m for m in secondary if m not in SECONDARY]
+        if bad:
+            ap.error(f"--secondary: unknown {bad}")
 
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
         return _spawn_ranks(args.gpus, sys.argv[1:])
@@ -295,6 +389,7 @@ def main() -> int:
         # never fall back silently: a CPU number is not the benchmark
         print("bench.py: no GPU visible (use --device cpu for the contract rehearsal)", file=sys.stderr)
         return 2
+    rccl_log = _rccl_debug_setup(int(os.environ.get("RANK", "0"))) if args.device != "cpu" else None
     ctx = DistContext.from_env(device="cpu" if args.device == "cpu" else None)
     cpu = ctx.device.type == "cpu"
     if ctx.world_size != args.gpus:
@@ -302,13 +397,12 @@ def main() -> int:
         ctx.shutdown()
         return 2
     torch.manual_seed(1234 + ctx.rank)
-    if args.model == "lstm":
-        elapsed, B, model, loss, run, eng, extra = bench_lstm(args, ctx)
-    elif args.model == "cnn":
-        elapsed, B, model, loss, run, eng, extra = bench_cnn(args, ctx)
-    else:
-        elapsed, B, model, loss, run, eng, extra = bench_mlp(args, ctx, online=args.model == "mlp_online")
+    elapsed, B, model, loss, run, eng, extra = _run_model(args, ctx)
     comm = _comm_ms(ctx, eng.grads)
+    grad_mb = round(eng.grads.numel() * 4 / 2**20, 3)
+    step_graph, comm_in_graph = bool(run.graphs), bool(run.captured_comm)
+    del run, eng
+    sec = _secondary(args, ctx, secondary) if secondary else None
 
     W = ctx.world_size
     if ctx.is_main:
@@ -347,12 +441,18 @@ def main() -> int:
             "backend": ctx.backend or ("none" if W == 1 else None),
             "rccl_version": rccl,
             "comm_ms": None if comm is None else round(comm, 4),
-            "grad_bucket_mb": round(eng.grads.numel() * 4 / 2**20, 3),
-            "step_graph": bool(run.graphs),
-            "comm_in_graph": bool(run.captured_comm),
+            "grad_bucket_mb": grad_mb,
+            "step_graph": step_graph,
+            "comm_in_graph": comm_in_graph,
             "train_loss": round(loss, 6),  # mean over the run
+            "timed_s": round(elapsed, 4),
             **extra,
         }
+        if W > 1 and not cpu:
+            rec["rccl"] = _rccl_summary(rccl_log)
+            rec["hsa_enable_ipc_mode_legacy"] = os.environ.get("HSA_ENABLE_IPC_MODE_LEGACY")
+        if sec is not None:
+            rec["secondary"] = sec
         print(json.dumps(rec), flush=True)
     ctx.shutdown()
     return 0

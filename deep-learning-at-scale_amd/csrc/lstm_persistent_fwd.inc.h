@@ -90,6 +90,7 @@ __global__ __launch_bounds__(256, 1) void lstm_fwd_persistent_kernel(
   // h_t staging [32][64] bf16, accessed only through inline asm (32-bit LDS address)
   const unsigned hb_lds = (unsigned)(uintptr_t)((__attribute__((address_space(3))) char*)(smem + HOFF));
   const unsigned flag_lds = (unsigned)(uintptr_t)((__attribute__((address_space(3))) char*)(smem + FOFF));
+  const unsigned lds_smem = (unsigned)(uintptr_t)((__attribute__((address_space(3))) char*)smem);
 
   constexpr int H = KA - 64, G = 4 * H, NB = G / 256, HB = H / 16;  // KX = 64 (host-checked)
   const int Bp = fn_rows(d.B);
@@ -442,7 +443,15 @@ __global__ __launch_bounds__(256, 1) void lstm_fwd_persistent_kernel(
       if constexpr (!FIRST) {
         if (c + 2 < NC) issue(c + 2, std::integral_constant<int, (P + 2) % 3>{});
       }
-      const char* cur = smem + P * SLOT;
+      // A fragment reads through asm with COUNTED waits: as C++ loads, the compiler's waitcnt
+      // pass put lgkmcnt(0) before every k-tile pair, so each wait also drained the reads of
+      // the NEXT k-tile issued just before it (9 exposed LDS latencies per chunk). Here the
+      // reads of k-tile kt + 1 are issued at the top of kt and kt waits with lgkmcnt(2): LDS
+      // returns in order, so everything but those 2 youngest reads has landed. The wait takes
+      // kt's fragments as "+v" operands, so no use of them moves above it. Per-chunk bases
+      // (ring slot + lane offset): the slot offset does not fit the 16-bit ds offset field.
+      const unsigned ab[2] = {lds_smem + (unsigned)(P * SLOT) + (unsigned)fa[0],
+                              lds_smem + (unsigned)(P * SLOT) + (unsigned)fa[1]};
 
       f32x4 acc[2][4];  // written first by k-tile 0's MFMAs (src C = 0: no zeroing writes)
       // MFMAs in inline asm with explicit register classes: weights of k-tiles < KTA as AGPR
@@ -530,8 +539,8 @@ __global__ __launch_bounds__(256, 1) void lstm_fwd_persistent_kernel(
 #undef WF_MF
 #undef WF_UNP
       };
-#pragma unroll
-      for (int i = 0; i < 2; ++i) a[0][i] = *reinterpret_cast<const bf16x8*>(cur + i * 2048 + fa[0]);
+      asm volatile("ds_read_b128 %0, %1" : "=v"(a[0][0]) : "v"(ab[0]) : "memory");
+      asm volatile("ds_read_b128 %0, %1 offset:2048" : "=v"(a[0][1]) : "v"(ab[0]) : "memory");
       if constexpr ((DBG & 32) != 0) {
         a[1][0] = a[0][0];
         a[1][1] = a[0][1];
@@ -539,10 +548,14 @@ __global__ __launch_bounds__(256, 1) void lstm_fwd_persistent_kernel(
       static_for<0, KT>([&](auto kc) {
         constexpr int kt = decltype(kc)::value;
         if constexpr (kt + 1 < KT && !(DBG & 32)) {  // DBG & 32: timing only, no fragment reads
-#pragma unroll
-          for (int i = 0; i < 2; ++i)
-            a[(kt + 1) & 1][i] =
-                *reinterpret_cast<const bf16x8*>(cur + ((kt + 1) >> 1) * 4096 + i * 2048 + fa[(kt + 1) & 1]);
+          constexpr int o = ((kt + 1) >> 1) * 4096;
+          asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(a[(kt + 1) & 1][0]) : "v"(ab[(kt + 1) & 1]), "i"(o)
+                       : "memory");
+          asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(a[(kt + 1) & 1][1]) : "v"(ab[(kt + 1) & 1]),
+                       "i"(o + 2048) : "memory");
+          asm volatile("s_waitcnt lgkmcnt(2)" : "+v"(a[kt & 1][0]), "+v"(a[kt & 1][1]) :: "memory");
+        } else {
+          asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(a[kt & 1][0]), "+v"(a[kt & 1][1]) :: "memory");
         }
         static_for<0, 8>([&](auto mc) {
           constexpr int i = decltype(mc)::value >> 2, j = decltype(mc)::value & 3;

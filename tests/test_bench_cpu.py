@@ -84,3 +84,18 @@ def test_bench_refuses_without_gpu():
     r = subprocess.run([sys.executable, "bench.py", "--steps", "1", "--warmup", "0"], capture_output=True,
                        text=True, env=env, cwd=ROOT, timeout=300)
     assert r.returncode == 2 and not r.stdout.strip()
+
+
+def test_bench_secondary_configs_dp2():
+    """BASELINE.json:8-10 ride in the headline's JSON line: a nested "secondary" object, one
+    entry per config with its own steps, ms/step, rows/s (whole-job aggregate) and timed
+    seconds; the headline value stays the LSTM's."""
+    B = 4
+    rec = _run(2, "lstm", ["--batch", str(B), "--seq", "6", "--hidden", "16", "--secondary", "mlp,mlp_online,cnn"])
+    assert rec["value"] == pytest.approx(B * 2 / (rec["ms_per_step"] / 1000.0), rel=1e-3)
+    sec = rec["secondary"]
+    assert set(sec) == {"mlp", "mlp_online", "cnn"}
+    for m, v in sec.items():
+        assert v["steps"] == 3 and v["warmup"] == 1 and v["global_batch"] == 2 * v["per_gpu_batch"]
+        assert v["value"] == pytest.approx(v["global_batch"] / (v["ms_per_step"] / 1000.0), rel=1e-3), (m, v)
+        assert v["timed_s"] == pytest.approx(v["ms_per_step"] * 3 / 1000.0, rel=1e-2)
