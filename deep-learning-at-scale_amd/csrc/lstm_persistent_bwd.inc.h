@@ -428,25 +428,36 @@ __global__ __launch_bounds__(256, 1) void lstm_bwd_persistent_kernel(
 
       f32x4 acc[4];  // written first by k-tile 0's MFMAs (src C = 0)
       f32x4 pr[4];
-      bf16x8 a[2];
+      // A fragments two k-tiles ahead (3-register ring): with one ahead (4 MFMAs, ~64 cycles)
+      // the ds_read latency under the concurrent LDS-DMA traffic was partly exposed at every
+      // k-tile. LDS returns in order; the waits count the reads younger than k-tile kt's:
+      // r_{kt+1}, r_{kt+2} and, at kt = 1, the 3 partial-sum reads issued at the end of kt = 0
+      // (RT > 0); k-tile KSUM waits for those partials too (they are summed there).
+      bf16x8 a[3];
       asm volatile("ds_read_b128 %0, %1" : "=v"(a[0]) : "v"(cur + fa[0]) : "memory");
+      if constexpr (KT > 1 && (DBG & 4096) == 0)
+        asm volatile("ds_read_b128 %0, %1" : "=v"(a[1]) : "v"(cur + fa[1]) : "memory");
       static_for<0, KT>([&](auto kc) {
         constexpr int kt = decltype(kc)::value;
         (void)acc;  // odr-use outside the asm operands: clang does not capture them implicitly
         (void)w;
         (void)pr;
-        if constexpr (kt + 1 < KT)
+        // A/B (WELLFLOW_PF_DBG=4096, production-correct): the round-2 one-ahead prefetch
+        constexpr int AHEAD = (DBG & 4096) ? 1 : 2;
+        if constexpr (kt + AHEAD < KT)
           asm volatile("ds_read_b128 %0, %1 offset:%2"
-                       : "=v"(a[(kt + 1) & 1])
-                       : "v"(cur + fa[(kt + 1) & 1]), "i"(((kt + 1) >> 1) * 2048)
+                       : "=v"(a[(kt + AHEAD) % 3])
+                       : "v"(cur + fa[(kt + AHEAD) & 1]), "i"(((kt + AHEAD) >> 1) * 2048)
                        : "memory");
-        if constexpr (kt + 1 < KT)
-          asm volatile("s_waitcnt lgkmcnt(1)" ::: "memory");
-        else
-          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        if constexpr (RT > 0 && kt == 1) {
-          // the wait above drained the partial reads issued at k-tile 0 (LDS returns in order):
-          // tie them to it, then the previous tile's dh
+        // k-tile whose top sums the partials: 2, or 1 where the cell backward's first use of dh
+        // (micro-stage 7) already falls into k-tile 1 (KT = 4, H = 128)
+        constexpr int KSUM = (KT >= 8 && AHEAD == 2) ? 2 : 1;
+        constexpr int YOUNGER = (kt + 1 < KT ? 1 : 0) + (AHEAD == 2 && kt + 2 < KT ? 1 : 0) +
+                                (RT > 0 && kt == 1 && KSUM == 2 ? 3 : 0);
+        asm volatile("s_waitcnt lgkmcnt(%0)" ::"n"(YOUNGER) : "memory");
+        if constexpr (RT > 0 && kt == KSUM) {
+          // the wait above drained the partial reads issued at k-tile 0 (LDS returns in order:
+          // only the fragment reads after them are younger): tie them to it, then the previous tile's dh
           asm volatile("" : "+v"(pr[0]), "+v"(pr[1]), "+v"(pr[2]), "+v"(pr[3]));
           dhp = dho + ((pr[0] + pr[1]) + (pr[2] + pr[3]));
         }
@@ -454,9 +465,9 @@ __global__ __launch_bounds__(256, 1) void lstm_bwd_persistent_kernel(
           constexpr int j = decltype(jc)::value;
           if constexpr (!(DBG & 2)) {
             if constexpr (kt == 0)
-              asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, 0" : "=&v"(acc[j]) : "v"(a[kt & 1]), "a"(w[kt][j]));
+              asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, 0" : "=&v"(acc[j]) : "v"(a[kt % 3]), "a"(w[kt][j]));
             else
-              asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+v"(acc[j]) : "v"(a[kt & 1]), "a"(w[kt][j]));
+              asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+v"(acc[j]) : "v"(a[kt % 3]), "a"(w[kt][j]));
           }
           if constexpr (MICRO && RT > 0) {
             // stage instances [qlo, qhi) after MFMA slot m, from k-tile 1 on (dh of the
@@ -507,7 +518,7 @@ __global__ __launch_bounds__(256, 1) void lstm_bwd_persistent_kernel(
         // the MFMAs above are inline asm, so the compiler knows neither their latency nor that
         // they still read this fragment: keep its registers allocated until here, so no VALU
         // result of the interleaved epilogue can land in them while the MFMAs are in flight
-        asm volatile("" ::"v"(a[kt & 1]));
+        asm volatile("" ::"v"(a[kt % 3]));
       });
       (void)kt_of_part;
       // parts that did not fit a short loop
@@ -564,6 +575,9 @@ template <int KT, int NRT>
 static int launch_pb(const bf16_t* WhhT, const float* Cst, const bf16_t* S, bf16_t* DG, const float* dcarry,
                       unsigned* sync, unsigned* stat, int grid, LstmDims d, hipStream_t s) {
   const void* f = reinterpret_cast<const void*>(&lstm_bwd_persistent_kernel<KT, NRT>);
+  if constexpr (KT == 16 && NRT == 16) {  // production-correct A/B variants (WELLFLOW_PF_DBG)
+    if (d.dbg == 4096) f = reinterpret_cast<const void*>(&lstm_bwd_persistent_kernel<KT, NRT, 4096>);
+  }
 #ifdef WF_DIAG  // timing-only diagnostic builds (WELLFLOW_PF_DBG; WELLFLOW_DIAG_BUILD=1)
   if constexpr (KT == 16 && NRT == 16) {
     switch (d.dbg) {

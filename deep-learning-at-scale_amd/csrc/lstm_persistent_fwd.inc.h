@@ -539,22 +539,33 @@ __global__ __launch_bounds__(256, 1) void lstm_fwd_persistent_kernel(
 #undef WF_MF
 #undef WF_UNP
       };
-      asm volatile("ds_read_b128 %0, %1" : "=v"(a[0][0]) : "v"(ab[0]) : "memory");
-      asm volatile("ds_read_b128 %0, %1 offset:2048" : "=v"(a[0][1]) : "v"(ab[0]) : "memory");
+      // A/B (WELLFLOW_PF_DBG=4096, production-correct): the round-2 C++ fragment loads
+      constexpr bool CXX_FRAG = (DBG & 4096) != 0;
+      if constexpr (CXX_FRAG) {
+        for (int i = 0; i < 2; ++i) a[0][i] = *reinterpret_cast<const bf16x8*>(smem + P * SLOT + i * 2048 + fa[0]);
+      } else {
+        asm volatile("ds_read_b128 %0, %1" : "=v"(a[0][0]) : "v"(ab[0]) : "memory");
+        asm volatile("ds_read_b128 %0, %1 offset:2048" : "=v"(a[0][1]) : "v"(ab[0]) : "memory");
+      }
       if constexpr ((DBG & 32) != 0) {
         a[1][0] = a[0][0];
         a[1][1] = a[0][1];
       }
       static_for<0, KT>([&](auto kc) {
         constexpr int kt = decltype(kc)::value;
-        if constexpr (kt + 1 < KT && !(DBG & 32)) {  // DBG & 32: timing only, no fragment reads
+        if constexpr (CXX_FRAG) {
+          if constexpr (kt + 1 < KT)
+            for (int i = 0; i < 2; ++i)
+              a[(kt + 1) & 1][i] = *reinterpret_cast<const bf16x8*>(smem + P * SLOT + ((kt + 1) >> 1) * 4096 +
+                                                                     i * 2048 + fa[(kt + 1) & 1]);
+        } else if constexpr (kt + 1 < KT && !(DBG & 32)) {  // DBG & 32: timing only, no fragment reads
           constexpr int o = ((kt + 1) >> 1) * 4096;
           asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(a[(kt + 1) & 1][0]) : "v"(ab[(kt + 1) & 1]), "i"(o)
                        : "memory");
           asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(a[(kt + 1) & 1][1]) : "v"(ab[(kt + 1) & 1]),
                        "i"(o + 2048) : "memory");
           asm volatile("s_waitcnt lgkmcnt(2)" : "+v"(a[kt & 1][0]), "+v"(a[kt & 1][1]) :: "memory");
-        } else {
+        } else if constexpr (!CXX_FRAG) {
           asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(a[kt & 1][0]), "+v"(a[kt & 1][1]) :: "memory");
         }
         static_for<0, 8>([&](auto mc) {
@@ -685,6 +696,9 @@ template <int KT, int NC>
 static int launch_pf(bf16_t* XH, const bf16_t* Wp, float* Cst, bf16_t* S, unsigned* sync, unsigned* stat, int grid,
                      LstmDims d, hipStream_t s) {
   const void* f = reinterpret_cast<const void*>(&lstm_fwd_persistent_kernel<KT, NC>);
+  if constexpr (KT == 18 && NC == 8) {  // production-correct A/B variants (WELLFLOW_PF_DBG)
+    if (d.dbg == 4096) f = reinterpret_cast<const void*>(&lstm_fwd_persistent_kernel<KT, NC, 4096>);
+  }
 #ifdef WF_DIAG  // timing-only diagnostic builds (WELLFLOW_PF_DBG >= 2; WELLFLOW_DIAG_BUILD=1)
   if constexpr (KT == 18 && NC == 8) {
     if (d.dbg == 2) f = reinterpret_cast<const void*>(&lstm_fwd_persistent_kernel<KT, NC, 2>);
