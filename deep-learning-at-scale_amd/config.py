@@ -27,7 +27,9 @@ MODEL_DEFAULTS = {
                 nesterov=True, batch_size=20, epochs=1000, patience=10),
     "mlp": dict(loss="mse", optimizer="adam", lr=1e-3, batch_size=256, epochs=200, patience=10),
     "mlp_online": dict(loss="mse", optimizer="adam", lr=1e-3, batch_size=256, epochs=50, patience=5),
-    "lstm": dict(loss="mse", optimizer="adam", lr=1e-3, batch_size=256, epochs=100, patience=10),
+    # batch_size 0 = auto: on the native GPU engine, the rows that fill one co-resident
+    # persistent grid (NativeLSTM.full_grid_batch: 8192 at H = 512 on 256 CUs); 256 otherwise
+    "lstm": dict(loss="mse", optimizer="adam", lr=1e-3, batch_size=0, epochs=100, patience=10),
     "gilbert": dict(loss="mse", epochs=0, batch_size=0),
 }
 
@@ -117,7 +119,8 @@ def build_parser(model: str) -> argparse.ArgumentParser:
     ap.add_argument("--seed", type=int)
     ap.add_argument("--split", type=_tuple_floats)
     ap.add_argument("--epochs", type=int)
-    ap.add_argument("--batch-size", type=int, dest="batch_size")
+    ap.add_argument("--batch-size", type=int, dest="batch_size",
+                    help="per-GPU rows per step (lstm: 0 = auto, sized to fill the GPU)")
     ap.add_argument("--patience", type=int)
     ap.add_argument("--loss", choices=["mse", "mae_clip"])
     ap.add_argument("--clip", type=float)

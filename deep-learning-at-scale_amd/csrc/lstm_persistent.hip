@@ -15,6 +15,10 @@ namespace wf {
 WF_PF_DECL_NC(6)
 WF_PF_DECL_NC(10)
 WF_PF_DECL_NC(18)
+WF_PF_DECL_NC(8)
+WF_PF_DECL_NC(12)
+WF_PF_DECL(20, 1)
+WF_PF_DECL(20, 8)
 
 namespace {
 constexpr int PF_ROWS = 32;  // rows per ring chunk (lstm_persistent_fwd.inc.h)
@@ -34,6 +38,12 @@ int launch_pf_variant(int KT, int NC, bf16_t* XH, const bf16_t* Wp, float* Cst, 
     WF_PF_CASE(6)
     WF_PF_CASE(10)
     WF_PF_CASE(18)
+    WF_PF_CASE(8)
+    WF_PF_CASE(12)
+    case 20:
+      if (NC == 1) return launch_pf_20_1(XH, Wp, Cst, S, sync, stat, grid, d, s);
+      if (NC == 8) return launch_pf_20_8(XH, Wp, Cst, S, sync, stat, grid, d, s);
+      return 0;
     default: return 0;
   }
 #undef WF_PF_CASE
@@ -52,13 +62,15 @@ long lstm_persistent_sync_total(int row_blocks) { return lstm_persistent_sync_wo
 // Batch split for the persistent schedules: the fewest equal sub-batches (launched one after
 // the other on the stream, each a full persistent launch over its row range, d.row_off) whose
 // grid of `rows_per_unit * units` rows per workgroup fits one workgroup per CU. Returns the
-// number of sub-batches (0 = none fits) and the chosen units per workgroup.
-int persistent_split(int B, int row_quantum, int max_units, int cols, int cus, int* units_out) {
+// number of sub-batches (0 = none fits) and the chosen units per workgroup; bit log2(u) of
+// unit_mask says the variant with u units per workgroup is built.
+int persistent_split(int B, int row_quantum, int max_units, int cols, int cus, int* units_out, unsigned unit_mask) {
   for (int nsub = 1; nsub <= 64; ++nsub) {
     if (B % nsub != 0) continue;
     const int Bs = B / nsub;
     if (Bs % row_quantum != 0) continue;
     for (int u = 1; u <= max_units; u *= 2) {
+      if (((unit_mask >> __builtin_ctz((unsigned)u)) & 1u) == 0) continue;  // variant not built
       if (Bs % (row_quantum * u) == 0 && (Bs / (row_quantum * u)) * cols <= cus) {
         *units_out = u;
         return nsub;
@@ -75,8 +87,9 @@ int launch_lstm_fwd_persistent(bf16_t* XH, const bf16_t* Wp, float* Cst, bf16_t*
                                long sync_words, LstmDims d, hipStream_t s) {
   const int KA = d.KX + d.H, G = 4 * d.H;
   if ((double)d.B * KA * 2 >= 2147483647.0) return 0;  // 32-bit buffer offsets within one timestep slab
-  if (d.KX % 64 != 0 || KA % 64 != 0 || G % 256 != 0 || d.B % PF_ROWS != 0 || d.KX != 64) return 0;
-  if (KA / 32 != 6 && KA / 32 != 10 && KA / 32 != 18) return 0;
+  if (d.KX % 64 != 0 || KA % 64 != 0 || G % 256 != 0 || d.B % PF_ROWS != 0) return 0;
+  if (d.KX != 64 && d.KX != 128) return 0;  // F <= 127
+  if (d.H != 128 && d.H != 256 && d.H != 512) return 0;
   int dev = 0, cus = 0;
   if (hipGetDevice(&dev) != hipSuccess ||
       hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
@@ -84,7 +97,7 @@ int launch_lstm_fwd_persistent(bf16_t* XH, const bf16_t* Wp, float* Cst, bf16_t*
   const int NB = G / 256;
   // fewest sub-batches, then the fewest 32-row chunks per workgroup, one workgroup per CU
   int NC = 0;
-  const int nsub = persistent_split(d.B, PF_ROWS, 8, NB, cus, &NC);
+  const int nsub = persistent_split(d.B, PF_ROWS, 8, NB, cus, &NC, KA / 32 == 20 ? 0x9u : 0xFu);
   if (nsub == 0) return 0;
   const int Bs = d.B / nsub, MB = Bs / (PF_ROWS * NC);
   if (sync_words < lstm_persistent_sync_total(MB)) return 0;

@@ -40,7 +40,8 @@ int launch_pb_variant(int KT, int NRT, const bf16_t* WhhT, const float* Cst, con
 }
 }  // namespace
 
-int persistent_split(int B, int row_quantum, int max_units, int cols, int cus, int* units_out);  // lstm_persistent.hip
+int persistent_split(int B, int row_quantum, int max_units, int cols, int cus, int* units_out,
+                     unsigned unit_mask);  // lstm_persistent.hip
 
 // Steps T-2 .. 0 of the backward in one launch per sub-batch (step T-1 must already be done:
 // DG[T-1] and the dc carry written by lstm_bwd_last_kernel). 1 = launched, 0 = the shape /
@@ -62,7 +63,7 @@ int launch_lstm_bwd_persistent(const bf16_t* WhhT, const float* Cst, const bf16_
   // fewest sub-batches, then the fewest row tiles per workgroup (a multiple of 4: the row-tile
   // loop is unrolled by 4; at most PB_MAX_RT: the dc carry lives in registers), one WG per CU
   int u = 0;
-  const int nsub = persistent_split(d.B, 64, PB_MAX_RT / 4, NB, cus, &u);
+  const int nsub = persistent_split(d.B, 64, PB_MAX_RT / 4, NB, cus, &u, 0xFu);
   if (nsub == 0) return 0;
   const int NRT = 4 * u, Bs = d.B / nsub, MB = Bs / (16 * NRT);
   if (sync_words < lstm_persistent_sync_total(MB)) return 0;

@@ -68,11 +68,13 @@ __global__ __launch_bounds__(256, 1) void lstm_fwd_persistent_kernel(
   constexpr int LPT = KS;                    // LDS-DMA instructions per wave per chunk
   // k-tiles whose weight fragments live in AGPRs (the rest in VGPRs): 256 AGPRs minus 2 x 32
   // accumulator registers (this chunk + the pipelined previous one) = 12 k-tiles x 4 x 4
-  constexpr int KTA = KT < 12 ? KT : 12;
+  // KT = 20 (KX = 128, H = 512): 14 k-tiles in AGPRs (224 + the 32 accumulators = 256), so
+  // the VGPR-resident weights stay at 6 k-tiles as at KT = 18
+  constexpr int KTA = KT < 12 ? KT : (KT >= 20 ? 14 : 12);
   constexpr int NSTORE = (DBG & 4) ? 1 : 7;  // stores per wave per chunk: 2 C, 4 S, 1 h
   // one asm statement per MFMA + cell-math micro-stage (H = 512; WELLFLOW_PF_DBG=512: pinned
   // C++ micro-stages instead, for A/B)
-  constexpr bool FUSED = KT == 18 && (DBG & (2 | 128 | 512)) == 0;
+  constexpr bool FUSED = KT >= 18 && (DBG & (2 | 128 | 512)) == 0;  // slots >= 144: plain MFMAs
   // the step top issues only chunk 0's pieces, so chunk 0 starts sooner after the hand-off
   // (every workgroup of the grid fetches its first chunks at once there); chunk 0 issues
   // chunks 1 and 2 from its MFMA loop (WELLFLOW_PF_DBG=1024: both at the step top, A/B)
@@ -92,7 +94,11 @@ __global__ __launch_bounds__(256, 1) void lstm_fwd_persistent_kernel(
   const unsigned flag_lds = (unsigned)(uintptr_t)((__attribute__((address_space(3))) char*)(smem + FOFF));
   const unsigned lds_smem = (unsigned)(uintptr_t)((__attribute__((address_space(3))) char*)smem);
 
-  constexpr int H = KA - 64, G = 4 * H, NB = G / 256, HB = H / 16;  // KX = 64 (host-checked)
+  // KX (x block + bias column, padded) = 64 for F <= 63, 128 for F <= 127; KT = KA / 32 tells
+  // them apart for H in {128, 256, 512}: 6 / 10 / 18 at KX = 64, 8 / 12 / 20 at KX = 128
+  constexpr int KXC = (KT == 8 || KT == 12 || KT == 20) ? 128 : 64;
+  constexpr int H = KA - KXC, G = 4 * H, NB = G / 256, HB = H / 16;
+  static_assert(H == 128 || H == 256 || H == 512, "KT must encode (KX, H)");
   const int Bp = fn_rows(d.B);
   const int lane = threadIdx.x & 63, l15 = lane & 15, g = lane >> 4;
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -217,7 +223,7 @@ __global__ __launch_bounds__(256, 1) void lstm_fwd_persistent_kernel(
     // (< B * KA * 2 < 2^31, host-checked) so any batch size fits the 32-bit offsets
     const __amdgpu_buffer_rsrc_t xh_rsrc =
         __builtin_amdgcn_make_buffer_rsrc(XH + (size_t)(t + 1) * d.B * KA, 0, 0x7FFFFFFF, 0x00020000);
-    const int hsoff = (int)(((size_t)rb * KA + 64 + n * 64) * 2);
+    const int hsoff = (int)(((size_t)rb * KA + KXC + n * 64) * 2);
 
     // cell epilogue element (row-tile i, row r) of the carried chunk: accp + c_{t-1} = cq[0]
     auto epi_elem = [&](int i, int r, float (&cv)[2][4], unsigned (&pk)[2][8], unsigned (&hv)[2][4]) {
@@ -477,9 +483,16 @@ __global__ __launch_bounds__(256, 1) void lstm_fwd_persistent_kernel(
       auto fused_slot = [&](auto kc, auto mc) {
         constexpr int kt = decltype(kc)::value, mm = decltype(mc)::value;
         constexpr int i = mm >> 2, j = mm & 3, m = kt * 8 + mm;
-        constexpr int el = 2 * (m / 36) + (m & 1), st = (m % 36) / 2, ei_ = el >> 2, er = el & 3;
+        constexpr int el = 2 * (m / 36) + (m & 1), st = (m % 36) / 2, ei_ = (el >> 2) & 1, er = el & 3;
         EpiMicro& E = e2[m & 1];
         const bf16x8& A = a[kt & 1][i];
+        if constexpr (m >= 144) {  // KT > 18: the 144 stages are placed, the rest are plain MFMAs
+          if constexpr (kt < KTA)
+            asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc[i][j]) : "v"(A), "a"(w[kt][j]));
+          else
+            asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc[i][j]) : "v"(A), "v"(w[kt][j]));
+          return;
+        }
 #define WF_UNP(...) __VA_ARGS__
 #define WF_MF(TXT, OUTS, INS)                                                                          \
   if constexpr (kt == 0)                                                                               \

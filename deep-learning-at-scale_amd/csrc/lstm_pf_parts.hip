@@ -5,6 +5,11 @@
 // wf-build-variants: -DWF_KT=6 -DWF_NC=1 | -DWF_KT=6 -DWF_NC=2 | -DWF_KT=6 -DWF_NC=4 | -DWF_KT=6 -DWF_NC=8
 // wf-build-variants: -DWF_KT=10 -DWF_NC=1 | -DWF_KT=10 -DWF_NC=2 | -DWF_KT=10 -DWF_NC=4 | -DWF_KT=10 -DWF_NC=8
 // wf-build-variants: -DWF_KT=18 -DWF_NC=1 | -DWF_KT=18 -DWF_NC=2 | -DWF_KT=18 -DWF_NC=4 | -DWF_KT=18 -DWF_NC=8
+// KX = 128 (64 <= F <= 127): KT = 8 / 12 / 20 for H = 128 / 256 / 512
+// wf-build-variants: -DWF_KT=8 -DWF_NC=1 | -DWF_KT=8 -DWF_NC=2 | -DWF_KT=8 -DWF_NC=4 | -DWF_KT=8 -DWF_NC=8
+// wf-build-variants: -DWF_KT=12 -DWF_NC=1 | -DWF_KT=12 -DWF_NC=2 | -DWF_KT=12 -DWF_NC=4 | -DWF_KT=12 -DWF_NC=8
+// (KT = 20 at NC = 2 / 4 spills hundreds of VGPRs: the launcher uses NC = 1 or 8 there)
+// wf-build-variants: -DWF_KT=20 -DWF_NC=1 | -DWF_KT=20 -DWF_NC=8
 #include "lstm_persistent_fwd.inc.h"
 
 #define WF_PF_NAME2(a, b) launch_pf_##a##_##b

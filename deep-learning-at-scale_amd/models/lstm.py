@@ -226,6 +226,17 @@ class NativeLSTM:
         self.last_backward_persistent = False
         self.sync_weights()
 
+    @staticmethod
+    def full_grid_batch(hidden: int, device) -> int:
+        """Rows per step that fill ONE co-resident persistent grid on this device: 256 rows
+        (8 chunks of 32) per workgroup, (4 hidden / 256) gate-column workgroups per row block,
+        one workgroup per CU (csrc/lstm_persistent.hip persistent_split) — 8192 at H = 512 on
+        a 256-CU MI355X. A job's default LSTM batch (config.py batch_size 0 = auto): the
+        reference's small batches (cnn.py:128 uses 20) would run a 64-workgroup grid on 256 CUs."""
+        props = torch.cuda.get_device_properties(device)
+        nb = max(1, 4 * hidden // 256)
+        return 256 * max(1, props.multi_processor_count // nb)
+
     # ------------------------------------------------------------------ weights
     def sync_weights(self) -> None:
         W, _, _ = self.lay.views(self.params)

@@ -82,7 +82,15 @@ def run_config(cfg: RunConfig, log=print) -> dict:
     dev = ctx.device
     native = dev.type == "cuda" and cfg.precision == "bf16"
     n_train = len(prepared.train[0])
+    if cfg.batch_size <= 0:  # auto (lstm): fill the GPU's persistent grid; 256 on the fp32 oracle
+        from ..models.lstm import NativeLSTM
+
+        cfg.batch_size = NativeLSTM.full_grid_batch(cfg.hidden, dev) if native and cfg.model == "lstm" else 256
+        say(f"Batch size (auto): {cfg.batch_size} rows per GPU")
     b = max(1, min(cfg.batch_size, n_train // max(ctx.world_size, 1)))
+    if native and cfg.model == "lstm" and b >= 64:
+        b -= b % 64  # the persistent kernels take batches in whole 64-row tiles
+        cfg.batch_size = b  # the Trainer's per-rank batch (Trainer._local_batch) is then exactly b
     eng, ref = registry.build_engine(cfg.model, cfg, prepared.n_features, prepared.n_outputs, b,
                                      dev, native, seed=cfg.seed)
     ctx.broadcast_(eng.params)  # C1

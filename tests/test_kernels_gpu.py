@@ -214,9 +214,11 @@ def test_losses():
         assert torch.allclose(cs, (pr.grad * scale).sum(0), rtol=1e-2, atol=1e-4)
 
 
-@pytest.mark.parametrize("B,H,T", [(8192, 512, 8), (512, 256, 6), (256, 128, 5), (2048, 512, 64),
-                                   (16384, 512, 4), (12288, 512, 3)])
-def test_lstm_persistent_forward_matches_per_step(B, H, T):
+@pytest.mark.parametrize("B,H,T,F", [(8192, 512, 8, 16), (512, 256, 6, 16), (256, 128, 5, 16), (2048, 512, 64, 16),
+                                     (16384, 512, 4, 16), (12288, 512, 3, 16),
+                                     # KX = 128 (64 <= F <= 127): one-hot-heavy feature vectors
+                                     (8192, 512, 6, 100), (1024, 512, 4, 100), (2048, 256, 5, 64), (512, 128, 4, 127)])
+def test_lstm_persistent_forward_matches_per_step(B, H, T, F):
     """The one-launch persistent forward (csrc/lstm_persistent.hip) must reproduce the
     per-step kernels: same MFMA k-order per output, so h/C/S agree to the last bf16 ulp
     apart from transcendental rounding (tolerance), and its spin bound must not trip.
@@ -224,7 +226,6 @@ def test_lstm_persistent_forward_matches_per_step(B, H, T):
     from wellflow.data.synth import synth_lstm_batch
     from wellflow.models.lstm import NativeLSTM, init_lstm_flat
 
-    F = 16
     eng = NativeLSTM(F, H, T, B, device=DEV)
     eng.params.copy_(init_lstm_flat(F, H, seed=1).to(DEV))
     eng.sync_weights()
@@ -242,6 +243,7 @@ def test_lstm_persistent_forward_matches_per_step(B, H, T):
     ok = C.lstm_forward_persistent(eng.XH, eng.Wp, eng.Cst, eng.S, eng.sync, *dims)
     torch.cuda.synchronize()
     assert ok, "persistent launch refused"
+    assert eng.lay.KX == (64 if F < 64 else 128)
     assert eng.persistent_error() == 0, "spin bound tripped"
     for name, a, b in zip(("XH", "C", "S"), (eng.XH, eng.Cst, eng.S), ref):
         d = (a.float() - b.float()).abs().max().item()
@@ -267,16 +269,15 @@ def test_weight_gradient_tiles_match_reference(tile, ksplit):
     assert err < 2e-3 * ref.abs().max().item(), (tile, err)
 
 
-@pytest.mark.parametrize("B,H,T", [(8192, 512, 8), (512, 256, 6), (256, 128, 5), (2048, 512, 64),
-                                   (16384, 512, 4)])
-def test_lstm_persistent_backward_matches_per_step(B, H, T):
+@pytest.mark.parametrize("B,H,T,F", [(8192, 512, 8, 16), (512, 256, 6, 16), (256, 128, 5, 16), (2048, 512, 64, 16),
+                                     (16384, 512, 4, 16), (8192, 512, 6, 100)])
+def test_lstm_persistent_backward_matches_per_step(B, H, T, F):
     """The one-launch persistent BPTT (csrc/lstm_persistent_bwd.hip) against the per-step
     backward kernels on the same forward state: the K-split dh partials are summed in a
     different fp32 order, so DG agrees to bf16 rounding and the weight gradient closely."""
     from wellflow.data.synth import synth_lstm_batch
     from wellflow.models.lstm import NativeLSTM, init_lstm_flat
 
-    F = 16
     eng = NativeLSTM(F, H, T, B, device=DEV)
     eng.params.copy_(init_lstm_flat(F, H, seed=4).to(DEV))
     eng.sync_weights()

@@ -67,8 +67,10 @@ def _setup(B, T, F, H, seed=0):
     return eng, flat, x.to(DEV), y.to(DEV)
 
 
-def test_lstm_headline_shape_matches_fp32():
-    B, T, F, H = 8192, 64, 16, 512
+@pytest.mark.parametrize("B,T,F,H", [(8192, 64, 16, 512),
+                                     # a one-hot-heavy table (F = 100: KX = 128) on the persistent path
+                                     (8192, 32, 100, 512)])
+def test_lstm_headline_shape_matches_fp32(B, T, F, H):
     eng, flat, x, y = _setup(B, T, F, H)
     ls = eng.forward_backward(x, y, grad_scale=1.0 / B).item()
     torch.cuda.synchronize()

@@ -28,34 +28,43 @@ def main():
     ap.add_argument("--model", default="lstm", choices=["lstm", "mlp", "mlp_online"])
     ap.add_argument("--epochs", type=int, default=4)
     ap.add_argument("--out", default=None)
+    ap.add_argument("--wells", type=int, default=6, help="synthetic wells: (wells - 1) + 2 one-hot + 9 "
+                    "continuous features (6 -> 16, 90 -> 100)")
+    ap.add_argument("--default-batch", action="store_true",
+                    help="the job's own default batch (lstm: auto) instead of the bench's per-GPU batch")
     a = ap.parse_args()
     from wellflow.config import parse_argv
     from wellflow.train.job import run_config
 
     if a.model == "lstm":
-        batch, extra, wells, steps = 8192, ["--seq-len", "64", "--hidden", "512"], 6, 40000
+        batch, extra, wells, steps = 8192, ["--seq-len", "64", "--hidden", "512"], a.wells, 40000 * 6 // a.wells
     elif a.model == "mlp":
         batch, extra, wells, steps = 262144, [], 6, 640000
     else:  # the stream: chunks of 8 mini-batches, each consumed once (train/online.py)
         batch, extra, wells, steps = 262144, ["--online-chunk", str(8 * 262144)], 6, 640000
     # 6 wells (3 fields): 5 + 2 one-hot columns + 9 continuous = 16 features, the bench's F
     argv = [NAMES, TYPES, "flow", "/tmp/wellflow_jobtp/", "--epochs", str(a.epochs), "--patience", "100",
-            "--synth-wells", str(wells), "--synth-steps", str(steps), "--batch-size", str(batch),
-            "--device", "cuda", "--verbose", "0"] + extra
+            "--synth-wells", str(wells), "--synth-steps", str(steps), "--device", "cuda", "--verbose", "0"] + extra
+    if not a.default_batch:
+        argv += ["--batch-size", str(batch)]
     cfg = parse_argv(a.model, argv)
     out = run_config(cfg, log=lambda *x, **k: None)
     from wellflow.data.pipeline import prepare  # noqa: F401  (feature count reported below)
     rps = out["history"]["rows_per_s"]
     steady = rps[1:] if len(rps) > 1 else rps
     job = max(steady)
+    batch = cfg.batch_size  # what the job ran (auto-sized when --default-batch)
+    F = out.get("n_features") or 16
     bench = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--model", a.model, "--batch", str(batch),
-                            "--steps", "20", "--warmup", "5"], capture_output=True, text=True, cwd=ROOT)
+                            "--features", str(F), "--secondary", "none", "--steps", "20", "--warmup", "5"],
+                           capture_output=True, text=True, cwd=ROOT)
     line = [ln for ln in bench.stdout.splitlines() if ln.startswith("{")]
     b = json.loads(line[-1])["value"] if line else None
     rec = {"model": a.model, "per_gpu_batch": batch, "job_rows_per_s_per_epoch": rps,
            "job_steady_rows_per_s": job, "bench_rows_per_s": b,
            "job_over_bench": None if not b else job / b, "steps": out["steps"], "epochs": out["epochs"],
-           "native": out["native"], "n_features": out.get("n_features"),
+           "native": out["native"], "n_features": out.get("n_features"), "persistent": out.get("persistent"),
+           "default_batch": a.default_batch,
            "data": f"synthetic well-log table {wells} wells x {steps} steps"}
     print(json.dumps(rec), flush=True)
     if a.out:
