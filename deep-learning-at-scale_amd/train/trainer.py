@@ -101,10 +101,19 @@ class Trainer:
         w, r = self.ctx.world_size, self.ctx.rank
         idx = np.arange(r, n, w)
         chunk = chunk or getattr(self.eng, "B", 4096) or 4096
-        s_loss, s_mse, cnt = 0.0, 0.0, 0
         Xd = X if (torch.is_tensor(X) or hasattr(X, "starts")) and getattr(X, "device", None) == self.eng.device \
             else None
         pf = self._eval_prefetcher(X, chunk) if Xd is None and len(idx) > chunk else None
+        try:
+            s_loss, s_mse, cnt = self._eval_chunks(X, Y, Xd, idx, chunk, pf)
+        finally:  # the gather threads and slot buffers go away on the error path too
+            if pf is not None:
+                pf.close()
+        s_loss, s_mse, cnt = self.ctx.sum_scalars(s_loss, s_mse, cnt)
+        return s_loss / max(cnt, 1), s_mse / max(cnt, 1)
+
+    def _eval_chunks(self, X, Y, Xd, idx, chunk, pf):
+        s_loss, s_mse, cnt = 0.0, 0.0, 0
         if pf is not None:
             pf.submit(0, idx[:chunk])
         for k, i in enumerate(range(0, len(idx), chunk)):
@@ -125,10 +134,7 @@ class Trainer:
             s_loss += per_element_loss(self.cfg.loss, pred, yb, self.cfg.clip).sum().item()
             s_mse += ((pred - yb) ** 2).sum().item()
             cnt += yb.numel()
-        if pf is not None:
-            pf.close()
-        s_loss, s_mse, cnt = self.ctx.sum_scalars(s_loss, s_mse, cnt)
-        return s_loss / max(cnt, 1), s_mse / max(cnt, 1)
+        return s_loss, s_mse, cnt
 
     def _eval_prefetcher(self, X, chunk: int):
         """Two-slot native window prefetcher for a host-resident window set (float32
@@ -140,10 +146,10 @@ class Trainer:
                 and native.wanted()):
             return None
         # targets come from Y per window; the prefetcher's per-row target buffer is unused.
-        # Pageable slots by default: with pinned slots (WELLFLOW_EVAL_PIN=1) allocated between
-        # the epochs of a graph-replayed LSTM job, later persistent launches completed only
-        # part of their steps (job bwd 0.11 vs 1.76 ms; caught by the completion counters,
-        # NativeLSTM.check_device_errors; profiles/r2_summary.md)
+        # Pageable slots by default (WELLFLOW_EVAL_PIN=1: pinned). Round 2 saw pinned slots
+        # break graph-replayed persistent launches; the cause was the per-launch memset of the
+        # sync words (profiles/r3_early_exit.md), fixed, and tests/test_job_gpu.py runs both.
+        # Pinned measured no faster for evaluation (1.69 vs 1.70 M rows/s job).
         return native.Prefetcher(rows, np.asarray(X.starts), np.zeros(len(rows), np.float32), X.T, chunk,
                                  nslots=2, threads=2, pin=os.environ.get("WELLFLOW_EVAL_PIN", "0") == "1")
 

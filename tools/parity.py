@@ -6,9 +6,14 @@ engine vs the fp32 PyTorch oracle over several seeds, both through the productio
 
     python tools/parity.py --model lstm --seeds 0,1,2 --out profiles/r2/parity_lstm.json
 
-Each seed fixes the synthetic table, the split, the init and the batch order of BOTH runs.
-Reported: per-precision mean +- std of the final and best val MSE, the mean gap, and the
-verdict ``pass`` = |mean gap| <= max(fp32 seed-to-seed std, 2 % of the fp32 mean).
+Each seed fixes the synthetic table, the split, the init and the batch order of BOTH runs,
+so the comparison is PAIRED: per seed, the relative gap of the best val MSE (the saved
+model's, ModelCheckpoint save_best_only, cnn.py:122) bf16 vs fp32. Both run to the
+reference's early stop (patience 10, cnn.py:121; ``--epochs`` caps the epochs). Reported:
+per-precision mean +- std, the paired relative gaps with their mean and 95 % t confidence
+interval, and ``pass`` = the interval contains 0 or |mean paired gap| <= 2 %. Results are
+written after every seed (``--out``), and ``--merge a.json b.json`` pools runs of several
+calls (seeds split over GPU calls).
 Defaults are the LSTM headline shapes (seq 64, hidden 512, batch 2048 per GPU) on a table
 large enough for ~40 steps per epoch. ``--dropout 0`` (the CNN default here) removes the
 only RNG that differs between the engines (native counter hash vs torch's Philox), so the
@@ -60,24 +65,68 @@ def _ms(xs):
     return {"mean": statistics.fmean(xs), "std": statistics.stdev(xs) if len(xs) > 1 else 0.0, "values": xs}
 
 
+def _t975(df: int) -> float:
+    from scipy import stats
+
+    return float(stats.t.ppf(0.975, df))
+
+
+def summarize(model, runs, meta) -> dict:
+    """Paired statistics over seeds present in both precisions."""
+    by = {p: {r["seed"]: r for r in runs[p]} for p in runs}
+    seeds = sorted(set(by["bf16"]) & set(by["fp32"]))
+    best = {p: _ms([by[p][s]["best_val_mse"] for s in seeds]) for p in runs}
+    fin = {p: _ms([by[p][s]["final_val_mse"] for s in seeds]) for p in runs}
+    rel = [by["bf16"][s]["best_val_mse"] / by["fp32"][s]["best_val_mse"] - 1.0 for s in seeds]
+    n = len(rel)
+    mean = statistics.fmean(rel) if rel else float("nan")
+    half = _t975(n - 1) * statistics.stdev(rel) / n ** 0.5 if n > 1 else float("inf")
+    ci = [mean - half, mean + half]
+    return {"model": model, "seeds": seeds, **meta, "best_val_mse": best, "final_val_mse": fin,
+            "paired_rel_gap_best": rel, "paired_rel_gap_mean": mean, "paired_rel_gap_ci95": ci,
+            "early_stopped": {p: [by[p][s].get("early_stopped") for s in seeds] for p in runs},
+            "epochs_run": {p: [len(by[p][s]["val_mse"]) for s in seeds] for p in runs},
+            "pass": n > 1 and (ci[0] <= 0.0 <= ci[1] or abs(mean) <= 0.02), "runs": runs}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--model", default="lstm", choices=sorted(DEFAULTS))
-    ap.add_argument("--seeds", default="0,1,2")
-    ap.add_argument("--epochs", type=int, default=None)
+    ap.add_argument("--seeds", default="0,1,2,3,4")
+    ap.add_argument("--epochs", type=int, default=None, help="epoch cap (default: converge, cap 80)")
+    ap.add_argument("--patience", type=int, default=10)
     ap.add_argument("--wells", type=int, default=None)
     ap.add_argument("--steps", type=int, default=None)
     ap.add_argument("--batch", type=int, default=None)
     ap.add_argument("--out", default=None)
+    ap.add_argument("--merge", nargs="+", default=None, help="pool the runs of these output files")
     a = ap.parse_args()
+    if a.merge:
+        parts = [json.load(open(f)) for f in a.merge]
+        runs = {"bf16": [], "fp32": []}
+        for part in parts:
+            for p in runs:
+                runs[p] += part["runs"][p]
+        meta = {k: parts[0][k] for k in ("epochs_cap", "patience", "per_gpu_batch", "data", "config_extra")}
+        summary = summarize(parts[0]["model"], runs, meta)
+        print(json.dumps({k: v for k, v in summary.items() if k != "runs"}), flush=True)
+        if a.out:
+            with open(a.out, "w") as fh:
+                json.dump(summary, fh, indent=1)
+        return 0 if summary["pass"] else 1
     wells, steps, batch, epochs, extra = DEFAULTS[a.model]
     wells, steps = a.wells or wells, a.steps or steps
-    batch, epochs = a.batch or batch, a.epochs or epochs
+    batch = a.batch or batch
+    epochs = a.epochs or 80
     seeds = [int(s) for s in a.seeds.split(",")]
     runs = {"bf16": [], "fp32": []}
+    meta = {"epochs_cap": epochs, "patience": a.patience, "per_gpu_batch": batch,
+            "data": f"synthetic Gilbert well logs, {wells} wells x {steps} steps, time-block split",
+            "config_extra": extra}
+    summary = None
     for seed in seeds:
         base = [NAMES, TYPES, "flow", f"/tmp/wellflow_parity_{a.model}_{seed}/", "--epochs", str(epochs),
-                "--patience", str(epochs + 1), "--synth-wells", str(wells), "--synth-steps", str(steps),
+                "--patience", str(a.patience), "--synth-wells", str(wells), "--synth-steps", str(steps),
                 "--batch-size", str(batch), "--device", "cuda", "--verbose", "0", "--seed", str(seed)] + extra
         for prec in ("bf16", "fp32"):
             cfg = parse_argv(a.model, base + ["--precision", prec])
@@ -85,31 +134,21 @@ def main():
             h = out["history"]
             runs[prec].append({"seed": seed, "native": out["native"], "val_mse": h["val_mse"],
                                "final_val_mse": h["val_mse"][-1], "best_val_mse": min(h["val_mse"]),
+                               "early_stopped": len(h["val_mse"]) < epochs,
                                "test_mse": out["test_mse"], "steps": out["steps"], "elapsed_s": out["elapsed"]})
-            print(f"seed {seed} {prec}: native={out['native']} steps={out['steps']} "
-                  f"val_mse={['%.5f' % v for v in h['val_mse']]}", flush=True)
-    fin = {p: _ms([r["final_val_mse"] for r in runs[p]]) for p in runs}
-    best = {p: _ms([r["best_val_mse"] for r in runs[p]]) for p in runs}
-    gap = fin["bf16"]["mean"] - fin["fp32"]["mean"]
-    tol = max(fin["fp32"]["std"], 0.02 * fin["fp32"]["mean"])
-    summary = {
-        "model": a.model, "epochs": epochs, "per_gpu_batch": batch, "seeds": seeds,
-        "data": f"synthetic Gilbert well logs, {wells} wells x {steps} steps, time-block split",
-        "config_extra": extra,
-        "final_val_mse": fin, "best_val_mse": best,
-        "mean_gap_bf16_minus_fp32": gap, "relative_mean_gap": gap / fin["fp32"]["mean"],
-        "tolerance": tol, "pass": abs(gap) <= tol,
-        "runs": runs,
-    }
-    if a.model in ("lstm", "mlp"):
-        cfg = parse_argv("gilbert", [NAMES, TYPES, "flow", "/tmp/wellflow_parity/", "--synth-wells", str(wells),
-                                     "--synth-steps", str(steps), "--seed", str(seeds[0])])
-        summary["gilbert_val_mse_standardized"] = gilbert_val_mse(cfg)
+            print(f"seed {seed} {prec}: native={out['native']} steps={out['steps']} epochs={len(h['val_mse'])} "
+                  f"best_val_mse={min(h['val_mse']):.6f} elapsed={out['elapsed']:.1f}s", flush=True)
+        summary = summarize(a.model, runs, meta)
+        if a.model in ("lstm", "mlp") and "gilbert_val_mse_standardized" not in meta:
+            cfg = parse_argv("gilbert", [NAMES, TYPES, "flow", "/tmp/wellflow_parity/", "--synth-wells", str(wells),
+                                         "--synth-steps", str(steps), "--seed", str(seeds[0])])
+            meta["gilbert_val_mse_standardized"] = gilbert_val_mse(cfg)
+            summary["gilbert_val_mse_standardized"] = meta["gilbert_val_mse_standardized"]
+        if a.out:  # after every seed: a call that runs out of time still leaves its seeds
+            os.makedirs(os.path.dirname(a.out) or ".", exist_ok=True)
+            with open(a.out, "w") as fh:
+                json.dump(summary, fh, indent=1)
     print(json.dumps({k: v for k, v in summary.items() if k != "runs"}), flush=True)
-    if a.out:
-        os.makedirs(os.path.dirname(a.out) or ".", exist_ok=True)
-        with open(a.out, "w") as fh:
-            json.dump(summary, fh, indent=1)
     return 0 if summary["pass"] else 1
 
 

@@ -46,6 +46,25 @@ def main():
         hs = f"{100 * h / (h + mi):.0f} %" if h is not None and mi is not None else "-"
         short = name.split("(")[0].replace("void ", "")
         print(f"| `{short}` | {cyc:.3g} | {util} | {ldss} | {ws} | {vm} | {rd} | {wr} | {hs} |")
+    # wave-cycle breakdown (SQ_WAIT_ANY + SQ_WAIT_INST_ANY + SQ_ACTIVE_INST_ANY ~= SQ_WAVE_CYCLES,
+    # MI355X_MICROARCH.md rocprofv3 PMC slots) and the issue mix, when those counters were taken
+    rows = []
+    for name, c in vals.items():
+        m = {k: sum(v) / len(v) for k, v in c.items()}
+        wc = m.get("SQ_WAVE_CYCLES")
+        if not wc or m.get("GRBM_GUI_ACTIVE", 0) / 8 < 1e4:
+            continue
+        f = lambda k: f"{100 * m[k] / wc:.0f} %" if k in m else "-"  # noqa: E731
+        mf = m.get("SQ_VALU_MFMA_BUSY_CYCLES")
+        co = f"{100 * m['SQ_VALU_MFMA_COEXEC_CYCLES'] / mf:.0f} %" if mf and "SQ_VALU_MFMA_COEXEC_CYCLES" in m else "-"
+        rows.append(f"| `{name.split('(')[0].replace('void ', '')}` | {f('SQ_WAIT_ANY')} | {f('SQ_WAIT_INST_ANY')} | "
+                    f"{f('SQ_WAIT_INST_LDS')} | {f('SQ_ACTIVE_INST_ANY')} | {f('SQ_ACTIVE_INST_VALU')} | "
+                    f"{f('SQ_ACTIVE_INST_LDS')} | {f('SQ_ACTIVE_INST_SCA')} | {co} |")
+    if rows and any("SQ_WAIT_INST_ANY" in c or "SQ_ACTIVE_INST_VALU" in c for c in vals.values()):
+        print()
+        print("| kernel | wait (waitcnt/barrier) | issue stall | LDS issue stall | active | active VALU | active LDS | active scalar | MFMA-VALU coexec / MFMA busy |")
+        print("|---|---|---|---|---|---|---|---|---|")
+        print("\n".join(rows))
 
 
 if __name__ == "__main__":
