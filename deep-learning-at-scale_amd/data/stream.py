@@ -11,6 +11,10 @@ DMA), so the H2D copy never runs synchronously from pageable memory.
 Ordering (measured on MI355X, tools/online_host.py, bench.py h2d_* fields): a copy-stream
 wait on an event of the compute stream (a cross-queue dependency, compute queue -> SDMA) made
 4-5 % of the 9.4 MB batch copies stall for 3-6 ms (0.38-0.47 ms per step instead of 0.275).
+Cause (profiles/r3_h2d_stall.md, tools/h2d_stall.py + a memory-copy trace): the DMA never
+takes more than ~0.27 ms; the SDMA queue notices a satisfied compute-queue dependency ~0.5 ms
+late at the median and ~7 ms late in a few percent of cases, and the compute stream, waiting on
+that copy, drains (blit copies resolve the same wait in ~0.05 ms).
 The slot's reuse is therefore ordered on the HOST: before refilling the slot of batch k-2 the
 producer synchronizes on an event recorded right after batch k-2's compute (batch k-1's compute
 is already queued, so the GPU never runs dry), and the copy itself has no queue dependency.
