@@ -130,12 +130,17 @@ def build(verbose: bool = False, jobs: int | None = None) -> str:
     objs = []
     # WELLFLOW_DIAG_BUILD=1: also the timing-only diagnostic kernel variants (WELLFLOW_PF_DBG,
     # tools/pf_time.py, pb_time.py, *_timeline.py); separate objects, so switching is a relink
-    diag = os.environ.get("WELLFLOW_DIAG_BUILD", "0") == "1"
+    # (=N or =N,M,..: only those WELLFLOW_PF_DBG variants, for a quick diagnostic build)
+    dval = os.environ.get("WELLFLOW_DIAG_BUILD", "0")
+    diag = dval not in ("", "0")
     for src in hip_srcs:
         deps = [src] + _local_deps(src)
         for tag, defs in _variants(src):
-            defs = defs + (["-DWF_DIAG"] if diag else [])
-            obj = os.path.join(BUILD_DIR, os.path.basename(src) + tag + (".diag" if diag else "") + ".o")
+            vals = [int(v) for v in dval.split(",")] if diag else []
+            defs = defs + (["-DWF_DIAG"] + ([f"-DWF_DIAG_SET={','.join(map(str, vals))}"] if dval != "1" else [])
+                           if diag else [])
+            dtag = (".diag" if dval == "1" else ".diag" + "_".join(map(str, vals))) if diag else ""
+            obj = os.path.join(BUILD_DIR, os.path.basename(src) + tag + dtag + ".o")
             objs.append(obj)
             if _stale(obj, deps):
                 tasks.append([hipcc, *HIPCC_FLAGS, *defs, f"-I{CSRC}", "-c", src, "-o", obj])

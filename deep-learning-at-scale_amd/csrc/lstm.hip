@@ -115,9 +115,9 @@ __global__ __launch_bounds__(64 * WM * WN) void lstm_fwd_step_kernel(int t, bf16
       if (m < d.B) hnext[(size_t)m * KA + u] = f2bf(og * tanhf_(c));
     }
     *reinterpret_cast<float4*>(cnext + blk * 256 + lane * 4) = make_float4(cv[0], cv[1], cv[2], cv[3]);
-    uint4* sp = reinterpret_cast<uint4*>(St + blk * 1024 + lane * 16);
-    st16(sp, make_uint4(pk[0], pk[1], pk[2], pk[3]), d.nt);
-    st16(sp + 1, make_uint4(pk[4], pk[5], pk[6], pk[7]), d.nt);
+    bf16_t* sb = St + blk * 1024 + lane * 8;  // FN S halves (lstm_layout.h kFnSHalf)
+    st16(sb, make_uint4(pk[0], pk[1], pk[2], pk[3]), d.nt);
+    st16(sb + kFnSHalf, make_uint4(pk[4], pk[5], pk[6], pk[7]), d.nt);
   }
 }
 
@@ -162,8 +162,8 @@ __device__ __forceinline__ void cell_bwd4(int t, int mrow0, int u, int lane, con
                                           float* __restrict__ dcarry, const LstmDims& d) {
   const int G = 4 * d.H, Bp = fn_rows(d.B);
   const size_t blk = fn_block(mrow0, u, d.H);
-  const uint4* sp = reinterpret_cast<const uint4*>(S + (size_t)t * Bp * G + blk * 1024 + lane * 16);
-  const uint4 s0 = ld16(sp, d.nt), s1 = ld16(sp + 1, d.nt);
+  const bf16_t* sb = S + (size_t)t * Bp * G + blk * 1024 + lane * 8;  // FN S halves (lstm_layout.h)
+  const uint4 s0 = ld16(sb, d.nt), s1 = ld16(sb + kFnSHalf, d.nt);
   const unsigned pk[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
   // only c_{t-1} is read: c_t = f * c_{t-1} + i * g is recomputed from the saved gates
   // (the same bf16 gates every other term of the cell backward uses), which drops one

@@ -18,6 +18,12 @@ __host__ __device__ __forceinline__ int dg_col(int gate, int u) { return 4 * u +
 // inside a block element (m, u) sits at lane ((m&15)>>2)*16 + (u&15), slot m&3 — exactly
 // where the 16x16 MFMA C map puts it, so every lane moves 16-32 contiguous bytes.
 // Batch rows are padded to a multiple of 16 (fn_rows).
+// S (saved gates, 4 bf16 per element = 32 B per lane per block) is stored as two HALVES of
+// 16 B per lane: rows 0-1 of the lane's 4 at bf16 offset lane * 8, rows 2-3 at 512 + lane * 8,
+// so each 16-B store / load instruction of a wave covers 1 KiB contiguously (a lane-interleaved
+// 32-B slot made every instruction touch twice the cache lines with 16-B holes; the
+// forward's C / S stores were 23 % of its time, tools/pf_time.py dbg 4).
+constexpr int kFnSHalf = 512;  // bf16 offset of the second half in a 16x16 S block
 __host__ __device__ __forceinline__ int fn_rows(int B) { return (B + 15) & ~15; }
 
 // Non-temporal 16-B accesses for the read-once / write-once streams (saved gates S, the

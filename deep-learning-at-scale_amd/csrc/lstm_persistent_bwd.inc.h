@@ -28,6 +28,25 @@
 //    row block depend on each other; every spin is bounded (error words 1 and sticky 0, all drain).
 // Step T-1 (dh from the regression head) is lstm_bwd_last_kernel in lstm.hip.
 #pragma once
+// diagnostic builds: WELLFLOW_DIAG_BUILD=1 instantiates every timing variant, =N or =N,M,..
+// only those WELLFLOW_PF_DBG values (fewer instantiations, minutes less to build)
+#ifdef WF_DIAG
+#ifndef WF_DIAG_SET
+#define WF_DIAG_SET 0
+#endif
+#ifndef WF_DIAG_SET_DEFINED
+#define WF_DIAG_SET_DEFINED
+namespace wf {
+constexpr int kDiagSet[] = {WF_DIAG_SET};
+constexpr bool diag_variant(int v) {
+  for (int x : kDiagSet)
+    if (x == 0 || x == v) return true;
+  return false;
+}
+}  // namespace wf
+#endif
+#define WF_DV(v) (::wf::diag_variant(v))
+#endif
 #include <cstdlib>
 
 #include "gemm_core.h"
@@ -131,7 +150,7 @@ __global__ __launch_bounds__(256, 1) void lstm_bwd_persistent_kernel(
   int fa[2];  // fragment byte offsets inside a 64-k step image, k-tile half 0 / 1
 #pragma unroll
   for (int hf = 0; hf < 2; ++hf) fa[hf] = l15 * 128 + (((4 * hf + g) ^ ((l15 >> 1) & 7)) << 4);
-  const int s_lane = ue / 16 * 1024 + lane * 16;                    // FN S slot (block column ue>>4)
+  const int s_lane = ue / 16 * 1024 + lane * 8;                     // FN S first half (block column ue>>4)
   const int c_lane = ue / 16 * 256 + lane * 4;                      // FN C slot
   const int ue2 = even ? ue : ue - 1;                               // first unit of this lane's 16-B run
   const int st_lane = ((4 * g + (even ? 0 : 1)) * G + 4 * ue2) * 2;  // byte offset (row 4g + r0, col 4*ue2)
@@ -161,7 +180,7 @@ __global__ __launch_bounds__(256, 1) void lstm_bwd_persistent_kernel(
     // nt on the read-once streams (256: default policy; A/B within run-to-run noise)
     constexpr int NTA = (DBG & 256) ? 0 : 2;
     sq0[Q] = __builtin_amdgcn_raw_buffer_load_b128(sr, s_vo, SO, NTA);
-    sq1[Q] = __builtin_amdgcn_raw_buffer_load_b128(sr, s_vo + 16, SO, NTA);
+    sq1[Q] = __builtin_amdgcn_raw_buffer_load_b128(sr, s_vo + 2 * kFnSHalf, SO, NTA);  // second half
     cq[Q] = __builtin_amdgcn_raw_buffer_load_b128(cr, c_vo, CO, NTA);
   };
   load_sc(d.T - 2, std::integral_constant<int, 0>{}, std::integral_constant<int, 0>{});
@@ -581,17 +600,17 @@ static int launch_pb(const bf16_t* WhhT, const float* Cst, const bf16_t* S, bf16
 #ifdef WF_DIAG  // timing-only diagnostic builds (WELLFLOW_PF_DBG; WELLFLOW_DIAG_BUILD=1)
   if constexpr (KT == 16 && NRT == 16) {
     switch (d.dbg) {
-      case 1: f = reinterpret_cast<const void*>(&lstm_bwd_persistent_kernel<KT, NRT, 1>); break;
-      case 2: f = reinterpret_cast<const void*>(&lstm_bwd_persistent_kernel<KT, NRT, 2>); break;
-      case 4: f = reinterpret_cast<const void*>(&lstm_bwd_persistent_kernel<KT, NRT, 4>); break;
-      case 8: f = reinterpret_cast<const void*>(&lstm_bwd_persistent_kernel<KT, NRT, 8>); break;
-      case 16: f = reinterpret_cast<const void*>(&lstm_bwd_persistent_kernel<KT, NRT, 16>); break;
-      case 32: f = reinterpret_cast<const void*>(&lstm_bwd_persistent_kernel<KT, NRT, 32>); break;
-      case 64: f = reinterpret_cast<const void*>(&lstm_bwd_persistent_kernel<KT, NRT, 64>); break;
-      case 96: f = reinterpret_cast<const void*>(&lstm_bwd_persistent_kernel<KT, NRT, 96>); break;
-      case 128: f = reinterpret_cast<const void*>(&lstm_bwd_persistent_kernel<KT, NRT, 128>); break;
-      case 256: f = reinterpret_cast<const void*>(&lstm_bwd_persistent_kernel<KT, NRT, 256>); break;
-      case 512: f = reinterpret_cast<const void*>(&lstm_bwd_persistent_kernel<KT, NRT, 512>); break;  // 8-part epilogue
+      case 1: if constexpr (WF_DV(1)) f = reinterpret_cast<const void*>(&lstm_bwd_persistent_kernel<KT, NRT, 1>); break;
+      case 2: if constexpr (WF_DV(2)) f = reinterpret_cast<const void*>(&lstm_bwd_persistent_kernel<KT, NRT, 2>); break;
+      case 4: if constexpr (WF_DV(4)) f = reinterpret_cast<const void*>(&lstm_bwd_persistent_kernel<KT, NRT, 4>); break;
+      case 8: if constexpr (WF_DV(8)) f = reinterpret_cast<const void*>(&lstm_bwd_persistent_kernel<KT, NRT, 8>); break;
+      case 16: if constexpr (WF_DV(16)) f = reinterpret_cast<const void*>(&lstm_bwd_persistent_kernel<KT, NRT, 16>); break;
+      case 32: if constexpr (WF_DV(32)) f = reinterpret_cast<const void*>(&lstm_bwd_persistent_kernel<KT, NRT, 32>); break;
+      case 64: if constexpr (WF_DV(64)) f = reinterpret_cast<const void*>(&lstm_bwd_persistent_kernel<KT, NRT, 64>); break;
+      case 96: if constexpr (WF_DV(96)) f = reinterpret_cast<const void*>(&lstm_bwd_persistent_kernel<KT, NRT, 96>); break;
+      case 128: if constexpr (WF_DV(128)) f = reinterpret_cast<const void*>(&lstm_bwd_persistent_kernel<KT, NRT, 128>); break;
+      case 256: if constexpr (WF_DV(256)) f = reinterpret_cast<const void*>(&lstm_bwd_persistent_kernel<KT, NRT, 256>); break;
+      case 512: if constexpr (WF_DV(512)) f = reinterpret_cast<const void*>(&lstm_bwd_persistent_kernel<KT, NRT, 512>); break;  // 8-part epilogue
       default: break;
     }
   }

@@ -25,6 +25,25 @@
 //    XCD-aware block map puts a row block's NB workgroups on one XCD (speed only).
 //  * every spin is bounded: on timeout the error word is set and all workgroups drain.
 #pragma once
+// diagnostic builds: WELLFLOW_DIAG_BUILD=1 instantiates every timing variant, =N or =N,M,..
+// only those WELLFLOW_PF_DBG values (fewer instantiations, minutes less to build)
+#ifdef WF_DIAG
+#ifndef WF_DIAG_SET
+#define WF_DIAG_SET 0
+#endif
+#ifndef WF_DIAG_SET_DEFINED
+#define WF_DIAG_SET_DEFINED
+namespace wf {
+constexpr int kDiagSet[] = {WF_DIAG_SET};
+constexpr bool diag_variant(int v) {
+  for (int x : kDiagSet)
+    if (x == 0 || x == v) return true;
+  return false;
+}
+}  // namespace wf
+#endif
+#define WF_DV(v) (::wf::diag_variant(v))
+#endif
 #include <cstdlib>
 
 #include "gemm_core.h"
@@ -108,7 +127,7 @@ __global__ __launch_bounds__(256, 1) void lstm_fwd_persistent_kernel(
   const int ub = n * 4 + wid;                // 16-unit block of this wave
   const int u = ub * 16 + l15;               // hidden unit of this lane
   const int loff_c = ub * 256 + lane * 4;    // float offset of this lane's C slot in a FN row block
-  const int loff_s = ub * 1024 + lane * 16;  // bf16 offset of this lane's S slot in a FN row block
+  const int loff_s = ub * 1024 + lane * 8;  // bf16 offset of this lane's first S half in a FN row block
   const int loff_h = (((int)threadIdx.x >> 3) * KA + ((int)threadIdx.x & 7) * 8) * 2;  // h publish
   // error word: word 0 of the per-launch block (word 1 in the round-2 layout A/B, PF_DBG bit 20)
   gu32* err = (gu32*)(sync + ((d.dbg >> 20) & 1));
@@ -347,8 +366,8 @@ __global__ __launch_bounds__(256, 1) void lstm_fwd_persistent_kernel(
               make_float4(cv[i][0], cv[i][1], cv[i][2], cv[i][3]);
         } else {
           const int hf = (k - 2) & 1;
-          uint4* sp = reinterpret_cast<uint4*>(St + (2 * e + i) * HB * 1024 + loff_s);
-          sp[hf] = make_uint4(pk[i][4 * hf], pk[i][4 * hf + 1], pk[i][4 * hf + 2], pk[i][4 * hf + 3]);
+          uint4* sp = reinterpret_cast<uint4*>(St + (2 * e + i) * HB * 1024 + loff_s + hf * kFnSHalf);
+          *sp = make_uint4(pk[i][4 * hf], pk[i][4 * hf + 1], pk[i][4 * hf + 2], pk[i][4 * hf + 3]);
         }
       }
     };
@@ -374,9 +393,9 @@ __global__ __launch_bounds__(256, 1) void lstm_fwd_persistent_kernel(
         if constexpr (!(DBG & 4)) {
           *reinterpret_cast<float4*>(cnext + (2 * e + i) * HB * 256 + loff_c) =
               make_float4(cv[i][0], cv[i][1], cv[i][2], cv[i][3]);
-          uint4* sp = reinterpret_cast<uint4*>(St + (2 * e + i) * HB * 1024 + loff_s);
-          sp[0] = make_uint4(pk[i][0], pk[i][1], pk[i][2], pk[i][3]);
-          sp[1] = make_uint4(pk[i][4], pk[i][5], pk[i][6], pk[i][7]);
+          bf16_t* sb = St + (2 * e + i) * HB * 1024 + loff_s;
+          *reinterpret_cast<uint4*>(sb) = make_uint4(pk[i][0], pk[i][1], pk[i][2], pk[i][3]);
+          *reinterpret_cast<uint4*>(sb + kFnSHalf) = make_uint4(pk[i][4], pk[i][5], pk[i][6], pk[i][7]);
         }
       }
 #pragma unroll
@@ -486,7 +505,8 @@ __global__ __launch_bounds__(256, 1) void lstm_fwd_persistent_kernel(
         constexpr int el = 2 * (m / 36) + (m & 1), st = (m % 36) / 2, ei_ = (el >> 2) & 1, er = el & 3;
         EpiMicro& E = e2[m & 1];
         const bf16x8& A = a[kt & 1][i];
-        if constexpr (m >= 144) {  // KT > 18: the 144 stages are placed, the rest are plain MFMAs
+        if constexpr (m >= 144 || (DBG & 8192) != 0) {  // KT > 18: the 144 stages are placed, the rest are
+                                                        // plain MFMAs (DBG 8192: timing only, no stages)
           if constexpr (kt < KTA)
             asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc[i][j]) : "v"(A), "a"(w[kt][j]));
           else
@@ -566,6 +586,9 @@ __global__ __launch_bounds__(256, 1) void lstm_fwd_persistent_kernel(
       }
       static_for<0, KT>([&](auto kc) {
         constexpr int kt = decltype(kc)::value;
+        if constexpr ((DBG & 16) != 0 && kt < 20) {  // timeline: k-tile starts of chunk 3, slots 42..
+          if (c == 3) stamp(t, 42 + kt);
+        }
         if constexpr (CXX_FRAG) {
           if constexpr (kt + 1 < KT)
             for (int i = 0; i < 2; ++i)
@@ -662,7 +685,7 @@ __global__ __launch_bounds__(256, 1) void lstm_fwd_persistent_kernel(
       }
       if constexpr (KT >= 16 && (DBG & 64)) {
         if (c > 0) rotate(cv);
-      } else if (c > 0) {
+      } else if (c > 0 && (DBG & 16384) == 0) {  // DBG 16384: timing only, no stores / publish
         epi_store(c - 1, cv, pk, hv);
         stamp(t, 5 + 5 * c);
         publish(c - 1);
@@ -714,15 +737,18 @@ static int launch_pf(bf16_t* XH, const bf16_t* Wp, float* Cst, bf16_t* S, unsign
   }
 #ifdef WF_DIAG  // timing-only diagnostic builds (WELLFLOW_PF_DBG >= 2; WELLFLOW_DIAG_BUILD=1)
   if constexpr (KT == 18 && NC == 8) {
-    if (d.dbg == 2) f = reinterpret_cast<const void*>(&lstm_fwd_persistent_kernel<KT, NC, 2>);
-    if (d.dbg == 4) f = reinterpret_cast<const void*>(&lstm_fwd_persistent_kernel<KT, NC, 4>);
-    if (d.dbg == 14) f = reinterpret_cast<const void*>(&lstm_fwd_persistent_kernel<KT, NC, 14>);
-    if (d.dbg == 16) f = reinterpret_cast<const void*>(&lstm_fwd_persistent_kernel<KT, NC, 16>);
-    if (d.dbg == 48) f = reinterpret_cast<const void*>(&lstm_fwd_persistent_kernel<KT, NC, 48>);
-    if (d.dbg == 64) f = reinterpret_cast<const void*>(&lstm_fwd_persistent_kernel<KT, NC, 64>);  // stores inside the loop
-    if (d.dbg == 1024) f = reinterpret_cast<const void*>(&lstm_fwd_persistent_kernel<KT, NC, 1024>);  // chunk 1 at the step top
-    if (d.dbg == 512) f = reinterpret_cast<const void*>(&lstm_fwd_persistent_kernel<KT, NC, 512>);  // pinned micro-stages
-    if (d.dbg == 128) f = reinterpret_cast<const void*>(&lstm_fwd_persistent_kernel<KT, NC, 128>);  // half-element epilogue
+    if constexpr (WF_DV(2)) { if (d.dbg == 2) f = reinterpret_cast<const void*>(&lstm_fwd_persistent_kernel<KT, NC, 2>); }
+    if constexpr (WF_DV(4)) { if (d.dbg == 4) f = reinterpret_cast<const void*>(&lstm_fwd_persistent_kernel<KT, NC, 4>); }
+    if constexpr (WF_DV(14)) { if (d.dbg == 14) f = reinterpret_cast<const void*>(&lstm_fwd_persistent_kernel<KT, NC, 14>); }
+    if constexpr (WF_DV(16)) { if (d.dbg == 16) f = reinterpret_cast<const void*>(&lstm_fwd_persistent_kernel<KT, NC, 16>); }
+    if constexpr (WF_DV(48)) { if (d.dbg == 48) f = reinterpret_cast<const void*>(&lstm_fwd_persistent_kernel<KT, NC, 48>); }
+    if constexpr (WF_DV(64)) { if (d.dbg == 64) f = reinterpret_cast<const void*>(&lstm_fwd_persistent_kernel<KT, NC, 64>); }  // stores inside the loop
+    if constexpr (WF_DV(1024)) { if (d.dbg == 1024) f = reinterpret_cast<const void*>(&lstm_fwd_persistent_kernel<KT, NC, 1024>); }  // chunk 1 at the step top
+    if constexpr (WF_DV(512)) { if (d.dbg == 512) f = reinterpret_cast<const void*>(&lstm_fwd_persistent_kernel<KT, NC, 512>); }  // pinned micro-stages
+    if constexpr (WF_DV(128)) { if (d.dbg == 128) f = reinterpret_cast<const void*>(&lstm_fwd_persistent_kernel<KT, NC, 128>); }  // half-element epilogue
+    if constexpr (WF_DV(8192)) { if (d.dbg == 8192) f = reinterpret_cast<const void*>(&lstm_fwd_persistent_kernel<KT, NC, 8192>); }  // no cell math in the loop
+    if constexpr (WF_DV(16384)) { if (d.dbg == 16384) f = reinterpret_cast<const void*>(&lstm_fwd_persistent_kernel<KT, NC, 16384>); }  // no stores / publish
+    if constexpr (WF_DV(24576)) { if (d.dbg == 24576) f = reinterpret_cast<const void*>(&lstm_fwd_persistent_kernel<KT, NC, 24576>); }  // neither
   }
 #endif
   void* args[] = {&XH, &Wp, &Cst, &S, &sync, &stat, &d};

@@ -32,3 +32,6 @@ d = np.diff(rel[:, 2:42].reshape(256, 8, 5)[:, 1:, :], axis=2).mean(axis=(0, 1))
 print("per chunk mean (c >= 1): wait %.2f  mfma %.2f  store %.2f  publish %.2f us" % tuple(d))
 top = rel[:, 2:42:5]
 print("chunk-to-chunk mean %.2f us" % np.diff(top, axis=1).mean())
+kt = rel[:, 42:42 + 18]  # chunk 3: k-tile starts (after_wait .. mfma_done)
+seg = np.diff(np.concatenate([kt, rel[:, 3 + 5 * 3 + 1:3 + 5 * 3 + 2]], axis=1), axis=1).mean(axis=0)
+print("chunk 3 per k-tile (us):", " ".join("%.3f" % v for v in seg))
