@@ -127,7 +127,10 @@ __global__ __launch_bounds__(256, 1) void lstm_fwd_persistent_kernel(
   const int ub = n * 4 + wid;                // 16-unit block of this wave
   const int u = ub * 16 + l15;               // hidden unit of this lane
   const int loff_c = ub * 256 + lane * 4;    // float offset of this lane's C slot in a FN row block
-  const int loff_s = ub * 1024 + lane * 8;  // bf16 offset of this lane's first S half in a FN row block
+  // bf16 offset of this lane's first S half in a FN row block (DBG 32768, timing only: the round-2
+  // lane-interleaved 32-B slot, second half 16 B after the first)
+  constexpr int SHALF = (DBG & 32768) ? 8 : kFnSHalf;
+  const int loff_s = ub * 1024 + lane * ((DBG & 32768) ? 16 : 8);
   const int loff_h = (((int)threadIdx.x >> 3) * KA + ((int)threadIdx.x & 7) * 8) * 2;  // h publish
   // error word: word 0 of the per-launch block (word 1 in the round-2 layout A/B, PF_DBG bit 20)
   gu32* err = (gu32*)(sync + ((d.dbg >> 20) & 1));
@@ -186,8 +189,9 @@ __global__ __launch_bounds__(256, 1) void lstm_fwd_persistent_kernel(
   for (int t = 0; t < d.T; ++t) {
     stamp(t, 0);
     if (t > 0) {
-      // ---- publish step t-1 (every wave drained its sc1 h stores) and wait for the row block
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      // ---- publish step t-1 (every wave drained its sc1 h stores: issued before the drain's
+      // NSTORE - 1 C / S stores, which may stay in flight) and wait for the row block
+      wait_vmcnt<(DBG & 65536) ? 0 : NSTORE - 1>();
       __builtin_amdgcn_s_barrier();
       asm volatile("" ::: "memory");
       // thread 0's view of the wait, kept for the exit record (persistent_guard.h)
@@ -366,7 +370,7 @@ __global__ __launch_bounds__(256, 1) void lstm_fwd_persistent_kernel(
               make_float4(cv[i][0], cv[i][1], cv[i][2], cv[i][3]);
         } else {
           const int hf = (k - 2) & 1;
-          uint4* sp = reinterpret_cast<uint4*>(St + (2 * e + i) * HB * 1024 + loff_s + hf * kFnSHalf);
+          uint4* sp = reinterpret_cast<uint4*>(St + (2 * e + i) * HB * 1024 + loff_s + hf * SHALF);
           *sp = make_uint4(pk[i][4 * hf], pk[i][4 * hf + 1], pk[i][4 * hf + 2], pk[i][4 * hf + 3]);
         }
       }
@@ -395,7 +399,7 @@ __global__ __launch_bounds__(256, 1) void lstm_fwd_persistent_kernel(
               make_float4(cv[i][0], cv[i][1], cv[i][2], cv[i][3]);
           bf16_t* sb = St + (2 * e + i) * HB * 1024 + loff_s;
           *reinterpret_cast<uint4*>(sb) = make_uint4(pk[i][0], pk[i][1], pk[i][2], pk[i][3]);
-          *reinterpret_cast<uint4*>(sb + kFnSHalf) = make_uint4(pk[i][4], pk[i][5], pk[i][6], pk[i][7]);
+          *reinterpret_cast<uint4*>(sb + SHALF) = make_uint4(pk[i][4], pk[i][5], pk[i][6], pk[i][7]);
         }
       }
 #pragma unroll
@@ -719,8 +723,21 @@ __global__ __launch_bounds__(256, 1) void lstm_fwd_persistent_kernel(
       unsigned pk[2][8], hv[2][4];
 #pragma unroll
       for (int e = 0; e < 8; ++e) epi_elem(e >> 2, e & 3, cv, pk, hv);
-      epi_store(NC - 1, cv, pk, hv);
-      publish(NC - 1);
+      // h first (the only bytes other workgroups read in this launch), then the C / S stores,
+      // so the step-top hand-off drains only the h store (vmcnt(NSTORE - 1)) and the last
+      // chunk's C / S stores complete behind the hand-off instead of in front of it
+      if constexpr ((DBG & 65536) != 0) {  // A/B: the round-2 order (stores, then h)
+        epi_store(NC - 1, cv, pk, hv);
+        publish(NC - 1);
+      } else {
+        epi_h(hv);
+        publish(NC - 1);
+        if constexpr (!(DBG & 4)) {
+#pragma unroll
+          for (int k = 0; k < 6; ++k) epi_cs(NC - 1, k, cv, pk);
+        }
+        rotate(cv);
+      }
     }
   }
   // completion count: every workgroup that ran all T steps adds T to DONE; any early exit
@@ -734,6 +751,7 @@ static int launch_pf(bf16_t* XH, const bf16_t* Wp, float* Cst, bf16_t* S, unsign
   const void* f = reinterpret_cast<const void*>(&lstm_fwd_persistent_kernel<KT, NC>);
   if constexpr (KT == 18 && NC == 8) {  // production-correct A/B variants (WELLFLOW_PF_DBG)
     if (d.dbg == 4096) f = reinterpret_cast<const void*>(&lstm_fwd_persistent_kernel<KT, NC, 4096>);
+    if (d.dbg == 65536) f = reinterpret_cast<const void*>(&lstm_fwd_persistent_kernel<KT, NC, 65536>);
   }
 #ifdef WF_DIAG  // timing-only diagnostic builds (WELLFLOW_PF_DBG >= 2; WELLFLOW_DIAG_BUILD=1)
   if constexpr (KT == 18 && NC == 8) {
@@ -749,6 +767,7 @@ static int launch_pf(bf16_t* XH, const bf16_t* Wp, float* Cst, bf16_t* S, unsign
     if constexpr (WF_DV(8192)) { if (d.dbg == 8192) f = reinterpret_cast<const void*>(&lstm_fwd_persistent_kernel<KT, NC, 8192>); }  // no cell math in the loop
     if constexpr (WF_DV(16384)) { if (d.dbg == 16384) f = reinterpret_cast<const void*>(&lstm_fwd_persistent_kernel<KT, NC, 16384>); }  // no stores / publish
     if constexpr (WF_DV(24576)) { if (d.dbg == 24576) f = reinterpret_cast<const void*>(&lstm_fwd_persistent_kernel<KT, NC, 24576>); }  // neither
+    if constexpr (WF_DV(32768)) { if (d.dbg == 32768) f = reinterpret_cast<const void*>(&lstm_fwd_persistent_kernel<KT, NC, 32768>); }  // round-2 S slots
   }
 #endif
   void* args[] = {&XH, &Wp, &Cst, &S, &sync, &stat, &d};
