@@ -135,6 +135,8 @@ wf::LstmDims lstm_dims(int64_t B, int64_t T, int64_t F, int64_t KX, int64_t H) {
   d.dbg = pd != nullptr ? std::atoi(pd) : 0;
   const char* sl = std::getenv("WELLFLOW_SPIN_LIMIT");  // tests: force the hand-off timeout path
   d.spin_limit = sl != nullptr ? (unsigned)std::strtoul(sl, nullptr, 10) : 0u;
+  const char* ft = std::getenv("WELLFLOW_FORCE_TIMEOUT");  // tests: every hand-off wait trips its bound
+  if (ft != nullptr && ft[0] == '1') d.dbg |= 1 << 21;
   return d;
 }
 

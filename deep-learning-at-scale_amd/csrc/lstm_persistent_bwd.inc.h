@@ -196,7 +196,8 @@ __global__ __launch_bounds__(256, 1) void lstm_bwd_persistent_kernel(
       asm volatile("" ::: "memory");
       // thread 0's view of the wait, kept for the exit record (persistent_guard.h)
       unsigned why = 0, seen_err = 0, seen_cnt = 0;
-      const unsigned target = (unsigned)(NB * s);
+      // (d.dbg bit 21, tests: an unreachable target, so the bounded spin trips deterministically)
+      const unsigned target = (unsigned)(NB * s) + (((d.dbg >> 21) & 1u) << 30);
       if (threadIdx.x == 0) {
         if constexpr ((DBG & 64) != 0) {  // plain DG stores: publish them with an agent release
           __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");

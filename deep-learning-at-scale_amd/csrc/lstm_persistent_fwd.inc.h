@@ -194,9 +194,11 @@ __global__ __launch_bounds__(256, 1) void lstm_fwd_persistent_kernel(
       wait_vmcnt<(DBG & 65536) ? 0 : NSTORE - 1>();
       __builtin_amdgcn_s_barrier();
       asm volatile("" ::: "memory");
+      stamp(t, 62);  // h stores drained, workgroup arrived
       // thread 0's view of the wait, kept for the exit record (persistent_guard.h)
       unsigned why = 0, seen_err = 0, seen_cnt = 0;
-      const unsigned target = (unsigned)(NB * t);
+      // (d.dbg bit 21, tests: an unreachable target, so the bounded spin trips deterministically)
+      const unsigned target = (unsigned)(NB * t) + (((d.dbg >> 21) & 1u) << 30);
       if (threadIdx.x == 0) {
         __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         unsigned spins = 0;
@@ -213,6 +215,7 @@ __global__ __launch_bounds__(256, 1) void lstm_fwd_persistent_kernel(
           }
           __builtin_amdgcn_s_sleep(2);
         }
+        stamp(t, 63);  // row block complete (poll matched)
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         const int ok = why == 0 ? 1 : 0;
@@ -726,6 +729,9 @@ __global__ __launch_bounds__(256, 1) void lstm_fwd_persistent_kernel(
       // h first (the only bytes other workgroups read in this launch), then the C / S stores,
       // so the step-top hand-off drains only the h store (vmcnt(NSTORE - 1)) and the last
       // chunk's C / S stores complete behind the hand-off instead of in front of it
+      // Deferring these six stores past the next step's hand-off (after chunk 0's loop, which
+      // stores nothing) measured neutral to worse: 1470-1486 us deferred vs 1454-1482 here
+      // (profiles/r3/ab_defer_drain_stores.txt). The write burst is not on the critical path.
       if constexpr ((DBG & 65536) != 0) {  // A/B: the round-2 order (stores, then h)
         epi_store(NC - 1, cv, pk, hv);
         publish(NC - 1);

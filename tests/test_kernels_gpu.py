@@ -320,10 +320,12 @@ def test_persistent_timeout_is_sticky_and_raises(monkeypatch):
     x, y = synth_lstm_batch(B, T, F, seed=0)
     x, y = x.to(DEV), y.to(DEV)
     monkeypatch.setenv("WELLFLOW_SPIN_LIMIT", "1")
+    monkeypatch.setenv("WELLFLOW_FORCE_TIMEOUT", "1")
     eng.forward_backward(x, y, 1.0 / B)
     torch.cuda.synchronize()
-    assert eng.persistent_error() != 0, "a 1-poll spin bound should trip on a 256-workgroup grid"
+    assert eng.persistent_error() != 0, "an unreachable target with a 1-poll spin bound must trip"
     monkeypatch.delenv("WELLFLOW_SPIN_LIMIT")
+    monkeypatch.delenv("WELLFLOW_FORCE_TIMEOUT")
     eng.forward_backward(x, y, 1.0 / B)  # a clean launch: resets its per-launch block, keeps the STAT block
     torch.cuda.synchronize()
     with pytest.raises(RuntimeError, match="spin bound"):
@@ -334,11 +336,13 @@ def test_persistent_timeout_is_sticky_and_raises(monkeypatch):
     eng.check_device_errors()
     # the production step raises on its first steps
     monkeypatch.setenv("WELLFLOW_SPIN_LIMIT", "1")
+    monkeypatch.setenv("WELLFLOW_FORCE_TIMEOUT", "1")
     opt = FlatAdam(eng.params, eng.grads, lr=1e-3, zero_grads=True)
     run = StepRunner(eng, opt, DistContext(device=torch.device(DEV)), 1.0 / B, lambda k: (x, y), graph=False)
     with pytest.raises(RuntimeError, match="spin bound"):
         run.run()
     monkeypatch.delenv("WELLFLOW_SPIN_LIMIT")
+    monkeypatch.delenv("WELLFLOW_FORCE_TIMEOUT")
     eng.reset_device_errors()
 
 
@@ -392,10 +396,14 @@ def test_persistent_exit_record(monkeypatch):
     eng.params.copy_(init_lstm_flat(F, H, seed=0).to(DEV))
     eng.sync_weights()
     x, y = synth_lstm_batch(B, T, F, seed=0)
+    # an unreachable hand-off target + a 1-poll bound: the exit no longer depends on the grid's
+    # timing (a faster step top left every workgroup inside a 1-poll bound)
     monkeypatch.setenv("WELLFLOW_SPIN_LIMIT", "1")
+    monkeypatch.setenv("WELLFLOW_FORCE_TIMEOUT", "1")
     eng.forward_backward(x.to(DEV), y.to(DEV), 1.0 / B)
     torch.cuda.synchronize()
     monkeypatch.delenv("WELLFLOW_SPIN_LIMIT")
+    monkeypatch.delenv("WELLFLOW_FORCE_TIMEOUT")
     fw = eng.persistent_stats()["forward"]
     assert fw["sticky"] == 1 and fw["exits"] > 0 and fw["done"] < fw["expect"], fw
     rec = fw["first_exit"]

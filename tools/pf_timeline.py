@@ -26,6 +26,8 @@ base = st[:, 0:1]
 rel = (st - base) / 1000.0  # us from step start
 names = ["sync_end"] + [f"c{c}_{k}" for c in range(8) for k in ("top", "after_wait", "mfma_done", "epi_done", "published")]
 print("step 10, us since step start (mean / max over 256 workgroups)")
+print(f"{'arrived':16s} {rel[:, 62].mean():8.2f} {rel[:, 62].max():8.2f}")
+print(f"{'poll_matched':16s} {rel[:, 63].mean():8.2f} {rel[:, 63].max():8.2f}")
 for i, nm in enumerate(names, start=1):
     print(f"{nm:16s} {rel[:, i].mean():8.2f} {rel[:, i].max():8.2f}")
 d = np.diff(rel[:, 2:42].reshape(256, 8, 5)[:, 1:, :], axis=2).mean(axis=(0, 1))  # chunks >= 1
