@@ -313,11 +313,13 @@ bool lstm_backward_dw(const at::Tensor& WhhT, const at::Tensor& XH, const at::Te
     e.ldo = KA;
     e.atomic = 1;
     // WELLFLOW_DW_BIG: 0 = 128x128 tile, 1 = 256x128 8-wave, 2 = 128x288 4-wave,
-    // 3 (default) = 256x192 8-wave (tools/tune_lstm.py, B = 8192, split-K 32:
-    // 1.35 / 1.60 / 1.28 ms for 1 / 2 / 3); shapes a tile cannot take fall back to 256x128
+    // 3 = 256x192 8-wave (tools/tune_lstm.py, B = 8192, split-K 32: 1.35 / 1.60 / 1.28 ms for
+    // 1 / 2 / 3), 4 / 5 = 256x192 with a 5- / 4-slot 32-deep ring, 6 = 256x192 with staggered
+    // wave groups, 7 (default) = 256x288 4-slot 32-deep ring (tools/dw_tiles.py: 1.107 ms vs
+    // 1.166 for 3, 1.149 for 4, 1.307 for 6); shapes a tile cannot take fall back to 256x128
     static const int big = [] {
       const char* v = std::getenv("WELLFLOW_DW_BIG");
-      return v == nullptr ? 3 : std::atoi(v);
+      return v == nullptr ? 7 : std::atoi(v);
     }();
     e.big_tile = big;
     const bf16_t* A = bfp(DG) + (size_t)t0 * B * G;

@@ -252,8 +252,119 @@ static void launch_dw_192(const bf16_t* A, long lda, const bf16_t* B, long ldb, 
                        N, kchunk, tiles, e.outF, e.ldo, e.alpha);
 }
 
+// 256x192, 8 waves of 64x96, 32-deep half steps through an NSLOT-deep ring (gemm_core.h
+// gemm_mainloop_glds_h): the same tile as launch_dw_192 with its DMA issued NSLOT - 1 half
+// steps ahead instead of one 64-deep step
+template <int BM, int BN, int NSLOT, int WM, int WN, int PRIO, int BKD = 32>
+__global__ __launch_bounds__(64 * WM * WN) void gemm_dw_h_kernel(const bf16_t* __restrict__ A, long lda,
+                                                        const bf16_t* __restrict__ B, long ldb, int N,
+                                                        int kchunk, int tiles, float* __restrict__ out,
+                                                        long ldo, float alpha) {
+  using C = GemmCfg<BM, BN, MN_CONTIG, MN_CONTIG, WM, WN>;
+  constexpr int STAGE = (BM + BN) * BKD * 2;
+  __shared__ __attribute__((aligned(16))) char smem[NSLOT * STAGE];
+  const int tiles_n = N / BN;
+  const int L = xcd_remap(blockIdx.x, gridDim.x);
+  const int split = L / tiles, t = L % tiles;
+  const int m0 = (t / tiles_n) * BM, n0 = (t % tiles_n) * BN;
+  f32x4 acc[C::TM][C::TN];
+  gemm_mainloop_glds_h<C, NSLOT, PRIO, BKD>(A, lda, B, ldb, split * kchunk, kchunk / BKD, m0, n0, smem, acc);
+  const AccCoord<C> cc(m0, n0);
+#pragma unroll
+  for (int j = 0; j < C::TN; ++j)
+#pragma unroll
+    for (int i = 0; i < C::TM; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        atomicAdd(out + (size_t)cc.row(i, r) * ldo + cc.col(j), alpha * acc[i][j][r]);
+}
+
+// the same tile and 2-slot 64-deep ring as launch_dw_192, wave groups staggered by a barrier
+template <int BM, int BN, int WM, int WN>
+__global__ __launch_bounds__(64 * WM * WN) void gemm_dw_s_kernel(const bf16_t* __restrict__ A, long lda,
+                                                        const bf16_t* __restrict__ B, long ldb, int N,
+                                                        int kchunk, int tiles, float* __restrict__ out,
+                                                        long ldo, float alpha) {
+  using C = GemmCfg<BM, BN, MN_CONTIG, MN_CONTIG, WM, WN>;
+  __shared__ __attribute__((aligned(16))) char smem[2 * C::STAGE];
+  const int tiles_n = N / BN;
+  const int L = xcd_remap(blockIdx.x, gridDim.x);
+  const int split = L / tiles, t = L % tiles;
+  const int m0 = (t / tiles_n) * BM, n0 = (t % tiles_n) * BN;
+  f32x4 acc[C::TM][C::TN];
+  gemm_mainloop_stag<C>(A, lda, B, ldb, split * kchunk, kchunk / 64, m0, n0, smem, acc);
+  const AccCoord<C> cc(m0, n0);
+#pragma unroll
+  for (int j = 0; j < C::TN; ++j)
+#pragma unroll
+    for (int i = 0; i < C::TM; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        atomicAdd(out + (size_t)cc.row(i, r) * ldo + cc.col(j), alpha * acc[i][j][r]);
+}
+
+static void launch_dw_192h(const bf16_t* A, long lda, const bf16_t* B, long ldb, int M, int N, int K,
+                           int ksplit, int nslot, const GemmEpilogue& e, hipStream_t s) {
+  constexpr int BM = 256, BN = 192;
+  const int tiles = (M / BM) * (N / BN);
+  int nsplit = ksplit;
+  while (nsplit > 1 && K % (64 * nsplit) != 0) --nsplit;
+  const int kchunk = K / nsplit;
+  const dim3 grid(tiles * nsplit);
+  if (nslot == 2)  // staggered wave groups (gemm_mainloop_stag)
+    hipLaunchKernelGGL((gemm_dw_s_kernel<BM, BN, 4, 2>), grid, dim3(512), 0, s, A, lda, B, ldb, N, kchunk, tiles,
+                       e.outF, e.ldo, e.alpha);
+  else if (nslot == 5)
+    hipLaunchKernelGGL((gemm_dw_h_kernel<BM, BN, 5, 4, 2, 1>), grid, dim3(512), 0, s, A, lda, B, ldb, N, kchunk,
+                       tiles, e.outF, e.ldo, e.alpha);
+  else
+    hipLaunchKernelGGL((gemm_dw_h_kernel<BM, BN, 4, 4, 2, 1>), grid, dim3(512), 0, s, A, lda, B, ldb, N, kchunk,
+                       tiles, e.outF, e.ldo, e.alpha);
+}
+
+// 256x288, 8 waves of 64x144, 4-slot 32-deep ring (136 KiB; a 2-stage 64-deep ring spilled 61 VGPRs)
+// (default: 1.107 vs 1.166 ms for 256x192 standalone, 1.150 vs 1.178 ms inside the bench step): N = 576 = 2 x 288, 24 % more
+// FLOP per staged byte than 256x192 (the dW loop's LDS-DMA bytes per CU per step, not its
+// MFMAs or the DMA latency, track its time across tiles: 256x128 1.33, 256x192 1.17 ms)
+static void launch_dw_288w(const bf16_t* A, long lda, const bf16_t* B, long ldb, int M, int N, int K,
+                           int ksplit, const GemmEpilogue& e, hipStream_t s) {
+  constexpr int BM = 256, BN = 288;
+  const int tiles = (M / BM) * (N / BN);
+  // one workgroup per CU: 16 tiles x split-K 16 on 256 CUs (tools/dw_tiles.py, B = 8192:
+  // split-K 16 / 32 / 64 = 1.107 / 1.115 / 1.160 ms)
+  static const int cus = [] {
+    int dev = 0, n = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      return 256;
+    return n;
+  }();
+  if (ksplit * tiles > cus && cus / tiles >= 1) ksplit = cus / tiles;
+  int nsplit = ksplit;
+  while (nsplit > 1 && K % (64 * nsplit) != 0) --nsplit;
+  const int kchunk = K / nsplit;
+  hipLaunchKernelGGL((gemm_dw_h_kernel<BM, BN, 4, 4, 2, 1, 32>), dim3(tiles * nsplit), dim3(512), 0, s, A, lda, B,
+                     ldb, N, kchunk, tiles, e.outF, e.ldo, e.alpha);
+}
+
 void launch_gemm(const bf16_t* A, long lda, int a_mn, const bf16_t* B, long ldb, int b_mn, int M,
                  int N, int K, int ksplit, const GemmEpilogue& e, hipStream_t s, bool glds_ok) {
+  if (a_mn && b_mn && glds_ok && e.atomic && e.big_tile == 7 && M % 256 == 0 && K % 64 == 0) {
+    if (N % 288 == 0) {
+      launch_dw_288w(A, lda, B, ldb, M, N, K, ksplit < 1 ? 1 : ksplit, e, s);
+      return;
+    }
+    if (N % 192 == 0) {  // e.g. H = 128 (KA = 192): the 256x192 tile
+      launch_dw_192(A, lda, B, ldb, M, N, K, ksplit < 1 ? 1 : ksplit, e, s);
+      return;
+    }
+  }
+  // 4 / 5: the 256x192 tile with the 5- / 4-slot half-step ring; 6: staggered wave groups
+  if (a_mn && b_mn && glds_ok && e.atomic && (e.big_tile >= 4 && e.big_tile <= 6) && M % 256 == 0 &&
+      N % 192 == 0 && K % 64 == 0) {
+    launch_dw_192h(A, lda, B, ldb, M, N, K, ksplit < 1 ? 1 : ksplit,
+                   e.big_tile == 4 ? 5 : (e.big_tile == 5 ? 4 : 2), e, s);
+    return;
+  }
   if (a_mn && b_mn && glds_ok && e.atomic && e.big_tile == 2 && M % 128 == 0 && N % 288 == 0 && K % 64 == 0) {
     launch_dw_288(A, lda, B, ldb, M, N, K, ksplit < 1 ? 1 : ksplit, e, s);
     return;

@@ -519,6 +519,247 @@ __device__ __forceinline__ void gemm_mainloop_glds2(const bf16_t* __restrict__ A
   asm volatile("" ::: "memory");
 }
 
+// ----------------------------------------------------------------------------------------
+// Half-step ring for the MN x MN weight-gradient GEMM: 32-deep K steps through an NSLOT-deep
+// LDS ring. With 64-deep steps the 256x192 tile fits only 2 stages in 160 KiB, so each step's
+// LDS-DMA had exactly one step of MFMA work (~1.5k cycles per SIMD) to land and the
+// vmcnt(0) before every barrier exposed the rest of its latency (PMC: 28 % wave-wait, 54 % MFMA
+// busy). 32-deep slots of the same tile (28 KiB) fit 5 deep: a piece is issued NSLOT - 1 half
+// steps ahead of its use. Pieces that do not split evenly over the waves (the 192-wide image
+// is 12 pieces per half step) go to the low waves, and each wave counts its own in vmcnt.
+template <int R, int L, int NT, int BKD>
+struct GldsOpH {
+  static_assert(L == MN_CONTIG, "half-step ring: MN-contiguous operands only");
+  static constexpr int BYTES = R * BKD * 2;
+  static constexpr int PIECES = BYTES / 1024;
+  static constexpr int NW = NT / 64;
+  static constexpr int MAXPW = (PIECES + NW - 1) / NW;  // pieces of the low waves
+  static constexpr int REM = PIECES % NW;               // waves < REM issue MAXPW, the rest MAXPW - 1
+  static_assert(BYTES % 1024 == 0 && PIECES >= NW, "tile image must be whole 1-KiB pieces, >= 1 per wave");
+  using SW = MnSwz<R>;
+  // buffer-resource form (buffer_load ... lds): a 32-bit per-lane voffset and a scalar step
+  // offset, no 64-bit per-lane addresses (global_load_lds with 64-bit VGPR addresses spilled
+  // the 288-wide tile's kernel). The workgroup's whole K range is < 2 GiB from its origin.
+  unsigned src[MAXPW];
+  __amdgpu_buffer_rsrc_t rsrc;
+  int kstep_bytes;
+
+  __device__ __forceinline__ void init(const bf16_t* p, long ld, int row0, int kbeg, int wid, int lane) {
+#pragma unroll
+    for (int i = 0; i < MAXPW; ++i) {
+      const int o = (i * NW + wid) * 1024 + lane * 16;
+      const int k = o / (R * 2), b = o % (R * 2);
+      const int col = (SW::data(b >> 5, SW::hk(k)) << 4) + (((b >> 4) & 1) << 3);
+      src[i] = (unsigned)(((long)k * ld + col) * 2);
+    }
+    rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16_t*>(p + (size_t)kbeg * ld + row0), 0, 0x7FFFFFFF,
+                                             0x00020000);
+    kstep_bytes = (int)(BKD * ld * 2);
+  }
+  __device__ __forceinline__ void issue(int step, char* lds_tile, int wid) const {
+    const int so = step * kstep_bytes;
+#pragma unroll
+    for (int i = 0; i < MAXPW; ++i) {
+      if (i + 1 < MAXPW || REM == 0 || wid < REM)  // wave-uniform
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (lds_void*)(lds_tile + (i * NW + wid) * 1024), 16, (int)src[i],
+                                                 so, 0, 0);
+    }
+  }
+};
+
+// BKD = 64 with NSLOT = 2: the plain 2-stage ring of gemm_mainloop_glds2, for tiles whose
+// pieces do not split evenly over the waves (the 288-wide image: 36 pieces per 64-deep step)
+template <class C, int NSLOT, int PRIO = 0, int BKD = 32>
+__device__ __forceinline__ void gemm_mainloop_glds_h(const bf16_t* __restrict__ A, long lda,
+                                                     const bf16_t* __restrict__ B, long ldb, int kbeg,
+                                                     int nh, int m0, int n0, char* smem,
+                                                     f32x4 (&acc)[C::TM][C::TN]) {
+  static_assert(BKD == 32 || BKD == 64, "32- or 64-deep steps");
+  static_assert(NSLOT >= 2 && NSLOT <= 6, "2..6 slots");
+  using OA = GldsOpH<C::BM, C::LA_, C::NT, BKD>;
+  using OB = GldsOpH<C::BN, C::LB_, C::NT, BKD>;
+  static_assert(OA::REM == 0 || OB::REM == 0, "at most one operand with an uneven piece split");
+  constexpr int STAGE = OA::BYTES + OB::BYTES;
+  constexpr int LHI = OA::MAXPW + OB::MAXPW;                       // pieces per half step, low waves
+  constexpr int LLO = LHI - ((OA::REM | OB::REM) != 0 ? 1 : 0);    // the other waves
+  constexpr int NHI = OA::REM ? OA::REM : (OB::REM ? OB::REM : C::NT / 64);
+  const int lane = threadIdx.x & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wm = wid / C::WN, wn = wid % C::WN;
+  const bool hi = wid < NHI;
+#pragma unroll
+  for (int i = 0; i < C::TM; ++i)
+#pragma unroll
+    for (int j = 0; j < C::TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  if (nh <= 0) return;
+  OA oa;
+  OB ob;
+  oa.init(A, lda, m0, kbeg, wid, lane);
+  ob.init(B, ldb, n0, kbeg, wid, lane);
+  FragReader<C::BM, C::LA_, C::WTM> fa;
+  FragReader<C::BN, C::LB_, C::WTN> fbr;
+  fa.init(wm * C::WTM, lane);
+  fbr.init(wn * C::WTN, lane);
+
+#pragma unroll
+  for (int s = 0; s < NSLOT - 1; ++s) {
+    if (s < nh) {
+      oa.issue(s, smem + s * STAGE, wid);
+      ob.issue(s, smem + s * STAGE + OA::BYTES, wid);
+    }
+  }
+  auto body = [&](int tt, auto uc) {
+    constexpr int u = decltype(uc)::value;  // == tt % NSLOT
+    // half steps issued after tt that may stay in flight
+    const int ahead = min(nh - 1, tt + NSLOT - 2) - tt;
+    // keep the previous step's MFMAs above this point: sunk below the barrier they would hold
+    // two steps' fragments at once (the 288-wide tile then spilled)
+    __builtin_amdgcn_sched_barrier(0);
+    static_for<0, NSLOT - 1>([&](auto ac) {
+      constexpr int a = NSLOT - 2 - decltype(ac)::value;  // steady state (NSLOT - 2) tested first
+      if (ahead == a) {
+        if (hi) wait_vmcnt<a * LHI>();
+        else wait_vmcnt<a * LLO>();
+      }
+    });
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    const int tn = tt + NSLOT - 1;
+    if (tn < nh) {
+      constexpr int sn = (u + NSLOT - 1) % NSLOT;
+      oa.issue(tn, smem + sn * STAGE, wid);
+      ob.issue(tn, smem + sn * STAGE + OA::BYTES, wid);
+    }
+    // slot origin as an opaque per-step value: with u * STAGE folded into every fragment
+    // address (beyond the 16-bit ds offset field) the compiler hoisted one address register
+    // per (slot, fragment) out of the loop, and the 288-wide tile spilled them
+    int so = u * STAGE;
+    asm volatile("" : "+v"(so));
+    const char* sl = smem + so;
+    static_for<0, BKD / 32>([&](auto kc) {
+      constexpr int KK = decltype(kc)::value;
+      bf16x8 a[C::TM], b[C::TN];
+#pragma unroll
+      for (int i = 0; i < C::TM; ++i) a[i] = fa.template frag<KK, 0>(sl, i);
+#pragma unroll
+      for (int j = 0; j < C::TN; ++j) b[j] = fbr.template frag<KK, OA::BYTES>(sl, j);
+      if constexpr (PRIO == 1) __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int i = 0; i < C::TM; ++i)
+#pragma unroll
+        for (int j = 0; j < C::TN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
+      if constexpr (PRIO == 1) __builtin_amdgcn_s_setprio(0);
+    });
+  };
+  int t = 0;
+  for (; t + NSLOT <= nh; t += NSLOT)
+    static_for<0, NSLOT>([&](auto uc) { body(t + decltype(uc)::value, uc); });
+  static_for<0, NSLOT>([&](auto uc) {
+    if (t + decltype(uc)::value < nh) body(t + decltype(uc)::value, uc);
+  });
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+// ----------------------------------------------------------------------------------------
+// Staggered wave groups (cdna_hip_programming.md §5 8-phase template, "if (wr == 1)
+// s_barrier"): same tile, 2-slot 64-deep ring and operand images as gemm_mainloop_glds2, but
+// every 32-deep phase is {fragment reads ; barrier ; MFMAs ; barrier} and waves 4-7 (the
+// second wave on each SIMD: waves go to SIMDs cyclically) run one barrier behind waves 0-3. In
+// every barrier interval one wave of a SIMD issues MFMAs while the other issues and waits for
+// its fragment reads; with one barrier per step both waves read, then both multiply (the
+// ring's DMA wait was not the limiter: the 5-slot half-step ring measured the same, 1.166 ms).
+// Barriers b = 0, 1, .. (after the prologue's): group A reads step t's phase 0 in interval 4t,
+// group B in 4t + 1, and so on. DMA(t + 1) into the slot of step t - 1 goes out after bar(4t),
+// when every read of that slot has retired (each wave's lgkmcnt wait precedes its MFMAs), and
+// every wave waits for its own pieces before bar(4t + 3), which precedes group A's first read
+// of step t + 1 (group A: its 4th barrier of step t, group B: its 3rd).
+template <class C, int PRIO = 1>
+__device__ __forceinline__ void gemm_mainloop_stag(const bf16_t* __restrict__ A, long lda,
+                                                   const bf16_t* __restrict__ B, long ldb, int kbeg,
+                                                   int nk, int m0, int n0, char* smem,
+                                                   f32x4 (&acc)[C::TM][C::TN]) {
+  static_assert(C::NT == 512, "two wave groups of 4 (one wave per SIMD each)");
+  using OA = GldsOperand<C::BM, C::LA_, C::NT>;
+  using OB = GldsOperand<C::BN, C::LB_, C::NT>;
+  constexpr int STAGE = OA::TILE_BYTES + OB::TILE_BYTES;
+  const int lane = threadIdx.x & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wm = wid / C::WN, wn = wid % C::WN;
+  const bool grp_b = wid >= 4;
+#pragma unroll
+  for (int i = 0; i < C::TM; ++i)
+#pragma unroll
+    for (int j = 0; j < C::TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  if (nk <= 0) return;
+  OA oa;
+  OB ob;
+  oa.init(A, lda, m0, kbeg, wid, lane);
+  ob.init(B, ldb, n0, kbeg, wid, lane);
+  FragReader<C::BM, C::LA_, C::WTM> fa;
+  FragReader<C::BN, C::LB_, C::WTN> fbr;
+  fa.init(wm * C::WTM, lane);
+  fbr.init(wn * C::WTN, lane);
+  auto bar = [] {
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+  };
+
+  oa.issue(0, smem, wid);
+  ob.issue(0, smem + OA::TILE_BYTES, wid);
+  wait_vmcnt<0>();
+  bar();
+  if (grp_b) bar();  // group B runs one barrier behind
+
+  auto body = [&](int tt, auto uc) {
+    constexpr int u = decltype(uc)::value;  // == tt & 1
+    const bool more = tt + 1 < nk;
+    if (grp_b && more) {  // B: right after bar(4t), its last barrier of step t - 1
+      oa.issue(tt + 1, smem + (u ^ 1) * STAGE, wid);
+      ob.issue(tt + 1, smem + (u ^ 1) * STAGE + OA::TILE_BYTES, wid);
+    }
+    static_for<0, 2>([&](auto kc) {
+      constexpr int KK = decltype(kc)::value;
+      bf16x8 a[C::TM], b[C::TN];
+#pragma unroll
+      for (int i = 0; i < C::TM; ++i) a[i] = fa.template frag<KK, u * STAGE>(smem, i);
+#pragma unroll
+      for (int j = 0; j < C::TN; ++j) b[j] = fbr.template frag<KK, u * STAGE + OA::TILE_BYTES>(smem, j);
+      if constexpr (KK == 1) {
+        if (grp_b) wait_vmcnt<0>();  // B: before its 3rd barrier of the step = bar(4t + 3)
+      }
+      bar();
+      if constexpr (KK == 0) {
+        if (!grp_b && more) {  // A: right after bar(4t)
+          oa.issue(tt + 1, smem + (u ^ 1) * STAGE, wid);
+          ob.issue(tt + 1, smem + (u ^ 1) * STAGE + OA::TILE_BYTES, wid);
+        }
+      }
+      if constexpr (PRIO == 1) __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int i = 0; i < C::TM; ++i)
+#pragma unroll
+        for (int j = 0; j < C::TN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
+      if constexpr (PRIO == 1) __builtin_amdgcn_s_setprio(0);
+      if constexpr (KK == 1) {
+        if (!grp_b) wait_vmcnt<0>();  // A: before its 4th barrier of the step = bar(4t + 3)
+      }
+      bar();
+    });
+  };
+  int t = 0;
+  for (; t + 2 <= nk; t += 2) {
+    body(t, std::integral_constant<int, 0>{});
+    body(t + 1, std::integral_constant<int, 1>{});
+  }
+  if (t < nk) body(t, std::integral_constant<int, 0>{});
+  if (!grp_b) bar();  // the barrier counts of the two groups meet again
+}
+
 // Output coordinates of accumulator element acc[i][j][r] (16x16 C/D map: col = lane&15,
 // row = 4*(lane>>4) + r).
 template <class C>

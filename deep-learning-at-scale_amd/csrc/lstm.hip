@@ -41,12 +41,22 @@ __global__ void lstm_pack_x_kernel(const float* __restrict__ x, bf16_t* __restri
     const int t = (int)(row / d.B);
     const float* src = x + (b * d.T + t) * d.F;
     unsigned pk[4];
+    // 8 features: two 16-B loads (rows are 16-B aligned when F % 4 == 0 and x is)
+    if ((d.F & 3) == 0 && c + 8 <= d.F && ((uintptr_t)x & 15u) == 0) {
+      const float4 lo = *reinterpret_cast<const float4*>(src + c);
+      const float4 hi = *reinterpret_cast<const float4*>(src + c + 4);
+      pk[0] = (unsigned)f2bf(lo.x) | ((unsigned)f2bf(lo.y) << 16);
+      pk[1] = (unsigned)f2bf(lo.z) | ((unsigned)f2bf(lo.w) << 16);
+      pk[2] = (unsigned)f2bf(hi.x) | ((unsigned)f2bf(hi.y) << 16);
+      pk[3] = (unsigned)f2bf(hi.z) | ((unsigned)f2bf(hi.w) << 16);
+    } else {
 #pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const int k0 = c + 2 * e, k1 = k0 + 1;
-      const float v0 = k0 < d.F ? src[k0] : (k0 == d.F ? 1.f : 0.f);
-      const float v1 = k1 < d.F ? src[k1] : (k1 == d.F ? 1.f : 0.f);
-      pk[e] = (unsigned)f2bf(v0) | ((unsigned)f2bf(v1) << 16);
+      for (int e = 0; e < 4; ++e) {
+        const int k0 = c + 2 * e, k1 = k0 + 1;
+        const float v0 = k0 < d.F ? src[k0] : (k0 == d.F ? 1.f : 0.f);
+        const float v1 = k1 < d.F ? src[k1] : (k1 == d.F ? 1.f : 0.f);
+        pk[e] = (unsigned)f2bf(v0) | ((unsigned)f2bf(v1) << 16);
+      }
     }
     *reinterpret_cast<uint4*>(XH + row * KA + c) = make_uint4(pk[0], pk[1], pk[2], pk[3]);
   }

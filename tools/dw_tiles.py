@@ -2,7 +2,8 @@
 K = T*B = 524288, MN x MN operands, split-K fp32 atomics): time per call, interleaved over
 rounds, and max |diff| against the default tile (3 = 256x192 64-deep 2-stage).
 
-    python tools/dw_tiles.py [tiles ...]      (default: 1 2 3)
+    python tools/dw_tiles.py [tiles ...]      (default: 1 2 3; 4 / 5 = 256x192 with the 5- / 4-slot
+                                              32-deep half-step ring)
 """
 import sys
 
