@@ -33,12 +33,17 @@ typedef __attribute__((address_space(3))) bf16x4 lds_bf16x4;
 // line, so row parity already shifts a 32-lane ds_read_b64_tr_b16 group by half a line; rotating
 // by h as well put lanes (q, g) and (q, g + 1) on one bank pair for j >= 5 (PMC: 7.7 % of the
 // dW kernel's cycles in bank conflicts). Rotation by h >> 1 is conflict-free for every j
-// (exhaustive check over the fragment-read lane pattern); C = 18 keeps rotation by h.
+// (exhaustive check over the fragment-read lane pattern). 288-wide (C = 18) images rotate by
+// h >> 2: a 576-B k-row is 64 B mod the bank line, so k & 3 already spreads a group's 8-B slots
+// over 4 row offsets and only the (k >> 3) & 1 half of h may rotate; rotation by h put 2-way
+// conflicts on the subtiles that wrap mod 18 (PMC: 5.2 % of the 256x288 dW kernel's cycles).
+// The offset table was found by exhaustive search over per-h rotations (0 conflicts for 32- and
+// 64-deep images).
 template <int R>
 struct MnSwz {
   static constexpr int C = R / 16;
   static constexpr bool POW2 = (C & (C - 1)) == 0;
-  static constexpr int RSH = C == 12 ? 1 : 0;
+  static constexpr int RSH = C == 12 ? 1 : (C == 18 ? 2 : 0);
   __host__ __device__ static constexpr int hmask() { return POW2 ? C - 1 : 7; }
   __device__ static __forceinline__ int hk(int k) { return ((k & 3) | ((k >> 1) & 4)) & hmask(); }
   __device__ static __forceinline__ int pos(int j, int h) { return POW2 ? (j ^ h) : (j + (h >> RSH)) % C; }
