@@ -455,7 +455,7 @@ bool mlp2_backward(c10::optional<at::Tensor> H1, const at::Tensor& H2, const at:
                    const at::Tensor& dZ2, c10::optional<at::Tensor> dW1, const at::Tensor& db1,
                    const at::Tensor& db2, const at::Tensor& dw3, const at::Tensor& db3, int64_t B,
                    c10::optional<at::Tensor> M2, c10::optional<at::Tensor> W1, c10::optional<at::Tensor> b1,
-                   c10::optional<at::Tensor> rows) {
+                   c10::optional<at::Tensor> rows, c10::optional<at::Tensor> red) {
   constexpr int64_t H = 256;
   const bool recompute = !H1.has_value() || !H1->defined();
   std::vector<const at::Tensor*> acts = {&H2, &dZ1, &dZ2};
@@ -482,12 +482,14 @@ bool mlp2_backward(c10::optional<at::Tensor> H1, const at::Tensor& H2, const at:
   const c10::hip::OptionalHIPGuardMasqueradingAsCUDA guard(H2.device());
   return wf::launch_mlp2_bwd(recompute ? nullptr : bfp(*H1), bfp(H2), mask_ptr(M2, B), fp(dy), fp(w3), bfp(W2), bfp(X),
                              (int)Fp, bfp(dZ1), bfp(dZ2), opt_ptr<float>(dW1, at::kFloat, "dW1", H * Fp), fp(db1),
-                             fp(db2), fp(dw3), fp(db3), (int)B, w1p, b1p, rows_ptr(rows, B), nrows, cur_stream());
+                             fp(db2), fp(dw3), fp(db3), (int)B, w1p, b1p, rows_ptr(rows, B), nrows, cur_stream(),
+                             opt_ptr<float>(red, at::kFloat, "red", wf::kMlpRedFloats));
 }
 
 // dW2 [256][256] += dZ2^T relu(X W1^T + b1), H1 recomputed (mlp_fused.hip mlp2_dw2_kernel).
 bool mlp2_dw2(const at::Tensor& dZ2, const at::Tensor& X, int64_t Fp, c10::optional<at::Tensor> rows,
-              const at::Tensor& W1, const at::Tensor& b1, int64_t B, int64_t nsplit, const at::Tensor& dW2) {
+              const at::Tensor& W1, const at::Tensor& b1, int64_t B, int64_t nsplit, const at::Tensor& dW2,
+              c10::optional<at::Tensor> red) {
   constexpr int64_t H = 256;
   check_t(dZ2, at::kBFloat16, "dZ2");
   check_extent(dZ2, B * H, "dZ2");
@@ -501,7 +503,29 @@ bool mlp2_dw2(const at::Tensor& dZ2, const at::Tensor& X, int64_t Fp, c10::optio
   check_extent(dW2, H * H, "dW2");
   const c10::hip::OptionalHIPGuardMasqueradingAsCUDA guard(dZ2.device());
   return wf::launch_mlp2_dw2(bfp(dZ2), bfp(X), (int)Fp, rows_ptr(rows, B), nrows, bfp(W1), fp(b1), (int)B, (int)nsplit,
-                             fp(dW2), cur_stream());
+                             fp(dW2), cur_stream(), opt_ptr<float>(red, at::kFloat, "red", wf::kMlpRedFloats));
+}
+
+// Sums the spread-reduction scratch of the 8-wave MLP training kernels into the gradients
+// (mlp_fused.hip mlp2_reduce_kernel) and zeroes it; null destinations are skipped.
+void mlp2_reduce(const at::Tensor& red, int64_t Fp, c10::optional<at::Tensor> loss_sum, const at::Tensor& db3,
+                 const at::Tensor& dw3, const at::Tensor& db1, const at::Tensor& db2, const at::Tensor& dW1,
+                 c10::optional<at::Tensor> dW2) {
+  constexpr int64_t H = 256;
+  check_t(red, at::kFloat, "red");
+  check_extent(red, wf::kMlpRedFloats, "red");
+  TORCH_CHECK(Fp > 0 && Fp <= 32, "mlp2_reduce: Fp <= 32");
+  for (const at::Tensor* t : {&dw3, &db1, &db2}) {
+    check_t(*t, at::kFloat, "dw3/db");
+    check_extent(*t, H, "dw3/db");
+  }
+  check_t(db3, at::kFloat, "db3");
+  check_extent(db3, 1, "db3");
+  check_t(dW1, at::kFloat, "dW1");
+  check_extent(dW1, H * Fp, "dW1");
+  const c10::hip::OptionalHIPGuardMasqueradingAsCUDA guard(red.device());
+  wf::launch_mlp2_reduce(fp(red), (int)Fp, opt_ptr<float>(loss_sum, at::kFloat, "loss_sum", 1), fp(db3), fp(dw3),
+                         fp(db1), fp(db2), fp(dW1), opt_ptr<float>(dW2, at::kFloat, "dW2", H * H), cur_stream());
 }
 
 // Fused MLP forward (mlp_fused.hip): both 256-wide hidden layers + head (+ MSE) in one launch.
@@ -512,7 +536,8 @@ bool mlp2_forward(const at::Tensor& X, int64_t Fp, const at::Tensor& W1, const a
                   c10::optional<at::Tensor> y, c10::optional<at::Tensor> H1, const at::Tensor& H2,
                   const at::Tensor& pred, c10::optional<at::Tensor> dy, c10::optional<at::Tensor> loss_sum,
                   double dy_scale, int64_t B, c10::optional<at::Tensor> M2,
-                  c10::optional<at::Tensor> dw3, c10::optional<at::Tensor> db3, c10::optional<at::Tensor> rows) {
+                  c10::optional<at::Tensor> dw3, c10::optional<at::Tensor> db3, c10::optional<at::Tensor> rows,
+                  c10::optional<at::Tensor> red) {
   constexpr int64_t H = 256;
   check_t(X, at::kBFloat16, "X");
   const int64_t nrows = check_x_rows(X, Fp, B, rows);
@@ -540,7 +565,8 @@ bool mlp2_forward(const at::Tensor& X, int64_t Fp, const at::Tensor& W1, const a
                              fp(pred),
                              opt_ptr<float>(dy, at::kFloat, "dy", B),
                              opt_ptr<float>(loss_sum, at::kFloat, "loss_sum", 1), (float)dy_scale, (int)B,
-                             rows_ptr(rows, B), nrows, cur_stream());
+                             rows_ptr(rows, B), nrows, cur_stream(),
+                             opt_ptr<float>(red, at::kFloat, "red", wf::kMlpRedFloats));
 }
 
 void head_bwd_w(const at::Tensor& Hm, int64_t ldh, int64_t B, int64_t Hd, const at::Tensor& dy,
@@ -714,6 +740,7 @@ PYBIND11_MODULE(_C, m) {
   WF_DEF(mlp2_forward);
   WF_DEF(mlp2_backward);
   WF_DEF(mlp2_dw2);
+  WF_DEF(mlp2_reduce);
   WF_DEF(lstm_pack_x);
   WF_DEF(lstm_forward);
   WF_DEF(lstm_forward_persistent);

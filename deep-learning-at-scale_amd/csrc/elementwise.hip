@@ -6,6 +6,8 @@
 // fp32 master buffer, float4-vectorised), K18 (casts).
 #include <cstdlib>
 
+#include <algorithm>
+
 #include "common.h"
 #include "kernels.h"
 
@@ -387,7 +389,15 @@ __global__ __launch_bounds__(256) void adam_dev_kernel(float* __restrict__ p, fl
 void launch_adam_dev(float* p, float* g, float* m, float* v, long n, float* step, float lr,
                      float b1, float b2, float eps, float wd, float gscale, bf16_t* shadow, int zero_g,
                      hipStream_t s) {
-  hipLaunchKernelGGL(adam_dev_kernel, dim3(ew_blocks(n)), dim3(256), 0, s, p, g, m, v, n, step, lr,
+  // every workgroup draws a ticket from ONE counter (step[1]) and same-address atomics serialise:
+  // at most WELLFLOW_ADAM_GRID (default 256) workgroups, grid-stride over the rest
+  static const int cap = [] {
+    const char* e = std::getenv("WELLFLOW_ADAM_GRID");
+    return e == nullptr ? 256 : std::max(1, std::atoi(e));
+  }();
+  int blocks = ew_blocks(n);
+  if (blocks > cap) blocks = cap;
+  hipLaunchKernelGGL(adam_dev_kernel, dim3(blocks), dim3(256), 0, s, p, g, m, v, n, step, lr,
                      b1, b2, eps, wd, gscale, shadow, zero_g);
 }
 

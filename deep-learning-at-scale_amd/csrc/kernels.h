@@ -72,10 +72,12 @@ void launch_lstm_pack_weights(const float* W, bf16_t* Wp, bf16_t* WhhT, LstmDims
 // ReLU, bias, linear head, optional MSE (y, dy = dy_scale * (pred - y), loss_sum += (pred - y)^2).
 // Writes H1, H2 ([B][256] bf16: the backward's saved activations) and pred. Returns false
 // (nothing launched) for shapes it does not cover.
+// red (optional): the spread-reduction scratch of the 8-wave training kernels (kMlpRed* below);
+// when given, their batch sums land there and launch_mlp2_reduce adds them to the gradients.
 bool launch_mlp2_fwd(const bf16_t* X, int Fp, const bf16_t* W1, const float* b1, const bf16_t* W2, const float* b2,
                      const float* w3, const float* b3, const float* y, bf16_t* H1, bf16_t* H2, unsigned* M2,
                      float* dw3, float* db3, float* pred, float* dy, float* loss_sum, float dy_scale, int B,
-                     const long long* rows, long nrows, hipStream_t s);
+                     const long long* rows, long nrows, hipStream_t s, float* red = nullptr);
 // Mask mode (M2 != nullptr; needs y, dw3, db3): H2 is NOT written — only its ReLU bitmask M2
 // ([B][8] u32, bit u of row r = word 8r + u / 32, bit u % 32) — and dw3 += H2^T dy,
 // db3 += sum dy are accumulated by the forward itself.
@@ -87,12 +89,20 @@ bool launch_mlp2_fwd(const bf16_t* X, int Fp, const bf16_t* W1, const float* b1,
 bool launch_mlp2_bwd(const bf16_t* H1, const bf16_t* H2, const unsigned* M2, const float* dy, const float* w3, const bf16_t* W2,
                      const bf16_t* X, int Fp, bf16_t* dZ1, bf16_t* dZ2, float* dW1, float* db1, float* db2,
                      float* dw3, float* db3, int B, const bf16_t* W1, const float* b1, const long long* rows,
-                     long nrows, hipStream_t s);
+                     long nrows, hipStream_t s, float* red = nullptr);
 // H1 == nullptr: recompute H1 from X with W1 / b1 (needs dW1 != nullptr, i.e. Fp <= 32);
 // rows != nullptr: dataset row indices of X (and y in the forward) per batch row.
 // dW2 += dZ2^T relu(X W1^T + b1) with H1 recomputed per chunk (B % 64 == 0, Fp <= 32)
 bool launch_mlp2_dw2(const bf16_t* dZ2, const bf16_t* X, int Fp, const long long* rows, long nrows, const bf16_t* W1,
-                     const float* b1, int B, int nsplit, float* dW2, hipStream_t s);
+                     const float* b1, int B, int nsplit, float* dW2, hipStream_t s, float* red = nullptr);
+// Spread-reduction scratch (floats): kMlpRedCopies rows of kMlpRedRow slots — [loss, db3,
+// dw3[256], db1[256], db2[256], dW1[256 x Fp]] — then kMlpRedCopies2 copies of dW2 [256 x 256].
+// Zero-initialised once; mlp2_reduce sums every copy into the gradients and zeroes it again.
+constexpr int kMlpRedCopies = 64, kMlpRedCopies2 = 4, kMlpRedRow = 9216;
+constexpr int kMlpRedLoss = 0, kMlpRedDb3 = 1, kMlpRedDw3 = 2, kMlpRedDb1 = 258, kMlpRedDb2 = 514, kMlpRedDW1 = 770;
+constexpr long kMlpRedFloats = (long)kMlpRedCopies * kMlpRedRow + (long)kMlpRedCopies2 * 65536;
+void launch_mlp2_reduce(float* red, int Fp, float* loss_sum, float* db3, float* dw3, float* db1, float* db2, float* dW1,
+                        float* dW2, hipStream_t s);
 
 // ---- regression head (N = 1) and losses ----
 void launch_head_fwd(const bf16_t* Hm, long ldh, int B, int Hd, const float* w, const float* b0,

@@ -36,7 +36,65 @@ int mlp_prio() {
   }();
   return p;
 }
+// WELLFLOW_MLP_DBG: timing-only switches of the 8-wave forward / backward (results are wrong)
+int mlp_dbg() {
+  static const int d = [] {
+    const char* e = std::getenv("WELLFLOW_MLP_DBG");
+    return e == nullptr ? 0 : std::atoi(e);
+  }();
+  return d;
+}
 constexpr int MF_ROWS = 64;  // rows per chunk
+}  // namespace
+
+// Spread reduction of the training kernels' batch sums (kernels.h kMlpRed*): every workgroup of
+// the 8-wave forward / backward used to atomically add its partial loss, dw3, db3, db1, db2
+// and dW1 straight into the gradient, i.e. 256 adders per address at the same moment, and the
+// atomic unit serialises same-address adds: ~25 us of each ~36 us one-chunk-per-workgroup
+// launch (WELLFLOW_MLP_DBG=1 A/B, profiles/r3_summary.md). They now add into copy
+// blockIdx % 16 of a scratch row (16 adders per address); dW2's 64 split-K adders per address
+// go to copy split % 4. mlp2_reduce_kernel sums the copies into the gradients and re-zeroes them.
+__global__ __launch_bounds__(256) void mlp2_reduce_kernel(float* __restrict__ red, int Fp, float* __restrict__ loss_sum,
+                                                          float* __restrict__ db3, float* __restrict__ dw3,
+                                                          float* __restrict__ db1, float* __restrict__ db2,
+                                                          float* __restrict__ dW1, float* __restrict__ dW2) {
+  const int na = kMlpRedDW1 + 256 * Fp;
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < na) {
+    float v = 0.f;
+#pragma unroll
+    for (int c = 0; c < kMlpRedCopies; ++c) {
+      v += red[c * kMlpRedRow + i];
+      red[c * kMlpRedRow + i] = 0.f;
+    }
+    float* dst = i == kMlpRedLoss ? loss_sum
+                 : i == kMlpRedDb3 ? db3
+                 : i < kMlpRedDb1  ? (dw3 != nullptr ? dw3 + (i - kMlpRedDw3) : nullptr)
+                 : i < kMlpRedDb2  ? (db1 != nullptr ? db1 + (i - kMlpRedDb1) : nullptr)
+                 : i < kMlpRedDW1  ? (db2 != nullptr ? db2 + (i - kMlpRedDb2) : nullptr)
+                                   : (dW1 != nullptr ? dW1 + (i - kMlpRedDW1) : nullptr);
+    if (dst != nullptr && v != 0.f) *dst += v;
+  } else if (i - na < 256 * 256) {
+    const int j = i - na;
+    float* r2 = red + kMlpRedCopies * kMlpRedRow;
+    float v = 0.f;
+#pragma unroll
+    for (int c = 0; c < kMlpRedCopies2; ++c) {
+      v += r2[c * 65536 + j];
+      r2[c * 65536 + j] = 0.f;
+    }
+    if (dW2 != nullptr && v != 0.f) dW2[j] += v;
+  }
+}
+
+void launch_mlp2_reduce(float* red, int Fp, float* loss_sum, float* db3, float* dw3, float* db1, float* db2, float* dW1,
+                        float* dW2, hipStream_t s) {
+  const int n = kMlpRedDW1 + 256 * Fp + 256 * 256;
+  hipLaunchKernelGGL(mlp2_reduce_kernel, dim3((n + 255) / 256), dim3(256), 0, s, red, Fp, loss_sum, db3, dw3, db1, db2,
+                     dW1, dW2);
+}
+
+namespace {
 // dataset row of batch row gr (indices clamped into the dataset: never an out-of-bounds read)
 __device__ __forceinline__ size_t data_row(const long long* rows, int gr, long nrows) {
   if (rows == nullptr) return (size_t)gr;
@@ -326,7 +384,9 @@ __global__ __launch_bounds__(512, 1) void mlp2_fwd_train_kernel(
     const bf16_t* __restrict__ W2, const float* __restrict__ b2, const float* __restrict__ w3,
     const float* __restrict__ b3, const float* __restrict__ y, unsigned* __restrict__ M2, float* __restrict__ dw3,
     float* __restrict__ db3, float* __restrict__ pred, float* __restrict__ dy, float* __restrict__ loss_sum,
-    float dy_scale, int B, const long long* __restrict__ rows, long nrows) {
+    float dy_scale, int B, const long long* __restrict__ rows, long nrows, int dbg, float* __restrict__ rscr) {
+  // dbg (WELLFLOW_MLP_DBG, timing only, wrong results): 1 = no epilogue atomics, 2 = no W2 loads
+  // rscr != nullptr: the batch sums go to copy blockIdx % 16 of the spread-reduction scratch
   constexpr int NW = 8, MT = 2;  // waves; 16-unit M tiles per wave
   __shared__ __attribute__((aligned(16))) char xs[MF_ROWS * MF_XROW];
   __shared__ __attribute__((aligned(16))) char h1s[MF_ROWS * MF_H * 2];
@@ -349,7 +409,9 @@ __global__ __launch_bounds__(512, 1) void mlp2_fwd_train_kernel(
                                 : bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
     }
 #pragma unroll
-    for (int kt = 0; kt < 8; ++kt) w2f[m][kt] = *reinterpret_cast<const bf16x8*>(W2 + (size_t)u * MF_H + 32 * kt + 8 * g);
+    for (int kt = 0; kt < 8; ++kt)
+      w2f[m][kt] = (dbg & 2) ? bf16x8{0, 0, 0, 0, 0, 0, 0, 0}
+                             : *reinterpret_cast<const bf16x8*>(W2 + (size_t)u * MF_H + 32 * kt + 8 * g);
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int uc = u0 + 16 * m + 4 * g + r;
@@ -504,6 +566,13 @@ __global__ __launch_bounds__(512, 1) void mlp2_fwd_train_kernel(
       for (int r = 0; r < 4; ++r)
 #pragma unroll
         for (int n = 0; n < 4; ++n) dw3r[m][r] += acc[m][n][r] * dyn[n];
+  }
+  if (dbg & 1) return;
+  if (rscr != nullptr) {
+    float* rb = rscr + (blockIdx.x & (kMlpRedCopies - 1)) * kMlpRedRow;
+    if (loss_sum != nullptr) loss_sum = rb + kMlpRedLoss;
+    dw3 = rb + kMlpRedDw3;
+    db3 = rb + kMlpRedDb3;
   }
   if (loss_sum != nullptr) {
     const float t = block_sum<512>(lsum, lred);
@@ -1080,7 +1149,10 @@ __global__ __launch_bounds__(512, 1) void mlp2_bwd_rc8_kernel(
     const unsigned* __restrict__ M2, const float* __restrict__ dy, const float* __restrict__ w3,
     const bf16_t* __restrict__ W2, const bf16_t* __restrict__ X, int Fp, bf16_t* __restrict__ dZ2,
     float* __restrict__ dW1, float* __restrict__ db1, float* __restrict__ db2, int B,
-    const bf16_t* __restrict__ W1, const float* __restrict__ b1, const long long* __restrict__ rows, long nrows) {
+    const bf16_t* __restrict__ W1, const float* __restrict__ b1, const long long* __restrict__ rows, long nrows,
+    int dbg, float* __restrict__ red) {
+  // red != nullptr: db1, db2, dW1 go to copy blockIdx % 16 of the spread-reduction scratch
+  // dbg (WELLFLOW_MLP_DBG, timing only, wrong results): 1 = no epilogue atomics, 2 = no W2^T gather
   constexpr int MT = 2, ZB = MF_ROWS * MF_H * 2, XB = MF_ROWS * MF_XROW;
   __shared__ __attribute__((aligned(16))) char zs[2 * ZB];  // dZ2 tiles (double-buffered)
   __shared__ __attribute__((aligned(16))) char hs[ZB];      // H1 -> dZ1 in place (wave-private units)
@@ -1099,7 +1171,7 @@ __global__ __launch_bounds__(512, 1) void mlp2_bwd_rc8_kernel(
 #pragma unroll
     for (int kt = 0; kt < 8; ++kt)
 #pragma unroll
-      for (int j = 0; j < 8; ++j) wt[m][kt][j] = (short)W2[(size_t)(32 * kt + 8 * g + j) * MF_H + k];
+      for (int j = 0; j < 8; ++j) wt[m][kt][j] = (dbg & 2) ? (short)0 : (short)W2[(size_t)(32 * kt + 8 * g + j) * MF_H + k];
     w1f[m] = 8 * g + 8 <= Fp ? *reinterpret_cast<const bf16x8*>(W1 + (size_t)k * Fp + 8 * g)
                              : bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
 #pragma unroll
@@ -1147,19 +1219,19 @@ __global__ __launch_bounds__(512, 1) void mlp2_bwd_rc8_kernel(
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const int r = rq + 16 * q, gr = row0 + r;
-      const unsigned bits = mb[q] >> (8 * (c & 3));
+      const int bits = (int)(mb[q] >> (8 * (c & 3)));
+      const int gyb = __float_as_int(gyv[q]);
       unsigned zw[4];
 #pragma unroll
       for (int p = 0; p < 4; ++p) {
-        unsigned pk = 0;
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-          const int e = 2 * p + h;
-          const bf16_t zb = f2bf(((bits >> e) & 1u) ? gyv[q] * w3c[e] : 0.f);
-          db2a[e] += bf2f(zb);
-          pk |= (unsigned)zb << (16 * h);
-        }
-        zw[p] = pk;
+        // bit e sign-extended (v_bfe_i32) masks dy: t = [H2 > 0] dy, two VALU ops per element
+        // instead of shift / and / compare / select. db2 = w3 * sum t is accumulated in fp32
+        // before the bf16 rounding of dZ2 (the reduction's w3 factor is applied once, below)
+        const float t0 = __int_as_float(__builtin_amdgcn_sbfe(bits, 2 * p, 1) & gyb);
+        const float t1 = __int_as_float(__builtin_amdgcn_sbfe(bits, 2 * p + 1, 1) & gyb);
+        db2a[2 * p] += t0;
+        db2a[2 * p + 1] += t1;
+        zw[p] = pk_bf16(t0 * w3c[2 * p], t1 * w3c[2 * p + 1]);
       }
       const uint4 zv = make_uint4(zw[0], zw[1], zw[2], zw[3]);
       *reinterpret_cast<uint4*>(zt + tile_off(r, 8 * c)) = zv;
@@ -1220,20 +1292,18 @@ __global__ __launch_bounds__(512, 1) void mlp2_bwd_rc8_kernel(
         const int r = 16 * n + l15;
         uint2* pp = reinterpret_cast<uint2*>(hs + tile_off(r, u0 + 16 * m + 4 * g));
         const uint2 hv = *pp;
-        const unsigned hw2[2] = {hv.x, hv.y};
+        const bool rok = row0 + r < B;
+        const int hw2[2] = {rok ? (int)hv.x : 0, rok ? (int)hv.y : 0};
         unsigned ow[2];
 #pragma unroll
         for (int q = 0; q < 2; ++q) {
-          unsigned pk = 0;
-#pragma unroll
-          for (int h = 0; h < 2; ++h) {
-            const int i = 2 * q + h;
-            const bool on = bf2f((bf16_t)(hw2[q] >> (16 * h))) > 0.f && row0 + r < B;
-            const bf16_t vb = f2bf(on ? acc[m][n][i] : 0.f);
-            db1a[m][i] += bf2f(vb);
-            pk |= (unsigned)vb << (16 * h);
-          }
-          ow[q] = pk;
+          // H1 >= 0 (relu), so H1 > 0 <=> the bf16 half is > 0 as a signed 16-bit integer (-0 is
+          // not): low half via the sign of (w << 16), high half as w > 0xFFFF signed
+          const bool on0 = (hw2[q] << 16) > 0, on1 = hw2[q] > 0xFFFF;
+          const float t0 = on0 ? acc[m][n][2 * q] : 0.f, t1 = on1 ? acc[m][n][2 * q + 1] : 0.f;
+          db1a[m][2 * q] += t0;  // fp32 before the bf16 rounding of dZ1
+          db1a[m][2 * q + 1] += t1;
+          ow[q] = pk_bf16(t0, t1);
         }
         *pp = make_uint2(ow[0], ow[1]);
       }
@@ -1273,6 +1343,13 @@ __global__ __launch_bounds__(512, 1) void mlp2_bwd_rc8_kernel(
     __builtin_amdgcn_wave_barrier();
   }
   // ---- reductions
+  if (dbg & 1) return;
+  if (red != nullptr) {
+    float* rb = red + (blockIdx.x & (kMlpRedCopies - 1)) * kMlpRedRow;
+    db1 = rb + kMlpRedDb1;
+    db2 = rb + kMlpRedDb2;
+    dW1 = rb + kMlpRedDW1;
+  }
 #pragma unroll
   for (int m = 0; m < MT; ++m)
 #pragma unroll
@@ -1296,7 +1373,7 @@ __global__ __launch_bounds__(512, 1) void mlp2_bwd_rc8_kernel(
   __syncthreads();  // the last chunk's dZ2 tile reads are done before zs becomes the db2 scratch
   float* sd = reinterpret_cast<float*>(zs);
 #pragma unroll
-  for (int e = 0; e < 8; ++e) sd[rq * MF_H + 8 * c + e] = db2a[e];
+  for (int e = 0; e < 8; ++e) sd[rq * MF_H + 8 * c + e] = db2a[e] * w3c[e];
   __syncthreads();
   if (threadIdx.x < MF_H) {
     float s2 = 0.f;
@@ -1330,7 +1407,7 @@ template <int NW, int PR = 0>  // PR: s_setprio(1) around each MFMA cluster (A/B
 __global__ __launch_bounds__(64 * NW, 1) void mlp2_dw2_kernel(const bf16_t* __restrict__ dZ2, const bf16_t* __restrict__ X,
                                                               int Fp, const long long* __restrict__ rows, long nrows,
                                                               const bf16_t* __restrict__ W1, const float* __restrict__ b1,
-                                                              int kchunk, float* __restrict__ dW2) {
+                                                              int kchunk, float* __restrict__ dW2, float* __restrict__ red) {
   static_assert(NW == 4 || NW == 8, "4 or 8 waves");
   constexpr int NT = 64 * NW, BM = 128, BN = 128, MTR = 128 / (16 * NW);  // H1 unit tiles per wave
   using C = GemmCfg<BM, BN, MN_CONTIG, MN_CONTIG, 2, NW / 2>;
@@ -1483,6 +1560,8 @@ __global__ __launch_bounds__(64 * NW, 1) void mlp2_dw2_kernel(const bf16_t* __re
   if (c + 1 < nk) body(c + 1, std::integral_constant<int, 1>{});
   if (c + 2 < nk) body(c + 2, std::integral_constant<int, 2>{});
   const AccCoord<C> cc(m0, n0);
+  // red != nullptr: copy split % 4 of the spread-reduction scratch (64 -> 16 adders per address)
+  if (red != nullptr) dW2 = red + kMlpRedCopies * kMlpRedRow + (split & (kMlpRedCopies2 - 1)) * 65536;
 #pragma unroll
   for (int j = 0; j < C::TN; ++j)
 #pragma unroll
@@ -1494,7 +1573,7 @@ __global__ __launch_bounds__(64 * NW, 1) void mlp2_dw2_kernel(const bf16_t* __re
 // dW2 [256][256] fp32 (atomics: zeroed or accumulating) from dZ2 [B][256], X rows (rows), W1, b1.
 // Needs B % 64 == 0 and Fp <= 32 (one K = 32 layer-1 step); false = not covered.
 bool launch_mlp2_dw2(const bf16_t* dZ2, const bf16_t* X, int Fp, const long long* rows, long nrows, const bf16_t* W1,
-                     const float* b1, int B, int nsplit, float* dW2, hipStream_t s) {
+                     const float* b1, int B, int nsplit, float* dW2, hipStream_t s, float* red) {
   if (B <= 0 || B % MF_ROWS != 0 || Fp > 32 || Fp % 8 != 0) return false;
   const int chunks = B / MF_ROWS;
   if (nsplit < 1) nsplit = 1;
@@ -1507,20 +1586,20 @@ bool launch_mlp2_dw2(const bf16_t* dZ2, const bf16_t* X, int Fp, const long long
   }();
   if (dw2_8 && (mlp_prio() & 4))
     hipLaunchKernelGGL((mlp2_dw2_kernel<8, 1>), dim3(4 * nsplit), dim3(512), 0, s, dZ2, X, Fp, rows, nrows, W1, b1, kchunk,
-                       dW2);
+                       dW2, red);
   else if (dw2_8)
     hipLaunchKernelGGL(mlp2_dw2_kernel<8>, dim3(4 * nsplit), dim3(512), 0, s, dZ2, X, Fp, rows, nrows, W1, b1, kchunk,
-                       dW2);
+                       dW2, red);
   else
     hipLaunchKernelGGL(mlp2_dw2_kernel<4>, dim3(4 * nsplit), dim3(256), 0, s, dZ2, X, Fp, rows, nrows, W1, b1, kchunk,
-                       dW2);
+                       dW2, red);
   return true;
 }
 
 bool launch_mlp2_bwd(const bf16_t* H1, const bf16_t* H2, const unsigned* M2, const float* dy, const float* w3, const bf16_t* W2,
                      const bf16_t* X, int Fp, bf16_t* dZ1, bf16_t* dZ2, float* dW1, float* db1, float* db2,
                      float* dw3, float* db3, int B, const bf16_t* W1, const float* b1, const long long* rows,
-                     long nrows, hipStream_t s) {
+                     long nrows, hipStream_t s, float* red) {
   if (B <= 0 || (dW1 != nullptr && (X == nullptr || Fp > 32 || Fp % 8 != 0))) return false;
   if (H1 == nullptr && (dW1 == nullptr || W1 == nullptr || b1 == nullptr)) return false;  // recompute needs the X tile
   if (rows != nullptr && dW1 == nullptr) return false;  // X is read only by the fused dW1 path
@@ -1538,13 +1617,13 @@ bool launch_mlp2_bwd(const bf16_t* H1, const bf16_t* H2, const unsigned* M2, con
     if (bwd8) {
       if (Fp <= 16 && (mlp_prio() & 2))
         hipLaunchKernelGGL((mlp2_bwd_rc8_kernel<1, 1>), dim3(grid), dim3(512), 0, s, M2, dy, w3, W2, X, Fp, dZ2, dW1, db1,
-                           db2, B, W1, b1, rows, nrows);
+                           db2, B, W1, b1, rows, nrows, mlp_dbg(), red);
       else if (Fp <= 16)
         hipLaunchKernelGGL(mlp2_bwd_rc8_kernel<1>, dim3(grid), dim3(512), 0, s, M2, dy, w3, W2, X, Fp, dZ2, dW1, db1,
-                           db2, B, W1, b1, rows, nrows);
+                           db2, B, W1, b1, rows, nrows, mlp_dbg(), red);
       else
         hipLaunchKernelGGL(mlp2_bwd_rc8_kernel<2>, dim3(grid), dim3(512), 0, s, M2, dy, w3, W2, X, Fp, dZ2, dW1, db1,
-                           db2, B, W1, b1, rows, nrows);
+                           db2, B, W1, b1, rows, nrows, mlp_dbg(), red);
       return true;
     }
     if (Fp <= 16)
@@ -1567,7 +1646,7 @@ bool launch_mlp2_bwd(const bf16_t* H1, const bf16_t* H2, const unsigned* M2, con
 bool launch_mlp2_fwd(const bf16_t* X, int Fp, const bf16_t* W1, const float* b1, const bf16_t* W2, const float* b2,
                      const float* w3, const float* b3, const float* y, bf16_t* H1, bf16_t* H2, unsigned* M2,
                      float* dw3, float* db3, float* pred, float* dy, float* loss_sum, float dy_scale, int B,
-                     const long long* rows, long nrows, hipStream_t s) {
+                     const long long* rows, long nrows, hipStream_t s, float* red) {
   if (Fp > 64 || Fp % 8 != 0 || B <= 0) return false;
   if (M2 != nullptr && (y == nullptr || dw3 == nullptr || db3 == nullptr)) return false;
   const int nchunks = (B + MF_ROWS - 1) / MF_ROWS;
@@ -1583,13 +1662,13 @@ bool launch_mlp2_fwd(const bf16_t* X, int Fp, const bf16_t* W1, const float* b1,
   if (fwd8 && M2 != nullptr && H1 == nullptr) {  // the training step (mask mode never writes H2)
     if (Fp <= 32 && (mlp_prio() & 1))
       hipLaunchKernelGGL((mlp2_fwd_train_kernel<1, 1>), dim3(grid), dim3(512), 0, s, X, Fp, W1, b1, W2, b2, w3, b3, y,
-                         M2, dw3, db3, pred, dy, loss_sum, dy_scale, B, rows, nrows);
+                         M2, dw3, db3, pred, dy, loss_sum, dy_scale, B, rows, nrows, mlp_dbg(), red);
     else if (Fp <= 32)
       hipLaunchKernelGGL(mlp2_fwd_train_kernel<1>, dim3(grid), dim3(512), 0, s, X, Fp, W1, b1, W2, b2, w3, b3, y, M2,
-                         dw3, db3, pred, dy, loss_sum, dy_scale, B, rows, nrows);
+                         dw3, db3, pred, dy, loss_sum, dy_scale, B, rows, nrows, mlp_dbg(), red);
     else
       hipLaunchKernelGGL(mlp2_fwd_train_kernel<2>, dim3(grid), dim3(512), 0, s, X, Fp, W1, b1, W2, b2, w3, b3, y, M2,
-                         dw3, db3, pred, dy, loss_sum, dy_scale, B, rows, nrows);
+                         dw3, db3, pred, dy, loss_sum, dy_scale, B, rows, nrows, mlp_dbg(), red);
     return true;
   }
   if (Fp <= 32)

@@ -26,6 +26,10 @@ import torch
 from torch import nn
 
 
+# floats of the spread-reduction scratch (csrc/kernels.h kMlpRedFloats: 64 x 9216 + 4 x 65536)
+MLP_RED_FLOATS = 64 * 9216 + 4 * 65536
+
+
 def _r8(x: int) -> int:
     return (x + 7) // 8 * 8
 
@@ -168,6 +172,12 @@ class NativeMLP:
         # dW2 = dZ2^T H1 as the generic split-K GEMM over a STORED H1 (the forward writes it)
         # instead of the H1-recomputing kernel (WELLFLOW_MLP_DW2=gemm)
         self.dw2_gemm = os.environ.get("WELLFLOW_MLP_DW2", "recompute") == "gemm"
+        # spread reduction of the fused training kernels' batch sums (csrc/mlp_fused.hip
+        # mlp2_reduce_kernel): 16 scratch copies instead of 256 same-address atomic adders per
+        # gradient entry, summed by one small launch (WELLFLOW_MLP_SPREAD=0: direct atomics)
+        spread = os.environ.get("WELLFLOW_MLP_SPREAD", "1") != "0"
+        self.red = (torch.zeros(MLP_RED_FLOATS, device=dev)
+                    if spread and self.hidden == (256, 256) and self.Fp <= 32 else None)
         self.sync_weights()
 
     def sync_weights(self) -> None:
@@ -189,20 +199,23 @@ class NativeMLP:
         pl, hw, hb = self.lay.views(self.params)
         gl, ghw, ghb = self.lay.views(self.grads)
         self._Xop = Xop
+        red = self.red
         if not self._fused_forward(B, y, self.dy, ls, 2.0 * float(grad_scale), (ghw, ghb),
-                                   store_h1=self.dw2_gemm, rows=rows):
+                                   store_h1=self.dw2_gemm, rows=rows, red=red):
             raise RuntimeError("NativeMLP: fused forward refused the recompute step")
         ok = C.mlp2_backward(None, self.Hs[1], self.dy, hw, wl[1][0], Xop, self.Fp, self.dZ[0], self.dZ[1],
-                             gl[0][0], gl[0][1], gl[1][1], ghw, ghb, B, self.M2, wl[0][0], pl[0][1], rows)
+                             gl[0][0], gl[0][1], gl[1][1], ghw, ghb, B, self.M2, wl[0][0], pl[0][1], rows, red)
         if self.dw2_gemm:
             from ..ops.native import gemm
 
             gemm(self.dZ[1], self.Hs[0], 256, 256, B, a_mn=True, lda=256, b_mn=True, ldb=256, outF=gl[1][0],
                  atomic=True, ksplit=max(1, min(64, B // 256)))
         else:
-            ok = ok and C.mlp2_dw2(self.dZ[1], Xop, self.Fp, rows, wl[0][0], pl[0][1], B, self.dw2_split, gl[1][0])
+            ok = ok and C.mlp2_dw2(self.dZ[1], Xop, self.Fp, rows, wl[0][0], pl[0][1], B, self.dw2_split, gl[1][0], red)
         if not ok:
             raise RuntimeError("NativeMLP: recompute backward refused (shape)")
+        if red is not None:
+            C.mlp2_reduce(red, self.Fp, ls, ghb, ghw, gl[0][1], gl[1][1], gl[0][0], None if self.dw2_gemm else gl[1][0])
         return ls
 
     def _load_x(self, x: torch.Tensor) -> int:
@@ -236,7 +249,7 @@ class NativeMLP:
             A, K = Hout, h
 
     def _fused_forward(self, B: int, y=None, dy=None, loss_sum=None, dy_scale: float = 0.0,
-                       head_grads=None, store_h1: bool = True, rows=None) -> bool:
+                       head_grads=None, store_h1: bool = True, rows=None, red=None) -> bool:
         """Both hidden layers + head (+ MSE) in ONE weight-stationary launch
         (csrc/mlp_fused.hip) for the BASELINE shape F -> 256 -> 256 -> 1; False = not covered.
         ``store_h1=False``: H1 is not written (inference, or a backward that recomputes it)."""
@@ -247,7 +260,7 @@ class NativeMLP:
         m2, dw3, db3 = (self.M2, *head_grads) if head_grads is not None else (None, None, None)
         return bool(self._C.mlp2_forward(self._Xop, self.Fp, wl[0][0], pl[0][1], wl[1][0], pl[1][1], hw, hb, y,
                                          self.Hs[0] if store_h1 else None, self.Hs[1], self.pred, dy, loss_sum,
-                                         float(dy_scale), B, m2, dw3, db3, rows))
+                                         float(dy_scale), B, m2, dw3, db3, rows, red))
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         B = self._load_x(x)
@@ -318,7 +331,7 @@ class NativeMLP:
         fused_bwd = (self.fused_bwd and self.hidden == (256, 256) and
                      C.mlp2_backward(self.Hs[0], self.Hs[1], self.dy, hw, wl[1][0], self._Xop, self.Fp,
                                      self.dZ[0], self.dZ[1], gl[0][0] if fused_dw1 else None, gl[0][1],
-                                     gl[1][1], ghw, ghb, B, self.M2 if use_mask else None, None, None, None))
+                                     gl[1][1], ghw, ghb, B, self.M2 if use_mask else None, None, None, None, None))
         if use_mask and not fused_bwd:
             raise RuntimeError("NativeMLP: H2 bitmask written but the fused backward did not launch")
         if not fused_bwd:

@@ -255,6 +255,41 @@ def test_mlp_recompute_step_matches_stored_h1(B, F):
     assert ((ga - gb).norm() / ga.norm()).item() < 1e-4
 
 
+def test_mlp_spread_reduction_matches_direct_atomics():
+    """The training step's batch sums through the 64-copy scratch + mlp2_reduce
+    (csrc/mlp_fused.hip) against direct same-address atomics (WELLFLOW_MLP_SPREAD=0); three
+    steps in a row must give the same gradients each time, i.e. the reduce re-zeroes its
+    scratch and leaves nothing behind for the next step."""
+    from wellflow.data.synth import synth_tabular_batch
+    from wellflow.models.mlp import NativeMLP, init_mlp_flat
+
+    B, F = 65536, 16
+    x, y = synth_tabular_batch(B, F, seed=13)
+    x, y = x.to(DEV), y.to(DEV)
+    flat = init_mlp_flat(F, (256, 256), seed=12).to(DEV)
+    engs = {}
+    for spread in ("1", "0"):
+        os.environ["WELLFLOW_MLP_SPREAD"] = spread
+        try:
+            eng = NativeMLP(F, (256, 256), B, device=DEV)
+        finally:
+            os.environ.pop("WELLFLOW_MLP_SPREAD", None)
+        eng.params.copy_(flat)
+        eng.sync_weights()
+        engs[spread] = eng
+    assert engs["1"].red is not None and engs["0"].red is None
+    ref_ls = engs["0"].forward_backward(x, y, grad_scale=1.0 / B).item()
+    torch.cuda.synchronize()
+    ref_g = engs["0"].grads.clone()
+    for _ in range(3):
+        ls = engs["1"].forward_backward(x, y, grad_scale=1.0 / B).item()
+        torch.cuda.synchronize()
+        g = engs["1"].grads
+        assert abs(ls - ref_ls) <= 1e-5 * abs(ref_ls)
+        assert ((g - ref_g).norm() / ref_g.norm()).item() < 1e-5
+    assert engs["1"].red.abs().max().item() == 0.0
+
+
 def test_mlp_row_indexed_step_matches_gathered_batch():
     """forward_backward(dataset, targets, rows=idx) reads the resident dataset through the
     index inside the fused kernels; it must equal the step on the explicitly gathered batch
