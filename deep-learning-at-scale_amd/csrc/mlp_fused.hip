@@ -1407,7 +1407,8 @@ template <int NW, int PR = 0>  // PR: s_setprio(1) around each MFMA cluster (A/B
 __global__ __launch_bounds__(64 * NW, 1) void mlp2_dw2_kernel(const bf16_t* __restrict__ dZ2, const bf16_t* __restrict__ X,
                                                               int Fp, const long long* __restrict__ rows, long nrows,
                                                               const bf16_t* __restrict__ W1, const float* __restrict__ b1,
-                                                              int kchunk, float* __restrict__ dW2, float* __restrict__ red) {
+                                                              int kchunk, float* __restrict__ dW2, float* __restrict__ red,
+                                                              int mlp_dbg_dev) {
   static_assert(NW == 4 || NW == 8, "4 or 8 waves");
   constexpr int NT = 64 * NW, BM = 128, BN = 128, MTR = 128 / (16 * NW);  // H1 unit tiles per wave
   using C = GemmCfg<BM, BN, MN_CONTIG, MN_CONTIG, 2, NW / 2>;
@@ -1562,6 +1563,7 @@ __global__ __launch_bounds__(64 * NW, 1) void mlp2_dw2_kernel(const bf16_t* __re
   const AccCoord<C> cc(m0, n0);
   // red != nullptr: copy split % 4 of the spread-reduction scratch (64 -> 16 adders per address)
   if (red != nullptr) dW2 = red + kMlpRedCopies * kMlpRedRow + (split & (kMlpRedCopies2 - 1)) * 65536;
+  if (mlp_dbg_dev & 1) return;  // timing only (WELLFLOW_MLP_DBG): no epilogue atomics
 #pragma unroll
   for (int j = 0; j < C::TN; ++j)
 #pragma unroll
@@ -1586,13 +1588,13 @@ bool launch_mlp2_dw2(const bf16_t* dZ2, const bf16_t* X, int Fp, const long long
   }();
   if (dw2_8 && (mlp_prio() & 4))
     hipLaunchKernelGGL((mlp2_dw2_kernel<8, 1>), dim3(4 * nsplit), dim3(512), 0, s, dZ2, X, Fp, rows, nrows, W1, b1, kchunk,
-                       dW2, red);
+                       dW2, red, mlp_dbg());
   else if (dw2_8)
     hipLaunchKernelGGL(mlp2_dw2_kernel<8>, dim3(4 * nsplit), dim3(512), 0, s, dZ2, X, Fp, rows, nrows, W1, b1, kchunk,
-                       dW2, red);
+                       dW2, red, mlp_dbg());
   else
     hipLaunchKernelGGL(mlp2_dw2_kernel<4>, dim3(4 * nsplit), dim3(256), 0, s, dZ2, X, Fp, rows, nrows, W1, b1, kchunk,
-                       dW2, red);
+                       dW2, red, mlp_dbg());
   return true;
 }
 
