@@ -200,20 +200,26 @@ class NativeMLP:
         gl, ghw, ghb = self.lay.views(self.grads)
         self._Xop = Xop
         red = self.red
-        if not self._fused_forward(B, y, self.dy, ls, 2.0 * float(grad_scale), (ghw, ghb),
-                                   store_h1=self.dw2_gemm, rows=rows, red=red):
-            raise RuntimeError("NativeMLP: fused forward refused the recompute step")
-        ok = C.mlp2_backward(None, self.Hs[1], self.dy, hw, wl[1][0], Xop, self.Fp, self.dZ[0], self.dZ[1],
-                             gl[0][0], gl[0][1], gl[1][1], ghw, ghb, B, self.M2, wl[0][0], pl[0][1], rows, red)
-        if self.dw2_gemm:
-            from ..ops.native import gemm
+        try:
+            if not self._fused_forward(B, y, self.dy, ls, 2.0 * float(grad_scale), (ghw, ghb),
+                                       store_h1=self.dw2_gemm, rows=rows, red=red):
+                raise RuntimeError("NativeMLP: fused forward refused the recompute step")
+            ok = C.mlp2_backward(None, self.Hs[1], self.dy, hw, wl[1][0], Xop, self.Fp, self.dZ[0], self.dZ[1],
+                                 gl[0][0], gl[0][1], gl[1][1], ghw, ghb, B, self.M2, wl[0][0], pl[0][1], rows, red)
+            if self.dw2_gemm:
+                from ..ops.native import gemm
 
-            gemm(self.dZ[1], self.Hs[0], 256, 256, B, a_mn=True, lda=256, b_mn=True, ldb=256, outF=gl[1][0],
-                 atomic=True, ksplit=max(1, min(64, B // 256)))
-        else:
-            ok = ok and C.mlp2_dw2(self.dZ[1], Xop, self.Fp, rows, wl[0][0], pl[0][1], B, self.dw2_split, gl[1][0], red)
-        if not ok:
-            raise RuntimeError("NativeMLP: recompute backward refused (shape)")
+                gemm(self.dZ[1], self.Hs[0], 256, 256, B, a_mn=True, lda=256, b_mn=True, ldb=256, outF=gl[1][0],
+                     atomic=True, ksplit=max(1, min(64, B // 256)))
+            else:
+                ok = ok and C.mlp2_dw2(self.dZ[1], Xop, self.Fp, rows, wl[0][0], pl[0][1], B, self.dw2_split,
+                                       gl[1][0], red)
+            if not ok:
+                raise RuntimeError("NativeMLP: recompute backward refused (shape)")
+        except BaseException:
+            if red is not None:  # partial sums of a step that did not finish must not reach the next one
+                red.zero_()
+            raise
         if red is not None:
             C.mlp2_reduce(red, self.Fp, ls, ghb, ghw, gl[0][1], gl[1][1], gl[0][0], None if self.dw2_gemm else gl[1][0])
         return ls
