@@ -493,19 +493,39 @@ __global__ __launch_bounds__(512, 1) void mlp2_fwd_train_kernel(
     for (int m = 0; m < MT; ++m)
 #pragma unroll
       for (int n = 0; n < 4; ++n) acc[m][n] = f32x4{0.f, 0.f, 0.f, 0.f};
-    if constexpr (PR) __builtin_amdgcn_s_setprio(1);
+    if constexpr (PR & 1) __builtin_amdgcn_s_setprio(1);
+    if constexpr ((PR & 2) != 0) {
+      // A/B (WELLFLOW_MLP_DBG bit 2): H1 fragments double-buffered one k-step ahead
+      bf16x8 hb[2][4];
 #pragma unroll
-    for (int kt = 0; kt < 8; ++kt) {
-      bf16x8 hb[4];
+      for (int n = 0; n < 4; ++n) hb[0][n] = *reinterpret_cast<const bf16x8*>(h1s + tile_off(16 * n + l15, 8 * g));
+      static_for<0, 8>([&](auto kc) {
+        constexpr int kt = decltype(kc)::value;
+        if constexpr (kt + 1 < 8) {
 #pragma unroll
-      for (int n = 0; n < 4; ++n) hb[n] = *reinterpret_cast<const bf16x8*>(h1s + tile_off(16 * n + l15, 32 * kt + 8 * g));
+          for (int n = 0; n < 4; ++n)
+            hb[(kt + 1) & 1][n] = *reinterpret_cast<const bf16x8*>(h1s + tile_off(16 * n + l15, 32 * (kt + 1) + 8 * g));
+        }
 #pragma unroll
-      for (int m = 0; m < MT; ++m)
+        for (int m = 0; m < MT; ++m)
 #pragma unroll
-        for (int n = 0; n < 4; ++n)
-          acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w2f[m][kt], hb[n], acc[m][n], 0, 0, 0);
+          for (int n = 0; n < 4; ++n)
+            acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w2f[m][kt], hb[kt & 1][n], acc[m][n], 0, 0, 0);
+      });
+    } else {
+#pragma unroll
+      for (int kt = 0; kt < 8; ++kt) {
+        bf16x8 hb[4];
+#pragma unroll
+        for (int n = 0; n < 4; ++n) hb[n] = *reinterpret_cast<const bf16x8*>(h1s + tile_off(16 * n + l15, 32 * kt + 8 * g));
+#pragma unroll
+        for (int m = 0; m < MT; ++m)
+#pragma unroll
+          for (int n = 0; n < 4; ++n)
+            acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w2f[m][kt], hb[n], acc[m][n], 0, 0, 0);
+      }
     }
-    if constexpr (PR) __builtin_amdgcn_s_setprio(0);
+    if constexpr (PR & 1) __builtin_amdgcn_s_setprio(0);
     // ---- H2 = relu(Z2 + b2) rounded to bf16 (the values the backward's mask describes), kept
     // in acc; head partial sums and ReLU bits of rows 16n + l15
     float hp[4] = {0.f, 0.f, 0.f, 0.f};
@@ -1664,6 +1684,9 @@ bool launch_mlp2_fwd(const bf16_t* X, int Fp, const bf16_t* W1, const float* b1,
   if (fwd8 && M2 != nullptr && H1 == nullptr) {  // the training step (mask mode never writes H2)
     if (Fp <= 32 && (mlp_prio() & 1))
       hipLaunchKernelGGL((mlp2_fwd_train_kernel<1, 1>), dim3(grid), dim3(512), 0, s, X, Fp, W1, b1, W2, b2, w3, b3, y,
+                         M2, dw3, db3, pred, dy, loss_sum, dy_scale, B, rows, nrows, mlp_dbg(), red);
+    else if (Fp <= 32 && (mlp_dbg() & 4))
+      hipLaunchKernelGGL((mlp2_fwd_train_kernel<1, 2>), dim3(grid), dim3(512), 0, s, X, Fp, W1, b1, W2, b2, w3, b3, y,
                          M2, dw3, db3, pred, dy, loss_sum, dy_scale, B, rows, nrows, mlp_dbg(), red);
     else if (Fp <= 32)
       hipLaunchKernelGGL(mlp2_fwd_train_kernel<1>, dim3(grid), dim3(512), 0, s, X, Fp, W1, b1, W2, b2, w3, b3, y, M2,
