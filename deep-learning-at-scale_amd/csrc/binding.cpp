@@ -508,7 +508,7 @@ bool mlp2_dw2(const at::Tensor& dZ2, const at::Tensor& X, int64_t Fp, c10::optio
 
 // Sums the spread-reduction scratch of the 8-wave MLP training kernels into the gradients
 // (mlp_fused.hip mlp2_reduce_kernel) and zeroes it; null destinations are skipped.
-void mlp2_reduce(const at::Tensor& red, int64_t Fp, c10::optional<at::Tensor> loss_sum, const at::Tensor& db3,
+void mlp2_reduce(const at::Tensor& red, int64_t Fp, int64_t B, c10::optional<at::Tensor> loss_sum, const at::Tensor& db3,
                  const at::Tensor& dw3, const at::Tensor& db1, const at::Tensor& db2, const at::Tensor& dW1,
                  c10::optional<at::Tensor> dW2) {
   constexpr int64_t H = 256;
@@ -524,7 +524,8 @@ void mlp2_reduce(const at::Tensor& red, int64_t Fp, c10::optional<at::Tensor> lo
   check_t(dW1, at::kFloat, "dW1");
   check_extent(dW1, H * Fp, "dW1");
   const c10::hip::OptionalHIPGuardMasqueradingAsCUDA guard(red.device());
-  wf::launch_mlp2_reduce(fp(red), (int)Fp, opt_ptr<float>(loss_sum, at::kFloat, "loss_sum", 1), fp(db3), fp(dw3),
+  TORCH_CHECK(B > 0, "mlp2_reduce: B > 0");
+  wf::launch_mlp2_reduce(fp(red), (int)Fp, (int)B, opt_ptr<float>(loss_sum, at::kFloat, "loss_sum", 1), fp(db3), fp(dw3),
                          fp(db1), fp(db2), fp(dW1), opt_ptr<float>(dW2, at::kFloat, "dW2", H * H), cur_stream());
 }
 

@@ -100,9 +100,17 @@ bool launch_mlp2_dw2(const bf16_t* dZ2, const bf16_t* X, int Fp, const long long
 // Zero-initialised once; mlp2_reduce sums every copy into the gradients and zeroes it again.
 constexpr int kMlpRedCopies = 64, kMlpRedCopies2 = 4, kMlpRedRow = 9216;
 constexpr int kMlpRedLoss = 0, kMlpRedDb3 = 1, kMlpRedDw3 = 2, kMlpRedDb1 = 258, kMlpRedDb2 = 514, kMlpRedDW1 = 770;
-constexpr long kMlpRedFloats = (long)kMlpRedCopies * kMlpRedRow + (long)kMlpRedCopies2 * 65536;
-void launch_mlp2_reduce(float* red, int Fp, float* loss_sum, float* db3, float* dw3, float* db1, float* db2, float* dW1,
-                        float* dW2, hipStream_t s);
+// then the backward's per-workgroup dW1 rows: [kMlpRedSlabRows][kMlpRedSlabRow] (plain stores,
+// summed over the launch's grid by the reduce: dW1 is 4096 values per workgroup, too many
+// atomic wave-instructions per CU even spread over copies)
+constexpr int kMlpRedSlabRows = 256, kMlpRedSlabRow = 256 * 32;
+constexpr long kMlpRedSlabOff = (long)kMlpRedCopies * kMlpRedRow + (long)kMlpRedCopies2 * 65536;
+constexpr long kMlpRedFloats = kMlpRedSlabOff + (long)kMlpRedSlabRows * kMlpRedSlabRow;
+// grid of the 8-wave training kernels for a batch (one workgroup per CU at most): the rows of
+// the dW1 slab the reduce sums
+int mlp2_train_grid(int B);
+void launch_mlp2_reduce(float* red, int Fp, int B, float* loss_sum, float* db3, float* dw3, float* db1, float* db2,
+                        float* dW1, float* dW2, hipStream_t s);
 
 // ---- regression head (N = 1) and losses ----
 void launch_head_fwd(const bf16_t* Hm, long ldh, int B, int Hd, const float* w, const float* b0,

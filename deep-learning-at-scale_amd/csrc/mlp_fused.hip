@@ -46,6 +46,7 @@ int mlp_dbg() {
 }
 constexpr int MF_ROWS = 64;  // rows per chunk
 }  // namespace
+constexpr int MF_ROWS_PUB = MF_ROWS;
 
 // Spread reduction of the training kernels' batch sums (kernels.h kMlpRed*): every workgroup of
 // the 8-wave forward / backward used to atomically add its partial loss, dw3, db3, db1, db2
@@ -54,12 +55,37 @@ constexpr int MF_ROWS = 64;  // rows per chunk
 // launch (WELLFLOW_MLP_DBG=1 A/B, profiles/r3_summary.md). They now add into copy
 // blockIdx % 16 of a scratch row (16 adders per address); dW2's 64 split-K adders per address
 // go to copy split % 4. mlp2_reduce_kernel sums the copies into the gradients and re-zeroes them.
-__global__ __launch_bounds__(256) void mlp2_reduce_kernel(float* __restrict__ red, int Fp, float* __restrict__ loss_sum,
+__global__ __launch_bounds__(256) void mlp2_reduce_kernel(float* __restrict__ red, int Fp, int nwg, int slab_blocks,
+                                                          float* __restrict__ loss_sum,
                                                           float* __restrict__ db3, float* __restrict__ dw3,
                                                           float* __restrict__ db1, float* __restrict__ db2,
                                                           float* __restrict__ dW1, float* __restrict__ dW2) {
+  if ((int)blockIdx.x < slab_blocks) {
+    // dW1 slab: block b sums 16 consecutive entries over the nwg (<= 256) workgroup rows in 16
+    // row groups, every thread's 16 loads independent (one latency round, not a chain)
+    __shared__ float part[16][16];
+    const int o = blockIdx.x * 16 + (threadIdx.x & 15), rg = threadIdx.x >> 4;
+    const float* sl = red + kMlpRedSlabOff;
+    float v[4] = {0.f, 0.f, 0.f, 0.f};
+    if (o < 256 * Fp) {
+#pragma unroll
+      for (int k = 0; k < kMlpRedSlabRows / 16; ++k) {
+        const int r = rg + 16 * k;
+        if (r < nwg) v[k & 3] += sl[(size_t)r * kMlpRedSlabRow + o];
+      }
+    }
+    part[rg][threadIdx.x & 15] = (v[0] + v[1]) + (v[2] + v[3]);
+    __syncthreads();
+    if (rg == 0 && o < 256 * Fp) {
+      float t = 0.f;
+#pragma unroll
+      for (int q = 0; q < 16; ++q) t += part[q][threadIdx.x];
+      if (dW1 != nullptr && t != 0.f) dW1[o] += t;
+    }
+    return;
+  }
   const int na = kMlpRedDW1 + 256 * Fp;
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  const int i = ((int)blockIdx.x - slab_blocks) * blockDim.x + threadIdx.x;
   if (i < na) {
     float v = 0.f;
 #pragma unroll
@@ -87,11 +113,25 @@ __global__ __launch_bounds__(256) void mlp2_reduce_kernel(float* __restrict__ re
   }
 }
 
-void launch_mlp2_reduce(float* red, int Fp, float* loss_sum, float* db3, float* dw3, float* db1, float* db2, float* dW1,
-                        float* dW2, hipStream_t s) {
+int mlp2_train_grid(int B) {
+  static const int cus = [] {
+    int dev = 0, n = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        n <= 0)
+      return 256;
+    return n;
+  }();
+  const int nchunks = (B + MF_ROWS_PUB - 1) / MF_ROWS_PUB;
+  const int g = nchunks < cus ? nchunks : cus;
+  return g < kMlpRedSlabRows ? g : kMlpRedSlabRows;
+}
+
+void launch_mlp2_reduce(float* red, int Fp, int B, float* loss_sum, float* db3, float* dw3, float* db1, float* db2,
+                        float* dW1, float* dW2, hipStream_t s) {
   const int n = kMlpRedDW1 + 256 * Fp + 256 * 256;
-  hipLaunchKernelGGL(mlp2_reduce_kernel, dim3((n + 255) / 256), dim3(256), 0, s, red, Fp, loss_sum, db3, dw3, db1, db2,
-                     dW1, dW2);
+  const int slab_blocks = (256 * Fp + 15) / 16;
+  hipLaunchKernelGGL(mlp2_reduce_kernel, dim3(slab_blocks + (n + 255) / 256), dim3(256), 0, s, red, Fp,
+                     mlp2_train_grid(B), slab_blocks, loss_sum, db3, dw3, db1, db2, dW1, dW2);
 }
 
 namespace {
@@ -1364,11 +1404,12 @@ __global__ __launch_bounds__(512, 1) void mlp2_bwd_rc8_kernel(
   }
   // ---- reductions
   if (dbg & 1) return;
+  float* slab = nullptr;  // this workgroup's dW1 row (plain stores, summed by mlp2_reduce)
   if (red != nullptr) {
     float* rb = red + (blockIdx.x & (kMlpRedCopies - 1)) * kMlpRedRow;
     db1 = rb + kMlpRedDb1;
     db2 = rb + kMlpRedDb2;
-    dW1 = rb + kMlpRedDW1;
+    slab = red + kMlpRedSlabOff + (size_t)blockIdx.x * kMlpRedSlabRow;
   }
 #pragma unroll
   for (int m = 0; m < MT; ++m)
@@ -1386,9 +1427,15 @@ __global__ __launch_bounds__(512, 1) void mlp2_bwd_rc8_kernel(
 #pragma unroll
     for (int f = 0; f < NFT; ++f) {
       const int ft = l15 + 16 * f;
-      if (ft < Fp)
+      if (ft < Fp) {
+        if (slab != nullptr) {
 #pragma unroll
-        for (int i = 0; i < 4; ++i) atomicAdd(dW1 + (size_t)(u0 + 16 * m + 4 * g + i) * Fp + ft, dw1a[m][f][i]);
+          for (int i = 0; i < 4; ++i) slab[(u0 + 16 * m + 4 * g + i) * Fp + ft] = dw1a[m][f][i];
+        } else {
+#pragma unroll
+          for (int i = 0; i < 4; ++i) atomicAdd(dW1 + (size_t)(u0 + 16 * m + 4 * g + i) * Fp + ft, dw1a[m][f][i]);
+        }
+      }
     }
   __syncthreads();  // the last chunk's dZ2 tile reads are done before zs becomes the db2 scratch
   float* sd = reinterpret_cast<float*>(zs);
@@ -1630,7 +1677,8 @@ bool launch_mlp2_bwd(const bf16_t* H1, const bf16_t* H2, const unsigned* M2, con
   if (hipGetDevice(&dev) != hipSuccess ||
       hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
     cus = 256;
-  const int grid = nchunks < cus ? nchunks : cus;
+  // with the spread scratch, the grid is the one mlp2_reduce sums the dW1 rows of
+  const int grid = red != nullptr ? mlp2_train_grid(B) : (nchunks < cus ? nchunks : cus);
   if (H1 == nullptr && M2 != nullptr && dW1 != nullptr) {  // the training step's configuration
     static const bool bwd8 = [] {
       const char* e = std::getenv("WELLFLOW_MLP_BWD8");

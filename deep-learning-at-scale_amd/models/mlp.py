@@ -26,8 +26,10 @@ import torch
 from torch import nn
 
 
-# floats of the spread-reduction scratch (csrc/kernels.h kMlpRedFloats: 64 x 9216 + 4 x 65536)
-MLP_RED_FLOATS = 64 * 9216 + 4 * 65536
+# floats of the spread-reduction scratch (csrc/kernels.h kMlpRedFloats: 64 x 9216 copies,
+# 4 x 65536 dW2 copies, 256 x 8192 dW1 workgroup rows)
+MLP_RED_COPY_FLOATS = 64 * 9216 + 4 * 65536  # the atomic copies: zero between steps
+MLP_RED_FLOATS = MLP_RED_COPY_FLOATS + 256 * 8192
 
 
 def _r8(x: int) -> int:
@@ -221,7 +223,8 @@ class NativeMLP:
                 red.zero_()
             raise
         if red is not None:
-            C.mlp2_reduce(red, self.Fp, ls, ghb, ghw, gl[0][1], gl[1][1], gl[0][0], None if self.dw2_gemm else gl[1][0])
+            C.mlp2_reduce(red, self.Fp, B, ls, ghb, ghw, gl[0][1], gl[1][1], gl[0][0],
+                          None if self.dw2_gemm else gl[1][0])
         return ls
 
     def _load_x(self, x: torch.Tensor) -> int:

@@ -256,12 +256,12 @@ def test_mlp_recompute_step_matches_stored_h1(B, F):
 
 
 def test_mlp_spread_reduction_matches_direct_atomics():
-    """The training step's batch sums through the 64-copy scratch + mlp2_reduce
-    (csrc/mlp_fused.hip) against direct same-address atomics (WELLFLOW_MLP_SPREAD=0); three
-    steps in a row must give the same gradients each time, i.e. the reduce re-zeroes its
-    scratch and leaves nothing behind for the next step."""
+    """The training step's batch sums through the 64-copy scratch, the backward's per-workgroup
+    dW1 rows and mlp2_reduce (csrc/mlp_fused.hip) against direct same-address atomics
+    (WELLFLOW_MLP_SPREAD=0); three steps in a row must give the same gradients each time, i.e.
+    the reduce re-zeroes the copies and leaves nothing behind for the next step."""
     from wellflow.data.synth import synth_tabular_batch
-    from wellflow.models.mlp import NativeMLP, init_mlp_flat
+    from wellflow.models.mlp import MLP_RED_COPY_FLOATS, NativeMLP, init_mlp_flat
 
     B, F = 65536, 16
     x, y = synth_tabular_batch(B, F, seed=13)
@@ -287,7 +287,8 @@ def test_mlp_spread_reduction_matches_direct_atomics():
         g = engs["1"].grads
         assert abs(ls - ref_ls) <= 1e-5 * abs(ref_ls)
         assert ((g - ref_g).norm() / ref_g.norm()).item() < 1e-5
-    assert engs["1"].red.abs().max().item() == 0.0
+    # the atomic copies are re-zeroed by the reduce (the dW1 rows after them are overwritten)
+    assert engs["1"].red[:MLP_RED_COPY_FLOATS].abs().max().item() == 0.0
 
 
 def test_mlp_row_indexed_step_matches_gathered_batch():

@@ -14,3 +14,4 @@ for arm in "WELLFLOW_MLP_DBG=0" "WELLFLOW_MLP_DBG=4" "WELLFLOW_MLP_PRIO=1" "WELL
     -- python3 bench.py --model mlp --secondary none > gpurun_out/mab_$i.log 2>&1 || exit $?
   echo "$arm $(grep -o '"value": [0-9.]*' gpurun_out/mab_$i.log | head -1) $(python3 tools/kstats.py gpurun_out/mab_$i/run_kernel_stats.csv | grep -E 'fwd_train' | awk '{print $(NF-2), $(NF-1)}')"
 done
+BATCHES="16384 262144" bash tools/r3_mlp_scan.sh
