@@ -53,8 +53,10 @@ constexpr int MF_ROWS_PUB = MF_ROWS;
 // and dW1 straight into the gradient, i.e. 256 adders per address at the same moment, and the
 // atomic unit serialises same-address adds: ~25 us of each ~36 us one-chunk-per-workgroup
 // launch (WELLFLOW_MLP_DBG=1 A/B, profiles/r3_summary.md). They now add into copy
-// blockIdx % 16 of a scratch row (16 adders per address); dW2's 64 split-K adders per address
-// go to copy split % 4. mlp2_reduce_kernel sums the copies into the gradients and re-zeroes them.
+// blockIdx % kMlpRedCopies (64) of a scratch row (4 adders per address); dW2's 64 split-K adders
+// per address go to copy split % 4; the backward's dW1 (4096 values per workgroup, too many
+// atomic wave-instructions per CU) goes out as plain per-workgroup rows. mlp2_reduce_kernel
+// sums copies and rows into the gradients and re-zeroes the copies.
 __global__ __launch_bounds__(256) void mlp2_reduce_kernel(float* __restrict__ red, int Fp, int nwg, int slab_blocks,
                                                           float* __restrict__ loss_sum,
                                                           float* __restrict__ db3, float* __restrict__ dw3,
@@ -426,7 +428,7 @@ __global__ __launch_bounds__(512, 1) void mlp2_fwd_train_kernel(
     float* __restrict__ db3, float* __restrict__ pred, float* __restrict__ dy, float* __restrict__ loss_sum,
     float dy_scale, int B, const long long* __restrict__ rows, long nrows, int dbg, float* __restrict__ rscr) {
   // dbg (WELLFLOW_MLP_DBG, timing only, wrong results): 1 = no epilogue atomics, 2 = no W2 loads
-  // rscr != nullptr: the batch sums go to copy blockIdx % 16 of the spread-reduction scratch
+  // rscr != nullptr: the batch sums go to copy blockIdx % kMlpRedCopies of the spread-reduction scratch
   constexpr int NW = 8, MT = 2;  // waves; 16-unit M tiles per wave
   __shared__ __attribute__((aligned(16))) char xs[MF_ROWS * MF_XROW];
   __shared__ __attribute__((aligned(16))) char h1s[MF_ROWS * MF_H * 2];
@@ -1211,7 +1213,7 @@ __global__ __launch_bounds__(512, 1) void mlp2_bwd_rc8_kernel(
     float* __restrict__ dW1, float* __restrict__ db1, float* __restrict__ db2, int B,
     const bf16_t* __restrict__ W1, const float* __restrict__ b1, const long long* __restrict__ rows, long nrows,
     int dbg, float* __restrict__ red) {
-  // red != nullptr: db1, db2, dW1 go to copy blockIdx % 16 of the spread-reduction scratch
+  // red != nullptr: db1, db2, dW1 go to copy blockIdx % kMlpRedCopies of the spread-reduction scratch
   // dbg (WELLFLOW_MLP_DBG, timing only, wrong results): 1 = no epilogue atomics, 2 = no W2^T gather
   constexpr int MT = 2, ZB = MF_ROWS * MF_H * 2, XB = MF_ROWS * MF_XROW;
   __shared__ __attribute__((aligned(16))) char zs[2 * ZB];  // dZ2 tiles (double-buffered)
