@@ -1213,7 +1213,7 @@ __global__ __launch_bounds__(512, 1) void mlp2_bwd_rc8_kernel(
     float* __restrict__ dW1, float* __restrict__ db1, float* __restrict__ db2, int B,
     const bf16_t* __restrict__ W1, const float* __restrict__ b1, const long long* __restrict__ rows, long nrows,
     int dbg, float* __restrict__ red) {
-  // red != nullptr: db1, db2, dW1 go to copy blockIdx % kMlpRedCopies of the spread-reduction scratch
+  // red != nullptr: db1, db2 go to copy blockIdx % kMlpRedCopies of the spread-reduction scratch, dW1 to this workgroup's row
   // dbg (WELLFLOW_MLP_DBG, timing only, wrong results): 1 = no epilogue atomics, 2 = no W2^T gather
   constexpr int MT = 2, ZB = MF_ROWS * MF_H * 2, XB = MF_ROWS * MF_XROW;
   __shared__ __attribute__((aligned(16))) char zs[2 * ZB];  // dZ2 tiles (double-buffered)
