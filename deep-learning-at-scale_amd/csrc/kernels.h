@@ -109,6 +109,7 @@ constexpr long kMlpRedFloats = kMlpRedSlabOff + (long)kMlpRedSlabRows * kMlpRedS
 // grid of the 8-wave training kernels for a batch (one workgroup per CU at most): the rows of
 // the dW1 slab the reduce sums
 int mlp2_train_grid(int B);
+bool mlp_bwd8();  // the 8-wave backward is selected (WELLFLOW_MLP_BWD8, default on)
 void launch_mlp2_reduce(float* red, int Fp, int B, float* loss_sum, float* db3, float* dw3, float* db1, float* db2,
                         float* dW1, float* dW2, hipStream_t s);
 

@@ -115,6 +115,14 @@ __global__ __launch_bounds__(256) void mlp2_reduce_kernel(float* __restrict__ re
   }
 }
 
+bool mlp_bwd8() {
+  static const bool v = [] {
+    const char* e = std::getenv("WELLFLOW_MLP_BWD8");
+    return e == nullptr || e[0] != '0';
+  }();
+  return v;
+}
+
 int mlp2_train_grid(int B) {
   static const int cus = [] {
     int dev = 0, n = 0;
@@ -131,7 +139,8 @@ int mlp2_train_grid(int B) {
 void launch_mlp2_reduce(float* red, int Fp, int B, float* loss_sum, float* db3, float* dw3, float* db1, float* db2,
                         float* dW1, float* dW2, hipStream_t s) {
   const int n = kMlpRedDW1 + 256 * Fp + 256 * 256;
-  const int slab_blocks = (256 * Fp + 15) / 16;
+  // the dW1 rows exist only when the 8-wave backward ran (the 4-wave one adds dW1 itself)
+  const int slab_blocks = mlp_bwd8() ? (256 * Fp + 15) / 16 : 0;
   hipLaunchKernelGGL(mlp2_reduce_kernel, dim3(slab_blocks + (n + 255) / 256), dim3(256), 0, s, red, Fp,
                      mlp2_train_grid(B), slab_blocks, loss_sum, db3, dw3, db1, db2, dW1, dW2);
 }
@@ -1682,11 +1691,7 @@ bool launch_mlp2_bwd(const bf16_t* H1, const bf16_t* H2, const unsigned* M2, con
   // with the spread scratch, the grid is the one mlp2_reduce sums the dW1 rows of
   const int grid = red != nullptr ? mlp2_train_grid(B) : (nchunks < cus ? nchunks : cus);
   if (H1 == nullptr && M2 != nullptr && dW1 != nullptr) {  // the training step's configuration
-    static const bool bwd8 = [] {
-      const char* e = std::getenv("WELLFLOW_MLP_BWD8");
-      return e == nullptr || e[0] != '0';
-    }();
-    if (bwd8) {
+    if (mlp_bwd8()) {
       if (Fp <= 16 && (mlp_prio() & 2))
         hipLaunchKernelGGL((mlp2_bwd_rc8_kernel<1, 1>), dim3(grid), dim3(512), 0, s, M2, dy, w3, W2, X, Fp, dZ2, dW1, db1,
                            db2, B, W1, b1, rows, nrows, mlp_dbg(), red);
