@@ -218,7 +218,8 @@ __global__ __launch_bounds__(256, 1) void lstm_bwd_persistent_kernel(
           }
           __builtin_amdgcn_s_sleep(2);
         }
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        // (d.dbg bit 22, WELLFLOW_PF_DBG=4194304: TIMING ONLY, unsafe — no acquire, to price it)
+        if (!((d.dbg >> 22) & 1)) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         const int ok = why == 0 ? 1 : 0;
         asm volatile("ds_write_b32 %0, %1" ::"v"(lds0 + FLAG), "v"(ok) : "memory");
