@@ -44,6 +44,24 @@ METRIC = "rows/sec (whole node), LSTM seq64 regression at 1/2/4/8 MI355X; val MS
 DEFAULT_BATCH = {"lstm": 8192, "mlp": 262144, "mlp_online": 262144, "cnn": 65536}
 
 
+# Timing-only / test-hook variables: a production _C.so ignores the first two (csrc/
+# persistent_guard.h kDbgMask, mlp_fused.hip kMlpDbgMask), the test hooks make a run fail; the
+# bench refuses all of them so no number is ever taken with one set (round-3 VERDICT item 2).
+DIAG_ENV = ("WELLFLOW_PF_DBG", "WELLFLOW_MLP_DBG", "WELLFLOW_FORCE_TIMEOUT", "WELLFLOW_SPIN_LIMIT",
+            "WELLFLOW_DIAG_BUILD")
+ENV_PREFIXES = ("WELLFLOW_", "HSA_", "HIP_", "NCCL_", "RCCL_", "GPU_MAX_", "ROCR_", "AMD_", "TORCH_NCCL_")
+
+
+def _diag_env() -> dict:
+    return {k: os.environ[k] for k in DIAG_ENV if os.environ.get(k, "") not in ("", "0")}
+
+
+def _env_record() -> dict:
+    """Every tuning / runtime variable this process saw (WELLFLOW_* knobs, HSA / HIP / RCCL
+    settings), so the JSON line says exactly what configuration produced the number."""
+    return {k: v for k, v in sorted(os.environ.items()) if k.startswith(ENV_PREFIXES)}
+
+
 def _free_port() -> int:
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
@@ -67,7 +85,14 @@ def _spawn_ranks(n: int, argv) -> int:
     return subprocess.run(cmd, env=env, cwd=ROOT).returncode
 
 
-def _timed(ctx, step, steps, warmup):
+def _timed(ctx, step, steps, warmup, min_s: float = 0.0):
+    """W untimed warmup steps, then EXACTLY `steps` timed steps bracketed by barrier +
+    synchronize on both sides; the max over ranks. With min_s > 0 (the secondary configs) a
+    short untimed probe first raises `steps` until the timed window is >= min_s on the slowest
+    rank, so one hiccup of tens of microseconds is not a percent of the number (round-3 VERDICT
+    weak #5). Returns (seconds, timed steps, total steps run)."""
+    import math
+
     import torch
 
     def sync():
@@ -76,6 +101,19 @@ def _timed(ctx, step, steps, warmup):
 
     for _ in range(warmup):
         step()
+    total = warmup
+    if min_s > 0:
+        probe = 5
+        ctx.barrier()
+        sync()
+        t0 = time.perf_counter()
+        for _ in range(probe):
+            step()
+        sync()
+        ctx.barrier()
+        per = ctx.max_scalar(time.perf_counter() - t0) / probe
+        total += probe
+        steps = max(steps, int(math.ceil(min_s * 1.1 / max(per, 1e-9))))
     ctx.barrier()
     sync()
     t0 = time.perf_counter()
@@ -83,7 +121,7 @@ def _timed(ctx, step, steps, warmup):
         step()
     sync()
     ctx.barrier()
-    return ctx.max_scalar(time.perf_counter() - t0)
+    return ctx.max_scalar(time.perf_counter() - t0), steps, total + steps
 
 
 def _comm_ms(ctx, buf, iters: int = 20) -> float | None:
@@ -167,11 +205,11 @@ def bench_lstm(args, ctx):
     x, y = x.to(ctx.device), y.to(ctx.device)
     run = StepRunner(eng, opt, ctx, 1.0 / (B * ctx.world_size), lambda k: (x, y),
                      graph=not (args.no_graph or eng.dw_chunk > 0), comm_in_graph=not args.eager_comm)
-    el = _timed(ctx, run.run, args.steps, args.warmup)
+    el, k, n = _timed(ctx, run.run, args.steps, args.warmup, args.min_timed_s)
     eng.check_device_errors()  # a timed-out persistent hand-off anywhere in the run fails the bench
     extra = {"persistent_fwd": eng.last_forward_persistent, "persistent_bwd": eng.last_backward_persistent}
     # the engine adds each step's loss straight into the runner's accumulator: mean over the run
-    return el, B, model, run.take_loss() / (B * (args.steps + args.warmup)), run, eng, extra
+    return el, k, B, model, run.take_loss() / (B * n), run, eng, extra
 
 
 def _cpu_rehearsal(args, ctx, model):
@@ -206,8 +244,8 @@ def _cpu_rehearsal(args, ctx, model):
     ctx.broadcast_(eng.params)
     opt = FlatAdam(eng.params, eng.grads, lr=args.lr)
     run = StepRunner(eng, opt, ctx, 1.0 / (B * ctx.world_size), lambda k: (x, y))
-    el = _timed(ctx, run.run, args.steps, args.warmup)
-    return el, B, model, run.take_loss() / (B * (args.steps + args.warmup)), run, eng, {}
+    el, k, n = _timed(ctx, run.run, args.steps, args.warmup, args.min_timed_s)
+    return el, k, B, model, run.take_loss() / (B * n), run, eng, {}
 
 
 def bench_cnn(args, ctx):
@@ -238,8 +276,8 @@ def bench_cnn(args, ctx):
     y = series[:, lay.input_len :].contiguous().to(ctx.device)
     run = StepRunner(eng, opt, ctx, 1.0 / (B * ctx.world_size * lay.outputs), lambda k: (x, y),
                      graph=not args.no_graph, comm_in_graph=not args.eager_comm)
-    el = _timed(ctx, run.run, args.steps, args.warmup)
-    return el, B, model, run.take_loss() / (B * lay.outputs * (args.steps + args.warmup)), run, eng, {}
+    el, k, n = _timed(ctx, run.run, args.steps, args.warmup, args.min_timed_s)
+    return el, k, B, model, run.take_loss() / (B * lay.outputs * n), run, eng, {}
 
 
 def bench_mlp(args, ctx, online: bool):
@@ -291,13 +329,13 @@ def bench_mlp(args, ctx, online: bool):
         x, y = x.to(ctx.device, eng.input_dtype), y.to(ctx.device)
         run = StepRunner(eng, opt, ctx, gscale, lambda k: (x, y), graph=graph, comm_in_graph=not args.eager_comm)
         step = run.run
-    el = _timed(ctx, step, args.steps, args.warmup)
+    el, k, n = _timed(ctx, step, args.steps, args.warmup, args.min_timed_s)
     if online:
         extra.update(streamer.copy_stats(skip=args.warmup))
         extra["h2d_mb_per_step"] = round((streamer.slots[0][0].numel() * streamer.slots[0][0].element_size()
                                           + streamer.slots[0][1].numel() * 4) / 1e6, 3)
     # the engine adds each step's loss straight into the runner's accumulator: mean over the run
-    return el, B, model, run.take_loss() / (B * (args.steps + args.warmup)), run, eng, extra
+    return el, k, B, model, run.take_loss() / (B * n), run, eng, extra
 
 
 SECONDARY = ("mlp", "mlp_online", "cnn")
@@ -326,13 +364,14 @@ def _secondary(args, ctx, models) -> dict:
         a = argparse.Namespace(**vars(args))
         a.model = m
         a.batch = (CPU_BATCH if ctx.device.type == "cpu" else DEFAULT_BATCH)[m]
+        a.min_timed_s = args.secondary_min_s  # the headline keeps the driver's --steps exactly
         gc.collect()
         if ctx.device.type == "cuda":
             torch.cuda.empty_cache()
-        el, B, desc, loss, run, eng, extra = _run_model(a, ctx)
+        el, k, B, desc, loss, run, eng, extra = _run_model(a, ctx)
         W = ctx.world_size
-        out[m] = {"metric": f"rows/sec (whole node), {m} regression training", "value": round(B * W * a.steps / el, 1),
-                  "unit": "rows/s", "ms_per_step": round(1000.0 * el / max(a.steps, 1), 4), "steps": a.steps,
+        out[m] = {"metric": f"rows/sec (whole node), {m} regression training", "value": round(B * W * k / el, 1),
+                  "unit": "rows/s", "ms_per_step": round(1000.0 * el / max(k, 1), 4), "steps": k,
                   "warmup": a.warmup, "timed_s": round(el, 4), "per_gpu_batch": B, "global_batch": B * W,
                   "model": desc, "train_loss": round(loss, 6), "step_graph": bool(run.graphs),
                   **{k: v for k, v in extra.items() if k.startswith("h2d") or k in ("persistent_fwd",)}}
@@ -363,14 +402,23 @@ def main() -> int:
     ap.add_argument("--secondary", default="auto",
                     help="comma list of configs timed after the headline (mlp,mlp_online,cnn), 'none'; "
                          "auto = all three after the default LSTM headline, none otherwise")
+    ap.add_argument("--secondary-min-s", type=float, default=None,
+                    help="minimum timed window per secondary config (its steps are raised to reach it); "
+                         "default 0.1 s on the GPU, 0 on the CPU rehearsal")
+    ap.add_argument("--parity", choices=["auto", "on", "none"], default="auto",
+                    help="after every timed region: 20-step Adam trajectory of the headline shape vs fp32 "
+                         "torch on the same GPU (auto = with the default headline)")
     args = ap.parse_args()
+    args.min_timed_s = 0.0  # the headline: exactly --steps
+    if args.secondary_min_s is None:
+        args.secondary_min_s = 0.0 if args.device == "cpu" else 0.1
     if args.batch is None:
         args.batch = DEFAULT_BATCH[args.model]
         if args.device == "cpu":  # the fp32 CPU rehearsal: N ranks share one host's memory
             args.batch = CPU_BATCH[args.model]
+    default_headline = args.model == "lstm" and (args.batch, args.seq, args.hidden, args.features) == (
+        DEFAULT_BATCH["lstm"] if args.device != "cpu" else CPU_BATCH["lstm"], 64, 512, 16)
     if args.secondary == "auto":
-        default_headline = args.model == "lstm" and (args.batch, args.seq, args.hidden, args.features) == (
-            DEFAULT_BATCH["lstm"] if args.device != "cpu" else CPU_BATCH["lstm"], 64, 512, 16)
         secondary = list(SECONDARY) if default_headline else []
     else:
         secondary = [m for m in args.secondary.split(",") if m and m != "none"]
@@ -378,6 +426,11 @@ def main() -> int:
         if bad:
             ap.error(f"--secondary: unknown {bad}")
 
+    bad = _diag_env()
+    if bad:
+        # timing-only switches produce a faster, WRONG step: never a benchmark number
+        print(f"bench.py: refusing to run with diagnostic variables set: {bad}", file=sys.stderr)
+        return 3
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
         return _spawn_ranks(args.gpus, sys.argv[1:])
 
@@ -396,13 +449,36 @@ def main() -> int:
         print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={ctx.world_size}", file=sys.stderr)
         ctx.shutdown()
         return 2
+    if not cpu:
+        from wellflow.ops.native import lib
+
+        if lib().diag_build():
+            print("bench.py: the loaded _C.so is a WF_DIAG build (timing-only variants live); "
+                  "rebuild without WELLFLOW_DIAG_BUILD", file=sys.stderr)
+            ctx.shutdown()
+            return 3
     torch.manual_seed(1234 + ctx.rank)
-    elapsed, B, model, loss, run, eng, extra = _run_model(args, ctx)
+    elapsed, steps, B, model, loss, run, eng, extra = _run_model(args, ctx)
+    assert steps == args.steps
     comm = _comm_ms(ctx, eng.grads)
     grad_mb = round(eng.grads.numel() * 4 / 2**20, 3)
     step_graph, comm_in_graph = bool(run.graphs), bool(run.captured_comm)
     del run, eng
     sec = _secondary(args, ctx, secondary) if secondary else None
+    par = None
+    if not cpu and (args.parity == "on" or (args.parity == "auto" and default_headline)):
+        # numerics of the headline step, after every timed region (rank 0's GPU; the others wait)
+        if ctx.is_main:
+            import gc
+
+            from wellflow.train.parity import lstm_adam_trajectory
+
+            gc.collect()
+            torch.cuda.empty_cache()
+            par = lstm_adam_trajectory(ctx.device)
+            par.pop("native", None)
+            par.pop("fp32", None)
+        ctx.barrier()
 
     W = ctx.world_size
     if ctx.is_main:
@@ -453,6 +529,9 @@ def main() -> int:
             rec["hsa_enable_ipc_mode_legacy"] = os.environ.get("HSA_ENABLE_IPC_MODE_LEGACY")
         if sec is not None:
             rec["secondary"] = sec
+        if par is not None:
+            rec["parity"] = par
+        rec["env"] = _env_record()
         print(json.dumps(rec), flush=True)
     ctx.shutdown()
     return 0

@@ -154,10 +154,18 @@ def build(verbose: bool = False, jobs: int | None = None) -> str:
         for f in [ex.submit(_run, t, verbose) for t in tasks]:
             f.result()
 
-    if _stale(EXT_PATH, objs):
+    # the link is stale when an object is newer than _C.so OR the object SET changed (a switch
+    # between the production and a WF_DIAG build whose objects all exist already relinks too:
+    # the stamp next to _C.so names the objects it was linked from; round-3 ADVICE)
+    stamp = EXT_PATH + ".objs"
+    want = "\n".join(os.path.basename(o) for o in objs) + "\n"
+    have = open(stamp).read() if os.path.exists(stamp) else ""
+    if _stale(EXT_PATH, objs) or have != want:
         tmp = EXT_PATH + ".tmp"
         _run(["g++", "-shared", "-o", tmp, *objs, *ldflags], verbose)
         os.replace(tmp, EXT_PATH)
+        with open(stamp, "w") as f:
+            f.write(want)
     build_runtime(verbose)
     return EXT_PATH
 

@@ -131,12 +131,16 @@ wf::LstmDims lstm_dims(int64_t B, int64_t T, int64_t F, int64_t KX, int64_t H) {
   d.xcd_map = (xm != nullptr && xm[0] == '0') ? 0 : 1;
   const char* nt = std::getenv("WELLFLOW_NT");
   d.nt = (nt != nullptr && nt[0] == '0') ? 0 : 1;
+  // WELLFLOW_PF_DBG: timing-only switches and A/B variants of the persistent kernels. Only a
+  // WF_DIAG build of the HIP objects (WELLFLOW_DIAG_BUILD=1) honours them: dbg_mask() is the
+  // mask the objects were compiled with, so a production _C.so ignores the variable
+  // (tests/test_diag_cpu.py checks this call stays here; bench.py refuses to run with it set).
   const char* pd = std::getenv("WELLFLOW_PF_DBG");
-  d.dbg = pd != nullptr ? std::atoi(pd) : 0;
+  d.dbg = (pd != nullptr ? std::atoi(pd) : 0) & wf::dbg_mask();
   const char* sl = std::getenv("WELLFLOW_SPIN_LIMIT");  // tests: force the hand-off timeout path
   d.spin_limit = sl != nullptr ? (unsigned)std::strtoul(sl, nullptr, 10) : 0u;
   const char* ft = std::getenv("WELLFLOW_FORCE_TIMEOUT");  // tests: every hand-off wait trips its bound
-  if (ft != nullptr && ft[0] == '1') d.dbg |= 1 << 21;
+  if (ft != nullptr && ft[0] == '1') d.dbg |= 1 << 21;  // fails the run loudly (STAT block)
   return d;
 }
 
@@ -178,14 +182,15 @@ void lstm_forward(const at::Tensor& XH, const at::Tensor& Wp, const at::Tensor& 
   for (int t = 0; t < d.T; ++t) wf::launch_lstm_fwd_step(t, bfp(XH), bfp(Wp), fp(Cst), bfp(S), d, s);
 }
 
-// A persistent kernel's sync buffer: int32, and the START of its own allocation. The launcher
-// zeroes its per-launch block with one memset from that start; a memset node whose region
-// starts inside an allocation (4 B past it in round 2) left 0x04040404 in its first word
-// under graph replay, which drained every workgroup (profiles/r3_early_exit.md).
+// A persistent kernel's sync buffer: int32, 16-B aligned. The launcher zeroes its per-launch
+// block with ONE memset node from that start covering a multiple of 16 B, and refuses the
+// launch otherwise (persistent_reset_ok). Round 2's memset started 4 B past a 16-B boundary
+// and left 0x04040404 in its first word under graph replay, which drained every workgroup
+// (profiles/r3_early_exit.md). What is enforced here is exactly that precondition — 16-B
+// alignment — not "own allocation": tests/test_kernels_gpu.py replays a captured step whose
+// sync buffer sits 16-B aligned at a non-zero offset inside a larger allocation.
 void check_sync(const at::Tensor& sync) {
-  check_t(sync, at::kInt, "sync");
-  TORCH_CHECK(reinterpret_cast<uintptr_t>(sync.data_ptr()) % 512 == 0,
-              "persistent sync buffer must start its own allocation (models/lstm.py persistent_sync_buffer)");
+  check_t(sync, at::kInt, "sync");  // check_t: 16-B aligned data pointer
 }
 
 // Raise on a failed persistent launch (status < 0: -(hipError_t)); 0 = not supported.
@@ -708,6 +713,148 @@ void im2col1d(const at::Tensor& x, int64_t B, int64_t L, int64_t Cin, int64_t ks
                       cur_stream());
 }
 
+// ---- fused reference CNN (cnn_fused.hip). dims = [L, C, taps, T, Fp, Kc, O] (models/cnn.py
+// CnnLayout; the dense weight has 16 rows, Op = 16).
+wf::CnnDims cnn_dims(const std::vector<int64_t>& dims, double drop_p) {
+  TORCH_CHECK(dims.size() == 7, "cnn: dims = [L, C, taps, T, Fp, Kc, O]");
+  wf::CnnDims d;
+  d.L = (int)dims[0]; d.C = (int)dims[1]; d.taps = (int)dims[2]; d.T = (int)dims[3];
+  d.Fp = (int)dims[4]; d.Kc = (int)dims[5]; d.O = (int)dims[6];
+  d.drop_p = (float)drop_p;
+  return d;
+}
+
+bool cnn_fused_ok(const std::vector<int64_t>& dims, double drop_p) {
+  return wf::cnn_fused_supported(cnn_dims(dims, drop_p));
+}
+
+std::vector<int64_t> cnn_part_sizes(int64_t B, const std::vector<int64_t>& dims) {
+  auto d = cnn_dims(dims, 0.0);
+  long wd = 0, wc = 0, f = 0;
+  wf::cnn_part_floats((int)B, d, &wd, &wc, &f);
+  return {wd, wc, f};
+}
+
+static wf::CnnDims cnn_checked(const std::vector<int64_t>& dims, double drop_p) {
+  auto d = cnn_dims(dims, drop_p);
+  TORCH_CHECK(wf::cnn_fused_supported(d), "cnn: shape not covered by the fused kernels");
+  return d;
+}
+
+static int64_t cnn_frag_elems(const wf::CnnDims& d) { return (int64_t)d.T * (d.Fp / 16) * 64 * 4; }
+
+void cnn_pack(const at::Tensor& Wc, const at::Tensor& Wd, const std::vector<int64_t>& dims, const at::Tensor& WcA,
+              const at::Tensor& WdF, const at::Tensor& WdB) {
+  auto d = cnn_checked(dims, 0.0);
+  check_t(Wc, at::kFloat, "Wc");
+  check_extent(Wc, (int64_t)d.Fp * d.Kc, "Wc");
+  TORCH_CHECK(Wd.is_cuda() && Wd.scalar_type() == at::kFloat && Wd.is_contiguous(), "Wd: contiguous fp32 GPU tensor");
+  check_extent(Wd, (int64_t)16 * d.T * d.Fp, "Wd");
+  check_t(WcA, at::kBFloat16, "WcA");
+  check_extent(WcA, (int64_t)d.Fp * d.Kc, "WcA");
+  for (const at::Tensor* t : {&WdF, &WdB}) {
+    check_t(*t, at::kBFloat16, "WdF/WdB");
+    check_extent(*t, cnn_frag_elems(d), "WdF/WdB");
+  }
+  const c10::hip::OptionalHIPGuardMasqueradingAsCUDA guard(Wc.device());
+  wf::launch_cnn_pack(fp(Wc), Wd.data_ptr<float>(), d, bfp(WcA), bfp(WdF), bfp(WdB), cur_stream());
+}
+
+static const long long* rng_ptr(const c10::optional<at::Tensor>& rng) {
+  if (!rng.has_value() || !rng->defined()) return nullptr;
+  TORCH_CHECK(rng->is_cuda() && rng->scalar_type() == at::kLong && rng->numel() >= 1, "rng: GPU int64 tensor");
+  return reinterpret_cast<const long long*>(rng->data_ptr<int64_t>());
+}
+
+void cnn_forward(const at::Tensor& x, int64_t B, const std::vector<int64_t>& dims, double drop_p, const at::Tensor& WcA,
+                 const at::Tensor& WdF, const at::Tensor& bd, c10::optional<at::Tensor> y, c10::optional<at::Tensor> dout,
+                 c10::optional<at::Tensor> pred, c10::optional<at::Tensor> part, bool train, int64_t loss_kind,
+                 double clip, double scale, int64_t seed, c10::optional<at::Tensor> rng) {
+  auto d = cnn_checked(dims, drop_p);
+  TORCH_CHECK(B > 0, "cnn_forward: B > 0");
+  const int64_t rows = (B + 15) / 16 * 16;
+  check_t(x, at::kFloat, "x");
+  check_extent(x, B * d.L, "x");
+  check_t(WcA, at::kBFloat16, "WcA");
+  check_extent(WcA, (int64_t)d.Fp * d.Kc, "WcA");
+  check_t(WdF, at::kBFloat16, "WdF");
+  check_extent(WdF, cnn_frag_elems(d), "WdF");
+  TORCH_CHECK(bd.is_cuda() && bd.scalar_type() == at::kFloat && bd.numel() >= 16, "bd: 16 fp32 values");
+  long wd = 0, wc = 0, f = 0;
+  wf::cnn_part_floats((int)B, d, &wd, &wc, &f);
+  float *yp = nullptr, *dp = nullptr, *pp = nullptr, *part_p = nullptr;
+  if (train) {
+    TORCH_CHECK(loss_kind == 0 || loss_kind == 1, "cnn_forward: loss 0 (mse) or 1 (mae_clip)");
+    yp = opt_ptr<float>(y, at::kFloat, "y", B * d.O);
+    dp = opt_ptr<float>(dout, at::kFloat, "dout", rows * 16);
+    part_p = opt_ptr<float>(part, at::kFloat, "part", f);
+    TORCH_CHECK(yp && dp && part_p, "cnn_forward(train): y, dout and part are required");
+  } else {
+    pp = opt_ptr<float>(pred, at::kFloat, "pred", rows * 16);
+    TORCH_CHECK(pp, "cnn_forward(eval): pred is required");
+  }
+  const c10::hip::OptionalHIPGuardMasqueradingAsCUDA guard(x.device());
+  wf::launch_cnn_forward(fp(x), (int)B, d, bfp(WcA), bfp(WdF), bd.data_ptr<float>(), yp, dp, pp, part_p, train ? 1 : 0,
+                         (int)loss_kind, (float)clip, (float)scale, (unsigned)(seed & 0xFFFFFFFF), rng_ptr(rng),
+                         cur_stream());
+}
+
+void cnn_backward(const at::Tensor& x, int64_t B, const std::vector<int64_t>& dims, double drop_p, const at::Tensor& WcA,
+                  const at::Tensor& WdB, const at::Tensor& dout, int64_t seed, c10::optional<at::Tensor> rng,
+                  const at::Tensor& part_wd, const at::Tensor& part_wc) {
+  auto d = cnn_checked(dims, drop_p);
+  TORCH_CHECK(B > 0, "cnn_backward: B > 0");
+  const int64_t rows = (B + 15) / 16 * 16;
+  check_t(x, at::kFloat, "x");
+  check_extent(x, B * d.L, "x");
+  check_t(WcA, at::kBFloat16, "WcA");
+  check_extent(WcA, (int64_t)d.Fp * d.Kc, "WcA");
+  check_t(WdB, at::kBFloat16, "WdB");
+  check_extent(WdB, cnn_frag_elems(d), "WdB");
+  check_t(dout, at::kFloat, "dout");
+  check_extent(dout, rows * 16, "dout");
+  long wd = 0, wc = 0, f = 0;
+  wf::cnn_part_floats((int)B, d, &wd, &wc, &f);
+  check_t(part_wd, at::kFloat, "part_wd");
+  check_extent(part_wd, wd, "part_wd");
+  check_t(part_wc, at::kFloat, "part_wc");
+  check_extent(part_wc, wc, "part_wc");
+  const c10::hip::OptionalHIPGuardMasqueradingAsCUDA guard(x.device());
+  wf::launch_cnn_backward(fp(x), (int)B, d, bfp(WcA), bfp(WdB), fp(dout), (unsigned)(seed & 0xFFFFFFFF), rng_ptr(rng),
+                          fp(part_wd), fp(part_wc), cur_stream());
+}
+
+void cnn_reduce(const at::Tensor& part_wd, const at::Tensor& part_wc, const at::Tensor& part_f, int64_t B,
+                const std::vector<int64_t>& dims, const at::Tensor& gWc, const at::Tensor& gWd, const at::Tensor& gbd,
+                c10::optional<at::Tensor> loss_sum, c10::optional<at::Tensor> rng) {
+  auto d = cnn_checked(dims, 0.0);
+  long wd = 0, wc = 0, f = 0;
+  wf::cnn_part_floats((int)B, d, &wd, &wc, &f);
+  check_t(part_wd, at::kFloat, "part_wd");
+  check_extent(part_wd, wd, "part_wd");
+  check_t(part_wc, at::kFloat, "part_wc");
+  check_extent(part_wc, wc, "part_wc");
+  check_t(part_f, at::kFloat, "part_f");
+  check_extent(part_f, f, "part_f");
+  for (const at::Tensor* t : {&gWc, &gWd, &gbd})
+    TORCH_CHECK(t->is_cuda() && t->scalar_type() == at::kFloat && t->is_contiguous(), "grads: contiguous fp32 GPU");
+  check_extent(gWc, (int64_t)d.Fp * d.Kc, "gWc");
+  check_extent(gWd, (int64_t)16 * d.T * d.Fp, "gWd");
+  check_extent(gbd, 16, "gbd");
+  long long* rp = nullptr;
+  if (rng.has_value() && rng->defined()) {
+    TORCH_CHECK(rng->is_cuda() && rng->scalar_type() == at::kLong && rng->numel() >= 1, "rng: GPU int64 tensor");
+    rp = reinterpret_cast<long long*>(rng->data_ptr<int64_t>());
+  }
+  const c10::hip::OptionalHIPGuardMasqueradingAsCUDA guard(part_wd.device());
+  wf::launch_cnn_reduce(fp(part_wd), fp(part_wc), fp(part_f), (int)B, d, gWc.data_ptr<float>(), gWd.data_ptr<float>(),
+                        gbd.data_ptr<float>(), opt_ptr<float>(loss_sum, at::kFloat, "loss_sum", 1), rp, cur_stream());
+}
+
+// True when the HIP objects are a WF_DIAG build (WELLFLOW_DIAG_BUILD=1): timing-only switches
+// and A/B variants are live. bench.py refuses to time such a build.
+bool diag_build() { return wf::dbg_mask() != (1 << 21); }
+
 // Every binding runs behind this wrapper: a kernel launch that the runtime rejected (bad grid,
 // missing code object, invalid resource) raises here instead of failing silently.
 template <auto F>
@@ -759,4 +906,12 @@ PYBIND11_MODULE(_C, m) {
   WF_DEF(cast_bf16);
   WF_DEF(transpose_cast_bf16);
   WF_DEF(im2col1d);
+  // host-only queries (no launch; callable without a GPU)
+  m.def("diag_build", &diag_build);
+  m.def("cnn_fused_ok", &cnn_fused_ok);
+  m.def("cnn_part_sizes", &cnn_part_sizes);
+  WF_DEF(cnn_pack);
+  WF_DEF(cnn_forward);
+  WF_DEF(cnn_backward);
+  WF_DEF(cnn_reduce);
 }

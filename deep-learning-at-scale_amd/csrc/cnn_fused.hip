@@ -1,0 +1,526 @@
+// wellflow — fused kernels of the reference's own model, the 1-D CNN of cnn.py:110-118
+// (SURVEY.md §2.4 K1-K9): Conv1D(1 -> 100 filters, width 13, valid) + ReLU -> Dropout(0.5) ->
+// Flatten -> Dense(3600 -> 12), clipped-MAE (or MSE) loss, Keras SGD-Nesterov.
+//
+// Why: the round-3 engine ran im2col to HBM + three generic 128x128 GEMM launches + a loss
+// kernel. The 36 x 100 activation of every window was written, re-read as the dense input and
+// as the ReLU/dropout mask, its gradient written and re-read (~3.2 GB of HBM per step at
+// B = 65,536), and the skinny GEMMs (N = 12 outputs, K = 13 taps) ran 128-wide tiles that were
+// 7/8 padding: 1.63 ms per step, ~1 % of the MFMA peak (round-3 VERDICT missing #1). Here the
+// activation never leaves the CU and every product is a 16x16x16 MFMA shaped to the layer:
+//
+//  * forward (cnn_fwd_kernel): one wave owns a group of 16 windows and walks the 36 output
+//    steps t. Per t: P^T[f x w] = Wc[f x kk] X_t^T[kk x w] (7 MFMAs over the 112 padded filters;
+//    the lane's B fragment x[w][t + kk] comes out of its window's samples held as bf16 pairs
+//    in registers, the conv bias rides in the K slot kk = 13 against a constant 1), ReLU and
+//    the dropout mask in registers, then out^T[j x w] += Wd_t^T[j x f] act^T[f x w] — the
+//    accumulator tile IS the next MFMA's B operand (rows f, no lane movement). The dense
+//    weights sit in LDS in a fragment-native image (one conflict-free ds_read_b64 per MFMA).
+//    The epilogue adds the dense bias, evaluates the loss and writes only dOut (64 B per
+//    window) and per-workgroup partials of the loss and of the dense-bias gradient.
+//  * backward (cnn_bwd_kernel): grid = (pairs of output steps) x (window chunks); the
+//    workgroup keeps its two steps' dense-weight fragments and the gradient tiles dWd_t and
+//    dWc in registers for its whole chunk. Per (16-window group, t) it recomputes P (7 MFMAs),
+//    dAct = dOut Wd_t (7), masks it with the SAME dropout bits and ReLU, and accumulates
+//    dWd_t += act^T dOut (7) and dWc += dP^T X_t (7) — the bias row kk = 13 of X is the
+//    constant 1, so that row of dWc is the conv-bias gradient. Partials go out once per
+//    workgroup; cnn_reduce_kernel sums them into the flat gradient and advances the dropout
+//    step counter.
+//
+// Dropout (p = 0.5, Keras inverted dropout) is a counter hash, never stored: the keep bit of
+// (window w, step t, filter f) is bit 4*(f >> 4) + (f & 3) of lowbias32(((w*T + t)*4 +
+// ((f >> 2) & 3)) ^ smix), smix mixing the engine seed and the device step counter (so every
+// hipGraph replay draws a new mask). The forward needs one hash per lane per step (its lane
+// holds filters 16b + 4q + r of one window), the backward four (four windows per lane).
+// wellflow/models/cnn.py cnn_dropout_mask mirrors it bit for bit for the fp32 tests. The
+// 1/(1-p) = 2 scale is applied to the dense output (forward) and to dOut (backward) instead
+// of to every activation.
+#include <cstdlib>
+
+#include "common.h"
+#include "kernels.h"
+
+namespace wf {
+
+namespace {
+constexpr int CNN_NW = 8;    // waves per workgroup (512 threads, 2 per SIMD)
+constexpr int CNN_TG = 2;    // output steps per backward workgroup
+constexpr int CNN_NFB = 7;   // 16-filter blocks (filters 97..112; the reference has 100)
+constexpr int CNN_T = 36;    // output steps (input 48, width 13)
+
+__device__ __forceinline__ f32x4 mfma16(bf16x4 a, bf16x4 b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a, b, c, 0, 0, 0);
+}
+typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ bf16x4 frag(unsigned lo, unsigned hi) {
+  return __builtin_bit_cast(bf16x4, (u32x2{lo, hi}));
+}
+__device__ __forceinline__ unsigned lowbias32(unsigned x) {
+  x ^= x >> 16;
+  x *= 0x7feb352du;
+  x ^= x >> 15;
+  x *= 0x846ca68bu;
+  x ^= x >> 16;
+  return x;
+}
+}  // namespace
+
+// step mix of the dropout hash: engine seed x device step counter (cnn.py cnn_dropout_mask)
+__device__ __forceinline__ unsigned cnn_seed_mix(unsigned seed, const long long* rng) {
+  const unsigned r = rng != nullptr ? (unsigned)rng[0] : 0u;
+  return lowbias32(seed ^ lowbias32(r + 0x9E3779B9u));
+}
+__device__ __forceinline__ unsigned cnn_mask_word(unsigned smix, int w, int t, int T, int q) {
+  return lowbias32((((unsigned)w * (unsigned)T + (unsigned)t) * 4u + (unsigned)q) ^ smix);
+}
+
+// The K-slot fix-up of an X fragment (lane quad q holds kk = 4q .. 4q+3): kk == taps is the
+// constant 1 of the folded conv bias, kk > taps are zero. Per-lane masks, one v_and_or each.
+struct KSlot {
+  unsigned keep0, keep1, one0, one1;
+  __device__ KSlot(int q, int taps) {
+    keep0 = keep1 = one0 = one1 = 0u;
+#pragma unroll
+    for (int jj = 0; jj < 4; ++jj) {
+      const int kk = 4 * q + jj;
+      const unsigned half = (jj & 1) ? 0xFFFF0000u : 0x0000FFFFu;
+      const unsigned onev = (jj & 1) ? 0x3F800000u : 0x00003F80u;  // bf16 1.0
+      unsigned& keep = jj < 2 ? keep0 : keep1;
+      unsigned& one = jj < 2 ? one0 : one1;
+      if (kk < taps) keep |= half;
+      if (kk == taps) one |= onev;
+    }
+  }
+  __device__ __forceinline__ bf16x4 apply(unsigned d0, unsigned d1) const {
+    return frag((d0 & keep0) | one0, (d1 & keep1) | one1);
+  }
+};
+
+// ------------------------------------------------------------------------------- forward
+// TRAIN: dropout (drop != 0), loss + dOut + partials. !TRAIN: predictions only (eval).
+template <int NFB, int T, bool TRAIN>
+__global__ __launch_bounds__(512, 1) void cnn_fwd_kernel(
+    const float* __restrict__ x, int B, int L, const bf16_t* __restrict__ WcA, int Kc,
+    const bf16x4* __restrict__ WdF, const float* __restrict__ bd, int O, const float* __restrict__ y,
+    float* __restrict__ dout, float* __restrict__ pred, float* __restrict__ part, int taps, int loss_kind,
+    float clip, float scale, float keep_scale, int drop, unsigned seed, const long long* __restrict__ rng) {
+  constexpr int XR = (T + 6) / 4 * 4;  // x samples per lane: 4q .. 4q + T + 2, whole float4s
+  constexpr int NFRAG = T * NFB * 64;
+  // ONE static LDS object: the dense weights' fragment image, then the wave partials
+  __shared__ __attribute__((aligned(16))) char smem[NFRAG * 8 + CNN_NW * 20 * 4];
+  bf16x4* wd_lds = reinterpret_cast<bf16x4*>(smem);
+  float* wpart = reinterpret_cast<float*>(smem + NFRAG * 8);
+  {
+    const uint4* src = reinterpret_cast<const uint4*>(WdF);
+    uint4* dst = reinterpret_cast<uint4*>(smem);
+    for (int i = threadIdx.x; i < NFRAG / 2; i += 512) dst[i] = src[i];
+  }
+  const int lane = threadIdx.x & 63, l15 = lane & 15, q = lane >> 4;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  // conv weights as the A operand: A[f = 16b + l15][kk = 4q + jj] (bias at kk = taps)
+  bf16x4 wc[NFB];
+#pragma unroll
+  for (int b = 0; b < NFB; ++b) wc[b] = *reinterpret_cast<const bf16x4*>(WcA + (size_t)(16 * b + l15) * Kc + 4 * q);
+  const KSlot ks(q, taps);
+  float bdj[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) bdj[r] = bd[4 * q + r];
+  const unsigned smix = (TRAIN && drop) ? cnn_seed_mix(seed, rng) : 0u;
+  float lsum = 0.f, dbd[4] = {0.f, 0.f, 0.f, 0.f};
+  __syncthreads();
+
+  const int ngroups = (B + 15) >> 4;
+  for (int g = blockIdx.x * CNN_NW + wid; g < ngroups; g += gridDim.x * CNN_NW) {
+    const int w = g * 16 + l15;  // this lane's window (B-operand column)
+    const bool wok = w < B;
+    unsigned xp[XR / 2];  // bf16 pairs (x[w][4q + 2i], x[w][4q + 2i + 1])
+    const float* xr = x + (size_t)(wok ? w : 0) * L + 4 * q;
+#pragma unroll
+    for (int k = 0; k < XR / 4; ++k) {
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (wok && 4 * q + 4 * k + 4 <= L) v = *reinterpret_cast<const float4*>(xr + 4 * k);
+      xp[2 * k] = pk_bf16(v.x, v.y);
+      xp[2 * k + 1] = pk_bf16(v.z, v.w);
+    }
+    f32x4 out = {0.f, 0.f, 0.f, 0.f};
+    // dense-weight fragments of step t, prefetched one step ahead; the scheduling barrier at the
+    // end of every step keeps the unrolled loop from hoisting all 252 LDS reads (404 spilled
+    // VGPRs without it)
+    bf16x4 wfr[NFB];
+#pragma unroll
+    for (int b = 0; b < NFB; ++b) wfr[b] = wd_lds[b * 64 + lane];
+#pragma unroll
+    for (int t = 0; t < T; ++t) {
+      bf16x4 wnx[NFB];
+#pragma unroll
+      for (int b = 0; b < NFB; ++b) wnx[b] = wd_lds[(((t + 1) % T) * NFB + b) * 64 + lane];
+      // X_t^T fragment: B[kk = 4q + jj][w = l15] = x[w][t + 4q + jj]
+      unsigned d0, d1;
+      if (t & 1) {
+        d0 = __builtin_amdgcn_alignbit(xp[(t + 1) / 2], xp[(t - 1) / 2], 16);
+        d1 = __builtin_amdgcn_alignbit(xp[(t + 3) / 2], xp[(t + 1) / 2], 16);
+      } else {
+        d0 = xp[t / 2];
+        d1 = xp[t / 2 + 1];
+      }
+      const bf16x4 xb = ks.apply(d0, d1);
+      const unsigned m = (TRAIN && drop) ? cnn_mask_word(smix, w, t, T, q) : 0xFFFFFFFFu;
+#pragma unroll
+      for (int b = 0; b < NFB; ++b) {
+        const f32x4 p = mfma16(wc[b], xb, f32x4{0.f, 0.f, 0.f, 0.f});  // rows f = 16b + 4q + r
+        float a[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) a[r] = ((m >> (4 * b + r)) & 1u) ? fmaxf(p[r], 0.f) : 0.f;
+        out = mfma16(wfr[b], frag(pk_bf16(a[0], a[1]), pk_bf16(a[2], a[3])), out);
+      }
+#pragma unroll
+      for (int b = 0; b < NFB; ++b) wfr[b] = wnx[b];
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    // lane holds out[j = 4q + r][w = l15]
+    float d[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int j = 4 * q + r;
+      const float pv = out[r] * keep_scale + bdj[r];
+      d[r] = 0.f;
+      if (TRAIN) {
+        if (wok && j < O) {
+          const float yv = y[(size_t)w * O + j];
+          float l, dd;
+          if (loss_kind == 0) {
+            const float e = pv - yv;
+            l = e * e;
+            dd = 2.f * e;
+          } else {
+            const float e = yv - pv, ae = fabsf(e);
+            l = fminf(ae, clip);
+            const float sg = e > 0.f ? 1.f : (e < 0.f ? -1.f : 0.f);
+            dd = ae <= clip ? -sg : 0.f;
+          }
+          lsum += l;
+          d[r] = dd * scale;
+          dbd[r] += d[r];
+        }
+      } else {
+        d[r] = pv;
+      }
+    }
+    // every row of the group, rows past B too (as zeros): the buffers hold whole groups and
+    // the backward reads whole groups (a smaller batch must not see a larger one's rows)
+    float* dst = (TRAIN ? dout : pred) + (size_t)w * 16 + 4 * q;
+    *reinterpret_cast<float4*>(dst) = make_float4(d[0], d[1], d[2], d[3]);
+  }
+  if (!TRAIN) return;
+  // dbd[j] over the 16 lanes of quad q, the loss over the wave; then over the 8 waves
+#pragma unroll
+  for (int o = 1; o < 16; o <<= 1) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) dbd[r] += __shfl_xor(dbd[r], o, 64);
+    lsum += __shfl_xor(lsum, o, 64);
+  }
+  lsum += __shfl_xor(lsum, 16, 64);
+  lsum += __shfl_xor(lsum, 32, 64);
+  if (l15 == 0) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) wpart[wid * 20 + 4 * q + r] = dbd[r];
+    if (q == 0) wpart[wid * 20 + 16] = lsum;
+  }
+  __syncthreads();
+  if (threadIdx.x < 17) {
+    float s = 0.f;
+#pragma unroll
+    for (int k = 0; k < CNN_NW; ++k) s += wpart[k * 20 + threadIdx.x];
+    part[blockIdx.x * 32 + threadIdx.x] = s;
+  }
+}
+
+// ------------------------------------------------------------------------------ backward
+template <int NFB, int TG>
+__global__ __launch_bounds__(512, 1) void cnn_bwd_kernel(
+    const float* __restrict__ x, int B, int L, const bf16_t* __restrict__ WcA, int Kc,
+    const bf16x4* __restrict__ WdB, const float* __restrict__ dout, int T, int taps, float keep_scale, int drop,
+    unsigned seed, const long long* __restrict__ rng, int nch, float* __restrict__ part_wd,
+    float* __restrict__ part_wc) {
+  __shared__ __attribute__((aligned(16))) f32x4 red[CNN_NW * TG * NFB * 64];
+  const int lane = threadIdx.x & 63, l15 = lane & 15, q = lane >> 4;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int ntg = (T + TG - 1) / TG;
+  // logical block: consecutive ids (one XCD under the round-robin deal) share a window chunk
+  const int lb = xcd_remap(blockIdx.x, gridDim.x);
+  const int ch = lb / ntg, tg = lb % ntg, t0 = tg * TG;
+  const int ngroups = (B + 15) >> 4;
+  const int gpc = (ngroups + nch - 1) / nch;
+  const int g_begin = ch * gpc, g_end = min(ngroups, g_begin + gpc);
+
+  // conv weights as the B operand of P[w x f]: B[kk = 4q + jj][f = 16b + l15]
+  bf16x4 wc[NFB];
+#pragma unroll
+  for (int b = 0; b < NFB; ++b) wc[b] = *reinterpret_cast<const bf16x4*>(WcA + (size_t)(16 * b + l15) * Kc + 4 * q);
+  // dense weights of this workgroup's steps as the B operand of dAct[w x f]: B[j = 4q + jj][f]
+  bf16x4 wdb[TG][NFB];
+#pragma unroll
+  for (int tt = 0; tt < TG; ++tt)
+#pragma unroll
+    for (int b = 0; b < NFB; ++b)
+      wdb[tt][b] = (t0 + tt < T) ? WdB[((t0 + tt) * NFB + b) * 64 + lane] : bf16x4{0, 0, 0, 0};
+  const KSlot ks(q, taps);
+  // the dWc B operand's row kk = l15: x for kk < taps, the constant 1 at kk = taps, else 0
+  const bool kx = l15 < taps;
+  const float kone = l15 == taps ? 1.f : 0.f;
+  const unsigned smix = drop ? cnn_seed_mix(seed, rng) : 0u;
+  const int hq = l15 >> 2, hbit = l15 & 3;  // dropout hash key / bit of this lane's filter column
+
+  f32x4 acc_wd[TG][NFB], acc_wc[NFB];
+#pragma unroll
+  for (int b = 0; b < NFB; ++b) {
+    acc_wc[b] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int tt = 0; tt < TG; ++tt) acc_wd[tt][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+
+  for (int g = g_begin + wid; g < g_end; g += CNN_NW) {
+    const int w0 = g * 16;
+    // dOut (x keep_scale) as A[w = l15][j = 4q + jj] and as B[w = 4q + jj][j = l15]; rows past B
+    // are zero in the buffer (the forward writes every row of the last group it owns)
+    const float4 da = *reinterpret_cast<const float4*>(dout + (size_t)(w0 + l15) * 16 + 4 * q);
+    const bf16x4 doA = frag(pk_bf16(da.x * keep_scale, da.y * keep_scale), pk_bf16(da.z * keep_scale, da.w * keep_scale));
+    float dbv[4];
+#pragma unroll
+    for (int jj = 0; jj < 4; ++jj) dbv[jj] = dout[(size_t)(w0 + 4 * q + jj) * 16 + l15] * keep_scale;
+    const bf16x4 doB = frag(pk_bf16(dbv[0], dbv[1]), pk_bf16(dbv[2], dbv[3]));
+    // x of this lane's window for the A operand: x[w0 + l15][t0 + 4q + i], i < TG + 3
+    const int wa = w0 + l15;
+    float xa[TG + 3];
+#pragma unroll
+    for (int i = 0; i < TG + 3; ++i) {
+      const int s = t0 + 4 * q + i;
+      xa[i] = (wa < B && s < L) ? x[(size_t)wa * L + s] : 0.f;
+    }
+    // x of the four windows w0 + 4q + jj at sample t + l15 for the dWc B operand
+    float xb[TG][4];
+#pragma unroll
+    for (int tt = 0; tt < TG; ++tt)
+#pragma unroll
+      for (int jj = 0; jj < 4; ++jj) {
+        const int wb = w0 + 4 * q + jj, s = t0 + tt + l15;
+        xb[tt][jj] = (kx && wb < B && s < L) ? x[(size_t)wb * L + s] : kone;
+      }
+#pragma unroll
+    for (int tt = 0; tt < TG; ++tt) {
+      const int t = t0 + tt;
+      if (t >= T) break;
+      const bf16x4 xA = ks.apply(pk_bf16(xa[tt], xa[tt + 1]), pk_bf16(xa[tt + 2], xa[tt + 3]));
+      const bf16x4 xB = frag(pk_bf16(xb[tt][0], xb[tt][1]), pk_bf16(xb[tt][2], xb[tt][3]));
+      unsigned m[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) m[r] = drop ? cnn_mask_word(smix, w0 + 4 * q + r, t, T, hq) : 0xFFFFFFFFu;
+#pragma unroll
+      for (int b = 0; b < NFB; ++b) {
+        const f32x4 p = mfma16(xA, wc[b], f32x4{0.f, 0.f, 0.f, 0.f});       // [w = 4q + r][f = 16b + l15]
+        const f32x4 dA = mfma16(doA, wdb[tt][b], f32x4{0.f, 0.f, 0.f, 0.f});  // same layout
+        float a[4], dp[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const bool keep = ((m[r] >> (4 * b + hbit)) & 1u) && p[r] > 0.f;
+          a[r] = keep ? p[r] : 0.f;
+          dp[r] = keep ? dA[r] : 0.f;
+        }
+        // act^T and dP^T as A operands: A[f = l15][w = 4q + jj]
+        acc_wd[tt][b] = mfma16(frag(pk_bf16(a[0], a[1]), pk_bf16(a[2], a[3])), doB, acc_wd[tt][b]);
+        acc_wc[b] = mfma16(frag(pk_bf16(dp[0], dp[1]), pk_bf16(dp[2], dp[3])), xB, acc_wc[b]);
+      }
+    }
+  }
+  // workgroup sums through LDS, one partial per workgroup (fragment layout: lane = 16q + col)
+#pragma unroll
+  for (int tt = 0; tt < TG; ++tt)
+#pragma unroll
+    for (int b = 0; b < NFB; ++b) red[((wid * TG + tt) * NFB + b) * 64 + lane] = acc_wd[tt][b];
+  __syncthreads();
+  for (int e = threadIdx.x; e < TG * NFB * 64; e += 512) {
+    f32x4 s = red[e];
+#pragma unroll
+    for (int k = 1; k < CNN_NW; ++k) s += red[k * TG * NFB * 64 + e];
+    const int tt = e / (NFB * 64), rest = e % (NFB * 64);
+    if (t0 + tt < T)
+      reinterpret_cast<f32x4*>(part_wd)[((size_t)ch * T + t0 + tt) * NFB * 64 + rest] = s;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int b = 0; b < NFB; ++b) red[(wid * NFB + b) * 64 + lane] = acc_wc[b];
+  __syncthreads();
+  for (int e = threadIdx.x; e < NFB * 64; e += 512) {
+    f32x4 s = red[e];
+#pragma unroll
+    for (int k = 1; k < CNN_NW; ++k) s += red[k * NFB * 64 + e];
+    reinterpret_cast<f32x4*>(part_wc)[(size_t)blockIdx.x * NFB * 64 + e] = s;
+  }
+}
+
+// ------------------------------------------------------------------------------- reduce
+// Sums the partials into the flat gradient (+=): blocks [0, nwd) the dense weights (one
+// thread per element, nch partials each), [nwd, nwd + nwc) the conv weights + bias (16
+// outputs per block, 16 thread groups over the workgroup partials), the last block the dense
+// bias, the loss, and the dropout step counter.
+__global__ __launch_bounds__(256) void cnn_reduce_kernel(
+    const float* __restrict__ part_wd, const float* __restrict__ part_wc, const float* __restrict__ part_f,
+    int nch, int nwgb, int nwgf, int T, int Fp, int NFB, int O, int taps, int Kc, int nwd, int nwc,
+    float* __restrict__ gWc, float* __restrict__ gWd, float* __restrict__ gbd, float* __restrict__ loss_sum,
+    long long* __restrict__ rng) {
+  const int bid = blockIdx.x;
+  if (bid < nwd) {
+    const int i = bid * 256 + threadIdx.x;  // (j, t, f), f fastest
+    const int nf = T * Fp;
+    if (i >= O * nf) return;
+    const int j = i / nf, rest = i % nf, t = rest / Fp, f = rest % Fp;
+    const int b = f >> 4, lanep = ((f & 15) >> 2) * 16 + j, r = f & 3;
+    const size_t stride = (size_t)T * NFB * 64 * 4;
+    const float* p = part_wd + (((size_t)t * NFB + b) * 64 + lanep) * 4 + r;
+    float s = 0.f;
+    for (int c = 0; c < nch; ++c) s += p[c * stride];
+    gWd[(size_t)j * nf + rest] += s;
+    return;
+  }
+  if (bid < nwd + nwc) {
+    __shared__ float sh[16][17];
+    const int o = (bid - nwd) * 16 + (threadIdx.x & 15), grp = threadIdx.x >> 4;  // o = f * 16 + kk
+    const int f = o >> 4, kk = o & 15;
+    float s = 0.f;
+    if (f < Fp && kk <= taps) {
+      const int b = f >> 4, lanep = ((f & 15) >> 2) * 16 + kk, r = f & 3;
+      const float* p = part_wc + (((size_t)b * 64 + lanep) * 4 + r);
+      const size_t stride = (size_t)NFB * 64 * 4;
+      for (int c = grp; c < nwgb; c += 16) s += p[c * stride];
+    }
+    sh[grp][threadIdx.x & 15] = s;
+    __syncthreads();
+    if (grp == 0 && f < Fp && kk <= taps) {
+      float tsum = 0.f;
+#pragma unroll
+      for (int k = 0; k < 16; ++k) tsum += sh[k][threadIdx.x & 15];
+      gWc[(size_t)f * Kc + kk] += tsum;
+    }
+    return;
+  }
+  // dense bias, loss, step counter
+  if (threadIdx.x < 17) {
+    float s = 0.f;
+    for (int c = 0; c < nwgf; ++c) s += part_f[c * 32 + threadIdx.x];
+    if (threadIdx.x < 16) {
+      if (threadIdx.x < O) gbd[threadIdx.x] += s;
+    } else if (loss_sum != nullptr) {
+      loss_sum[0] += s;
+    }
+  }
+  if (threadIdx.x == 0 && rng != nullptr) rng[0] += 1;
+}
+
+// --------------------------------------------------------------------------------- pack
+// fp32 flat parameters -> the bf16 operand images: WcA [Fp][Kc] (a plain cast, the bias in
+// column taps), WdF (forward A fragments: lane (j = l15, q) holds Wd[j][t Fp + 16b + 4q + jj])
+// and WdB (backward B fragments: lane (f = l15, q) holds Wd[4q + jj][t Fp + 16b + f]), both
+// [T][NFB][64 lanes][4] — rows j >= O are zero.
+__global__ __launch_bounds__(256) void cnn_pack_kernel(const float* __restrict__ Wc, const float* __restrict__ Wd,
+                                                       int T, int Fp, int NFB, int Kc, int O, bf16_t* __restrict__ WcA,
+                                                       bf16_t* __restrict__ WdF, bf16_t* __restrict__ WdB) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  const int nfr = T * NFB * 64;
+  const long nf = (long)T * Fp;
+  if (i < nfr) {
+    const int lane = i & 63, tb = i >> 6, t = tb / NFB, b = tb % NFB;
+    const int l15 = lane & 15, q = lane >> 4;
+    unsigned short vf[4], vb[4];
+#pragma unroll
+    for (int jj = 0; jj < 4; ++jj) {
+      const int j = l15, f = 16 * b + 4 * q + jj;
+      vf[jj] = j < O ? f2bf(Wd[(long)j * nf + (long)t * Fp + f]) : 0;
+      const int j2 = 4 * q + jj, f2 = 16 * b + l15;
+      vb[jj] = j2 < O ? f2bf(Wd[(long)j2 * nf + (long)t * Fp + f2]) : 0;
+    }
+    *reinterpret_cast<uint2*>(WdF + (size_t)i * 4) = uint2{vf[0] | ((unsigned)vf[1] << 16), vf[2] | ((unsigned)vf[3] << 16)};
+    *reinterpret_cast<uint2*>(WdB + (size_t)i * 4) = uint2{vb[0] | ((unsigned)vb[1] << 16), vb[2] | ((unsigned)vb[3] << 16)};
+  } else if (i < nfr + Fp * Kc) {
+    const int k = i - nfr;
+    WcA[k] = f2bf(Wc[k]);
+  }
+}
+
+// -------------------------------------------------------------------------------- launch
+bool cnn_fused_supported(const CnnDims& d) {
+  return d.C == 1 && d.T == CNN_T && (d.Fp >> 4) == CNN_NFB && d.Fp % 16 == 0 && d.taps <= 15 && d.Kc == 16 &&
+         d.O >= 1 && d.O <= 16 && d.L % 4 == 0 && d.L == d.T + d.taps - 1 && (d.drop_p == 0.f || d.drop_p == 0.5f);
+}
+
+int cnn_fwd_grid(int B) {
+  static const int cus = [] {
+    int dev = 0, n = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        n <= 0)
+      n = 256;
+    return n;
+  }();
+  const int ngroups = (B + 15) / 16;
+  return std::max(1, std::min(cus, (ngroups + CNN_NW - 1) / CNN_NW));
+}
+
+int cnn_bwd_chunks(int B) {
+  const int ntg = (CNN_T + CNN_TG - 1) / CNN_TG;
+  const int ngroups = (B + 15) / 16;
+  const int cus = cnn_fwd_grid(1 << 30);  // the CU count
+  return std::max(1, std::min(std::max(1, cus / ntg), (ngroups + CNN_NW - 1) / CNN_NW));
+}
+
+void launch_cnn_pack(const float* Wc, const float* Wd, const CnnDims& d, bf16_t* WcA, bf16_t* WdF, bf16_t* WdB,
+                     hipStream_t s) {
+  const int n = d.T * (d.Fp / 16) * 64 + d.Fp * d.Kc;
+  hipLaunchKernelGGL(cnn_pack_kernel, dim3((n + 255) / 256), dim3(256), 0, s, Wc, Wd, d.T, d.Fp, d.Fp / 16, d.Kc,
+                     d.O, WcA, WdF, WdB);
+}
+
+void launch_cnn_forward(const float* x, int B, const CnnDims& d, const bf16_t* WcA, const bf16_t* WdF,
+                        const float* bd, const float* y, float* dout, float* pred, float* part, int train,
+                        int loss_kind, float clip, float scale, unsigned seed, const long long* rng, hipStream_t s) {
+  const int grid = cnn_fwd_grid(B);
+  const int drop = (train && d.drop_p > 0.f) ? 1 : 0;
+  const float keep_scale = drop ? 1.f / (1.f - d.drop_p) : 1.f;
+  if (train)
+    hipLaunchKernelGGL((cnn_fwd_kernel<CNN_NFB, CNN_T, true>), dim3(grid), dim3(512), 0, s, x, B, d.L, WcA, d.Kc,
+                       reinterpret_cast<const bf16x4*>(WdF), bd, d.O, y, dout, pred, part, d.taps, loss_kind, clip,
+                       scale, keep_scale, drop, seed, rng);
+  else
+    hipLaunchKernelGGL((cnn_fwd_kernel<CNN_NFB, CNN_T, false>), dim3(grid), dim3(512), 0, s, x, B, d.L, WcA, d.Kc,
+                       reinterpret_cast<const bf16x4*>(WdF), bd, d.O, y, dout, pred, part, d.taps, loss_kind, clip,
+                       scale, keep_scale, 0, seed, rng);
+}
+
+void launch_cnn_backward(const float* x, int B, const CnnDims& d, const bf16_t* WcA, const bf16_t* WdB,
+                         const float* dout, unsigned seed, const long long* rng, float* part_wd, float* part_wc,
+                         hipStream_t s) {
+  const int ntg = (d.T + CNN_TG - 1) / CNN_TG;
+  const int nch = cnn_bwd_chunks(B);
+  const int drop = d.drop_p > 0.f ? 1 : 0;
+  const float keep_scale = drop ? 1.f / (1.f - d.drop_p) : 1.f;
+  hipLaunchKernelGGL((cnn_bwd_kernel<CNN_NFB, CNN_TG>), dim3(ntg * nch), dim3(512), 0, s, x, B, d.L, WcA, d.Kc,
+                     reinterpret_cast<const bf16x4*>(WdB), dout, d.T, d.taps, keep_scale, drop, seed, rng, nch,
+                     part_wd, part_wc);
+}
+
+void launch_cnn_reduce(const float* part_wd, const float* part_wc, const float* part_f, int B, const CnnDims& d,
+                       float* gWc, float* gWd, float* gbd, float* loss_sum, long long* rng, hipStream_t s) {
+  const int nch = cnn_bwd_chunks(B), ntg = (d.T + CNN_TG - 1) / CNN_TG;
+  const int nwd = (d.O * d.T * d.Fp + 255) / 256, nwc = d.Fp;  // 16 (f, kk) outputs per block: Fp * 16 / 16
+  hipLaunchKernelGGL(cnn_reduce_kernel, dim3(nwd + nwc + 1), dim3(256), 0, s, part_wd, part_wc, part_f, nch,
+                     ntg * nch, cnn_fwd_grid(B), d.T, d.Fp, d.Fp / 16, d.O, d.taps, d.Kc, nwd, nwc, gWc, gWd, gbd,
+                     loss_sum, rng);
+}
+
+long cnn_part_floats(int B, const CnnDims& d, long* wd, long* wc, long* f) {
+  const int nch = cnn_bwd_chunks(B), ntg = (d.T + CNN_TG - 1) / CNN_TG;
+  *wd = (long)nch * d.T * (d.Fp / 16) * 64 * 4;
+  *wc = (long)ntg * nch * (d.Fp / 16) * 64 * 4;
+  *f = (long)cnn_fwd_grid(B) * 32;
+  return *wd + *wc + *f;
+}
+
+}  // namespace wf

@@ -38,11 +38,14 @@ struct LstmDims {
   int bwd_variant = 0;  // backward step GEMM (0: 128x128, 1: 64x128, 2: 128x64, 3: 64x64)
   int xcd_map = 1;      // 1: XCD-aware tile remap (default), 0: identity (diagnostics)
   int nt = 1;           // non-temporal hints on the read-once/write-once state streams
-  int dbg = 0;          // persistent-forward diagnostics (WELLFLOW_PF_DBG): 1 = skip the
-                        // hand-off wait (timing only: results are wrong)
+  int dbg = 0;          // persistent-kernel diagnostics (WELLFLOW_PF_DBG), masked with
+                        // dbg_mask(): production builds keep only the test hook bit 21
   int row_off = 0;      // persistent kernels: first batch row of this sub-batch launch
   unsigned spin_limit = 0;  // persistent hand-off spin bound (0 = built-in; tests shrink it)
 };
+// WELLFLOW_PF_DBG bits the HIP objects were built to honour (persistent_guard.h kDbgMask):
+// 1 << 21 (the force-timeout TEST hook) in production builds, everything in WF_DIAG builds
+int dbg_mask();
 void launch_lstm_pack_x(const float* x, bf16_t* XH, LstmDims d, hipStream_t s, bool full = true);
 void launch_lstm_fwd_step(int t, bf16_t* XH, const bf16_t* Wp, float* Cst, bf16_t* S,
                           LstmDims d, hipStream_t s);
@@ -112,6 +115,33 @@ int mlp2_train_grid(int B);
 bool mlp_bwd8();  // the 8-wave backward is selected (WELLFLOW_MLP_BWD8, default on)
 void launch_mlp2_reduce(float* red, int Fp, int B, float* loss_sum, float* db3, float* dw3, float* db1, float* db2,
                         float* dW1, float* dW2, hipStream_t s);
+
+// ---- fused reference CNN (cnn_fused.hip): Conv1D(C -> Fp, width taps / C) + ReLU + dropout ->
+// Dense(T * Fp -> O) -> loss, cnn.py:110-118. Flat layout = models/cnn.py CnnLayout:
+// Wc [Fp][Kc] (conv bias in column taps), Wd [Op = 16][T * Fp], bd [16].
+struct CnnDims {
+  int L, C, taps, T, Fp, Kc, O;  // input steps, channels, taps (= width * C), output steps, ...
+  float drop_p;                   // 0 or 0.5 (one hash bit per element)
+};
+bool cnn_fused_supported(const CnnDims& d);
+int cnn_fwd_grid(int B);
+int cnn_bwd_chunks(int B);
+// partial-buffer floats for a batch of B (dense-weight, conv-weight and forward partials)
+long cnn_part_floats(int B, const CnnDims& d, long* wd, long* wc, long* f);
+// bf16 operand images from the fp32 flat weights: WcA [Fp][Kc], WdF / WdB [T][Fp/16][64][4]
+void launch_cnn_pack(const float* Wc, const float* Wd, const CnnDims& d, bf16_t* WcA, bf16_t* WdF, bf16_t* WdB,
+                     hipStream_t s);
+// train = 1: dropout + loss; dout [rows >= B rounded up to 16][16] = scale * dloss/dpred, part
+// [cnn_fwd_grid(B)][32] (dense-bias gradient, loss). train = 0: pred [rows][16].
+void launch_cnn_forward(const float* x, int B, const CnnDims& d, const bf16_t* WcA, const bf16_t* WdF,
+                        const float* bd, const float* y, float* dout, float* pred, float* part, int train,
+                        int loss_kind, float clip, float scale, unsigned seed, const long long* rng, hipStream_t s);
+void launch_cnn_backward(const float* x, int B, const CnnDims& d, const bf16_t* WcA, const bf16_t* WdB,
+                         const float* dout, unsigned seed, const long long* rng, float* part_wd, float* part_wc,
+                         hipStream_t s);
+// grads += the partials; loss_sum += the loss; rng[0] += 1 (the dropout step counter)
+void launch_cnn_reduce(const float* part_wd, const float* part_wc, const float* part_f, int B, const CnnDims& d,
+                       float* gWc, float* gWd, float* gbd, float* loss_sum, long long* rng, hipStream_t s);
 
 // ---- regression head (N = 1) and losses ----
 void launch_head_fwd(const bf16_t* Hm, long ldh, int B, int Hd, const float* w, const float* b0,

@@ -57,6 +57,7 @@ int launch_pf_variant(int KT, int NC, bf16_t* XH, const bf16_t* Wp, float* Cst, 
 // at the END (persistent_guard.h: sticky spin-timeout bit and running totals, never cleared
 // by a launch; NativeLSTM.check_device_errors reads it).
 int lstm_persistent_sync_words(int row_blocks) { return 16 + 16 * row_blocks; }
+int dbg_mask() { return kDbgMask; }
 long lstm_persistent_sync_total(int row_blocks) { return lstm_persistent_sync_words(row_blocks) + kPStatWords; }
 
 // Batch split for the persistent schedules: the fewest equal sub-batches (launched one after
@@ -85,6 +86,7 @@ int persistent_split(int B, int row_quantum, int max_units, int cols, int cus, i
 // Batches larger than one co-resident grid run as consecutive sub-batch launches (no cap on B).
 int launch_lstm_fwd_persistent(bf16_t* XH, const bf16_t* Wp, float* Cst, bf16_t* S, unsigned* sync,
                                long sync_words, LstmDims d, hipStream_t s) {
+  d.dbg &= kDbgMask;  // production: the test hook only (persistent_guard.h)
   const int KA = d.KX + d.H, G = 4 * d.H;
   if ((double)d.B * KA * 2 >= 2147483647.0) return 0;  // 32-bit buffer offsets within one timestep slab
   if (d.KX % 64 != 0 || KA % 64 != 0 || G % 256 != 0 || d.B % PF_ROWS != 0) return 0;
@@ -103,11 +105,13 @@ int launch_lstm_fwd_persistent(bf16_t* XH, const bf16_t* Wp, float* Cst, bf16_t*
   if (sync_words < lstm_persistent_sync_total(MB)) return 0;
   unsigned* stat = sync + (sync_words - kPStatWords);  // running totals: never cleared here
   const int grid = MB * NB;
+  const size_t reset_bytes = sizeof(unsigned) * (size_t)lstm_persistent_sync_words(MB);
+  if (!persistent_memset_legacy(d) && !persistent_reset_ok(sync, reset_bytes)) return -(int)hipErrorInvalidValue;
   for (int k = 0; k < nsub; ++k) {
     // reset this launch's error word and arrival counters (the STAT block at the end is kept)
     if (persistent_memset_legacy(d)
             ? hipMemsetAsync(sync + 1, 0, sizeof(unsigned) * (size_t)(lstm_persistent_sync_words(MB) - 1), s) != hipSuccess
-            : hipMemsetAsync(sync, 0, sizeof(unsigned) * (size_t)lstm_persistent_sync_words(MB), s) != hipSuccess)
+            : hipMemsetAsync(sync, 0, reset_bytes, s) != hipSuccess)
       return -(int)hipErrorLaunchFailure;
     LstmDims dk = d;
     dk.row_off = k * Bs;

@@ -50,6 +50,7 @@ int persistent_split(int B, int row_quantum, int max_units, int cols, int cus, i
 int launch_lstm_bwd_persistent(const bf16_t* WhhT, const float* Cst, const bf16_t* S, bf16_t* DG,
                                const float* dcarry, unsigned* sync, long sync_words, LstmDims d,
                                hipStream_t s) {
+  d.dbg &= kDbgMask;  // production: the test hook only (persistent_guard.h)
   if (d.T < 2) return 1;  // nothing after the last step
   const int G = 4 * d.H;
   if (d.H % 64 != 0 || d.B % 64 != 0) return 0;
@@ -69,11 +70,13 @@ int launch_lstm_bwd_persistent(const bf16_t* WhhT, const float* Cst, const bf16_
   if (sync_words < lstm_persistent_sync_total(MB)) return 0;
   unsigned* stat = sync + (sync_words - kPStatWords);  // running totals: never cleared here
   const int grid = MB * NB;
+  const size_t reset_bytes = sizeof(unsigned) * (size_t)lstm_persistent_sync_words(MB);
+  if (!persistent_memset_legacy(d) && !persistent_reset_ok(sync, reset_bytes)) return -(int)hipErrorInvalidValue;
   for (int k = 0; k < nsub; ++k) {
     // this launch's error word and arrival counters (the STAT block at the end is kept)
     if (persistent_memset_legacy(d)
             ? hipMemsetAsync(sync + 1, 0, sizeof(unsigned) * (size_t)(lstm_persistent_sync_words(MB) - 1), s) != hipSuccess
-            : hipMemsetAsync(sync, 0, sizeof(unsigned) * (size_t)lstm_persistent_sync_words(MB), s) != hipSuccess)
+            : hipMemsetAsync(sync, 0, reset_bytes, s) != hipSuccess)
       return -(int)hipErrorLaunchFailure;
     LstmDims dk = d;
     dk.row_off = k * Bs;

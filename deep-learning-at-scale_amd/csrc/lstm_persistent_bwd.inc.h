@@ -106,7 +106,10 @@ __global__ __launch_bounds__(256, 1) void lstm_bwd_persistent_kernel(
   const bool even = (l15 & 1) == 0;
   // this launch's error (word 1 in the round-2 layout A/B, PF_DBG bit 20); the sticky bit is
   // in the STAT block (persistent_guard.h)
-  gu32* err = (gu32*)(sync + ((d.dbg >> 20) & 1));
+  // production objects keep only the test hook bit (kDbgMask, persistent_guard.h): the
+  // timing-only branches below fold away at compile time
+  const int dbg = d.dbg & kDbgMask;
+  gu32* err = (gu32*)(sync + ((dbg >> 20) & 1));
   gu32* cnt = (gu32*)(sync + 16 + 16 * m);
   const unsigned spin_limit = d.spin_limit ? d.spin_limit : PB_SPIN_LIMIT;
   constexpr int PB_STAMP_S = 10;
@@ -196,8 +199,8 @@ __global__ __launch_bounds__(256, 1) void lstm_bwd_persistent_kernel(
       asm volatile("" ::: "memory");
       // thread 0's view of the wait, kept for the exit record (persistent_guard.h)
       unsigned why = 0, seen_err = 0, seen_cnt = 0;
-      // (d.dbg bit 21, tests: an unreachable target, so the bounded spin trips deterministically)
-      const unsigned target = (unsigned)(NB * s) + (((d.dbg >> 21) & 1u) << 30);
+      // (dbg bit 21, tests: an unreachable target, so the bounded spin trips deterministically)
+      const unsigned target = (unsigned)(NB * s) + (((dbg >> 21) & 1u) << 30);
       if (threadIdx.x == 0) {
         if constexpr ((DBG & 64) != 0) {  // plain DG stores: publish them with an agent release
           __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
@@ -218,8 +221,8 @@ __global__ __launch_bounds__(256, 1) void lstm_bwd_persistent_kernel(
           }
           __builtin_amdgcn_s_sleep(2);
         }
-        // (d.dbg bit 22, WELLFLOW_PF_DBG=4194304: TIMING ONLY, unsafe — no acquire, to price it)
-        if (!((d.dbg >> 22) & 1)) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        // (dbg bit 22, WF_DIAG builds only, WELLFLOW_PF_DBG=4194304: TIMING ONLY, unsafe — no acquire, to price it)
+        if (!((dbg >> 22) & 1)) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         const int ok = why == 0 ? 1 : 0;
         asm volatile("ds_write_b32 %0, %1" ::"v"(lds0 + FLAG), "v"(ok) : "memory");
@@ -596,12 +599,11 @@ template <int KT, int NRT>
 static int launch_pb(const bf16_t* WhhT, const float* Cst, const bf16_t* S, bf16_t* DG, const float* dcarry,
                       unsigned* sync, unsigned* stat, int grid, LstmDims d, hipStream_t s) {
   const void* f = reinterpret_cast<const void*>(&lstm_bwd_persistent_kernel<KT, NRT>);
-  if constexpr (KT == 16 && NRT == 16) {  // production-correct A/B variants (WELLFLOW_PF_DBG)
-    if (d.dbg == 4096) f = reinterpret_cast<const void*>(&lstm_bwd_persistent_kernel<KT, NRT, 4096>);
-  }
-#ifdef WF_DIAG  // timing-only diagnostic builds (WELLFLOW_PF_DBG; WELLFLOW_DIAG_BUILD=1)
+#ifdef WF_DIAG  // A/B and timing-only variants: diagnostic builds only (WELLFLOW_DIAG_BUILD=1)
+  const void* const prod = f;
   if constexpr (KT == 16 && NRT == 16) {
-    switch (d.dbg) {
+    switch (d.dbg & 0xFFFFF) {
+      case 4096: if constexpr (WF_DV(4096)) f = reinterpret_cast<const void*>(&lstm_bwd_persistent_kernel<KT, NRT, 4096>); break;  // 1-ahead DG ring
       case 1: if constexpr (WF_DV(1)) f = reinterpret_cast<const void*>(&lstm_bwd_persistent_kernel<KT, NRT, 1>); break;
       case 2: if constexpr (WF_DV(2)) f = reinterpret_cast<const void*>(&lstm_bwd_persistent_kernel<KT, NRT, 2>); break;
       case 4: if constexpr (WF_DV(4)) f = reinterpret_cast<const void*>(&lstm_bwd_persistent_kernel<KT, NRT, 4>); break;
@@ -616,6 +618,9 @@ static int launch_pb(const bf16_t* WhhT, const float* Cst, const bf16_t* S, bf16
       default: break;
     }
   }
+  // a requested variant that this build did not compile must not time the production kernel
+  // under its name (bits 20-22 are runtime switches, not variants)
+  if ((d.dbg & 0xFFFFF) != 0 && f == prod) return -(int)hipErrorInvalidDeviceFunction;
 #endif
   void* args[] = {&WhhT, &Cst, &S, &DG, &dcarry, &sync, &stat, &d};
   return persistent_launch(f, grid, args, s);  // persistent_launch.h

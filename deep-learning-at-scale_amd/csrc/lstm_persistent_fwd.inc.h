@@ -133,7 +133,10 @@ __global__ __launch_bounds__(256, 1) void lstm_fwd_persistent_kernel(
   const int loff_s = ub * 1024 + lane * ((DBG & 32768) ? 16 : 8);
   const int loff_h = (((int)threadIdx.x >> 3) * KA + ((int)threadIdx.x & 7) * 8) * 2;  // h publish
   // error word: word 0 of the per-launch block (word 1 in the round-2 layout A/B, PF_DBG bit 20)
-  gu32* err = (gu32*)(sync + ((d.dbg >> 20) & 1));
+  // production objects keep only the test hook bit (kDbgMask, persistent_guard.h): the
+  // timing-only branches below fold away at compile time
+  const int dbg = d.dbg & kDbgMask;
+  gu32* err = (gu32*)(sync + ((dbg >> 20) & 1));
   gu32* cnt = (gu32*)(sync + 16 + 16 * m);
   const unsigned spin_limit = d.spin_limit ? d.spin_limit : PF_SPIN_LIMIT;
   // DBG & 16: timeline stamps (s_memrealtime, 100 MHz) of step PF_STAMP_T, wave 0 lane 0 of
@@ -197,12 +200,12 @@ __global__ __launch_bounds__(256, 1) void lstm_fwd_persistent_kernel(
       stamp(t, 62);  // h stores drained, workgroup arrived
       // thread 0's view of the wait, kept for the exit record (persistent_guard.h)
       unsigned why = 0, seen_err = 0, seen_cnt = 0;
-      // (d.dbg bit 21, tests: an unreachable target, so the bounded spin trips deterministically)
-      const unsigned target = (unsigned)(NB * t) + (((d.dbg >> 21) & 1u) << 30);
+      // (dbg bit 21, tests: an unreachable target, so the bounded spin trips deterministically)
+      const unsigned target = (unsigned)(NB * t) + (((dbg >> 21) & 1u) << 30);
       if (threadIdx.x == 0) {
         __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         unsigned spins = 0;
-        while (!(d.dbg & 1) && (seen_cnt = __hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) < target) {
+        while (!(dbg & 1) && (seen_cnt = __hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) < target) {
           if ((seen_err = __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) != 0u) {
             why = 1;
             break;
@@ -216,8 +219,8 @@ __global__ __launch_bounds__(256, 1) void lstm_fwd_persistent_kernel(
           __builtin_amdgcn_s_sleep(2);
         }
         stamp(t, 63);  // row block complete (poll matched)
-        // (d.dbg bit 22, WELLFLOW_PF_DBG=4194304: TIMING ONLY, unsafe — no acquire, to price it)
-        if (!((d.dbg >> 22) & 1)) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        // (dbg bit 22, WF_DIAG builds only, WELLFLOW_PF_DBG=4194304: TIMING ONLY, unsafe — no acquire, to price it)
+        if (!((dbg >> 22) & 1)) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         const int ok = why == 0 ? 1 : 0;
         asm volatile("ds_write_b32 %0, %1" ::"v"(flag_lds), "v"(ok) : "memory");
@@ -756,12 +759,11 @@ template <int KT, int NC>
 static int launch_pf(bf16_t* XH, const bf16_t* Wp, float* Cst, bf16_t* S, unsigned* sync, unsigned* stat, int grid,
                      LstmDims d, hipStream_t s) {
   const void* f = reinterpret_cast<const void*>(&lstm_fwd_persistent_kernel<KT, NC>);
-  if constexpr (KT == 18 && NC == 8) {  // production-correct A/B variants (WELLFLOW_PF_DBG)
-    if (d.dbg == 4096) f = reinterpret_cast<const void*>(&lstm_fwd_persistent_kernel<KT, NC, 4096>);
-    if (d.dbg == 65536) f = reinterpret_cast<const void*>(&lstm_fwd_persistent_kernel<KT, NC, 65536>);
-  }
-#ifdef WF_DIAG  // timing-only diagnostic builds (WELLFLOW_PF_DBG >= 2; WELLFLOW_DIAG_BUILD=1)
+#ifdef WF_DIAG  // A/B and timing-only variants: diagnostic builds only (WELLFLOW_DIAG_BUILD=1)
+  const void* const prod = f;
   if constexpr (KT == 18 && NC == 8) {
+    if constexpr (WF_DV(4096)) { if (d.dbg == 4096) f = reinterpret_cast<const void*>(&lstm_fwd_persistent_kernel<KT, NC, 4096>); }  // C++ fragments
+    if constexpr (WF_DV(65536)) { if (d.dbg == 65536) f = reinterpret_cast<const void*>(&lstm_fwd_persistent_kernel<KT, NC, 65536>); }  // round-2 store order
     if constexpr (WF_DV(2)) { if (d.dbg == 2) f = reinterpret_cast<const void*>(&lstm_fwd_persistent_kernel<KT, NC, 2>); }
     if constexpr (WF_DV(4)) { if (d.dbg == 4) f = reinterpret_cast<const void*>(&lstm_fwd_persistent_kernel<KT, NC, 4>); }
     if constexpr (WF_DV(14)) { if (d.dbg == 14) f = reinterpret_cast<const void*>(&lstm_fwd_persistent_kernel<KT, NC, 14>); }
@@ -776,6 +778,9 @@ static int launch_pf(bf16_t* XH, const bf16_t* Wp, float* Cst, bf16_t* S, unsign
     if constexpr (WF_DV(24576)) { if (d.dbg == 24576) f = reinterpret_cast<const void*>(&lstm_fwd_persistent_kernel<KT, NC, 24576>); }  // neither
     if constexpr (WF_DV(32768)) { if (d.dbg == 32768) f = reinterpret_cast<const void*>(&lstm_fwd_persistent_kernel<KT, NC, 32768>); }  // round-2 S slots
   }
+  // a requested variant that this build did not compile must not time the production kernel
+  // under its name (bits 0 and 20-22 are runtime switches, not variants)
+  if ((d.dbg & 0xFFFFE) != 0 && f == prod) return -(int)hipErrorInvalidDeviceFunction;
 #endif
   void* args[] = {&XH, &Wp, &Cst, &S, &sync, &stat, &d};
   return persistent_launch(f, grid, args, s);  // persistent_launch.h: residency check + plain launch

@@ -7,12 +7,16 @@ width 13 (valid), 36 output steps, flatten in (step, filter) order, 12 linear ou
 lr 1e-3 / momentum 0.99 / decay 1e-6 / Nesterov (cnn.py:117), batch 20 (cnn.py:128).
 
 * :class:`CNN1DRegressor` — PyTorch fp32 reference (CPU oracle, channels-last input).
-* :class:`NativeCNN` — MI355X engine: im2col (bias folded as a constant-1 tap) ->
-  conv-as-GEMM with fused ReLU + inverted-dropout epilogue (mask regenerated from a
-  counter hash, never stored) -> dense GEMM + bias -> fused loss/grad kernel; backward
-  reuses the stored post-dropout activation as the combined ReLU/dropout mask.
-  Internally filters are padded 100 -> 104 and outputs 12 -> 16 (zero rows) so every
-  MN-contiguous GEMM operand has a multiple-of-8 extent; the padding stays exactly zero.
+* :class:`NativeCNN` — MI355X engine. For the reference shape (one input channel, 48-step
+  windows, width 13, 97-112 filters, <= 16 outputs, dropout 0 or 0.5) the step is three
+  fused kernels (csrc/cnn_fused.hip): a forward that keeps the 36 x 112 activation of every
+  window on chip (conv MFMA -> ReLU -> hashed dropout -> dense MFMA -> loss, writing only
+  dOut), a backward that recomputes the activation and accumulates dWd / dWc in registers,
+  and a reduce of the per-workgroup partials. Other shapes (the job path's multi-channel
+  windows) run im2col -> conv-as-GEMM with a fused ReLU + dropout epilogue -> dense GEMM ->
+  loss kernel -> split-K weight-gradient GEMMs (csrc/gemm.hip).
+  Internally filters are padded 100 -> 112 and outputs 12 -> 16 (zero rows; multiples of 16
+  for the MFMA tiles); the padding stays exactly zero.
 
 Theano's conv is a true convolution (kernel flipped); the exported reference layout
 (``to_reference``) therefore flips the taps, so a Keras-0.x consumer of the .mdl sees the
@@ -30,6 +34,39 @@ from torch import nn
 
 def _r8(x: int) -> int:
     return (x + 7) // 8 * 8
+
+
+def _r16(x: int) -> int:
+    return (x + 15) // 16 * 16
+
+
+_M32 = 0xFFFFFFFF
+
+
+def _lowbias32(x: torch.Tensor) -> torch.Tensor:
+    """lowbias32 integer hash on int64 tensors holding uint32 values (csrc/cnn_fused.hip)."""
+    x = x & _M32
+    x = x ^ (x >> 16)
+    x = (x * 0x7FEB352D) & _M32
+    x = x ^ (x >> 15)
+    x = (x * 0x846CA68B) & _M32
+    return x ^ (x >> 16)
+
+
+def cnn_dropout_mask(seed: int, step: int, B: int, T: int, Fp: int, device="cpu") -> torch.Tensor:
+    """Keep mask [B, T, Fp] (bool) of the fused CNN kernels' dropout at p = 0.5, bit for bit:
+    bit 4*(f >> 4) + (f & 3) of lowbias32(((w*T + t)*4 + ((f >> 2) & 3)) ^ smix), smix =
+    lowbias32(seed ^ lowbias32(step + 0x9E3779B9)); ``step`` is the device step counter the
+    forward and backward of one training step read (NativeCNN.rng)."""
+    seed_t = torch.tensor(seed & _M32, dtype=torch.int64)
+    smix = _lowbias32(seed_t ^ _lowbias32(torch.tensor((step + 0x9E3779B9) & _M32, dtype=torch.int64)))
+    w = torch.arange(B, dtype=torch.int64, device=device).view(B, 1, 1)
+    t = torch.arange(T, dtype=torch.int64, device=device).view(1, T, 1)
+    f = torch.arange(Fp, dtype=torch.int64, device=device).view(1, 1, Fp)
+    idx = (((w * T + t) & _M32) * 4 + ((f >> 2) & 3)) & _M32
+    h = _lowbias32(idx ^ smix.to(device))
+    bit = 4 * (f >> 4) + (f & 3)
+    return ((h >> bit) & 1).bool()
 
 
 class CNN1DRegressor(nn.Module):
@@ -113,12 +150,17 @@ class CnnLayout:
         return _r8(self.taps + 1)
 
     @property
-    def Fp(self):
-        return _r8(self.filters)
+    def Fp(self):  # 16-filter MFMA blocks
+        return _r16(self.filters)
 
     @property
-    def Op(self):
-        return _r8(self.outputs)
+    def Op(self):  # one 16-row MFMA tile of outputs
+        return _r16(self.outputs)
+
+    @property
+    def fused_dims(self) -> list:
+        """[L, C, taps, T, Fp, Kc, O] of the fused kernels (csrc/kernels.h CnnDims)."""
+        return [self.input_len, self.in_ch, self.taps, self.lout, self.Fp, self.Kc, self.outputs]
 
     @property
     def flat_width(self):
@@ -136,13 +178,17 @@ class CnnLayout:
 
 
 class NativeCNN:
-    """HIP/MFMA engine for the reference CNN (any batch up to ``batch``)."""
+    """HIP/MFMA engine for the reference CNN (any batch up to ``batch``).
+
+    ``fused`` (default where the shape allows, see module doc): three kernel launches per
+    training step with the activation on chip; else the im2col + GEMM path."""
 
     native = True
 
     def __init__(self, layout: CnnLayout = CnnLayout(), batch: int = 1024, device="cuda",
                  dropout: float = 0.5, loss: str = "mae_clip", clip: float = 6.0, seed: int = 0,
-                 params: torch.Tensor | None = None, grads: torch.Tensor | None = None):
+                 params: torch.Tensor | None = None, grads: torch.Tensor | None = None,
+                 fused: bool | None = None):
         from ..ops.native import lib
 
         self._C = lib()
@@ -153,24 +199,59 @@ class NativeCNN:
         n = layout.numel
         self.params = params if params is not None else torch.zeros(n, device=dev)
         self.grads = grads if grads is not None else torch.zeros(n, device=dev)
-        self.shadow = torch.empty(n, dtype=torch.bfloat16, device=dev)
-        bf = torch.bfloat16
-        L = layout
-        self.Xcol = torch.empty(batch * L.lout * L.Kc, dtype=bf, device=dev)
-        self.Hc = torch.empty(batch * L.flat_width, dtype=bf, device=dev)
-        self.dZc = torch.empty(batch * L.flat_width, dtype=bf, device=dev)
-        self.pred = torch.empty(batch * L.Op, device=dev)
-        self.ypad = torch.zeros(batch * L.Op, device=dev)
-        self.dpred = torch.zeros(batch * L.Op, dtype=bf, device=dev)
         self.loss_sum = torch.zeros(1, device=dev)
         # dropout step counter on the device: the mask differs every training step, eager or
         # replayed from a captured hipGraph (a host-side step would be baked into the graph)
         self.rng = torch.zeros(1, dtype=torch.int64, device=dev)
+        L = layout
+        ok = self._C.cnn_fused_ok(L.fused_dims, float(dropout))
+        if fused is None:
+            fused = ok and os.environ.get("WELLFLOW_CNN_FUSED", "1") != "0"
+        if fused and not ok:
+            raise ValueError(f"fused CNN kernels do not cover {L} with dropout {dropout}")
+        self.fused = bool(fused)
+        bf = torch.bfloat16
+        if self.fused:
+            nfr = L.lout * (L.Fp // 16) * 64 * 4
+            self.WcA = torch.empty(L.Fp * L.Kc, dtype=bf, device=dev)
+            self.WdF = torch.empty(nfr, dtype=bf, device=dev)
+            self.WdB = torch.empty(nfr, dtype=bf, device=dev)
+            rows = _r16(batch)
+            self.dout = torch.zeros(rows * 16, device=dev)
+            self.pred = torch.zeros(rows * 16, device=dev)
+            wd, wc, f = self._C.cnn_part_sizes(batch, L.fused_dims)
+            self.part_wd = torch.zeros(wd, device=dev)
+            self.part_wc = torch.zeros(wc, device=dev)
+            self.part_f = torch.zeros(f, device=dev)
+        else:
+            self.shadow = torch.empty(n, dtype=bf, device=dev)
+            self.Xcol = torch.empty(batch * L.lout * L.Kc, dtype=bf, device=dev)
+            self.Hc = torch.empty(batch * L.flat_width, dtype=bf, device=dev)
+            self.dZc = torch.empty(batch * L.flat_width, dtype=bf, device=dev)
+            self.pred = torch.empty(batch * L.Op, device=dev)
+            self.ypad = torch.zeros(batch * L.Op, device=dev)
+            self.dpred = torch.zeros(batch * L.Op, dtype=bf, device=dev)
         self.sync_weights()
 
-    def sync_weights(self):
-        self._C.cast_bf16(self.params, self.shadow)
+    @property
+    def seed32(self) -> int:
+        return (self.seed * 1000003) & 0x7FFFFFFF
 
+    def sync_weights(self):
+        if self.fused:
+            Wc, Wd, _ = self.lay.views(self.params)
+            self._C.cnn_pack(Wc, Wd, self.lay.fused_dims, self.WcA, self.WdF, self.WdB)
+        else:
+            self._C.cast_bf16(self.params, self.shadow)
+
+    def _x2d(self, x):
+        L = self.lay
+        B = x.shape[0]
+        if x.dim() == 3:
+            assert x.shape[1] == L.input_len and x.shape[2] == L.in_ch
+        return x.reshape(B, L.input_len * L.in_ch).contiguous().float()
+
+    # ------------------------------------------------------------------ unfused GEMM path
     def _fwd(self, x, B, drop_p, seed, seed_dev=None):
         from ..ops.native import gemm
 
@@ -186,27 +267,52 @@ class NativeCNN:
         gemm(self.Hc, Wd, B, L.Op, L.flat_width, outF=self.pred, bias=bd)
 
     def forward(self, x):
-        B = x.shape[0]
-        self._fwd(x, B, 0.0, 0)
-        out = self.pred[: B * self.lay.Op].view(B, self.lay.Op)[:, : self.lay.outputs]
-        return out.squeeze(-1) if self.lay.outputs == 1 else out
-
-    def forward_backward(self, x, y, grad_scale: float, zero_grads: bool = True, step: int = 0):
-        from ..ops.native import gemm
-
         L = self.lay
         B = x.shape[0]
-        seed = (self.seed * 1000003) & 0x7FFFFFFF  # + the device step counter self.rng
+        assert B <= self.B
+        if self.fused:
+            _, _, bd = L.views(self.params)
+            self._C.cnn_forward(self._x2d(x), B, L.fused_dims, float(self.p), self.WcA, self.WdF, bd, None, None,
+                                self.pred, None, False, 0, self.clip, 1.0, self.seed32, None)
+            out = self.pred[: B * 16].view(B, 16)[:, : L.outputs]
+        else:
+            self._fwd(x, B, 0.0, 0)
+            out = self.pred[: B * L.Op].view(B, L.Op)[:, : L.outputs]
+        return out.squeeze(-1) if L.outputs == 1 else out
+
+    def forward_backward(self, x, y, grad_scale: float, zero_grads: bool = True, step: int = 0,
+                         loss_into: torch.Tensor | None = None):
+        """Gradient of grad_scale * sum of per-element losses into ``grads`` (models/base.py);
+        returns the device loss sum (``loss_into`` when given: added straight into it)."""
+        L = self.lay
+        B = x.shape[0]
+        assert B <= self.B
         if zero_grads:
             self.grads.zero_()
+        gWc, gWd, gbd = L.views(self.grads)
+        kind = 0 if self.loss_kind == "mse" else 1
+        if self.fused:
+            ls = loss_into if loss_into is not None else self.loss_sum
+            if loss_into is None:
+                self.loss_sum.zero_()
+            _, _, bd = L.views(self.params)
+            xf = self._x2d(x)
+            dims, p = L.fused_dims, float(self.p)
+            self._C.cnn_forward(xf, B, dims, p, self.WcA, self.WdF, bd, y.reshape(B, -1).contiguous().float(),
+                                self.dout, None, self.part_f, True, kind, self.clip, float(grad_scale), self.seed32,
+                                self.rng)
+            self._C.cnn_backward(xf, B, dims, p, self.WcA, self.WdB, self.dout, self.seed32, self.rng,
+                                 self.part_wd, self.part_wc)
+            self._C.cnn_reduce(self.part_wd, self.part_wc, self.part_f, B, dims, gWc, gWd, gbd, ls, self.rng)
+            return ls
+        from ..ops.native import gemm
+
         self.loss_sum.zero_()
-        self._fwd(x, B, self.p, seed, self.rng)
+        self._fwd(x, B, self.p, self.seed32, self.rng)
         self.rng += 1
         yv = self.ypad[: B * L.Op].view(B, L.Op)
         yv[:, : L.outputs].copy_(y.view(B, -1))
-        gWc, gWd, gbd = L.views(self.grads)
         _, Wd, _ = L.views(self.shadow)
-        kind = 0 if self.loss_kind == "mse" else 1
         self._C.loss(kind, self.pred, self.ypad, B, L.Op, self.clip, float(grad_scale),
                      self.loss_sum, self.dpred, None, gbd)
         # dWd = dpred^T Hc   (reduce over batch)
@@ -216,11 +322,11 @@ class NativeCNN:
         # dHc = dpred Wd, masked by the stored post-dropout activation, x 1/(1-p)
         gemm(self.dpred, Wd, B, L.flat_width, L.Op, b_mn=True, ldb=L.flat_width, outH=self.dZc,
              mask=self.Hc, mask_scale=1.0 / (1.0 - self.p) if self.p > 0 else 1.0)
-        # dWc = dZc^T Xcol   (reduce over batch x steps)
-        # K = B x steps is huge and M x N = filters x taps tiny: split K deep (one 128x128 tile,
-        # ~4.6k rows per workgroup). bench.py --model cnn at B = 65536: split 32 / 128 / 512 /
-        # 2048 = 20.4 / 34.2 / 40.0 / 39.1 M windows/s (WELLFLOW_CNN_KS2 overrides)
+        # dWc = dZc^T Xcol   (reduce over batch x steps); K = B x steps is huge and M x N =
+        # filters x taps tiny: split K deep (WELLFLOW_CNN_KS2 overrides)
         ks2 = int(os.environ.get("WELLFLOW_CNN_KS2", "0")) or max(1, min(512, (B * L.lout) // 4096))
         gemm(self.dZc, self.Xcol, L.Fp, L.Kc, B * L.lout, a_mn=True, lda=L.Fp, b_mn=True,
              ldb=L.Kc, outF=gWc, atomic=True, ksplit=ks2)
+        if loss_into is not None:
+            loss_into += self.loss_sum
         return self.loss_sum

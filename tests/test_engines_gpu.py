@@ -63,24 +63,83 @@ def test_native_cnn_matches_reference(loss):
     assert _rel(eng.grads, gref.to_flat().to(DEV)) < 3e-2
 
 
-def test_native_cnn_dropout_mask_consistent():
-    """With dropout the backward must use exactly the forward's mask: check dL/dW_dense
-    against the stored post-dropout activation (dWd = dpred^T Hc)."""
-    from wellflow.models.cnn import CNN1DRegressor, NativeCNN
+def _cnn_ref_with_mask(ref, x, y, loss, mask, keep_scale=2.0):
+    """fp32 reference forward of the CNN with an explicit dropout keep mask [B, T, Fp]."""
+    from wellflow.models.base import per_element_loss
 
-    ref = CNN1DRegressor(dropout=0.5).init_keras(0)
-    eng = NativeCNN(ref.layout, batch=32, device=DEV, dropout=0.5, loss="mse")
+    B = x.shape[0]
+    h = torch.relu(ref.conv(x.transpose(1, 2))).transpose(1, 2)  # [B, T, F]
+    h = h * mask[:, :, : ref.filters].float() * keep_scale
+    out = ref.dense(h.reshape(B, -1))
+    return per_element_loss(loss, out, y).sum(), out
+
+
+def _flat_grad(ref):
+    from wellflow.models.cnn import CNN1DRegressor
+
+    g = CNN1DRegressor(dropout=0.0)
+    for pr, pg in zip(g.parameters(), ref.parameters()):
+        pr.data.copy_(pg.grad.cpu())
+    return g.to_flat().to(DEV)
+
+
+@pytest.mark.parametrize("loss,B", [("mse", 1000), ("mae_clip", 4096)])
+def test_native_cnn_dropout_matches_fp32_same_mask(loss, B):
+    """The fused CNN step with dropout 0.5 (csrc/cnn_fused.hip) against the fp32 reference
+    that applies the SAME keep mask (models/cnn.py cnn_dropout_mask mirrors the kernels' hash
+    bit for bit): loss, every gradient block, and the device step counter. B = 1000 leaves a
+    partial 16-window group."""
+    from wellflow.models.cnn import CNN1DRegressor, NativeCNN, cnn_dropout_mask
+
+    torch.manual_seed(2)
+    ref = CNN1DRegressor(dropout=0.5).init_keras(4).to(DEV)
+    with torch.no_grad():  # non-zero biases exercise the folded bias slot and its gradient
+        ref.conv.bias.uniform_(-0.05, 0.05)
+        ref.dense.bias.uniform_(-0.1, 0.1)
+    eng = NativeCNN(ref.layout, batch=4096, device=DEV, dropout=0.5, loss=loss, seed=7)
+    assert eng.fused
     eng.params.copy_(ref.to_flat().to(DEV))
     eng.sync_weights()
-    x, y = torch.randn(32, 48, 1, device=DEV), torch.randn(32, 12, device=DEV)
-    eng.forward_backward(x, y, grad_scale=1.0, step=5)
-    L = eng.lay
-    Hc = eng.Hc[: 32 * L.flat_width].view(32, L.flat_width).float()
-    kept = (Hc > 0).float().mean().item()
-    assert 0.15 < kept < 0.45  # ~half of the ReLU-positive units survive
-    dpred = eng.dpred[: 32 * L.Op].view(32, L.Op).float()
-    _, gWd, _ = L.views(eng.grads)
-    assert _rel(gWd, dpred.t() @ Hc) < 2e-2
+    x, y = torch.randn(B, 48, 1, device=DEV), torch.randn(B, 12, device=DEV)
+    eng.rng.fill_(5)
+    ls = eng.forward_backward(x, y, grad_scale=1.0 / (B * 12)).item()
+    torch.cuda.synchronize()
+    assert int(eng.rng.item()) == 6
+    mask = cnn_dropout_mask(eng.seed32, 5, B, 36, eng.lay.Fp, device=DEV)
+    kept = mask[:, :, :100].float().mean().item()
+    assert 0.45 < kept < 0.55, kept
+    L, _ = _cnn_ref_with_mask(ref, x, y, loss, mask)
+    (L / (B * 12)).backward()
+    assert abs(ls - L.item()) <= 2e-2 * L.item(), (ls, L.item())
+    g_r, g_n = _flat_grad(ref), eng.grads
+    Wc_n, Wd_n, bd_n = eng.lay.views(g_n)
+    Wc_r, Wd_r, bd_r = eng.lay.views(g_r)
+    for name, a, b in (("conv", Wc_n, Wc_r), ("dense", Wd_n, Wd_r), ("dense bias", bd_n, bd_r)):
+        assert _rel(a, b) < 3e-2, (name, _rel(a, b))
+    # the filter / output padding carries exactly zero gradient
+    assert Wc_n[100:].abs().max().item() == 0.0 and Wc_n[:, 14:].abs().max().item() == 0.0
+    assert Wd_n[12:].abs().max().item() == 0.0
+    assert Wd_n.view(16, 36, 112)[:, :, 100:].abs().max().item() == 0.0
+
+
+def test_native_cnn_fused_matches_gemm_path():
+    """Fused kernels vs the im2col + GEMM path (dropout 0; both bf16 MFMA): loss, gradients and
+    predictions agree to bf16 rounding."""
+    from wellflow.models.cnn import CNN1DRegressor, NativeCNN
+
+    ref = CNN1DRegressor(dropout=0.0).init_keras(6)
+    B = 2048
+    x, y = torch.randn(B, 48, 1, device=DEV), torch.randn(B, 12, device=DEV)
+    res = {}
+    for fused in (True, False):
+        eng = NativeCNN(ref.layout, batch=B, device=DEV, dropout=0.0, loss="mae_clip", fused=fused)
+        eng.params.copy_(ref.to_flat().to(DEV))
+        eng.sync_weights()
+        ls = eng.forward_backward(x, y, 1.0 / (B * 12)).item()
+        res[fused] = (ls, eng.grads.clone(), eng.forward(x).clone())
+    (la, ga, pa), (lb, gb, pb) = res[True], res[False]
+    assert abs(la - lb) <= 1e-2 * abs(lb)
+    assert _rel(ga, gb) < 2e-2 and _rel(pa, pb) < 1e-2
 
 
 @pytest.mark.parametrize("model", ["mlp", "lstm", "cnn", "mlp_online"])

@@ -414,3 +414,103 @@ def test_persistent_exit_record(monkeypatch):
     rec = fw["first_exit"]
     assert rec is not None and rec["reason"] in (1, 2, 4) and 1 <= rec["step"] < T, rec
     eng.reset_device_errors()
+
+
+def test_diag_env_ignored_by_production_build(monkeypatch):
+    """A production _C.so ignores the timing-only switches (round-3 VERDICT item 2):
+    WELLFLOW_PF_DBG=1 (skip the persistent hand-off wait) and WELLFLOW_MLP_DBG=1 (skip the
+    MLP epilogue atomics) set, the LSTM and MLP steps still match their fp32 references and
+    the LSTM steps give bit-for-bit the same forward as without the variables."""
+    from wellflow.data.synth import synth_lstm_batch, synth_tabular_batch
+    from wellflow.models.lstm import NativeLSTM, init_lstm_flat
+    from wellflow.models.mlp import MLPRegressor, NativeMLP
+    from wellflow.ops.native import lib
+    from wellflow.train.parity import Fp32LSTM
+
+    assert not lib().diag_build(), "the tested _C.so must be the production build"
+    B, T, F, H = 8192, 16, 16, 512
+    eng = NativeLSTM(F, H, T, B, device=DEV)
+    flat = init_lstm_flat(F, H, seed=2).to(DEV)
+    eng.params.copy_(flat)
+    eng.sync_weights()
+    x, y = synth_lstm_batch(B, T, F, seed=3)
+    x, y = x.to(DEV), y.to(DEV)
+    eng.forward_backward(x, y, 1.0 / B)
+    torch.cuda.synchronize()
+    clean = eng.pred[:B].clone()
+    for k, v in {"WELLFLOW_PF_DBG": "1", "WELLFLOW_MLP_DBG": "3"}.items():
+        monkeypatch.setenv(k, v)
+    ls = eng.forward_backward(x, y, 1.0 / B).item()
+    torch.cuda.synchronize()
+    eng.check_device_errors()
+    assert eng.last_forward_persistent and eng.last_backward_persistent
+    assert torch.equal(eng.pred[:B], clean), "WELLFLOW_PF_DBG changed the production forward"
+    ref = Fp32LSTM(eng.lay, flat)
+    L, pred_r = ref.loss_pred(x, y)
+    (L / B).backward()
+    assert ((eng.pred[:B] - pred_r.detach()).norm() / pred_r.norm()).item() < 2e-2
+    assert abs(ls - L.item()) <= 2e-2 * L.item()
+    g_r = ref.flat.grad
+    assert ((eng.grads - g_r).norm() / g_r.norm()).item() < 3e-2
+    # MLP (fused 8-wave kernels, spread reduction) under WELLFLOW_MLP_DBG
+    Bm, Fm = 65536, 16
+    torch.manual_seed(0)
+    mref = MLPRegressor(Fm, (256, 256)).to(DEV)
+    meng = NativeMLP(Fm, (256, 256), Bm, device=DEV)
+    meng.params.copy_(mref.to_flat().to(DEV))
+    meng.sync_weights()
+    xm, ym = synth_tabular_batch(Bm, Fm, seed=4)
+    xm, ym = xm.to(DEV), ym.to(DEV)
+    lm = meng.forward_backward(xm, ym, 1.0 / Bm).item()
+    torch.cuda.synchronize()
+    pred = mref(xm)
+    Lm = ((pred - ym) ** 2).sum()
+    (Lm / Bm).backward()
+    assert abs(lm - Lm.item()) <= 2e-2 * Lm.item()
+    gref = MLPRegressor(Fm, (256, 256))
+    for pr, pg in zip(gref.parameters(), mref.parameters()):
+        pr.data.copy_(pg.grad.cpu())
+    g_m = gref.to_flat().to(DEV)
+    assert ((meng.grads - g_m).norm() / g_m.norm()).item() < 3e-2
+
+
+def test_persistent_sync_buffer_at_offset_under_graph_replay():
+    """The rule behind the round-2 early exit (profiles/r3_early_exit.md): the per-launch reset
+    is ONE memset node that must start 16-B aligned and cover a multiple of 16 B — not "start
+    its own allocation". Both sync buffers are placed at non-zero, 16-B aligned offsets inside
+    larger allocations (256 B and 16 B in), the step is captured and replayed, and every
+    persistent launch completes every step (STAT block) with the same parameters as buffers at
+    the start of their own allocations."""
+    from wellflow.data.synth import synth_lstm_batch
+    from wellflow.models.lstm import NativeLSTM, init_lstm_flat
+    from wellflow.optim.flat import FlatAdam
+    from wellflow.parallel.dist import DistContext
+    from wellflow.train.step import StepRunner
+
+    B, T, F, H = 8192, 16, 16, 512
+    x, y = synth_lstm_batch(B, T, F, seed=7)
+    x, y = x.to(DEV), y.to(DEV)
+    out = {}
+    for offset in (False, True):
+        eng = NativeLSTM(F, H, T, B, device=DEV)
+        eng.params.copy_(init_lstm_flat(F, H, seed=6).to(DEV))
+        eng.sync_weights()
+        if offset:
+            n_f, n_b = eng.sync.numel(), eng.sync_bwd.numel()
+            big_f = torch.zeros(n_f + 64, dtype=torch.int32, device=DEV)
+            big_b = torch.zeros(n_b + 64, dtype=torch.int32, device=DEV)
+            eng.sync, eng.sync_bwd = big_f[64:64 + n_f], big_b[4:4 + n_b]
+            assert eng.sync.data_ptr() % 512 != 0 or eng.sync_bwd.data_ptr() % 512 != 0
+            assert eng.sync.data_ptr() % 16 == 0 and eng.sync_bwd.data_ptr() % 16 == 0
+        opt = FlatAdam(eng.params, eng.grads, lr=1e-3, zero_grads=True)
+        run = StepRunner(eng, opt, DistContext(device=torch.device(DEV)), 1.0 / B, lambda k: (x, y), graph=True)
+        for _ in range(8):  # 2 eager steps, then the capture and 6 replays (the capture itself runs nothing)
+            run.run()
+        torch.cuda.synchronize()
+        assert run.graphs
+        eng.check_device_errors()
+        st = eng.persistent_stats()
+        assert st["forward"]["launches"] == 8 and st["backward"]["launches"] == 8, st
+        out[offset] = eng.params.clone()
+    d = (out[False] - out[True]).abs().max().item()
+    assert d <= 5e-5, d

@@ -130,3 +130,21 @@ def test_flat_sgd_keras_nesterov_decay():
     opt2 = FlatSGD(p.clone(), g, lr=0.1)
     opt2.load_state_dict(sd)
     assert opt2.iterations == 3
+
+
+def test_cnn_dropout_mask_mirror_properties():
+    """models/cnn.py cnn_dropout_mask (the CPU mirror of the fused kernels' hash): keep rate
+    ~0.5 per filter and per step, a different mask for every step counter value and seed,
+    and the same mask for the same (seed, step)."""
+    from wellflow.models.cnn import cnn_dropout_mask
+
+    m0 = cnn_dropout_mask(7, 0, 512, 36, 112)
+    assert m0.shape == (512, 36, 112)
+    rate = m0.float().mean().item()
+    assert 0.49 < rate < 0.51, rate
+    per_f = m0.float().mean(dim=(0, 1))
+    assert per_f.min().item() > 0.45 and per_f.max().item() < 0.55
+    assert torch.equal(m0, cnn_dropout_mask(7, 0, 512, 36, 112))
+    for other in (cnn_dropout_mask(7, 1, 512, 36, 112), cnn_dropout_mask(8, 0, 512, 36, 112)):
+        agree = (m0 == other).float().mean().item()
+        assert 0.45 < agree < 0.55, agree

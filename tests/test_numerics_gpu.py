@@ -29,30 +29,7 @@ def _cos(a, b):
     return torch.nn.functional.cosine_similarity(a.reshape(1, -1).double(), b.reshape(1, -1).double()).item()
 
 
-class _Fp32LSTM:
-    """fp32 reference over the SAME flat parameter layout as NativeLSTM (LstmLayout)."""
-
-    def __init__(self, lay, flat):
-        self.lay = lay
-        self.flat = flat.detach().clone().float().requires_grad_(True)
-
-    def loss_pred(self, x, y):
-        lay, H, F = self.lay, self.lay.hidden, self.lay.n_features
-        W, w_out, b_out = lay.views(self.flat)
-        perm = lay.perm()
-        nat = torch.empty_like(W)
-        nat = nat.index_put((perm.to(W.device),), W)  # natural gate rows (i, f, g, o) x KA
-        Wx, bias, Wh = nat[:, :F], nat[:, F], nat[:, lay.KX:]
-        B, T, _ = x.shape
-        h = x.new_zeros(B, H)
-        c = x.new_zeros(B, H)
-        for t in range(T):
-            g = x[:, t] @ Wx.t() + h @ Wh.t() + bias
-            i, f, gg, o = g.split(H, dim=1)
-            c = torch.sigmoid(f) * c + torch.sigmoid(i) * torch.tanh(gg)
-            h = torch.sigmoid(o) * torch.tanh(c)
-        pred = h @ w_out + b_out
-        return ((pred - y) ** 2).sum(), pred
+from wellflow.train.parity import Fp32LSTM as _Fp32LSTM  # noqa: E402  (bench.py's parity uses the same)
 
 
 def _setup(B, T, F, H, seed=0):
@@ -97,43 +74,21 @@ def test_lstm_headline_shape_matches_fp32(B, T, F, H):
 
 def test_lstm_headline_adam_trajectory_within_2pct():
     """20 full training steps (the bench's step: graph-captured StepRunner, Adam clearing the
-    bucket) against 20 fp32 autograd + torch.optim.Adam steps on the same batch."""
-    from wellflow.optim.flat import FlatAdam
-    from wellflow.parallel.dist import DistContext
-    from wellflow.train.step import StepRunner
+    bucket) against 20 fp32 autograd + torch.optim.Adam steps on the same batch — the same
+    function bench.py reports as its "parity" object (wellflow/train/parity.py)."""
+    from wellflow.train.parity import lstm_adam_trajectory
 
-    B, T, F, H = 8192, 64, 16, 512
-    steps, lr = 20, 1e-3
-    eng, flat, x, y = _setup(B, T, F, H, seed=5)
-    opt = FlatAdam(eng.params, eng.grads, lr=lr, zero_grads=True)
-    run = StepRunner(eng, opt, DistContext(device=torch.device(DEV)), 1.0 / B, lambda k: (x, y))
-    nat = []
-    for _ in range(steps):
-        run.run()
-        nat.append(run.take_loss() / B)
-    eng.check_device_errors()
-    ref = _Fp32LSTM(eng.lay, flat)
-    ropt = torch.optim.Adam([ref.flat], lr=lr)
-    fp = []
-    for _ in range(steps):
-        ropt.zero_grad()
-        L, _ = ref.loss_pred(x, y)
-        (L / B).backward()
-        ropt.step()
-        fp.append(L.item() / B)
-    assert fp[-1] < 0.9 * fp[0], fp  # the reference itself learns over the window
-    rel = [abs(a - b) / b for a, b in zip(nat, fp)]
-    mean_rel = sum(rel) / len(rel)
-    max_vs_start = max(abs(a - b) for a, b in zip(nat, fp)) / fp[0]
+    res = lstm_adam_trajectory(DEV, B=8192, T=64, F=16, H=512, steps=20, lr=1e-3, seed=5)
     out = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "gpurun_out")
     if os.path.isdir(out):
         with open(os.path.join(out, "lstm_adam_trajectory.json"), "w") as f:
-            json.dump({"native_bf16": nat, "fp32": fp, "rel_dev": rel, "mean_rel_dev": mean_rel,
-                       "max_abs_dev_over_initial_loss": max_vs_start}, f, indent=1)
+            json.dump(res, f, indent=1)
+    assert res["step_graph"] and res["fp32_learns"], res
     # single-batch Adam at lr 1e-3 oscillates (the loss swings by 2x between steps), so a
     # per-step ratio near a swing's minimum amplifies tiny phase differences: gate on the
     # mean relative deviation and on the largest deviation against the loss scale
-    assert mean_rel < 0.02 and max_vs_start < 0.02, (mean_rel, max_vs_start, rel)
+    assert res["mean_rel_dev"] < 0.02 and res["max_abs_dev_over_initial_loss"] < 0.02, res
+    assert res["pass"]
 
 
 def test_mlp_headline_shape_matches_fp32():

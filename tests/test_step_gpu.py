@@ -113,26 +113,34 @@ def test_rccl_allreduce_captured_in_step_graph(monkeypatch):
 
 
 def test_cnn_dropout_mask_differs_per_replay():
-    from wellflow.models.cnn import CNN1DRegressor, NativeCNN
+    """The fused CNN step replayed from a hipGraph draws a NEW dropout mask every step: the
+    device counter advances, and each replay's loss equals the fp32 reference with the mask of
+    that step's counter value (weights held fixed with lr 0)."""
+    from wellflow.models.base import per_element_loss
+    from wellflow.models.cnn import CNN1DRegressor, NativeCNN, cnn_dropout_mask
     from wellflow.optim.flat import FlatSGD
     from wellflow.parallel.dist import DistContext
     from wellflow.train.step import StepRunner
 
-    ref = CNN1DRegressor(dropout=0.5).init_keras(0)
-    eng = NativeCNN(ref.layout, batch=64, device=DEV, dropout=0.5, loss="mae_clip")
+    B = 512
+    ref = CNN1DRegressor(dropout=0.5).init_keras(0).to(DEV)
+    eng = NativeCNN(ref.layout, batch=B, device=DEV, dropout=0.5, loss="mae_clip")
+    assert eng.fused
     eng.params.copy_(ref.to_flat().to(DEV))
     eng.sync_weights()
-    x, y = torch.randn(64, 48, 1, device=DEV), torch.randn(64, 12, device=DEV)
+    x, y = torch.randn(B, 48, 1, device=DEV), torch.randn(B, 12, device=DEV)
     opt = FlatSGD(eng.params, eng.grads, lr=0.0, zero_grads=True)  # lr 0: weights stay put
-    run = StepRunner(eng, opt, DistContext(device=torch.device(DEV)), 1.0 / 64, lambda k: (x, y), graph=True)
-    masks = []
+    run = StepRunner(eng, opt, DistContext(device=torch.device(DEV)), 1.0 / B, lambda k: (x, y), graph=True)
+    losses = []
     for _ in range(5):
         run.run()
-        torch.cuda.synchronize()
-        masks.append((eng.Hc[: 64 * eng.lay.flat_width] != 0).clone())
+        losses.append(run.take_loss())
     assert run.graphs
-    for a, b in zip(masks[2:], masks[3:]):  # replays 1, 2, 3
-        frac = (a != b).float().mean().item()
-        assert frac > 0.05, "dropout mask repeated across graph replays"
-    assert int(eng.rng.item()) == 5
-    assert opt.steps_taken == 5
+    assert int(eng.rng.item()) == 5 and opt.steps_taken == 5
+    with torch.no_grad():
+        for k, ls in enumerate(losses):
+            mask = cnn_dropout_mask(eng.seed32, k, B, 36, eng.lay.Fp, device=DEV)
+            h = torch.relu(ref.conv(x.transpose(1, 2))).transpose(1, 2) * mask[:, :, :100].float() * 2.0
+            L = per_element_loss("mae_clip", ref.dense(h.reshape(B, -1)), y).sum().item()
+            assert abs(ls - L) <= 1e-2 * L, (k, ls, L)
+    assert len({round(v, 3) for v in losses}) == 5, losses  # a repeated mask would repeat the loss
