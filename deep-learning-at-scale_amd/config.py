@@ -25,10 +25,14 @@ import os
 MODEL_DEFAULTS = {
     "cnn": dict(loss="mae_clip", optimizer="sgd", lr=0.001, momentum=0.99, decay=1e-6,
                 nesterov=True, batch_size=20, epochs=1000, patience=10),
-    "mlp": dict(loss="mse", optimizer="adam", lr=1e-3, batch_size=256, epochs=200, patience=10),
-    "mlp_online": dict(loss="mse", optimizer="adam", lr=1e-3, batch_size=256, epochs=50, patience=5),
-    # batch_size 0 = auto: on the native GPU engine, the rows that fill one co-resident
-    # persistent grid (NativeLSTM.full_grid_batch: 8192 at H = 512 on 256 CUs); 256 otherwise
+    # batch_size 0 = auto (train/job.py auto_batch): on a GPU the rows that fill the device
+    # (mlp: NativeMLP.full_batch, 262,144 on 256 CUs; lstm: one co-resident persistent grid,
+    # NativeLSTM.full_grid_batch, 8192 at H = 512), capped at 1/8 of the rank's training rows,
+    # the same for --precision bf16 and fp32; 256 on the CPU. online_chunk 0 = auto: 8
+    # mini-batches per rank per stream chunk.
+    "mlp": dict(loss="mse", optimizer="adam", lr=1e-3, batch_size=0, epochs=200, patience=10),
+    "mlp_online": dict(loss="mse", optimizer="adam", lr=1e-3, batch_size=0, epochs=50, patience=5,
+                       online_chunk=0),
     "lstm": dict(loss="mse", optimizer="adam", lr=1e-3, batch_size=0, epochs=100, patience=10),
     "gilbert": dict(loss="mse", epochs=0, batch_size=0),
 }
@@ -75,7 +79,7 @@ class RunConfig:
     window_split: str = "time"
     synth_wells: int = 16
     synth_steps: int = 600
-    online_chunk: int = 4096     # dynamic model: rows per streamed chunk
+    online_chunk: int = 4096     # dynamic model: rows per streamed chunk (mlp_online default 0 = auto)
     max_steps: int = 0           # 0 = no cap (tests / smoke)
     resume: bool = False
     verbose: int = 2             # Keras verbose=2: one line per epoch (cnn.py:128)
@@ -120,7 +124,7 @@ def build_parser(model: str) -> argparse.ArgumentParser:
     ap.add_argument("--split", type=_tuple_floats)
     ap.add_argument("--epochs", type=int)
     ap.add_argument("--batch-size", type=int, dest="batch_size",
-                    help="per-GPU rows per step (lstm: 0 = auto, sized to fill the GPU)")
+                    help="per-GPU rows per step (lstm, mlp, mlp_online: 0 = auto, sized to fill the GPU)")
     ap.add_argument("--patience", type=int)
     ap.add_argument("--loss", choices=["mse", "mae_clip"])
     ap.add_argument("--clip", type=float)

@@ -149,7 +149,7 @@ void check_lstm_state(const at::Tensor& XH, const at::Tensor& Cst, const at::Ten
   const int64_t KA = d.KX + d.H, G = 4 * d.H;
   const int64_t Bp = (d.B + 15) / 16 * 16;  // fragment-native state is padded to 16 rows
   check_t(XH, at::kBFloat16, "XH");
-  check_t(Cst, at::kFloat, "Cst");
+  check_t(Cst, at::kBFloat16, "Cst");  // bf16 cell-state history (lstm_layout.h)
   check_t(S, at::kBFloat16, "S");
   check_extent(XH, (int64_t)(d.T + 1) * d.B * KA, "XH");
   check_extent(Cst, (int64_t)(d.T + 1) * Bp * d.H, "Cst");
@@ -169,17 +169,21 @@ void lstm_pack_x(const at::Tensor& x, const at::Tensor& XH, int64_t B, int64_t T
   wf::launch_lstm_pack_x(fp(x), bfp(XH), d, cur_stream(), full);
 }
 
+// cf32: fp32 [Bp][H] in-place state slab of the per-step path (c_{t-1} -> c_t; e.g. the
+// engine's dcarry buffer, which the backward re-initialises)
 void lstm_forward(const at::Tensor& XH, const at::Tensor& Wp, const at::Tensor& Cst,
-                  const at::Tensor& S, int64_t B, int64_t T, int64_t F, int64_t KX, int64_t H,
-                  int64_t variant) {
+                  const at::Tensor& S, const at::Tensor& cf32, int64_t B, int64_t T, int64_t F, int64_t KX,
+                  int64_t H, int64_t variant) {
   auto d = lstm_dims(B, T, F, KX, H);
   d.fwd_variant = (int)variant;
   check_lstm_state(XH, Cst, S, d);
   check_t(Wp, at::kBFloat16, "Wp");
   check_extent(Wp, 4 * H * (KX + H), "Wp");
+  check_t(cf32, at::kFloat, "cf32");
+  check_extent(cf32, (B + 15) / 16 * 16 * H, "cf32");
   const c10::hip::OptionalHIPGuardMasqueradingAsCUDA guard(XH.device());
   auto s = cur_stream();
-  for (int t = 0; t < d.T; ++t) wf::launch_lstm_fwd_step(t, bfp(XH), bfp(Wp), fp(Cst), bfp(S), d, s);
+  for (int t = 0; t < d.T; ++t) wf::launch_lstm_fwd_step(t, bfp(XH), bfp(Wp), bfp(Cst), bfp(S), fp(cf32), d, s);
 }
 
 // A persistent kernel's sync buffer: int32, 16-B aligned. The launcher zeroes its per-launch
@@ -211,7 +215,7 @@ bool lstm_forward_persistent(const at::Tensor& XH, const at::Tensor& Wp, const a
   check_extent(Wp, 4 * H * (KX + H), "Wp");
   check_sync(sync);
   const c10::hip::OptionalHIPGuardMasqueradingAsCUDA guard(XH.device());
-  return persistent_status(wf::launch_lstm_fwd_persistent(bfp(XH), bfp(Wp), fp(Cst), bfp(S),
+  return persistent_status(wf::launch_lstm_fwd_persistent(bfp(XH), bfp(Wp), bfp(Cst), bfp(S),
                                                           reinterpret_cast<unsigned*>(sync.data_ptr<int>()),
                                                           sync.numel(), d, cur_stream()),
                            "persistent LSTM forward");
@@ -238,9 +242,9 @@ void lstm_backward(const at::Tensor& WhhT, const at::Tensor& XH, const at::Tenso
   auto s = cur_stream();
   if (sync.has_value()) {  // step T-1, then the persistent chain (tools/pb_time.py)
     check_sync(*sync);
-    wf::launch_lstm_bwd_step(d.T - 1, bfp(WhhT), fp(Cst), bfp(S), bfp(DG), fp(dcarry), fp(dy),
+    wf::launch_lstm_bwd_step(d.T - 1, bfp(WhhT), bfp(Cst), bfp(S), bfp(DG), fp(dcarry), fp(dy),
                              fp(w_out), d, s);
-    TORCH_CHECK(persistent_status(wf::launch_lstm_bwd_persistent(bfp(WhhT), fp(Cst), bfp(S), bfp(DG), fp(dcarry),
+    TORCH_CHECK(persistent_status(wf::launch_lstm_bwd_persistent(bfp(WhhT), bfp(Cst), bfp(S), bfp(DG), fp(dcarry),
                                                                  reinterpret_cast<unsigned*>(sync->data_ptr<int>()),
                                                                  sync->numel(), d, s),
                                   "persistent LSTM backward"),
@@ -248,7 +252,7 @@ void lstm_backward(const at::Tensor& WhhT, const at::Tensor& XH, const at::Tenso
     return;
   }
   for (int t = d.T - 1; t >= 0; --t)
-    wf::launch_lstm_bwd_step(t, bfp(WhhT), fp(Cst), bfp(S), bfp(DG), fp(dcarry), fp(dy),
+    wf::launch_lstm_bwd_step(t, bfp(WhhT), bfp(Cst), bfp(S), bfp(DG), fp(dcarry), fp(dy),
                              fp(w_out), d, s);
 }
 
@@ -339,19 +343,19 @@ bool lstm_backward_dw(const at::Tensor& WhhT, const at::Tensor& XH, const at::Te
   if (chunk <= 0) {
     // step T-1 (dh from the head), then steps T-2 .. 0 in one persistent launch when a sync
     // buffer is given and the shape fits (lstm_persistent_bwd.hip), else per-step kernels
-    wf::launch_lstm_bwd_step(d.T - 1, bfp(WhhT), fp(Cst), bfp(S), bfp(DG), fp(dcarry), fp(dy),
+    wf::launch_lstm_bwd_step(d.T - 1, bfp(WhhT), bfp(Cst), bfp(S), bfp(DG), fp(dcarry), fp(dy),
                              fp(w_out), d, main);
     bool done = false;
     if (sync.has_value()) {
       check_sync(*sync);
-      done = persistent_status(wf::launch_lstm_bwd_persistent(bfp(WhhT), fp(Cst), bfp(S), bfp(DG), fp(dcarry),
+      done = persistent_status(wf::launch_lstm_bwd_persistent(bfp(WhhT), bfp(Cst), bfp(S), bfp(DG), fp(dcarry),
                                                               reinterpret_cast<unsigned*>(sync->data_ptr<int>()),
                                                               sync->numel(), d, main),
                                "persistent LSTM backward");
     }
     if (!done)
       for (int t = d.T - 2; t >= 0; --t)
-        wf::launch_lstm_bwd_step(t, bfp(WhhT), fp(Cst), bfp(S), bfp(DG), fp(dcarry), fp(dy),
+        wf::launch_lstm_bwd_step(t, bfp(WhhT), bfp(Cst), bfp(S), bfp(DG), fp(dcarry), fp(dy),
                                  fp(w_out), d, main);
     dw(0, d.T, main);
     return done;
@@ -363,7 +367,7 @@ bool lstm_backward_dw(const at::Tensor& WhhT, const at::Tensor& XH, const at::Te
   TORCH_CHECK(hipStreamWaitEvent(ss.lo, ss.ev[0], 0) == hipSuccess, "wait");
   int t_end = d.T, k = 0;
   for (int t = d.T - 1; t >= 0; --t) {
-    wf::launch_lstm_bwd_step(t, bfp(WhhT), fp(Cst), bfp(S), bfp(DG), fp(dcarry), fp(dy),
+    wf::launch_lstm_bwd_step(t, bfp(WhhT), bfp(Cst), bfp(S), bfp(DG), fp(dcarry), fp(dy),
                              fp(w_out), d, ss.hi);
     if (t % chunk == 0) {  // DG[t .. t_end) complete
       hipEvent_t e = ss.ev[3 + k++];

@@ -34,8 +34,8 @@ void launch_gemm(const bf16_t* A, long lda, int a_mn, const bf16_t* B, long ldb,
 // ---- LSTM (single layer, batch-first input, seq-to-one regression) ----
 struct LstmDims {
   int B, T, F, KX, H;  // G = 4H, KA = KX + H
-  int fwd_variant = 0;  // tile shape of the forward step GEMM (0: 128x128, 1: 64x128, 2: 256x128)
-  int bwd_variant = 0;  // backward step GEMM (0: 128x128, 1: 64x128, 2: 128x64, 3: 64x64)
+  int fwd_variant = 0;  // per-step forward tile: 6 = 256x256 glds ring, else 128x128 (lstm.hip)
+  int bwd_variant = 0;  // per-step backward tile: 8 = 128x128 8-wave glds ring, else 128x128
   int xcd_map = 1;      // 1: XCD-aware tile remap (default), 0: identity (diagnostics)
   int nt = 1;           // non-temporal hints on the read-once/write-once state streams
   int dbg = 0;          // persistent-kernel diagnostics (WELLFLOW_PF_DBG), masked with
@@ -47,7 +47,9 @@ struct LstmDims {
 // 1 << 21 (the force-timeout TEST hook) in production builds, everything in WF_DIAG builds
 int dbg_mask();
 void launch_lstm_pack_x(const float* x, bf16_t* XH, LstmDims d, hipStream_t s, bool full = true);
-void launch_lstm_fwd_step(int t, bf16_t* XH, const bf16_t* Wp, float* Cst, bf16_t* S,
+// Cst: the cell-state history c_t (bf16, FN layout, slab t + 1; slab 0 = c_{-1} = 0) the backward
+// reads; the per-step forward carries c in fp32 in the in-place state slab cf32 ([Bp][H], FN).
+void launch_lstm_fwd_step(int t, bf16_t* XH, const bf16_t* Wp, bf16_t* Cst, bf16_t* S, float* cf32,
                           LstmDims d, hipStream_t s);
 // All T forward steps in ONE persistent launch per sub-batch (lstm_persistent.hip). `sync`
 // must hold lstm_persistent_sync_total(row blocks) words (16 + 16 * (B / 32 + 1) + 64 always
@@ -57,15 +59,15 @@ void launch_lstm_fwd_step(int t, bf16_t* XH, const bf16_t* Wp, float* Cst, bf16_
 // < 0 = -(hipError_t) of a failed launch.
 int lstm_persistent_sync_words(int row_blocks);
 long lstm_persistent_sync_total(int row_blocks);
-int launch_lstm_fwd_persistent(bf16_t* XH, const bf16_t* Wp, float* Cst, bf16_t* S, unsigned* sync,
+int launch_lstm_fwd_persistent(bf16_t* XH, const bf16_t* Wp, bf16_t* Cst, bf16_t* S, unsigned* sync,
                                 long sync_words, LstmDims d, hipStream_t s);
 // Backward steps T-2 .. 0 in ONE persistent launch per sub-batch (lstm_persistent_bwd.hip),
 // after step T-1 ran (launch_lstm_bwd_step(T-1, ...)). Same `sync` contract and return
 // codes as the forward.
-int launch_lstm_bwd_persistent(const bf16_t* WhhT, const float* Cst, const bf16_t* S, bf16_t* DG,
+int launch_lstm_bwd_persistent(const bf16_t* WhhT, const bf16_t* Cst, const bf16_t* S, bf16_t* DG,
                                 const float* dcarry, unsigned* sync, long sync_words, LstmDims d,
                                 hipStream_t s);
-void launch_lstm_bwd_step(int t, const bf16_t* WhhT, const float* Cst, const bf16_t* S,
+void launch_lstm_bwd_step(int t, const bf16_t* WhhT, const bf16_t* Cst, const bf16_t* S,
                           bf16_t* DG, float* dcarry, const float* dy, const float* w_out,
                           LstmDims d, hipStream_t s);
 void launch_lstm_pack_weights(const float* W, bf16_t* Wp, bf16_t* WhhT, LstmDims d,

@@ -75,8 +75,9 @@ void launch_lstm_pack_x(const float* x, bf16_t* XH, LstmDims d, hipStream_t s, b
 template <int BM, int WM, int WN, int STAGES>
 __global__ __launch_bounds__(64 * WM * WN) void lstm_fwd_step_kernel(int t, bf16_t* __restrict__ XH,
                                                             const bf16_t* __restrict__ Wp,
-                                                            float* __restrict__ Cst,
-                                                            bf16_t* __restrict__ S, LstmDims d) {
+                                                            bf16_t* __restrict__ Cst,
+                                                            bf16_t* __restrict__ S, float* __restrict__ cf32,
+                                                            LstmDims d) {
   // wave N tile must be 64 = 4 gates x 16 units
   using C = GemmCfg<BM, 64 * WN, K_CONTIG, K_CONTIG, WM, WN>;
   constexpr int LDSB = STAGES * C::STAGE > C::LDS_BYTES ? STAGES * C::STAGE : C::LDS_BYTES;
@@ -91,7 +92,8 @@ __global__ __launch_bounds__(64 * WM * WN) void lstm_fwd_step_kernel(int t, bf16
   const int lane = threadIdx.x & 63;
   const int u = (cc.nb >> 6) * 16 + (lane & 15);
   const int Bp = fn_rows(d.B);
-  const float* cprev = Cst + (size_t)t * Bp * d.H;
+  // c_{t-1} in fp32 from the in-place state slab cf32 (FN layout; every element is read and
+  // rewritten by the same lane, c_{-1} = 0); the bf16 history Cst is for the backward only
 
   f32x4 acc[C::TM][C::TN];
   if constexpr (STAGES >= 2)
@@ -99,7 +101,7 @@ __global__ __launch_bounds__(64 * WM * WN) void lstm_fwd_step_kernel(int t, bf16
   else
     gemm_mainloop<C>(A, KA, d.B, Wp, KA, G, 0, KA, m0, n0, smem, acc);
 
-  float* cnext = Cst + (size_t)(t + 1) * Bp * d.H;
+  bf16_t* cnext = Cst + (size_t)(t + 1) * Bp * d.H;
   bf16_t* hnext = XH + (size_t)(t + 1) * d.B * KA + d.KX;
   bf16_t* St = S + (size_t)t * Bp * G;
 #pragma unroll
@@ -107,7 +109,8 @@ __global__ __launch_bounds__(64 * WM * WN) void lstm_fwd_step_kernel(int t, bf16
     const int mrow0 = cc.mb + i * 16;
     if (mrow0 >= d.B) continue;
     const size_t blk = fn_block(mrow0, u, d.H);
-    const float4 cp = *reinterpret_cast<const float4*>(cprev + blk * 256 + lane * 4);
+    float4* cst = reinterpret_cast<float4*>(cf32 + blk * 256 + lane * 4);
+    const float4 cp = t > 0 ? *cst : make_float4(0.f, 0.f, 0.f, 0.f);
     const float cpv[4] = {cp.x, cp.y, cp.z, cp.w};
     float cv[4];
     unsigned pk[8];
@@ -124,7 +127,8 @@ __global__ __launch_bounds__(64 * WM * WN) void lstm_fwd_step_kernel(int t, bf16
       const int m = mrow0 + 4 * (lane >> 4) + r;
       if (m < d.B) hnext[(size_t)m * KA + u] = f2bf(og * tanhf_(c));
     }
-    *reinterpret_cast<float4*>(cnext + blk * 256 + lane * 4) = make_float4(cv[0], cv[1], cv[2], cv[3]);
+    *cst = make_float4(cv[0], cv[1], cv[2], cv[3]);
+    *reinterpret_cast<uint2*>(cnext + blk * 256 + lane * 4) = make_uint2(pk_bf16(cv[0], cv[1]), pk_bf16(cv[2], cv[3]));
     bf16_t* sb = St + blk * 1024 + lane * 8;  // FN S halves (lstm_layout.h kFnSHalf)
     st16(sb, make_uint4(pk[0], pk[1], pk[2], pk[3]), d.nt);
     st16(sb + kFnSHalf, make_uint4(pk[4], pk[5], pk[6], pk[7]), d.nt);
@@ -132,42 +136,34 @@ __global__ __launch_bounds__(64 * WM * WN) void lstm_fwd_step_kernel(int t, bf16
 }
 
 template <int BM, int WM, int WN, int STAGES = 0>
-static void fwd_cfg(int t, bf16_t* XH, const bf16_t* Wp, float* Cst, bf16_t* S, LstmDims d,
+static void fwd_cfg(int t, bf16_t* XH, const bf16_t* Wp, bf16_t* Cst, bf16_t* S, float* cf32, LstmDims d,
                     hipStream_t s) {
   if (STAGES >= 2 && (d.B % BM != 0 || (4 * d.H) % (64 * WN) != 0)) {  // partial tiles
-    fwd_cfg<BM, WM, WN, 0>(t, XH, Wp, Cst, S, d, s);
+    fwd_cfg<BM, WM, WN, 0>(t, XH, Wp, Cst, S, cf32, d, s);
     return;
   }
   const int tiles = ((d.B + BM - 1) / BM) * (4 * d.H / (64 * WN));
   hipLaunchKernelGGL((lstm_fwd_step_kernel<BM, WM, WN, STAGES>), dim3(tiles), dim3(64 * WM * WN), 0,
-                     s, t, XH, Wp, Cst, S, d);
+                     s, t, XH, Wp, Cst, S, cf32, d);
 }
 
-void launch_lstm_fwd_step(int t, bf16_t* XH, const bf16_t* Wp, float* Cst, bf16_t* S,
+// Per-step forward (the fallback of shapes the persistent forward does not take). Two tile
+// shapes stay built: 6 = 256x256, 8 waves, 2-stage glds ring (tools/tune_lstm.py, the engine
+// default) and 0 = 128x128 register-staged (any batch); the round-1 tuning zoo is retired.
+void launch_lstm_fwd_step(int t, bf16_t* XH, const bf16_t* Wp, bf16_t* Cst, bf16_t* S, float* cf32,
                           LstmDims d, hipStream_t s) {
-  switch (d.fwd_variant) {
-    case 1: fwd_cfg<64, 2, 2>(t, XH, Wp, Cst, S, d, s); break;
-    case 2: fwd_cfg<256, 2, 2>(t, XH, Wp, Cst, S, d, s); break;
-    case 3: fwd_cfg<256, 4, 2>(t, XH, Wp, Cst, S, d, s); break;   // 256x128, 8 waves
-    case 4: fwd_cfg<128, 2, 4>(t, XH, Wp, Cst, S, d, s); break;   // 128x256, 8 waves
-    case 5: fwd_cfg<256, 2, 4>(t, XH, Wp, Cst, S, d, s); break;   // 256x256, 8 waves
-    case 6: fwd_cfg<256, 2, 4, 2>(t, XH, Wp, Cst, S, d, s); break;  // glds, 2 stages (128 KiB)
-    case 7: fwd_cfg<128, 2, 4, 3>(t, XH, Wp, Cst, S, d, s); break;  // glds, 3 stages (144 KiB)
-    case 8: fwd_cfg<128, 2, 2, 3>(t, XH, Wp, Cst, S, d, s); break;  // glds, 3 stages (96 KiB)
-    case 9: fwd_cfg<256, 4, 2, 3>(t, XH, Wp, Cst, S, d, s); break;  // glds, 3 stages (144 KiB)
-    case 10: fwd_cfg<128, 2, 2, 2>(t, XH, Wp, Cst, S, d, s); break; // glds, 2 stages (64 KiB)
-    case 11: fwd_cfg<128, 2, 2, 4>(t, XH, Wp, Cst, S, d, s); break; // glds, 4 stages (128 KiB)
-    default: fwd_cfg<128, 2, 2>(t, XH, Wp, Cst, S, d, s); break;
-  }
+  if (d.fwd_variant == 6)
+    fwd_cfg<256, 2, 4, 2>(t, XH, Wp, Cst, S, cf32, d, s);
+  else
+    fwd_cfg<128, 2, 2>(t, XH, Wp, Cst, S, cf32, d, s);
 }
 
 // Cell backward for the 4 rows (mrow0 + 4*(lane>>4) + r) x unit u of step t held by this
 // lane, given dh for them: reads the lane's fragment-native S / C / dc-carry slots with
 // 16-B vector accesses, updates the carry and writes the gate gradients into DG[t]
 // (row-major, dg_col order: it is the next GEMM's A operand and the dW GEMM's M side).
-template <bool LITE = false>  // LITE: timing-only (no c_t / dc-carry traffic; wrong results)
 __device__ __forceinline__ void cell_bwd4(int t, int mrow0, int u, int lane, const float (&dh)[4],
-                                          const float* __restrict__ Cst,
+                                          const bf16_t* __restrict__ Cst,
                                           const bf16_t* __restrict__ S, bf16_t* __restrict__ DG,
                                           float* __restrict__ dcarry, const LstmDims& d) {
   const int G = 4 * d.H, Bp = fn_rows(d.B);
@@ -178,11 +174,12 @@ __device__ __forceinline__ void cell_bwd4(int t, int mrow0, int u, int lane, con
   // only c_{t-1} is read: c_t = f * c_{t-1} + i * g is recomputed from the saved gates
   // (the same bf16 gates every other term of the cell backward uses), which drops one
   // 16.8 MB state read per step at B = 8192
-  const uint4 p4u = ld16(Cst + (size_t)t * Bp * d.H + blk * 256 + lane * 4, d.nt);
-  const float4 p4 = make_float4(__uint_as_float(p4u.x), __uint_as_float(p4u.y), __uint_as_float(p4u.z),
-                                __uint_as_float(p4u.w));
+  // (bf16 history: 4 values = 8 B per lane)
+  const uint2 p2 = *reinterpret_cast<const uint2*>(Cst + (size_t)t * Bp * d.H + blk * 256 + lane * 4);
+  const float4 p4 = make_float4(__uint_as_float(p2.x << 16), __uint_as_float(p2.x & 0xffff0000u),
+                                __uint_as_float(p2.y << 16), __uint_as_float(p2.y & 0xffff0000u));
   float4* dcp = reinterpret_cast<float4*>(dcarry + blk * 256 + lane * 4);
-  const float4 k4 = LITE ? p4 : *dcp;
+  const float4 k4 = *dcp;
   const float pv[4] = {p4.x, p4.y, p4.z, p4.w};
   const float kv[4] = {k4.x, k4.y, k4.z, k4.w};
   float nk[4];
@@ -202,13 +199,12 @@ __device__ __forceinline__ void cell_bwd4(int t, int mrow0, int u, int lane, con
       *reinterpret_cast<uint2*>(dgt + (size_t)m * G + dg_col(0, u)) = v;
     }
   }
-  if (!LITE) *dcp = make_float4(nk[0], nk[1], nk[2], nk[3]);
-  else if (nk[0] == 12345.f) *dcp = make_float4(nk[0], nk[1], nk[2], nk[3]);  // keep nk live
+  *dcp = make_float4(nk[0], nk[1], nk[2], nk[3]);
 }
 
 // t = T-1: dh comes from the regression head, dh[m][u] = dy[m] * w_out[u]; the carry
 // starts at 0. One thread per (fragment-native block, lane) = 4 rows of one unit.
-__global__ void lstm_bwd_last_kernel(const float* __restrict__ Cst, const bf16_t* __restrict__ S,
+__global__ void lstm_bwd_last_kernel(const bf16_t* __restrict__ Cst, const bf16_t* __restrict__ S,
                                      bf16_t* __restrict__ DG, float* __restrict__ dcarry,
                                      const float* __restrict__ dy, const float* __restrict__ w_out,
                                      LstmDims d) {
@@ -230,9 +226,9 @@ __global__ void lstm_bwd_last_kernel(const float* __restrict__ Cst, const bf16_t
   }
 }
 
-template <int BM, int BN, int WM, int WN, int STAGES, bool LITE = false>
+template <int BM, int BN, int WM, int WN, int STAGES>
 __global__ __launch_bounds__(64 * WM * WN) void lstm_bwd_step_kernel(int t, const bf16_t* __restrict__ WhhT,
-                                                            const float* __restrict__ Cst,
+                                                            const bf16_t* __restrict__ Cst,
                                                             const bf16_t* __restrict__ S,
                                                             bf16_t* __restrict__ DG,
                                                             float* __restrict__ dcarry, LstmDims d) {
@@ -261,24 +257,24 @@ __global__ __launch_bounds__(64 * WM * WN) void lstm_bwd_step_kernel(int t, cons
       const int mrow0 = cc.mb + i * 16;
       if (mrow0 >= d.B) continue;
       const float dh[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
-      cell_bwd4<LITE>(t, mrow0, u, lane, dh, Cst, S, DG, dcarry, d);
+      cell_bwd4(t, mrow0, u, lane, dh, Cst, S, DG, dcarry, d);
     }
   }
 }
 
-template <int BM, int BN, int WM = 2, int WN = 2, int STAGES = 0, bool LITE = false>
-static void bwd_cfg(int t, const bf16_t* WhhT, const float* Cst, const bf16_t* S, bf16_t* DG,
+template <int BM, int BN, int WM = 2, int WN = 2, int STAGES = 0>
+static void bwd_cfg(int t, const bf16_t* WhhT, const bf16_t* Cst, const bf16_t* S, bf16_t* DG,
                     float* dcarry, LstmDims d, hipStream_t s) {
   if (STAGES >= 2 && d.B % BM != 0) {
     bwd_cfg<BM, BN, WM, WN, 0>(t, WhhT, Cst, S, DG, dcarry, d, s);
     return;
   }
   const int tiles = ((d.B + BM - 1) / BM) * (d.H / BN);
-  hipLaunchKernelGGL((lstm_bwd_step_kernel<BM, BN, WM, WN, STAGES, LITE>), dim3(tiles), dim3(64 * WM * WN),
+  hipLaunchKernelGGL((lstm_bwd_step_kernel<BM, BN, WM, WN, STAGES>), dim3(tiles), dim3(64 * WM * WN),
                      0, s, t, WhhT, Cst, S, DG, dcarry, d);
 }
 
-void launch_lstm_bwd_step(int t, const bf16_t* WhhT, const float* Cst, const bf16_t* S,
+void launch_lstm_bwd_step(int t, const bf16_t* WhhT, const bf16_t* Cst, const bf16_t* S,
                           bf16_t* DG, float* dcarry, const float* dy, const float* w_out,
                           LstmDims d, hipStream_t s) {
   if (t == d.T - 1) {
@@ -289,30 +285,12 @@ void launch_lstm_bwd_step(int t, const bf16_t* WhhT, const float* Cst, const bf1
                        dy, w_out, d);
     return;
   }
-  switch (d.bwd_variant) {
-    case 1: bwd_cfg<64, 128>(t, WhhT, Cst, S, DG, dcarry, d, s); break;
-    case 2: bwd_cfg<128, 64>(t, WhhT, Cst, S, DG, dcarry, d, s); break;
-    case 3: bwd_cfg<64, 64>(t, WhhT, Cst, S, DG, dcarry, d, s); break;
-    case 4: bwd_cfg<128, 128, 2, 4>(t, WhhT, Cst, S, DG, dcarry, d, s); break;  // 8 waves
-    case 5: bwd_cfg<128, 128, 4, 2>(t, WhhT, Cst, S, DG, dcarry, d, s); break;  // 8 waves
-    case 6: bwd_cfg<128, 64, 2, 2>(t, WhhT, Cst, S, DG, dcarry, d, s); break;
-    case 7: bwd_cfg<64, 64, 2, 2, 3>(t, WhhT, Cst, S, DG, dcarry, d, s); break;    // glds
-    case 8: bwd_cfg<128, 128, 2, 4, 3>(t, WhhT, Cst, S, DG, dcarry, d, s); break;  // glds 8w
-    case 9: bwd_cfg<64, 128, 2, 2, 3>(t, WhhT, Cst, S, DG, dcarry, d, s); break;   // glds
-    case 10: bwd_cfg<128, 64, 2, 2, 3>(t, WhhT, Cst, S, DG, dcarry, d, s); break;  // glds
-    case 11: bwd_cfg<128, 128, 2, 2, 3>(t, WhhT, Cst, S, DG, dcarry, d, s); break; // glds 4w
-    case 12: bwd_cfg<64, 64, 2, 2, 4>(t, WhhT, Cst, S, DG, dcarry, d, s); break;   // glds 4st
-    case 13: bwd_cfg<128, 128, 2, 4, 4>(t, WhhT, Cst, S, DG, dcarry, d, s); break; // 8w 4st 128K
-    case 14: bwd_cfg<64, 128, 2, 2, 4>(t, WhhT, Cst, S, DG, dcarry, d, s); break;  // 4st 96K
-    case 15: bwd_cfg<128, 64, 2, 2, 4>(t, WhhT, Cst, S, DG, dcarry, d, s); break;  // 4st 96K
-    case 16: bwd_cfg<128, 128, 4, 4, 3>(t, WhhT, Cst, S, DG, dcarry, d, s); break; // 16 waves
-    case 17: bwd_cfg<128, 128, 4, 4, 4>(t, WhhT, Cst, S, DG, dcarry, d, s); break; // 16w 4st
-    case 19: bwd_cfg<128, 128, 2, 4, 4>(t, WhhT, Cst, S, DG, dcarry, d, s); break;  // 8w 4st (128 KiB)
-    case 20: bwd_cfg<128, 128, 2, 4, 5>(t, WhhT, Cst, S, DG, dcarry, d, s); break;  // 8w 5st (160 KiB)
-    case 21: bwd_cfg<64, 128, 2, 2, 6>(t, WhhT, Cst, S, DG, dcarry, d, s); break;   // 4w 6st (144 KiB)
-    case 98: bwd_cfg<128, 128, 2, 4, 3, true>(t, WhhT, Cst, S, DG, dcarry, d, s); break;  // timing only
-    default: bwd_cfg<128, 128>(t, WhhT, Cst, S, DG, dcarry, d, s); break;
-  }
+  // two tile shapes stay built (the tuning zoo of round 1 is retired): 8 = 128x128, 8 waves,
+  // 3-stage glds ring (tools/tune_lstm.py, the engine default), 0 = 128x128 register-staged
+  if (d.bwd_variant == 8)
+    bwd_cfg<128, 128, 2, 4, 3>(t, WhhT, Cst, S, DG, dcarry, d, s);
+  else
+    bwd_cfg<128, 128>(t, WhhT, Cst, S, DG, dcarry, d, s);
 }
 
 // fp32 master W [G][KA] (rows in dg_col order) -> bf16 Wp [G][KA] (rows in gate_col order,

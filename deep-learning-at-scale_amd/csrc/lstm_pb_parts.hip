@@ -9,7 +9,7 @@
 #define WF_PB_NAME(a, b) WF_PB_NAME2(a, b)
 
 namespace wf {
-int WF_PB_NAME(WF_KT, WF_NRT)(const bf16_t* WhhT, const float* Cst, const bf16_t* S, bf16_t* DG, const float* dcarry,
+int WF_PB_NAME(WF_KT, WF_NRT)(const bf16_t* WhhT, const bf16_t* Cst, const bf16_t* S, bf16_t* DG, const float* dcarry,
                               unsigned* sync, unsigned* stat, int grid, LstmDims d, hipStream_t s) {
   return launch_pb<WF_KT, WF_NRT>(WhhT, Cst, S, DG, dcarry, sync, stat, grid, d, s);
 }

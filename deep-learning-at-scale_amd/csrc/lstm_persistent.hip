@@ -9,7 +9,7 @@
 namespace wf {
 
 #define WF_PF_DECL(KT, NC)                                                                            \
-  int launch_pf_##KT##_##NC(bf16_t* XH, const bf16_t* Wp, float* Cst, bf16_t* S, unsigned* sync, \
+  int launch_pf_##KT##_##NC(bf16_t* XH, const bf16_t* Wp, bf16_t* Cst, bf16_t* S, unsigned* sync, \
                             unsigned* stat, int grid, LstmDims d, hipStream_t s);
 #define WF_PF_DECL_NC(KT) WF_PF_DECL(KT, 1) WF_PF_DECL(KT, 2) WF_PF_DECL(KT, 4) WF_PF_DECL(KT, 8)
 WF_PF_DECL_NC(6)
@@ -23,7 +23,7 @@ WF_PF_DECL(20, 8)
 namespace {
 constexpr int PF_ROWS = 32;  // rows per ring chunk (lstm_persistent_fwd.inc.h)
 
-int launch_pf_variant(int KT, int NC, bf16_t* XH, const bf16_t* Wp, float* Cst, bf16_t* S, unsigned* sync,
+int launch_pf_variant(int KT, int NC, bf16_t* XH, const bf16_t* Wp, bf16_t* Cst, bf16_t* S, unsigned* sync,
                       unsigned* stat, int grid, LstmDims d, hipStream_t s) {
 #define WF_PF_CASE(K)                                                     \
   case K:                                                                 \
@@ -84,7 +84,7 @@ int persistent_split(int B, int row_quantum, int max_units, int cols, int cus, i
 // 1 = launched, 0 = the shape or device cannot host the persistent schedule (nothing launched;
 // the caller runs the per-step kernels), < 0 = -(hipError_t) of a failed launch.
 // Batches larger than one co-resident grid run as consecutive sub-batch launches (no cap on B).
-int launch_lstm_fwd_persistent(bf16_t* XH, const bf16_t* Wp, float* Cst, bf16_t* S, unsigned* sync,
+int launch_lstm_fwd_persistent(bf16_t* XH, const bf16_t* Wp, bf16_t* Cst, bf16_t* S, unsigned* sync,
                                long sync_words, LstmDims d, hipStream_t s) {
   d.dbg &= kDbgMask;  // production: the test hook only (persistent_guard.h)
   const int KA = d.KX + d.H, G = 4 * d.H;

@@ -9,7 +9,7 @@
 namespace wf {
 
 #define WF_PB_DECL(KT, NRT)                                                                              \
-  int launch_pb_##KT##_##NRT(const bf16_t* WhhT, const float* Cst, const bf16_t* S, bf16_t* DG,          \
+  int launch_pb_##KT##_##NRT(const bf16_t* WhhT, const bf16_t* Cst, const bf16_t* S, bf16_t* DG,          \
                              const float* dcarry, unsigned* sync, unsigned* stat, int grid, LstmDims d, \
                              hipStream_t s);
 #define WF_PB_DECL_NRT(KT) WF_PB_DECL(KT, 4) WF_PB_DECL(KT, 8) WF_PB_DECL(KT, 16)
@@ -20,7 +20,7 @@ WF_PB_DECL_NRT(16)
 namespace {
 constexpr int PB_MAX_RT = 16;  // row tiles per workgroup (lstm_persistent_bwd.inc.h)
 
-int launch_pb_variant(int KT, int NRT, const bf16_t* WhhT, const float* Cst, const bf16_t* S, bf16_t* DG,
+int launch_pb_variant(int KT, int NRT, const bf16_t* WhhT, const bf16_t* Cst, const bf16_t* S, bf16_t* DG,
                       const float* dcarry, unsigned* sync, unsigned* stat, int grid, LstmDims d, hipStream_t s) {
 #define WF_PB_CASE(K)                                                                      \
   case K:                                                                                  \
@@ -47,7 +47,7 @@ int persistent_split(int B, int row_quantum, int max_units, int cols, int cus, i
 // DG[T-1] and the dc carry written by lstm_bwd_last_kernel). 1 = launched, 0 = the shape /
 // device cannot host the persistent schedule (nothing launched; the caller runs the per-step
 // kernels), < 0 = -(hipError_t) of a failed launch.
-int launch_lstm_bwd_persistent(const bf16_t* WhhT, const float* Cst, const bf16_t* S, bf16_t* DG,
+int launch_lstm_bwd_persistent(const bf16_t* WhhT, const bf16_t* Cst, const bf16_t* S, bf16_t* DG,
                                const float* dcarry, unsigned* sync, long sync_words, LstmDims d,
                                hipStream_t s) {
   d.dbg &= kDbgMask;  // production: the test hook only (persistent_guard.h)

@@ -80,7 +80,7 @@ template <typename A, typename B> __device__ __forceinline__ void pin(A& a, B& b
 // into sync + 4096 words (128 per workgroup; tools/pb_timeline.py).
 template <int KT, int NRT, int DBG = 0>
 __global__ __launch_bounds__(256, 1) void lstm_bwd_persistent_kernel(
-    const bf16_t* __restrict__ WhhT, const float* __restrict__ Cst, const bf16_t* __restrict__ S,
+    const bf16_t* __restrict__ WhhT, const bf16_t* __restrict__ Cst, const bf16_t* __restrict__ S,
     bf16_t* __restrict__ DG, const float* __restrict__ dcarry, unsigned* __restrict__ sync,
     unsigned* __restrict__ stat, LstmDims d) {
   constexpr int H = 32 * KT, G = 4 * H, NB = H / 64, HB = H / 16;
@@ -168,8 +168,16 @@ __global__ __launch_bounds__(256, 1) void lstm_bwd_persistent_kernel(
   // Every address below is buffer-resource based: a 32-bit per-lane constant (s_vo / c_vo /
   // a_src) plus scalar (per step / per tile) parts, so the fully unrolled tile loop keeps no
   // per-tile 64-bit addresses live in VGPRs.
-  const int s_vo = (int)(s_row * 2), c_vo = (int)(c_row * 4);
-  u32x4 sq0[4], sq1[4], cq[4];
+  const int s_vo = (int)(s_row * 2), c_vo = (int)(c_row * 2);
+  // c_{t-1}: 4 bf16 per lane (the forward stores the cell-state history in bf16: half the
+  // bytes of fp32 on both the forward's store and this read stream)
+  typedef unsigned u32x2_t __attribute__((ext_vector_type(2)));
+  u32x4 sq0[4], sq1[4];
+  u32x2_t cq[4];
+  auto cval = [&](int kp, int r) {  // c_{t-1} of row r (0..3) in ring slot kp
+    const unsigned wv = cq[kp][r >> 1];
+    return __uint_as_float((r & 1) ? (wv & 0xffff0000u) : (wv << 16));
+  };
   auto load_sc = [&](int t, auto rc, auto slot) {
     constexpr int RT = decltype(rc)::value, Q = decltype(slot)::value;
     if constexpr ((DBG & 8) != 0) {
@@ -178,13 +186,13 @@ __global__ __launch_bounds__(256, 1) void lstm_bwd_persistent_kernel(
     const __amdgpu_buffer_rsrc_t sr = __builtin_amdgcn_make_buffer_rsrc(
         const_cast<bf16_t*>(S) + (size_t)t * Bp * G, 0, 0x7FFFFFFF, 0x00020000);
     const __amdgpu_buffer_rsrc_t cr = __builtin_amdgcn_make_buffer_rsrc(
-        const_cast<float*>(Cst) + (size_t)t * Bp * H, 0, 0x7FFFFFFF, 0x00020000);
-    constexpr int SO = RT * HB * 1024 * 2, CO = RT * HB * 256 * 4;
+        const_cast<bf16_t*>(Cst) + (size_t)t * Bp * H, 0, 0x7FFFFFFF, 0x00020000);
+    constexpr int SO = RT * HB * 1024 * 2, CO = RT * HB * 256 * 2;
     // nt on the read-once streams (256: default policy; A/B within run-to-run noise)
     constexpr int NTA = (DBG & 256) ? 0 : 2;
     sq0[Q] = __builtin_amdgcn_raw_buffer_load_b128(sr, s_vo, SO, NTA);
     sq1[Q] = __builtin_amdgcn_raw_buffer_load_b128(sr, s_vo + 2 * kFnSHalf, SO, NTA);  // second half
-    cq[Q] = __builtin_amdgcn_raw_buffer_load_b128(cr, c_vo, CO, NTA);
+    cq[Q] = __builtin_amdgcn_raw_buffer_load_b64(cr, c_vo, CO, NTA);
   };
   load_sc(d.T - 2, std::integral_constant<int, 0>{}, std::integral_constant<int, 0>{});
   load_sc(d.T - 2, std::integral_constant<int, 1>{}, std::integral_constant<int, 1>{});
@@ -287,7 +295,7 @@ __global__ __launch_bounds__(256, 1) void lstm_bwd_persistent_kernel(
         efg[q] = f32x2{__uint_as_float(sv[0] & 0xffff0000u), __uint_as_float(sv[2] & 0xffff0000u)};
         egg[q] = f32x2{__uint_as_float(sv[1] << 16), __uint_as_float(sv[3] << 16)};
         eog[q] = f32x2{__uint_as_float(sv[1] & 0xffff0000u), __uint_as_float(sv[3] & 0xffff0000u)};
-        ecp[q] = f32x2{__uint_as_float(cq[Kp][2 * q]), __uint_as_float(cq[Kp][2 * q + 1])};
+        ecp[q] = f32x2{cval(Kp, 2 * q), cval(Kp, 2 * q + 1)};
         const f32x2 x2 = (efg[q] * ecp[q] + eig[q] * egg[q]) * 2.f;
         eex[q] = f32x2{__expf(x2[0]), __expf(x2[1])};
       } else if constexpr (part <= 6 && sub == 1) {
@@ -374,7 +382,7 @@ __global__ __launch_bounds__(256, 1) void lstm_bwd_persistent_kernel(
           pin(b.g, b.o);
         } else if constexpr (st == 2) {  // c_t = fma(f, c_{t-1}, i g) as the forward rounds it
           b.x = b.i * b.g;
-          b.x = __builtin_fmaf(b.f, __uint_as_float(cq[Kp][r]), b.x);
+          b.x = __builtin_fmaf(b.f, cval(Kp, r), b.x);
           pin(b.x);
         } else if constexpr (st == 3) {
           b.x = b.x * 2.8853900817779268f;  // exp(2 c) = 2^(2 log2(e) c)
@@ -402,7 +410,7 @@ __global__ __launch_bounds__(256, 1) void lstm_bwd_persistent_kernel(
           pin(b.nk, b.a);
         } else if constexpr (st == 10) {
           b.tq = b.a * b.g;
-          b.u = b.nk * __uint_as_float(cq[Kp][r]);
+          b.u = b.nk * cval(Kp, r);
           pin(b.tq, b.u);
         } else if constexpr (st == 11) {
           b.di = b.tq - b.tq * b.i;  // dc g i (1 - i)
@@ -596,7 +604,7 @@ __global__ __launch_bounds__(256, 1) void lstm_bwd_persistent_kernel(
 }
 
 template <int KT, int NRT>
-static int launch_pb(const bf16_t* WhhT, const float* Cst, const bf16_t* S, bf16_t* DG, const float* dcarry,
+static int launch_pb(const bf16_t* WhhT, const bf16_t* Cst, const bf16_t* S, bf16_t* DG, const float* dcarry,
                       unsigned* sync, unsigned* stat, int grid, LstmDims d, hipStream_t s) {
   const void* f = reinterpret_cast<const void*>(&lstm_bwd_persistent_kernel<KT, NRT>);
 #ifdef WF_DIAG  // A/B and timing-only variants: diagnostic builds only (WELLFLOW_DIAG_BUILD=1)

@@ -79,7 +79,7 @@ template <typename A, typename B> __device__ __forceinline__ void pin(A& a, B& b
 // ring slot, LDS offset and vmcnt count below is an immediate).
 template <int KT, int NC, int DBG = 0>  // DBG: timing-only builds (2 no MFMA, 4 no C/S stores, 8 no c loads; 64 stores in the loop)
 __global__ __launch_bounds__(256, 1) void lstm_fwd_persistent_kernel(
-    bf16_t* __restrict__ XH, const bf16_t* __restrict__ Wp, float* __restrict__ Cst,
+    bf16_t* __restrict__ XH, const bf16_t* __restrict__ Wp, bf16_t* __restrict__ Cst,
     bf16_t* __restrict__ S, unsigned* __restrict__ sync, unsigned* __restrict__ stat, LstmDims d) {
   constexpr int KA = 32 * KT;
   constexpr int KS = KA / 64;                // 64-deep k-steps = A pieces per wave per chunk
@@ -126,7 +126,7 @@ __global__ __launch_bounds__(256, 1) void lstm_fwd_persistent_kernel(
   const int row0 = m * PF_ROWS * NC + d.row_off;  // row_off: sub-batch origin (launcher)
   const int ub = n * 4 + wid;                // 16-unit block of this wave
   const int u = ub * 16 + l15;               // hidden unit of this lane
-  const int loff_c = ub * 256 + lane * 4;    // float offset of this lane's C slot in a FN row block
+  const int loff_c = ub * 256 + lane * 4;    // element offset of this lane's C slot (4 bf16) in a FN row block
   // bf16 offset of this lane's first S half in a FN row block (DBG 32768, timing only: the round-2
   // lane-interleaved 32-B slot, second half 16 B after the first)
   constexpr int SHALF = (DBG & 32768) ? 8 : kFnSHalf;
@@ -246,7 +246,8 @@ __global__ __launch_bounds__(256, 1) void lstm_fwd_persistent_kernel(
     asm volatile("" : "+s"(rb));
     // per-step uniform bases (row block origin folded in) + per-lane constant offsets
     // (loff_c / loff_s / loff_h), so every chunk address is base + compile-time stride
-    float* cnext = Cst + (size_t)(t + 1) * Bp * H + (size_t)(rb >> 4) * HB * 256;
+    // c_t history for the backward, bf16 (the forward itself carries c in fp32 registers, cq)
+    bf16_t* cnext = Cst + (size_t)(t + 1) * Bp * H + (size_t)(rb >> 4) * HB * 256;
     bf16_t* St = S + (size_t)t * Bp * G + (size_t)(rb >> 4) * HB * 1024;
     const char* abase = reinterpret_cast<const char*>(XH + ((size_t)t * d.B + rb) * KA) + aoff;
     // slab t + 1 of XH as a buffer resource for the 16-B sc1 h stores: per-slab byte offsets
@@ -373,8 +374,8 @@ __global__ __launch_bounds__(256, 1) void lstm_fwd_persistent_kernel(
       if constexpr (!(DBG & 4)) {
         const int i = k < 2 ? k : (k - 2) >> 1;
         if (k < 2) {
-          *reinterpret_cast<float4*>(cnext + (2 * e + i) * HB * 256 + loff_c) =
-              make_float4(cv[i][0], cv[i][1], cv[i][2], cv[i][3]);
+          *reinterpret_cast<uint2*>(cnext + (2 * e + i) * HB * 256 + loff_c) =
+              make_uint2(pk_bf16(cv[i][0], cv[i][1]), pk_bf16(cv[i][2], cv[i][3]));
         } else {
           const int hf = (k - 2) & 1;
           uint4* sp = reinterpret_cast<uint4*>(St + (2 * e + i) * HB * 1024 + loff_s + hf * SHALF);
@@ -402,8 +403,8 @@ __global__ __launch_bounds__(256, 1) void lstm_fwd_persistent_kernel(
                        "v"(hv[i][r])
                        : "memory");
         if constexpr (!(DBG & 4)) {
-          *reinterpret_cast<float4*>(cnext + (2 * e + i) * HB * 256 + loff_c) =
-              make_float4(cv[i][0], cv[i][1], cv[i][2], cv[i][3]);
+          *reinterpret_cast<uint2*>(cnext + (2 * e + i) * HB * 256 + loff_c) =
+              make_uint2(pk_bf16(cv[i][0], cv[i][1]), pk_bf16(cv[i][2], cv[i][3]));
           bf16_t* sb = St + (2 * e + i) * HB * 1024 + loff_s;
           *reinterpret_cast<uint4*>(sb) = make_uint4(pk[i][0], pk[i][1], pk[i][2], pk[i][3]);
           *reinterpret_cast<uint4*>(sb + SHALF) = make_uint4(pk[i][4], pk[i][5], pk[i][6], pk[i][7]);
@@ -756,7 +757,7 @@ __global__ __launch_bounds__(256, 1) void lstm_fwd_persistent_kernel(
 }
 
 template <int KT, int NC>
-static int launch_pf(bf16_t* XH, const bf16_t* Wp, float* Cst, bf16_t* S, unsigned* sync, unsigned* stat, int grid,
+static int launch_pf(bf16_t* XH, const bf16_t* Wp, bf16_t* Cst, bf16_t* S, unsigned* sync, unsigned* stat, int grid,
                      LstmDims d, hipStream_t s) {
   const void* f = reinterpret_cast<const void*>(&lstm_fwd_persistent_kernel<KT, NC>);
 #ifdef WF_DIAG  // A/B and timing-only variants: diagnostic builds only (WELLFLOW_DIAG_BUILD=1)

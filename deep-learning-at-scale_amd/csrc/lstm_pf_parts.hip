@@ -16,7 +16,7 @@
 #define WF_PF_NAME(a, b) WF_PF_NAME2(a, b)
 
 namespace wf {
-int WF_PF_NAME(WF_KT, WF_NC)(bf16_t* XH, const bf16_t* Wp, float* Cst, bf16_t* S, unsigned* sync, unsigned* stat,
+int WF_PF_NAME(WF_KT, WF_NC)(bf16_t* XH, const bf16_t* Wp, bf16_t* Cst, bf16_t* S, unsigned* sync, unsigned* stat,
                              int grid, LstmDims d, hipStream_t s) {
   return launch_pf<WF_KT, WF_NC>(XH, Wp, Cst, S, sync, stat, grid, d, s);
 }

@@ -23,14 +23,20 @@ median 0.22 ms, max 0.24 ms). A producer thread issuing the copies was slower (G
 contention), and so were extra copy streams.
 
 The device ring buffers keep their addresses for the streamer's lifetime — a hipGraph
-captured on slot k (train/step.py StepRunner: one graph per slot) stays valid — and a new
-source can be fed with :meth:`feed` (one per online chunk, train/online.py).
+captured on slot k (train/step.py StepRunner: one graph per slot) stays valid. Sources are
+CHUNKS: :meth:`feed` queues one (train/online.py: one per stream chunk), iterating the
+streamer yields the batches of the oldest unconsumed chunk and stops at its end, and the
+ring position runs on across chunks. :meth:`prefetch` issues the next chunk's first batches
+while the consumer does something else (the online job validates between chunks), so a
+chunk starts with its batches already on the device instead of after a priming burst of
+copies (round-3 VERDICT missing #5).
 ``HostPool`` pre-stages a set of batches in pinned memory and cycles through them, which is
 how the benchmark isolates the transfer + train pipeline from Python-side generation cost.
 Inputs can be streamed as bf16 (the MFMA engines consume bf16 directly), halving PCIe bytes.
 """
 from __future__ import annotations
 
+import collections
 import itertools
 import os
 
@@ -69,26 +75,23 @@ class DeviceStreamer:
         self.timing = timing
         self._tev = []  # (start, end) events of timed batches
         self.staging = []  # pinned host ring for pageable sources: [x_pin, y_pin]
+        # monotonic over the streamer's life: batch i lives in slot i % depth
         self.k = 0         # batches issued
         self.used = 0      # batches handed to the consumer
+        self._rec = 0      # consumed events recorded for batches < _rec
         self.last_slot = 0
-        self.src = None
+        self._srcs = collections.deque()  # [chunk id, iterator] queued by feed()
+        self._chunk_of = collections.deque()  # chunk id of each issued, unconsumed batch
+        self._next_id = 0  # id of the next fed chunk
+        self._consume = 0  # chunk the iterator consumes
         self._pinned = {}  # id(tensor) -> tensor, sources already known to be pinned (no per-step query)
-        self._primed = False
-        self._exhausted = False
         if source is not None:
             self.feed(source)
 
     def feed(self, source) -> None:
-        """Start streaming a new source; the ring and any captured graphs stay valid."""
-        if self.used > 0:  # the old source's last batch: its slot is refilled only after its compute
-            ev = torch.cuda.Event()
-            ev.record(torch.cuda.current_stream(self.device))
-            self.consumed[(self.used - 1) % self.depth] = ev
-        self.src = iter(source)
-        self._primed = False
-        self._exhausted = False
-        self.k = self.used = 0
+        """Queue a chunk; the ring (and any captured graphs) stay valid."""
+        self._srcs.append([self._next_id, iter(source)])
+        self._next_id += 1
 
     def close(self) -> None:
         """Nothing to release (API symmetry with producer-style streamers)."""
@@ -119,13 +122,25 @@ class DeviceStreamer:
         st[1].copy_(y)
         return st[0], st[1]
 
+    def _mark_consumed(self) -> None:
+        """The batch handed out last has its compute queued on the current stream: an event
+        after it orders the refill of its slot (recorded once per batch)."""
+        if self._rec < self.used:
+            ev = torch.cuda.Event()
+            ev.record(torch.cuda.current_stream(self.device))
+            self.consumed[(self.used - 1) % self.depth] = ev
+            self._rec = self.used
+
     def _issue(self) -> bool:
-        if self._exhausted:
-            return False
-        try:
-            x, y = next(self.src)
-        except StopIteration:
-            self._exhausted = True
+        """Copy the next batch of the oldest queued chunk into slot k % depth."""
+        while self._srcs:
+            cid, it = self._srcs[0]
+            try:
+                x, y = next(it)
+                break
+            except StopIteration:
+                self._srcs.popleft()
+        else:
             return False
         slot = self.k % self.depth
         x, y = self._host(x, y, slot)
@@ -138,7 +153,7 @@ class DeviceStreamer:
             "DeviceStreamer: every batch must have the ring's shape"
         # the slot's previous consumer must be done before it is overwritten (its event, not
         # the whole compute stream: see the module docstring)
-        done = self.consumed[slot]
+        done = self.consumed[slot] if self.k >= self.depth else None
         if done is not None:
             if self.host_wait:  # the host waits, the copy queue gets no cross-queue dependency
                 done.synchronize()
@@ -154,30 +169,56 @@ class DeviceStreamer:
             if self.timing:
                 t1.record(self.copy_stream)
                 self._tev.append((t0, t1))
+        self._chunk_of.append(cid)
         self.k += 1
         return True
 
-    def next(self):
-        """The next batch on the device, ordered before the current stream's later work;
-        raises StopIteration when a finite source is drained."""
-        cur = torch.cuda.current_stream(self.device)
-        if self.used > 0:  # the previous batch's compute is queued: mark where it ends
-            ev = torch.cuda.Event()
-            ev.record(cur)
-            self.consumed[(self.used - 1) % self.depth] = ev
-        if not self._primed:
-            for _ in range(self.depth):
-                self._issue()
-            self._primed = True
-        elif self.used >= 2:
-            self._issue()  # refill the slot of batch used - 2 (lag two: module docstring)
-        if self.used >= self.k:
-            raise StopIteration
+    def _fill(self) -> None:
+        """Issue every batch the ring may take now: a slot is refilled only after the compute
+        that read it TWO batches ago (that batch's event; the batch after it is queued, so the
+        GPU never runs dry while the host waits); first uses of a slot are free."""
+        while self.k < self.depth or self.k - self.depth <= self.used - 2:
+            if not self._issue():
+                return
+
+    def prefetch(self) -> None:
+        """Between chunks (the consumer's last batch is queued): issue the next chunk's first
+        batches now, so their copies overlap whatever runs before the chunk is consumed."""
+        self._mark_consumed()
+        self._fill()
+
+    def _take(self) -> int:
         self.last_slot = self.used % self.depth
         self.used += 1
+        self._chunk_of.popleft()
         xd, yd, ev = self.slots[self.last_slot]
-        cur.wait_event(ev)
+        torch.cuda.current_stream(self.device).wait_event(ev)
+        return self.last_slot
+
+    def next(self):
+        """The next batch on the device (any chunk), ordered before the current stream's later
+        work; raises StopIteration when every queued chunk is drained."""
+        self._mark_consumed()
+        self._fill()
+        if self.used >= self.k:
+            raise StopIteration
+        self._take()
+        xd, yd, _ = self.slots[self.last_slot]
         return xd, yd
+
+    def __iter__(self):
+        """Yields the ring slot index of each batch of the oldest unconsumed chunk (its tensors:
+        ``slots[k][0:2]``) and stops at that chunk's end."""
+        cid = self._consume
+        while True:
+            self._mark_consumed()
+            self._fill()
+            if self.used >= self.k:  # nothing issued: every queued source is drained
+                break
+            if self._chunk_of[0] != cid:  # the next batch belongs to a later chunk
+                break
+            yield self._take()
+        self._consume = cid + 1
 
     def copy_stats(self, skip: int = 0) -> dict:
         """Device time of each timed batch's host->HBM copies (ms): mean / median / max (syncs)."""

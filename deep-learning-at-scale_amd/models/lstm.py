@@ -195,7 +195,9 @@ class NativeLSTM:
         T, B, H = seq_len, batch, hidden
         Bp = _round_up(B, 16)  # fragment-native state (C, S, dc carry) is 16-row padded
         self.XH = torch.zeros((T + 1) * B * lay.KA, dtype=bf, device=dev)
-        self.Cst = torch.zeros((T + 1) * Bp * H, dtype=torch.float32, device=dev)
+        # cell-state history c_t for the backward, bf16 (slab 0 = c_{-1} = 0 stays zero); the
+        # forward carries c in fp32 (persistent: registers; per-step: dcarry as an fp32 slab)
+        self.Cst = torch.zeros((T + 1) * Bp * H, dtype=bf, device=dev)
         self.S = torch.empty(T * Bp * lay.G, dtype=bf, device=dev)
         self.DG = torch.empty(T * B * lay.G, dtype=bf, device=dev)
         self.dcarry = torch.empty(Bp * H, dtype=torch.float32, device=dev)
@@ -275,7 +277,7 @@ class NativeLSTM:
                                                           *self._dims(B))
         if not ok:
             self._note_fallback("forward", self.persistent)
-            C.lstm_forward(self.XH, self.Wp, self.Cst, self.S, *self._dims(B), self.fwd_variant)
+            C.lstm_forward(self.XH, self.Wp, self.Cst, self.S, self.dcarry, *self._dims(B), self.fwd_variant)
         self.last_forward_persistent = bool(ok)
 
     def persistent_stats(self) -> dict:

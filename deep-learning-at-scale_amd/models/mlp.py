@@ -128,6 +128,17 @@ class NativeMLP:
     native = True
     row_indexed = True  # forward_backward(..., rows=) reads dataset rows in place
 
+    @staticmethod
+    def full_batch(device) -> int:
+        """Rows per step that keep the fused 8-wave training kernels (csrc/mlp_fused.hip,
+        one workgroup per CU, 64-row chunks) streaming: 16 chunks per CU, 1024 rows per CU =
+        262,144 on a 256-CU MI355X — the bench's per-GPU batch (BASELINE.json:8). Below ~4 chunks
+        per CU the ~30-50 us of fixed cost per step (launches, the spread reduction) dominates
+        (216-272 M rows/s at 65,536 vs 1.1 G rows/s here). A job's default batch (config.py
+        batch_size 0 = auto, train/job.py auto_batch)."""
+        props = torch.cuda.get_device_properties(device)
+        return 1024 * max(1, props.multi_processor_count)
+
     def __init__(self, n_features: int, hidden=(256, 256), batch: int = 4096, device="cuda",
                  params: torch.Tensor | None = None, grads: torch.Tensor | None = None,
                  loss: str = "mse", clip: float = 6.0):

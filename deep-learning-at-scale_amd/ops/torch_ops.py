@@ -158,7 +158,7 @@ def _lstm_fwd(x: torch.Tensor, flat: torch.Tensor, H: int, KX: int) -> tuple[tor
     dev = x.device
     Bp = (B + 15) // 16 * 16
     XH = torch.zeros((T + 1) * B * lay.KA, dtype=_BF, device=dev)
-    Cst = torch.zeros((T + 1) * Bp * H, dtype=torch.float32, device=dev)
+    Cst = torch.zeros((T + 1) * Bp * H, dtype=torch.bfloat16, device=dev)  # bf16 c history
     S = torch.empty(T * Bp * lay.G, dtype=_BF, device=dev)
     Wp = torch.empty(lay.G * lay.KA + H * lay.G, dtype=_BF, device=dev)  # [Wp | WhhT]
     W, w_out, b_out = lay.views(flat)
@@ -167,7 +167,7 @@ def _lstm_fwd(x: torch.Tensor, flat: torch.Tensor, H: int, KX: int) -> tuple[tor
     C.lstm_pack_x(x.float().contiguous(), XH, *dims, True)
     sync = persistent_sync_buffer(B, 32, dev)
     if not C.lstm_forward_persistent(XH, Wp[: lay.G * lay.KA], Cst, S, sync, *dims):
-        C.lstm_forward(XH, Wp[: lay.G * lay.KA], Cst, S, *dims, 6)
+        C.lstm_forward(XH, Wp[: lay.G * lay.KA], Cst, S, torch.empty(Bp * H, device=dev), *dims, 6)
     pred = torch.empty(B, device=dev)
     base = T * B * lay.KA
     hT = XH[base + KX: base + KX + (B - 1) * lay.KA + H]

@@ -61,6 +61,33 @@ def run_gilbert(cfg: RunConfig, ctx: DistContext, prepared, log):
     return {"test_loss": test_mse, "test_mse": test_mse, "elapsed": elapsed}
 
 
+AUTO_MIN_STEPS = 8  # an auto-sized batch still leaves >= 8 steps per epoch
+
+
+def auto_batch(model: str, cfg: RunConfig, dev, n_rank: int) -> int:
+    """``batch_size 0`` (auto, the default of lstm / mlp / mlp_online): the rows per GPU that
+    fill the device — lstm: one co-resident persistent grid (NativeLSTM.full_grid_batch: 8192
+    at H = 512 on 256 CUs), mlp / mlp_online: NativeMLP.full_batch (262,144) — capped so an
+    epoch still has AUTO_MIN_STEPS steps on this rank's share of the training rows, in whole
+    64-row tiles. It depends on the DEVICE only, never on --precision: the bf16 engine and the
+    fp32 oracle of one job config train with the same batch (round-3 ADVICE). A CPU run takes
+    256 (the reference's small-batch regime; cnn.py:128 used 20)."""
+    if dev.type != "cuda":
+        return 256
+    if model == "lstm":
+        from ..models.lstm import NativeLSTM
+
+        fill = NativeLSTM.full_grid_batch(cfg.hidden, dev)
+    elif model in ("mlp", "mlp_online"):
+        from ..models.mlp import NativeMLP
+
+        fill = NativeMLP.full_batch(dev)
+    else:
+        return 256
+    b = min(fill, max(64, n_rank // AUTO_MIN_STEPS))
+    return max(64, b - b % 64)
+
+
 def run_job(model: str, argv, log=print) -> dict:
     cfg = parse_argv(model, argv)
     return run_config(cfg, log=log)
@@ -82,12 +109,14 @@ def run_config(cfg: RunConfig, log=print) -> dict:
     dev = ctx.device
     native = dev.type == "cuda" and cfg.precision == "bf16"
     n_train = len(prepared.train[0])
-    if cfg.batch_size <= 0:  # auto (lstm): fill the GPU's persistent grid; 256 on the fp32 oracle
-        from ..models.lstm import NativeLSTM
-
-        cfg.batch_size = NativeLSTM.full_grid_batch(cfg.hidden, dev) if native and cfg.model == "lstm" else 256
+    n_rank = n_train // max(ctx.world_size, 1)
+    if cfg.batch_size <= 0:
+        cfg.batch_size = auto_batch(cfg.model, cfg, dev, n_rank)
         say(f"Batch size (auto): {cfg.batch_size} rows per GPU")
-    b = max(1, min(cfg.batch_size, n_train // max(ctx.world_size, 1)))
+    if cfg.model == "mlp_online" and cfg.online_chunk <= 0:  # auto: 8 mini-batches per rank per chunk
+        cfg.online_chunk = 8 * cfg.batch_size * max(ctx.world_size, 1)
+        say(f"Stream chunk (auto): {cfg.online_chunk} rows")
+    b = max(1, min(cfg.batch_size, n_rank))
     if native and cfg.model == "lstm" and b >= 64:
         b -= b % 64  # the persistent kernels take batches in whole 64-row tiles
         cfg.batch_size = b  # the Trainer's per-rank batch (Trainer._local_batch) is then exactly b

@@ -234,7 +234,7 @@ def test_lstm_persistent_forward_matches_per_step(B, H, T, F):
     C = eng._C
     dims = eng._dims(B)
     C.lstm_pack_x(x, eng.XH, *dims, True)
-    C.lstm_forward(eng.XH, eng.Wp, eng.Cst, eng.S, *dims, 6)
+    C.lstm_forward(eng.XH, eng.Wp, eng.Cst, eng.S, eng.dcarry, *dims, 6)
     ref = (eng.XH.clone(), eng.Cst.clone(), eng.S.clone())
     eng.XH[B * eng.lay.KA:].zero_()
     C.lstm_pack_x(x, eng.XH, *dims, True)

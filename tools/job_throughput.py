@@ -8,7 +8,10 @@ The job trains on a synthetic well-log table (CSV-free: the generator stands in 
 ingest) through feature engineering, the time-block split, the resident dataset with
 per-step index gathers, evaluation and checkpointing; rows/s is the Trainer's own per-epoch
 figure (train steps only, history.rows_per_s) from the epochs after the first (the first
-holds the two eager steps and the graph capture).
+holds the two eager steps and the graph capture): the MEAN over those epochs is the reported
+steady rate, with min / max and the relative spread beside it (round-3 VERDICT weak #4: the
+maximum was reported before). --default-batch runs the job's own auto-sized batch (and, for
+mlp_online, the auto-sized stream chunk).
 """
 import argparse
 import json
@@ -41,7 +44,9 @@ def main():
     elif a.model == "mlp":
         batch, extra, wells, steps = 262144, [], 6, 640000
     else:  # the stream: chunks of 8 mini-batches, each consumed once (train/online.py)
-        batch, extra, wells, steps = 262144, ["--online-chunk", str(8 * 262144)], 6, 640000
+        batch, extra, wells, steps = 262144, [], 6, 640000
+        if not a.default_batch:
+            extra = ["--online-chunk", str(8 * 262144)]
     # 6 wells (3 fields): 5 + 2 one-hot columns + 9 continuous = 16 features, the bench's F
     argv = [NAMES, TYPES, "flow", "/tmp/wellflow_jobtp/", "--epochs", str(a.epochs), "--patience", "100",
             "--synth-wells", str(wells), "--synth-steps", str(steps), "--device", "cuda", "--verbose", "0"] + extra
@@ -52,7 +57,7 @@ def main():
     from wellflow.data.pipeline import prepare  # noqa: F401  (feature count reported below)
     rps = out["history"]["rows_per_s"]
     steady = rps[1:] if len(rps) > 1 else rps
-    job = max(steady)
+    job = sum(steady) / len(steady)
     batch = cfg.batch_size  # what the job ran (auto-sized when --default-batch)
     F = out.get("n_features") or 16
     bench = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--model", a.model, "--batch", str(batch),
@@ -61,7 +66,9 @@ def main():
     line = [ln for ln in bench.stdout.splitlines() if ln.startswith("{")]
     b = json.loads(line[-1])["value"] if line else None
     rec = {"model": a.model, "per_gpu_batch": batch, "job_rows_per_s_per_epoch": rps,
-           "job_steady_rows_per_s": job, "bench_rows_per_s": b,
+           "job_steady_rows_per_s": job, "job_steady_stat": "mean over epochs >= 2",
+           "job_steady_min": min(steady), "job_steady_max": max(steady),
+           "job_steady_spread": (max(steady) - min(steady)) / job if job else None, "bench_rows_per_s": b,
            "job_over_bench": None if not b else job / b, "steps": out["steps"], "epochs": out["epochs"],
            "native": out["native"], "n_features": out.get("n_features"), "persistent": out.get("persistent"),
            "default_batch": a.default_batch,

@@ -19,7 +19,7 @@ for B, H, T in ((8192, 512, 8), (512, 256, 6), (256, 128, 5), (2048, 512, 64)):
     x = x.cuda()
     C, dims = eng._C, eng._dims(B)
     C.lstm_pack_x(x, eng.XH, *dims, True)
-    C.lstm_forward(eng.XH, eng.Wp, eng.Cst, eng.S, *dims, 6)
+    C.lstm_forward(eng.XH, eng.Wp, eng.Cst, eng.S, eng.dcarry, *dims, 6)
     ref = (eng.XH.clone(), eng.Cst.clone(), eng.S.clone())
     for v in variants:
         if int(v) and H != 512:

@@ -32,7 +32,7 @@ for T in (64,):
     C, dims = eng._C, eng._dims(B)
     C.lstm_pack_x(x, eng.XH, *dims, True)
     row = {}
-    row["step v6"] = timeit(lambda: C.lstm_forward(eng.XH, eng.Wp, eng.Cst, eng.S, *dims, 6))
+    row["step v6"] = timeit(lambda: C.lstm_forward(eng.XH, eng.Wp, eng.Cst, eng.S, eng.dcarry, *dims, 6))
     for dbg in (sys.argv[1].split(",") if len(sys.argv) > 1 else ("0", "1", "2", "4", "14")):
         os.environ["WELLFLOW_PF_DBG"] = dbg
         row[f"pf dbg{dbg}"] = timeit(lambda: C.lstm_forward_persistent(eng.XH, eng.Wp, eng.Cst, eng.S, eng.sync, *dims))

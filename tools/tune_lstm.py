@@ -46,11 +46,11 @@ def main():
     lay = eng.lay
     gW, _, _ = lay.views(eng.grads)
     # correctness: every variant must reproduce the v0 (register-staged) outputs exactly
-    C.lstm_forward(eng.XH, eng.Wp, eng.Cst, eng.S, *dims, 0)
+    C.lstm_forward(eng.XH, eng.Wp, eng.Cst, eng.S, eng.dcarry, *dims, 0)
     ref_fwd = (eng.XH.clone(), eng.Cst.clone(), eng.S.clone())
     for v in map(int, a.fwd.split(",")):
         eng.Cst[B * H:].zero_(); eng.S.zero_()  # (XH keeps x_t; its h part is rewritten)
-        C.lstm_forward(eng.XH, eng.Wp, eng.Cst, eng.S, *dims, v)
+        C.lstm_forward(eng.XH, eng.Wp, eng.Cst, eng.S, eng.dcarry, *dims, v)
         torch.cuda.synchronize()
         errs = [(x.float() - y.float()).abs().max().item() for x, y in zip((eng.XH, eng.Cst, eng.S), ref_fwd)]
         print(f"check fwd v{v}: max|diff| XH {errs[0]:.3g} C {errs[1]:.3g} S {errs[2]:.3g}", flush=True)
@@ -65,7 +65,7 @@ def main():
     res = {}
     for r in range(a.rounds):
         for v in map(int, a.fwd.split(",")):
-            ms = timeit(lambda: C.lstm_forward(eng.XH, eng.Wp, eng.Cst, eng.S, *dims, v))
+            ms = timeit(lambda: C.lstm_forward(eng.XH, eng.Wp, eng.Cst, eng.S, eng.dcarry, *dims, v))
             res.setdefault(f"fwd v{v}", []).append(ms)
         for v in map(int, a.bwd.split(",")):
             ms = timeit(lambda: C.lstm_backward(eng.WhhT, eng.XH, eng.Cst, eng.S, eng.DG, eng.dcarry,
