@@ -538,6 +538,40 @@ void mlp2_reduce(const at::Tensor& red, int64_t Fp, int64_t B, c10::optional<at:
                          fp(db1), fp(db2), fp(dW1), opt_ptr<float>(dW2, at::kFloat, "dW2", H * H), cur_stream());
 }
 
+// MLP training step forward + backward in one launch (mlp_step.hip); the batch sums land in
+// the spread scratch `red` (mlp2_reduce adds them), dZ2 feeds mlp2_dw2. False = not covered.
+bool mlp2_step(const at::Tensor& X, int64_t Fp, const at::Tensor& W1, const at::Tensor& b1, const at::Tensor& W2,
+               const at::Tensor& b2, const at::Tensor& w3, const at::Tensor& b3, const at::Tensor& y, double dy_scale,
+               int64_t B, c10::optional<at::Tensor> rows, const at::Tensor& dZ2, c10::optional<at::Tensor> pred,
+               const at::Tensor& red) {
+  constexpr int64_t H = 256;
+  check_t(X, at::kBFloat16, "X");
+  const int64_t nrows = check_x_rows(X, Fp, B, rows);
+  check_t(W1, at::kBFloat16, "W1");
+  check_extent(W1, H * Fp, "W1");
+  check_t(W2, at::kBFloat16, "W2");
+  check_extent(W2, H * H, "W2");
+  for (const at::Tensor* t : {&b1, &b2, &w3}) {
+    check_t(*t, at::kFloat, "bias/w3");
+    check_extent(*t, H, "bias/w3");
+  }
+  check_t(b3, at::kFloat, "b3");
+  check_extent(b3, 1, "b3");
+  check_t(y, at::kFloat, "y");
+  check_extent(y, nrows, "y");
+  check_t(dZ2, at::kBFloat16, "dZ2");
+  check_extent(dZ2, B * H, "dZ2");
+  check_t(red, at::kFloat, "red");
+  check_extent(red, wf::kMlpRedFloats, "red");
+  for (const at::Tensor* t : {&X, &W1, &W2, &dZ2})
+    TORCH_CHECK(reinterpret_cast<uintptr_t>(t->data_ptr()) % 16 == 0, "mlp2_step: bf16 operands must be 16-B aligned");
+  TORCH_CHECK(B > 0, "mlp2_step: B > 0");
+  const c10::hip::OptionalHIPGuardMasqueradingAsCUDA guard(X.device());
+  return wf::launch_mlp2_step(bfp(X), (int)Fp, bfp(W1), fp(b1), bfp(W2), fp(b2), fp(w3), fp(b3), fp(y), (float)dy_scale,
+                              (int)B, rows_ptr(rows, B), nrows, bfp(dZ2), opt_ptr<float>(pred, at::kFloat, "pred", B),
+                              fp(red), cur_stream());
+}
+
 // Fused MLP forward (mlp_fused.hip): both 256-wide hidden layers + head (+ MSE) in one launch.
 // Returns false (nothing launched) when the shape is not covered; the caller then runs the
 // per-layer GEMMs + head kernel.
@@ -893,6 +927,7 @@ PYBIND11_MODULE(_C, m) {
   WF_DEF(mlp2_backward);
   WF_DEF(mlp2_dw2);
   WF_DEF(mlp2_reduce);
+  WF_DEF(mlp2_step);
   WF_DEF(lstm_pack_x);
   WF_DEF(lstm_forward);
   WF_DEF(lstm_forward_persistent);

@@ -117,6 +117,13 @@ int mlp2_train_grid(int B);
 bool mlp_bwd8();  // the 8-wave backward is selected (WELLFLOW_MLP_BWD8, default on)
 void launch_mlp2_reduce(float* red, int Fp, int B, float* loss_sum, float* db3, float* dw3, float* db1, float* db2,
                         float* dW1, float* dW2, hipStream_t s);
+// The training step's forward + backward in ONE launch (mlp_step.hip): from X (rows), y, the
+// bf16 weights and fp32 biases / head — dZ2 ([B][256] bf16, mlp2_dw2's operand), pred (optional)
+// and every batch sum except dW2 (loss, db3, dw3, db1, db2, dW1) into the spread scratch `red`,
+// which launch_mlp2_reduce then adds to the gradients. Fp <= 32; false = not covered.
+bool launch_mlp2_step(const bf16_t* X, int Fp, const bf16_t* W1, const float* b1, const bf16_t* W2, const float* b2,
+                      const float* w3, const float* b3, const float* y, float dy_scale, int B, const long long* rows,
+                      long nrows, bf16_t* dZ2, float* pred, float* red, hipStream_t s);
 
 // ---- fused reference CNN (cnn_fused.hip): Conv1D(C -> Fp, width taps / C) + ReLU + dropout ->
 // Dense(T * Fp -> O) -> loss, cnn.py:110-118. Flat layout = models/cnn.py CnnLayout:

@@ -23,6 +23,7 @@
 #include "common.h"
 #include "gemm_core.h"
 #include "kernels.h"
+#include "mlp_tiles.h"
 
 namespace wf {
 
@@ -52,7 +53,6 @@ int mlp_dbg() {
 constexpr int kMlpDbgMask = 0;
 int mlp_dbg() { return 0; }
 #endif
-constexpr int MF_ROWS = 64;  // rows per chunk
 }  // namespace
 constexpr int MF_ROWS_PUB = MF_ROWS;
 
@@ -153,29 +153,6 @@ void launch_mlp2_reduce(float* red, int Fp, int B, float* loss_sum, float* db3, 
                      mlp2_train_grid(B), slab_blocks, loss_sum, db3, dw3, db1, db2, dW1, dW2);
 }
 
-namespace {
-// dataset row of batch row gr (indices clamped into the dataset: never an out-of-bounds read)
-__device__ __forceinline__ size_t data_row(const long long* rows, int gr, long nrows) {
-  if (rows == nullptr) return (size_t)gr;
-  long long r = rows[gr];
-  r = r < 0 ? 0 : (r >= nrows ? nrows - 1 : r);
-  return (size_t)r;
-}
-constexpr int MF_H = 256;    // hidden width (both layers)
-
-// [64 rows][256 units] bf16 tile, 16-B chunk c (units 8c..8c+7) of row r at chunk c ^ (r & 15)
-// (32 chunks per row, 512-B rows): the B-fragment reads (16 rows x one chunk) hit 16 distinct
-// 16-B bank groups, as do the row-wise copy-out reads.
-__device__ __forceinline__ int tile_off(int row, int unit) {
-  const int c = unit >> 3;
-  return row * (MF_H * 2) + ((c ^ (row & 15)) << 4) + ((unit & 7) << 1);
-}
-// [64 rows][64 features] bf16 input tile (8 chunks per row, 128-B rows: rows r and r + 2
-// share banks, so the chunk is swizzled by (row >> 1) & 7 — 16-row fragment reads of one
-// chunk hit 16 distinct bank groups)
-constexpr int MF_XROW = 128;
-__device__ __forceinline__ int xtile_off(int row, int chunk) { return row * MF_XROW + ((chunk ^ ((row >> 1) & 7)) << 4); }
-}  // namespace
 
 template <int KT1>  // layer-1 K steps of 32 features: 1 (Fp <= 32) or 2 (Fp <= 64)
 __global__ __launch_bounds__(256, 1) void mlp2_fwd_kernel(

@@ -1,0 +1,371 @@
+// wellflow — the MLP training step's forward AND backward in one persistent launch
+// (F -> 256 -> 256 -> 1, ReLU, MSE; reference mlp.py model + train_step). SURVEY.md §2.4 K9-K11.
+//
+// Replaces mlp2_fwd_train_kernel + mlp2_bwd_rc8_kernel (mlp_fused.hip) for the training step:
+// per 64-row chunk the X tile is staged ONCE, layer 1 runs once (the two-kernel path ran it in
+// the forward and again in the backward), H2 never leaves the registers (no ReLU bitmask round
+// trip through HBM) and dy never leaves the workgroup. Per chunk and wave (8 waves, wave w owns
+// hidden units [32w, 32w + 32) of both layers):
+//   layer 1   H1^T = relu(W1 X^T + b1)        own units -> LDS tile (bf16)        8 MFMA
+//   layer 2   Z2^T = W2 H1^T                  own units, K = all of H1           64 MFMA
+//   head      p = H2 w3 + b3 (partials over waves via LDS), dy = s (p - y), loss, dw3, db3
+//   dZ2       = dy w3^T * [H2 > 0]            own units -> LDS tile + HBM (dW2's operand)
+//   dH1^T     = W2^T dZ2^T                    own units k, K = all of dZ2        64 MFMA
+//   dZ1       = dH1 * [H1 > 0]                in place over the wave's own H1 columns
+//   dW1^T    += dZ1^T X                       ds_read_b64_tr_b16 fragments     2 NFT MFMA
+// W1 rows, W2 rows (layer 2 A operand) and W2^T rows (dH1 A operand) stay in registers for the
+// whole launch; b1 / b2 / w3 are read from LDS. Four workgroup barriers per chunk (X staged,
+// H1 complete, head partials complete, dZ2 complete). Batch sums go to the spread-reduction
+// scratch exactly as the two kernels' did (kMlpRedCopies copies + the per-workgroup dW1 rows),
+// so mlp2_dw2 and mlp2_reduce run unchanged after it.
+#include "common.h"
+#include "gemm_core.h"
+#include "kernels.h"
+#include "mlp_tiles.h"
+
+namespace wf {
+
+namespace {
+template <int NFT>  // 16-feature tiles of dW1: 1 (Fp <= 16) or 2 (Fp <= 32)
+__global__ __launch_bounds__(512, 1) void mlp2_step_kernel(
+    const bf16_t* __restrict__ X, int Fp, const bf16_t* __restrict__ W1, const float* __restrict__ b1,
+    const bf16_t* __restrict__ W2, const float* __restrict__ b2, const float* __restrict__ w3,
+    const float* __restrict__ b3, const float* __restrict__ y, float dy_scale, int B,
+    const long long* __restrict__ rows, long nrows, bf16_t* __restrict__ dZ2, float* __restrict__ pred,
+    float* __restrict__ red) {
+  constexpr int MT = 2, NW = 8, XB = MF_ROWS * MF_XROW;
+  __shared__ __attribute__((aligned(16))) char xs[2 * XB];              // X tiles (double-buffered)
+  __shared__ __attribute__((aligned(16))) char h1s[MF_ROWS * MF_H * 2];  // H1 -> dZ1 (own columns)
+  __shared__ __attribute__((aligned(16))) char zs[MF_ROWS * MF_H * 2];   // dZ2
+  __shared__ __attribute__((aligned(16))) float hred[MF_ROWS][NW];       // head partials
+  __shared__ __attribute__((aligned(16))) float cst[3][MF_H];            // b1, b2, w3
+  __shared__ float ys[2][MF_ROWS];
+  __shared__ float lred[NW];
+  // lane-private running sums of dw3, db1, db2 (slot [wave][sum][4m + r][lane]): 24 VGPRs
+  // cheaper in LDS (one ds_add per value per chunk) than in the register file
+  __shared__ __attribute__((aligned(16))) float part[NW][3][2 * 4][64];
+
+  const int tid = threadIdx.x, lane = tid & 63, l15 = lane & 15, g = lane >> 4;
+  const int wid = tid >> 6;
+  const int u0 = wid * 16 * MT;
+  const int tq = l15 >> 2, tp = lane & 3;  // ds_read_b64_tr_b16 lane coordinates
+  for (int i = tid; i < 3 * MF_H; i += 64 * NW) cst[i / MF_H][i % MF_H] = (i < MF_H ? b1 : i < 2 * MF_H ? b2 : w3)[i % MF_H];
+
+  bf16x8 w1f[MT], wt[MT][8];
+#pragma unroll
+  for (int m = 0; m < MT; ++m) {
+    const int u = u0 + 16 * m + l15;
+    w1f[m] = 8 * g + 8 <= Fp ? *reinterpret_cast<const bf16x8*>(W1 + (size_t)u * Fp + 8 * g)
+                             : bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+    for (int kt = 0; kt < 8; ++kt)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) wt[m][kt][j] = (short)W2[(size_t)(32 * kt + 8 * g + j) * MF_H + u];
+  }
+  // layer 2's A operand (W2 rows of the own units) is streamed from L2 per K step, WD steps
+  // ahead: holding it too (64 VGPRs) would not fit beside W2^T in the 256-VGPR budget of two
+  // waves per SIMD
+  constexpr int WD = 3;
+  const int w2lane = (u0 + l15) * MF_H + 8 * g;  // element offset of the lane's m = 0 fragment
+  const bf16_t* w2c = W2;  // laundered per chunk (below): the loads must not be hoisted out of the loop
+  auto w2frag = [&](int m, int kt) { return *reinterpret_cast<const bf16x8*>(w2c + w2lane + 16 * MF_H * m + 32 * kt); };
+  f32x4 dw1a[MT][NFT];
+#pragma unroll
+  for (int m = 0; m < MT; ++m)
+#pragma unroll
+    for (int f = 0; f < NFT; ++f) dw1a[m][f] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int k = 0; k < 3 * MT * 4; ++k) part[wid][k / (MT * 4)][k % (MT * 4)][lane] = 0.f;
+  constexpr int P_DW3 = 0, P_DB1 = 1, P_DB2 = 2;
+  const float bias3 = b3[0];
+  float lsum = 0.f, db3a = 0.f;
+
+  // next chunk's inputs: threads 0..255 one 16-B X row segment each (row t >> 2, chunk t & 3),
+  // threads 256..319 one target
+  uint4 xv = make_uint4(0, 0, 0, 0);
+  float yv = 0.f;
+  auto prefetch = [&](int ch) {
+    if (tid < 256) {
+      const int r = tid >> 2, c = tid & 3, gr = ch * MF_ROWS + r;
+      xv = (gr < B && 8 * c + 8 <= Fp) ? *reinterpret_cast<const uint4*>(X + data_row(rows, gr, nrows) * Fp + 8 * c)
+                                       : make_uint4(0, 0, 0, 0);
+    } else if (tid < 256 + MF_ROWS) {
+      const int gr = ch * MF_ROWS + tid - 256;
+      yv = gr < B ? y[data_row(rows, gr, nrows)] : 0.f;
+    }
+  };
+  const int nchunks = (B + MF_ROWS - 1) / MF_ROWS;
+  if ((int)blockIdx.x < nchunks) prefetch(blockIdx.x);
+  int par = 0;
+  for (int ch = blockIdx.x; ch < nchunks; ch += gridDim.x, par ^= 1) {
+    const int row0 = ch * MF_ROWS;
+    char* xt = xs + par * XB;
+    if (tid < 256)
+      *reinterpret_cast<uint4*>(xt + xtile_off(tid >> 2, tid & 3)) = xv;
+    else if (tid < 256 + MF_ROWS)
+      ys[par][tid - 256] = yv;
+    __syncthreads();  // B1: X / y staged (and, first chunk, cst)
+    if (ch + (int)gridDim.x < nchunks) prefetch(ch + gridDim.x);
+
+    // ---- layer 1 (own units): H1 -> h1s; the first W2 fragments of layer 2 in flight
+    bf16x8 w2r[WD][MT];
+    w2c = W2;
+    asm volatile("" : "+s"(w2c));
+#pragma unroll
+    for (int k = 0; k < WD; ++k)
+#pragma unroll
+      for (int m = 0; m < MT; ++m) w2r[k][m] = w2frag(m, k);
+    f32x4 acc[MT][4];
+#pragma unroll
+    for (int n = 0; n < 4; ++n) {
+      const bf16x8 xb = *reinterpret_cast<const bf16x8*>(xt + xtile_off(16 * n + l15, g));
+#pragma unroll
+      for (int m = 0; m < MT; ++m)
+        acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w1f[m], xb, f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+    }
+#pragma unroll
+    for (int m = 0; m < MT; ++m) {
+      const float4 bb = *reinterpret_cast<const float4*>(&cst[0][u0 + 16 * m + 4 * g]);
+#pragma unroll
+      for (int n = 0; n < 4; ++n) {
+        const unsigned p0 = pk_bf16(fmaxf(acc[m][n][0] + bb.x, 0.f), fmaxf(acc[m][n][1] + bb.y, 0.f));
+        const unsigned p1 = pk_bf16(fmaxf(acc[m][n][2] + bb.z, 0.f), fmaxf(acc[m][n][3] + bb.w, 0.f));
+        *reinterpret_cast<uint2*>(h1s + tile_off(16 * n + l15, u0 + 16 * m + 4 * g)) = make_uint2(p0, p1);
+      }
+    }
+    __syncthreads();  // B2: H1 complete
+
+    // ---- layer 2 (own units, K = 256)
+#pragma unroll
+    for (int m = 0; m < MT; ++m)
+#pragma unroll
+      for (int n = 0; n < 4; ++n) acc[m][n] = f32x4{0.f, 0.f, 0.f, 0.f};
+    static_for<0, 8>([&](auto kc) {
+      constexpr int kt = decltype(kc)::value;
+      bf16x8 hb[4];
+#pragma unroll
+      for (int n = 0; n < 4; ++n) hb[n] = *reinterpret_cast<const bf16x8*>(h1s + tile_off(16 * n + l15, 32 * kt + 8 * g));
+#pragma unroll
+      for (int m = 0; m < MT; ++m)
+#pragma unroll
+        for (int n = 0; n < 4; ++n)
+          acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w2r[kt % WD][m], hb[n], acc[m][n], 0, 0, 0);
+      if constexpr (kt + WD < 8) {  // refill the slot just consumed
+#pragma unroll
+        for (int m = 0; m < MT; ++m) w2r[kt % WD][m] = w2frag(m, kt + WD);
+      }
+    });
+    // H2 = relu(Z2 + b2) rounded to bf16 (the stored-activation numerics of the reference
+    // path), kept in acc; head partials of rows 16n + l15
+    float hp[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int m = 0; m < MT; ++m) {
+      const float4 bb = *reinterpret_cast<const float4*>(&cst[1][u0 + 16 * m + 4 * g]);
+      const float4 ww = *reinterpret_cast<const float4*>(&cst[2][u0 + 16 * m + 4 * g]);
+      const float bv[4] = {bb.x, bb.y, bb.z, bb.w}, wv[4] = {ww.x, ww.y, ww.z, ww.w};
+#pragma unroll
+      for (int n = 0; n < 4; ++n)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float v = bf2f(f2bf(fmaxf(acc[m][n][r] + bv[r], 0.f)));
+          acc[m][n][r] = v;
+          hp[n] += v * wv[r];
+        }
+    }
+#pragma unroll
+    for (int n = 0; n < 4; ++n) {
+      hp[n] += __shfl_xor(hp[n], 16, 64);
+      hp[n] += __shfl_xor(hp[n], 32, 64);
+    }
+    if (g == 0) {
+#pragma unroll
+      for (int n = 0; n < 4; ++n) hred[16 * n + l15][wid] = hp[n];
+    }
+    __syncthreads();  // B3: head partials complete
+
+    // ---- prediction, dy, loss of rows 16n + l15 (every wave needs dy); wave 0 lane group g
+    // owns row 16g + l15's outputs
+    float dyn[4];
+#pragma unroll
+    for (int n = 0; n < 4; ++n) {
+      const int r = 16 * n + l15, gr = row0 + r;
+      const float4 pa = *reinterpret_cast<const float4*>(&hred[r][0]);
+      const float4 pb = *reinterpret_cast<const float4*>(&hred[r][4]);
+      const float p = ((pa.x + pa.y) + (pa.z + pa.w)) + ((pb.x + pb.y) + (pb.z + pb.w)) + bias3;
+      dyn[n] = 0.f;
+      if (gr < B) {
+        const float diff = p - ys[par][r];
+        dyn[n] = dy_scale * diff;
+        if (wid == 0 && g == n) {
+          if (pred != nullptr) pred[gr] = p;
+          lsum += diff * diff;
+          db3a += dyn[n];
+        }
+      }
+    }
+    // ---- dZ2 = dy w3^T * [H2 > 0] (own units) -> zs; dw3, db2 partials (fp32, pre-rounding)
+#pragma unroll
+    for (int m = 0; m < MT; ++m) {
+      const float4 ww = *reinterpret_cast<const float4*>(&cst[2][u0 + 16 * m + 4 * g]);
+      const float wv[4] = {ww.x, ww.y, ww.z, ww.w};
+      float s3[4] = {0.f, 0.f, 0.f, 0.f}, s2[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int n = 0; n < 4; ++n) {
+        float t[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          s3[r] += acc[m][n][r] * dyn[n];
+          t[r] = acc[m][n][r] > 0.f ? dyn[n] : 0.f;
+          s2[r] += t[r];
+        }
+        *reinterpret_cast<uint2*>(zs + tile_off(16 * n + l15, u0 + 16 * m + 4 * g)) =
+            make_uint2(pk_bf16(t[0] * wv[0], t[1] * wv[1]), pk_bf16(t[2] * wv[2], t[3] * wv[3]));
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        atomicAdd(&part[wid][P_DW3][4 * m + r][lane], s3[r]);
+        atomicAdd(&part[wid][P_DB2][4 * m + r][lane], s2[r]);
+      }
+    }
+    __syncthreads();  // B4: dZ2 complete
+
+    // ---- dZ2 copy-out: 16-B row segments, thread t always chunk t & 31 (coalesced 512-B rows)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int r = (tid >> 5) + 16 * i, c = tid & 31;
+      if (row0 + r < B)
+        *reinterpret_cast<uint4*>(dZ2 + (size_t)(row0 + r) * MF_H + 8 * c) =
+            *reinterpret_cast<const uint4*>(zs + tile_off(r, 8 * c));
+    }
+    // ---- dH1^T (own units k, K = 256 output units) = W2^T dZ2^T
+#pragma unroll
+    for (int m = 0; m < MT; ++m)
+#pragma unroll
+      for (int n = 0; n < 4; ++n) acc[m][n] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int kt = 0; kt < 8; ++kt) {
+      bf16x8 zb[4];
+#pragma unroll
+      for (int n = 0; n < 4; ++n) zb[n] = *reinterpret_cast<const bf16x8*>(zs + tile_off(16 * n + l15, 32 * kt + 8 * g));
+#pragma unroll
+      for (int m = 0; m < MT; ++m)
+#pragma unroll
+        for (int n = 0; n < 4; ++n)
+          acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wt[m][kt], zb[n], acc[m][n], 0, 0, 0);
+    }
+    // ---- dZ1 = dH1 * [H1 > 0] over the same 8 bytes of h1s; db1 partials
+#pragma unroll
+    for (int m = 0; m < MT; ++m) {
+      float s1[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int n = 0; n < 4; ++n) {
+        const int r = 16 * n + l15;
+        uint2* pp = reinterpret_cast<uint2*>(h1s + tile_off(r, u0 + 16 * m + 4 * g));
+        const uint2 hv = *pp;
+        const bool rok = row0 + r < B;
+        const int hw2[2] = {rok ? (int)hv.x : 0, rok ? (int)hv.y : 0};
+        unsigned ow[2];
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+          // H1 >= 0 (relu): H1 > 0 <=> the bf16 half is > 0 as a signed 16-bit integer
+          const bool on0 = (hw2[q] << 16) > 0, on1 = hw2[q] > 0xFFFF;
+          const float t0 = on0 ? acc[m][n][2 * q] : 0.f, t1 = on1 ? acc[m][n][2 * q + 1] : 0.f;
+          s1[2 * q] += t0;
+          s1[2 * q + 1] += t1;
+          ow[q] = pk_bf16(t0, t1);
+        }
+        *pp = make_uint2(ow[0], ow[1]);
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) atomicAdd(&part[wid][P_DB1][4 * m + r][lane], s1[r]);
+    }
+    // the dW1 fragments read other lanes' dZ1 (same wave): complete the writes first
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
+    // ---- dW1^T slice (32 units x Fp) += dZ1^T X over the chunk's rows
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      bf16x8 af[MT], bfr[NFT];
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int r = 32 * kk + 8 * g + 4 * h + tq;
+#pragma unroll
+        for (int m = 0; m < MT; ++m) {
+          const bf16x4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_bf16x4*)(h1s + tile_off(r, u0 + 16 * m + 4 * tp)));
+#pragma unroll
+          for (int e = 0; e < 4; ++e) af[m][4 * h + e] = v[e];
+        }
+#pragma unroll
+        for (int f = 0; f < NFT; ++f) {
+          const int f0 = 16 * f + 4 * tp;
+          const bf16x4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+              (lds_bf16x4*)(xt + xtile_off(r, f0 >> 3) + ((f0 & 7) << 1)));
+#pragma unroll
+          for (int e = 0; e < 4; ++e) bfr[f][4 * h + e] = v[e];
+        }
+      }
+#pragma unroll
+      for (int m = 0; m < MT; ++m)
+#pragma unroll
+        for (int f = 0; f < NFT; ++f)
+          dw1a[m][f] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[m], bfr[f], dw1a[m][f], 0, 0, 0);
+    }
+    // h1s columns are rewritten by this wave's next layer 1: its dW1 reads must be complete
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
+  }
+
+  // ---- batch sums -> copy blockIdx % kMlpRedCopies of the scratch; dW1 -> this workgroup's row
+  float* rb = red + (blockIdx.x & (kMlpRedCopies - 1)) * kMlpRedRow;
+  float* slab = red + kMlpRedSlabOff + (size_t)blockIdx.x * kMlpRedSlabRow;
+  const float tl = block_sum<512>(lsum, lred);
+  if (tid == 0 && tl != 0.f) atomicAdd(rb + kMlpRedLoss, tl);
+  const float t3 = block_sum<512>(db3a, lred);
+  if (tid == 0 && t3 != 0.f) atomicAdd(rb + kMlpRedDb3, t3);
+#pragma unroll
+  for (int m = 0; m < MT; ++m)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int u = u0 + 16 * m + 4 * g + r;
+      float v[3] = {part[wid][P_DW3][4 * m + r][lane], part[wid][P_DB1][4 * m + r][lane],
+                    part[wid][P_DB2][4 * m + r][lane] * cst[2][u]};
+#pragma unroll
+      for (int k = 0; k < 3; ++k) {
+        v[k] += __shfl_xor(v[k], 1, 64);
+        v[k] += __shfl_xor(v[k], 2, 64);
+        v[k] += __shfl_xor(v[k], 4, 64);
+        v[k] += __shfl_xor(v[k], 8, 64);
+      }
+      if (l15 == 0) {
+        if (v[0] != 0.f) atomicAdd(rb + kMlpRedDw3 + u, v[0]);
+        if (v[1] != 0.f) atomicAdd(rb + kMlpRedDb1 + u, v[1]);
+        if (v[2] != 0.f) atomicAdd(rb + kMlpRedDb2 + u, v[2]);
+      }
+    }
+#pragma unroll
+  for (int m = 0; m < MT; ++m)
+#pragma unroll
+    for (int f = 0; f < NFT; ++f) {
+      const int ft = l15 + 16 * f;
+      if (ft < Fp)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) slab[(u0 + 16 * m + 4 * g + i) * Fp + ft] = dw1a[m][f][i];
+    }
+}
+}  // namespace
+
+bool launch_mlp2_step(const bf16_t* X, int Fp, const bf16_t* W1, const float* b1, const bf16_t* W2, const float* b2,
+                      const float* w3, const float* b3, const float* y, float dy_scale, int B, const long long* rows,
+                      long nrows, bf16_t* dZ2, float* pred, float* red, hipStream_t s) {
+  // the reduce sums the dW1 rows only when it expects the 8-wave backward's layout
+  if (B <= 0 || Fp > 32 || Fp % 8 != 0 || red == nullptr || !mlp_bwd8()) return false;
+  const int grid = mlp2_train_grid(B);  // the dW1 rows mlp2_reduce sums
+  if (Fp <= 16)
+    hipLaunchKernelGGL(mlp2_step_kernel<1>, dim3(grid), dim3(512), 0, s, X, Fp, W1, b1, W2, b2, w3, b3, y, dy_scale, B,
+                       rows, nrows, dZ2, pred, red);
+  else
+    hipLaunchKernelGGL(mlp2_step_kernel<2>, dim3(grid), dim3(512), 0, s, X, Fp, W1, b1, W2, b2, w3, b3, y, dy_scale, B,
+                       rows, nrows, dZ2, pred, red);
+  return true;
+}
+
+}  // namespace wf

@@ -189,6 +189,9 @@ class NativeMLP:
         # mlp2_reduce_kernel): 16 scratch copies instead of 256 same-address atomic adders per
         # gradient entry, summed by one small launch (WELLFLOW_MLP_SPREAD=0: direct atomics)
         spread = os.environ.get("WELLFLOW_MLP_SPREAD", "1") != "0"
+        # forward + backward of the training step in ONE launch (csrc/mlp_step.hip) instead of
+        # the fused forward + fused backward pair (WELLFLOW_MLP_STEP=0: the pair)
+        self.step_fused = os.environ.get("WELLFLOW_MLP_STEP", "1") != "0"
         self.red = (torch.zeros(MLP_RED_FLOATS, device=dev)
                     if spread and self.hidden == (256, 256) and self.Fp <= 32 else None)
         self.sync_weights()
@@ -214,6 +217,14 @@ class NativeMLP:
         self._Xop = Xop
         red = self.red
         try:
+            if red is not None and self.step_fused and not self.dw2_gemm:
+                if not C.mlp2_step(Xop, self.Fp, wl[0][0], pl[0][1], wl[1][0], pl[1][1], hw, hb, y,
+                                   2.0 * float(grad_scale), B, rows, self.dZ[1], self.pred, red):
+                    raise RuntimeError("NativeMLP: fused step refused the shape")
+                if not C.mlp2_dw2(self.dZ[1], Xop, self.Fp, rows, wl[0][0], pl[0][1], B, self.dw2_split, gl[1][0], red):
+                    raise RuntimeError("NativeMLP: dW2 kernel refused the shape")
+                C.mlp2_reduce(red, self.Fp, B, ls, ghb, ghw, gl[0][1], gl[1][1], gl[0][0], gl[1][0])
+                return ls
             if not self._fused_forward(B, y, self.dy, ls, 2.0 * float(grad_scale), (ghw, ghb),
                                        store_h1=self.dw2_gemm, rows=rows, red=red):
                 raise RuntimeError("NativeMLP: fused forward refused the recompute step")

@@ -3,6 +3,11 @@
 set -o pipefail
 export TMPDIR=/tmp
 mkdir -p gpurun_out/r4
+for a in "1 527 8" "0 528 8" "4 528 8" "1 528 8"; do
+  timeout -k 10 60 tools/memset_repro.bin $a >> gpurun_out/r4/memset_repro.log 2>&1; r=$?
+  [ $r -le 1 ] || { echo "memset repro rc=$r"; exit $r; }
+done
+grep RESULT gpurun_out/r4/memset_repro.log
 timeout -k 10 1000 python -u -m pytest tests -x -v -m gpu --timeout 300 --timeout-method thread \
   > gpurun_out/r4/s2_tests.log 2>&1; rc=$?
 grep -E "passed|failed|error" gpurun_out/r4/s2_tests.log | tail -3

@@ -372,3 +372,39 @@ def test_mlp_row_indexed_step_matches_gathered_batch():
     assert torch.equal(pa, eng.pred[:B])
     assert abs(ls_a - ls_b) <= 1e-5 * abs(ls_a)
     assert ((ga - eng.grads).norm() / ga.norm()).item() < 1e-4
+
+
+@pytest.mark.parametrize("B,F,indexed", [(262144, 16, False), (4096, 32, False), (16384, 16, True), (128, 8, False)])
+def test_mlp_one_launch_step_matches_two_kernel_step(B, F, indexed):
+    """The training step's forward + backward in ONE launch (csrc/mlp_step.hip: X staged once,
+    layer 1 computed once, H2 and dy never leave the workgroup) against the fused forward +
+    fused backward pair (csrc/mlp_fused.hip) it replaces: same predictions, loss and gradients
+    up to the fp32 summation order; both use the spread scratch, which must be left zeroed."""
+    from wellflow.data.synth import synth_tabular_batch
+    from wellflow.models.mlp import MLP_RED_COPY_FLOATS, NativeMLP, init_mlp_flat
+
+    eng = NativeMLP(F, (256, 256), B, device=DEV)
+    eng.params.copy_(init_mlp_flat(F, (256, 256), seed=21).to(DEV))
+    eng.sync_weights()
+    N = 3 * B if indexed else B
+    X, Y = synth_tabular_batch(N, F, seed=22)
+    X, Y = X.to(DEV), Y.to(DEV)
+    idx = torch.randperm(N, device=DEV)[:B] if indexed else None
+    if indexed:
+        X = X.to(torch.bfloat16)
+    out = {}
+    for fused in (False, True):
+        eng.step_fused = fused
+        eng.dZ[1].fill_(float("nan"))
+        ls = eng.forward_backward(X, Y, grad_scale=1.0 / B, rows=idx).item()
+        torch.cuda.synchronize()
+        out[fused] = (ls, eng.pred[:B].clone(), eng.grads.clone(), eng.dZ[1][: B * 256].clone())
+        assert eng.red[:MLP_RED_COPY_FLOATS].abs().max().item() == 0.0
+    (la, pa, ga, za), (lb, pb, gb, zb) = out[False], out[True]
+    assert eng._recompute_ok(B)
+    torch.testing.assert_close(pa, pb, rtol=1e-5, atol=1e-6)
+    assert abs(la - lb) <= 1e-5 * abs(la) + 1e-7
+    assert torch.isfinite(gb).all()
+    # dZ2 (dW2's operand) is bit-identical: same H2 rounding, same dy, same bf16 product
+    assert torch.equal(za, zb)
+    assert ((ga - gb).norm() / ga.norm()).item() < 1e-5
