@@ -123,7 +123,13 @@ void launch_mlp2_reduce(float* red, int Fp, int B, float* loss_sum, float* db3, 
 // which launch_mlp2_reduce then adds to the gradients. Fp <= 32; false = not covered.
 bool launch_mlp2_step(const bf16_t* X, int Fp, const bf16_t* W1, const float* b1, const bf16_t* W2, const float* b2,
                       const float* w3, const float* b3, const float* y, float dy_scale, int B, const long long* rows,
-                      long nrows, bf16_t* dZ2, float* pred, float* red, hipStream_t s);
+                      long nrows, bf16_t* dZ2, float* pred, float* red, bool dz_frag, hipStream_t s);
+// dz_frag: dZ2 is written in the fragment layout of launch_mlp2_dw2f (B % 64 == 0) instead of
+// [B][256]: fragment (S, b) of rows 32S .. 32S + 31 x units 16b .. 16b + 15 at element
+// (S * 16 + b) * 512, lane (l15, g) = 16 B = rows 32S + 8g .. + 7 of unit 16b + l15.
+// dW2 from that layout without LDS (mlp_step.hip mlp2_dw2f_kernel) into the scratch's dW2 copies.
+bool launch_mlp2_dw2f(const bf16_t* dZ2F, const bf16_t* X, int Fp, const long long* rows, long nrows, const bf16_t* W1,
+                      const float* b1, int B, int nsplit, float* red, hipStream_t s);
 
 // ---- fused reference CNN (cnn_fused.hip): Conv1D(C -> Fp, width taps / C) + ReLU + dropout ->
 // Dense(T * Fp -> O) -> loss, cnn.py:110-118. Flat layout = models/cnn.py CnnLayout:

@@ -18,6 +18,9 @@
 // H1 complete, head partials complete, dZ2 complete). Batch sums go to the spread-reduction
 // scratch exactly as the two kernels' did (kMlpRedCopies copies + the per-workgroup dW1 rows),
 // so mlp2_dw2 and mlp2_reduce run unchanged after it.
+#include <cstdlib>
+#include <type_traits>
+
 #include "common.h"
 #include "gemm_core.h"
 #include "kernels.h"
@@ -26,7 +29,8 @@
 namespace wf {
 
 namespace {
-template <int NFT>  // 16-feature tiles of dW1: 1 (Fp <= 16) or 2 (Fp <= 32)
+// FRAG: dZ2 leaves in the MFMA-fragment layout of mlp2_dw2f_kernel (below) instead of [B][256]
+template <int NFT, bool FRAG>  // NFT: 16-feature tiles of dW1: 1 (Fp <= 16) or 2 (Fp <= 32)
 __global__ __launch_bounds__(512, 1) void mlp2_step_kernel(
     const bf16_t* __restrict__ X, int Fp, const bf16_t* __restrict__ W1, const float* __restrict__ b1,
     const bf16_t* __restrict__ W2, const float* __restrict__ b2, const float* __restrict__ w3,
@@ -228,13 +232,33 @@ __global__ __launch_bounds__(512, 1) void mlp2_step_kernel(
     }
     __syncthreads();  // B4: dZ2 complete
 
-    // ---- dZ2 copy-out: 16-B row segments, thread t always chunk t & 31 (coalesced 512-B rows)
+    if constexpr (FRAG) {
+      // ---- dZ2 copy-out as dW2 A fragments: fragment (s, b) = 32 rows x 16 units, lane
+      // (l15, g) 16 B = rows 32s + 8g .. + 7 of unit 16b + l15 (two ds_read_b64_tr_b16); wave w
+      // writes fragments 4w .. 4w + 3, one coalesced 1-KiB store each (B % 64 == 0)
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int r = (tid >> 5) + 16 * i, c = tid & 31;
-      if (row0 + r < B)
-        *reinterpret_cast<uint4*>(dZ2 + (size_t)(row0 + r) * MF_H + 8 * c) =
-            *reinterpret_cast<const uint4*>(zs + tile_off(r, 8 * c));
+      for (int q = 0; q < 4; ++q) {
+        const int f = 4 * wid + q, sst = f >> 4, b = f & 15;
+        bf16x8 v;
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const bf16x4 t = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+              (lds_bf16x4*)(zs + tile_off(32 * sst + 8 * g + 4 * h + tq, 16 * b + 4 * tp)));
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[4 * h + e] = t[e];
+        }
+        const size_t S = (size_t)(row0 >> 5) + sst;
+        *reinterpret_cast<bf16x8*>(dZ2 + ((S * 16 + b) * 64 + lane) * 8) = v;
+      }
+    } else {
+      // ---- dZ2 copy-out: 16-B row segments, thread t always chunk t & 31 (coalesced 512-B rows)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int r = (tid >> 5) + 16 * i, c = tid & 31;
+        if (row0 + r < B)
+          *reinterpret_cast<uint4*>(dZ2 + (size_t)(row0 + r) * MF_H + 8 * c) =
+              *reinterpret_cast<const uint4*>(zs + tile_off(r, 8 * c));
+      }
     }
     // ---- dH1^T (own units k, K = 256 output units) = W2^T dZ2^T
 #pragma unroll
@@ -351,20 +375,153 @@ __global__ __launch_bounds__(512, 1) void mlp2_step_kernel(
         for (int i = 0; i < 4; ++i) slab[(u0 + 16 * m + 4 * g + i) * Fp + ft] = dw1a[m][f][i];
     }
 }
+
+// ----------------------------------------------------------------------------------------
+// dW2 [256 out][256 in] += dZ2^T H1, H1 = relu(X W1^T + b1) recomputed, WITHOUT LDS: dZ2 arrives
+// in the fragment layout written by mlp2_step_kernel<., true> (fragment (S, b) = rows
+// 32S .. 32S + 31 x units 16b .. 16b + 15, 1 KiB, lane (l15, g) = rows 32S + 8g + j of unit
+// 16b + l15), so every A operand is ONE coalesced 16-B load per lane. H1 is recomputed
+// straight into the B-operand layout: the recompute MFMA's A operand (X rows) takes its 16
+// rows in the order 8(i >> 2) + 4h + (i & 3), so output lane (l15, g) holds rows 8g + 4h + r
+// of unit l15 — exactly the K = rows slots of the dW MFMA's B fragment; no transpose, no LDS
+// round trip (the LDS-staged mlp2_dw2_kernel spent its time on H1-image writes and fragment
+// reads: 16 % bank conflicts, ~1.7k LDS cycles per chunk against 512 MFMA cycles).
+//  * workgroup = 256 (out) x 128 (in) tile of one row range; 8 waves of 64 x 64 (wave w:
+//    out rows 64 (w >> 1), in columns 128 t + 64 (w & 1)); per 32-row step a wave runs 8
+//    recompute + 16 dW MFMAs (16x16x32).
+//  * grid = 2 tiles x nsplit row ranges; xcd_remap keeps a range's two tiles on one XCD, so
+//    the second reader of each dZ2 fragment hits L2.
+//  * dataset row ids of the range (rows != nullptr) go to LDS once (a per-step global index
+//    load would sit in front of every X load).
+//  * the next step's fragments are loaded while this step's MFMAs run (register double buffer).
+constexpr int DW2F_MAX_ROWS = 8192;
+__global__ __launch_bounds__(512, 1) void mlp2_dw2f_kernel(const bf16_t* __restrict__ dZ2F, const bf16_t* __restrict__ X,
+                                                           int Fp, const long long* __restrict__ rows, long nrows,
+                                                           const bf16_t* __restrict__ W1, const float* __restrict__ b1,
+                                                           int kchunk, float* __restrict__ dW2) {
+  __shared__ int ridx[DW2F_MAX_ROWS];
+  const int tid = threadIdx.x, lane = tid & 63, l15 = lane & 15, g = lane >> 4;
+  const int wid = tid >> 6, wm = wid >> 1;
+  const int L = xcd_remap(blockIdx.x, gridDim.x);
+  const int split = L >> 1, t = L & 1;
+  const int n0 = 128 * t + 64 * (wid & 1);  // in units (H1) of this wave
+  const int kbeg = split * kchunk, nsteps = kchunk / 32;
+  if (rows != nullptr) {
+    for (int i = tid; i < kchunk; i += 512) ridx[i] = (int)data_row(rows, kbeg + i, nrows);
+    __syncthreads();
+  }
+  // recompute operands: W1 rows of the wave's 64 in units (K = features 8g .. 8g + 7; zero past Fp)
+  bf16x8 w1f[4];
+  float bias[4];
+#pragma unroll
+  for (int nb = 0; nb < 4; ++nb) {
+    const int u = n0 + 16 * nb + l15;
+    w1f[nb] = 8 * g + 8 <= Fp ? *reinterpret_cast<const bf16x8*>(W1 + (size_t)u * Fp + 8 * g)
+                              : bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
+    bias[nb] = b1[u];
+  }
+  // X fragment of this lane: row slot i = l15 -> local row 8 (l15 >> 2) + 4h + (l15 & 3) of
+  // the step; feature chunk g (past Fp: chunk 0 of the same row — finite values times zero W1)
+  const int xg = 8 * g + 8 <= Fp ? g : 0;
+  const int xr0 = 8 * (l15 >> 2) + (l15 & 3);
+  auto xfrag = [&](int st, int h) {
+    const int lr = 32 * st + xr0 + 4 * h;  // row within the range
+    const size_t dr = rows != nullptr ? (size_t)ridx[lr] : (size_t)(kbeg + lr);
+    return *reinterpret_cast<const bf16x8*>(X + dr * Fp + 8 * xg);
+  };
+  // dZ2 fragment (step st of the range, out block 4 wm + mb)
+  const bf16_t* zbase = dZ2F + ((size_t)(kbeg >> 5) * 16 + 4 * wm) * 512 + lane * 8;
+  auto afrag = [&](int st, int mb) { return *reinterpret_cast<const bf16x8*>(zbase + ((size_t)st * 16 + mb) * 512); };
+
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  // ring of FD register buffers: step st + FD - 1 is requested while step st computes (HBM
+  // latency under load is several steps' worth of MFMA time)
+  constexpr int FD = 4;
+  bf16x8 a[FD][4], xf[FD][2];
+  auto fetch = [&](int st, int p) {
+#pragma unroll
+    for (int mb = 0; mb < 4; ++mb) a[p][mb] = afrag(st, mb);
+    xf[p][0] = xfrag(st, 0);
+    xf[p][1] = xfrag(st, 1);
+  };
+  static_for<0, FD - 1>([&](auto pc) {
+    if (decltype(pc)::value < nsteps) fetch(decltype(pc)::value, decltype(pc)::value);
+  });
+  auto body = [&](int st, auto pc) {
+    constexpr int P = decltype(pc)::value;  // register buffer of step st (== st % FD)
+    if (st + FD - 1 < nsteps) fetch(st + FD - 1, (P + FD - 1) % FD);
+    bf16x8 hb[4];
+#pragma unroll
+    for (int nb = 0; nb < 4; ++nb) {
+      const f32x4 c0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xf[P][0], w1f[nb], f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+      const f32x4 c1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xf[P][1], w1f[nb], f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+      const unsigned p0 = pk_bf16(fmaxf(c0[0] + bias[nb], 0.f), fmaxf(c0[1] + bias[nb], 0.f));
+      const unsigned p1 = pk_bf16(fmaxf(c0[2] + bias[nb], 0.f), fmaxf(c0[3] + bias[nb], 0.f));
+      const unsigned p2 = pk_bf16(fmaxf(c1[0] + bias[nb], 0.f), fmaxf(c1[1] + bias[nb], 0.f));
+      const unsigned p3 = pk_bf16(fmaxf(c1[2] + bias[nb], 0.f), fmaxf(c1[3] + bias[nb], 0.f));
+      typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
+      hb[nb] = __builtin_bit_cast(bf16x8, (u32x4_t{p0, p1, p2, p3}));
+    }
+#pragma unroll
+    for (int mb = 0; mb < 4; ++mb)
+#pragma unroll
+      for (int nb = 0; nb < 4; ++nb)
+        acc[mb][nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[P][mb], hb[nb], acc[mb][nb], 0, 0, 0);
+  };
+  int st = 0;
+  for (; st + FD <= nsteps; st += FD) static_for<0, FD>([&](auto pc) { body(st + decltype(pc)::value, pc); });
+  static_for<0, FD - 1>([&](auto pc) {
+    if (st + decltype(pc)::value < nsteps) body(st + decltype(pc)::value, pc);
+  });
+  // out unit 64 wm + 16 mb + 4g + r, in unit n0 + 16 nb + l15
+  float* dst = dW2 + (size_t)(split & (kMlpRedCopies2 - 1)) * 65536;
+#pragma unroll
+  for (int mb = 0; mb < 4; ++mb)
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+      for (int nb = 0; nb < 4; ++nb)
+        atomicAdd(dst + (size_t)(64 * wm + 16 * mb + 4 * g + r) * MF_H + n0 + 16 * nb + l15, acc[mb][nb][r]);
+}
 }  // namespace
 
 bool launch_mlp2_step(const bf16_t* X, int Fp, const bf16_t* W1, const float* b1, const bf16_t* W2, const float* b2,
                       const float* w3, const float* b3, const float* y, float dy_scale, int B, const long long* rows,
-                      long nrows, bf16_t* dZ2, float* pred, float* red, hipStream_t s) {
+                      long nrows, bf16_t* dZ2, float* pred, float* red, bool dz_frag, hipStream_t s) {
   // the reduce sums the dW1 rows only when it expects the 8-wave backward's layout
   if (B <= 0 || Fp > 32 || Fp % 8 != 0 || red == nullptr || !mlp_bwd8()) return false;
+  if (dz_frag && B % MF_ROWS != 0) return false;
   const int grid = mlp2_train_grid(B);  // the dW1 rows mlp2_reduce sums
-  if (Fp <= 16)
-    hipLaunchKernelGGL(mlp2_step_kernel<1>, dim3(grid), dim3(512), 0, s, X, Fp, W1, b1, W2, b2, w3, b3, y, dy_scale, B,
-                       rows, nrows, dZ2, pred, red);
-  else
-    hipLaunchKernelGGL(mlp2_step_kernel<2>, dim3(grid), dim3(512), 0, s, X, Fp, W1, b1, W2, b2, w3, b3, y, dy_scale, B,
-                       rows, nrows, dZ2, pred, red);
+#define WF_STEP(NFT, FR)                                                                                            \
+  hipLaunchKernelGGL((mlp2_step_kernel<NFT, FR>), dim3(grid), dim3(512), 0, s, X, Fp, W1, b1, W2, b2, w3, b3, y, \
+                     dy_scale, B, rows, nrows, dZ2, pred, red)
+  if (Fp <= 16) {
+    if (dz_frag) WF_STEP(1, true); else WF_STEP(1, false);
+  } else {
+    if (dz_frag) WF_STEP(2, true); else WF_STEP(2, false);
+  }
+#undef WF_STEP
+  return true;
+}
+
+// dW2 (the spread scratch's dW2 copies: red + kMlpRedCopies * kMlpRedRow) from the fragment-
+// layout dZ2; B % 64 == 0, Fp <= 32. nsplit row ranges (<= 128: two tiles per range, one
+// workgroup per CU). False = not covered.
+bool launch_mlp2_dw2f(const bf16_t* dZ2F, const bf16_t* X, int Fp, const long long* rows, long nrows, const bf16_t* W1,
+                      const float* b1, int B, int nsplit, float* red, hipStream_t s) {
+  if (B <= 0 || B % MF_ROWS != 0 || Fp > 32 || Fp % 8 != 0 || red == nullptr) return false;
+  const int chunks = B / MF_ROWS;
+  if (nsplit < 1) nsplit = 1;
+  if (nsplit > 128) nsplit = 128;
+  while (nsplit > 1 && chunks % nsplit != 0) --nsplit;
+  const int kchunk = (chunks / nsplit) * MF_ROWS;
+  if (rows != nullptr && kchunk > DW2F_MAX_ROWS) return false;
+  hipLaunchKernelGGL(mlp2_dw2f_kernel, dim3(2 * nsplit), dim3(512), 0, s, dZ2F, X, Fp, rows, nrows, W1, b1, kchunk,
+                     red + (size_t)kMlpRedCopies * kMlpRedRow);
   return true;
 }
 

@@ -192,6 +192,10 @@ class NativeMLP:
         # forward + backward of the training step in ONE launch (csrc/mlp_step.hip) instead of
         # the fused forward + fused backward pair (WELLFLOW_MLP_STEP=0: the pair)
         self.step_fused = os.environ.get("WELLFLOW_MLP_STEP", "1") != "0"
+        # ... writing dZ2 in the dW2 kernel's MFMA-fragment layout, read by the LDS-free dW2 kernel
+        # (csrc/mlp_step.hip mlp2_dw2f_kernel; WELLFLOW_MLP_DW2F=0: row-major dZ2 + mlp2_dw2)
+        self.dw2_frag = os.environ.get("WELLFLOW_MLP_DW2F", "1") != "0"
+        self.dw2f_split = int(os.environ.get("WELLFLOW_MLP_DW2F_SPLIT", "128"))
         self.red = (torch.zeros(MLP_RED_FLOATS, device=dev)
                     if spread and self.hidden == (256, 256) and self.Fp <= 32 else None)
         self.sync_weights()
@@ -218,10 +222,14 @@ class NativeMLP:
         red = self.red
         try:
             if red is not None and self.step_fused and not self.dw2_gemm:
+                frag = self.dw2_frag
                 if not C.mlp2_step(Xop, self.Fp, wl[0][0], pl[0][1], wl[1][0], pl[1][1], hw, hb, y,
-                                   2.0 * float(grad_scale), B, rows, self.dZ[1], self.pred, red):
+                                   2.0 * float(grad_scale), B, rows, self.dZ[1], self.pred, red, frag):
                     raise RuntimeError("NativeMLP: fused step refused the shape")
-                if not C.mlp2_dw2(self.dZ[1], Xop, self.Fp, rows, wl[0][0], pl[0][1], B, self.dw2_split, gl[1][0], red):
+                ok = (C.mlp2_dw2f(self.dZ[1], Xop, self.Fp, rows, wl[0][0], pl[0][1], B, self.dw2f_split, red) if frag
+                      else C.mlp2_dw2(self.dZ[1], Xop, self.Fp, rows, wl[0][0], pl[0][1], B, self.dw2_split, gl[1][0],
+                                      red))
+                if not ok:
                     raise RuntimeError("NativeMLP: dW2 kernel refused the shape")
                 C.mlp2_reduce(red, self.Fp, B, ls, ghb, ghw, gl[0][1], gl[1][1], gl[0][0], gl[1][0])
                 return ls

@@ -374,12 +374,20 @@ def test_mlp_row_indexed_step_matches_gathered_batch():
     assert ((ga - eng.grads).norm() / ga.norm()).item() < 1e-4
 
 
+def _dz2_from_frag(zf: torch.Tensor, B: int) -> torch.Tensor:
+    """[B][256] view of a dZ2 written in the fragment layout (csrc/kernels.h launch_mlp2_step):
+    element ((S * 16 + b) * 64 + 16 g + l) * 8 + j = row 32 S + 8 g + j, unit 16 b + l."""
+    return zf[: B * 256].view(B // 32, 16, 4, 16, 8).permute(0, 2, 4, 1, 3).reshape(B, 256)
+
+
 @pytest.mark.parametrize("B,F,indexed", [(262144, 16, False), (4096, 32, False), (16384, 16, True), (128, 8, False)])
 def test_mlp_one_launch_step_matches_two_kernel_step(B, F, indexed):
     """The training step's forward + backward in ONE launch (csrc/mlp_step.hip: X staged once,
-    layer 1 computed once, H2 and dy never leave the workgroup) against the fused forward +
-    fused backward pair (csrc/mlp_fused.hip) it replaces: same predictions, loss and gradients
-    up to the fp32 summation order; both use the spread scratch, which must be left zeroed."""
+    layer 1 computed once, H2 and dy never leave the workgroup), with dZ2 row-major + the
+    LDS-staged dW2 kernel and with dZ2 in the fragment layout + the LDS-free dW2 kernel, against
+    the fused forward + fused backward pair (csrc/mlp_fused.hip) it replaces: same predictions,
+    loss and gradients up to the fp32 summation order, bit-identical dZ2; the spread scratch
+    must be left zeroed."""
     from wellflow.data.synth import synth_tabular_batch
     from wellflow.models.mlp import MLP_RED_COPY_FLOATS, NativeMLP, init_mlp_flat
 
@@ -393,18 +401,21 @@ def test_mlp_one_launch_step_matches_two_kernel_step(B, F, indexed):
     if indexed:
         X = X.to(torch.bfloat16)
     out = {}
-    for fused in (False, True):
-        eng.step_fused = fused
+    for name, fused, frag in (("pair", False, False), ("step", True, False), ("step_frag", True, True)):
+        eng.step_fused, eng.dw2_frag = fused, frag
         eng.dZ[1].fill_(float("nan"))
         ls = eng.forward_backward(X, Y, grad_scale=1.0 / B, rows=idx).item()
         torch.cuda.synchronize()
-        out[fused] = (ls, eng.pred[:B].clone(), eng.grads.clone(), eng.dZ[1][: B * 256].clone())
-        assert eng.red[:MLP_RED_COPY_FLOATS].abs().max().item() == 0.0
-    (la, pa, ga, za), (lb, pb, gb, zb) = out[False], out[True]
+        z = _dz2_from_frag(eng.dZ[1], B) if frag else eng.dZ[1][: B * 256].view(B, 256)
+        out[name] = (ls, eng.pred[:B].clone(), eng.grads.clone(), z.clone())
+        assert eng.red[:MLP_RED_COPY_FLOATS].abs().max().item() == 0.0, name
     assert eng._recompute_ok(B)
-    torch.testing.assert_close(pa, pb, rtol=1e-5, atol=1e-6)
-    assert abs(la - lb) <= 1e-5 * abs(la) + 1e-7
-    assert torch.isfinite(gb).all()
-    # dZ2 (dW2's operand) is bit-identical: same H2 rounding, same dy, same bf16 product
-    assert torch.equal(za, zb)
-    assert ((ga - gb).norm() / ga.norm()).item() < 1e-5
+    la, pa, ga, za = out["pair"]
+    for name in ("step", "step_frag"):
+        lb, pb, gb, zb = out[name]
+        torch.testing.assert_close(pa, pb, rtol=1e-5, atol=1e-6)
+        assert abs(la - lb) <= 1e-5 * abs(la) + 1e-7, name
+        assert torch.isfinite(gb).all(), name
+        # dZ2 (dW2's operand) is bit-identical: same H2 rounding, same dy, same bf16 product
+        assert torch.equal(za, zb), name
+        assert ((ga - gb).norm() / ga.norm()).item() < 1e-5, name
