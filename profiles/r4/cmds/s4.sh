@@ -1,0 +1,8 @@
+# round 4, session 4: paired converged val-MSE parity at the job's default batch (batch 0 = auto)
+set -o pipefail
+export TMPDIR=/tmp
+mkdir -p gpurun_out/r4
+M=${MODEL:-mlp}; S=${SEEDS:-0,1,2,3,4}; TAG=${TAG:-a}
+timeout -k 10 ${TLIM:-1100} python -u tools/parity.py --model $M --seeds $S --batch 0 \
+  --out gpurun_out/r4/parity_${M}_${TAG}.json > gpurun_out/r4/parity_${M}_${TAG}.log 2>&1
+rc=$?; tail -12 gpurun_out/r4/parity_${M}_${TAG}.log | cut -c1-400; exit $rc
