@@ -71,8 +71,13 @@ __global__ __launch_bounds__(512, 1) void mlp2_step_kernel(
   // waves per SIMD
   constexpr int WD = 3;
   const int w2lane = (u0 + l15) * MF_H + 8 * g;  // element offset of the lane's m = 0 fragment
-  const bf16_t* w2c = W2;  // laundered per chunk (below): the loads must not be hoisted out of the loop
-  auto w2frag = [&](int m, int kt) { return *reinterpret_cast<const bf16x8*>(w2c + w2lane + 16 * MF_H * m + 32 * kt); };
+  // a zero laundered per chunk (below) keeps the loads inside the chunk loop (hoisted, they
+  // would pin 64 VGPRs); laundering the pointer itself would lose its global address space
+  // (flat loads: counted in lgkmcnt too, so every LDS wait would wait for them)
+  int w2z = 0;
+  auto w2frag = [&](int m, int kt) {
+    return *reinterpret_cast<const bf16x8*>(W2 + (w2z + w2lane + 16 * MF_H * m + 32 * kt));
+  };
   f32x4 dw1a[MT][NFT];
 #pragma unroll
   for (int m = 0; m < MT; ++m)
@@ -112,8 +117,8 @@ __global__ __launch_bounds__(512, 1) void mlp2_step_kernel(
 
     // ---- layer 1 (own units): H1 -> h1s; the first W2 fragments of layer 2 in flight
     bf16x8 w2r[WD][MT];
-    w2c = W2;
-    asm volatile("" : "+s"(w2c));
+    w2z = 0;
+    asm volatile("" : "+s"(w2z));
 #pragma unroll
     for (int k = 0; k < WD; ++k)
 #pragma unroll
@@ -406,10 +411,9 @@ __global__ __launch_bounds__(512, 1) void mlp2_dw2f_kernel(const bf16_t* __restr
   const int split = L >> 1, t = L & 1;
   const int n0 = 128 * t + 64 * (wid & 1);  // in units (H1) of this wave
   const int kbeg = split * kchunk, nsteps = kchunk / 32;
-  if (rows != nullptr) {
-    for (int i = tid; i < kchunk; i += 512) ridx[i] = (int)data_row(rows, kbeg + i, nrows);
-    __syncthreads();
-  }
+  // row ids of the range (identity without `rows`): the X loads below then never branch
+  for (int i = tid; i < kchunk; i += 512) ridx[i] = rows != nullptr ? (int)data_row(rows, kbeg + i, nrows) : kbeg + i;
+  __syncthreads();
   // recompute operands: W1 rows of the wave's 64 in units (K = features 8g .. 8g + 7; zero past Fp)
   bf16x8 w1f[4];
   float bias[4];
@@ -426,8 +430,7 @@ __global__ __launch_bounds__(512, 1) void mlp2_dw2f_kernel(const bf16_t* __restr
   const int xr0 = 8 * (l15 >> 2) + (l15 & 3);
   auto xfrag = [&](int st, int h) {
     const int lr = 32 * st + xr0 + 4 * h;  // row within the range
-    const size_t dr = rows != nullptr ? (size_t)ridx[lr] : (size_t)(kbeg + lr);
-    return *reinterpret_cast<const bf16x8*>(X + dr * Fp + 8 * xg);
+    return *reinterpret_cast<const bf16x8*>(X + (size_t)ridx[lr] * Fp + 8 * xg);
   };
   // dZ2 fragment (step st of the range, out block 4 wm + mb)
   const bf16_t* zbase = dZ2F + ((size_t)(kbeg >> 5) * 16 + 4 * wm) * 512 + lane * 8;
@@ -448,12 +451,13 @@ __global__ __launch_bounds__(512, 1) void mlp2_dw2f_kernel(const bf16_t* __restr
     xf[p][0] = xfrag(st, 0);
     xf[p][1] = xfrag(st, 1);
   };
-  static_for<0, FD - 1>([&](auto pc) {
-    if (decltype(pc)::value < nsteps) fetch(decltype(pc)::value, decltype(pc)::value);
-  });
+  // fetches past the range re-read its last step (valid memory, never used): no branches, so
+  // the compiler's vmcnt counting stays exact across the unrolled loop
+  const int last = nsteps - 1;
+  static_for<0, FD - 1>([&](auto pc) { fetch(min(decltype(pc)::value, last), decltype(pc)::value); });
   auto body = [&](int st, auto pc) {
     constexpr int P = decltype(pc)::value;  // register buffer of step st (== st % FD)
-    if (st + FD - 1 < nsteps) fetch(st + FD - 1, (P + FD - 1) % FD);
+    fetch(min(st + FD - 1, last), (P + FD - 1) % FD);
     bf16x8 hb[4];
 #pragma unroll
     for (int nb = 0; nb < 4; ++nb) {
