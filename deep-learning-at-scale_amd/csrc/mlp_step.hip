@@ -45,9 +45,11 @@ __global__ __launch_bounds__(512, 1) void mlp2_step_kernel(
   __shared__ __attribute__((aligned(16))) float cst[3][MF_H];            // b1, b2, w3
   __shared__ float ys[2][MF_ROWS];
   __shared__ float lred[NW];
-  // lane-private running sums of dw3, db1, db2 (slot [wave][sum][4m + r][lane]): 24 VGPRs
-  // cheaper in LDS (one ds_add per value per chunk) than in the register file
-  __shared__ __attribute__((aligned(16))) float part[NW][3][2 * 4][64];
+  // lane-private running sums of dw3, db1, db2 (float4 slot [wave][sum][m][lane] = r 0..3):
+  // 24 VGPRs cheaper in LDS than in the register file. Plain read-add-write of the lane's own
+  // 16 B (ds_read_b128 / ds_write_b128, conflict-free): LDS float atomics (ds_add_f32) made
+  // the LDS the bottleneck of the whole kernel (PMC: LDS busy 70 %, 30 cycles per LDS op)
+  __shared__ __attribute__((aligned(16))) float4 part[NW][3][2][64];
 
   const int tid = threadIdx.x, lane = tid & 63, l15 = lane & 15, g = lane >> 4;
   const int wid = tid >> 6;
@@ -83,7 +85,15 @@ __global__ __launch_bounds__(512, 1) void mlp2_step_kernel(
   for (int m = 0; m < MT; ++m)
 #pragma unroll
     for (int f = 0; f < NFT; ++f) dw1a[m][f] = f32x4{0.f, 0.f, 0.f, 0.f};
-  for (int k = 0; k < 3 * MT * 4; ++k) part[wid][k / (MT * 4)][k % (MT * 4)][lane] = 0.f;
+  for (int k = 0; k < 3 * MT; ++k) part[wid][k / MT][k % MT][lane] = make_float4(0.f, 0.f, 0.f, 0.f);
+  auto acc4 = [&](int P, int m, const float (&v)[4]) {
+    float4 a = part[wid][P][m][lane];
+    a.x += v[0];
+    a.y += v[1];
+    a.z += v[2];
+    a.w += v[3];
+    part[wid][P][m][lane] = a;
+  };
   constexpr int P_DW3 = 0, P_DB1 = 1, P_DB2 = 2;
   const float bias3 = b3[0];
   float lsum = 0.f, db3a = 0.f;
@@ -229,11 +239,8 @@ __global__ __launch_bounds__(512, 1) void mlp2_step_kernel(
         *reinterpret_cast<uint2*>(zs + tile_off(16 * n + l15, u0 + 16 * m + 4 * g)) =
             make_uint2(pk_bf16(t[0] * wv[0], t[1] * wv[1]), pk_bf16(t[2] * wv[2], t[3] * wv[3]));
       }
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        atomicAdd(&part[wid][P_DW3][4 * m + r][lane], s3[r]);
-        atomicAdd(&part[wid][P_DB2][4 * m + r][lane], s2[r]);
-      }
+      acc4(P_DW3, m, s3);
+      acc4(P_DB2, m, s2);
     }
     __syncthreads();  // B4: dZ2 complete
 
@@ -304,8 +311,7 @@ __global__ __launch_bounds__(512, 1) void mlp2_step_kernel(
         }
         *pp = make_uint2(ow[0], ow[1]);
       }
-#pragma unroll
-      for (int r = 0; r < 4; ++r) atomicAdd(&part[wid][P_DB1][4 * m + r][lane], s1[r]);
+      acc4(P_DB1, m, s1);
     }
     // the dW1 fragments read other lanes' dZ1 (same wave): complete the writes first
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -355,8 +361,10 @@ __global__ __launch_bounds__(512, 1) void mlp2_step_kernel(
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int u = u0 + 16 * m + 4 * g + r;
-      float v[3] = {part[wid][P_DW3][4 * m + r][lane], part[wid][P_DB1][4 * m + r][lane],
-                    part[wid][P_DB2][4 * m + r][lane] * cst[2][u]};
+      const float4 a3 = part[wid][P_DW3][m][lane], a1 = part[wid][P_DB1][m][lane], a2 = part[wid][P_DB2][m][lane];
+      const float pick3[4] = {a3.x, a3.y, a3.z, a3.w}, pick1[4] = {a1.x, a1.y, a1.z, a1.w},
+                  pick2[4] = {a2.x, a2.y, a2.z, a2.w};
+      float v[3] = {pick3[r], pick1[r], pick2[r] * cst[2][u]};
 #pragma unroll
       for (int k = 0; k < 3; ++k) {
         v[k] += __shfl_xor(v[k], 1, 64);
