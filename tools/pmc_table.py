@@ -16,6 +16,10 @@ import os
 import sys
 
 
+def _short(name: str) -> str:
+    return name.replace("(anonymous namespace)::", "").split("(")[0].replace("void ", "")
+
+
 def main():
     d = sys.argv[1]
     want = sys.argv[2:]
@@ -44,7 +48,7 @@ def main():
         wr = f"{m['WRITE_SIZE'] / 1e6:.2f}" if "WRITE_SIZE" in m else "-"
         h, mi = m.get("TCC_HIT_sum"), m.get("TCC_MISS_sum")
         hs = f"{100 * h / (h + mi):.0f} %" if h is not None and mi is not None else "-"
-        short = name.split("(")[0].replace("void ", "")
+        short = _short(name)
         print(f"| `{short}` | {cyc:.3g} | {util} | {ldss} | {ws} | {vm} | {rd} | {wr} | {hs} |")
     # wave-cycle breakdown (SQ_WAIT_ANY + SQ_WAIT_INST_ANY + SQ_ACTIVE_INST_ANY ~= SQ_WAVE_CYCLES,
     # MI355X_MICROARCH.md rocprofv3 PMC slots) and the issue mix, when those counters were taken
@@ -57,7 +61,7 @@ def main():
         f = lambda k: f"{100 * m[k] / wc:.0f} %" if k in m else "-"  # noqa: E731
         mf = m.get("SQ_VALU_MFMA_BUSY_CYCLES")
         co = f"{100 * m['SQ_VALU_MFMA_COEXEC_CYCLES'] / mf:.0f} %" if mf and "SQ_VALU_MFMA_COEXEC_CYCLES" in m else "-"
-        rows.append(f"| `{name.split('(')[0].replace('void ', '')}` | {f('SQ_WAIT_ANY')} | {f('SQ_WAIT_INST_ANY')} | "
+        rows.append(f"| `{_short(name)}` | {f('SQ_WAIT_ANY')} | {f('SQ_WAIT_INST_ANY')} | "
                     f"{f('SQ_WAIT_INST_LDS')} | {f('SQ_ACTIVE_INST_ANY')} | {f('SQ_ACTIVE_INST_VALU')} | "
                     f"{f('SQ_ACTIVE_INST_LDS')} | {f('SQ_ACTIVE_INST_SCA')} | {co} |")
     if rows and any("SQ_WAIT_INST_ANY" in c or "SQ_ACTIVE_INST_VALU" in c for c in vals.values()):
