@@ -390,114 +390,142 @@ __global__ __launch_bounds__(512, 1) void mlp2_step_kernel(
 }
 
 // ----------------------------------------------------------------------------------------
-// dW2 [256 out][256 in] += dZ2^T H1, H1 = relu(X W1^T + b1) recomputed, WITHOUT LDS: dZ2 arrives
-// in the fragment layout written by mlp2_step_kernel<., true> (fragment (S, b) = rows
-// 32S .. 32S + 31 x units 16b .. 16b + 15, 1 KiB, lane (l15, g) = rows 32S + 8g + j of unit
-// 16b + l15), so every A operand is ONE coalesced 16-B load per lane. H1 is recomputed
-// straight into the B-operand layout: the recompute MFMA's A operand (X rows) takes its 16
-// rows in the order 8(i >> 2) + 4h + (i & 3), so output lane (l15, g) holds rows 8g + 4h + r
-// of unit l15 — exactly the K = rows slots of the dW MFMA's B fragment; no transpose, no LDS
-// round trip (the LDS-staged mlp2_dw2_kernel spent its time on H1-image writes and fragment
-// reads: 16 % bank conflicts, ~1.7k LDS cycles per chunk against 512 MFMA cycles).
-//  * workgroup = 256 (out) x 128 (in) tile of one row range; 8 waves of 64 x 64 (wave w:
-//    out rows 64 (w >> 1), in columns 128 t + 64 (w & 1)); per 32-row step a wave runs 8
-//    recompute + 16 dW MFMAs (16x16x32).
+// dW2 [256 out][256 in] += dZ2^T H1, H1 = relu(X W1^T + b1) recomputed. dZ2 arrives in the
+// fragment layout written by mlp2_step_kernel<., true> (fragment (S, b) = rows 32S .. 32S + 31
+// x units 16b .. 16b + 15, 1 KiB, lane (l15, g) = rows 32S + 8g + j of unit 16b + l15), so a
+// fragment is ONE 1-KiB LDS-DMA wave-instruction in and ONE conflict-free ds_read_b128 out.
+// H1 is recomputed straight into the B-operand layout: the recompute MFMA's A operand (X rows)
+// takes its 16 rows in the order 8(i >> 2) + 4h + (i & 3), so output lane (l15, g) holds rows
+// 8g + 4h + r of unit l15 — exactly the K = rows slots of the dW MFMA's B fragment (no
+// transpose, no H1 image in LDS: the LDS-staged mlp2_dw2_kernel spent its time writing that
+// image, 16 % bank conflicts).
+//  * workgroup = 256 (out) x 128 (in) tile of one row range, 8 waves of 128 x 32 (wave w: out
+//    rows 128 (w >> 2), in columns 128 t + 32 (w & 3)); per 32-row step a wave runs 4
+//    recompute + 16 dW MFMAs (16x16x32). H1 of a column block is rebuilt by 2 waves (not 4).
+//  * per 64-row chunk the workgroup DMAs 32 dZ2 fragments (4 per wave) + the 4-KiB X tile
+//    (waves 0-3, one piece each, rows through the LDS row-id table) into a 4-slot ring, 3 chunks
+//    ahead; one barrier per chunk. Fetches past the range re-load its last chunk (never read),
+//    so every wave's DMA count per chunk is fixed and the vmcnt waits are immediates.
 //  * grid = 2 tiles x nsplit row ranges; xcd_remap keeps a range's two tiles on one XCD, so
 //    the second reader of each dZ2 fragment hits L2.
-//  * dataset row ids of the range (rows != nullptr) go to LDS once (a per-step global index
-//    load would sit in front of every X load).
-//  * the next step's fragments are loaded while this step's MFMAs run (register double buffer).
-constexpr int DW2F_MAX_ROWS = 8192;
+constexpr int DW2F_MAX_ROWS = 2048;                      // rows per workgroup (the row-id table)
+constexpr int DW2F_SLOTS = 4;                            // ring depth (chunks)
+constexpr int DW2F_ABYTES = 32 * 1024;                   // 2 steps x 16 dZ2 fragments
+constexpr int DW2F_SLOT = DW2F_ABYTES + MF_ROWS * 64;    // + X tile [64 rows][64 B]
 __global__ __launch_bounds__(512, 1) void mlp2_dw2f_kernel(const bf16_t* __restrict__ dZ2F, const bf16_t* __restrict__ X,
                                                            int Fp, const long long* __restrict__ rows, long nrows,
                                                            const bf16_t* __restrict__ W1, const float* __restrict__ b1,
                                                            int kchunk, float* __restrict__ dW2) {
-  __shared__ int ridx[DW2F_MAX_ROWS];
+  __shared__ __attribute__((aligned(16))) char smem[DW2F_SLOTS * DW2F_SLOT + DW2F_MAX_ROWS * 4];
+  int* ridx = reinterpret_cast<int*>(smem + DW2F_SLOTS * DW2F_SLOT);
   const int tid = threadIdx.x, lane = tid & 63, l15 = lane & 15, g = lane >> 4;
-  const int wid = tid >> 6, wm = wid >> 1;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6), wm = wid >> 2;
+  const bool xw = wid < 4;  // this wave also DMAs one X piece per chunk
   const int L = xcd_remap(blockIdx.x, gridDim.x);
   const int split = L >> 1, t = L & 1;
-  const int n0 = 128 * t + 64 * (wid & 1);  // in units (H1) of this wave
-  const int kbeg = split * kchunk, nsteps = kchunk / 32;
-  // row ids of the range (identity without `rows`): the X loads below then never branch
+  const int n0 = 128 * t + 32 * (wid & 3);  // in units (H1) of this wave
+  const int kbeg = split * kchunk, nch = kchunk / MF_ROWS;
+  // row ids of the range (identity without `rows`)
   for (int i = tid; i < kchunk; i += 512) ridx[i] = rows != nullptr ? (int)data_row(rows, kbeg + i, nrows) : kbeg + i;
   __syncthreads();
-  // recompute operands: W1 rows of the wave's 64 in units (K = features 8g .. 8g + 7; zero past Fp)
-  bf16x8 w1f[4];
-  float bias[4];
+
+  // recompute operands: W1 rows of the wave's 32 in units (K = features 8g .. 8g + 7; zero past Fp)
+  bf16x8 w1f[2];
+  float bias[2];
 #pragma unroll
-  for (int nb = 0; nb < 4; ++nb) {
+  for (int nb = 0; nb < 2; ++nb) {
     const int u = n0 + 16 * nb + l15;
     w1f[nb] = 8 * g + 8 <= Fp ? *reinterpret_cast<const bf16x8*>(W1 + (size_t)u * Fp + 8 * g)
                               : bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
     bias[nb] = b1[u];
   }
-  // X fragment of this lane: row slot i = l15 -> local row 8 (l15 >> 2) + 4h + (l15 & 3) of
-  // the step; feature chunk g (past Fp: chunk 0 of the same row — finite values times zero W1)
+  // DMA sources. dZ2 fragments: wave w moves blocks 2w, 2w + 1 of both steps (4 pieces).
+  const bf16_t* zsrc = dZ2F + ((size_t)(kbeg >> 5) * 16 + 2 * wid) * 512 + lane * 8;
+  // X piece (waves 0-3): LDS position (row 16w + (lane >> 2), slot lane & 3) holds feature chunk
+  // slot ^ ((row >> 3) & 3) (conflict-free fragment reads below); chunks past Fp fetch chunk 0
+  // of the same row (finite values, multiplied by zero W1 columns)
+  const int xrow = 16 * (wid & 3) + (lane >> 2);
+  int xq = (lane & 3) ^ ((xrow >> 3) & 3);
+  if (8 * xq + 8 > Fp) xq = 0;
+  auto issue = [&](int c, int slot) {
+    char* st = smem + slot * DW2F_SLOT;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {  // (step k >> 1, block 2w + (k & 1))
+      const bf16_t* src = zsrc + ((size_t)(2 * c + (k >> 1)) * 16 + (k & 1)) * 512;
+      __builtin_amdgcn_global_load_lds((const void*)src, (lds_void*)(st + ((k >> 1) * 16 + 2 * wid + (k & 1)) * 1024), 16, 0, 0);
+    }
+    if (xw) {
+      const size_t xr = (size_t)ridx[c * MF_ROWS + xrow];
+      __builtin_amdgcn_global_load_lds((const void*)(X + xr * Fp + 8 * xq), (lds_void*)(st + DW2F_ABYTES + wid * 1024), 16, 0, 0);
+    }
+  };
+  // wait until at most n chunks' DMAs of this wave are in flight (5 per chunk for waves 0-3, else 4)
+  auto dma_wait = [&](auto nc) {
+    constexpr int n = decltype(nc)::value;
+    if (xw)
+      wait_vmcnt<5 * n>();
+    else
+      wait_vmcnt<4 * n>();
+  };
+  // recompute A operand: row slot l15 -> local row 8 (l15 >> 2) + 4h + (l15 & 3) of the step,
+  // feature chunk xg at its swizzled LDS position
   const int xg = 8 * g + 8 <= Fp ? g : 0;
   const int xr0 = 8 * (l15 >> 2) + (l15 & 3);
-  auto xfrag = [&](int st, int h) {
-    const int lr = 32 * st + xr0 + 4 * h;  // row within the range
-    return *reinterpret_cast<const bf16x8*>(X + (size_t)ridx[lr] * Fp + 8 * xg);
-  };
-  // dZ2 fragment (step st of the range, out block 4 wm + mb)
-  const bf16_t* zbase = dZ2F + ((size_t)(kbeg >> 5) * 16 + 4 * wm) * 512 + lane * 8;
-  auto afrag = [&](int st, int mb) { return *reinterpret_cast<const bf16x8*>(zbase + ((size_t)st * 16 + mb) * 512); };
 
-  f32x4 acc[4][4];
+  f32x4 acc[8][2];
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+  for (int i = 0; i < 8; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  // ring of FD register buffers: step st + FD - 1 is requested while step st computes (HBM
-  // latency under load is several steps' worth of MFMA time)
-  constexpr int FD = 4;
-  bf16x8 a[FD][4], xf[FD][2];
-  auto fetch = [&](int st, int p) {
+    for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int last = nch - 1;
 #pragma unroll
-    for (int mb = 0; mb < 4; ++mb) a[p][mb] = afrag(st, mb);
-    xf[p][0] = xfrag(st, 0);
-    xf[p][1] = xfrag(st, 1);
-  };
-  // fetches past the range re-read its last step (valid memory, never used): no branches, so
-  // the compiler's vmcnt counting stays exact across the unrolled loop
-  const int last = nsteps - 1;
-  static_for<0, FD - 1>([&](auto pc) { fetch(min(decltype(pc)::value, last), decltype(pc)::value); });
-  auto body = [&](int st, auto pc) {
-    constexpr int P = decltype(pc)::value;  // register buffer of step st (== st % FD)
-    fetch(min(st + FD - 1, last), (P + FD - 1) % FD);
-    bf16x8 hb[4];
+  for (int k = 0; k < DW2F_SLOTS - 1; ++k) issue(min(k, last), k);
+  for (int c = 0; c < nch; ++c) {
+    const int slot = c & (DW2F_SLOTS - 1);
+    dma_wait(std::integral_constant<int, DW2F_SLOTS - 2>{});  // chunk c's pieces (this wave) landed
+    __builtin_amdgcn_s_barrier();                              // ... every wave's; slot c - 1 free
+    asm volatile("" ::: "memory");
+    issue(min(c + DW2F_SLOTS - 1, last), (c + DW2F_SLOTS - 1) & (DW2F_SLOTS - 1));
+    const char* st = smem + slot * DW2F_SLOT;
 #pragma unroll
-    for (int nb = 0; nb < 4; ++nb) {
-      const f32x4 c0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xf[P][0], w1f[nb], f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
-      const f32x4 c1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xf[P][1], w1f[nb], f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
-      const unsigned p0 = pk_bf16(fmaxf(c0[0] + bias[nb], 0.f), fmaxf(c0[1] + bias[nb], 0.f));
-      const unsigned p1 = pk_bf16(fmaxf(c0[2] + bias[nb], 0.f), fmaxf(c0[3] + bias[nb], 0.f));
-      const unsigned p2 = pk_bf16(fmaxf(c1[0] + bias[nb], 0.f), fmaxf(c1[1] + bias[nb], 0.f));
-      const unsigned p3 = pk_bf16(fmaxf(c1[2] + bias[nb], 0.f), fmaxf(c1[3] + bias[nb], 0.f));
-      typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
-      hb[nb] = __builtin_bit_cast(bf16x8, (u32x4_t{p0, p1, p2, p3}));
+    for (int s2 = 0; s2 < 2; ++s2) {
+      bf16x8 hb[2];
+      bf16x8 xf[2];
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int r = 32 * s2 + xr0 + 4 * h;
+        xf[h] = *reinterpret_cast<const bf16x8*>(st + DW2F_ABYTES + r * 64 + ((xg ^ ((r >> 3) & 3)) << 4));
+      }
+#pragma unroll
+      for (int nb = 0; nb < 2; ++nb) {
+        const f32x4 c0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xf[0], w1f[nb], f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+        const f32x4 c1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xf[1], w1f[nb], f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+        const unsigned p0 = pk_bf16(fmaxf(c0[0] + bias[nb], 0.f), fmaxf(c0[1] + bias[nb], 0.f));
+        const unsigned p1 = pk_bf16(fmaxf(c0[2] + bias[nb], 0.f), fmaxf(c0[3] + bias[nb], 0.f));
+        const unsigned p2 = pk_bf16(fmaxf(c1[0] + bias[nb], 0.f), fmaxf(c1[1] + bias[nb], 0.f));
+        const unsigned p3 = pk_bf16(fmaxf(c1[2] + bias[nb], 0.f), fmaxf(c1[3] + bias[nb], 0.f));
+        typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
+        hb[nb] = __builtin_bit_cast(bf16x8, (u32x4_t{p0, p1, p2, p3}));
+      }
+#pragma unroll
+      for (int mb = 0; mb < 8; ++mb) {
+        const bf16x8 a = *reinterpret_cast<const bf16x8*>(st + (s2 * 16 + 8 * wm + mb) * 1024 + lane * 16);
+#pragma unroll
+        for (int nb = 0; nb < 2; ++nb) acc[mb][nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, hb[nb], acc[mb][nb], 0, 0, 0);
+      }
     }
-#pragma unroll
-    for (int mb = 0; mb < 4; ++mb)
-#pragma unroll
-      for (int nb = 0; nb < 4; ++nb)
-        acc[mb][nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[P][mb], hb[nb], acc[mb][nb], 0, 0, 0);
-  };
-  int st = 0;
-  for (; st + FD <= nsteps; st += FD) static_for<0, FD>([&](auto pc) { body(st + decltype(pc)::value, pc); });
-  static_for<0, FD - 1>([&](auto pc) {
-    if (st + decltype(pc)::value < nsteps) body(st + decltype(pc)::value, pc);
-  });
-  // out unit 64 wm + 16 mb + 4g + r, in unit n0 + 16 nb + l15
+  }
+  wait_vmcnt<0>();  // the clamped fetches past the range must land before the workgroup ends
+  // out unit 128 wm + 16 mb + 4g + r, in unit n0 + 16 nb + l15
   float* dst = dW2 + (size_t)(split & (kMlpRedCopies2 - 1)) * 65536;
 #pragma unroll
-  for (int mb = 0; mb < 4; ++mb)
+  for (int mb = 0; mb < 8; ++mb)
 #pragma unroll
     for (int r = 0; r < 4; ++r)
 #pragma unroll
-      for (int nb = 0; nb < 4; ++nb)
-        atomicAdd(dst + (size_t)(64 * wm + 16 * mb + 4 * g + r) * MF_H + n0 + 16 * nb + l15, acc[mb][nb][r]);
+      for (int nb = 0; nb < 2; ++nb)
+        atomicAdd(dst + (size_t)(128 * wm + 16 * mb + 4 * g + r) * MF_H + n0 + 16 * nb + l15, acc[mb][nb][r]);
 }
 }  // namespace
 
@@ -522,18 +550,25 @@ bool launch_mlp2_step(const bf16_t* X, int Fp, const bf16_t* W1, const float* b1
 
 // dW2 (the spread scratch's dW2 copies: red + kMlpRedCopies * kMlpRedRow) from the fragment-
 // layout dZ2; B % 64 == 0, Fp <= 32. nsplit row ranges (<= 128: two tiles per range, one
-// workgroup per CU). False = not covered.
+// workgroup per CU); batches beyond 128 ranges of DW2F_MAX_ROWS rows run as consecutive
+// launches over row blocks. False = not covered.
 bool launch_mlp2_dw2f(const bf16_t* dZ2F, const bf16_t* X, int Fp, const long long* rows, long nrows, const bf16_t* W1,
                       const float* b1, int B, int nsplit, float* red, hipStream_t s) {
   if (B <= 0 || B % MF_ROWS != 0 || Fp > 32 || Fp % 8 != 0 || red == nullptr) return false;
-  const int chunks = B / MF_ROWS;
-  if (nsplit < 1) nsplit = 1;
-  if (nsplit > 128) nsplit = 128;
-  while (nsplit > 1 && chunks % nsplit != 0) --nsplit;
-  const int kchunk = (chunks / nsplit) * MF_ROWS;
-  if (rows != nullptr && kchunk > DW2F_MAX_ROWS) return false;
-  hipLaunchKernelGGL(mlp2_dw2f_kernel, dim3(2 * nsplit), dim3(512), 0, s, dZ2F, X, Fp, rows, nrows, W1, b1, kchunk,
-                     red + (size_t)kMlpRedCopies * kMlpRedRow);
+  constexpr int kMaxBlock = 128 * DW2F_MAX_ROWS;  // rows per launch
+  for (int r0 = 0; r0 < B; r0 += kMaxBlock) {
+    const int Bb = B - r0 < kMaxBlock ? B - r0 : kMaxBlock;
+    const int chunks = Bb / MF_ROWS;
+    int ns = nsplit < 1 ? 1 : (nsplit > 128 ? 128 : nsplit);
+    while (ns < 128 && (chunks + ns - 1) / ns * MF_ROWS > DW2F_MAX_ROWS) ++ns;
+    while (ns > 1 && chunks % ns != 0) --ns;
+    const int kchunk = (chunks / ns) * MF_ROWS;
+    if (kchunk > DW2F_MAX_ROWS) return false;  // (unreachable for B % 64 == 0)
+    // row block r0: dZ2 fragments start at step r0 / 32; X through `rows` (offset) or directly
+    hipLaunchKernelGGL(mlp2_dw2f_kernel, dim3(2 * ns), dim3(512), 0, s, dZ2F + (size_t)r0 * MF_H,
+                       rows != nullptr ? X : X + (size_t)r0 * Fp, Fp, rows != nullptr ? rows + r0 : nullptr,
+                       rows != nullptr ? nrows : (long)Bb, W1, b1, kchunk, red + (size_t)kMlpRedCopies * kMlpRedRow);
+  }
   return true;
 }
 

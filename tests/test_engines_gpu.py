@@ -384,7 +384,8 @@ def _dz2_from_frag(zf: torch.Tensor, B: int) -> torch.Tensor:
     return zf[: B * 256].view(B // 32, 16, 4, 16, 8).permute(0, 2, 4, 1, 3).reshape(B, 256)
 
 
-@pytest.mark.parametrize("B,F,indexed", [(262144, 16, False), (4096, 32, False), (16384, 16, True), (128, 8, False)])
+@pytest.mark.parametrize("B,F,indexed", [(262144, 16, False), (327680, 16, False), (4096, 32, False), (16384, 16, True),
+                                       (128, 8, False)])
 def test_mlp_one_launch_step_matches_two_kernel_step(B, F, indexed):
     """The training step's forward + backward in ONE launch (csrc/mlp_step.hip: X staged once,
     layer 1 computed once, H2 and dy never leave the workgroup), with dZ2 row-major + the
