@@ -76,9 +76,24 @@ __global__ __launch_bounds__(512, 1) void mlp2_step_kernel(
   // a zero laundered per chunk (below) keeps the loads inside the chunk loop (hoisted, they
   // would pin 64 VGPRs); laundering the pointer itself would lose its global address space
   // (flat loads: counted in lgkmcnt too, so every LDS wait would wait for them)
+  // Buffer loads: the per-fragment offset is an immediate / SGPR, no 64-bit address VALU.
   int w2z = 0;
+  const __amdgpu_buffer_rsrc_t w2rs = __builtin_amdgcn_make_buffer_rsrc((void*)W2, 0, 0x7FFFFFFF, 0x00020000);
   auto w2frag = [&](int m, int kt) {
-    return *reinterpret_cast<const bf16x8*>(W2 + (w2z + w2lane + 16 * MF_H * m + 32 * kt));
+    typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
+    return __builtin_bit_cast(bf16x8, (u32x4_t)__builtin_amdgcn_raw_buffer_load_b128(
+                                          w2rs, 2 * (w2z + w2lane), 2 * (16 * MF_H * m + 32 * kt), 0));
+  };
+  // the first WD K steps of layer 2, requested one chunk early (right after the previous
+  // chunk's dH1 MFMAs): they land during dZ1 / dW1, the staging barrier and layer 1
+  bf16x8 w2r[WD][MT];
+  auto w2first = [&]() {
+    w2z = 0;
+    asm volatile("" : "+s"(w2z));
+#pragma unroll
+    for (int k = 0; k < WD; ++k)
+#pragma unroll
+      for (int m = 0; m < MT; ++m) w2r[k][m] = w2frag(m, k);
   };
   f32x4 dw1a[MT][NFT];
 #pragma unroll
@@ -114,6 +129,7 @@ __global__ __launch_bounds__(512, 1) void mlp2_step_kernel(
   };
   const int nchunks = (B + MF_ROWS - 1) / MF_ROWS;
   if ((int)blockIdx.x < nchunks) prefetch(blockIdx.x);
+  w2first();
   int par = 0;
   for (int ch = blockIdx.x; ch < nchunks; ch += gridDim.x, par ^= 1) {
     const int row0 = ch * MF_ROWS;
@@ -126,13 +142,6 @@ __global__ __launch_bounds__(512, 1) void mlp2_step_kernel(
     if (ch + (int)gridDim.x < nchunks) prefetch(ch + gridDim.x);
 
     // ---- layer 1 (own units): H1 -> h1s; the first W2 fragments of layer 2 in flight
-    bf16x8 w2r[WD][MT];
-    w2z = 0;
-    asm volatile("" : "+s"(w2z));
-#pragma unroll
-    for (int k = 0; k < WD; ++k)
-#pragma unroll
-      for (int m = 0; m < MT; ++m) w2r[k][m] = w2frag(m, k);
     f32x4 acc[MT][4];
 #pragma unroll
     for (int n = 0; n < 4; ++n) {
@@ -288,6 +297,7 @@ __global__ __launch_bounds__(512, 1) void mlp2_step_kernel(
         for (int n = 0; n < 4; ++n)
           acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wt[m][kt], zb[n], acc[m][n], 0, 0, 0);
     }
+    w2first();  // the next chunk's first layer-2 fragments
     // ---- dZ1 = dH1 * [H1 > 0] over the same 8 bytes of h1s; db1 partials
 #pragma unroll
     for (int m = 0; m < MT; ++m) {
