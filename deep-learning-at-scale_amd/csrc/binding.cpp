@@ -519,7 +519,7 @@ bool mlp2_dw2(const at::Tensor& dZ2, const at::Tensor& X, int64_t Fp, c10::optio
 // (mlp_fused.hip mlp2_reduce_kernel) and zeroes it; null destinations are skipped.
 void mlp2_reduce(const at::Tensor& red, int64_t Fp, int64_t B, c10::optional<at::Tensor> loss_sum, const at::Tensor& db3,
                  const at::Tensor& dw3, const at::Tensor& db1, const at::Tensor& db2, const at::Tensor& dW1,
-                 c10::optional<at::Tensor> dW2) {
+                 c10::optional<at::Tensor> dW2, int64_t dw2_rows) {
   constexpr int64_t H = 256;
   check_t(red, at::kFloat, "red");
   check_extent(red, wf::kMlpRedFloats, "red");
@@ -535,7 +535,8 @@ void mlp2_reduce(const at::Tensor& red, int64_t Fp, int64_t B, c10::optional<at:
   const c10::hip::OptionalHIPGuardMasqueradingAsCUDA guard(red.device());
   TORCH_CHECK(B > 0, "mlp2_reduce: B > 0");
   wf::launch_mlp2_reduce(fp(red), (int)Fp, (int)B, opt_ptr<float>(loss_sum, at::kFloat, "loss_sum", 1), fp(db3), fp(dw3),
-                         fp(db1), fp(db2), fp(dW1), opt_ptr<float>(dW2, at::kFloat, "dW2", H * H), cur_stream());
+                         fp(db1), fp(db2), fp(dW1), opt_ptr<float>(dW2, at::kFloat, "dW2", H * H), cur_stream(),
+                         (int)dw2_rows);
 }
 
 // MLP training step forward + backward in one launch (mlp_step.hip); the batch sums land in
@@ -574,7 +575,7 @@ bool mlp2_step(const at::Tensor& X, int64_t Fp, const at::Tensor& W1, const at::
 
 // dW2 from the fragment-layout dZ2 of mlp2_step(dz_frag=True) into the spread scratch's dW2
 // copies (mlp_step.hip mlp2_dw2f_kernel; mlp2_reduce adds them). False = not covered.
-bool mlp2_dw2f(const at::Tensor& dZ2F, const at::Tensor& X, int64_t Fp, c10::optional<at::Tensor> rows,
+int64_t mlp2_dw2f(const at::Tensor& dZ2F, const at::Tensor& X, int64_t Fp, c10::optional<at::Tensor> rows,
                const at::Tensor& W1, const at::Tensor& b1, int64_t B, int64_t nsplit, const at::Tensor& red) {
   constexpr int64_t H = 256;
   check_t(dZ2F, at::kBFloat16, "dZ2F");

@@ -110,13 +110,19 @@ constexpr int kMlpRedLoss = 0, kMlpRedDb3 = 1, kMlpRedDw3 = 2, kMlpRedDb1 = 258,
 // atomic wave-instructions per CU even spread over copies)
 constexpr int kMlpRedSlabRows = 256, kMlpRedSlabRow = 256 * 32;
 constexpr long kMlpRedSlabOff = (long)kMlpRedCopies * kMlpRedRow + (long)kMlpRedCopies2 * 65536;
-constexpr long kMlpRedFloats = kMlpRedSlabOff + (long)kMlpRedSlabRows * kMlpRedSlabRow;
+// then the dW2 rows of the fragment-layout dW2 kernel: [kMlpRedSlab2Rows][256 x 256] (plain
+// stores of each workgroup's partial tile, summed by the reduce: 8M float atomics per step
+// were the dW2 kernel's bottleneck)
+constexpr int kMlpRedSlab2Rows = 256;
+constexpr long kMlpRedSlab2Off = kMlpRedSlabOff + (long)kMlpRedSlabRows * kMlpRedSlabRow;
+constexpr long kMlpRedFloats = kMlpRedSlab2Off + (long)kMlpRedSlab2Rows * 65536;
 // grid of the 8-wave training kernels for a batch (one workgroup per CU at most): the rows of
 // the dW1 slab the reduce sums
 int mlp2_train_grid(int B);
 bool mlp_bwd8();  // the 8-wave backward is selected (WELLFLOW_MLP_BWD8, default on)
 void launch_mlp2_reduce(float* red, int Fp, int B, float* loss_sum, float* db3, float* dw3, float* db1, float* db2,
-                        float* dW1, float* dW2, hipStream_t s);
+                        float* dW1, float* dW2, hipStream_t s, int dw2_rows = 0);
+// dw2_rows: dW2 slab rows (launch_mlp2_dw2f's return value) summed into dW2 as well
 // The training step's forward + backward in ONE launch (mlp_step.hip): from X (rows), y, the
 // bf16 weights and fp32 biases / head — dZ2 ([B][256] bf16, mlp2_dw2's operand), pred (optional)
 // and every batch sum except dW2 (loss, db3, dw3, db1, db2, dW1) into the spread scratch `red`,
@@ -128,8 +134,9 @@ bool launch_mlp2_step(const bf16_t* X, int Fp, const bf16_t* W1, const float* b1
 // [B][256]: fragment (S, b) of rows 32S .. 32S + 31 x units 16b .. 16b + 15 at element
 // (S * 16 + b) * 512, lane (l15, g) = 16 B = rows 32S + 8g .. + 7 of unit 16b + l15.
 // dW2 from that layout without LDS (mlp_step.hip mlp2_dw2f_kernel) into the scratch's dW2 copies.
-bool launch_mlp2_dw2f(const bf16_t* dZ2F, const bf16_t* X, int Fp, const long long* rows, long nrows, const bf16_t* W1,
-                      const float* b1, int B, int nsplit, float* red, hipStream_t s);
+// Returns the dW2 slab rows written (> 0), or 0 = not covered (nothing launched).
+int launch_mlp2_dw2f(const bf16_t* dZ2F, const bf16_t* X, int Fp, const long long* rows, long nrows, const bf16_t* W1,
+                     const float* b1, int B, int nsplit, float* red, hipStream_t s);
 
 // ---- fused reference CNN (cnn_fused.hip): Conv1D(C -> Fp, width taps / C) + ReLU + dropout ->
 // Dense(T * Fp -> O) -> loss, cnn.py:110-118. Flat layout = models/cnn.py CnnLayout:

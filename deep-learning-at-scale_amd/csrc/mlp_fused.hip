@@ -69,7 +69,7 @@ __global__ __launch_bounds__(256) void mlp2_reduce_kernel(float* __restrict__ re
                                                           float* __restrict__ loss_sum,
                                                           float* __restrict__ db3, float* __restrict__ dw3,
                                                           float* __restrict__ db1, float* __restrict__ db2,
-                                                          float* __restrict__ dW1, float* __restrict__ dW2) {
+                                                          float* __restrict__ dW1, float* __restrict__ dW2, int dw2_rows) {
   if ((int)blockIdx.x < slab_blocks) {
     // dW1 slab: block b sums 16 consecutive entries over the nwg (<= 256) workgroup rows in 16
     // row groups, every thread's 16 loads independent (one latency round, not a chain)
@@ -119,6 +119,15 @@ __global__ __launch_bounds__(256) void mlp2_reduce_kernel(float* __restrict__ re
       v += r2[c * 65536 + j];
       r2[c * 65536 + j] = 0.f;
     }
+    // the dW2 kernel's per-workgroup rows (plain stores, overwritten every step: not zeroed)
+    const float* s2 = red + kMlpRedSlab2Off + j;
+    float p[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    int r = 0;
+    for (; r + 8 <= dw2_rows; r += 8)
+#pragma unroll
+      for (int k = 0; k < 8; ++k) p[k] += s2[(size_t)(r + k) * 65536];
+    for (; r < dw2_rows; ++r) p[0] += s2[(size_t)r * 65536];
+    v += ((p[0] + p[1]) + (p[2] + p[3])) + ((p[4] + p[5]) + (p[6] + p[7]));
     if (dW2 != nullptr && v != 0.f) dW2[j] += v;
   }
 }
@@ -145,12 +154,13 @@ int mlp2_train_grid(int B) {
 }
 
 void launch_mlp2_reduce(float* red, int Fp, int B, float* loss_sum, float* db3, float* dw3, float* db1, float* db2,
-                        float* dW1, float* dW2, hipStream_t s) {
+                        float* dW1, float* dW2, hipStream_t s, int dw2_rows) {
   const int n = kMlpRedDW1 + 256 * Fp + 256 * 256;
   // the dW1 rows exist only when the 8-wave backward ran (the 4-wave one adds dW1 itself)
   const int slab_blocks = mlp_bwd8() ? (256 * Fp + 15) / 16 : 0;
   hipLaunchKernelGGL(mlp2_reduce_kernel, dim3(slab_blocks + (n + 255) / 256), dim3(256), 0, s, red, Fp,
-                     mlp2_train_grid(B), slab_blocks, loss_sum, db3, dw3, db1, db2, dW1, dW2);
+                     mlp2_train_grid(B), slab_blocks, loss_sum, db3, dw3, db1, db2, dW1, dW2,
+                     dw2_rows < 0 ? 0 : (dw2_rows > kMlpRedSlab2Rows ? kMlpRedSlab2Rows : dw2_rows));
 }
 
 

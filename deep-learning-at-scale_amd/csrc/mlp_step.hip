@@ -425,7 +425,8 @@ constexpr int DW2F_SLOT = DW2F_ABYTES + MF_ROWS * 64;    // + X tile [64 rows][6
 __global__ __launch_bounds__(512, 1) void mlp2_dw2f_kernel(const bf16_t* __restrict__ dZ2F, const bf16_t* __restrict__ X,
                                                            int Fp, const long long* __restrict__ rows, long nrows,
                                                            const bf16_t* __restrict__ W1, const float* __restrict__ b1,
-                                                           int kchunk, float* __restrict__ dW2) {
+                                                           int kchunk, float* __restrict__ dW2, float* __restrict__ slab,
+                                                           int slab_row0) {
   __shared__ __attribute__((aligned(16))) char smem[DW2F_SLOTS * DW2F_SLOT + DW2F_MAX_ROWS * 4];
   int* ridx = reinterpret_cast<int*>(smem + DW2F_SLOTS * DW2F_SLOT);
   const int tid = threadIdx.x, lane = tid & 63, l15 = lane & 15, g = lane >> 4;
@@ -527,15 +528,27 @@ __global__ __launch_bounds__(512, 1) void mlp2_dw2f_kernel(const bf16_t* __restr
     }
   }
   wait_vmcnt<0>();  // the clamped fetches past the range must land before the workgroup ends
-  // out unit 128 wm + 16 mb + 4g + r, in unit n0 + 16 nb + l15
-  float* dst = dW2 + (size_t)(split & (kMlpRedCopies2 - 1)) * 65536;
+  // out unit 128 wm + 16 mb + 4g + r, in unit n0 + 16 nb + l15: plain stores into this range's
+  // slab row (the reduce sums the rows); past the slab, atomics into a dW2 copy
+  const int srow = slab_row0 + split;
+  if (srow < kMlpRedSlab2Rows) {
+    float* dst = slab + (size_t)srow * 65536;
 #pragma unroll
-  for (int mb = 0; mb < 8; ++mb)
+    for (int mb = 0; mb < 8; ++mb)
 #pragma unroll
-    for (int r = 0; r < 4; ++r)
+      for (int r = 0; r < 4; ++r)
 #pragma unroll
-      for (int nb = 0; nb < 2; ++nb)
-        atomicAdd(dst + (size_t)(128 * wm + 16 * mb + 4 * g + r) * MF_H + n0 + 16 * nb + l15, acc[mb][nb][r]);
+        for (int nb = 0; nb < 2; ++nb) dst[(size_t)(128 * wm + 16 * mb + 4 * g + r) * MF_H + n0 + 16 * nb + l15] = acc[mb][nb][r];
+  } else {
+    float* dst = dW2 + (size_t)(split & (kMlpRedCopies2 - 1)) * 65536;
+#pragma unroll
+    for (int mb = 0; mb < 8; ++mb)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int nb = 0; nb < 2; ++nb)
+          atomicAdd(dst + (size_t)(128 * wm + 16 * mb + 4 * g + r) * MF_H + n0 + 16 * nb + l15, acc[mb][nb][r]);
+  }
 }
 }  // namespace
 
@@ -562,10 +575,11 @@ bool launch_mlp2_step(const bf16_t* X, int Fp, const bf16_t* W1, const float* b1
 // layout dZ2; B % 64 == 0, Fp <= 32. nsplit row ranges (<= 128: two tiles per range, one
 // workgroup per CU); batches beyond 128 ranges of DW2F_MAX_ROWS rows run as consecutive
 // launches over row blocks. False = not covered.
-bool launch_mlp2_dw2f(const bf16_t* dZ2F, const bf16_t* X, int Fp, const long long* rows, long nrows, const bf16_t* W1,
-                      const float* b1, int B, int nsplit, float* red, hipStream_t s) {
-  if (B <= 0 || B % MF_ROWS != 0 || Fp > 32 || Fp % 8 != 0 || red == nullptr) return false;
+int launch_mlp2_dw2f(const bf16_t* dZ2F, const bf16_t* X, int Fp, const long long* rows, long nrows, const bf16_t* W1,
+                     const float* b1, int B, int nsplit, float* red, hipStream_t s) {
+  if (B <= 0 || B % MF_ROWS != 0 || Fp > 32 || Fp % 8 != 0 || red == nullptr) return 0;
   constexpr int kMaxBlock = 128 * DW2F_MAX_ROWS;  // rows per launch
+  int srow = 0;  // slab rows used so far (the launches' ranges stack)
   for (int r0 = 0; r0 < B; r0 += kMaxBlock) {
     const int Bb = B - r0 < kMaxBlock ? B - r0 : kMaxBlock;
     const int chunks = Bb / MF_ROWS;
@@ -573,13 +587,15 @@ bool launch_mlp2_dw2f(const bf16_t* dZ2F, const bf16_t* X, int Fp, const long lo
     while (ns < 128 && (chunks + ns - 1) / ns * MF_ROWS > DW2F_MAX_ROWS) ++ns;
     while (ns > 1 && chunks % ns != 0) --ns;
     const int kchunk = (chunks / ns) * MF_ROWS;
-    if (kchunk > DW2F_MAX_ROWS) return false;  // (unreachable for B % 64 == 0)
+    if (kchunk > DW2F_MAX_ROWS) return 0;  // (unreachable for B % 64 == 0)
     // row block r0: dZ2 fragments start at step r0 / 32; X through `rows` (offset) or directly
     hipLaunchKernelGGL(mlp2_dw2f_kernel, dim3(2 * ns), dim3(512), 0, s, dZ2F + (size_t)r0 * MF_H,
                        rows != nullptr ? X : X + (size_t)r0 * Fp, Fp, rows != nullptr ? rows + r0 : nullptr,
-                       rows != nullptr ? nrows : (long)Bb, W1, b1, kchunk, red + (size_t)kMlpRedCopies * kMlpRedRow);
+                       rows != nullptr ? nrows : (long)Bb, W1, b1, kchunk, red + (size_t)kMlpRedCopies * kMlpRedRow,
+                       red + kMlpRedSlab2Off, srow);
+    srow += ns;
   }
-  return true;
+  return srow < kMlpRedSlab2Rows ? srow : kMlpRedSlab2Rows;
 }
 
 }  // namespace wf

@@ -230,12 +230,3 @@ class DeviceStreamer:
         return {"h2d_ms_mean": round(sum(ms) / len(ms), 4), "h2d_ms_median": round(srt[len(srt) // 2], 4),
                 "h2d_ms_max": round(srt[-1], 4), "h2d_batches": len(ms),
                 "h2d_over_1ms": sum(1 for v in ms if v > 1.0)}
-
-    def __iter__(self):
-        """Yields the ring slot index of each batch (its tensors: ``slots[k][0:2]``)."""
-        while True:
-            try:
-                self.next()
-            except StopIteration:
-                return
-            yield self.last_slot

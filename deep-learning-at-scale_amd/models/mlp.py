@@ -29,7 +29,7 @@ from torch import nn
 # floats of the spread-reduction scratch (csrc/kernels.h kMlpRedFloats: 64 x 9216 copies,
 # 4 x 65536 dW2 copies, 256 x 8192 dW1 workgroup rows)
 MLP_RED_COPY_FLOATS = 64 * 9216 + 4 * 65536  # the atomic copies: zero between steps
-MLP_RED_FLOATS = MLP_RED_COPY_FLOATS + 256 * 8192
+MLP_RED_FLOATS = MLP_RED_COPY_FLOATS + 256 * 8192 + 256 * 65536  # + dW1 rows + dW2 rows (csrc/kernels.h)
 
 
 def _r8(x: int) -> int:
@@ -226,12 +226,16 @@ class NativeMLP:
                 if not C.mlp2_step(Xop, self.Fp, wl[0][0], pl[0][1], wl[1][0], pl[1][1], hw, hb, y,
                                    2.0 * float(grad_scale), B, rows, self.dZ[1], self.pred, red, frag):
                     raise RuntimeError("NativeMLP: fused step refused the shape")
-                ok = (C.mlp2_dw2f(self.dZ[1], Xop, self.Fp, rows, wl[0][0], pl[0][1], B, self.dw2f_split, red) if frag
-                      else C.mlp2_dw2(self.dZ[1], Xop, self.Fp, rows, wl[0][0], pl[0][1], B, self.dw2_split, gl[1][0],
-                                      red))
+                if frag:  # dW2 partials as slab rows (their count) summed by the reduce
+                    ok = dw2_rows = C.mlp2_dw2f(self.dZ[1], Xop, self.Fp, rows, wl[0][0], pl[0][1], B,
+                                                self.dw2f_split, red)
+                else:
+                    dw2_rows = 0
+                    ok = C.mlp2_dw2(self.dZ[1], Xop, self.Fp, rows, wl[0][0], pl[0][1], B, self.dw2_split, gl[1][0],
+                                    red)
                 if not ok:
                     raise RuntimeError("NativeMLP: dW2 kernel refused the shape")
-                C.mlp2_reduce(red, self.Fp, B, ls, ghb, ghw, gl[0][1], gl[1][1], gl[0][0], gl[1][0])
+                C.mlp2_reduce(red, self.Fp, B, ls, ghb, ghw, gl[0][1], gl[1][1], gl[0][0], gl[1][0], int(dw2_rows))
                 return ls
             if not self._fused_forward(B, y, self.dy, ls, 2.0 * float(grad_scale), (ghw, ghb),
                                        store_h1=self.dw2_gemm, rows=rows, red=red):
@@ -254,7 +258,7 @@ class NativeMLP:
             raise
         if red is not None:
             C.mlp2_reduce(red, self.Fp, B, ls, ghb, ghw, gl[0][1], gl[1][1], gl[0][0],
-                          None if self.dw2_gemm else gl[1][0])
+                          None if self.dw2_gemm else gl[1][0], 0)
         return ls
 
     def _load_x(self, x: torch.Tensor) -> int:
