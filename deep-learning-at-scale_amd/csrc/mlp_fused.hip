@@ -95,8 +95,11 @@ __global__ __launch_bounds__(256) void mlp2_reduce_kernel(float* __restrict__ re
     return;
   }
   const int na = kMlpRedDW1 + 256 * Fp;
-  const int i = ((int)blockIdx.x - slab_blocks) * blockDim.x + threadIdx.x;
-  if (i < na) {
+  const int nA = (na + 255) / 256;  // blocks of the small sums
+  const int bx = (int)blockIdx.x - slab_blocks;
+  if (bx < nA) {
+    const int i = bx * 256 + threadIdx.x;
+    if (i >= na) return;
     float v = 0.f;
 #pragma unroll
     for (int c = 0; c < kMlpRedCopies; ++c) {
@@ -110,25 +113,35 @@ __global__ __launch_bounds__(256) void mlp2_reduce_kernel(float* __restrict__ re
                  : i < kMlpRedDW1  ? (db2 != nullptr ? db2 + (i - kMlpRedDb2) : nullptr)
                                    : (dW1 != nullptr ? dW1 + (i - kMlpRedDW1) : nullptr);
     if (dst != nullptr && v != 0.f) *dst += v;
-  } else if (i - na < 256 * 256) {
-    const int j = i - na;
+    return;
+  }
+  // dW2: block = 64 consecutive entries x 4 row groups: group 0 also sums (and re-zeroes) the
+  // kMlpRedCopies2 atomic copies; every group sums every 4th of the dW2 kernel's slab rows
+  // (plain stores, overwritten every step: not zeroed); the groups meet in LDS
+  __shared__ float part2[4][64];
+  const int e = threadIdx.x & 63, q = threadIdx.x >> 6;
+  const int j = (bx - nA) * 64 + e;
+  float v = 0.f;
+  if (q == 0) {
     float* r2 = red + kMlpRedCopies * kMlpRedRow;
-    float v = 0.f;
 #pragma unroll
     for (int c = 0; c < kMlpRedCopies2; ++c) {
       v += r2[c * 65536 + j];
       r2[c * 65536 + j] = 0.f;
     }
-    // the dW2 kernel's per-workgroup rows (plain stores, overwritten every step: not zeroed)
-    const float* s2 = red + kMlpRedSlab2Off + j;
-    float p[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    int r = 0;
-    for (; r + 8 <= dw2_rows; r += 8)
+  }
+  const float* s2 = red + kMlpRedSlab2Off + j;
+  float p[4] = {0.f, 0.f, 0.f, 0.f};
+  int r = q;
+  for (; r + 12 < dw2_rows; r += 16)
 #pragma unroll
-      for (int k = 0; k < 8; ++k) p[k] += s2[(size_t)(r + k) * 65536];
-    for (; r < dw2_rows; ++r) p[0] += s2[(size_t)r * 65536];
-    v += ((p[0] + p[1]) + (p[2] + p[3])) + ((p[4] + p[5]) + (p[6] + p[7]));
-    if (dW2 != nullptr && v != 0.f) dW2[j] += v;
+    for (int k = 0; k < 4; ++k) p[k] += s2[(size_t)(r + 4 * k) * 65536];
+  for (; r < dw2_rows; r += 4) p[0] += s2[(size_t)r * 65536];
+  part2[q][e] = v + ((p[0] + p[1]) + (p[2] + p[3]));
+  __syncthreads();
+  if (q == 0) {
+    const float t = (part2[0][e] + part2[1][e]) + (part2[2][e] + part2[3][e]);
+    if (dW2 != nullptr && t != 0.f) dW2[j] += t;
   }
 }
 
@@ -155,10 +168,10 @@ int mlp2_train_grid(int B) {
 
 void launch_mlp2_reduce(float* red, int Fp, int B, float* loss_sum, float* db3, float* dw3, float* db1, float* db2,
                         float* dW1, float* dW2, hipStream_t s, int dw2_rows) {
-  const int n = kMlpRedDW1 + 256 * Fp + 256 * 256;
+  const int na = kMlpRedDW1 + 256 * Fp;
   // the dW1 rows exist only when the 8-wave backward ran (the 4-wave one adds dW1 itself)
   const int slab_blocks = mlp_bwd8() ? (256 * Fp + 15) / 16 : 0;
-  hipLaunchKernelGGL(mlp2_reduce_kernel, dim3(slab_blocks + (n + 255) / 256), dim3(256), 0, s, red, Fp,
+  hipLaunchKernelGGL(mlp2_reduce_kernel, dim3(slab_blocks + (na + 255) / 256 + 65536 / 64), dim3(256), 0, s, red, Fp,
                      mlp2_train_grid(B), slab_blocks, loss_sum, db3, dw3, db1, db2, dW1, dW2,
                      dw2_rows < 0 ? 0 : (dw2_rows > kMlpRedSlab2Rows ? kMlpRedSlab2Rows : dw2_rows));
 }
