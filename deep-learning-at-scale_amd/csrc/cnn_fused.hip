@@ -377,9 +377,13 @@ __global__ __launch_bounds__(256) void cnn_reduce_kernel(
     const int b = f >> 4, lanep = ((f & 15) >> 2) * 16 + j, r = f & 3;
     const size_t stride = (size_t)T * NFB * 64 * 4;
     const float* p = part_wd + (((size_t)t * NFB + b) * 64 + lanep) * 4 + r;
-    float s = 0.f;
-    for (int c = 0; c < nch; ++c) s += p[c * stride];
-    gWd[(size_t)j * nf + rest] += s;
+    float s4[4] = {0.f, 0.f, 0.f, 0.f};  // independent loads: one latency round per 4 chunks
+    int c = 0;
+    for (; c + 4 <= nch; c += 4)
+#pragma unroll
+      for (int k = 0; k < 4; ++k) s4[k] += p[(size_t)(c + k) * stride];
+    for (; c < nch; ++c) s4[0] += p[(size_t)c * stride];
+    gWd[(size_t)j * nf + rest] += (s4[0] + s4[1]) + (s4[2] + s4[3]);
     return;
   }
   if (bid < nwd + nwc) {
@@ -391,7 +395,13 @@ __global__ __launch_bounds__(256) void cnn_reduce_kernel(
       const int b = f >> 4, lanep = ((f & 15) >> 2) * 16 + kk, r = f & 3;
       const float* p = part_wc + (((size_t)b * 64 + lanep) * 4 + r);
       const size_t stride = (size_t)NFB * 64 * 4;
-      for (int c = grp; c < nwgb; c += 16) s += p[c * stride];
+      float s4[4] = {0.f, 0.f, 0.f, 0.f};
+      int c = grp;
+      for (; c + 48 < nwgb; c += 64)
+#pragma unroll
+        for (int k = 0; k < 4; ++k) s4[k] += p[(size_t)(c + 16 * k) * stride];
+      for (; c < nwgb; c += 16) s4[0] += p[(size_t)c * stride];
+      s = (s4[0] + s4[1]) + (s4[2] + s4[3]);
     }
     sh[grp][threadIdx.x & 15] = s;
     __syncthreads();
@@ -403,10 +413,28 @@ __global__ __launch_bounds__(256) void cnn_reduce_kernel(
     }
     return;
   }
-  // dense bias, loss, step counter
+  // dense bias, loss, step counter: thread c loads forward workgroup c's 17 partials (one
+  // latency round; the serial 256-load chain per output took 63 us), LDS columns summed by 17
+  // threads
+  __shared__ float pf[17][257];
+  {
+    float v[17];
+#pragma unroll
+    for (int k = 0; k < 17; ++k) v[k] = 0.f;
+    for (int c = threadIdx.x; c < nwgf; c += 256)
+#pragma unroll
+      for (int k = 0; k < 17; ++k) v[k] += part_f[c * 32 + k];
+#pragma unroll
+    for (int k = 0; k < 17; ++k) pf[k][threadIdx.x] = v[k];
+  }
+  __syncthreads();
   if (threadIdx.x < 17) {
-    float s = 0.f;
-    for (int c = 0; c < nwgf; ++c) s += part_f[c * 32 + threadIdx.x];
+    float s4[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll 8
+    for (int c = 0; c < 256; c += 4)
+#pragma unroll
+      for (int k = 0; k < 4; ++k) s4[k] += pf[threadIdx.x][c + k];
+    const float s = (s4[0] + s4[1]) + (s4[2] + s4[3]);
     if (threadIdx.x < 16) {
       if (threadIdx.x < O) gbd[threadIdx.x] += s;
     } else if (loss_sum != nullptr) {
