@@ -2,7 +2,10 @@
 set -o pipefail
 export TMPDIR=/tmp
 mkdir -p gpurun_out/r4
-M=${MODEL:-mlp}; S=${SEEDS:-0,1,2,3,4}; TAG=${TAG:-a}
-timeout -k 10 ${TLIM:-1100} python -u tools/parity.py --model $M --seeds $S --batch 0 \
-  --out gpurun_out/r4/parity_${M}_${TAG}.json > gpurun_out/r4/parity_${M}_${TAG}.log 2>&1
-rc=$?; tail -12 gpurun_out/r4/parity_${M}_${TAG}.log | cut -c1-400; exit $rc
+S=${SEEDS:-0,1,2,3,4,5,6,7}; TAG=${TAG:-a}
+for M in ${MODELS:-mlp lstm}; do
+  timeout -k 10 ${TLIM:-540} python -u tools/parity.py --model $M --seeds $S --batch 0 \
+    --out gpurun_out/r4/parity_${M}_${TAG}.json > gpurun_out/r4/parity_${M}_${TAG}.log 2>&1
+  rc=$?; tail -6 gpurun_out/r4/parity_${M}_${TAG}.log | cut -c1-400
+  [ $rc -eq 0 ] || exit $rc
+done
