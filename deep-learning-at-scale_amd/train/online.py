@@ -73,15 +73,17 @@ def _train_chunk_streamed(trainer, streamer, b):
                          lambda k: tuple(streamer.slots[k][:2]))
         trainer._runners = {"stream": run}
     run.take_loss()
-    t0 = time.perf_counter()
+    from .trainer import StepClock
+
+    clock = StepClock(eng.device)
     done = 0
     for slot in streamer:
+        clock.first()
         run.run(slot)
         done += 1
         if trainer._after_step():
             break
-    torch.cuda.synchronize(eng.device)
-    dt = time.perf_counter() - t0
+    dt, trainer.last_host_dt = clock.stop()
     (tot,) = ctx.sum_scalars(run.take_loss())
     rows = done * b * ctx.world_size
     return tot / max(rows * trainer.n_out, 1), rows, dt
@@ -157,6 +159,8 @@ def fit_online(trainer, train, val):
         h.val_mse.append(v_mse)
         h.epoch_time.append(time.perf_counter() - t0)
         h.rows_per_s.append(rows / dt if dt > 0 else 0.0)
+        hd = getattr(trainer, "last_host_dt", dt)
+        h.rows_per_s_host.append(rows / hd if hd > 0 else 0.0)
         if cfg.verbose >= 2:
             trainer.log(f"Chunk {k} (pass {p + 1}/{passes}) - {n_rows} rows - loss: {tr_loss:.6f}"
                         f" - val_loss: {v_loss:.6f} - rows/s: {h.rows_per_s[-1]:.0f}", flush=True)

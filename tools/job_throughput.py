@@ -7,7 +7,8 @@ StepRunner) at the bench's per-GPU batch, next to bench.py's number for the same
 The job trains on a synthetic well-log table (CSV-free: the generator stands in for the
 ingest) through feature engineering, the time-block split, the resident dataset with
 per-step index gathers, evaluation and checkpointing; rows/s is the Trainer's own per-epoch
-figure (train steps only, history.rows_per_s) from the epochs after the first (the first
+figure (train steps only, history.rows_per_s: device-timed, CUDA events around the step
+launches; the host-clock figure is reported beside it) from the epochs after the first (the first
 holds the two eager steps and the graph capture): the MEAN over those epochs is the reported
 steady rate, with min / max and the relative spread beside it (round-3 VERDICT weak #4: the
 maximum was reported before). --default-batch runs the job's own auto-sized batch (and, for
@@ -72,6 +73,12 @@ def main():
            "job_over_bench": None if not b else job / b, "steps": out["steps"], "epochs": out["epochs"],
            "native": out["native"], "n_features": out.get("n_features"), "persistent": out.get("persistent"),
            "default_batch": a.default_batch,
+           # the same steps on the host clock (includes issue time before the first launch and
+           # the final synchronize of each epoch / stream chunk)
+           "job_rows_per_s_per_epoch_host": out["history"].get("rows_per_s_host"),
+           "job_steady_rows_per_s_host": (sum(out["history"]["rows_per_s_host"][1:]) /
+                                          max(1, len(out["history"]["rows_per_s_host"][1:])))
+           if out["history"].get("rows_per_s_host") else None,
            "data": f"synthetic well-log table {wells} wells x {steps} steps"}
     print(json.dumps(rec), flush=True)
     if a.out:
