@@ -30,13 +30,15 @@ namespace wf {
 
 namespace {
 // FRAG: dZ2 leaves in the MFMA-fragment layout of mlp2_dw2f_kernel (below) instead of [B][256]
-template <int NFT, bool FRAG>  // NFT: 16-feature tiles of dW1: 1 (Fp <= 16) or 2 (Fp <= 32)
+// STAMP (WF_DIAG builds only, WELLFLOW_MLP_STAMP=1, tools/mlp_timeline.py): lane 0 of every wave
+// writes s_memtime at 13 phase boundaries of its 5th chunk into `stamps` (results unchanged)
+template <int NFT, bool FRAG, bool STAMP = false>  // NFT: 16-feature tiles of dW1: 1 (Fp <= 16) or 2 (Fp <= 32)
 __global__ __launch_bounds__(512, 1) void mlp2_step_kernel(
     const bf16_t* __restrict__ X, int Fp, const bf16_t* __restrict__ W1, const float* __restrict__ b1,
     const bf16_t* __restrict__ W2, const float* __restrict__ b2, const float* __restrict__ w3,
     const float* __restrict__ b3, const float* __restrict__ y, float dy_scale, int B,
     const long long* __restrict__ rows, long nrows, bf16_t* __restrict__ dZ2, float* __restrict__ pred,
-    float* __restrict__ red) {
+    float* __restrict__ red, unsigned long long* __restrict__ stamps = nullptr) {
   constexpr int MT = 2, NW = 8, XB = MF_ROWS * MF_XROW;
   __shared__ __attribute__((aligned(16))) char xs[2 * XB];              // X tiles (double-buffered)
   __shared__ __attribute__((aligned(16))) char h1s[MF_ROWS * MF_H * 2];  // H1 -> dZ1 (own columns)
@@ -133,12 +135,20 @@ __global__ __launch_bounds__(512, 1) void mlp2_step_kernel(
   int par = 0;
   for (int ch = blockIdx.x; ch < nchunks; ch += gridDim.x, par ^= 1) {
     const int row0 = ch * MF_ROWS;
+    auto stamp = [&](int k) {
+      if constexpr (STAMP) {
+        if (ch == (int)blockIdx.x + 4 * (int)gridDim.x && lane == 0)
+          stamps[((size_t)blockIdx.x * NW + wid) * 16 + k] = __builtin_amdgcn_s_memtime();
+      }
+    };
+    stamp(0);
     char* xt = xs + par * XB;
     if (tid < 256)
       *reinterpret_cast<uint4*>(xt + xtile_off(tid >> 2, tid & 3)) = xv;
     else if (tid < 256 + MF_ROWS)
       ys[par][tid - 256] = yv;
     __syncthreads();  // B1: X / y staged (and, first chunk, cst)
+    stamp(1);
     if (ch + (int)gridDim.x < nchunks) prefetch(ch + gridDim.x);
 
     // ---- layer 1 (own units): H1 -> h1s; the first W2 fragments of layer 2 in flight
@@ -160,7 +170,9 @@ __global__ __launch_bounds__(512, 1) void mlp2_step_kernel(
         *reinterpret_cast<uint2*>(h1s + tile_off(16 * n + l15, u0 + 16 * m + 4 * g)) = make_uint2(p0, p1);
       }
     }
+    stamp(2);
     __syncthreads();  // B2: H1 complete
+    stamp(3);
 
     // ---- layer 2 (own units, K = 256)
 #pragma unroll
@@ -182,6 +194,7 @@ __global__ __launch_bounds__(512, 1) void mlp2_step_kernel(
         for (int m = 0; m < MT; ++m) w2r[kt % WD][m] = w2frag(m, kt + WD);
       }
     });
+    stamp(4);
     // H2 = relu(Z2 + b2) rounded to bf16 (the stored-activation numerics of the reference
     // path), kept in acc; head partials of rows 16n + l15
     float hp[4] = {0.f, 0.f, 0.f, 0.f};
@@ -208,7 +221,9 @@ __global__ __launch_bounds__(512, 1) void mlp2_step_kernel(
 #pragma unroll
       for (int n = 0; n < 4; ++n) hred[16 * n + l15][wid] = hp[n];
     }
+    stamp(5);
     __syncthreads();  // B3: head partials complete
+    stamp(6);
 
     // ---- prediction, dy, loss of rows 16n + l15 (every wave needs dy); wave 0 lane group g
     // owns row 16g + l15's outputs
@@ -251,7 +266,9 @@ __global__ __launch_bounds__(512, 1) void mlp2_step_kernel(
       acc4(P_DW3, m, s3);
       acc4(P_DB2, m, s2);
     }
+    stamp(7);
     __syncthreads();  // B4: dZ2 complete
+    stamp(8);
 
     if constexpr (FRAG) {
       // ---- dZ2 copy-out as dW2 A fragments: fragment (s, b) = 32 rows x 16 units, lane
@@ -281,6 +298,7 @@ __global__ __launch_bounds__(512, 1) void mlp2_step_kernel(
               *reinterpret_cast<const uint4*>(zs + tile_off(r, 8 * c));
       }
     }
+    stamp(9);
     // ---- dH1^T (own units k, K = 256 output units) = W2^T dZ2^T
 #pragma unroll
     for (int m = 0; m < MT; ++m)
@@ -297,6 +315,7 @@ __global__ __launch_bounds__(512, 1) void mlp2_step_kernel(
         for (int n = 0; n < 4; ++n)
           acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wt[m][kt], zb[n], acc[m][n], 0, 0, 0);
     }
+    stamp(10);
     w2first();  // the next chunk's first layer-2 fragments
     // ---- dZ1 = dH1 * [H1 > 0] over the same 8 bytes of h1s; db1 partials
 #pragma unroll
@@ -323,6 +342,7 @@ __global__ __launch_bounds__(512, 1) void mlp2_step_kernel(
       }
       acc4(P_DB1, m, s1);
     }
+    stamp(11);
     // the dW1 fragments read other lanes' dZ1 (same wave): complete the writes first
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_wave_barrier();
@@ -357,6 +377,7 @@ __global__ __launch_bounds__(512, 1) void mlp2_step_kernel(
     // h1s columns are rewritten by this wave's next layer 1: its dW1 reads must be complete
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_wave_barrier();
+    stamp(12);
   }
 
   // ---- batch sums -> copy blockIdx % kMlpRedCopies of the scratch; dW1 -> this workgroup's row
@@ -559,6 +580,17 @@ bool launch_mlp2_step(const bf16_t* X, int Fp, const bf16_t* W1, const float* b1
   if (B <= 0 || Fp > 32 || Fp % 8 != 0 || red == nullptr || !mlp_bwd8()) return false;
   if (dz_frag && B % MF_ROWS != 0) return false;
   const int grid = mlp2_train_grid(B);  // the dW1 rows mlp2_reduce sums
+#ifdef WF_DIAG
+  // phase stamps (tools/mlp_timeline.py): into dW2 slab rows 200.. of the scratch (unused by a
+  // step of <= 200 dW2 ranges)
+  static const bool stamp = std::getenv("WELLFLOW_MLP_STAMP") != nullptr;
+  if (stamp && Fp <= 16 && dz_frag) {
+    hipLaunchKernelGGL((mlp2_step_kernel<1, true, true>), dim3(grid), dim3(512), 0, s, X, Fp, W1, b1, W2, b2, w3, b3, y,
+                       dy_scale, B, rows, nrows, dZ2, pred, red,
+                       reinterpret_cast<unsigned long long*>(red + kMlpRedSlab2Off + 200L * 65536));
+    return true;
+  }
+#endif
 #define WF_STEP(NFT, FR)                                                                                            \
   hipLaunchKernelGGL((mlp2_step_kernel<NFT, FR>), dim3(grid), dim3(512), 0, s, X, Fp, W1, b1, W2, b2, w3, b3, y, \
                      dy_scale, B, rows, nrows, dZ2, pred, red)
