@@ -30,8 +30,8 @@ namespace wf {
 
 namespace {
 // FRAG: dZ2 leaves in the MFMA-fragment layout of mlp2_dw2f_kernel (below) instead of [B][256]
-// STAMP (WF_DIAG builds only, WELLFLOW_MLP_STAMP=1, tools/mlp_timeline.py): lane 0 of every wave
-// writes s_memtime at 13 phase boundaries of its 5th chunk into `stamps` (results unchanged)
+// STAMP (WELLFLOW_MLP_STAMP=1, tools/mlp_timeline.py): lane 0 of every wave writes s_memtime at
+// 13 phase boundaries of its 5th chunk into `stamps` (results unchanged)
 template <int NFT, bool FRAG, bool STAMP = false>  // NFT: 16-feature tiles of dW1: 1 (Fp <= 16) or 2 (Fp <= 32)
 __global__ __launch_bounds__(512, 1) void mlp2_step_kernel(
     const bf16_t* __restrict__ X, int Fp, const bf16_t* __restrict__ W1, const float* __restrict__ b1,
@@ -580,9 +580,8 @@ bool launch_mlp2_step(const bf16_t* X, int Fp, const bf16_t* W1, const float* b1
   if (B <= 0 || Fp > 32 || Fp % 8 != 0 || red == nullptr || !mlp_bwd8()) return false;
   if (dz_frag && B % MF_ROWS != 0) return false;
   const int grid = mlp2_train_grid(B);  // the dW1 rows mlp2_reduce sums
-#ifdef WF_DIAG
-  // phase stamps (tools/mlp_timeline.py): into dW2 slab rows 200.. of the scratch (unused by a
-  // step of <= 200 dW2 ranges)
+  // phase stamps (tools/mlp_timeline.py; results unchanged, so not a WF_DIAG-only switch):
+  // into dW2 slab rows 200.. of the scratch (unused by a step of <= 200 dW2 ranges)
   static const bool stamp = std::getenv("WELLFLOW_MLP_STAMP") != nullptr;
   if (stamp && Fp <= 16 && dz_frag) {
     hipLaunchKernelGGL((mlp2_step_kernel<1, true, true>), dim3(grid), dim3(512), 0, s, X, Fp, W1, b1, W2, b2, w3, b3, y,
@@ -590,7 +589,6 @@ bool launch_mlp2_step(const bf16_t* X, int Fp, const bf16_t* W1, const float* b1
                        reinterpret_cast<unsigned long long*>(red + kMlpRedSlab2Off + 200L * 65536));
     return true;
   }
-#endif
 #define WF_STEP(NFT, FR)                                                                                            \
   hipLaunchKernelGGL((mlp2_step_kernel<NFT, FR>), dim3(grid), dim3(512), 0, s, X, Fp, W1, b1, W2, b2, w3, b3, y, \
                      dy_scale, B, rows, nrows, dZ2, pred, red)

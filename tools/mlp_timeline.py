@@ -1,8 +1,8 @@
 #!/usr/bin/env python3
 """Per-phase timeline of the one-launch MLP training step (csrc/mlp_step.hip mlp2_step_kernel):
 lane 0 of every wave stamps s_memtime (shader cycles) at 13 phase boundaries of its 5th
-64-row chunk. Needs a WF_DIAG build (WELLFLOW_DIAG_BUILD=<n> python -c "import
-__graft_entry__ as g; g.build()") and WELLFLOW_MLP_STAMP=1; results are unchanged.
+64-row chunk when WELLFLOW_MLP_STAMP=1 (the stamped variant is built into the production
+library: it changes no result, it only writes timestamps into an unused scratch region).
 
     WELLFLOW_MLP_STAMP=1 python tools/mlp_timeline.py [--batch 262144]
 
@@ -29,10 +29,6 @@ def main():
 
     from wellflow.data.synth import synth_tabular_batch
     from wellflow.models.mlp import NativeMLP, init_mlp_flat
-    from wellflow.ops.native import lib
-
-    if not lib().diag_build():
-        raise SystemExit("needs a WF_DIAG build (WELLFLOW_DIAG_BUILD=<n>)")
     dev = torch.device("cuda")
     eng = NativeMLP(a.features, (256, 256), a.batch, device=dev)
     eng.params.copy_(init_mlp_flat(a.features, (256, 256), seed=0).to(dev))
