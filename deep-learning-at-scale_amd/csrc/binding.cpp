@@ -636,6 +636,30 @@ bool mlp2_forward(const at::Tensor& X, int64_t Fp, const at::Tensor& W1, const a
                              opt_ptr<float>(red, at::kFloat, "red", wf::kMlpRedFloats));
 }
 
+// head forward + MSE + head weight gradient in one pass over H (elementwise.hip); false = shape
+// not covered (the caller runs head_fwd + head_bwd_w)
+bool head_fwd_bwd(const at::Tensor& Hm, int64_t ldh, int64_t B, int64_t Hd, const at::Tensor& w, const at::Tensor& b0,
+                  const at::Tensor& target, const at::Tensor& pred, const at::Tensor& dy,
+                  c10::optional<at::Tensor> loss_sum, double dy_scale, const at::Tensor& dw, c10::optional<at::Tensor> db) {
+  check_head_h(Hm, ldh, B, Hd);
+  TORCH_CHECK(Hd % 8 == 0 && ldh % 8 == 0, "head: Hd and ldh must be multiples of 8");
+  check_t(w, at::kFloat, "w");
+  check_extent(w, Hd, "w");
+  check_t(b0, at::kFloat, "b0");
+  check_t(target, at::kFloat, "target");
+  check_extent(target, B, "target");
+  check_t(pred, at::kFloat, "pred");
+  check_extent(pred, B, "pred");
+  check_t(dy, at::kFloat, "dy");
+  check_extent(dy, B, "dy");
+  check_t(dw, at::kFloat, "dw");
+  check_extent(dw, Hd, "dw");
+  const c10::hip::OptionalHIPGuardMasqueradingAsCUDA guard(Hm.device());
+  return wf::launch_head_fwd_bwd(bfp(Hm), ldh, (int)B, (int)Hd, fp(w), fp(b0), fp(target), fp(pred), fp(dy),
+                                 opt_ptr<float>(loss_sum, at::kFloat, "loss_sum", 1), (float)dy_scale, fp(dw),
+                                 opt_ptr<float>(db, at::kFloat, "db", 1), cur_stream());
+}
+
 void head_bwd_w(const at::Tensor& Hm, int64_t ldh, int64_t B, int64_t Hd, const at::Tensor& dy,
                 const at::Tensor& dw, c10::optional<at::Tensor> db) {
   check_head_h(Hm, ldh, B, Hd);
@@ -960,6 +984,7 @@ PYBIND11_MODULE(_C, m) {
   WF_DEF(lstm_pack_weights);
   WF_DEF(head_fwd);
   WF_DEF(head_bwd_w);
+  WF_DEF(head_fwd_bwd);
   WF_DEF(head_bwd_x);
   WF_DEF(loss);
   WF_DEF(adam);

@@ -100,6 +100,103 @@ void launch_head_fwd(const bf16_t* Hm, long ldh, int B, int Hd, const float* w, 
 #undef HEAD_FWD
 }
 
+// Regression head forward + MSE + head weight gradient in ONE pass over H (the LSTM's last
+// hidden state): a row group of LPR lanes (LPR * 8 == Hd: each lane holds 8 columns of the row)
+// forms pred, dy = s (pred - y) and the loss, then every lane adds dy * h to its 8 columns of
+// dw — the h values are still in its registers, so head_bwd_w's second read of H and its
+// launch disappear. Four rows per group are in flight at once (independent loads).
+template <int LPR>
+__global__ __launch_bounds__(256) void head_fwd_bwd_kernel(const bf16_t* __restrict__ Hm, long ldh, int B, int Hd,
+                                                           const float* __restrict__ w, const float* __restrict__ b0,
+                                                           const float* __restrict__ target, float* __restrict__ pred,
+                                                           float* __restrict__ dy, float* __restrict__ loss_sum,
+                                                           float dy_scale, float* __restrict__ dw, float* __restrict__ db) {
+  constexpr int RPB = 256 / LPR, U = 4;
+  __shared__ float red[4];
+  __shared__ float dws[RPB][LPR * 8];
+  const int sub = threadIdx.x % LPR, grp = threadIdx.x / LPR;
+  const float bias = b0[0];
+  float wv[8], dwp[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    wv[e] = w[sub * 8 + e];
+    dwp[e] = 0.f;
+  }
+  float lsum = 0.f, dsum = 0.f;
+  for (int rb = blockIdx.x * RPB * U; rb < B; rb += gridDim.x * RPB * U) {
+    bf16x8 v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int b = rb + u * RPB + grp;
+      v[u] = b < B ? *reinterpret_cast<const bf16x8*>(Hm + (size_t)b * ldh + sub * 8) : bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int b = rb + u * RPB + grp;
+      float h[8], acc = 0.f;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        h[e] = bf2f((bf16_t)v[u][e]);
+        acc += h[e] * wv[e];
+      }
+#pragma unroll
+      for (int o = LPR / 2; o > 0; o >>= 1) acc += __shfl_xor(acc, o, 64);
+      if (b < B) {
+        const float p = acc + bias, diff = p - target[b], g = dy_scale * diff;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) dwp[e] += g * h[e];
+        if (sub == 0) {
+          pred[b] = p;
+          dy[b] = g;
+          lsum += diff * diff;
+          dsum += g;
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int e = 0; e < 8; ++e) dws[grp][sub * 8 + e] = dwp[e];
+  __syncthreads();
+  for (int col = threadIdx.x; col < Hd; col += 256) {
+    float t = 0.f;
+#pragma unroll
+    for (int q = 0; q < RPB; ++q) t += dws[q][col];
+    if (t != 0.f) atomicAdd(dw + col, t);
+  }
+  if (loss_sum != nullptr) {
+    const float t = block_sum<256>(lsum, red);
+    if (threadIdx.x == 0) atomicAdd(loss_sum, t);
+  }
+  if (db != nullptr) {
+    const float t = block_sum<256>(dsum, red);
+    if (threadIdx.x == 0) atomicAdd(db, t);
+  }
+}
+
+bool launch_head_fwd_bwd(const bf16_t* Hm, long ldh, int B, int Hd, const float* w, const float* b0,
+                         const float* target, float* pred, float* dy, float* loss_sum, float dy_scale, float* dw,
+                         float* db, hipStream_t s) {
+  const int lpr = lanes_per_row(Hd);
+  if (lpr * 8 != Hd || target == nullptr || dy == nullptr || dw == nullptr) return false;
+  const int rows_per_block = (256 / lpr) * 4;
+  int grid = (B + rows_per_block - 1) / rows_per_block;
+  if (grid > 128) grid = 128;  // per-column atomics per block (head_bwd_w's measured cap)
+#define HEAD_FB(L)                                                                                              \
+  hipLaunchKernelGGL(head_fwd_bwd_kernel<L>, dim3(grid), dim3(256), 0, s, Hm, ldh, B, Hd, w, b0, target, pred, dy, \
+                     loss_sum, dy_scale, dw, db)
+  switch (lpr) {
+    case 1: HEAD_FB(1); break;
+    case 2: HEAD_FB(2); break;
+    case 4: HEAD_FB(4); break;
+    case 8: HEAD_FB(8); break;
+    case 16: HEAD_FB(16); break;
+    case 32: HEAD_FB(32); break;
+    default: HEAD_FB(64); break;
+  }
+#undef HEAD_FB
+  return true;
+}
+
 // Column-chunk x row-group layout shared by the two head backward kernels: a thread owns
 // 8 consecutive units (16-B loads/stores) of rows rg, rg + RG, ...; partial column sums
 // are combined through LDS and leave the block with one atomic per column.

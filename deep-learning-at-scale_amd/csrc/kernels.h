@@ -169,6 +169,10 @@ void launch_cnn_reduce(const float* part_wd, const float* part_wc, const float* 
 void launch_head_fwd(const bf16_t* Hm, long ldh, int B, int Hd, const float* w, const float* b0,
                      const float* target, float* pred, float* dy, float* loss_sum, float dy_scale,
                      hipStream_t s);
+// head forward + MSE + dw / db in one pass (Hd = 8 * a power of two <= 512); false = not covered
+bool launch_head_fwd_bwd(const bf16_t* Hm, long ldh, int B, int Hd, const float* w, const float* b0,
+                         const float* target, float* pred, float* dy, float* loss_sum, float dy_scale, float* dw,
+                         float* db, hipStream_t s);
 void launch_head_bwd_w(const bf16_t* Hm, long ldh, int B, int Hd, const float* dy, float* dw,
                        float* db, hipStream_t s);
 void launch_head_bwd_x(const bf16_t* Hm, long ldh, int B, int Hd, const float* dy, const float* w,

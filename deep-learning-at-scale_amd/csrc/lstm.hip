@@ -162,6 +162,7 @@ void launch_lstm_fwd_step(int t, bf16_t* XH, const bf16_t* Wp, bf16_t* Cst, bf16
 // lane, given dh for them: reads the lane's fragment-native S / C / dc-carry slots with
 // 16-B vector accesses, updates the carry and writes the gate gradients into DG[t]
 // (row-major, dg_col order: it is the next GEMM's A operand and the dW GEMM's M side).
+template <bool FIRST = false>  // FIRST: step T-1, the dc carry starts at zero (not read)
 __device__ __forceinline__ void cell_bwd4(int t, int mrow0, int u, int lane, const float (&dh)[4],
                                           const bf16_t* __restrict__ Cst,
                                           const bf16_t* __restrict__ S, bf16_t* __restrict__ DG,
@@ -179,7 +180,7 @@ __device__ __forceinline__ void cell_bwd4(int t, int mrow0, int u, int lane, con
   const float4 p4 = make_float4(__uint_as_float(p2.x << 16), __uint_as_float(p2.x & 0xffff0000u),
                                 __uint_as_float(p2.y << 16), __uint_as_float(p2.y & 0xffff0000u));
   float4* dcp = reinterpret_cast<float4*>(dcarry + blk * 256 + lane * 4);
-  const float4 k4 = *dcp;
+  const float4 k4 = FIRST ? make_float4(0.f, 0.f, 0.f, 0.f) : *dcp;
   const float pv[4] = {p4.x, p4.y, p4.z, p4.w};
   const float kv[4] = {k4.x, k4.y, k4.z, k4.w};
   float nk[4];
@@ -215,14 +216,13 @@ __global__ void lstm_bwd_last_kernel(const bf16_t* __restrict__ Cst, const bf16_
     const int lane = idx & 63;
     const long blk = idx >> 6;
     const int mrow0 = (int)(blk / ub) * 16, u = (int)(blk % ub) * 16 + (lane & 15);
-    *reinterpret_cast<float4*>(dcarry + blk * 256 + lane * 4) = make_float4(0.f, 0.f, 0.f, 0.f);
     float dh[4];
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int m = mrow0 + 4 * (lane >> 4) + r;
       dh[r] = m < d.B ? dy[m] * w_out[u] : 0.f;
     }
-    cell_bwd4(d.T - 1, mrow0, u, lane, dh, Cst, S, DG, dcarry, d);
+    cell_bwd4<true>(d.T - 1, mrow0, u, lane, dh, Cst, S, DG, dcarry, d);
   }
 }
 

@@ -367,14 +367,20 @@ class NativeLSTM:
         self._forward_steps(B)
         hT = self._hT(B)
         y = y.contiguous().float()
-        if self.loss_kind == "mse":  # head + MSE + dy fused in one kernel
-            C.head_fwd(hT, lay.KA, B, self.H, w_out, b_out, y, self.pred, self.dy,
-                       ls, 2.0 * float(grad_scale))
-        else:
-            C.head_fwd(hT, lay.KA, B, self.H, w_out, b_out, None, self.pred, None, None, 0.0)
-            C.loss(1, self.pred, y, B, 1, self.clip, float(grad_scale), ls, None,
-                   self.dy, None)
-        C.head_bwd_w(hT, lay.KA, B, self.H, self.dy, gw_out, gb_out)
+        # head + MSE + dy + the head's weight gradient in ONE pass over h_T (elementwise.hip
+        # head_fwd_bwd_kernel) when the shape allows, else the forward kernel + head_bwd_w
+        fused_head = (self.loss_kind == "mse" and
+                      C.head_fwd_bwd(hT, lay.KA, B, self.H, w_out, b_out, y, self.pred, self.dy, ls,
+                                     2.0 * float(grad_scale), gw_out, gb_out))
+        if not fused_head:
+            if self.loss_kind == "mse":  # head + MSE + dy fused in one kernel
+                C.head_fwd(hT, lay.KA, B, self.H, w_out, b_out, y, self.pred, self.dy,
+                           ls, 2.0 * float(grad_scale))
+            else:
+                C.head_fwd(hT, lay.KA, B, self.H, w_out, b_out, None, self.pred, None, None, 0.0)
+                C.loss(1, self.pred, y, B, 1, self.clip, float(grad_scale), ls, None,
+                       self.dy, None)
+            C.head_bwd_w(hT, lay.KA, B, self.H, self.dy, gw_out, gb_out)
         # BPTT chain (high-priority stream) + dWcat = sum_{t,b} dG_t[b]^T [x_t | 1 | h_{t-1}][b]
         # as split-K GEMM chunks on a low-priority stream, overlapped with the chain.
         K = self.T * B
