@@ -32,7 +32,10 @@ namespace {
 // FRAG: dZ2 leaves in the MFMA-fragment layout of mlp2_dw2f_kernel (below) instead of [B][256]
 // STAMP (WELLFLOW_MLP_STAMP=1, tools/mlp_timeline.py): lane 0 of every wave writes s_memtime at
 // 13 phase boundaries of its 5th chunk into `stamps` (results unchanged)
-template <int NFT, bool FRAG, bool STAMP = false>  // NFT: 16-feature tiles of dW1: 1 (Fp <= 16) or 2 (Fp <= 32)
+// EARLY: the next chunk's X / y tile is staged into the other LDS buffer before the dZ2
+// barrier of this chunk, so that barrier also publishes it: three workgroup barriers per chunk
+// instead of four (WELLFLOW_MLP_STEP_B4=1: the four-barrier order, identical results)
+template <int NFT, bool FRAG, bool STAMP = false, bool EARLY = true>  // NFT: 16-feature tiles of dW1: 1 (Fp <= 16) or 2 (Fp <= 32)
 __global__ __launch_bounds__(512, 1) void mlp2_step_kernel(
     const bf16_t* __restrict__ X, int Fp, const bf16_t* __restrict__ W1, const float* __restrict__ b1,
     const bf16_t* __restrict__ W2, const float* __restrict__ b2, const float* __restrict__ w3,
@@ -130,7 +133,19 @@ __global__ __launch_bounds__(512, 1) void mlp2_step_kernel(
     }
   };
   const int nchunks = (B + MF_ROWS - 1) / MF_ROWS;
+  auto stage = [&](int p) {  // the prefetched chunk -> X / y buffer p
+    if (tid < 256)
+      *reinterpret_cast<uint4*>(xs + p * XB + xtile_off(tid >> 2, tid & 3)) = xv;
+    else if (tid < 256 + MF_ROWS)
+      ys[p][tid - 256] = yv;
+  };
   if ((int)blockIdx.x < nchunks) prefetch(blockIdx.x);
+  if constexpr (EARLY) {
+    // first chunk staged here (its barrier also publishes cst), the second one prefetched
+    stage(0);
+    __syncthreads();
+    if ((int)blockIdx.x + (int)gridDim.x < nchunks) prefetch(blockIdx.x + gridDim.x);
+  }
   w2first();
   int par = 0;
   for (int ch = blockIdx.x; ch < nchunks; ch += gridDim.x, par ^= 1) {
@@ -143,13 +158,14 @@ __global__ __launch_bounds__(512, 1) void mlp2_step_kernel(
     };
     stamp(0);
     char* xt = xs + par * XB;
-    if (tid < 256)
-      *reinterpret_cast<uint4*>(xt + xtile_off(tid >> 2, tid & 3)) = xv;
-    else if (tid < 256 + MF_ROWS)
-      ys[par][tid - 256] = yv;
-    __syncthreads();  // B1: X / y staged (and, first chunk, cst)
+    if constexpr (!EARLY) {
+      stage(par);
+      __syncthreads();  // B1: X / y staged (and, first chunk, cst)
+    }
     stamp(1);
-    if (ch + (int)gridDim.x < nchunks) prefetch(ch + gridDim.x);
+    if constexpr (!EARLY) {
+      if (ch + (int)gridDim.x < nchunks) prefetch(ch + gridDim.x);
+    }
 
     // ---- layer 1 (own units): H1 -> h1s; the first W2 fragments of layer 2 in flight
     f32x4 acc[MT][4];
@@ -266,9 +282,17 @@ __global__ __launch_bounds__(512, 1) void mlp2_step_kernel(
       acc4(P_DW3, m, s3);
       acc4(P_DB2, m, s2);
     }
+    // EARLY: the next chunk's X / y into the other buffer (its last readers — layer 1 and dW1
+    // of the previous chunk — are behind this chunk's B2), published by B4
+    if constexpr (EARLY) {
+      if (ch + (int)gridDim.x < nchunks) stage(par ^ 1);
+    }
     stamp(7);
-    __syncthreads();  // B4: dZ2 complete
+    __syncthreads();  // B4: dZ2 complete (EARLY: and the next chunk's X / y staged)
     stamp(8);
+    if constexpr (EARLY) {
+      if (ch + 2 * (int)gridDim.x < nchunks) prefetch(ch + 2 * gridDim.x);
+    }
 
     if constexpr (FRAG) {
       // ---- dZ2 copy-out as dW2 A fragments: fragment (s, b) = 32 rows x 16 units, lane
@@ -587,6 +611,15 @@ bool launch_mlp2_step(const bf16_t* X, int Fp, const bf16_t* W1, const float* b1
     hipLaunchKernelGGL((mlp2_step_kernel<1, true, true>), dim3(grid), dim3(512), 0, s, X, Fp, W1, b1, W2, b2, w3, b3, y,
                        dy_scale, B, rows, nrows, dZ2, pred, red,
                        reinterpret_cast<unsigned long long*>(red + kMlpRedSlab2Off + 200L * 65536));
+    return true;
+  }
+  static const bool b4 = [] {
+    const char* e = std::getenv("WELLFLOW_MLP_STEP_B4");
+    return e != nullptr && e[0] == '1';
+  }();
+  if (b4 && Fp <= 16 && dz_frag) {  // A/B: the four-barrier chunk order
+    hipLaunchKernelGGL((mlp2_step_kernel<1, true, false, false>), dim3(grid), dim3(512), 0, s, X, Fp, W1, b1, W2, b2,
+                       w3, b3, y, dy_scale, B, rows, nrows, dZ2, pred, red, nullptr);
     return true;
   }
 #define WF_STEP(NFT, FR)                                                                                            \
