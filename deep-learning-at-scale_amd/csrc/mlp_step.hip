@@ -534,19 +534,10 @@ __global__ __launch_bounds__(512, 1) void mlp2_dw2f_kernel(const bf16_t* __restr
 #pragma unroll
     for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  const int last = nch - 1;
-#pragma unroll
-  for (int k = 0; k < DW2F_SLOTS - 1; ++k) issue(min(k, last), k);
-  for (int c = 0; c < nch; ++c) {
-    const int slot = c & (DW2F_SLOTS - 1);
-    dma_wait(std::integral_constant<int, DW2F_SLOTS - 2>{});  // chunk c's pieces (this wave) landed
-    __builtin_amdgcn_s_barrier();                              // ... every wave's; slot c - 1 free
-    asm volatile("" ::: "memory");
-    issue(min(c + DW2F_SLOTS - 1, last), (c + DW2F_SLOTS - 1) & (DW2F_SLOTS - 1));
-    const char* st = smem + slot * DW2F_SLOT;
+  // H1 of a chunk (both 32-row steps) -> B fragments hb[step][nb]
+  auto recompute = [&](const char* st, bf16x8 (&hb)[2][2]) {
 #pragma unroll
     for (int s2 = 0; s2 < 2; ++s2) {
-      bf16x8 hb[2];
       bf16x8 xf[2];
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
@@ -562,16 +553,52 @@ __global__ __launch_bounds__(512, 1) void mlp2_dw2f_kernel(const bf16_t* __restr
         const unsigned p2 = pk_bf16(fmaxf(c1[0] + bias[nb], 0.f), fmaxf(c1[1] + bias[nb], 0.f));
         const unsigned p3 = pk_bf16(fmaxf(c1[2] + bias[nb], 0.f), fmaxf(c1[3] + bias[nb], 0.f));
         typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
-        hb[nb] = __builtin_bit_cast(bf16x8, (u32x4_t{p0, p1, p2, p3}));
-      }
-#pragma unroll
-      for (int mb = 0; mb < 8; ++mb) {
-        const bf16x8 a = *reinterpret_cast<const bf16x8*>(st + (s2 * 16 + 8 * wm + mb) * 1024 + lane * 16);
-#pragma unroll
-        for (int nb = 0; nb < 2; ++nb) acc[mb][nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, hb[nb], acc[mb][nb], 0, 0, 0);
+        hb[s2][nb] = __builtin_bit_cast(bf16x8, (u32x4_t{p0, p1, p2, p3}));
       }
     }
+  };
+  auto dw = [&](const char* st, const bf16x8 (&hb)[2][2]) {
+    // all 16 A fragments of the chunk requested before the first MFMA (one LDS latency, not 8)
+    bf16x8 a[2][8];
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+      for (int mb = 0; mb < 8; ++mb)
+        a[s2][mb] = *reinterpret_cast<const bf16x8*>(st + (s2 * 16 + 8 * wm + mb) * 1024 + lane * 16);
+    __builtin_amdgcn_sched_barrier(0);  // (the scheduler would pair each read with its MFMAs)
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+      for (int mb = 0; mb < 8; ++mb)
+#pragma unroll
+        for (int nb = 0; nb < 2; ++nb)
+          acc[mb][nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[s2][mb], hb[s2][nb], acc[mb][nb], 0, 0, 0);
+  };
+  // Software pipeline: chunk c + 1's H1 is rebuilt while chunk c's dW MFMAs run (independent
+  // work in one wave: the rebuild's VALU epilogue issues in the MFMAs' shadow). Chunks c + 2,
+  // c + 3 are in flight; chunk c + 3 goes into chunk c - 1's slot, free after this barrier.
+  const int last = nch - 1;
+#pragma unroll
+  for (int k = 0; k < DW2F_SLOTS - 1; ++k) issue(min(k, last), k);
+  dma_wait(std::integral_constant<int, DW2F_SLOTS - 2>{});  // chunk 0 (this wave's pieces)
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+  bf16x8 hA[2][2], hB[2][2];
+  recompute(smem, hA);
+  auto body = [&](int c, bf16x8 (&hcur)[2][2], bf16x8 (&hnext)[2][2]) {
+    dma_wait(std::integral_constant<int, DW2F_SLOTS - 3>{});  // chunk c + 1 landed (this wave)
+    __builtin_amdgcn_s_barrier();                              // ... every wave's; slot c - 1 free
+    asm volatile("" ::: "memory");
+    issue(min(c + DW2F_SLOTS - 1, last), (c + DW2F_SLOTS - 1) & (DW2F_SLOTS - 1));
+    if (c + 1 < nch) recompute(smem + ((c + 1) & (DW2F_SLOTS - 1)) * DW2F_SLOT, hnext);
+    dw(smem + (c & (DW2F_SLOTS - 1)) * DW2F_SLOT, hcur);
+  };
+  int c = 0;
+  for (; c + 2 <= nch; c += 2) {
+    body(c, hA, hB);
+    body(c + 1, hB, hA);
   }
+  if (c < nch) body(c, hA, hB);
   wait_vmcnt<0>();  // the clamped fetches past the range must land before the workgroup ends
   // out unit 128 wm + 16 mb + 4g + r, in unit n0 + 16 nb + l15: plain stores into this range's
   // slab row (the reduce sums the rows); past the slab, atomics into a dW2 copy
