@@ -148,3 +148,43 @@ def test_cnn_dropout_mask_mirror_properties():
     for other in (cnn_dropout_mask(7, 1, 512, 36, 112), cnn_dropout_mask(8, 0, 512, 36, 112)):
         agree = (m0 == other).float().mean().item()
         assert 0.45 < agree < 0.55, agree
+
+
+def test_mlp_recompute_row_permutation_feeds_dw_fragment():
+    """Index algebra of csrc/mlp_step.hip mlp2_dw2f_kernel, checked on the CPU with the MFMA
+    16x16x32 lane conventions (A: lane (i, g) holds A[i][8g + j]; B: lane (n, g) holds
+    B[8g + j][n]; C: lane (n, g) holds C[4g + r][n]): the recompute's A operand takes row
+    slot i from local row 8 (i >> 2) + 4h + (i & 3), so output lane (n, g), accumulator r of
+    half h holds H1[row 8g + 4h + r][unit n] — exactly the B fragment slot j = 4h + r of the
+    dW MFMA (K = rows 8g + j). Also the dZ2 fragment layout round trip."""
+    import numpy as np
+
+    rng = np.random.default_rng(0)
+    X = rng.standard_normal((32, 32)).astype(np.float32)   # 32 rows of one step x 32 features
+    W1 = rng.standard_normal((16, 32)).astype(np.float32)  # 16 units
+    H1 = X @ W1.T                                           # [row][unit]
+    bfrag = np.zeros((16, 4, 8), np.float32)                # B fragment: [lane n][g][j]
+    for h in range(2):
+        A = np.stack([X[8 * (i >> 2) + 4 * h + (i & 3)] for i in range(16)])  # row slot i
+        C = A @ W1.T                                        # C[slot][unit]
+        for n in range(16):
+            for g in range(4):
+                for r in range(4):
+                    bfrag[n, g, 4 * h + r] = C[4 * g + r, n]
+    for n in range(16):
+        for g in range(4):
+            for j in range(8):
+                assert bfrag[n, g, j] == H1[8 * g + j, n]
+    # dZ2 fragment layout: element ((S * 16 + b) * 64 + 16 g + l) * 8 + j = row 32 S + 8 g + j,
+    # unit 16 b + l; the test helper's inverse permutation recovers [B][256]
+    B = 64
+    Z = rng.standard_normal((B, 256)).astype(np.float32)
+    F = np.zeros(B * 256, np.float32)
+    for S in range(B // 32):
+        for b in range(16):
+            for g in range(4):
+                for l in range(16):
+                    for j in range(8):
+                        F[((S * 16 + b) * 64 + 16 * g + l) * 8 + j] = Z[32 * S + 8 * g + j, 16 * b + l]
+    back = F.reshape(B // 32, 16, 4, 16, 8).transpose(0, 2, 4, 1, 3).reshape(B, 256)
+    assert np.array_equal(back, Z)
