@@ -13,11 +13,14 @@
 //   dH1^T     = W2^T dZ2^T                    own units k, K = all of dZ2        64 MFMA
 //   dZ1       = dH1 * [H1 > 0]                in place over the wave's own H1 columns
 //   dW1^T    += dZ1^T X                       ds_read_b64_tr_b16 fragments     2 NFT MFMA
-// W1 rows, W2 rows (layer 2 A operand) and W2^T rows (dH1 A operand) stay in registers for the
-// whole launch; b1 / b2 / w3 are read from LDS. Four workgroup barriers per chunk (X staged,
-// H1 complete, head partials complete, dZ2 complete). Batch sums go to the spread-reduction
-// scratch exactly as the two kernels' did (kMlpRedCopies copies + the per-workgroup dW1 rows),
-// so mlp2_dw2 and mlp2_reduce run unchanged after it.
+// W1 rows and W2^T rows (dH1 A operand) stay in registers for the whole launch; layer 2's A
+// operand (W2 rows) streams from L2 by buffer loads, the first K steps requested a chunk early
+// (both W2 images would not fit the 256-VGPR budget of two waves per SIMD); b1 / b2 / w3 are
+// read from LDS. Three workgroup barriers per chunk (H1 complete, head partials complete, dZ2
+// complete — the next chunk's X / y tile is staged before the last one, which publishes it).
+// Batch sums go to the spread-reduction scratch as the two kernels' did (kMlpRedCopies copies +
+// the per-workgroup dW1 rows); dZ2 leaves either row-major (for mlp2_dw2) or in the fragment
+// layout of mlp2_dw2f_kernel below; mlp2_reduce sums everything into the gradients.
 #include <cstdlib>
 #include <type_traits>
 
