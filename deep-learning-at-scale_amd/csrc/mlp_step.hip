@@ -35,14 +35,11 @@ namespace {
 // FRAG: dZ2 leaves in the MFMA-fragment layout of mlp2_dw2f_kernel (below) instead of [B][256]
 // STAMP (WELLFLOW_MLP_STAMP=1, tools/mlp_timeline.py): lane 0 of every wave writes s_memtime at
 // 13 phase boundaries of its 5th chunk into `stamps` (results unchanged)
-// EARLY: the next chunk's X / y tile is staged into the other LDS buffer before the dZ2
-// barrier of this chunk, so that barrier also publishes it: three workgroup barriers per chunk
-// instead of four (WELLFLOW_MLP_STEP_B4=1: the four-barrier order, identical results)
-template <int NFT, bool FRAG, bool STAMP = false, bool EARLY = true>  // NFT: 16-feature tiles of dW1: 1 (Fp <= 16) or 2 (Fp <= 32)
+template <int NFT, bool FRAG, bool STAMP = false>  // NFT: 16-feature tiles of dW1: 1 (Fp <= 16) or 2 (Fp <= 32)
 __global__ __launch_bounds__(512, 1) void mlp2_step_kernel(
     const bf16_t* __restrict__ X, int Fp, const bf16_t* __restrict__ W1, const float* __restrict__ b1,
-    const bf16_t* __restrict__ W2, const float* __restrict__ b2, const float* __restrict__ w3,
-    const float* __restrict__ b3, const float* __restrict__ y, float dy_scale, int B,
+    const bf16_t* __restrict__ W2, const bf16_t* __restrict__ W2T, const float* __restrict__ b2,
+    const float* __restrict__ w3, const float* __restrict__ b3, const float* __restrict__ y, float dy_scale, int B,
     const long long* __restrict__ rows, long nrows, bf16_t* __restrict__ dZ2, float* __restrict__ pred,
     float* __restrict__ red, unsigned long long* __restrict__ stamps = nullptr) {
   constexpr int MT = 2, NW = 8, XB = MF_ROWS * MF_XROW;
@@ -65,43 +62,39 @@ __global__ __launch_bounds__(512, 1) void mlp2_step_kernel(
   const int tq = l15 >> 2, tp = lane & 3;  // ds_read_b64_tr_b16 lane coordinates
   for (int i = tid; i < 3 * MF_H; i += 64 * NW) cst[i / MF_H][i % MF_H] = (i < MF_H ? b1 : i < 2 * MF_H ? b2 : w3)[i % MF_H];
 
-  bf16x8 w1f[MT], wt[MT][8];
+  bf16x8 w1f[MT];
 #pragma unroll
   for (int m = 0; m < MT; ++m) {
     const int u = u0 + 16 * m + l15;
     w1f[m] = 8 * g + 8 <= Fp ? *reinterpret_cast<const bf16x8*>(W1 + (size_t)u * Fp + 8 * g)
                              : bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
-#pragma unroll
-    for (int kt = 0; kt < 8; ++kt)
-#pragma unroll
-      for (int j = 0; j < 8; ++j) wt[m][kt][j] = (short)W2[(size_t)(32 * kt + 8 * g + j) * MF_H + u];
   }
-  // layer 2's A operand (W2 rows of the own units) is streamed from L2 per K step, WD steps
-  // ahead: holding it too (64 VGPRs) would not fit beside W2^T in the 256-VGPR budget of two
-  // waves per SIMD
-  constexpr int WD = 3;
-  const int w2lane = (u0 + l15) * MF_H + 8 * g;  // element offset of the lane's m = 0 fragment
-  // a zero laundered per chunk (below) keeps the loads inside the chunk loop (hoisted, they
-  // would pin 64 VGPRs); laundering the pointer itself would lose its global address space
-  // (flat loads: counted in lgkmcnt too, so every LDS wait would wait for them)
-  // Buffer loads: the per-fragment offset is an immediate / SGPR, no 64-bit address VALU.
-  int w2z = 0;
+  // ONE 64-VGPR weight buffer serves both big GEMMs: W2 rows of the wave's units (layer 2's A
+  // operand) and W2^T rows (dH1's A operand, from the transposed copy mlp2_w2t_kernel writes
+  // each step) take turns in it. Each image is requested right after the other GEMM's last
+  // MFMA, i.e. ~3,000 cycles (head / dZ2, or dZ1 / dW1 / layer 1) before its first use, so L2
+  // latency is hidden; two resident images would not fit the 256-VGPR budget of two waves per
+  // SIMD, and streaming W2 3 K-steps ahead left layer 2 at 5,900 cycles per chunk against
+  // 2,050 for the resident-W2^T dH1 (tools/mlp_timeline.py, profiles/r4/final/mlp_timeline.txt).
+  const int wlane = (u0 + l15) * MF_H + 8 * g;  // element offset of the lane's m = 0 fragment
+  // a zero laundered per request keeps the loads where they are issued (hoisted out of the
+  // chunk loop they would pin both images); buffer loads: offsets are immediates / SGPRs
+  int wz = 0;
   const __amdgpu_buffer_rsrc_t w2rs = __builtin_amdgcn_make_buffer_rsrc((void*)W2, 0, 0x7FFFFFFF, 0x00020000);
-  auto w2frag = [&](int m, int kt) {
-    typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
-    return __builtin_bit_cast(bf16x8, (u32x4_t)__builtin_amdgcn_raw_buffer_load_b128(
-                                          w2rs, 2 * (w2z + w2lane), 2 * (16 * MF_H * m + 32 * kt), 0));
-  };
-  // the first WD K steps of layer 2, requested one chunk early (right after the previous
-  // chunk's dH1 MFMAs): they land during dZ1 / dW1, the staging barrier and layer 1
-  bf16x8 w2r[WD][MT];
-  auto w2first = [&]() {
-    w2z = 0;
-    asm volatile("" : "+s"(w2z));
+  const __amdgpu_buffer_rsrc_t w2trs = __builtin_amdgcn_make_buffer_rsrc((void*)W2T, 0, 0x7FFFFFFF, 0x00020000);
+  bf16x8 wb[MT][8];
+  auto loadw = [&](const __amdgpu_buffer_rsrc_t rs) {
+    wz = 0;
+    asm volatile("" : "+s"(wz));
 #pragma unroll
-    for (int k = 0; k < WD; ++k)
+    for (int m = 0; m < MT; ++m)
 #pragma unroll
-      for (int m = 0; m < MT; ++m) w2r[k][m] = w2frag(m, k);
+      for (int kt = 0; kt < 8; ++kt) {
+        typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
+        wb[m][kt] = __builtin_bit_cast(bf16x8, (u32x4_t)__builtin_amdgcn_raw_buffer_load_b128(
+                                                   rs, 2 * (wz + wlane), 2 * (16 * MF_H * m + 32 * kt), 0));
+      }
+    __builtin_amdgcn_sched_barrier(0);  // issued here, not sunk toward the first use
   };
   f32x4 dw1a[MT][NFT];
 #pragma unroll
@@ -143,13 +136,12 @@ __global__ __launch_bounds__(512, 1) void mlp2_step_kernel(
       ys[p][tid - 256] = yv;
   };
   if ((int)blockIdx.x < nchunks) prefetch(blockIdx.x);
-  if constexpr (EARLY) {
-    // first chunk staged here (its barrier also publishes cst), the second one prefetched
-    stage(0);
-    __syncthreads();
-    if ((int)blockIdx.x + (int)gridDim.x < nchunks) prefetch(blockIdx.x + gridDim.x);
-  }
-  w2first();
+  // first chunk staged here (its barrier also publishes cst), the second one prefetched; every
+  // later chunk is staged before the previous chunk's dZ2 barrier, which publishes it
+  loadw(w2rs);
+  stage(0);
+  __syncthreads();
+  if ((int)blockIdx.x + (int)gridDim.x < nchunks) prefetch(blockIdx.x + gridDim.x);
   int par = 0;
   for (int ch = blockIdx.x; ch < nchunks; ch += gridDim.x, par ^= 1) {
     const int row0 = ch * MF_ROWS;
@@ -161,16 +153,9 @@ __global__ __launch_bounds__(512, 1) void mlp2_step_kernel(
     };
     stamp(0);
     char* xt = xs + par * XB;
-    if constexpr (!EARLY) {
-      stage(par);
-      __syncthreads();  // B1: X / y staged (and, first chunk, cst)
-    }
     stamp(1);
-    if constexpr (!EARLY) {
-      if (ch + (int)gridDim.x < nchunks) prefetch(ch + gridDim.x);
-    }
 
-    // ---- layer 1 (own units): H1 -> h1s; the first W2 fragments of layer 2 in flight
+    // ---- layer 1 (own units): H1 -> h1s (W2 in flight into the weight buffer)
     f32x4 acc[MT][4];
 #pragma unroll
     for (int n = 0; n < 4; ++n) {
@@ -198,8 +183,8 @@ __global__ __launch_bounds__(512, 1) void mlp2_step_kernel(
     for (int m = 0; m < MT; ++m)
 #pragma unroll
       for (int n = 0; n < 4; ++n) acc[m][n] = f32x4{0.f, 0.f, 0.f, 0.f};
-    static_for<0, 8>([&](auto kc) {
-      constexpr int kt = decltype(kc)::value;
+#pragma unroll
+    for (int kt = 0; kt < 8; ++kt) {
       bf16x8 hb[4];
 #pragma unroll
       for (int n = 0; n < 4; ++n) hb[n] = *reinterpret_cast<const bf16x8*>(h1s + tile_off(16 * n + l15, 32 * kt + 8 * g));
@@ -207,12 +192,9 @@ __global__ __launch_bounds__(512, 1) void mlp2_step_kernel(
       for (int m = 0; m < MT; ++m)
 #pragma unroll
         for (int n = 0; n < 4; ++n)
-          acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w2r[kt % WD][m], hb[n], acc[m][n], 0, 0, 0);
-      if constexpr (kt + WD < 8) {  // refill the slot just consumed
-#pragma unroll
-        for (int m = 0; m < MT; ++m) w2r[kt % WD][m] = w2frag(m, kt + WD);
-      }
-    });
+          acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wb[m][kt], hb[n], acc[m][n], 0, 0, 0);
+    }
+    loadw(w2trs);  // dH1's W2^T image: lands during the head / dZ2 phases
     stamp(4);
     // H2 = relu(Z2 + b2) rounded to bf16 (the stored-activation numerics of the reference
     // path), kept in acc; head partials of rows 16n + l15
@@ -285,17 +267,13 @@ __global__ __launch_bounds__(512, 1) void mlp2_step_kernel(
       acc4(P_DW3, m, s3);
       acc4(P_DB2, m, s2);
     }
-    // EARLY: the next chunk's X / y into the other buffer (its last readers — layer 1 and dW1
-    // of the previous chunk — are behind this chunk's B2), published by B4
-    if constexpr (EARLY) {
-      if (ch + (int)gridDim.x < nchunks) stage(par ^ 1);
-    }
+    // the next chunk's X / y into the other buffer (its last readers — layer 1 and dW1 of the
+    // previous chunk — are behind this chunk's B2), published by B4
+    if (ch + (int)gridDim.x < nchunks) stage(par ^ 1);
     stamp(7);
-    __syncthreads();  // B4: dZ2 complete (EARLY: and the next chunk's X / y staged)
+    __syncthreads();  // B4: dZ2 complete, next chunk's X / y staged
     stamp(8);
-    if constexpr (EARLY) {
-      if (ch + 2 * (int)gridDim.x < nchunks) prefetch(ch + 2 * gridDim.x);
-    }
+    if (ch + 2 * (int)gridDim.x < nchunks) prefetch(ch + 2 * gridDim.x);
 
     if constexpr (FRAG) {
       // ---- dZ2 copy-out as dW2 A fragments: fragment (s, b) = 32 rows x 16 units, lane
@@ -340,10 +318,10 @@ __global__ __launch_bounds__(512, 1) void mlp2_step_kernel(
       for (int m = 0; m < MT; ++m)
 #pragma unroll
         for (int n = 0; n < 4; ++n)
-          acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wt[m][kt], zb[n], acc[m][n], 0, 0, 0);
+          acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wb[m][kt], zb[n], acc[m][n], 0, 0, 0);
     }
     stamp(10);
-    w2first();  // the next chunk's first layer-2 fragments
+    loadw(w2rs);  // the next chunk's W2 image: lands during dZ1 / dW1 / layer 1
     // ---- dZ1 = dH1 * [H1 > 0] over the same 8 bytes of h1s; db1 partials
 #pragma unroll
     for (int m = 0; m < MT; ++m) {
@@ -537,10 +515,19 @@ __global__ __launch_bounds__(512, 1) void mlp2_dw2f_kernel(const bf16_t* __restr
 #pragma unroll
     for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  // H1 of a chunk (both 32-row steps) -> B fragments hb[step][nb]
-  auto recompute = [&](const char* st, bf16x8 (&hb)[2][2]) {
+  const int last = nch - 1;
+#pragma unroll
+  for (int k = 0; k < DW2F_SLOTS - 1; ++k) issue(min(k, last), k);
+  for (int c = 0; c < nch; ++c) {
+    const int slot = c & (DW2F_SLOTS - 1);
+    dma_wait(std::integral_constant<int, DW2F_SLOTS - 2>{});  // chunk c's pieces (this wave) landed
+    __builtin_amdgcn_s_barrier();                              // ... every wave's; slot c - 1 free
+    asm volatile("" ::: "memory");
+    issue(min(c + DW2F_SLOTS - 1, last), (c + DW2F_SLOTS - 1) & (DW2F_SLOTS - 1));
+    const char* st = smem + slot * DW2F_SLOT;
 #pragma unroll
     for (int s2 = 0; s2 < 2; ++s2) {
+      bf16x8 hb[2];
       bf16x8 xf[2];
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
@@ -556,52 +543,16 @@ __global__ __launch_bounds__(512, 1) void mlp2_dw2f_kernel(const bf16_t* __restr
         const unsigned p2 = pk_bf16(fmaxf(c1[0] + bias[nb], 0.f), fmaxf(c1[1] + bias[nb], 0.f));
         const unsigned p3 = pk_bf16(fmaxf(c1[2] + bias[nb], 0.f), fmaxf(c1[3] + bias[nb], 0.f));
         typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
-        hb[s2][nb] = __builtin_bit_cast(bf16x8, (u32x4_t{p0, p1, p2, p3}));
+        hb[nb] = __builtin_bit_cast(bf16x8, (u32x4_t{p0, p1, p2, p3}));
+      }
+#pragma unroll
+      for (int mb = 0; mb < 8; ++mb) {
+        const bf16x8 a = *reinterpret_cast<const bf16x8*>(st + (s2 * 16 + 8 * wm + mb) * 1024 + lane * 16);
+#pragma unroll
+        for (int nb = 0; nb < 2; ++nb) acc[mb][nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, hb[nb], acc[mb][nb], 0, 0, 0);
       }
     }
-  };
-  auto dw = [&](const char* st, const bf16x8 (&hb)[2][2]) {
-    // all 16 A fragments of the chunk requested before the first MFMA (one LDS latency, not 8)
-    bf16x8 a[2][8];
-#pragma unroll
-    for (int s2 = 0; s2 < 2; ++s2)
-#pragma unroll
-      for (int mb = 0; mb < 8; ++mb)
-        a[s2][mb] = *reinterpret_cast<const bf16x8*>(st + (s2 * 16 + 8 * wm + mb) * 1024 + lane * 16);
-    __builtin_amdgcn_sched_barrier(0);  // (the scheduler would pair each read with its MFMAs)
-#pragma unroll
-    for (int s2 = 0; s2 < 2; ++s2)
-#pragma unroll
-      for (int mb = 0; mb < 8; ++mb)
-#pragma unroll
-        for (int nb = 0; nb < 2; ++nb)
-          acc[mb][nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[s2][mb], hb[s2][nb], acc[mb][nb], 0, 0, 0);
-  };
-  // Software pipeline: chunk c + 1's H1 is rebuilt while chunk c's dW MFMAs run (independent
-  // work in one wave: the rebuild's VALU epilogue issues in the MFMAs' shadow). Chunks c + 2,
-  // c + 3 are in flight; chunk c + 3 goes into chunk c - 1's slot, free after this barrier.
-  const int last = nch - 1;
-#pragma unroll
-  for (int k = 0; k < DW2F_SLOTS - 1; ++k) issue(min(k, last), k);
-  dma_wait(std::integral_constant<int, DW2F_SLOTS - 2>{});  // chunk 0 (this wave's pieces)
-  __builtin_amdgcn_s_barrier();
-  asm volatile("" ::: "memory");
-  bf16x8 hA[2][2], hB[2][2];
-  recompute(smem, hA);
-  auto body = [&](int c, bf16x8 (&hcur)[2][2], bf16x8 (&hnext)[2][2]) {
-    dma_wait(std::integral_constant<int, DW2F_SLOTS - 3>{});  // chunk c + 1 landed (this wave)
-    __builtin_amdgcn_s_barrier();                              // ... every wave's; slot c - 1 free
-    asm volatile("" ::: "memory");
-    issue(min(c + DW2F_SLOTS - 1, last), (c + DW2F_SLOTS - 1) & (DW2F_SLOTS - 1));
-    if (c + 1 < nch) recompute(smem + ((c + 1) & (DW2F_SLOTS - 1)) * DW2F_SLOT, hnext);
-    dw(smem + (c & (DW2F_SLOTS - 1)) * DW2F_SLOT, hcur);
-  };
-  int c = 0;
-  for (; c + 2 <= nch; c += 2) {
-    body(c, hA, hB);
-    body(c + 1, hB, hA);
   }
-  if (c < nch) body(c, hA, hB);
   wait_vmcnt<0>();  // the clamped fetches past the range must land before the workgroup ends
   // out unit 128 wm + 16 mb + 4g + r, in unit n0 + 16 nb + l15: plain stores into this range's
   // slab row (the reduce sums the rows); past the slab, atomics into a dW2 copy
@@ -625,35 +576,40 @@ __global__ __launch_bounds__(512, 1) void mlp2_dw2f_kernel(const bf16_t* __restr
           atomicAdd(dst + (size_t)(128 * wm + 16 * mb + 4 * g + r) * MF_H + n0 + 16 * nb + l15, acc[mb][nb][r]);
   }
 }
+
+// W2T [256][256] bf16 = W2 transposed (the step kernel's dH1 operand image)
+__global__ __launch_bounds__(256) void mlp2_w2t_kernel(const bf16_t* __restrict__ W2, bf16_t* __restrict__ W2T) {
+  __shared__ bf16_t tile[64][65];
+  const int bx = blockIdx.x & 3, by = blockIdx.x >> 2;  // 4 x 4 tiles of 64 x 64
+  for (int i = threadIdx.x; i < 64 * 64; i += 256) tile[i >> 6][i & 63] = W2[(size_t)(64 * by + (i >> 6)) * MF_H + 64 * bx + (i & 63)];
+  __syncthreads();
+  for (int i = threadIdx.x; i < 64 * 64; i += 256) W2T[(size_t)(64 * bx + (i >> 6)) * MF_H + 64 * by + (i & 63)] = tile[i & 63][i >> 6];
+}
 }  // namespace
 
-bool launch_mlp2_step(const bf16_t* X, int Fp, const bf16_t* W1, const float* b1, const bf16_t* W2, const float* b2,
-                      const float* w3, const float* b3, const float* y, float dy_scale, int B, const long long* rows,
-                      long nrows, bf16_t* dZ2, float* pred, float* red, bool dz_frag, hipStream_t s) {
+void launch_mlp2_w2t(const bf16_t* W2, bf16_t* W2T, hipStream_t s) {
+  hipLaunchKernelGGL(mlp2_w2t_kernel, dim3(16), dim3(256), 0, s, W2, W2T);
+}
+
+bool launch_mlp2_step(const bf16_t* X, int Fp, const bf16_t* W1, const float* b1, const bf16_t* W2, const bf16_t* W2T,
+                      const float* b2, const float* w3, const float* b3, const float* y, float dy_scale, int B,
+                      const long long* rows, long nrows, bf16_t* dZ2, float* pred, float* red, bool dz_frag,
+                      hipStream_t s) {
   // the reduce sums the dW1 rows only when it expects the 8-wave backward's layout
-  if (B <= 0 || Fp > 32 || Fp % 8 != 0 || red == nullptr || !mlp_bwd8()) return false;
+  if (B <= 0 || Fp > 32 || Fp % 8 != 0 || red == nullptr || W2T == nullptr || !mlp_bwd8()) return false;
   if (dz_frag && B % MF_ROWS != 0) return false;
   const int grid = mlp2_train_grid(B);  // the dW1 rows mlp2_reduce sums
   // phase stamps (tools/mlp_timeline.py; results unchanged, so not a WF_DIAG-only switch):
   // into dW2 slab rows 200.. of the scratch (unused by a step of <= 200 dW2 ranges)
   static const bool stamp = std::getenv("WELLFLOW_MLP_STAMP") != nullptr;
   if (stamp && Fp <= 16 && dz_frag) {
-    hipLaunchKernelGGL((mlp2_step_kernel<1, true, true>), dim3(grid), dim3(512), 0, s, X, Fp, W1, b1, W2, b2, w3, b3, y,
-                       dy_scale, B, rows, nrows, dZ2, pred, red,
+    hipLaunchKernelGGL((mlp2_step_kernel<1, true, true>), dim3(grid), dim3(512), 0, s, X, Fp, W1, b1, W2, W2T, b2, w3,
+                       b3, y, dy_scale, B, rows, nrows, dZ2, pred, red,
                        reinterpret_cast<unsigned long long*>(red + kMlpRedSlab2Off + 200L * 65536));
     return true;
   }
-  static const bool b4 = [] {
-    const char* e = std::getenv("WELLFLOW_MLP_STEP_B4");
-    return e != nullptr && e[0] == '1';
-  }();
-  if (b4 && Fp <= 16 && dz_frag) {  // A/B: the four-barrier chunk order
-    hipLaunchKernelGGL((mlp2_step_kernel<1, true, false, false>), dim3(grid), dim3(512), 0, s, X, Fp, W1, b1, W2, b2,
-                       w3, b3, y, dy_scale, B, rows, nrows, dZ2, pred, red, nullptr);
-    return true;
-  }
-#define WF_STEP(NFT, FR)                                                                                            \
-  hipLaunchKernelGGL((mlp2_step_kernel<NFT, FR>), dim3(grid), dim3(512), 0, s, X, Fp, W1, b1, W2, b2, w3, b3, y, \
+#define WF_STEP(NFT, FR)                                                                                                \
+  hipLaunchKernelGGL((mlp2_step_kernel<NFT, FR>), dim3(grid), dim3(512), 0, s, X, Fp, W1, b1, W2, W2T, b2, w3, b3, y, \
                      dy_scale, B, rows, nrows, dZ2, pred, red)
   if (Fp <= 16) {
     if (dz_frag) WF_STEP(1, true); else WF_STEP(1, false);
