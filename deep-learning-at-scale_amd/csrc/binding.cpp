@@ -542,7 +542,7 @@ void mlp2_reduce(const at::Tensor& red, int64_t Fp, int64_t B, c10::optional<at:
 // MLP training step forward + backward in one launch (mlp_step.hip); the batch sums land in
 // the spread scratch `red` (mlp2_reduce adds them), dZ2 feeds mlp2_dw2. False = not covered.
 bool mlp2_step(const at::Tensor& X, int64_t Fp, const at::Tensor& W1, const at::Tensor& b1, const at::Tensor& W2,
-               const at::Tensor& W2T, const at::Tensor& b2, const at::Tensor& w3, const at::Tensor& b3, const at::Tensor& y, double dy_scale,
+               const at::Tensor& b2, const at::Tensor& w3, const at::Tensor& b3, const at::Tensor& y, double dy_scale,
                int64_t B, c10::optional<at::Tensor> rows, const at::Tensor& dZ2, c10::optional<at::Tensor> pred,
                const at::Tensor& red, bool dz_frag) {
   constexpr int64_t H = 256;
@@ -552,8 +552,6 @@ bool mlp2_step(const at::Tensor& X, int64_t Fp, const at::Tensor& W1, const at::
   check_extent(W1, H * Fp, "W1");
   check_t(W2, at::kBFloat16, "W2");
   check_extent(W2, H * H, "W2");
-  check_t(W2T, at::kBFloat16, "W2T");
-  check_extent(W2T, H * H, "W2T");
   for (const at::Tensor* t : {&b1, &b2, &w3}) {
     check_t(*t, at::kFloat, "bias/w3");
     check_extent(*t, H, "bias/w3");
@@ -566,13 +564,11 @@ bool mlp2_step(const at::Tensor& X, int64_t Fp, const at::Tensor& W1, const at::
   check_extent(dZ2, B * H, "dZ2");
   check_t(red, at::kFloat, "red");
   check_extent(red, wf::kMlpRedFloats, "red");
-  for (const at::Tensor* t : {&X, &W1, &W2, &W2T, &dZ2})
+  for (const at::Tensor* t : {&X, &W1, &W2, &dZ2})
     TORCH_CHECK(reinterpret_cast<uintptr_t>(t->data_ptr()) % 16 == 0, "mlp2_step: bf16 operands must be 16-B aligned");
   TORCH_CHECK(B > 0, "mlp2_step: B > 0");
   const c10::hip::OptionalHIPGuardMasqueradingAsCUDA guard(X.device());
-  // W2T = W2 transposed, rewritten from this step's bf16 weights (stream-ordered before the step)
-  wf::launch_mlp2_w2t(bfp(W2), bfp(W2T), cur_stream());
-  return wf::launch_mlp2_step(bfp(X), (int)Fp, bfp(W1), fp(b1), bfp(W2), bfp(W2T), fp(b2), fp(w3), fp(b3), fp(y), (float)dy_scale,
+  return wf::launch_mlp2_step(bfp(X), (int)Fp, bfp(W1), fp(b1), bfp(W2), fp(b2), fp(w3), fp(b3), fp(y), (float)dy_scale,
                               (int)B, rows_ptr(rows, B), nrows, bfp(dZ2), opt_ptr<float>(pred, at::kFloat, "pred", B),
                               fp(red), dz_frag, cur_stream());
 }

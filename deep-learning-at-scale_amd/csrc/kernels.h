@@ -127,12 +127,9 @@ void launch_mlp2_reduce(float* red, int Fp, int B, float* loss_sum, float* db3, 
 // bf16 weights and fp32 biases / head — dZ2 ([B][256] bf16, mlp2_dw2's operand), pred (optional)
 // and every batch sum except dW2 (loss, db3, dw3, db1, db2, dW1) into the spread scratch `red`,
 // which launch_mlp2_reduce then adds to the gradients. Fp <= 32; false = not covered.
-// W2T = W2 transposed ([256][256] bf16; the step kernel's dH1 operand, rewritten each step)
-void launch_mlp2_w2t(const bf16_t* W2, bf16_t* W2T, hipStream_t s);
-bool launch_mlp2_step(const bf16_t* X, int Fp, const bf16_t* W1, const float* b1, const bf16_t* W2, const bf16_t* W2T,
-                      const float* b2, const float* w3, const float* b3, const float* y, float dy_scale, int B,
-                      const long long* rows, long nrows, bf16_t* dZ2, float* pred, float* red, bool dz_frag,
-                      hipStream_t s);
+bool launch_mlp2_step(const bf16_t* X, int Fp, const bf16_t* W1, const float* b1, const bf16_t* W2, const float* b2,
+                      const float* w3, const float* b3, const float* y, float dy_scale, int B, const long long* rows,
+                      long nrows, bf16_t* dZ2, float* pred, float* red, bool dz_frag, hipStream_t s);
 // dz_frag: dZ2 is written in the fragment layout of launch_mlp2_dw2f (B % 64 == 0) instead of
 // [B][256]: fragment (S, b) of rows 32S .. 32S + 31 x units 16b .. 16b + 15 at element
 // (S * 16 + b) * 512, lane (l15, g) = 16 B = rows 32S + 8g .. + 7 of unit 16b + l15.

@@ -38,8 +38,8 @@ namespace {
 template <int NFT, bool FRAG, bool STAMP = false>  // NFT: 16-feature tiles of dW1: 1 (Fp <= 16) or 2 (Fp <= 32)
 __global__ __launch_bounds__(512, 1) void mlp2_step_kernel(
     const bf16_t* __restrict__ X, int Fp, const bf16_t* __restrict__ W1, const float* __restrict__ b1,
-    const bf16_t* __restrict__ W2, const bf16_t* __restrict__ W2T, const float* __restrict__ b2,
-    const float* __restrict__ w3, const float* __restrict__ b3, const float* __restrict__ y, float dy_scale, int B,
+    const bf16_t* __restrict__ W2, const float* __restrict__ b2, const float* __restrict__ w3,
+    const float* __restrict__ b3, const float* __restrict__ y, float dy_scale, int B,
     const long long* __restrict__ rows, long nrows, bf16_t* __restrict__ dZ2, float* __restrict__ pred,
     float* __restrict__ red, unsigned long long* __restrict__ stamps = nullptr) {
   constexpr int MT = 2, NW = 8, XB = MF_ROWS * MF_XROW;
@@ -62,39 +62,43 @@ __global__ __launch_bounds__(512, 1) void mlp2_step_kernel(
   const int tq = l15 >> 2, tp = lane & 3;  // ds_read_b64_tr_b16 lane coordinates
   for (int i = tid; i < 3 * MF_H; i += 64 * NW) cst[i / MF_H][i % MF_H] = (i < MF_H ? b1 : i < 2 * MF_H ? b2 : w3)[i % MF_H];
 
-  bf16x8 w1f[MT];
+  bf16x8 w1f[MT], wt[MT][8];
 #pragma unroll
   for (int m = 0; m < MT; ++m) {
     const int u = u0 + 16 * m + l15;
     w1f[m] = 8 * g + 8 <= Fp ? *reinterpret_cast<const bf16x8*>(W1 + (size_t)u * Fp + 8 * g)
                              : bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+    for (int kt = 0; kt < 8; ++kt)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) wt[m][kt][j] = (short)W2[(size_t)(32 * kt + 8 * g + j) * MF_H + u];
   }
-  // ONE 64-VGPR weight buffer serves both big GEMMs: W2 rows of the wave's units (layer 2's A
-  // operand) and W2^T rows (dH1's A operand, from the transposed copy mlp2_w2t_kernel writes
-  // each step) take turns in it. Each image is requested right after the other GEMM's last
-  // MFMA, i.e. ~3,000 cycles (head / dZ2, or dZ1 / dW1 / layer 1) before its first use, so L2
-  // latency is hidden; two resident images would not fit the 256-VGPR budget of two waves per
-  // SIMD, and streaming W2 3 K-steps ahead left layer 2 at 5,900 cycles per chunk against
-  // 2,050 for the resident-W2^T dH1 (tools/mlp_timeline.py, profiles/r4/final/mlp_timeline.txt).
-  const int wlane = (u0 + l15) * MF_H + 8 * g;  // element offset of the lane's m = 0 fragment
-  // a zero laundered per request keeps the loads where they are issued (hoisted out of the
-  // chunk loop they would pin both images); buffer loads: offsets are immediates / SGPRs
-  int wz = 0;
+  // layer 2's A operand (W2 rows of the own units) is streamed from L2 per K step, WD steps
+  // ahead: holding it too (64 VGPRs) would not fit beside W2^T in the 256-VGPR budget of two
+  // waves per SIMD
+  constexpr int WD = 3;
+  const int w2lane = (u0 + l15) * MF_H + 8 * g;  // element offset of the lane's m = 0 fragment
+  // a zero laundered per chunk (below) keeps the loads inside the chunk loop (hoisted, they
+  // would pin 64 VGPRs); laundering the pointer itself would lose its global address space
+  // (flat loads: counted in lgkmcnt too, so every LDS wait would wait for them)
+  // Buffer loads: the per-fragment offset is an immediate / SGPR, no 64-bit address VALU.
+  int w2z = 0;
   const __amdgpu_buffer_rsrc_t w2rs = __builtin_amdgcn_make_buffer_rsrc((void*)W2, 0, 0x7FFFFFFF, 0x00020000);
-  const __amdgpu_buffer_rsrc_t w2trs = __builtin_amdgcn_make_buffer_rsrc((void*)W2T, 0, 0x7FFFFFFF, 0x00020000);
-  bf16x8 wb[MT][8];
-  auto loadw = [&](const __amdgpu_buffer_rsrc_t rs) {
-    wz = 0;
-    asm volatile("" : "+s"(wz));
+  auto w2frag = [&](int m, int kt) {
+    typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
+    return __builtin_bit_cast(bf16x8, (u32x4_t)__builtin_amdgcn_raw_buffer_load_b128(
+                                          w2rs, 2 * (w2z + w2lane), 2 * (16 * MF_H * m + 32 * kt), 0));
+  };
+  // the first WD K steps of layer 2, requested one chunk early (right after the previous
+  // chunk's dH1 MFMAs): they land during dZ1 / dW1, the staging barrier and layer 1
+  bf16x8 w2r[WD][MT];
+  auto w2first = [&]() {
+    w2z = 0;
+    asm volatile("" : "+s"(w2z));
 #pragma unroll
-    for (int m = 0; m < MT; ++m)
+    for (int k = 0; k < WD; ++k)
 #pragma unroll
-      for (int kt = 0; kt < 8; ++kt) {
-        typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
-        wb[m][kt] = __builtin_bit_cast(bf16x8, (u32x4_t)__builtin_amdgcn_raw_buffer_load_b128(
-                                                   rs, 2 * (wz + wlane), 2 * (16 * MF_H * m + 32 * kt), 0));
-      }
-    __builtin_amdgcn_sched_barrier(0);  // issued here, not sunk toward the first use
+      for (int m = 0; m < MT; ++m) w2r[k][m] = w2frag(m, k);
   };
   f32x4 dw1a[MT][NFT];
 #pragma unroll
@@ -137,11 +141,12 @@ __global__ __launch_bounds__(512, 1) void mlp2_step_kernel(
   };
   if ((int)blockIdx.x < nchunks) prefetch(blockIdx.x);
   // first chunk staged here (its barrier also publishes cst), the second one prefetched; every
-  // later chunk is staged before the previous chunk's dZ2 barrier, which publishes it
-  loadw(w2rs);
+  // later chunk is staged before the previous chunk's dZ2 barrier, which publishes it (three
+  // workgroup barriers per chunk; the four-barrier order measured 0.4 % slower, r4/final)
   stage(0);
   __syncthreads();
   if ((int)blockIdx.x + (int)gridDim.x < nchunks) prefetch(blockIdx.x + gridDim.x);
+  w2first();
   int par = 0;
   for (int ch = blockIdx.x; ch < nchunks; ch += gridDim.x, par ^= 1) {
     const int row0 = ch * MF_ROWS;
@@ -155,7 +160,7 @@ __global__ __launch_bounds__(512, 1) void mlp2_step_kernel(
     char* xt = xs + par * XB;
     stamp(1);
 
-    // ---- layer 1 (own units): H1 -> h1s (W2 in flight into the weight buffer)
+    // ---- layer 1 (own units): H1 -> h1s; the first W2 fragments of layer 2 in flight
     f32x4 acc[MT][4];
 #pragma unroll
     for (int n = 0; n < 4; ++n) {
@@ -183,8 +188,8 @@ __global__ __launch_bounds__(512, 1) void mlp2_step_kernel(
     for (int m = 0; m < MT; ++m)
 #pragma unroll
       for (int n = 0; n < 4; ++n) acc[m][n] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int kt = 0; kt < 8; ++kt) {
+    static_for<0, 8>([&](auto kc) {
+      constexpr int kt = decltype(kc)::value;
       bf16x8 hb[4];
 #pragma unroll
       for (int n = 0; n < 4; ++n) hb[n] = *reinterpret_cast<const bf16x8*>(h1s + tile_off(16 * n + l15, 32 * kt + 8 * g));
@@ -192,9 +197,12 @@ __global__ __launch_bounds__(512, 1) void mlp2_step_kernel(
       for (int m = 0; m < MT; ++m)
 #pragma unroll
         for (int n = 0; n < 4; ++n)
-          acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wb[m][kt], hb[n], acc[m][n], 0, 0, 0);
-    }
-    loadw(w2trs);  // dH1's W2^T image: lands during the head / dZ2 phases
+          acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w2r[kt % WD][m], hb[n], acc[m][n], 0, 0, 0);
+      if constexpr (kt + WD < 8) {  // refill the slot just consumed
+#pragma unroll
+        for (int m = 0; m < MT; ++m) w2r[kt % WD][m] = w2frag(m, kt + WD);
+      }
+    });
     stamp(4);
     // H2 = relu(Z2 + b2) rounded to bf16 (the stored-activation numerics of the reference
     // path), kept in acc; head partials of rows 16n + l15
@@ -318,10 +326,10 @@ __global__ __launch_bounds__(512, 1) void mlp2_step_kernel(
       for (int m = 0; m < MT; ++m)
 #pragma unroll
         for (int n = 0; n < 4; ++n)
-          acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wb[m][kt], zb[n], acc[m][n], 0, 0, 0);
+          acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wt[m][kt], zb[n], acc[m][n], 0, 0, 0);
     }
     stamp(10);
-    loadw(w2rs);  // the next chunk's W2 image: lands during dZ1 / dW1 / layer 1
+    w2first();  // the next chunk's first layer-2 fragments
     // ---- dZ1 = dH1 * [H1 > 0] over the same 8 bytes of h1s; db1 partials
 #pragma unroll
     for (int m = 0; m < MT; ++m) {
@@ -576,40 +584,26 @@ __global__ __launch_bounds__(512, 1) void mlp2_dw2f_kernel(const bf16_t* __restr
           atomicAdd(dst + (size_t)(128 * wm + 16 * mb + 4 * g + r) * MF_H + n0 + 16 * nb + l15, acc[mb][nb][r]);
   }
 }
-
-// W2T [256][256] bf16 = W2 transposed (the step kernel's dH1 operand image)
-__global__ __launch_bounds__(256) void mlp2_w2t_kernel(const bf16_t* __restrict__ W2, bf16_t* __restrict__ W2T) {
-  __shared__ bf16_t tile[64][65];
-  const int bx = blockIdx.x & 3, by = blockIdx.x >> 2;  // 4 x 4 tiles of 64 x 64
-  for (int i = threadIdx.x; i < 64 * 64; i += 256) tile[i >> 6][i & 63] = W2[(size_t)(64 * by + (i >> 6)) * MF_H + 64 * bx + (i & 63)];
-  __syncthreads();
-  for (int i = threadIdx.x; i < 64 * 64; i += 256) W2T[(size_t)(64 * bx + (i >> 6)) * MF_H + 64 * by + (i & 63)] = tile[i & 63][i >> 6];
-}
 }  // namespace
 
-void launch_mlp2_w2t(const bf16_t* W2, bf16_t* W2T, hipStream_t s) {
-  hipLaunchKernelGGL(mlp2_w2t_kernel, dim3(16), dim3(256), 0, s, W2, W2T);
-}
-
-bool launch_mlp2_step(const bf16_t* X, int Fp, const bf16_t* W1, const float* b1, const bf16_t* W2, const bf16_t* W2T,
-                      const float* b2, const float* w3, const float* b3, const float* y, float dy_scale, int B,
-                      const long long* rows, long nrows, bf16_t* dZ2, float* pred, float* red, bool dz_frag,
-                      hipStream_t s) {
+bool launch_mlp2_step(const bf16_t* X, int Fp, const bf16_t* W1, const float* b1, const bf16_t* W2, const float* b2,
+                      const float* w3, const float* b3, const float* y, float dy_scale, int B, const long long* rows,
+                      long nrows, bf16_t* dZ2, float* pred, float* red, bool dz_frag, hipStream_t s) {
   // the reduce sums the dW1 rows only when it expects the 8-wave backward's layout
-  if (B <= 0 || Fp > 32 || Fp % 8 != 0 || red == nullptr || W2T == nullptr || !mlp_bwd8()) return false;
+  if (B <= 0 || Fp > 32 || Fp % 8 != 0 || red == nullptr || !mlp_bwd8()) return false;
   if (dz_frag && B % MF_ROWS != 0) return false;
   const int grid = mlp2_train_grid(B);  // the dW1 rows mlp2_reduce sums
   // phase stamps (tools/mlp_timeline.py; results unchanged, so not a WF_DIAG-only switch):
   // into dW2 slab rows 200.. of the scratch (unused by a step of <= 200 dW2 ranges)
   static const bool stamp = std::getenv("WELLFLOW_MLP_STAMP") != nullptr;
   if (stamp && Fp <= 16 && dz_frag) {
-    hipLaunchKernelGGL((mlp2_step_kernel<1, true, true>), dim3(grid), dim3(512), 0, s, X, Fp, W1, b1, W2, W2T, b2, w3,
-                       b3, y, dy_scale, B, rows, nrows, dZ2, pred, red,
+    hipLaunchKernelGGL((mlp2_step_kernel<1, true, true>), dim3(grid), dim3(512), 0, s, X, Fp, W1, b1, W2, b2, w3, b3, y,
+                       dy_scale, B, rows, nrows, dZ2, pred, red,
                        reinterpret_cast<unsigned long long*>(red + kMlpRedSlab2Off + 200L * 65536));
     return true;
   }
-#define WF_STEP(NFT, FR)                                                                                                \
-  hipLaunchKernelGGL((mlp2_step_kernel<NFT, FR>), dim3(grid), dim3(512), 0, s, X, Fp, W1, b1, W2, W2T, b2, w3, b3, y, \
+#define WF_STEP(NFT, FR)                                                                                            \
+  hipLaunchKernelGGL((mlp2_step_kernel<NFT, FR>), dim3(grid), dim3(512), 0, s, X, Fp, W1, b1, W2, b2, w3, b3, y, \
                      dy_scale, B, rows, nrows, dZ2, pred, red)
   if (Fp <= 16) {
     if (dz_frag) WF_STEP(1, true); else WF_STEP(1, false);

@@ -195,8 +195,6 @@ class NativeMLP:
         # ... writing dZ2 in the dW2 kernel's MFMA-fragment layout, read by the LDS-free dW2 kernel
         # (csrc/mlp_step.hip mlp2_dw2f_kernel; WELLFLOW_MLP_DW2F=0: row-major dZ2 + mlp2_dw2)
         self.dw2_frag = os.environ.get("WELLFLOW_MLP_DW2F", "1") != "0"
-        # W2 transposed (bf16), the one-launch step's dH1 operand image (rewritten each step)
-        self.W2T = torch.empty(256 * 256, dtype=torch.bfloat16, device=dev) if self.hidden == (256, 256) else None
         self.dw2f_split = int(os.environ.get("WELLFLOW_MLP_DW2F_SPLIT", "128"))
         self.red = (torch.zeros(MLP_RED_FLOATS, device=dev)
                     if spread and self.hidden == (256, 256) and self.Fp <= 32 else None)
@@ -225,7 +223,7 @@ class NativeMLP:
         try:
             if red is not None and self.step_fused and not self.dw2_gemm:
                 frag = self.dw2_frag
-                if not C.mlp2_step(Xop, self.Fp, wl[0][0], pl[0][1], wl[1][0], self.W2T, pl[1][1], hw, hb, y,
+                if not C.mlp2_step(Xop, self.Fp, wl[0][0], pl[0][1], wl[1][0], pl[1][1], hw, hb, y,
                                    2.0 * float(grad_scale), B, rows, self.dZ[1], self.pred, red, frag):
                     raise RuntimeError("NativeMLP: fused step refused the shape")
                 if frag:  # dW2 partials as slab rows (their count) summed by the reduce
