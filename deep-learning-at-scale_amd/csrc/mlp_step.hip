@@ -236,7 +236,8 @@ __global__ __launch_bounds__(512, 1) void mlp2_step_kernel(
 
     // ---- prediction, dy, loss of rows 16n + l15 (every wave needs dy); wave 0 lane group g
     // owns row 16g + l15's outputs
-    float dyn[4];
+    float dyn[4], pst = 0.f;
+    int pgr = -1;  // the prediction this lane stores (after the next W2 request, below)
 #pragma unroll
     for (int n = 0; n < 4; ++n) {
       const int r = 16 * n + l15, gr = row0 + r;
@@ -248,7 +249,8 @@ __global__ __launch_bounds__(512, 1) void mlp2_step_kernel(
         const float diff = p - ys[par][r];
         dyn[n] = dy_scale * diff;
         if (wid == 0 && g == n) {
-          if (pred != nullptr) pred[gr] = p;
+          pst = p;
+          pgr = gr;
           lsum += diff * diff;
           db3a += dyn[n];
         }
@@ -283,6 +285,30 @@ __global__ __launch_bounds__(512, 1) void mlp2_step_kernel(
     stamp(8);
     if (ch + 2 * (int)gridDim.x < nchunks) prefetch(ch + 2 * gridDim.x);
 
+    stamp(9);
+    // ---- dH1^T (own units k, K = 256 output units) = W2^T dZ2^T
+#pragma unroll
+    for (int m = 0; m < MT; ++m)
+#pragma unroll
+      for (int n = 0; n < 4; ++n) acc[m][n] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int kt = 0; kt < 8; ++kt) {
+      bf16x8 zb[4];
+#pragma unroll
+      for (int n = 0; n < 4; ++n) zb[n] = *reinterpret_cast<const bf16x8*>(zs + tile_off(16 * n + l15, 32 * kt + 8 * g));
+#pragma unroll
+      for (int m = 0; m < MT; ++m)
+#pragma unroll
+        for (int n = 0; n < 4; ++n)
+          acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wt[m][kt], zb[n], acc[m][n], 0, 0, 0);
+    }
+    stamp(10);
+    w2first();  // the next chunk's first layer-2 fragments
+    // Global stores only AFTER that request: vmcnt counts stores too and completes in order, so
+    // a store issued before a load holds every wait for that load until the store is
+    // acknowledged — with the dZ2 copy-out before dH1, layer 2 of the next chunk waited on it
+    // (5.9k cycles per chunk against a 2.0k MFMA floor, tools/mlp_timeline.py)
+    if (pgr >= 0 && pred != nullptr) pred[pgr] = pst;
     if constexpr (FRAG) {
       // ---- dZ2 copy-out as dW2 A fragments: fragment (s, b) = 32 rows x 16 units, lane
       // (l15, g) 16 B = rows 32s + 8g .. + 7 of unit 16b + l15 (two ds_read_b64_tr_b16); wave w
@@ -311,25 +337,6 @@ __global__ __launch_bounds__(512, 1) void mlp2_step_kernel(
               *reinterpret_cast<const uint4*>(zs + tile_off(r, 8 * c));
       }
     }
-    stamp(9);
-    // ---- dH1^T (own units k, K = 256 output units) = W2^T dZ2^T
-#pragma unroll
-    for (int m = 0; m < MT; ++m)
-#pragma unroll
-      for (int n = 0; n < 4; ++n) acc[m][n] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int kt = 0; kt < 8; ++kt) {
-      bf16x8 zb[4];
-#pragma unroll
-      for (int n = 0; n < 4; ++n) zb[n] = *reinterpret_cast<const bf16x8*>(zs + tile_off(16 * n + l15, 32 * kt + 8 * g));
-#pragma unroll
-      for (int m = 0; m < MT; ++m)
-#pragma unroll
-        for (int n = 0; n < 4; ++n)
-          acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wt[m][kt], zb[n], acc[m][n], 0, 0, 0);
-    }
-    stamp(10);
-    w2first();  // the next chunk's first layer-2 fragments
     // ---- dZ1 = dH1 * [H1 > 0] over the same 8 bytes of h1s; db1 partials
 #pragma unroll
     for (int m = 0; m < MT; ++m) {

@@ -14,8 +14,9 @@ import sys
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
-PHASES = ["stage X/y + B1", "layer 1 + H1 store", "B2 wait", "layer 2 MFMA", "H2 epilogue + head partials",
-          "B3 wait", "dy + dZ2 + sums", "B4 wait", "dZ2 copy-out", "dH1 MFMA", "W2 issue + dZ1 + sums", "dW1"]
+PHASES = ["chunk top", "layer 1 + H1 store", "B2 wait", "layer 2 MFMA", "H2 epilogue + head partials",
+          "B3 wait", "dy + dZ2 + stage next X", "B4 wait", "X prefetch", "dH1 MFMA",
+          "W2 issue + stores + dZ1 + sums", "dW1"]
 
 
 def main():
