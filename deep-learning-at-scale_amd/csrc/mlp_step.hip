@@ -188,17 +188,28 @@ __global__ __launch_bounds__(512, 1) void mlp2_step_kernel(
     for (int m = 0; m < MT; ++m)
 #pragma unroll
       for (int n = 0; n < 4; ++n) acc[m][n] = f32x4{0.f, 0.f, 0.f, 0.f};
+    // H1 fragments rotate through ONE set of 4 registers: fragment n of K step kt + 1 is read
+    // right after the two MFMAs that consume fragment n of step kt (their operands are read at
+    // issue), so each read has 6 MFMAs of cover and no extra VGPRs. The compiler otherwise
+    // issued all 4 reads of a step in front of its MFMAs and waited for each (the layer ran at
+    // 5.9k cycles per chunk against 2.0k for dH1, which it happened to pipeline).
+    bf16x8 hb[4];
+#pragma unroll
+    for (int n = 0; n < 4; ++n) hb[n] = *reinterpret_cast<const bf16x8*>(h1s + tile_off(16 * n + l15, 8 * g));
     static_for<0, 8>([&](auto kc) {
       constexpr int kt = decltype(kc)::value;
-      bf16x8 hb[4];
 #pragma unroll
-      for (int n = 0; n < 4; ++n) hb[n] = *reinterpret_cast<const bf16x8*>(h1s + tile_off(16 * n + l15, 32 * kt + 8 * g));
+      for (int n = 0; n < 4; ++n) {
 #pragma unroll
-      for (int m = 0; m < MT; ++m)
-#pragma unroll
-        for (int n = 0; n < 4; ++n)
+        for (int m = 0; m < MT; ++m)
           acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w2r[kt % WD][m], hb[n], acc[m][n], 0, 0, 0);
-      if constexpr (kt + WD < 8) {  // refill the slot just consumed
+        if constexpr (kt + 1 < 8) {
+          __builtin_amdgcn_sched_barrier(0);  // keep the read here: the scheduler sinks it to its use
+          hb[n] = *reinterpret_cast<const bf16x8*>(h1s + tile_off(16 * n + l15, 32 * (kt + 1) + 8 * g));
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      }
+      if constexpr (kt + WD < 8) {  // refill the W2 slot just consumed
 #pragma unroll
         for (int m = 0; m < MT; ++m) w2r[kt % WD][m] = w2frag(m, kt + WD);
       }
