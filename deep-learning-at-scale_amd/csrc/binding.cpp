@@ -295,7 +295,8 @@ bool lstm_backward_dw(const at::Tensor& WhhT, const at::Tensor& XH, const at::Te
                       const at::Tensor& S, const at::Tensor& DG, const at::Tensor& dcarry,
                       const at::Tensor& dy, const at::Tensor& w_out, const at::Tensor& gW,
                       int64_t B, int64_t T, int64_t F, int64_t KX, int64_t H, int64_t variant,
-                      int64_t chunk, int64_t ksplit, const c10::optional<at::Tensor>& sync) {
+                      int64_t chunk, int64_t ksplit, const c10::optional<at::Tensor>& sync,
+                      const c10::optional<at::Tensor>& dw_slab) {
   auto d = lstm_dims(B, T, F, KX, H);
   d.bwd_variant = (int)variant;
   check_lstm_state(XH, Cst, S, d);
@@ -331,6 +332,11 @@ bool lstm_backward_dw(const at::Tensor& WhhT, const at::Tensor& XH, const at::Te
       return v == nullptr ? 7 : std::atoi(v);
     }();
     e.big_tile = big;
+    if (dw_slab.has_value()) {  // split-K partials plain-stored, one reduce (gemm.hip launch_dw_288w)
+      check_t(*dw_slab, at::kFloat, "dw_slab");
+      e.slab = fp(*dw_slab);
+      e.slab_cap = dw_slab->numel();
+    }
     const bf16_t* A = bfp(DG) + (size_t)t0 * B * G;
     const bf16_t* Bm = bfp(XH) + (size_t)t0 * B * KA;
     // whole-tile over-read of XH columns 576..639 stays inside XH (its slab T follows)

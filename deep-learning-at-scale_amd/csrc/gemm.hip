@@ -259,7 +259,8 @@ template <int BM, int BN, int NSLOT, int WM, int WN, int PRIO, int BKD = 32>
 __global__ __launch_bounds__(64 * WM * WN) void gemm_dw_h_kernel(const bf16_t* __restrict__ A, long lda,
                                                         const bf16_t* __restrict__ B, long ldb, int N,
                                                         int kchunk, int tiles, float* __restrict__ out,
-                                                        long ldo, float alpha) {
+                                                        long ldo, float alpha, float* __restrict__ slab,
+                                                        long slab_stride) {
   using C = GemmCfg<BM, BN, MN_CONTIG, MN_CONTIG, WM, WN>;
   constexpr int STAGE = (BM + BN) * BKD * 2;
   __shared__ __attribute__((aligned(16))) char smem[NSLOT * STAGE];
@@ -270,6 +271,16 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_dw_h_kernel(const bf16_t* _
   f32x4 acc[C::TM][C::TN];
   gemm_mainloop_glds_h<C, NSLOT, PRIO, BKD>(A, lda, B, ldb, split * kchunk, kchunk / BKD, m0, n0, smem, acc);
   const AccCoord<C> cc(m0, n0);
+  if (slab != nullptr) {  // this split's partial tile, plain-stored (dw_slab_reduce_kernel adds the splits)
+    float* o = slab + (size_t)split * slab_stride;
+#pragma unroll
+    for (int j = 0; j < C::TN; ++j)
+#pragma unroll
+      for (int i = 0; i < C::TM; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) o[(size_t)cc.row(i, r) * ldo + cc.col(j)] = alpha * acc[i][j][r];
+    return;
+  }
 #pragma unroll
   for (int j = 0; j < C::TN; ++j)
 #pragma unroll
@@ -316,10 +327,32 @@ static void launch_dw_192h(const bf16_t* A, long lda, const bf16_t* B, long ldb,
                        e.outF, e.ldo, e.alpha);
   else if (nslot == 5)
     hipLaunchKernelGGL((gemm_dw_h_kernel<BM, BN, 5, 4, 2, 1>), grid, dim3(512), 0, s, A, lda, B, ldb, N, kchunk,
-                       tiles, e.outF, e.ldo, e.alpha);
+                       tiles, e.outF, e.ldo, e.alpha, nullptr, 0L);
   else
     hipLaunchKernelGGL((gemm_dw_h_kernel<BM, BN, 4, 4, 2, 1>), grid, dim3(512), 0, s, A, lda, B, ldb, N, kchunk,
-                       tiles, e.outF, e.ldo, e.alpha);
+                       tiles, e.outF, e.ldo, e.alpha, nullptr, 0L);
+}
+
+// out[i] += sum over the nsplit slab slices (float4 per thread, all slice loads in flight)
+__global__ __launch_bounds__(256) void dw_slab_reduce_kernel(float* __restrict__ out, const float* __restrict__ slab,
+                                                             int nsplit, long n4) {
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n4) return;
+  const float4* src = reinterpret_cast<const float4*>(slab) + i;
+  float4 a = reinterpret_cast<float4*>(out)[i];
+  for (int s0 = 0; s0 < nsplit; s0 += 8) {
+    float4 v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = s0 + j < nsplit ? src[(size_t)(s0 + j) * n4] : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      a.x += v[j].x;
+      a.y += v[j].y;
+      a.z += v[j].z;
+      a.w += v[j].w;
+    }
+  }
+  reinterpret_cast<float4*>(out)[i] = a;
 }
 
 // 256x288, 8 waves of 64x144, 4-slot 32-deep ring (136 KiB; a 2-stage 64-deep ring spilled 61 VGPRs)
@@ -342,8 +375,17 @@ static void launch_dw_288w(const bf16_t* A, long lda, const bf16_t* B, long ldb,
   int nsplit = ksplit;
   while (nsplit > 1 && K % (64 * nsplit) != 0) --nsplit;
   const int kchunk = K / nsplit;
+  // split-K partials: fp32 atomics into the output (2048 x 576 x 16 splits = 75 MB of 64-B-segment
+  // atomics at the tail of the kernel) or, given a slab, plain stores + one reduce
+  const long mn = (long)M * N;
+  const bool use_slab = e.slab != nullptr && e.ldo == N && nsplit > 1 && (long)nsplit * mn <= e.slab_cap && mn % 4 == 0;
   hipLaunchKernelGGL((gemm_dw_h_kernel<BM, BN, 4, 4, 2, 1, 32>), dim3(tiles * nsplit), dim3(512), 0, s, A, lda, B,
-                     ldb, N, kchunk, tiles, e.outF, e.ldo, e.alpha);
+                     ldb, N, kchunk, tiles, e.outF, e.ldo, e.alpha, use_slab ? e.slab : nullptr, use_slab ? mn : 0L);
+  if (use_slab) {
+    const long n4 = mn / 4;
+    hipLaunchKernelGGL(dw_slab_reduce_kernel, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, s, e.outF,
+                       (const float*)e.slab, nsplit, n4);
+  }
 }
 
 void launch_gemm(const bf16_t* A, long lda, int a_mn, const bf16_t* B, long ldb, int b_mn, int M,

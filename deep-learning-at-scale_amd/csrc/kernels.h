@@ -25,6 +25,8 @@ struct GemmEpilogue {
   const long long* seed_dev = nullptr;  // optional device step counter mixed into the seed (graph replays)
   int stage_ok = 0;              // host-verified: bf16 output/mask tiles may go through LDS
   int big_tile = 0;              // MN x MN split-K weight gradient: 1 = 256x128 8-wave tile, 2 = 128x288
+  float* slab = nullptr;         // split-K partial slab (256x288 dW tile, ldo == N): plain stores of
+  long slab_cap = 0;             // each split's tile, then one reduce adds the splits into outF
 };
 
 void launch_gemm(const bf16_t* A, long lda, int a_mn, const bf16_t* B, long ldb, int b_mn, int M,

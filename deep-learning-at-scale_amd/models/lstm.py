@@ -224,6 +224,12 @@ class NativeLSTM:
         # timesteps per overlapped dW GEMM chunk; 0 = serial dW at the end (measured faster:
         # the BPTT chain already fills every CU, overlapping only adds contention)
         self.dw_chunk = 0
+        # split-K partial slab of the dW GEMM (csrc/gemm.hip launch_dw_288w): each split's tile
+        # plain-stored and one reduce, instead of fp32 atomics into gW (WELLFLOW_DW_SLAB=0: atomics)
+        self.dw_slab = None
+        if os.environ.get("WELLFLOW_DW_SLAB", "1") != "0":
+            self.dw_slab = torch.empty(max(1, min(32, T * B // 16384)) * lay.G * lay.KA,
+                                       dtype=torch.float32, device=dev)
         self._fallback_noted = set()
         self.last_backward_persistent = False
         self.sync_weights()
@@ -389,7 +395,8 @@ class NativeLSTM:
             ksplit = max(1, ksplit * self.dw_chunk // self.T)
         pb = C.lstm_backward_dw(self.WhhT, self.XH, self.Cst, self.S, self.DG, self.dcarry, self.dy,
                                 w_out, gW, *self._dims(B), self.bwd_variant, self.dw_chunk, ksplit,
-                                self.sync_bwd if self.persistent_bwd and self.dw_chunk <= 0 else None)
+                                self.sync_bwd if self.persistent_bwd and self.dw_chunk <= 0 else None,
+                                self.dw_slab if self.dw_chunk <= 0 else None)
         self.last_backward_persistent = bool(pb)
         if not pb and self.dw_chunk <= 0:
             self._note_fallback("backward", self.persistent_bwd)

@@ -213,7 +213,7 @@ def _lstm_bwd(dpred: torch.Tensor, XH: torch.Tensor, Cst: torch.Tensor, S: torch
     sync = persistent_sync_buffer(B, 64, dev)
     ksplit = max(1, min(32, T * B // 16384))
     C.lstm_backward_dw(Wp[lay.G * lay.KA:], XH, Cst, S, DG, dcarry, dy, w_out.contiguous(), gW, *dims, 8, 0,
-                       ksplit, sync)
+                       ksplit, sync, None)
     if pstat_error(decode_pstat(sync[-PSTAT_WORDS:].tolist())):
         raise RuntimeError("wellflow::lstm_regressor: persistent backward left work undone "
                            f"{decode_pstat(sync[-PSTAT_WORDS:].tolist())}")
