@@ -41,7 +41,7 @@ __global__ __launch_bounds__(512, 1) void mlp2_step_kernel(
     const bf16_t* __restrict__ W2, const float* __restrict__ b2, const float* __restrict__ w3,
     const float* __restrict__ b3, const float* __restrict__ y, float dy_scale, int B,
     const long long* __restrict__ rows, long nrows, bf16_t* __restrict__ dZ2, float* __restrict__ pred,
-    float* __restrict__ red, unsigned long long* __restrict__ stamps = nullptr) {
+    float* __restrict__ red, int prio, unsigned long long* __restrict__ stamps = nullptr) {
   constexpr int MT = 2, NW = 8, XB = MF_ROWS * MF_XROW;
   __shared__ __attribute__((aligned(16))) char xs[2 * XB];              // X tiles (double-buffered)
   __shared__ __attribute__((aligned(16))) char h1s[MF_ROWS * MF_H * 2];  // H1 -> dZ1 (own columns)
@@ -147,6 +147,9 @@ __global__ __launch_bounds__(512, 1) void mlp2_step_kernel(
   __syncthreads();
   if ((int)blockIdx.x + (int)gridDim.x < nchunks) prefetch(blockIdx.x + gridDim.x);
   w2first();
+  // static priority for the second-dispatched half (waves 4-7), which otherwise loses every VALU
+  // arbitration to its SIMD partner (MI355X_MICROARCH.md "two waves per SIMD", item 4)
+  if (prio && __builtin_amdgcn_readfirstlane(wid) >= 4) __builtin_amdgcn_s_setprio(1);
   int par = 0;
   for (int ch = blockIdx.x; ch < nchunks; ch += gridDim.x, par ^= 1) {
     const int row0 = ch * MF_ROWS;
@@ -478,7 +481,7 @@ __global__ __launch_bounds__(512, 1) void mlp2_dw2f_kernel(const bf16_t* __restr
                                                            int Fp, const long long* __restrict__ rows, long nrows,
                                                            const bf16_t* __restrict__ W1, const float* __restrict__ b1,
                                                            int kchunk, float* __restrict__ dW2, float* __restrict__ slab,
-                                                           int slab_row0) {
+                                                           int slab_row0, int prio) {
   __shared__ __attribute__((aligned(16))) char smem[DW2F_SLOTS * DW2F_SLOT + DW2F_MAX_ROWS * 4];
   int* ridx = reinterpret_cast<int*>(smem + DW2F_SLOTS * DW2F_SLOT);
   const int tid = threadIdx.x, lane = tid & 63, l15 = lane & 15, g = lane >> 4;
@@ -491,6 +494,7 @@ __global__ __launch_bounds__(512, 1) void mlp2_dw2f_kernel(const bf16_t* __restr
   // row ids of the range (identity without `rows`)
   for (int i = tid; i < kchunk; i += 512) ridx[i] = rows != nullptr ? (int)data_row(rows, kbeg + i, nrows) : kbeg + i;
   __syncthreads();
+  if (prio && wid >= 4) __builtin_amdgcn_s_setprio(1);  // static priority for the younger half
 
   // recompute operands: W1 rows of the wave's 32 in units (K = features 8g .. 8g + 7; zero past Fp)
   bf16x8 w1f[2];
@@ -614,15 +618,21 @@ bool launch_mlp2_step(const bf16_t* X, int Fp, const bf16_t* W1, const float* b1
   // phase stamps (tools/mlp_timeline.py; results unchanged, so not a WF_DIAG-only switch):
   // into dW2 slab rows 200.. of the scratch (unused by a step of <= 200 dW2 ranges)
   static const bool stamp = std::getenv("WELLFLOW_MLP_STAMP") != nullptr;
+  // WELLFLOW_MLP_PRIO=0/1: static s_setprio 1 for waves 4-7 off / on (default on: +0.2 to +1.1 %
+  // in three interleaved pairs, chunk span 17.5k -> 17.1k cycles, profiles/r4/mlp_prio)
+  static const int prio = [] {
+    const char* v = std::getenv("WELLFLOW_MLP_PRIO");
+    return v == nullptr ? 1 : std::atoi(v);
+  }();
   if (stamp && Fp <= 16 && dz_frag) {
     hipLaunchKernelGGL((mlp2_step_kernel<1, true, true>), dim3(grid), dim3(512), 0, s, X, Fp, W1, b1, W2, b2, w3, b3, y,
-                       dy_scale, B, rows, nrows, dZ2, pred, red,
+                       dy_scale, B, rows, nrows, dZ2, pred, red, prio,
                        reinterpret_cast<unsigned long long*>(red + kMlpRedSlab2Off + 200L * 65536));
     return true;
   }
 #define WF_STEP(NFT, FR)                                                                                            \
   hipLaunchKernelGGL((mlp2_step_kernel<NFT, FR>), dim3(grid), dim3(512), 0, s, X, Fp, W1, b1, W2, b2, w3, b3, y, \
-                     dy_scale, B, rows, nrows, dZ2, pred, red)
+                     dy_scale, B, rows, nrows, dZ2, pred, red, prio)
   if (Fp <= 16) {
     if (dz_frag) WF_STEP(1, true); else WF_STEP(1, false);
   } else {
@@ -640,6 +650,12 @@ int launch_mlp2_dw2f(const bf16_t* dZ2F, const bf16_t* X, int Fp, const long lon
                      const float* b1, int B, int nsplit, float* red, hipStream_t s) {
   if (B <= 0 || B % MF_ROWS != 0 || Fp > 32 || Fp % 8 != 0 || red == nullptr) return 0;
   constexpr int kMaxBlock = 128 * DW2F_MAX_ROWS;  // rows per launch
+  // WELLFLOW_DW2F_PRIO=0/1: static s_setprio 1 for waves 4-7 off / on (default on: 48.2 -> 47.0 us,
+  // +0.3 to +0.6 % in three interleaved pairs, profiles/r4/mlp_prio)
+  static const int prio = [] {
+    const char* v = std::getenv("WELLFLOW_DW2F_PRIO");
+    return v == nullptr ? 1 : std::atoi(v);
+  }();
   int srow = 0;  // slab rows used so far (the launches' ranges stack)
   for (int r0 = 0; r0 < B; r0 += kMaxBlock) {
     const int Bb = B - r0 < kMaxBlock ? B - r0 : kMaxBlock;
@@ -653,7 +669,7 @@ int launch_mlp2_dw2f(const bf16_t* dZ2F, const bf16_t* X, int Fp, const long lon
     hipLaunchKernelGGL(mlp2_dw2f_kernel, dim3(2 * ns), dim3(512), 0, s, dZ2F + (size_t)r0 * MF_H,
                        rows != nullptr ? X : X + (size_t)r0 * Fp, Fp, rows != nullptr ? rows + r0 : nullptr,
                        rows != nullptr ? nrows : (long)Bb, W1, b1, kchunk, red + (size_t)kMlpRedCopies * kMlpRedRow,
-                       red + kMlpRedSlab2Off, srow);
+                       red + kMlpRedSlab2Off, srow, prio);
     srow += ns;
   }
   return srow < kMlpRedSlab2Rows ? srow : kMlpRedSlab2Rows;

@@ -1,0 +1,15 @@
+# round 4, session 19: MLP step kernel, static s_setprio 1 for waves 4-7 (WELLFLOW_MLP_PRIO) A/B + timeline
+set -o pipefail
+export TMPDIR=/tmp
+mkdir -p gpurun_out/r4
+WELLFLOW_MLP_PRIO=1 timeout -k 10 300 python -u -m pytest tests/test_engines_gpu.py -v -m gpu \
+  --timeout 120 --timeout-method thread -k "mlp" > gpurun_out/r4/s19_tests.log 2>&1; rc=$?
+grep -E "passed|failed" gpurun_out/r4/s19_tests.log | tail -1
+[ $rc -eq 0 ] || { tail -40 gpurun_out/r4/s19_tests.log; exit $rc; }
+for cfg in 1 0 1 0 1 0; do
+  WELLFLOW_MLP_PRIO=$cfg timeout -k 10 200 python bench.py --model mlp --steps 600 --warmup 10 --secondary none --parity none \
+    > gpurun_out/r4/mlp_s19_$cfg.log 2>&1 || { tail -20 gpurun_out/r4/mlp_s19_$cfg.log; exit 1; }
+  echo "PRIO=$cfg $(grep -o '"value": [0-9.]*, "unit": "rows/s", "n_gpus": 1, "steps": [0-9]*, "warmup": [0-9]*, "ms_per_step": [0-9.]*' gpurun_out/r4/mlp_s19_$cfg.log)"
+done
+WELLFLOW_MLP_PRIO=1 WELLFLOW_MLP_STAMP=1 timeout -k 10 120 python -u tools/mlp_timeline.py > gpurun_out/r4/mlp_timeline19.txt 2>&1 || { tail -20 gpurun_out/r4/mlp_timeline19.txt; exit 1; }
+grep -v amdgpu.ids gpurun_out/r4/mlp_timeline19.txt
