@@ -477,6 +477,7 @@ constexpr int DW2F_MAX_ROWS = 2048;                      // rows per workgroup (
 constexpr int DW2F_SLOTS = 4;                            // ring depth (chunks)
 constexpr int DW2F_ABYTES = 32 * 1024;                   // 2 steps x 16 dZ2 fragments
 constexpr int DW2F_SLOT = DW2F_ABYTES + MF_ROWS * 64;    // + X tile [64 rows][64 B]
+template <bool PF>  // PF: LDS fragments read a half-chunk ahead (WELLFLOW_DW2F_PF, A/B)
 __global__ __launch_bounds__(512, 1) void mlp2_dw2f_kernel(const bf16_t* __restrict__ dZ2F, const bf16_t* __restrict__ X,
                                                            int Fp, const long long* __restrict__ rows, long nrows,
                                                            const bf16_t* __restrict__ W1, const float* __restrict__ b1,
@@ -555,15 +556,35 @@ __global__ __launch_bounds__(512, 1) void mlp2_dw2f_kernel(const bf16_t* __restr
     asm volatile("" ::: "memory");
     issue(min(c + DW2F_SLOTS - 1, last), (c + DW2F_SLOTS - 1) & (DW2F_SLOTS - 1));
     const char* st = smem + slot * DW2F_SLOT;
-#pragma unroll
-    for (int s2 = 0; s2 < 2; ++s2) {
-      bf16x8 hb[2];
-      bf16x8 xf[2];
+    // LDS fragments one half-chunk ahead, pinned: half 0's 10 reads before its recompute, half
+    // 1's between half 0's recompute and its dW MFMAs. Left to the scheduler, each pair of dZ2
+    // reads sat right before its 4 MFMAs behind an lgkmcnt(0) (LDS latency every 4 MFMAs)
+    bf16x8 xfa[2][2], afa[2][8];
+    auto frags = [&](int s2) {
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
         const int r = 32 * s2 + xr0 + 4 * h;
-        xf[h] = *reinterpret_cast<const bf16x8*>(st + DW2F_ABYTES + r * 64 + ((xg ^ ((r >> 3) & 3)) << 4));
+        xfa[s2][h] = *reinterpret_cast<const bf16x8*>(st + DW2F_ABYTES + r * 64 + ((xg ^ ((r >> 3) & 3)) << 4));
       }
+      __builtin_amdgcn_sched_barrier(0);  // X first: the recompute needs it before the dZ2 fragments
+#pragma unroll
+      for (int mb = 0; mb < 8; ++mb)
+        afa[s2][mb] = *reinterpret_cast<const bf16x8*>(st + (s2 * 16 + 8 * wm + mb) * 1024 + lane * 16);
+    };
+    if constexpr (PF) {
+      frags(0);
+      __builtin_amdgcn_sched_barrier(0);
+    } else {
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int r = xr0 + 4 * h;
+        xfa[0][h] = *reinterpret_cast<const bf16x8*>(st + DW2F_ABYTES + r * 64 + ((xg ^ ((r >> 3) & 3)) << 4));
+      }
+    }
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) {
+      bf16x8 hb[2];
+      const bf16x8(&xf)[2] = xfa[s2];
 #pragma unroll
       for (int nb = 0; nb < 2; ++nb) {
         const f32x4 c0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xf[0], w1f[nb], f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
@@ -575,11 +596,29 @@ __global__ __launch_bounds__(512, 1) void mlp2_dw2f_kernel(const bf16_t* __restr
         typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
         hb[nb] = __builtin_bit_cast(bf16x8, (u32x4_t{p0, p1, p2, p3}));
       }
+      if constexpr (PF) {
+        if (s2 == 0) {
+          __builtin_amdgcn_sched_barrier(0);
+          frags(1);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      } else {
+        if (s2 == 0) {
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            const int r = 32 + xr0 + 4 * h;
+            xfa[1][h] = *reinterpret_cast<const bf16x8*>(st + DW2F_ABYTES + r * 64 + ((xg ^ ((r >> 3) & 3)) << 4));
+          }
+        }
+#pragma unroll
+        for (int mb = 0; mb < 8; ++mb)
+          afa[s2][mb] = *reinterpret_cast<const bf16x8*>(st + (s2 * 16 + 8 * wm + mb) * 1024 + lane * 16);
+      }
 #pragma unroll
       for (int mb = 0; mb < 8; ++mb) {
-        const bf16x8 a = *reinterpret_cast<const bf16x8*>(st + (s2 * 16 + 8 * wm + mb) * 1024 + lane * 16);
 #pragma unroll
-        for (int nb = 0; nb < 2; ++nb) acc[mb][nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, hb[nb], acc[mb][nb], 0, 0, 0);
+        for (int nb = 0; nb < 2; ++nb)
+          acc[mb][nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(afa[s2][mb], hb[nb], acc[mb][nb], 0, 0, 0);
       }
     }
   }
@@ -618,10 +657,10 @@ bool launch_mlp2_step(const bf16_t* X, int Fp, const bf16_t* W1, const float* b1
   // phase stamps (tools/mlp_timeline.py; results unchanged, so not a WF_DIAG-only switch):
   // into dW2 slab rows 200.. of the scratch (unused by a step of <= 200 dW2 ranges)
   static const bool stamp = std::getenv("WELLFLOW_MLP_STAMP") != nullptr;
-  // WELLFLOW_MLP_PRIO=0/1: static s_setprio 1 for waves 4-7 off / on (default on: +0.2 to +1.1 %
+  // WELLFLOW_STEP_PRIO=0/1: static s_setprio 1 for waves 4-7 off / on (default on: +0.2 to +1.1 %
   // in three interleaved pairs, chunk span 17.5k -> 17.1k cycles, profiles/r4/mlp_prio)
   static const int prio = [] {
-    const char* v = std::getenv("WELLFLOW_MLP_PRIO");
+    const char* v = std::getenv("WELLFLOW_STEP_PRIO");
     return v == nullptr ? 1 : std::atoi(v);
   }();
   if (stamp && Fp <= 16 && dz_frag) {
@@ -656,6 +695,11 @@ int launch_mlp2_dw2f(const bf16_t* dZ2F, const bf16_t* X, int Fp, const long lon
     const char* v = std::getenv("WELLFLOW_DW2F_PRIO");
     return v == nullptr ? 1 : std::atoi(v);
   }();
+  // WELLFLOW_DW2F_PF=0/1: per-step fragment reads / reads a half-chunk ahead
+  static const bool pf = [] {
+    const char* v = std::getenv("WELLFLOW_DW2F_PF");
+    return v == nullptr ? true : std::atoi(v) != 0;
+  }();
   int srow = 0;  // slab rows used so far (the launches' ranges stack)
   for (int r0 = 0; r0 < B; r0 += kMaxBlock) {
     const int Bb = B - r0 < kMaxBlock ? B - r0 : kMaxBlock;
@@ -666,10 +710,16 @@ int launch_mlp2_dw2f(const bf16_t* dZ2F, const bf16_t* X, int Fp, const long lon
     const int kchunk = (chunks / ns) * MF_ROWS;
     if (kchunk > DW2F_MAX_ROWS) return 0;  // (unreachable for B % 64 == 0)
     // row block r0: dZ2 fragments start at step r0 / 32; X through `rows` (offset) or directly
-    hipLaunchKernelGGL(mlp2_dw2f_kernel, dim3(2 * ns), dim3(512), 0, s, dZ2F + (size_t)r0 * MF_H,
-                       rows != nullptr ? X : X + (size_t)r0 * Fp, Fp, rows != nullptr ? rows + r0 : nullptr,
-                       rows != nullptr ? nrows : (long)Bb, W1, b1, kchunk, red + (size_t)kMlpRedCopies * kMlpRedRow,
-                       red + kMlpRedSlab2Off, srow, prio);
+    if (pf)
+      hipLaunchKernelGGL(mlp2_dw2f_kernel<true>, dim3(2 * ns), dim3(512), 0, s, dZ2F + (size_t)r0 * MF_H,
+                         rows != nullptr ? X : X + (size_t)r0 * Fp, Fp, rows != nullptr ? rows + r0 : nullptr,
+                         rows != nullptr ? nrows : (long)Bb, W1, b1, kchunk, red + (size_t)kMlpRedCopies * kMlpRedRow,
+                         red + kMlpRedSlab2Off, srow, prio);
+    else
+      hipLaunchKernelGGL(mlp2_dw2f_kernel<false>, dim3(2 * ns), dim3(512), 0, s, dZ2F + (size_t)r0 * MF_H,
+                         rows != nullptr ? X : X + (size_t)r0 * Fp, Fp, rows != nullptr ? rows + r0 : nullptr,
+                         rows != nullptr ? nrows : (long)Bb, W1, b1, kchunk, red + (size_t)kMlpRedCopies * kMlpRedRow,
+                         red + kMlpRedSlab2Off, srow, prio);
     srow += ns;
   }
   return srow < kMlpRedSlab2Rows ? srow : kMlpRedSlab2Rows;
