@@ -379,8 +379,17 @@ static void launch_dw_288w(const bf16_t* A, long lda, const bf16_t* B, long ldb,
   // atomics at the tail of the kernel) or, given a slab, plain stores + one reduce
   const long mn = (long)M * N;
   const bool use_slab = e.slab != nullptr && e.ldo == N && nsplit > 1 && (long)nsplit * mn <= e.slab_cap && mn % 4 == 0;
-  hipLaunchKernelGGL((gemm_dw_h_kernel<BM, BN, 4, 4, 2, 1, 32>), dim3(tiles * nsplit), dim3(512), 0, s, A, lda, B,
-                     ldb, N, kchunk, tiles, e.outF, e.ldo, e.alpha, use_slab ? e.slab : nullptr, use_slab ? mn : 0L);
+  // WELLFLOW_DW288_PRIO: 1 = s_setprio 1 around each MFMA cluster, 3 = static priority for waves 4-7
+  static const int prio = [] {
+    const char* v = std::getenv("WELLFLOW_DW288_PRIO");
+    return v == nullptr ? 1 : std::atoi(v);
+  }();
+  if (prio == 3)
+    hipLaunchKernelGGL((gemm_dw_h_kernel<BM, BN, 4, 4, 2, 3, 32>), dim3(tiles * nsplit), dim3(512), 0, s, A, lda, B,
+                       ldb, N, kchunk, tiles, e.outF, e.ldo, e.alpha, use_slab ? e.slab : nullptr, use_slab ? mn : 0L);
+  else
+    hipLaunchKernelGGL((gemm_dw_h_kernel<BM, BN, 4, 4, 2, 1, 32>), dim3(tiles * nsplit), dim3(512), 0, s, A, lda, B,
+                       ldb, N, kchunk, tiles, e.outF, e.ldo, e.alpha, use_slab ? e.slab : nullptr, use_slab ? mn : 0L);
   if (use_slab) {
     const long n4 = mn / 4;
     hipLaunchKernelGGL(dw_slab_reduce_kernel, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, s, e.outF,

@@ -597,6 +597,10 @@ __device__ __forceinline__ void gemm_mainloop_glds_h(const bf16_t* __restrict__ 
 #pragma unroll
     for (int j = 0; j < C::TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   if (nh <= 0) return;
+  // PRIO 3: static s_setprio 1 for the second-dispatched half of the waves (no per-cluster flips)
+  if constexpr (PRIO == 3) {
+    if (wid >= C::NT / 128) __builtin_amdgcn_s_setprio(1);
+  }
   OA oa;
   OB ob;
   oa.init(A, lda, m0, kbeg, wid, lane);
