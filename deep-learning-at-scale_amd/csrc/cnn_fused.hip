@@ -103,7 +103,7 @@ __global__ __launch_bounds__(512, 1) void cnn_fwd_kernel(
     const float* __restrict__ x, int B, int L, const bf16_t* __restrict__ WcA, int Kc,
     const bf16x4* __restrict__ WdF, const float* __restrict__ bd, int O, const float* __restrict__ y,
     float* __restrict__ dout, float* __restrict__ pred, float* __restrict__ part, int taps, int loss_kind,
-    float clip, float scale, float keep_scale, int drop, unsigned seed, const long long* __restrict__ rng) {
+    float clip, float scale, float keep_scale, int drop, unsigned seed, const long long* __restrict__ rng, int prio) {
   constexpr int XR = (T + 6) / 4 * 4;  // x samples per lane: 4q .. 4q + T + 2, whole float4s
   constexpr int NFRAG = T * NFB * 64;
   // ONE static LDS object: the dense weights' fragment image, then the wave partials
@@ -117,6 +117,7 @@ __global__ __launch_bounds__(512, 1) void cnn_fwd_kernel(
   }
   const int lane = threadIdx.x & 63, l15 = lane & 15, q = lane >> 4;
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  if (prio && wid >= 4) __builtin_amdgcn_s_setprio(1);  // static priority, younger half (A/B)
   // conv weights as the A operand: A[f = 16b + l15][kk = 4q + jj] (bias at kk = taps)
   bf16x4 wc[NFB];
 #pragma unroll
@@ -241,10 +242,11 @@ __global__ __launch_bounds__(512, 1) void cnn_bwd_kernel(
     const float* __restrict__ x, int B, int L, const bf16_t* __restrict__ WcA, int Kc,
     const bf16x4* __restrict__ WdB, const float* __restrict__ dout, int T, int taps, float keep_scale, int drop,
     unsigned seed, const long long* __restrict__ rng, int nch, float* __restrict__ part_wd,
-    float* __restrict__ part_wc) {
+    float* __restrict__ part_wc, int prio) {
   __shared__ __attribute__((aligned(16))) f32x4 red[CNN_NW * TG * NFB * 64];
   const int lane = threadIdx.x & 63, l15 = lane & 15, q = lane >> 4;
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  if (prio && wid >= 4) __builtin_amdgcn_s_setprio(1);  // static priority, younger half (A/B)
   const int ntg = (T + TG - 1) / TG;
   // logical block: consecutive ids (one XCD under the round-robin deal) share a window chunk
   const int lb = xcd_remap(blockIdx.x, gridDim.x);
@@ -506,6 +508,15 @@ void launch_cnn_pack(const float* Wc, const float* Wd, const CnnDims& d, bf16_t*
                      d.O, WcA, WdF, WdB);
 }
 
+// WELLFLOW_CNN_PRIO=0/1: static s_setprio 1 for waves 4-7 of the forward / backward kernels
+static int cnn_prio() {
+  static const int p = [] {
+    const char* v = std::getenv("WELLFLOW_CNN_PRIO");
+    return v == nullptr ? 0 : std::atoi(v);
+  }();
+  return p;
+}
+
 void launch_cnn_forward(const float* x, int B, const CnnDims& d, const bf16_t* WcA, const bf16_t* WdF,
                         const float* bd, const float* y, float* dout, float* pred, float* part, int train,
                         int loss_kind, float clip, float scale, unsigned seed, const long long* rng, hipStream_t s) {
@@ -515,11 +526,11 @@ void launch_cnn_forward(const float* x, int B, const CnnDims& d, const bf16_t* W
   if (train)
     hipLaunchKernelGGL((cnn_fwd_kernel<CNN_NFB, CNN_T, true>), dim3(grid), dim3(512), 0, s, x, B, d.L, WcA, d.Kc,
                        reinterpret_cast<const bf16x4*>(WdF), bd, d.O, y, dout, pred, part, d.taps, loss_kind, clip,
-                       scale, keep_scale, drop, seed, rng);
+                       scale, keep_scale, drop, seed, rng, cnn_prio());
   else
     hipLaunchKernelGGL((cnn_fwd_kernel<CNN_NFB, CNN_T, false>), dim3(grid), dim3(512), 0, s, x, B, d.L, WcA, d.Kc,
                        reinterpret_cast<const bf16x4*>(WdF), bd, d.O, y, dout, pred, part, d.taps, loss_kind, clip,
-                       scale, keep_scale, 0, seed, rng);
+                       scale, keep_scale, 0, seed, rng, cnn_prio());
 }
 
 void launch_cnn_backward(const float* x, int B, const CnnDims& d, const bf16_t* WcA, const bf16_t* WdB,
@@ -531,7 +542,7 @@ void launch_cnn_backward(const float* x, int B, const CnnDims& d, const bf16_t* 
   const float keep_scale = drop ? 1.f / (1.f - d.drop_p) : 1.f;
   hipLaunchKernelGGL((cnn_bwd_kernel<CNN_NFB, CNN_TG>), dim3(ntg * nch), dim3(512), 0, s, x, B, d.L, WcA, d.Kc,
                      reinterpret_cast<const bf16x4*>(WdB), dout, d.T, d.taps, keep_scale, drop, seed, rng, nch,
-                     part_wd, part_wc);
+                     part_wd, part_wc, cnn_prio());
 }
 
 void launch_cnn_reduce(const float* part_wd, const float* part_wc, const float* part_f, int B, const CnnDims& d,
