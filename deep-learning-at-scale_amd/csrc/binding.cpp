@@ -186,13 +186,10 @@ void lstm_forward(const at::Tensor& XH, const at::Tensor& Wp, const at::Tensor& 
   for (int t = 0; t < d.T; ++t) wf::launch_lstm_fwd_step(t, bfp(XH), bfp(Wp), bfp(Cst), bfp(S), fp(cf32), d, s);
 }
 
-// A persistent kernel's sync buffer: int32, 16-B aligned. The launcher zeroes its per-launch
-// block with ONE memset node from that start covering a multiple of 16 B, and refuses the
-// launch otherwise (persistent_reset_ok). Round 2's memset started 4 B past a 16-B boundary
-// and left 0x04040404 in its first word under graph replay, which drained every workgroup
-// (profiles/r3_early_exit.md). What is enforced here is exactly that precondition — 16-B
-// alignment — not "own allocation": tests/test_kernels_gpu.py replays a captured step whose
-// sync buffer sits 16-B aligned at a non-zero offset inside a larger allocation.
+// A persistent kernel's sync buffer: int32, 16-B aligned, zeroed once by its owner. No launch
+// resets it (csrc/persistent_sync.h: monotonic launch epochs and arrival counters), so there is
+// no memset node in a captured step at all (round 2's early exit was an unaligned per-launch
+// memset node under graph replay, profiles/r3_early_exit.md).
 void check_sync(const at::Tensor& sync) {
   check_t(sync, at::kInt, "sync");  // check_t: 16-B aligned data pointer
 }
@@ -205,7 +202,7 @@ bool persistent_status(int st, const char* what) {
 
 // All T steps in one persistent launch per sub-batch (lstm_persistent.hip). Returns false
 // (nothing launched) when the shape or device cannot host it and raises when the launch
-// fails; `sync` (int32) word 0 is the sticky spin-timeout flag.
+// fails; `sync` (int32): csrc/persistent_sync.h (hand-off words) + the STAT block at its end.
 bool lstm_forward_persistent(const at::Tensor& XH, const at::Tensor& Wp, const at::Tensor& Cst,
                              const at::Tensor& S, const at::Tensor& sync, int64_t B, int64_t T, int64_t F,
                              int64_t KX, int64_t H) {

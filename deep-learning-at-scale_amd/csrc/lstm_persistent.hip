@@ -50,12 +50,11 @@ int launch_pf_variant(int KT, int NC, bf16_t* XH, const bf16_t* Wp, bf16_t* Cst,
 }
 }  // namespace
 
-// sync buffer (uint32 words): a per-launch block at the START, [0] error of the current launch
-// (all workgroups drain when it is set), [16 + 16*m] arrivals of row block m — zeroed by the
-// launcher before every launch (one memset from the allocation start, a multiple of 16 B:
-// cdna_hip_programming.md "Re-initialise every call") — and the 64-word completion STAT block
-// at the END (persistent_guard.h: sticky spin-timeout bit and running totals, never cleared
-// by a launch; NativeLSTM.check_device_errors reads it).
+// sync buffer (uint32 words): one 64-B line of monotonic hand-off words per row block after a
+// 16-word head (persistent_sync.h: launch epoch, group arrival counters, tagged error word;
+// zeroed once, never by a launch) and the 64-word completion STAT block at the END
+// (persistent_guard.h: sticky spin-timeout bit and running totals; NativeLSTM.check_device_errors
+// reads it).
 int lstm_persistent_sync_words(int row_blocks) { return 16 + 16 * row_blocks; }
 int dbg_mask() { return kDbgMask; }
 long lstm_persistent_sync_total(int row_blocks) { return lstm_persistent_sync_words(row_blocks) + kPStatWords; }
@@ -105,14 +104,9 @@ int launch_lstm_fwd_persistent(bf16_t* XH, const bf16_t* Wp, bf16_t* Cst, bf16_t
   if (sync_words < lstm_persistent_sync_total(MB)) return 0;
   unsigned* stat = sync + (sync_words - kPStatWords);  // running totals: never cleared here
   const int grid = MB * NB;
-  const size_t reset_bytes = sizeof(unsigned) * (size_t)lstm_persistent_sync_words(MB);
-  if (!persistent_memset_legacy(d) && !persistent_reset_ok(sync, reset_bytes)) return -(int)hipErrorInvalidValue;
+  // no per-launch reset: the hand-off words only count up (persistent_sync.h); the buffer is
+  // zeroed at allocation and by NativeLSTM.reset_device_errors
   for (int k = 0; k < nsub; ++k) {
-    // reset this launch's error word and arrival counters (the STAT block at the end is kept)
-    if (persistent_memset_legacy(d)
-            ? hipMemsetAsync(sync + 1, 0, sizeof(unsigned) * (size_t)(lstm_persistent_sync_words(MB) - 1), s) != hipSuccess
-            : hipMemsetAsync(sync, 0, reset_bytes, s) != hipSuccess)
-      return -(int)hipErrorLaunchFailure;
     LstmDims dk = d;
     dk.row_off = k * Bs;
     // KA / 32 = 6, 10, 18: H = 128, 256, 512

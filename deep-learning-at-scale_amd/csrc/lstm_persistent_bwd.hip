@@ -70,14 +70,9 @@ int launch_lstm_bwd_persistent(const bf16_t* WhhT, const bf16_t* Cst, const bf16
   if (sync_words < lstm_persistent_sync_total(MB)) return 0;
   unsigned* stat = sync + (sync_words - kPStatWords);  // running totals: never cleared here
   const int grid = MB * NB;
-  const size_t reset_bytes = sizeof(unsigned) * (size_t)lstm_persistent_sync_words(MB);
-  if (!persistent_memset_legacy(d) && !persistent_reset_ok(sync, reset_bytes)) return -(int)hipErrorInvalidValue;
+  // no per-launch reset: the hand-off words only count up (persistent_sync.h); the buffer is
+  // zeroed at allocation and by NativeLSTM.reset_device_errors
   for (int k = 0; k < nsub; ++k) {
-    // this launch's error word and arrival counters (the STAT block at the end is kept)
-    if (persistent_memset_legacy(d)
-            ? hipMemsetAsync(sync + 1, 0, sizeof(unsigned) * (size_t)(lstm_persistent_sync_words(MB) - 1), s) != hipSuccess
-            : hipMemsetAsync(sync, 0, reset_bytes, s) != hipSuccess)
-      return -(int)hipErrorLaunchFailure;
     LstmDims dk = d;
     dk.row_off = k * Bs;
     const int r = launch_pb_variant(d.H / 32, NRT, WhhT, Cst, S, DG, dcarry, sync, stat, grid, dk, s);

@@ -18,14 +18,29 @@
 //    into the next tile's loop), each wave then owning one 16-unit tile for the cell backward.
 //  * the dc carry of the workgroup's rows x units lives in VGPRs for the whole sequence (it
 //    never touches HBM); c_{t-1} and the saved gates S_t are read once (register ring,
-//    two row tiles ahead); the cell backward of tile r-1 runs in packed fp32 inside tile r's
-//    MFMA loop; DG_t is written once with 16-B write-through (sc1) stores (lane pairs
+//    two row tiles ahead); the cell backward of tile r-1 runs in fp32 micro-stages inside tile
+//    r's MFMA loop; DG_t is written once with 16-B write-through (sc1) stores (lane pairs
 //    exchange halves by DPP so each store is a whole 16-B (row, 2 units) run).
-//  * hand-off (cdna_hip_programming.md Guideline 16, recipe R1, as in the forward): every
-//    wave drains its stores (vmcnt(0)), workgroup barrier, ONE lane adds to the row
-//    block's arrival counter (agent scope); consumers poll relaxed with s_sleep, then ONE
-//    agent-scope acquire, then the LDS-DMA loads of DG_{t+1}. Only the H/64 workgroups of one
-//    row block depend on each other; every spin is bounded (error words 1 and sticky 0, all drain).
+//  * SPLIT-PHASE hand-off (round 5). Batch rows are independent, so row tile r of step t
+//    needs DG_{t+1} only of ITS rows — written by the row block's NB workgroups while they
+//    ran tile r of the previous step, most of a step earlier. The NRT row tiles form NG groups
+//    of GS tiles with one arrival counter each (persistent_sync.h): a workgroup publishes a
+//    group (its waves drained the group's DG stores, workgroup barrier, one lane's agent-scope
+//    add) a few tiles after the group's last tile, and every wave polls the counter of the
+//    group its NEXT first-of-group tile needs two tiles ahead (one sc1 load, no spin). If the
+//    poll matched, the wave streams that tile's A pieces in the previous tile's loop as for
+//    any other tile — across the step boundary too: tile 0 of step t-1 is fetched during
+//    tile NRT-1 of step t — else (a lagging peer) it waits at that tile (bounded spin) and
+//    fetches it then. The round-4 kernel instead stopped every step: drain, barrier, add,
+//    poll the whole row block, acquire, then fetch tile 0 (timeline: 4.2 us of a 28 us step).
+//  * visibility (cdna_hip_programming.md Guideline 16; MI355X_MICROARCH.md "Valid forms",
+//    table row 1): every DG byte is stored sc1 by its producer, every storing wave waits for
+//    its stores before the workgroup barrier behind which one lane adds to the counter, every
+//    consumer wave polls the counter with an sc1 load itself and only then issues its A
+//    loads, all with sc1 (the LDS-DMA form of the validated sc1 load-to-register: same
+//    buffer_load path, L1 bypassed), so no acquire (L1 invalidate) is needed.
+//  * every spin is bounded; a failing wave records why and runs on without waiting (results
+//    garbage, the STAT block says so), so nothing can hang.
 // Step T-1 (dh from the regression head) is lstm_bwd_last_kernel in lstm.hip.
 #pragma once
 // diagnostic builds: WELLFLOW_DIAG_BUILD=1 instantiates every timing variant, =N or =N,M,..
@@ -54,13 +69,13 @@ constexpr bool diag_variant(int v) {
 #include "lstm_layout.h"
 #include "persistent_guard.h"
 #include "persistent_launch.h"
+#include "persistent_sync.h"
 
 namespace wf {
 
 namespace {
 constexpr unsigned PB_SPIN_LIMIT = 1u << 21;
 constexpr int PB_MAX_RT = 16;  // row tiles per workgroup (dc carry in registers: 4 VGPRs each)
-typedef __attribute__((address_space(1))) unsigned gu32;
 // empty volatile asm redefining the value ("+v"): its producer stays above this point and its
 // consumers below it (lstm_persistent.hip uses the same pins)
 template <typename A> __device__ __forceinline__ void pin(A& a) { asm volatile("" : "+v"(a)); }
@@ -69,15 +84,19 @@ template <typename A, typename B> __device__ __forceinline__ void pin(A& a, B& b
 }
 }  // namespace
 
+// Row tiles per hand-off group. A group's DG stores are known complete three tiles after its
+// last tile (the stores of tile r issue in tile r+1's loop; a tile-top wait covers them two
+// tiles later), and its first tile is polled two tiles before it runs, so a group must leave
+// NRT - GS - 4 >= 0 tiles between its publish and its next poll: 8 of 16 (slack 4), 2 of 8
+// (slack 2). NRT = 4 runs as one group: the old per-step hand-off (every poll falls back).
+constexpr int pb_group_size(int nrt) { return nrt >= 16 ? 8 : (nrt >= 8 ? 2 : nrt); }
+
 // KT = H / 32 k-tiles per wave (each wave's K quarter of G = 4H is H wide); NRT row tiles
 // of 16 rows per workgroup (compile-time: the row-tile loop is fully unrolled so the dc
 // carry, the prefetch rings and every vmcnt below are static).
-// DBG (timing-only builds, results wrong; WELLFLOW_PF_DBG at H = 512, NRT = 16):
-// 1 no hand-off wait, 2 no MFMA, 4 no DG stores, 8 no S / c loads, 16 no A loads, 128 A
-// always from row tile 0 (same bytes, L2-hot), 256 default-policy (not nt) S / c loads;
-// 64 = plain (L2-resident) DG stores + agent release before the arrival add (correct results);
-// 32 = timeline: s_memrealtime stamps of step PB_STAMP_S, wave 0 lane 0 of every workgroup,
-// into sync + 4096 words (128 per workgroup; tools/pb_timeline.py).
+// DBG (WF_DIAG timing-only builds, results wrong): 2 no MFMA, 16 no A loads after tile 1,
+// 32 timeline (s_memrealtime stamps of step PB_STAMP_S, wave 0 lane 0 of every workgroup,
+// into sync + 4096 words, 128 per workgroup; tools/pb_timeline.py).
 template <int KT, int NRT, int DBG = 0>
 __global__ __launch_bounds__(256, 1) void lstm_bwd_persistent_kernel(
     const bf16_t* __restrict__ WhhT, const bf16_t* __restrict__ Cst, const bf16_t* __restrict__ S,
@@ -85,11 +104,16 @@ __global__ __launch_bounds__(256, 1) void lstm_bwd_persistent_kernel(
     unsigned* __restrict__ stat, LstmDims d) {
   constexpr int H = 32 * KT, G = 4 * H, NB = H / 64, HB = H / 16;
   constexpr int KS = KT / 2;             // 64-wide k-steps per wave per row tile
-  constexpr bool MICRO = (DBG & 512) == 0;  // cell backward as per-MFMA micro-stages (bstage)
+  constexpr int GS = pb_group_size(NRT), NG = NRT / GS;
+  static_assert(NG <= kPSyncMaxGroups && NRT % GS == 0, "hand-off groups");
+  static_assert(NG == 1 || (GS >= 2 && NRT - GS - 4 >= 0), "a group must publish before its next poll");
   constexpr int WSLOT = 16 * KT * 64;    // bytes of one wave's A tile: 16 rows x H k (bf16)
   constexpr int RING = 4 * 2 * WSLOT;    // [wave][2 slots]
   constexpr int RED = RING;              // partial sums [parity][src wave][unit tile][lane] x 16 B
-  constexpr int FLAG = RED + (1 * 16 + 0 * 4 + 0) * 1024;  // slot [1][0][0]: never written (own tile)
+  // slots [p][w][w] of RED are never written (a wave's own unit tile stays in registers):
+  // [0][0][0] holds the epoch / started ordinal broadcast, [0][1][1] the per-wave failed words
+  constexpr int BCAST = RED + (0 * 16 + 0 * 4 + 0) * 1024;
+  constexpr int FAILW = RED + (0 * 16 + 1 * 4 + 1) * 1024;
   // ONE static LDS object (see lstm_persistent.hip: with several, the waitcnt pass guards LDS
   // accesses behind the LDS-DMA with vmcnt(0)); LDS writes go through inline asm.
   __shared__ __attribute__((aligned(16))) char smem[RED + 2 * 16 * 1024];
@@ -104,14 +128,13 @@ __global__ __launch_bounds__(256, 1) void lstm_bwd_persistent_kernel(
   const int row0 = m * 16 * NRT + d.row_off;  // row_off: sub-batch origin (launcher)
   const int ue = n * 64 + wid * 16 + l15;  // unit of this lane's cell backward
   const bool even = (l15 & 1) == 0;
-  // this launch's error (word 1 in the round-2 layout A/B, PF_DBG bit 20); the sticky bit is
-  // in the STAT block (persistent_guard.h)
-  // production objects keep only the test hook bit (kDbgMask, persistent_guard.h): the
-  // timing-only branches below fold away at compile time
+  // production objects keep only the test hook bit (kDbgMask, persistent_guard.h)
   const int dbg = d.dbg & kDbgMask;
-  gu32* err = (gu32*)(sync + ((dbg >> 20) & 1));
-  gu32* cnt = (gu32*)(sync + 16 + 16 * m);
+  ps_u32* rbw = psync_rb(sync, m);
+  ps_u32* err = rbw + kPSyncErr;
   const unsigned spin_limit = d.spin_limit ? d.spin_limit : PB_SPIN_LIMIT;
+  // (dbg bit 21, tests: an unreachable target, so every poll fails and the bounded spin trips)
+  const unsigned force = ((dbg >> 21) & 1u) << 30;
   constexpr int PB_STAMP_S = 10;
   unsigned long long* stamps = reinterpret_cast<unsigned long long*>(sync + 4096) + blockIdx.x * 128;
   auto stamp = [&](int s, int slot) {
@@ -120,9 +143,13 @@ __global__ __launch_bounds__(256, 1) void lstm_bwd_persistent_kernel(
     }
   };
 
-  // completion guard (persistent_guard.h): started / expected counts before any exit path
-  unsigned ord = 0;
-  if (threadIdx.x == 0) ord = pguard_start(stat, (unsigned)(d.T - 1));
+  // completion guard (persistent_guard.h) and this launch's epoch (persistent_sync.h)
+  if (threadIdx.x == 0) {
+    const unsigned ord = pguard_start(stat, (unsigned)(d.T - 1));
+    const unsigned e = __hip_atomic_fetch_add(rbw + kPSyncStart, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) / NB;
+    asm volatile("ds_write_b64 %0, %1" ::"v"(lds0 + BCAST), "v"((unsigned long long)e | ((unsigned long long)ord << 32))
+                 : "memory");
+  }
   // ---- prologue: stationary W_hh^T fragments (B operand: lane = unit col l15, k 8g..8g+7)
   bf16x8 w[KT][4];
 #pragma unroll
@@ -139,6 +166,24 @@ __global__ __launch_bounds__(256, 1) void lstm_bwd_persistent_kernel(
   asm volatile("" ::: "memory");
   __builtin_amdgcn_s_waitcnt(0xF70);  // vmcnt(0)
   __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  unsigned long long eo;
+  asm volatile("ds_read_b64 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(eo) : "v"(lds0 + BCAST) : "memory");
+  const unsigned epoch = __builtin_amdgcn_readfirstlane((unsigned)eo);
+  const unsigned ord = __builtin_amdgcn_readfirstlane((unsigned)(eo >> 32));
+  const unsigned tag = epoch + 1u;
+  // publishes of group g per launch: every step for groups published inside their step, all
+  // but the last step for groups published at tile 1 of the next step (see pub_tile below)
+  auto pub_rt = [](int gg) { return (gg + 1) * GS + 2; };  // global tile index of group gg's publish
+  auto group_base = [&](int gg) -> unsigned {
+    const bool in_step = NG == 1 || pub_rt(gg) <= NRT - 1;
+    return epoch * (unsigned)NB * (unsigned)(in_step ? d.T - 1 : d.T - 2);
+  };
+  // arrivals group gg must show before step sg reads it: all NB workgroups published it for
+  // steps 0 .. sg-1
+  auto target = [&](int gg, int sg) { return group_base(gg) + (unsigned)(NB * sg) + force; };
+  unsigned failed = 0;  // uniform: this wave failed a hand-off (runs on, never waits again)
 
   // ---- per-lane constant offsets
   // A (DG_{t+1}) staging: one LDS-DMA instruction = 8 rows x 128 B (full lines) of the wave's
@@ -180,147 +225,95 @@ __global__ __launch_bounds__(256, 1) void lstm_bwd_persistent_kernel(
   };
   auto load_sc = [&](int t, auto rc, auto slot) {
     constexpr int RT = decltype(rc)::value, Q = decltype(slot)::value;
-    if constexpr ((DBG & 8) != 0) {
-      if (t < d.T - 2 || RT > 1) return;
-    }
     const __amdgpu_buffer_rsrc_t sr = __builtin_amdgcn_make_buffer_rsrc(
         const_cast<bf16_t*>(S) + (size_t)t * Bp * G, 0, 0x7FFFFFFF, 0x00020000);
     const __amdgpu_buffer_rsrc_t cr = __builtin_amdgcn_make_buffer_rsrc(
         const_cast<bf16_t*>(Cst) + (size_t)t * Bp * H, 0, 0x7FFFFFFF, 0x00020000);
     constexpr int SO = RT * HB * 1024 * 2, CO = RT * HB * 256 * 2;
-    // nt on the read-once streams (256: default policy; A/B within run-to-run noise)
-    constexpr int NTA = (DBG & 256) ? 0 : 2;
-    sq0[Q] = __builtin_amdgcn_raw_buffer_load_b128(sr, s_vo, SO, NTA);
-    sq1[Q] = __builtin_amdgcn_raw_buffer_load_b128(sr, s_vo + 2 * kFnSHalf, SO, NTA);  // second half
-    cq[Q] = __builtin_amdgcn_raw_buffer_load_b64(cr, c_vo, CO, NTA);
+    // nt on the read-once streams
+    sq0[Q] = __builtin_amdgcn_raw_buffer_load_b128(sr, s_vo, SO, 2);
+    sq1[Q] = __builtin_amdgcn_raw_buffer_load_b128(sr, s_vo + 2 * kFnSHalf, SO, 2);  // second half
+    cq[Q] = __builtin_amdgcn_raw_buffer_load_b64(cr, c_vo, CO, 2);
   };
+  // A tile TI of the step whose A resource is `ar` -> ring slot TI & 1; piece i = k-step i / 2,
+  // rows 8 * (i % 2) .. of the wave's K quarter, 1 KB, sc1 (the hand-off's consumer side)
+  auto issue_a = [&](const __amdgpu_buffer_rsrc_t& ar, auto tc, auto ic) {
+    constexpr int TI = decltype(tc)::value, i = decltype(ic)::value, ks = i / 2, hf = i % 2;
+    if constexpr ((DBG & 16) != 0) {
+      if (TI > 1) return;
+    }
+    const unsigned dst = a_lds + (TI & 1) * WSLOT + ks * 2048 + hf * 1024;
+    // (the instruction offset would also move the LDS address: the k-step goes into soffset)
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(ar, (lds_void*)(uintptr_t)dst, 16, hf ? a_vo1 : a_vo,
+                                             TI * 16 * G * 2 + ks * 128, 0, 16);
+  };
+  auto a_rsrc_of = [&](int tt) {  // A of the step with t = tt: DG_{tt+1}, this row block
+    return __builtin_amdgcn_make_buffer_rsrc(DG + ((size_t)(tt + 1) * d.B + row0) * G, 0, 0x7FFFFFFF, 0x00020000);
+  };
+  // sc1 poll of a group counter: one uniform load (every lane, one address). Inline asm, so it
+  // stays where it is written (the compiler sinks the S / c buffer loads to the end of the
+  // loop, behind the DG stores; a tracked poll there made its first use wait for those stores)
+  // and the tile-top wait that covers it names its register (poll_wait).
+  auto poll = [&](int gg) {
+    unsigned v;
+    const unsigned* pa = sync + kPSyncHead + kPSyncRowBlock * m + kPSyncGroup + gg;
+    asm volatile("global_load_dword %0, %1, off sc1" : "=v"(v) : "v"(pa) : "memory");
+    return v;
+  };
+  // blocking wait of this wave for group gg before step sg (slow path); a failure is recorded
+  // once and turns every later wait of the wave into a no-op
+  auto wait_group = [&](int gg, int sg) {
+    if (failed) return;
+    unsigned seen_cnt = 0, seen_err = 0;
+    const unsigned tg = target(gg, sg);
+    const unsigned why = psync_wait(rbw + kPSyncGroup + gg, err, tg, tag, spin_limit, stat, &seen_cnt, &seen_err);
+    if (why != 0) {
+      failed = 1;
+      if (lane == 0) pguard_exit(stat, (unsigned)sg, why, seen_err, seen_cnt, tg, (unsigned)gg, ord);
+    }
+  };
+  auto publish = [&](int gg) {  // behind a workgroup barrier every wave reached after its stores drained
+    if (threadIdx.x == 0) __hip_atomic_fetch_add(rbw + kPSyncGroup + gg, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  };
+
+  constexpr int NSC = 3;  // S / c loads per tile
+  constexpr int NST = 2;  // DG stores per tile
   load_sc(d.T - 2, std::integral_constant<int, 0>{}, std::integral_constant<int, 0>{});
   load_sc(d.T - 2, std::integral_constant<int, 1>{}, std::integral_constant<int, 1>{});
+  {  // A(0) of the first step: DG_{T-1} was written by the previous kernel (lstm_bwd_last_kernel)
+    const __amdgpu_buffer_rsrc_t ar = a_rsrc_of(d.T - 2);
+    static_for<0, 2 * KS>([&](auto ic) { issue_a(ar, std::integral_constant<int, 0>{}, ic); });
+  }
+  // fast[gg]: this wave already streamed the first tile of group gg (its poll matched two tiles
+  // ahead); at step 0 every group is ready (DG_{T-1} comes from the previous kernel)
+  unsigned fast[NG];
+#pragma unroll
+  for (int gg = 0; gg < NG; ++gg) fast[gg] = 1;
+  unsigned pv = 0;  // the outstanding poll's value (uniform)
+
+  // dh partial of the previous tile, own unit tile (the other three go through LDS)
+  f32x4 dho = f32x4{0.f, 0.f, 0.f, 0.f};
+  const unsigned rd_base = lds0 + RED + wid * 1024 + lane * 16;  // red[.][.][wid][lane]
 
   for (int s = 0; s < d.T - 1; ++s) {
     const int t = d.T - 2 - s;
+    const bool last_step = s == d.T - 2;
     stamp(s, 0);
-    if (s > 0) {
-      // ---- publish step s-1 (every wave drained its DG stores) and wait for the row block
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();
-      asm volatile("" ::: "memory");
-      // thread 0's view of the wait, kept for the exit record (persistent_guard.h)
-      unsigned why = 0, seen_err = 0, seen_cnt = 0;
-      // (dbg bit 21, tests: an unreachable target, so the bounded spin trips deterministically)
-      const unsigned target = (unsigned)(NB * s) + (((dbg >> 21) & 1u) << 30);
-      if (threadIdx.x == 0) {
-        if constexpr ((DBG & 64) != 0) {  // plain DG stores: publish them with an agent release
-          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        }
-        __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        unsigned spins = 0;
-        while (!(DBG & 1) && (seen_cnt = __hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) < target) {
-          if ((seen_err = __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) != 0u) {
-            why = 1;
-            break;
-          }
-          if (++spins > spin_limit) {
-            __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            pguard_sticky(stat);
-            why = 2;
-            break;
-          }
-          __builtin_amdgcn_s_sleep(2);
-        }
-        // (dbg bit 22, WF_DIAG builds only, WELLFLOW_PF_DBG=4194304: TIMING ONLY, unsafe — no acquire, to price it)
-        if (!((dbg >> 22) & 1)) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        const int ok = why == 0 ? 1 : 0;
-        asm volatile("ds_write_b32 %0, %1" ::"v"(lds0 + FLAG), "v"(ok) : "memory");
-      }
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();
-      int okv;
-      asm volatile("ds_read_b32 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(okv) : "v"(lds0 + FLAG) : "memory");
-      if (__builtin_amdgcn_readfirstlane(okv) != 1) {  // uniform
-        if (lane == 0)
-          pguard_exit(stat, (unsigned)s, wid != 0 ? 4u : (why != 0 ? why : 3u), seen_err, seen_cnt, target,
-                      (unsigned)okv, ord);
-        return;
-      }
-    }
-
-    stamp(s, 1);
-    const __amdgpu_buffer_rsrc_t a_rsrc =
-        __builtin_amdgcn_make_buffer_rsrc(DG + ((size_t)(t + 1) * d.B + row0) * G, 0, 0x7FFFFFFF, 0x00020000);
+    const __amdgpu_buffer_rsrc_t a_rsrc = a_rsrc_of(t);
+    const __amdgpu_buffer_rsrc_t an_rsrc = a_rsrc_of(t > 0 ? t - 1 : t);  // next step's A (DG_t)
     const __amdgpu_buffer_rsrc_t dg_rsrc =
         __builtin_amdgcn_make_buffer_rsrc(DG + (size_t)t * d.B * G, 0, 0x7FFFFFFF, 0x00020000);
     const int st_base = row0 * G * 2 + st_lane;
-    // A tile rt of this wave -> ring slot rt & 1: KS k-steps x 2 row halves, 1 KB each
-    // piece i (k-step i / 2, rows 8 * (i % 2) ..) of A tile RT of this wave -> ring slot RT & 1
-    auto issue_a = [&](auto rc, auto ic) {
-      constexpr int RT = decltype(rc)::value, i = decltype(ic)::value, ks = i / 2, hf = i % 2;
-      if constexpr ((DBG & 16) != 0) {
-        if (RT > 1) return;
-      }
-      const unsigned dst = a_lds + (RT & 1) * WSLOT + ks * 2048 + hf * 1024;
-      // (the instruction offset would also move the LDS address: the k-step goes into soffset)
-      constexpr int RTS = (DBG & 128) ? 0 : RT;  // timing build 128: always row tile 0 (L2-hot lines)
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(a_rsrc, (lds_void*)(uintptr_t)dst, 16, hf ? a_vo1 : a_vo,
-                                               RTS * 16 * G * 2 + ks * 128, 0, 0);
-    };
-    constexpr int NA = ((DBG & 16) != 0) ? 0 : 2 * KS;  // DMA instructions per A tile (= KT)
-    constexpr int NSC = ((DBG & 8) != 0) ? 0 : 3;       // S / c loads per tile
-    constexpr int NST = ((DBG & 4) != 0) ? 0 : 2;       // DG stores per tile
-    static_assert(2 * KS == KT, "two A pieces per k-tile over the first half of the loop");
-    (void)NA;
-    static_for<0, 2 * KS>([&](auto ic) { issue_a(std::integral_constant<int, 0>{}, ic); });
 
-    // Cell backward of row tile RTp (its dh in dhp, its saved gates / c_{t-1} in ring slot
-    // RTp % 3, its carry in dcr[RTp]) in parts 1..EPI_PARTS, two rows at a time in packed fp32
-    // (v_pk_fma / v_pk_mul: half the VALU issue of the scalar form), so that tile RTp + 1's
-    // MFMA loop can issue one part per k-tile in the MFMAs' shadow (software pipeline).
-    //   per row pair q: part 3q+1 gates, x = f c + i g, e = exp(2x); part 3q+2 tanh, dc, carry;
-    //   part 3q+3 the four gate gradients, packed to bf16; part 7 lane-pair exchange; 8 stores.
-    constexpr int EPI_PARTS = 8;
+    // Cell backward parts 7 (lane-pair exchange) and 8 (the two DG stores) of row tile RTp.
     typedef float f32x2 __attribute__((ext_vector_type(2)));
     f32x4 dhp = f32x4{0.f, 0.f, 0.f, 0.f};
     unsigned ev[4][2];
     f32x4 enk;
-    f32x2 eig[2], efg[2], egg[2], eog[2], ecp[2], eex[2], etc[2], edc[2], eq[2];
     u32x4 elo, ehi;
     auto epi = [&](auto rpc, auto partc) {
-      constexpr int RTp = decltype(rpc)::value, part = decltype(partc)::value, Kp = RTp % 4;
-      constexpr int q = (part - 1) / 3, sub = (part - 1) % 3;
-      if constexpr (part <= 6 && sub == 0) {
-        const u32x4 sv = q == 0 ? sq0[Kp] : sq1[Kp];  // rows 2q, 2q+1: (i|f), (g|o) per row
-        eig[q] = f32x2{__uint_as_float(sv[0] << 16), __uint_as_float(sv[2] << 16)};
-        efg[q] = f32x2{__uint_as_float(sv[0] & 0xffff0000u), __uint_as_float(sv[2] & 0xffff0000u)};
-        egg[q] = f32x2{__uint_as_float(sv[1] << 16), __uint_as_float(sv[3] << 16)};
-        eog[q] = f32x2{__uint_as_float(sv[1] & 0xffff0000u), __uint_as_float(sv[3] & 0xffff0000u)};
-        ecp[q] = f32x2{cval(Kp, 2 * q), cval(Kp, 2 * q + 1)};
-        const f32x2 x2 = (efg[q] * ecp[q] + eig[q] * egg[q]) * 2.f;
-        eex[q] = f32x2{__expf(x2[0]), __expf(x2[1])};
-      } else if constexpr (part <= 6 && sub == 1) {
-        etc[q] = 1.f - 2.f * f32x2{__builtin_amdgcn_rcpf(eex[q][0] + 1.f), __builtin_amdgcn_rcpf(eex[q][1] + 1.f)};
-        const f32x2 dh = f32x2{dhp[2 * q], dhp[2 * q + 1]};
-        const f32x2 kv = f32x2{dcr[RTp][2 * q], dcr[RTp][2 * q + 1]};
-        eq[q] = dh * eog[q];
-        edc[q] = eq[q] * (1.f - etc[q] * etc[q]) + kv;
-        const f32x2 nk = edc[q] * efg[q];
-        enk[2 * q] = nk[0];
-        enk[2 * q + 1] = nk[1];
-      } else if constexpr (part <= 6 && sub == 2) {
-        const f32x2 a = edc[q] * eig[q], tq = a * egg[q];
-        const f32x2 di = tq - tq * eig[q];          // dc g i (1 - i)
-        const f32x2 dg = a - tq * egg[q];           // dc i (1 - g^2)
-        const f32x2 u = edc[q] * efg[q] * ecp[q];
-        const f32x2 df = u - u * efg[q];            // dc c_{t-1} f (1 - f)
-        const f32x2 e = eq[q] * etc[q];
-        const f32x2 dO = e - e * eog[q];            // dh tanh(c) o (1 - o)
-#pragma unroll
-        for (int k = 0; k < 2; ++k) {
-          ev[2 * q + k][0] = pk_bf16(di[k], df[k]);  // one v_cvt_pk_bf16_f32 per pair
-          ev[2 * q + k][1] = pk_bf16(dg[k], dO[k]);
-        }
-      } else if constexpr (part == 7) {
+      constexpr int RTp = decltype(rpc)::value, part = decltype(partc)::value;
+      if constexpr (part == 7) {
         dcr[RTp] = enk;
         // lane pair (2i, 2i+1) = units (u, u+1): the even lane stores rows 0, 2 and the odd
         // lane rows 1, 3 of both units, each a 16-B run [4 gates of u | 4 gates of u+1]
@@ -339,13 +332,9 @@ __global__ __launch_bounds__(256, 1) void lstm_bwd_persistent_kernel(
         }
       } else if constexpr (part == 8) {
         constexpr int SOFF = RTp * 16 * G * 2;
-        if constexpr ((DBG & 4) != 0) {
-          if (elo[0] == 0x7fc07fc1u && ehi[1] == 0x7fc07fc1u) dcr[RTp][0] = 1.f;  // keep the values live
-        } else {
-          constexpr int AUX = (DBG & 64) ? 0 : 16;  // sc1 (write-through) unless released
-          __builtin_amdgcn_raw_buffer_store_b128(elo, dg_rsrc, st_base, SOFF, AUX);
-          __builtin_amdgcn_raw_buffer_store_b128(ehi, dg_rsrc, st_base, SOFF + 2 * G * 2, AUX);
-        }
+        // sc1 (write-through): the hand-off's producer side
+        __builtin_amdgcn_raw_buffer_store_b128(elo, dg_rsrc, st_base, SOFF, 16);
+        __builtin_amdgcn_raw_buffer_store_b128(ehi, dg_rsrc, st_base, SOFF + 2 * G * 2, 16);
       }
     };
 
@@ -356,7 +345,6 @@ __global__ __launch_bounds__(256, 1) void lstm_bwd_persistent_kernel(
     // 2p + (q & 1); q = 60: lane-pair exchange (part 7); q = 62: DG stores (part 8). Every
     // stage pins its values with empty "+v" asm, so the compiler can neither sink the math
     // below the MFMAs nor hoist it above them (it had gathered each part into one clump).
-    // WELLFLOW_PF_DBG=512: the 8-part schedule instead (A/B).
     struct BRow {
       unsigned sa, sb;
       float i, f, g, o, x, tc, eq, dc, nk, a, tq, u, di, dg, df, e;
@@ -441,21 +429,58 @@ __global__ __launch_bounds__(256, 1) void lstm_bwd_persistent_kernel(
     // red[r & 1] at its end and runs on; tile r+1's loop passes a barrier after its first
     // k-tile (the writes drained by that k-tile's lgkmcnt wait), issues the partial reads, and
     // sums them at k-tile 1 (so their LDS latency hides under MFMAs). The last tile of a step
-    // exchanges at once (its cell backward drains before the hand-off).
-    f32x4 dho = f32x4{0.f, 0.f, 0.f, 0.f};  // own partial of the previous tile (its unit tile)
-    const unsigned rd_base = lds0 + RED + wid * 1024 + lane * 16;  // red[.][.][wid][lane]
-    auto kt_of_part = [](int p) { return 2 * p - 1 + (p == 1 ? 1 : 0); };  // parts at k-tiles 2,3,5,..,15
-
+    // exchanges at once and runs its cell backward there (the next step's tile 0 needs the
+    // carry, and the step's last group is published from it).
     static_for<0, NRT>([&](auto rc) {
       constexpr int RT = decltype(rc)::value, P = RT & 1;
+      constexpr bool GFIRST = RT % GS == 0;
+      constexpr int GRT = RT / GS;
+      // ---- first tile of a group whose poll did not match two tiles ago: wait, then fetch
+      if constexpr (GFIRST && NG > 1) {
+        if (!fast[GRT]) {
+          stamp(s, 1);
+          wait_group(GRT, s);
+          static_for<0, 2 * KS>([&](auto ic) { issue_a(a_rsrc, rc, ic); });
+          wait_vmcnt<0>();
+        }
+      } else if constexpr (NG == 1 && RT == 0) {
+        if (s > 0) {  // one group: the old per-step hand-off (published at the previous step's end)
+          wait_group(0, s);
+          static_for<0, 2 * KS>([&](auto ic) { issue_a(a_rsrc, rc, ic); });
+          wait_vmcnt<0>();
+        }
+      }
       // ---- wait for A(RT): its pieces were issued in the first half of tile RT-1's MFMA loop;
       // after the last one came tile RT-1's S / c loads (of tile RT+1 or of the next step) and
-      // tile RT-2's DG stores (epilogue part 8, if RT-1 > 0), which may stay in flight
-      if constexpr (RT == 0)
-        wait_vmcnt<0>();
-      else
-        wait_vmcnt<NSC + (RT >= 2 ? NST : 0)>();
+      // tile RT-2's DG stores (epilogue part 8, if RT-1 > 0), which may stay in flight; at tile
+      // 0 the previous step's last two tiles' stores too
+      if constexpr (RT == 0) {
+        if (s == 0)
+          wait_vmcnt<0>();
+        else
+          wait_vmcnt<NSC + 2 * NST>();
+      } else if constexpr (RT == 1) {
+        wait_vmcnt<NSC>();
+      } else if constexpr (NG > 1 && (RT + 1 == NRT || (RT + 1) % GS == 0)) {
+        // the poll issued in the previous loop is older than its S / c loads and DG stores:
+        // this wait covers it (the operand keeps its consumers below the wait)
+        asm volatile("s_waitcnt vmcnt(%1)" : "+v"(pv) : "n"(NSC + NST) : "memory");
+      } else {
+        wait_vmcnt<NSC + NST>();
+      }
       stamp(s, 2 + 5 * RT);
+      // ---- the poll issued in the previous tile's loop decides whether this tile's loop
+      // streams the next group's first tile (RT + 1 = first of a group at this step, or tile 0
+      // of the next step)
+      constexpr bool NEXT_GFIRST = NG > 1 && (RT + 1 == NRT || (RT + 1) % GS == 0);
+      constexpr int NGRP = (RT + 1 == NRT) ? 0 : (RT + 1) / GS;
+      if constexpr (NEXT_GFIRST) {
+        if (RT + 1 == NRT) {
+          fast[NGRP] = last_step ? 0u : (failed | (psync_reached(__builtin_amdgcn_readfirstlane(pv), target(NGRP, s + 1)) ? 1u : 0u));
+        } else {
+          fast[NGRP] = s == 0 ? 1u : (failed | (psync_reached(__builtin_amdgcn_readfirstlane(pv), target(NGRP, s)) ? 1u : 0u));
+        }
+      }
       const unsigned cur = a_lds + P * WSLOT;
 
       f32x4 acc[4];  // written first by k-tile 0's MFMAs (src C = 0)
@@ -467,25 +492,22 @@ __global__ __launch_bounds__(256, 1) void lstm_bwd_persistent_kernel(
       // (RT > 0); k-tile KSUM waits for those partials too (they are summed there).
       bf16x8 a[3];
       asm volatile("ds_read_b128 %0, %1" : "=v"(a[0]) : "v"(cur + fa[0]) : "memory");
-      if constexpr (KT > 1 && (DBG & 4096) == 0)
+      if constexpr (KT > 1)
         asm volatile("ds_read_b128 %0, %1" : "=v"(a[1]) : "v"(cur + fa[1]) : "memory");
       static_for<0, KT>([&](auto kc) {
         constexpr int kt = decltype(kc)::value;
         (void)acc;  // odr-use outside the asm operands: clang does not capture them implicitly
         (void)w;
         (void)pr;
-        // A/B (WELLFLOW_PF_DBG=4096, production-correct): the round-2 one-ahead prefetch
-        constexpr int AHEAD = (DBG & 4096) ? 1 : 2;
-        if constexpr (kt + AHEAD < KT)
+        if constexpr (kt + 2 < KT)
           asm volatile("ds_read_b128 %0, %1 offset:%2"
-                       : "=v"(a[(kt + AHEAD) % 3])
-                       : "v"(cur + fa[(kt + AHEAD) & 1]), "i"(((kt + AHEAD) >> 1) * 2048)
+                       : "=v"(a[(kt + 2) % 3])
+                       : "v"(cur + fa[(kt + 2) & 1]), "i"(((kt + 2) >> 1) * 2048)
                        : "memory");
         // k-tile whose top sums the partials: 2, or 1 where the cell backward's first use of dh
         // (micro-stage 7) already falls into k-tile 1 (KT = 4, H = 128)
-        constexpr int KSUM = (KT >= 8 && AHEAD == 2) ? 2 : 1;
-        constexpr int YOUNGER = (kt + 1 < KT ? 1 : 0) + (AHEAD == 2 && kt + 2 < KT ? 1 : 0) +
-                                (RT > 0 && kt == 1 && KSUM == 2 ? 3 : 0);
+        constexpr int KSUM = KT >= 8 ? 2 : 1;
+        constexpr int YOUNGER = (kt + 1 < KT ? 1 : 0) + (kt + 2 < KT ? 1 : 0) + (RT > 0 && kt == 1 && KSUM == 2 ? 3 : 0);
         asm volatile("s_waitcnt lgkmcnt(%0)" ::"n"(YOUNGER) : "memory");
         if constexpr (RT > 0 && kt == KSUM) {
           // the wait above drained the partial reads issued at k-tile 0 (LDS returns in order:
@@ -501,7 +523,7 @@ __global__ __launch_bounds__(256, 1) void lstm_bwd_persistent_kernel(
             else
               asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+v"(acc[j]) : "v"(a[kt % 3]), "a"(w[kt][j]));
           }
-          if constexpr (MICRO && RT > 0) {
+          if constexpr (RT > 0) {
             // stage instances [qlo, qhi) after MFMA slot m, from k-tile 1 on (dh of the
             // previous tile is summed at the top of k-tile 1)
             constexpr int S = 4 * KT - 4, m = kt * 4 + j - 4;
@@ -513,13 +535,32 @@ __global__ __launch_bounds__(256, 1) void lstm_bwd_persistent_kernel(
         });
         // two A pieces of the next tile per k-tile over the first half of the loop: the vector-
         // memory queue drains under the MFMAs instead of blocking the wave before them, and the
-        // last piece lands well before the next tile needs it
-        if constexpr (RT + 1 < NRT && 2 * kt < KT) {
-          issue_a(std::integral_constant<int, RT + 1>{}, std::integral_constant<int, 2 * kt>{});
-          issue_a(std::integral_constant<int, RT + 1>{}, std::integral_constant<int, 2 * kt + 1>{});
+        // last piece lands well before the next tile needs it. The next tile is tile 0 of the
+        // next step at RT = NRT - 1, and a group's first tile only when its poll matched.
+        if constexpr (2 * kt < KT) {
+          if constexpr (RT + 1 == NRT) {
+            if constexpr (NG > 1) {
+              if (fast[0] && !last_step) {
+                issue_a(an_rsrc, std::integral_constant<int, 0>{}, std::integral_constant<int, 2 * kt>{});
+                issue_a(an_rsrc, std::integral_constant<int, 0>{}, std::integral_constant<int, 2 * kt + 1>{});
+              }
+            }
+          } else if constexpr ((RT + 1) % GS == 0) {
+            if (fast[(RT + 1) / GS]) {
+              issue_a(a_rsrc, std::integral_constant<int, RT + 1>{}, std::integral_constant<int, 2 * kt>{});
+              issue_a(a_rsrc, std::integral_constant<int, RT + 1>{}, std::integral_constant<int, 2 * kt + 1>{});
+            }
+          } else {
+            issue_a(a_rsrc, std::integral_constant<int, RT + 1>{}, std::integral_constant<int, 2 * kt>{});
+            issue_a(a_rsrc, std::integral_constant<int, RT + 1>{}, std::integral_constant<int, 2 * kt + 1>{});
+          }
         }
         if constexpr (kt == KT / 2 - 1) {  // S / c of tile RT + 2 right after the last A piece
           __builtin_amdgcn_sched_barrier(0);
+          // the poll for the first tile of the group two tiles ahead (after the A pieces: an
+          // L2 round trip; before the S / c loads: HBM latency would hold it in the queue)
+          constexpr bool POLL = NG > 1 && (RT + 2 == NRT || (RT + 2 < NRT && (RT + 2) % GS == 0));
+          if constexpr (POLL) pv = poll(RT + 2 == NRT ? 0 : (RT + 2) / GS);
           if constexpr (RT + 2 < NRT)
             load_sc(t, std::integral_constant<int, RT + 2>{}, std::integral_constant<int, (RT + 2) % 4>{});
           else  // tiles 0 / 1 of the next step (t - 1; past step 0: a harmless reload, same count)
@@ -528,8 +569,22 @@ __global__ __launch_bounds__(256, 1) void lstm_bwd_persistent_kernel(
           __builtin_amdgcn_sched_barrier(0);
         }
         if constexpr (RT > 0 && kt == 0) {
-          // every wave's partial writes of tile RT-1 were drained by its lgkmcnt wait above
+          // every wave's partial writes of tile RT-1 were drained by its lgkmcnt wait above, and
+          // every wave's DG stores older than its tile-top wait have completed
           __builtin_amdgcn_s_barrier();
+          // publish a group whose last DG stores every wave has now drained: in-step groups at
+          // tile (last + 3); groups whose publish tile falls past the step end (the step's last
+          // group among them) at tile 1 of the next step
+          static_for<0, NG>([&](auto gc) {
+            constexpr int gg = decltype(gc)::value;
+            if constexpr (NG > 1) {
+              constexpr int pr_t = (gg + 1) * GS + 2;
+              if constexpr (pr_t <= NRT - 1 && RT == pr_t) publish(gg);
+              if constexpr (pr_t > NRT - 1 && RT == 1) {
+                if (s > 0) publish(gg);
+              }
+            }
+          });
           static_for<0, 4>([&](auto wc) {
             constexpr int w2 = decltype(wc)::value;
             (void)pr;
@@ -541,22 +596,10 @@ __global__ __launch_bounds__(256, 1) void lstm_bwd_persistent_kernel(
               pr[w2] = f32x4{0.f, 0.f, 0.f, 0.f};
           });
         }
-        // parts of the previous tile's cell backward (part p at k-tile kt_of_part(p))
-        static_for<1, EPI_PARTS + 1>([&](auto pc) {
-          constexpr int p = decltype(pc)::value;
-          if constexpr (!MICRO && RT > 0 && 2 * p - 1 + (p == 1 ? 1 : 0) == kt)
-            epi(std::integral_constant<int, RT - 1>{}, pc);
-        });
         // the MFMAs above are inline asm, so the compiler knows neither their latency nor that
         // they still read this fragment: keep its registers allocated until here, so no VALU
         // result of the interleaved epilogue can land in them while the MFMAs are in flight
         asm volatile("" ::"v"(a[kt % 3]));
-      });
-      (void)kt_of_part;
-      // parts that did not fit a short loop
-      static_for<1, EPI_PARTS + 1>([&](auto pc) {
-        constexpr int p = decltype(pc)::value;
-        if constexpr (!MICRO && RT > 0 && 2 * p - 1 + (p == 1 ? 1 : 0) >= KT) epi(std::integral_constant<int, RT - 1>{}, pc);
       });
       // VALU / LDS reads of MFMA results: cover the pipeline (nothing is padded after asm)
       asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 3" ::: "memory");
@@ -590,39 +633,40 @@ __global__ __launch_bounds__(256, 1) void lstm_bwd_persistent_kernel(
         asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(acc[0]), "+v"(acc[1]), "+v"(acc[2]), "+v"(acc[3]) :: "memory");
         dhp = (acc[0] + acc[1]) + (acc[2] + acc[3]);
         stamp(s, 5 + 5 * RT);
-        if constexpr (MICRO)
-          static_for<0, 64>([&](auto qc) { bstage(std::integral_constant<int, RT>{}, qc); });
-        else
-          static_for<1, EPI_PARTS + 1>([&](auto pc) { epi(std::integral_constant<int, RT>{}, pc); });
+        static_for<0, 64>([&](auto qc) { bstage(std::integral_constant<int, RT>{}, qc); });
+        if constexpr (NG == 1) {  // one group: publish the whole step now (drain, barrier, add)
+          wait_vmcnt<0>();
+          __builtin_amdgcn_s_barrier();
+          publish(0);
+        }
       }
       stamp(s, 6 + 5 * RT);
       __builtin_amdgcn_sched_barrier(0);
     });
   }
-  // completion count (DONE vs EXPECT, persistent_guard.h)
-  if (threadIdx.x == 0) pguard_done(stat, (unsigned)(d.T - 1));
+  // completion count (DONE vs EXPECT, persistent_guard.h): only if no wave failed a hand-off
+  wait_vmcnt<0>();
+  asm volatile("ds_write_b32 %0, %1" ::"v"(lds0 + FAILW + wid * 4), "v"(failed) : "memory");
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  if (threadIdx.x == 0) {
+    u32x4 fw;
+    asm volatile("ds_read_b128 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(fw) : "v"(lds0 + FAILW) : "memory");
+    if ((fw[0] | fw[1] | fw[2] | fw[3]) == 0u) pguard_done(stat, (unsigned)(d.T - 1));
+  }
 }
 
 template <int KT, int NRT>
 static int launch_pb(const bf16_t* WhhT, const bf16_t* Cst, const bf16_t* S, bf16_t* DG, const float* dcarry,
                       unsigned* sync, unsigned* stat, int grid, LstmDims d, hipStream_t s) {
   const void* f = reinterpret_cast<const void*>(&lstm_bwd_persistent_kernel<KT, NRT>);
-#ifdef WF_DIAG  // A/B and timing-only variants: diagnostic builds only (WELLFLOW_DIAG_BUILD=1)
+#ifdef WF_DIAG  // timing-only variants: diagnostic builds only (WELLFLOW_DIAG_BUILD=1)
   const void* const prod = f;
   if constexpr (KT == 16 && NRT == 16) {
     switch (d.dbg & 0xFFFFF) {
-      case 4096: if constexpr (WF_DV(4096)) f = reinterpret_cast<const void*>(&lstm_bwd_persistent_kernel<KT, NRT, 4096>); break;  // 1-ahead DG ring
-      case 1: if constexpr (WF_DV(1)) f = reinterpret_cast<const void*>(&lstm_bwd_persistent_kernel<KT, NRT, 1>); break;
       case 2: if constexpr (WF_DV(2)) f = reinterpret_cast<const void*>(&lstm_bwd_persistent_kernel<KT, NRT, 2>); break;
-      case 4: if constexpr (WF_DV(4)) f = reinterpret_cast<const void*>(&lstm_bwd_persistent_kernel<KT, NRT, 4>); break;
-      case 8: if constexpr (WF_DV(8)) f = reinterpret_cast<const void*>(&lstm_bwd_persistent_kernel<KT, NRT, 8>); break;
       case 16: if constexpr (WF_DV(16)) f = reinterpret_cast<const void*>(&lstm_bwd_persistent_kernel<KT, NRT, 16>); break;
       case 32: if constexpr (WF_DV(32)) f = reinterpret_cast<const void*>(&lstm_bwd_persistent_kernel<KT, NRT, 32>); break;
-      case 64: if constexpr (WF_DV(64)) f = reinterpret_cast<const void*>(&lstm_bwd_persistent_kernel<KT, NRT, 64>); break;
-      case 96: if constexpr (WF_DV(96)) f = reinterpret_cast<const void*>(&lstm_bwd_persistent_kernel<KT, NRT, 96>); break;
-      case 128: if constexpr (WF_DV(128)) f = reinterpret_cast<const void*>(&lstm_bwd_persistent_kernel<KT, NRT, 128>); break;
-      case 256: if constexpr (WF_DV(256)) f = reinterpret_cast<const void*>(&lstm_bwd_persistent_kernel<KT, NRT, 256>); break;
-      case 512: if constexpr (WF_DV(512)) f = reinterpret_cast<const void*>(&lstm_bwd_persistent_kernel<KT, NRT, 512>); break;  // 8-part epilogue
       default: break;
     }
   }

@@ -17,13 +17,16 @@
 //  * the fused cell epilogue is the per-step kernel's (same FN layouts for C / S, so the
 //    backward pass is unchanged); h_t is staged through LDS and published with 8-B
 //    write-through (sc1) stores.
-//  * hand-off (cdna_hip_programming.md Guideline 16, recipe R1): every wave drains its
-//    stores (vmcnt(0)), workgroup barrier, ONE lane adds to the row block's arrival counter
-//    (agent-scope atomic); the consumer polls that counter relaxed with s_sleep, then ONE
-//    agent-scope acquire, then plain / LDS-DMA loads. Only the NB workgroups of one row
-//    block depend on each other, so row blocks drift freely (no grid barrier), and the
+//  * hand-off (cdna_hip_programming.md Guideline 16; MI355X_MICROARCH.md "Valid forms" row 1):
+//    h is stored sc1, every storing wave drains its stores before a workgroup barrier behind
+//    which ONE lane adds to an arrival counter (agent-scope atomic), consumers poll it with sc1
+//    loads and then load the chunk with sc1 LDS-DMA — no acquire. Counters only count up
+//    (persistent_sync.h: launch epochs, no per-launch memset). At NC = 8 the hand-off is
+//    SPLIT-PHASE per chunk (see SPLIT below): no step-top stop. Only the NB workgroups of one
+//    row block depend on each other, so row blocks drift freely (no grid barrier), and the
 //    XCD-aware block map puts a row block's NB workgroups on one XCD (speed only).
-//  * every spin is bounded: on timeout the error word is set and all workgroups drain.
+//  * every spin is bounded: a wave that times out records why and runs on without waiting
+//    (results garbage, reported through the STAT block), so nothing can hang.
 #pragma once
 // diagnostic builds: WELLFLOW_DIAG_BUILD=1 instantiates every timing variant, =N or =N,M,..
 // only those WELLFLOW_PF_DBG values (fewer instantiations, minutes less to build)
@@ -51,6 +54,7 @@ constexpr bool diag_variant(int v) {
 #include "lstm_layout.h"
 #include "persistent_guard.h"
 #include "persistent_launch.h"
+#include "persistent_sync.h"
 
 namespace wf {
 
@@ -98,6 +102,16 @@ __global__ __launch_bounds__(256, 1) void lstm_fwd_persistent_kernel(
   // (every workgroup of the grid fetches its first chunks at once there); chunk 0 issues
   // chunks 1 and 2 from its MFMA loop (WELLFLOW_PF_DBG=1024: both at the step top, A/B)
   constexpr bool PF01 = NC >= 3 && (DBG & (2 | 1024)) == 0;
+  // SPLIT-PHASE hand-off (round 5, NC = 8: the rows of ONE chunk depend only on the same
+  // chunk of the previous step, whose h every workgroup of the row block publishes two chunks
+  // after finishing it): one arrival counter per chunk, the chunk pieces two chunks ahead
+  // across the step boundary (chunks 0 / 1 of step t+1 during chunks NC-2 / NC-1 of step t),
+  // the last chunk's cell epilogue in the next step's first MFMA loop like any other, and a
+  // per-wave sc1 poll two chunks before each fetch — no step-top stop. A 4-slot ring (slot =
+  // chunk % 4 in every step). Smaller NC keep the per-step hand-off: a chunk's own next-step
+  // input would be published too late to fetch ahead (NC < 8), or at all (NC = 1).
+  constexpr bool SPLIT = NC == 8 && 4 * ABYTES + PF_ROWS * 64 * 2 + 32 <= 163840;  // KX = 128: 3 slots only
+  constexpr int NSLOT = SPLIT ? 4 : 3;
   // Distinct static LDS objects per ring slot: the compiler then proves the slot being
   // filled by LDS-DMA disjoint from the slots being read, and inserts no vmcnt(0) of its own.
   // EXACTLY ONE static LDS variable, compile-time offsets for every ring slot, the h staging
@@ -106,8 +120,9 @@ __global__ __launch_bounds__(256, 1) void lstm_fwd_persistent_kernel(
   // the LDS-DMA into the ring and guards the first read of every slot with vmcnt(0) — which
   // drained the whole prefetch ring every chunk (measured: loads no longer overlapped MFMA).
   constexpr int SLOT = ABYTES;
-  constexpr int HOFF = 3 * SLOT, FOFF = HOFF + PF_ROWS * 64 * 2;
-  __shared__ __attribute__((aligned(16))) char smem[FOFF + 16];
+  constexpr int HOFF = NSLOT * SLOT, FOFF = HOFF + PF_ROWS * 64 * 2;
+  // [FOFF] flag, [FOFF + 8] epoch | ordinal, [FOFF + 16] per-wave failed words
+  __shared__ __attribute__((aligned(16))) char smem[FOFF + 32];
   // h_t staging [32][64] bf16, accessed only through inline asm (32-bit LDS address)
   const unsigned hb_lds = (unsigned)(uintptr_t)((__attribute__((address_space(3))) char*)(smem + HOFF));
   const unsigned flag_lds = (unsigned)(uintptr_t)((__attribute__((address_space(3))) char*)(smem + FOFF));
@@ -136,9 +151,11 @@ __global__ __launch_bounds__(256, 1) void lstm_fwd_persistent_kernel(
   // production objects keep only the test hook bit (kDbgMask, persistent_guard.h): the
   // timing-only branches below fold away at compile time
   const int dbg = d.dbg & kDbgMask;
-  gu32* err = (gu32*)(sync + ((dbg >> 20) & 1));
-  gu32* cnt = (gu32*)(sync + 16 + 16 * m);
+  ps_u32* rbw = psync_rb(sync, m);
+  ps_u32* err = rbw + kPSyncErr;
   const unsigned spin_limit = d.spin_limit ? d.spin_limit : PF_SPIN_LIMIT;
+  // (dbg bit 21, tests: an unreachable target, so the polls fail and the bounded spin trips)
+  const unsigned force = ((dbg >> 21) & 1u) << 30;
   // DBG & 16: timeline stamps (s_memrealtime, 100 MHz) of step PF_STAMP_T, wave 0 lane 0 of
   // every workgroup, into sync + 4096 words (64 slots per workgroup; diagnostics only)
   constexpr int PF_STAMP_T = 10;
@@ -149,9 +166,13 @@ __global__ __launch_bounds__(256, 1) void lstm_fwd_persistent_kernel(
     }
   };
 
-  // completion guard (persistent_guard.h): started / expected counts before any exit path
-  unsigned ord = 0;
-  if (threadIdx.x == 0) ord = pguard_start(stat, (unsigned)d.T);
+  // completion guard (persistent_guard.h) and this launch's epoch (persistent_sync.h)
+  if (threadIdx.x == 0) {
+    const unsigned o = pguard_start(stat, (unsigned)d.T);
+    const unsigned e = __hip_atomic_fetch_add(rbw + kPSyncStart, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) / NB;
+    asm volatile("ds_write_b64 %0, %1" ::"v"(flag_lds + 8), "v"((unsigned long long)e | ((unsigned long long)o << 32))
+                 : "memory");
+  }
   // ---- prologue: stationary weight fragments (B operand: lane holds col l15, k 8g..8g+7)
   bf16x8 w[KT][4];
 #pragma unroll
@@ -165,6 +186,48 @@ __global__ __launch_bounds__(256, 1) void lstm_fwd_persistent_kernel(
   asm volatile("" ::: "memory");
   __builtin_amdgcn_s_waitcnt(0xF70);  // vmcnt(0) expcnt(7) lgkmcnt(15)
   __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  unsigned long long eo;
+  asm volatile("ds_read_b64 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(eo) : "v"(flag_lds + 8) : "memory");
+  const unsigned epoch = __builtin_amdgcn_readfirstlane((unsigned)eo);
+  const unsigned ord = __builtin_amdgcn_readfirstlane((unsigned)(eo >> 32));
+  const unsigned tag = epoch + 1u;
+  // arrivals a consumer needs before step tt reads chunk cc (SPLIT) / before step tt (per-step
+  // hand-off): every workgroup of the row block published it for steps 0 .. tt-1. SPLIT
+  // publishes chunk cc at the top of chunk cc + 2: in every step for cc <= NC-3, in all but the
+  // last step for the last two chunks; the per-step hand-off counts steps 1 .. T-1.
+  auto target = [&](int cc, int tt) -> unsigned {
+    const unsigned per_launch = SPLIT ? (unsigned)(cc <= NC - 3 ? d.T : d.T - 1) : (unsigned)(d.T - 1);
+    return epoch * (unsigned)NB * per_launch + (unsigned)(NB * (SPLIT ? tt : tt)) + force;
+  };
+  unsigned failed = 0;  // uniform: this wave failed a hand-off (runs on, never waits again)
+  // SPLIT: blocking wait of this wave for chunk cc before step tt reads it (a poll that did
+  // not match); a failure is recorded once and makes every later wait a no-op
+  auto wait_chunk = [&](int cc, int tt) {
+    if (failed) return;
+    unsigned seen_cnt = 0, seen_err = 0;
+    const unsigned tg = target(cc, tt);
+    const unsigned why = psync_wait(rbw + kPSyncGroup + cc, err, tg, tag, spin_limit, stat, &seen_cnt, &seen_err);
+    if (why != 0) {
+      failed = 1;
+      if (lane == 0) pguard_exit(stat, (unsigned)tt, why, seen_err, seen_cnt, tg, (unsigned)cc, ord);
+    }
+  };
+  // sc1 poll of chunk cc's counter (one uniform load; inline asm, so it stays where written
+  // and the chunk-top wait that covers it names its register)
+  auto poll = [&](int cc) {
+    unsigned v;
+    const unsigned* pa = sync + kPSyncHead + kPSyncRowBlock * m + kPSyncGroup + cc;
+    asm volatile("global_load_dword %0, %1, off sc1" : "=v"(v) : "v"(pa) : "memory");
+    return v;
+  };
+  unsigned pvr[2] = {0u, 0u};  // SPLIT: polls in flight (chunk j polls for chunk j + 4)
+  // per-step store bases of the previous step (SPLIT: chunk 0 finalizes the previous step's
+  // last chunk)
+  bf16_t* cnext_p = nullptr;
+  bf16_t* St_p = nullptr;
+  __amdgpu_buffer_rsrc_t xh_rsrc_p = __builtin_amdgcn_make_buffer_rsrc(XH, 0, 0, 0x00020000);
 
   // A piece s of this wave: k-step s, rows wid*8 + (lane>>3); the K_CONTIG 16-B chunk
   // swizzle (row>>1)&7 = 4(wid&1) + g is lane-constant, so it moves onto the source offset.
@@ -191,52 +254,37 @@ __global__ __launch_bounds__(256, 1) void lstm_fwd_persistent_kernel(
 
   for (int t = 0; t < d.T; ++t) {
     stamp(t, 0);
-    if (t > 0) {
-      // ---- publish step t-1 (every wave drained its sc1 h stores: issued before the drain's
-      // NSTORE - 1 C / S stores, which may stay in flight) and wait for the row block
-      wait_vmcnt<(DBG & 65536) ? 0 : NSTORE - 1>();
+    if (!SPLIT && t > 0) {
+      // ---- per-step hand-off (NC < 8): publish step t-1 (every wave drained its sc1 h
+      // stores: issued before the drain's NSTORE - 1 C / S stores, which may stay in flight),
+      // then thread 0 waits for the row block; the other waves load after the barrier it
+      // joins (MI355X_MICROARCH.md "Valid forms" row 1: sc1 stores, sc1 loads, no acquire)
+      wait_vmcnt<NSTORE - 1>();
       __builtin_amdgcn_s_barrier();
       asm volatile("" ::: "memory");
       stamp(t, 62);  // h stores drained, workgroup arrived
-      // thread 0's view of the wait, kept for the exit record (persistent_guard.h)
-      unsigned why = 0, seen_err = 0, seen_cnt = 0;
-      // (dbg bit 21, tests: an unreachable target, so the bounded spin trips deterministically)
-      const unsigned target = (unsigned)(NB * t) + (((dbg >> 21) & 1u) << 30);
       if (threadIdx.x == 0) {
-        __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        unsigned spins = 0;
-        while (!(dbg & 1) && (seen_cnt = __hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) < target) {
-          if ((seen_err = __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) != 0u) {
-            why = 1;
-            break;
+        __hip_atomic_fetch_add(rbw + kPSyncGroup, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        unsigned f = failed;
+        if (!f) {
+          unsigned seen_cnt = 0, seen_err = 0;
+          const unsigned tg = target(0, t);
+          const unsigned why = psync_wait(rbw + kPSyncGroup, err, tg, tag, spin_limit, stat, &seen_cnt, &seen_err);
+          if (why != 0) {
+            f = 1;
+            pguard_exit(stat, (unsigned)t, why, seen_err, seen_cnt, tg, 0u, ord);
           }
-          if (++spins > spin_limit) {
-            __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            pguard_sticky(stat);
-            why = 2;
-            break;
-          }
-          __builtin_amdgcn_s_sleep(2);
         }
         stamp(t, 63);  // row block complete (poll matched)
-        // (dbg bit 22, WF_DIAG builds only, WELLFLOW_PF_DBG=4194304: TIMING ONLY, unsafe — no acquire, to price it)
-        if (!((dbg >> 22) & 1)) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        const int ok = why == 0 ? 1 : 0;
-        asm volatile("ds_write_b32 %0, %1" ::"v"(flag_lds), "v"(ok) : "memory");
+        asm volatile("ds_write_b32 %0, %1" ::"v"(flag_lds), "v"(f) : "memory");
       }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();
       // the flag word through ds_read in asm (a volatile C++ access became a flat load with
       // sc0 sc1 and a vmcnt + lgkmcnt wait, every step)
-      int okv;
-      asm volatile("ds_read_b32 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(okv) : "v"(flag_lds) : "memory");
-      if (__builtin_amdgcn_readfirstlane(okv) != 1) {  // uniform: every wave reads the same word
-        if (lane == 0)
-          pguard_exit(stat, (unsigned)t, wid != 0 ? 4u : (why != 0 ? why : 3u), seen_err, seen_cnt, target,
-                      (unsigned)okv, ord);
-        return;
-      }
+      unsigned fv;
+      asm volatile("ds_read_b32 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(fv) : "v"(flag_lds) : "memory");
+      failed = __builtin_amdgcn_readfirstlane(fv);  // a failed workgroup runs on without waiting
     }
     stamp(t, 1);
     // opaque per-step copy of the row origin: stops the compiler hoisting every chunk's
@@ -250,6 +298,8 @@ __global__ __launch_bounds__(256, 1) void lstm_fwd_persistent_kernel(
     bf16_t* cnext = Cst + (size_t)(t + 1) * Bp * H + (size_t)(rb >> 4) * HB * 256;
     bf16_t* St = S + (size_t)t * Bp * G + (size_t)(rb >> 4) * HB * 1024;
     const char* abase = reinterpret_cast<const char*>(XH + ((size_t)t * d.B + rb) * KA) + aoff;
+    // SPLIT: the next step's A (XH has T + 1 slabs, so slab t + 1 always exists)
+    const char* abase_n = reinterpret_cast<const char*>(XH + ((size_t)(t + 1) * d.B + rb) * KA) + aoff;
     // slab t + 1 of XH as a buffer resource for the 16-B sc1 h stores: per-slab byte offsets
     // (< B * KA * 2 < 2^31, host-checked) so any batch size fits the 32-bit offsets
     const __amdgpu_buffer_rsrc_t xh_rsrc =
@@ -431,6 +481,38 @@ __global__ __launch_bounds__(256, 1) void lstm_fwd_persistent_kernel(
       __builtin_amdgcn_raw_buffer_store_b128(vv, xh_rsrc, loff_h, hsoff + e * PF_ROWS * KA * 2, 16 /* sc1 */);
     };
 
+    // SPLIT: stores of chunk e with explicit bases (chunk 0 finalizes the previous step's last
+    // chunk): h staged in LDS and stored FIRST (one 16-B sc1 store per thread), then the C / S
+    // stores, so the next chunk top's vmcnt(NSTORE - 1) leaves only those in flight and the
+    // chunk can be published there; then the c-queue rotation
+    auto epi_store_split = [&](int e, bf16_t* cnx, bf16_t* stp, const __amdgpu_buffer_rsrc_t& xrs,
+                               const float (&cv)[2][4], const unsigned (&pk)[2][8], const unsigned (&hv)[2][4]) {
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          asm volatile("ds_write_b16 %0, %1" ::"v"(hb_lds + 2u * ((i * 16 + 4 * g + r) * 64 + wid * 16 + l15)),
+                       "v"(hv[i][r])
+                       : "memory");
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      u32x4 vv;  // row threadIdx>>3, 16-B column threadIdx&7 of the [32][64] bf16 tile
+      asm volatile("ds_read_b128 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=&v"(vv) : "v"(hb_lds + 16u * threadIdx.x) : "memory");
+      __builtin_amdgcn_raw_buffer_store_b128(vv, xrs, loff_h, hsoff + e * PF_ROWS * KA * 2, 16 /* sc1 */);
+      if constexpr (!(DBG & 4)) {
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+          *reinterpret_cast<uint2*>(cnx + (2 * e + i) * HB * 256 + loff_c) =
+              make_uint2(pk_bf16(cv[i][0], cv[i][1]), pk_bf16(cv[i][2], cv[i][3]));
+          bf16_t* sb = stp + (2 * e + i) * HB * 1024 + loff_s;
+          *reinterpret_cast<uint4*>(sb) = make_uint4(pk[i][0], pk[i][1], pk[i][2], pk[i][3]);
+          *reinterpret_cast<uint4*>(sb + SHALF) = make_uint4(pk[i][4], pk[i][5], pk[i][6], pk[i][7]);
+        }
+      }
+      rotate(cv);
+    };
+
     // chunk c -> ring slot c % 3: KS A pieces + this wave's 2 FN blocks of c_{t-1}
     auto issue = [&](int c, auto sc) {  // chunk c into ring slot SL (= c % 3)
       constexpr int SL = decltype(sc)::value;
@@ -439,17 +521,29 @@ __global__ __launch_bounds__(256, 1) void lstm_fwd_persistent_kernel(
 #pragma unroll
       for (int s = 0; s < KS; ++s)
         __builtin_amdgcn_global_load_lds((const void*)(src + s * 128), (lds_void*)(ra + s * 4096 + wid * 1024),
-                                         16, 0, 0);
+                                         16, 0, 16 /* sc1 */);
+    };
+    // SPLIT: chunk c of the step whose A base is `base` into ring slot SL
+    auto issue_b = [&](const char* base, int c, auto sc) {
+      constexpr int SL = decltype(sc)::value;
+      char* ra = smem + SL * SLOT;
+      const char* src = base + (size_t)c * ABYTES;
+#pragma unroll
+      for (int s = 0; s < KS; ++s)
+        __builtin_amdgcn_global_load_lds((const void*)(src + s * 128), (lds_void*)(ra + s * 4096 + wid * 1024),
+                                         16, 0, 16 /* sc1 */);
     };
     // piece s of chunk c into ring slot SL
     auto issue_piece = [&](int c, auto sc, int s) {
       constexpr int SL = decltype(sc)::value;
       const char* src = abase + (size_t)c * ABYTES;
       __builtin_amdgcn_global_load_lds((const void*)(src + s * 128), (lds_void*)(smem + SL * SLOT + s * 4096 + wid * 1024),
-                                       16, 0, 0);
+                                       16, 0, 16 /* sc1 */);
     };
-    issue(0, std::integral_constant<int, 0>{});
-    if constexpr (NC > 1 && !PF01) issue(1, std::integral_constant<int, 1>{});
+    if constexpr (!SPLIT) {  // per-step hand-off: chunk 0 (and 1) at the step top
+      issue(0, std::integral_constant<int, 0>{});
+      if constexpr (NC > 1 && !PF01) issue(1, std::integral_constant<int, 1>{});
+    }
 
     // chunk body, ring slot P = c % 3 compile-time (3 bodies in a runtime loop keep the
     // register pressure of a 3-chunk kernel; a fully unrolled NC = 8 spilled)
@@ -462,7 +556,15 @@ __global__ __launch_bounds__(256, 1) void lstm_fwd_persistent_kernel(
       // vector-memory ops issued after chunk c's LDS-DMA (top of c issues c+2, then stores)
       // (issue order: prologue glds 0, 1; chunk k: glds k+2, then the stores of chunk k-1,
       // NSTORE per wave, none in chunk 0)
-      if (c == 0) {
+      // SPLIT: chunk j (global) waits until only chunk j-2's C / S stores are in flight: its
+      // own pieces, chunk j+1's, chunk j-2's h store (published below) and the poll issued
+      // at the top of chunk j-2 (its register is an operand: no use moves above the wait)
+      if constexpr (SPLIT) {
+        if (t == 0 && c < 2)
+          wait_vmcnt<LPT>();
+        else
+          asm volatile("s_waitcnt vmcnt(%1)" : "+v"(pvr[P & 1]) : "n"(NSTORE - 1) : "memory");
+      } else if (c == 0) {
         if (NC > 1 && !FIRST) wait_vmcnt<LPT>(); else wait_vmcnt<0>();
       } else if (c == 1) {
         if (NC > 2) wait_vmcnt<LPT>(); else wait_vmcnt<0>();
@@ -477,7 +579,23 @@ __global__ __launch_bounds__(256, 1) void lstm_fwd_persistent_kernel(
       asm volatile("" ::: "memory");
       __builtin_amdgcn_sched_barrier(0);  // keep each chunk's code (and live ranges) to itself
       stamp(t, 3 + 5 * c);
-      if constexpr (!FIRST) {
+      if constexpr (SPLIT) {
+        // publish chunk j-2: every wave drained its h store before the barrier above
+        if ((t > 0 || c >= 2) && threadIdx.x == 0)
+          __hip_atomic_fetch_add(rbw + kPSyncGroup + (c >= 2 ? c - 2 : c + NC - 2), 1u, __ATOMIC_RELAXED,
+                                 __HIP_MEMORY_SCOPE_AGENT);
+        // chunk j+2: its h rows were published by the row block at least 4 chunks ago; the
+        // poll of two chunks ago says whether all arrived, else wait here (bounded)
+        const int c2 = c + 2 < NC ? c + 2 : c + 2 - NC, t2 = c + 2 < NC ? t : t + 1;
+        if (t2 < d.T) {
+          if (t2 >= 1 && !failed && !psync_reached(__builtin_amdgcn_readfirstlane(pvr[P & 1]), target(c2, t2)))
+            wait_chunk(c2, t2);
+          issue_b(t2 == t ? abase : abase_n, c2, std::integral_constant<int, (P + 2) % NSLOT>{});
+        }
+        // poll for chunk j+4 (read at the top of chunk j+2)
+        const int c4 = c + 4 < NC ? c + 4 : c + 4 - NC, t4 = c + 4 < NC ? t : t + 1;
+        if (t4 >= 1 && t4 < d.T) pvr[P & 1] = poll(c4);
+      } else if constexpr (!FIRST) {
         if (c + 2 < NC) issue(c + 2, std::integral_constant<int, (P + 2) % 3>{});
       }
       // A fragment reads through asm with COUNTED waits: as C++ loads, the compiler's waitcnt
@@ -695,7 +813,14 @@ __global__ __launch_bounds__(256, 1) void lstm_fwd_persistent_kernel(
         asm volatile("" ::"v"(sink));
         stamp(t, 4 + 5 * c);
       }
-      if constexpr (KT >= 16 && (DBG & 64)) {
+      if constexpr (SPLIT) {
+        if (t > 0 || c > 0) {
+          const bool prv = c == 0;  // the previous step's last chunk
+          epi_store_split(prv ? NC - 1 : c - 1, prv ? cnext_p : cnext, prv ? St_p : St, prv ? xh_rsrc_p : xh_rsrc,
+                          cv, pk, hv);
+          stamp(t, 5 + 5 * c);
+        }
+      } else if constexpr (KT >= 16 && (DBG & 64)) {
         if (c > 0) rotate(cv);
       } else if (c > 0 && (DBG & 16384) == 0) {  // DBG 16384: timing only, no stores / publish
         epi_store(c - 1, cv, pk, hv);
@@ -711,49 +836,81 @@ __global__ __launch_bounds__(256, 1) void lstm_fwd_persistent_kernel(
     using S0 = std::integral_constant<int, 0>;
     using S1 = std::integral_constant<int, 1>;
     using S2 = std::integral_constant<int, 2>;
+    using S3 = std::integral_constant<int, 3>;
     using NF = std::false_type;
-    if constexpr (PF01) {
-      chunk(0, S0{}, std::true_type{});
-      for (int c = 1; c < NC; c += 3) {
-        chunk(c, S1{}, NF{});
-        if (c + 1 < NC) chunk(c + 1, S2{}, NF{});
-        if (c + 2 < NC) chunk(c + 2, S0{}, NF{});
+    if constexpr (SPLIT) {
+      if (t == 0) {  // chunks 0 and 1 of step 0 (XH[0] = [x_0 | 1 | h_-1 = 0] is written before the launch)
+        issue_b(abase, 0, S0{});
+        issue_b(abase, 1, S1{});
+      }
+      for (int c = 0; c < NC; c += 4) {
+        chunk(c, S0{}, NF{});
+        chunk(c + 1, S1{}, NF{});
+        chunk(c + 2, S2{}, NF{});
+        chunk(c + 3, S3{}, NF{});
+      }
+      if (t == d.T - 1) {  // drain: the last chunk's epilogue (h_T is the regression head's input)
+        float cv[2][4];
+        unsigned pk[2][8], hv[2][4];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) epi_elem(e >> 2, e & 3, cv, pk, hv);
+        epi_store_split(NC - 1, cnext, St, xh_rsrc, cv, pk, hv);
       }
     } else {
-      for (int c = 0; c < NC; c += 3) {
-        chunk(c, S0{}, NF{});
-        if (c + 1 < NC) chunk(c + 1, S1{}, NF{});
-        if (c + 2 < NC) chunk(c + 2, S2{}, NF{});
-      }
-    }
-    {  // drain: the last chunk's epilogue
-      float cv[2][4];
-      unsigned pk[2][8], hv[2][4];
-#pragma unroll
-      for (int e = 0; e < 8; ++e) epi_elem(e >> 2, e & 3, cv, pk, hv);
-      // h first (the only bytes other workgroups read in this launch), then the C / S stores,
-      // so the step-top hand-off drains only the h store (vmcnt(NSTORE - 1)) and the last
-      // chunk's C / S stores complete behind the hand-off instead of in front of it
-      // Deferring these six stores past the next step's hand-off (after chunk 0's loop, which
-      // stores nothing) measured neutral to worse: 1470-1486 us deferred vs 1454-1482 here
-      // (profiles/r3/ab_defer_drain_stores.txt). The write burst is not on the critical path.
-      if constexpr ((DBG & 65536) != 0) {  // A/B: the round-2 order (stores, then h)
-        epi_store(NC - 1, cv, pk, hv);
-        publish(NC - 1);
-      } else {
-        epi_h(hv);
-        publish(NC - 1);
-        if constexpr (!(DBG & 4)) {
-#pragma unroll
-          for (int k = 0; k < 6; ++k) epi_cs(NC - 1, k, cv, pk);
+      if constexpr (PF01) {
+        chunk(0, S0{}, std::true_type{});
+        for (int c = 1; c < NC; c += 3) {
+          chunk(c, S1{}, NF{});
+          if (c + 1 < NC) chunk(c + 1, S2{}, NF{});
+          if (c + 2 < NC) chunk(c + 2, S0{}, NF{});
         }
-        rotate(cv);
+      } else {
+        for (int c = 0; c < NC; c += 3) {
+          chunk(c, S0{}, NF{});
+          if (c + 1 < NC) chunk(c + 1, S1{}, NF{});
+          if (c + 2 < NC) chunk(c + 2, S2{}, NF{});
+        }
+      }
+      {  // drain: the last chunk's epilogue
+        float cv[2][4];
+        unsigned pk[2][8], hv[2][4];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) epi_elem(e >> 2, e & 3, cv, pk, hv);
+        // h first (the only bytes other workgroups read in this launch), then the C / S stores,
+        // so the step-top hand-off drains only the h store (vmcnt(NSTORE - 1)) and the last
+        // chunk's C / S stores complete behind the hand-off instead of in front of it
+        // Deferring these six stores past the next step's hand-off (after chunk 0's loop, which
+        // stores nothing) measured neutral to worse: 1470-1486 us deferred vs 1454-1482 here
+        // (profiles/r3/ab_defer_drain_stores.txt). The write burst is not on the critical path.
+        if constexpr ((DBG & 65536) != 0) {  // A/B: the round-2 order (stores, then h)
+          epi_store(NC - 1, cv, pk, hv);
+          publish(NC - 1);
+        } else {
+          epi_h(hv);
+          publish(NC - 1);
+          if constexpr (!(DBG & 4)) {
+#pragma unroll
+            for (int k = 0; k < 6; ++k) epi_cs(NC - 1, k, cv, pk);
+          }
+          rotate(cv);
+        }
       }
     }
+    cnext_p = cnext;
+    St_p = St;
+    xh_rsrc_p = xh_rsrc;
   }
-  // completion count: every workgroup that ran all T steps adds T to DONE; any early exit
-  // leaves DONE short of EXPECT, which the host check reports even when no spin bound tripped
-  if (threadIdx.x == 0) pguard_done(stat, (unsigned)d.T);
+  // completion count: a workgroup none of whose waves failed a hand-off adds T to DONE; a
+  // failure leaves DONE short of EXPECT, which the host check reports
+  wait_vmcnt<0>();
+  asm volatile("ds_write_b32 %0, %1" ::"v"(flag_lds + 16 + 4 * wid), "v"(failed) : "memory");
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  if (threadIdx.x == 0) {
+    u32x4 fw;
+    asm volatile("ds_read_b128 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(fw) : "v"(flag_lds + 16) : "memory");
+    if ((fw[0] | fw[1] | fw[2] | fw[3]) == 0u) pguard_done(stat, (unsigned)d.T);
+  }
 }
 
 template <int KT, int NC>

@@ -74,30 +74,16 @@ __device__ __forceinline__ void pguard_sticky(unsigned* stat) {
 }
 
 // WELLFLOW_PF_DBG bits a build honours. Production objects (no WF_DIAG) keep only the TEST hook
-// bit 21 (WELLFLOW_FORCE_TIMEOUT: every hand-off wait trips its bound, so the run FAILS loudly
-// through the STAT block); every timing-only switch that changes results — bit 0 (skip the
-// hand-off wait), bit 20 (the legacy memset), bit 22 (no acquire after the poll) — and every
-// A/B kernel variant exists only in WF_DIAG builds (WELLFLOW_DIAG_BUILD=1, _build.py). The
-// launchers mask LstmDims::dbg with it and the kernels mask again, so a stray environment
-// variable cannot reach a production kernel (round-3 VERDICT weak #3).
+// bit 21 (WELLFLOW_FORCE_TIMEOUT: every hand-off poll misses and every wait trips its bound, so
+// the run FAILS loudly through the STAT block); the timing-only kernel variants exist only in
+// WF_DIAG builds (WELLFLOW_DIAG_BUILD=1, _build.py). The launchers mask LstmDims::dbg with it
+// and the kernels mask again, so a stray environment variable cannot reach a production kernel
+// (round-3 VERDICT weak #3).
 constexpr int kDbgTestBits = 1 << 21;
 #ifdef WF_DIAG
 constexpr int kDbgMask = ~0;
 #else
 constexpr int kDbgMask = kDbgTestBits;
 #endif
-
-// Diagnostic A/B (WELLFLOW_PF_DBG bit 20, WF_DIAG builds only): the round-2 per-launch reset,
-// a memset starting 4 B past the allocation (words 1 .. 16 + 16 MB - 1, error word 1) instead
-// of one whole-block memset from word 0. Host-side only; the kernels then read their error
-// word at word 1.
-template <typename D> inline bool persistent_memset_legacy(const D& d) { return (((d.dbg & kDbgMask) >> 20) & 1) != 0; }
-
-// The per-launch reset must be ONE memset node that starts 16-B aligned at the sync buffer's
-// own allocation and covers a multiple of 16 B (profiles/r3_early_exit.md: an unaligned memset
-// node under graph replay left 0x04040404 in the error word). Returns false to refuse a launch.
-inline bool persistent_reset_ok(const void* p, size_t bytes) {
-  return (reinterpret_cast<uintptr_t>(p) & 15u) == 0 && (bytes & 15u) == 0;
-}
 
 }  // namespace wf

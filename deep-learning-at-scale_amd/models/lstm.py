@@ -125,9 +125,10 @@ _EXIT_REASONS = {1: "the launch's error word was set while it polled (another wo
 
 
 def persistent_sync_buffer(B: int, row_quantum: int, device) -> torch.Tensor:
-    """int32 sync buffer of a persistent LSTM kernel for batches <= B: the per-launch block
-    (error word + one arrival counter per row block of ``row_quantum`` rows, zeroed by the
-    launcher) and the STAT block of running completion totals at its end."""
+    """int32 sync buffer of a persistent LSTM kernel for batches <= B, zeroed here once: one
+    64-B line of hand-off words per row block of ``row_quantum`` rows (launch epoch, group
+    arrival counters, tagged error word; csrc/persistent_sync.h — they only count up, no
+    launch resets them) and the STAT block of running completion totals at its end."""
     return torch.zeros(16 + 16 * (B // row_quantum + 1) + PSTAT_WORDS, dtype=torch.int32, device=device)
 
 
@@ -299,8 +300,11 @@ class NativeLSTM:
         return pstat_error(st["forward"]) | (pstat_error(st["backward"]) << 4)
 
     def reset_device_errors(self) -> None:
-        self.sync[-PSTAT_WORDS:].zero_()
-        self.sync_bwd[-PSTAT_WORDS:].zero_()
+        """Zero both sync buffers WHOLE: the STAT totals and the monotonic hand-off words
+        (csrc/persistent_sync.h: launch epochs and group arrival counters only count up, and
+        no launch resets them, so they are cleared only together, between launches)."""
+        self.sync.zero_()
+        self.sync_bwd.zero_()
 
     def check_device_errors(self) -> None:
         """Raise if any persistent launch since the last reset left work undone (a tripped

@@ -38,7 +38,7 @@ w_out = eng.lay.views(eng.params)[1]
 args = (eng.WhhT, eng.XH, eng.Cst, eng.S, eng.DG, eng.dcarry, eng.dy, w_out, *dims)
 row = {"step v8": timeit(lambda: C.lstm_backward(*args, 8, None))}
 ref = eng.DG.clone()
-for dbg in ("0", "64", "512"):  # correct builds must match the per-step kernels
+for dbg in os.environ.get("PB_CHECK", "0").split(","):  # correct builds must match the per-step kernels
     os.environ["WELLFLOW_PF_DBG"] = dbg
     eng.DG.zero_()
     C.lstm_backward(*args, 8, eng.sync_bwd)
