@@ -397,6 +397,8 @@ def main() -> int:
     ap.add_argument("--bwd-variant", type=int, default=None)
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--eager-comm", action="store_true", help="all-reduce between two graphs, not captured")
+    ap.add_argument("--comm-dtype", choices=["fp32", "bf16"], default="fp32",
+                    help="C2 gradient all-reduce precision (parallel/dist.py; default fp32)")
     ap.add_argument("--stream-fp32", action="store_true", help="mlp_online: stream fp32 features")
     ap.add_argument("--host-pool", type=int, default=8, help="mlp_online: distinct pinned host batches cycled")
     ap.add_argument("--device", choices=["auto", "cpu"], default="auto",
@@ -445,7 +447,7 @@ def main() -> int:
         print("bench.py: no GPU visible (use --device cpu for the contract rehearsal)", file=sys.stderr)
         return 2
     rccl_log = _rccl_debug_setup(int(os.environ.get("RANK", "0"))) if args.device != "cpu" else None
-    ctx = DistContext.from_env(device="cpu" if args.device == "cpu" else None)
+    ctx = DistContext.from_env(device="cpu" if args.device == "cpu" else None, comm_dtype=args.comm_dtype)
     cpu = ctx.device.type == "cpu"
     if ctx.world_size != args.gpus:
         print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={ctx.world_size}", file=sys.stderr)
@@ -520,6 +522,7 @@ def main() -> int:
             "rccl_version": rccl,
             "comm_ms": None if comm is None else round(comm, 4),
             "grad_bucket_mb": grad_mb,
+            "comm_dtype": args.comm_dtype,
             "step_graph": step_graph,
             "comm_in_graph": comm_in_graph,
             "train_loss": round(loss, 6),  # mean over the run

@@ -72,6 +72,7 @@ class RunConfig:
     # runtime
     device: str = "auto"         # auto | cpu | cuda
     precision: str = "bf16"      # bf16 (native MFMA path) | fp32 (torch oracle)
+    comm_dtype: str = "fp32"     # C2 gradient all-reduce precision: fp32 | bf16 (parallel/dist.py)
     group_col: str = ""          # series id column for windowing (default: first string col)
     # windowed models (lstm, cnn): "time" = contiguous per-series blocks in time order with a
     # one-window gap between splits (no row of a val/test window inside any training window);
@@ -140,6 +141,8 @@ def build_parser(model: str) -> argparse.ArgumentParser:
     ap.add_argument("--dropout", type=float)
     ap.add_argument("--device", choices=["auto", "cpu", "cuda"])
     ap.add_argument("--precision", choices=["bf16", "fp32"])
+    ap.add_argument("--comm-dtype", dest="comm_dtype", choices=["fp32", "bf16"],
+                    help="data-parallel gradient all-reduce precision (default fp32)")
     ap.add_argument("--group-col", dest="group_col")
     ap.add_argument("--window-split", dest="window_split", choices=["time", "random"])
     ap.add_argument("--synth-wells", type=int, dest="synth_wells")

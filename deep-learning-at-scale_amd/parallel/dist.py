@@ -15,6 +15,12 @@ xGMI mesh (a 4.7 MB ring all-reduce at 8 ranks is ~7-50 us, versus a ~10-30 us R
 launch/protocol floor): ONE flat bucket per step is the latency-optimal choice. Larger
 models can set ``bucket_bytes`` to split the flat buffer into equal chunks that are
 reduced back-to-back on a side stream (see :meth:`all_reduce_sum_`).
+
+Gradient-comm precision (SURVEY.md §2.5 "bf16 halves them", §7.4 item 7 "an fp32 all-reduce
+option"): ``comm_dtype`` "fp32" (default) reduces the fp32 bucket as is; "bf16" rounds it into a
+preallocated bf16 twin, reduces that (half the bytes on every xGMI hop) and widens the sum back
+into the fp32 bucket the optimizer reads. The twin lives as long as the context, so a captured
+step graph replays the same cast / reduce / cast on the same addresses.
 """
 from __future__ import annotations
 
@@ -23,6 +29,8 @@ import os
 
 import torch
 import torch.distributed as dist
+
+COMM_DTYPES = {"fp32": torch.float32, "bf16": torch.bfloat16}
 
 
 def _base_store(rank: int, world: int, timeout_s: float):
@@ -35,18 +43,22 @@ def _base_store(rank: int, world: int, timeout_s: float):
 class DistContext:
     def __init__(self, rank: int = 0, world_size: int = 1, local_rank: int = 0,
                  device: torch.device | None = None, backend: str | None = None,
-                 bucket_bytes: int = 0):
+                 bucket_bytes: int = 0, comm_dtype: str = "fp32"):
         self.rank, self.world_size, self.local_rank = rank, world_size, local_rank
         self.device = device or torch.device("cpu")
         self.backend = backend
         self.bucket_bytes = bucket_bytes
+        if comm_dtype not in COMM_DTYPES:
+            raise ValueError(f"comm_dtype must be one of {sorted(COMM_DTYPES)}, got {comm_dtype!r}")
+        self.comm_dtype = comm_dtype
+        self._lowp: dict = {}  # fp32 bucket (data_ptr, numel) -> its bf16 reduction twin
         self.forced = False
 
     # ---------------------------------------------------------------- bootstrap
     @classmethod
     def from_env(cls, backend: str | None = None, timeout_s: float = 600.0,
                  bucket_bytes: int = 0, device: str | None = None,
-                 force_group: bool = False) -> "DistContext":
+                 force_group: bool = False, comm_dtype: str = "fp32") -> "DistContext":
         """Read torchrun's RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* and init the group.
 
         Device selection happens BEFORE any CUDA call so each rank pins its own GPU.
@@ -79,7 +91,7 @@ class DistContext:
                 # transport addresses. Namespace every attempt's keys.
                 kw["store"] = dist.PrefixStore(f"wellflow/attempt_{restart}", _base_store(rank, world, timeout_s))
             dist.init_process_group(**kw)
-        ctx = cls(rank, world, local, dev, backend, bucket_bytes)
+        ctx = cls(rank, world, local, dev, backend, bucket_bytes, comm_dtype)
         ctx.forced = bool(force_group)
         return ctx
 
@@ -98,8 +110,23 @@ class DistContext:
         return t
 
     def all_reduce_sum_(self, t: torch.Tensor) -> torch.Tensor:
+        """C2: in-place SUM over ranks, in ``comm_dtype`` (fp32 tensors only are narrowed)."""
         if not self.distributed:
             return t
+        low = COMM_DTYPES[self.comm_dtype]
+        if low != torch.float32 and t.dtype == torch.float32:
+            key = (t.data_ptr(), t.numel())
+            buf = self._lowp.get(key)
+            if buf is None:
+                buf = self._lowp[key] = torch.empty(t.numel(), dtype=low, device=t.device)
+            buf.copy_(t.reshape(-1))
+            self._reduce(buf)
+            t.reshape(-1).copy_(buf)
+            return t
+        self._reduce(t)
+        return t
+
+    def _reduce(self, t: torch.Tensor) -> None:
         if self.bucket_bytes and t.numel() * t.element_size() > self.bucket_bytes:
             n = max(1, self.bucket_bytes // t.element_size())
             works = [dist.all_reduce(t[i : i + n], async_op=True) for i in range(0, t.numel(), n)]
@@ -107,7 +134,6 @@ class DistContext:
                 w.wait()
         else:
             dist.all_reduce(t)
-        return t
 
     def all_reduce_avg_(self, t: torch.Tensor) -> torch.Tensor:
         self.all_reduce_sum_(t)

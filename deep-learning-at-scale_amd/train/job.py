@@ -95,7 +95,7 @@ def run_job(model: str, argv, log=print) -> dict:
 
 def run_config(cfg: RunConfig, log=print) -> dict:
     device = None if cfg.device == "auto" else cfg.device
-    ctx = DistContext.from_env(device=device)
+    ctx = DistContext.from_env(device=device, comm_dtype=cfg.comm_dtype)
     say = log if ctx.is_main else (lambda *a, **k: None)
     schema = parse_schema(cfg.column_names, cfg.column_types)
     say(schema)  # cnn.py:62

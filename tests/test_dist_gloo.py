@@ -182,3 +182,59 @@ def test_dp_step_runner_equals_single_process_step(tmp_path, world, kind):
         assert rr["err"] < 1e-5, rr
         assert abs(rr["loss"] - rr["rloss"]) < 1e-4 * abs(rr["rloss"]), rr
     assert all(rr["p0"] == res[0]["p0"] for rr in res)
+
+
+@pytest.mark.parametrize("world,kind", [(2, "lstm"), (4, "mlp")])
+def test_dp_bf16_comm_matches_fp32(tmp_path, world, kind):
+    """C2 in bf16 (DistContext comm_dtype="bf16": the fp32 bucket rounded into a bf16 twin,
+    reduced, widened back; SURVEY.md §2.5 "bf16 halves them"): the reduced gradient of one
+    StepRunner step agrees with the fp32 reduction to bf16 rounding (relative L2 < 2^-7) and
+    with the single-process gradient of the concatenated batch; every rank holds the same
+    result; the twin is one buffer, reused by every step."""
+    res = _torchrun(tmp_path, """
+        from wellflow.models.base import TorchEngine
+        from wellflow.models.mlp import MLPRegressor
+        from wellflow.models.lstm import LSTMRegressor
+        from wellflow.optim.flat import FlatSGD
+        from wellflow.train.step import StepRunner
+        KIND = __KIND__
+        N = 32
+        def make():
+            return MLPRegressor(6, (16, 8)) if KIND == "mlp" else LSTMRegressor(6, 8)
+        g = torch.Generator().manual_seed(0)
+        X = torch.randn(*((N, 6) if KIND == "mlp" else (N, 5, 6)), generator=g)
+        Y = torch.randn(N, generator=g)
+        ctx = DistContext.from_env(device="cpu", comm_dtype="bf16")
+        W, r = ctx.world_size, ctx.rank
+        B = N // W
+        xs, ys = X[r * B:(r + 1) * B], Y[r * B:(r + 1) * B]
+        torch.manual_seed(100)
+        eng = TorchEngine(make(), loss="mse")
+        p0 = eng.params.clone()
+        # lr 0: the step leaves the parameters alone and the reduced gradient in the bucket
+        run = StepRunner(eng, FlatSGD(eng.params, eng.grads, lr=0.0, momentum=0.0), ctx, 1.0 / N,
+                         lambda k: (xs, ys), graph=False)
+        grads = []
+        for s in range(2):
+            run.run(s)
+            grads.append(eng.grads.clone())
+        g16 = grads[-1]
+        ctx.comm_dtype = "fp32"
+        eng.params.copy_(p0)
+        run.run(2)
+        g32 = eng.grads.clone()
+        ref = TorchEngine(make(), loss="mse")
+        ref.params.copy_(p0)
+        ref.sync_weights() if hasattr(ref, "sync_weights") else None
+        ref.forward_backward(X, Y, 1.0 / N)
+        rel = lambda a, b: ((a - b).norm() / b.norm()).item()
+        json.dump({"r16": rel(g16, g32), "rref": rel(g16, ref.grads), "r32": rel(g32, ref.grads),
+                   "same": torch.equal(grads[0], grads[1]), "twins": len(ctx._lowp),
+                   "g": g16[:6].tolist()}, open(f"{OUT}/rank{r}.json", "w"))
+        ctx.shutdown()
+    """.replace("__KIND__", repr(kind)), world)
+    for rr in res:
+        assert 0 < rr["r16"] < 2 ** -7, rr   # bf16 rounding, and the bf16 path really ran
+        assert rr["rref"] < 2 ** -7 and rr["r32"] < 1e-5, rr
+        assert rr["same"] and rr["twins"] == 1, rr
+    assert all(rr["g"] == res[0]["g"] for rr in res)
