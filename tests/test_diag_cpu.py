@@ -77,12 +77,20 @@ def test_mlp_dbg_only_in_diag_builds():
     assert s.count("dbg &= kMlpDbgMask;") == 2 and "mlp_dbg_dev &= kMlpDbgMask;" in s
 
 
-def test_launchers_assert_aligned_reset():
-    for name in ("lstm_persistent.hip", "lstm_persistent_bwd.hip"):
+def test_persistent_launchers_never_memset():
+    """Round-4 VERDICT item 4: no memset node precedes a persistent launch — the hand-off words
+    only count up (csrc/persistent_sync.h: launch epochs, group arrival counters, a tagged error
+    word), so neither launcher nor kernel source may reset the sync buffer, and the kernels
+    derive their targets from the epoch."""
+    for name in ("lstm_persistent.hip", "lstm_persistent_bwd.hip", "lstm_persistent_fwd.inc.h",
+                 "lstm_persistent_bwd.inc.h", "binding.cpp"):
         s = _read(name)
-        assert "persistent_reset_ok(sync, reset_bytes)" in s, name
-    g = _read("persistent_guard.h")
-    assert "(reinterpret_cast<uintptr_t>(p) & 15u) == 0 && (bytes & 15u) == 0" in g
+        assert "hipMemset" not in s and "memset(" not in s, name
+    for name in ("lstm_persistent_fwd.inc.h", "lstm_persistent_bwd.inc.h"):
+        s = _read(name)
+        assert "kPSyncStart" in s and "epoch" in s and "psync_wait" in s, name
+    sync = _read("persistent_sync.h")
+    assert "psync_reached" in sync and "(int)(v - target) >= 0" in sync
 
 
 def test_bench_refuses_diag_env():
