@@ -475,13 +475,17 @@ def main() -> int:
         if ctx.is_main:
             import gc
 
-            from wellflow.train.parity import lstm_adam_trajectory
+            from wellflow.train.parity import cnn_sgd_trajectory, lstm_adam_trajectory, mlp_adam_trajectory
 
-            gc.collect()
-            torch.cuda.empty_cache()
-            par = lstm_adam_trajectory(ctx.device)
-            par.pop("native", None)
-            par.pop("fp32", None)
+            par = {}
+            for name, fn in (("lstm", lstm_adam_trajectory), ("mlp", mlp_adam_trajectory), ("cnn", cnn_sgd_trajectory)):
+                gc.collect()
+                torch.cuda.empty_cache()
+                r = fn(ctx.device)
+                r.pop("native", None)
+                r.pop("fp32", None)
+                par[name] = r
+            par["pass"] = all(par[k]["pass"] for k in ("lstm", "mlp", "cnn"))
         ctx.barrier()
 
     W = ctx.world_size

@@ -19,11 +19,17 @@ namespace {
 
 using wf::bf16_t;
 
+// A/B and diagnostic environment overrides are read only when the HIP objects are a WF_DIAG
+// build (wf::dbg_mask() is ~0 there): a production _C.so reads exactly the documented knobs
+// (README "Environment knobs"; tests/test_diag_cpu.py checks the set).
+int diag_env(const char* name, int dflt) {
+  if (wf::dbg_mask() != ~0) return dflt;
+  const char* v = std::getenv(name);
+  return v != nullptr ? std::atoi(v) : dflt;
+}
+
 bool disable_glds() {
-  static const bool off = [] {
-    const char* v = std::getenv("WELLFLOW_NO_GLDS");
-    return v != nullptr && v[0] == '1';
-  }();
+  static const bool off = diag_env("WELLFLOW_NO_GLDS", 0) == 1;  // register-staged GEMM (A/B)
   return off;
 }
 
@@ -127,10 +133,8 @@ wf::LstmDims lstm_dims(int64_t B, int64_t T, int64_t F, int64_t KX, int64_t H) {
   TORCH_CHECK(KX % 64 == 0 && F + 1 <= KX, "lstm: KX must be a multiple of 64 and > F");
   wf::LstmDims d;
   d.B = (int)B; d.T = (int)T; d.F = (int)F; d.KX = (int)KX; d.H = (int)H;
-  const char* xm = std::getenv("WELLFLOW_XCD_MAP");  // diagnostics: 0 = identity tile order
-  d.xcd_map = (xm != nullptr && xm[0] == '0') ? 0 : 1;
-  const char* nt = std::getenv("WELLFLOW_NT");
-  d.nt = (nt != nullptr && nt[0] == '0') ? 0 : 1;
+  d.xcd_map = diag_env("WELLFLOW_XCD_MAP", 1) == 0 ? 0 : 1;  // diagnostics: 0 = identity tile order
+  d.nt = diag_env("WELLFLOW_NT", 1) == 0 ? 0 : 1;
   // WELLFLOW_PF_DBG: timing-only switches and A/B variants of the persistent kernels. Only a
   // WF_DIAG build of the HIP objects (WELLFLOW_DIAG_BUILD=1) honours them: dbg_mask() is the
   // mask the objects were compiled with, so a production _C.so ignores the variable
@@ -324,10 +328,7 @@ bool lstm_backward_dw(const at::Tensor& WhhT, const at::Tensor& XH, const at::Te
     // 1 / 2 / 3), 4 / 5 = 256x192 with a 5- / 4-slot 32-deep ring, 6 = 256x192 with staggered
     // wave groups, 7 (default) = 256x288 4-slot 32-deep ring (tools/dw_tiles.py: 1.107 ms vs
     // 1.166 for 3, 1.149 for 4, 1.307 for 6); shapes a tile cannot take fall back to 256x128
-    static const int big = [] {
-      const char* v = std::getenv("WELLFLOW_DW_BIG");
-      return v == nullptr ? 7 : std::atoi(v);
-    }();
+    static const int big = diag_env("WELLFLOW_DW_BIG", 7);
     e.big_tile = big;
     if (dw_slab.has_value()) {  // split-K partials plain-stored, one reduce (gemm.hip launch_dw_288w)
       check_t(*dw_slab, at::kFloat, "dw_slab");

@@ -28,10 +28,14 @@
 //    step counter.
 //
 // Dropout (p = 0.5, Keras inverted dropout) is a counter hash, never stored: the keep bit of
-// (window w, step t, filter f) is bit 4*(f >> 4) + (f & 3) of lowbias32(((w*T + t)*4 +
-// ((f >> 2) & 3)) ^ smix), smix mixing the engine seed and the device step counter (so every
-// hipGraph replay draws a new mask). The forward needs one hash per lane per step (its lane
-// holds filters 16b + 4q + r of one window), the backward four (four windows per lane).
+// (window w, step t, filter f = 16b + 4q + r) is bit k + 16 (r & 1), k = 2b + (r >> 1), of
+// lowbias32(((w*T + t)*4 + q) ^ smix), smix mixing the engine seed and the device step counter
+// (so every hipGraph replay draws a new mask). The forward needs one hash per lane per step (its
+// lane holds filters 16b + 4q + r of one window), the backward four (four windows per lane).
+// The two keep bits of a bf16 pair (r, r+1 of block b: k = 2b + r/2) sit 16 bits apart, so ONE
+// shift moves both into the pair's sign bits: OR-ing them into the packed activations makes a
+// dropped value negative, and one packed int16 max with 0 is ReLU and dropout of both halves
+// (bf16 orders like int16 on the non-negative side; every negative, -0 included, becomes +0).
 // wellflow/models/cnn.py cnn_dropout_mask mirrors it bit for bit for the fp32 tests. The
 // 1/(1-p) = 2 scale is applied to the dense output (forward) and to dOut (backward) instead
 // of to every activation.
@@ -52,8 +56,24 @@ __device__ __forceinline__ f32x4 mfma16(bf16x4 a, bf16x4 b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a, b, c, 0, 0, 0);
 }
 typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+typedef unsigned u32x4v __attribute__((ext_vector_type(4)));
+typedef short i16x2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ bf16x4 frag(unsigned lo, unsigned hi) {
   return __builtin_bit_cast(bf16x4, (u32x2{lo, hi}));
+}
+__device__ __forceinline__ bf16x8 frag8(unsigned a, unsigned b, unsigned c, unsigned d) {
+  return __builtin_bit_cast(bf16x8, (u32x4v{a, b, c, d}));
+}
+// ReLU of a packed bf16 pair: one v_pk_max_i16 against 0 (see the dropout note above)
+__device__ __forceinline__ unsigned relu_pk(unsigned v) {
+  const i16x2 r = __builtin_elementwise_max(__builtin_bit_cast(i16x2, v), (i16x2{0, 0}));
+  return __builtin_bit_cast(unsigned, r);
+}
+// dropout of pair k given the lane's INVERTED mask word mi = ~m: keep bits k and k + 16 (set =
+// dropped after the inversion) into the two sign bits, so relu_pk zeroes a dropped value:
+// v_lshlrev + v_and_or_b32
+__device__ __forceinline__ unsigned drop_pk(unsigned v, unsigned mi, int k) {
+  return (mi << (15 - k)) & 0x80008000u | v;
 }
 __device__ __forceinline__ unsigned lowbias32(unsigned x) {
   x ^= x >> 16;
@@ -97,8 +117,9 @@ struct KSlot {
 };
 
 // ------------------------------------------------------------------------------- forward
-// TRAIN: dropout (drop != 0), loss + dOut + partials. !TRAIN: predictions only (eval).
-template <int NFB, int T, bool TRAIN>
+// TRAIN: loss + dOut + partials, DROP: dropout (compile-time: a runtime flag became a
+// v_cndmask per pair). !TRAIN: predictions only (eval).
+template <int NFB, int T, bool TRAIN, bool DROP>
 __global__ __launch_bounds__(512, 1) void cnn_fwd_kernel(
     const float* __restrict__ x, int B, int L, const bf16_t* __restrict__ WcA, int Kc,
     const bf16x4* __restrict__ WdF, const float* __restrict__ bd, int O, const float* __restrict__ y,
@@ -106,9 +127,10 @@ __global__ __launch_bounds__(512, 1) void cnn_fwd_kernel(
     float clip, float scale, float keep_scale, int drop, unsigned seed, const long long* __restrict__ rng, int prio) {
   constexpr int XR = (T + 6) / 4 * 4;  // x samples per lane: 4q .. 4q + T + 2, whole float4s
   constexpr int NFRAG = T * NFB * 64;
+  static_assert(NFB == 7, "dense fragments: 3 filter-block pairs (16x16x32) + block 6 (16x16x16)");
+  constexpr int TB = NFB * 64 * 8;  // bytes of one step's dense fragments
   // ONE static LDS object: the dense weights' fragment image, then the wave partials
   __shared__ __attribute__((aligned(16))) char smem[NFRAG * 8 + CNN_NW * 20 * 4];
-  bf16x4* wd_lds = reinterpret_cast<bf16x4*>(smem);
   float* wpart = reinterpret_cast<float*>(smem + NFRAG * 8);
   {
     const uint4* src = reinterpret_cast<const uint4*>(WdF);
@@ -117,7 +139,7 @@ __global__ __launch_bounds__(512, 1) void cnn_fwd_kernel(
   }
   const int lane = threadIdx.x & 63, l15 = lane & 15, q = lane >> 4;
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  if (prio && wid >= 4) __builtin_amdgcn_s_setprio(1);  // static priority, younger half (A/B)
+  (void)prio;
   // conv weights as the A operand: A[f = 16b + l15][kk = 4q + jj] (bias at kk = taps)
   bf16x4 wc[NFB];
 #pragma unroll
@@ -126,7 +148,8 @@ __global__ __launch_bounds__(512, 1) void cnn_fwd_kernel(
   float bdj[4];
 #pragma unroll
   for (int r = 0; r < 4; ++r) bdj[r] = bd[4 * q + r];
-  const unsigned smix = (TRAIN && drop) ? cnn_seed_mix(seed, rng) : 0u;
+  (void)drop;
+  const unsigned smix = DROP ? cnn_seed_mix(seed, rng) : 0u;
   float lsum = 0.f, dbd[4] = {0.f, 0.f, 0.f, 0.f};
   __syncthreads();
 
@@ -144,17 +167,22 @@ __global__ __launch_bounds__(512, 1) void cnn_fwd_kernel(
       xp[2 * k + 1] = pk_bf16(v.z, v.w);
     }
     f32x4 out = {0.f, 0.f, 0.f, 0.f};
-    // dense-weight fragments of step t, prefetched one step ahead; the scheduling barrier at the
-    // end of every step keeps the unrolled loop from hoisting all 252 LDS reads (404 spilled
-    // VGPRs without it)
-    bf16x4 wfr[NFB];
+    // dense-weight fragments of step t (pairs of 16-filter blocks as 16x16x32 A operands, block
+    // 6 as a 16x16x16 one), prefetched one step ahead; the scheduling barrier at the end of
+    // every step keeps the unrolled loop from hoisting all the LDS reads (spills without it)
+    const char* wdl = smem;
+    bf16x8 wp[3];
+    bf16x4 w6;
 #pragma unroll
-    for (int b = 0; b < NFB; ++b) wfr[b] = wd_lds[b * 64 + lane];
+    for (int p = 0; p < 3; ++p) wp[p] = *reinterpret_cast<const bf16x8*>(wdl + p * 1024 + lane * 16);
+    w6 = *reinterpret_cast<const bf16x4*>(wdl + 3072 + lane * 8);
 #pragma unroll
     for (int t = 0; t < T; ++t) {
-      bf16x4 wnx[NFB];
+      const char* wn = wdl + ((t + 1) % T) * TB;
+      bf16x8 wpn[3];
 #pragma unroll
-      for (int b = 0; b < NFB; ++b) wnx[b] = wd_lds[(((t + 1) % T) * NFB + b) * 64 + lane];
+      for (int p = 0; p < 3; ++p) wpn[p] = *reinterpret_cast<const bf16x8*>(wn + p * 1024 + lane * 16);
+      const bf16x4 w6n = *reinterpret_cast<const bf16x4*>(wn + 3072 + lane * 8);
       // X_t^T fragment: B[kk = 4q + jj][w = l15] = x[w][t + 4q + jj]
       unsigned d0, d1;
       if (t & 1) {
@@ -165,17 +193,29 @@ __global__ __launch_bounds__(512, 1) void cnn_fwd_kernel(
         d1 = xp[t / 2 + 1];
       }
       const bf16x4 xb = ks.apply(d0, d1);
-      const unsigned m = (TRAIN && drop) ? cnn_mask_word(smix, w, t, T, q) : 0xFFFFFFFFu;
+      const unsigned mi = DROP ? ~cnn_mask_word(smix, w, t, T, q) : 0u;
+      // act pairs: rows f = 16b + 4q + {0,1} and {2,3} of each block, bf16, ReLU + dropout
+      unsigned act[NFB][2];
 #pragma unroll
       for (int b = 0; b < NFB; ++b) {
-        const f32x4 p = mfma16(wc[b], xb, f32x4{0.f, 0.f, 0.f, 0.f});  // rows f = 16b + 4q + r
-        float a[4];
+        const f32x4 pv = mfma16(wc[b], xb, f32x4{0.f, 0.f, 0.f, 0.f});  // rows f = 16b + 4q + r
 #pragma unroll
-        for (int r = 0; r < 4; ++r) a[r] = ((m >> (4 * b + r)) & 1u) ? fmaxf(p[r], 0.f) : 0.f;
-        out = mfma16(wfr[b], frag(pk_bf16(a[0], a[1]), pk_bf16(a[2], a[3])), out);
+        for (int h = 0; h < 2; ++h) {
+          unsigned v = pk_bf16(pv[2 * h], pv[2 * h + 1]);
+          if constexpr (DROP) v = drop_pk(v, mi, 2 * b + h);
+          act[b][h] = relu_pk(v);
+        }
       }
+      // out^T[j x w] += Wd_t^T[j x f] act^T[f x w]: blocks (0,1) (2,3) (4,5) on the double-rate
+      // 16x16x32 (k-slots 8q..8q+3 = block 2p, 8q+4..8q+7 = block 2p+1), block 6 on 16x16x16
 #pragma unroll
-      for (int b = 0; b < NFB; ++b) wfr[b] = wnx[b];
+      for (int p = 0; p < 3; ++p)
+        out = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+            wp[p], frag8(act[2 * p][0], act[2 * p][1], act[2 * p + 1][0], act[2 * p + 1][1]), out, 0, 0, 0);
+      out = mfma16(w6, frag(act[6][0], act[6][1]), out);
+#pragma unroll
+      for (int p = 0; p < 3; ++p) wp[p] = wpn[p];
+      w6 = w6n;
       __builtin_amdgcn_sched_barrier(0);
     }
     // lane holds out[j = 4q + r][w = l15]
@@ -237,7 +277,7 @@ __global__ __launch_bounds__(512, 1) void cnn_fwd_kernel(
 }
 
 // ------------------------------------------------------------------------------ backward
-template <int NFB, int TG>
+template <int NFB, int TG, bool DROP>
 __global__ __launch_bounds__(512, 1) void cnn_bwd_kernel(
     const float* __restrict__ x, int B, int L, const bf16_t* __restrict__ WcA, int Kc,
     const bf16x4* __restrict__ WdB, const float* __restrict__ dout, int T, int taps, float keep_scale, int drop,
@@ -246,7 +286,8 @@ __global__ __launch_bounds__(512, 1) void cnn_bwd_kernel(
   __shared__ __attribute__((aligned(16))) f32x4 red[CNN_NW * TG * NFB * 64];
   const int lane = threadIdx.x & 63, l15 = lane & 15, q = lane >> 4;
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  if (prio && wid >= 4) __builtin_amdgcn_s_setprio(1);  // static priority, younger half (A/B)
+  (void)prio;
+  (void)drop;
   const int ntg = (T + TG - 1) / TG;
   // logical block: consecutive ids (one XCD under the round-robin deal) share a window chunk
   const int lb = xcd_remap(blockIdx.x, gridDim.x);
@@ -270,8 +311,9 @@ __global__ __launch_bounds__(512, 1) void cnn_bwd_kernel(
   // the dWc B operand's row kk = l15: x for kk < taps, the constant 1 at kk = taps, else 0
   const bool kx = l15 < taps;
   const float kone = l15 == taps ? 1.f : 0.f;
-  const unsigned smix = drop ? cnn_seed_mix(seed, rng) : 0u;
-  const int hq = l15 >> 2, hbit = l15 & 3;  // dropout hash key / bit of this lane's filter column
+  const unsigned smix = DROP ? cnn_seed_mix(seed, rng) : 0u;
+  // dropout hash key of this lane's filter column f = 16b + l15 and its bit: 2b + hb0
+  const int hq = l15 >> 2, hb0 = ((l15 & 3) >> 1) + 16 * (l15 & 1);
 
   f32x4 acc_wd[TG][NFB], acc_wc[NFB];
 #pragma unroll
@@ -292,12 +334,15 @@ __global__ __launch_bounds__(512, 1) void cnn_bwd_kernel(
     for (int jj = 0; jj < 4; ++jj) dbv[jj] = dout[(size_t)(w0 + 4 * q + jj) * 16 + l15] * keep_scale;
     const bf16x4 doB = frag(pk_bf16(dbv[0], dbv[1]), pk_bf16(dbv[2], dbv[3]));
     // x of this lane's window for the A operand: x[w0 + l15][t0 + 4q + i], i < TG + 3
-    const int wa = w0 + l15;
+    // (branch-free: every load reads a clamped, in-range address and a select applies the
+    // bounds, instead of an exec-masked branch around each load)
+    const int wa = w0 + l15, wac = min(wa, B - 1);
     float xa[TG + 3];
 #pragma unroll
     for (int i = 0; i < TG + 3; ++i) {
       const int s = t0 + 4 * q + i;
-      xa[i] = (wa < B && s < L) ? x[(size_t)wa * L + s] : 0.f;
+      const float v = x[(size_t)wac * L + min(s, L - 1)];
+      xa[i] = (wa < B && s < L) ? v : 0.f;
     }
     // x of the four windows w0 + 4q + jj at sample t + l15 for the dWc B operand
     float xb[TG][4];
@@ -306,7 +351,8 @@ __global__ __launch_bounds__(512, 1) void cnn_bwd_kernel(
 #pragma unroll
       for (int jj = 0; jj < 4; ++jj) {
         const int wb = w0 + 4 * q + jj, s = t0 + tt + l15;
-        xb[tt][jj] = (kx && wb < B && s < L) ? x[(size_t)wb * L + s] : kone;
+        const float v = x[(size_t)min(wb, B - 1) * L + min(s, L - 1)];
+        xb[tt][jj] = (kx && wb < B && s < L) ? v : kone;
       }
 #pragma unroll
     for (int tt = 0; tt < TG; ++tt) {
@@ -314,23 +360,38 @@ __global__ __launch_bounds__(512, 1) void cnn_bwd_kernel(
       if (t >= T) break;
       const bf16x4 xA = ks.apply(pk_bf16(xa[tt], xa[tt + 1]), pk_bf16(xa[tt + 2], xa[tt + 3]));
       const bf16x4 xB = frag(pk_bf16(xb[tt][0], xb[tt][1]), pk_bf16(xb[tt][2], xb[tt][3]));
-      unsigned m[4];
+      // dropout: the lane holds windows 4q + r of filter column 16b + l15, keep bit 2b + hb0 of
+      // window r's hash word. The inverted words of windows (0, 1) and (2, 3) are packed so the
+      // bit of block b sits at 2b (first window) and 2b + 16 (second): one shift per block puts
+      // both into a packed pair's sign bits (drop_pk), as in the forward
+      unsigned pm[2] = {0u, 0u};
+      if constexpr (DROP) {
+        unsigned mi[4];
 #pragma unroll
-      for (int r = 0; r < 4; ++r) m[r] = drop ? cnn_mask_word(smix, w0 + 4 * q + r, t, T, hq) : 0xFFFFFFFFu;
+        for (int r = 0; r < 4; ++r) mi[r] = ~cnn_mask_word(smix, w0 + 4 * q + r, t, T, hq) >> hb0;
+#pragma unroll
+        for (int h = 0; h < 2; ++h) pm[h] = (mi[2 * h] & 0xFFFFu) | (mi[2 * h + 1] << 16);
+      }
 #pragma unroll
       for (int b = 0; b < NFB; ++b) {
         const f32x4 p = mfma16(xA, wc[b], f32x4{0.f, 0.f, 0.f, 0.f});       // [w = 4q + r][f = 16b + l15]
         const f32x4 dA = mfma16(doA, wdb[tt][b], f32x4{0.f, 0.f, 0.f, 0.f});  // same layout
-        float a[4], dp[4];
+        // act = ReLU + dropout on packed pairs; dP = dAct where act != 0 (kept and p > 0): the
+        // packed bf16 dAct times min(act, 1) as int16 lanes (x 1 keeps the bits, x 0 clears)
+        unsigned a[2], dp[2];
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const bool keep = ((m[r] >> (4 * b + hbit)) & 1u) && p[r] > 0.f;
-          a[r] = keep ? p[r] : 0.f;
-          dp[r] = keep ? dA[r] : 0.f;
+        for (int h = 0; h < 2; ++h) {
+          unsigned v = pk_bf16(p[2 * h], p[2 * h + 1]);
+          if constexpr (DROP) v = drop_pk(v, pm[h], 2 * b);
+          a[h] = relu_pk(v);
+          // (inline asm: the compiler rewrote the min / multiply into 6 compares and selects)
+          unsigned one, d = pk_bf16(dA[2 * h], dA[2 * h + 1]);
+          asm("v_pk_min_u16 %0, %1, %2" : "=v"(one) : "v"(a[h]), "s"(0x00010001u));
+          asm("v_pk_mul_lo_u16 %0, %1, %2" : "=v"(dp[h]) : "v"(d), "v"(one));
         }
         // act^T and dP^T as A operands: A[f = l15][w = 4q + jj]
-        acc_wd[tt][b] = mfma16(frag(pk_bf16(a[0], a[1]), pk_bf16(a[2], a[3])), doB, acc_wd[tt][b]);
-        acc_wc[b] = mfma16(frag(pk_bf16(dp[0], dp[1]), pk_bf16(dp[2], dp[3])), xB, acc_wc[b]);
+        acc_wd[tt][b] = mfma16(frag(a[0], a[1]), doB, acc_wd[tt][b]);
+        acc_wc[b] = mfma16(frag(dp[0], dp[1]), xB, acc_wc[b]);
       }
     }
   }
@@ -458,12 +519,16 @@ __global__ __launch_bounds__(256) void cnn_pack_kernel(const float* __restrict__
   const int nfr = T * NFB * 64;
   const long nf = (long)T * Fp;
   if (i < nfr) {
+    // WdB (8-B unit i): [T][NFB][64 lanes][4]; WdF: per step 3 block pairs of [64 lanes][8]
+    // (block 2p in the lane's first 8 B, 2p+1 in the next) then block 6 [64 lanes][4]
     const int lane = i & 63, tb = i >> 6, t = tb / NFB, b = tb % NFB;
     const int l15 = lane & 15, q = lane >> 4;
+    const int e = i % (NFB * 64);  // 8-B unit within step t of the WdF image
+    const int bf = e < 384 ? 2 * (e / 128) + (e & 1) : 6, lf = e < 384 ? (e % 128) >> 1 : e - 384;
     unsigned short vf[4], vb[4];
 #pragma unroll
     for (int jj = 0; jj < 4; ++jj) {
-      const int j = l15, f = 16 * b + 4 * q + jj;
+      const int j = lf & 15, f = 16 * bf + 4 * (lf >> 4) + jj;
       vf[jj] = j < O ? f2bf(Wd[(long)j * nf + (long)t * Fp + f]) : 0;
       const int j2 = 4 * q + jj, f2 = 16 * b + l15;
       vb[jj] = j2 < O ? f2bf(Wd[(long)j2 * nf + (long)t * Fp + f2]) : 0;
@@ -508,29 +573,24 @@ void launch_cnn_pack(const float* Wc, const float* Wd, const CnnDims& d, bf16_t*
                      d.O, WcA, WdF, WdB);
 }
 
-// WELLFLOW_CNN_PRIO=0/1: static s_setprio 1 for waves 4-7 of the forward / backward kernels
-static int cnn_prio() {
-  static const int p = [] {
-    const char* v = std::getenv("WELLFLOW_CNN_PRIO");
-    return v == nullptr ? 0 : std::atoi(v);
-  }();
-  return p;
-}
-
 void launch_cnn_forward(const float* x, int B, const CnnDims& d, const bf16_t* WcA, const bf16_t* WdF,
                         const float* bd, const float* y, float* dout, float* pred, float* part, int train,
                         int loss_kind, float clip, float scale, unsigned seed, const long long* rng, hipStream_t s) {
   const int grid = cnn_fwd_grid(B);
   const int drop = (train && d.drop_p > 0.f) ? 1 : 0;
   const float keep_scale = drop ? 1.f / (1.f - d.drop_p) : 1.f;
-  if (train)
-    hipLaunchKernelGGL((cnn_fwd_kernel<CNN_NFB, CNN_T, true>), dim3(grid), dim3(512), 0, s, x, B, d.L, WcA, d.Kc,
-                       reinterpret_cast<const bf16x4*>(WdF), bd, d.O, y, dout, pred, part, d.taps, loss_kind, clip,
-                       scale, keep_scale, drop, seed, rng, cnn_prio());
+  if (train && drop)
+    hipLaunchKernelGGL((cnn_fwd_kernel<CNN_NFB, CNN_T, true, true>), dim3(grid), dim3(512), 0, s, x, B, d.L, WcA,
+                       d.Kc, reinterpret_cast<const bf16x4*>(WdF), bd, d.O, y, dout, pred, part, d.taps, loss_kind,
+                       clip, scale, keep_scale, drop, seed, rng, 0);
+  else if (train)
+    hipLaunchKernelGGL((cnn_fwd_kernel<CNN_NFB, CNN_T, true, false>), dim3(grid), dim3(512), 0, s, x, B, d.L, WcA,
+                       d.Kc, reinterpret_cast<const bf16x4*>(WdF), bd, d.O, y, dout, pred, part, d.taps, loss_kind,
+                       clip, scale, keep_scale, 0, seed, rng, 0);
   else
-    hipLaunchKernelGGL((cnn_fwd_kernel<CNN_NFB, CNN_T, false>), dim3(grid), dim3(512), 0, s, x, B, d.L, WcA, d.Kc,
-                       reinterpret_cast<const bf16x4*>(WdF), bd, d.O, y, dout, pred, part, d.taps, loss_kind, clip,
-                       scale, keep_scale, 0, seed, rng, cnn_prio());
+    hipLaunchKernelGGL((cnn_fwd_kernel<CNN_NFB, CNN_T, false, false>), dim3(grid), dim3(512), 0, s, x, B, d.L, WcA,
+                       d.Kc, reinterpret_cast<const bf16x4*>(WdF), bd, d.O, y, dout, pred, part, d.taps, loss_kind,
+                       clip, scale, keep_scale, 0, seed, rng, 0);
 }
 
 void launch_cnn_backward(const float* x, int B, const CnnDims& d, const bf16_t* WcA, const bf16_t* WdB,
@@ -540,9 +600,14 @@ void launch_cnn_backward(const float* x, int B, const CnnDims& d, const bf16_t* 
   const int nch = cnn_bwd_chunks(B);
   const int drop = d.drop_p > 0.f ? 1 : 0;
   const float keep_scale = drop ? 1.f / (1.f - d.drop_p) : 1.f;
-  hipLaunchKernelGGL((cnn_bwd_kernel<CNN_NFB, CNN_TG>), dim3(ntg * nch), dim3(512), 0, s, x, B, d.L, WcA, d.Kc,
-                     reinterpret_cast<const bf16x4*>(WdB), dout, d.T, d.taps, keep_scale, drop, seed, rng, nch,
-                     part_wd, part_wc, cnn_prio());
+  if (drop)
+    hipLaunchKernelGGL((cnn_bwd_kernel<CNN_NFB, CNN_TG, true>), dim3(ntg * nch), dim3(512), 0, s, x, B, d.L, WcA,
+                       d.Kc, reinterpret_cast<const bf16x4*>(WdB), dout, d.T, d.taps, keep_scale, drop, seed, rng, nch,
+                       part_wd, part_wc, 0);
+  else
+    hipLaunchKernelGGL((cnn_bwd_kernel<CNN_NFB, CNN_TG, false>), dim3(ntg * nch), dim3(512), 0, s, x, B, d.L, WcA,
+                       d.Kc, reinterpret_cast<const bf16x4*>(WdB), dout, d.T, d.taps, keep_scale, drop, seed, rng, nch,
+                       part_wd, part_wc, 0);
 }
 
 void launch_cnn_reduce(const float* part_wd, const float* part_wc, const float* part_f, int B, const CnnDims& d,

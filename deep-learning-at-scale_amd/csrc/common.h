@@ -11,6 +11,8 @@
 #include <hip/hip_bf16.h>
 #include <stdint.h>
 
+#include <cstdlib>
+
 namespace wf {
 
 typedef unsigned short bf16_t;
@@ -19,6 +21,20 @@ typedef short bf16x4 __attribute__((ext_vector_type(4)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int kWave = 64;
+
+// Environment overrides of A/B variants and tuning sweeps: only WF_DIAG builds
+// (WELLFLOW_DIAG_BUILD=1) read them; a production build compiles every such read to its
+// default, so the set of WELLFLOW_* variables a production _C.so reads is exactly the
+// documented list (README "Environment knobs", tests/test_diag_cpu.py).
+inline int diag_env_int(const char* name, int dflt) {
+#ifdef WF_DIAG
+  const char* v = std::getenv(name);
+  return v != nullptr ? std::atoi(v) : dflt;
+#else
+  (void)name;
+  return dflt;
+#endif
+}
 
 __device__ __forceinline__ float bf2f(bf16_t x) {
   return __uint_as_float(static_cast<unsigned>(x) << 16);

@@ -79,11 +79,7 @@ void launch_head_fwd(const bf16_t* Hm, long ldh, int B, int Hd, const float* w, 
   // one same-address loss atomic per block: cap the grid. LSTM head (B = 8192, Hd = 512,
   // kernel trace, tools/gpu.sh ksweep WELLFLOW_HEAD_GRID): 30.8 us at 2048 blocks, 18.3 at 1024, 13.4 at 512,
   // 14.0 at 256 — the atomics serialise, not the loads (WELLFLOW_HEAD_GRID overrides)
-  static const int cap = [] {
-    const char* e = std::getenv("WELLFLOW_HEAD_GRID");
-    const int v = e != nullptr ? std::atoi(e) : 0;
-    return v > 0 ? v : 512;
-  }();
+  static const int cap = std::max(1, diag_env_int("WELLFLOW_HEAD_GRID", 512));  // sweep: WF_DIAG builds only
   if (grid > cap) grid = cap;
 #define HEAD_FWD(L)                                                                              \
   hipLaunchKernelGGL(head_fwd_kernel<L>, dim3(grid), dim3(256), 0, s, Hm, ldh, B, Hd, w, b0, target, \
@@ -262,11 +258,7 @@ void launch_head_bwd_w(const bf16_t* Hm, long ldh, int B, int Hd, const float* d
   // per-column atomics per block: cap the grid. LSTM head (B = 8192, Hd = 512, kernel trace,
   // tools/gpu.sh ksweep WELLFLOW_HEADW_GRID): 16.2 us at 512 blocks, 11.0 at 256, 10.3 at 128, 13.6 at 64
   // (WELLFLOW_HEADW_GRID overrides)
-  static const int cap = [] {
-    const char* e = std::getenv("WELLFLOW_HEADW_GRID");
-    const int v = e != nullptr ? std::atoi(e) : 0;
-    return v > 0 ? v : 128;
-  }();
+  static const int cap = std::max(1, diag_env_int("WELLFLOW_HEADW_GRID", 128));  // sweep: WF_DIAG builds only
   if (grid > cap) grid = cap;
   hipLaunchKernelGGL(head_bwd_w_kernel, dim3(grid), dim3(256), 0, s, Hm, ldh, B, Hd, dy, dw, db, g);
 }
@@ -488,10 +480,7 @@ void launch_adam_dev(float* p, float* g, float* m, float* v, long n, float* step
                      hipStream_t s) {
   // every workgroup draws a ticket from ONE counter (step[1]) and same-address atomics serialise:
   // at most WELLFLOW_ADAM_GRID (default 256) workgroups, grid-stride over the rest
-  static const int cap = [] {
-    const char* e = std::getenv("WELLFLOW_ADAM_GRID");
-    return e == nullptr ? 256 : std::max(1, std::atoi(e));
-  }();
+  static const int cap = std::max(1, diag_env_int("WELLFLOW_ADAM_GRID", 256));  // sweep: WF_DIAG builds only
   int blocks = ew_blocks(n);
   if (blocks > cap) blocks = cap;
   hipLaunchKernelGGL(adam_dev_kernel, dim3(blocks), dim3(256), 0, s, p, g, m, v, n, step, lr,

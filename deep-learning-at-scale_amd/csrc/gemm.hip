@@ -237,10 +237,7 @@ static void launch_dw_192(const bf16_t* A, long lda, const bf16_t* B, long ldb, 
   // s_setprio(1) around each MFMA cluster (cdna_hip_programming.md §5.5 T5: hipcc then keeps
   // the clusters between the barriers): 1.24 -> 1.16 ms at B = 8192 (WELLFLOW_DW_PRIO=0/2: off /
   // static priority for waves 4-7, no gain)
-  static const int prio = [] {
-    const char* v = std::getenv("WELLFLOW_DW_PRIO");
-    return v == nullptr ? 1 : std::atoi(v);
-  }();
+  constexpr int prio = 1;  // WELLFLOW_DW_PRIO=0/2 measured no gain (round 2): knob removed in round 5
   if (prio == 1)
     hipLaunchKernelGGL((gemm_dw_kernel<BM, BN, 2, 4, 2, 1>), dim3(tiles * nsplit), dim3(512), 0, s, A, lda, B, ldb,
                        N, kchunk, tiles, e.outF, e.ldo, e.alpha);
@@ -379,11 +376,9 @@ static void launch_dw_288w(const bf16_t* A, long lda, const bf16_t* B, long ldb,
   // atomics at the tail of the kernel) or, given a slab, plain stores + one reduce
   const long mn = (long)M * N;
   const bool use_slab = e.slab != nullptr && e.ldo == N && nsplit > 1 && (long)nsplit * mn <= e.slab_cap && mn % 4 == 0;
-  // WELLFLOW_DW288_PRIO: 1 = s_setprio 1 around each MFMA cluster, 3 = static priority for waves 4-7
-  static const int prio = [] {
-    const char* v = std::getenv("WELLFLOW_DW288_PRIO");
-    return v == nullptr ? 1 : std::atoi(v);
-  }();
+  // s_setprio 1 around each MFMA cluster (static priority for waves 4-7 measured slower, r4/lstm_dw_prio;
+  // the WELLFLOW_DW288_PRIO knob was removed in round 5)
+  constexpr int prio = 1;
   if (prio == 3)
     hipLaunchKernelGGL((gemm_dw_h_kernel<BM, BN, 4, 4, 2, 3, 32>), dim3(tiles * nsplit), dim3(512), 0, s, A, lda, B,
                        ldb, N, kchunk, tiles, e.outF, e.ldo, e.alpha, use_slab ? e.slab : nullptr, use_slab ? mn : 0L);

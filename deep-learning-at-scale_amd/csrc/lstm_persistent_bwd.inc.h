@@ -109,11 +109,14 @@ __global__ __launch_bounds__(256, 1) void lstm_bwd_persistent_kernel(
   static_assert(NG == 1 || (GS >= 2 && NRT - GS - 4 >= 0), "a group must publish before its next poll");
   constexpr int WSLOT = 16 * KT * 64;    // bytes of one wave's A tile: 16 rows x H k (bf16)
   constexpr int RING = 4 * 2 * WSLOT;    // [wave][2 slots]
-  constexpr int RED = RING;              // partial sums [parity][src wave][unit tile][lane] x 16 B
-  // slots [p][w][w] of RED are never written (a wave's own unit tile stays in registers):
-  // [0][0][0] holds the epoch / started ordinal broadcast, [0][1][1] the per-wave failed words
+  // partial sums [parity][src wave][rotation slot j][lane] x 16 B: wave w multiplies unit tile
+  // (w + j) & 3 into acc[j], so its own tile is always acc[0] (no per-wave select) and slot j
+  // of wave w holds unit tile (w + j) & 3 for the wave that owns it
+  constexpr int RED = RING;
+  // slots [p][w][0] of RED are never written (the own tile stays in registers): [0][0][0]
+  // holds the epoch / started ordinal broadcast, [0][1][0] the per-wave failed words
   constexpr int BCAST = RED + (0 * 16 + 0 * 4 + 0) * 1024;
-  constexpr int FAILW = RED + (0 * 16 + 1 * 4 + 1) * 1024;
+  constexpr int FAILW = RED + (0 * 16 + 1 * 4 + 0) * 1024;
   // ONE static LDS object (see lstm_persistent.hip: with several, the waitcnt pass guards LDS
   // accesses behind the LDS-DMA with vmcnt(0)); LDS writes go through inline asm.
   __shared__ __attribute__((aligned(16))) char smem[RED + 2 * 16 * 1024];
@@ -154,7 +157,7 @@ __global__ __launch_bounds__(256, 1) void lstm_bwd_persistent_kernel(
   bf16x8 w[KT][4];
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
-    const bf16_t* wr = WhhT + (size_t)(n * 64 + j * 16 + l15) * G + wid * H + 8 * g;
+    const bf16_t* wr = WhhT + (size_t)(n * 64 + ((wid + j) & 3) * 16 + l15) * G + wid * H + 8 * g;
 #pragma unroll
     for (int kt = 0; kt < KT; ++kt) w[kt][j] = *reinterpret_cast<const bf16x8*>(wr + 32 * kt);
   }
@@ -293,7 +296,12 @@ __global__ __launch_bounds__(256, 1) void lstm_bwd_persistent_kernel(
 
   // dh partial of the previous tile, own unit tile (the other three go through LDS)
   f32x4 dho = f32x4{0.f, 0.f, 0.f, 0.f};
-  const unsigned rd_base = lds0 + RED + wid * 1024 + lane * 16;  // red[.][.][wid][lane]
+  // where the other waves' partials of this wave's unit tile sit: slot j of wave (wid - j) & 3
+  // (+ parity * 16 KB as an immediate)
+  unsigned rdj[4];
+#pragma unroll
+  for (int j = 1; j < 4; ++j) rdj[j] = lds0 + RED + ((wid - j) & 3) * 4096 + j * 1024 + lane * 16;
+  const unsigned wr_base = lds0 + RED + wid * 4096 + lane * 16;  // red[.][wid][.][lane]
 
   for (int s = 0; s < d.T - 1; ++s) {
     const int t = d.T - 2 - s;
@@ -512,8 +520,8 @@ __global__ __launch_bounds__(256, 1) void lstm_bwd_persistent_kernel(
         if constexpr (RT > 0 && kt == KSUM) {
           // the wait above drained the partial reads issued at k-tile 0 (LDS returns in order:
           // only the fragment reads after them are younger): tie them to it, then the previous tile's dh
-          asm volatile("" : "+v"(pr[0]), "+v"(pr[1]), "+v"(pr[2]), "+v"(pr[3]));
-          dhp = dho + ((pr[0] + pr[1]) + (pr[2] + pr[3]));
+          asm volatile("" : "+v"(pr[1]), "+v"(pr[2]), "+v"(pr[3]));
+          dhp = dho + ((pr[1] + pr[2]) + pr[3]);
         }
         static_for<0, 4>([&](auto jc) {
           constexpr int j = decltype(jc)::value;
@@ -585,15 +593,12 @@ __global__ __launch_bounds__(256, 1) void lstm_bwd_persistent_kernel(
               }
             }
           });
-          static_for<0, 4>([&](auto wc) {
-            constexpr int w2 = decltype(wc)::value;
+          static_for<1, 4>([&](auto jc) {
+            constexpr int j = decltype(jc)::value;
             (void)pr;
-            (void)rd_base;
-            if (w2 != wid)
-              asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(pr[w2]) : "v"(rd_base),
-                           "i"((((RT - 1) & 1) * 4 + w2) * 4 * 1024) : "memory");
-            else
-              pr[w2] = f32x4{0.f, 0.f, 0.f, 0.f};
+            (void)rdj;
+            asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(pr[j]) : "v"(rdj[j]), "i"(((RT - 1) & 1) * 16384)
+                         : "memory");
           });
         }
         // the MFMAs above are inline asm, so the compiler knows neither their latency nor that
@@ -610,23 +615,21 @@ __global__ __launch_bounds__(256, 1) void lstm_bwd_persistent_kernel(
         stamp(s, 3 + 5 * RT);
       }
 
-      // ---- K-split partials -> red[P] (the own unit tile stays in registers: dho)
-      dho = wid == 0 ? acc[0] : wid == 1 ? acc[1] : wid == 2 ? acc[2] : acc[3];
-      const unsigned rbase = lds0 + RED + (P * 4 + wid) * 4 * 1024 + lane * 16;  // red[P][wid][.][lane]
+      // ---- K-split partials -> red[P][wid][1..3] (the own unit tile stays in registers: dho)
+      dho = acc[0];
 #pragma unroll
-      for (int j = 0; j < 4; ++j)
-        if (j != wid) asm volatile("ds_write_b128 %0, %1 offset:%2" ::"v"(rbase), "v"(acc[j]), "i"(j * 1024) : "memory");
+      for (int j = 1; j < 4; ++j)
+        asm volatile("ds_write_b128 %0, %1 offset:%2" ::"v"(wr_base), "v"(acc[j]), "i"(P * 16384 + j * 1024) : "memory");
       __builtin_amdgcn_sched_barrier(0);
       stamp(s, 4 + 5 * RT);
       if constexpr (RT + 1 == NRT) {  // last tile: exchange now, drain its cell backward
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();
-        static_for<0, 4>([&](auto wc) {
-          constexpr int w2 = decltype(wc)::value;
+        static_for<1, 4>([&](auto jc) {
+          constexpr int j = decltype(jc)::value;
           (void)acc;
-          (void)rd_base;
-          if (w2 != wid)
-            asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(acc[w2]) : "v"(rd_base), "i"((P * 4 + w2) * 4 * 1024) : "memory");
+          (void)rdj;
+          asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(acc[j]) : "v"(rdj[j]), "i"(P * 16384) : "memory");
         });
         // the wait takes the accumulators as operands: the compiler sees inline-asm outputs as
         // ready at once and would otherwise schedule the sum between the reads and the wait

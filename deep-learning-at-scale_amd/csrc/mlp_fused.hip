@@ -31,10 +31,7 @@ namespace {
 // WELLFLOW_MLP_PRIO bit mask: s_setprio(1) around the MFMA clusters of 1 forward, 2 backward,
 // 4 dW2 (8-wave kernels)
 int mlp_prio() {
-  static const int p = [] {
-    const char* e = std::getenv("WELLFLOW_MLP_PRIO");
-    return e == nullptr ? 0 : std::atoi(e);
-  }();
+  static const int p = diag_env_int("WELLFLOW_MLP_PRIO", 0);  // A/B, WF_DIAG builds only
   return p;
 }
 // WELLFLOW_MLP_DBG: timing-only switches of the 8-wave forward / backward (results are wrong).
@@ -146,10 +143,7 @@ __global__ __launch_bounds__(256) void mlp2_reduce_kernel(float* __restrict__ re
 }
 
 bool mlp_bwd8() {
-  static const bool v = [] {
-    const char* e = std::getenv("WELLFLOW_MLP_BWD8");
-    return e == nullptr || e[0] != '0';
-  }();
+  static const bool v = diag_env_int("WELLFLOW_MLP_BWD8", 1) != 0;  // A/B, WF_DIAG builds only
   return v;
 }
 
@@ -1673,10 +1667,7 @@ bool launch_mlp2_dw2(const bf16_t* dZ2, const bf16_t* X, int Fp, const long long
   while (nsplit > 1 && chunks % nsplit != 0) --nsplit;
   const int kchunk = (chunks / nsplit) * MF_ROWS;
   if (rows != nullptr && kchunk > DW2_MAX_ROWS) return false;
-  static const bool dw2_8 = [] {
-    const char* e = std::getenv("WELLFLOW_MLP_DW2_8");
-    return e == nullptr || e[0] != '0';
-  }();
+  static const bool dw2_8 = diag_env_int("WELLFLOW_MLP_DW2_8", 1) != 0;  // A/B, WF_DIAG builds only
   if (dw2_8 && (mlp_prio() & 4))
     hipLaunchKernelGGL((mlp2_dw2_kernel<8, 1>), dim3(4 * nsplit), dim3(512), 0, s, dZ2, X, Fp, rows, nrows, W1, b1, kchunk,
                        dW2, red, mlp_dbg());
@@ -1745,10 +1736,7 @@ bool launch_mlp2_fwd(const bf16_t* X, int Fp, const bf16_t* W1, const float* b1,
       hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
     cus = 256;
   const int grid = nchunks < cus ? nchunks : cus;
-  static const bool fwd8 = [] {
-    const char* e = std::getenv("WELLFLOW_MLP_FWD8");
-    return e == nullptr || e[0] != '0';
-  }();
+  static const bool fwd8 = diag_env_int("WELLFLOW_MLP_FWD8", 1) != 0;  // A/B, WF_DIAG builds only
   if (fwd8 && M2 != nullptr && H1 == nullptr) {  // the training step (mask mode never writes H2)
     if (Fp <= 32 && (mlp_prio() & 1))
       hipLaunchKernelGGL((mlp2_fwd_train_kernel<1, 1>), dim3(grid), dim3(512), 0, s, X, Fp, W1, b1, W2, b2, w3, b3, y,

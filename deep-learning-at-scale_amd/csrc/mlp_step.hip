@@ -656,13 +656,10 @@ bool launch_mlp2_step(const bf16_t* X, int Fp, const bf16_t* W1, const float* b1
   const int grid = mlp2_train_grid(B);  // the dW1 rows mlp2_reduce sums
   // phase stamps (tools/mlp_timeline.py; results unchanged, so not a WF_DIAG-only switch):
   // into dW2 slab rows 200.. of the scratch (unused by a step of <= 200 dW2 ranges)
-  static const bool stamp = std::getenv("WELLFLOW_MLP_STAMP") != nullptr;
-  // WELLFLOW_STEP_PRIO=0/1: static s_setprio 1 for waves 4-7 off / on (default on: +0.2 to +1.1 %
-  // in three interleaved pairs, chunk span 17.5k -> 17.1k cycles, profiles/r4/mlp_prio)
-  static const int prio = [] {
-    const char* v = std::getenv("WELLFLOW_STEP_PRIO");
-    return v == nullptr ? 1 : std::atoi(v);
-  }();
+  static const bool stamp = diag_env_int("WELLFLOW_MLP_STAMP", 0) != 0;  // WF_DIAG builds only
+  // static s_setprio 1 for waves 4-7 (+0.2 to +1.1 % in three interleaved pairs, chunk span
+  // 17.5k -> 17.1k cycles, profiles/r4/mlp_prio; the WELLFLOW_STEP_PRIO A/B knob was removed)
+  constexpr int prio = 1;
   if (stamp && Fp <= 16 && dz_frag) {
     hipLaunchKernelGGL((mlp2_step_kernel<1, true, true>), dim3(grid), dim3(512), 0, s, X, Fp, W1, b1, W2, b2, w3, b3, y,
                        dy_scale, B, rows, nrows, dZ2, pred, red, prio,
@@ -689,17 +686,11 @@ int launch_mlp2_dw2f(const bf16_t* dZ2F, const bf16_t* X, int Fp, const long lon
                      const float* b1, int B, int nsplit, float* red, hipStream_t s) {
   if (B <= 0 || B % MF_ROWS != 0 || Fp > 32 || Fp % 8 != 0 || red == nullptr) return 0;
   constexpr int kMaxBlock = 128 * DW2F_MAX_ROWS;  // rows per launch
-  // WELLFLOW_DW2F_PRIO=0/1: static s_setprio 1 for waves 4-7 off / on (default on: 48.2 -> 47.0 us,
-  // +0.3 to +0.6 % in three interleaved pairs, profiles/r4/mlp_prio)
-  static const int prio = [] {
-    const char* v = std::getenv("WELLFLOW_DW2F_PRIO");
-    return v == nullptr ? 1 : std::atoi(v);
-  }();
-  // WELLFLOW_DW2F_PF=0/1: per-step fragment reads / reads a half-chunk ahead
-  static const bool pf = [] {
-    const char* v = std::getenv("WELLFLOW_DW2F_PF");
-    return v == nullptr ? true : std::atoi(v) != 0;
-  }();
+  // static s_setprio 1 for waves 4-7 (48.2 -> 47.0 us, +0.3 to +0.6 % in three interleaved pairs,
+  // profiles/r4/mlp_prio; the WELLFLOW_DW2F_PRIO A/B knob was removed)
+  constexpr int prio = 1;
+  // fragment reads a half-chunk ahead (+0.5 %, profiles/r4/mlp_dw2f_pf; knob removed)
+  constexpr bool pf = true;
   int srow = 0;  // slab rows used so far (the launches' ranges stack)
   for (int r0 = 0; r0 < B; r0 += kMaxBlock) {
     const int Bb = B - r0 < kMaxBlock ? B - r0 : kMaxBlock;

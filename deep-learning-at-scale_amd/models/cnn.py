@@ -55,7 +55,8 @@ def _lowbias32(x: torch.Tensor) -> torch.Tensor:
 
 def cnn_dropout_mask(seed: int, step: int, B: int, T: int, Fp: int, device="cpu") -> torch.Tensor:
     """Keep mask [B, T, Fp] (bool) of the fused CNN kernels' dropout at p = 0.5, bit for bit:
-    bit 4*(f >> 4) + (f & 3) of lowbias32(((w*T + t)*4 + ((f >> 2) & 3)) ^ smix), smix =
+    bit 2*(f >> 4) + ((f & 3) >> 1) + 16*(f & 1) of lowbias32(((w*T + t)*4 + ((f >> 2) & 3)) ^
+    smix) (the two bits of a packed bf16 pair 16 apart: csrc/cnn_fused.hip), smix =
     lowbias32(seed ^ lowbias32(step + 0x9E3779B9)); ``step`` is the device step counter the
     forward and backward of one training step read (NativeCNN.rng)."""
     seed_t = torch.tensor(seed & _M32, dtype=torch.int64)
@@ -65,7 +66,7 @@ def cnn_dropout_mask(seed: int, step: int, B: int, T: int, Fp: int, device="cpu"
     f = torch.arange(Fp, dtype=torch.int64, device=device).view(1, 1, Fp)
     idx = (((w * T + t) & _M32) * 4 + ((f >> 2) & 3)) & _M32
     h = _lowbias32(idx ^ smix.to(device))
-    bit = 4 * (f >> 4) + (f & 3)
+    bit = 2 * (f >> 4) + ((f & 3) >> 1) + 16 * (f & 1)
     return ((h >> bit) & 1).bool()
 
 
