@@ -1,5 +1,8 @@
 """Per-row-tile timeline of the persistent backward (diagnostic build WELLFLOW_PF_DBG=32):
-s_memrealtime stamps (100 MHz) of step 10, wave 0 of every workgroup, averaged."""
+s_memrealtime stamps (100 MHz) of step 10, wave 0 of every workgroup, averaged.
+Slots (csrc/lstm_persistent_bwd.inc.h): 0 step top, 1 slow-path wait entered (a group's poll
+missed; absent when every poll matched), 2 + 5 RT + {0 A(RT) landed, 1 MFMAs done, 2 partials
+written, 3 (last tile) partials summed, 4 tile end}."""
 import os
 import sys
 
@@ -22,17 +25,21 @@ args = (eng.WhhT, eng.XH, eng.Cst, eng.S, eng.DG, eng.dcarry, eng.dy, w_out, *di
 sync = torch.zeros(4096 + 2 * 128 * 256 + 64, dtype=torch.int32, device="cuda")  # + the STAT block
 os.environ["WELLFLOW_PF_DBG"] = sys.argv[1] if len(sys.argv) > 1 else "32"
 for _ in range(3):
+    sync[4096:-64].zero_()
     C.lstm_backward(*args, 8, sync)
 torch.cuda.synchronize()
-st = sync[4096:-64].view(torch.int64).view(256, 128).cpu().numpy().astype(np.float64) * 10.0  # ns
+raw = sync[4096:-64].view(torch.int64).view(256, 128).cpu().numpy().astype(np.float64)
+st = np.where(raw > 0, raw * 10.0, np.nan)  # ns; unset slots -> NaN
 rel = (st - st[:, 0:1]) / 1000.0  # us from step start
 print("step 10, us since step start (mean / max over 256 workgroups)")
-print(f"{'handoff_done':16s} {rel[:, 1].mean():8.2f} {rel[:, 1].max():8.2f}")
+slow = np.isfinite(rel[:, 1]).sum()
+print(f"slow-path waits at step 10: {slow} of 256 workgroups")
 t5 = rel[:, 2:2 + 5 * NRT].reshape(256, NRT, 5)
-for k, nm in enumerate(("a_ready", "mfma_done", "barrier_done", "epi_start", "stored")):
-    print(f"tile0 {nm:12s} {t5[:, 0, k].mean():8.2f}   tile15 {t5[:, NRT - 1, k].mean():8.2f}")
-d = np.diff(t5[:, 1:, :], axis=2).mean(axis=(0, 1))
+for k, nm in enumerate(("a_ready", "mfma_done", "written", "summed", "end")):
+    print(f"tile0 {nm:10s} {np.nanmean(t5[:, 0, k]):8.2f}   tile15 {np.nanmean(t5[:, NRT - 1, k]):8.2f}")
 top = t5[:, :, 0]
-print("per tile mean (t >= 1): mfma %.3f  exch+barrier %.3f  partial reads %.3f  epilogue+stores %.3f us" % tuple(d))
-print("tile-to-tile (a_ready) mean %.3f us; stored -> next a_ready %.3f us" %
-      (np.diff(top, axis=1).mean(), (t5[:, 1:, 0] - t5[:, :-1, 4]).mean()))
+print("per tile mean: a_ready->mfma_done %.3f  mfma_done->written %.3f  end->next a_ready %.3f us" %
+      (np.nanmean(t5[:, :, 1] - t5[:, :, 0]), np.nanmean(t5[:, :, 2] - t5[:, :, 1]),
+       np.nanmean(t5[:, 1:, 0] - t5[:, :-1, 4])))
+print("tile-to-tile (a_ready) mean %.3f us; step span (tile 0 a_ready -> tile 15 end) %.2f us" %
+      (np.nanmean(np.diff(top, axis=1)), np.nanmean(t5[:, NRT - 1, 4] - t5[:, 0, 0])))
