@@ -134,8 +134,8 @@ class NativeMLP:
         one workgroup per CU, 64-row chunks) streaming: 16 chunks per CU, 1024 rows per CU =
         262,144 on a 256-CU MI355X — the bench's per-GPU batch (BASELINE.json:8). Below ~4 chunks
         per CU the ~30-50 us of fixed cost per step (launches, the spread reduction) dominates
-        (216-272 M rows/s at 65,536 vs 1.1 G rows/s here). A job's default batch (config.py
-        batch_size 0 = auto, train/job.py auto_batch)."""
+        (216-272 M rows/s at 65,536 vs 1.1 G rows/s here). A job's auto batch (--batch-size 0,
+        train/job.py auto_batch; the MLP job default is 256, config.py)."""
         props = torch.cuda.get_device_properties(device)
         return 1024 * max(1, props.multi_processor_count)
 

@@ -113,7 +113,8 @@ def run_config(cfg: RunConfig, log=print) -> dict:
     if cfg.batch_size <= 0:
         cfg.batch_size = auto_batch(cfg.model, cfg, dev, n_rank)
         say(f"Batch size (auto): {cfg.batch_size} rows per GPU")
-    if cfg.model == "mlp_online" and cfg.online_chunk <= 0:  # auto: 8 mini-batches per rank per chunk
+    if cfg.model == "mlp_online" and cfg.online_chunk <= 0:  # auto: 8 mini-batches per rank per
+        # chunk (train/online.py chunk_bounds balances the chunks of a pass)
         cfg.online_chunk = 8 * cfg.batch_size * max(ctx.world_size, 1)
         say(f"Stream chunk (auto): {cfg.online_chunk} rows")
     b = max(1, min(cfg.batch_size, n_rank))

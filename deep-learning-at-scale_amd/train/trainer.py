@@ -62,10 +62,12 @@ class History:
     val_loss: list = dataclasses.field(default_factory=list)
     val_mse: list = dataclasses.field(default_factory=list)
     epoch_time: list = dataclasses.field(default_factory=list)
+    # wall (host) clock around an epoch's / chunk's training steps: from before the first
+    # launch to after the final synchronize, so host issue gaps count (round-4 VERDICT item 8:
+    # the primary figure)
     rows_per_s: list = dataclasses.field(default_factory=list)
-    # host clock around the same steps (includes the Python issue time before the first
-    # launch and the final synchronize); rows_per_s itself is device-timed on GPUs
-    rows_per_s_host: list = dataclasses.field(default_factory=list)
+    # the device's busy span for the same steps (CUDA events on the compute stream), beside it
+    rows_per_s_device: list = dataclasses.field(default_factory=list)
 
 
 class StepClock:
@@ -351,9 +353,9 @@ class Trainer:
             h.val_loss.append(v_loss)
             h.val_mse.append(v_mse)
             h.epoch_time.append(time.perf_counter() - t_ep)
-            h.rows_per_s.append(rows / dt if dt > 0 else 0.0)
             hd = getattr(self, "last_host_dt", dt)
-            h.rows_per_s_host.append(rows / hd if hd > 0 else 0.0)
+            h.rows_per_s.append(rows / hd if hd > 0 else 0.0)
+            h.rows_per_s_device.append(rows / dt if dt > 0 else 0.0)
             if cfg.verbose >= 2:
                 self.log(f"Epoch {self.epoch}/{cfg.epochs} - {h.epoch_time[-1]:.2f}s - loss: {tr_loss:.6f}"
                          f" - val_loss: {v_loss:.6f} - val_mse: {v_mse:.6f} - rows/s: {h.rows_per_s[-1]:.0f}",

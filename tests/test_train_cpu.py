@@ -135,3 +135,32 @@ def test_evaluate_with_native_window_prefetcher_matches_plain_gather(monkeypatch
     monkeypatch.setenv("WELLFLOW_NATIVE_IO", "0")
     plain = tr.evaluate(X, Y, chunk=50)
     assert with_pf == pytest.approx(plain, rel=1e-6)
+
+
+def test_stream_chunks_are_balanced():
+    """chunk_bounds: the chunks of a pass hold equal full-batch counts (+-1) and every full
+    batch is kept (round-4 VERDICT item 8: an 8 + 1 split made every other chunk pay the
+    fixed per-chunk cost over one step)."""
+    import numpy as np
+
+    from wellflow.train.online import chunk_bounds, rank_batches, rank_shard
+
+    for n, b, w in [(2_457_600, 262_144, 1), (2_457_600, 65_536, 4), (100_000, 256, 2), (20_485, 256, 1),
+                    (1000, 256, 8), (121 * 512, 256, 2), (37 * 100 + 5, 100, 1), (9 * 4096 + 7, 4096, 1)]:
+        unit = b * w
+        starts = chunk_bounds(n, 8 * unit, unit)
+        ends = starts[1:] + [n]
+        full = [(e - s) // unit for s, e in zip(starts, ends)]
+        assert starts[0] == 0 and all(e > s for s, e in zip(starts, ends))
+        if n >= unit:
+            assert max(full) - min(full) <= 1 and max(full) <= 8, (n, b, w, full)
+            assert sum(full) == n // unit  # no full batch lost to the chunking
+    X = np.arange(1000 * 2, dtype=np.float32).reshape(1000, 2)
+    Y = np.arange(1000, dtype=np.float32)
+    seen = []
+    for r in range(2):  # the shards of 2 ranks cover exactly the chunks' per-rank rows
+        Xs, Ys, table = rank_shard(X, Y, 8 * 64 * 2, r, 2, unit=64 * 2)
+        for off, n_rows, per_rank in table:
+            for xb, yb in rank_batches(Xs[off : off + per_rank], Ys[off : off + per_rank], 64, 0, 1):
+                seen.extend(yb.tolist())
+    assert len(seen) == len(set(seen)) == (1000 // 128) * 128
