@@ -229,11 +229,26 @@ class NativeLSTM:
         # plain-stored and one reduce, instead of fp32 atomics into gW (WELLFLOW_DW_SLAB=0: atomics)
         self.dw_slab = None
         if os.environ.get("WELLFLOW_DW_SLAB", "1") != "0":
-            self.dw_slab = torch.empty(max(1, min(32, T * B // 16384)) * lay.G * lay.KA,
+            self.dw_slab = torch.empty(self._dw_slab_splits(lay.G, lay.KA, T * B, dev) * lay.G * lay.KA,
                                        dtype=torch.float32, device=dev)
         self._fallback_noted = set()
         self.last_backward_persistent = False
         self.sync_weights()
+
+    @staticmethod
+    def _dw_slab_splits(G: int, KA: int, K: int, device) -> int:
+        """Split-K partials the dW GEMM will actually store (csrc/gemm.hip launch_dw_288w: the
+        heuristic split min(32, K / 16384), clamped to one workgroup per CU, i.e. CUs / tiles =
+        16 on 256 CUs), so the slab is no larger than what is written (round-4 ADVICE: 32 splits
+        were allocated, 151 MB at the default shape, half never written). A larger explicit
+        dw_ksplit than this falls back to atomics in the launcher (slab_cap check)."""
+        ks = max(1, min(32, K // 16384))
+        if G % 256 == 0 and KA % 288 == 0:
+            tiles = (G // 256) * (KA // 288)
+            cus = torch.cuda.get_device_properties(device).multi_processor_count
+            if ks * tiles > cus and cus // tiles >= 1:
+                ks = cus // tiles
+        return ks
 
     @staticmethod
     def full_grid_batch(hidden: int, device) -> int:

@@ -202,9 +202,25 @@ class Trainer:
             "history": dataclasses.asdict(self.history),
             "extra": self.extra_state,
             "numpy_seed": int(self.cfg.seed),
+            "layout": self._layout_tag(),
         }
 
+    def _layout_tag(self) -> dict:
+        """What the flat parameter vector means: its length and the engine's layout (e.g. the
+        CNN's padded filter count), checked on resume (round-4 ADVICE: a layout change used to
+        surface as a bare size mismatch inside params.copy_)."""
+        lay = getattr(self.eng, "lay", None) or getattr(self.eng, "layout", None)
+        return {"engine": type(self.eng).__name__, "numel": int(self.eng.params.numel()),
+                "layout": repr(lay) if lay is not None else None}
+
     def load_state_dict(self, sd: dict) -> None:
+        mine, theirs = self._layout_tag(), sd.get("layout")
+        if sd["params"].numel() != mine["numel"] or (theirs and theirs.get("layout") and mine["layout"]
+                                                     and theirs["layout"] != mine["layout"]):
+            raise ValueError(
+                f"checkpoint parameter layout does not match this engine: checkpoint {theirs or 'untagged'} "
+                f"with {sd['params'].numel()} values, engine {mine}. It was written by a different model "
+                "configuration or an older flat layout; start without --resume (or remap the weights).")
         self.eng.params.copy_(sd["params"].to(self.eng.params.device))
         self.eng.sync_weights()
         if getattr(self.eng, "rng", None) is not None:  # dropout stream continues where it stopped
@@ -215,7 +231,8 @@ class Trainer:
         es = sd["early_stopping"]
         self.stopper = EarlyStopping(int(es["patience"]), float(es["best"]), int(es["wait"]),
                                      bool(es["stopped"]))
-        self.history = History(**{k: list(v) for k, v in sd["history"].items()})
+        known = {f.name for f in dataclasses.fields(History)}  # (rows_per_s_host: pre-round-5 name)
+        self.history = History(**{k: list(v) for k, v in sd["history"].items() if k in known})
         self.extra_state = dict(sd.get("extra", {}))
 
     def try_resume(self) -> bool:

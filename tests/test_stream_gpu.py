@@ -56,3 +56,36 @@ def test_streamer_feed_second_source_and_bf16_cast():
             seen += 1
         assert seen == n
     st.close()
+
+
+@pytest.mark.parametrize("pinned", [False, True])
+def test_streamer_prefetch_at_chunk_boundaries(pinned):
+    """The online job's pattern (train/online.py): feed chunk 0, consume it; feed chunk 1 and
+    prefetch() (its first batches copy while the job validates); slow compute on the consumer
+    stream; consume chunk 1; feed chunk 2 + prefetch; consume chunk 2. Every batch arrives
+    exactly once, in its chunk, in order, with its bytes — no batch skipped, duplicated or
+    overwritten at a boundary (round-4 ADVICE: only feed-after-drain was covered)."""
+    from wellflow.data.stream import DeviceStreamer
+
+    chunks = [_batches(n, B=2048, seed=10 + c, pinned=pinned) for c, n in enumerate((8, 5, 9))]
+    st = DeviceStreamer(None, DEV, depth=4)
+    big = torch.randn(2048, 2048, device=DEV)
+    got = []
+    for c, src in enumerate(chunks):
+        if c == 0:
+            st.feed(src)
+        mine = []
+        for slot in st:
+            xd, yd = st.slots[slot][0], st.slots[slot][1]
+            mine.append((xd.clone(), yd.clone()))  # copies queued on the consumer stream
+        got.append(mine)
+        if c + 1 < len(chunks):
+            st.feed(chunks[c + 1])
+            st.prefetch()
+            for _ in range(20):  # "validation": slow work while the next chunk's copies run
+                big = torch.tanh(big @ big * 1e-3)
+    torch.cuda.synchronize()
+    for c, (mine, src) in enumerate(zip(got, chunks)):
+        assert len(mine) == len(src), (c, len(mine), len(src))
+        for i, ((xd, yd), (x, y)) in enumerate(zip(mine, src)):
+            assert torch.equal(xd.cpu(), x) and torch.equal(yd.cpu(), y), (c, i)

@@ -164,3 +164,20 @@ def test_stream_chunks_are_balanced():
             for xb, yb in rank_batches(Xs[off : off + per_rank], Ys[off : off + per_rank], 64, 0, 1):
                 seen.extend(yb.tolist())
     assert len(seen) == len(set(seen)) == (1000 // 128) * 128
+
+
+def test_resume_with_other_layout_fails_clearly(tmp_path):
+    """A checkpoint whose flat parameter layout differs from the engine's (another hidden
+    size, or an older padding) is refused with a message naming both layouts (round-4 ADVICE)."""
+    import pytest as _pytest
+
+    from wellflow.train.job import run_job
+    from wellflow.utils.checkpoint import load_state
+
+    base = [NAMES, TYPES, "flow", str(tmp_path), "--epochs", "1", "--synth-wells", "3",
+            "--synth-steps", "120", "--device", "cpu", "--batch-size", "32", "--verbose", "0"]
+    run_job("mlp", base, log=lambda *a, **k: None)
+    st = load_state(str(tmp_path / "models" / "mlp.ckpt"))
+    assert st["layout"]["numel"] == st["params"].numel()
+    with _pytest.raises(ValueError, match="layout does not match"):
+        run_job("mlp", base + ["--mlp-hidden", "64,64", "--resume"], log=lambda *a, **k: None)
