@@ -301,7 +301,8 @@ def bench_mlp(args, ctx, online: bool):
     ctx.broadcast_(eng.params)
     eng.sync_weights()
     # Adam writes the bf16 compute copy and clears the gradient bucket in its own launch
-    opt = FlatAdam(eng.params, eng.grads, lr=args.lr, shadow=eng.shadow, zero_grads=True)
+    opt = FlatAdam(eng.params, eng.grads, lr=args.lr, shadow=eng.shadow, zero_grads=True,
+                   shadow_t=eng.shadow_t)
     gscale = 1.0 / (B * ctx.world_size)
     graph = not args.no_graph
     extra = {}

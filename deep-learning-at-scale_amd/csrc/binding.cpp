@@ -548,7 +548,7 @@ void mlp2_reduce(const at::Tensor& red, int64_t Fp, int64_t B, c10::optional<at:
 bool mlp2_step(const at::Tensor& X, int64_t Fp, const at::Tensor& W1, const at::Tensor& b1, const at::Tensor& W2,
                const at::Tensor& b2, const at::Tensor& w3, const at::Tensor& b3, const at::Tensor& y, double dy_scale,
                int64_t B, c10::optional<at::Tensor> rows, const at::Tensor& dZ2, c10::optional<at::Tensor> pred,
-               const at::Tensor& red, bool dz_frag) {
+               const at::Tensor& red, bool dz_frag, c10::optional<at::Tensor> W2T) {
   constexpr int64_t H = 256;
   check_t(X, at::kBFloat16, "X");
   const int64_t nrows = check_x_rows(X, Fp, B, rows);
@@ -571,10 +571,17 @@ bool mlp2_step(const at::Tensor& X, int64_t Fp, const at::Tensor& W1, const at::
   for (const at::Tensor* t : {&X, &W1, &W2, &dZ2})
     TORCH_CHECK(reinterpret_cast<uintptr_t>(t->data_ptr()) % 16 == 0, "mlp2_step: bf16 operands must be 16-B aligned");
   TORCH_CHECK(B > 0, "mlp2_step: B > 0");
+  const bf16_t* w2t = nullptr;
+  if (W2T.has_value()) {
+    check_t(*W2T, at::kBFloat16, "W2T");
+    check_extent(*W2T, H * H, "W2T");
+    TORCH_CHECK(reinterpret_cast<uintptr_t>(W2T->data_ptr()) % 16 == 0, "mlp2_step: W2T must be 16-B aligned");
+    w2t = bfp(*W2T);
+  }
   const c10::hip::OptionalHIPGuardMasqueradingAsCUDA guard(X.device());
   return wf::launch_mlp2_step(bfp(X), (int)Fp, bfp(W1), fp(b1), bfp(W2), fp(b2), fp(w3), fp(b3), fp(y), (float)dy_scale,
                               (int)B, rows_ptr(rows, B), nrows, bfp(dZ2), opt_ptr<float>(pred, at::kFloat, "pred", B),
-                              fp(red), dz_frag, cur_stream());
+                              fp(red), dz_frag, cur_stream(), w2t);
 }
 
 // dW2 from the fragment-layout dZ2 of mlp2_step(dz_frag=True) into the spread scratch's dW2
@@ -725,7 +732,8 @@ void adam(const at::Tensor& p, const at::Tensor& g, const at::Tensor& m, const a
 
 void adam_dev(const at::Tensor& p, const at::Tensor& g, const at::Tensor& m, const at::Tensor& v,
               const at::Tensor& step, double lr, double b1, double b2, double eps, double wd,
-              double gscale, c10::optional<at::Tensor> shadow, bool zero_g) {
+              double gscale, c10::optional<at::Tensor> shadow, bool zero_g,
+              c10::optional<at::Tensor> shadow_t, int64_t t_off, int64_t t_rows, int64_t t_cols) {
   check_t(p, at::kFloat, "p");
   check_t(g, at::kFloat, "g");
   check_t(m, at::kFloat, "m");
@@ -737,9 +745,16 @@ void adam_dev(const at::Tensor& p, const at::Tensor& g, const at::Tensor& m, con
   for (const at::Tensor* t : {&p, &g, &m, &v})
     TORCH_CHECK(reinterpret_cast<uintptr_t>(t->data_ptr()) % 16 == 0, "adam: buffers must be 16-B aligned");
   const c10::hip::OptionalHIPGuardMasqueradingAsCUDA guard(p.device());
+  // shadow_t: a transposed bf16 copy of the [t_rows][t_cols] block at element t_off (e.g. the
+  // MLP's W2^T, read by mlp2_step128_kernel) written in the same launch
+  bf16_t* tdst = nullptr;
+  if (shadow_t.has_value()) {
+    TORCH_CHECK(t_off >= 0 && t_rows > 0 && t_cols > 0 && t_off + t_rows * t_cols <= n, "adam: shadow_t block outside p");
+    tdst = opt_ptr<bf16_t>(shadow_t, at::kBFloat16, "shadow_t", t_rows * t_cols);
+  }
   wf::launch_adam_dev(fp(p), fp(g), fp(m), fp(v), n, fp(step), (float)lr, (float)b1, (float)b2,
                       (float)eps, (float)wd, (float)gscale, opt_ptr<bf16_t>(shadow, at::kBFloat16, "shadow", n),
-                      zero_g ? 1 : 0, cur_stream());
+                      zero_g ? 1 : 0, cur_stream(), tdst, (long)t_off, (int)t_rows, (int)t_cols);
 }
 
 void sgd(const at::Tensor& p, const at::Tensor& g, const at::Tensor& vel, double lr,

@@ -436,7 +436,8 @@ __global__ __launch_bounds__(256) void adam_dev_kernel(float* __restrict__ p, fl
                                                        float* __restrict__ m, float* __restrict__ v,
                                                        long n, float* __restrict__ step, float lr,
                                                        float b1, float b2, float eps, float wd,
-                                                       float gscale, bf16_t* __restrict__ shadow, int zero_g) {
+                                                       float gscale, bf16_t* __restrict__ shadow, int zero_g,
+                                                       bf16_t* __restrict__ tdst, long t_off, int t_rows, int t_cols) {
   const float t = step[0] + 1.f;
   const float bc1 = 1.f - __powf(b1, t), bc2 = 1.f - __powf(b2, t);
   const long n4 = n / 4;
@@ -459,11 +460,24 @@ __global__ __launch_bounds__(256) void adam_dev_kernel(float* __restrict__ p, fl
       const unsigned hi = (unsigned)f2bf(pp.z) | ((unsigned)f2bf(pp.w) << 16);
       reinterpret_cast<uint2*>(shadow)[i] = make_uint2(lo, hi);
     }
+    if (tdst != nullptr) {  // transposed copy of one block (rows x cols at element t_off)
+      const long e0 = 4 * i - t_off;
+      if (e0 + 3 >= 0 && e0 < (long)t_rows * t_cols) {
+        const float pv[4] = {pp.x, pp.y, pp.z, pp.w};
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const long e = e0 + q;
+          if (e >= 0 && e < (long)t_rows * t_cols) tdst[(e % t_cols) * t_rows + e / t_cols] = f2bf(pv[q]);
+        }
+      }
+    }
   }
   for (long i = n4 * 4 + blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += stride) {
     adam_one(p[i], g[i] * gscale, m[i], v[i], lr, b1, b2, eps, wd, bc1, bc2);
     if (zero_g) g[i] = 0.f;
     if (shadow != nullptr) shadow[i] = f2bf(p[i]);
+    const long e = i - t_off;
+    if (tdst != nullptr && e >= 0 && e < (long)t_rows * t_cols) tdst[(e % t_cols) * t_rows + e / t_cols] = f2bf(p[i]);
   }
   __syncthreads();  // every thread of this workgroup has read step[0]
   if (threadIdx.x == 0) {
@@ -477,14 +491,14 @@ __global__ __launch_bounds__(256) void adam_dev_kernel(float* __restrict__ p, fl
 
 void launch_adam_dev(float* p, float* g, float* m, float* v, long n, float* step, float lr,
                      float b1, float b2, float eps, float wd, float gscale, bf16_t* shadow, int zero_g,
-                     hipStream_t s) {
+                     hipStream_t s, bf16_t* tdst, long t_off, int t_rows, int t_cols) {
   // every workgroup draws a ticket from ONE counter (step[1]) and same-address atomics serialise:
   // at most WELLFLOW_ADAM_GRID (default 256) workgroups, grid-stride over the rest
   static const int cap = std::max(1, diag_env_int("WELLFLOW_ADAM_GRID", 256));  // sweep: WF_DIAG builds only
   int blocks = ew_blocks(n);
   if (blocks > cap) blocks = cap;
   hipLaunchKernelGGL(adam_dev_kernel, dim3(blocks), dim3(256), 0, s, p, g, m, v, n, step, lr,
-                     b1, b2, eps, wd, gscale, shadow, zero_g);
+                     b1, b2, eps, wd, gscale, shadow, zero_g, tdst, t_off, t_rows, t_cols);
 }
 
 // Keras-0.x SGD: v = mu v - lr_t g; p += mu v - lr_t g (Nesterov) or p += v.

@@ -131,7 +131,10 @@ void launch_mlp2_reduce(float* red, int Fp, int B, float* loss_sum, float* db3, 
 // which launch_mlp2_reduce then adds to the gradients. Fp <= 32; false = not covered.
 bool launch_mlp2_step(const bf16_t* X, int Fp, const bf16_t* W1, const float* b1, const bf16_t* W2, const float* b2,
                       const float* w3, const float* b3, const float* y, float dy_scale, int B, const long long* rows,
-                      long nrows, bf16_t* dZ2, float* pred, float* red, bool dz_frag, hipStream_t s);
+                      long nrows, bf16_t* dZ2, float* pred, float* red, bool dz_frag, hipStream_t s,
+                      const bf16_t* W2T = nullptr);
+// W2T (optional, [256][256] bf16 = W2 transposed): with dz_frag, the 128-row-pass kernel that
+// streams both weight images (mlp2_step128_kernel) instead of holding W2^T in registers.
 // dz_frag: dZ2 is written in the fragment layout of launch_mlp2_dw2f (B % 64 == 0) instead of
 // [B][256]: fragment (S, b) of rows 32S .. 32S + 31 x units 16b .. 16b + 15 at element
 // (S * 16 + b) * 512, lane (l15, g) = 16 B = rows 32S + 8g .. + 7 of unit 16b + l15.
@@ -188,7 +191,7 @@ void launch_adam(float* p, const float* g, float* m, float* v, long n, float lr,
                  float b2, float eps, float wd, float bc1, float bc2, float gscale, hipStream_t s);
 void launch_adam_dev(float* p, float* g, float* m, float* v, long n, float* step, float lr,
                      float b1, float b2, float eps, float wd, float gscale, bf16_t* shadow, int zero_g,
-                     hipStream_t s);
+                     hipStream_t s, bf16_t* tdst = nullptr, long t_off = 0, int t_rows = 0, int t_cols = 0);
 void launch_sgd(float* p, const float* g, float* vel, long n, float lr, float momentum,
                 int nesterov, float gscale, hipStream_t s);
 void launch_sgd_dev(float* p, float* g, float* vel, long n, float* step, float lr, float decay, float momentum,

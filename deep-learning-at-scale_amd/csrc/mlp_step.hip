@@ -455,6 +455,389 @@ __global__ __launch_bounds__(512, 1) void mlp2_step_kernel(
 }
 
 // ----------------------------------------------------------------------------------------
+// 128-row passes (round-4 VERDICT item 3): the same step as mlp2_step_kernel over TWO 64-row
+// chunks at a time, with BOTH layer-2 weight images streamed from L2 — W2 rows for layer 2 and
+// W2^T rows (a transposed bf16 copy the optimizer / sync_weights writes) for dH1 — so every
+// streamed fragment feeds 8 row tiles instead of 4: per row, L2 bytes halve for layer 2 and the
+// 64 VGPRs of the resident W2^T image pay for the doubled accumulators (acc[2][8]). The two
+// GEMMs run one continuous 16-step fragment stream per pass (8 W2 K-steps, then 8 W2^T K-steps,
+// WD = 4 slots ahead; 16 % WD == 0 keeps every slot index static). Batch sums live in registers
+// (the 48-KiB LDS sum block of the 64-row kernel does not fit beside the 128-row tiles).
+// LDS: X (double-buffered, 64-B rows, Fp <= 32) 16 KiB + H1 64 KiB + dZ2 64 KiB + head 4 KiB.
+// Rows past B are masked (dy = 0, no stores); FRAG fragments of rows >= B are not written.
+__device__ __forceinline__ int x4_off(int row, int chunk) { return row * 64 + ((chunk ^ ((row >> 2) & 3)) << 4); }
+
+template <int NFT>
+__global__ __launch_bounds__(512, 1) void mlp2_step128_kernel(
+    const bf16_t* __restrict__ X, int Fp, const bf16_t* __restrict__ W1, const float* __restrict__ b1,
+    const bf16_t* __restrict__ W2, const bf16_t* __restrict__ W2T, const float* __restrict__ b2,
+    const float* __restrict__ w3, const float* __restrict__ b3, const float* __restrict__ y, float dy_scale, int B,
+    const long long* __restrict__ rows, long nrows, bf16_t* __restrict__ dZ2, float* __restrict__ pred,
+    float* __restrict__ red, int prio) {
+  constexpr int MT = 2, NR = 8, NW = 8, R = 128, XB = R * 64, WD = 4;
+  static_assert(16 % WD == 0, "stream slots must repeat every pass");
+  __shared__ __attribute__((aligned(16))) char xs[2 * XB];          // X tiles (double-buffered)
+  __shared__ __attribute__((aligned(16))) char h1s[R * MF_H * 2];   // H1 -> dZ1 (own columns)
+  __shared__ __attribute__((aligned(16))) char zs[R * MF_H * 2];    // dZ2
+  __shared__ __attribute__((aligned(16))) float hred[R][NW];        // head partials
+  __shared__ __attribute__((aligned(16))) float cst[3][MF_H];       // b1, b2, w3
+  __shared__ float ys[2][R];
+  __shared__ float lred[NW];
+
+  const int tid = threadIdx.x, lane = tid & 63, l15 = lane & 15, g = lane >> 4;
+  const int wid = tid >> 6;
+  const int u0 = wid * 16 * MT;
+  const int tq = l15 >> 2, tp = lane & 3;  // ds_read_b64_tr_b16 lane coordinates
+  for (int i = tid; i < 3 * MF_H; i += 64 * NW) cst[i / MF_H][i % MF_H] = (i < MF_H ? b1 : i < 2 * MF_H ? b2 : w3)[i % MF_H];
+
+  bf16x8 w1f[MT];
+#pragma unroll
+  for (int m = 0; m < MT; ++m) {
+    const int u = u0 + 16 * m + l15;
+    w1f[m] = 8 * g + 8 <= Fp ? *reinterpret_cast<const bf16x8*>(W1 + (size_t)u * Fp + 8 * g)
+                             : bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
+  }
+  // the fragment stream: step s < 8 = W2 K-step s (layer 2), 8 <= s < 16 = W2^T K-step s - 8
+  // (dH1); lane fragment (m, kt) = 16 B at row u0 + 16m + l15, columns 32kt + 8g (both images
+  // are [256][256] row-major, so one offset formula serves both resources)
+  int w2z = 0;  // laundered zero: keeps the loads inside the pass loop (hoisted they pin VGPRs)
+  const __amdgpu_buffer_rsrc_t rsA = __builtin_amdgcn_make_buffer_rsrc((void*)W2, 0, 0x7FFFFFFF, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rsT = __builtin_amdgcn_make_buffer_rsrc((void*)W2T, 0, 0x7FFFFFFF, 0x00020000);
+  const int wlane = (u0 + l15) * MF_H + 8 * g;
+  auto wfrag = [&](int s, int m) {
+    typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
+    const int kt = s & 7;
+    return __builtin_bit_cast(bf16x8, (u32x4_t)__builtin_amdgcn_raw_buffer_load_b128(
+                                          s < 8 ? rsA : rsT, 2 * (w2z + wlane), 2 * (16 * MF_H * m + 32 * kt), 0));
+  };
+  bf16x8 wr[WD][MT];
+  auto wfirst = [&]() {  // stream steps 0 .. WD - 1 (the next pass's first layer-2 fragments)
+    w2z = 0;
+    asm volatile("" : "+s"(w2z));
+#pragma unroll
+    for (int s = 0; s < WD; ++s)
+#pragma unroll
+      for (int m = 0; m < MT; ++m) wr[s][m] = wfrag(s, m);
+  };
+  f32x4 dw1a[MT][NFT];
+#pragma unroll
+  for (int m = 0; m < MT; ++m)
+#pragma unroll
+    for (int f = 0; f < NFT; ++f) dw1a[m][f] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float sum3[MT][4], sum1[MT][4], sum2[MT][4];  // dw3, db1, db2 partials (lane's units 4g + r)
+#pragma unroll
+  for (int m = 0; m < MT; ++m)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) sum3[m][r] = sum1[m][r] = sum2[m][r] = 0.f;
+  const float bias3 = b3[0];
+  float lsum = 0.f, db3a = 0.f;
+
+  // next pass's inputs: thread t one 16-B X segment (row t >> 2, chunk t & 3); threads < 128 a target
+  uint4 xv = make_uint4(0, 0, 0, 0);
+  float yv = 0.f;
+  auto prefetch = [&](int ps) {
+    const int r = tid >> 2, c = tid & 3, gr = ps * R + r;
+    xv = (gr < B && 8 * c + 8 <= Fp) ? *reinterpret_cast<const uint4*>(X + data_row(rows, gr, nrows) * Fp + 8 * c)
+                                     : make_uint4(0, 0, 0, 0);
+    if (tid < R) {
+      const int gy = ps * R + tid;
+      yv = gy < B ? y[data_row(rows, gy, nrows)] : 0.f;
+    }
+  };
+  const int npass = (B + R - 1) / R;
+  auto stage = [&](int p) {
+    *reinterpret_cast<uint4*>(xs + p * XB + x4_off(tid >> 2, tid & 3)) = xv;
+    if (tid < R) ys[p][tid] = yv;
+  };
+  if ((int)blockIdx.x < npass) prefetch(blockIdx.x);
+  stage(0);
+  __syncthreads();
+  if ((int)blockIdx.x + (int)gridDim.x < npass) prefetch(blockIdx.x + gridDim.x);
+  wfirst();
+  if (prio && __builtin_amdgcn_readfirstlane(wid) >= 4) __builtin_amdgcn_s_setprio(1);
+  int par = 0;
+  for (int ps = blockIdx.x; ps < npass; ps += gridDim.x, par ^= 1) {
+    const int row0 = ps * R;
+    char* xt = xs + par * XB;
+    // the lane coordinates, laundered per pass: every LDS address below derives from them, and
+    // as loop invariants the compiler hoisted ~40 swizzled addresses out of the pass loop and
+    // spilled them (one VGPR each); recomputed here they live for one phase
+    int lnv = lane;
+    asm volatile("" : "+v"(lnv));
+    const int l15 = lnv & 15, g = lnv >> 4, tq = l15 >> 2, tp = lnv & 3;
+
+    // ---- layer 1 (own units, 8 row tiles): H1 -> h1s
+    f32x4 acc[MT][NR];
+#pragma unroll
+    for (int n = 0; n < NR; ++n) {
+      const bf16x8 xb = *reinterpret_cast<const bf16x8*>(xt + x4_off(16 * n + l15, g));
+#pragma unroll
+      for (int m = 0; m < MT; ++m)
+        acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w1f[m], xb, f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+    }
+#pragma unroll
+    for (int m = 0; m < MT; ++m) {
+      const float4 bb = *reinterpret_cast<const float4*>(&cst[0][u0 + 16 * m + 4 * g]);
+#pragma unroll
+      for (int n = 0; n < NR; ++n) {
+        const unsigned p0 = pk_bf16(fmaxf(acc[m][n][0] + bb.x, 0.f), fmaxf(acc[m][n][1] + bb.y, 0.f));
+        const unsigned p1 = pk_bf16(fmaxf(acc[m][n][2] + bb.z, 0.f), fmaxf(acc[m][n][3] + bb.w, 0.f));
+        *reinterpret_cast<uint2*>(h1s + tile_off(16 * n + l15, u0 + 16 * m + 4 * g)) = make_uint2(p0, p1);
+      }
+    }
+    __syncthreads();  // B2: H1 complete
+
+    // ---- layer 2 (own units, K = 256): stream steps 0..7; the B fragments (H1) rotate through
+    // one set of NR registers, fragment n of K step kt + 1 read right after its two MFMAs of kt
+#pragma unroll
+    for (int m = 0; m < MT; ++m)
+#pragma unroll
+      for (int n = 0; n < NR; ++n) acc[m][n] = f32x4{0.f, 0.f, 0.f, 0.f};
+    bf16x8 hb[NR];
+#pragma unroll
+    for (int n = 0; n < NR; ++n) hb[n] = *reinterpret_cast<const bf16x8*>(h1s + tile_off(16 * n + l15, 8 * g));
+    static_for<0, 8>([&](auto kc) {
+      constexpr int kt = decltype(kc)::value;
+#pragma unroll
+      for (int n = 0; n < NR; ++n) {
+#pragma unroll
+        for (int m = 0; m < MT; ++m)
+          acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wr[kt % WD][m], hb[n], acc[m][n], 0, 0, 0);
+        if constexpr (kt + 1 < 8) {
+          __builtin_amdgcn_sched_barrier(0);
+          hb[n] = *reinterpret_cast<const bf16x8*>(h1s + tile_off(16 * n + l15, 32 * (kt + 1) + 8 * g));
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      }
+#pragma unroll
+      for (int m = 0; m < MT; ++m) wr[kt % WD][m] = wfrag(kt + WD, m);  // steps WD .. 7 + WD (W2^T from 8)
+    });
+    // H2 = relu(Z2 + b2) rounded to bf16, kept in acc; head partials of rows 16n + l15
+    float hp[NR];
+#pragma unroll
+    for (int n = 0; n < NR; ++n) hp[n] = 0.f;
+#pragma unroll
+    for (int m = 0; m < MT; ++m) {
+      const float4 bb = *reinterpret_cast<const float4*>(&cst[1][u0 + 16 * m + 4 * g]);
+      const float4 ww = *reinterpret_cast<const float4*>(&cst[2][u0 + 16 * m + 4 * g]);
+      const float bv[4] = {bb.x, bb.y, bb.z, bb.w}, wv[4] = {ww.x, ww.y, ww.z, ww.w};
+#pragma unroll
+      for (int n = 0; n < NR; ++n)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float v = bf2f(f2bf(fmaxf(acc[m][n][r] + bv[r], 0.f)));
+          acc[m][n][r] = v;
+          hp[n] += v * wv[r];
+        }
+    }
+#pragma unroll
+    for (int n = 0; n < NR; ++n) {
+      hp[n] += __shfl_xor(hp[n], 16, 64);
+      hp[n] += __shfl_xor(hp[n], 32, 64);
+    }
+    if (g == 0) {
+#pragma unroll
+      for (int n = 0; n < NR; ++n) hred[16 * n + l15][wid] = hp[n];
+    }
+    __syncthreads();  // B3: head partials complete
+
+    // ---- prediction, dy, loss of rows 16n + l15; wave 0 lane group g owns rows 16n + l15 for
+    // n = g and n = g + 4 (their loss, db3 and prediction store)
+    float dyn[NR], pst[2] = {0.f, 0.f};
+    int pgr[2] = {-1, -1};
+#pragma unroll
+    for (int n = 0; n < NR; ++n) {
+      const int r = 16 * n + l15, gr = row0 + r;
+      const float4 pa = *reinterpret_cast<const float4*>(&hred[r][0]);
+      const float4 pb = *reinterpret_cast<const float4*>(&hred[r][4]);
+      const float p = ((pa.x + pa.y) + (pa.z + pa.w)) + ((pb.x + pb.y) + (pb.z + pb.w)) + bias3;
+      dyn[n] = 0.f;
+      if (gr < B) {
+        const float diff = p - ys[par][r];
+        dyn[n] = dy_scale * diff;
+        if (wid == 0 && (n & 3) == g) {
+          pst[n >> 2] = p;
+          pgr[n >> 2] = gr;
+          lsum += diff * diff;
+          db3a += dyn[n];
+        }
+      }
+    }
+    // ---- dZ2 = dy w3^T * [H2 > 0] (own units) -> zs; dw3, db2 partials
+#pragma unroll
+    for (int m = 0; m < MT; ++m) {
+      const float4 ww = *reinterpret_cast<const float4*>(&cst[2][u0 + 16 * m + 4 * g]);
+      const float wv[4] = {ww.x, ww.y, ww.z, ww.w};
+#pragma unroll
+      for (int n = 0; n < NR; ++n) {
+        float t[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          sum3[m][r] += acc[m][n][r] * dyn[n];
+          t[r] = acc[m][n][r] > 0.f ? dyn[n] : 0.f;
+          sum2[m][r] += t[r];
+        }
+        *reinterpret_cast<uint2*>(zs + tile_off(16 * n + l15, u0 + 16 * m + 4 * g)) =
+            make_uint2(pk_bf16(t[0] * wv[0], t[1] * wv[1]), pk_bf16(t[2] * wv[2], t[3] * wv[3]));
+      }
+    }
+    // the sums materialised HERE: left to itself the compiler sank these adds to the end of the
+    // pass and kept all 64 H2 values (and the dZ2 masks) alive through dH1 — 200+ spilled VGPRs
+#pragma unroll
+    for (int m = 0; m < MT; ++m)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) asm volatile("" : "+v"(sum3[m][r]), "+v"(sum2[m][r]));
+    asm volatile("" : "+v"(lsum), "+v"(db3a));
+    if (ps + (int)gridDim.x < npass) stage(par ^ 1);
+    __syncthreads();  // B4: dZ2 complete, next pass's X / y staged
+    if (ps + 2 * (int)gridDim.x < npass) prefetch(ps + 2 * gridDim.x);
+
+    // ---- dH1^T (own units k, K = 256 output units) = W2^T dZ2^T: stream steps 8..15
+#pragma unroll
+    for (int m = 0; m < MT; ++m)
+#pragma unroll
+      for (int n = 0; n < NR; ++n) acc[m][n] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int n = 0; n < NR; ++n) hb[n] = *reinterpret_cast<const bf16x8*>(zs + tile_off(16 * n + l15, 8 * g));
+    w2z = 0;
+    asm volatile("" : "+s"(w2z));
+    static_for<0, 8>([&](auto kc) {
+      constexpr int kt = decltype(kc)::value;
+#pragma unroll
+      for (int n = 0; n < NR; ++n) {
+#pragma unroll
+        for (int m = 0; m < MT; ++m)
+          acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wr[(8 + kt) % WD][m], hb[n], acc[m][n], 0, 0, 0);
+        if constexpr (kt + 1 < 8) {
+          __builtin_amdgcn_sched_barrier(0);
+          hb[n] = *reinterpret_cast<const bf16x8*>(zs + tile_off(16 * n + l15, 32 * (kt + 1) + 8 * g));
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      }
+      // refill: W2^T steps 8 + kt + WD while they last, then the next pass's first W2 steps
+#pragma unroll
+      for (int m = 0; m < MT; ++m) wr[(8 + kt) % WD][m] = wfrag((8 + kt + WD) & 15, m);
+    });
+    // global stores only after the next pass's W2 requests (vmcnt counts stores, in order)
+#pragma unroll
+    for (int q = 0; q < 2; ++q)
+      if (pgr[q] >= 0 && pred != nullptr) pred[pgr[q]] = pst[q];
+    // ---- dZ2 copy-out as dW2 A fragments (fragment (S, b) = 32 rows x 16 units; wave w writes
+    // fragments 8w .. 8w + 7 of the pass: row group S = row0 / 32 + (f >> 4), unit block f & 15)
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const int f = 8 * wid + q, sst = f >> 4, b = f & 15;
+      if (row0 + 32 * sst < B) {
+        bf16x8 v;
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const bf16x4 t = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+              (lds_bf16x4*)(zs + tile_off(32 * sst + 8 * g + 4 * h + tq, 16 * b + 4 * tp)));
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[4 * h + e] = t[e];
+        }
+        const size_t S = (size_t)(row0 >> 5) + sst;
+        *reinterpret_cast<bf16x8*>(dZ2 + ((S * 16 + b) * 64 + lnv) * 8) = v;
+      }
+    }
+    // ---- dZ1 = dH1 * [H1 > 0] over the same 8 bytes of h1s; db1 partials
+#pragma unroll
+    for (int m = 0; m < MT; ++m) {
+#pragma unroll
+      for (int n = 0; n < NR; ++n) {
+        const int r = 16 * n + l15;
+        uint2* pp = reinterpret_cast<uint2*>(h1s + tile_off(r, u0 + 16 * m + 4 * g));
+        const uint2 hv = *pp;
+        const bool rok = row0 + r < B;
+        const int hw2[2] = {rok ? (int)hv.x : 0, rok ? (int)hv.y : 0};
+        unsigned ow[2];
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+          const bool on0 = (hw2[q] << 16) > 0, on1 = hw2[q] > 0xFFFF;
+          const float t0 = on0 ? acc[m][n][2 * q] : 0.f, t1 = on1 ? acc[m][n][2 * q + 1] : 0.f;
+          sum1[m][2 * q] += t0;
+          sum1[m][2 * q + 1] += t1;
+          ow[q] = pk_bf16(t0, t1);
+        }
+        *pp = make_uint2(ow[0], ow[1]);
+      }
+    }
+#pragma unroll
+    for (int m = 0; m < MT; ++m)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) asm volatile("" : "+v"(sum1[m][r]));
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
+    // ---- dW1^T slice (32 units x Fp) += dZ1^T X over the pass's 128 rows
+#pragma unroll
+    for (int kk = 0; kk < R / 32; ++kk) {
+      bf16x8 af[MT], bfr[NFT];
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int r = 32 * kk + 8 * g + 4 * h + tq;
+#pragma unroll
+        for (int m = 0; m < MT; ++m) {
+          const bf16x4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_bf16x4*)(h1s + tile_off(r, u0 + 16 * m + 4 * tp)));
+#pragma unroll
+          for (int e = 0; e < 4; ++e) af[m][4 * h + e] = v[e];
+        }
+#pragma unroll
+        for (int f = 0; f < NFT; ++f) {
+          const int f0 = 16 * f + 4 * tp;
+          const bf16x4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+              (lds_bf16x4*)(xt + x4_off(r, f0 >> 3) + ((f0 & 7) << 1)));
+#pragma unroll
+          for (int e = 0; e < 4; ++e) bfr[f][4 * h + e] = v[e];
+        }
+      }
+#pragma unroll
+      for (int m = 0; m < MT; ++m)
+#pragma unroll
+        for (int f = 0; f < NFT; ++f)
+          dw1a[m][f] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[m], bfr[f], dw1a[m][f], 0, 0, 0);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
+  }
+
+  // ---- batch sums -> copy blockIdx % kMlpRedCopies of the scratch; dW1 -> this workgroup's row
+  float* rb = red + (blockIdx.x & (kMlpRedCopies - 1)) * kMlpRedRow;
+  float* slab = red + kMlpRedSlabOff + (size_t)blockIdx.x * kMlpRedSlabRow;
+  const float tl = block_sum<512>(lsum, lred);
+  if (tid == 0 && tl != 0.f) atomicAdd(rb + kMlpRedLoss, tl);
+  const float t3 = block_sum<512>(db3a, lred);
+  if (tid == 0 && t3 != 0.f) atomicAdd(rb + kMlpRedDb3, t3);
+#pragma unroll
+  for (int m = 0; m < MT; ++m)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int u = u0 + 16 * m + 4 * g + r;
+      float v[3] = {sum3[m][r], sum1[m][r], sum2[m][r] * cst[2][u]};
+#pragma unroll
+      for (int k = 0; k < 3; ++k) {
+        v[k] += __shfl_xor(v[k], 1, 64);
+        v[k] += __shfl_xor(v[k], 2, 64);
+        v[k] += __shfl_xor(v[k], 4, 64);
+        v[k] += __shfl_xor(v[k], 8, 64);
+      }
+      if (l15 == 0) {
+        if (v[0] != 0.f) atomicAdd(rb + kMlpRedDw3 + u, v[0]);
+        if (v[1] != 0.f) atomicAdd(rb + kMlpRedDb1 + u, v[1]);
+        if (v[2] != 0.f) atomicAdd(rb + kMlpRedDb2 + u, v[2]);
+      }
+    }
+#pragma unroll
+  for (int m = 0; m < MT; ++m)
+#pragma unroll
+    for (int f = 0; f < NFT; ++f) {
+      const int ft = l15 + 16 * f;
+      if (ft < Fp)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) slab[(u0 + 16 * m + 4 * g + i) * Fp + ft] = dw1a[m][f][i];
+    }
+}
+
+// ----------------------------------------------------------------------------------------
 // dW2 [256 out][256 in] += dZ2^T H1, H1 = relu(X W1^T + b1) recomputed. dZ2 arrives in the
 // fragment layout written by mlp2_step_kernel<., true> (fragment (S, b) = rows 32S .. 32S + 31
 // x units 16b .. 16b + 15, 1 KiB, lane (l15, g) = rows 32S + 8g + j of unit 16b + l15), so a
@@ -649,7 +1032,8 @@ __global__ __launch_bounds__(512, 1) void mlp2_dw2f_kernel(const bf16_t* __restr
 
 bool launch_mlp2_step(const bf16_t* X, int Fp, const bf16_t* W1, const float* b1, const bf16_t* W2, const float* b2,
                       const float* w3, const float* b3, const float* y, float dy_scale, int B, const long long* rows,
-                      long nrows, bf16_t* dZ2, float* pred, float* red, bool dz_frag, hipStream_t s) {
+                      long nrows, bf16_t* dZ2, float* pred, float* red, bool dz_frag, hipStream_t s,
+                      const bf16_t* W2T) {
   // the reduce sums the dW1 rows only when it expects the 8-wave backward's layout
   if (B <= 0 || Fp > 32 || Fp % 8 != 0 || red == nullptr || !mlp_bwd8()) return false;
   if (dz_frag && B % MF_ROWS != 0) return false;
@@ -660,6 +1044,15 @@ bool launch_mlp2_step(const bf16_t* X, int Fp, const bf16_t* W1, const float* b1
   // static s_setprio 1 for waves 4-7 (+0.2 to +1.1 % in three interleaved pairs, chunk span
   // 17.5k -> 17.1k cycles, profiles/r4/mlp_prio; the WELLFLOW_STEP_PRIO A/B knob was removed)
   constexpr int prio = 1;
+  if (W2T != nullptr && dz_frag && !stamp) {  // 128-row passes, both weight images streamed
+    if (Fp <= 16)
+      hipLaunchKernelGGL(mlp2_step128_kernel<1>, dim3(grid), dim3(512), 0, s, X, Fp, W1, b1, W2, W2T, b2, w3, b3, y,
+                         dy_scale, B, rows, nrows, dZ2, pred, red, prio);
+    else
+      hipLaunchKernelGGL(mlp2_step128_kernel<2>, dim3(grid), dim3(512), 0, s, X, Fp, W1, b1, W2, W2T, b2, w3, b3, y,
+                         dy_scale, B, rows, nrows, dZ2, pred, red, prio);
+    return true;
+  }
   if (stamp && Fp <= 16 && dz_frag) {
     hipLaunchKernelGGL((mlp2_step_kernel<1, true, true>), dim3(grid), dim3(512), 0, s, X, Fp, W1, b1, W2, b2, w3, b3, y,
                        dy_scale, B, rows, nrows, dZ2, pred, red, prio,

@@ -198,10 +198,27 @@ class NativeMLP:
         self.dw2f_split = int(os.environ.get("WELLFLOW_MLP_DW2F_SPLIT", "128"))
         self.red = (torch.zeros(MLP_RED_FLOATS, device=dev)
                     if spread and self.hidden == (256, 256) and self.Fp <= 32 else None)
+        # the one-launch step in 128-row passes with W2 AND W2^T streamed from L2
+        # (csrc/mlp_step.hip mlp2_step128_kernel; WELLFLOW_MLP_STEP128=0: 64-row passes, W2^T in
+        # registers): needs the transposed bf16 copy below, written with the shadow
+        self.w2t = None
+        if (self.red is not None and self.dw2_frag and os.environ.get("WELLFLOW_MLP_STEP128", "1") != "0"):
+            self.w2t = torch.empty(256 * 256, dtype=bf, device=dev)
         self.sync_weights()
+
+    @property
+    def shadow_t(self):
+        """(tensor, offset, rows, cols): the transposed bf16 block the optimizer writes beside
+        the shadow (optim/flat.py FlatAdam shadow_t), or None."""
+        if self.w2t is None:
+            return None
+        return (self.w2t, self.lay.offsets()[0][1][0], 256, 256)
 
     def sync_weights(self) -> None:
         self._C.cast_bf16(self.params, self.shadow)
+        if self.w2t is not None:
+            _, off, r, c = self.shadow_t
+            self.w2t.view(c, r).copy_(self.params[off : off + r * c].view(r, c).t())
 
     def _step_recompute(self, Xop, y, rows, grad_scale: float, zero_grads: bool, loss_into=None) -> torch.Tensor:
         """fused forward (H2 -> bitmask, head gradients) -> fused backward (dZ2, dZ1, dW1, biases;
@@ -224,7 +241,8 @@ class NativeMLP:
             if red is not None and self.step_fused and not self.dw2_gemm:
                 frag = self.dw2_frag
                 if not C.mlp2_step(Xop, self.Fp, wl[0][0], pl[0][1], wl[1][0], pl[1][1], hw, hb, y,
-                                   2.0 * float(grad_scale), B, rows, self.dZ[1], self.pred, red, frag):
+                                   2.0 * float(grad_scale), B, rows, self.dZ[1], self.pred, red, frag,
+                                   self.w2t if frag else None):
                     raise RuntimeError("NativeMLP: fused step refused the shape")
                 if frag:  # dW2 partials as slab rows (their count) summed by the reduce
                     ok = dw2_rows = C.mlp2_dw2f(self.dZ[1], Xop, self.Fp, rows, wl[0][0], pl[0][1], B,

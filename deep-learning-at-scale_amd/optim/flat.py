@@ -16,14 +16,17 @@ class FlatAdam:
 
     def __init__(self, params: torch.Tensor, grads: torch.Tensor, lr: float = 1e-3,
                  betas=(0.9, 0.999), eps: float = 1e-8, weight_decay: float = 0.0,
-                 shadow: torch.Tensor | None = None, zero_grads: bool = False):
+                 shadow: torch.Tensor | None = None, zero_grads: bool = False, shadow_t=None):
         """GPU fusions: ``shadow`` (bf16, same numel) receives the updated weights in the same
         launch (an engine whose compute copy is a plain cast, e.g. NativeMLP.shadow);
+        ``shadow_t`` = (bf16 tensor, offset, rows, cols) receives one [rows][cols] block
+        transposed in the same launch (NativeMLP.shadow_t: W2^T of the 128-row step kernel);
         ``zero_grads`` clears the gradient bucket after the update (the next
         forward_backward then runs with zero_grads=False)."""
         assert params.dtype == torch.float32 and params.shape == grads.shape
         self.params, self.grads = params, grads
         self.shadow, self.zero_grads = shadow, zero_grads
+        self.shadow_t = shadow_t
         self.lr, self.betas, self.eps, self.weight_decay = lr, tuple(betas), eps, weight_decay
         self.m = torch.zeros_like(params)
         self.v = torch.zeros_like(params)
@@ -38,8 +41,9 @@ class FlatAdam:
         if self.params.is_cuda:
             from ..ops.native import lib
 
+            st = self.shadow_t or (None, 0, 0, 0)
             lib().adam_dev(self.params, self.grads, self.m, self.v, self.step_dev, self.lr, b1, b2,
-                           self.eps, self.weight_decay, grad_scale, self.shadow, self.zero_grads)
+                           self.eps, self.weight_decay, grad_scale, self.shadow, self.zero_grads, *st)
             return
         bc1, bc2 = 1.0 - b1**self.t, 1.0 - b2**self.t
         g = self.grads * grad_scale
@@ -51,6 +55,9 @@ class FlatAdam:
         self.params.sub_(self.lr * upd)
         if self.shadow is not None:
             self.shadow.copy_(self.params)
+        if self.shadow_t is not None:
+            t, off, r, c = self.shadow_t
+            t.view(c, r).copy_(self.params[off : off + r * c].view(r, c).t())
         if self.zero_grads:
             self.grads.zero_()
 

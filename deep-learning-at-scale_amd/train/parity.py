@@ -134,7 +134,7 @@ def mlp_adam_trajectory(device, B: int = 262144, F: int = 16, steps: int = 20, l
     eng.sync_weights()
     x, y = synth_tabular_batch(B, F, seed=seed + 1)
     x, y = x.to(dev), y.to(dev)
-    opt = FlatAdam(eng.params, eng.grads, lr=lr, shadow=eng.shadow, zero_grads=True)
+    opt = FlatAdam(eng.params, eng.grads, lr=lr, shadow=eng.shadow, zero_grads=True, shadow_t=eng.shadow_t)
     run = StepRunner(eng, opt, DistContext(device=dev), 1.0 / B, lambda k: (x, y))
     nat = []
     for _ in range(steps):

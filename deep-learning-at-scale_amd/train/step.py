@@ -49,7 +49,9 @@ class StepRunner:
         # Adam writing the engine's bf16 compute copy in its own launch (NativeMLP.shadow)
         # replaces the separate repack
         sh = getattr(opt, "shadow", None)
-        self.fused_shadow = sh is not None and sh is getattr(eng, "shadow", None)
+        est, ost = getattr(eng, "shadow_t", None), getattr(opt, "shadow_t", None)
+        self.fused_shadow = (sh is not None and sh is getattr(eng, "shadow", None) and
+                             (est is None or (ost is not None and ost[0] is est[0])))
         self.loss_acc = torch.zeros(1, device=eng.device) if accumulate_loss else None
         # engines that add the batch loss straight into the accumulator (no zero + add launches)
         try:

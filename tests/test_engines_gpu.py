@@ -385,14 +385,15 @@ def _dz2_from_frag(zf: torch.Tensor, B: int) -> torch.Tensor:
 
 
 @pytest.mark.parametrize("B,F,indexed", [(262144, 16, False), (327680, 16, False), (4096, 32, False), (16384, 16, True),
-                                       (128, 8, False)])
+                                       (128, 8, False), (4160, 16, False), (64, 16, False)])
 def test_mlp_one_launch_step_matches_two_kernel_step(B, F, indexed):
     """The training step's forward + backward in ONE launch (csrc/mlp_step.hip: X staged once,
     layer 1 computed once, H2 and dy never leave the workgroup), with dZ2 row-major + the
     LDS-staged dW2 kernel and with dZ2 in the fragment layout + the LDS-free dW2 kernel, against
     the fused forward + fused backward pair (csrc/mlp_fused.hip) it replaces: same predictions,
     loss and gradients up to the fp32 summation order, bit-identical dZ2; the spread scratch
-    must be left zeroed."""
+    must be left zeroed. "step_frag" is the 128-row-pass kernel streaming W2 and W2^T
+    (mlp2_step128_kernel; B = 4160 and 64 end in a half pass), "step_frag64" the 64-row one."""
     from wellflow.data.synth import synth_tabular_batch
     from wellflow.models.mlp import MLP_RED_COPY_FLOATS, NativeMLP, init_mlp_flat
 
@@ -406,8 +407,12 @@ def test_mlp_one_launch_step_matches_two_kernel_step(B, F, indexed):
     if indexed:
         X = X.to(torch.bfloat16)
     out = {}
-    for name, fused, frag in (("pair", False, False), ("step", True, False), ("step_frag", True, True)):
+    w2t = eng.w2t
+    assert w2t is not None  # the default engine streams both weight images
+    for name, fused, frag in (("pair", False, False), ("step", True, False), ("step_frag", True, True),
+                              ("step_frag64", True, True)):
         eng.step_fused, eng.dw2_frag = fused, frag
+        eng.w2t = None if name == "step_frag64" else w2t
         eng.dZ[1].fill_(float("nan"))
         ls = eng.forward_backward(X, Y, grad_scale=1.0 / B, rows=idx).item()
         torch.cuda.synchronize()
@@ -416,7 +421,7 @@ def test_mlp_one_launch_step_matches_two_kernel_step(B, F, indexed):
         assert eng.red[:MLP_RED_COPY_FLOATS].abs().max().item() == 0.0, name
     assert eng._recompute_ok(B)
     la, pa, ga, za = out["pair"]
-    for name in ("step", "step_frag"):
+    for name in ("step", "step_frag", "step_frag64"):
         lb, pb, gb, zb = out[name]
         torch.testing.assert_close(pa, pb, rtol=1e-5, atol=1e-6)
         assert abs(la - lb) <= 1e-5 * abs(la) + 1e-7, name

@@ -172,7 +172,10 @@ def test_fused_device_adam(n):
     p = torch.randn(n, device=DEV)
     g = torch.zeros(n, device=DEV)
     shadow = torch.empty(n, dtype=torch.bfloat16, device=DEV)
-    opt = FlatAdam(p, g, lr=1e-3, shadow=shadow, zero_grads=True)
+    # + a transposed bf16 copy of one [rows][cols] block at an unaligned offset (MLP W2^T)
+    t_off, t_r, t_c = 7, 24, 40
+    shadow_t = torch.empty(t_r * t_c, dtype=torch.bfloat16, device=DEV)
+    opt = FlatAdam(p, g, lr=1e-3, shadow=shadow, zero_grads=True, shadow_t=(shadow_t, t_off, t_r, t_c))
     pr = p.clone().requires_grad_(True)
     ref = torch.optim.Adam([pr], lr=1e-3)
     for step in range(1, 6):
@@ -186,6 +189,8 @@ def test_fused_device_adam(n):
         assert g.abs().max().item() == 0.0
     assert torch.allclose(p, pr.detach(), atol=1e-6, rtol=1e-5)
     assert torch.equal(shadow, p.to(torch.bfloat16))
+    want_t = p[t_off : t_off + t_r * t_c].view(t_r, t_c).t().contiguous().to(torch.bfloat16).view(-1)
+    assert torch.equal(shadow_t, want_t)
 
 
 def test_losses():
