@@ -384,10 +384,13 @@ __global__ __launch_bounds__(512, 1) void cnn_bwd_kernel(
           unsigned v = pk_bf16(p[2 * h], p[2 * h + 1]);
           if constexpr (DROP) v = drop_pk(v, pm[h], 2 * b);
           a[h] = relu_pk(v);
-          // (inline asm: the compiler rewrote the min / multiply into 6 compares and selects)
+          // (inline asm: the compiler rewrote the min / multiply into 6 compares and selects).
+          // dp feeds an MFMA operand next, and hipcc pads nothing inside an asm string: the
+          // VALU-write -> MFMA-operand wait states are the s_nop 1 at its end (without it the
+          // MFMA read stale dp on some blocks: NaN conv-weight gradients)
           unsigned one, d = pk_bf16(dA[2 * h], dA[2 * h + 1]);
           asm("v_pk_min_u16 %0, %1, %2" : "=v"(one) : "v"(a[h]), "s"(0x00010001u));
-          asm("v_pk_mul_lo_u16 %0, %1, %2" : "=v"(dp[h]) : "v"(d), "v"(one));
+          asm("v_pk_mul_lo_u16 %0, %1, %2\n\ts_nop 1" : "=v"(dp[h]) : "v"(d), "v"(one));
         }
         // act^T and dP^T as A operands: A[f = l15][w = 4q + jj]
         acc_wd[tt][b] = mfma16(frag(a[0], a[1]), doB, acc_wd[tt][b]);
