@@ -213,6 +213,13 @@ __global__ __launch_bounds__(512, 1) void cnn_fwd_kernel(
         out = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
             wp[p], frag8(act[2 * p][0], act[2 * p][1], act[2 * p + 1][0], act[2 * p + 1][1]), out, 0, 0, 0);
       out = mfma16(w6, frag(act[6][0], act[6][1]), out);
+      // xb stays live to the end of the step: with its registers free right after the last conv
+      // MFMA, hipcc reallocated them to the next VALU result in the very next instruction, and in
+      // the dropout build that corrupted 2 % of dOut on this hardware (a VALU write of an MFMA's
+      // SrcB at 0 wait states; bit-exact against a bf16 emulation with this line,
+      // tests/test_engines_gpu.py::test_native_cnn_bit_exact_vs_bf16_emulation,
+      // profiles/r5/mfma_srcb_war.md)
+      asm volatile("" ::"v"(xb));
 #pragma unroll
       for (int p = 0; p < 3; ++p) wp[p] = wpn[p];
       w6 = w6n;

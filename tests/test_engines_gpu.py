@@ -83,6 +83,52 @@ def _flat_grad(ref):
     return g.to_flat().to(DEV)
 
 
+@pytest.mark.parametrize("loss,B,p", [("mse", 1000, 0.5), ("mae_clip", 4096, 0.5), ("mse", 64, 0.5), ("mse", 1000, 0.0),
+                                      ("mae_clip", 65536, 0.5)])
+def test_native_cnn_bit_exact_vs_bf16_emulation(loss, B, p):
+    """The fused CNN step against a torch emulation of ITS OWN roundings (bf16 x, weights,
+    pre-activation, dOut x keep-scale and dAct; fp32 sums) with the same dropout mask: dOut and
+    both weight gradients agree to fp32 summation order. The fp32-reference tests above have
+    2-5 % tolerances (bf16 vs fp32), which a corrupted MFMA operand passed in round 5 (2 % of
+    dOut wrong from a VALU write of the conv MFMA's SrcB at 0 wait states); this one does not."""
+    from wellflow.models.base import per_element_loss
+    from wellflow.models.cnn import CNN1DRegressor, NativeCNN, cnn_dropout_mask
+
+    bf = lambda t: t.to(torch.bfloat16).float()  # noqa: E731
+    torch.manual_seed(2)
+    ref = CNN1DRegressor(dropout=p).init_keras(4).to(DEV)
+    with torch.no_grad():
+        ref.conv.bias.uniform_(-0.05, 0.05)
+        ref.dense.bias.uniform_(-0.1, 0.1)
+    eng = NativeCNN(ref.layout, batch=max(4096, B), device=DEV, dropout=p, loss=loss, seed=7)
+    eng.params.copy_(ref.to_flat().to(DEV))
+    eng.sync_weights()
+    x, y = torch.randn(B, 48, 1, device=DEV), torch.randn(B, 12, device=DEV)
+    eng.rng.fill_(5)
+    eng.forward_backward(x, y, grad_scale=1.0 / (B * 12))
+    torch.cuda.synchronize()
+    ks = 2.0 if p > 0 else 1.0
+    mask = cnn_dropout_mask(eng.seed32, 5, B, 36, eng.lay.Fp, device=DEV)[:, :, :100].float()
+    if p == 0:
+        mask = torch.ones_like(mask)
+    Wc, bc = ref.conv.weight.detach().view(100, 13), ref.conv.bias.detach()
+    Wd, bd = ref.dense.weight.detach().view(12, 36, 100), ref.dense.bias.detach()
+    xw = bf(x.view(B, 48))
+    win = torch.stack([xw[:, t : t + 13] for t in range(36)], 1)  # [B, T, taps]
+    act = torch.relu(bf(win @ bf(Wc).t() + bf(bc))) * mask
+    o = (torch.einsum("btf,jtf->bj", act, bf(Wd)) * ks + bd).requires_grad_(True)
+    per_element_loss(loss, o, y).sum().mul(1.0 / (B * 12)).backward()
+    doA = bf(o.grad * ks)
+    gWd = torch.einsum("btf,bj->jtf", act, doA)
+    dp = bf(torch.einsum("bj,jtf->btf", doA, bf(Wd))) * (act != 0).float()
+    gWc = torch.cat([torch.einsum("btf,btk->fk", dp, win), dp.sum((0, 1))[:, None]], 1)
+    Wc_n, Wd_n, _ = eng.lay.views(eng.grads)
+    rel = lambda a, b: ((a - b).norm() / b.norm()).item()  # noqa: E731
+    assert rel(eng.dout[: B * 16].view(B, 16)[:, :12], o.grad) < 1e-4
+    assert rel(Wd_n[:12].view(12, 36, 112)[:, :, :100], gWd) < 1e-4
+    assert rel(Wc_n[:100, :14], gWc) < 1e-4
+
+
 @pytest.mark.parametrize("loss,B", [("mse", 1000), ("mae_clip", 4096), ("mae_clip", 65536)])
 def test_native_cnn_dropout_matches_fp32_same_mask(loss, B):
     """The fused CNN step with dropout 0.5 (csrc/cnn_fused.hip) against the fp32 reference
