@@ -154,18 +154,29 @@ __global__ __launch_bounds__(512, 1) void cnn_fwd_kernel(
   __syncthreads();
 
   const int ngroups = (B + 15) >> 4;
-  for (int g = blockIdx.x * CNN_NW + wid; g < ngroups; g += gridDim.x * CNN_NW) {
+  // the lane's x samples, loaded one group AHEAD (issued before this group's 36 steps, consumed
+  // a group later): raw float4s from a clamped in-range address, bounds applied at consumption
+  float4 xnx[XR / 4];
+  auto load_x = [&](int g) {
+    const int wc = min(g * 16 + l15, B - 1);
+#pragma unroll
+    for (int k = 0; k < XR / 4; ++k)
+      xnx[k] = *reinterpret_cast<const float4*>(x + (size_t)wc * L + min(4 * q + 4 * k, L - 4));
+  };
+  const int gstride = gridDim.x * CNN_NW;
+  if ((int)blockIdx.x * CNN_NW + wid < ngroups) load_x(blockIdx.x * CNN_NW + wid);
+  for (int g = blockIdx.x * CNN_NW + wid; g < ngroups; g += gstride) {
     const int w = g * 16 + l15;  // this lane's window (B-operand column)
     const bool wok = w < B;
     unsigned xp[XR / 2];  // bf16 pairs (x[w][4q + 2i], x[w][4q + 2i + 1])
-    const float* xr = x + (size_t)(wok ? w : 0) * L + 4 * q;
 #pragma unroll
     for (int k = 0; k < XR / 4; ++k) {
-      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (wok && 4 * q + 4 * k + 4 <= L) v = *reinterpret_cast<const float4*>(xr + 4 * k);
-      xp[2 * k] = pk_bf16(v.x, v.y);
-      xp[2 * k + 1] = pk_bf16(v.z, v.w);
+      const bool ok = wok && 4 * q + 4 * k + 4 <= L;
+      const float4 v = xnx[k];
+      xp[2 * k] = ok ? pk_bf16(v.x, v.y) : 0u;
+      xp[2 * k + 1] = ok ? pk_bf16(v.z, v.w) : 0u;
     }
+    load_x(min(g + gstride, ngroups - 1));  // (the last group re-loads itself: never read)
     f32x4 out = {0.f, 0.f, 0.f, 0.f};
     // dense-weight fragments of step t (pairs of 16-filter blocks as 16x16x32 A operands, block
     // 6 as a 16x16x16 one), prefetched one step ahead; the scheduling barrier at the end of
@@ -330,27 +341,44 @@ __global__ __launch_bounds__(512, 1) void cnn_bwd_kernel(
     for (int tt = 0; tt < TG; ++tt) acc_wd[tt][b] = f32x4{0.f, 0.f, 0.f, 0.f};
   }
 
+  // the group's global operands, loaded one group AHEAD (issued before the current group's
+  // MFMAs, consumed a group later): at one load round per group their L2 latency was exposed
+  // once per 16 windows. Raw values only; bounds selects are applied at consumption. Rows past
+  // B of dOut are zero in the buffer (the forward writes every row of the last group it owns);
+  // x addresses are clamped in range (the selects zero what they stand for).
+  struct GroupLoads {
+    float4 da;
+    float dbv[4], xa[TG + 3], xb[TG][4];
+  };
+  auto load_group = [&](int g, GroupLoads& G) {
+    const int w0 = g * 16;
+    G.da = *reinterpret_cast<const float4*>(dout + (size_t)(w0 + l15) * 16 + 4 * q);
+#pragma unroll
+    for (int jj = 0; jj < 4; ++jj) G.dbv[jj] = dout[(size_t)(w0 + 4 * q + jj) * 16 + l15];
+    const int wac = min(w0 + l15, B - 1);
+#pragma unroll
+    for (int i = 0; i < TG + 3; ++i) G.xa[i] = x[(size_t)wac * L + min(t0 + 4 * q + i, L - 1)];
+#pragma unroll
+    for (int tt = 0; tt < TG; ++tt)
+#pragma unroll
+      for (int jj = 0; jj < 4; ++jj) G.xb[tt][jj] = x[(size_t)min(w0 + 4 * q + jj, B - 1) * L + min(t0 + tt + l15, L - 1)];
+  };
+  GroupLoads nxt;
+  if (g_begin + wid < g_end) load_group(g_begin + wid, nxt);
   for (int g = g_begin + wid; g < g_end; g += CNN_NW) {
     const int w0 = g * 16;
-    // dOut (x keep_scale) as A[w = l15][j = 4q + jj] and as B[w = 4q + jj][j = l15]; rows past B
-    // are zero in the buffer (the forward writes every row of the last group it owns)
-    const float4 da = *reinterpret_cast<const float4*>(dout + (size_t)(w0 + l15) * 16 + 4 * q);
+    const GroupLoads cur = nxt;
+    load_group(min(g + CNN_NW, g_end - 1), nxt);  // (the last group re-loads itself: never read)
+    // dOut (x keep_scale) as A[w = l15][j = 4q + jj] and as B[w = 4q + jj][j = l15]
+    const float4 da = cur.da;
     const bf16x4 doA = frag(pk_bf16(da.x * keep_scale, da.y * keep_scale), pk_bf16(da.z * keep_scale, da.w * keep_scale));
-    float dbv[4];
-#pragma unroll
-    for (int jj = 0; jj < 4; ++jj) dbv[jj] = dout[(size_t)(w0 + 4 * q + jj) * 16 + l15] * keep_scale;
-    const bf16x4 doB = frag(pk_bf16(dbv[0], dbv[1]), pk_bf16(dbv[2], dbv[3]));
+    const bf16x4 doB = frag(pk_bf16(cur.dbv[0] * keep_scale, cur.dbv[1] * keep_scale),
+                            pk_bf16(cur.dbv[2] * keep_scale, cur.dbv[3] * keep_scale));
     // x of this lane's window for the A operand: x[w0 + l15][t0 + 4q + i], i < TG + 3
-    // (branch-free: every load reads a clamped, in-range address and a select applies the
-    // bounds, instead of an exec-masked branch around each load)
-    const int wa = w0 + l15, wac = min(wa, B - 1);
+    const int wa = w0 + l15;
     float xa[TG + 3];
 #pragma unroll
-    for (int i = 0; i < TG + 3; ++i) {
-      const int s = t0 + 4 * q + i;
-      const float v = x[(size_t)wac * L + min(s, L - 1)];
-      xa[i] = (wa < B && s < L) ? v : 0.f;
-    }
+    for (int i = 0; i < TG + 3; ++i) xa[i] = (wa < B && t0 + 4 * q + i < L) ? cur.xa[i] : 0.f;
     // x of the four windows w0 + 4q + jj at sample t + l15 for the dWc B operand
     float xb[TG][4];
 #pragma unroll
@@ -358,8 +386,7 @@ __global__ __launch_bounds__(512, 1) void cnn_bwd_kernel(
 #pragma unroll
       for (int jj = 0; jj < 4; ++jj) {
         const int wb = w0 + 4 * q + jj, s = t0 + tt + l15;
-        const float v = x[(size_t)min(wb, B - 1) * L + min(s, L - 1)];
-        xb[tt][jj] = (kx && wb < B && s < L) ? v : kone;
+        xb[tt][jj] = (kx && wb < B && s < L) ? cur.xb[tt][jj] : kone;
       }
 #pragma unroll
     for (int tt = 0; tt < TG; ++tt) {
