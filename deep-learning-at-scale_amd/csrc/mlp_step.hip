@@ -467,7 +467,7 @@ __global__ __launch_bounds__(512, 1) void mlp2_step_kernel(
 // Rows past B are masked (dy = 0, no stores); FRAG fragments of rows >= B are not written.
 __device__ __forceinline__ int x4_off(int row, int chunk) { return row * 64 + ((chunk ^ ((row >> 2) & 3)) << 4); }
 
-template <int NFT>
+template <int NFT, bool MASK>
 __global__ __launch_bounds__(512, 1) void mlp2_step128_kernel(
     const bf16_t* __restrict__ X, int Fp, const bf16_t* __restrict__ W1, const float* __restrict__ b1,
     const bf16_t* __restrict__ W2, const bf16_t* __restrict__ W2T, const float* __restrict__ b2,
@@ -643,7 +643,7 @@ __global__ __launch_bounds__(512, 1) void mlp2_step128_kernel(
 
     // ---- prediction, dy, loss of rows 16n + l15; wave 0 lane group g owns rows 16n + l15 for
     // n = g and n = g + 4 (their loss, db3 and prediction store)
-    float dyn[NR], pst[2] = {0.f, 0.f};
+    float dyn[NR], pst[2] = {0.f, 0.f}, pdy[2] = {0.f, 0.f};
     int pgr[2] = {-1, -1};
 #pragma unroll
     for (int n = 0; n < NR; ++n) {
@@ -657,11 +657,29 @@ __global__ __launch_bounds__(512, 1) void mlp2_step128_kernel(
         dyn[n] = dy_scale * diff;
         if (wid == 0 && (n & 3) == g) {
           pst[n >> 2] = p;
+          pdy[n >> 2] = dyn[n];
           pgr[n >> 2] = gr;
           lsum += diff * diff;
           db3a += dyn[n];
         }
       }
+    }
+    // MASK: the [H2 > 0] bits instead of dZ2 for the dW2 kernel (dZ2 = bf16(dy w3) where set, so
+    // dy and the bits rebuild it bit for bit): ballot (m, n, r) = rows 16n + (bit & 15) of unit
+    // u0 + 16m + 4(bit >> 4) + r, gathered into lane k = (m * 8 + n) * 4 + r
+    unsigned mlo = 0u, mhi = 0u;
+    if constexpr (MASK) {
+#pragma unroll
+      for (int m = 0; m < MT; ++m)
+#pragma unroll
+        for (int n = 0; n < NR; ++n)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const unsigned long long bl = __ballot(acc[m][n][r] > 0.f);
+            const bool mine = lnv == (m * NR + n) * 4 + r;
+            mlo = mine ? (unsigned)bl : mlo;
+            mhi = mine ? (unsigned)(bl >> 32) : mhi;
+          }
     }
     // ---- dZ2 = dy w3^T * [H2 > 0] (own units) -> zs; dw3, db2 partials
 #pragma unroll
@@ -688,6 +706,16 @@ __global__ __launch_bounds__(512, 1) void mlp2_step128_kernel(
 #pragma unroll
       for (int r = 0; r < 4; ++r) asm volatile("" : "+v"(sum3[m][r]), "+v"(sum2[m][r]));
     asm volatile("" : "+v"(lsum), "+v"(db3a));
+    if constexpr (MASK) {
+      // the pass's bits (wave w: 512 B at word (ps * 8 + w) * 64) and dy of its rows (< B), stored
+      // here (kept to after dH1 the two words pushed the kernel into 23 more spills)
+      unsigned long long* mk = reinterpret_cast<unsigned long long*>(dZ2);
+      float* dyo = reinterpret_cast<float*>(reinterpret_cast<char*>(dZ2) + (size_t)npass * 4096);
+      mk[((size_t)ps * NW + wid) * 64 + lnv] = ((unsigned long long)mhi << 32) | mlo;
+#pragma unroll
+      for (int q = 0; q < 2; ++q)
+        if (pgr[q] >= 0) dyo[pgr[q]] = pdy[q];
+    }
     if (ps + (int)gridDim.x < npass) stage(par ^ 1);
     __syncthreads();  // B4: dZ2 complete, next pass's X / y staged
     if (ps + 2 * (int)gridDim.x < npass) prefetch(ps + 2 * gridDim.x);
@@ -725,7 +753,7 @@ __global__ __launch_bounds__(512, 1) void mlp2_step128_kernel(
     // ---- dZ2 copy-out as dW2 A fragments (fragment (S, b) = 32 rows x 16 units; wave w writes
     // fragments 8w .. 8w + 7 of the pass: row group S = row0 / 32 + (f >> 4), unit block f & 15)
 #pragma unroll
-    for (int q = 0; q < 8; ++q) {
+    for (int q = 0; q < (MASK ? 0 : 8); ++q) {
       const int f = 8 * wid + q, sst = f >> 4, b = f & 15;
       if (row0 + 32 * sst < B) {
         bf16x8 v;
@@ -1028,12 +1056,209 @@ __global__ __launch_bounds__(512, 1) void mlp2_dw2f_kernel(const bf16_t* __restr
           atomicAdd(dst + (size_t)(128 * wm + 16 * mb + 4 * g + r) * MF_H + n0 + 16 * nb + l15, acc[mb][nb][r]);
   }
 }
+
+// ----------------------------------------------------------------------------------------
+// dW2 from the [H2 > 0] bits and dy (mlp2_step128_kernel<., MASK = true>) instead of a stored
+// dZ2: 36 B per row from HBM instead of 512 (round-5; the dZ2 round trip was 134 MB written +
+// 134 MB read per step at B = 262,144). The same tile, MFMAs and order as mlp2_dw2f_kernel, so
+// dW2 is bit-identical; the 32 dZ2 fragments of a 64-row chunk are rebuilt in LDS from the
+// bits (dZ2 = bf16(dy w3[u]) where set): each wave rebuilds 4 fragments of the NEXT chunk
+// while the workgroup computes this one, so one barrier per chunk still suffices.
+//  * DMA ring (4 slots, 3 chunks ahead) per chunk: the 2-KiB bit block (waves 0-1: 16 runs of
+//    128 B, one per (step-kernel wave, unit tile)), the chunk's 64 dy (wave 2) and the X tile
+//    (waves 0-3, as mlp2_dw2f_kernel); rebuilt fragments in a 2 x 32-KiB double buffer.
+constexpr int DW2M_SLOTS = 4;
+constexpr int DW2M_MB = 2048, DW2M_DYB = 1024, DW2M_XB = MF_ROWS * 64;
+constexpr int DW2M_SLOT = DW2M_MB + DW2M_DYB + DW2M_XB;
+constexpr int DW2M_FRAG = 32 * 1024;
+__global__ __launch_bounds__(512, 1) void mlp2_dw2m_kernel(const unsigned long long* __restrict__ mk,
+                                                           const float* __restrict__ dyo, const bf16_t* __restrict__ X,
+                                                           int Fp, const long long* __restrict__ rows, long nrows,
+                                                           const bf16_t* __restrict__ W1, const float* __restrict__ b1,
+                                                           const float* __restrict__ w3, int kchunk,
+                                                           float* __restrict__ dW2, float* __restrict__ slab,
+                                                           int slab_row0, int prio) {
+  __shared__ __attribute__((aligned(16))) char smem[DW2M_SLOTS * DW2M_SLOT + 2 * DW2M_FRAG + DW2F_MAX_ROWS * 4];
+  char* fragb = smem + DW2M_SLOTS * DW2M_SLOT;
+  int* ridx = reinterpret_cast<int*>(fragb + 2 * DW2M_FRAG);
+  const int tid = threadIdx.x, lane = tid & 63, l15 = lane & 15, g = lane >> 4;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6), wm = wid >> 2;
+  const int L = xcd_remap(blockIdx.x, gridDim.x);
+  const int split = L >> 1, t = L & 1;
+  const int n0 = 128 * t + 32 * (wid & 3);
+  const int kbeg = split * kchunk, nch = kchunk / MF_ROWS;
+  for (int i = tid; i < kchunk; i += 512) ridx[i] = rows != nullptr ? (int)data_row(rows, kbeg + i, nrows) : kbeg + i;
+  __syncthreads();
+  if (prio && wid >= 4) __builtin_amdgcn_s_setprio(1);
+
+  bf16x8 w1f[2];
+  float bias[2];
+#pragma unroll
+  for (int nb = 0; nb < 2; ++nb) {
+    const int u = n0 + 16 * nb + l15;
+    w1f[nb] = 8 * g + 8 <= Fp ? *reinterpret_cast<const bf16x8*>(W1 + (size_t)u * Fp + 8 * g)
+                              : bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
+    bias[nb] = b1[u];
+  }
+  // the 4 fragments this wave rebuilds per chunk: f = 4 wid + qq -> (32-row step f >> 4, unit
+  // block f & 15); lane unit u = 16 b + l15 = step-kernel wave b >> 1, tile b & 1, lane group
+  // l15 >> 2, r = l15 & 3; its 8 rows 8g .. 8g + 7 of the step sit in bits 16 (l15 >> 2) + 8 (g & 1)
+  // of the ballot word of tile n' = 2 (f >> 4) + (g >> 1) of the chunk's half pass
+  float w3u[4];
+  int wofs[4];
+#pragma unroll
+  for (int qq = 0; qq < 4; ++qq) {
+    const int f = 4 * wid + qq, s2 = f >> 4, b = f & 15;
+    w3u[qq] = w3[16 * b + l15];
+    wofs[qq] = (((b >> 1) * 2 + (b & 1)) * 16 + (2 * s2 + (g >> 1)) * 4 + (l15 & 3)) * 8;
+  }
+  const int bsh = 16 * (l15 >> 2) + 8 * (g & 1);
+
+  const int xrow = 16 * (wid & 3) + (lane >> 2);
+  int xq = (lane & 3) ^ ((xrow >> 3) & 3);
+  if (8 * xq + 8 > Fp) xq = 0;
+  auto issue = [&](int c, int slot) {
+    char* st = smem + slot * DW2M_SLOT;
+    const int r0 = kbeg + c * MF_ROWS, ps = r0 >> 7, hh = (r0 >> 6) & 1;
+    if (wid < 2) {  // bit block: 16 runs of 128 B (step-kernel wave w, tile m: words n' = 4 hh .. 4 hh + 3)
+      const int o = wid * 1024 + lane * 16, sg = o >> 7;
+      const char* src = reinterpret_cast<const char*>(mk) +
+                        ((((size_t)ps * 8 + (sg >> 1)) * 64 + ((sg & 1) * 8 + 4 * hh) * 4) * 8 + (o & 127));
+      __builtin_amdgcn_global_load_lds((const void*)src, (lds_void*)(st + wid * 1024), 16, 0, 0);
+    } else if (wid == 2) {  // dy of the 64 rows (lanes 16.. repeat lanes 0..15)
+      __builtin_amdgcn_global_load_lds((const void*)(dyo + r0 + 4 * (lane & 15)), (lds_void*)(st + DW2M_MB), 16, 0, 0);
+    }
+    if (wid < 4) {
+      const size_t xr = (size_t)ridx[c * MF_ROWS + xrow];
+      __builtin_amdgcn_global_load_lds((const void*)(X + xr * Fp + 8 * xq),
+                                       (lds_void*)(st + DW2M_MB + DW2M_DYB + wid * 1024), 16, 0, 0);
+    }
+  };
+  // at most n chunks' DMAs of this wave in flight (waves 0-2 issue 2 per chunk, wave 3 one)
+  auto dma_wait = [&](auto nc) {
+    constexpr int n = decltype(nc)::value;
+    if (wid < 3)
+      wait_vmcnt<2 * n>();
+    else if (wid == 3)
+      wait_vmcnt<n>();
+  };
+  // rebuild this wave's 4 fragments of the chunk in DMA slot `slot` into fragment buffer fb
+  auto rebuild = [&](int slot, char* fb) {
+    const char* st = smem + slot * DW2M_SLOT;
+#pragma unroll
+    for (int qq = 0; qq < 4; ++qq) {
+      const int f = 4 * wid + qq, s2 = f >> 4;
+      const unsigned long long word = *reinterpret_cast<const unsigned long long*>(st + wofs[qq]);
+      const unsigned bits = (unsigned)(word >> bsh);
+      const float4 d0 = *reinterpret_cast<const float4*>(st + DW2M_MB + (32 * s2 + 8 * g) * 4);
+      const float4 d1 = *reinterpret_cast<const float4*>(st + DW2M_MB + (32 * s2 + 8 * g + 4) * 4);
+      const float dv[8] = {d0.x, d0.y, d0.z, d0.w, d1.x, d1.y, d1.z, d1.w};
+      unsigned pk[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const unsigned lo = (bits >> (2 * i)) & 1u ? 0x0000FFFFu : 0u, hi = (bits >> (2 * i + 1)) & 1u ? 0xFFFF0000u : 0u;
+        pk[i] = pk_bf16(dv[2 * i] * w3u[qq], dv[2 * i + 1] * w3u[qq]) & (lo | hi);
+      }
+      *reinterpret_cast<uint4*>(fb + f * 1024 + lane * 16) = make_uint4(pk[0], pk[1], pk[2], pk[3]);
+    }
+  };
+  const int xg = 8 * g + 8 <= Fp ? g : 0;
+  const int xr0 = 8 * (l15 >> 2) + (l15 & 3);
+
+  f32x4 acc[8][2];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int last = nch - 1;
+#pragma unroll
+  for (int k = 0; k < DW2M_SLOTS - 1; ++k) issue(min(k, last), k);
+  dma_wait(std::integral_constant<int, DW2M_SLOTS - 2>{});  // chunk 0 (this wave's pieces)
+  __builtin_amdgcn_s_barrier();                              // ... every wave's
+  asm volatile("" ::: "memory");
+  rebuild(0, fragb);
+  for (int c = 0; c < nch; ++c) {
+    const int slot = c & (DW2M_SLOTS - 1);
+    // chunk c + 1's pieces landed (this wave); the barrier publishes them and chunk c's rebuilt
+    // fragments, and frees fragment buffer (c + 1) & 1 and DMA slot (c - 1) & 3
+    dma_wait(std::integral_constant<int, DW2M_SLOTS - 3>{});
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    issue(min(c + DW2M_SLOTS - 1, last), (c + DW2M_SLOTS - 1) & (DW2M_SLOTS - 1));
+    if (c + 1 < nch) rebuild((c + 1) & (DW2M_SLOTS - 1), fragb + ((c + 1) & 1) * DW2M_FRAG);
+    const char* st = smem + slot * DW2M_SLOT;
+    const char* xs = st + DW2M_MB + DW2M_DYB;
+    const char* fa = fragb + (c & 1) * DW2M_FRAG;
+    bf16x8 xfa[2][2], afa[2][8];
+    auto frags = [&](int s2) {
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int r = 32 * s2 + xr0 + 4 * h;
+        xfa[s2][h] = *reinterpret_cast<const bf16x8*>(xs + r * 64 + ((xg ^ ((r >> 3) & 3)) << 4));
+      }
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int mb = 0; mb < 8; ++mb)
+        afa[s2][mb] = *reinterpret_cast<const bf16x8*>(fa + (s2 * 16 + 8 * wm + mb) * 1024 + lane * 16);
+    };
+    frags(0);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) {
+      bf16x8 hb[2];
+      const bf16x8(&xf)[2] = xfa[s2];
+#pragma unroll
+      for (int nb = 0; nb < 2; ++nb) {
+        const f32x4 c0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xf[0], w1f[nb], f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+        const f32x4 c1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xf[1], w1f[nb], f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+        const unsigned p0 = pk_bf16(fmaxf(c0[0] + bias[nb], 0.f), fmaxf(c0[1] + bias[nb], 0.f));
+        const unsigned p1 = pk_bf16(fmaxf(c0[2] + bias[nb], 0.f), fmaxf(c0[3] + bias[nb], 0.f));
+        const unsigned p2 = pk_bf16(fmaxf(c1[0] + bias[nb], 0.f), fmaxf(c1[1] + bias[nb], 0.f));
+        const unsigned p3 = pk_bf16(fmaxf(c1[2] + bias[nb], 0.f), fmaxf(c1[3] + bias[nb], 0.f));
+        typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
+        hb[nb] = __builtin_bit_cast(bf16x8, (u32x4_t{p0, p1, p2, p3}));
+      }
+      if (s2 == 0) {
+        __builtin_amdgcn_sched_barrier(0);
+        frags(1);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+#pragma unroll
+      for (int mb = 0; mb < 8; ++mb) {
+#pragma unroll
+        for (int nb = 0; nb < 2; ++nb)
+          acc[mb][nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(afa[s2][mb], hb[nb], acc[mb][nb], 0, 0, 0);
+      }
+    }
+  }
+  wait_vmcnt<0>();  // the clamped fetches past the range must land before the workgroup ends
+  const int srow = slab_row0 + split;
+  if (srow < kMlpRedSlab2Rows) {
+    float* dst = slab + (size_t)srow * 65536;
+#pragma unroll
+    for (int mb = 0; mb < 8; ++mb)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int nb = 0; nb < 2; ++nb) dst[(size_t)(128 * wm + 16 * mb + 4 * g + r) * MF_H + n0 + 16 * nb + l15] = acc[mb][nb][r];
+  } else {
+    float* dst = dW2 + (size_t)(split & (kMlpRedCopies2 - 1)) * 65536;
+#pragma unroll
+    for (int mb = 0; mb < 8; ++mb)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int nb = 0; nb < 2; ++nb)
+          atomicAdd(dst + (size_t)(128 * wm + 16 * mb + 4 * g + r) * MF_H + n0 + 16 * nb + l15, acc[mb][nb][r]);
+  }
+}
 }  // namespace
 
 bool launch_mlp2_step(const bf16_t* X, int Fp, const bf16_t* W1, const float* b1, const bf16_t* W2, const float* b2,
                       const float* w3, const float* b3, const float* y, float dy_scale, int B, const long long* rows,
                       long nrows, bf16_t* dZ2, float* pred, float* red, bool dz_frag, hipStream_t s,
-                      const bf16_t* W2T) {
+                      const bf16_t* W2T, bool dz_mask) {
   // the reduce sums the dW1 rows only when it expects the 8-wave backward's layout
   if (B <= 0 || Fp > 32 || Fp % 8 != 0 || red == nullptr || !mlp_bwd8()) return false;
   if (dz_frag && B % MF_ROWS != 0) return false;
@@ -1044,13 +1269,17 @@ bool launch_mlp2_step(const bf16_t* X, int Fp, const bf16_t* W1, const float* b1
   // static s_setprio 1 for waves 4-7 (+0.2 to +1.1 % in three interleaved pairs, chunk span
   // 17.5k -> 17.1k cycles, profiles/r4/mlp_prio; the WELLFLOW_STEP_PRIO A/B knob was removed)
   constexpr int prio = 1;
+  if (dz_mask && W2T == nullptr) return false;  // the [H2 > 0]-bit output exists in the 128-row kernel only
   if (W2T != nullptr && dz_frag && !stamp) {  // 128-row passes, both weight images streamed
-    if (Fp <= 16)
-      hipLaunchKernelGGL(mlp2_step128_kernel<1>, dim3(grid), dim3(512), 0, s, X, Fp, W1, b1, W2, W2T, b2, w3, b3, y,
-                         dy_scale, B, rows, nrows, dZ2, pred, red, prio);
-    else
-      hipLaunchKernelGGL(mlp2_step128_kernel<2>, dim3(grid), dim3(512), 0, s, X, Fp, W1, b1, W2, W2T, b2, w3, b3, y,
-                         dy_scale, B, rows, nrows, dZ2, pred, red, prio);
+#define WF_STEP128(NFT, MK)                                                                                      \
+  hipLaunchKernelGGL((mlp2_step128_kernel<NFT, MK>), dim3(grid), dim3(512), 0, s, X, Fp, W1, b1, W2, W2T, b2, w3, b3, \
+                     y, dy_scale, B, rows, nrows, dZ2, pred, red, prio)
+    if (Fp <= 16) {
+      if (dz_mask) WF_STEP128(1, true); else WF_STEP128(1, false);
+    } else {
+      if (dz_mask) WF_STEP128(2, true); else WF_STEP128(2, false);
+    }
+#undef WF_STEP128
     return true;
   }
   if (stamp && Fp <= 16 && dz_frag) {
@@ -1109,4 +1338,30 @@ int launch_mlp2_dw2f(const bf16_t* dZ2F, const bf16_t* X, int Fp, const long lon
   return srow < kMlpRedSlab2Rows ? srow : kMlpRedSlab2Rows;
 }
 
+
+int launch_mlp2_dw2m(const bf16_t* mkbuf, const bf16_t* X, int Fp, const long long* rows, long nrows, const bf16_t* W1,
+                     const float* b1, const float* w3, int B, int nsplit, float* red, hipStream_t s) {
+  if (B <= 0 || B % MF_ROWS != 0 || Fp > 32 || Fp % 8 != 0 || red == nullptr) return 0;
+  const unsigned long long* mk = reinterpret_cast<const unsigned long long*>(mkbuf);
+  const float* dyo = reinterpret_cast<const float*>(reinterpret_cast<const char*>(mkbuf) + (size_t)((B + 127) / 128) * 4096);
+  constexpr int kMaxBlock = 128 * DW2F_MAX_ROWS;
+  constexpr int prio = 1;
+  int srow = 0;
+  for (int r0 = 0; r0 < B; r0 += kMaxBlock) {
+    const int Bb = B - r0 < kMaxBlock ? B - r0 : kMaxBlock;
+    const int chunks = Bb / MF_ROWS;
+    int ns = nsplit < 1 ? 1 : (nsplit > 128 ? 128 : nsplit);
+    while (ns < 128 && (chunks + ns - 1) / ns * MF_ROWS > DW2F_MAX_ROWS) ++ns;
+    while (ns > 1 && chunks % ns != 0) --ns;
+    const int kchunk = (chunks / ns) * MF_ROWS;
+    if (kchunk > DW2F_MAX_ROWS) return 0;
+    // row block r0 (a multiple of 128 * 2048 rows: whole passes): its bit words start at pass r0 / 128
+    hipLaunchKernelGGL(mlp2_dw2m_kernel, dim3(2 * ns), dim3(512), 0, s, mk + (size_t)(r0 / 128) * 512, dyo + r0,
+                       rows != nullptr ? X : X + (size_t)r0 * Fp, Fp, rows != nullptr ? rows + r0 : nullptr,
+                       rows != nullptr ? nrows : (long)Bb, W1, b1, w3, kchunk, red + (size_t)kMlpRedCopies * kMlpRedRow,
+                       red + kMlpRedSlab2Off, srow, prio);
+    srow += ns;
+  }
+  return srow < kMlpRedSlab2Rows ? srow : kMlpRedSlab2Rows;
+}
 }  // namespace wf

@@ -204,6 +204,10 @@ class NativeMLP:
         self.w2t = None
         if (self.red is not None and self.dw2_frag and os.environ.get("WELLFLOW_MLP_STEP128", "1") != "0"):
             self.w2t = torch.empty(256 * 256, dtype=bf, device=dev)
+        # ... and instead of dZ2 (512 B per row through HBM) only the [H2 > 0] bits and dy (36 B),
+        # from which the dW2 kernel rebuilds dZ2 bit for bit (mlp2_dw2m_kernel; WELLFLOW_MLP_DW2M=0:
+        # the fragment-layout dZ2)
+        self.dw2_mask = self.w2t is not None and os.environ.get("WELLFLOW_MLP_DW2M", "1") != "0"
         self.sync_weights()
 
     @property
@@ -240,11 +244,15 @@ class NativeMLP:
         try:
             if red is not None and self.step_fused and not self.dw2_gemm:
                 frag = self.dw2_frag
+                w2t = self.w2t if frag else None
+                mask = w2t is not None and self.dw2_mask
                 if not C.mlp2_step(Xop, self.Fp, wl[0][0], pl[0][1], wl[1][0], pl[1][1], hw, hb, y,
-                                   2.0 * float(grad_scale), B, rows, self.dZ[1], self.pred, red, frag,
-                                   self.w2t if frag else None):
+                                   2.0 * float(grad_scale), B, rows, self.dZ[1], self.pred, red, frag, w2t, mask):
                     raise RuntimeError("NativeMLP: fused step refused the shape")
-                if frag:  # dW2 partials as slab rows (their count) summed by the reduce
+                if mask:  # dZ2 rebuilt from the bits + dy in the dW2 kernel
+                    ok = dw2_rows = C.mlp2_dw2m(self.dZ[1], Xop, self.Fp, rows, wl[0][0], pl[0][1], hw, B,
+                                                self.dw2f_split, red)
+                elif frag:  # dW2 partials as slab rows (their count) summed by the reduce
                     ok = dw2_rows = C.mlp2_dw2f(self.dZ[1], Xop, self.Fp, rows, wl[0][0], pl[0][1], B,
                                                 self.dw2f_split, red)
                 else:
