@@ -352,7 +352,9 @@ __global__ __launch_bounds__(256) void dw_slab_reduce_kernel(float* __restrict__
   reinterpret_cast<float4*>(out)[i] = a;
 }
 
-// 256x288, 8 waves of 64x144, 4-slot 32-deep ring (136 KiB; a 2-stage 64-deep ring spilled 61 VGPRs)
+// 256x288, 8 waves of 64x144, 4-slot 32-deep ring (136 KiB; a 2-stage 64-deep ring spilled 61 VGPRs).
+// Round 5: 4 waves of 128x144 (one per SIMD, accumulators in AGPRs; 35 % fewer LDS fragment
+// reads) measured 1.18-1.25 vs 1.03 ms standalone (tools/dw_tiles.py, profiles/r5/notes.md): removed
 // (default: 1.107 vs 1.166 ms for 256x192 standalone, 1.150 vs 1.178 ms inside the bench step): N = 576 = 2 x 288, 24 % more
 // FLOP per staged byte than 256x192 (the dW loop's LDS-DMA bytes per CU per step, not its
 // MFMAs or the DMA latency, track its time across tiles: 256x128 1.33, 256x192 1.17 ms)

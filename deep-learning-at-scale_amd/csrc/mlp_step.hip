@@ -1059,18 +1059,20 @@ __global__ __launch_bounds__(512, 1) void mlp2_dw2f_kernel(const bf16_t* __restr
 
 // ----------------------------------------------------------------------------------------
 // dW2 from the [H2 > 0] bits and dy (mlp2_step128_kernel<., MASK = true>) instead of a stored
-// dZ2: 36 B per row from HBM instead of 512 (round-5; the dZ2 round trip was 134 MB written +
-// 134 MB read per step at B = 262,144). The same tile, MFMAs and order as mlp2_dw2f_kernel, so
-// dW2 is bit-identical; the 32 dZ2 fragments of a 64-row chunk are rebuilt in LDS from the
-// bits (dZ2 = bf16(dy w3[u]) where set): each wave rebuilds 4 fragments of the NEXT chunk
-// while the workgroup computes this one, so one barrier per chunk still suffices.
-//  * DMA ring (4 slots, 3 chunks ahead) per chunk: the 2-KiB bit block (waves 0-1: 16 runs of
-//    128 B, one per (step-kernel wave, unit tile)), the chunk's 64 dy (wave 2) and the X tile
-//    (waves 0-3, as mlp2_dw2f_kernel); rebuilt fragments in a 2 x 32-KiB double buffer.
+// dZ2: 36 B per row from HBM instead of 512 (round 5; the dZ2 round trip was 134 MB written +
+// 134 MB read per step at B = 262,144). dZ2 = bf16(dy w3[u]) where a bit is set, so the rebuilt
+// fragments equal mlp2_dw2f_kernel's input bit for bit.
+//  * workgroup = 128 (out) x 256 (in) tile of one row range (mlp2_dw2f_kernel: 256 x 128): wave w
+//    owns in columns 32w and all 128 out rows, so H1 is recomputed once per column (twice there)
+//    and a chunk needs only its 16 dZ2 fragments of the tile's out units, 2 rebuilt per wave.
+//  * per 64-row chunk the DMA ring (4 slots, 3 chunks ahead) brings the 1-KiB bit block of the
+//    tile's 4 step-kernel waves (wave 0), the chunk's 64 dy (wave 1) and the 4-KiB X tile (waves
+//    0-3); each wave rebuilds its fragments of the NEXT chunk into a 2 x 16-KiB double buffer
+//    while the workgroup computes this one: one barrier per chunk.
 constexpr int DW2M_SLOTS = 4;
-constexpr int DW2M_MB = 2048, DW2M_DYB = 1024, DW2M_XB = MF_ROWS * 64;
+constexpr int DW2M_MB = 1024, DW2M_DYB = 1024, DW2M_XB = MF_ROWS * 64;
 constexpr int DW2M_SLOT = DW2M_MB + DW2M_DYB + DW2M_XB;
-constexpr int DW2M_FRAG = 32 * 1024;
+constexpr int DW2M_FRAG = 16 * 1024;
 __global__ __launch_bounds__(512, 1) void mlp2_dw2m_kernel(const unsigned long long* __restrict__ mk,
                                                            const float* __restrict__ dyo, const bf16_t* __restrict__ X,
                                                            int Fp, const long long* __restrict__ rows, long nrows,
@@ -1082,10 +1084,10 @@ __global__ __launch_bounds__(512, 1) void mlp2_dw2m_kernel(const unsigned long l
   char* fragb = smem + DW2M_SLOTS * DW2M_SLOT;
   int* ridx = reinterpret_cast<int*>(fragb + 2 * DW2M_FRAG);
   const int tid = threadIdx.x, lane = tid & 63, l15 = lane & 15, g = lane >> 4;
-  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6), wm = wid >> 2;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int L = xcd_remap(blockIdx.x, gridDim.x);
   const int split = L >> 1, t = L & 1;
-  const int n0 = 128 * t + 32 * (wid & 3);
+  const int o0 = 128 * t, n0 = 32 * wid;  // out rows of the tile, in columns of this wave
   const int kbeg = split * kchunk, nch = kchunk / MF_ROWS;
   for (int i = tid; i < kchunk; i += 512) ridx[i] = rows != nullptr ? (int)data_row(rows, kbeg + i, nrows) : kbeg + i;
   __syncthreads();
@@ -1100,17 +1102,18 @@ __global__ __launch_bounds__(512, 1) void mlp2_dw2m_kernel(const unsigned long l
                               : bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
     bias[nb] = b1[u];
   }
-  // the 4 fragments this wave rebuilds per chunk: f = 4 wid + qq -> (32-row step f >> 4, unit
-  // block f & 15); lane unit u = 16 b + l15 = step-kernel wave b >> 1, tile b & 1, lane group
-  // l15 >> 2, r = l15 & 3; its 8 rows 8g .. 8g + 7 of the step sit in bits 16 (l15 >> 2) + 8 (g & 1)
-  // of the ballot word of tile n' = 2 (f >> 4) + (g >> 1) of the chunk's half pass
-  float w3u[4];
-  int wofs[4];
+  // the 2 fragments this wave rebuilds per chunk: f = 2 wid + qq -> (32-row step f >> 3, out
+  // block mb = f & 7 of the tile); lane unit u = o0 + 16 mb + l15 = step-kernel wave u >> 5, tile
+  // (u >> 4) & 1, lane group l15 >> 2, r = l15 & 3; its 8 rows 8g .. 8g + 7 of the step are bits
+  // 16 (l15 >> 2) + 8 (g & 1) of the ballot word of tile n' = 2 (f >> 3) + (g >> 1) of the half pass
+  float w3u[2];
+  int wofs[2];
 #pragma unroll
-  for (int qq = 0; qq < 4; ++qq) {
-    const int f = 4 * wid + qq, s2 = f >> 4, b = f & 15;
-    w3u[qq] = w3[16 * b + l15];
-    wofs[qq] = (((b >> 1) * 2 + (b & 1)) * 16 + (2 * s2 + (g >> 1)) * 4 + (l15 & 3)) * 8;
+  for (int qq = 0; qq < 2; ++qq) {
+    const int f = 2 * wid + qq, s2 = f >> 3, mb = f & 7, u = o0 + 16 * mb + l15;
+    w3u[qq] = w3[u];
+    // bit block in LDS: run (step-kernel wave (u >> 5) - 4t, tile (u >> 4) & 1) of 16 words
+    wofs[qq] = ((((u >> 5) - 4 * t) * 2 + ((u >> 4) & 1)) * 16 + (2 * s2 + (g >> 1)) * 4 + (l15 & 3)) * 8;
   }
   const int bsh = 16 * (l15 >> 2) + 8 * (g & 1);
 
@@ -1120,12 +1123,12 @@ __global__ __launch_bounds__(512, 1) void mlp2_dw2m_kernel(const unsigned long l
   auto issue = [&](int c, int slot) {
     char* st = smem + slot * DW2M_SLOT;
     const int r0 = kbeg + c * MF_ROWS, ps = r0 >> 7, hh = (r0 >> 6) & 1;
-    if (wid < 2) {  // bit block: 16 runs of 128 B (step-kernel wave w, tile m: words n' = 4 hh .. 4 hh + 3)
-      const int o = wid * 1024 + lane * 16, sg = o >> 7;
+    if (wid == 0) {  // bits: 8 runs of 128 B (step-kernel waves 4t .. 4t + 3 x tiles 0, 1: words n' = 4 hh ..)
+      const int sg = lane >> 3;
       const char* src = reinterpret_cast<const char*>(mk) +
-                        ((((size_t)ps * 8 + (sg >> 1)) * 64 + ((sg & 1) * 8 + 4 * hh) * 4) * 8 + (o & 127));
-      __builtin_amdgcn_global_load_lds((const void*)src, (lds_void*)(st + wid * 1024), 16, 0, 0);
-    } else if (wid == 2) {  // dy of the 64 rows (lanes 16.. repeat lanes 0..15)
+                        ((((size_t)ps * 8 + 4 * t + (sg >> 1)) * 64 + ((sg & 1) * 8 + 4 * hh) * 4) * 8 + (lane & 7) * 16);
+      __builtin_amdgcn_global_load_lds((const void*)src, (lds_void*)st, 16, 0, 0);
+    } else if (wid == 1) {  // dy of the 64 rows (lanes 16.. repeat lanes 0..15)
       __builtin_amdgcn_global_load_lds((const void*)(dyo + r0 + 4 * (lane & 15)), (lds_void*)(st + DW2M_MB), 16, 0, 0);
     }
     if (wid < 4) {
@@ -1134,33 +1137,32 @@ __global__ __launch_bounds__(512, 1) void mlp2_dw2m_kernel(const unsigned long l
                                        (lds_void*)(st + DW2M_MB + DW2M_DYB + wid * 1024), 16, 0, 0);
     }
   };
-  // at most n chunks' DMAs of this wave in flight (waves 0-2 issue 2 per chunk, wave 3 one)
+  // at most n chunks' DMAs of this wave in flight (waves 0-1 issue 2 per chunk, 2-3 one)
   auto dma_wait = [&](auto nc) {
     constexpr int n = decltype(nc)::value;
-    if (wid < 3)
+    if (wid < 2)
       wait_vmcnt<2 * n>();
-    else if (wid == 3)
+    else if (wid < 4)
       wait_vmcnt<n>();
   };
-  // rebuild this wave's 4 fragments of the chunk in DMA slot `slot` into fragment buffer fb
-  auto rebuild = [&](int slot, char* fb) {
+  // rebuild fragment qq of this wave for the chunk in DMA slot `slot` into fragment buffer fb
+  auto rebuild = [&](int slot, char* fb, int qq) {
     const char* st = smem + slot * DW2M_SLOT;
+    const int f = 2 * wid + qq, s2 = f >> 3;
+    const unsigned long long word = *reinterpret_cast<const unsigned long long*>(st + wofs[qq]);
+    const unsigned bits = (unsigned)(word >> bsh);
+    const float4 d0 = *reinterpret_cast<const float4*>(st + DW2M_MB + (32 * s2 + 8 * g) * 4);
+    const float4 d1 = *reinterpret_cast<const float4*>(st + DW2M_MB + (32 * s2 + 8 * g + 4) * 4);
+    const float dv[8] = {d0.x, d0.y, d0.z, d0.w, d1.x, d1.y, d1.z, d1.w};
+    unsigned pk[4];
 #pragma unroll
-    for (int qq = 0; qq < 4; ++qq) {
-      const int f = 4 * wid + qq, s2 = f >> 4;
-      const unsigned long long word = *reinterpret_cast<const unsigned long long*>(st + wofs[qq]);
-      const unsigned bits = (unsigned)(word >> bsh);
-      const float4 d0 = *reinterpret_cast<const float4*>(st + DW2M_MB + (32 * s2 + 8 * g) * 4);
-      const float4 d1 = *reinterpret_cast<const float4*>(st + DW2M_MB + (32 * s2 + 8 * g + 4) * 4);
-      const float dv[8] = {d0.x, d0.y, d0.z, d0.w, d1.x, d1.y, d1.z, d1.w};
-      unsigned pk[4];
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const unsigned lo = (bits >> (2 * i)) & 1u ? 0x0000FFFFu : 0u, hi = (bits >> (2 * i + 1)) & 1u ? 0xFFFF0000u : 0u;
-        pk[i] = pk_bf16(dv[2 * i] * w3u[qq], dv[2 * i + 1] * w3u[qq]) & (lo | hi);
-      }
-      *reinterpret_cast<uint4*>(fb + f * 1024 + lane * 16) = make_uint4(pk[0], pk[1], pk[2], pk[3]);
+    for (int i = 0; i < 4; ++i) {
+      // sign-extended 1-bit fields (v_bfe_i32): all ones where the bit is set
+      const unsigned mlo = (unsigned)((int)(bits << (31 - 2 * i)) >> 31);
+      const unsigned mhi = (unsigned)((int)(bits << (30 - 2 * i)) >> 31);
+      pk[i] = pk_bf16(dv[2 * i] * w3u[qq], dv[2 * i + 1] * w3u[qq]) & ((mlo & 0xFFFFu) | (mhi & 0xFFFF0000u));
     }
+    *reinterpret_cast<uint4*>(fb + f * 1024 + lane * 16) = make_uint4(pk[0], pk[1], pk[2], pk[3]);
   };
   const int xg = 8 * g + 8 <= Fp ? g : 0;
   const int xr0 = 8 * (l15 >> 2) + (l15 & 3);
@@ -1177,7 +1179,8 @@ __global__ __launch_bounds__(512, 1) void mlp2_dw2m_kernel(const unsigned long l
   dma_wait(std::integral_constant<int, DW2M_SLOTS - 2>{});  // chunk 0 (this wave's pieces)
   __builtin_amdgcn_s_barrier();                              // ... every wave's
   asm volatile("" ::: "memory");
-  rebuild(0, fragb);
+  rebuild(0, fragb, 0);
+  rebuild(0, fragb, 1);
   for (int c = 0; c < nch; ++c) {
     const int slot = c & (DW2M_SLOTS - 1);
     // chunk c + 1's pieces landed (this wave); the barrier publishes them and chunk c's rebuilt
@@ -1186,7 +1189,10 @@ __global__ __launch_bounds__(512, 1) void mlp2_dw2m_kernel(const unsigned long l
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
     issue(min(c + DW2M_SLOTS - 1, last), (c + DW2M_SLOTS - 1) & (DW2M_SLOTS - 1));
-    if (c + 1 < nch) rebuild((c + 1) & (DW2M_SLOTS - 1), fragb + ((c + 1) & 1) * DW2M_FRAG);
+    // the next chunk's fragments are rebuilt in the MFMA shadow of this one (one after each 32-row
+    // step's dW MFMAs; the last chunk rebuilds a harmless copy of itself into the idle buffer)
+    const int nslot = (min(c + 1, last)) & (DW2M_SLOTS - 1);
+    char* nfb = fragb + ((c + 1) & 1) * DW2M_FRAG;
     const char* st = smem + slot * DW2M_SLOT;
     const char* xs = st + DW2M_MB + DW2M_DYB;
     const char* fa = fragb + (c & 1) * DW2M_FRAG;
@@ -1200,7 +1206,7 @@ __global__ __launch_bounds__(512, 1) void mlp2_dw2m_kernel(const unsigned long l
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int mb = 0; mb < 8; ++mb)
-        afa[s2][mb] = *reinterpret_cast<const bf16x8*>(fa + (s2 * 16 + 8 * wm + mb) * 1024 + lane * 16);
+        afa[s2][mb] = *reinterpret_cast<const bf16x8*>(fa + (s2 * 8 + mb) * 1024 + lane * 16);
     };
     frags(0);
     __builtin_amdgcn_sched_barrier(0);
@@ -1230,6 +1236,9 @@ __global__ __launch_bounds__(512, 1) void mlp2_dw2m_kernel(const unsigned long l
         for (int nb = 0; nb < 2; ++nb)
           acc[mb][nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(afa[s2][mb], hb[nb], acc[mb][nb], 0, 0, 0);
       }
+      __builtin_amdgcn_sched_barrier(0);
+      rebuild(nslot, nfb, s2);
+      __builtin_amdgcn_sched_barrier(0);
     }
   }
   wait_vmcnt<0>();  // the clamped fetches past the range must land before the workgroup ends
@@ -1241,7 +1250,7 @@ __global__ __launch_bounds__(512, 1) void mlp2_dw2m_kernel(const unsigned long l
 #pragma unroll
       for (int r = 0; r < 4; ++r)
 #pragma unroll
-        for (int nb = 0; nb < 2; ++nb) dst[(size_t)(128 * wm + 16 * mb + 4 * g + r) * MF_H + n0 + 16 * nb + l15] = acc[mb][nb][r];
+        for (int nb = 0; nb < 2; ++nb) dst[(size_t)(o0 + 16 * mb + 4 * g + r) * MF_H + n0 + 16 * nb + l15] = acc[mb][nb][r];
   } else {
     float* dst = dW2 + (size_t)(split & (kMlpRedCopies2 - 1)) * 65536;
 #pragma unroll
@@ -1250,7 +1259,7 @@ __global__ __launch_bounds__(512, 1) void mlp2_dw2m_kernel(const unsigned long l
       for (int r = 0; r < 4; ++r)
 #pragma unroll
         for (int nb = 0; nb < 2; ++nb)
-          atomicAdd(dst + (size_t)(128 * wm + 16 * mb + 4 * g + r) * MF_H + n0 + 16 * nb + l15, acc[mb][nb][r]);
+          atomicAdd(dst + (size_t)(o0 + 16 * mb + 4 * g + r) * MF_H + n0 + 16 * nb + l15, acc[mb][nb][r]);
   }
 }
 }  // namespace

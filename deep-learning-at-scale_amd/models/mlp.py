@@ -204,10 +204,11 @@ class NativeMLP:
         self.w2t = None
         if (self.red is not None and self.dw2_frag and os.environ.get("WELLFLOW_MLP_STEP128", "1") != "0"):
             self.w2t = torch.empty(256 * 256, dtype=bf, device=dev)
-        # ... and instead of dZ2 (512 B per row through HBM) only the [H2 > 0] bits and dy (36 B),
-        # from which the dW2 kernel rebuilds dZ2 bit for bit (mlp2_dw2m_kernel; WELLFLOW_MLP_DW2M=0:
-        # the fragment-layout dZ2)
-        self.dw2_mask = self.w2t is not None and os.environ.get("WELLFLOW_MLP_DW2M", "1") != "0"
+        # ... optionally passing only the [H2 > 0] bits and dy (36 B per row instead of dZ2's 512) to
+        # a dW2 kernel that rebuilds dZ2 bit for bit (mlp2_dw2m_kernel; WELLFLOW_MLP_DW2M=1). Off by
+        # default: measured 1.43 vs 1.46 G rows/s (the rebuild's VALU costs more than the HBM
+        # round trip it saves; profiles/r5/notes.md)
+        self.dw2_mask = self.w2t is not None and os.environ.get("WELLFLOW_MLP_DW2M", "0") == "1"
         self.sync_weights()
 
     @property
