@@ -271,7 +271,8 @@ def bench_cnn(args, ctx):
     eng.params.copy_(ref.to_flat().to(ctx.device))
     ctx.broadcast_(eng.params)
     eng.sync_weights()
-    opt = FlatSGD(eng.params, eng.grads, zero_grads=True)
+    # SGD refreshes the engine's bf16 operand images in the same launch (no pack launch per step)
+    opt = FlatSGD(eng.params, eng.grads, zero_grads=True, writeback=eng)
     g = torch.Generator(device="cpu").manual_seed(ctx.rank)
     series = torch.randn(B, lay.input_len + lay.outputs, generator=g).cumsum(1) * 0.1  # random-walk windows
     x = series[:, : lay.input_len].contiguous().to(ctx.device)

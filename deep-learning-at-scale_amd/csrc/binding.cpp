@@ -889,6 +889,28 @@ void cnn_pack(const at::Tensor& Wc, const at::Tensor& Wd, const std::vector<int6
   wf::launch_cnn_pack(fp(Wc), Wd.data_ptr<float>(), d, bfp(WcA), bfp(WdF), bfp(WdB), cur_stream());
 }
 
+// Keras SGD on the CNN's flat parameters + the bf16 operand images (cnn_pack's output) in one launch
+void cnn_sgd_pack(const at::Tensor& p, const at::Tensor& g, const at::Tensor& vel, const at::Tensor& step, double lr,
+                  double decay, double momentum, bool nesterov, double gscale, bool zero_g,
+                  const std::vector<int64_t>& dims, const at::Tensor& WcA, const at::Tensor& WdF, const at::Tensor& WdB) {
+  auto d = cnn_checked(dims, 0.0);
+  for (const at::Tensor* t : {&p, &g, &vel}) check_t(*t, at::kFloat, "p/g/vel");
+  const int64_t n = p.numel();
+  TORCH_CHECK(g.numel() == n && vel.numel() == n, "cnn_sgd_pack: size mismatch");
+  TORCH_CHECK(n >= (int64_t)d.Fp * d.Kc + (int64_t)16 * d.T * d.Fp, "cnn_sgd_pack: p shorter than the CNN layout");
+  check_t(step, at::kFloat, "step");
+  check_extent(step, 2, "step");
+  check_t(WcA, at::kBFloat16, "WcA");
+  check_extent(WcA, (int64_t)d.Fp * d.Kc, "WcA");
+  for (const at::Tensor* t : {&WdF, &WdB}) {
+    check_t(*t, at::kBFloat16, "WdF/WdB");
+    check_extent(*t, cnn_frag_elems(d), "WdF/WdB");
+  }
+  const c10::hip::OptionalHIPGuardMasqueradingAsCUDA guard(p.device());
+  wf::launch_cnn_sgd_pack(fp(p), fp(g), fp(vel), n, fp(step), (float)lr, (float)decay, (float)momentum, nesterov ? 1 : 0,
+                          (float)gscale, zero_g ? 1 : 0, d, bfp(WcA), bfp(WdF), bfp(WdB), cur_stream());
+}
+
 static const long long* rng_ptr(const c10::optional<at::Tensor>& rng) {
   if (!rng.has_value() || !rng->defined()) return nullptr;
   TORCH_CHECK(rng->is_cuda() && rng->scalar_type() == at::kLong && rng->numel() >= 1, "rng: GPU int64 tensor");
@@ -1044,6 +1066,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("cnn_fused_ok", &cnn_fused_ok);
   m.def("cnn_part_sizes", &cnn_part_sizes);
   WF_DEF(cnn_pack);
+  WF_DEF(cnn_sgd_pack);
   WF_DEF(cnn_forward);
   WF_DEF(cnn_backward);
   WF_DEF(cnn_reduce);

@@ -578,6 +578,54 @@ __global__ __launch_bounds__(256) void cnn_pack_kernel(const float* __restrict__
   }
 }
 
+// ------------------------------------------------------------------------ SGD + pack
+// Keras SGD (elementwise.hip sgd_dev_kernel: device iteration counter, Nesterov) over the flat
+// parameters [Wc Fp x Kc | Wd 16 x T Fp | bd] AND, in the same pass, the bf16 operand images
+// cnn_pack_kernel would write next (WcA, WdF, WdB): one launch per update instead of two
+// (round 5). Each updated weight is scattered to its image positions (the inverse of the pack
+// kernel's gather); rows j >= O of the dense block are padding and stay zero.
+__global__ __launch_bounds__(256) void cnn_sgd_pack_kernel(float* __restrict__ p, float* __restrict__ g,
+                                                           float* __restrict__ vel, long n, float* __restrict__ step,
+                                                           float lr, float decay, float momentum, int nesterov,
+                                                           float gscale, int zero_g, int T, int Fp, int NFB, int Kc,
+                                                           int O, bf16_t* __restrict__ WcA, bf16_t* __restrict__ WdF,
+                                                           bf16_t* __restrict__ WdB) {
+  const float it = step[0];
+  const float lr_t = lr / (1.f + decay * it);
+  const long nc = (long)Fp * Kc, nf = (long)T * Fp, nd = 16 * nf;
+  const long stride = (long)gridDim.x * blockDim.x;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += stride) {
+    const float gi = g[i] * gscale;
+    const float v = momentum * vel[i] - lr_t * gi;
+    vel[i] = v;
+    const float pn = p[i] + (nesterov ? (momentum * v - lr_t * gi) : v);
+    p[i] = pn;
+    if (zero_g) g[i] = 0.f;
+    if (i < nc) {
+      WcA[i] = f2bf(pn);
+    } else if (i < nc + nd) {
+      const long e = i - nc;
+      const int j = (int)(e / nf), rest = (int)(e % nf), t = rest / Fp, f = rest % Fp;
+      const unsigned short h = j < O ? f2bf(pn) : 0;
+      const int b = f >> 4, l15 = f & 15;
+      // WdB: lane 16 (j >> 2) + (f & 15) of block b, element j & 3
+      WdB[(((size_t)t * NFB + b) * 64 + 16 * (j >> 2) + l15) * 4 + (j & 3)] = h;
+      // WdF: lf = 16 q + j (q = (f & 15) >> 2); pairs of blocks (2p, 2p + 1) interleave per lane
+      const int lf = 16 * (l15 >> 2) + j;
+      const int eu = b < 6 ? 128 * (b >> 1) + 2 * lf + (b & 1) : 384 + lf;
+      WdF[((size_t)t * NFB * 64 + eu) * 4 + (f & 3)] = h;
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    unsigned* ticket = reinterpret_cast<unsigned*>(step + 1);
+    if (atomicAdd(ticket, 1u) == gridDim.x - 1) {
+      step[0] = it + 1.f;
+      *ticket = 0u;
+    }
+  }
+}
+
 // -------------------------------------------------------------------------------- launch
 bool cnn_fused_supported(const CnnDims& d) {
   return d.C == 1 && d.T == CNN_T && (d.Fp >> 4) == CNN_NFB && d.Fp % 16 == 0 && d.taps <= 15 && d.Kc == 16 &&
@@ -608,6 +656,16 @@ void launch_cnn_pack(const float* Wc, const float* Wd, const CnnDims& d, bf16_t*
   const int n = d.T * (d.Fp / 16) * 64 + d.Fp * d.Kc;
   hipLaunchKernelGGL(cnn_pack_kernel, dim3((n + 255) / 256), dim3(256), 0, s, Wc, Wd, d.T, d.Fp, d.Fp / 16, d.Kc,
                      d.O, WcA, WdF, WdB);
+}
+
+void launch_cnn_sgd_pack(float* p, float* g, float* vel, long n, float* step, float lr, float decay, float momentum,
+                         int nesterov, float gscale, int zero_g, const CnnDims& d, bf16_t* WcA, bf16_t* WdF,
+                         bf16_t* WdB, hipStream_t s) {
+  long b = (n + 255) / 256;
+  if (b > 2048) b = 2048;
+  if (b < 1) b = 1;
+  hipLaunchKernelGGL(cnn_sgd_pack_kernel, dim3((int)b), dim3(256), 0, s, p, g, vel, n, step, lr, decay, momentum,
+                     nesterov, gscale, zero_g, d.T, d.Fp, d.Fp / 16, d.Kc, d.O, WcA, WdF, WdB);
 }
 
 void launch_cnn_forward(const float* x, int B, const CnnDims& d, const bf16_t* WcA, const bf16_t* WdF,

@@ -163,6 +163,10 @@ int cnn_bwd_chunks(int B);
 // partial-buffer floats for a batch of B (dense-weight, conv-weight and forward partials)
 long cnn_part_floats(int B, const CnnDims& d, long* wd, long* wc, long* f);
 // bf16 operand images from the fp32 flat weights: WcA [Fp][Kc], WdF / WdB [T][Fp/16][64][4]
+// Keras SGD over the CNN's flat parameters + the bf16 operand images of launch_cnn_pack, one launch
+void launch_cnn_sgd_pack(float* p, float* g, float* vel, long n, float* step, float lr, float decay, float momentum,
+                         int nesterov, float gscale, int zero_g, const CnnDims& d, bf16_t* WcA, bf16_t* WdF,
+                         bf16_t* WdB, hipStream_t s);
 void launch_cnn_pack(const float* Wc, const float* Wd, const CnnDims& d, bf16_t* WcA, bf16_t* WdF, bf16_t* WdB,
                      hipStream_t s);
 // train = 1: dropout + loss; dout [rows >= B rounded up to 16][16] = scale * dloss/dpred, part

@@ -238,6 +238,17 @@ class NativeCNN:
     def seed32(self) -> int:
         return (self.seed * 1000003) & 0x7FFFFFFF
 
+    def fused_sgd(self, opt, grad_scale: float) -> bool:
+        """The optimizer's update and this engine's operand images in ONE launch (optim/flat.py
+        FlatSGD ``writeback``; csrc/cnn_fused.hip cnn_sgd_pack_kernel); False = not covered (the
+        caller runs the plain update and sync_weights)."""
+        if not self.fused:
+            return False
+        self._C.cnn_sgd_pack(self.params, self.grads, opt.vel, opt.step_dev, opt.lr, opt.decay, opt.momentum,
+                             opt.nesterov, grad_scale, opt.zero_grads, self.lay.fused_dims, self.WcA, self.WdF,
+                             self.WdB)
+        return True
+
     def sync_weights(self):
         if self.fused:
             Wc, Wd, _ = self.lay.views(self.params)

@@ -95,8 +95,12 @@ class FlatSGD:
 
     def __init__(self, params: torch.Tensor, grads: torch.Tensor, lr: float = 0.001,
                  momentum: float = 0.99, decay: float = 1e-6, nesterov: bool = True,
-                 zero_grads: bool = False):
+                 zero_grads: bool = False, writeback=None):
+        """``writeback``: an engine whose ``fused_sgd(opt, grad_scale)`` runs this update AND
+        refreshes its compute copies in one launch (NativeCNN: the bf16 operand images), so no
+        separate sync_weights launch follows (train/step.py StepRunner)."""
         self.params, self.grads = params, grads
+        self.writeback = writeback
         self.lr, self.momentum, self.decay, self.nesterov = lr, momentum, decay, nesterov
         self.zero_grads = zero_grads
         self.vel = torch.zeros_like(params)
@@ -110,6 +114,9 @@ class FlatSGD:
             from ..ops.native import lib
 
             self.iterations += 1
+            wb = self.writeback
+            if wb is not None and wb.params is self.params and wb.fused_sgd(self, grad_scale):
+                return
             lib().sgd_dev(self.params, self.grads, self.vel, self.step_dev, self.lr, self.decay, self.momentum,
                           self.nesterov, grad_scale, self.zero_grads)
             return

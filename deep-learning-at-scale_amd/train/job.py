@@ -32,7 +32,8 @@ from .trainer import Trainer
 def _optimizer(cfg: RunConfig, eng):
     if cfg.optimizer == "sgd":
         return make_optimizer("sgd", eng.params, eng.grads, lr=cfg.lr, momentum=cfg.momentum,
-                              decay=cfg.decay, nesterov=cfg.nesterov)
+                              decay=cfg.decay, nesterov=cfg.nesterov,
+                              writeback=eng if hasattr(eng, "fused_sgd") else None)
     return make_optimizer("adam", eng.params, eng.grads, lr=cfg.lr, weight_decay=cfg.weight_decay)
 
 

@@ -52,6 +52,9 @@ class StepRunner:
         est, ost = getattr(eng, "shadow_t", None), getattr(opt, "shadow_t", None)
         self.fused_shadow = (sh is not None and sh is getattr(eng, "shadow", None) and
                              (est is None or (ost is not None and ost[0] is est[0])))
+        # ... or an optimizer that refreshes the engine's compute copies itself (FlatSGD writeback)
+        if getattr(opt, "writeback", None) is eng and getattr(eng, "fused", False):
+            self.fused_shadow = True
         self.loss_acc = torch.zeros(1, device=eng.device) if accumulate_loss else None
         # engines that add the batch loss straight into the accumulator (no zero + add launches)
         try:

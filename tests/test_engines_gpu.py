@@ -83,6 +83,37 @@ def _flat_grad(ref):
     return g.to_flat().to(DEV)
 
 
+def test_cnn_sgd_writeback_equals_sgd_then_pack():
+    """FlatSGD(writeback=NativeCNN): the update and the bf16 operand images in one launch
+    (csrc/cnn_fused.hip cnn_sgd_pack_kernel) == the plain SGD launch followed by cnn_pack: same
+    parameters, velocities, device step counter and bit-identical images after 3 updates."""
+    from wellflow.models.cnn import CNN1DRegressor, NativeCNN
+    from wellflow.optim.flat import FlatSGD
+
+    torch.manual_seed(3)
+    ref = CNN1DRegressor(dropout=0.5).init_keras(5).to(DEV)
+    engs, opts = [], []
+    for wb in (False, True):
+        eng = NativeCNN(ref.layout, batch=512, device=DEV, dropout=0.5, loss="mae_clip", seed=3)
+        eng.params.copy_(ref.to_flat().to(DEV))
+        eng.sync_weights()
+        engs.append(eng)
+        opts.append(FlatSGD(eng.params, eng.grads, lr=0.01, zero_grads=True, writeback=eng if wb else None))
+    x, y = torch.randn(512, 48, 1, device=DEV), torch.randn(512, 12, device=DEV)
+    for _ in range(3):
+        for eng, opt in zip(engs, opts):
+            eng.forward_backward(x, y, grad_scale=1.0 / (512 * 12), zero_grads=False)
+            opt.step()
+            if opt.writeback is None:
+                eng.sync_weights()
+    torch.cuda.synchronize()
+    a, b = engs
+    assert torch.equal(a.params, b.params) and torch.equal(opts[0].vel, opts[1].vel)
+    assert torch.equal(opts[0].step_dev, opts[1].step_dev)
+    for nm in ("WcA", "WdF", "WdB"):
+        assert torch.equal(getattr(a, nm), getattr(b, nm)), nm
+
+
 @pytest.mark.parametrize("loss,B,p", [("mse", 1000, 0.5), ("mae_clip", 4096, 0.5), ("mse", 64, 0.5), ("mse", 1000, 0.0),
                                       ("mae_clip", 65536, 0.5)])
 def test_native_cnn_bit_exact_vs_bf16_emulation(loss, B, p):
