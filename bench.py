@@ -202,7 +202,8 @@ def bench_lstm(args, ctx):
     ctx.broadcast_(eng.params)  # C1: identical init on every rank
     eng.sync_weights()
     # Adam clears the gradient bucket in its own launch (no fill kernel before the backward)
-    opt = FlatAdam(eng.params, eng.grads, lr=args.lr, zero_grads=True)
+    # Adam refreshes the engine's bf16 weight copies (Wp, WhhT) in the same launch
+    opt = FlatAdam(eng.params, eng.grads, lr=args.lr, zero_grads=True, writeback=eng)
     x, y = synth_lstm_batch(B, T, F, seed=ctx.rank)  # Gilbert-consistent windows, GPU-resident
     x, y = x.to(ctx.device), y.to(ctx.device)
     run = StepRunner(eng, opt, ctx, 1.0 / (B * ctx.world_size), lambda k: (x, y),

@@ -388,6 +388,28 @@ bool lstm_backward_dw(const at::Tensor& WhhT, const at::Tensor& XH, const at::Te
   return false;
 }
 
+// Adam on the LSTM's flat parameters + Wp / WhhT (lstm_pack_weights' output) in one launch
+void lstm_adam_pack(const at::Tensor& p, const at::Tensor& g, const at::Tensor& m, const at::Tensor& v,
+                    const at::Tensor& step, double lr, double b1, double b2, double eps, double wd, double gscale,
+                    bool zero_g, const at::Tensor& Wp, const at::Tensor& WhhT, int64_t H, int64_t KX) {
+  for (const at::Tensor* t : {&p, &g, &m, &v}) check_t(*t, at::kFloat, "p/g/m/v");
+  const int64_t n = p.numel();
+  TORCH_CHECK(g.numel() == n && m.numel() == n && v.numel() == n, "lstm_adam_pack: size mismatch");
+  TORCH_CHECK(KX % 4 == 0 && H % 4 == 0 && n >= 4 * H * (KX + H), "lstm_adam_pack: layout");
+  for (const at::Tensor* t : {&p, &g, &m, &v})
+    TORCH_CHECK(reinterpret_cast<uintptr_t>(t->data_ptr()) % 16 == 0, "lstm_adam_pack: buffers must be 16-B aligned");
+  check_t(step, at::kFloat, "step");
+  check_extent(step, 2, "step");
+  check_t(Wp, at::kBFloat16, "Wp");
+  check_t(WhhT, at::kBFloat16, "WhhT");
+  check_extent(Wp, 4 * H * (KX + H), "Wp");
+  check_extent(WhhT, H * 4 * H, "WhhT");
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(Wp.data_ptr()) % 8 == 0, "lstm_adam_pack: Wp must be 8-B aligned");
+  const c10::hip::OptionalHIPGuardMasqueradingAsCUDA guard(p.device());
+  wf::launch_lstm_adam_pack(fp(p), fp(g), fp(m), fp(v), n, fp(step), (float)lr, (float)b1, (float)b2, (float)eps,
+                            (float)wd, (float)gscale, zero_g ? 1 : 0, (int)KX, (int)H, bfp(Wp), bfp(WhhT), cur_stream());
+}
+
 void lstm_pack_weights(const at::Tensor& W, const at::Tensor& Wp, const at::Tensor& WhhT,
                        int64_t H, int64_t KX) {
   auto d = lstm_dims(1, 1, 0, KX, H);
@@ -1049,6 +1071,7 @@ PYBIND11_MODULE(_C, m) {
   WF_DEF(lstm_backward);
   WF_DEF(lstm_backward_dw);
   WF_DEF(lstm_pack_weights);
+  WF_DEF(lstm_adam_pack);
   WF_DEF(head_fwd);
   WF_DEF(head_bwd_w);
   WF_DEF(head_fwd_bwd);

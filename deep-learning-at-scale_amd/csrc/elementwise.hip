@@ -10,6 +10,7 @@
 
 #include "common.h"
 #include "kernels.h"
+#include "lstm_layout.h"
 
 namespace wf {
 
@@ -487,6 +488,74 @@ __global__ __launch_bounds__(256) void adam_dev_kernel(float* __restrict__ p, fl
       *ticket = 0u;
     }
   }
+}
+
+// Adam (as adam_dev_kernel) over the LSTM's flat parameters [W G x KA | w_out | b_out] AND, in
+// the same pass, the bf16 compute copies lstm_pack_weights_kernel (lstm.hip) would write next:
+// Wp (gate_col row order, rows pre-scaled for the exp2-form activations) and WhhT ([H][G], the
+// backward's). One launch per update instead of two (round 5; FlatAdam writeback).
+__global__ __launch_bounds__(256) void lstm_adam_pack_kernel(float* __restrict__ p, float* __restrict__ g,
+                                                             float* __restrict__ m, float* __restrict__ v, long n,
+                                                             float* __restrict__ step, float lr, float b1, float b2,
+                                                             float eps, float wd, float gscale, int zero_g, int KX, int H,
+                                                             bf16_t* __restrict__ Wp, bf16_t* __restrict__ WhhT) {
+  const float t = step[0] + 1.f;
+  const float bc1 = 1.f - __powf(b1, t), bc2 = 1.f - __powf(b2, t);
+  const int KA = KX + H, G = 4 * H;
+  const long nw4 = (long)G * KA / 4;  // KA % 4 == 0: a float4 never straddles a W row
+  const long n4 = n / 4;
+  const long stride = (long)gridDim.x * blockDim.x;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n4; i += stride) {
+    float4 pp = reinterpret_cast<float4*>(p)[i];
+    float4 gg = reinterpret_cast<const float4*>(g)[i];
+    float4 mm = reinterpret_cast<float4*>(m)[i];
+    float4 vv = reinterpret_cast<float4*>(v)[i];
+    adam_one(pp.x, gg.x * gscale, mm.x, vv.x, lr, b1, b2, eps, wd, bc1, bc2);
+    adam_one(pp.y, gg.y * gscale, mm.y, vv.y, lr, b1, b2, eps, wd, bc1, bc2);
+    adam_one(pp.z, gg.z * gscale, mm.z, vv.z, lr, b1, b2, eps, wd, bc1, bc2);
+    adam_one(pp.w, gg.w * gscale, mm.w, vv.w, lr, b1, b2, eps, wd, bc1, bc2);
+    reinterpret_cast<float4*>(p)[i] = pp;
+    reinterpret_cast<float4*>(m)[i] = mm;
+    reinterpret_cast<float4*>(v)[i] = vv;
+    if (zero_g) reinterpret_cast<float4*>(g)[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (i < nw4) {
+      const long idx = 4 * i;
+      const int k = (int)(idx % KA), r = (int)(idx / KA);
+      const float sc = (r & 3) == 2 ? kLstmTanhScale : kLstmSigScale;
+      const unsigned lo = (unsigned)f2bf(pp.x * sc) | ((unsigned)f2bf(pp.y * sc) << 16);
+      const unsigned hi = (unsigned)f2bf(pp.z * sc) | ((unsigned)f2bf(pp.w * sc) << 16);
+      *reinterpret_cast<uint2*>(Wp + (size_t)gate_col(r & 3, r >> 2) * KA + k) = make_uint2(lo, hi);
+      if (k >= KX) {  // (KX % 4 == 0: all four or none)
+        bf16_t* col = WhhT + (size_t)(k - KX) * G + r;
+        col[0] = f2bf(pp.x);
+        col[(size_t)G] = f2bf(pp.y);
+        col[(size_t)2 * G] = f2bf(pp.z);
+        col[(size_t)3 * G] = f2bf(pp.w);
+      }
+    }
+  }
+  for (long i = n4 * 4 + blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += stride) {
+    adam_one(p[i], g[i] * gscale, m[i], v[i], lr, b1, b2, eps, wd, bc1, bc2);
+    if (zero_g) g[i] = 0.f;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    unsigned* ticket = reinterpret_cast<unsigned*>(step + 1);
+    if (atomicAdd(ticket, 1u) == gridDim.x - 1) {
+      step[0] = t;
+      *ticket = 0u;
+    }
+  }
+}
+
+void launch_lstm_adam_pack(float* p, float* g, float* m, float* v, long n, float* step, float lr, float b1, float b2,
+                           float eps, float wd, float gscale, int zero_g, int KX, int H, bf16_t* Wp, bf16_t* WhhT,
+                           hipStream_t s) {
+  static const int cap = std::max(1, diag_env_int("WELLFLOW_ADAM_GRID", 256));
+  int blocks = ew_blocks(n);
+  if (blocks > cap) blocks = cap;
+  hipLaunchKernelGGL(lstm_adam_pack_kernel, dim3(blocks), dim3(256), 0, s, p, g, m, v, n, step, lr, b1, b2, eps, wd,
+                     gscale, zero_g, KX, H, Wp, WhhT);
 }
 
 void launch_adam_dev(float* p, float* g, float* m, float* v, long n, float* step, float lr,

@@ -200,6 +200,10 @@ void launch_loss(int kind, const float* pred, const float* y, int B, int O, floa
 // ---- optimizers and casts over flat fp32 buffers ----
 void launch_adam(float* p, const float* g, float* m, float* v, long n, float lr, float b1,
                  float b2, float eps, float wd, float bc1, float bc2, float gscale, hipStream_t s);
+// Adam over the LSTM's flat parameters + its bf16 compute copies Wp / WhhT (lstm_pack_weights) in one launch
+void launch_lstm_adam_pack(float* p, float* g, float* m, float* v, long n, float* step, float lr, float b1, float b2,
+                           float eps, float wd, float gscale, int zero_g, int KX, int H, bf16_t* Wp, bf16_t* WhhT,
+                           hipStream_t s);
 void launch_adam_dev(float* p, float* g, float* m, float* v, long n, float* step, float lr,
                      float b1, float b2, float eps, float wd, float gscale, bf16_t* shadow, int zero_g,
                      hipStream_t s, bf16_t* tdst = nullptr, long t_off = 0, int t_rows = 0, int t_cols = 0);

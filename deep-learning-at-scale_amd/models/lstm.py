@@ -262,6 +262,16 @@ class NativeLSTM:
         return 256 * max(1, props.multi_processor_count // nb)
 
     # ------------------------------------------------------------------ weights
+    def fused_adam(self, opt, grad_scale: float) -> bool:
+        """The optimizer's Adam update and this engine's bf16 compute copies (Wp, WhhT) in ONE
+        launch (optim/flat.py FlatAdam ``writeback``; csrc/elementwise.hip lstm_adam_pack_kernel)."""
+        if opt.shadow is not None or opt.shadow_t is not None:
+            return False
+        b1, b2 = opt.betas
+        self._C.lstm_adam_pack(self.params, self.grads, opt.m, opt.v, opt.step_dev, opt.lr, b1, b2, opt.eps,
+                               opt.weight_decay, grad_scale, opt.zero_grads, self.Wp, self.WhhT, self.H, self.lay.KX)
+        return True
+
     def sync_weights(self) -> None:
         W, _, _ = self.lay.views(self.params)
         self._C.lstm_pack_weights(W, self.Wp, self.WhhT, self.H, self.lay.KX)

@@ -16,17 +16,21 @@ class FlatAdam:
 
     def __init__(self, params: torch.Tensor, grads: torch.Tensor, lr: float = 1e-3,
                  betas=(0.9, 0.999), eps: float = 1e-8, weight_decay: float = 0.0,
-                 shadow: torch.Tensor | None = None, zero_grads: bool = False, shadow_t=None):
+                 shadow: torch.Tensor | None = None, zero_grads: bool = False, shadow_t=None,
+                 writeback=None):
         """GPU fusions: ``shadow`` (bf16, same numel) receives the updated weights in the same
         launch (an engine whose compute copy is a plain cast, e.g. NativeMLP.shadow);
         ``shadow_t`` = (bf16 tensor, offset, rows, cols) receives one [rows][cols] block
         transposed in the same launch (NativeMLP.shadow_t: W2^T of the 128-row step kernel);
         ``zero_grads`` clears the gradient bucket after the update (the next
-        forward_backward then runs with zero_grads=False)."""
+        forward_backward then runs with zero_grads=False); ``writeback``: an engine whose
+        ``fused_adam(opt, grad_scale)`` runs this update AND refreshes its compute copies in one
+        launch (NativeLSTM: Wp / WhhT), so no sync_weights launch follows (train/step.py)."""
         assert params.dtype == torch.float32 and params.shape == grads.shape
         self.params, self.grads = params, grads
         self.shadow, self.zero_grads = shadow, zero_grads
         self.shadow_t = shadow_t
+        self.writeback = writeback
         self.lr, self.betas, self.eps, self.weight_decay = lr, tuple(betas), eps, weight_decay
         self.m = torch.zeros_like(params)
         self.v = torch.zeros_like(params)
@@ -41,6 +45,9 @@ class FlatAdam:
         if self.params.is_cuda:
             from ..ops.native import lib
 
+            wb = self.writeback
+            if wb is not None and wb.params is self.params and wb.fused_adam(self, grad_scale):
+                return
             st = self.shadow_t or (None, 0, 0, 0)
             lib().adam_dev(self.params, self.grads, self.m, self.v, self.step_dev, self.lr, b1, b2,
                            self.eps, self.weight_decay, grad_scale, self.shadow, self.zero_grads, *st)

@@ -34,7 +34,8 @@ def _optimizer(cfg: RunConfig, eng):
         return make_optimizer("sgd", eng.params, eng.grads, lr=cfg.lr, momentum=cfg.momentum,
                               decay=cfg.decay, nesterov=cfg.nesterov,
                               writeback=eng if hasattr(eng, "fused_sgd") else None)
-    return make_optimizer("adam", eng.params, eng.grads, lr=cfg.lr, weight_decay=cfg.weight_decay)
+    return make_optimizer("adam", eng.params, eng.grads, lr=cfg.lr, weight_decay=cfg.weight_decay,
+                          writeback=eng if hasattr(eng, "fused_adam") else None)
 
 
 def _save_best(cfg, name, ref, prepared):

@@ -53,7 +53,7 @@ class StepRunner:
         self.fused_shadow = (sh is not None and sh is getattr(eng, "shadow", None) and
                              (est is None or (ost is not None and ost[0] is est[0])))
         # ... or an optimizer that refreshes the engine's compute copies itself (FlatSGD writeback)
-        if getattr(opt, "writeback", None) is eng and getattr(eng, "fused", False):
+        if getattr(opt, "writeback", None) is eng and (getattr(eng, "fused", False) or hasattr(eng, "fused_adam")):
             self.fused_shadow = True
         self.loss_acc = torch.zeros(1, device=eng.device) if accumulate_loss else None
         # engines that add the batch loss straight into the accumulator (no zero + add launches)

@@ -83,6 +83,35 @@ def _flat_grad(ref):
     return g.to_flat().to(DEV)
 
 
+def test_lstm_adam_writeback_equals_adam_then_pack():
+    """FlatAdam(writeback=NativeLSTM): Adam and the bf16 weight copies Wp / WhhT in one launch
+    (csrc/elementwise.hip lstm_adam_pack_kernel) == adam_dev followed by lstm_pack_weights."""
+    from wellflow.data.synth import synth_lstm_batch
+    from wellflow.models.lstm import NativeLSTM, init_lstm_flat
+    from wellflow.optim.flat import FlatAdam
+
+    B, T, F, H = 512, 8, 16, 512
+    x, y = synth_lstm_batch(B, T, F, seed=4)
+    x, y = x.to(DEV), y.to(DEV)
+    engs, opts = [], []
+    for wb in (False, True):
+        eng = NativeLSTM(F, H, T, B, device=DEV)
+        eng.params.copy_(init_lstm_flat(F, H, seed=2).to(DEV))
+        eng.sync_weights()
+        engs.append(eng)
+        opts.append(FlatAdam(eng.params, eng.grads, lr=1e-3, zero_grads=True, writeback=eng if wb else None))
+    for _ in range(3):
+        for eng, opt in zip(engs, opts):
+            eng.forward_backward(x, y, 1.0 / B, zero_grads=False)
+            opt.step()
+            if opt.writeback is None:
+                eng.sync_weights()
+    torch.cuda.synchronize()
+    a, b = engs
+    assert torch.equal(a.params, b.params) and torch.equal(opts[0].m, opts[1].m) and torch.equal(opts[0].v, opts[1].v)
+    assert torch.equal(a.Wp, b.Wp) and torch.equal(a.WhhT, b.WhhT)
+
+
 def test_cnn_sgd_writeback_equals_sgd_then_pack():
     """FlatSGD(writeback=NativeCNN): the update and the bf16 operand images in one launch
     (csrc/cnn_fused.hip cnn_sgd_pack_kernel) == the plain SGD launch followed by cnn_pack: same
