@@ -400,9 +400,14 @@ __global__ __launch_bounds__(512, 1) void cnn_bwd_kernel(
       // both into a packed pair's sign bits (drop_pk), as in the forward
       unsigned pm[2] = {0u, 0u};
       if constexpr (DROP) {
-        unsigned mi[4];
-#pragma unroll
-        for (int r = 0; r < 4; ++r) mi[r] = ~cnn_mask_word(smix, w0 + 4 * q + r, t, T, hq) >> hb0;
+        // the 4 words this lane needs (windows 4q + r, key hq = l15 >> 2) are exactly the ones
+        // its quad (lanes 4 hq + 0..3 of row q) computes, one each: ONE hash per lane and a DPP
+        // quad broadcast per window instead of four hashes (two quarter-rate multiplies each)
+        const unsigned own = cnn_mask_word(smix, w0 + 4 * q + (l15 & 3), t, T, hq);
+        const unsigned mi[4] = {~(unsigned)__builtin_amdgcn_mov_dpp((int)own, 0x00, 0xF, 0xF, false) >> hb0,
+                                ~(unsigned)__builtin_amdgcn_mov_dpp((int)own, 0x55, 0xF, 0xF, false) >> hb0,
+                                ~(unsigned)__builtin_amdgcn_mov_dpp((int)own, 0xAA, 0xF, 0xF, false) >> hb0,
+                                ~(unsigned)__builtin_amdgcn_mov_dpp((int)own, 0xFF, 0xF, 0xF, false) >> hb0};
 #pragma unroll
         for (int h = 0; h < 2; ++h) pm[h] = (mi[2 * h] & 0xFFFFu) | (mi[2 * h + 1] << 16);
       }
