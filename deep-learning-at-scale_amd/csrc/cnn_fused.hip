@@ -132,14 +132,31 @@ __global__ __launch_bounds__(512, 1) void cnn_fwd_kernel(
   // ONE static LDS object: the dense weights' fragment image, then the wave partials
   __shared__ __attribute__((aligned(16))) char smem[NFRAG * 8 + CNN_NW * 20 * 4];
   float* wpart = reinterpret_cast<float*>(smem + NFRAG * 8);
-  {
-    const uint4* src = reinterpret_cast<const uint4*>(WdF);
-    uint4* dst = reinterpret_cast<uint4*>(smem);
-    for (int i = threadIdx.x; i < NFRAG / 2; i += 512) dst[i] = src[i];
-  }
   const int lane = threadIdx.x & 63, l15 = lane & 15, q = lane >> 4;
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   (void)prio;
+  const int ngroups = (B + 15) >> 4;
+  // the lane's x samples, loaded one group AHEAD (issued before this group's 36 steps, consumed
+  // a group later): raw float4s from a clamped in-range address, bounds applied at consumption
+  float4 xnx[XR / 4];
+  auto load_x = [&](int g) {
+    const int wc = min(g * 16 + l15, B - 1);
+#pragma unroll
+    for (int k = 0; k < XR / 4; ++k)
+      xnx[k] = *reinterpret_cast<const float4*>(x + (size_t)wc * L + min(4 * q + 4 * k, L - 4));
+  };
+  const int gstride = gridDim.x * CNN_NW;
+  // the first group's x and the dense weights' fragment image go out together: the image as
+  // 1-KiB LDS-DMA pieces (global_load_lds, wave w moves pieces w, w + 8, ..; no register round
+  // trip), the x loads behind them, one wait for both
+  if ((int)blockIdx.x * CNN_NW + wid < ngroups) load_x(blockIdx.x * CNN_NW + wid);
+  {
+    typedef __attribute__((address_space(3))) void lds_v;
+    const char* src = reinterpret_cast<const char*>(WdF);
+    for (int pc = wid; pc < NFRAG * 8 / 1024; pc += CNN_NW)
+      __builtin_amdgcn_global_load_lds((const void*)(src + pc * 1024 + lane * 16), (lds_v*)(smem + pc * 1024), 16, 0, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
   // conv weights as the A operand: A[f = 16b + l15][kk = 4q + jj] (bias at kk = taps)
   bf16x4 wc[NFB];
 #pragma unroll
@@ -153,18 +170,6 @@ __global__ __launch_bounds__(512, 1) void cnn_fwd_kernel(
   float lsum = 0.f, dbd[4] = {0.f, 0.f, 0.f, 0.f};
   __syncthreads();
 
-  const int ngroups = (B + 15) >> 4;
-  // the lane's x samples, loaded one group AHEAD (issued before this group's 36 steps, consumed
-  // a group later): raw float4s from a clamped in-range address, bounds applied at consumption
-  float4 xnx[XR / 4];
-  auto load_x = [&](int g) {
-    const int wc = min(g * 16 + l15, B - 1);
-#pragma unroll
-    for (int k = 0; k < XR / 4; ++k)
-      xnx[k] = *reinterpret_cast<const float4*>(x + (size_t)wc * L + min(4 * q + 4 * k, L - 4));
-  };
-  const int gstride = gridDim.x * CNN_NW;
-  if ((int)blockIdx.x * CNN_NW + wid < ngroups) load_x(blockIdx.x * CNN_NW + wid);
   for (int g = blockIdx.x * CNN_NW + wid; g < ngroups; g += gstride) {
     const int w = g * 16 + l15;  // this lane's window (B-operand column)
     const bool wok = w < B;
