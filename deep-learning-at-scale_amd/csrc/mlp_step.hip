@@ -20,7 +20,7 @@
 // complete — the next chunk's X / y tile is staged before the last one, which publishes it).
 // Batch sums go to the spread-reduction scratch as the two kernels' did (kMlpRedCopies copies +
 // the per-workgroup dW1 rows); dZ2 leaves either row-major (for mlp2_dw2) or in the fragment
-// layout of mlp2_dw2f_kernel below; mlp2_reduce sums everything into the gradients.
+// layout of the dW2 kernels below; mlp2_reduce sums everything into the gradients.
 #include <cstdlib>
 #include <type_traits>
 
@@ -32,7 +32,7 @@
 namespace wf {
 
 namespace {
-// FRAG: dZ2 leaves in the MFMA-fragment layout of mlp2_dw2f_kernel (below) instead of [B][256]
+// FRAG: dZ2 leaves in the MFMA-fragment layout of the dW2 kernels (below) instead of [B][256]
 // STAMP (WELLFLOW_MLP_STAMP=1, tools/mlp_timeline.py): lane 0 of every wave writes s_memtime at
 // 13 phase boundaries of its 5th chunk into `stamps` (results unchanged)
 template <int NFT, bool FRAG, bool STAMP = false>  // NFT: 16-feature tiles of dW1: 1 (Fp <= 16) or 2 (Fp <= 32)
@@ -875,194 +875,23 @@ __global__ __launch_bounds__(512, 1) void mlp2_step128_kernel(
 // 8g + 4h + r of unit l15 — exactly the K = rows slots of the dW MFMA's B fragment (no
 // transpose, no H1 image in LDS: the LDS-staged mlp2_dw2_kernel spent its time writing that
 // image, 16 % bank conflicts).
-//  * workgroup = 256 (out) x 128 (in) tile of one row range, 8 waves of 128 x 32 (wave w: out
-//    rows 128 (w >> 2), in columns 128 t + 32 (w & 3)); per 32-row step a wave runs 4
-//    recompute + 16 dW MFMAs (16x16x32). H1 of a column block is rebuilt by 2 waves (not 4).
-//  * per 64-row chunk the workgroup DMAs 32 dZ2 fragments (4 per wave) + the 4-KiB X tile
+//  * (round 4, mlp2_dw2f_kernel: 256 (out) x 128 (in) tiles, 32 fragments per chunk; round 5:
+//    mlp2_dw2g_kernel below, 128 x 256 tiles, 16 fragments per chunk.) Per 32-row step a wave
+//    runs 4 recompute + 16 dW MFMAs (16x16x32).
+//  * per 64-row chunk the workgroup DMAs its dZ2 fragments (2 per wave) + the 4-KiB X tile
 //    (waves 0-3, one piece each, rows through the LDS row-id table) into a 4-slot ring, 3 chunks
 //    ahead; one barrier per chunk. Fetches past the range re-load its last chunk (never read),
 //    so every wave's DMA count per chunk is fixed and the vmcnt waits are immediates.
 //  * grid = 2 tiles x nsplit row ranges; xcd_remap keeps a range's two tiles on one XCD, so
-//    the second reader of each dZ2 fragment hits L2.
+//    X (read by both tiles) hits L2 the second time.
 constexpr int DW2F_MAX_ROWS = 2048;                      // rows per workgroup (the row-id table)
-constexpr int DW2F_SLOTS = 4;                            // ring depth (chunks)
-constexpr int DW2F_ABYTES = 32 * 1024;                   // 2 steps x 16 dZ2 fragments
-constexpr int DW2F_SLOT = DW2F_ABYTES + MF_ROWS * 64;    // + X tile [64 rows][64 B]
-template <bool PF>  // PF: LDS fragments read a half-chunk ahead (WELLFLOW_DW2F_PF, A/B)
-__global__ __launch_bounds__(512, 1) void mlp2_dw2f_kernel(const bf16_t* __restrict__ dZ2F, const bf16_t* __restrict__ X,
-                                                           int Fp, const long long* __restrict__ rows, long nrows,
-                                                           const bf16_t* __restrict__ W1, const float* __restrict__ b1,
-                                                           int kchunk, float* __restrict__ dW2, float* __restrict__ slab,
-                                                           int slab_row0, int prio) {
-  __shared__ __attribute__((aligned(16))) char smem[DW2F_SLOTS * DW2F_SLOT + DW2F_MAX_ROWS * 4];
-  int* ridx = reinterpret_cast<int*>(smem + DW2F_SLOTS * DW2F_SLOT);
-  const int tid = threadIdx.x, lane = tid & 63, l15 = lane & 15, g = lane >> 4;
-  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6), wm = wid >> 2;
-  const bool xw = wid < 4;  // this wave also DMAs one X piece per chunk
-  const int L = xcd_remap(blockIdx.x, gridDim.x);
-  const int split = L >> 1, t = L & 1;
-  const int n0 = 128 * t + 32 * (wid & 3);  // in units (H1) of this wave
-  const int kbeg = split * kchunk, nch = kchunk / MF_ROWS;
-  // row ids of the range (identity without `rows`)
-  for (int i = tid; i < kchunk; i += 512) ridx[i] = rows != nullptr ? (int)data_row(rows, kbeg + i, nrows) : kbeg + i;
-  __syncthreads();
-  if (prio && wid >= 4) __builtin_amdgcn_s_setprio(1);  // static priority for the younger half
-
-  // recompute operands: W1 rows of the wave's 32 in units (K = features 8g .. 8g + 7; zero past Fp)
-  bf16x8 w1f[2];
-  float bias[2];
-#pragma unroll
-  for (int nb = 0; nb < 2; ++nb) {
-    const int u = n0 + 16 * nb + l15;
-    w1f[nb] = 8 * g + 8 <= Fp ? *reinterpret_cast<const bf16x8*>(W1 + (size_t)u * Fp + 8 * g)
-                              : bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
-    bias[nb] = b1[u];
-  }
-  // DMA sources. dZ2 fragments: wave w moves blocks 2w, 2w + 1 of both steps (4 pieces).
-  const bf16_t* zsrc = dZ2F + ((size_t)(kbeg >> 5) * 16 + 2 * wid) * 512 + lane * 8;
-  // X piece (waves 0-3): LDS position (row 16w + (lane >> 2), slot lane & 3) holds feature chunk
-  // slot ^ ((row >> 3) & 3) (conflict-free fragment reads below); chunks past Fp fetch chunk 0
-  // of the same row (finite values, multiplied by zero W1 columns)
-  const int xrow = 16 * (wid & 3) + (lane >> 2);
-  int xq = (lane & 3) ^ ((xrow >> 3) & 3);
-  if (8 * xq + 8 > Fp) xq = 0;
-  auto issue = [&](int c, int slot) {
-    char* st = smem + slot * DW2F_SLOT;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {  // (step k >> 1, block 2w + (k & 1))
-      const bf16_t* src = zsrc + ((size_t)(2 * c + (k >> 1)) * 16 + (k & 1)) * 512;
-      __builtin_amdgcn_global_load_lds((const void*)src, (lds_void*)(st + ((k >> 1) * 16 + 2 * wid + (k & 1)) * 1024), 16, 0, 0);
-    }
-    if (xw) {
-      const size_t xr = (size_t)ridx[c * MF_ROWS + xrow];
-      __builtin_amdgcn_global_load_lds((const void*)(X + xr * Fp + 8 * xq), (lds_void*)(st + DW2F_ABYTES + wid * 1024), 16, 0, 0);
-    }
-  };
-  // wait until at most n chunks' DMAs of this wave are in flight (5 per chunk for waves 0-3, else 4)
-  auto dma_wait = [&](auto nc) {
-    constexpr int n = decltype(nc)::value;
-    if (xw)
-      wait_vmcnt<5 * n>();
-    else
-      wait_vmcnt<4 * n>();
-  };
-  // recompute A operand: row slot l15 -> local row 8 (l15 >> 2) + 4h + (l15 & 3) of the step,
-  // feature chunk xg at its swizzled LDS position
-  const int xg = 8 * g + 8 <= Fp ? g : 0;
-  const int xr0 = 8 * (l15 >> 2) + (l15 & 3);
-
-  f32x4 acc[8][2];
-#pragma unroll
-  for (int i = 0; i < 8; ++i)
-#pragma unroll
-    for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  const int last = nch - 1;
-#pragma unroll
-  for (int k = 0; k < DW2F_SLOTS - 1; ++k) issue(min(k, last), k);
-  for (int c = 0; c < nch; ++c) {
-    const int slot = c & (DW2F_SLOTS - 1);
-    dma_wait(std::integral_constant<int, DW2F_SLOTS - 2>{});  // chunk c's pieces (this wave) landed
-    __builtin_amdgcn_s_barrier();                              // ... every wave's; slot c - 1 free
-    asm volatile("" ::: "memory");
-    issue(min(c + DW2F_SLOTS - 1, last), (c + DW2F_SLOTS - 1) & (DW2F_SLOTS - 1));
-    const char* st = smem + slot * DW2F_SLOT;
-    // LDS fragments one half-chunk ahead, pinned: half 0's 10 reads before its recompute, half
-    // 1's between half 0's recompute and its dW MFMAs. Left to the scheduler, each pair of dZ2
-    // reads sat right before its 4 MFMAs behind an lgkmcnt(0) (LDS latency every 4 MFMAs)
-    bf16x8 xfa[2][2], afa[2][8];
-    auto frags = [&](int s2) {
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        const int r = 32 * s2 + xr0 + 4 * h;
-        xfa[s2][h] = *reinterpret_cast<const bf16x8*>(st + DW2F_ABYTES + r * 64 + ((xg ^ ((r >> 3) & 3)) << 4));
-      }
-      __builtin_amdgcn_sched_barrier(0);  // X first: the recompute needs it before the dZ2 fragments
-#pragma unroll
-      for (int mb = 0; mb < 8; ++mb)
-        afa[s2][mb] = *reinterpret_cast<const bf16x8*>(st + (s2 * 16 + 8 * wm + mb) * 1024 + lane * 16);
-    };
-    if constexpr (PF) {
-      frags(0);
-      __builtin_amdgcn_sched_barrier(0);
-    } else {
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        const int r = xr0 + 4 * h;
-        xfa[0][h] = *reinterpret_cast<const bf16x8*>(st + DW2F_ABYTES + r * 64 + ((xg ^ ((r >> 3) & 3)) << 4));
-      }
-    }
-#pragma unroll
-    for (int s2 = 0; s2 < 2; ++s2) {
-      bf16x8 hb[2];
-      const bf16x8(&xf)[2] = xfa[s2];
-#pragma unroll
-      for (int nb = 0; nb < 2; ++nb) {
-        const f32x4 c0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xf[0], w1f[nb], f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
-        const f32x4 c1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xf[1], w1f[nb], f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
-        const unsigned p0 = pk_bf16(fmaxf(c0[0] + bias[nb], 0.f), fmaxf(c0[1] + bias[nb], 0.f));
-        const unsigned p1 = pk_bf16(fmaxf(c0[2] + bias[nb], 0.f), fmaxf(c0[3] + bias[nb], 0.f));
-        const unsigned p2 = pk_bf16(fmaxf(c1[0] + bias[nb], 0.f), fmaxf(c1[1] + bias[nb], 0.f));
-        const unsigned p3 = pk_bf16(fmaxf(c1[2] + bias[nb], 0.f), fmaxf(c1[3] + bias[nb], 0.f));
-        typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
-        hb[nb] = __builtin_bit_cast(bf16x8, (u32x4_t{p0, p1, p2, p3}));
-      }
-      if constexpr (PF) {
-        if (s2 == 0) {
-          __builtin_amdgcn_sched_barrier(0);
-          frags(1);
-          __builtin_amdgcn_sched_barrier(0);
-        }
-      } else {
-        if (s2 == 0) {
-#pragma unroll
-          for (int h = 0; h < 2; ++h) {
-            const int r = 32 + xr0 + 4 * h;
-            xfa[1][h] = *reinterpret_cast<const bf16x8*>(st + DW2F_ABYTES + r * 64 + ((xg ^ ((r >> 3) & 3)) << 4));
-          }
-        }
-#pragma unroll
-        for (int mb = 0; mb < 8; ++mb)
-          afa[s2][mb] = *reinterpret_cast<const bf16x8*>(st + (s2 * 16 + 8 * wm + mb) * 1024 + lane * 16);
-      }
-#pragma unroll
-      for (int mb = 0; mb < 8; ++mb) {
-#pragma unroll
-        for (int nb = 0; nb < 2; ++nb)
-          acc[mb][nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(afa[s2][mb], hb[nb], acc[mb][nb], 0, 0, 0);
-      }
-    }
-  }
-  wait_vmcnt<0>();  // the clamped fetches past the range must land before the workgroup ends
-  // out unit 128 wm + 16 mb + 4g + r, in unit n0 + 16 nb + l15: plain stores into this range's
-  // slab row (the reduce sums the rows); past the slab, atomics into a dW2 copy
-  const int srow = slab_row0 + split;
-  if (srow < kMlpRedSlab2Rows) {
-    float* dst = slab + (size_t)srow * 65536;
-#pragma unroll
-    for (int mb = 0; mb < 8; ++mb)
-#pragma unroll
-      for (int r = 0; r < 4; ++r)
-#pragma unroll
-        for (int nb = 0; nb < 2; ++nb) dst[(size_t)(128 * wm + 16 * mb + 4 * g + r) * MF_H + n0 + 16 * nb + l15] = acc[mb][nb][r];
-  } else {
-    float* dst = dW2 + (size_t)(split & (kMlpRedCopies2 - 1)) * 65536;
-#pragma unroll
-    for (int mb = 0; mb < 8; ++mb)
-#pragma unroll
-      for (int r = 0; r < 4; ++r)
-#pragma unroll
-        for (int nb = 0; nb < 2; ++nb)
-          atomicAdd(dst + (size_t)(128 * wm + 16 * mb + 4 * g + r) * MF_H + n0 + 16 * nb + l15, acc[mb][nb][r]);
-  }
-}
 
 // ----------------------------------------------------------------------------------------
 // dW2 from the [H2 > 0] bits and dy (mlp2_step128_kernel<., MASK = true>) instead of a stored
 // dZ2: 36 B per row from HBM instead of 512 (round 5; the dZ2 round trip was 134 MB written +
 // 134 MB read per step at B = 262,144). dZ2 = bf16(dy w3[u]) where a bit is set, so the rebuilt
-// fragments equal mlp2_dw2f_kernel's input bit for bit.
-//  * workgroup = 128 (out) x 256 (in) tile of one row range (mlp2_dw2f_kernel: 256 x 128): wave w
+// fragments equal mlp2_dw2g_kernel's input bit for bit.
+//  * workgroup = 128 (out) x 256 (in) tile of one row range (as mlp2_dw2g_kernel): wave w
 //    owns in columns 32w and all 128 out rows, so H1 is recomputed once per column (twice there)
 //    and a chunk needs only its 16 dZ2 fragments of the tile's out units, 2 rebuilt per wave.
 //  * per 64-row chunk the DMA ring (4 slots, 3 chunks ahead) brings the 1-KiB bit block of the
@@ -1262,6 +1091,151 @@ __global__ __launch_bounds__(512, 1) void mlp2_dw2m_kernel(const unsigned long l
           atomicAdd(dst + (size_t)(o0 + 16 * mb + 4 * g + r) * MF_H + n0 + 16 * nb + l15, acc[mb][nb][r]);
   }
 }
+
+// ----------------------------------------------------------------------------------------
+// dW2 from the fragment-layout dZ2 (the method above) with a 128 (out) x 256 (in) tile (round
+// 5; round 4 used 256 x 128 tiles, mlp2_dw2f_kernel): wave w owns in columns 32w and all 128
+// out rows, so a chunk needs only the 16 dZ2 fragments of the tile's out units (16 KiB of
+// LDS-DMA instead of 32) and H1 is recomputed once per column (twice there); the MFMAs per
+// (out, in) element and their order are unchanged (bit-identical dW2), +0.4 % step rate.
+constexpr int DW2G_SLOTS = 4;
+constexpr int DW2G_ABYTES = 16 * 1024;                  // 2 steps x 8 dZ2 fragments
+constexpr int DW2G_SLOT = DW2G_ABYTES + MF_ROWS * 64;   // + X tile [64 rows][64 B]
+__global__ __launch_bounds__(512, 1) void mlp2_dw2g_kernel(const bf16_t* __restrict__ dZ2F, const bf16_t* __restrict__ X,
+                                                           int Fp, const long long* __restrict__ rows, long nrows,
+                                                           const bf16_t* __restrict__ W1, const float* __restrict__ b1,
+                                                           int kchunk, float* __restrict__ dW2, float* __restrict__ slab,
+                                                           int slab_row0, int prio) {
+  __shared__ __attribute__((aligned(16))) char smem[DW2G_SLOTS * DW2G_SLOT + DW2F_MAX_ROWS * 4];
+  int* ridx = reinterpret_cast<int*>(smem + DW2G_SLOTS * DW2G_SLOT);
+  const int tid = threadIdx.x, lane = tid & 63, l15 = lane & 15, g = lane >> 4;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const bool xw = wid < 4;  // this wave also DMAs one X piece per chunk
+  const int L = xcd_remap(blockIdx.x, gridDim.x);
+  const int split = L >> 1, t = L & 1;
+  const int o0 = 128 * t, n0 = 32 * wid;
+  const int kbeg = split * kchunk, nch = kchunk / MF_ROWS;
+  for (int i = tid; i < kchunk; i += 512) ridx[i] = rows != nullptr ? (int)data_row(rows, kbeg + i, nrows) : kbeg + i;
+  __syncthreads();
+  if (prio && wid >= 4) __builtin_amdgcn_s_setprio(1);
+
+  bf16x8 w1f[2];
+  float bias[2];
+#pragma unroll
+  for (int nb = 0; nb < 2; ++nb) {
+    const int u = n0 + 16 * nb + l15;
+    w1f[nb] = 8 * g + 8 <= Fp ? *reinterpret_cast<const bf16x8*>(W1 + (size_t)u * Fp + 8 * g)
+                              : bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
+    bias[nb] = b1[u];
+  }
+  // DMA sources. dZ2 fragments (S, b) of the tile: b = 8t + mb; wave w moves (step w >> 2,
+  // blocks 8t + 2 (w & 3) + {0, 1})
+  const bf16_t* zsrc = dZ2F + ((size_t)(kbeg >> 5) * 16 + 8 * t + 2 * (wid & 3)) * 512 + lane * 8;
+  const int xrow = 16 * (wid & 3) + (lane >> 2);
+  int xq = (lane & 3) ^ ((xrow >> 3) & 3);
+  if (8 * xq + 8 > Fp) xq = 0;
+  auto issue = [&](int c, int slot) {
+    char* st = smem + slot * DW2G_SLOT;
+    const int s2 = wid >> 2;
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const bf16_t* src = zsrc + ((size_t)(2 * c + s2) * 16 + k) * 512;
+      __builtin_amdgcn_global_load_lds((const void*)src, (lds_void*)(st + (s2 * 8 + 2 * (wid & 3) + k) * 1024), 16, 0, 0);
+    }
+    if (xw) {
+      const size_t xr = (size_t)ridx[c * MF_ROWS + xrow];
+      __builtin_amdgcn_global_load_lds((const void*)(X + xr * Fp + 8 * xq), (lds_void*)(st + DW2G_ABYTES + wid * 1024), 16, 0, 0);
+    }
+  };
+  auto dma_wait = [&](auto nc) {
+    constexpr int n = decltype(nc)::value;
+    if (xw)
+      wait_vmcnt<3 * n>();
+    else
+      wait_vmcnt<2 * n>();
+  };
+  const int xg = 8 * g + 8 <= Fp ? g : 0;
+  const int xr0 = 8 * (l15 >> 2) + (l15 & 3);
+
+  f32x4 acc[8][2];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int last = nch - 1;
+#pragma unroll
+  for (int k = 0; k < DW2G_SLOTS - 1; ++k) issue(min(k, last), k);
+  for (int c = 0; c < nch; ++c) {
+    const int slot = c & (DW2G_SLOTS - 1);
+    dma_wait(std::integral_constant<int, DW2G_SLOTS - 2>{});  // chunk c's pieces (this wave) landed
+    __builtin_amdgcn_s_barrier();                              // ... every wave's; slot c - 1 free
+    asm volatile("" ::: "memory");
+    issue(min(c + DW2G_SLOTS - 1, last), (c + DW2G_SLOTS - 1) & (DW2G_SLOTS - 1));
+    const char* st = smem + slot * DW2G_SLOT;
+    bf16x8 xfa[2][2], afa[2][8];
+    auto frags = [&](int s2) {
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int r = 32 * s2 + xr0 + 4 * h;
+        xfa[s2][h] = *reinterpret_cast<const bf16x8*>(st + DW2G_ABYTES + r * 64 + ((xg ^ ((r >> 3) & 3)) << 4));
+      }
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int mb = 0; mb < 8; ++mb)
+        afa[s2][mb] = *reinterpret_cast<const bf16x8*>(st + (s2 * 8 + mb) * 1024 + lane * 16);
+    };
+    frags(0);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) {
+      bf16x8 hb[2];
+      const bf16x8(&xf)[2] = xfa[s2];
+#pragma unroll
+      for (int nb = 0; nb < 2; ++nb) {
+        const f32x4 c0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xf[0], w1f[nb], f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+        const f32x4 c1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xf[1], w1f[nb], f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+        const unsigned p0 = pk_bf16(fmaxf(c0[0] + bias[nb], 0.f), fmaxf(c0[1] + bias[nb], 0.f));
+        const unsigned p1 = pk_bf16(fmaxf(c0[2] + bias[nb], 0.f), fmaxf(c0[3] + bias[nb], 0.f));
+        const unsigned p2 = pk_bf16(fmaxf(c1[0] + bias[nb], 0.f), fmaxf(c1[1] + bias[nb], 0.f));
+        const unsigned p3 = pk_bf16(fmaxf(c1[2] + bias[nb], 0.f), fmaxf(c1[3] + bias[nb], 0.f));
+        typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
+        hb[nb] = __builtin_bit_cast(bf16x8, (u32x4_t{p0, p1, p2, p3}));
+      }
+      if (s2 == 0) {
+        __builtin_amdgcn_sched_barrier(0);
+        frags(1);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+#pragma unroll
+      for (int mb = 0; mb < 8; ++mb) {
+#pragma unroll
+        for (int nb = 0; nb < 2; ++nb)
+          acc[mb][nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(afa[s2][mb], hb[nb], acc[mb][nb], 0, 0, 0);
+      }
+    }
+  }
+  wait_vmcnt<0>();  // the clamped fetches past the range must land before the workgroup ends
+  const int srow = slab_row0 + split;
+  if (srow < kMlpRedSlab2Rows) {
+    float* dst = slab + (size_t)srow * 65536;
+#pragma unroll
+    for (int mb = 0; mb < 8; ++mb)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int nb = 0; nb < 2; ++nb) dst[(size_t)(o0 + 16 * mb + 4 * g + r) * MF_H + n0 + 16 * nb + l15] = acc[mb][nb][r];
+  } else {
+    float* dst = dW2 + (size_t)(split & (kMlpRedCopies2 - 1)) * 65536;
+#pragma unroll
+    for (int mb = 0; mb < 8; ++mb)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int nb = 0; nb < 2; ++nb)
+          atomicAdd(dst + (size_t)(o0 + 16 * mb + 4 * g + r) * MF_H + n0 + 16 * nb + l15, acc[mb][nb][r]);
+  }
+}
 }  // namespace
 
 bool launch_mlp2_step(const bf16_t* X, int Fp, const bf16_t* W1, const float* b1, const bf16_t* W2, const float* b2,
@@ -1320,8 +1294,6 @@ int launch_mlp2_dw2f(const bf16_t* dZ2F, const bf16_t* X, int Fp, const long lon
   // static s_setprio 1 for waves 4-7 (48.2 -> 47.0 us, +0.3 to +0.6 % in three interleaved pairs,
   // profiles/r4/mlp_prio; the WELLFLOW_DW2F_PRIO A/B knob was removed)
   constexpr int prio = 1;
-  // fragment reads a half-chunk ahead (+0.5 %, profiles/r4/mlp_dw2f_pf; knob removed)
-  constexpr bool pf = true;
   int srow = 0;  // slab rows used so far (the launches' ranges stack)
   for (int r0 = 0; r0 < B; r0 += kMaxBlock) {
     const int Bb = B - r0 < kMaxBlock ? B - r0 : kMaxBlock;
@@ -1332,16 +1304,10 @@ int launch_mlp2_dw2f(const bf16_t* dZ2F, const bf16_t* X, int Fp, const long lon
     const int kchunk = (chunks / ns) * MF_ROWS;
     if (kchunk > DW2F_MAX_ROWS) return 0;  // (unreachable for B % 64 == 0)
     // row block r0: dZ2 fragments start at step r0 / 32; X through `rows` (offset) or directly
-    if (pf)
-      hipLaunchKernelGGL(mlp2_dw2f_kernel<true>, dim3(2 * ns), dim3(512), 0, s, dZ2F + (size_t)r0 * MF_H,
-                         rows != nullptr ? X : X + (size_t)r0 * Fp, Fp, rows != nullptr ? rows + r0 : nullptr,
-                         rows != nullptr ? nrows : (long)Bb, W1, b1, kchunk, red + (size_t)kMlpRedCopies * kMlpRedRow,
-                         red + kMlpRedSlab2Off, srow, prio);
-    else
-      hipLaunchKernelGGL(mlp2_dw2f_kernel<false>, dim3(2 * ns), dim3(512), 0, s, dZ2F + (size_t)r0 * MF_H,
-                         rows != nullptr ? X : X + (size_t)r0 * Fp, Fp, rows != nullptr ? rows + r0 : nullptr,
-                         rows != nullptr ? nrows : (long)Bb, W1, b1, kchunk, red + (size_t)kMlpRedCopies * kMlpRedRow,
-                         red + kMlpRedSlab2Off, srow, prio);
+    hipLaunchKernelGGL(mlp2_dw2g_kernel, dim3(2 * ns), dim3(512), 0, s, dZ2F + (size_t)r0 * MF_H,
+                       rows != nullptr ? X : X + (size_t)r0 * Fp, Fp, rows != nullptr ? rows + r0 : nullptr,
+                       rows != nullptr ? nrows : (long)Bb, W1, b1, kchunk, red + (size_t)kMlpRedCopies * kMlpRedRow,
+                       red + kMlpRedSlab2Off, srow, prio);
     srow += ns;
   }
   return srow < kMlpRedSlab2Rows ? srow : kMlpRedSlab2Rows;
