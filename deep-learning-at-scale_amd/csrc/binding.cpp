@@ -570,7 +570,7 @@ void mlp2_reduce(const at::Tensor& red, int64_t Fp, int64_t B, c10::optional<at:
 bool mlp2_step(const at::Tensor& X, int64_t Fp, const at::Tensor& W1, const at::Tensor& b1, const at::Tensor& W2,
                const at::Tensor& b2, const at::Tensor& w3, const at::Tensor& b3, const at::Tensor& y, double dy_scale,
                int64_t B, c10::optional<at::Tensor> rows, const at::Tensor& dZ2, c10::optional<at::Tensor> pred,
-               const at::Tensor& red, bool dz_frag, c10::optional<at::Tensor> W2T, bool dz_mask) {
+               const at::Tensor& red, bool dz_frag, c10::optional<at::Tensor> W2T) {
   constexpr int64_t H = 256;
   check_t(X, at::kBFloat16, "X");
   const int64_t nrows = check_x_rows(X, Fp, B, rows);
@@ -603,7 +603,7 @@ bool mlp2_step(const at::Tensor& X, int64_t Fp, const at::Tensor& W1, const at::
   const c10::hip::OptionalHIPGuardMasqueradingAsCUDA guard(X.device());
   return wf::launch_mlp2_step(bfp(X), (int)Fp, bfp(W1), fp(b1), bfp(W2), fp(b2), fp(w3), fp(b3), fp(y), (float)dy_scale,
                               (int)B, rows_ptr(rows, B), nrows, bfp(dZ2), opt_ptr<float>(pred, at::kFloat, "pred", B),
-                              fp(red), dz_frag, cur_stream(), w2t, dz_mask);
+                              fp(red), dz_frag, cur_stream(), w2t);
 }
 
 // dW2 from the fragment-layout dZ2 of mlp2_step(dz_frag=True) into the spread scratch's dW2
@@ -626,31 +626,6 @@ int64_t mlp2_dw2f(const at::Tensor& dZ2F, const at::Tensor& X, int64_t Fp, c10::
   const c10::hip::OptionalHIPGuardMasqueradingAsCUDA guard(dZ2F.device());
   return wf::launch_mlp2_dw2f(bfp(dZ2F), bfp(X), (int)Fp, rows_ptr(rows, B), nrows, bfp(W1), fp(b1), (int)B, (int)nsplit,
                               fp(red), cur_stream());
-}
-
-// dW2 from the [H2 > 0] bits + dy that mlp2_step(dz_mask=True) wrote into the dZ2 buffer
-int64_t mlp2_dw2m(const at::Tensor& mkbuf, const at::Tensor& X, int64_t Fp, c10::optional<at::Tensor> rows,
-                  const at::Tensor& W1, const at::Tensor& b1, const at::Tensor& w3, int64_t B, int64_t nsplit,
-                  const at::Tensor& red) {
-  constexpr int64_t H = 256;
-  check_t(mkbuf, at::kBFloat16, "mkbuf");
-  // bits: 4 KiB per 128-row pass, then dy: 4 B per row (the dZ2 buffer holds 512 B per row)
-  TORCH_CHECK(((B + 127) / 128) * 4096 + B * 4 <= mkbuf.numel() * 2, "mlp2_dw2m: mkbuf too small");
-  check_t(X, at::kBFloat16, "X");
-  const int64_t nrows = check_x_rows(X, Fp, B, rows);
-  check_t(W1, at::kBFloat16, "W1");
-  check_extent(W1, H * Fp, "W1");
-  check_t(b1, at::kFloat, "b1");
-  check_extent(b1, H, "b1");
-  check_t(w3, at::kFloat, "w3");
-  check_extent(w3, H, "w3");
-  check_t(red, at::kFloat, "red");
-  check_extent(red, wf::kMlpRedFloats, "red");
-  for (const at::Tensor* t : {&mkbuf, &X, &W1})
-    TORCH_CHECK(reinterpret_cast<uintptr_t>(t->data_ptr()) % 16 == 0, "mlp2_dw2m: operands must be 16-B aligned");
-  const c10::hip::OptionalHIPGuardMasqueradingAsCUDA guard(mkbuf.device());
-  return wf::launch_mlp2_dw2m(bfp(mkbuf), bfp(X), (int)Fp, rows_ptr(rows, B), nrows, bfp(W1), fp(b1), fp(w3), (int)B,
-                              (int)nsplit, fp(red), cur_stream());
 }
 
 // Fused MLP forward (mlp_fused.hip): both 256-wide hidden layers + head (+ MSE) in one launch.
@@ -1064,7 +1039,6 @@ PYBIND11_MODULE(_C, m) {
   WF_DEF(mlp2_reduce);
   WF_DEF(mlp2_step);
   WF_DEF(mlp2_dw2f);
-  WF_DEF(mlp2_dw2m);
   WF_DEF(lstm_pack_x);
   WF_DEF(lstm_forward);
   WF_DEF(lstm_forward_persistent);

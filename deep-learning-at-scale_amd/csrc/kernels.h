@@ -132,10 +132,7 @@ void launch_mlp2_reduce(float* red, int Fp, int B, float* loss_sum, float* db3, 
 bool launch_mlp2_step(const bf16_t* X, int Fp, const bf16_t* W1, const float* b1, const bf16_t* W2, const float* b2,
                       const float* w3, const float* b3, const float* y, float dy_scale, int B, const long long* rows,
                       long nrows, bf16_t* dZ2, float* pred, float* red, bool dz_frag, hipStream_t s,
-                      const bf16_t* W2T = nullptr, bool dz_mask = false);
-// dz_mask (with W2T and dz_frag): instead of dZ2, the [H2 > 0] bits and dy go to the dZ2 buffer
-// (launch_mlp2_dw2m's input layout: per 128-row pass 8 waves x 64 ballot words, 4 KiB, then dy
-// [B] floats at byte ceil(B / 128) * 4096); dZ2 = bf16(dy w3) where a bit is set.
+                      const bf16_t* W2T = nullptr);
 // W2T (optional, [256][256] bf16 = W2 transposed): with dz_frag, the 128-row-pass kernel that
 // streams both weight images (mlp2_step128_kernel) instead of holding W2^T in registers.
 // dz_frag: dZ2 is written in the fragment layout of launch_mlp2_dw2f (B % 64 == 0) instead of
@@ -143,10 +140,6 @@ bool launch_mlp2_step(const bf16_t* X, int Fp, const bf16_t* W1, const float* b1
 // (S * 16 + b) * 512, lane (l15, g) = 16 B = rows 32S + 8g .. + 7 of unit 16b + l15.
 // dW2 from that layout without LDS (mlp_step.hip mlp2_dw2f_kernel) into the scratch's dW2 copies.
 // Returns the dW2 slab rows written (> 0), or 0 = not covered (nothing launched).
-// dW2 from the [H2 > 0] bits + dy written by launch_mlp2_step(..., dz_mask = true) (same tile
-// and MFMA order as launch_mlp2_dw2f: bit-identical dW2). Returns the dW2 slab rows, 0 = not covered.
-int launch_mlp2_dw2m(const bf16_t* mkbuf, const bf16_t* X, int Fp, const long long* rows, long nrows, const bf16_t* W1,
-                     const float* b1, const float* w3, int B, int nsplit, float* red, hipStream_t s);
 int launch_mlp2_dw2f(const bf16_t* dZ2F, const bf16_t* X, int Fp, const long long* rows, long nrows, const bf16_t* W1,
                      const float* b1, int B, int nsplit, float* red, hipStream_t s);
 

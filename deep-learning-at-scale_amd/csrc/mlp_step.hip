@@ -467,7 +467,27 @@ __global__ __launch_bounds__(512, 1) void mlp2_step_kernel(
 // Rows past B are masked (dy = 0, no stores); FRAG fragments of rows >= B are not written.
 __device__ __forceinline__ int x4_off(int row, int chunk) { return row * 64 + ((chunk ^ ((row >> 2) & 3)) << 4); }
 
-template <int NFT, bool MASK>
+// Packed-bf16 epilogue helpers of the 128-row kernel (round 5: its passes were VALU-bound —
+// 1.5k VALU vs 280 MFMA per wave and pass, 20 % MFMA busy, profiles/r5/pmc_mlp):
+//   relu_pk: ReLU of a packed pair, one v_pk_max_i16 (a negative bf16 is a negative int16, and
+//            relu(round(x)) == round(relu(x)) bit for bit);
+//   mask_pk: "d where h != 0" per 16-bit half, v_pk_min_u16 + v_pk_mul_lo_u16 (h is a ReLU
+//            output >= 0, so min(h, 1) is the 0/1 mask); asm because the compiler rewrites the
+//            pair into two compares, two selects and a merge.
+typedef short s16x2_t __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ unsigned relu_pk(unsigned p) {
+  return __builtin_bit_cast(unsigned, __builtin_elementwise_max(__builtin_bit_cast(s16x2_t, p), (s16x2_t){0, 0}));
+}
+__device__ __forceinline__ unsigned mask_pk(unsigned d, unsigned h) {
+  unsigned o;
+  asm("v_pk_min_u16 %0, %1, %3\n\tv_pk_mul_lo_u16 %0, %2, %0" : "=&v"(o) : "v"(h), "v"(d), "s"(0x00010001u));
+  return o;
+}
+__device__ __forceinline__ f32x2_t bf_lo_hi(unsigned q) {  // packed bf16 pair -> two floats
+  return f32x2_t{__uint_as_float(q << 16), __uint_as_float(q & 0xFFFF0000u)};
+}
+
+template <int NFT>
 __global__ __launch_bounds__(512, 1) void mlp2_step128_kernel(
     const bf16_t* __restrict__ X, int Fp, const bf16_t* __restrict__ W1, const float* __restrict__ b1,
     const bf16_t* __restrict__ W2, const bf16_t* __restrict__ W2T, const float* __restrict__ b2,
@@ -504,8 +524,8 @@ __global__ __launch_bounds__(512, 1) void mlp2_step128_kernel(
   const __amdgpu_buffer_rsrc_t rsA = __builtin_amdgcn_make_buffer_rsrc((void*)W2, 0, 0x7FFFFFFF, 0x00020000);
   const __amdgpu_buffer_rsrc_t rsT = __builtin_amdgcn_make_buffer_rsrc((void*)W2T, 0, 0x7FFFFFFF, 0x00020000);
   const int wlane = (u0 + l15) * MF_H + 8 * g;
+  typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
   auto wfrag = [&](int s, int m) {
-    typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
     const int kt = s & 7;
     return __builtin_bit_cast(bf16x8, (u32x4_t)__builtin_amdgcn_raw_buffer_load_b128(
                                           s < 8 ? rsA : rsT, 2 * (w2z + wlane), 2 * (16 * MF_H * m + 32 * kt), 0));
@@ -524,75 +544,111 @@ __global__ __launch_bounds__(512, 1) void mlp2_step128_kernel(
   for (int m = 0; m < MT; ++m)
 #pragma unroll
     for (int f = 0; f < NFT; ++f) dw1a[m][f] = f32x4{0.f, 0.f, 0.f, 0.f};
-  float sum3[MT][4], sum1[MT][4], sum2[MT][4];  // dw3, db1, db2 partials (lane's units 4g + r)
+  // batch sums: dw3 partials as fp32 pairs (the lane's row, units 4g + {0, 1} and 4g + {2, 3});
+  // db1 and db2 as MFMA accumulators against an all-ones B operand — the column sums of the
+  // bf16 dZ1 / dZ2 fragments the dW1 and copy-out phases already hold (A layout: M = units,
+  // K = rows), 16 MFMAs per pass instead of ~250 VALU of masked fp32 adds
+  f32x2_t s3[MT][2];
+  f32x4 db1a[MT], db2a[MT];
 #pragma unroll
-  for (int m = 0; m < MT; ++m)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) sum3[m][r] = sum1[m][r] = sum2[m][r] = 0.f;
+  for (int m = 0; m < MT; ++m) {
+    s3[m][0] = s3[m][1] = f32x2_t{0.f, 0.f};
+    db1a[m] = db2a[m] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+  const bf16x8 ones = __builtin_bit_cast(bf16x8, (u32x4_t{0x3F803F80u, 0x3F803F80u, 0x3F803F80u, 0x3F803F80u}));
   const float bias3 = b3[0];
   float lsum = 0.f, db3a = 0.f;
 
-  // next pass's inputs: thread t one 16-B X segment (row t >> 2, chunk t & 3); threads < 128 a target
+  // next pass's inputs: thread t one 16-B X segment (row t >> 2, chunk t & 3); threads < 128 a target.
+  // Row-indexed batches (rows != nullptr, nrows < 2^31): a pass's dataset row ids are loaded one
+  // pass before its gathers — loaded right before them, the dependent wait after B4 also drained
+  // every W2^T stream fragment in flight
   uint4 xv = make_uint4(0, 0, 0, 0);
   float yv = 0.f;
-  auto prefetch = [&](int ps) {
+  int ixn = 0, iyn = 0;  // clamped row ids of the pass the next prefetch() gathers
+  auto fetch_ids = [&](int ps, int tid) {
+    if (rows != nullptr) {
+      auto clampr = [&](long long r) { return (int)(r < 0 ? 0 : (r >= nrows ? nrows - 1 : r)); };
+      const int gr = ps * R + (tid >> 2), gy = ps * R + tid;
+      ixn = gr < B ? clampr(rows[gr]) : 0;
+      if (tid < R) iyn = gy < B ? clampr(rows[gy]) : 0;
+    }
+  };
+  auto prefetch = [&](int ps, int tid) {
     const int r = tid >> 2, c = tid & 3, gr = ps * R + r;
-    xv = (gr < B && 8 * c + 8 <= Fp) ? *reinterpret_cast<const uint4*>(X + data_row(rows, gr, nrows) * Fp + 8 * c)
-                                     : make_uint4(0, 0, 0, 0);
+    const size_t xr = rows != nullptr ? (size_t)ixn : (size_t)gr;
+    xv = (gr < B && 8 * c + 8 <= Fp) ? *reinterpret_cast<const uint4*>(X + xr * Fp + 8 * c) : make_uint4(0, 0, 0, 0);
     if (tid < R) {
       const int gy = ps * R + tid;
-      yv = gy < B ? y[data_row(rows, gy, nrows)] : 0.f;
+      yv = gy < B ? y[rows != nullptr ? (size_t)iyn : (size_t)gy] : 0.f;
     }
   };
   const int npass = (B + R - 1) / R;
-  auto stage = [&](int p) {
+  auto stage = [&](int p, int tid) {
     *reinterpret_cast<uint4*>(xs + p * XB + x4_off(tid >> 2, tid & 3)) = xv;
     if (tid < R) ys[p][tid] = yv;
   };
-  if ((int)blockIdx.x < npass) prefetch(blockIdx.x);
-  stage(0);
+  const int G = gridDim.x;
+  if ((int)blockIdx.x < npass) {
+    fetch_ids(blockIdx.x, tid);
+    prefetch(blockIdx.x, tid);
+  }
+  stage(0, tid);
   __syncthreads();
-  if ((int)blockIdx.x + (int)gridDim.x < npass) prefetch(blockIdx.x + gridDim.x);
+  if ((int)blockIdx.x + G < npass) {
+    fetch_ids(blockIdx.x + G, tid);
+    prefetch(blockIdx.x + G, tid);
+  }
+  if ((int)blockIdx.x + 2 * G < npass) fetch_ids(blockIdx.x + 2 * G, tid);
   wfirst();
   if (prio && __builtin_amdgcn_readfirstlane(wid) >= 4) __builtin_amdgcn_s_setprio(1);
   int par = 0;
-  for (int ps = blockIdx.x; ps < npass; ps += gridDim.x, par ^= 1) {
+  for (int ps = blockIdx.x; ps < npass; ps += G, par ^= 1) {
     const int row0 = ps * R;
     char* xt = xs + par * XB;
     // the lane coordinates, laundered per pass: every LDS address below derives from them, and
     // as loop invariants the compiler hoisted ~40 swizzled addresses out of the pass loop and
     // spilled them (one VGPR each); recomputed here they live for one phase
-    int lnv = lane;
-    asm volatile("" : "+v"(lnv));
+    int lnv = lane, tdv = tid;
+    asm volatile("" : "+v"(lnv), "+v"(tdv));
     const int l15 = lnv & 15, g = lnv >> 4, tq = l15 >> 2, tp = lnv & 3;
 
-    // ---- layer 1 (own units, 8 row tiles): H1 -> h1s
+    // ---- layer 1 (own units, 8 row tiles): H1 = relu(W1 X^T + b1) -> h1s; b1 enters as the
+    // MFMA's C operand, the ReLU on the packed bf16 pair
     f32x4 acc[MT][NR];
+    {
+      f32x4 bv[MT];
 #pragma unroll
-    for (int n = 0; n < NR; ++n) {
-      const bf16x8 xb = *reinterpret_cast<const bf16x8*>(xt + x4_off(16 * n + l15, g));
-#pragma unroll
-      for (int m = 0; m < MT; ++m)
-        acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w1f[m], xb, f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
-    }
-#pragma unroll
-    for (int m = 0; m < MT; ++m) {
-      const float4 bb = *reinterpret_cast<const float4*>(&cst[0][u0 + 16 * m + 4 * g]);
+      for (int m = 0; m < MT; ++m) {
+        const float4 bb = *reinterpret_cast<const float4*>(&cst[0][u0 + 16 * m + 4 * g]);
+        bv[m] = f32x4{bb.x, bb.y, bb.z, bb.w};
+      }
 #pragma unroll
       for (int n = 0; n < NR; ++n) {
-        const unsigned p0 = pk_bf16(fmaxf(acc[m][n][0] + bb.x, 0.f), fmaxf(acc[m][n][1] + bb.y, 0.f));
-        const unsigned p1 = pk_bf16(fmaxf(acc[m][n][2] + bb.z, 0.f), fmaxf(acc[m][n][3] + bb.w, 0.f));
-        *reinterpret_cast<uint2*>(h1s + tile_off(16 * n + l15, u0 + 16 * m + 4 * g)) = make_uint2(p0, p1);
+        const bf16x8 xb = *reinterpret_cast<const bf16x8*>(xt + x4_off(16 * n + l15, g));
+#pragma unroll
+        for (int m = 0; m < MT; ++m) acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w1f[m], xb, bv[m], 0, 0, 0);
       }
     }
-    __syncthreads();  // B2: H1 complete
-
-    // ---- layer 2 (own units, K = 256): stream steps 0..7; the B fragments (H1) rotate through
-    // one set of NR registers, fragment n of K step kt + 1 read right after its two MFMAs of kt
 #pragma unroll
     for (int m = 0; m < MT; ++m)
 #pragma unroll
-      for (int n = 0; n < NR; ++n) acc[m][n] = f32x4{0.f, 0.f, 0.f, 0.f};
+      for (int n = 0; n < NR; ++n) {
+        const unsigned p0 = relu_pk(pk_bf16(acc[m][n][0], acc[m][n][1]));
+        const unsigned p1 = relu_pk(pk_bf16(acc[m][n][2], acc[m][n][3]));
+        *reinterpret_cast<uint2*>(h1s + tile_off(16 * n + l15, u0 + 16 * m + 4 * g)) = make_uint2(p0, p1);
+      }
+    __syncthreads();  // B2: H1 complete
+
+    // ---- layer 2 (own units, K = 256): stream steps 0..7; the B fragments (H1) rotate through
+    // one set of NR registers, fragment n of K step kt + 1 read right after its two MFMAs of kt;
+    // b2 is the first K step's C operand
+    f32x4 bv2[MT];
+#pragma unroll
+    for (int m = 0; m < MT; ++m) {
+      const float4 bb = *reinterpret_cast<const float4*>(&cst[1][u0 + 16 * m + 4 * g]);
+      bv2[m] = f32x4{bb.x, bb.y, bb.z, bb.w};
+    }
     bf16x8 hb[NR];
 #pragma unroll
     for (int n = 0; n < NR; ++n) hb[n] = *reinterpret_cast<const bf16x8*>(h1s + tile_off(16 * n + l15, 8 * g));
@@ -602,7 +658,7 @@ __global__ __launch_bounds__(512, 1) void mlp2_step128_kernel(
       for (int n = 0; n < NR; ++n) {
 #pragma unroll
         for (int m = 0; m < MT; ++m)
-          acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wr[kt % WD][m], hb[n], acc[m][n], 0, 0, 0);
+          acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wr[kt % WD][m], hb[n], kt == 0 ? bv2[m] : acc[m][n], 0, 0, 0);
         if constexpr (kt + 1 < 8) {
           __builtin_amdgcn_sched_barrier(0);
           hb[n] = *reinterpret_cast<const bf16x8*>(h1s + tile_off(16 * n + l15, 32 * (kt + 1) + 8 * g));
@@ -612,38 +668,36 @@ __global__ __launch_bounds__(512, 1) void mlp2_step128_kernel(
 #pragma unroll
       for (int m = 0; m < MT; ++m) wr[kt % WD][m] = wfrag(kt + WD, m);  // steps WD .. 7 + WD (W2^T from 8)
     });
-    // H2 = relu(Z2 + b2) rounded to bf16, kept in acc; head partials of rows 16n + l15
-    float hp[NR];
+    // H2 = relu(Z2 + b2) rounded to bf16 (packed ReLU), kept in acc as floats; head partials of
+    // rows 16n + l15 as packed fp32 FMAs over unit pairs
+    f32x2_t hp2[NR];
 #pragma unroll
-    for (int n = 0; n < NR; ++n) hp[n] = 0.f;
+    for (int n = 0; n < NR; ++n) hp2[n] = f32x2_t{0.f, 0.f};
 #pragma unroll
     for (int m = 0; m < MT; ++m) {
-      const float4 bb = *reinterpret_cast<const float4*>(&cst[1][u0 + 16 * m + 4 * g]);
       const float4 ww = *reinterpret_cast<const float4*>(&cst[2][u0 + 16 * m + 4 * g]);
-      const float bv[4] = {bb.x, bb.y, bb.z, bb.w}, wv[4] = {ww.x, ww.y, ww.z, ww.w};
+      const f32x2_t w01{ww.x, ww.y}, w23{ww.z, ww.w};
 #pragma unroll
-      for (int n = 0; n < NR; ++n)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const float v = bf2f(f2bf(fmaxf(acc[m][n][r] + bv[r], 0.f)));
-          acc[m][n][r] = v;
-          hp[n] += v * wv[r];
-        }
+      for (int n = 0; n < NR; ++n) {
+        const f32x2_t v01 = bf_lo_hi(relu_pk(pk_bf16(acc[m][n][0], acc[m][n][1])));
+        const f32x2_t v23 = bf_lo_hi(relu_pk(pk_bf16(acc[m][n][2], acc[m][n][3])));
+        acc[m][n] = f32x4{v01.x, v01.y, v23.x, v23.y};
+        hp2[n] = __builtin_elementwise_fma(v01, w01, hp2[n]);
+        hp2[n] = __builtin_elementwise_fma(v23, w23, hp2[n]);
+      }
     }
 #pragma unroll
     for (int n = 0; n < NR; ++n) {
-      hp[n] += __shfl_xor(hp[n], 16, 64);
-      hp[n] += __shfl_xor(hp[n], 32, 64);
-    }
-    if (g == 0) {
-#pragma unroll
-      for (int n = 0; n < NR; ++n) hred[16 * n + l15][wid] = hp[n];
+      float hp = hp2[n].x + hp2[n].y;
+      hp += __shfl_xor(hp, 16, 64);
+      hp += __shfl_xor(hp, 32, 64);
+      if (g == 0) hred[16 * n + l15][wid] = hp;
     }
     __syncthreads();  // B3: head partials complete
 
     // ---- prediction, dy, loss of rows 16n + l15; wave 0 lane group g owns rows 16n + l15 for
     // n = g and n = g + 4 (their loss, db3 and prediction store)
-    float dyn[NR], pst[2] = {0.f, 0.f}, pdy[2] = {0.f, 0.f};
+    float dyn[NR], pst[2] = {0.f, 0.f};
     int pgr[2] = {-1, -1};
 #pragma unroll
     for (int n = 0; n < NR; ++n) {
@@ -657,74 +711,67 @@ __global__ __launch_bounds__(512, 1) void mlp2_step128_kernel(
         dyn[n] = dy_scale * diff;
         if (wid == 0 && (n & 3) == g) {
           pst[n >> 2] = p;
-          pdy[n >> 2] = dyn[n];
           pgr[n >> 2] = gr;
           lsum += diff * diff;
           db3a += dyn[n];
         }
       }
     }
-    // MASK: the [H2 > 0] bits instead of dZ2 for the dW2 kernel (dZ2 = bf16(dy w3) where set, so
-    // dy and the bits rebuild it bit for bit): ballot (m, n, r) = rows 16n + (bit & 15) of unit
-    // u0 + 16m + 4(bit >> 4) + r, gathered into lane k = (m * 8 + n) * 4 + r
-    unsigned mlo = 0u, mhi = 0u;
-    if constexpr (MASK) {
-#pragma unroll
-      for (int m = 0; m < MT; ++m)
-#pragma unroll
-        for (int n = 0; n < NR; ++n)
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const unsigned long long bl = __ballot(acc[m][n][r] > 0.f);
-            const bool mine = lnv == (m * NR + n) * 4 + r;
-            mlo = mine ? (unsigned)bl : mlo;
-            mhi = mine ? (unsigned)(bl >> 32) : mhi;
-          }
-    }
-    // ---- dZ2 = dy w3^T * [H2 > 0] (own units) -> zs; dw3, db2 partials
+    // ---- dZ2 = bf16(dy w3) where H2 > 0 (own units) -> zs; dw3 partials. The product is rounded
+    // first and masked on the packed pair (the same bits as rounding the masked product)
 #pragma unroll
     for (int m = 0; m < MT; ++m) {
       const float4 ww = *reinterpret_cast<const float4*>(&cst[2][u0 + 16 * m + 4 * g]);
-      const float wv[4] = {ww.x, ww.y, ww.z, ww.w};
+      const f32x2_t w01{ww.x, ww.y}, w23{ww.z, ww.w};
 #pragma unroll
       for (int n = 0; n < NR; ++n) {
-        float t[4];
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          sum3[m][r] += acc[m][n][r] * dyn[n];
-          t[r] = acc[m][n][r] > 0.f ? dyn[n] : 0.f;
-          sum2[m][r] += t[r];
-        }
-        *reinterpret_cast<uint2*>(zs + tile_off(16 * n + l15, u0 + 16 * m + 4 * g)) =
-            make_uint2(pk_bf16(t[0] * wv[0], t[1] * wv[1]), pk_bf16(t[2] * wv[2], t[3] * wv[3]));
+        const f32x2_t dd{dyn[n], dyn[n]};
+        const f32x2_t v01{acc[m][n][0], acc[m][n][1]}, v23{acc[m][n][2], acc[m][n][3]};
+        s3[m][0] = __builtin_elementwise_fma(v01, dd, s3[m][0]);
+        s3[m][1] = __builtin_elementwise_fma(v23, dd, s3[m][1]);
+        const f32x2_t z01 = dd * w01, z23 = dd * w23;
+        const unsigned d0 = mask_pk(pk_bf16(z01.x, z01.y), pk_bf16(v01.x, v01.y));
+        const unsigned d1 = mask_pk(pk_bf16(z23.x, z23.y), pk_bf16(v23.x, v23.y));
+        *reinterpret_cast<uint2*>(zs + tile_off(16 * n + l15, u0 + 16 * m + 4 * g)) = make_uint2(d0, d1);
       }
     }
     // the sums materialised HERE: left to itself the compiler sank these adds to the end of the
-    // pass and kept all 64 H2 values (and the dZ2 masks) alive through dH1 — 200+ spilled VGPRs
+    // pass and kept all 64 H2 values alive through dH1 — 200+ spilled VGPRs
 #pragma unroll
-    for (int m = 0; m < MT; ++m)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) asm volatile("" : "+v"(sum3[m][r]), "+v"(sum2[m][r]));
+    for (int m = 0; m < MT; ++m) asm volatile("" : "+v"(s3[m][0]), "+v"(s3[m][1]));
     asm volatile("" : "+v"(lsum), "+v"(db3a));
-    if constexpr (MASK) {
-      // the pass's bits (wave w: 512 B at word (ps * 8 + w) * 64) and dy of its rows (< B), stored
-      // here (kept to after dH1 the two words pushed the kernel into 23 more spills)
-      unsigned long long* mk = reinterpret_cast<unsigned long long*>(dZ2);
-      float* dyo = reinterpret_cast<float*>(reinterpret_cast<char*>(dZ2) + (size_t)npass * 4096);
-      mk[((size_t)ps * NW + wid) * 64 + lnv] = ((unsigned long long)mhi << 32) | mlo;
-#pragma unroll
-      for (int q = 0; q < 2; ++q)
-        if (pgr[q] >= 0) dyo[pgr[q]] = pdy[q];
-    }
-    if (ps + (int)gridDim.x < npass) stage(par ^ 1);
+    if (ps + G < npass) stage(par ^ 1, tdv);
     __syncthreads();  // B4: dZ2 complete, next pass's X / y staged
-    if (ps + 2 * (int)gridDim.x < npass) prefetch(ps + 2 * gridDim.x);
+    if (ps + 2 * G < npass) {
+      prefetch(ps + 2 * G, tdv);
+      if (ps + 3 * G < npass) fetch_ids(ps + 3 * G, tdv);
+    }
 
+    // ---- dZ2 copy-out as dW2 A fragments (fragment (S, b) = 32 rows x 16 units): wave w writes
+    // the pass's 4 row groups of its own unit blocks 2w, 2w + 1, and sums each fragment's rows
+    // into db2 on the way (one MFMA against the ones operand)
+    // (rows past B hold zeros in zs: read and summed unconditionally, only the store is skipped).
+    // Here, before dH1, the H2 / dH1 accumulators are dead: room for the 8 fragments in flight
+    bf16x8 onesv = ones;
+    asm volatile("" : "+v"(onesv));  // one 4-VGPR copy per phase (left alone the splat was rebuilt per MFMA)
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const int mq = q & 1, sst = q >> 1, b = 2 * wid + mq;
+      bf16x8 v;
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const bf16x4 t = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+            (lds_bf16x4*)(zs + tile_off(32 * sst + 8 * g + 4 * h + tq, 16 * b + 4 * tp)));
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[4 * h + e] = t[e];
+      }
+      db2a[mq] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(v, onesv, db2a[mq], 0, 0, 0);
+      if (row0 + 32 * sst < B) {
+        const size_t S = (size_t)(row0 >> 5) + sst;
+        *reinterpret_cast<bf16x8*>(dZ2 + ((S * 16 + b) * 64 + lnv) * 8) = v;
+      }
+    }
     // ---- dH1^T (own units k, K = 256 output units) = W2^T dZ2^T: stream steps 8..15
-#pragma unroll
-    for (int m = 0; m < MT; ++m)
-#pragma unroll
-      for (int n = 0; n < NR; ++n) acc[m][n] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int n = 0; n < NR; ++n) hb[n] = *reinterpret_cast<const bf16x8*>(zs + tile_off(16 * n + l15, 8 * g));
     w2z = 0;
@@ -735,7 +782,8 @@ __global__ __launch_bounds__(512, 1) void mlp2_step128_kernel(
       for (int n = 0; n < NR; ++n) {
 #pragma unroll
         for (int m = 0; m < MT; ++m)
-          acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wr[(8 + kt) % WD][m], hb[n], acc[m][n], 0, 0, 0);
+          acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wr[(8 + kt) % WD][m], hb[n],
+                                                              kt == 0 ? f32x4{0.f, 0.f, 0.f, 0.f} : acc[m][n], 0, 0, 0);
         if constexpr (kt + 1 < 8) {
           __builtin_amdgcn_sched_barrier(0);
           hb[n] = *reinterpret_cast<const bf16x8*>(zs + tile_off(16 * n + l15, 32 * (kt + 1) + 8 * g));
@@ -750,53 +798,24 @@ __global__ __launch_bounds__(512, 1) void mlp2_step128_kernel(
 #pragma unroll
     for (int q = 0; q < 2; ++q)
       if (pgr[q] >= 0 && pred != nullptr) pred[pgr[q]] = pst[q];
-    // ---- dZ2 copy-out as dW2 A fragments (fragment (S, b) = 32 rows x 16 units; wave w writes
-    // fragments 8w .. 8w + 7 of the pass: row group S = row0 / 32 + (f >> 4), unit block f & 15)
-#pragma unroll
-    for (int q = 0; q < (MASK ? 0 : 8); ++q) {
-      const int f = 8 * wid + q, sst = f >> 4, b = f & 15;
-      if (row0 + 32 * sst < B) {
-        bf16x8 v;
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-          const bf16x4 t = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-              (lds_bf16x4*)(zs + tile_off(32 * sst + 8 * g + 4 * h + tq, 16 * b + 4 * tp)));
-#pragma unroll
-          for (int e = 0; e < 4; ++e) v[4 * h + e] = t[e];
-        }
-        const size_t S = (size_t)(row0 >> 5) + sst;
-        *reinterpret_cast<bf16x8*>(dZ2 + ((S * 16 + b) * 64 + lnv) * 8) = v;
-      }
-    }
-    // ---- dZ1 = dH1 * [H1 > 0] over the same 8 bytes of h1s; db1 partials
+    // ---- dZ1 = bf16(dH1) where H1 > 0, over the same 8 bytes of h1s (rows past B: dZ2 = 0 there,
+    // so dH1 and dZ1 are zero without a row test)
 #pragma unroll
     for (int m = 0; m < MT; ++m) {
 #pragma unroll
       for (int n = 0; n < NR; ++n) {
-        const int r = 16 * n + l15;
-        uint2* pp = reinterpret_cast<uint2*>(h1s + tile_off(r, u0 + 16 * m + 4 * g));
+        uint2* pp = reinterpret_cast<uint2*>(h1s + tile_off(16 * n + l15, u0 + 16 * m + 4 * g));
         const uint2 hv = *pp;
-        const bool rok = row0 + r < B;
-        const int hw2[2] = {rok ? (int)hv.x : 0, rok ? (int)hv.y : 0};
-        unsigned ow[2];
-#pragma unroll
-        for (int q = 0; q < 2; ++q) {
-          const bool on0 = (hw2[q] << 16) > 0, on1 = hw2[q] > 0xFFFF;
-          const float t0 = on0 ? acc[m][n][2 * q] : 0.f, t1 = on1 ? acc[m][n][2 * q + 1] : 0.f;
-          sum1[m][2 * q] += t0;
-          sum1[m][2 * q + 1] += t1;
-          ow[q] = pk_bf16(t0, t1);
-        }
-        *pp = make_uint2(ow[0], ow[1]);
+        const unsigned o0 = mask_pk(pk_bf16(acc[m][n][0], acc[m][n][1]), hv.x);
+        const unsigned o1 = mask_pk(pk_bf16(acc[m][n][2], acc[m][n][3]), hv.y);
+        *pp = make_uint2(o0, o1);
       }
     }
-#pragma unroll
-    for (int m = 0; m < MT; ++m)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) asm volatile("" : "+v"(sum1[m][r]));
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_wave_barrier();
-    // ---- dW1^T slice (32 units x Fp) += dZ1^T X over the pass's 128 rows
+    // ---- dW1^T slice (32 units x Fp) += dZ1^T X over the pass's 128 rows; db1 += dZ1^T 1
+    onesv = ones;
+    asm volatile("" : "+v"(onesv));
 #pragma unroll
     for (int kk = 0; kk < R / 32; ++kk) {
       bf16x8 af[MT], bfr[NFT];
@@ -819,16 +838,19 @@ __global__ __launch_bounds__(512, 1) void mlp2_step128_kernel(
         }
       }
 #pragma unroll
-      for (int m = 0; m < MT; ++m)
+      for (int m = 0; m < MT; ++m) {
 #pragma unroll
         for (int f = 0; f < NFT; ++f)
           dw1a[m][f] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[m], bfr[f], dw1a[m][f], 0, 0, 0);
+        db1a[m] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[m], onesv, db1a[m], 0, 0, 0);
+      }
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_wave_barrier();
   }
 
-  // ---- batch sums -> copy blockIdx % kMlpRedCopies of the scratch; dW1 -> this workgroup's row
+  // ---- batch sums -> copy blockIdx % kMlpRedCopies of the scratch; dW1 -> this workgroup's row.
+  // db1 / db2: every column of the ones-MFMA accumulators holds the same sums (lanes l15 == 0)
   float* rb = red + (blockIdx.x & (kMlpRedCopies - 1)) * kMlpRedRow;
   float* slab = red + kMlpRedSlabOff + (size_t)blockIdx.x * kMlpRedSlabRow;
   const float tl = block_sum<512>(lsum, lred);
@@ -840,18 +862,15 @@ __global__ __launch_bounds__(512, 1) void mlp2_step128_kernel(
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int u = u0 + 16 * m + 4 * g + r;
-      float v[3] = {sum3[m][r], sum1[m][r], sum2[m][r] * cst[2][u]};
-#pragma unroll
-      for (int k = 0; k < 3; ++k) {
-        v[k] += __shfl_xor(v[k], 1, 64);
-        v[k] += __shfl_xor(v[k], 2, 64);
-        v[k] += __shfl_xor(v[k], 4, 64);
-        v[k] += __shfl_xor(v[k], 8, 64);
-      }
+      float v = s3[m][r >> 1][r & 1];
+      v += __shfl_xor(v, 1, 64);
+      v += __shfl_xor(v, 2, 64);
+      v += __shfl_xor(v, 4, 64);
+      v += __shfl_xor(v, 8, 64);
       if (l15 == 0) {
-        if (v[0] != 0.f) atomicAdd(rb + kMlpRedDw3 + u, v[0]);
-        if (v[1] != 0.f) atomicAdd(rb + kMlpRedDb1 + u, v[1]);
-        if (v[2] != 0.f) atomicAdd(rb + kMlpRedDb2 + u, v[2]);
+        if (v != 0.f) atomicAdd(rb + kMlpRedDw3 + u, v);
+        if (db1a[m][r] != 0.f) atomicAdd(rb + kMlpRedDb1 + u, db1a[m][r]);
+        if (db2a[m][r] != 0.f) atomicAdd(rb + kMlpRedDb2 + u, db2a[m][r]);
       }
     }
 #pragma unroll
@@ -885,212 +904,6 @@ __global__ __launch_bounds__(512, 1) void mlp2_step128_kernel(
 //  * grid = 2 tiles x nsplit row ranges; xcd_remap keeps a range's two tiles on one XCD, so
 //    X (read by both tiles) hits L2 the second time.
 constexpr int DW2F_MAX_ROWS = 2048;                      // rows per workgroup (the row-id table)
-
-// ----------------------------------------------------------------------------------------
-// dW2 from the [H2 > 0] bits and dy (mlp2_step128_kernel<., MASK = true>) instead of a stored
-// dZ2: 36 B per row from HBM instead of 512 (round 5; the dZ2 round trip was 134 MB written +
-// 134 MB read per step at B = 262,144). dZ2 = bf16(dy w3[u]) where a bit is set, so the rebuilt
-// fragments equal mlp2_dw2g_kernel's input bit for bit.
-//  * workgroup = 128 (out) x 256 (in) tile of one row range (as mlp2_dw2g_kernel): wave w
-//    owns in columns 32w and all 128 out rows, so H1 is recomputed once per column (twice there)
-//    and a chunk needs only its 16 dZ2 fragments of the tile's out units, 2 rebuilt per wave.
-//  * per 64-row chunk the DMA ring (4 slots, 3 chunks ahead) brings the 1-KiB bit block of the
-//    tile's 4 step-kernel waves (wave 0), the chunk's 64 dy (wave 1) and the 4-KiB X tile (waves
-//    0-3); each wave rebuilds its fragments of the NEXT chunk into a 2 x 16-KiB double buffer
-//    while the workgroup computes this one: one barrier per chunk.
-constexpr int DW2M_SLOTS = 4;
-constexpr int DW2M_MB = 1024, DW2M_DYB = 1024, DW2M_XB = MF_ROWS * 64;
-constexpr int DW2M_SLOT = DW2M_MB + DW2M_DYB + DW2M_XB;
-constexpr int DW2M_FRAG = 16 * 1024;
-__global__ __launch_bounds__(512, 1) void mlp2_dw2m_kernel(const unsigned long long* __restrict__ mk,
-                                                           const float* __restrict__ dyo, const bf16_t* __restrict__ X,
-                                                           int Fp, const long long* __restrict__ rows, long nrows,
-                                                           const bf16_t* __restrict__ W1, const float* __restrict__ b1,
-                                                           const float* __restrict__ w3, int kchunk,
-                                                           float* __restrict__ dW2, float* __restrict__ slab,
-                                                           int slab_row0, int prio) {
-  __shared__ __attribute__((aligned(16))) char smem[DW2M_SLOTS * DW2M_SLOT + 2 * DW2M_FRAG + DW2F_MAX_ROWS * 4];
-  char* fragb = smem + DW2M_SLOTS * DW2M_SLOT;
-  int* ridx = reinterpret_cast<int*>(fragb + 2 * DW2M_FRAG);
-  const int tid = threadIdx.x, lane = tid & 63, l15 = lane & 15, g = lane >> 4;
-  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int L = xcd_remap(blockIdx.x, gridDim.x);
-  const int split = L >> 1, t = L & 1;
-  const int o0 = 128 * t, n0 = 32 * wid;  // out rows of the tile, in columns of this wave
-  const int kbeg = split * kchunk, nch = kchunk / MF_ROWS;
-  for (int i = tid; i < kchunk; i += 512) ridx[i] = rows != nullptr ? (int)data_row(rows, kbeg + i, nrows) : kbeg + i;
-  __syncthreads();
-  if (prio && wid >= 4) __builtin_amdgcn_s_setprio(1);
-
-  bf16x8 w1f[2];
-  float bias[2];
-#pragma unroll
-  for (int nb = 0; nb < 2; ++nb) {
-    const int u = n0 + 16 * nb + l15;
-    w1f[nb] = 8 * g + 8 <= Fp ? *reinterpret_cast<const bf16x8*>(W1 + (size_t)u * Fp + 8 * g)
-                              : bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
-    bias[nb] = b1[u];
-  }
-  // the 2 fragments this wave rebuilds per chunk: f = 2 wid + qq -> (32-row step f >> 3, out
-  // block mb = f & 7 of the tile); lane unit u = o0 + 16 mb + l15 = step-kernel wave u >> 5, tile
-  // (u >> 4) & 1, lane group l15 >> 2, r = l15 & 3; its 8 rows 8g .. 8g + 7 of the step are bits
-  // 16 (l15 >> 2) + 8 (g & 1) of the ballot word of tile n' = 2 (f >> 3) + (g >> 1) of the half pass
-  float w3u[2];
-  int wofs[2];
-#pragma unroll
-  for (int qq = 0; qq < 2; ++qq) {
-    const int f = 2 * wid + qq, s2 = f >> 3, mb = f & 7, u = o0 + 16 * mb + l15;
-    w3u[qq] = w3[u];
-    // bit block in LDS: run (step-kernel wave (u >> 5) - 4t, tile (u >> 4) & 1) of 16 words
-    wofs[qq] = ((((u >> 5) - 4 * t) * 2 + ((u >> 4) & 1)) * 16 + (2 * s2 + (g >> 1)) * 4 + (l15 & 3)) * 8;
-  }
-  const int bsh = 16 * (l15 >> 2) + 8 * (g & 1);
-
-  const int xrow = 16 * (wid & 3) + (lane >> 2);
-  int xq = (lane & 3) ^ ((xrow >> 3) & 3);
-  if (8 * xq + 8 > Fp) xq = 0;
-  auto issue = [&](int c, int slot) {
-    char* st = smem + slot * DW2M_SLOT;
-    const int r0 = kbeg + c * MF_ROWS, ps = r0 >> 7, hh = (r0 >> 6) & 1;
-    if (wid == 0) {  // bits: 8 runs of 128 B (step-kernel waves 4t .. 4t + 3 x tiles 0, 1: words n' = 4 hh ..)
-      const int sg = lane >> 3;
-      const char* src = reinterpret_cast<const char*>(mk) +
-                        ((((size_t)ps * 8 + 4 * t + (sg >> 1)) * 64 + ((sg & 1) * 8 + 4 * hh) * 4) * 8 + (lane & 7) * 16);
-      __builtin_amdgcn_global_load_lds((const void*)src, (lds_void*)st, 16, 0, 0);
-    } else if (wid == 1) {  // dy of the 64 rows (lanes 16.. repeat lanes 0..15)
-      __builtin_amdgcn_global_load_lds((const void*)(dyo + r0 + 4 * (lane & 15)), (lds_void*)(st + DW2M_MB), 16, 0, 0);
-    }
-    if (wid < 4) {
-      const size_t xr = (size_t)ridx[c * MF_ROWS + xrow];
-      __builtin_amdgcn_global_load_lds((const void*)(X + xr * Fp + 8 * xq),
-                                       (lds_void*)(st + DW2M_MB + DW2M_DYB + wid * 1024), 16, 0, 0);
-    }
-  };
-  // at most n chunks' DMAs of this wave in flight (waves 0-1 issue 2 per chunk, 2-3 one)
-  auto dma_wait = [&](auto nc) {
-    constexpr int n = decltype(nc)::value;
-    if (wid < 2)
-      wait_vmcnt<2 * n>();
-    else if (wid < 4)
-      wait_vmcnt<n>();
-  };
-  // rebuild fragment qq of this wave for the chunk in DMA slot `slot` into fragment buffer fb
-  auto rebuild = [&](int slot, char* fb, int qq) {
-    const char* st = smem + slot * DW2M_SLOT;
-    const int f = 2 * wid + qq, s2 = f >> 3;
-    const unsigned long long word = *reinterpret_cast<const unsigned long long*>(st + wofs[qq]);
-    const unsigned bits = (unsigned)(word >> bsh);
-    const float4 d0 = *reinterpret_cast<const float4*>(st + DW2M_MB + (32 * s2 + 8 * g) * 4);
-    const float4 d1 = *reinterpret_cast<const float4*>(st + DW2M_MB + (32 * s2 + 8 * g + 4) * 4);
-    const float dv[8] = {d0.x, d0.y, d0.z, d0.w, d1.x, d1.y, d1.z, d1.w};
-    unsigned pk[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      // sign-extended 1-bit fields (v_bfe_i32): all ones where the bit is set
-      const unsigned mlo = (unsigned)((int)(bits << (31 - 2 * i)) >> 31);
-      const unsigned mhi = (unsigned)((int)(bits << (30 - 2 * i)) >> 31);
-      pk[i] = pk_bf16(dv[2 * i] * w3u[qq], dv[2 * i + 1] * w3u[qq]) & ((mlo & 0xFFFFu) | (mhi & 0xFFFF0000u));
-    }
-    *reinterpret_cast<uint4*>(fb + f * 1024 + lane * 16) = make_uint4(pk[0], pk[1], pk[2], pk[3]);
-  };
-  const int xg = 8 * g + 8 <= Fp ? g : 0;
-  const int xr0 = 8 * (l15 >> 2) + (l15 & 3);
-
-  f32x4 acc[8][2];
-#pragma unroll
-  for (int i = 0; i < 8; ++i)
-#pragma unroll
-    for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  const int last = nch - 1;
-#pragma unroll
-  for (int k = 0; k < DW2M_SLOTS - 1; ++k) issue(min(k, last), k);
-  dma_wait(std::integral_constant<int, DW2M_SLOTS - 2>{});  // chunk 0 (this wave's pieces)
-  __builtin_amdgcn_s_barrier();                              // ... every wave's
-  asm volatile("" ::: "memory");
-  rebuild(0, fragb, 0);
-  rebuild(0, fragb, 1);
-  for (int c = 0; c < nch; ++c) {
-    const int slot = c & (DW2M_SLOTS - 1);
-    // chunk c + 1's pieces landed (this wave); the barrier publishes them and chunk c's rebuilt
-    // fragments, and frees fragment buffer (c + 1) & 1 and DMA slot (c - 1) & 3
-    dma_wait(std::integral_constant<int, DW2M_SLOTS - 3>{});
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-    issue(min(c + DW2M_SLOTS - 1, last), (c + DW2M_SLOTS - 1) & (DW2M_SLOTS - 1));
-    // the next chunk's fragments are rebuilt in the MFMA shadow of this one (one after each 32-row
-    // step's dW MFMAs; the last chunk rebuilds a harmless copy of itself into the idle buffer)
-    const int nslot = (min(c + 1, last)) & (DW2M_SLOTS - 1);
-    char* nfb = fragb + ((c + 1) & 1) * DW2M_FRAG;
-    const char* st = smem + slot * DW2M_SLOT;
-    const char* xs = st + DW2M_MB + DW2M_DYB;
-    const char* fa = fragb + (c & 1) * DW2M_FRAG;
-    bf16x8 xfa[2][2], afa[2][8];
-    auto frags = [&](int s2) {
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        const int r = 32 * s2 + xr0 + 4 * h;
-        xfa[s2][h] = *reinterpret_cast<const bf16x8*>(xs + r * 64 + ((xg ^ ((r >> 3) & 3)) << 4));
-      }
-      __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-      for (int mb = 0; mb < 8; ++mb)
-        afa[s2][mb] = *reinterpret_cast<const bf16x8*>(fa + (s2 * 8 + mb) * 1024 + lane * 16);
-    };
-    frags(0);
-    __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-    for (int s2 = 0; s2 < 2; ++s2) {
-      bf16x8 hb[2];
-      const bf16x8(&xf)[2] = xfa[s2];
-#pragma unroll
-      for (int nb = 0; nb < 2; ++nb) {
-        const f32x4 c0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xf[0], w1f[nb], f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
-        const f32x4 c1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xf[1], w1f[nb], f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
-        const unsigned p0 = pk_bf16(fmaxf(c0[0] + bias[nb], 0.f), fmaxf(c0[1] + bias[nb], 0.f));
-        const unsigned p1 = pk_bf16(fmaxf(c0[2] + bias[nb], 0.f), fmaxf(c0[3] + bias[nb], 0.f));
-        const unsigned p2 = pk_bf16(fmaxf(c1[0] + bias[nb], 0.f), fmaxf(c1[1] + bias[nb], 0.f));
-        const unsigned p3 = pk_bf16(fmaxf(c1[2] + bias[nb], 0.f), fmaxf(c1[3] + bias[nb], 0.f));
-        typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
-        hb[nb] = __builtin_bit_cast(bf16x8, (u32x4_t{p0, p1, p2, p3}));
-      }
-      if (s2 == 0) {
-        __builtin_amdgcn_sched_barrier(0);
-        frags(1);
-        __builtin_amdgcn_sched_barrier(0);
-      }
-#pragma unroll
-      for (int mb = 0; mb < 8; ++mb) {
-#pragma unroll
-        for (int nb = 0; nb < 2; ++nb)
-          acc[mb][nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(afa[s2][mb], hb[nb], acc[mb][nb], 0, 0, 0);
-      }
-      __builtin_amdgcn_sched_barrier(0);
-      rebuild(nslot, nfb, s2);
-      __builtin_amdgcn_sched_barrier(0);
-    }
-  }
-  wait_vmcnt<0>();  // the clamped fetches past the range must land before the workgroup ends
-  const int srow = slab_row0 + split;
-  if (srow < kMlpRedSlab2Rows) {
-    float* dst = slab + (size_t)srow * 65536;
-#pragma unroll
-    for (int mb = 0; mb < 8; ++mb)
-#pragma unroll
-      for (int r = 0; r < 4; ++r)
-#pragma unroll
-        for (int nb = 0; nb < 2; ++nb) dst[(size_t)(o0 + 16 * mb + 4 * g + r) * MF_H + n0 + 16 * nb + l15] = acc[mb][nb][r];
-  } else {
-    float* dst = dW2 + (size_t)(split & (kMlpRedCopies2 - 1)) * 65536;
-#pragma unroll
-    for (int mb = 0; mb < 8; ++mb)
-#pragma unroll
-      for (int r = 0; r < 4; ++r)
-#pragma unroll
-        for (int nb = 0; nb < 2; ++nb)
-          atomicAdd(dst + (size_t)(o0 + 16 * mb + 4 * g + r) * MF_H + n0 + 16 * nb + l15, acc[mb][nb][r]);
-  }
-}
 
 // ----------------------------------------------------------------------------------------
 // dW2 from the fragment-layout dZ2 (the method above) with a 128 (out) x 256 (in) tile (round
@@ -1241,7 +1054,7 @@ __global__ __launch_bounds__(512, 1) void mlp2_dw2g_kernel(const bf16_t* __restr
 bool launch_mlp2_step(const bf16_t* X, int Fp, const bf16_t* W1, const float* b1, const bf16_t* W2, const float* b2,
                       const float* w3, const float* b3, const float* y, float dy_scale, int B, const long long* rows,
                       long nrows, bf16_t* dZ2, float* pred, float* red, bool dz_frag, hipStream_t s,
-                      const bf16_t* W2T, bool dz_mask) {
+                      const bf16_t* W2T) {
   // the reduce sums the dW1 rows only when it expects the 8-wave backward's layout
   if (B <= 0 || Fp > 32 || Fp % 8 != 0 || red == nullptr || !mlp_bwd8()) return false;
   if (dz_frag && B % MF_ROWS != 0) return false;
@@ -1252,17 +1065,14 @@ bool launch_mlp2_step(const bf16_t* X, int Fp, const bf16_t* W1, const float* b1
   // static s_setprio 1 for waves 4-7 (+0.2 to +1.1 % in three interleaved pairs, chunk span
   // 17.5k -> 17.1k cycles, profiles/r4/mlp_prio; the WELLFLOW_STEP_PRIO A/B knob was removed)
   constexpr int prio = 1;
-  if (dz_mask && W2T == nullptr) return false;  // the [H2 > 0]-bit output exists in the 128-row kernel only
   if (W2T != nullptr && dz_frag && !stamp) {  // 128-row passes, both weight images streamed
-#define WF_STEP128(NFT, MK)                                                                                      \
-  hipLaunchKernelGGL((mlp2_step128_kernel<NFT, MK>), dim3(grid), dim3(512), 0, s, X, Fp, W1, b1, W2, W2T, b2, w3, b3, \
-                     y, dy_scale, B, rows, nrows, dZ2, pred, red, prio)
-    if (Fp <= 16) {
-      if (dz_mask) WF_STEP128(1, true); else WF_STEP128(1, false);
-    } else {
-      if (dz_mask) WF_STEP128(2, true); else WF_STEP128(2, false);
-    }
-#undef WF_STEP128
+    if (rows != nullptr && nrows > 0x7FFFFFFFL) return false;  // 32-bit row ids in the kernel
+    if (Fp <= 16)
+      hipLaunchKernelGGL(mlp2_step128_kernel<1>, dim3(grid), dim3(512), 0, s, X, Fp, W1, b1, W2, W2T, b2, w3, b3, y,
+                         dy_scale, B, rows, nrows, dZ2, pred, red, prio);
+    else
+      hipLaunchKernelGGL(mlp2_step128_kernel<2>, dim3(grid), dim3(512), 0, s, X, Fp, W1, b1, W2, W2T, b2, w3, b3, y,
+                         dy_scale, B, rows, nrows, dZ2, pred, red, prio);
     return true;
   }
   if (stamp && Fp <= 16 && dz_frag) {
@@ -1314,29 +1124,4 @@ int launch_mlp2_dw2f(const bf16_t* dZ2F, const bf16_t* X, int Fp, const long lon
 }
 
 
-int launch_mlp2_dw2m(const bf16_t* mkbuf, const bf16_t* X, int Fp, const long long* rows, long nrows, const bf16_t* W1,
-                     const float* b1, const float* w3, int B, int nsplit, float* red, hipStream_t s) {
-  if (B <= 0 || B % MF_ROWS != 0 || Fp > 32 || Fp % 8 != 0 || red == nullptr) return 0;
-  const unsigned long long* mk = reinterpret_cast<const unsigned long long*>(mkbuf);
-  const float* dyo = reinterpret_cast<const float*>(reinterpret_cast<const char*>(mkbuf) + (size_t)((B + 127) / 128) * 4096);
-  constexpr int kMaxBlock = 128 * DW2F_MAX_ROWS;
-  constexpr int prio = 1;
-  int srow = 0;
-  for (int r0 = 0; r0 < B; r0 += kMaxBlock) {
-    const int Bb = B - r0 < kMaxBlock ? B - r0 : kMaxBlock;
-    const int chunks = Bb / MF_ROWS;
-    int ns = nsplit < 1 ? 1 : (nsplit > 128 ? 128 : nsplit);
-    while (ns < 128 && (chunks + ns - 1) / ns * MF_ROWS > DW2F_MAX_ROWS) ++ns;
-    while (ns > 1 && chunks % ns != 0) --ns;
-    const int kchunk = (chunks / ns) * MF_ROWS;
-    if (kchunk > DW2F_MAX_ROWS) return 0;
-    // row block r0 (a multiple of 128 * 2048 rows: whole passes): its bit words start at pass r0 / 128
-    hipLaunchKernelGGL(mlp2_dw2m_kernel, dim3(2 * ns), dim3(512), 0, s, mk + (size_t)(r0 / 128) * 512, dyo + r0,
-                       rows != nullptr ? X : X + (size_t)r0 * Fp, Fp, rows != nullptr ? rows + r0 : nullptr,
-                       rows != nullptr ? nrows : (long)Bb, W1, b1, w3, kchunk, red + (size_t)kMlpRedCopies * kMlpRedRow,
-                       red + kMlpRedSlab2Off, srow, prio);
-    srow += ns;
-  }
-  return srow < kMlpRedSlab2Rows ? srow : kMlpRedSlab2Rows;
-}
 }  // namespace wf

@@ -204,11 +204,6 @@ class NativeMLP:
         self.w2t = None
         if (self.red is not None and self.dw2_frag and os.environ.get("WELLFLOW_MLP_STEP128", "1") != "0"):
             self.w2t = torch.empty(256 * 256, dtype=bf, device=dev)
-        # ... optionally passing only the [H2 > 0] bits and dy (36 B per row instead of dZ2's 512) to
-        # a dW2 kernel that rebuilds dZ2 bit for bit (mlp2_dw2m_kernel; WELLFLOW_MLP_DW2M=1). Off by
-        # default: measured 1.43 vs 1.46 G rows/s (the rebuild's VALU costs more than the HBM
-        # round trip it saves; profiles/r5/notes.md)
-        self.dw2_mask = self.w2t is not None and os.environ.get("WELLFLOW_MLP_DW2M", "0") == "1"
         self.sync_weights()
 
     @property
@@ -246,14 +241,10 @@ class NativeMLP:
             if red is not None and self.step_fused and not self.dw2_gemm:
                 frag = self.dw2_frag
                 w2t = self.w2t if frag else None
-                mask = w2t is not None and self.dw2_mask
                 if not C.mlp2_step(Xop, self.Fp, wl[0][0], pl[0][1], wl[1][0], pl[1][1], hw, hb, y,
-                                   2.0 * float(grad_scale), B, rows, self.dZ[1], self.pred, red, frag, w2t, mask):
+                                   2.0 * float(grad_scale), B, rows, self.dZ[1], self.pred, red, frag, w2t):
                     raise RuntimeError("NativeMLP: fused step refused the shape")
-                if mask:  # dZ2 rebuilt from the bits + dy in the dW2 kernel
-                    ok = dw2_rows = C.mlp2_dw2m(self.dZ[1], Xop, self.Fp, rows, wl[0][0], pl[0][1], hw, B,
-                                                self.dw2f_split, red)
-                elif frag:  # dW2 partials as slab rows (their count) summed by the reduce
+                if frag:  # dW2 partials as slab rows (their count) summed by the reduce
                     ok = dw2_rows = C.mlp2_dw2f(self.dZ[1], Xop, self.Fp, rows, wl[0][0], pl[0][1], B,
                                                 self.dw2f_split, red)
                 else:

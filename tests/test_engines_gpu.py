@@ -411,6 +411,29 @@ def test_mlp_bf16_input_matches_fp32_input():
     assert ((ga - gb).norm() / ga.norm()).item() < 1e-5
 
 
+def _mlp_step_close(la, pa, ga, lb, pb, gb, tag, flips: bool) -> None:
+    """Two MLP training-step paths agree: predictions, loss and gradients up to the fp32 sum
+    order (flips=False), or — against mlp2_step128_kernel, which folds b1 / b2 into the MFMA
+    accumulator and takes db1 / db2 as MFMA sums of the bf16 dZ1 / dZ2 — up to that order
+    moving a few H1 / H2 values across a bf16 rounding boundary (one ulp, 2^-8 relative, in a
+    fraction of a percent of the elements; flips=True)."""
+    assert torch.isfinite(gb).all(), tag
+    if not flips:
+        torch.testing.assert_close(pa, pb, rtol=1e-5, atol=1e-6)
+        assert abs(la - lb) <= 1e-5 * abs(la) + 1e-7, tag
+        assert ((ga - gb).norm() / ga.norm()).item() < 1e-4, tag
+        return
+    d = (pa - pb).abs()
+    off = (d > 1e-5 * pa.abs() + 1e-6).float().mean().item()
+    scale = pa.abs().max().item() + 1.0
+    print(f"{tag}: pred off-tolerance {off:.4%}, max |d| {d.max().item():.2e}, loss rel "
+          f"{abs(la - lb) / abs(la):.2e}, grad rel-norm {((ga - gb).norm() / ga.norm()).item():.2e}")
+    assert off < 0.01, tag
+    assert d.max().item() <= 2e-3 * scale, tag
+    assert abs(la - lb) <= 1e-4 * abs(la) + 1e-7, tag
+    assert ((ga - gb).norm() / ga.norm()).item() < 2e-3, tag
+
+
 @pytest.mark.parametrize("B,F", [(262144, 16), (4096, 32), (128, 8)])
 def test_mlp_recompute_step_matches_stored_h1(B, F):
     """The H1-free training step (fused forward writes only the H2 bitmask; the fused backward
@@ -435,11 +458,9 @@ def test_mlp_recompute_step_matches_stored_h1(B, F):
         out[rec] = (ls, eng.pred[:B].clone(), eng.grads.clone())
     assert eng._recompute_ok(B)
     (la, pa, ga), (lb, pb, gb) = out[False], out[True]
-    # the training forward (8 waves, 32 units each) sums the head in a different fp32 order
-    torch.testing.assert_close(pa, pb, rtol=1e-5, atol=1e-6)
-    assert abs(la - lb) <= 1e-5 * abs(la) + 1e-7
-    assert torch.isfinite(gb).all()
-    assert ((ga - gb).norm() / ga.norm()).item() < 1e-4
+    # the training forward (8 waves, 32 units each) sums the head in a different fp32 order;
+    # the default recompute step is the 128-row kernel when the engine holds W2^T
+    _mlp_step_close(la, pa, ga, lb, pb, gb, "recompute", flips=eng.w2t is not None)
 
 
 def test_mlp_spread_reduction_matches_direct_atomics():
@@ -534,10 +555,9 @@ def test_mlp_one_launch_step_matches_two_kernel_step(B, F, indexed):
     w2t = eng.w2t
     assert w2t is not None  # the default engine streams both weight images
     for name, fused, frag in (("pair", False, False), ("step", True, False), ("step_frag", True, True),
-                              ("step_frag64", True, True), ("step_mask", True, True)):
+                              ("step_frag64", True, True)):
         eng.step_fused, eng.dw2_frag = fused, frag
         eng.w2t = None if name == "step_frag64" else w2t
-        eng.dw2_mask = name == "step_mask"
         eng.dZ[1].fill_(float("nan"))
         ls = eng.forward_backward(X, Y, grad_scale=1.0 / B, rows=idx).item()
         torch.cuda.synchronize()
@@ -546,18 +566,19 @@ def test_mlp_one_launch_step_matches_two_kernel_step(B, F, indexed):
         assert eng.red[:MLP_RED_COPY_FLOATS].abs().max().item() == 0.0, name
     assert eng._recompute_ok(B)
     la, pa, ga, za = out["pair"]
-    for name in ("step", "step_frag", "step_frag64", "step_mask"):
+    for name in ("step", "step_frag", "step_frag64"):
         lb, pb, gb, zb = out[name]
-        torch.testing.assert_close(pa, pb, rtol=1e-5, atol=1e-6)
-        assert abs(la - lb) <= 1e-5 * abs(la) + 1e-7, name
-        assert torch.isfinite(gb).all(), name
-        # dZ2 (dW2's operand) is bit-identical: same H2 rounding, same dy, same bf16 product
-        if zb is not None:
+        _mlp_step_close(la, pa, ga, lb, pb, gb, name, flips=name == "step_frag")
+        if name != "step_frag":
+            # dZ2 (dW2's operand) is bit-identical: same H2 rounding, same dy, same bf16 product
             assert torch.equal(za, zb), name
-        assert ((ga - gb).norm() / ga.norm()).item() < 1e-5, name
-    # dZ2 rebuilt from the bits in the dW2 kernel: the same MFMAs in the same order as the
-    # fragment-layout kernel, so dW2 (every gradient) is bit-identical to the 128-row FRAG step
-    from wellflow.models.mlp import MlpLayout
-
-    gf, gm = MlpLayout(F, (256, 256)).views(out["step_frag"][2]), MlpLayout(F, (256, 256)).views(out["step_mask"][2])
-    assert torch.equal(gf[0][1][0], gm[0][1][0])  # dW2
+        else:
+            # the 128-row kernel folds b1 / b2 into the MFMA accumulator (fp32 sum order): the
+            # rows whose H1 / H2 round differently get a slightly different prediction, hence dy
+            # (dZ2 = bf16(dy w3)); an H2 within fp32 noise of 0 may flip its ReLU mask
+            a, b = za.float(), zb.float()
+            print(f"{name}: dZ2 differs in {(a != b).float().mean().item():.4%}, rel-norm "
+                  f"{((a - b).norm() / a.norm()).item():.2e}, mask flips {((a == 0) != (b == 0)).sum().item()}")
+            assert (a != b).float().mean().item() < 0.01, name
+            assert ((a - b).norm() / a.norm()).item() < 1e-3, name
+            assert ((a == 0) != (b == 0)).float().mean().item() < 1e-5, name
