@@ -487,19 +487,21 @@ __device__ __forceinline__ f32x2_t bf_lo_hi(unsigned q) {  // packed bf16 pair -
   return f32x2_t{__uint_as_float(q << 16), __uint_as_float(q & 0xFFFF0000u)};
 }
 
-template <int NFT>
+// STAMP (WELLFLOW_MLP_STAMP=1 in a WF_DIAG build, tools/mlp_timeline.py --k128): lane 0 of every
+// wave writes s_memtime at 13 phase boundaries of its 3rd pass into `stamps` (results unchanged)
+template <int NFT, bool STAMP = false>
 __global__ __launch_bounds__(512, 1) void mlp2_step128_kernel(
     const bf16_t* __restrict__ X, int Fp, const bf16_t* __restrict__ W1, const float* __restrict__ b1,
     const bf16_t* __restrict__ W2, const bf16_t* __restrict__ W2T, const float* __restrict__ b2,
     const float* __restrict__ w3, const float* __restrict__ b3, const float* __restrict__ y, float dy_scale, int B,
     const long long* __restrict__ rows, long nrows, bf16_t* __restrict__ dZ2, float* __restrict__ pred,
-    float* __restrict__ red, int prio) {
+    float* __restrict__ red, int prio, unsigned long long* __restrict__ stamps = nullptr) {
   constexpr int MT = 2, NR = 8, NW = 8, R = 128, XB = R * 64, WD = 4;
   static_assert(16 % WD == 0, "stream slots must repeat every pass");
   __shared__ __attribute__((aligned(16))) char xs[2 * XB];          // X tiles (double-buffered)
   __shared__ __attribute__((aligned(16))) char h1s[R * MF_H * 2];   // H1 -> dZ1 (own columns)
   __shared__ __attribute__((aligned(16))) char zs[R * MF_H * 2];    // dZ2
-  __shared__ __attribute__((aligned(16))) float hred[R][NW];        // head partials
+  __shared__ __attribute__((aligned(16))) float hred[R][NW + 4];    // head partials (48-B rows: conflict-free float4 reads)
   __shared__ __attribute__((aligned(16))) float cst[3][MF_H];       // b1, b2, w3
   __shared__ float ys[2][R];
   __shared__ float lred[NW];
@@ -559,34 +561,30 @@ __global__ __launch_bounds__(512, 1) void mlp2_step128_kernel(
   const float bias3 = b3[0];
   float lsum = 0.f, db3a = 0.f;
 
-  // next pass's inputs: thread t one 16-B X segment (row t >> 2, chunk t & 3); threads < 128 a target.
-  // Row-indexed batches (rows != nullptr, nrows < 2^31): a pass's dataset row ids are loaded one
-  // pass before its gathers — loaded right before them, the dependent wait after B4 also drained
-  // every W2^T stream fragment in flight
+  // next pass's inputs: thread t one 16-B X segment (row t >> 2, chunk t & 3), threads 4r the
+  // target of row r. Row-indexed batches (rows != nullptr, nrows < 2^31): a pass's dataset row
+  // ids are loaded one pass before its gathers — loaded right before them, the dependent wait
+  // after B4 also drained every W2^T stream fragment in flight
   uint4 xv = make_uint4(0, 0, 0, 0);
   float yv = 0.f;
-  int ixn = 0, iyn = 0;  // clamped row ids of the pass the next prefetch() gathers
+  int ixn = 0;  // clamped row id (row t >> 2) of the pass the next prefetch() gathers
   auto fetch_ids = [&](int ps, int tid) {
     if (rows != nullptr) {
-      auto clampr = [&](long long r) { return (int)(r < 0 ? 0 : (r >= nrows ? nrows - 1 : r)); };
-      const int gr = ps * R + (tid >> 2), gy = ps * R + tid;
-      ixn = gr < B ? clampr(rows[gr]) : 0;
-      if (tid < R) iyn = gy < B ? clampr(rows[gy]) : 0;
+      const int gr = ps * R + (tid >> 2);
+      const long long r = gr < B ? rows[gr] : 0;
+      ixn = (int)(r < 0 ? 0 : (r >= nrows ? nrows - 1 : r));
     }
   };
   auto prefetch = [&](int ps, int tid) {
     const int r = tid >> 2, c = tid & 3, gr = ps * R + r;
     const size_t xr = rows != nullptr ? (size_t)ixn : (size_t)gr;
     xv = (gr < B && 8 * c + 8 <= Fp) ? *reinterpret_cast<const uint4*>(X + xr * Fp + 8 * c) : make_uint4(0, 0, 0, 0);
-    if (tid < R) {
-      const int gy = ps * R + tid;
-      yv = gy < B ? y[rows != nullptr ? (size_t)iyn : (size_t)gy] : 0.f;
-    }
+    if (c == 0) yv = gr < B ? y[xr] : 0.f;
   };
   const int npass = (B + R - 1) / R;
   auto stage = [&](int p, int tid) {
     *reinterpret_cast<uint4*>(xs + p * XB + x4_off(tid >> 2, tid & 3)) = xv;
-    if (tid < R) ys[p][tid] = yv;
+    if ((tid & 3) == 0) ys[p][tid >> 2] = yv;
   };
   const int G = gridDim.x;
   if ((int)blockIdx.x < npass) {
@@ -605,6 +603,13 @@ __global__ __launch_bounds__(512, 1) void mlp2_step128_kernel(
   int par = 0;
   for (int ps = blockIdx.x; ps < npass; ps += G, par ^= 1) {
     const int row0 = ps * R;
+    auto stamp = [&](int k) {
+      if constexpr (STAMP) {
+        if (ps == (int)blockIdx.x + 2 * G && lane == 0)
+          stamps[((size_t)blockIdx.x * NW + wid) * 16 + k] = __builtin_amdgcn_s_memtime();
+      }
+    };
+    stamp(0);
     char* xt = xs + par * XB;
     // the lane coordinates, laundered per pass: every LDS address below derives from them, and
     // as loop invariants the compiler hoisted ~40 swizzled addresses out of the pass loop and
@@ -638,7 +643,9 @@ __global__ __launch_bounds__(512, 1) void mlp2_step128_kernel(
         const unsigned p1 = relu_pk(pk_bf16(acc[m][n][2], acc[m][n][3]));
         *reinterpret_cast<uint2*>(h1s + tile_off(16 * n + l15, u0 + 16 * m + 4 * g)) = make_uint2(p0, p1);
       }
+    stamp(1);
     __syncthreads();  // B2: H1 complete
+    stamp(2);
 
     // ---- layer 2 (own units, K = 256): stream steps 0..7; the B fragments (H1) rotate through
     // one set of NR registers, fragment n of K step kt + 1 read right after its two MFMAs of kt;
@@ -668,6 +675,7 @@ __global__ __launch_bounds__(512, 1) void mlp2_step128_kernel(
 #pragma unroll
       for (int m = 0; m < MT; ++m) wr[kt % WD][m] = wfrag(kt + WD, m);  // steps WD .. 7 + WD (W2^T from 8)
     });
+    stamp(3);
     // H2 = relu(Z2 + b2) rounded to bf16 (packed ReLU), kept in acc as floats; head partials of
     // rows 16n + l15 as packed fp32 FMAs over unit pairs
     f32x2_t hp2[NR];
@@ -693,30 +701,41 @@ __global__ __launch_bounds__(512, 1) void mlp2_step128_kernel(
       hp += __shfl_xor(hp, 32, 64);
       if (g == 0) hred[16 * n + l15][wid] = hp;
     }
+    stamp(4);
     __syncthreads();  // B3: head partials complete
+    stamp(5);
 
-    // ---- prediction, dy, loss of rows 16n + l15; wave 0 lane group g owns rows 16n + l15 for
-    // n = g and n = g + 4 (their loss, db3 and prediction store)
-    float dyn[NR], pst[2] = {0.f, 0.f};
-    int pgr[2] = {-1, -1};
+    // ---- prediction, dy of rows 16n + l15 (every wave needs dy), branch-free; wave 0 lane group
+    // g owns rows 16n + l15 for n = g and g + 4 (their loss, db3 and prediction store): selected
+    // on the way, accounted after the loop (per-row branches here cost ~1.8k cycles per pass)
+    float dyn[NR], pq[2] = {0.f, 0.f}, dq[2] = {0.f, 0.f};
 #pragma unroll
     for (int n = 0; n < NR; ++n) {
-      const int r = 16 * n + l15, gr = row0 + r;
+      const int r = 16 * n + l15;
       const float4 pa = *reinterpret_cast<const float4*>(&hred[r][0]);
       const float4 pb = *reinterpret_cast<const float4*>(&hred[r][4]);
       const float p = ((pa.x + pa.y) + (pa.z + pa.w)) + ((pb.x + pb.y) + (pb.z + pb.w)) + bias3;
-      dyn[n] = 0.f;
-      if (gr < B) {
-        const float diff = p - ys[par][r];
-        dyn[n] = dy_scale * diff;
-        if (wid == 0 && (n & 3) == g) {
-          pst[n >> 2] = p;
-          pgr[n >> 2] = gr;
-          lsum += diff * diff;
-          db3a += dyn[n];
-        }
+      const float diff = p - ys[par][r];
+      dyn[n] = row0 + r < B ? dy_scale * diff : 0.f;
+      const bool own = (n & 3) == g;
+      pq[n >> 2] = own ? p : pq[n >> 2];
+      dq[n >> 2] = own ? diff : dq[n >> 2];
+      if (n & 1) __builtin_amdgcn_sched_barrier(0);  // <= 4 head float4 reads in flight (VGPRs)
+    }
+    float pst[2] = {0.f, 0.f};
+    int pgr[2] = {-1, -1};
+    if (wid == 0) {
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        const int gr = row0 + 16 * (g + 4 * q) + l15;
+        const bool ok = gr < B;
+        pst[q] = pq[q];
+        pgr[q] = ok ? gr : -1;
+        lsum += ok ? dq[q] * dq[q] : 0.f;
+        db3a += ok ? dy_scale * dq[q] : 0.f;
       }
     }
+    stamp(6);
     // ---- dZ2 = bf16(dy w3) where H2 > 0 (own units) -> zs; dw3 partials. The product is rounded
     // first and masked on the packed pair (the same bits as rounding the masked product)
 #pragma unroll
@@ -741,36 +760,15 @@ __global__ __launch_bounds__(512, 1) void mlp2_step128_kernel(
     for (int m = 0; m < MT; ++m) asm volatile("" : "+v"(s3[m][0]), "+v"(s3[m][1]));
     asm volatile("" : "+v"(lsum), "+v"(db3a));
     if (ps + G < npass) stage(par ^ 1, tdv);
+    stamp(7);
     __syncthreads();  // B4: dZ2 complete, next pass's X / y staged
     if (ps + 2 * G < npass) {
       prefetch(ps + 2 * G, tdv);
       if (ps + 3 * G < npass) fetch_ids(ps + 3 * G, tdv);
     }
+    stamp(8);
 
-    // ---- dZ2 copy-out as dW2 A fragments (fragment (S, b) = 32 rows x 16 units): wave w writes
-    // the pass's 4 row groups of its own unit blocks 2w, 2w + 1, and sums each fragment's rows
-    // into db2 on the way (one MFMA against the ones operand)
-    // (rows past B hold zeros in zs: read and summed unconditionally, only the store is skipped).
-    // Here, before dH1, the H2 / dH1 accumulators are dead: room for the 8 fragments in flight
-    bf16x8 onesv = ones;
-    asm volatile("" : "+v"(onesv));  // one 4-VGPR copy per phase (left alone the splat was rebuilt per MFMA)
-#pragma unroll
-    for (int q = 0; q < 8; ++q) {
-      const int mq = q & 1, sst = q >> 1, b = 2 * wid + mq;
-      bf16x8 v;
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        const bf16x4 t = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-            (lds_bf16x4*)(zs + tile_off(32 * sst + 8 * g + 4 * h + tq, 16 * b + 4 * tp)));
-#pragma unroll
-        for (int e = 0; e < 4; ++e) v[4 * h + e] = t[e];
-      }
-      db2a[mq] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(v, onesv, db2a[mq], 0, 0, 0);
-      if (row0 + 32 * sst < B) {
-        const size_t S = (size_t)(row0 >> 5) + sst;
-        *reinterpret_cast<bf16x8*>(dZ2 + ((S * 16 + b) * 64 + lnv) * 8) = v;
-      }
-    }
+    stamp(9);
     // ---- dH1^T (own units k, K = 256 output units) = W2^T dZ2^T: stream steps 8..15
 #pragma unroll
     for (int n = 0; n < NR; ++n) hb[n] = *reinterpret_cast<const bf16x8*>(zs + tile_off(16 * n + l15, 8 * g));
@@ -798,6 +796,7 @@ __global__ __launch_bounds__(512, 1) void mlp2_step128_kernel(
 #pragma unroll
     for (int q = 0; q < 2; ++q)
       if (pgr[q] >= 0 && pred != nullptr) pred[pgr[q]] = pst[q];
+    stamp(10);
     // ---- dZ1 = bf16(dH1) where H1 > 0, over the same 8 bytes of h1s (rows past B: dZ2 = 0 there,
     // so dH1 and dZ1 are zero without a row test)
 #pragma unroll
@@ -813,11 +812,35 @@ __global__ __launch_bounds__(512, 1) void mlp2_step128_kernel(
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_wave_barrier();
-    // ---- dW1^T slice (32 units x Fp) += dZ1^T X over the pass's 128 rows; db1 += dZ1^T 1
-    onesv = ones;
-    asm volatile("" : "+v"(onesv));
+    stamp(11);
+    // ---- dW1^T slice (32 units x Fp) += dZ1^T X over the pass's 128 rows; db1 += dZ1^T 1. The
+    // dZ2 copy-out as dW2 A fragments rides along (fragment (S, b) = 32 rows x 16 units; wave w
+    // writes the pass's 4 row groups of its own unit blocks 2w, 2w + 1, two per K step, and sums
+    // each fragment's rows into db2 with one MFMA against the ones operand): here the dH1
+    // accumulators are dead, the next pass's W2 requests are out (vmcnt counts stores, in order),
+    // and the stores overlap MFMAs — as a phase of its own after B4 it cost 2.4k cycles per pass
+    // (tools/mlp_timeline.py). Rows past B hold zeros in zs (summed, store skipped)
+    bf16x8 onesv = ones;
+    asm volatile("" : "+v"(onesv));  // one 4-VGPR copy (left alone the splat was rebuilt per MFMA)
 #pragma unroll
     for (int kk = 0; kk < R / 32; ++kk) {
+#pragma unroll
+      for (int qq = 0; qq < 2; ++qq) {  // copy-out fragments 2kk, 2kk + 1: unit block 2w + qq, rows 32kk..
+        const int b = 2 * wid + qq;
+        bf16x8 v;
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const bf16x4 t = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+              (lds_bf16x4*)(zs + tile_off(32 * kk + 8 * g + 4 * h + tq, 16 * b + 4 * tp)));
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[4 * h + e] = t[e];
+        }
+        db2a[qq] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(v, onesv, db2a[qq], 0, 0, 0);
+        if (row0 + 32 * kk < B) {
+          const size_t S = (size_t)(row0 >> 5) + kk;
+          *reinterpret_cast<bf16x8*>(dZ2 + ((S * 16 + b) * 64 + lnv) * 8) = v;
+        }
+      }
       bf16x8 af[MT], bfr[NFT];
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
@@ -847,6 +870,7 @@ __global__ __launch_bounds__(512, 1) void mlp2_step128_kernel(
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_wave_barrier();
+    stamp(12);
   }
 
   // ---- batch sums -> copy blockIdx % kMlpRedCopies of the scratch; dW1 -> this workgroup's row.
@@ -1065,8 +1089,14 @@ bool launch_mlp2_step(const bf16_t* X, int Fp, const bf16_t* W1, const float* b1
   // static s_setprio 1 for waves 4-7 (+0.2 to +1.1 % in three interleaved pairs, chunk span
   // 17.5k -> 17.1k cycles, profiles/r4/mlp_prio; the WELLFLOW_STEP_PRIO A/B knob was removed)
   constexpr int prio = 1;
-  if (W2T != nullptr && dz_frag && !stamp) {  // 128-row passes, both weight images streamed
+  if (W2T != nullptr && dz_frag) {  // 128-row passes, both weight images streamed
     if (rows != nullptr && nrows > 0x7FFFFFFFL) return false;  // 32-bit row ids in the kernel
+    if (stamp && Fp <= 16) {
+      hipLaunchKernelGGL((mlp2_step128_kernel<1, true>), dim3(grid), dim3(512), 0, s, X, Fp, W1, b1, W2, W2T, b2, w3, b3,
+                         y, dy_scale, B, rows, nrows, dZ2, pred, red, prio,
+                         reinterpret_cast<unsigned long long*>(red + kMlpRedSlab2Off + 200L * 65536));
+      return true;
+    }
     if (Fp <= 16)
       hipLaunchKernelGGL(mlp2_step128_kernel<1>, dim3(grid), dim3(512), 0, s, X, Fp, W1, b1, W2, W2T, b2, w3, b3, y,
                          dy_scale, B, rows, nrows, dZ2, pred, red, prio);

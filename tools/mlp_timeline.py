@@ -1,8 +1,9 @@
 #!/usr/bin/env python3
-"""Per-phase timeline of the one-launch MLP training step (csrc/mlp_step.hip mlp2_step_kernel):
-lane 0 of every wave stamps s_memtime (shader cycles) at 13 phase boundaries of its 5th
-64-row chunk when WELLFLOW_MLP_STAMP=1 (the stamped variant is built into the production
-library: it changes no result, it only writes timestamps into an unused scratch region).
+"""Per-phase timeline of the one-launch MLP training step (csrc/mlp_step.hip): lane 0 of every
+wave stamps s_memtime (shader cycles) at 13 phase boundaries of one pass when
+WELLFLOW_MLP_STAMP=1 in a WF_DIAG build (WELLFLOW_DIAG_BUILD=1; the stamps change no result,
+they only go to an unused scratch region) — the 128-row kernel (mlp2_step128_kernel, the
+default; its 3rd pass) or, with WELLFLOW_MLP_STEP128=0, the 64-row one (its 5th chunk).
 
     WELLFLOW_MLP_STAMP=1 python tools/mlp_timeline.py [--batch 262144]
 
@@ -14,6 +15,9 @@ import sys
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
+PHASES128 = ["layer 1 + H1 store", "B2 wait", "layer 2 MFMA", "H2 epilogue + head partials",
+             "B3 wait", "prediction + dy", "dZ2 + stage next X", "B4 wait + X prefetch", "dZ2 copy-out + db2",
+             "dH1 MFMA", "dZ1", "dW1 + db1"]  # 12 intervals of 13 stamps
 PHASES = ["chunk top", "layer 1 + H1 store", "B2 wait", "layer 2 MFMA", "H2 epilogue + head partials",
           "B3 wait", "dy + dZ2 + stage next X", "B4 wait", "X prefetch", "dH1 MFMA",
           "W2 issue + stores + dZ1 + sums", "dW1"]
@@ -47,7 +51,8 @@ def main():
     t = t[valid]
     d = t[:, 1:] - t[:, :-1]
     print(f"waves stamped: {int(valid.sum())}; chunk span mean {float((t[:, -1] - t[:, 0]).mean()):.0f} cycles")
-    for i, name in enumerate(PHASES):
+    phases = PHASES128 if eng.w2t is not None else PHASES
+    for i, name in enumerate(phases):
         print(f"{i:2d} {name:30s} mean {float(d[:, i].mean()):8.0f}  max {float(d[:, i].max()):8.0f}")
 
 
