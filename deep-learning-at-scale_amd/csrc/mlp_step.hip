@@ -696,9 +696,13 @@ __global__ __launch_bounds__(512, 1) void mlp2_step128_kernel(
     }
 #pragma unroll
     for (int n = 0; n < NR; ++n) {
+      // sum over the 4 lane groups with two VALU lane swaps (v_permlane32/16_swap; the shuffles
+      // went through the LDS pipe): lanes 0-15 end with the row's partial over all 32 units
       float hp = hp2[n].x + hp2[n].y;
-      hp += __shfl_xor(hp, 16, 64);
-      hp += __shfl_xor(hp, 32, 64);
+      const unsigned hu = __float_as_uint(hp);
+      hp += __uint_as_float(__builtin_amdgcn_permlane32_swap(hu, hu, false, false)[1]);  // + lane l + 32
+      const unsigned tu = __float_as_uint(hp);
+      hp += __uint_as_float(__builtin_amdgcn_permlane16_swap(tu, tu, false, false)[1]);  // + lane l + 16
       if (g == 0) hred[16 * n + l15][wid] = hp;
     }
     stamp(4);
@@ -1030,12 +1034,14 @@ __global__ __launch_bounds__(512, 1) void mlp2_dw2g_kernel(const bf16_t* __restr
       const bf16x8(&xf)[2] = xfa[s2];
 #pragma unroll
       for (int nb = 0; nb < 2; ++nb) {
-        const f32x4 c0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xf[0], w1f[nb], f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
-        const f32x4 c1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xf[1], w1f[nb], f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
-        const unsigned p0 = pk_bf16(fmaxf(c0[0] + bias[nb], 0.f), fmaxf(c0[1] + bias[nb], 0.f));
-        const unsigned p1 = pk_bf16(fmaxf(c0[2] + bias[nb], 0.f), fmaxf(c0[3] + bias[nb], 0.f));
-        const unsigned p2 = pk_bf16(fmaxf(c1[0] + bias[nb], 0.f), fmaxf(c1[1] + bias[nb], 0.f));
-        const unsigned p3 = pk_bf16(fmaxf(c1[2] + bias[nb], 0.f), fmaxf(c1[3] + bias[nb], 0.f));
+        // b1 as the C operand and the ReLU on the packed pair: the step kernel's H1, bit for bit
+        const f32x4 bc{bias[nb], bias[nb], bias[nb], bias[nb]};
+        const f32x4 c0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xf[0], w1f[nb], bc, 0, 0, 0);
+        const f32x4 c1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xf[1], w1f[nb], bc, 0, 0, 0);
+        const unsigned p0 = relu_pk(pk_bf16(c0[0], c0[1]));
+        const unsigned p1 = relu_pk(pk_bf16(c0[2], c0[3]));
+        const unsigned p2 = relu_pk(pk_bf16(c1[0], c1[1]));
+        const unsigned p3 = relu_pk(pk_bf16(c1[2], c1[3]));
         typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
         hb[nb] = __builtin_bit_cast(bf16x8, (u32x4_t{p0, p1, p2, p3}));
       }
