@@ -85,12 +85,14 @@ def _spawn_ranks(n: int, argv) -> int:
     return subprocess.run(cmd, env=env, cwd=ROOT).returncode
 
 
-def _timed(ctx, step, steps, warmup, min_s: float = 0.0):
+def _timed(ctx, step, steps, warmup, min_s: float = 0.0, many=None, graph_steps: int = 1):
     """W untimed warmup steps, then EXACTLY `steps` timed steps bracketed by barrier +
     synchronize on both sides; the max over ranks. With min_s > 0 (the secondary configs) a
     short untimed probe first raises `steps` until the timed window is >= min_s on the slowest
     rank, so one hiccup of tens of microseconds is not a percent of the number (round-3 VERDICT
-    weak #5). Returns (seconds, timed steps, total steps run)."""
+    weak #5). ``many(n)`` (StepRunner.run_many): the timed steps run as replays of one
+    ``graph_steps``-step graph (every step complete, the remainder as single steps).
+    Returns (seconds, timed steps, total steps run)."""
     import math
 
     import torch
@@ -116,10 +118,16 @@ def _timed(ctx, step, steps, warmup, min_s: float = 0.0):
         # 1.5x margin: the probe's per-step estimate carries its own sync overhead and the
         # streamed config varies step to step (round 4: 1.1x left 0.079-0.098 s windows)
         steps = max(steps, int(math.ceil(min_s * 1.5 / max(per, 1e-9))))
+    n = graph_steps if many is not None and graph_steps > 1 else 1
+    if n > 1:
+        many(n)  # capture (untimed): one n-step replay of warmup
+        total += n
     ctx.barrier()
     sync()
     t0 = time.perf_counter()
-    for _ in range(steps):
+    for _ in range(steps // n):
+        many(n) if n > 1 else step()
+    for _ in range(steps % n):
         step()
     sync()
     ctx.barrier()
@@ -208,7 +216,7 @@ def bench_lstm(args, ctx):
     x, y = x.to(ctx.device), y.to(ctx.device)
     run = StepRunner(eng, opt, ctx, 1.0 / (B * ctx.world_size), lambda k: (x, y),
                      graph=not (args.no_graph or eng.dw_chunk > 0), comm_in_graph=not args.eager_comm)
-    el, k, n = _timed(ctx, run.run, args.steps, args.warmup, args.min_timed_s)
+    el, k, n = _timed(ctx, run.run, args.steps, args.warmup, args.min_timed_s, run.run_many, args.graph_steps)
     eng.check_device_errors()  # a timed-out persistent hand-off anywhere in the run fails the bench
     extra = {"persistent_fwd": eng.last_forward_persistent, "persistent_bwd": eng.last_backward_persistent}
     # the engine adds each step's loss straight into the runner's accumulator: mean over the run
@@ -280,7 +288,7 @@ def bench_cnn(args, ctx):
     y = series[:, lay.input_len :].contiguous().to(ctx.device)
     run = StepRunner(eng, opt, ctx, 1.0 / (B * ctx.world_size * lay.outputs), lambda k: (x, y),
                      graph=not args.no_graph, comm_in_graph=not args.eager_comm)
-    el, k, n = _timed(ctx, run.run, args.steps, args.warmup, args.min_timed_s)
+    el, k, n = _timed(ctx, run.run, args.steps, args.warmup, args.min_timed_s, run.run_many, args.graph_steps)
     return el, k, B, model, run.take_loss() / (B * lay.outputs * n), run, eng, {}
 
 
@@ -334,7 +342,9 @@ def bench_mlp(args, ctx, online: bool):
         x, y = x.to(ctx.device, eng.input_dtype), y.to(ctx.device)
         run = StepRunner(eng, opt, ctx, gscale, lambda k: (x, y), graph=graph, comm_in_graph=not args.eager_comm)
         step = run.run
-    el, k, n = _timed(ctx, step, args.steps, args.warmup, args.min_timed_s)
+    # the streamed config changes its input slot every step: single-step replays
+    el, k, n = _timed(ctx, step, args.steps, args.warmup, args.min_timed_s,
+                      None if online else run.run_many, args.graph_steps)
     if online:
         extra.update(streamer.copy_stats(skip=args.warmup))
         extra["h2d_mb_per_step"] = round((streamer.slots[0][0].numel() * streamer.slots[0][0].element_size()
@@ -379,6 +389,8 @@ def _secondary(args, ctx, models) -> dict:
                   "unit": "rows/s", "ms_per_step": round(1000.0 * el / max(k, 1), 4), "steps": k,
                   "warmup": a.warmup, "timed_s": round(el, 4), "per_gpu_batch": B, "global_batch": B * W,
                   "model": desc, "train_loss": round(loss, 6), "step_graph": bool(run.graphs),
+                  "graph_steps": max((key[2] for key in run.graphs if isinstance(key, tuple) and key[0] == "many"),
+                                     default=1),
                   **{k: v for k, v in extra.items() if k.startswith("h2d") or k in ("persistent_fwd",)}}
         del run, eng
     return out
@@ -399,6 +411,8 @@ def main() -> int:
     ap.add_argument("--fwd-variant", type=int, default=None)
     ap.add_argument("--bwd-variant", type=int, default=None)
     ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--graph-steps", type=int, default=8,
+                    help="timed steps per captured graph replay (StepRunner.run_many; 1 = one replay per step)")
     ap.add_argument("--eager-comm", action="store_true", help="all-reduce between two graphs, not captured")
     ap.add_argument("--comm-dtype", choices=["fp32", "bf16"], default="fp32",
                     help="C2 gradient all-reduce precision (parallel/dist.py; default fp32)")
@@ -470,6 +484,7 @@ def main() -> int:
     comm = _comm_ms(ctx, eng.grads)
     grad_mb = round(eng.grads.numel() * 4 / 2**20, 3)
     step_graph, comm_in_graph = bool(run.graphs), bool(run.captured_comm)
+    graph_steps = max((key[2] for key in run.graphs if isinstance(key, tuple) and key[0] == "many"), default=1)
     del run, eng
     sec = _secondary(args, ctx, secondary) if secondary else None
     par = None
@@ -531,6 +546,7 @@ def main() -> int:
             "grad_bucket_mb": grad_mb,
             "comm_dtype": args.comm_dtype,
             "step_graph": step_graph,
+            "graph_steps": graph_steps,
             "comm_in_graph": comm_in_graph,
             "train_loss": round(loss, 6),  # mean over the run
             "timed_s": round(elapsed, 4),

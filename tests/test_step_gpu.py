@@ -176,3 +176,81 @@ def test_cnn_dropout_mask_differs_per_replay():
             L = per_element_loss("mae_clip", ref.dense(h.reshape(B, -1)), y).sum().item()
             assert abs(ls - L) <= 1e-2 * L, (k, ls, L)
     assert len({round(v, 3) for v in losses}) == 5, losses  # a repeated mask would repeat the loss
+
+
+def _cnn(B=4096, seed=0):
+    from wellflow.models.cnn import CNN1DRegressor, NativeCNN
+
+    ref = CNN1DRegressor(dropout=0.5).init_keras(seed).to(DEV)
+    eng = NativeCNN(ref.layout, batch=B, device=DEV, dropout=0.5, loss="mae_clip")
+    eng.params.copy_(ref.to_flat().to(DEV))
+    eng.sync_weights()
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    series = torch.randn(B, 60, generator=g).cumsum(1) * 0.1
+    return eng, series[:, :48].contiguous().to(DEV), series[:, 48:].contiguous().to(DEV)
+
+
+@pytest.mark.parametrize("model", ["lstm", "mlp", "cnn"])
+def test_run_many_equals_single_replays(model):
+    """StepRunner.run_many(n): n steps captured into ONE graph replay (what bench.py times with
+    --graph-steps) against n single-step replays: the same kernels in the same order — the
+    optimizer's device step counter and the CNN's dropout counter advance per step — so the
+    same parameters and loss up to the run-to-run atomics order of the batch sums."""
+    from wellflow.optim.flat import FlatAdam, FlatSGD
+    from wellflow.parallel.dist import DistContext
+    from wellflow.train.step import StepRunner
+
+    make = {"lstm": _lstm, "mlp": _mlp, "cnn": _cnn}[model]
+    out = {}
+    for tag in ("single", "single2", "many"):
+        eng, x, y = make()
+        if model == "cnn":
+            opt = FlatSGD(eng.params, eng.grads, zero_grads=True, writeback=eng)
+        elif model == "lstm":
+            opt = FlatAdam(eng.params, eng.grads, lr=1e-3, zero_grads=True, writeback=eng)
+        else:
+            opt = FlatAdam(eng.params, eng.grads, lr=1e-3, shadow=eng.shadow, zero_grads=True, shadow_t=eng.shadow_t)
+        run = StepRunner(eng, opt, DistContext(device=torch.device(DEV)), 1.0 / len(y), lambda k: (x, y), graph=True)
+        for _ in range(3):
+            run.run()
+        if tag == "many":
+            run.run_many(4)
+            run.run_many(4)
+            assert ("many", 0, 4) in run.graphs
+        else:
+            for _ in range(8):
+                run.run()
+        torch.cuda.synchronize()
+        out[tag] = (eng.params.clone(), run.take_loss(), opt.steps_taken,
+                    int(eng.rng.item()) if model == "cnn" else None)
+        del run, opt, eng
+    (pa, la, sa, ra), (pb, lb, _, _), (pm, lm, sm, rm) = out["single"], out["single2"], out["many"]
+    assert sa == sm == 11 and ra == rm
+    # the batch sums' fp32 atomics make two single-replay runs differ a little already (Adam
+    # magnifies that on near-zero gradients): the n-step replay must not differ more than that
+    noise = (pa - pb).norm().item()
+    assert (pm - pa).norm().item() <= 3.0 * noise + 1e-6 * pa.norm().item(), (noise, (pm - pa).norm().item())
+    assert abs(lm - la) <= 3.0 * abs(lb - la) + 1e-5 * abs(la)
+
+
+def test_trainer_graph_steps_equal_single_steps(monkeypatch, tmp_path):
+    """The resident-data training loop (Trainer.train_steps) in groups
+    of WELLFLOW_GRAPH_STEPS steps per replay, rows from a static order buffer, against one
+    replay per step: the same loss history and test loss."""
+    from wellflow.train.job import run_job
+
+    names = "well,field,t,whp,choke,glr,temp,water_cut,dsp,flow"
+    types = "string,string,int,float,float,float,float,float,float,float"
+    res = {}
+    for gs in ("1", "4"):
+        monkeypatch.setenv("WELLFLOW_GRAPH_STEPS", gs)
+        args = [names, types, "flow", str(tmp_path / gs) + "/", "--epochs", "2", "--synth-wells", "6",
+                "--synth-steps", "20000", "--batch-size", "4096", "--device", "cuda", "--verbose", "0",
+                "--patience", "100"]
+        out = run_job("mlp", args, log=lambda *a, **k: None)
+        res[gs] = out
+    a, b = res["1"], res["4"]
+    assert a["steps"] == b["steps"] and a["steps"] >= 16, (a["steps"], b["steps"])
+    for x, y in zip(a["history"]["loss"], b["history"]["loss"]):
+        assert abs(x - y) <= 1e-5 * abs(x), (a["history"]["loss"], b["history"]["loss"])
+    assert abs(a["test_loss"] - b["test_loss"]) <= 1e-5 * abs(a["test_loss"])
