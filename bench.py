@@ -337,10 +337,18 @@ def bench_mlp(args, ctx, online: bool):
             streamer.next()
             run.run(streamer.last_slot)
     else:
-        x, y = synth_tabular_batch(B, F, seed=ctx.rank)
-        # resident in the engine's input format, as the job path keeps its datasets (Trainer)
+        nb = max(1, args.mlp_batches)
+        x, y = synth_tabular_batch(B * nb, F, seed=ctx.rank)
+        # resident in the engine's input format, as the job path keeps its datasets (Trainer);
+        # --mlp-batches N: N distinct resident batches, step i of a graph replay reads batch
+        # i % N (fresh rows every step, as a training pass over a table does)
         x, y = x.to(ctx.device, eng.input_dtype), y.to(ctx.device)
-        run = StepRunner(eng, opt, ctx, gscale, lambda k: (x, y), graph=graph, comm_in_graph=not args.eager_comm)
+
+        def inputs(k):
+            j = (k[1] if isinstance(k, tuple) else 0) % nb
+            return x[j * B : (j + 1) * B], y[j * B : (j + 1) * B]
+
+        run = StepRunner(eng, opt, ctx, gscale, inputs, graph=graph, comm_in_graph=not args.eager_comm)
         step = run.run
     # the streamed config changes its input slot every step: single-step replays
     el, k, n = _timed(ctx, step, args.steps, args.warmup, args.min_timed_s,
@@ -411,6 +419,8 @@ def main() -> int:
     ap.add_argument("--fwd-variant", type=int, default=None)
     ap.add_argument("--bwd-variant", type=int, default=None)
     ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--mlp-batches", type=int, default=1,
+                    help="mlp: distinct resident batches cycled through a graph replay's steps")
     ap.add_argument("--graph-steps", type=int, default=8,
                     help="timed steps per captured graph replay (StepRunner.run_many; 1 = one replay per step)")
     ap.add_argument("--eager-comm", action="store_true", help="all-reduce between two graphs, not captured")

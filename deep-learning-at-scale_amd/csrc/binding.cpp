@@ -813,6 +813,22 @@ void cast_bf16(const at::Tensor& src, const at::Tensor& dst) {
   wf::launch_cast_bf16(fp(src), bfp(dst), src.numel(), cur_stream());
 }
 
+// out[r] = src[idx[r]] (rows of any dtype, contiguous, row size a multiple of 4 B; ids clamped)
+void gather_rows(const at::Tensor& src, const at::Tensor& idx, const at::Tensor& out) {
+  TORCH_CHECK(src.is_cuda() && idx.is_cuda() && out.is_cuda(), "gather_rows: GPU tensors");
+  TORCH_CHECK(src.is_contiguous() && out.is_contiguous() && idx.is_contiguous(), "gather_rows: contiguous tensors");
+  TORCH_CHECK(idx.scalar_type() == at::kLong && idx.dim() == 1, "gather_rows: idx int64 [m]");
+  TORCH_CHECK(src.scalar_type() == out.scalar_type() && src.dim() >= 1 && out.dim() == src.dim(), "gather_rows: dtype / rank");
+  TORCH_CHECK(src.size(0) > 0 && out.size(0) == idx.size(0), "gather_rows: out rows == idx size");
+  const int64_t rb = src.numel() / src.size(0) * src.element_size();
+  TORCH_CHECK(rb > 0 && rb % 4 == 0 && out.numel() / std::max<int64_t>(out.size(0), 1) * out.element_size() == rb,
+              "gather_rows: row bytes must match and be a multiple of 4");
+  if (idx.size(0) == 0) return;
+  const c10::hip::OptionalHIPGuardMasqueradingAsCUDA guard(src.device());
+  wf::launch_gather_rows(src.data_ptr(), reinterpret_cast<const long long*>(idx.data_ptr<int64_t>()), out.data_ptr(), idx.size(0), (int)rb, src.size(0),
+                         cur_stream());
+}
+
 void transpose_cast_bf16(const at::Tensor& src, int64_t lds, int64_t rows, int64_t cols,
                          const at::Tensor& dst, int64_t ldd) {
   TORCH_CHECK(src.is_cuda() && src.scalar_type() == at::kFloat, "src: fp32 GPU tensor");
@@ -1056,6 +1072,7 @@ PYBIND11_MODULE(_C, m) {
   WF_DEF(sgd);
   WF_DEF(sgd_dev);
   WF_DEF(cast_bf16);
+  WF_DEF(gather_rows);
   WF_DEF(transpose_cast_bf16);
   WF_DEF(im2col1d);
   // host-only queries (no launch; callable without a GPU)

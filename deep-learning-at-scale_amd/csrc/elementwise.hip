@@ -642,6 +642,44 @@ void launch_cast_bf16(const float* src, bf16_t* dst, long n, hipStream_t s) {
   hipLaunchKernelGGL(cast_bf16_kernel, dim3((int)b), dim3(256), 0, s, src, dst, n);
 }
 
+// ---------------------------------------------------------------- row gather
+// dst[r] = src[clamp(idx[r])] for rows of row_bytes (a multiple of 4): the epoch's shuffle
+// materialised once (train/trainer.py Trainer._permuted). Each thread moves VEC bytes; with
+// 16-B pieces a 32-B feature row is 2 lanes and consecutive lanes cover consecutive dst rows,
+// so the writes coalesce and each gathered row is one 32-B sector read (torch's index_select
+// spent ~530 us on the 2.4M x 32-B MLP table, this moves it at the sector rate).
+template <int VEC>
+__global__ void gather_rows_kernel(const char* __restrict__ src, const long long* __restrict__ idx,
+                                   char* __restrict__ dst, long m, int row_bytes, long nsrc) {
+  typedef unsigned u32v __attribute__((ext_vector_type(VEC / 4)));
+  const int per = row_bytes / VEC;
+  const long total = m * per;
+  const long stride = (long)gridDim.x * blockDim.x;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += stride) {
+    const long r = i / per;
+    const int c = (int)(i - r * per);
+    long long sr = idx[r];
+    sr = sr < 0 ? 0 : (sr >= nsrc ? nsrc - 1 : sr);
+    *reinterpret_cast<u32v*>(dst + r * row_bytes + (long)c * VEC) =
+        *reinterpret_cast<const u32v*>(src + sr * row_bytes + (long)c * VEC);
+  }
+}
+
+void launch_gather_rows(const void* src, const long long* idx, void* dst, long m, int row_bytes, long nsrc,
+                        hipStream_t s) {
+  const int vec = (row_bytes % 16 == 0 && ((uintptr_t)src | (uintptr_t)dst) % 16 == 0) ? 16 : 4;
+  const long total = m * (row_bytes / vec);
+  long b = (total + 255) / 256;
+  if (b > 8192) b = 8192;
+  if (b < 1) b = 1;
+  if (vec == 16)
+    hipLaunchKernelGGL(gather_rows_kernel<16>, dim3((int)b), dim3(256), 0, s, (const char*)src, idx, (char*)dst, m,
+                       row_bytes, nsrc);
+  else
+    hipLaunchKernelGGL(gather_rows_kernel<4>, dim3((int)b), dim3(256), 0, s, (const char*)src, idx, (char*)dst, m,
+                       row_bytes, nsrc);
+}
+
 // dst[c][r] = bf16(src[r*lds + c]) for r < rows, c < cols; 32x32 tiles through LDS.
 __global__ void transpose_cast_kernel(const float* __restrict__ src, long lds, int rows, int cols,
                                       bf16_t* __restrict__ dst, long ldd) {

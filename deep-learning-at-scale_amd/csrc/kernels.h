@@ -205,6 +205,9 @@ void launch_sgd(float* p, const float* g, float* vel, long n, float lr, float mo
 void launch_sgd_dev(float* p, float* g, float* vel, long n, float* step, float lr, float decay, float momentum,
                     int nesterov, float gscale, int zero_g, hipStream_t s);
 void launch_cast_bf16(const float* src, bf16_t* dst, long n, hipStream_t s);
+// dst[r] = src[clamp(idx[r], 0, nsrc - 1)], rows of row_bytes (multiple of 4) bytes
+void launch_gather_rows(const void* src, const long long* idx, void* dst, long m, int row_bytes, long nsrc,
+                        hipStream_t s);
 void launch_transpose_cast_bf16(const float* src, long lds, int rows, int cols, bf16_t* dst,
                                 long ldd, hipStream_t s);
 void launch_im2col1d(const float* x, int B, int L, int Cin, int ksz, int Lout, int Kp,

@@ -30,12 +30,23 @@ from .trainer import Trainer
 
 
 def _optimizer(cfg: RunConfig, eng):
+    """The optimizer with the same launch fusions bench.py times: on a native engine the update
+    also clears the gradient bucket (zero_grads), and it refreshes the engine's compute copies in
+    the same launch — NativeLSTM / NativeCNN through their fused writebacks, NativeMLP through
+    its bf16 shadow and the transposed W2 block — so no zero-fill or sync_weights launches run
+    per step (without them the MLP job's step ran ~17 % slower on the device than the bench's)."""
+    native = bool(getattr(eng, "native", False))
     if cfg.optimizer == "sgd":
         return make_optimizer("sgd", eng.params, eng.grads, lr=cfg.lr, momentum=cfg.momentum,
-                              decay=cfg.decay, nesterov=cfg.nesterov,
+                              decay=cfg.decay, nesterov=cfg.nesterov, zero_grads=native,
                               writeback=eng if hasattr(eng, "fused_sgd") else None)
+    kw = {}
+    if hasattr(eng, "fused_adam"):
+        kw["writeback"] = eng
+    elif native and getattr(eng, "shadow", None) is not None and hasattr(eng, "shadow_t"):
+        kw.update(shadow=eng.shadow, shadow_t=eng.shadow_t)  # NativeMLP
     return make_optimizer("adam", eng.params, eng.grads, lr=cfg.lr, weight_decay=cfg.weight_decay,
-                          writeback=eng if hasattr(eng, "fused_adam") else None)
+                          zero_grads=native, **kw)
 
 
 def _save_best(cfg, name, ref, prepared):
@@ -115,9 +126,12 @@ def run_config(cfg: RunConfig, log=print) -> dict:
     if cfg.batch_size <= 0:
         cfg.batch_size = auto_batch(cfg.model, cfg, dev, n_rank)
         say(f"Batch size (auto): {cfg.batch_size} rows per GPU")
-    if cfg.model == "mlp_online" and cfg.online_chunk <= 0:  # auto: 8 mini-batches per rank per
-        # chunk (train/online.py chunk_bounds balances the chunks of a pass)
-        cfg.online_chunk = 8 * cfg.batch_size * max(ctx.world_size, 1)
+    if cfg.model == "mlp_online" and cfg.online_chunk <= 0:  # auto: 32 mini-batches per rank per
+        # chunk (train/online.py chunk_bounds balances the chunks of a pass). A chunk ends with a
+        # validation pass and a checkpoint, and its first replay's launch latency and final sync
+        # are host time the GPU waits out: ~0.1 ms per chunk, 8 % of an 8-batch chunk of 262,144
+        # rows (round 5 used 8), 2 % at 32
+        cfg.online_chunk = 32 * cfg.batch_size * max(ctx.world_size, 1)
         say(f"Stream chunk (auto): {cfg.online_chunk} rows")
     b = max(1, min(cfg.batch_size, n_rank))
     if native and cfg.model == "lstm" and b >= 64:

@@ -167,6 +167,19 @@ class StepRunner:
                 self._update()
         return g
 
+    def prepare_many(self, n: int, key=0) -> bool:
+        """Capture (without running) the n-step graph of ``key``, so its first use is a plain
+        replay; False when the step cannot be captured whole or is not warmed up yet."""
+        if n <= 1 or not self.graph or self.calls <= self.eager_steps + 1:
+            return False
+        gk = ("many", key, n)
+        if gk not in self.graphs:
+            g = self._capture_many(key, n)
+            if g is None:
+                return False
+            self.graphs[gk] = g
+        return True
+
     def run_many(self, n: int, key=0) -> None:
         """``n`` full training steps as ONE graph replay (no host sync): step i reads
         ``inputs((key, i))``. Each step is exactly :meth:`run`'s (same kernels, same order, the

@@ -304,13 +304,43 @@ class Trainer:
             self._inject_fault()
         return bool(cfg.max_steps and self.global_step >= cfg.max_steps)
 
-    def train_steps(self, Xd, Yd, order: torch.Tensor, b: int):
+    def _permuted(self, Xd, Yd, order):
+        """The epoch's shuffle materialised: this rank's rows gathered once, in ``order``, into
+        persistent device buffers (two row-gather launches per epoch), so each step reads its
+        batch as a contiguous slice instead of one 32-B row at a random address per batch row
+        (the MLP job ran at 0.75 of the resident-batch bench that way). Only for row-indexed
+        engines on a GPU and while the copy takes under a quarter of the device's memory; None =
+        keep gathering from the dataset in place."""
+        eng = self.eng
+        if not (getattr(eng, "row_indexed", False) and torch.is_tensor(Xd) and torch.is_tensor(Yd)
+                and Xd.device.type == "cuda"):
+            return None
+        m = len(order)
+        need = m * (Xd[0].numel() * Xd.element_size() + Yd[0].numel() * Yd.element_size())
+        if need > torch.cuda.get_device_properties(Xd.device).total_memory // 4:
+            return None
+        key = ("perm", Xd.dtype, Yd.dtype, tuple(Xd.shape[1:]), tuple(Yd.shape[1:]), m)
+        bufs = self._idx.get(key)
+        if bufs is None:
+            bufs = self._idx[key] = (torch.empty((m,) + tuple(Xd.shape[1:]), dtype=Xd.dtype, device=Xd.device),
+                                     torch.empty((m,) + tuple(Yd.shape[1:]), dtype=Yd.dtype, device=Yd.device))
+        C = getattr(eng, "_C", None)
+        for src, dst in ((Xd, bufs[0]), (Yd, bufs[1])):
+            if C is not None and src.is_contiguous() and (src[0].numel() * src.element_size()) % 4 == 0:
+                C.gather_rows(src, order, dst)  # csrc/elementwise.hip gather_rows_kernel
+            else:
+                torch.index_select(src, 0, order, out=dst)
+        return bufs
+
+    def train_steps(self, Xd, Yd, order: torch.Tensor, b: int, sliced: bool = False):
         """One pass over ``order`` (device index tensor of this rank) in batches of ``b``.
 
         Each step gathers its batch from the resident dataset through a STATIC index buffer
         inside the captured step, so the whole step (gather, fwd, bwd, all-reduce, update)
         is one graph replay; the remainder that does not fill a batch is dropped (the native
-        engines run fixed-shape batches)."""
+        engines run fixed-shape batches). ``sliced``: Xd / Yd already hold the pass's rows in
+        order (Trainer._permuted): step j reads rows j*b .. (j+1)*b - 1 as a contiguous slice,
+        a fixed address per step, so every step's graph is captured once and no index is read."""
         eng, ctx = self.eng, self.ctx
         steps = len(order) // b
         if steps == 0 and len(order) > 0 and not getattr(eng, "native", False):
@@ -324,14 +354,21 @@ class Trainer:
         # rows from slice i of a static order buffer filled by one copy per group; the per-step
         # index copy + replay gap (~8 us of a 165-us MLP step) goes away. Row-indexed engines,
         # no per-step fault injection.
-        n_many = _graph_steps() if (row_indexed and eng.device.type == "cuda" and self.cfg.fail_at_step < 0) else 1
+        n_many = (_graph_steps() if ((row_indexed or sliced) and eng.device.type == "cuda" and self.cfg.fail_at_step < 0)
+                  else 1)
+        if n_many > 1 and steps > 1:  # balanced groups: 9 steps run as one 9-step replay, not 8 + 1
+            groups = max(1, round(steps / n_many))
+            n_many = -(-steps // groups)
         ordbuf = None
-        if n_many > 1 and steps >= n_many:
+        if n_many > 1 and steps >= n_many and not sliced:
             ordbuf = self._idx.get(("many", b, n_many))
             if ordbuf is None:
                 ordbuf = self._idx[("many", b, n_many)] = torch.zeros(n_many * b, dtype=torch.long, device=eng.device)
 
         def inputs(k):
+            if sliced:  # step j = k (single) or k[0] + k[1] (step k[1] of the group starting at k[0])
+                j = k[0] + k[1] if isinstance(k, tuple) else k
+                return Xd[j * b : (j + 1) * b], Yd[j * b : (j + 1) * b]
             if row_indexed:  # the engine's kernels read the rows through the index
                 if isinstance(k, tuple):  # step k[1] of a run_many group
                     return Xd, Yd, ordbuf[k[1] * b : (k[1] + 1) * b]
@@ -341,19 +378,31 @@ class Trainer:
             return Xd[idx], Yd.index_select(0, idx)
 
         run = self._runner(("resident", id(Xd), id(Yd)), inputs, b)
-        run.take_loss()
+        if run.loss_acc is not None:
+            run.loss_acc.zero_()  # no take_loss() here: its sync left the GPU idle through the first launch
         clock = StepClock(eng.device)
         done = 0
         cfg = self.cfg
         s = 0
+        prepared = False
         while s < steps:
             clock.first()
             n = n_many
-            if (ordbuf is None or s + n > steps or run.calls <= run.eager_steps + 1
+            if sliced and n > 1 and not prepared and run.calls > run.eager_steps + 1:
+                # every aligned group's graph (starts 0, n, 2n, ...) captured up front, in the first
+                # epoch: later epochs replay only, none of them pays a capture
+                prepared = all(run.prepare_many(n, g0) for g0 in range(0, steps - n + 1, n))
+            if ((ordbuf is None and not sliced) or n <= 1 or s + n > steps or run.calls <= run.eager_steps + 1
+                    or (sliced and s % n != 0)
                     or (cfg.max_steps and self.global_step + n > cfg.max_steps)):
-                idx.copy_(order[s * b : (s + 1) * b])
-                run.run()
+                if sliced:
+                    run.run(s)
+                else:
+                    idx.copy_(order[s * b : (s + 1) * b])
+                    run.run()
                 n = 1
+            elif sliced:
+                run.run_many(n, s)
             else:
                 ordbuf.copy_(order[s * b : (s + n) * b])
                 run.run_many(n)
@@ -392,8 +441,13 @@ class Trainer:
             perm = np.random.default_rng(cfg.seed + 7919 * self.epoch).permutation(n)
             mine = perm[ctx.rank * per_rank : (ctx.rank + 1) * per_rank]
             order = torch.as_tensor(mine, device=dev)
+            src = self._permuted(Xd, Yd, order)
+            if src is not None:  # this epoch's rows in shuffled order, read as contiguous slices
+                Xs, Ys = src
+            else:
+                Xs, Ys = Xd, Yd
             with trace_range("train_epoch", dev):
-                tr_loss, rows, dt = self.train_steps(Xd, Yd, order, b)
+                tr_loss, rows, dt = self.train_steps(Xs, Ys, order, b, sliced=src is not None)
             self.check_device()
             with trace_range("evaluate", dev):
                 v_loss, v_mse = self.evaluate(*val)

@@ -518,3 +518,23 @@ def test_persistent_sync_buffer_at_offset_under_graph_replay():
         out[offset] = eng.params.clone()
     d = (out[False] - out[True]).abs().max().item()
     assert d <= 5e-5, d
+
+
+@pytest.mark.parametrize("shape,dtype", [((100003, 16), torch.bfloat16), ((50001,), torch.float32),
+                                         ((7777, 3), torch.float32), ((4096, 32), torch.bfloat16)])
+def test_gather_rows_matches_index_select(shape, dtype):
+    """csrc/elementwise.hip gather_rows (the trainer's per-epoch shuffle copy) against
+    torch.index_select: bit-identical rows for 32-B / 64-B rows (16-B pieces) and 4-B / 12-B rows
+    (4-B pieces); ids are clamped to the table."""
+    from wellflow import _C
+
+    src = torch.randn(shape, device="cuda").to(dtype)
+    n = shape[0]
+    idx = torch.randint(0, n, (n // 2 + 3,), device="cuda")
+    out = torch.empty((len(idx),) + tuple(shape[1:]), dtype=dtype, device="cuda")
+    _C.gather_rows(src, idx, out)
+    assert torch.equal(out, src.index_select(0, idx))
+    idx2 = torch.tensor([-5, 0, n - 1, n + 7], device="cuda")
+    out2 = torch.empty((4,) + tuple(shape[1:]), dtype=dtype, device="cuda")
+    _C.gather_rows(src, idx2, out2)
+    assert torch.equal(out2, src.index_select(0, idx2.clamp(0, n - 1)))

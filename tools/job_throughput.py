@@ -36,6 +36,8 @@ def main():
     ap.add_argument("--out", default=None)
     ap.add_argument("--wells", type=int, default=6, help="synthetic wells: (wells - 1) + 2 one-hot + 9 "
                     "continuous features (6 -> 16, 90 -> 100)")
+    ap.add_argument("--scale", type=int, default=4, help="MLP tables: 640,000 x scale steps per well "
+                    "(4: ~36 mini-batches of 262,144 per pass; 1 = the round-4/5 table, 9 per pass)")
     ap.add_argument("--default-batch", action="store_true",
                     help="the job's own default batch (lstm: auto) instead of the bench's per-GPU batch")
     a = ap.parse_args()
@@ -44,11 +46,11 @@ def main():
 
     if a.model == "lstm":
         batch, extra, wells, steps = 8192, ["--seq-len", "64", "--hidden", "512"], a.wells, 40000 * 6 // a.wells
-    elif a.model == "mlp":
-        batch, extra, wells, steps = 262144, [], 6, 640000
-    else:  # the stream: chunks of 8 mini-batches, each consumed once (train/online.py)
-        batch, extra, wells, steps = 262144, [], 6, 640000
-        extra = ["--online-chunk", "0"]  # auto: ~8 batches per chunk, balanced (train/job.py auto_chunk)
+    elif a.model == "mlp":  # 15.4 M rows: ~36 steps of 262,144 per epoch
+        batch, extra, wells, steps = 262144, [], 6, 640000 * a.scale
+    else:  # the stream: chunks of 32 mini-batches, each consumed once (train/online.py)
+        batch, extra, wells, steps = 262144, [], 6, 640000 * a.scale
+        extra = ["--online-chunk", "0"]  # auto: ~32 batches per chunk, balanced (train/job.py)
     # 6 wells (3 fields): 5 + 2 one-hot columns + 9 continuous = 16 features, the bench's F
     argv = [NAMES, TYPES, "flow", "/tmp/wellflow_jobtp/", "--epochs", str(a.epochs), "--patience", "100",
             "--synth-wells", str(wells), "--synth-steps", str(steps), "--device", "cuda", "--verbose", "0"] + extra
@@ -57,10 +59,9 @@ def main():
     out = run_config(cfg, log=lambda *x, **k: None)
     from wellflow.data.pipeline import prepare  # noqa: F401  (feature count reported below)
     rps = out["history"]["rows_per_s"]  # wall clock
-    # warm-up epochs: the first (eager steps + graph capture); for the stream also the next two,
-    # whose batches still hit ring slots seen fewer than the StepRunner's eager + capture count
-    # (4 ring slots, 4-5 batches per auto chunk)
-    skip = 3 if a.model == "mlp_online" else 1
+    # warm-up epoch: the first (eager steps + graph captures; with 32-batch chunks the stream's
+    # 4 ring slots are all captured inside it)
+    skip = 1
     steady = rps[skip:] if len(rps) > skip else rps
     job = sum(steady) / len(steady)
     dev = out["history"].get("rows_per_s_device") or []
