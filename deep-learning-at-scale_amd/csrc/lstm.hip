@@ -63,7 +63,10 @@ __global__ void lstm_pack_x_kernel(const float* __restrict__ x, bf16_t* __restri
 }
 
 void launch_lstm_pack_x(const float* x, bf16_t* XH, LstmDims d, hipStream_t s, bool full) {
-  const int cpr = full ? (d.KX >> 3) : (d.F + 1 + 7) / 8;
+  // per-step packs round the chunks written up to whole 64-B segments (4 chunks; the rest of the
+  // block is the constant zero padding): 48 of a row's 128-B x block left a partial 32-B sector
+  int cpr = full ? (d.KX >> 3) : ((d.F + 1 + 7) / 8 + 3) / 4 * 4;
+  if (cpr > (d.KX >> 3)) cpr = d.KX >> 3;
   const long total = (long)d.T * d.B * cpr;
   int blocks = (int)((total + 255) / 256);
   if (blocks > 16384) blocks = 16384;

@@ -254,3 +254,36 @@ def test_trainer_graph_steps_equal_single_steps(monkeypatch, tmp_path):
     for x, y in zip(a["history"]["loss"], b["history"]["loss"]):
         assert abs(x - y) <= 1e-5 * abs(x), (a["history"]["loss"], b["history"]["loss"])
     assert abs(a["test_loss"] - b["test_loss"]) <= 1e-5 * abs(a["test_loss"])
+
+
+@pytest.mark.parametrize("comm_in_graph", [True, False])
+def test_run_many_with_rccl_group(monkeypatch, comm_in_graph):
+    """run_many under a forced RCCL group (world 1): with the all-reduce captured, n steps (and
+    n all-reduces) replay as one graph; with the split-graph fallback, run_many degrades to n
+    single steps. Either way the parameters equal n single steps of the eager reference."""
+    from wellflow.optim.flat import FlatAdam
+    from wellflow.parallel.dist import DistContext
+    from wellflow.train.step import StepRunner
+
+    for k, v in {"RANK": "0", "LOCAL_RANK": "0", "WORLD_SIZE": "1", "MASTER_ADDR": "127.0.0.1",
+                 "MASTER_PORT": str(_port())}.items():
+        monkeypatch.setenv(k, v)
+    monkeypatch.delenv("TORCHELASTIC_RESTART_COUNT", raising=False)
+    ctx = DistContext.from_env(force_group=True)
+    try:
+        eng_e, x, y = _mlp()
+        pe = _eager_reference(eng_e, x, y, 11)
+        eng, _, _ = _mlp()
+        opt = FlatAdam(eng.params, eng.grads, lr=1e-3, shadow=eng.shadow, zero_grads=True, shadow_t=eng.shadow_t)
+        run = StepRunner(eng, opt, ctx, 1.0 / len(y), lambda k: (x, y), graph=True, comm_in_graph=comm_in_graph)
+        for _ in range(3):
+            run.run()
+        run.run_many(4)
+        run.run_many(4)
+        torch.cuda.synchronize()
+        assert opt.steps_taken == 11
+        assert (("many", 0, 4) in run.graphs) == comm_in_graph
+        d = (pe - eng.params).abs().max().item()
+        assert d <= 5e-5, d
+    finally:
+        ctx.shutdown()
