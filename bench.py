@@ -85,7 +85,10 @@ def _spawn_ranks(n: int, argv) -> int:
     return subprocess.run(cmd, env=env, cwd=ROOT).returncode
 
 
-def _timed(ctx, step, steps, warmup, min_s: float = 0.0, many=None, graph_steps: int = 1):
+_LAST_TIMED = {"untimed": 0}  # steps the last _timed() ran outside its window (warm-up, probe, captures)
+
+
+def _timed(ctx, step, steps, warmup, min_s: float = 0.0, many=None, graph_steps: int = 1, warm_ms: float = 25.0):
     """W untimed warmup steps, then EXACTLY `steps` timed steps bracketed by barrier +
     synchronize on both sides; the max over ranks. With min_s > 0 (the secondary configs) a
     short untimed probe first raises `steps` until the timed window is >= min_s on the slowest
@@ -104,6 +107,7 @@ def _timed(ctx, step, steps, warmup, min_s: float = 0.0, many=None, graph_steps:
     for _ in range(warmup):
         step()
     total = warmup
+    per = None  # seconds per step, from the probe (secondaries)
     if min_s > 0:
         probe = 20
         ctx.barrier()
@@ -120,8 +124,22 @@ def _timed(ctx, step, steps, warmup, min_s: float = 0.0, many=None, graph_steps:
         steps = max(steps, int(math.ceil(min_s * 1.5 / max(per, 1e-9))))
     n = graph_steps if many is not None and graph_steps > 1 else 1
     if n > 1:
-        many(n)  # capture (untimed): one n-step replay of warmup
+        many(n)  # capture (untimed) + one n-step replay of warmup
         total += n
+        # the capture leaves the GPU idle for a while and its clock ramps down (an 8-step MLP replay
+        # after 10 ms idle runs ~14 % slow: tools/idle_gap_probe.py); more untimed replays, ~warm_ms
+        # of steps, bring it back before the window opens (the line reports them: untimed_steps)
+        if per is None:
+            sync()
+            t1 = time.perf_counter()
+            many(n)
+            sync()
+            per = ctx.max_scalar(time.perf_counter() - t1) / n
+            total += n
+        extra = int(math.ceil(warm_ms / 1e3 / (n * per))) if (per and warm_ms > 0) else 0
+        for _ in range(min(extra, 64)):
+            many(n)
+            total += n
     ctx.barrier()
     sync()
     t0 = time.perf_counter()
@@ -131,6 +149,7 @@ def _timed(ctx, step, steps, warmup, min_s: float = 0.0, many=None, graph_steps:
         step()
     sync()
     ctx.barrier()
+    _LAST_TIMED["untimed"] = total
     return ctx.max_scalar(time.perf_counter() - t0), steps, total + steps
 
 
@@ -216,7 +235,8 @@ def bench_lstm(args, ctx):
     x, y = x.to(ctx.device), y.to(ctx.device)
     run = StepRunner(eng, opt, ctx, 1.0 / (B * ctx.world_size), lambda k: (x, y),
                      graph=not (args.no_graph or eng.dw_chunk > 0), comm_in_graph=not args.eager_comm)
-    el, k, n = _timed(ctx, run.run, args.steps, args.warmup, args.min_timed_s, run.run_many, args.graph_steps)
+    el, k, n = _timed(ctx, run.run, args.steps, args.warmup, args.min_timed_s, run.run_many, args.graph_steps,
+                      warm_ms=args.warm_ms)
     eng.check_device_errors()  # a timed-out persistent hand-off anywhere in the run fails the bench
     extra = {"persistent_fwd": eng.last_forward_persistent, "persistent_bwd": eng.last_backward_persistent}
     # the engine adds each step's loss straight into the runner's accumulator: mean over the run
@@ -288,7 +308,8 @@ def bench_cnn(args, ctx):
     y = series[:, lay.input_len :].contiguous().to(ctx.device)
     run = StepRunner(eng, opt, ctx, 1.0 / (B * ctx.world_size * lay.outputs), lambda k: (x, y),
                      graph=not args.no_graph, comm_in_graph=not args.eager_comm)
-    el, k, n = _timed(ctx, run.run, args.steps, args.warmup, args.min_timed_s, run.run_many, args.graph_steps)
+    el, k, n = _timed(ctx, run.run, args.steps, args.warmup, args.min_timed_s, run.run_many, args.graph_steps,
+                      warm_ms=args.warm_ms)
     return el, k, B, model, run.take_loss() / (B * lay.outputs * n), run, eng, {}
 
 
@@ -352,7 +373,7 @@ def bench_mlp(args, ctx, online: bool):
         step = run.run
     # the streamed config changes its input slot every step: single-step replays
     el, k, n = _timed(ctx, step, args.steps, args.warmup, args.min_timed_s,
-                      None if online else run.run_many, args.graph_steps)
+                      None if online else run.run_many, args.graph_steps, warm_ms=args.warm_ms)
     if online:
         extra.update(streamer.copy_stats(skip=args.warmup))
         extra["h2d_mb_per_step"] = round((streamer.slots[0][0].numel() * streamer.slots[0][0].element_size()
@@ -392,10 +413,12 @@ def _secondary(args, ctx, models) -> dict:
         if ctx.device.type == "cuda":
             torch.cuda.empty_cache()
         el, k, B, desc, loss, run, eng, extra = _run_model(a, ctx)
+        untimed = _LAST_TIMED["untimed"]
         W = ctx.world_size
         out[m] = {"metric": f"rows/sec (whole node), {m} regression training", "value": round(B * W * k / el, 1),
                   "unit": "rows/s", "ms_per_step": round(1000.0 * el / max(k, 1), 4), "steps": k,
-                  "warmup": a.warmup, "timed_s": round(el, 4), "per_gpu_batch": B, "global_batch": B * W,
+                  "warmup": a.warmup, "untimed_steps": untimed, "timed_s": round(el, 4), "per_gpu_batch": B,
+                  "global_batch": B * W,
                   "model": desc, "train_loss": round(loss, 6), "step_graph": bool(run.graphs),
                   "graph_steps": max((key[2] for key in run.graphs if isinstance(key, tuple) and key[0] == "many"),
                                      default=1),
@@ -421,6 +444,8 @@ def main() -> int:
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--mlp-batches", type=int, default=1,
                     help="mlp: distinct resident batches cycled through a graph replay's steps")
+    ap.add_argument("--warm-ms", type=float, default=25.0,
+                    help="untimed n-step replays of about this much work after the graph capture")
     ap.add_argument("--graph-steps", type=int, default=8,
                     help="timed steps per captured graph replay (StepRunner.run_many; 1 = one replay per step)")
     ap.add_argument("--eager-comm", action="store_true", help="all-reduce between two graphs, not captured")
@@ -490,6 +515,7 @@ def main() -> int:
             return 3
     torch.manual_seed(1234 + ctx.rank)
     elapsed, steps, B, model, loss, run, eng, extra = _run_model(args, ctx)
+    untimed = _LAST_TIMED["untimed"]
     assert steps == args.steps
     comm = _comm_ms(ctx, eng.grads)
     grad_mb = round(eng.grads.numel() * 4 / 2**20, 3)
@@ -534,6 +560,9 @@ def main() -> int:
             "n_gpus": W,
             "steps": args.steps,
             "warmup": args.warmup,
+            # every step run outside the timed window: the W warm-up steps, the graph captures'
+            # replays and the post-capture warm replays (--warm-ms)
+            "untimed_steps": untimed,
             "ms_per_step": round(1000.0 * elapsed / max(args.steps, 1), 4),
             "higher_is_better": True,
             "scaling": "weak",
