@@ -137,12 +137,34 @@ class Trainer:
         per_rank = n_train // max(self.ctx.world_size, 1)
         return max(1, min(self.cfg.batch_size, per_rank))
 
+    def resident(self, X, Y):
+        """(X, Y) of an evaluation split as device tensors in the engine's input format, cached
+        per split, for native GPU engines on plain arrays (the small well-log sets fit HBM whole);
+        anything else comes back unchanged. Evaluating from host arrays cost ~220 ms per MLP
+        epoch of 7 ms of training (a numpy gather + copy + two syncs per chunk)."""
+        eng = self.eng
+        if not (getattr(eng, "native", False) and eng.device.type == "cuda") or hasattr(X, "starts"):
+            return X, Y
+        key = ("resident", id(X), id(Y))
+        hit = self._idx.get(key)
+        if hit is not None and hit[0] is X and hit[1] is Y:
+            return hit[2], hit[3]
+        Xd, Yd = _to_dev(X, eng.device), _to_dev(Y, eng.device)
+        in_dt = getattr(eng, "input_dtype", None)
+        if in_dt is not None and Xd.dtype != in_dt:
+            Xd = Xd.to(in_dt)
+        self._idx[key] = (X, Y, Xd, Yd)
+        return Xd, Yd
+
     def evaluate(self, X, Y, chunk: int | None = None):
         """-> (mean training-loss, mean MSE) over the split, all-reduced across ranks."""
         n = len(X)
         if n == 0:
             return float("nan"), float("nan")
+        X, Y = self.resident(X, Y)
         w, r = self.ctx.world_size, self.ctx.rank
+        if torch.is_tensor(X) and torch.is_tensor(Y) and X.device == self.eng.device == Y.device:
+            return self._eval_device(X, Y, w, r, chunk)
         idx = np.arange(r, n, w)
         chunk = chunk or getattr(self.eng, "B", 4096) or 4096
         Xd = X if (torch.is_tensor(X) or hasattr(X, "starts")) and getattr(X, "device", None) == self.eng.device \
@@ -154,6 +176,24 @@ class Trainer:
             if pf is not None:
                 pf.close()
         s_loss, s_mse, cnt = self.ctx.sum_scalars(s_loss, s_mse, cnt)
+        return s_loss / max(cnt, 1), s_mse / max(cnt, 1)
+
+    def _eval_device(self, X, Y, w: int, r: int, chunk: int | None):
+        """Device-resident split: rank r's rows r, r + w, ... as strided slices (no gather),
+        the sums accumulated on the device and read back once."""
+        chunk = chunk or getattr(self.eng, "B", 4096) or 4096
+        Xr, Yr = X[r::w], Y[r::w]
+        acc = torch.zeros(2, dtype=torch.float64, device=X.device)
+        for i in range(0, len(Xr), chunk):
+            xb, yb = Xr[i : i + chunk], Yr[i : i + chunk]
+            if not xb.is_contiguous():
+                xb = xb.contiguous()
+            yb = yb.float()
+            pred = self.eng.forward(xb).float().reshape(yb.shape)
+            acc[0] += per_element_loss(self.cfg.loss, pred, yb, self.cfg.clip).sum()
+            acc[1] += ((pred - yb) ** 2).sum()
+        s_loss, s_mse = acc.tolist()
+        s_loss, s_mse, cnt = self.ctx.sum_scalars(s_loss, s_mse, float(Yr.numel()))
         return s_loss / max(cnt, 1), s_mse / max(cnt, 1)
 
     def _eval_chunks(self, X, Y, Xd, idx, chunk, pf):
@@ -304,6 +344,21 @@ class Trainer:
             self._inject_fault()
         return bool(cfg.max_steps and self.global_step >= cfg.max_steps)
 
+    def _epoch_order(self, n: int, per_rank: int, dev):
+        """This rank's rows of the epoch's shuffle (seed + 7919 * epoch, the same on every rank).
+        On a GPU the permutation is drawn on the device (torch.randperm with a seeded device
+        generator): the host numpy permutation + 78-MB index copy took ~200 ms per epoch of a
+        15 M-row table (the MLP job's epochs train for 7 ms)."""
+        cfg, ctx = self.cfg, self.ctx
+        seed = cfg.seed + 7919 * self.epoch
+        if torch.device(dev).type == "cuda":
+            g = torch.Generator(device=dev)
+            g.manual_seed(seed)
+            perm = torch.randperm(n, generator=g, device=dev)
+            return perm[ctx.rank * per_rank : (ctx.rank + 1) * per_rank]
+        perm = np.random.default_rng(seed).permutation(n)
+        return torch.as_tensor(perm[ctx.rank * per_rank : (ctx.rank + 1) * per_rank], device=dev)
+
     def _permuted(self, Xd, Yd, order):
         """The epoch's shuffle materialised: this rank's rows gathered once, in ``order``, into
         persistent device buffers (two row-gather launches per epoch), so each step reads its
@@ -438,9 +493,7 @@ class Trainer:
         per_rank = n // max(ctx.world_size, 1)
         while self.epoch < cfg.epochs and not self.stopper.stopped:
             t_ep = time.perf_counter()
-            perm = np.random.default_rng(cfg.seed + 7919 * self.epoch).permutation(n)
-            mine = perm[ctx.rank * per_rank : (ctx.rank + 1) * per_rank]
-            order = torch.as_tensor(mine, device=dev)
+            order = self._epoch_order(n, per_rank, dev)
             src = self._permuted(Xd, Yd, order)
             if src is not None:  # this epoch's rows in shuffled order, read as contiguous slices
                 Xs, Ys = src

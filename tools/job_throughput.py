@@ -88,6 +88,8 @@ def main():
            # the device-busy span of the same steps (CUDA events), beside the wall-clock figure
            "job_rows_per_s_per_epoch_device": dev, "job_steady_rows_per_s_device": dev_mean,
            "job_steady_spread_device": dev_spread,
+           # wall seconds per epoch (training + evaluation + checkpoint) beside the training span
+           "epoch_time_s": out["history"].get("epoch_time"),
            "data": f"synthetic well-log table {wells} wells x {steps} steps"}
     print(json.dumps(rec), flush=True)
     if a.out:
