@@ -143,15 +143,15 @@ class Trainer:
         anything else comes back unchanged. Evaluating from host arrays cost ~220 ms per MLP
         epoch of 7 ms of training (a numpy gather + copy + two syncs per chunk)."""
         eng = self.eng
-        if not (getattr(eng, "native", False) and eng.device.type == "cuda") or hasattr(X, "starts"):
+        if not (getattr(eng, "native", False) and eng.device.type == "cuda"):
             return X, Y
         key = ("resident", id(X), id(Y))
         hit = self._idx.get(key)
         if hit is not None and hit[0] is X and hit[1] is Y:
             return hit[2], hit[3]
-        Xd, Yd = _to_dev(X, eng.device), _to_dev(Y, eng.device)
+        Xd, Yd = _to_dev(X, eng.device), _to_dev(Y, eng.device)  # windows: rows + starts on the device
         in_dt = getattr(eng, "input_dtype", None)
-        if in_dt is not None and Xd.dtype != in_dt:
+        if in_dt is not None and torch.is_tensor(Xd) and Xd.dtype != in_dt:
             Xd = Xd.to(in_dt)
         self._idx[key] = (X, Y, Xd, Yd)
         return Xd, Yd
@@ -163,7 +163,8 @@ class Trainer:
             return float("nan"), float("nan")
         X, Y = self.resident(X, Y)
         w, r = self.ctx.world_size, self.ctx.rank
-        if torch.is_tensor(X) and torch.is_tensor(Y) and X.device == self.eng.device == Y.device:
+        dev = self.eng.device
+        if torch.is_tensor(Y) and Y.device == dev and getattr(X, "device", None) == dev:
             return self._eval_device(X, Y, w, r, chunk)
         idx = np.arange(r, n, w)
         chunk = chunk or getattr(self.eng, "B", 4096) or 4096
@@ -179,13 +180,17 @@ class Trainer:
         return s_loss / max(cnt, 1), s_mse / max(cnt, 1)
 
     def _eval_device(self, X, Y, w: int, r: int, chunk: int | None):
-        """Device-resident split: rank r's rows r, r + w, ... as strided slices (no gather),
-        the sums accumulated on the device and read back once."""
+        """Device-resident split: rank r's rows r, r + w, ... as strided slices (no gather; a
+        window set gathers each chunk's windows on the GPU), the sums accumulated on the device
+        and read back once."""
         chunk = chunk or getattr(self.eng, "B", 4096) or 4096
-        Xr, Yr = X[r::w], Y[r::w]
-        acc = torch.zeros(2, dtype=torch.float64, device=X.device)
-        for i in range(0, len(Xr), chunk):
-            xb, yb = Xr[i : i + chunk], Yr[i : i + chunk]
+        windows = hasattr(X, "starts")  # device windows: each chunk gathered on the GPU
+        ridx = torch.arange(r, len(X), w, device=Y.device) if windows else None
+        Xr, Yr = (X, Y[r::w]) if windows else (X[r::w], Y[r::w])
+        acc = torch.zeros(2, dtype=torch.float64, device=Y.device)
+        for i in range(0, len(Yr), chunk):
+            xb = X[ridx[i : i + chunk]] if windows else Xr[i : i + chunk]
+            yb = Yr[i : i + chunk]
             if not xb.is_contiguous():
                 xb = xb.contiguous()
             yb = yb.float()
