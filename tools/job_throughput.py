@@ -59,9 +59,11 @@ def main():
     out = run_config(cfg, log=lambda *x, **k: None)
     from wellflow.data.pipeline import prepare  # noqa: F401  (feature count reported below)
     rps = out["history"]["rows_per_s"]  # wall clock
-    # warm-up epoch: the first (eager steps + graph captures; with 32-batch chunks the stream's
-    # 4 ring slots are all captured inside it)
-    skip = 1
+    # warm-up: the first epoch (eager steps + graph captures; with 32-batch chunks the stream's
+    # 4 ring slots are all captured inside it); for the stream also the next two ~5-ms chunks,
+    # over which the GPU clock is still ramping up from the idle before the job (their rate
+    # climbs 1.31 -> 1.37 G, then holds at 1.39-1.43: tools/idle_gap_probe.py)
+    skip = 3 if a.model == "mlp_online" else 1
     steady = rps[skip:] if len(rps) > skip else rps
     job = sum(steady) / len(steady)
     dev = out["history"].get("rows_per_s_device") or []
