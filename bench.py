@@ -349,7 +349,9 @@ def bench_mlp(args, ctx, online: bool):
                         x_dtype=x_dtype)
         # copies bracketed by events: the JSON reports their device time (a shared host's PCIe
         # load shows up here, not in the kernels)
-        streamer = DeviceStreamer(pool, ctx.device, depth=4, timing=True)
+        # every 16th batch's copies timed (all of them cost this PCIe-bound config ~5 %)
+        streamer = DeviceStreamer(pool, ctx.device, depth=args.stream_depth,
+                                  timing=0 if args.no_h2d_timing else 16)
         # one captured step per ring slot (the graph reads that slot's buffers)
         run = StepRunner(eng, opt, ctx, gscale, lambda k: tuple(streamer.slots[k][:2]), graph=graph,
                          comm_in_graph=not args.eager_comm)
@@ -375,7 +377,7 @@ def bench_mlp(args, ctx, online: bool):
     el, k, n = _timed(ctx, step, args.steps, args.warmup, args.min_timed_s,
                       None if online else run.run_many, args.graph_steps, warm_ms=args.warm_ms)
     if online:
-        extra.update(streamer.copy_stats(skip=args.warmup))
+        extra.update(streamer.copy_stats(skip=1))
         extra["h2d_mb_per_step"] = round((streamer.slots[0][0].numel() * streamer.slots[0][0].element_size()
                                           + streamer.slots[0][1].numel() * 4) / 1e6, 3)
     # the engine adds each step's loss straight into the runner's accumulator: mean over the run
@@ -452,6 +454,8 @@ def main() -> int:
     ap.add_argument("--comm-dtype", choices=["fp32", "bf16"], default="fp32",
                     help="C2 gradient all-reduce precision (parallel/dist.py; default fp32)")
     ap.add_argument("--stream-fp32", action="store_true", help="mlp_online: stream fp32 features")
+    ap.add_argument("--stream-depth", type=int, default=4, help="mlp_online: device ring slots")
+    ap.add_argument("--no-h2d-timing", action="store_true", help="mlp_online: no events around the copies (default: every 16th batch timed)")
     ap.add_argument("--host-pool", type=int, default=8, help="mlp_online: distinct pinned host batches cycled")
     ap.add_argument("--device", choices=["auto", "cpu"], default="auto",
                     help="cpu: rehearse the launch/timing/JSON contract on the fp32 reference over gloo")

@@ -59,9 +59,11 @@ class HostPool:
 
 
 class DeviceStreamer:
-    def __init__(self, source, device, depth: int = 4, x_dtype=None, timing: bool = False):
+    def __init__(self, source, device, depth: int = 4, x_dtype=None, timing: bool | int = False):
         """``x_dtype``: cast features on the host before the copy (e.g. torch.bfloat16);
-        ``timing``: bracket every batch's copies with events (:meth:`copy_stats`)."""
+        ``timing``: bracket the copies with events (:meth:`copy_stats`) — True for every batch,
+        an int N for every N-th batch (the two event records per copy cost the PCIe-bound
+        streamed bench ~5 % when every batch is timed)."""
         assert depth >= 3, "the refill lags two batches behind the consumer (module docstring)"
         self.device = torch.device(device)
         self.copy_stream = torch.cuda.Stream(device=self.device)
@@ -72,7 +74,7 @@ class DeviceStreamer:
         # slot reuse is ordered on the host (event.synchronize) instead of by a copy-queue wait
         # on the compute stream: module docstring (WELLFLOW_H2D_HOSTWAIT=0: queue wait)
         self.host_wait = os.environ.get("WELLFLOW_H2D_HOSTWAIT", "1") != "0"
-        self.timing = timing
+        self.timing = int(timing) if timing else 0  # time every N-th batch (0: none)
         self._tev = []  # (start, end) events of timed batches
         self.staging = []  # pinned host ring for pageable sources: [x_pin, y_pin]
         # monotonic over the streamer's life: batch i lives in slot i % depth
@@ -159,14 +161,15 @@ class DeviceStreamer:
                 done.synchronize()
             else:
                 self.copy_stream.wait_event(done)
+        timed = self.timing and self.k % self.timing == 0
         with torch.cuda.stream(self.copy_stream):
-            if self.timing:
+            if timed:
                 t0, t1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 t0.record(self.copy_stream)
             xd.copy_(x, non_blocking=True)
             yd.copy_(y, non_blocking=True)
             ev.record(self.copy_stream)
-            if self.timing:
+            if timed:
                 t1.record(self.copy_stream)
                 self._tev.append((t0, t1))
         self._chunk_of.append(cid)
@@ -221,7 +224,8 @@ class DeviceStreamer:
         self._consume = cid + 1
 
     def copy_stats(self, skip: int = 0) -> dict:
-        """Device time of each timed batch's host->HBM copies (ms): mean / median / max (syncs)."""
+        """Device time of each timed batch's host->HBM copies (ms): mean / median / max (syncs);
+        ``skip``: timed batches to leave out at the start."""
         torch.cuda.synchronize(self.device)
         ms = [a.elapsed_time(b) for a, b in list(self._tev)[skip:]]
         if not ms:
