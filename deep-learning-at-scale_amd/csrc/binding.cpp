@@ -395,7 +395,7 @@ void lstm_adam_pack(const at::Tensor& p, const at::Tensor& g, const at::Tensor& 
   for (const at::Tensor* t : {&p, &g, &m, &v}) check_t(*t, at::kFloat, "p/g/m/v");
   const int64_t n = p.numel();
   TORCH_CHECK(g.numel() == n && m.numel() == n && v.numel() == n, "lstm_adam_pack: size mismatch");
-  TORCH_CHECK(KX % 4 == 0 && H % 4 == 0 && n >= 4 * H * (KX + H), "lstm_adam_pack: layout");
+  TORCH_CHECK(KX % 32 == 0 && H % 32 == 0 && n >= 4 * H * (KX + H), "lstm_adam_pack: layout (KX, H multiples of 32)");
   for (const at::Tensor* t : {&p, &g, &m, &v})
     TORCH_CHECK(reinterpret_cast<uintptr_t>(t->data_ptr()) % 16 == 0, "lstm_adam_pack: buffers must be 16-B aligned");
   check_t(step, at::kFloat, "step");

@@ -502,10 +502,17 @@ __global__ __launch_bounds__(256) void lstm_adam_pack_kernel(float* __restrict__
   const float t = step[0] + 1.f;
   const float bc1 = 1.f - __powf(b1, t), bc2 = 1.f - __powf(b2, t);
   const int KA = KX + H, G = 4 * H;
-  const long nw4 = (long)G * KA / 4;  // KA % 4 == 0: a float4 never straddles a W row
-  const long n4 = n / 4;
-  const long stride = (long)gridDim.x * blockDim.x;
-  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n4; i += stride) {
+  // the W block in 32 x 32 tiles (KX, H multiples of 32, host-checked): thread = 4 consecutive
+  // columns of one row, so the Adam streams and the Wp rows stay float4 / 8-B coalesced, and the
+  // W_hh^T image goes out through an LDS transpose as 64-B runs of 32 rows (written straight from
+  // the row-major loop it was 2-B stores 4 KiB apart: ~3x the kernel's streaming time)
+  __shared__ bf16_t tt[32][36];  // [k][r]
+  const int tilesK = KA / 32, ntiles = (G / 32) * tilesK;
+  const int rr = threadIdx.x >> 3, kk = (threadIdx.x & 7) * 4;
+  for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    const int r0 = (tile / tilesK) * 32, k0 = (tile % tilesK) * 32;
+    const int r = r0 + rr, k = k0 + kk;
+    const long i = ((long)r * KA + k) >> 2;
     float4 pp = reinterpret_cast<float4*>(p)[i];
     float4 gg = reinterpret_cast<const float4*>(g)[i];
     float4 mm = reinterpret_cast<float4*>(m)[i];
@@ -518,23 +525,26 @@ __global__ __launch_bounds__(256) void lstm_adam_pack_kernel(float* __restrict__
     reinterpret_cast<float4*>(m)[i] = mm;
     reinterpret_cast<float4*>(v)[i] = vv;
     if (zero_g) reinterpret_cast<float4*>(g)[i] = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (i < nw4) {
-      const long idx = 4 * i;
-      const int k = (int)(idx % KA), r = (int)(idx / KA);
-      const float sc = (r & 3) == 2 ? kLstmTanhScale : kLstmSigScale;
-      const unsigned lo = (unsigned)f2bf(pp.x * sc) | ((unsigned)f2bf(pp.y * sc) << 16);
-      const unsigned hi = (unsigned)f2bf(pp.z * sc) | ((unsigned)f2bf(pp.w * sc) << 16);
-      *reinterpret_cast<uint2*>(Wp + (size_t)gate_col(r & 3, r >> 2) * KA + k) = make_uint2(lo, hi);
-      if (k >= KX) {  // (KX % 4 == 0: all four or none)
-        bf16_t* col = WhhT + (size_t)(k - KX) * G + r;
-        col[0] = f2bf(pp.x);
-        col[(size_t)G] = f2bf(pp.y);
-        col[(size_t)2 * G] = f2bf(pp.z);
-        col[(size_t)3 * G] = f2bf(pp.w);
-      }
+    const float sc = (r & 3) == 2 ? kLstmTanhScale : kLstmSigScale;
+    const unsigned lo = (unsigned)f2bf(pp.x * sc) | ((unsigned)f2bf(pp.y * sc) << 16);
+    const unsigned hi = (unsigned)f2bf(pp.z * sc) | ((unsigned)f2bf(pp.w * sc) << 16);
+    *reinterpret_cast<uint2*>(Wp + (size_t)gate_col(r & 3, r >> 2) * KA + k) = make_uint2(lo, hi);
+    if (k0 >= KX) {  // block-uniform: the tile lies wholly in the h columns
+      tt[kk][rr] = f2bf(pp.x);
+      tt[kk + 1][rr] = f2bf(pp.y);
+      tt[kk + 2][rr] = f2bf(pp.z);
+      tt[kk + 3][rr] = f2bf(pp.w);
+      __syncthreads();
+      const int kt = threadIdx.x >> 3, rc = (threadIdx.x & 7) * 4;
+      const unsigned w0 = (unsigned)tt[kt][rc] | ((unsigned)tt[kt][rc + 1] << 16);
+      const unsigned w1 = (unsigned)tt[kt][rc + 2] | ((unsigned)tt[kt][rc + 3] << 16);
+      *reinterpret_cast<uint2*>(WhhT + (size_t)(k0 - KX + kt) * G + r0 + rc) = make_uint2(w0, w1);
+      __syncthreads();
     }
   }
-  for (long i = n4 * 4 + blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += stride) {
+  // the head (w_out, b_out) past the W block
+  const long stride = (long)gridDim.x * blockDim.x;
+  for (long i = (long)G * KA + blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += stride) {
     adam_one(p[i], g[i] * gscale, m[i], v[i], lr, b1, b2, eps, wd, bc1, bc2);
     if (zero_g) g[i] = 0.f;
   }

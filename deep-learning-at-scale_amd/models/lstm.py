@@ -265,8 +265,8 @@ class NativeLSTM:
     def fused_adam(self, opt, grad_scale: float) -> bool:
         """The optimizer's Adam update and this engine's bf16 compute copies (Wp, WhhT) in ONE
         launch (optim/flat.py FlatAdam ``writeback``; csrc/elementwise.hip lstm_adam_pack_kernel)."""
-        if opt.shadow is not None or opt.shadow_t is not None:
-            return False
+        if opt.shadow is not None or opt.shadow_t is not None or self.H % 32 or self.lay.KX % 32:
+            return False  # (the kernel transposes W_hh in 32 x 32 tiles)
         b1, b2 = opt.betas
         self._C.lstm_adam_pack(self.params, self.grads, opt.m, opt.v, opt.step_dev, opt.lr, b1, b2, opt.eps,
                                opt.weight_decay, grad_scale, opt.zero_grads, self.Wp, self.WhhT, self.H, self.lay.KX)
