@@ -149,6 +149,10 @@ class Trainer:
         hit = self._idx.get(key)
         if hit is not None and hit[0] is X and hit[1] is Y:
             return hit[2], hit[3]
+        rows = getattr(X, "rows", X)  # windows: their row table is what moves
+        nbytes = getattr(rows, "nbytes", 0) or (rows.numel() * rows.element_size() if torch.is_tensor(rows) else 0)
+        if nbytes > torch.cuda.get_device_properties(eng.device).total_memory // 8:
+            return X, Y  # a split this large stays on the host (chunked path)
         Xd, Yd = _to_dev(X, eng.device), _to_dev(Y, eng.device)  # windows: rows + starts on the device
         in_dt = getattr(eng, "input_dtype", None)
         if in_dt is not None and torch.is_tensor(Xd) and Xd.dtype != in_dt:
