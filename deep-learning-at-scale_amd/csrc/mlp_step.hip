@@ -939,7 +939,7 @@ constexpr int DW2F_MAX_ROWS = 2048;                      // rows per workgroup (
 // out rows, so a chunk needs only the 16 dZ2 fragments of the tile's out units (16 KiB of
 // LDS-DMA instead of 32) and H1 is recomputed once per column (twice there); the MFMAs per
 // (out, in) element and their order are unchanged (bit-identical dW2), +0.4 % step rate.
-constexpr int DW2G_SLOTS = 4;
+constexpr int DW2G_SLOTS = 6;  // 5 chunks in flight (128 KiB of LDS with the row-id table)
 constexpr int DW2G_ABYTES = 16 * 1024;                  // 2 steps x 8 dZ2 fragments
 constexpr int DW2G_SLOT = DW2G_ABYTES + MF_ROWS * 64;   // + X tile [64 rows][64 B]
 __global__ __launch_bounds__(512, 1) void mlp2_dw2g_kernel(const bf16_t* __restrict__ dZ2F, const bf16_t* __restrict__ X,
@@ -1008,11 +1008,11 @@ __global__ __launch_bounds__(512, 1) void mlp2_dw2g_kernel(const bf16_t* __restr
 #pragma unroll
   for (int k = 0; k < DW2G_SLOTS - 1; ++k) issue(min(k, last), k);
   for (int c = 0; c < nch; ++c) {
-    const int slot = c & (DW2G_SLOTS - 1);
+    const int slot = c % DW2G_SLOTS;
     dma_wait(std::integral_constant<int, DW2G_SLOTS - 2>{});  // chunk c's pieces (this wave) landed
     __builtin_amdgcn_s_barrier();                              // ... every wave's; slot c - 1 free
     asm volatile("" ::: "memory");
-    issue(min(c + DW2G_SLOTS - 1, last), (c + DW2G_SLOTS - 1) & (DW2G_SLOTS - 1));
+    issue(min(c + DW2G_SLOTS - 1, last), (c + DW2G_SLOTS - 1) % DW2G_SLOTS);
     const char* st = smem + slot * DW2G_SLOT;
     bf16x8 xfa[2][2], afa[2][8];
     auto frags = [&](int s2) {
