@@ -1097,18 +1097,20 @@ bool launch_mlp2_step(const bf16_t* X, int Fp, const bf16_t* W1, const float* b1
   constexpr int prio = 1;
   if (W2T != nullptr && dz_frag) {  // 128-row passes, both weight images streamed
     if (rows != nullptr && nrows > 0x7FFFFFFFL) return false;  // 32-bit row ids in the kernel
+    // the same static priority split for the 128-row kernel (A/B: WELLFLOW_MLP_PRIO128, WF_DIAG only)
+    static const int prio128 = diag_env_int("WELLFLOW_MLP_PRIO128", prio);
     if (stamp && Fp <= 16) {
       hipLaunchKernelGGL((mlp2_step128_kernel<1, true>), dim3(grid), dim3(512), 0, s, X, Fp, W1, b1, W2, W2T, b2, w3, b3,
-                         y, dy_scale, B, rows, nrows, dZ2, pred, red, prio,
+                         y, dy_scale, B, rows, nrows, dZ2, pred, red, prio128,
                          reinterpret_cast<unsigned long long*>(red + kMlpRedSlab2Off + 200L * 65536));
       return true;
     }
     if (Fp <= 16)
       hipLaunchKernelGGL(mlp2_step128_kernel<1>, dim3(grid), dim3(512), 0, s, X, Fp, W1, b1, W2, W2T, b2, w3, b3, y,
-                         dy_scale, B, rows, nrows, dZ2, pred, red, prio);
+                         dy_scale, B, rows, nrows, dZ2, pred, red, prio128);
     else
       hipLaunchKernelGGL(mlp2_step128_kernel<2>, dim3(grid), dim3(512), 0, s, X, Fp, W1, b1, W2, W2T, b2, w3, b3, y,
-                         dy_scale, B, rows, nrows, dZ2, pred, red, prio);
+                         dy_scale, B, rows, nrows, dZ2, pred, red, prio128);
     return true;
   }
   if (stamp && Fp <= 16 && dz_frag) {
