@@ -42,6 +42,7 @@
 #include <cstdlib>
 
 #include "common.h"
+#include "gemm_core.h"
 #include "kernels.h"
 
 namespace wf {
@@ -138,12 +139,18 @@ __global__ __launch_bounds__(512, 1) void cnn_fwd_kernel(
   const int ngroups = (B + 15) >> 4;
   // the lane's x samples, loaded one group AHEAD (issued before this group's 36 steps, consumed
   // a group later): raw float4s from a clamped in-range address, bounds applied at consumption
+  // (and, training, its 4 targets: a load in the epilogue exposed its latency once per group)
   float4 xnx[XR / 4];
+  float ynx[4];
   auto load_x = [&](int g) {
     const int wc = min(g * 16 + l15, B - 1);
 #pragma unroll
     for (int k = 0; k < XR / 4; ++k)
       xnx[k] = *reinterpret_cast<const float4*>(x + (size_t)wc * L + min(4 * q + 4 * k, L - 4));
+    if constexpr (TRAIN) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) ynx[r] = y[(size_t)wc * O + min(4 * q + r, O - 1)];
+    }
   };
   const int gstride = gridDim.x * CNN_NW;
   // the first group's x and the dense weights' fragment image go out together: the image as
@@ -181,6 +188,9 @@ __global__ __launch_bounds__(512, 1) void cnn_fwd_kernel(
       xp[2 * k] = ok ? pk_bf16(v.x, v.y) : 0u;
       xp[2 * k + 1] = ok ? pk_bf16(v.z, v.w) : 0u;
     }
+    float ycur[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) ycur[r] = TRAIN ? ynx[r] : 0.f;
     load_x(min(g + gstride, ngroups - 1));  // (the last group re-loads itself: never read)
     f32x4 out = {0.f, 0.f, 0.f, 0.f};
     // dense-weight fragments of step t (pairs of 16-filter blocks as 16x16x32 A operands, block
@@ -250,7 +260,7 @@ __global__ __launch_bounds__(512, 1) void cnn_fwd_kernel(
       d[r] = 0.f;
       if (TRAIN) {
         if (wok && j < O) {
-          const float yv = y[(size_t)w * O + j];
+          const float yv = ycur[r];
           float l, dd;
           if (loss_kind == 0) {
             const float e = pv - yv;
@@ -346,34 +356,65 @@ __global__ __launch_bounds__(512, 1) void cnn_bwd_kernel(
     for (int tt = 0; tt < TG; ++tt) acc_wd[tt][b] = f32x4{0.f, 0.f, 0.f, 0.f};
   }
 
-  // the group's global operands, loaded one group AHEAD (issued before the current group's
-  // MFMAs, consumed a group later): at one load round per group their L2 latency was exposed
-  // once per 16 windows. Raw values only; bounds selects are applied at consumption. Rows past
-  // B of dOut are zero in the buffer (the forward writes every row of the last group it owns);
-  // x addresses are clamped in range (the selects zero what they stand for).
+  // the group's global operands through a per-wave LDS ring, two groups AHEAD: 6 LDS-DMA
+  // instructions per group (dOut rows [16][16] as one 16-B piece per lane, the x window [16
+  // rows][XS samples] as five 4-B pieces per lane), counted vmcnt waits, plain LDS reads at
+  // consumption. (Round 5 before: register loads one group ahead, 39 % of the cycles still
+  // waiting on them; two register sets rotate through copies that wait for the newest loads.)
+  // Raw values only; bounds selects are applied at consumption. Rows past B of dOut are zero
+  // in the buffer (the forward writes every row of the last group it owns); x addresses are
+  // clamped in range (the selects zero what they stand for). The ring aliases `red`, used only
+  // after the loop.
+  constexpr int XS = 20;                  // x samples per ring row: t0 .. t0 + 19 (TG + 15 used)
+  constexpr int GSLOT = 1024 + 16 * XS * 4;
+  constexpr int NSLOT = 3;  // two groups in flight (three: 72.55 vs 72.63 us, no gain)
+  static_assert(TG + 15 <= XS && 16 * XS <= 5 * 64, "x window: five 64-lane pieces");
+  static_assert(CNN_NW * NSLOT * GSLOT <= (int)sizeof(red), "ring inside the reduction buffer");
+  typedef __attribute__((address_space(3))) void lds_v;
+  char* ring = reinterpret_cast<char*>(red) + wid * (NSLOT * GSLOT);
+  int xoff[5];  // ring element 64k + lane -> (row, sample): row * L + clamped sample
+#pragma unroll
+  for (int k = 0; k < 5; ++k) {
+    const int e = 64 * k + lane, r = min(e / XS, 15);
+    xoff[k] = r * L + min(t0 + e % XS, L - 1);
+  }
+  auto issue = [&](int g, int slot) {
+    char* st = ring + slot * GSLOT;
+    const int w0 = g * 16;
+    __builtin_amdgcn_global_load_lds((const void*)(dout + (size_t)w0 * 16 + lane * 4), (lds_v*)st, 16, 0, 0);
+    if (w0 + 15 < B) {
+      const float* xg = x + (size_t)w0 * L;
+#pragma unroll
+      for (int k = 0; k < 5; ++k)
+        __builtin_amdgcn_global_load_lds((const void*)(xg + xoff[k]), (lds_v*)(st + 1024 + 256 * k), 4, 0, 0);
+    } else {  // the batch's last, partial group: rows clamped to B - 1
+#pragma unroll
+      for (int k = 0; k < 5; ++k) {
+        const int e = 64 * k + lane, r = min(e / XS, 15);
+        const float* src = x + (size_t)min(w0 + r, B - 1) * L + (xoff[k] - r * L);
+        __builtin_amdgcn_global_load_lds((const void*)src, (lds_v*)(st + 1024 + 256 * k), 4, 0, 0);
+      }
+    }
+  };
   struct GroupLoads {
     float4 da;
     float dbv[4], xa[TG + 3], xb[TG][4];
   };
-  auto load_group = [&](int g, GroupLoads& G) {
-    const int w0 = g * 16;
-    G.da = *reinterpret_cast<const float4*>(dout + (size_t)(w0 + l15) * 16 + 4 * q);
+  auto read_group = [&](int slot, GroupLoads& G) {
+    const float* D = reinterpret_cast<const float*>(ring + slot * GSLOT);
+    const float* X = D + 256;
+    G.da = make_float4(D[l15 * 16 + 4 * q], D[l15 * 16 + 4 * q + 1], D[l15 * 16 + 4 * q + 2], D[l15 * 16 + 4 * q + 3]);
 #pragma unroll
-    for (int jj = 0; jj < 4; ++jj) G.dbv[jj] = dout[(size_t)(w0 + 4 * q + jj) * 16 + l15];
-    const int wac = min(w0 + l15, B - 1);
+    for (int jj = 0; jj < 4; ++jj) G.dbv[jj] = D[(4 * q + jj) * 16 + l15];
 #pragma unroll
-    for (int i = 0; i < TG + 3; ++i) G.xa[i] = x[(size_t)wac * L + min(t0 + 4 * q + i, L - 1)];
+    for (int i = 0; i < TG + 3; ++i) G.xa[i] = X[l15 * XS + 4 * q + i];
 #pragma unroll
     for (int tt = 0; tt < TG; ++tt)
 #pragma unroll
-      for (int jj = 0; jj < 4; ++jj) G.xb[tt][jj] = x[(size_t)min(w0 + 4 * q + jj, B - 1) * L + min(t0 + tt + l15, L - 1)];
+      for (int jj = 0; jj < 4; ++jj) G.xb[tt][jj] = X[(4 * q + jj) * XS + tt + l15];
   };
-  GroupLoads nxt;
-  if (g_begin + wid < g_end) load_group(g_begin + wid, nxt);
-  for (int g = g_begin + wid; g < g_end; g += CNN_NW) {
+  auto process = [&](const GroupLoads& cur, int g) {
     const int w0 = g * 16;
-    const GroupLoads cur = nxt;
-    load_group(min(g + CNN_NW, g_end - 1), nxt);  // (the last group re-loads itself: never read)
     // dOut (x keep_scale) as A[w = l15][j = 4q + jj] and as B[w = 4q + jj][j = l15]
     const float4 da = cur.da;
     const bf16x4 doA = frag(pk_bf16(da.x * keep_scale, da.y * keep_scale), pk_bf16(da.z * keep_scale, da.w * keep_scale));
@@ -441,7 +482,25 @@ __global__ __launch_bounds__(512, 1) void cnn_bwd_kernel(
         acc_wc[b] = mfma16(frag(dp[0], dp[1]), xB, acc_wc[b]);
       }
     }
+  };
+  const int gs = g_begin + wid;
+  if (gs < g_end) {
+#pragma unroll
+    for (int k = 0; k < NSLOT - 1; ++k) issue(min(gs + k * CNN_NW, g_end - 1), k);
   }
+  int slot = 0;
+  for (int g = gs; g < g_end; g += CNN_NW) {
+    // slot (slot - 1) mod NSLOT was read by the previous group (its values are in registers)
+    asm volatile("" ::: "memory");
+    issue(min(g + (NSLOT - 1) * CNN_NW, g_end - 1), slot == 0 ? NSLOT - 1 : slot - 1);  // (past the end: never read)
+    wait_vmcnt<6 * (NSLOT - 1)>();  // this group's 6 pieces landed (the newer groups' may be in flight)
+    GroupLoads cur;
+    read_group(slot, cur);
+    process(cur, g);
+    slot = slot == NSLOT - 1 ? 0 : slot + 1;
+  }
+  wait_vmcnt<0>();  // the ring aliases `red`: every wave's pieces land before anyone writes it
+  __syncthreads();
   // workgroup sums through LDS, one partial per workgroup (fragment layout: lane = 16q + col)
 #pragma unroll
   for (int tt = 0; tt < TG; ++tt)
