@@ -434,12 +434,23 @@ __global__ __launch_bounds__(512, 1) void cnn_bwd_kernel(
         const int wb = w0 + 4 * q + jj, s = t0 + tt + l15;
         xb[tt][jj] = (kx && wb < B && s < L) ? cur.xb[tt][jj] : kone;
       }
+    // dWc += dP^T X over BOTH steps in one double-rate 16x16x32 MFMA per block: the K slots of
+    // lane group q are (step 0, windows 4q .. 4q+3) then (step 1, the same windows) — exactly
+    // the dP values and X samples the lane holds after each step (7 MFMAs per group saved)
+    static_assert(TG == 2, "dWc pairs the workgroup's two steps into one K = 32 product");
+    unsigned dpk[TG][NFB][2], xbp[TG][2];
 #pragma unroll
     for (int tt = 0; tt < TG; ++tt) {
       const int t = t0 + tt;
-      if (t >= T) break;
+      if (t >= T) {  // (odd T: the pair's second step is absent; zeros contribute nothing)
+#pragma unroll
+        for (int b = 0; b < NFB; ++b) dpk[tt][b][0] = dpk[tt][b][1] = 0u;
+        xbp[tt][0] = xbp[tt][1] = 0u;
+        continue;
+      }
       const bf16x4 xA = ks.apply(pk_bf16(xa[tt], xa[tt + 1]), pk_bf16(xa[tt + 2], xa[tt + 3]));
-      const bf16x4 xB = frag(pk_bf16(xb[tt][0], xb[tt][1]), pk_bf16(xb[tt][2], xb[tt][3]));
+      xbp[tt][0] = pk_bf16(xb[tt][0], xb[tt][1]);
+      xbp[tt][1] = pk_bf16(xb[tt][2], xb[tt][3]);
       // dropout: the lane holds windows 4q + r of filter column 16b + l15, keep bit 2b + hb0 of
       // window r's hash word. The inverted words of windows (0, 1) and (2, 3) are packed so the
       // bit of block b sits at 2b (first window) and 2b + 16 (second): one shift per block puts
@@ -477,11 +488,16 @@ __global__ __launch_bounds__(512, 1) void cnn_bwd_kernel(
           asm("v_pk_min_u16 %0, %1, %2" : "=v"(one) : "v"(a[h]), "s"(0x00010001u));
           asm("v_pk_mul_lo_u16 %0, %1, %2\n\ts_nop 1" : "=v"(dp[h]) : "v"(d), "v"(one));
         }
-        // act^T and dP^T as A operands: A[f = l15][w = 4q + jj]
+        // act^T as the A operand: A[f = l15][w = 4q + jj]
         acc_wd[tt][b] = mfma16(frag(a[0], a[1]), doB, acc_wd[tt][b]);
-        acc_wc[b] = mfma16(frag(dp[0], dp[1]), xB, acc_wc[b]);
+        dpk[tt][b][0] = dp[0];
+        dpk[tt][b][1] = dp[1];
       }
     }
+#pragma unroll
+    for (int b = 0; b < NFB; ++b)
+      acc_wc[b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(frag8(dpk[0][b][0], dpk[0][b][1], dpk[1][b][0], dpk[1][b][1]),
+                                                          frag8(xbp[0][0], xbp[0][1], xbp[1][0], xbp[1][1]), acc_wc[b], 0, 0, 0);
   };
   const int gs = g_begin + wid;
   if (gs < g_end) {
