@@ -481,12 +481,13 @@ __global__ __launch_bounds__(512, 1) void cnn_bwd_kernel(
           if constexpr (DROP) v = drop_pk(v, pm[h], 2 * b);
           a[h] = relu_pk(v);
           // (inline asm: the compiler rewrote the min / multiply into 6 compares and selects).
-          // dp feeds an MFMA operand next, and hipcc pads nothing inside an asm string: the
-          // VALU-write -> MFMA-operand wait states are the s_nop 1 at its end (without it the
+          // dp becomes an MFMA operand, and hipcc pads nothing after an asm string: the
+          // VALU-write -> MFMA-operand wait states are the s_nop before the paired dWc MFMAs
+          // below (round 5 before the pairing: an s_nop 1 in every multiply; without any the
           // MFMA read stale dp on some blocks: NaN conv-weight gradients)
           unsigned one, d = pk_bf16(dA[2 * h], dA[2 * h + 1]);
           asm("v_pk_min_u16 %0, %1, %2" : "=v"(one) : "v"(a[h]), "s"(0x00010001u));
-          asm("v_pk_mul_lo_u16 %0, %1, %2\n\ts_nop 1" : "=v"(dp[h]) : "v"(d), "v"(one));
+          asm("v_pk_mul_lo_u16 %0, %1, %2" : "=v"(dp[h]) : "v"(d), "v"(one));
         }
         // act^T as the A operand: A[f = l15][w = 4q + jj]
         acc_wd[tt][b] = mfma16(frag(a[0], a[1]), doB, acc_wd[tt][b]);
@@ -494,6 +495,10 @@ __global__ __launch_bounds__(512, 1) void cnn_bwd_kernel(
         dpk[tt][b][1] = dp[1];
       }
     }
+    // every multiply above stays above (no scheduling across), then the wait states
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_nop 1");
+    __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int b = 0; b < NFB; ++b)
       acc_wc[b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(frag8(dpk[0][b][0], dpk[0][b][1], dpk[1][b][0], dpk[1][b][1]),
