@@ -567,12 +567,17 @@ __global__ __launch_bounds__(256) void cnn_reduce_kernel(
     const int b = f >> 4, lanep = ((f & 15) >> 2) * 16 + j, r = f & 3;
     const size_t stride = (size_t)T * NFB * 64 * 4;
     const float* p = part_wd + (((size_t)t * NFB + b) * 64 + lanep) * 4 + r;
-    float s4[4] = {0.f, 0.f, 0.f, 0.f};  // independent loads: one latency round per 4 chunks
-    int c = 0;
-    for (; c + 4 <= nch; c += 4)
+    // 16 independent loads per latency round (one round at the 14 chunks of 256 CUs; was one
+    // round per 4 chunks): past the end they re-load the last chunk and are dropped
+    float s4[4] = {0.f, 0.f, 0.f, 0.f};
+    for (int c = 0; c < nch; c += 16) {
+      float v[16];
 #pragma unroll
-      for (int k = 0; k < 4; ++k) s4[k] += p[(size_t)(c + k) * stride];
-    for (; c < nch; ++c) s4[0] += p[(size_t)c * stride];
+      for (int k = 0; k < 16; ++k) v[k] = p[(size_t)min(c + k, nch - 1) * stride];
+#pragma unroll
+      for (int k = 0; k < 16; ++k)
+        if (c + k < nch) s4[k & 3] += v[k];
+    }
     gWd[(size_t)j * nf + rest] += (s4[0] + s4[1]) + (s4[2] + s4[3]);
     return;
   }
@@ -585,12 +590,16 @@ __global__ __launch_bounds__(256) void cnn_reduce_kernel(
       const int b = f >> 4, lanep = ((f & 15) >> 2) * 16 + kk, r = f & 3;
       const float* p = part_wc + (((size_t)b * 64 + lanep) * 4 + r);
       const size_t stride = (size_t)NFB * 64 * 4;
+      // 16 independent loads per round, as above (one round at 252 workgroup partials)
       float s4[4] = {0.f, 0.f, 0.f, 0.f};
-      int c = grp;
-      for (; c + 48 < nwgb; c += 64)
+      for (int c = grp; c < nwgb; c += 256) {
+        float v[16];
 #pragma unroll
-        for (int k = 0; k < 4; ++k) s4[k] += p[(size_t)(c + 16 * k) * stride];
-      for (; c < nwgb; c += 16) s4[0] += p[(size_t)c * stride];
+        for (int k = 0; k < 16; ++k) v[k] = p[(size_t)min(c + 16 * k, nwgb - 1) * stride];
+#pragma unroll
+        for (int k = 0; k < 16; ++k)
+          if (c + 16 * k < nwgb) s4[k & 3] += v[k];
+      }
       s = (s4[0] + s4[1]) + (s4[2] + s4[3]);
     }
     sh[grp][threadIdx.x & 15] = s;
@@ -618,13 +627,20 @@ __global__ __launch_bounds__(256) void cnn_reduce_kernel(
     for (int k = 0; k < 17; ++k) pf[k][threadIdx.x] = v[k];
   }
   __syncthreads();
+  // 15 threads per column (255 of 256) sum every 15th entry, then 17 threads the 15 sums (the
+  // 17-thread pass over 256 entries each was a 64-deep chain of LDS reads)
+  __shared__ float pf2[17][16];
+  if (threadIdx.x < 255) {
+    const int k = threadIdx.x / 15, part = threadIdx.x % 15;
+    float sp = 0.f;
+    for (int c = part; c < 256; c += 15) sp += pf[k][c];
+    pf2[k][part] = sp;
+  }
+  __syncthreads();
   if (threadIdx.x < 17) {
-    float s4[4] = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll 8
-    for (int c = 0; c < 256; c += 4)
+    float s = 0.f;
 #pragma unroll
-      for (int k = 0; k < 4; ++k) s4[k] += pf[threadIdx.x][c + k];
-    const float s = (s4[0] + s4[1]) + (s4[2] + s4[3]);
+    for (int part = 0; part < 15; ++part) s += pf2[threadIdx.x][part];
     if (threadIdx.x < 16) {
       if (threadIdx.x < O) gbd[threadIdx.x] += s;
     } else if (loss_sum != nullptr) {
