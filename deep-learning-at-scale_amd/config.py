@@ -28,8 +28,8 @@ MODEL_DEFAULTS = {
     # batch_size 0 = auto (train/job.py auto_batch): on a GPU the rows that fill the device
     # (mlp: NativeMLP.full_batch, 262,144 on 256 CUs; lstm: one co-resident persistent grid,
     # NativeLSTM.full_grid_batch, 8192 at H = 512), capped at 1/8 of the rank's training rows,
-    # the same for --precision bf16 and fp32; 256 on the CPU. online_chunk 0 = auto: 32
-    # mini-batches per rank per stream chunk.
+    # the same for --precision bf16 and fp32; 256 on the CPU. online_chunk 0 = auto: sized in
+    # rows (train/job.py auto_online_chunk: up to 2M rows per rank, >= 4 chunks per pass).
     # The LSTM defaults to auto (its val-MSE parity at the auto batch: profiles/r3/
     # parity_lstm_paired_10seeds.json). The MLPs keep the small-batch regime (256) as their job
     # default: the fill-the-GPU batch leaves ~8 Adam steps per epoch on a 2M-row table and its

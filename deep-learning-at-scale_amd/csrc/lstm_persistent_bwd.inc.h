@@ -149,9 +149,17 @@ __global__ __launch_bounds__(256, 1) void lstm_bwd_persistent_kernel(
   // completion guard (persistent_guard.h) and this launch's epoch (persistent_sync.h)
   if (threadIdx.x == 0) {
     const unsigned ord = pguard_start(stat, (unsigned)(d.T - 1));
+    // a buffer last used by a launch of another (NRT, T, NB) fails loudly (persistent_sync.h)
+    const unsigned sig = psync_sig(1u, (unsigned)NRT, (unsigned)d.T, (unsigned)NB);
+    const unsigned bad = psync_check_sig(sync, sig);
+    if (bad) {
+      pguard_exit(stat, 0u, 5u, bad, 0u, sig, 0u, ord);
+      pguard_sticky(stat);
+    }
     const unsigned e = __hip_atomic_fetch_add(rbw + kPSyncStart, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) / NB;
     asm volatile("ds_write_b64 %0, %1" ::"v"(lds0 + BCAST), "v"((unsigned long long)e | ((unsigned long long)ord << 32))
                  : "memory");
+    asm volatile("ds_write_b32 %0, %1" ::"v"(lds0 + BCAST + 8), "v"(bad) : "memory");
   }
   // ---- prologue: stationary W_hh^T fragments (B operand: lane = unit col l15, k 8g..8g+7)
   bf16x8 w[KT][4];
@@ -172,7 +180,11 @@ __global__ __launch_bounds__(256, 1) void lstm_bwd_persistent_kernel(
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();
   unsigned long long eo;
-  asm volatile("ds_read_b64 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(eo) : "v"(lds0 + BCAST) : "memory");
+  unsigned sigbad;
+  asm volatile("ds_read_b64 %0, %2\n\tds_read_b32 %1, %3\n\ts_waitcnt lgkmcnt(0)"
+               : "=&v"(eo), "=&v"(sigbad)
+               : "v"(lds0 + BCAST), "v"(lds0 + BCAST + 8)
+               : "memory");
   const unsigned epoch = __builtin_amdgcn_readfirstlane((unsigned)eo);
   const unsigned ord = __builtin_amdgcn_readfirstlane((unsigned)(eo >> 32));
   const unsigned tag = epoch + 1u;
@@ -186,7 +198,8 @@ __global__ __launch_bounds__(256, 1) void lstm_bwd_persistent_kernel(
   // arrivals group gg must show before step sg reads it: all NB workgroups published it for
   // steps 0 .. sg-1
   auto target = [&](int gg, int sg) { return group_base(gg) + (unsigned)(NB * sg) + force; };
-  unsigned failed = 0;  // uniform: this wave failed a hand-off (runs on, never waits again)
+  // uniform: this wave failed a hand-off or the signature check (runs on, never waits again)
+  unsigned failed = __builtin_amdgcn_readfirstlane(sigbad) != 0u ? 1u : 0u;
 
   // ---- per-lane constant offsets
   // A (DG_{t+1}) staging: one LDS-DMA instruction = 8 rows x 128 B (full lines) of the wave's

@@ -93,7 +93,7 @@ __global__ __launch_bounds__(256, 1) void lstm_fwd_persistent_kernel(
   // accumulator registers (this chunk + the pipelined previous one) = 12 k-tiles x 4 x 4
   // KT = 20 (KX = 128, H = 512): 14 k-tiles in AGPRs (224 + the 32 accumulators = 256), so
   // the VGPR-resident weights stay at 6 k-tiles as at KT = 18
-  constexpr int KTA = KT < 12 ? KT : (KT >= 20 ? 14 : 12);
+  constexpr int KTA_ = KT < 12 ? KT : (KT >= 20 ? 14 : 12);
   constexpr int NSTORE = (DBG & 4) ? 1 : 7;  // stores per wave per chunk: 2 C, 4 S, 1 h
   // one asm statement per MFMA + cell-math micro-stage (H = 512; WELLFLOW_PF_DBG=512: pinned
   // C++ micro-stages instead, for A/B)
@@ -103,15 +103,30 @@ __global__ __launch_bounds__(256, 1) void lstm_fwd_persistent_kernel(
   // chunks 1 and 2 from its MFMA loop (WELLFLOW_PF_DBG=1024: both at the step top, A/B)
   constexpr bool PF01 = NC >= 3 && (DBG & (2 | 1024)) == 0;
   // SPLIT-PHASE hand-off (round 5, NC = 8: the rows of ONE chunk depend only on the same
-  // chunk of the previous step, whose h every workgroup of the row block publishes two chunks
-  // after finishing it): one arrival counter per chunk, the chunk pieces two chunks ahead
+  // chunk of the previous step, whose h every workgroup of the row block publishes three
+  // chunks after finishing it — round 6, was two: the publishing wait no longer covers the h
+  // store just issued): one arrival counter per chunk, the chunk pieces two chunks ahead
   // across the step boundary (chunks 0 / 1 of step t+1 during chunks NC-2 / NC-1 of step t),
   // the last chunk's cell epilogue in the next step's first MFMA loop like any other, and a
-  // per-wave sc1 poll two chunks before each fetch — no step-top stop. A 4-slot ring (slot =
+  // per-wave sc1 poll one chunk before each fetch — no step-top stop. A 4-slot ring (slot =
   // chunk % 4 in every step). Smaller NC keep the per-step hand-off: a chunk's own next-step
   // input would be published too late to fetch ahead (NC < 8), or at all (NC = 1).
   constexpr bool SPLIT = NC == 8 && 4 * ABYTES + PF_ROWS * 64 * 2 + 32 <= 163840;  // KX = 128: 3 slots only
   constexpr int NSLOT = SPLIT ? 4 : 3;
+  // ALT (round 6; the H = 512 split-phase production path): the accumulators live in VGPRs as
+  // TWO sets that alternate between chunk bodies (body P accumulates into set P & 1 while its
+  // fused cell stages read the previous chunk's set directly), so no chunk copies its 32
+  // accumulators out (32 v_accvgpr_read per chunk before) and no AGPR holds an accumulator:
+  // 14 k-tiles of weights fit the AGPR file (VGPR weights 4 k-tiles, as many registers as before)
+  constexpr bool ALT = FUSED && SPLIT && (DBG & 2048) == 0;  // DBG 2048 (A/B): AGPR accumulators + copy
+  // SPLIT publish delay (round 6): chunk j publishes chunk j - PD, polled one chunk before its
+  // fetch; DBG 262144 (A/B): the round-5 form, PD = 2 with the poll two chunks before
+  constexpr bool PUB3 = (DBG & 262144) == 0;
+  constexpr int PD = PUB3 ? 3 : 2, PL = PUB3 ? 1 : 2;
+  // DBG 256 (A/B, measured slower): each wave publishes its own 32-B piece of every h row
+  // (no staging barrier); the production form writes whole 128-B lines, one per 8 lanes
+  constexpr bool WAVE_H = (DBG & 256) != 0;
+  constexpr int KTA = ALT ? 14 : KTA_;
   // Distinct static LDS objects per ring slot: the compiler then proves the slot being
   // filled by LDS-DMA disjoint from the slots being read, and inserts no vmcnt(0) of its own.
   // EXACTLY ONE static LDS variable, compile-time offsets for every ring slot, the h staging
@@ -147,6 +162,10 @@ __global__ __launch_bounds__(256, 1) void lstm_fwd_persistent_kernel(
   constexpr int SHALF = (DBG & 32768) ? 8 : kFnSHalf;
   const int loff_s = ub * 1024 + lane * ((DBG & 32768) ? 16 : 8);
   const int loff_h = (((int)threadIdx.x >> 3) * KA + ((int)threadIdx.x & 7) * 8) * 2;  // h publish
+  // SPLIT: each wave publishes its OWN 16 units of the chunk's 32 rows (row lane >> 1, 8-unit
+  // half lane & 1: 32 B per row per wave), so its LDS staging needs no workgroup barrier
+  const int loff_hw = ((lane >> 1) * KA + wid * 16 + 8 * (lane & 1)) * 2;
+  const unsigned hb_rd = hb_lds + (unsigned)((lane >> 1) * 128 + wid * 32 + (lane & 1) * 16);
   // error word: word 0 of the per-launch block (word 1 in the round-2 layout A/B, PF_DBG bit 20)
   // production objects keep only the test hook bit (kDbgMask, persistent_guard.h): the
   // timing-only branches below fold away at compile time
@@ -169,9 +188,17 @@ __global__ __launch_bounds__(256, 1) void lstm_fwd_persistent_kernel(
   // completion guard (persistent_guard.h) and this launch's epoch (persistent_sync.h)
   if (threadIdx.x == 0) {
     const unsigned o = pguard_start(stat, (unsigned)d.T);
+    // a buffer last used by a launch of another (NC, T, NB) fails loudly (persistent_sync.h)
+    const unsigned sig = psync_sig(0u, (unsigned)NC, (unsigned)d.T, (unsigned)NB);
+    const unsigned bad = psync_check_sig(sync, sig);
+    if (bad) {
+      pguard_exit(stat, 0u, 5u, bad, 0u, sig, 0u, o);
+      pguard_sticky(stat);
+    }
     const unsigned e = __hip_atomic_fetch_add(rbw + kPSyncStart, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) / NB;
     asm volatile("ds_write_b64 %0, %1" ::"v"(flag_lds + 8), "v"((unsigned long long)e | ((unsigned long long)o << 32))
                  : "memory");
+    asm volatile("ds_write_b32 %0, %1" ::"v"(flag_lds), "v"(bad) : "memory");
   }
   // ---- prologue: stationary weight fragments (B operand: lane holds col l15, k 8g..8g+7)
   bf16x8 w[KT][4];
@@ -189,19 +216,24 @@ __global__ __launch_bounds__(256, 1) void lstm_fwd_persistent_kernel(
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();
   unsigned long long eo;
-  asm volatile("ds_read_b64 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(eo) : "v"(flag_lds + 8) : "memory");
+  unsigned sigbad;
+  asm volatile("ds_read_b64 %0, %2\n\tds_read_b32 %1, %3\n\ts_waitcnt lgkmcnt(0)"
+               : "=&v"(eo), "=&v"(sigbad)
+               : "v"(flag_lds + 8), "v"(flag_lds)
+               : "memory");
   const unsigned epoch = __builtin_amdgcn_readfirstlane((unsigned)eo);
   const unsigned ord = __builtin_amdgcn_readfirstlane((unsigned)(eo >> 32));
   const unsigned tag = epoch + 1u;
   // arrivals a consumer needs before step tt reads chunk cc (SPLIT) / before step tt (per-step
   // hand-off): every workgroup of the row block published it for steps 0 .. tt-1. SPLIT
-  // publishes chunk cc at the top of chunk cc + 2: in every step for cc <= NC-3, in all but the
-  // last step for the last two chunks; the per-step hand-off counts steps 1 .. T-1.
+  // publishes chunk cc at the top of chunk cc + 3: in every step for cc <= NC-4, in all but the
+  // last step for the last three chunks; the per-step hand-off counts steps 1 .. T-1.
   auto target = [&](int cc, int tt) -> unsigned {
-    const unsigned per_launch = SPLIT ? (unsigned)(cc <= NC - 3 ? d.T : d.T - 1) : (unsigned)(d.T - 1);
+    const unsigned per_launch = SPLIT ? (unsigned)(cc <= NC - 1 - PD ? d.T : d.T - 1) : (unsigned)(d.T - 1);
     return epoch * (unsigned)NB * per_launch + (unsigned)(NB * (SPLIT ? tt : tt)) + force;
   };
-  unsigned failed = 0;  // uniform: this wave failed a hand-off (runs on, never waits again)
+  // uniform: this wave failed a hand-off or the signature check (runs on, never waits again)
+  unsigned failed = __builtin_amdgcn_readfirstlane(sigbad) != 0u ? 1u : 0u;
   // SPLIT: blocking wait of this wave for chunk cc before step tt reads it (a poll that did
   // not match); a failure is recorded once and makes every later wait a no-op
   auto wait_chunk = [&](int cc, int tt) {
@@ -222,7 +254,7 @@ __global__ __launch_bounds__(256, 1) void lstm_fwd_persistent_kernel(
     asm volatile("global_load_dword %0, %1, off sc1" : "=v"(v) : "v"(pa) : "memory");
     return v;
   };
-  unsigned pvr[2] = {0u, 0u};  // SPLIT: polls in flight (chunk j polls for chunk j + 4)
+  unsigned pvr[2] = {0u, 0u};  // SPLIT: the polls in flight (chunk j polls for chunk j + 2 + PL)
   // per-step store bases of the previous step (SPLIT: chunk 0 finalizes the previous step's
   // last chunk)
   bf16_t* cnext_p = nullptr;
@@ -246,7 +278,14 @@ __global__ __launch_bounds__(256, 1) void lstm_fwd_persistent_kernel(
 #pragma unroll
     for (int i = 0; i < 2; ++i) cq[q][i] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  f32x4 accp[2][4];  // gate pre-activations of the previous chunk (software pipeline)
+  f32x4 accp[2][4];  // gate pre-activations of the previous chunk (software pipeline; !ALT)
+  f32x4 accs[2][2][4];  // ALT: the two alternating accumulator sets
+#pragma unroll
+  for (int q = 0; q < 2; ++q)
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) accs[q][i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int i = 0; i < 2; ++i)
 #pragma unroll
@@ -307,16 +346,23 @@ __global__ __launch_bounds__(256, 1) void lstm_fwd_persistent_kernel(
     const int hsoff = (int)(((size_t)rb * KA + KXC + n * 64) * 2);
 
     // cell epilogue element (row-tile i, row r) of the carried chunk: accp + c_{t-1} = cq[0]
-    auto epi_elem = [&](int i, int r, float (&cv)[2][4], unsigned (&pk)[2][8], unsigned (&hv)[2][4]) {
-      const float ig = sigmoid_pre(accp[i][0][r]);  // Wp carries the gate scales (pack kernel)
-      const float fg = sigmoid_pre(accp[i][1][r]);
-      const float gg = tanh_pre(accp[i][2][r]);
-      const float og = sigmoid_pre(accp[i][3][r]);
+    auto epi_elem_src = [&](const f32x4 (&src)[2][4], int i, int r, float (&cv)[2][4], unsigned (&pk)[2][8],
+                            unsigned (&hv)[2][4]) {
+      const float ig = sigmoid_pre(src[i][0][r]);  // Wp carries the gate scales (pack kernel)
+      const float fg = sigmoid_pre(src[i][1][r]);
+      const float gg = tanh_pre(src[i][2][r]);
+      const float og = sigmoid_pre(src[i][3][r]);
       const float cn = fg * cq[0][i][r] + ig * gg;
       cv[i][r] = cn;
       pk[i][2 * r] = pk_bf16(ig, fg);
       pk[i][2 * r + 1] = pk_bf16(gg, og);
       hv[i][r] = f2bf(og * tanhf_(cn));
+    };
+    auto epi_elem = [&](int i, int r, float (&cv)[2][4], unsigned (&pk)[2][8], unsigned (&hv)[2][4]) {
+      if constexpr (ALT)
+        epi_elem_src(accs[(NC - 1) & 1], i, r, cv, pk, hv);  // the drain: the last chunk's set
+      else
+        epi_elem_src(accp, i, r, cv, pk, hv);
     };
     // The same element in two halves pinned to k-tile positions of the next chunk's MFMA
     // loop. Empty asm statements take the inputs and produce the outputs at that point:
@@ -494,12 +540,22 @@ __global__ __launch_bounds__(256, 1) void lstm_fwd_persistent_kernel(
           asm volatile("ds_write_b16 %0, %1" ::"v"(hb_lds + 2u * ((i * 16 + 4 * g + r) * 64 + wid * 16 + l15)),
                        "v"(hv[i][r])
                        : "memory");
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();
-      asm volatile("" ::: "memory");
-      u32x4 vv;  // row threadIdx>>3, 16-B column threadIdx&7 of the [32][64] bf16 tile
-      asm volatile("ds_read_b128 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=&v"(vv) : "v"(hb_lds + 16u * threadIdx.x) : "memory");
-      __builtin_amdgcn_raw_buffer_store_b128(vv, xrs, loff_h, hsoff + e * PF_ROWS * KA * 2, 16 /* sc1 */);
+      u32x4 vv;
+      if constexpr (WAVE_H) {
+        // the wave's own [32 rows][16 units] block back as 16-B pieces (LDS executes one wave's
+        // accesses in order: no barrier). Measured +0.4 ms per forward: every 128-B h line is
+        // then four 32-B write-through pieces from four waves instead of one whole-line store
+        asm volatile("ds_read_b128 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=&v"(vv) : "v"(hb_rd) : "memory");
+        __builtin_amdgcn_raw_buffer_store_b128(vv, xrs, loff_hw, hsoff + e * PF_ROWS * KA * 2, 16 /* sc1 */);
+      } else {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        // row threadIdx>>3, 16-B column threadIdx&7 of the [32][64] bf16 tile: whole 128-B lines
+        asm volatile("ds_read_b128 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=&v"(vv) : "v"(hb_lds + 16u * threadIdx.x)
+                     : "memory");
+        __builtin_amdgcn_raw_buffer_store_b128(vv, xrs, loff_h, hsoff + e * PF_ROWS * KA * 2, 16 /* sc1 */);
+      }
       if constexpr (!(DBG & 4)) {
 #pragma unroll
         for (int i = 0; i < 2; ++i) {
@@ -525,6 +581,16 @@ __global__ __launch_bounds__(256, 1) void lstm_fwd_persistent_kernel(
     };
     // SPLIT: chunk c of the step whose A base is `base` into ring slot SL
     auto issue_b = [&](const char* base, int c, auto sc) {
+      constexpr int SL = decltype(sc)::value;
+      if constexpr ((DBG & 131072) != 0) return;  // timing only: no LDS-DMA after step 0 (stale A)
+      char* ra = smem + SL * SLOT;
+      const char* src = base + (size_t)c * ABYTES;
+#pragma unroll
+      for (int s = 0; s < KS; ++s)
+        __builtin_amdgcn_global_load_lds((const void*)(src + s * 128), (lds_void*)(ra + s * 4096 + wid * 1024),
+                                         16, 0, 16 /* sc1 */);
+    };
+    auto issue_b0 = [&](const char* base, int c, auto sc) {  // step 0's first two chunks (every build)
       constexpr int SL = decltype(sc)::value;
       char* ra = smem + SL * SLOT;
       const char* src = base + (size_t)c * ABYTES;
@@ -556,14 +622,16 @@ __global__ __launch_bounds__(256, 1) void lstm_fwd_persistent_kernel(
       // vector-memory ops issued after chunk c's LDS-DMA (top of c issues c+2, then stores)
       // (issue order: prologue glds 0, 1; chunk k: glds k+2, then the stores of chunk k-1,
       // NSTORE per wave, none in chunk 0)
-      // SPLIT: chunk j (global) waits until only chunk j-2's C / S stores are in flight: its
-      // own pieces, chunk j+1's, chunk j-2's h store (published below) and the poll issued
-      // at the top of chunk j-2 (its register is an operand: no use moves above the wait)
+      // SPLIT: chunk j (global) waits until only chunk j-1's h and C / S stores are in flight:
+      // its own pieces, chunk j+1's, the poll issued at the top of chunk j-1 (its register is
+      // an operand: no use moves above the wait) and chunk j-3's h store (published below).
+      // Round 6: the h store of chunk j-2, issued just before this wait, no longer has to land
+      // first (it is published one chunk later), so no chunk top waits out a write-through.
       if constexpr (SPLIT) {
         if (t == 0 && c < 2)
           wait_vmcnt<LPT>();
         else
-          asm volatile("s_waitcnt vmcnt(%1)" : "+v"(pvr[P & 1]) : "n"(NSTORE - 1) : "memory");
+          asm volatile("s_waitcnt vmcnt(%1)" : "+v"(pvr[P % PL]) : "n"(NSTORE - 1 + (PUB3 ? 1 : 0)) : "memory");
       } else if (c == 0) {
         if (NC > 1 && !FIRST) wait_vmcnt<LPT>(); else wait_vmcnt<0>();
       } else if (c == 1) {
@@ -580,21 +648,22 @@ __global__ __launch_bounds__(256, 1) void lstm_fwd_persistent_kernel(
       __builtin_amdgcn_sched_barrier(0);  // keep each chunk's code (and live ranges) to itself
       stamp(t, 3 + 5 * c);
       if constexpr (SPLIT) {
-        // publish chunk j-2: every wave drained its h store before the barrier above
-        if ((t > 0 || c >= 2) && threadIdx.x == 0)
-          __hip_atomic_fetch_add(rbw + kPSyncGroup + (c >= 2 ? c - 2 : c + NC - 2), 1u, __ATOMIC_RELAXED,
+        // publish chunk j-PD: every wave drained its h store before the barrier above
+        if ((t > 0 || c >= PD) && threadIdx.x == 0)
+          __hip_atomic_fetch_add(rbw + kPSyncGroup + (c >= PD ? c - PD : c + NC - PD), 1u, __ATOMIC_RELAXED,
                                  __HIP_MEMORY_SCOPE_AGENT);
-        // chunk j+2: its h rows were published by the row block at least 4 chunks ago; the
-        // poll of two chunks ago says whether all arrived, else wait here (bounded)
+        // chunk j+2: its h rows were published by the row block 3 chunks ago; the poll of one
+        // chunk ago says whether all arrived, else wait here (bounded)
         const int c2 = c + 2 < NC ? c + 2 : c + 2 - NC, t2 = c + 2 < NC ? t : t + 1;
         if (t2 < d.T) {
-          if (t2 >= 1 && !failed && !psync_reached(__builtin_amdgcn_readfirstlane(pvr[P & 1]), target(c2, t2)))
+          if (t2 >= 1 && !failed && !psync_reached(__builtin_amdgcn_readfirstlane(pvr[P % PL]), target(c2, t2)))
             wait_chunk(c2, t2);
-          issue_b(t2 == t ? abase : abase_n, c2, std::integral_constant<int, (P + 2) % NSLOT>{});
+          if (t2 > 0 || (DBG & 131072) == 0)
+            issue_b(t2 == t ? abase : abase_n, c2, std::integral_constant<int, (P + 2) % NSLOT>{});
         }
-        // poll for chunk j+4 (read at the top of chunk j+2)
-        const int c4 = c + 4 < NC ? c + 4 : c + 4 - NC, t4 = c + 4 < NC ? t : t + 1;
-        if (t4 >= 1 && t4 < d.T) pvr[P & 1] = poll(c4);
+        // poll for chunk j+2+PL (read at the top of chunk j+PL)
+        const int c3 = c + 2 + PL < NC ? c + 2 + PL : c + 2 + PL - NC, t3 = c + 2 + PL < NC ? t : t + 1;
+        if (t3 >= 1 && t3 < d.T) pvr[P % PL] = poll(c3);
       } else if constexpr (!FIRST) {
         if (c + 2 < NC) issue(c + 2, std::integral_constant<int, (P + 2) % 3>{});
       }
@@ -608,7 +677,14 @@ __global__ __launch_bounds__(256, 1) void lstm_fwd_persistent_kernel(
       const unsigned ab[2] = {lds_smem + (unsigned)(P * SLOT) + (unsigned)fa[0],
                               lds_smem + (unsigned)(P * SLOT) + (unsigned)fa[1]};
 
-      f32x4 acc[2][4];  // written first by k-tile 0's MFMAs (src C = 0: no zeroing writes)
+      f32x4 acc_l[2][4];  // written first by k-tile 0's MFMAs (src C = 0: no zeroing writes)
+      // ALT: this body's set and the previous chunk's (read by the fused stages)
+      f32x4(&acc)[2][4] = [&]() -> f32x4(&)[2][4] {
+        if constexpr (ALT) return accs[P & 1]; else return acc_l;
+      }();
+      f32x4(&accq)[2][4] = [&]() -> f32x4(&)[2][4] {
+        if constexpr (ALT) return accs[(P & 1) ^ 1]; else return accp;
+      }();
       // MFMAs in inline asm with explicit register classes: weights of k-tiles < KTA as AGPR
       // operands, the rest as VGPR operands, accumulators in AGPRs. With the builtin the
       // register allocator shuffled the 288 weight registers through v_accvgpr_read/mov copies
@@ -637,7 +713,13 @@ __global__ __launch_bounds__(256, 1) void lstm_fwd_persistent_kernel(
         const bf16x8& A = a[kt & 1][i];
         if constexpr (m >= 144 || (DBG & 8192) != 0) {  // KT > 18: the 144 stages are placed, the rest are
                                                         // plain MFMAs (DBG 8192: timing only, no stages)
-          if constexpr (kt < KTA)
+          if constexpr (ALT && kt == 0)
+            asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, 0" : "=&v"(acc[i][j]) : "v"(A), "a"(w[kt][j]));
+          else if constexpr (ALT && kt < KTA)
+            asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+v"(acc[i][j]) : "v"(A), "a"(w[kt][j]));
+          else if constexpr (ALT)
+            asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+v"(acc[i][j]) : "v"(A), "v"(w[kt][j]));
+          else if constexpr (kt < KTA)
             asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc[i][j]) : "v"(A), "a"(w[kt][j]));
           else
             asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc[i][j]) : "v"(A), "v"(w[kt][j]));
@@ -645,7 +727,16 @@ __global__ __launch_bounds__(256, 1) void lstm_fwd_persistent_kernel(
         }
 #define WF_UNP(...) __VA_ARGS__
 #define WF_MF(TXT, OUTS, INS)                                                                          \
-  if constexpr (kt == 0)                                                                               \
+  if constexpr (ALT && kt == 0)                                                                        \
+    asm volatile("v_mfma_f32_16x16x32_bf16 %[c], %[a], %[b], 0\n\t" TXT                                \
+                 : [c] "=&v"(acc[i][j]), WF_UNP OUTS : [a] "v"(A), [b] "a"(w[kt][j]) WF_UNP INS);    \
+  else if constexpr (ALT && kt < KTA)                                                                  \
+    asm volatile("v_mfma_f32_16x16x32_bf16 %[c], %[a], %[b], %[c]\n\t" TXT                             \
+                 : [c] "+v"(acc[i][j]), WF_UNP OUTS : [a] "v"(A), [b] "a"(w[kt][j]) WF_UNP INS);     \
+  else if constexpr (ALT)                                                                              \
+    asm volatile("v_mfma_f32_16x16x32_bf16 %[c], %[a], %[b], %[c]\n\t" TXT                             \
+                 : [c] "+v"(acc[i][j]), WF_UNP OUTS : [a] "v"(A), [b] "v"(w[kt][j]) WF_UNP INS);     \
+  else if constexpr (kt == 0)                                                                          \
     asm volatile("v_mfma_f32_16x16x32_bf16 %[c], %[a], %[b], 0\n\t" TXT                                \
                  : [c] "=&a"(acc[i][j]), WF_UNP OUTS : [a] "v"(A), [b] "a"(w[kt][j]) WF_UNP INS);    \
   else if constexpr (kt < KTA)                                                                         \
@@ -655,13 +746,13 @@ __global__ __launch_bounds__(256, 1) void lstm_fwd_persistent_kernel(
     asm volatile("v_mfma_f32_16x16x32_bf16 %[c], %[a], %[b], %[c]\n\t" TXT                             \
                  : [c] "+a"(acc[i][j]), WF_UNP OUTS : [a] "v"(A), [b] "v"(w[kt][j]) WF_UNP INS);
         if constexpr (st == 0) {
-          WF_MF("v_exp_f32 %[o], %[x]", ([o] "=&v"(E.ei)), (, [x] "v"(accp[ei_][0][er])))
+          WF_MF("v_exp_f32 %[o], %[x]", ([o] "=&v"(E.ei)), (, [x] "v"(accq[ei_][0][er])))
         } else if constexpr (st == 1) {
-          WF_MF("v_exp_f32 %[o], %[x]", ([o] "=&v"(E.ef)), (, [x] "v"(accp[ei_][1][er])))
+          WF_MF("v_exp_f32 %[o], %[x]", ([o] "=&v"(E.ef)), (, [x] "v"(accq[ei_][1][er])))
         } else if constexpr (st == 2) {
-          WF_MF("v_exp_f32 %[o], %[x]", ([o] "=&v"(E.eg)), (, [x] "v"(accp[ei_][2][er])))
+          WF_MF("v_exp_f32 %[o], %[x]", ([o] "=&v"(E.eg)), (, [x] "v"(accq[ei_][2][er])))
         } else if constexpr (st == 3) {
-          WF_MF("v_exp_f32 %[o], %[x]", ([o] "=&v"(E.eo)), (, [x] "v"(accp[ei_][3][er])))
+          WF_MF("v_exp_f32 %[o], %[x]", ([o] "=&v"(E.eo)), (, [x] "v"(accq[ei_][3][er])))
         } else if constexpr (st == 4) {
           WF_MF("v_add_f32 %[p], 1.0, %[p]\n\tv_add_f32 %[q], 1.0, %[q]", ([p] "+v"(E.ei), [q] "+v"(E.ef)), ())
         } else if constexpr (st == 5) {
@@ -803,11 +894,18 @@ __global__ __launch_bounds__(256, 1) void lstm_fwd_persistent_kernel(
       // padding, so no read of them (the accp copy, or the drain's cell math at NC = 1) can
       // be scheduled above it: the compiler sees an inline-asm MFMA's result as ready at
       // once and had put v_accvgpr_reads 2 instructions behind the last MFMAs (tools/mfma_war.py).
-      asm volatile("s_nop 7\n\ts_nop 7"
-                   : "+a"(acc[0][0]), "+a"(acc[0][1]), "+a"(acc[0][2]), "+a"(acc[0][3]), "+a"(acc[1][0]),
-                     "+a"(acc[1][1]), "+a"(acc[1][2]), "+a"(acc[1][3])
-                   :
-                   : "memory");
+      if constexpr (ALT)  // the set's next reader is the next body's first stage: one pad is plenty
+        asm volatile("s_nop 7"
+                     : "+v"(acc[0][0]), "+v"(acc[0][1]), "+v"(acc[0][2]), "+v"(acc[0][3]), "+v"(acc[1][0]),
+                       "+v"(acc[1][1]), "+v"(acc[1][2]), "+v"(acc[1][3])
+                     :
+                     : "memory");
+      else
+        asm volatile("s_nop 7\n\ts_nop 7"
+                     : "+a"(acc[0][0]), "+a"(acc[0][1]), "+a"(acc[0][2]), "+a"(acc[0][3]), "+a"(acc[1][0]),
+                       "+a"(acc[1][1]), "+a"(acc[1][2]), "+a"(acc[1][3])
+                     :
+                     : "memory");
       if constexpr ((DBG & 16) != 0) {  // MFMA completion: consume a result before stamping
         float sink = acc[1][3][3];
         asm volatile("" ::"v"(sink));
@@ -827,10 +925,12 @@ __global__ __launch_bounds__(256, 1) void lstm_fwd_persistent_kernel(
         stamp(t, 5 + 5 * c);
         publish(c - 1);
       }
+      if constexpr (!ALT) {
 #pragma unroll
-      for (int i = 0; i < 2; ++i)
+        for (int i = 0; i < 2; ++i)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) accp[i][j] = acc[i][j];
+          for (int j = 0; j < 4; ++j) accp[i][j] = acc[i][j];
+      }
       stamp(t, 6 + 5 * c);
     };
     using S0 = std::integral_constant<int, 0>;
@@ -840,8 +940,8 @@ __global__ __launch_bounds__(256, 1) void lstm_fwd_persistent_kernel(
     using NF = std::false_type;
     if constexpr (SPLIT) {
       if (t == 0) {  // chunks 0 and 1 of step 0 (XH[0] = [x_0 | 1 | h_-1 = 0] is written before the launch)
-        issue_b(abase, 0, S0{});
-        issue_b(abase, 1, S1{});
+        issue_b0(abase, 0, S0{});
+        issue_b0(abase, 1, S1{});
       }
       for (int c = 0; c < NC; c += 4) {
         chunk(c, S0{}, NF{});
@@ -934,6 +1034,15 @@ static int launch_pf(bf16_t* XH, const bf16_t* Wp, bf16_t* Cst, bf16_t* S, unsig
     if constexpr (WF_DV(8192)) { if (d.dbg == 8192) f = reinterpret_cast<const void*>(&lstm_fwd_persistent_kernel<KT, NC, 8192>); }  // no cell math in the loop
     if constexpr (WF_DV(16384)) { if (d.dbg == 16384) f = reinterpret_cast<const void*>(&lstm_fwd_persistent_kernel<KT, NC, 16384>); }  // no stores / publish
     if constexpr (WF_DV(24576)) { if (d.dbg == 24576) f = reinterpret_cast<const void*>(&lstm_fwd_persistent_kernel<KT, NC, 24576>); }  // neither
+    if constexpr (WF_DV(256)) { if (d.dbg == 256) f = reinterpret_cast<const void*>(&lstm_fwd_persistent_kernel<KT, NC, 256>); }  // per-wave h pieces
+    if constexpr (WF_DV(2048)) { if (d.dbg == 2048) f = reinterpret_cast<const void*>(&lstm_fwd_persistent_kernel<KT, NC, 2048>); }  // AGPR accumulators
+    if constexpr (WF_DV(262144)) { if (d.dbg == 262144) f = reinterpret_cast<const void*>(&lstm_fwd_persistent_kernel<KT, NC, 262144>); }  // round-5 publish delay
+    if constexpr (WF_DV(264192)) { if (d.dbg == 264192) f = reinterpret_cast<const void*>(&lstm_fwd_persistent_kernel<KT, NC, 264192>); }  // the round-5 kernel
+    if constexpr (WF_DV(32)) { if (d.dbg == 32) f = reinterpret_cast<const void*>(&lstm_fwd_persistent_kernel<KT, NC, 32>); }  // no fragment reads
+    if constexpr (WF_DV(8224)) { if (d.dbg == 8224) f = reinterpret_cast<const void*>(&lstm_fwd_persistent_kernel<KT, NC, 8224>); }  // neither cell math nor fragment reads
+    if constexpr (WF_DV(131072)) { if (d.dbg == 131072) f = reinterpret_cast<const void*>(&lstm_fwd_persistent_kernel<KT, NC, 131072>); }  // no LDS-DMA
+    if constexpr (WF_DV(139296)) { if (d.dbg == 139296) f = reinterpret_cast<const void*>(&lstm_fwd_persistent_kernel<KT, NC, 139296>); }  // bare MFMAs + hand-off + stores
+    if constexpr (WF_DV(139300)) { if (d.dbg == 139300) f = reinterpret_cast<const void*>(&lstm_fwd_persistent_kernel<KT, NC, 139300>); }  // bare MFMAs + hand-off, no C/S stores
     if constexpr (WF_DV(32768)) { if (d.dbg == 32768) f = reinterpret_cast<const void*>(&lstm_fwd_persistent_kernel<KT, NC, 32768>); }  // round-2 S slots
   }
   // a requested variant that this build did not compile must not time the production kernel

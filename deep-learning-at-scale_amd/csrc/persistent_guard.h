@@ -20,7 +20,8 @@
 //       workgroup (STARTED before its own add: ordinal / grid = launch index since the reset)
 //   reasons: 1 the launch's error word was set while polling (another workgroup's spin bound);
 //            2 this workgroup's own spin bound; 3 wave 0 read a flag != 1 from LDS although its
-//            own poll succeeded; 4 another wave read a flag != 1 (LDS hand-off flag)
+//            own poll succeeded; 4 another wave read a flag != 1 (LDS hand-off flag); 5 the
+//            sync buffer's launch signature (persistent_sync.h) differs from this launch's
 // Host side: NativeLSTM.persistent_error / check_device_errors (models/lstm.py). All adds are
 // relaxed agent-scope atomics (one lane per workgroup; MI355X_MICROARCH.md fanin: ~11-13 ns each).
 #pragma once

@@ -26,7 +26,7 @@
 
 namespace wf {
 
-constexpr int kPSyncHead = 16;      // words before the first row block
+constexpr int kPSyncHead = 16;      // words before the first row block (word 0: launch signature)
 constexpr int kPSyncRowBlock = 16;  // words per row block
 constexpr int kPSyncStart = 0, kPSyncGroup = 1, kPSyncErr = 12;
 constexpr int kPSyncMaxGroups = 8;
@@ -39,6 +39,24 @@ __device__ __forceinline__ ps_u32* psync_rb(unsigned* sync, int m) {
 
 // (counter - target) as a signed distance: the counters may wrap after ~2^31 publishes
 __device__ __forceinline__ bool psync_reached(unsigned v, unsigned target) { return (int)(v - target) >= 0; }
+
+// Launch SIGNATURE in head word 0. The epoch targets above assume every launch on one buffer
+// published the same number of groups per launch: same kernel, same row tiles per workgroup
+// (NC), same steps (T), same column blocks (NB). A launch of another shape on the same buffer
+// (e.g. a smaller batch choosing a different NC) would see counters already past its targets
+// and read unpublished data (round-5 ADVICE). So the first launch after the buffer is zeroed
+// claims word 0 with its signature, and a launch with a different one fails loudly (reason 5,
+// every wave runs on without waiting, the STAT check raises) instead of racing.
+__device__ __forceinline__ unsigned psync_sig(unsigned kind, unsigned nc, unsigned steps, unsigned nb) {
+  return 0x80000000u | ((kind & 3u) << 29) | ((nc & 15u) << 25) | ((nb & 31u) << 20) | (steps & 0xFFFFFu);
+}
+// thread 0 of every workgroup, before its first wait: 0 = ok, else the conflicting signature
+__device__ __forceinline__ unsigned psync_check_sig(unsigned* sync, unsigned sig) {
+  unsigned prev = 0u;
+  __hip_atomic_compare_exchange_strong((ps_u32*)sync, &prev, sig, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
+  return (prev == 0u || prev == sig) ? 0u : prev;
+}
 
 // Blocking wait of ONE wave (every lane runs it, uniform address): relaxed agent-scope (sc1)
 // poll of a group counter with s_sleep, bounded; the error word is checked so a failure

@@ -5,11 +5,15 @@ Two implementations with one parameter layout:
 
 * :class:`LSTMRegressor` — plain PyTorch fp32 module (``nn.LSTM`` + linear head). It is
   the CPU oracle for val-MSE parity and the reference for the kernel tests.
-* :class:`NativeLSTM` — the MI355X engine: one fused MFMA GEMM + cell kernel per
-  timestep forward, one fused GEMM + cell-backward kernel per timestep backward, and a
-  single split-K weight-gradient GEMM over all (t, b) (csrc/lstm.hip, csrc/gemm.hip).
+* :class:`NativeLSTM` — the MI355X engine: ONE persistent launch for the whole forward
+  (all T steps; gate weights resident in registers, h handed between workgroups in-launch:
+  csrc/lstm_persistent_fwd.inc.h), step T-1 of the backward plus ONE persistent launch for
+  steps T-2..0 (csrc/lstm_persistent_bwd.inc.h), and a single split-K weight-gradient GEMM
+  over all (t, b) (csrc/gemm_core.h). The per-timestep kernels of csrc/lstm.hip remain the
+  fallback for shapes the persistent schedule cannot host (a one-time notice says so).
   Parameters live in a flat fp32 master buffer (so the optimizer and the DP all-reduce
-  are one launch / one collective each); bf16 shadows are repacked after every update.
+  are one launch / one collective each); the fused Adam launch also writes the bf16 operand
+  images the kernels read.
 
 Flat layout (``LstmLayout``): ``[Wcat (4H x KA, unit-major rows 4u+g) | w_out (H) | b_out (1)]``
 with ``Wcat = [W_ih | b_ih + b_hh | 0 ... | W_hh]`` (KA = KX + H, KX = 64-aligned, the
@@ -121,7 +125,9 @@ _PST_REC = 8
 _EXIT_REASONS = {1: "the launch's error word was set while it polled (another workgroup's spin bound)",
                  2: "its own hand-off spin bound tripped",
                  3: "wave 0 read a hand-off flag != 1 from LDS although its own poll succeeded",
-                 4: "a wave read a hand-off flag != 1 from LDS"}
+                 4: "a wave read a hand-off flag != 1 from LDS",
+                 5: "the sync buffer was last used by a launch of another shape (row tiles, steps): "
+                    "zero it (reset_device_errors) before changing the batch"}
 
 
 def persistent_sync_buffer(B: int, row_quantum: int, device) -> torch.Tensor:

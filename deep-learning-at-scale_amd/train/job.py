@@ -101,6 +101,25 @@ def auto_batch(model: str, cfg: RunConfig, dev, n_rank: int) -> int:
     return max(64, b - b % 64)
 
 
+ONLINE_CHUNK_ROWS = 1 << 21  # auto stream chunk: rows per rank (the round-4 default: 8 x 262,144)
+ONLINE_MIN_CHUNKS = 4        # ... but at least this many chunks (validation points) per pass
+ONLINE_MIN_BATCHES = 32      # ... and at least this many mini-batches per chunk
+
+
+def auto_online_chunk(batch: int, n_rank: int, world: int) -> int:
+    """``online_chunk 0`` (auto): stream-chunk rows over ALL ranks, sized in ROWS, not in
+    mini-batches (round-5 ADVICE): a chunk ends with a validation pass, a checkpoint and an
+    early-stopping update (train/online.py), so at the job default batch of 256 a chunk of a few
+    mini-batches would make validation I/O dominate and let patience=5 stop after ~40K rows.
+    Per rank: ONLINE_CHUNK_ROWS, capped so a pass still has ONLINE_MIN_CHUNKS chunks, never
+    under ONLINE_MIN_BATCHES mini-batches (a chunk's first replay and final sync are ~0.1 ms of
+    host time the GPU waits out: 2 % of a 32-batch chunk of 262,144 rows), in whole batches."""
+    batch = max(1, int(batch))
+    per_rank = min(ONLINE_CHUNK_ROWS, max(1, n_rank // ONLINE_MIN_CHUNKS))
+    per_rank = max(per_rank - per_rank % batch, ONLINE_MIN_BATCHES * batch)
+    return per_rank * max(1, int(world))
+
+
 def run_job(model: str, argv, log=print) -> dict:
     cfg = parse_argv(model, argv)
     return run_config(cfg, log=log)
@@ -126,12 +145,8 @@ def run_config(cfg: RunConfig, log=print) -> dict:
     if cfg.batch_size <= 0:
         cfg.batch_size = auto_batch(cfg.model, cfg, dev, n_rank)
         say(f"Batch size (auto): {cfg.batch_size} rows per GPU")
-    if cfg.model == "mlp_online" and cfg.online_chunk <= 0:  # auto: 32 mini-batches per rank per
-        # chunk (train/online.py chunk_bounds balances the chunks of a pass). A chunk ends with a
-        # validation pass and a checkpoint, and its first replay's launch latency and final sync
-        # are host time the GPU waits out: ~0.1 ms per chunk, 8 % of an 8-batch chunk of 262,144
-        # rows (round 5 used 8), 2 % at 32
-        cfg.online_chunk = 32 * cfg.batch_size * max(ctx.world_size, 1)
+    if cfg.model == "mlp_online" and cfg.online_chunk <= 0:
+        cfg.online_chunk = auto_online_chunk(cfg.batch_size, n_rank, ctx.world_size)
         say(f"Stream chunk (auto): {cfg.online_chunk} rows")
     b = max(1, min(cfg.batch_size, n_rank))
     if native and cfg.model == "lstm" and b >= 64:

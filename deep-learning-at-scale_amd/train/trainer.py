@@ -109,6 +109,13 @@ def _graph_steps() -> int:
         return 8
 
 
+# The pre-permuted (sliced) epoch path keys its captured graphs by step offset: one graph per
+# aligned n-step group plus the singles, all kept for the job. Above this many steps per epoch
+# (the job default batch 256 on a multi-million-row table: thousands) the epoch takes the
+# row-indexed path instead, whose graphs are keyed by n only (round-5 ADVICE).
+MAX_SLICED_STEPS = 128
+
+
 def _to_dev(a, device):
     if hasattr(a, "to") and hasattr(a, "starts"):  # data.features.SeriesWindows: rows + starts
         return a.to(device)
@@ -503,7 +510,7 @@ class Trainer:
         while self.epoch < cfg.epochs and not self.stopper.stopped:
             t_ep = time.perf_counter()
             order = self._epoch_order(n, per_rank, dev)
-            src = self._permuted(Xd, Yd, order)
+            src = self._permuted(Xd, Yd, order) if per_rank // max(b, 1) <= MAX_SLICED_STEPS else None
             if src is not None:  # this epoch's rows in shuffled order, read as contiguous slices
                 Xs, Ys = src
             else:

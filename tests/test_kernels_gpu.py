@@ -420,6 +420,39 @@ def test_persistent_exit_record(monkeypatch):
     eng.reset_device_errors()
 
 
+def test_persistent_sync_signature_mismatch_fails_loudly():
+    """Round-5 ADVICE: the hand-off epoch targets assume every launch on one sync buffer had the
+    same (row tiles per workgroup, steps, column blocks). A launch of another shape on a buffer
+    that is not re-zeroed must fail LOUDLY (exit reason 5, check_device_errors raises) instead
+    of reading unpublished h; after reset_device_errors the new shape runs clean."""
+    from wellflow.data.synth import synth_lstm_batch
+    from wellflow.models.lstm import NativeLSTM, init_lstm_flat
+
+    B, T, F, H = 8192, 8, 16, 512
+    eng = NativeLSTM(F, H, T, B, device=DEV)
+    eng.params.copy_(init_lstm_flat(F, H, seed=0).to(DEV))
+    eng.sync_weights()
+    x, _ = synth_lstm_batch(B, T, F, seed=0)
+    C = eng._C
+    C.lstm_pack_x(x.to(DEV), eng.XH, *eng._dims(B), True)
+    assert C.lstm_forward_persistent(eng.XH, eng.Wp, eng.Cst, eng.S, eng.sync, *eng._dims(B))
+    torch.cuda.synchronize()
+    assert eng.persistent_error() == 0
+    short = (B, T - 3, F, eng.lay.KX, H)  # same buffers, fewer steps: another signature
+    assert C.lstm_forward_persistent(eng.XH, eng.Wp, eng.Cst, eng.S, eng.sync, *short)
+    torch.cuda.synchronize()
+    fw = eng.persistent_stats()["forward"]
+    assert fw["sticky"] == 1 and fw["done"] < fw["expect"], fw
+    assert fw["first_exit"] is not None and fw["first_exit"]["reason"] == 5, fw
+    with pytest.raises(RuntimeError):
+        eng.check_device_errors()
+    eng.reset_device_errors()
+    assert C.lstm_forward_persistent(eng.XH, eng.Wp, eng.Cst, eng.S, eng.sync, *short)
+    torch.cuda.synchronize()
+    assert eng.persistent_error() == 0
+    eng.reset_device_errors()
+
+
 def test_diag_env_ignored_by_production_build(monkeypatch):
     """A production _C.so ignores the timing-only switches (round-3 VERDICT item 2):
     WELLFLOW_PF_DBG=1 (skip the persistent hand-off wait) and WELLFLOW_MLP_DBG=1 (skip the

@@ -181,3 +181,35 @@ def test_resume_with_other_layout_fails_clearly(tmp_path):
     assert st["layout"]["numel"] == st["params"].numel()
     with _pytest.raises(ValueError, match="layout does not match"):
         run_job("mlp", base + ["--mlp-hidden", "64,64", "--resume"], log=lambda *a, **k: None)
+
+
+def test_auto_online_chunk_is_sized_in_rows():
+    """Round-5 ADVICE: the auto stream chunk (online_chunk 0) is sized in ROWS, not in
+    mini-batches: at the job default batch of 256 a chunk is no longer 8,192 rows per rank (which
+    made validation / checkpoint I/O dominate and let patience 5 stop after ~40K rows)."""
+    from wellflow.train.job import ONLINE_CHUNK_ROWS, auto_online_chunk
+
+    # a 15 M-row stream on one rank at batch 256: 2M-row chunks (the round-4 size), whole batches
+    c = auto_online_chunk(256, 15_000_000, 1)
+    assert c == ONLINE_CHUNK_ROWS and c % 256 == 0
+    # at DP=8 the chunk covers every rank's share
+    assert auto_online_chunk(256, 15_000_000, 8) == 8 * ONLINE_CHUNK_ROWS
+    # a short stream still gets >= 4 validation points per pass ...
+    c = auto_online_chunk(256, 400_000, 1)
+    assert 400_000 // c >= 4 and c % 256 == 0
+    # ... and never fewer than 32 mini-batches per chunk (262,144-row batches: 32 x B)
+    assert auto_online_chunk(262_144, 15_000_000, 1) == 32 * 262_144
+    assert parse_argv("mlp_online", ["a", "float", "a", "/tmp/"]).online_chunk == 0  # 0 = auto
+
+
+def test_sliced_epochs_bound_the_graph_count():
+    """Round-5 ADVICE: the pre-permuted (sliced) epoch path keys its graphs by step offset, so it
+    is taken only up to MAX_SLICED_STEPS steps per epoch; longer epochs use the row-indexed path,
+    whose graphs are keyed by the group length only."""
+    import inspect
+
+    from wellflow.train import trainer
+
+    assert 16 <= trainer.MAX_SLICED_STEPS <= 512
+    src = inspect.getsource(trainer.Trainer.fit)
+    assert "MAX_SLICED_STEPS" in src and "_permuted" in src

@@ -31,7 +31,7 @@ TYPES = "string,string,int,float,float,float,float,float,float,float"
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--model", default="lstm", choices=["lstm", "mlp", "mlp_online"])
+    ap.add_argument("--model", default="lstm", choices=["lstm", "mlp", "mlp_online", "cnn"])
     ap.add_argument("--epochs", type=int, default=4)
     ap.add_argument("--out", default=None)
     ap.add_argument("--wells", type=int, default=6, help="synthetic wells: (wells - 1) + 2 one-hot + 9 "
@@ -39,7 +39,9 @@ def main():
     ap.add_argument("--scale", type=int, default=4, help="MLP tables: 640,000 x scale steps per well "
                     "(4: ~36 mini-batches of 262,144 per pass; 1 = the round-4/5 table, 9 per pass)")
     ap.add_argument("--default-batch", action="store_true",
-                    help="the job's own default batch (lstm: auto) instead of the bench's per-GPU batch")
+                    help="the submission's OWN defaults (no --batch-size: cnn 20 (cnn.py:128), mlp / "
+                    "mlp_online 256, lstm auto; config.py MODEL_DEFAULTS) on a table sized so an epoch "
+                    "holds ~1-2 K steps, instead of the bench's per-GPU batch")
     a = ap.parse_args()
     from wellflow.config import parse_argv
     from wellflow.train.job import run_config
@@ -48,13 +50,20 @@ def main():
         batch, extra, wells, steps = 8192, ["--seq-len", "64", "--hidden", "512"], a.wells, 40000 * 6 // a.wells
     elif a.model == "mlp":  # 15.4 M rows: ~36 steps of 262,144 per epoch
         batch, extra, wells, steps = 262144, [], 6, 640000 * a.scale
-    else:  # the stream: chunks of 32 mini-batches, each consumed once (train/online.py)
+    elif a.model == "cnn":  # the reference model (cnn.py:110-118), 48-step windows, 12 outputs
+        batch, extra, wells, steps = 65536, [], 6, 40000
+    else:  # the stream: chunks sized in rows (train/job.py auto_online_chunk), each consumed once
         batch, extra, wells, steps = 262144, [], 6, 640000 * a.scale
-        extra = ["--online-chunk", "0"]  # auto: ~32 batches per chunk, balanced (train/job.py)
+        extra = ["--online-chunk", "0"]
+    if a.default_batch and a.model in ("mlp", "mlp_online"):
+        steps = 64000  # 6 x 64,000 rows: ~1,500 steps of 256 per epoch
+    if a.default_batch and a.model == "cnn":
+        steps = 6000   # ~1,400 windows of 20 per epoch
     # 6 wells (3 fields): 5 + 2 one-hot columns + 9 continuous = 16 features, the bench's F
     argv = [NAMES, TYPES, "flow", "/tmp/wellflow_jobtp/", "--epochs", str(a.epochs), "--patience", "100",
             "--synth-wells", str(wells), "--synth-steps", str(steps), "--device", "cuda", "--verbose", "0"] + extra
-    argv += ["--batch-size", "0" if a.default_batch else str(batch)]
+    if not a.default_batch:
+        argv += ["--batch-size", str(batch)]
     cfg = parse_argv(a.model, argv)
     out = run_config(cfg, log=lambda *x, **k: None)
     from wellflow.data.pipeline import prepare  # noqa: F401  (feature count reported below)
@@ -73,7 +82,7 @@ def main():
     batch = cfg.batch_size  # what the job ran (auto-sized when --default-batch)
     F = out.get("n_features") or 16
     # >= ~50 ms timed for the sub-millisecond MLP steps (20 steps of 0.18 ms read ~15 % low)
-    nsteps = "20" if a.model == "lstm" else "300"
+    nsteps = "20" if a.model == "lstm" else ("3000" if batch <= 1024 else "300")
     bench = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--model", a.model, "--batch", str(batch),
                             "--features", str(F), "--secondary", "none", "--parity", "none", "--steps", nsteps,
                             "--warmup", "5"],
