@@ -113,19 +113,21 @@ __global__ __launch_bounds__(256, 1) void lstm_fwd_persistent_kernel(
   // input would be published too late to fetch ahead (NC < 8), or at all (NC = 1).
   constexpr bool SPLIT = NC == 8 && 4 * ABYTES + PF_ROWS * 64 * 2 + 32 <= 163840;  // KX = 128: 3 slots only
   constexpr int NSLOT = SPLIT ? 4 : 3;
-  // ALT (round 6; the H = 512 split-phase production path): the accumulators live in VGPRs as
-  // TWO sets that alternate between chunk bodies (body P accumulates into set P & 1 while its
-  // fused cell stages read the previous chunk's set directly), so no chunk copies its 32
-  // accumulators out (32 v_accvgpr_read per chunk before) and no AGPR holds an accumulator:
-  // 14 k-tiles of weights fit the AGPR file (VGPR weights 4 k-tiles, as many registers as before)
-  constexpr bool ALT = FUSED && SPLIT && (DBG & 2048) == 0;  // DBG 2048 (A/B): AGPR accumulators + copy
+  // ALT (DBG 2048, A/B only; measured SLOWER: 1.36 vs 1.28 ms interleaved,
+  // profiles/r6/forward_budget.md): the accumulators in VGPRs as TWO sets that alternate
+  // between chunk bodies (body P accumulates into set P & 1 while its fused cell stages read the
+  // previous chunk's set directly), so no chunk copies its 32 accumulators out of the AGPRs and
+  // 14 k-tiles of weights fit the AGPR file. Production keeps the AGPR accumulators + copy.
+  constexpr bool ALT = FUSED && SPLIT && (DBG & 2048) != 0;
   // SPLIT publish delay (round 6): chunk j publishes chunk j - PD, polled one chunk before its
   // fetch; DBG 262144 (A/B): the round-5 form, PD = 2 with the poll two chunks before
   constexpr bool PUB3 = (DBG & 262144) == 0;
-  constexpr int PD = PUB3 ? 3 : 2, PL = PUB3 ? 1 : 2;
+  // DBG 8 (A/B): with PD = 3, poll two chunks before the fetch instead of one
+  constexpr int PD = PUB3 ? 3 : 2, PL = (PUB3 && (DBG & 8) == 0) ? 1 : 2;
   // DBG 256 (A/B, measured slower): each wave publishes its own 32-B piece of every h row
   // (no staging barrier); the production form writes whole 128-B lines, one per 8 lanes
   constexpr bool WAVE_H = (DBG & 256) != 0;
+  constexpr bool NOHO = (DBG & 524288) != 0;  // timing only: no hand-off (no publish, poll or wait)
   constexpr int KTA = ALT ? 14 : KTA_;
   // Distinct static LDS objects per ring slot: the compiler then proves the slot being
   // filled by LDS-DMA disjoint from the slots being read, and inserts no vmcnt(0) of its own.
@@ -238,6 +240,9 @@ __global__ __launch_bounds__(256, 1) void lstm_fwd_persistent_kernel(
   // not match); a failure is recorded once and makes every later wait a no-op
   auto wait_chunk = [&](int cc, int tt) {
     if (failed) return;
+#ifdef WF_DIAG
+    if (lane == 0) pguard_add(stat + 20, 1u);  // diagnostics: blocking waits (tools/pf_budget.py)
+#endif
     unsigned seen_cnt = 0, seen_err = 0;
     const unsigned tg = target(cc, tt);
     const unsigned why = psync_wait(rbw + kPSyncGroup + cc, err, tg, tag, spin_limit, stat, &seen_cnt, &seen_err);
@@ -631,7 +636,11 @@ __global__ __launch_bounds__(256, 1) void lstm_fwd_persistent_kernel(
         if (t == 0 && c < 2)
           wait_vmcnt<LPT>();
         else
-          asm volatile("s_waitcnt vmcnt(%1)" : "+v"(pvr[P % PL]) : "n"(NSTORE - 1 + (PUB3 ? 1 : 0)) : "memory");
+          // in flight at this wait (issue order): ... | top j-2: pieces j, poll | end j-2: h j-3, C/S
+          // | top j-1: pieces j+1, poll | end j-1: h j-2, C/S (NSTORE - 1) | — PD = 3 keeps h j-2 in
+          // flight (NSTORE), with PL = 2 also the pieces and poll of j-1 (the poll read here is j-2's)
+          asm volatile("s_waitcnt vmcnt(%1)" : "+v"(pvr[P % PL])
+                       : "n"(PD == 2 ? NSTORE - 1 : (PL == 1 ? NSTORE : NSTORE + LPT + 1)) : "memory");
       } else if (c == 0) {
         if (NC > 1 && !FIRST) wait_vmcnt<LPT>(); else wait_vmcnt<0>();
       } else if (c == 1) {
@@ -649,21 +658,21 @@ __global__ __launch_bounds__(256, 1) void lstm_fwd_persistent_kernel(
       stamp(t, 3 + 5 * c);
       if constexpr (SPLIT) {
         // publish chunk j-PD: every wave drained its h store before the barrier above
-        if ((t > 0 || c >= PD) && threadIdx.x == 0)
+        if (!NOHO && (t > 0 || c >= PD) && threadIdx.x == 0)
           __hip_atomic_fetch_add(rbw + kPSyncGroup + (c >= PD ? c - PD : c + NC - PD), 1u, __ATOMIC_RELAXED,
                                  __HIP_MEMORY_SCOPE_AGENT);
         // chunk j+2: its h rows were published by the row block 3 chunks ago; the poll of one
         // chunk ago says whether all arrived, else wait here (bounded)
         const int c2 = c + 2 < NC ? c + 2 : c + 2 - NC, t2 = c + 2 < NC ? t : t + 1;
         if (t2 < d.T) {
-          if (t2 >= 1 && !failed && !psync_reached(__builtin_amdgcn_readfirstlane(pvr[P % PL]), target(c2, t2)))
+          if (!NOHO && t2 >= 1 && !failed && !psync_reached(__builtin_amdgcn_readfirstlane(pvr[P % PL]), target(c2, t2)))
             wait_chunk(c2, t2);
           if (t2 > 0 || (DBG & 131072) == 0)
             issue_b(t2 == t ? abase : abase_n, c2, std::integral_constant<int, (P + 2) % NSLOT>{});
         }
         // poll for chunk j+2+PL (read at the top of chunk j+PL)
         const int c3 = c + 2 + PL < NC ? c + 2 + PL : c + 2 + PL - NC, t3 = c + 2 + PL < NC ? t : t + 1;
-        if (t3 >= 1 && t3 < d.T) pvr[P % PL] = poll(c3);
+        if (!NOHO && t3 >= 1 && t3 < d.T) pvr[P % PL] = poll(c3);
       } else if constexpr (!FIRST) {
         if (c + 2 < NC) issue(c + 2, std::integral_constant<int, (P + 2) % 3>{});
       }
@@ -1038,6 +1047,10 @@ static int launch_pf(bf16_t* XH, const bf16_t* Wp, bf16_t* Cst, bf16_t* S, unsig
     if constexpr (WF_DV(2048)) { if (d.dbg == 2048) f = reinterpret_cast<const void*>(&lstm_fwd_persistent_kernel<KT, NC, 2048>); }  // AGPR accumulators
     if constexpr (WF_DV(262144)) { if (d.dbg == 262144) f = reinterpret_cast<const void*>(&lstm_fwd_persistent_kernel<KT, NC, 262144>); }  // round-5 publish delay
     if constexpr (WF_DV(264192)) { if (d.dbg == 264192) f = reinterpret_cast<const void*>(&lstm_fwd_persistent_kernel<KT, NC, 264192>); }  // the round-5 kernel
+    if constexpr (WF_DV(8)) { if (d.dbg == 8) f = reinterpret_cast<const void*>(&lstm_fwd_persistent_kernel<KT, NC, 8>); }  // poll two chunks ahead
+    if constexpr (WF_DV(524288)) { if (d.dbg == 524288) f = reinterpret_cast<const void*>(&lstm_fwd_persistent_kernel<KT, NC, 524288>); }  // no hand-off
+    if constexpr (WF_DV(663584)) { if (d.dbg == 663584) f = reinterpret_cast<const void*>(&lstm_fwd_persistent_kernel<KT, NC, 663584>); }  // bare MFMAs + stores, no hand-off
+    if constexpr (WF_DV(663588)) { if (d.dbg == 663588) f = reinterpret_cast<const void*>(&lstm_fwd_persistent_kernel<KT, NC, 663588>); }  // bare MFMAs, h staging only
     if constexpr (WF_DV(32)) { if (d.dbg == 32) f = reinterpret_cast<const void*>(&lstm_fwd_persistent_kernel<KT, NC, 32>); }  // no fragment reads
     if constexpr (WF_DV(8224)) { if (d.dbg == 8224) f = reinterpret_cast<const void*>(&lstm_fwd_persistent_kernel<KT, NC, 8224>); }  // neither cell math nor fragment reads
     if constexpr (WF_DV(131072)) { if (d.dbg == 131072) f = reinterpret_cast<const void*>(&lstm_fwd_persistent_kernel<KT, NC, 131072>); }  // no LDS-DMA

@@ -31,6 +31,8 @@ import os
 import torch
 from torch import nn
 
+from .base import note_slow_path
+
 
 def _r8(x: int) -> int:
     return (x + 7) // 8 * 8
@@ -178,6 +180,26 @@ class CnnLayout:
                 flat[b : b + self.Op])
 
 
+def cnn_fast_path_reason(layout: "CnnLayout", dropout: float) -> str | None:
+    """None when the fused CNN kernels cover this layout (a Python mirror of
+    csrc/cnn_fused.hip cnn_fused_supported), else why not: the step then runs im2col + the
+    generic split-K GEMMs (7 launches; NativeCNN announces it once: note_slow_path)."""
+    L = layout
+    if L.in_ch != 1:
+        return f"{L.in_ch} input channels (the fused kernels take the reference's single-channel series)"
+    if L.lout != 36 or L.Fp != 112:
+        return f"{L.lout} output steps x {L.Fp} padded filters (fused: 36 x 112, the reference's 48-step window, 100 filters)"
+    if L.taps > 15 or L.Kc != 16:
+        return f"{L.taps} taps (fused: <= 15, one 16-wide K slot with the bias)"
+    if not 1 <= L.outputs <= 16:
+        return f"{L.outputs} outputs (fused: 1 .. 16)"
+    if L.input_len % 4 != 0:
+        return f"window length {L.input_len} not a multiple of 4"
+    if dropout not in (0.0, 0.5):
+        return f"dropout {dropout} (fused: 0 or 0.5)"
+    return None
+
+
 class NativeCNN:
     """HIP/MFMA engine for the reference CNN (any batch up to ``batch``).
 
@@ -206,8 +228,14 @@ class NativeCNN:
         self.rng = torch.zeros(1, dtype=torch.int64, device=dev)
         L = layout
         ok = self._C.cnn_fused_ok(L.fused_dims, float(dropout))
+        why = cnn_fast_path_reason(L, float(dropout))
+        assert (why is None) == bool(ok), (why, ok)  # the Python mirror must agree with the kernels
         if fused is None:
             fused = ok and os.environ.get("WELLFLOW_CNN_FUSED", "1") != "0"
+        if not fused:
+            note_slow_path("CNN", "training step runs im2col + generic GEMMs",
+                           why or "fused kernels disabled (WELLFLOW_CNN_FUSED=0)",
+                           f"window {L.input_len}x{L.in_ch} filters {L.filters} k {L.kernel} out {L.outputs} B={batch}")
         if fused and not ok:
             raise ValueError(f"fused CNN kernels do not cover {L} with dropout {dropout}")
         self.fused = bool(fused)

@@ -6,7 +6,7 @@
 #   tools/gpu.sh pmc TAG "CTRS" [args]  one rocprofv3 --pmc pass (<= 8 SQ counters) -> gpurun_out/pmc_TAG
 #   tools/gpu.sh all              tests + smoke + the three benches
 #   tools/gpu.sh sweep VAR "v1 v2 .." [bench args]   bench.py once per env value VAR=v (e.g.
-#                                 WELLFLOW_HEAD_GRID, WELLFLOW_MLP_DW2_SPLIT, WELLFLOW_DW_BIG)
+#                                 WELLFLOW_MLP_STEP128, WELLFLOW_DW_SLAB)
 #   tools/gpu.sh ksweep VAR "v1 v2 .." KERNEL [bench args]  the same under rocprofv3 --kernel-trace,
 #                                 printing the stats line of kernels matching KERNEL per value
 #   tools/gpu.sh pmcsets "SET1" "SET2" ..   one rocprofv3 --pmc pass per counter set over a 2-step
