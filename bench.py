@@ -86,6 +86,7 @@ def _spawn_ranks(n: int, argv) -> int:
 
 
 _LAST_TIMED = {"untimed": 0}  # steps the last _timed() ran outside its window (warm-up, probe, captures)
+_SAMPLER = {}  # "s": this rank's GpuStateSampler (GPU runs), bracketing every timed window
 
 
 def _timed(ctx, step, steps, warmup, min_s: float = 0.0, many=None, graph_steps: int = 1, warm_ms: float = 25.0):
@@ -140,6 +141,9 @@ def _timed(ctx, step, steps, warmup, min_s: float = 0.0, many=None, graph_steps:
         for _ in range(min(extra, 64)):
             many(n)
             total += n
+    smp = _SAMPLER.get("s")
+    if smp is not None:
+        smp.start()  # a sysfs read + a sleeping thread: nothing on the GPU's queues
     ctx.barrier()
     sync()
     t0 = time.perf_counter()
@@ -149,8 +153,10 @@ def _timed(ctx, step, steps, warmup, min_s: float = 0.0, many=None, graph_steps:
         step()
     sync()
     ctx.barrier()
+    el = time.perf_counter() - t0
     _LAST_TIMED["untimed"] = total
-    return ctx.max_scalar(time.perf_counter() - t0), steps, total + steps
+    _LAST_TIMED["gpu_state"] = smp.stop() if smp is not None else None
+    return ctx.max_scalar(el), steps, total + steps
 
 
 def _comm_ms(ctx, buf, iters: int = 20) -> float | None:
@@ -441,6 +447,8 @@ def _secondary(args, ctx, models) -> dict:
                                      default=1),
                   **comm_rec,
                   **{k: v for k, v in extra.items() if k.startswith("h2d") or k in ("persistent_fwd",)}}
+        if _LAST_TIMED.get("gpu_state") is not None:
+            out[m]["gpu_state"] = _LAST_TIMED["gpu_state"]
         if W > 1 and ctx.device.type == "cuda":
             out[m]["rccl"] = _rccl_summary(os.environ.get("NCCL_DEBUG_FILE"))
         del run, eng
@@ -536,8 +544,15 @@ def main() -> int:
             ctx.shutdown()
             return 3
     torch.manual_seed(1234 + ctx.rank)
+    if not cpu:
+        from wellflow.utils.gpustate import GpuStateSampler
+
+        smp = GpuStateSampler(ctx.device.index or 0)
+        if smp.available:
+            _SAMPLER["s"] = smp
     elapsed, steps, B, model, loss, run, eng, extra = _run_model(args, ctx)
     untimed = _LAST_TIMED["untimed"]
+    gpu_state = _LAST_TIMED.get("gpu_state")
     assert steps == args.steps
     comm = _comm_ms(ctx, eng.grads)
     grad_mb = round(eng.grads.numel() * 4 / 2**20, 3)
@@ -616,6 +631,9 @@ def main() -> int:
         if W > 1 and not cpu:
             rec["rccl"] = _rccl_summary(rccl_log)
             rec["hsa_enable_ipc_mode_legacy"] = os.environ.get("HSA_ENABLE_IPC_MODE_LEGACY")
+        # rank 0's GPU over the headline's timed window: sampled gfx clock, socket power, hotspot
+        # temperature and the firmware's limiter residencies (utils/gpustate.py); None off-GPU
+        rec["gpu_state"] = gpu_state
         if sec is not None:
             rec["secondary"] = sec
         if par is not None:

@@ -570,7 +570,7 @@ void mlp2_reduce(const at::Tensor& red, int64_t Fp, int64_t B, c10::optional<at:
 bool mlp2_step(const at::Tensor& X, int64_t Fp, const at::Tensor& W1, const at::Tensor& b1, const at::Tensor& W2,
                const at::Tensor& b2, const at::Tensor& w3, const at::Tensor& b3, const at::Tensor& y, double dy_scale,
                int64_t B, c10::optional<at::Tensor> rows, const at::Tensor& dZ2, c10::optional<at::Tensor> pred,
-               const at::Tensor& red, bool dz_frag, c10::optional<at::Tensor> W2T) {
+               const at::Tensor& red, bool dz_frag, c10::optional<at::Tensor> W2T, double clip) {
   constexpr int64_t H = 256;
   check_t(X, at::kBFloat16, "X");
   const int64_t nrows = check_x_rows(X, Fp, B, rows);
@@ -603,7 +603,7 @@ bool mlp2_step(const at::Tensor& X, int64_t Fp, const at::Tensor& W1, const at::
   const c10::hip::OptionalHIPGuardMasqueradingAsCUDA guard(X.device());
   return wf::launch_mlp2_step(bfp(X), (int)Fp, bfp(W1), fp(b1), bfp(W2), fp(b2), fp(w3), fp(b3), fp(y), (float)dy_scale,
                               (int)B, rows_ptr(rows, B), nrows, bfp(dZ2), opt_ptr<float>(pred, at::kFloat, "pred", B),
-                              fp(red), dz_frag, cur_stream(), w2t);
+                              fp(red), dz_frag, cur_stream(), w2t, (float)clip);
 }
 
 // dW2 from the fragment-layout dZ2 of mlp2_step(dz_frag=True) into the spread scratch's dW2

@@ -532,7 +532,7 @@ __device__ __forceinline__ void gemm_mainloop_glds2(const bf16_t* __restrict__ A
 // busy). 32-deep slots of the same tile (28 KiB) fit 5 deep: a piece is issued NSLOT - 1 half
 // steps ahead of its use. Pieces that do not split evenly over the waves (the 192-wide image
 // is 12 pieces per half step) go to the low waves, and each wave counts its own in vmcnt.
-template <int R, int L, int NT, int BKD>
+template <int R, int L, int NT, int BKD, bool GL = false>
 struct GldsOpH {
   static_assert(L == MN_CONTIG, "half-step ring: MN-contiguous operands only");
   static constexpr int BYTES = R * BKD * 2;
@@ -547,6 +547,7 @@ struct GldsOpH {
   // the 288-wide tile's kernel). The workgroup's whole K range is < 2 GiB from its origin.
   unsigned src[MAXPW];
   __amdgpu_buffer_rsrc_t rsrc;
+  const char* base;  // GL: the same origin as a plain pointer
   int kstep_bytes;
 
   __device__ __forceinline__ void init(const bf16_t* p, long ld, int row0, int kbeg, int wid, int lane) {
@@ -559,30 +560,45 @@ struct GldsOpH {
     }
     rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16_t*>(p + (size_t)kbeg * ld + row0), 0, 0x7FFFFFFF,
                                              0x00020000);
+    base = reinterpret_cast<const char*>(p + (size_t)kbeg * ld + row0);
     kstep_bytes = (int)(BKD * ld * 2);
   }
   __device__ __forceinline__ void issue(int step, char* lds_tile, int wid) const {
     const int so = step * kstep_bytes;
 #pragma unroll
     for (int i = 0; i < MAXPW; ++i) {
-      if (i + 1 < MAXPW || REM == 0 || wid < REM)  // wave-uniform
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (lds_void*)(lds_tile + (i * NW + wid) * 1024), 16, (int)src[i],
-                                                 so, 0, 0);
+      if (i + 1 < MAXPW || REM == 0 || wid < REM) {  // wave-uniform
+        if constexpr (GL) {
+          // global_load_lds (round 6, tile 8 A/B) in its saddr form: the uniform base + step in
+          // SGPRs, the 32-bit lane offset in a VGPR (the builtin made 64-bit per-lane addresses
+          // and spilled). Tried because the probe charged the MUBUF form ~2x its issue time;
+          // the dW GEMM measured 5 % SLOWER with it (profiles/r6/diag/glds.txt). Inline asm: M0
+          // through its constraint, one wait state after the M0 write; the counted vmcnt waits
+          // of the ring cover it like the builtin.
+          const char* b = base + so;
+          const unsigned la = (unsigned)(uintptr_t)((lds_void*)(lds_tile + (i * NW + wid) * 1024));
+          asm volatile("s_nop 0\n\tglobal_load_lds_dwordx4 %0, %1" ::"v"(src[i]), "s"(b),
+                       "{m0}"(__builtin_amdgcn_readfirstlane(la))
+                       : "memory");
+        } else
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (lds_void*)(lds_tile + (i * NW + wid) * 1024), 16, (int)src[i],
+                                                   so, 0, 0);
+      }
     }
   }
 };
 
 // BKD = 64 with NSLOT = 2: the plain 2-stage ring of gemm_mainloop_glds2, for tiles whose
 // pieces do not split evenly over the waves (the 288-wide image: 36 pieces per 64-deep step)
-template <class C, int NSLOT, int PRIO = 0, int BKD = 32>
+template <class C, int NSLOT, int PRIO = 0, int BKD = 32, bool GL = false>
 __device__ __forceinline__ void gemm_mainloop_glds_h(const bf16_t* __restrict__ A, long lda,
                                                      const bf16_t* __restrict__ B, long ldb, int kbeg,
                                                      int nh, int m0, int n0, char* smem,
                                                      f32x4 (&acc)[C::TM][C::TN]) {
   static_assert(BKD == 32 || BKD == 64, "32- or 64-deep steps");
   static_assert(NSLOT >= 2 && NSLOT <= 6, "2..6 slots");
-  using OA = GldsOpH<C::BM, C::LA_, C::NT, BKD>;
-  using OB = GldsOpH<C::BN, C::LB_, C::NT, BKD>;
+  using OA = GldsOpH<C::BM, C::LA_, C::NT, BKD, GL>;
+  using OB = GldsOpH<C::BN, C::LB_, C::NT, BKD, GL>;
   static_assert(OA::REM == 0 || OB::REM == 0, "at most one operand with an uneven piece split");
   constexpr int STAGE = OA::BYTES + OB::BYTES;
   constexpr int LHI = OA::MAXPW + OB::MAXPW;                       // pieces per half step, low waves

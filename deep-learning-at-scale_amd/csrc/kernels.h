@@ -132,7 +132,8 @@ void launch_mlp2_reduce(float* red, int Fp, int B, float* loss_sum, float* db3, 
 bool launch_mlp2_step(const bf16_t* X, int Fp, const bf16_t* W1, const float* b1, const bf16_t* W2, const float* b2,
                       const float* w3, const float* b3, const float* y, float dy_scale, int B, const long long* rows,
                       long nrows, bf16_t* dZ2, float* pred, float* red, bool dz_frag, hipStream_t s,
-                      const bf16_t* W2T = nullptr);
+                      const bf16_t* W2T = nullptr, float clip = 0.f);
+// clip > 0: the clipped-MAE loss min(|p - y|, clip) instead of MSE (dy_scale = grad_scale then)
 // W2T (optional, [256][256] bf16 = W2 transposed): with dz_frag, the 128-row-pass kernel that
 // streams both weight images (mlp2_step128_kernel) instead of holding W2^T in registers.
 // dz_frag: dZ2 is written in the fragment layout of launch_mlp2_dw2f (B % 64 == 0) instead of

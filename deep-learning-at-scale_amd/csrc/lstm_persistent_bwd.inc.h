@@ -97,6 +97,12 @@ constexpr int pb_group_size(int nrt) { return nrt >= 16 ? 8 : (nrt >= 8 ? 2 : nr
 // DBG (WF_DIAG timing-only builds, results wrong): 2 no MFMA, 16 no A loads after tile 1,
 // 32 timeline (s_memrealtime stamps of step PB_STAMP_S, wave 0 lane 0 of every workgroup,
 // into sync + 4096 words, 128 per workgroup; tools/pb_timeline.py).
+// an A source: the buffer resource (MUBUF LDS-DMA) and the plain pointer (global_load_lds)
+struct ASrc {
+  __amdgpu_buffer_rsrc_t r;
+  const char* p;
+};
+
 template <int KT, int NRT, int DBG = 0>
 __global__ __launch_bounds__(256, 1) void lstm_bwd_persistent_kernel(
     const bf16_t* __restrict__ WhhT, const bf16_t* __restrict__ Cst, const bf16_t* __restrict__ S,
@@ -105,6 +111,7 @@ __global__ __launch_bounds__(256, 1) void lstm_bwd_persistent_kernel(
   constexpr int H = 32 * KT, G = 4 * H, NB = H / 64, HB = H / 16;
   constexpr int KS = KT / 2;             // 64-wide k-steps per wave per row tile
   constexpr int GS = pb_group_size(NRT), NG = NRT / GS;
+  constexpr bool GLDS = (DBG & 64) != 0;  // A pieces by global_load_lds (A/B; see issue_a)
   static_assert(NG <= kPSyncMaxGroups && NRT % GS == 0, "hand-off groups");
   static_assert(NG == 1 || (GS >= 2 && NRT - GS - 4 >= 0), "a group must publish before its next poll");
   constexpr int WSLOT = 16 * KT * 64;    // bytes of one wave's A tile: 16 rows x H k (bf16)
@@ -253,19 +260,30 @@ __global__ __launch_bounds__(256, 1) void lstm_bwd_persistent_kernel(
   };
   // A tile TI of the step whose A resource is `ar` -> ring slot TI & 1; piece i = k-step i / 2,
   // rows 8 * (i % 2) .. of the wave's K quarter, 1 KB, sc1 (the hand-off's consumer side)
-  auto issue_a = [&](const __amdgpu_buffer_rsrc_t& ar, auto tc, auto ic) {
+  auto issue_a = [&](const ASrc& ar, auto tc, auto ic) {
     constexpr int TI = decltype(tc)::value, i = decltype(ic)::value, ks = i / 2, hf = i % 2;
     if constexpr ((DBG & 16) != 0) {
       if (TI > 1) return;
     }
     const unsigned dst = a_lds + (TI & 1) * WSLOT + ks * 2048 + hf * 1024;
-    // (the instruction offset would also move the LDS address: the k-step goes into soffset)
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(ar, (lds_void*)(uintptr_t)dst, 16, hf ? a_vo1 : a_vo,
-                                             TI * 16 * G * 2 + ks * 128, 0, 16);
+    if constexpr (GLDS) {
+      // global_load_lds (round 6, DBG 64 A/B): same bytes, same LDS image, sc1. Tried because
+      // the probe charged the MUBUF form ~2x its issue time beside MFMAs; in the real kernel it
+      // measured SLOWER (1.492 vs 1.466 ms, profiles/r6/diag/glds.txt): MUBUF stays
+      const char* src = ar.p + (hf ? a_vo1 : a_vo) + TI * 16 * G * 2 + ks * 128;
+      __builtin_amdgcn_global_load_lds((const void*)src, (lds_void*)(uintptr_t)dst, 16, 0, 16 /* sc1 */);
+    } else {
+      // (the instruction offset would also move the LDS address: the k-step goes into soffset)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(ar.r, (lds_void*)(uintptr_t)dst, 16, hf ? a_vo1 : a_vo,
+                                               TI * 16 * G * 2 + ks * 128, 0, 16);
+    }
   };
-  auto a_rsrc_of = [&](int tt) {  // A of the step with t = tt: DG_{tt+1}, this row block
-    return __builtin_amdgcn_make_buffer_rsrc(DG + ((size_t)(tt + 1) * d.B + row0) * G, 0, 0x7FFFFFFF, 0x00020000);
+  auto a_rsrc_of = [&](int tt) -> ASrc {  // A of the step with t = tt: DG_{tt+1}, this row block
+    const bf16_t* b = DG + ((size_t)(tt + 1) * d.B + row0) * G;
+    return ASrc{__builtin_amdgcn_make_buffer_rsrc(const_cast<bf16_t*>(b), 0, 0x7FFFFFFF, 0x00020000),
+                reinterpret_cast<const char*>(b)};
   };
+
   // sc1 poll of a group counter: one uniform load (every lane, one address). Inline asm, so it
   // stays where it is written (the compiler sinks the S / c buffer loads to the end of the
   // loop, behind the DG stores; a tracked poll there made its first use wait for those stores)
@@ -297,7 +315,7 @@ __global__ __launch_bounds__(256, 1) void lstm_bwd_persistent_kernel(
   load_sc(d.T - 2, std::integral_constant<int, 0>{}, std::integral_constant<int, 0>{});
   load_sc(d.T - 2, std::integral_constant<int, 1>{}, std::integral_constant<int, 1>{});
   {  // A(0) of the first step: DG_{T-1} was written by the previous kernel (lstm_bwd_last_kernel)
-    const __amdgpu_buffer_rsrc_t ar = a_rsrc_of(d.T - 2);
+    const ASrc ar = a_rsrc_of(d.T - 2);
     static_for<0, 2 * KS>([&](auto ic) { issue_a(ar, std::integral_constant<int, 0>{}, ic); });
   }
   // fast[gg]: this wave already streamed the first tile of group gg (its poll matched two tiles
@@ -320,8 +338,8 @@ __global__ __launch_bounds__(256, 1) void lstm_bwd_persistent_kernel(
     const int t = d.T - 2 - s;
     const bool last_step = s == d.T - 2;
     stamp(s, 0);
-    const __amdgpu_buffer_rsrc_t a_rsrc = a_rsrc_of(t);
-    const __amdgpu_buffer_rsrc_t an_rsrc = a_rsrc_of(t > 0 ? t - 1 : t);  // next step's A (DG_t)
+    const ASrc a_rsrc = a_rsrc_of(t);
+    const ASrc an_rsrc = a_rsrc_of(t > 0 ? t - 1 : t);  // next step's A (DG_t)
     const __amdgpu_buffer_rsrc_t dg_rsrc =
         __builtin_amdgcn_make_buffer_rsrc(DG + (size_t)t * d.B * G, 0, 0x7FFFFFFF, 0x00020000);
     const int st_base = row0 * G * 2 + st_lane;
@@ -683,6 +701,7 @@ static int launch_pb(const bf16_t* WhhT, const bf16_t* Cst, const bf16_t* S, bf1
       case 2: if constexpr (WF_DV(2)) f = reinterpret_cast<const void*>(&lstm_bwd_persistent_kernel<KT, NRT, 2>); break;
       case 16: if constexpr (WF_DV(16)) f = reinterpret_cast<const void*>(&lstm_bwd_persistent_kernel<KT, NRT, 16>); break;
       case 32: if constexpr (WF_DV(32)) f = reinterpret_cast<const void*>(&lstm_bwd_persistent_kernel<KT, NRT, 32>); break;
+      case 64: if constexpr (WF_DV(64)) f = reinterpret_cast<const void*>(&lstm_bwd_persistent_kernel<KT, NRT, 64>); break;
       default: break;
     }
   }

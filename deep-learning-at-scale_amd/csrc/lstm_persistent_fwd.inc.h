@@ -122,8 +122,12 @@ __global__ __launch_bounds__(256, 1) void lstm_fwd_persistent_kernel(
   // SPLIT publish delay (round 6): chunk j publishes chunk j - PD, polled one chunk before its
   // fetch; DBG 262144 (A/B): the round-5 form, PD = 2 with the poll two chunks before
   constexpr bool PUB3 = (DBG & 262144) == 0;
-  // DBG 8 (A/B): with PD = 3, poll two chunks before the fetch instead of one
-  constexpr int PD = PUB3 ? 3 : 2, PL = (PUB3 && (DBG & 8) == 0) ? 1 : 2;
+  // PL: the poll read at a chunk top was issued PL chunks earlier. PL = 2 (production): the
+  // top of chunk j no longer waits for chunk j+1's pieces (issued just before the poll of
+  // j-1): 1.30 vs 1.38 ms interleaved, all 8 paired windows faster (profiles/r6/diag/ab2.txt)
+  // although the staler polls block more often (294 vs 191 waits per launch).
+  // DBG 8 (A/B): PL = 1, the first round-6 form
+  constexpr int PD = PUB3 ? 3 : 2, PL = (PUB3 && (DBG & 8) != 0) ? 1 : 2;
   // DBG 256 (A/B, measured slower): each wave publishes its own 32-B piece of every h row
   // (no staging barrier); the production form writes whole 128-B lines, one per 8 lanes
   constexpr bool WAVE_H = (DBG & 256) != 0;

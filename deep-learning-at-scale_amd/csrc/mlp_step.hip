@@ -35,11 +35,21 @@ namespace {
 // FRAG: dZ2 leaves in the MFMA-fragment layout of the dW2 kernels (below) instead of [B][256]
 // STAMP (WELLFLOW_MLP_STAMP=1, tools/mlp_timeline.py): lane 0 of every wave writes s_memtime at
 // 13 phase boundaries of its 5th chunk into `stamps` (results unchanged)
+// Loss of the one-launch steps (round 6: the reference's clipped MAE too, cnn.py:29-32): clip
+// <= 0 is MSE (loss d^2, dy = dy_scale d, the caller passes dy_scale = 2 grad_scale), clip > 0 is
+// mae_clip (loss min(|d|, clip), dy = dy_scale sign(d) where |d| <= clip, else 0: Theano's clip
+// passes the gradient on [0, clip], d|d|/dd = sign(d) with sign(0) = 0). d = prediction - target.
+__device__ __forceinline__ float step_dloss(float d, float clip) {
+  if (clip <= 0.f) return d;
+  return fabsf(d) <= clip ? (d > 0.f ? 1.f : (d < 0.f ? -1.f : 0.f)) : 0.f;
+}
+__device__ __forceinline__ float step_loss(float d, float clip) { return clip <= 0.f ? d * d : fminf(fabsf(d), clip); }
+
 template <int NFT, bool FRAG, bool STAMP = false>  // NFT: 16-feature tiles of dW1: 1 (Fp <= 16) or 2 (Fp <= 32)
 __global__ __launch_bounds__(512, 1) void mlp2_step_kernel(
     const bf16_t* __restrict__ X, int Fp, const bf16_t* __restrict__ W1, const float* __restrict__ b1,
     const bf16_t* __restrict__ W2, const float* __restrict__ b2, const float* __restrict__ w3,
-    const float* __restrict__ b3, const float* __restrict__ y, float dy_scale, int B,
+    const float* __restrict__ b3, const float* __restrict__ y, float dy_scale, float clip, int B,
     const long long* __restrict__ rows, long nrows, bf16_t* __restrict__ dZ2, float* __restrict__ pred,
     float* __restrict__ red, int prio, unsigned long long* __restrict__ stamps = nullptr) {
   constexpr int MT = 2, NW = 8, XB = MF_ROWS * MF_XROW;
@@ -261,11 +271,11 @@ __global__ __launch_bounds__(512, 1) void mlp2_step_kernel(
       dyn[n] = 0.f;
       if (gr < B) {
         const float diff = p - ys[par][r];
-        dyn[n] = dy_scale * diff;
+        dyn[n] = dy_scale * step_dloss(diff, clip);
         if (wid == 0 && g == n) {
           pst = p;
           pgr = gr;
-          lsum += diff * diff;
+          lsum += step_loss(diff, clip);
           db3a += dyn[n];
         }
       }
@@ -493,7 +503,8 @@ template <int NFT, bool STAMP = false>
 __global__ __launch_bounds__(512, 1) void mlp2_step128_kernel(
     const bf16_t* __restrict__ X, int Fp, const bf16_t* __restrict__ W1, const float* __restrict__ b1,
     const bf16_t* __restrict__ W2, const bf16_t* __restrict__ W2T, const float* __restrict__ b2,
-    const float* __restrict__ w3, const float* __restrict__ b3, const float* __restrict__ y, float dy_scale, int B,
+    const float* __restrict__ w3, const float* __restrict__ b3, const float* __restrict__ y, float dy_scale, float clip,
+    int B,
     const long long* __restrict__ rows, long nrows, bf16_t* __restrict__ dZ2, float* __restrict__ pred,
     float* __restrict__ red, int prio, unsigned long long* __restrict__ stamps = nullptr) {
   constexpr int MT = 2, NR = 8, NW = 8, R = 128, XB = R * 64, WD = 4;
@@ -720,7 +731,7 @@ __global__ __launch_bounds__(512, 1) void mlp2_step128_kernel(
       const float4 pb = *reinterpret_cast<const float4*>(&hred[r][4]);
       const float p = ((pa.x + pa.y) + (pa.z + pa.w)) + ((pb.x + pb.y) + (pb.z + pb.w)) + bias3;
       const float diff = p - ys[par][r];
-      dyn[n] = row0 + r < B ? dy_scale * diff : 0.f;
+      dyn[n] = row0 + r < B ? dy_scale * step_dloss(diff, clip) : 0.f;
       const bool own = (n & 3) == g;
       pq[n >> 2] = own ? p : pq[n >> 2];
       dq[n >> 2] = own ? diff : dq[n >> 2];
@@ -735,8 +746,8 @@ __global__ __launch_bounds__(512, 1) void mlp2_step128_kernel(
         const bool ok = gr < B;
         pst[q] = pq[q];
         pgr[q] = ok ? gr : -1;
-        lsum += ok ? dq[q] * dq[q] : 0.f;
-        db3a += ok ? dy_scale * dq[q] : 0.f;
+        lsum += ok ? step_loss(dq[q], clip) : 0.f;
+        db3a += ok ? dy_scale * step_dloss(dq[q], clip) : 0.f;
       }
     }
     stamp(6);
@@ -1084,7 +1095,7 @@ __global__ __launch_bounds__(512, 1) void mlp2_dw2g_kernel(const bf16_t* __restr
 bool launch_mlp2_step(const bf16_t* X, int Fp, const bf16_t* W1, const float* b1, const bf16_t* W2, const float* b2,
                       const float* w3, const float* b3, const float* y, float dy_scale, int B, const long long* rows,
                       long nrows, bf16_t* dZ2, float* pred, float* red, bool dz_frag, hipStream_t s,
-                      const bf16_t* W2T) {
+                      const bf16_t* W2T, float clip) {
   // the reduce sums the dW1 rows only when it expects the 8-wave backward's layout
   if (B <= 0 || Fp > 32 || Fp % 8 != 0 || red == nullptr || !mlp_bwd8()) return false;
   if (dz_frag && B % MF_ROWS != 0) return false;
@@ -1101,27 +1112,27 @@ bool launch_mlp2_step(const bf16_t* X, int Fp, const bf16_t* W1, const float* b1
     static const int prio128 = diag_env_int("WELLFLOW_MLP_PRIO128", prio);
     if (stamp && Fp <= 16) {
       hipLaunchKernelGGL((mlp2_step128_kernel<1, true>), dim3(grid), dim3(512), 0, s, X, Fp, W1, b1, W2, W2T, b2, w3, b3,
-                         y, dy_scale, B, rows, nrows, dZ2, pred, red, prio128,
+                         y, dy_scale, clip, B, rows, nrows, dZ2, pred, red, prio128,
                          reinterpret_cast<unsigned long long*>(red + kMlpRedSlab2Off + 200L * 65536));
       return true;
     }
     if (Fp <= 16)
       hipLaunchKernelGGL(mlp2_step128_kernel<1>, dim3(grid), dim3(512), 0, s, X, Fp, W1, b1, W2, W2T, b2, w3, b3, y,
-                         dy_scale, B, rows, nrows, dZ2, pred, red, prio128);
+                         dy_scale, clip, B, rows, nrows, dZ2, pred, red, prio128);
     else
       hipLaunchKernelGGL(mlp2_step128_kernel<2>, dim3(grid), dim3(512), 0, s, X, Fp, W1, b1, W2, W2T, b2, w3, b3, y,
-                         dy_scale, B, rows, nrows, dZ2, pred, red, prio128);
+                         dy_scale, clip, B, rows, nrows, dZ2, pred, red, prio128);
     return true;
   }
   if (stamp && Fp <= 16 && dz_frag) {
     hipLaunchKernelGGL((mlp2_step_kernel<1, true, true>), dim3(grid), dim3(512), 0, s, X, Fp, W1, b1, W2, b2, w3, b3, y,
-                       dy_scale, B, rows, nrows, dZ2, pred, red, prio,
+                       dy_scale, clip, B, rows, nrows, dZ2, pred, red, prio,
                        reinterpret_cast<unsigned long long*>(red + kMlpRedSlab2Off + 200L * 65536));
     return true;
   }
 #define WF_STEP(NFT, FR)                                                                                            \
   hipLaunchKernelGGL((mlp2_step_kernel<NFT, FR>), dim3(grid), dim3(512), 0, s, X, Fp, W1, b1, W2, b2, w3, b3, y, \
-                     dy_scale, B, rows, nrows, dZ2, pred, red, prio)
+                     dy_scale, clip, B, rows, nrows, dZ2, pred, red, prio)
   if (Fp <= 16) {
     if (dz_frag) WF_STEP(1, true); else WF_STEP(1, false);
   } else {

@@ -132,8 +132,8 @@ def mlp_fast_path_reason(hidden, Fp: int, loss: str, B: int) -> str | None:
         return f"hidden {tuple(hidden)} is not the fused (256, 256) shape"
     if Fp > 32:
         return f"{Fp} padded input features > 32 (the one-launch step holds one 32-wide K tile of W1)"
-    if loss != "mse":
-        return f"loss {loss!r} is not fused into the one-launch step (mse only)"
+    if loss not in ("mse", "mae_clip"):
+        return f"loss {loss!r} is not fused into the one-launch step (mse, mae_clip)"
     if B % 64 != 0:
         return f"batch {B} is not a multiple of the 64-row tile"
     return None
@@ -174,6 +174,15 @@ class NativeMLP:
         bf = torch.bfloat16
         self.Fp = _r8(n_features)
         self.X = torch.zeros(batch * self.Fp, dtype=bf, device=dev)
+        # the MFMA input format: the Trainer keeps resident datasets in it (half the bytes of
+        # fp32, and the per-step gather IS the engine's input: no cast kernel)
+        self.input_dtype = torch.bfloat16 if self.Fp == n_features else torch.float32
+        self._Xop = self.X  # the X operand of the current step (self.X or a bf16 batch read in place)
+        self.Hs = [torch.empty(batch * h, dtype=bf, device=dev) for h in self.hidden]
+        self.dZ = [torch.empty(batch * h, dtype=bf, device=dev) for h in self.hidden]
+        self.pred = torch.empty(batch, device=dev)
+        self.dy = torch.empty(batch, device=dev)
+        self.loss_sum = torch.zeros(1, device=dev)
         # Paths (round 6: two env reads left, round-5 VERDICT weak #7). For the BASELINE shape
         # (hidden 256 x 256, Fp <= 32, MSE; mlp_fast_path_reason) a training step is the
         # one-launch step kernel in 128-row passes with W2 and W2^T streamed (csrc/mlp_step.hip
@@ -204,7 +213,7 @@ class NativeMLP:
         # transposed bf16 copy, written with the shadow); WELLFLOW_MLP_STEP128=0 (A/B,
         # tools/mlp_timeline.py): 64-row passes with W2^T in registers
         self.w2t = None
-        if self.red is not None and os.environ.get("WELLFLOW_MLP_STEP128", "1") != "0":
+        if self.red is not None and self.dw2_frag and os.environ.get("WELLFLOW_MLP_STEP128", "1") != "0":
             self.w2t = torch.empty(256 * 256, dtype=bf, device=dev)
         self.sync_weights()
 
@@ -243,8 +252,10 @@ class NativeMLP:
             if red is not None and self.step_fused and not self.dw2_gemm:
                 frag = self.dw2_frag
                 w2t = self.w2t if frag else None
+                mae = self.loss_kind == "mae_clip"  # dy = grad_scale sign(d) [|d| <= clip]; MSE 2 grad_scale d
                 if not C.mlp2_step(Xop, self.Fp, wl[0][0], pl[0][1], wl[1][0], pl[1][1], hw, hb, y,
-                                   2.0 * float(grad_scale), B, rows, self.dZ[1], self.pred, red, frag, w2t):
+                                   (1.0 if mae else 2.0) * float(grad_scale), B, rows, self.dZ[1], self.pred, red,
+                                   frag, w2t, float(self.clip) if mae else 0.0):
                     raise RuntimeError("NativeMLP: fused step refused the shape")
                 if frag:  # dW2 partials as slab rows (their count) summed by the reduce
                     ok = dw2_rows = C.mlp2_dw2f(self.dZ[1], Xop, self.Fp, rows, wl[0][0], pl[0][1], B,
@@ -342,6 +353,12 @@ class NativeMLP:
         if why is not None:
             note_slow_path("MLP", "training step runs the multi-launch path", why,
                            f"F={self.F} hidden={self.hidden} B={B} loss={self.loss_kind}")
+            return False
+        if self.loss_kind != "mse" and (self.red is None or not self.step_fused):
+            # the clipped MAE is fused into the one-launch step only (not the kernel pair)
+            note_slow_path("MLP", "training step runs the multi-launch path",
+                           f"loss {self.loss_kind!r} needs the one-launch step (WELLFLOW_MLP_SPREAD=0 set)",
+                           f"F={self.F} hidden={self.hidden} B={B}")
             return False
         return self.recompute_h1 and self.fused and self.fused_bwd and self.mask_h2
 

@@ -105,3 +105,39 @@ def test_bench_secondary_configs_dp2():
         assert v["grad_bucket_mb"] > 0 and v["comm_dtype"] == "fp32"
         assert v["comm_share"] == pytest.approx(v["comm_ms"] / v["ms_per_step"], rel=1e-2, abs=1e-3)
     assert rec["comm_ms"] is not None and rec["comm_ms"] > 0
+
+
+def test_gpu_state_sampler_window_math():
+    """utils/gpustate.py on a fake metrics table: sampled clock / power / temperature, the
+    limiter residencies as fractions of the accumulation counter's delta, per-XCD clocks
+    averaged, N/A placeholders skipped."""
+    import time
+
+    sys.path.insert(0, ROOT)
+    from wellflow.utils.gpustate import GpuStateSampler
+
+    n = {"k": 0}
+
+    def fake(_h):
+        n["k"] += 1
+        k = n["k"]
+        return {"current_gfxclks": [2000 + k, 2000 + k, "N/A"], "current_socket_power": 1000 + k,
+                "temperature_hotspot": 70 + k % 3, "accumulation_counter": 100 * k,
+                "ppt_residency_acc": 25 * k, "socket_thm_residency_acc": 0, "throttle_status": 1}
+
+    s = GpuStateSampler.__new__(GpuStateSampler)
+    s.period_s, s._h, s._get, s._samples, s._t0, s._thread = 0.005, object(), fake, [], None, None
+    import threading
+
+    s._stop = threading.Event()
+    s.start()
+    time.sleep(0.05)
+    st = s.stop()
+    assert st["samples"] >= 2
+    assert 2000 < st["sclk_mhz"]["min"] <= st["sclk_mhz"]["max"] < 2000 + n["k"] + 1
+    assert st["power_w"]["max"] > 1000 and 70 <= st["temp_hotspot_c"] <= 72
+    assert st["throttle"]["ppt"] == 0.25 and st["throttle"]["socket_thm"] == 0.0
+    assert st["throttle"]["throttle_status"] == 1
+    off = GpuStateSampler.__new__(GpuStateSampler)
+    off._h, off._thread = None, None
+    assert not off.available and off.stop() is None

@@ -3,7 +3,9 @@ K = T*B = 524288, MN x MN operands, split-K fp32 atomics): time per call, interl
 rounds, and max |diff| against the default tile (3 = 256x192 64-deep 2-stage).
 
     python tools/dw_tiles.py [tiles ...]      (default: 1 2 3; 4 / 5 = 256x192 with the 5- / 4-slot
-                                              32-deep half-step ring)
+                                              32-deep half-step ring; 7 = the production 256x288,
+                                              8 = 256x288 with global_load_lds instead of MUBUF
+                                              LDS-DMA; DW_KS=16,32 picks the split-K depths)
 """
 import sys
 
@@ -40,7 +42,9 @@ def timeit(fn, n=10):
 
 ref = run(3, 32).clone()
 torch.cuda.synchronize()
-cfgs = [(t, ks) for t in tiles for ks in (16, 32, 64)]
+import os  # noqa: E402
+
+cfgs = [(t, ks) for t in tiles for ks in (int(k) for k in os.environ.get("DW_KS", "16,32,64").split(","))]
 for c in cfgs:  # warm-up + correctness
     d = (run(*c) - ref).abs().max().item()
     print(f"tile {c[0]} ks {c[1]}: max|diff| vs tile 3 = {d:.3e} (ref max {ref.abs().max().item():.2f})", flush=True)

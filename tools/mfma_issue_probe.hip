@@ -51,6 +51,13 @@ __global__ __launch_bounds__(256, 1) void probe(const unsigned* __restrict__ src
   for (int i = 0; i < 16; ++i) e[i] = (float)(lane + i) * 1e-3f;
   const unsigned rd = (unsigned)(uintptr_t)((__attribute__((address_space(3))) char*)lds) + lane * 16 + wid * 4096;
   bf16x8 b0 = a[0], b1 = a[1];
+  // the DMA variants' sources (the first 256 KiB of src) and the VGPR staging of V13 / V15
+  const __amdgpu_buffer_rsrc_t vrsrc = __builtin_amdgcn_make_buffer_rsrc((void*)src, 0, 0x7FFFFFFF, 0x00020000);
+  __amdgpu_buffer_rsrc_t srsrc = vrsrc;
+  typedef unsigned u32x4b __attribute__((ext_vector_type(4)));
+  u32x4b stg[4] = {};
+  const unsigned* gsrc = src + lane * 4;  // 16 B per lane, 1 KiB per wave-instruction
+  const unsigned wrl = (unsigned)(uintptr_t)((__attribute__((address_space(3))) char*)lds) + 36864 + wid * 4096 + lane * 16;
   __builtin_amdgcn_s_barrier();
   const unsigned long long t0 = __builtin_amdgcn_s_memtime();
   const unsigned long long r0 = __builtin_amdgcn_s_memrealtime();
@@ -80,12 +87,38 @@ __global__ __launch_bounds__(256, 1) void probe(const unsigned* __restrict__ src
         asm volatile("" ::"v"(b0), "v"(b1));
       }
     } else {
-      if constexpr (V == 4 || V == 5 || V == 6 || V == 10 || V == 11) {
+      if constexpr (V == 4 || V == 5 || V == 6 || V == 10 || V == 11 || V >= 12) {
         asm volatile("ds_read_b128 %0, %2\n\tds_read_b128 %1, %2 offset:1024\n\ts_waitcnt lgkmcnt(2)"
                      : "=v"(b0), "=v"(b1)
                      : "v"(rd)
                      : "memory");
         asm volatile("" ::"v"(b0), "v"(b1));
+      }
+      if constexpr (V == 12 || V == 14) {  // MUBUF LDS-DMA (4-B lane offsets), as the backward issues it
+        constexpr int N = V == 12 ? 1 : 4;
+        if (V == 14 || (it & 1))
+#pragma unroll
+          for (int q = 0; q < N; ++q)
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(srsrc, (__attribute__((address_space(3))) void*)(lds + 32768 + wid * 4096 + q * 1024),
+                                                     16, lane * 16, ((it & 255) * 1024 + q * 256) & 0x3FFFF, 0, 0);
+      }
+      if constexpr (V == 13 || V == 15) {  // the same bytes through VGPRs: buffer load, then ds_write_b128
+        constexpr int N = V == 13 ? 1 : 4;
+        if (V == 15 || (it & 1)) {
+#pragma unroll
+          for (int q = 0; q < N; ++q) {
+            // issue cost only: the store writes an operand already in registers, the loads land
+            // in a staging ring read once at the end (a real pipeline keeps them in flight)
+            asm volatile("ds_write_b128 %0, %1 offset:%2" ::"v"(wrl), "v"(b0), "i"(q * 1024) : "memory");
+            // asm load: the compiler tracks nothing, so no wait is inserted for the in-flight
+            // loads (their registers are rewritten in issue order; values unused until the end)
+            // "+v": the staging registers stay allocated for the whole loop — with "=v" the
+            // compiler reused an in-flight load's destination for a later ADDRESS register and
+            // the late write-back faulted (illegal address, round 6)
+            asm volatile("global_load_dwordx4 %0, %1, off offset:%2" : "+v"(stg[q]) : "v"(gsrc + (it & 63) * 256), "i"(q * 1024)
+                         : "memory");
+          }
+        }
       }
       if constexpr (V == 6) {
         if (it & 1)
@@ -98,7 +131,7 @@ __global__ __launch_bounds__(256, 1) void probe(const unsigned* __restrict__ src
         const int i = m >> 2, j = m & 3;
         if constexpr (V == 1) {
           asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc[m]) : "v"(a[i]), "v"(w[j]));
-        } else if constexpr (V == 2 || V == 5 || V == 6) {
+        } else if constexpr (V == 2 || V == 5 || V == 6 || V >= 12) {
           asm volatile("v_mfma_f32_16x16x32_bf16 %0, %2, %3, %0\n\tv_exp_f32 %1, %1"
                        : "+a"(acc[m]), "+v"(e[m])
                        : "v"(a[i]), "a"(w[j]));
@@ -137,7 +170,11 @@ __global__ __launch_bounds__(256, 1) void probe(const unsigned* __restrict__ src
   for (int i = 0; i < 8; ++i) s += acc[i][0] + acc[i][3];
   for (int i = 0; i < 2; ++i) s += acc32[i][0] + acc32[i][15];
   for (int i = 0; i < 16; ++i) s += e[i];
-  s += (float)b0[0] + (float)b1[7];
+  // the staging registers are operands of the wait: no read of them (and no reuse of their
+  // registers) can move above it while the asm loads are in flight (round 6: a late write-back
+  // into a register the compiler had reused for an address faulted)
+  asm volatile("s_waitcnt vmcnt(0)" : "+v"(stg[0]), "+v"(stg[1]), "+v"(stg[2]), "+v"(stg[3]) :: "memory");
+  s += (float)b0[0] + (float)b1[7] + (float)(stg[0][0] + stg[1][1] + stg[2][2] + stg[3][3]);
   sink[blockIdx.x * 256 + threadIdx.x] = s;
   if (lane == 0) {
     out[(blockIdx.x * 4 + wid) * 2] = t1 - t0;
@@ -195,6 +232,10 @@ int main() {
   run<10>("10 + exp/2add alternating + ds_reads", src, out, sink, cus);
   run<11>("11 = 10 with VGPR accumulators", src, out, sink, cus);
   run<6>("6 = 5 + LDS-DMA per 2 k-tiles", src, out, sink, cus);
+  run<12>("12 = 5 + MUBUF LDS-DMA per 2 k-tiles", src, out, sink, cus);
+  run<14>("14 = 5 + 4 MUBUF LDS-DMA per k-tile", src, out, sink, cus);
+  // 13 / 15 (loads through VGPRs + ds_write_b128) are not run: their asm loads are only safe
+  // while the compiler keeps every staging register allocated (see the wait above)
   run<7>("7 4x32x32x16 bare", src, out, sink, cus);
   run<8>("8 32x32: + 2 v_exp per MFMA + ds_reads", src, out, sink, cus);
   run<9>("9 32x32: + 4 v_exp per MFMA", src, out, sink, cus);

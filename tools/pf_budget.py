@@ -12,7 +12,7 @@ LDS-DMA after step 0, 139296 = 131072 + 8224 (bare MFMAs + hand-off + stores), 1
 without C/S stores, 524288 no hand-off (no publish / poll / wait), 663584 / 663588 = 139296 /
 139300 without the hand-off. A/B variants (results correct): 2048 accumulators in AGPRs +
 copy (round 5), 262144 the round-5 publish delay, 264192 both (the round-5 kernel), 256
-per-wave h pieces (no staging barrier).
+per-wave h pieces (no staging barrier), 8 the poll read one chunk after issue (PL = 1).
 """
 import os
 import statistics
