@@ -549,7 +549,7 @@ void mlp2_reduce(const at::Tensor& red, int64_t Fp, int64_t B, c10::optional<at:
   constexpr int64_t H = 256;
   check_t(red, at::kFloat, "red");
   check_extent(red, wf::kMlpRedFloats, "red");
-  TORCH_CHECK(Fp > 0 && Fp <= 32, "mlp2_reduce: Fp <= 32");
+  TORCH_CHECK(Fp > 0 && Fp <= 64, "mlp2_reduce: Fp <= 64");
   for (const at::Tensor* t : {&dw3, &db1, &db2}) {
     check_t(*t, at::kFloat, "dw3/db");
     check_extent(*t, H, "dw3/db");

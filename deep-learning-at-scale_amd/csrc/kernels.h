@@ -103,14 +103,15 @@ bool launch_mlp2_bwd(const bf16_t* H1, const bf16_t* H2, const unsigned* M2, con
 bool launch_mlp2_dw2(const bf16_t* dZ2, const bf16_t* X, int Fp, const long long* rows, long nrows, const bf16_t* W1,
                      const float* b1, int B, int nsplit, float* dW2, hipStream_t s, float* red = nullptr);
 // Spread-reduction scratch (floats): kMlpRedCopies rows of kMlpRedRow slots — [loss, db3,
-// dw3[256], db1[256], db2[256], dW1[256 x Fp]] — then kMlpRedCopies2 copies of dW2 [256 x 256].
+// dw3[256], db1[256], db2[256]] (slots from kMlpRedDW1 on are unused: every dW1 goes out as the
+// per-workgroup rows below) — then kMlpRedCopies2 copies of dW2 [256 x 256].
 // Zero-initialised once; mlp2_reduce sums every copy into the gradients and zeroes it again.
 constexpr int kMlpRedCopies = 64, kMlpRedCopies2 = 4, kMlpRedRow = 9216;
 constexpr int kMlpRedLoss = 0, kMlpRedDb3 = 1, kMlpRedDw3 = 2, kMlpRedDb1 = 258, kMlpRedDb2 = 514, kMlpRedDW1 = 770;
 // then the backward's per-workgroup dW1 rows: [kMlpRedSlabRows][kMlpRedSlabRow] (plain stores,
 // summed over the launch's grid by the reduce: dW1 is 4096 values per workgroup, too many
 // atomic wave-instructions per CU even spread over copies)
-constexpr int kMlpRedSlabRows = 256, kMlpRedSlabRow = 256 * 32;
+constexpr int kMlpRedSlabRows = 256, kMlpRedSlabRow = 256 * 64;  // Fp <= 64
 constexpr long kMlpRedSlabOff = (long)kMlpRedCopies * kMlpRedRow + (long)kMlpRedCopies2 * 65536;
 // then the dW2 rows of the fragment-layout dW2 kernel: [kMlpRedSlab2Rows][256 x 256] (plain
 // stores of each workgroup's partial tile, summed by the reduce: 8M float atomics per step

@@ -91,7 +91,7 @@ __global__ __launch_bounds__(256) void mlp2_reduce_kernel(float* __restrict__ re
     }
     return;
   }
-  const int na = kMlpRedDW1 + 256 * Fp;
+  const int na = kMlpRedDW1;         // the small sums (no dW1 in the copies)
   const int nA = (na + 255) / 256;  // blocks of the small sums
   const int bx = (int)blockIdx.x - slab_blocks;
   if (bx < nA) {
@@ -107,8 +107,7 @@ __global__ __launch_bounds__(256) void mlp2_reduce_kernel(float* __restrict__ re
                  : i == kMlpRedDb3 ? db3
                  : i < kMlpRedDb1  ? (dw3 != nullptr ? dw3 + (i - kMlpRedDw3) : nullptr)
                  : i < kMlpRedDb2  ? (db1 != nullptr ? db1 + (i - kMlpRedDb1) : nullptr)
-                 : i < kMlpRedDW1  ? (db2 != nullptr ? db2 + (i - kMlpRedDb2) : nullptr)
-                                   : (dW1 != nullptr ? dW1 + (i - kMlpRedDW1) : nullptr);
+                                   : (db2 != nullptr ? db2 + (i - kMlpRedDb2) : nullptr);
     if (dst != nullptr && v != 0.f) *dst += v;
     return;
   }
@@ -162,7 +161,7 @@ int mlp2_train_grid(int B) {
 
 void launch_mlp2_reduce(float* red, int Fp, int B, float* loss_sum, float* db3, float* dw3, float* db1, float* db2,
                         float* dW1, float* dW2, hipStream_t s, int dw2_rows) {
-  const int na = kMlpRedDW1 + 256 * Fp;
+  const int na = kMlpRedDW1;
   // the dW1 rows exist only when the 8-wave backward ran (the 4-wave one adds dW1 itself)
   const int slab_blocks = mlp_bwd8() ? (256 * Fp + 15) / 16 : 0;
   hipLaunchKernelGGL(mlp2_reduce_kernel, dim3(slab_blocks + (na + 255) / 256 + 65536 / 64), dim3(256), 0, s, red, Fp,

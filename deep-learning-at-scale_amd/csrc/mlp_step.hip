@@ -474,8 +474,19 @@ __global__ __launch_bounds__(512, 1) void mlp2_step_kernel(
 // WD = 4 slots ahead; 16 % WD == 0 keeps every slot index static). Batch sums live in registers
 // (the 48-KiB LDS sum block of the 64-row kernel does not fit beside the 128-row tiles).
 // LDS: X (double-buffered, 64-B rows, Fp <= 32) 16 KiB + H1 64 KiB + dZ2 64 KiB + head 4 KiB.
+// Fp <= 64 (NFT = 4, round 6): 128-B X rows, two layer-1 K steps and ONE X buffer (two would
+// not fit beside H1 and dZ2), staged at the top of each pass between two barriers.
 // Rows past B are masked (dy = 0, no stores); FRAG fragments of rows >= B are not written.
 __device__ __forceinline__ int x4_off(int row, int chunk) { return row * 64 + ((chunk ^ ((row >> 2) & 3)) << 4); }
+// 128-B rows: 16-B chunk c of row r at slot c ^ ((r >> 1) & 7), so the layer-1 fragment reads
+// (rows 16n + l15, chunks g / g + 4) hit 16 distinct 16-B slots in every ds_read_b128 lane group
+template <int XW>
+__device__ __forceinline__ int x_off(int row, int chunk) {
+  if constexpr (XW == 64)
+    return x4_off(row, chunk);
+  else
+    return row * 128 + ((chunk ^ ((row >> 1) & 7)) << 4);
+}
 
 // Packed-bf16 epilogue helpers of the 128-row kernel (round 5: its passes were VALU-bound —
 // 1.5k VALU vs 280 MFMA per wave and pass, 20 % MFMA busy, profiles/r5/pmc_mlp):
@@ -499,7 +510,7 @@ __device__ __forceinline__ f32x2_t bf_lo_hi(unsigned q) {  // packed bf16 pair -
 
 // STAMP (WELLFLOW_MLP_STAMP=1 in a WF_DIAG build, tools/mlp_timeline.py --k128): lane 0 of every
 // wave writes s_memtime at 13 phase boundaries of its 3rd pass into `stamps` (results unchanged)
-template <int NFT, bool STAMP = false>
+template <int NFT, bool STAMP = false>  // NFT: 16-feature tiles of dW1: 1, 2 or 4 (Fp <= 16 / 32 / 64)
 __global__ __launch_bounds__(512, 1) void mlp2_step128_kernel(
     const bf16_t* __restrict__ X, int Fp, const bf16_t* __restrict__ W1, const float* __restrict__ b1,
     const bf16_t* __restrict__ W2, const bf16_t* __restrict__ W2T, const float* __restrict__ b2,
@@ -507,9 +518,12 @@ __global__ __launch_bounds__(512, 1) void mlp2_step128_kernel(
     int B,
     const long long* __restrict__ rows, long nrows, bf16_t* __restrict__ dZ2, float* __restrict__ pred,
     float* __restrict__ red, int prio, unsigned long long* __restrict__ stamps = nullptr) {
-  constexpr int MT = 2, NR = 8, NW = 8, R = 128, XB = R * 64, WD = 4;
+  constexpr int MT = 2, NR = 8, NW = 8, R = 128, WD = 4;
+  constexpr int KT1 = NFT > 2 ? 2 : 1;  // layer-1 K steps of 32 features
+  constexpr bool SB = KT1 == 2;         // one X buffer, staged at the pass top
+  constexpr int XW = 64 * KT1, CPR = XW / 16, XB = R * XW, NP = R * CPR / 512;  // row bytes, chunks / row, pieces / thread
   static_assert(16 % WD == 0, "stream slots must repeat every pass");
-  __shared__ __attribute__((aligned(16))) char xs[2 * XB];          // X tiles (double-buffered)
+  __shared__ __attribute__((aligned(16))) char xs[(SB ? 1 : 2) * XB];  // X tiles (double-buffered for KT1 = 1)
   __shared__ __attribute__((aligned(16))) char h1s[R * MF_H * 2];   // H1 -> dZ1 (own columns)
   __shared__ __attribute__((aligned(16))) char zs[R * MF_H * 2];    // dZ2
   __shared__ __attribute__((aligned(16))) float hred[R][NW + 4];    // head partials (48-B rows: conflict-free float4 reads)
@@ -523,13 +537,20 @@ __global__ __launch_bounds__(512, 1) void mlp2_step128_kernel(
   const int tq = l15 >> 2, tp = lane & 3;  // ds_read_b64_tr_b16 lane coordinates
   for (int i = tid; i < 3 * MF_H; i += 64 * NW) cst[i / MF_H][i % MF_H] = (i < MF_H ? b1 : i < 2 * MF_H ? b2 : w3)[i % MF_H];
 
-  bf16x8 w1f[MT];
+  // W1 fragments: resident for KT1 = 1; KT1 = 2 re-reads them (L2) at every pass top so their
+  // 16 VGPRs are free through the stream loops (resident, the kernel spilled 73 VGPRs)
+  bf16x8 w1f[MT][KT1];
+  auto load_w1 = [&](int z) {
 #pragma unroll
-  for (int m = 0; m < MT; ++m) {
-    const int u = u0 + 16 * m + l15;
-    w1f[m] = 8 * g + 8 <= Fp ? *reinterpret_cast<const bf16x8*>(W1 + (size_t)u * Fp + 8 * g)
-                             : bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
-  }
+    for (int m = 0; m < MT; ++m)
+#pragma unroll
+      for (int k = 0; k < KT1; ++k) {
+        const int u = u0 + 16 * m + l15, f = 32 * k + 8 * g;
+        w1f[m][k] = f + 8 <= Fp ? *reinterpret_cast<const bf16x8*>(W1 + (size_t)(u * Fp + f + z))
+                                : bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
+      }
+  };
+  if constexpr (!SB) load_w1(0);
   // the fragment stream: step s < 8 = W2 K-step s (layer 2), 8 <= s < 16 = W2^T K-step s - 8
   // (dH1); lane fragment (m, kt) = 16 B at row u0 + 16m + l15, columns 32kt + 8g (both images
   // are [256][256] row-major, so one offset formula serves both resources)
@@ -572,30 +593,46 @@ __global__ __launch_bounds__(512, 1) void mlp2_step128_kernel(
   const float bias3 = b3[0];
   float lsum = 0.f, db3a = 0.f;
 
-  // next pass's inputs: thread t one 16-B X segment (row t >> 2, chunk t & 3), threads 4r the
-  // target of row r. Row-indexed batches (rows != nullptr, nrows < 2^31): a pass's dataset row
+  // next pass's inputs: thread t NP 16-B X segments (piece t + 512k: row (t + 512k) / CPR, chunk
+  // t % CPR), the chunk-0 threads the target of their row. Row-indexed batches (rows != nullptr, nrows < 2^31): a pass's dataset row
   // ids are loaded one pass before its gathers — loaded right before them, the dependent wait
   // after B4 also drained every W2^T stream fragment in flight
-  uint4 xv = make_uint4(0, 0, 0, 0);
-  float yv = 0.f;
-  int ixn = 0;  // clamped row id (row t >> 2) of the pass the next prefetch() gathers
+  uint4 xv[NP];
+  float yv[NP];
+  int ixn[NP];  // clamped row ids (of the piece rows) of the pass the next prefetch() gathers
+#pragma unroll
+  for (int k = 0; k < NP; ++k) {
+    xv[k] = make_uint4(0, 0, 0, 0);
+    yv[k] = 0.f;
+    ixn[k] = 0;
+  }
   auto fetch_ids = [&](int ps, int tid) {
     if (rows != nullptr) {
-      const int gr = ps * R + (tid >> 2);
-      const long long r = gr < B ? rows[gr] : 0;
-      ixn = (int)(r < 0 ? 0 : (r >= nrows ? nrows - 1 : r));
+#pragma unroll
+      for (int k = 0; k < NP; ++k) {
+        const int gr = ps * R + (tid + 512 * k) / CPR;
+        const long long r = gr < B ? rows[gr] : 0;
+        ixn[k] = (int)(r < 0 ? 0 : (r >= nrows ? nrows - 1 : r));
+      }
     }
   };
   auto prefetch = [&](int ps, int tid) {
-    const int r = tid >> 2, c = tid & 3, gr = ps * R + r;
-    const size_t xr = rows != nullptr ? (size_t)ixn : (size_t)gr;
-    xv = (gr < B && 8 * c + 8 <= Fp) ? *reinterpret_cast<const uint4*>(X + xr * Fp + 8 * c) : make_uint4(0, 0, 0, 0);
-    if (c == 0) yv = gr < B ? y[xr] : 0.f;
+#pragma unroll
+    for (int k = 0; k < NP; ++k) {
+      const int r = (tid + 512 * k) / CPR, c = tid % CPR, gr = ps * R + r;
+      const size_t xr = rows != nullptr ? (size_t)ixn[k] : (size_t)gr;
+      xv[k] = (gr < B && 8 * c + 8 <= Fp) ? *reinterpret_cast<const uint4*>(X + xr * Fp + 8 * c) : make_uint4(0, 0, 0, 0);
+      if (c == 0) yv[k] = gr < B ? y[xr] : 0.f;
+    }
   };
   const int npass = (B + R - 1) / R;
   auto stage = [&](int p, int tid) {
-    *reinterpret_cast<uint4*>(xs + p * XB + x4_off(tid >> 2, tid & 3)) = xv;
-    if ((tid & 3) == 0) ys[p][tid >> 2] = yv;
+#pragma unroll
+    for (int k = 0; k < NP; ++k) {
+      const int r = (tid + 512 * k) / CPR, c = tid % CPR;
+      *reinterpret_cast<uint4*>(xs + p * XB + x_off<XW>(r, c)) = xv[k];
+      if (c == 0) ys[p][r] = yv[k];
+    }
   };
   const int G = gridDim.x;
   if ((int)blockIdx.x < npass) {
@@ -604,11 +641,15 @@ __global__ __launch_bounds__(512, 1) void mlp2_step128_kernel(
   }
   stage(0, tid);
   __syncthreads();
-  if ((int)blockIdx.x + G < npass) {
-    fetch_ids(blockIdx.x + G, tid);
-    prefetch(blockIdx.x + G, tid);
+  if constexpr (SB) {  // pass b + G is prefetched after B4 of pass b
+    if ((int)blockIdx.x + G < npass) fetch_ids(blockIdx.x + G, tid);
+  } else {
+    if ((int)blockIdx.x + G < npass) {
+      fetch_ids(blockIdx.x + G, tid);
+      prefetch(blockIdx.x + G, tid);
+    }
+    if ((int)blockIdx.x + 2 * G < npass) fetch_ids(blockIdx.x + 2 * G, tid);
   }
-  if ((int)blockIdx.x + 2 * G < npass) fetch_ids(blockIdx.x + 2 * G, tid);
   wfirst();
   if (prio && __builtin_amdgcn_readfirstlane(wid) >= 4) __builtin_amdgcn_s_setprio(1);
   int par = 0;
@@ -620,8 +661,19 @@ __global__ __launch_bounds__(512, 1) void mlp2_step128_kernel(
           stamps[((size_t)blockIdx.x * NW + wid) * 16 + k] = __builtin_amdgcn_s_memtime();
       }
     };
+    if constexpr (SB) {
+      int w1z = 0;  // laundered zero: the loads stay in the loop (hoisted they pin 16 VGPRs)
+      asm volatile("" : "+s"(w1z));
+      load_w1(w1z);
+      if (ps != (int)blockIdx.x) {  // every wave's dW1 reads of the previous X are done: stage
+        __syncthreads();
+        stage(0, tid);
+        __syncthreads();
+      }
+    }
+    const int xbuf = SB ? 0 : par;  // this pass's X / target buffer
     stamp(0);
-    char* xt = xs + par * XB;
+    char* xt = xs + xbuf * XB;
     // the lane coordinates, laundered per pass: every LDS address below derives from them, and
     // as loop invariants the compiler hoisted ~40 swizzled addresses out of the pass loop and
     // spilled them (one VGPR each); recomputed here they live for one phase
@@ -641,9 +693,14 @@ __global__ __launch_bounds__(512, 1) void mlp2_step128_kernel(
       }
 #pragma unroll
       for (int n = 0; n < NR; ++n) {
-        const bf16x8 xb = *reinterpret_cast<const bf16x8*>(xt + x4_off(16 * n + l15, g));
+        bf16x8 xb[KT1];
 #pragma unroll
-        for (int m = 0; m < MT; ++m) acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w1f[m], xb, bv[m], 0, 0, 0);
+        for (int k = 0; k < KT1; ++k) xb[k] = *reinterpret_cast<const bf16x8*>(xt + x_off<XW>(16 * n + l15, g + 4 * k));
+#pragma unroll
+        for (int m = 0; m < MT; ++m) {
+          acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w1f[m][0], xb[0], bv[m], 0, 0, 0);
+          if constexpr (KT1 == 2) acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w1f[m][1], xb[1], acc[m][n], 0, 0, 0);
+        }
       }
     }
 #pragma unroll
@@ -730,7 +787,7 @@ __global__ __launch_bounds__(512, 1) void mlp2_step128_kernel(
       const float4 pa = *reinterpret_cast<const float4*>(&hred[r][0]);
       const float4 pb = *reinterpret_cast<const float4*>(&hred[r][4]);
       const float p = ((pa.x + pa.y) + (pa.z + pa.w)) + ((pb.x + pb.y) + (pb.z + pb.w)) + bias3;
-      const float diff = p - ys[par][r];
+      const float diff = p - ys[xbuf][r];
       dyn[n] = row0 + r < B ? dy_scale * step_dloss(diff, clip) : 0.f;
       const bool own = (n & 3) == g;
       pq[n >> 2] = own ? p : pq[n >> 2];
@@ -774,10 +831,14 @@ __global__ __launch_bounds__(512, 1) void mlp2_step128_kernel(
 #pragma unroll
     for (int m = 0; m < MT; ++m) asm volatile("" : "+v"(s3[m][0]), "+v"(s3[m][1]));
     asm volatile("" : "+v"(lsum), "+v"(db3a));
-    if (ps + G < npass) stage(par ^ 1, tdv);
+    if constexpr (!SB) {
+      if (ps + G < npass) stage(par ^ 1, tdv);
+    }
     stamp(7);
-    __syncthreads();  // B4: dZ2 complete, next pass's X / y staged
-    if (ps + 2 * G < npass) {
+    __syncthreads();  // B4: dZ2 complete, next pass's X / y staged (KT1 = 1)
+    if constexpr (SB) {
+      // (pass ps + G is prefetched after the dH1 stream below: its 8 X VGPRs not live there)
+    } else if (ps + 2 * G < npass) {
       prefetch(ps + 2 * G, tdv);
       if (ps + 3 * G < npass) fetch_ids(ps + 3 * G, tdv);
     }
@@ -807,6 +868,12 @@ __global__ __launch_bounds__(512, 1) void mlp2_step128_kernel(
 #pragma unroll
       for (int m = 0; m < MT; ++m) wr[(8 + kt) % WD][m] = wfrag((8 + kt + WD) & 15, m);
     });
+    if constexpr (SB) {
+      if (ps + G < npass) {
+        prefetch(ps + G, tdv);
+        if (ps + 2 * G < npass) fetch_ids(ps + 2 * G, tdv);
+      }
+    }
     // global stores only after the next pass's W2 requests (vmcnt counts stores, in order)
 #pragma unroll
     for (int q = 0; q < 2; ++q)
@@ -870,7 +937,7 @@ __global__ __launch_bounds__(512, 1) void mlp2_step128_kernel(
         for (int f = 0; f < NFT; ++f) {
           const int f0 = 16 * f + 4 * tp;
           const bf16x4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-              (lds_bf16x4*)(xt + x4_off(r, f0 >> 3) + ((f0 & 7) << 1)));
+              (lds_bf16x4*)(xt + x_off<XW>(r, f0 >> 3) + ((f0 & 7) << 1)));
 #pragma unroll
           for (int e = 0; e < 4; ++e) bfr[f][4 * h + e] = v[e];
         }
@@ -952,17 +1019,24 @@ constexpr int DW2F_MAX_ROWS = 2048;                      // rows per workgroup (
 // (out, in) element and their order are unchanged (bit-identical dW2), +0.4 % step rate.
 constexpr int DW2G_SLOTS = 6;  // 5 chunks in flight (128 KiB of LDS with the row-id table)
 constexpr int DW2G_ABYTES = 16 * 1024;                  // 2 steps x 8 dZ2 fragments
-constexpr int DW2G_SLOT = DW2G_ABYTES + MF_ROWS * 64;   // + X tile [64 rows][64 B]
+// + the X tile [64 rows][32 KT1 bf16]. KT1 = 2 (Fp <= 64, round 6): 128-B rows (6 slots: 152 KiB
+// of LDS with the row-id table), every wave DMAs one 8-row X piece per chunk, and the recompute
+// runs two K steps; chunk c of row r at slot c ^ (((r >> 1) & 1) | ((r >> 2) & 6)) (the rows one
+// ds_read_b128 lane group reads land on 16 distinct 16-B slots)
+template <int KT1>
+constexpr int dw2g_slot() { return DW2G_ABYTES + MF_ROWS * 64 * KT1; }
+template <int KT1>
 __global__ __launch_bounds__(512, 1) void mlp2_dw2g_kernel(const bf16_t* __restrict__ dZ2F, const bf16_t* __restrict__ X,
                                                            int Fp, const long long* __restrict__ rows, long nrows,
                                                            const bf16_t* __restrict__ W1, const float* __restrict__ b1,
                                                            int kchunk, float* __restrict__ dW2, float* __restrict__ slab,
                                                            int slab_row0, int prio) {
+  constexpr int DW2G_SLOT = dw2g_slot<KT1>(), XW = 64 * KT1;
   __shared__ __attribute__((aligned(16))) char smem[DW2G_SLOTS * DW2G_SLOT + DW2F_MAX_ROWS * 4];
   int* ridx = reinterpret_cast<int*>(smem + DW2G_SLOTS * DW2G_SLOT);
   const int tid = threadIdx.x, lane = tid & 63, l15 = lane & 15, g = lane >> 4;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const bool xw = wid < 4;  // this wave also DMAs one X piece per chunk
+  const bool xw = KT1 == 2 || wid < 4;  // this wave also DMAs one X piece per chunk
   const int L = xcd_remap(blockIdx.x, gridDim.x);
   const int split = L >> 1, t = L & 1;
   const int o0 = 128 * t, n0 = 32 * wid;
@@ -971,20 +1045,26 @@ __global__ __launch_bounds__(512, 1) void mlp2_dw2g_kernel(const bf16_t* __restr
   __syncthreads();
   if (prio && wid >= 4) __builtin_amdgcn_s_setprio(1);
 
-  bf16x8 w1f[2];
+  bf16x8 w1f[2][KT1];
   float bias[2];
 #pragma unroll
   for (int nb = 0; nb < 2; ++nb) {
     const int u = n0 + 16 * nb + l15;
-    w1f[nb] = 8 * g + 8 <= Fp ? *reinterpret_cast<const bf16x8*>(W1 + (size_t)u * Fp + 8 * g)
-                              : bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+    for (int k = 0; k < KT1; ++k) {
+      const int f = 32 * k + 8 * g;
+      w1f[nb][k] = f + 8 <= Fp ? *reinterpret_cast<const bf16x8*>(W1 + (size_t)u * Fp + f) : bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
+    }
     bias[nb] = b1[u];
   }
+  auto xswz = [](int r) { return KT1 == 1 ? (r >> 3) & 3 : ((r >> 1) & 1) | ((r >> 2) & 6); };
   // DMA sources. dZ2 fragments (S, b) of the tile: b = 8t + mb; wave w moves (step w >> 2,
   // blocks 8t + 2 (w & 3) + {0, 1})
   const bf16_t* zsrc = dZ2F + ((size_t)(kbeg >> 5) * 16 + 8 * t + 2 * (wid & 3)) * 512 + lane * 8;
-  const int xrow = 16 * (wid & 3) + (lane >> 2);
-  int xq = (lane & 3) ^ ((xrow >> 3) & 3);
+  // X piece of this wave: KT1 = 1 rows 16w + lane / 4 (waves 0-3), KT1 = 2 rows 8w + lane / 8;
+  // lane = the LDS slot, loading the chunk stored there (chunks past Fp: chunk 0, times zero W1)
+  const int xrow = KT1 == 1 ? 16 * (wid & 3) + (lane >> 2) : 8 * wid + (lane >> 3);
+  int xq = (lane & (4 * KT1 - 1)) ^ xswz(xrow);
   if (8 * xq + 8 > Fp) xq = 0;
   auto issue = [&](int c, int slot) {
     char* st = smem + slot * DW2G_SLOT;
@@ -1006,7 +1086,9 @@ __global__ __launch_bounds__(512, 1) void mlp2_dw2g_kernel(const bf16_t* __restr
     else
       wait_vmcnt<2 * n>();
   };
-  const int xg = 8 * g + 8 <= Fp ? g : 0;
+  int xg[KT1];
+#pragma unroll
+  for (int k = 0; k < KT1; ++k) xg[k] = 8 * (g + 4 * k) + 8 <= Fp ? g + 4 * k : 0;
   const int xr0 = 8 * (l15 >> 2) + (l15 & 3);
 
   f32x4 acc[8][2];
@@ -1025,12 +1107,14 @@ __global__ __launch_bounds__(512, 1) void mlp2_dw2g_kernel(const bf16_t* __restr
     asm volatile("" ::: "memory");
     issue(min(c + DW2G_SLOTS - 1, last), (c + DW2G_SLOTS - 1) % DW2G_SLOTS);
     const char* st = smem + slot * DW2G_SLOT;
-    bf16x8 xfa[2][2], afa[2][8];
+    bf16x8 xfa[2][2][KT1], afa[2][8];
     auto frags = [&](int s2) {
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
         const int r = 32 * s2 + xr0 + 4 * h;
-        xfa[s2][h] = *reinterpret_cast<const bf16x8*>(st + DW2G_ABYTES + r * 64 + ((xg ^ ((r >> 3) & 3)) << 4));
+#pragma unroll
+        for (int k = 0; k < KT1; ++k)
+          xfa[s2][h][k] = *reinterpret_cast<const bf16x8*>(st + DW2G_ABYTES + r * XW + ((xg[k] ^ xswz(r)) << 4));
       }
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
@@ -1042,13 +1126,18 @@ __global__ __launch_bounds__(512, 1) void mlp2_dw2g_kernel(const bf16_t* __restr
 #pragma unroll
     for (int s2 = 0; s2 < 2; ++s2) {
       bf16x8 hb[2];
-      const bf16x8(&xf)[2] = xfa[s2];
+      const bf16x8(&xf)[2][KT1] = xfa[s2];
 #pragma unroll
       for (int nb = 0; nb < 2; ++nb) {
         // b1 as the C operand and the ReLU on the packed pair: the step kernel's H1, bit for bit
+        // (the same K-step order)
         const f32x4 bc{bias[nb], bias[nb], bias[nb], bias[nb]};
-        const f32x4 c0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xf[0], w1f[nb], bc, 0, 0, 0);
-        const f32x4 c1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xf[1], w1f[nb], bc, 0, 0, 0);
+        f32x4 c0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xf[0][0], w1f[nb][0], bc, 0, 0, 0);
+        f32x4 c1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xf[1][0], w1f[nb][0], bc, 0, 0, 0);
+        if constexpr (KT1 == 2) {
+          c0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xf[0][1], w1f[nb][1], c0, 0, 0, 0);
+          c1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xf[1][1], w1f[nb][1], c1, 0, 0, 0);
+        }
         const unsigned p0 = relu_pk(pk_bf16(c0[0], c0[1]));
         const unsigned p1 = relu_pk(pk_bf16(c0[2], c0[3]));
         const unsigned p2 = relu_pk(pk_bf16(c1[0], c1[1]));
@@ -1097,8 +1186,9 @@ bool launch_mlp2_step(const bf16_t* X, int Fp, const bf16_t* W1, const float* b1
                       long nrows, bf16_t* dZ2, float* pred, float* red, bool dz_frag, hipStream_t s,
                       const bf16_t* W2T, float clip) {
   // the reduce sums the dW1 rows only when it expects the 8-wave backward's layout
-  if (B <= 0 || Fp > 32 || Fp % 8 != 0 || red == nullptr || !mlp_bwd8()) return false;
+  if (B <= 0 || Fp > 64 || Fp % 8 != 0 || red == nullptr || !mlp_bwd8()) return false;
   if (dz_frag && B % MF_ROWS != 0) return false;
+  if (Fp > 32 && (W2T == nullptr || !dz_frag)) return false;  // Fp <= 64: the 128-row kernel only
   const int grid = mlp2_train_grid(B);  // the dW1 rows mlp2_reduce sums
   // phase stamps (tools/mlp_timeline.py; results unchanged, so not a WF_DIAG-only switch):
   // into dW2 slab rows 200.. of the scratch (unused by a step of <= 200 dW2 ranges)
@@ -1119,8 +1209,11 @@ bool launch_mlp2_step(const bf16_t* X, int Fp, const bf16_t* W1, const float* b1
     if (Fp <= 16)
       hipLaunchKernelGGL(mlp2_step128_kernel<1>, dim3(grid), dim3(512), 0, s, X, Fp, W1, b1, W2, W2T, b2, w3, b3, y,
                          dy_scale, clip, B, rows, nrows, dZ2, pred, red, prio128);
-    else
+    else if (Fp <= 32)
       hipLaunchKernelGGL(mlp2_step128_kernel<2>, dim3(grid), dim3(512), 0, s, X, Fp, W1, b1, W2, W2T, b2, w3, b3, y,
+                         dy_scale, clip, B, rows, nrows, dZ2, pred, red, prio128);
+    else
+      hipLaunchKernelGGL(mlp2_step128_kernel<4>, dim3(grid), dim3(512), 0, s, X, Fp, W1, b1, W2, W2T, b2, w3, b3, y,
                          dy_scale, clip, B, rows, nrows, dZ2, pred, red, prio128);
     return true;
   }
@@ -1143,12 +1236,12 @@ bool launch_mlp2_step(const bf16_t* X, int Fp, const bf16_t* W1, const float* b1
 }
 
 // dW2 (the spread scratch's dW2 copies: red + kMlpRedCopies * kMlpRedRow) from the fragment-
-// layout dZ2; B % 64 == 0, Fp <= 32. nsplit row ranges (<= 128: two tiles per range, one
+// layout dZ2; B % 64 == 0, Fp <= 64. nsplit row ranges (<= 128: two tiles per range, one
 // workgroup per CU); batches beyond 128 ranges of DW2F_MAX_ROWS rows run as consecutive
 // launches over row blocks. False = not covered.
 int launch_mlp2_dw2f(const bf16_t* dZ2F, const bf16_t* X, int Fp, const long long* rows, long nrows, const bf16_t* W1,
                      const float* b1, int B, int nsplit, float* red, hipStream_t s) {
-  if (B <= 0 || B % MF_ROWS != 0 || Fp > 32 || Fp % 8 != 0 || red == nullptr) return 0;
+  if (B <= 0 || B % MF_ROWS != 0 || Fp > 64 || Fp % 8 != 0 || red == nullptr) return 0;
   constexpr int kMaxBlock = 128 * DW2F_MAX_ROWS;  // rows per launch
   // static s_setprio 1 for waves 4-7 (48.2 -> 47.0 us, +0.3 to +0.6 % in three interleaved pairs,
   // profiles/r4/mlp_prio; the WELLFLOW_DW2F_PRIO A/B knob was removed)
@@ -1163,7 +1256,7 @@ int launch_mlp2_dw2f(const bf16_t* dZ2F, const bf16_t* X, int Fp, const long lon
     const int kchunk = (chunks / ns) * MF_ROWS;
     if (kchunk > DW2F_MAX_ROWS) return 0;  // (unreachable for B % 64 == 0)
     // row block r0: dZ2 fragments start at step r0 / 32; X through `rows` (offset) or directly
-    hipLaunchKernelGGL(mlp2_dw2g_kernel, dim3(2 * ns), dim3(512), 0, s, dZ2F + (size_t)r0 * MF_H,
+    hipLaunchKernelGGL(Fp <= 32 ? mlp2_dw2g_kernel<1> : mlp2_dw2g_kernel<2>, dim3(2 * ns), dim3(512), 0, s, dZ2F + (size_t)r0 * MF_H,
                        rows != nullptr ? X : X + (size_t)r0 * Fp, Fp, rows != nullptr ? rows + r0 : nullptr,
                        rows != nullptr ? nrows : (long)Bb, W1, b1, kchunk, red + (size_t)kMlpRedCopies * kMlpRedRow,
                        red + kMlpRedSlab2Off, srow, prio);

@@ -201,7 +201,9 @@ def test_slow_path_notices_fire_once(capsys):
     assert mlp_fast_path_reason((256, 256), 16, "mse", 262144) is None
     assert mlp_fast_path_reason((256, 256), 32, "mse", 256) is None
     assert mlp_fast_path_reason((256, 256), 16, "mae_clip", 256) is None  # fused since round 6
-    for args, word in ((((256, 256), 48, "mse", 256), "features"), (((256, 256), 16, "huber", 256), "loss"),
+    assert mlp_fast_path_reason((256, 256), 48, "mse", 256) is None  # Fp <= 64 since round 6
+    assert mlp_fast_path_reason((256, 256), 64, "mae_clip", 256) is None
+    for args, word in ((((256, 256), 72, "mse", 256), "features"), (((256, 256), 16, "huber", 256), "loss"),
                        (((128, 128), 16, "mse", 256), "hidden"), (((256, 256), 16, "mse", 100), "batch")):
         why = mlp_fast_path_reason(*args)
         assert why is not None and word in why, (args, why)
@@ -209,8 +211,8 @@ def test_slow_path_notices_fire_once(capsys):
     assert cnn_fast_path_reason(CnnLayout(), 0.0) is None
     assert "channels" in cnn_fast_path_reason(CnnLayout(48, 16, 100, 13, 1), 0.5)
     assert "dropout" in cnn_fast_path_reason(CnnLayout(), 0.3)
-    why = mlp_fast_path_reason((256, 256), 48, "mse", 256)
-    assert note_slow_path("MLP", "training step runs the multi-launch path", why, "F=48 test")
-    assert not note_slow_path("MLP", "training step runs the multi-launch path", why, "F=48 test")  # once
+    why = mlp_fast_path_reason((256, 256), 72, "mse", 256)
+    assert note_slow_path("MLP", "training step runs the multi-launch path", why, "F=72 test")
+    assert not note_slow_path("MLP", "training step runs the multi-launch path", why, "F=72 test")  # once
     err = capsys.readouterr().err
-    assert err.count("wellflow: MLP training step runs the multi-launch path") == 1 and "48 padded" in err
+    assert err.count("wellflow: MLP training step runs the multi-launch path") == 1 and "72 padded" in err

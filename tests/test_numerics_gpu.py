@@ -91,14 +91,19 @@ def test_lstm_headline_adam_trajectory_within_2pct():
     assert res["pass"]
 
 
-def test_mlp_headline_shape_matches_fp32():
+@pytest.mark.parametrize("loss", ["mse", "mae_clip"])
+def test_mlp_headline_shape_matches_fp32(loss):
+    """The one-launch step at the bench shape vs fp32 torch; mae_clip (fused since round 6)
+    with a clip that cuts part of the batch off (zero gradient beyond it)."""
     from wellflow.data.synth import synth_tabular_batch
-    from wellflow.models.mlp import MLPRegressor, NativeMLP
+    from wellflow.models.base import per_element_loss
+    from wellflow.models.mlp import MLPRegressor, NativeMLP, mlp_fast_path_reason
 
-    B, F = 262144, 16
+    B, F, clip = 262144, 16, 1.0
     torch.manual_seed(0)
     ref = MLPRegressor(F, (256, 256)).to(DEV)
-    eng = NativeMLP(F, (256, 256), B, device=DEV)
+    eng = NativeMLP(F, (256, 256), B, device=DEV, loss=loss, clip=clip)
+    assert mlp_fast_path_reason((256, 256), F, loss, B) is None
     eng.params.copy_(ref.to_flat().to(DEV))
     eng.sync_weights()
     x, y = synth_tabular_batch(B, F, seed=11)
@@ -107,8 +112,11 @@ def test_mlp_headline_shape_matches_fp32():
     torch.cuda.synchronize()
     assert eng.fused and eng.fused_bwd and eng.mask_h2  # the bench configuration
     pred = ref(x)
-    L = ((pred - y) ** 2).sum()
+    L = per_element_loss(loss, pred, y, clip).sum()
     (L / B).backward()
+    if loss == "mae_clip":
+        cut = ((pred - y).abs() > clip).float().mean().item()
+        assert 0.01 < cut < 0.99, cut  # both branches of the clipped gradient exercised
     assert _rel(eng.pred[:B], pred.detach()) < 2e-2
     assert abs(ls - L.item()) <= 2e-2 * L.item()
     gref = MLPRegressor(F, (256, 256))
@@ -129,3 +137,51 @@ def test_secondary_trajectories_match_fp32(which):
     r = (mlp_adam_trajectory if which == "mlp" else cnn_sgd_trajectory)("cuda")
     assert r["step_graph"], r
     assert r["pass"], {k: v for k, v in r.items() if k not in ("native", "fp32")}
+
+
+@pytest.mark.parametrize("F,loss,B,indexed", [(48, "mse", 65536, False), (64, "mae_clip", 32768, False),
+                                              (40, "mse", 4160, False), (48, "mse", 16384, True)])
+def test_mlp_wide_features_one_launch_matches_fp32(F, loss, B, indexed):
+    """33-64 input features in the one-launch step (round 6, round-5 VERDICT item 4): 128-B X
+    rows, two layer-1 K steps, one X buffer, dW1 over four 16-feature tiles, and the dW2 kernel
+    recomputing H1 over two K steps; vs fp32 torch. B = 4160 ends in a half pass; the indexed
+    case gathers a resident bf16 dataset through the row ids inside both kernels."""
+    from wellflow.data.synth import synth_tabular_batch
+    from wellflow.models.base import per_element_loss
+    from wellflow.models.mlp import MLP_RED_COPY_FLOATS, MLPRegressor, NativeMLP, mlp_fast_path_reason
+
+    clip = 1.0
+    torch.manual_seed(3)
+    ref = MLPRegressor(F, (256, 256)).to(DEV)
+    eng = NativeMLP(F, (256, 256), B, device=DEV, loss=loss, clip=clip)
+    eng.params.copy_(ref.to_flat().to(DEV))
+    eng.sync_weights()
+    assert mlp_fast_path_reason((256, 256), eng.Fp, loss, B) is None and eng._recompute_ok(B)
+    N = 3 * B if indexed else B
+    X, Y = synth_tabular_batch(N, F, seed=12)
+    X, Y = X.to(DEV), Y.to(DEV)
+    if indexed:
+        X = X.to(torch.bfloat16)
+        idx = torch.randperm(N, device=DEV)[:B]
+        ls = eng.forward_backward(X, Y, grad_scale=1.0 / B, rows=idx).item()
+        x, y = X.index_select(0, idx).float(), Y.index_select(0, idx)
+    else:
+        ls = eng.forward_backward(X, Y, grad_scale=1.0 / B).item()
+        x, y = X, Y
+    torch.cuda.synchronize()
+    assert eng.red[:MLP_RED_COPY_FLOATS].abs().max().item() == 0.0  # the reduce re-zeroed the copies
+    pred = ref(x)
+    L = per_element_loss(loss, pred, y, clip).sum()
+    (L / B).backward()
+    assert _rel(eng.pred[:B], pred.detach()) < 2e-2
+    assert abs(ls - L.item()) <= 2e-2 * L.item()
+    gref = MLPRegressor(F, (256, 256))
+    for pr, pg in zip(gref.parameters(), ref.parameters()):
+        pr.data.copy_(pg.grad.cpu())
+    g_r = gref.to_flat().to(DEV)
+    r, c = _rel(eng.grads, g_r), _cos(eng.grads, g_r)
+    assert r < 3e-2 and c > 0.999, (r, c)
+    # dW1 (the four-tile slab) on its own: the block most changed by the wide path
+    n1 = 256 * F
+    r1 = _rel(eng.grads[:n1], g_r[:n1])
+    assert r1 < 3e-2, r1
