@@ -385,9 +385,27 @@ def bench_mlp(args, ctx, online: bool):
 
         run = StepRunner(eng, opt, ctx, gscale, inputs, graph=graph, comm_in_graph=not args.eager_comm)
         step = run.run
+        many = run.run_many
+        if ctx.world_size == 1 and not args.no_small and eng.small_steps_reason(B, opt) is None:
+            # small batches (<= 256 rows, one process): the Trainer's path — n complete steps
+            # (forward, backward, Adam) per persistent launch (NativeMLP.fused_steps); step i of
+            # a launch reads batch i % N of the resident set through row ids
+            # as the Trainer: up to 256 steps per launch (the timed window is one launch at <= 256 steps)
+            nmax = max(1, min(args.steps, 256))
+            ridx = torch.arange(nmax * B, device=ctx.device) % (B * nb)
+
+            def many(n):  # noqa: F811 - replaces the graph replay for this path
+                eng.fused_steps(x, y, B, n, opt, gscale, rows=ridx[: n * B], loss_into=run.loss_acc)
+
+            def step():  # noqa: F811
+                many(1)
+
+            extra["small_fused_steps_per_launch"] = nmax
     # the streamed config changes its input slot every step: single-step replays
-    el, k, n = _timed(ctx, step, args.steps, args.warmup, args.min_timed_s,
-                      None if online else run.run_many, args.graph_steps, warm_ms=args.warm_ms)
+    el, k, n = _timed(ctx, step, args.steps, args.warmup, args.min_timed_s, None if online else many,
+                      extra.get("small_fused_steps_per_launch", args.graph_steps), warm_ms=args.warm_ms)
+    if not online and "small_fused_steps_per_launch" in extra:
+        eng.check_device_errors()
     if online:
         extra.update(streamer.copy_stats(skip=1))
         extra["h2d_mb_per_step"] = round((streamer.slots[0][0].numel() * streamer.slots[0][0].element_size()
@@ -477,6 +495,8 @@ def main() -> int:
     ap.add_argument("--graph-steps", type=int, default=8,
                     help="timed steps per captured graph replay (StepRunner.run_many; 1 = one replay per step)")
     ap.add_argument("--eager-comm", action="store_true", help="all-reduce between two graphs, not captured")
+    ap.add_argument("--no-small", action="store_true",
+                    help="mlp, <= 256 rows: the regular step graphs instead of the persistent K-step launch")
     ap.add_argument("--comm-dtype", choices=["fp32", "bf16"], default="fp32",
                     help="C2 gradient all-reduce precision (parallel/dist.py; default fp32)")
     ap.add_argument("--stream-fp32", action="store_true", help="mlp_online: stream fp32 features")

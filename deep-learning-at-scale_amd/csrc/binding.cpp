@@ -606,6 +606,83 @@ bool mlp2_step(const at::Tensor& X, int64_t Fp, const at::Tensor& W1, const at::
                               fp(red), dz_frag, cur_stream(), w2t, (float)clip);
 }
 
+int64_t mlp_small_scratch_floats() { return wf::kMlpSmallScratch; }
+
+// K small-batch MLP training steps (forward, backward, Adam) in ONE persistent launch
+// (mlp_small.hip). X / Y: the dataset (bf16 [N][Fp], fp32 [N]) read through rows [K * B] (or
+// contiguous from row 0); params / m / v / step: the flat parameters and FlatAdam state, updated
+// in place; offs: (W1, b1, W2, b2, w3, b3) element offsets of the MlpLayout. False = not covered.
+bool mlp_small_steps(const at::Tensor& X, const at::Tensor& Y, c10::optional<at::Tensor> rows, int64_t Fp, int64_t B,
+                     int64_t K, const at::Tensor& params, const at::Tensor& m, const at::Tensor& v,
+                     const at::Tensor& step, double lr, double b1, double b2, double eps, double wd, double dy_scale,
+                     double clip, c10::optional<at::Tensor> shadow, c10::optional<at::Tensor> w2t,
+                     c10::optional<at::Tensor> loss_acc, const at::Tensor& scr, const at::Tensor& sync,
+                     std::vector<int64_t> offs, c10::optional<at::Tensor> stamps) {
+  constexpr int64_t H = 256;
+  TORCH_CHECK(offs.size() == 6, "mlp_small_steps: offs = (W1, b1, W2, b2, w3, b3)");
+  TORCH_CHECK(K > 0 && B > 0, "mlp_small_steps: K, B > 0");
+  check_t(X, at::kBFloat16, "X");
+  check_t(Y, at::kFloat, "Y");
+  int64_t nrows;
+  const long long* rp = nullptr;
+  if (rows.has_value() && rows->defined()) {
+    rp = rows_ptr(rows, K * B);
+    nrows = X.numel() / Fp;
+    TORCH_CHECK(nrows > 0, "X: empty dataset");
+  } else {
+    check_extent(X, K * B * Fp, "X");
+    nrows = K * B;
+  }
+  check_extent(Y, nrows, "Y");
+  const int64_t n = params.numel();
+  for (const at::Tensor* t : {&params, &m, &v}) {
+    check_t(*t, at::kFloat, "params/m/v");
+    check_extent(*t, n, "params/m/v");
+  }
+  TORCH_CHECK(offs[0] + H * Fp <= n && offs[2] + H * H <= n && offs[5] < n && offs[1] + H <= n && offs[3] + H <= n &&
+                  offs[4] + H <= n, "mlp_small_steps: parameter offsets out of range");
+  check_t(step, at::kFloat, "step");
+  check_t(scr, at::kFloat, "scr");
+  check_extent(scr, wf::kMlpSmallScratch, "scr");
+  check_t(sync, at::kInt, "sync");
+  check_extent(sync, 4, "sync");
+  const c10::hip::OptionalHIPGuardMasqueradingAsCUDA guard(X.device());
+  wf::MlpSmallArgs a{};
+  a.X = bfp(X);
+  a.Y = fp(Y);
+  a.rows = rp;
+  a.nrows = (long)nrows;
+  a.Fp = (int)Fp;
+  a.B = (int)B;
+  a.K = (int)K;
+  a.p = fp(params);
+  a.m = fp(m);
+  a.v = fp(v);
+  a.step = fp(step);
+  a.lr = (float)lr;
+  a.b1 = (float)b1;
+  a.b2 = (float)b2;
+  a.eps = (float)eps;
+  a.wd = (float)wd;
+  a.dy_scale = (float)dy_scale;
+  a.clip = (float)clip;
+  a.shadow = opt_ptr<bf16_t>(shadow, at::kBFloat16, "shadow", n);
+  a.w2t = opt_ptr<bf16_t>(w2t, at::kBFloat16, "w2t", H * H);
+  a.loss_acc = opt_ptr<float>(loss_acc, at::kFloat, "loss_acc", 1);
+  a.scr = fp(scr);
+  a.sync = reinterpret_cast<unsigned*>(sync.data_ptr<int>());
+  const char* sl = std::getenv("WELLFLOW_SPIN_LIMIT");  // tests: force the hand-off timeout path
+  a.spin_limit = sl != nullptr ? (unsigned)std::strtoul(sl, nullptr, 10) : (1u << 22);
+  a.oW1 = (long)offs[0];
+  a.ob1 = (long)offs[1];
+  a.oW2 = (long)offs[2];
+  a.ob2 = (long)offs[3];
+  a.ow3 = (long)offs[4];
+  a.ob3 = (long)offs[5];
+  a.stamps = reinterpret_cast<unsigned long long*>(opt_ptr<int64_t>(stamps, at::kLong, "stamps", 16 * 64 * 16));
+  return wf::launch_mlp_small(a, cur_stream());
+}
+
 // dW2 from the fragment-layout dZ2 of mlp2_step(dz_frag=True) into the spread scratch's dW2
 // copies (mlp_step.hip mlp2_dw2f_kernel; mlp2_reduce adds them). False = not covered.
 int64_t mlp2_dw2f(const at::Tensor& dZ2F, const at::Tensor& X, int64_t Fp, c10::optional<at::Tensor> rows,
@@ -1055,6 +1132,8 @@ PYBIND11_MODULE(_C, m) {
   WF_DEF(mlp2_reduce);
   WF_DEF(mlp2_step);
   WF_DEF(mlp2_dw2f);
+  WF_DEF(mlp_small_steps);
+  WF_DEF(mlp_small_scratch_floats);
   WF_DEF(lstm_pack_x);
   WF_DEF(lstm_forward);
   WF_DEF(lstm_forward_persistent);

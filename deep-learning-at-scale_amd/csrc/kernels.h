@@ -122,6 +122,35 @@ constexpr long kMlpRedFloats = kMlpRedSlab2Off + (long)kMlpRedSlab2Rows * 65536;
 // grid of the 8-wave training kernels for a batch (one workgroup per CU at most): the rows of
 // the dW1 slab the reduce sums
 int mlp2_train_grid(int B);
+// K small-batch MLP training steps (forward, backward, Adam) in one persistent launch of 16
+// workgroups (mlp_small.hip): hidden (256, 256), Fp <= 32, 32 <= B <= 256, B % 32 == 0.
+// rows: dataset row ids [K * B] (nullptr: step k reads rows k B .. k B + B - 1 of X / Y).
+// p / m / v / step: the flat fp32 parameters and FlatAdam state (updated in place);
+// shadow / w2t: the engine's bf16 images written at the end; loss_acc += each step's loss sum.
+// scr: kMlpSmallScratch floats; sync: 4 words zeroed once ([0] counter, [1] exits, [2] sticky
+// error, [3] completed launches).
+constexpr int kMlpSmallScratch = 49728 + 65536;
+struct MlpSmallArgs {
+  const bf16_t* X;
+  const float* Y;
+  const long long* rows;
+  long nrows;
+  int Fp, B, K;
+  float* p;
+  float* m;
+  float* v;
+  float* step;
+  float lr, b1, b2, eps, wd, dy_scale, clip;
+  bf16_t* shadow;
+  bf16_t* w2t;
+  float* loss_acc;
+  float* scr;
+  unsigned* sync;
+  unsigned spin_limit;
+  long oW1, ob1, oW2, ob2, ow3, ob3;
+  unsigned long long* stamps;  // diagnostics (tools/small_timeline.py): [16][64 steps][16] s_memrealtime, or null
+};
+bool launch_mlp_small(const MlpSmallArgs& a, hipStream_t s);
 bool mlp_bwd8();  // the 8-wave backward is selected (WELLFLOW_MLP_BWD8, default on)
 void launch_mlp2_reduce(float* red, int Fp, int B, float* loss_sum, float* db3, float* dw3, float* db1, float* db2,
                         float* dW1, float* dW2, hipStream_t s, int dw2_rows = 0);

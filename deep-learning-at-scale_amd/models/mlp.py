@@ -368,6 +368,70 @@ class NativeMLP:
             return False
         return self.recompute_h1 and self.fused and self.fused_bwd and self.mask_h2
 
+    # ------------------------------------------------------------------ small batches
+    SMALL_MAX_B = 256  # csrc/mlp_small.hip: 16 workgroups, the batch resident in each
+
+    def small_steps_reason(self, B: int, opt=None) -> str | None:
+        """None when K training steps of batch ``B`` can run as ONE persistent launch
+        (csrc/mlp_small.hip: forward, backward and Adam, weights and Adam state resident in 16
+        workgroups); else why not."""
+        if self.device.type != "cuda":
+            return "not on a GPU"
+        if self.hidden != (256, 256) or self.Fp > 32:
+            return f"shape F={self.F} hidden={self.hidden} (needs hidden (256, 256), <= 32 features)"
+        if B % 32 != 0 or not 32 <= B <= self.SMALL_MAX_B:
+            return f"batch {B} (needs 32 <= B <= {self.SMALL_MAX_B}, B % 32 == 0)"
+        if self.loss_kind not in ("mse", "mae_clip"):
+            return f"loss {self.loss_kind!r}"
+        if opt is not None:
+            from ..optim.flat import FlatAdam
+
+            if not isinstance(opt, FlatAdam) or opt.params is not self.params or opt.step_dev is None:
+                return "optimizer is not a device FlatAdam over this engine's parameters"
+        return None
+
+    def fused_steps(self, X: torch.Tensor, Y: torch.Tensor, B: int, K: int, opt, grad_scale: float,
+                    rows: torch.Tensor | None = None, loss_into: torch.Tensor | None = None,
+                    stamps: torch.Tensor | None = None) -> None:
+        """K complete training steps (forward, backward, Adam update of ``opt``) in ONE launch.
+        Step k reads dataset rows ``rows[k B : (k + 1) B]`` of ``X`` (bf16 [N][Fp]) / ``Y``, or
+        rows k B .. of ``X`` / ``Y`` when ``rows`` is None. ``loss_into`` += each step's loss
+        sum. The gradient bucket is not written (the update happens inside the launch); the
+        engine's bf16 images are refreshed at the end. Equals K single steps of this path bit
+        for bit (tests/test_small_gpu.py)."""
+        why = self.small_steps_reason(B, opt)
+        if why is not None:
+            raise RuntimeError(f"NativeMLP.fused_steps: {why}")
+        if getattr(self, "_small_scr", None) is None:
+            self._small_scr = torch.zeros(self._C.mlp_small_scratch_floats(), device=self.device)
+            self._small_sync = torch.zeros(4, dtype=torch.int32, device=self.device)
+        (w1, b1), (w2, b2) = self.lay.offsets()[0]
+        _, hw, hb, _ = self.lay.offsets()
+        mae = self.loss_kind == "mae_clip"
+        Xf = X.reshape(-1)
+        if Xf.dtype != torch.bfloat16:
+            raise RuntimeError("NativeMLP.fused_steps: X must be the bf16 input format (input_dtype)")
+        b1_, b2_ = opt.betas
+        ok = self._C.mlp_small_steps(Xf, Y.reshape(-1).float() if Y.dtype != torch.float32 else Y.reshape(-1),
+                                     rows, self.Fp, B, K, self.params, opt.m, opt.v, opt.step_dev, opt.lr, b1_, b2_,
+                                     opt.eps, opt.weight_decay, (1.0 if mae else 2.0) * float(grad_scale),
+                                     float(self.clip) if mae else 0.0, self.shadow, self.w2t, loss_into,
+                                     self._small_scr, self._small_sync, [w1, b1, w2, b2, hw, hb], stamps)
+        if not ok:
+            raise RuntimeError("NativeMLP.fused_steps: the launcher refused the shape")
+        opt.t += K
+
+    def check_device_errors(self) -> None:
+        """Raise if a small-batch launch's hand-off timed out (sticky word; the buffer is reset)."""
+        sync = getattr(self, "_small_sync", None)
+        if sync is None:
+            return
+        err = int(sync[2].item())
+        if err:
+            sync.zero_()
+            raise RuntimeError("NativeMLP: a small-batch persistent launch timed out in a hand-off "
+                               "(results of that launch are invalid)")
+
     def forward_backward(self, x: torch.Tensor, y: torch.Tensor, grad_scale: float,
                          zero_grads: bool = True, step: int = 0, rows: torch.Tensor | None = None,
                          loss_into: torch.Tensor | None = None) -> torch.Tensor:

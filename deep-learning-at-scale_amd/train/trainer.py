@@ -114,6 +114,9 @@ def _graph_steps() -> int:
 # (the job default batch 256 on a multi-million-row table: thousands) the epoch takes the
 # row-indexed path instead, whose graphs are keyed by n only (round-5 ADVICE).
 MAX_SLICED_STEPS = 128
+# steps per persistent small-batch launch (NativeMLP.fused_steps): one ~5-us launch per this many
+# steps; the Trainer's per-step bookkeeping runs on the host after each launch
+SMALL_STEPS_PER_LAUNCH = 256
 
 
 def _to_dev(a, device):
@@ -456,7 +459,34 @@ class Trainer:
         cfg = self.cfg
         s = 0
         prepared = False
-        while s < steps:
+        # small batches (the MLP job default, 256 rows): up to SMALL_STEPS_PER_LAUNCH complete
+        # steps — forward, backward AND the Adam update — per persistent launch
+        # (NativeMLP.fused_steps, csrc/mlp_small.hip); one process (the update has no all-reduce)
+        small = (getattr(eng, "small_steps_reason", None) is not None and ctx.world_size == 1 and cfg.fail_at_step < 0
+                 and torch.is_tensor(Xd) and Xd.dtype == torch.bfloat16 and (sliced or row_indexed)
+                 and eng.small_steps_reason(b, self.opt) is None)
+        while small and s < steps:
+            clock.first()
+            n = min(steps - s, SMALL_STEPS_PER_LAUNCH)
+            if cfg.max_steps:
+                n = max(0, min(n, cfg.max_steps - self.global_step))
+            if n == 0:
+                break
+            gscale = 1.0 / (b * ctx.world_size * self.n_out)
+            if sliced:
+                eng.fused_steps(Xd[s * b : (s + n) * b], Yd[s * b : (s + n) * b], b, n, self.opt, gscale,
+                                loss_into=run.loss_acc)
+            else:
+                eng.fused_steps(Xd, Yd, b, n, self.opt, gscale, rows=order[s * b : (s + n) * b],
+                                loss_into=run.loss_acc)
+            stop = False
+            for _ in range(n):
+                stop = self._after_step() or stop
+            done += n
+            s += n
+            if stop:
+                break
+        while not small and s < steps:
             clock.first()
             n = n_many
             if sliced and n > 1 and not prepared and run.calls > run.eager_steps + 1:
