@@ -318,11 +318,27 @@ def bench_cnn(args, ctx):
     series = torch.randn(B, lay.input_len + lay.outputs, generator=g).cumsum(1) * 0.1  # random-walk windows
     x = series[:, : lay.input_len].contiguous().to(ctx.device)
     y = series[:, lay.input_len :].contiguous().to(ctx.device)
-    run = StepRunner(eng, opt, ctx, 1.0 / (B * ctx.world_size * lay.outputs), lambda k: (x, y),
-                     graph=not args.no_graph, comm_in_graph=not args.eager_comm)
-    el, k, n = _timed(ctx, run.run, args.steps, args.warmup, args.min_timed_s, run.run_many, args.graph_steps,
-                      warm_ms=args.warm_ms)
-    return el, k, B, model, run.take_loss() / (B * lay.outputs * n), run, eng, {}
+    gscale = 1.0 / (B * ctx.world_size * lay.outputs)
+    run = StepRunner(eng, opt, ctx, gscale, lambda k: (x, y), graph=not args.no_graph,
+                     comm_in_graph=not args.eager_comm)
+    step, many, gsteps, extra = run.run, run.run_many, args.graph_steps, {}
+    if ctx.world_size == 1 and not args.no_small and eng.small_steps_reason(B, opt, x) is None:
+        # small batches (the reference's 20 windows, one process): the Trainer's path — n complete
+        # steps per persistent launch (NativeCNN.fused_steps, csrc/cnn_small.hip)
+        gsteps = max(1, min(args.steps, 256))
+        ridx = torch.arange(B, device=ctx.device).repeat(gsteps)  # the one resident batch, every step
+
+        def many(n):  # noqa: F811
+            eng.fused_steps(x, y, B, n, opt, gscale, rows=ridx[: n * B], loss_into=run.loss_acc)
+
+        def step():  # noqa: F811
+            many(1)
+
+        extra["small_fused_steps_per_launch"] = gsteps
+    el, k, n = _timed(ctx, step, args.steps, args.warmup, args.min_timed_s, many, gsteps, warm_ms=args.warm_ms)
+    if extra:
+        eng.check_device_errors()
+    return el, k, B, model, run.take_loss() / (B * lay.outputs * n), run, eng, extra
 
 
 def bench_mlp(args, ctx, online: bool):
@@ -464,7 +480,8 @@ def _secondary(args, ctx, models) -> dict:
                   "graph_steps": max((key[2] for key in run.graphs if isinstance(key, tuple) and key[0] == "many"),
                                      default=1),
                   **comm_rec,
-                  **{k: v for k, v in extra.items() if k.startswith("h2d") or k in ("persistent_fwd",)}}
+                  **{k: v for k, v in extra.items()
+                     if k.startswith("h2d") or k in ("persistent_fwd", "small_fused_steps_per_launch")}}
         if _LAST_TIMED.get("gpu_state") is not None:
             out[m]["gpu_state"] = _LAST_TIMED["gpu_state"]
         if W > 1 and ctx.device.type == "cuda":
@@ -496,7 +513,8 @@ def main() -> int:
                     help="timed steps per captured graph replay (StepRunner.run_many; 1 = one replay per step)")
     ap.add_argument("--eager-comm", action="store_true", help="all-reduce between two graphs, not captured")
     ap.add_argument("--no-small", action="store_true",
-                    help="mlp, <= 256 rows: the regular step graphs instead of the persistent K-step launch")
+                    help="mlp <= 256 rows / cnn <= 64 windows: the regular step graphs instead of the "
+                         "persistent K-step launch")
     ap.add_argument("--comm-dtype", choices=["fp32", "bf16"], default="fp32",
                     help="C2 gradient all-reduce precision (parallel/dist.py; default fp32)")
     ap.add_argument("--stream-fp32", action="store_true", help="mlp_online: stream fp32 features")

@@ -608,6 +608,8 @@ bool mlp2_step(const at::Tensor& X, int64_t Fp, const at::Tensor& W1, const at::
 
 int64_t mlp_small_scratch_floats() { return wf::kMlpSmallScratch; }
 
+
+
 // K small-batch MLP training steps (forward, backward, Adam) in ONE persistent launch
 // (mlp_small.hip). X / Y: the dataset (bf16 [N][Fp], fp32 [N]) read through rows [K * B] (or
 // contiguous from row 0); params / m / v / step: the flat parameters and FlatAdam state, updated
@@ -962,6 +964,80 @@ static wf::CnnDims cnn_checked(const std::vector<int64_t>& dims, double drop_p) 
 
 static int64_t cnn_frag_elems(const wf::CnnDims& d) { return (int64_t)d.T * (d.Fp / 16) * 64 * 4; }
 
+int64_t cnn_small_scratch_floats() { return wf::kCnnSmallScratch; }
+
+// K small-batch CNN training steps (forward, backward, Keras SGD) in ONE persistent launch
+// (cnn_small.hip). X [N][48] / Y [N][O] fp32 through rows [K * B] (or contiguous); params / vel
+// / step: flat parameters and FlatSGD state; rng: the engine's dropout step counter. False =
+// not covered.
+bool cnn_small_steps(const at::Tensor& X, const at::Tensor& Y, c10::optional<at::Tensor> rows, int64_t B, int64_t K,
+                     std::vector<int64_t> dims, double drop_p, int64_t loss_kind, double clip, double scale,
+                     int64_t seed, const at::Tensor& rng, const at::Tensor& params, const at::Tensor& vel,
+                     const at::Tensor& step, double lr, double decay, double momentum, bool nesterov, double gscale,
+                     c10::optional<at::Tensor> loss_acc, const at::Tensor& scr, const at::Tensor& sync,
+                     int64_t filters, c10::optional<at::Tensor> stamps) {
+  const wf::CnnDims d = cnn_checked(dims, drop_p);
+  TORCH_CHECK(d.L == 48 && d.C == 1 && d.Fp == 112 && d.Kc == 16 && d.T == 36, "cnn_small_steps: the reference layout only");
+  TORCH_CHECK(K > 0 && B > 0 && B <= 64, "cnn_small_steps: 0 < B <= 64, K > 0");
+  check_t(X, at::kFloat, "X");
+  check_t(Y, at::kFloat, "Y");
+  int64_t nrows;
+  const long long* rp = nullptr;
+  if (rows.has_value() && rows->defined()) {
+    rp = rows_ptr(rows, K * B);
+    nrows = X.numel() / d.L;
+    TORCH_CHECK(nrows > 0, "X: empty dataset");
+  } else {
+    nrows = K * B;
+    check_extent(X, nrows * d.L, "X");
+  }
+  check_extent(Y, nrows * d.O, "Y");
+  const int64_t n = (int64_t)d.Fp * d.Kc + 16LL * d.T * d.Fp + 16;
+  for (const at::Tensor* t : {&params, &vel}) {
+    check_t(*t, at::kFloat, "params/vel");
+    check_extent(*t, n, "params/vel");
+  }
+  check_t(step, at::kFloat, "step");
+  TORCH_CHECK(rng.is_cuda() && rng.scalar_type() == at::kLong && rng.numel() >= 1, "rng: int64 GPU counter");
+  check_t(scr, at::kFloat, "scr");
+  check_extent(scr, wf::kCnnSmallScratch, "scr");
+  check_t(sync, at::kInt, "sync");
+  check_extent(sync, 4, "sync");
+  const c10::hip::OptionalHIPGuardMasqueradingAsCUDA guard(X.device());
+  wf::CnnSmallArgs a{};
+  a.X = fp(X);
+  a.Y = fp(Y);
+  a.rows = rp;
+  a.nrows = (long)nrows;
+  a.B = (int)B;
+  a.K = (int)K;
+  a.O = d.O;
+  a.taps = d.taps;
+  a.filters = (int)filters;
+  a.drop = drop_p > 0.0 ? 1 : 0;
+  a.loss_kind = (int)loss_kind;
+  a.keep_scale = drop_p > 0.0 ? (float)(1.0 / (1.0 - drop_p)) : 1.f;
+  a.clip = (float)clip;
+  a.scale = (float)scale;
+  a.seed = (unsigned)seed;
+  a.rng = reinterpret_cast<long long*>(rng.data_ptr<int64_t>());
+  a.p = fp(params);
+  a.vel = fp(vel);
+  a.step = fp(step);
+  a.lr = (float)lr;
+  a.decay = (float)decay;
+  a.momentum = (float)momentum;
+  a.gscale = (float)gscale;
+  a.nesterov = nesterov ? 1 : 0;
+  a.loss_acc = opt_ptr<float>(loss_acc, at::kFloat, "loss_acc", 1);
+  a.scr = fp(scr);
+  a.sync = reinterpret_cast<unsigned*>(sync.data_ptr<int>());
+  const char* sl = std::getenv("WELLFLOW_SPIN_LIMIT");  // tests: force the hand-off timeout path
+  a.spin_limit = sl != nullptr ? (unsigned)std::strtoul(sl, nullptr, 10) : (1u << 22);
+  a.stamps = reinterpret_cast<unsigned long long*>(opt_ptr<int64_t>(stamps, at::kLong, "stamps", 28 * 64 * 16));
+  return wf::launch_cnn_small(a, cur_stream());
+}
+
 void cnn_pack(const at::Tensor& Wc, const at::Tensor& Wd, const std::vector<int64_t>& dims, const at::Tensor& WcA,
               const at::Tensor& WdF, const at::Tensor& WdB) {
   auto d = cnn_checked(dims, 0.0);
@@ -1134,6 +1210,8 @@ PYBIND11_MODULE(_C, m) {
   WF_DEF(mlp2_dw2f);
   WF_DEF(mlp_small_steps);
   WF_DEF(mlp_small_scratch_floats);
+  WF_DEF(cnn_small_steps);
+  WF_DEF(cnn_small_scratch_floats);
   WF_DEF(lstm_pack_x);
   WF_DEF(lstm_forward);
   WF_DEF(lstm_forward_persistent);

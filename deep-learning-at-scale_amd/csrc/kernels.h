@@ -151,6 +151,33 @@ struct MlpSmallArgs {
   unsigned long long* stamps;  // diagnostics (tools/small_timeline.py): [16][64 steps][16] s_memrealtime, or null
 };
 bool launch_mlp_small(const MlpSmallArgs& a, hipStream_t s);
+// K small-batch training steps of the reference CNN (conv 13 taps -> 36 steps x filters, ReLU,
+// dropout, dense -> O outputs, Keras SGD) in one persistent launch of ceil(filters / 4)
+// workgroups (cnn_small.hip); B <= 64. X [N][48] / Y [N][O] fp32 read through rows [K * B]
+// (nullptr: contiguous); p / vel / step: the flat parameters and FlatSGD state; rng: the
+// engine's dropout step counter (+= K); scr: kCnnSmallScratch floats; sync: 4 words, zeroed once.
+constexpr int kCnnSmallScratch = 2 * 28 * 64 * 16 * 2 + 2 * 64 * 16 * 2;
+struct CnnSmallArgs {
+  const float* X;
+  const float* Y;
+  const long long* rows;
+  long nrows;
+  int B, K, O, taps, filters, drop, loss_kind;
+  float keep_scale, clip, scale;
+  unsigned seed;
+  long long* rng;
+  float* p;
+  float* vel;
+  float* step;
+  float lr, decay, momentum, gscale;
+  int nesterov;
+  float* loss_acc;
+  float* scr;
+  unsigned* sync;
+  unsigned spin_limit;
+  unsigned long long* stamps;  // diagnostics (tools/small_timeline.py --cnn): [G][64 steps][16], or null
+};
+bool launch_cnn_small(const CnnSmallArgs& a, hipStream_t s);
 bool mlp_bwd8();  // the 8-wave backward is selected (WELLFLOW_MLP_BWD8, default on)
 void launch_mlp2_reduce(float* red, int Fp, int B, float* loss_sum, float* db3, float* dw3, float* db1, float* db2,
                         float* dW1, float* dW2, hipStream_t s, int dw2_rows = 0);

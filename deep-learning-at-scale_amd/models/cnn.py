@@ -266,11 +266,76 @@ class NativeCNN:
     def seed32(self) -> int:
         return (self.seed * 1000003) & 0x7FFFFFFF
 
+    # ------------------------------------------------------------------ small batches
+    SMALL_MAX_B = 64  # csrc/cnn_small.hip: every worker holds the whole batch's activations
+
+    def small_steps_reason(self, B: int, opt=None, X=None) -> str | None:
+        """None when K training steps of batch ``B`` can run as ONE persistent launch
+        (csrc/cnn_small.hip: forward, backward and the Keras SGD update; 25 workgroups of 4
+        filters, one exchange per step); else why not."""
+        if self.device.type != "cuda":
+            return "not on a GPU"
+        if not self.fused:
+            return "layout not covered by the fused kernels"
+        L = self.lay
+        if L.input_len != 48 or L.kernel != 13 or L.in_ch != 1:
+            return f"window {L.input_len}x{L.in_ch}, kernel {L.kernel} (needs the reference's 48 x 1, 13)"
+        if not 4 <= B <= self.SMALL_MAX_B or B % 4:
+            return f"batch {B} (needs 4 <= B <= {self.SMALL_MAX_B}, B % 4 == 0)"
+        if opt is not None:
+            from ..optim.flat import FlatSGD
+
+            if not isinstance(opt, FlatSGD) or opt.params is not self.params or opt.step_dev is None:
+                return "optimizer is not a device FlatSGD over this engine's parameters"
+        if X is not None and not (torch.is_tensor(X) and X.dtype == torch.float32 and X.is_cuda):
+            return "data not a resident fp32 tensor"
+        return None
+
+    def fused_steps(self, X: torch.Tensor, Y: torch.Tensor, B: int, K: int, opt, grad_scale: float,
+                    rows: torch.Tensor | None = None, loss_into: torch.Tensor | None = None,
+                    stamps: torch.Tensor | None = None) -> None:
+        """K complete training steps (forward with the engine's dropout stream, backward, the
+        Keras SGD update of ``opt``) in ONE launch. Step k reads windows ``rows[k B : (k + 1) B]``
+        of ``X`` ([N][48] fp32) / ``Y`` ([N][outputs]), or windows k B .. when ``rows`` is None.
+        ``loss_into`` += each step's loss sum. The gradient bucket is not written; the bf16
+        operand images are refreshed after the launch. Equals K single steps of this path bit for
+        bit (tests/test_small_gpu.py)."""
+        why = self.small_steps_reason(B, opt, X)
+        if why is not None:
+            raise RuntimeError(f"NativeCNN.fused_steps: {why}")
+        if getattr(self, "_small_scr", None) is None:
+            self._small_scr = torch.zeros(self._C.cnn_small_scratch_floats(), device=self.device)
+            self._small_sync = torch.zeros(4, dtype=torch.int32, device=self.device)
+        kind = 0 if self.loss_kind == "mse" else 1
+        ok = self._C.cnn_small_steps(X.reshape(-1), Y.reshape(-1).float(), rows, B, K, self.lay.fused_dims,
+                                     float(self.p), kind, float(self.clip), float(grad_scale), self.seed32, self.rng,
+                                     self.params, opt.vel, opt.step_dev, opt.lr, opt.decay, opt.momentum,
+                                     bool(opt.nesterov), 1.0, loss_into, self._small_scr, self._small_sync,
+                                     self.lay.filters, stamps)
+        if not ok:
+            raise RuntimeError("NativeCNN.fused_steps: the launcher refused the shape")
+        opt.iterations += K
+        self.sync_weights()  # the bf16 operand images of the regular kernels (evaluation)
+
+    def check_device_errors(self) -> None:
+        """Raise if a small-batch launch's hand-off timed out (sticky word; the buffer is reset)."""
+        sync = getattr(self, "_small_sync", None)
+        if sync is None:
+            return
+        if int(sync[2].item()):
+            sync.zero_()
+            raise RuntimeError("NativeCNN: a small-batch persistent launch timed out in a hand-off "
+                               "(results of that launch are invalid)")
+
+    def fused_sgd_ok(self, opt) -> bool:
+        """Whether :meth:`fused_sgd` covers ``opt`` (train/step.py's sync_weights decision)."""
+        return bool(self.fused)
+
     def fused_sgd(self, opt, grad_scale: float) -> bool:
         """The optimizer's update and this engine's operand images in ONE launch (optim/flat.py
         FlatSGD ``writeback``; csrc/cnn_fused.hip cnn_sgd_pack_kernel); False = not covered (the
         caller runs the plain update and sync_weights)."""
-        if not self.fused:
+        if not self.fused_sgd_ok(opt):
             return False
         self._C.cnn_sgd_pack(self.params, self.grads, opt.vel, opt.step_dev, opt.lr, opt.decay, opt.momentum,
                              opt.nesterov, grad_scale, opt.zero_grads, self.lay.fused_dims, self.WcA, self.WdF,

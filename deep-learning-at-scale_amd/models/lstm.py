@@ -268,11 +268,17 @@ class NativeLSTM:
         return 256 * max(1, props.multi_processor_count // nb)
 
     # ------------------------------------------------------------------ weights
+    def fused_adam_ok(self, opt) -> bool:
+        """Whether :meth:`fused_adam` covers ``opt`` (train/step.py decides from the same
+        predicate whether the step still needs its own sync_weights launch)."""
+        # (the kernel transposes W_hh in 32 x 32 tiles)
+        return opt.shadow is None and opt.shadow_t is None and self.H % 32 == 0 and self.lay.KX % 32 == 0
+
     def fused_adam(self, opt, grad_scale: float) -> bool:
         """The optimizer's Adam update and this engine's bf16 compute copies (Wp, WhhT) in ONE
         launch (optim/flat.py FlatAdam ``writeback``; csrc/elementwise.hip lstm_adam_pack_kernel)."""
-        if opt.shadow is not None or opt.shadow_t is not None or self.H % 32 or self.lay.KX % 32:
-            return False  # (the kernel transposes W_hh in 32 x 32 tiles)
+        if not self.fused_adam_ok(opt):
+            return False
         b1, b2 = opt.betas
         self._C.lstm_adam_pack(self.params, self.grads, opt.m, opt.v, opt.step_dev, opt.lr, b1, b2, opt.eps,
                                opt.weight_decay, grad_scale, opt.zero_grads, self.Wp, self.WhhT, self.H, self.lay.KX)

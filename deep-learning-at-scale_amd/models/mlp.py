@@ -371,7 +371,7 @@ class NativeMLP:
     # ------------------------------------------------------------------ small batches
     SMALL_MAX_B = 256  # csrc/mlp_small.hip: 16 workgroups, the batch resident in each
 
-    def small_steps_reason(self, B: int, opt=None) -> str | None:
+    def small_steps_reason(self, B: int, opt=None, X=None) -> str | None:
         """None when K training steps of batch ``B`` can run as ONE persistent launch
         (csrc/mlp_small.hip: forward, backward and Adam, weights and Adam state resident in 16
         workgroups); else why not."""
@@ -388,6 +388,8 @@ class NativeMLP:
 
             if not isinstance(opt, FlatAdam) or opt.params is not self.params or opt.step_dev is None:
                 return "optimizer is not a device FlatAdam over this engine's parameters"
+        if X is not None and not (torch.is_tensor(X) and X.dtype == torch.bfloat16 and X.is_cuda):
+            return "data not a resident bf16 tensor (the engine's input_dtype)"
         return None
 
     def fused_steps(self, X: torch.Tensor, Y: torch.Tensor, B: int, K: int, opt, grad_scale: float,

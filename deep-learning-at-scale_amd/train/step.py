@@ -52,9 +52,13 @@ class StepRunner:
         est, ost = getattr(eng, "shadow_t", None), getattr(opt, "shadow_t", None)
         self.fused_shadow = (sh is not None and sh is getattr(eng, "shadow", None) and
                              (est is None or (ost is not None and ost[0] is est[0])))
-        # ... or an optimizer that refreshes the engine's compute copies itself (FlatSGD writeback)
-        if getattr(opt, "writeback", None) is eng and (getattr(eng, "fused", False) or hasattr(eng, "fused_adam")):
-            self.fused_shadow = True
+        # ... or an optimizer whose writeback refreshes the engine's compute copies in its own
+        # launch — only when the engine's fused update covers THIS optimizer (the same predicate
+        # fused_adam / fused_sgd check: otherwise the plain update runs and sync_weights must follow)
+        if getattr(opt, "writeback", None) is eng:
+            ok = getattr(eng, "fused_adam_ok", None) or getattr(eng, "fused_sgd_ok", None)
+            if ok is not None and ok(opt):
+                self.fused_shadow = True
         self.loss_acc = torch.zeros(1, device=eng.device) if accumulate_loss else None
         # engines that add the batch loss straight into the accumulator (no zero + add launches)
         try:

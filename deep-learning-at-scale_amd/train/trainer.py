@@ -459,12 +459,12 @@ class Trainer:
         cfg = self.cfg
         s = 0
         prepared = False
-        # small batches (the MLP job default, 256 rows): up to SMALL_STEPS_PER_LAUNCH complete
-        # steps — forward, backward AND the Adam update — per persistent launch
-        # (NativeMLP.fused_steps, csrc/mlp_small.hip); one process (the update has no all-reduce)
+        # small batches (the job defaults: MLP 256 rows, CNN 20 windows): up to
+        # SMALL_STEPS_PER_LAUNCH complete steps — forward, backward AND the optimizer update — per
+        # persistent launch (NativeMLP / NativeCNN.fused_steps, csrc/mlp_small.hip, cnn_small.hip);
+        # one process (the update has no all-reduce)
         small = (getattr(eng, "small_steps_reason", None) is not None and ctx.world_size == 1 and cfg.fail_at_step < 0
-                 and torch.is_tensor(Xd) and Xd.dtype == torch.bfloat16 and (sliced or row_indexed)
-                 and eng.small_steps_reason(b, self.opt) is None)
+                 and eng.small_steps_reason(b, self.opt, Xd) is None)
         while small and s < steps:
             clock.first()
             n = min(steps - s, SMALL_STEPS_PER_LAUNCH)

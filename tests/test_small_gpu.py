@@ -164,3 +164,111 @@ def test_small_spin_bound_fails_loudly():
     eng.fused_steps(X[: 4 * B], Y[: 4 * B], B, 4, opt, 1.0 / B)
     torch.cuda.synchronize()
     eng.check_device_errors()
+
+
+# ---------------------------------------------------------------------------- CNN (B = 20)
+def _cnn_setup(B=20, N=None, seed=4, loss="mae_clip", dropout=0.5):
+    from wellflow.models.cnn import CNN1DRegressor, CnnLayout, NativeCNN
+    from wellflow.optim.flat import FlatSGD
+
+    lay = CnnLayout()
+    torch.manual_seed(seed)
+    ref = CNN1DRegressor(lay.input_len, lay.in_ch, lay.filters, lay.kernel, lay.outputs).init_keras(seed)
+    with torch.no_grad():
+        ref.conv.bias.uniform_(-0.05, 0.05)
+        ref.dense.bias.uniform_(-0.05, 0.05)
+    flat = ref.to_flat()
+    eng = NativeCNN(lay, B, DEV, dropout=dropout, loss=loss, seed=seed)
+    eng.params.copy_(flat.to(DEV))
+    eng.sync_weights()
+    opt = FlatSGD(eng.params, eng.grads, zero_grads=True, writeback=eng)
+    N = N or 24 * B
+    g = torch.Generator(device="cpu").manual_seed(seed + 1)
+    series = torch.randn(N, lay.input_len + lay.outputs, generator=g).cumsum(1) * 0.1
+    X = series[:, : lay.input_len].contiguous().to(DEV)
+    Y = series[:, lay.input_len:].contiguous().to(DEV)
+    return eng, opt, ref, X, Y, lay
+
+
+def test_cnn_small_k_fused_equals_k_single():
+    B, K = 20, 8
+    out = []
+    for split in ([8], [1] * 8, [3, 5]):
+        eng, opt, _, X, Y, _ = _cnn_setup(B=B)
+        rows = torch.randperm(X.shape[0], generator=torch.Generator().manual_seed(2))[: K * B].to(DEV)
+        acc = torch.zeros(1, device=DEV)
+        s = 0
+        for k in split:
+            eng.fused_steps(X, Y, B, k, opt, 1.0 / (B * 12), rows=rows[s * B : (s + k) * B], loss_into=acc)
+            s += k
+        torch.cuda.synchronize()
+        eng.check_device_errors()
+        out.append([eng.params.clone(), opt.vel.clone(), opt.step_dev[:1].clone(), eng.rng.clone(), acc.clone()])
+        assert int(eng.rng.item()) == K and int(opt.step_dev[0].item()) == K
+    for other in out[1:]:
+        for a, b in zip(out[0], other):
+            assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("loss,dropout", [("mae_clip", 0.5), ("mse", 0.0)])
+def test_cnn_small_trajectory_matches_fp32(loss, dropout):
+    """20 Keras SGD-Nesterov steps at the reference's batch of 20 on distinct batches against
+    fp32 autograd of CNN1DRegressor with the SAME dropout keep masks (cnn_dropout_mask of the
+    engine's device step counter): the fused launch computes in fp32, so the per-step losses
+    agree to rounding."""
+    from wellflow.models.base import per_element_loss
+    from wellflow.models.cnn import cnn_dropout_mask
+
+    B, steps = 20, 20
+    eng, opt, ref, X, Y, lay = _cnn_setup(B=B, N=steps * B, loss=loss, dropout=dropout)
+    scale = 1.0 / (B * lay.outputs)
+    step0, seed32 = int(eng.rng.item()), eng.seed32
+    nat = []
+    acc = torch.zeros(1, device=DEV)
+    for k in range(steps):
+        acc.zero_()
+        eng.fused_steps(X[k * B : (k + 1) * B], Y[k * B : (k + 1) * B], B, 1, opt, scale, loss_into=acc)
+        nat.append(acc.item() * scale)
+    eng.check_device_errors()
+    ref = ref.to(DEV)
+    params = list(ref.parameters())
+    vel = [torch.zeros_like(p) for p in params]
+    lr, mu, decay = 0.001, 0.99, 1e-6
+    fp = []
+    for k in range(steps):
+        for p in params:
+            p.grad = None
+        xc = X[k * B : (k + 1) * B].view(B, lay.input_len, 1)
+        h = torch.relu(ref.conv(xc.transpose(1, 2))).transpose(1, 2)
+        if dropout > 0:
+            mask = cnn_dropout_mask(seed32, step0 + k, B, lay.lout, lay.Fp, device=DEV)
+            h = h * mask[:, :, : lay.filters].float() * 2.0
+        out = ref.dense(h.reshape(B, -1))
+        L = per_element_loss(loss, out, Y[k * B : (k + 1) * B]).sum()
+        (L * scale).backward()
+        lr_t = lr / (1.0 + decay * k)
+        with torch.no_grad():
+            for p, v in zip(params, vel):
+                v.mul_(mu).sub_(lr_t * p.grad)
+                p.add_(mu * v - lr_t * p.grad)
+        fp.append(L.item() * scale)
+    rel = [abs(a - b) / b for a, b in zip(nat, fp)]
+    assert max(rel) < 1e-3, (nat, fp)
+    p_ref = ref.to_flat().to(DEV)
+    assert ((eng.params - p_ref).norm() / p_ref.norm()).item() < 1e-4
+
+
+def test_cnn_small_spin_bound_fails_loudly():
+    B = 20
+    eng, opt, _, X, Y, _ = _cnn_setup(B=B)
+    os.environ["WELLFLOW_SPIN_LIMIT"] = "1"
+    try:
+        eng.fused_steps(X[: 4 * B], Y[: 4 * B], B, 4, opt, 1.0 / B)
+        torch.cuda.synchronize()
+    finally:
+        del os.environ["WELLFLOW_SPIN_LIMIT"]
+    with pytest.raises(RuntimeError, match="timed out"):
+        eng.check_device_errors()
+    eng.fused_steps(X[: 4 * B], Y[: 4 * B], B, 4, opt, 1.0 / B)
+    torch.cuda.synchronize()
+    eng.check_device_errors()

@@ -213,3 +213,38 @@ def test_sliced_epochs_bound_the_graph_count():
     assert 16 <= trainer.MAX_SLICED_STEPS <= 512
     src = inspect.getsource(trainer.Trainer.fit)
     assert "MAX_SLICED_STEPS" in src and "_permuted" in src
+
+
+def test_writeback_skips_sync_only_when_the_fused_update_covers_the_optimizer():
+    """StepRunner leaves out sync_weights only when the engine's fused optimizer launch will
+    actually run for this optimizer (round-5 ADVICE: an LSTM engine with a shadow-writing Adam
+    fell back to the plain update and trained on stale compute copies)."""
+    import torch
+
+    from wellflow.parallel.dist import DistContext
+    from wellflow.train.step import StepRunner
+
+    class Eng:
+        device = torch.device("cpu")
+        grads = torch.zeros(4)
+
+        def __init__(self, ok):
+            self.ok = ok
+
+        def fused_adam_ok(self, opt):
+            return self.ok
+
+        def forward_backward(self, x, y, grad_scale, zero_grads=True):
+            return torch.zeros(1)
+
+    class Opt:
+        shadow = None
+        zero_grads = False
+
+        def __init__(self, eng):
+            self.writeback = eng
+
+    for ok in (True, False):
+        eng = Eng(ok)
+        run = StepRunner(eng, Opt(eng), DistContext(device="cpu"), 1.0, lambda k: (None, None), graph=False)
+        assert run.fused_shadow is ok
