@@ -20,6 +20,7 @@
 // (cnn_fused.hip, models/cnn.py cnn_dropout_mask) from the engine's device step counter.
 // Bounded polls: a lost hand-off sets a sticky error word (results garbage, the host raises).
 // Every reduction has a fixed order, so K fused steps equal K single-step launches bit for bit.
+#include <type_traits>
 #include "common.h"
 #include "kernels.h"
 
@@ -58,15 +59,18 @@ __global__ __launch_bounds__(CS_NT, 1) void cnn_small_kernel(const CnnSmallArgs 
   const int wk = blockIdx.x, G = gridDim.x;
   const int f0 = CS_FPW * wk;  // first owned filter
   // LDS
-  __shared__ float xs[CS_MAXB][CS_L];
+  __shared__ __attribute__((aligned(16))) float xs[CS_MAXB][CS_L];
   __shared__ float ysm[CS_MAXB][CS_OP];
-  __shared__ __attribute__((aligned(16))) float act[CS_MAXB][CS_T][CS_FPW];  // relu(P) kept (unscaled), then dP
+  // [.][filter][step]: steps fastest, so lanes over consecutive steps hit consecutive banks in
+  // every loop below ([.][step][filter] put the dWc loop into 16-way bank conflicts)
+  __shared__ __attribute__((aligned(16))) float act[CS_MAXB][CS_FPW][CS_T];  // relu(P) kept (unscaled), then dP
   __shared__ float dout[CS_MAXB][CS_OP];
-  __shared__ float wc[CS_FPW][CS_KC], vc[CS_FPW][CS_KC];
-  __shared__ __attribute__((aligned(16))) float wd[CS_OP][CS_T][CS_FPW];
-  __shared__ float vd[CS_OP][CS_T][CS_FPW];
+  __shared__ __attribute__((aligned(16))) float wc[CS_FPW][CS_KC];
+  __shared__ float vc[CS_FPW][CS_KC];
+  __shared__ __attribute__((aligned(16))) float wd[CS_OP][CS_FPW][CS_T];
+  __shared__ float vd[CS_OP][CS_FPW][CS_T];
   __shared__ float bd[CS_OP], vb[CS_OP];
-  __shared__ float gwc[CS_FPW][CS_TAPS + 1][CS_T];  // dWc partials per output step
+  __shared__ __attribute__((aligned(16))) float gwc[CS_FPW][CS_TAPS + 1][CS_T];  // dWc partials per output step
   __shared__ float lred[CS_NT / 64];
   __shared__ float red2[48][28];                   // hop 1 of the output sums: [own output][share]
   __shared__ unsigned sflag;
@@ -87,10 +91,10 @@ __global__ __launch_bounds__(CS_NT, 1) void cnn_small_kernel(const CnnSmallArgs 
     vc[fl][kk] = a.vel[e];
   }
   for (int i = tid; i < CS_OP * CS_T * CS_FPW; i += CS_NT) {
-    const int j = i / (CS_T * CS_FPW), t = (i / CS_FPW) % CS_T, fl = i % CS_FPW;
+    const int j = i / (CS_T * CS_FPW), fl = (i / CS_T) % CS_FPW, t = i % CS_T;
     const long e = oWd + (long)j * CS_T * CS_FP + t * CS_FP + f0 + fl;
-    wd[j][t][fl] = a.p[e];
-    vd[j][t][fl] = a.vel[e];
+    wd[j][fl][t] = a.p[e];
+    vd[j][fl][t] = a.vel[e];
   }
   if (tid < CS_OP) {
     bd[tid] = a.p[obd + tid];
@@ -176,41 +180,58 @@ __global__ __launch_bounds__(CS_NT, 1) void cnn_small_kernel(const CnnSmallArgs 
     const unsigned smix = cs_lowbias32(a.seed ^ cs_lowbias32(rstep + 0x9E3779B9u));
     // (every loop below has compile-time trip counts and is unrolled: the runtime-bounded forms
     // were LDS-latency chains, one load -> wait -> fma per iteration: conv 9.3 us per step)
-    float wcr[CS_TAPS + 1];  // this thread's filter (fl = tid % 4 for every i below)
+    // task (window, filter, 4 steps): x[t4 .. t4 + 15] and the filter row in 8 float4 reads
+    for (int i = tid; i < B * CS_FPW * (CS_T / 4); i += CS_NT) {
+      const int w = i / (CS_FPW * (CS_T / 4)), fl = (i / (CS_T / 4)) % CS_FPW, t4 = 4 * (i % (CS_T / 4));
+      float wcr[CS_KC], xw[16];
 #pragma unroll
-    for (int kk = 0; kk <= CS_TAPS; ++kk) wcr[kk] = wc[tid % CS_FPW][kk];
-    for (int i = tid; i < B * CS_T * CS_FPW; i += CS_NT) {
-      const int w = i / (CS_T * CS_FPW), t = (i / CS_FPW) % CS_T, fl = i % CS_FPW;
-      float xw[CS_TAPS];
-#pragma unroll
-      for (int kk = 0; kk < CS_TAPS; ++kk) xw[kk] = xs[w][t + kk];
-      float pv = wcr[CS_TAPS];  // the conv bias (K slot = taps)
-#pragma unroll
-      for (int kk = 0; kk < CS_TAPS; ++kk) pv = fmaf(wcr[kk], xw[kk], pv);
-      bool keep = true;
-      if (a.drop) {  // the fused kernels' keep bit (cnn_fused.hip cnn_mask_word)
-        const int f = f0 + fl, q = (f >> 2) & 3, r = f & 3, b = f >> 4;
-        const unsigned m = cs_lowbias32((((unsigned)w * CS_T + (unsigned)t) * 4u + (unsigned)q) ^ smix);
-        keep = ((m >> (2 * b + (r >> 1) + 16 * (r & 1))) & 1u) != 0u;
+      for (int c = 0; c < 4; ++c) {
+        *reinterpret_cast<float4*>(&wcr[4 * c]) = *reinterpret_cast<const float4*>(&wc[fl][4 * c]);
+        *reinterpret_cast<float4*>(&xw[4 * c]) = *reinterpret_cast<const float4*>(&xs[w][t4 + 4 * c]);
       }
-      act[w][t][fl] = (keep && pv > 0.f) ? pv : 0.f;
+      float pv[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        pv[e] = wcr[CS_TAPS];  // the conv bias (K slot = taps)
+#pragma unroll
+        for (int kk = 0; kk < CS_TAPS; ++kk) pv[e] = fmaf(wcr[kk], xw[e + kk], pv[e]);
+      }
+      float o[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        bool keep = true;
+        if (a.drop) {  // the fused kernels' keep bit (cnn_fused.hip cnn_mask_word)
+          const int f = f0 + fl, q = (f >> 2) & 3, r = f & 3, b = f >> 4;
+          const unsigned m = cs_lowbias32((((unsigned)w * CS_T + (unsigned)(t4 + e)) * 4u + (unsigned)q) ^ smix);
+          keep = ((m >> (2 * b + (r >> 1) + 16 * (r & 1))) & 1u) != 0u;
+        }
+        o[e] = (keep && pv[e] > 0.f) ? pv[e] : 0.f;
+      }
+      *reinterpret_cast<float4*>(&act[w][fl][t4]) = make_float4(o[0], o[1], o[2], o[3]);
     }
     __syncthreads();
     stamp(2);
     // ---- this worker's share of the dense outputs -> granules (parity par)
-    for (int i = tid; i < B * O; i += CS_NT) {
-      const int w = i / O, j = i % O;
+    // (vectorised over 4 consecutive steps in every loop below: float4 LDS reads, 4 outputs per
+    // task; each phase was LDS-instruction bound at one element per task)
+    // four lanes per (window, output), one filter each, combined by two xor shuffles
+    for (int i0 = 0; i0 < 4 * B * O; i0 += CS_NT) {
+      const int i = i0 + tid;
+      const bool act_i = i < 4 * B * O;
+      const int pr = act_i ? i >> 2 : 0, fl = i & 3, w = pr / O, j = pr % O;
       float s = 0.f;
-#pragma unroll 6
-      for (int t = 0; t < CS_T; ++t) {
-        const float4 wv = *reinterpret_cast<const float4*>(&wd[j][t][0]);
-        const float4 av = *reinterpret_cast<const float4*>(&act[w][t][0]);
+#pragma unroll
+      for (int t4 = 0; t4 < CS_T; t4 += 4) {
+        const float4 wv = *reinterpret_cast<const float4*>(&wd[j][fl][t4]);
+        const float4 av = *reinterpret_cast<const float4*>(&act[w][fl][t4]);
         s = fmaf(wv.x, av.x, s);
         s = fmaf(wv.y, av.y, s);
         s = fmaf(wv.z, av.z, s);
         s = fmaf(wv.w, av.w, s);
       }
-      st8(__float_as_uint(s), tag, CS_P1 + ((par * G + wk) * CS_MAXB * CS_OP + w * CS_OP + j) * 2);
+      s += __shfl_xor(s, 1, 64);
+      s += __shfl_xor(s, 2, 64);
+      if (act_i && fl == 0) st8(__float_as_uint(s), tag, CS_P1 + ((par * G + wk) * CS_MAXB * CS_OP + w * CS_OP + j) * 2);
     }
     stamp(3);
     // ---- the shares are summed in two hops (one 25-way read of every output per worker moved
@@ -298,47 +319,83 @@ __global__ __launch_bounds__(CS_NT, 1) void cnn_small_kernel(const CnnSmallArgs 
     }
     stamp(4);
     // ---- dWd (own columns) = ks * dOut^T act, then dAct = ks * dOut Wd masked -> dP (in act)
-    float gwd[(CS_OP * CS_T * CS_FPW + CS_NT - 1) / CS_NT];
+    // task (j, fl, 4 steps), tid < CS_OP * CS_FPW * CS_T / 4 = 576: the SGD below updates the
+    // same 4 parameters in the same thread
+    constexpr int NWD = CS_OP * CS_FPW * (CS_T / 4);
+    float4 gwd = make_float4(0.f, 0.f, 0.f, 0.f);
+    const int dj = tid / (CS_FPW * (CS_T / 4)), dfl = (tid / (CS_T / 4)) % CS_FPW, dt4 = 4 * (tid % (CS_T / 4));
+    if (tid < NWD && dj < O) {
+      float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+      for (int w0 = 0; w0 < B; w0 += 4) {  // B % 4 == 0 (launcher)
 #pragma unroll
-    for (int q = 0; q < (CS_OP * CS_T * CS_FPW + CS_NT - 1) / CS_NT; ++q) {
-      const int i = tid + CS_NT * q;
-      gwd[q] = 0.f;
-      if (i < CS_OP * CS_T * CS_FPW) {
-        const int j = i / (CS_T * CS_FPW), t = (i / CS_FPW) % CS_T, fl = i % CS_FPW;
-        if (j < O) {
-          float s = 0.f;
-          for (int w0 = 0; w0 < B; w0 += 4) {  // B % 4 == 0 (launcher)
-#pragma unroll
-            for (int w = w0; w < w0 + 4; ++w) s = fmaf(dout[w][j], act[w][t][fl], s);
-          }
-          gwd[q] = ks * s;
+        for (int w = w0; w < w0 + 4; ++w) {
+          const float d = dout[w][dj];
+          const float4 av = *reinterpret_cast<const float4*>(&act[w][dfl][dt4]);
+          s.x = fmaf(d, av.x, s.x);
+          s.y = fmaf(d, av.y, s.y);
+          s.z = fmaf(d, av.z, s.z);
+          s.w = fmaf(d, av.w, s.w);
         }
       }
+      gwd = make_float4(ks * s.x, ks * s.y, ks * s.z, ks * s.w);
     }
     __syncthreads();  // act read by every dWd before it becomes dP
     stamp(5);
-    for (int i = tid; i < B * CS_T * CS_FPW; i += CS_NT) {
-      const int w = i / (CS_T * CS_FPW), t = (i / CS_FPW) % CS_T, fl = i % CS_FPW;
-      float s = 0.f;
+    for (int i = tid; i < B * CS_FPW * (CS_T / 4); i += CS_NT) {
+      const int w = i / (CS_FPW * (CS_T / 4)), fl = (i / (CS_T / 4)) % CS_FPW, t4 = 4 * (i % (CS_T / 4));
+      float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
       for (int j = 0; j < CS_OP; ++j)
-        if (j < O) s = fmaf(dout[w][j], wd[j][t][fl], s);
-      act[w][t][fl] = act[w][t][fl] > 0.f ? ks * s : 0.f;
+        if (j < O) {
+          const float d = dout[w][j];
+          const float4 wv = *reinterpret_cast<const float4*>(&wd[j][fl][t4]);
+          s.x = fmaf(d, wv.x, s.x);
+          s.y = fmaf(d, wv.y, s.y);
+          s.z = fmaf(d, wv.z, s.z);
+          s.w = fmaf(d, wv.w, s.w);
+        }
+      float4* ap = reinterpret_cast<float4*>(&act[w][fl][t4]);
+      const float4 av = *ap;
+      *ap = make_float4(av.x > 0.f ? ks * s.x : 0.f, av.y > 0.f ? ks * s.y : 0.f, av.z > 0.f ? ks * s.z : 0.f,
+                        av.w > 0.f ? ks * s.w : 0.f);
     }
     __syncthreads();
     stamp(6);
     // dWc[fl][kk] = sum_{t, w} dP[w][t][fl] x[w][t + kk] (kk = taps: the conv bias, sum dP): task
     // (fl, kk, t) with t fastest sums over the windows (consecutive lanes read consecutive
     // steps: the window-strided form of this loop ran into 16-way bank conflicts, 10 us)
-    for (int i = tid; i < CS_FPW * (CS_TAPS + 1) * CS_T; i += CS_NT) {
-      const int fl = i / ((CS_TAPS + 1) * CS_T), kk = (i / CS_T) % (CS_TAPS + 1), t = i % CS_T;
-      float s = 0.f;
-      for (int w0 = 0; w0 < B; w0 += 4) {
+    // task (filter, 4 steps, window class w % 4, tap half): one float4 of dP and three of x give
+    // 4 x 7 products per window; the partial for (filter, tap) lands in gwc[fl][kk][4 t4i + wq]
+    // (36 partials per parameter, summed in the SGD below)
+    // (the tap half is wave-uniform: threads [0, 144) take kk 0..6, threads [192, 336) kk 7..13,
+    // so both halves index their x registers with compile-time offsets)
+    auto dwc_half = [&](auto khc, int u) {
+      constexpr int kh = decltype(khc)::value;
+      const int wq = u & 3, t4i = (u >> 2) % (CS_T / 4), fl = u / (4 * (CS_T / 4));
+      const int t4 = 4 * t4i;
+      float s[7];
 #pragma unroll
-        for (int w = w0; w < w0 + 4; ++w) s = fmaf(act[w][t][fl], kk < CS_TAPS ? xs[w][t + kk] : 1.f, s);
+      for (int q = 0; q < 7; ++q) s[q] = 0.f;
+      for (int w = wq; w < B; w += 4) {  // B % 4 == 0 (launcher)
+        const float4 av = *reinterpret_cast<const float4*>(&act[w][fl][t4]);
+        const float d[4] = {av.x, av.y, av.z, av.w};
+        float xw[12];  // x[t4 + 4 kh + j]
+#pragma unroll
+        for (int c = 0; c < 3; ++c)
+          *reinterpret_cast<float4*>(&xw[4 * c]) = *reinterpret_cast<const float4*>(&xs[w][t4 + 4 * kh + 4 * c]);
+#pragma unroll
+        for (int q = 0; q < 7; ++q) {
+          const int kk = 7 * kh + q;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) s[q] = fmaf(d[e], kk < CS_TAPS ? xw[e + kk - 4 * kh] : 1.f, s[q]);
+        }
       }
-      gwc[fl][kk][t] = s;
-    }
+#pragma unroll
+      for (int q = 0; q < 7; ++q) gwc[fl][7 * kh + q][4 * t4i + wq] = s[q];
+    };
+    constexpr int NDWC = CS_FPW * (CS_T / 4) * 4;  // 144
+    if (tid < NDWC) dwc_half(std::integral_constant<int, 0>{}, tid);
+    else if (tid >= 192 && tid < 192 + NDWC) dwc_half(std::integral_constant<int, 1>{}, tid - 192);
     __syncthreads();
     stamp(7);
     // ---- Keras SGD (lr / (1 + decay * iterations), momentum, Nesterov) on the own parameters and
@@ -351,13 +408,11 @@ __global__ __launch_bounds__(CS_NT, 1) void cnn_small_kernel(const CnnSmallArgs 
       v = vn;
       p += a.nesterov ? (a.momentum * vn - lr_t * gi) : vn;
     };
-#pragma unroll
-    for (int q = 0; q < (CS_OP * CS_T * CS_FPW + CS_NT - 1) / CS_NT; ++q) {
-      const int i = tid + CS_NT * q;
-      if (i < CS_OP * CS_T * CS_FPW) {
-        const int j = i / (CS_T * CS_FPW), t = (i / CS_FPW) % CS_T, fl = i % CS_FPW;
-        if (j < O && f0 + fl < a.filters) sgd(wd[j][t][fl], vd[j][t][fl], gwd[q]);
-      }
+    if (tid < NWD && dj < O && f0 + dfl < a.filters) {
+      sgd(wd[dj][dfl][dt4], vd[dj][dfl][dt4], gwd.x);
+      sgd(wd[dj][dfl][dt4 + 1], vd[dj][dfl][dt4 + 1], gwd.y);
+      sgd(wd[dj][dfl][dt4 + 2], vd[dj][dfl][dt4 + 2], gwd.z);
+      sgd(wd[dj][dfl][dt4 + 3], vd[dj][dfl][dt4 + 3], gwd.w);
     }
     if (tid < CS_FPW * CS_KC) {
       const int fl = tid / CS_KC, kk = tid % CS_KC;
@@ -385,10 +440,10 @@ __global__ __launch_bounds__(CS_NT, 1) void cnn_small_kernel(const CnnSmallArgs 
     a.vel[e] = vc[fl][kk];
   }
   for (int i = tid; i < CS_OP * CS_T * CS_FPW; i += CS_NT) {
-    const int j = i / (CS_T * CS_FPW), t = (i / CS_FPW) % CS_T, fl = i % CS_FPW;
+    const int j = i / (CS_T * CS_FPW), fl = (i / CS_T) % CS_FPW, t = i % CS_T;
     const long e = oWd + (long)j * CS_T * CS_FP + t * CS_FP + f0 + fl;
-    a.p[e] = wd[j][t][fl];
-    a.vel[e] = vd[j][t][fl];
+    a.p[e] = wd[j][fl][t];
+    a.vel[e] = vd[j][fl][t];
   }
   if (wk == 0 && tid < CS_OP) {
     a.p[obd + tid] = bd[tid];
