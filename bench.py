@@ -387,13 +387,52 @@ def bench_mlp(args, ctx, online: bool):
         def step():
             streamer.next()
             run.run(streamer.last_slot)
+
+        many = None
+        if ctx.world_size == 1 and not args.no_small and eng.small_steps_reason(B, opt) is None:
+            # small batches on one GPU: the job's path (train/online.py _ChunkStage) — a stream
+            # chunk of n batches crosses PCIe as ONE async copy into a device buffer (two,
+            # alternating: the next chunk's copy overlaps this launch) and its batches train as
+            # n complete steps per persistent launch (NativeMLP.fused_steps)
+            nmax = max(1, min(args.steps, 256))
+            xh, yh = synth_tabular_batch(nmax * B, F, seed=1000 * ctx.rank)
+            xh = eng.to_input_format(xh).pin_memory()
+            yh = yh.float().pin_memory()
+            bufs = [(torch.empty_like(xh, device=ctx.device), torch.empty_like(yh, device=ctx.device)) for _ in range(2)]
+            cstream, events, staged, launches = torch.cuda.Stream(ctx.device), [None, None], [0, 0], [0]
+
+            def stage(j, rows):  # launch j's rows (the next launch's: prefetched behind this one)
+                with torch.cuda.stream(cstream):
+                    # buffer j % 2 was last read by launch j - 2, enqueued before this copy
+                    cstream.wait_stream(torch.cuda.current_stream(ctx.device))
+                    bufs[j % 2][0][:rows].copy_(xh[:rows], non_blocking=True)
+                    bufs[j % 2][1][:rows].copy_(yh[:rows], non_blocking=True)
+                    events[j % 2] = torch.cuda.Event()
+                    events[j % 2].record(cstream)
+                staged[j % 2] = rows
+
+            def many(n):
+                j = launches[0]
+                launches[0] += 1
+                if j == 0 or staged[j % 2] < n * B:
+                    stage(j, n * B)
+                torch.cuda.current_stream(ctx.device).wait_event(events[j % 2])
+                xb, yb = bufs[j % 2]
+                eng.fused_steps(xb, yb, B, n, opt, gscale, loss_into=run.loss_acc)
+                stage(j + 1, n * B)
+
+            def step():  # noqa: F811
+                many(1)
+
+            extra["small_fused_steps_per_launch"] = nmax
+            extra["online_chunk_rows"] = nmax * B
     else:
         nb = max(1, args.mlp_batches)
         x, y = synth_tabular_batch(B * nb, F, seed=ctx.rank)
         # resident in the engine's input format, as the job path keeps its datasets (Trainer);
         # --mlp-batches N: N distinct resident batches, step i of a graph replay reads batch
         # i % N (fresh rows every step, as a training pass over a table does)
-        x, y = x.to(ctx.device, eng.input_dtype), y.to(ctx.device)
+        x, y = eng.to_input_format(x.to(ctx.device)), y.to(ctx.device)
 
         def inputs(k):
             j = (k[1] if isinstance(k, tuple) else 0) % nb
@@ -418,11 +457,11 @@ def bench_mlp(args, ctx, online: bool):
 
             extra["small_fused_steps_per_launch"] = nmax
     # the streamed config changes its input slot every step: single-step replays
-    el, k, n = _timed(ctx, step, args.steps, args.warmup, args.min_timed_s, None if online else many,
+    el, k, n = _timed(ctx, step, args.steps, args.warmup, args.min_timed_s, many,
                       extra.get("small_fused_steps_per_launch", args.graph_steps), warm_ms=args.warm_ms)
-    if not online and "small_fused_steps_per_launch" in extra:
+    if "small_fused_steps_per_launch" in extra:
         eng.check_device_errors()
-    if online:
+    if online and "small_fused_steps_per_launch" not in extra:
         extra.update(streamer.copy_stats(skip=1))
         extra["h2d_mb_per_step"] = round((streamer.slots[0][0].numel() * streamer.slots[0][0].element_size()
                                           + streamer.slots[0][1].numel() * 4) / 1e6, 3)

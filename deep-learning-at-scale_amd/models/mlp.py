@@ -175,8 +175,9 @@ class NativeMLP:
         self.Fp = _r8(n_features)
         self.X = torch.zeros(batch * self.Fp, dtype=bf, device=dev)
         # the MFMA input format: the Trainer keeps resident datasets in it (half the bytes of
-        # fp32, and the per-step gather IS the engine's input: no cast kernel)
-        self.input_dtype = torch.bfloat16 if self.Fp == n_features else torch.float32
+        # fp32, and the per-step gather IS the engine's input: no cast kernel): bf16 rows of Fp
+        # columns, the features zero-padded to a multiple of 8 (to_input_format)
+        self.input_dtype = torch.bfloat16
         self._Xop = self.X  # the X operand of the current step (self.X or a bf16 batch read in place)
         self.Hs = [torch.empty(batch * h, dtype=bf, device=dev) for h in self.hidden]
         self.dZ = [torch.empty(batch * h, dtype=bf, device=dev) for h in self.hidden]
@@ -292,21 +293,35 @@ class NativeMLP:
                           None if self.dw2_gemm else gl[1][0], 0)
         return ls
 
+    def to_input_format(self, X) -> torch.Tensor:
+        """A dataset ([N][F], any dtype / device) in the engine's resident input format: bf16
+        [N][Fp], features zero-padded to Fp (a multiple of 8). Every path reads it in place or
+        copies it as is — the K-step launches (fused_steps) and the row-indexed step need it."""
+        X = torch.as_tensor(X)
+        if X.dim() == 2 and X.shape[1] == self.Fp and X.dtype == torch.bfloat16:
+            return X
+        if X.shape[1] == self.Fp:
+            return X.to(torch.bfloat16)
+        out = torch.zeros((X.shape[0], self.Fp), dtype=torch.bfloat16, device=X.device)
+        out[:, : self.F] = X
+        return out
+
     def _load_x(self, x: torch.Tensor) -> int:
         B = x.shape[0]
-        assert B <= self.B and x.shape[1] == self.F
+        assert B <= self.B and x.shape[1] in (self.F, self.Fp)
+        fmt = x.shape[1] == self.Fp  # input-format width (to_input_format; == F when F % 8 == 0)
         self._Xop_rows = B
         self._Xop = self.X
         Xv = self.X[: B * self.Fp].view(B, self.Fp)
-        if (self.x_inplace and x.dtype == torch.bfloat16 and self.Fp == self.F and x.is_contiguous()
+        if (self.x_inplace and x.dtype == torch.bfloat16 and fmt and x.is_contiguous()
                 and x.device == self.device
                 and x.data_ptr() % 16 == 0):
             # already in the MFMA input format (bf16-streamed online batches, whose ring slot
             # is not overwritten before this step's kernels ran): read it in place
             self._Xop = x.view(-1)
-        elif x.dtype == torch.bfloat16 and self.Fp == self.F:
+        elif x.dtype == torch.bfloat16 and fmt:
             Xv.copy_(x)
-        elif self.Fp == self.F:
+        elif fmt:
             self._C.cast_bf16(x.contiguous().float(), Xv)
         else:
             self._C.transpose_cast_bf16(x.t().contiguous().float(), B, self.F, B, Xv, self.Fp)

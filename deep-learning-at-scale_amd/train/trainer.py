@@ -119,6 +119,17 @@ MAX_SLICED_STEPS = 128
 SMALL_STEPS_PER_LAUNCH = 256
 
 
+def _input_format(eng, Xd):
+    """A resident dataset in the engine's input format (``to_input_format``, else ``input_dtype``)."""
+    if not torch.is_tensor(Xd):
+        return Xd
+    fmt = getattr(eng, "to_input_format", None)
+    if fmt is not None:
+        return fmt(Xd)
+    in_dt = getattr(eng, "input_dtype", None)
+    return Xd.to(in_dt) if in_dt is not None and Xd.dtype != in_dt else Xd
+
+
 def _to_dev(a, device):
     if hasattr(a, "to") and hasattr(a, "starts"):  # data.features.SeriesWindows: rows + starts
         return a.to(device)
@@ -164,9 +175,7 @@ class Trainer:
         if nbytes > torch.cuda.get_device_properties(eng.device).total_memory // 8:
             return X, Y  # a split this large stays on the host (chunked path)
         Xd, Yd = _to_dev(X, eng.device), _to_dev(Y, eng.device)  # windows: rows + starts on the device
-        in_dt = getattr(eng, "input_dtype", None)
-        if in_dt is not None and torch.is_tensor(Xd) and Xd.dtype != in_dt:
-            Xd = Xd.to(in_dt)
+        Xd = _input_format(eng, Xd)
         self._idx[key] = (X, Y, Xd, Yd)
         return Xd, Yd
 
@@ -531,9 +540,7 @@ class Trainer:
         dev = self.eng.device
         # resident dataset in device memory (288 GB HBM: the small well-log sets fit whole)
         Xd, Yd = _to_dev(Xtr, dev), _to_dev(Ytr, dev)
-        in_dt = getattr(self.eng, "input_dtype", None)
-        if in_dt is not None and torch.is_tensor(Xd) and Xd.dtype != in_dt:
-            Xd = Xd.to(in_dt)  # engine input format (NativeMLP: bf16, read in place)
+        Xd = _input_format(self.eng, Xd)  # engine input format (NativeMLP: bf16 [N][Fp], read in place)
         n = len(Xd)
         b = self._local_batch(n)
         per_rank = n // max(ctx.world_size, 1)

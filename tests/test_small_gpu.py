@@ -272,3 +272,40 @@ def test_cnn_small_spin_bound_fails_loudly():
     eng.fused_steps(X[: 4 * B], Y[: 4 * B], B, 4, opt, 1.0 / B)
     torch.cuda.synchronize()
     eng.check_device_errors()
+
+
+def test_online_job_stages_chunks_into_k_step_launches(tmp_path, monkeypatch):
+    """mlp_online at its job default (256-row batches, one GPU): every stream chunk is one
+    host -> HBM copy and its batches run as K-step launches (train/online.py _ChunkStage);
+    the per-chunk training losses match the per-batch ring path (regular one-launch steps)."""
+    from wellflow.models.mlp import NativeMLP
+    from wellflow.train import online
+    from wellflow.train.job import run_job
+
+    used = []
+
+    class Spy(online._ChunkStage):
+        def __init__(self, *a, **k):
+            used.append(1)
+            super().__init__(*a, **k)
+
+    monkeypatch.setattr(online, "_ChunkStage", Spy)
+    names = "well,field,t,whp,choke,glr,temp,water_cut,dsp,flow"
+    types = "string,string,int,float,float,float,float,float,float,float"
+
+    def job(sub):
+        args = [names, types, "flow", str(tmp_path / sub), "--epochs", "2", "--synth-wells", "8",
+                "--synth-steps", "600", "--device", "cuda", "--online-chunk", "1024", "--seed", "3"]
+        return run_job("mlp_online", args, log=lambda *a, **k: None)
+
+    a = job("staged")
+    assert used and a["native"] is True
+    monkeypatch.setattr(NativeMLP, "small_steps_reason", lambda self, *args, **kw: "off")
+    used.clear()
+    b = job("ring")
+    assert not used
+    la, lb = a["history"]["loss"], b["history"]["loss"]
+    assert len(la) == len(lb) >= 4
+    for x, y in zip(la, lb):
+        assert abs(x - y) <= 0.03 * abs(y) + 1e-4, (la, lb)
+    assert abs(a["test_loss"] - b["test_loss"]) <= 0.05 * abs(b["test_loss"]) + 1e-4
