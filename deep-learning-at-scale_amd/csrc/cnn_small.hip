@@ -72,7 +72,7 @@ __global__ __launch_bounds__(CS_NT, 1) void cnn_small_kernel(const CnnSmallArgs 
   __shared__ float bd[CS_OP], vb[CS_OP];
   __shared__ __attribute__((aligned(16))) float gwc[CS_FPW][CS_TAPS + 1][CS_T];  // dWc partials per output step
   __shared__ float lred[CS_NT / 64];
-  __shared__ float red2[48][28];                   // hop 1 of the output sums: [own output][share]
+  __shared__ __attribute__((aligned(16))) float red2[48][28];  // hop 1 of the output sums: [own output][share]
   __shared__ unsigned sflag;
 
   const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)a.scr, 0, 0x7FFFFFFF, 0x00020000);
@@ -155,6 +155,7 @@ __global__ __launch_bounds__(CS_NT, 1) void cnn_small_kernel(const CnnSmallArgs 
   fetch_ids(0);
   prefetch();
   fetch_ids(1);
+  for (int i = tid; i < 48 * 28; i += CS_NT) (&red2[0][0])[i] = 0.f;
   __syncthreads();
 
   unsigned gspins = 0;
@@ -235,8 +236,9 @@ __global__ __launch_bounds__(CS_NT, 1) void cnn_small_kernel(const CnnSmallArgs 
     }
     stamp(3);
     // ---- the shares are summed in two hops (one 25-way read of every output per worker moved
-    // 48 KiB per worker per poll round: 9.4 us): worker wk sums outputs o = wk + G l over the G
-    // shares (fixed order) and publishes them; then every worker reads the B x O sums
+    // 48 KiB per worker per poll round: 9.4 us; watching one granule per producer, then reading
+    // all shares once: 5.4 us, the bulk read alone 3.5): worker wk sums outputs o = wk + G l over
+    // the G shares (fixed order) and publishes them; then every worker reads the B x O sums
     auto poll_more = [&](bool ok) {
       if (__builtin_amdgcn_ballot_w64(!ok) == 0ull || sflag != 0u) return false;
       if ((++gspins & 63u) == 0u &&
@@ -274,9 +276,19 @@ __global__ __launch_bounds__(CS_NT, 1) void cnn_small_kernel(const CnnSmallArgs 
     __syncthreads();
     for (int l = tid; l < nl; l += CS_NT) {
       float sum = 0.f;
-      for (int g = 0; g < G; ++g) sum += red2[l][g];
+      // shares g >= G stay zero (cleared at launch start): 7 float4 reads, one add chain in share
+      // order (a runtime-bounded loop was 25 dependent LDS round trips, ~0.6 us)
+#pragma unroll
+      for (int c = 0; c < 7; ++c) {
+        const float4 v = *reinterpret_cast<const float4*>(&red2[l][4 * c]);
+        sum += v.x;
+        sum += v.y;
+        sum += v.z;
+        sum += v.w;
+      }
       st8(__float_as_uint(sum), tag, CS_P2 + (par * CS_MAXB * CS_OP + wk + G * l) * 2);
     }
+    stamp(9);
     // ---- every output: prediction, loss, dOut
     float lsum = 0.f;
     for (int i0 = 0; i0 < nout; i0 += CS_NT) {
@@ -311,6 +323,7 @@ __global__ __launch_bounds__(CS_NT, 1) void cnn_small_kernel(const CnnSmallArgs 
         dout[w][j] = dd * a.scale;
       }
     }
+    stamp(10);
     if (wk == 0) {
       const float ls = block_sum<CS_NT>(lsum, lred);
       if (tid == 0 && a.loss_acc != nullptr) atomicAdd(a.loss_acc, ls);
@@ -469,6 +482,7 @@ bool launch_cnn_small(const CnnSmallArgs& a, hipStream_t s) {
     return false;
   const int G = (a.filters + CS_FPW - 1) / CS_FPW;
   if (G * CS_FPW > CS_FP || G > 28 || CS_P2 + 2 * CS_MAXB * CS_OP * 2 > kCnnSmallScratch) return false;
+  if ((a.B * a.O + G - 1) / G > 48) return false;  // hop-1 outputs per worker (red2 rows)
   hipLaunchKernelGGL(cnn_small_kernel, dim3(G), dim3(CS_NT), 0, s, a);
   return true;
 }

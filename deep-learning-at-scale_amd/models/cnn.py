@@ -282,6 +282,9 @@ class NativeCNN:
             return f"window {L.input_len}x{L.in_ch}, kernel {L.kernel} (needs the reference's 48 x 1, 13)"
         if not 4 <= B <= self.SMALL_MAX_B or B % 4:
             return f"batch {B} (needs 4 <= B <= {self.SMALL_MAX_B}, B % 4 == 0)"
+        G = -(-L.filters // 4)  # workgroups of 4 filters; each sums <= 48 of the B x outputs
+        if G > 28 or -(-B * L.outputs // G) > 48:
+            return f"{L.filters} filters x batch {B} x {L.outputs} outputs (needs <= 112 filters, <= 48 outputs per 4 filters)"
         if opt is not None:
             from ..optim.flat import FlatSGD
 

@@ -1,5 +1,5 @@
 """Phase timeline of the persistent small-batch CNN launch (csrc/cnn_small.hip): s_memrealtime
-(100 MHz) stamps at 9 phase boundaries of every step, thread 0 of each worker.
+(100 MHz) stamps at 11 phase boundaries of every step, thread 0 of each worker.
 
     python tools/small_timeline_cnn.py [B]   -> median microseconds per phase (steps 8..63)
 """
@@ -42,3 +42,6 @@ print(f"step period (median over workers): {statistics.median(per):.2f} us")
 for p in range(8):
     d = [float(s[w, k, p + 1] - s[w, k, p]) for w in range(G) for k in range(8, K)]
     print(f"  {PH[p]:<24} median {statistics.median(d):6.2f} us  max {max(d):6.2f}")
+for name, a, b in (("hop 1 (own sums)", 3, 9), ("hop 2 poll", 9, 10), ("loss / dOut tail", 10, 4)):
+    d = [float(s[w, k, b] - s[w, k, a]) for w in range(G) for k in range(8, K)]
+    print(f"    of the poll: {name:<18} median {statistics.median(d):6.2f} us  max {max(d):6.2f}")
