@@ -173,6 +173,24 @@ void lstm_pack_x(const at::Tensor& x, const at::Tensor& XH, int64_t B, int64_t T
   wf::launch_lstm_pack_x(fp(x), bfp(XH), d, cur_stream(), full);
 }
 
+// the batch's windows read in place from the resident row table: batch row b = rows
+// starts[idx[b]] .. + T - 1 of `table` (data/features.py SeriesWindows)
+void lstm_pack_x_win(const at::Tensor& table, const at::Tensor& starts, const at::Tensor& idx, const at::Tensor& XH,
+                     int64_t B, int64_t T, int64_t F, int64_t KX, int64_t H, bool full) {
+  auto d = lstm_dims(B, T, F, KX, H);
+  check_t(table, at::kFloat, "table");
+  TORCH_CHECK(table.dim() == 2 && table.size(1) == F && table.size(0) >= T, "lstm_pack_x_win: table must be [>= T][F]");
+  check_t(starts, at::kLong, "starts");
+  check_t(idx, at::kLong, "idx");
+  check_extent(idx, B, "idx");
+  TORCH_CHECK(starts.numel() >= 1, "lstm_pack_x_win: no windows");
+  check_t(XH, at::kBFloat16, "XH");
+  check_extent(XH, (T + 1) * B * (KX + H), "XH");
+  const c10::hip::OptionalHIPGuardMasqueradingAsCUDA guard(table.device());
+  wf::launch_lstm_pack_x(fp(table), bfp(XH), d, cur_stream(), full, reinterpret_cast<const long*>(starts.data_ptr<int64_t>()),
+                         reinterpret_cast<const long*>(idx.data_ptr<int64_t>()), starts.numel(), table.size(0));
+}
+
 // cf32: fp32 [Bp][H] in-place state slab of the per-step path (c_{t-1} -> c_t; e.g. the
 // engine's dcarry buffer, which the backward re-initialises)
 void lstm_forward(const at::Tensor& XH, const at::Tensor& Wp, const at::Tensor& Cst,
@@ -1213,6 +1231,7 @@ PYBIND11_MODULE(_C, m) {
   WF_DEF(cnn_small_steps);
   WF_DEF(cnn_small_scratch_floats);
   WF_DEF(lstm_pack_x);
+  WF_DEF(lstm_pack_x_win);
   WF_DEF(lstm_forward);
   WF_DEF(lstm_forward_persistent);
   WF_DEF(lstm_backward);

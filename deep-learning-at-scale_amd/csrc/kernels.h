@@ -48,7 +48,9 @@ struct LstmDims {
 // WELLFLOW_PF_DBG bits the HIP objects were built to honour (persistent_guard.h kDbgMask):
 // 1 << 21 (the force-timeout TEST hook) in production builds, everything in WF_DIAG builds
 int dbg_mask();
-void launch_lstm_pack_x(const float* x, bf16_t* XH, LstmDims d, hipStream_t s, bool full = true);
+// starts / idx (optional): x is a [nrows][F] row table, batch row b = the window at row starts[idx[b]]
+void launch_lstm_pack_x(const float* x, bf16_t* XH, LstmDims d, hipStream_t s, bool full = true,
+                        const long* starts = nullptr, const long* idx = nullptr, long nwin = 0, long nrows = 0);
 // Cst: the cell-state history c_t (bf16, FN layout, slab t + 1; slab 0 = c_{-1} = 0) the backward
 // reads; the per-step forward carries c in fp32 in the in-place state slab cf32 ([Bp][H], FN).
 void launch_lstm_fwd_step(int t, bf16_t* XH, const bf16_t* Wp, bf16_t* Cst, bf16_t* S, float* cf32,

@@ -29,8 +29,17 @@ namespace wf {
 // cpr = 16-B chunks written per row: all KX/8 (full: the constant 1 column and the zero
 // padding too) or only the ones holding features and the 1 column (the rest of the x block is
 // constant, so after one full pack of a buffer the per-step pack writes 3 of 8 chunks at F = 16)
+// win != nullptr: x is a per-row feature table [nrows][F] and batch row b is the length-T
+// window starting at row starts[idx[b]] (data/features.py SeriesWindows read in place: the job's
+// per-step torch gather of the [B][T][F] windows cost ~150 us of a 4.2-ms step)
+struct PackWin {
+  const long* starts;
+  const long* idx;
+  long nwin, nrows;
+};
+
 __global__ void lstm_pack_x_kernel(const float* __restrict__ x, bf16_t* __restrict__ XH,
-                                   LstmDims d, int cpr) {
+                                   LstmDims d, int cpr, PackWin win) {
   const int KA = d.KX + d.H, CPR = cpr;
   const long total = (long)d.T * d.B * CPR;
   for (long idx = blockIdx.x * (long)blockDim.x + threadIdx.x; idx < total;
@@ -39,7 +48,16 @@ __global__ void lstm_pack_x_kernel(const float* __restrict__ x, bf16_t* __restri
     const long row = idx / CPR;  // = t * B + b
     const long b = row % d.B;
     const int t = (int)(row / d.B);
-    const float* src = x + (b * d.T + t) * d.F;
+    const float* src;
+    if (win.idx != nullptr) {  // ids clamped into the tables (a bad id reads a valid row, never faults)
+      long w = win.idx[b];
+      w = w < 0 ? 0 : (w >= win.nwin ? win.nwin - 1 : w);
+      long r0 = win.starts[w];
+      r0 = r0 < 0 ? 0 : (r0 > win.nrows - d.T ? win.nrows - d.T : r0);
+      src = x + (r0 + t) * d.F;
+    } else {
+      src = x + (b * d.T + t) * d.F;
+    }
     unsigned pk[4];
     // 8 features: two 16-B loads (rows are 16-B aligned when F % 4 == 0 and x is)
     if ((d.F & 3) == 0 && c + 8 <= d.F && ((uintptr_t)x & 15u) == 0) {
@@ -62,7 +80,8 @@ __global__ void lstm_pack_x_kernel(const float* __restrict__ x, bf16_t* __restri
   }
 }
 
-void launch_lstm_pack_x(const float* x, bf16_t* XH, LstmDims d, hipStream_t s, bool full) {
+void launch_lstm_pack_x(const float* x, bf16_t* XH, LstmDims d, hipStream_t s, bool full, const long* starts,
+                        const long* idx, long nwin, long nrows) {
   // per-step packs round the chunks written up to whole 64-B segments (4 chunks; the rest of the
   // block is the constant zero padding): 48 of a row's 128-B x block left a partial 32-B sector
   int cpr = full ? (d.KX >> 3) : ((d.F + 1 + 7) / 8 + 3) / 4 * 4;
@@ -70,7 +89,7 @@ void launch_lstm_pack_x(const float* x, bf16_t* XH, LstmDims d, hipStream_t s, b
   const long total = (long)d.T * d.B * cpr;
   int blocks = (int)((total + 255) / 256);
   if (blocks > 16384) blocks = 16384;
-  hipLaunchKernelGGL(lstm_pack_x_kernel, dim3(blocks), dim3(256), 0, s, x, XH, d, cpr);
+  hipLaunchKernelGGL(lstm_pack_x_kernel, dim3(blocks), dim3(256), 0, s, x, XH, d, cpr, PackWin{starts, idx, nwin, nrows});
 }
 
 // STAGES == 0: register-staged mainloop (any batch); STAGES >= 2: direct-to-LDS ring

@@ -183,6 +183,7 @@ class NativeLSTM:
     """
 
     native = True
+    window_indexed = True  # forward_backward(windows, y, ..., rows=) reads the windows in place
 
     def __init__(self, n_features: int, hidden: int, seq_len: int, batch: int,
                  device="cuda", params: torch.Tensor | None = None,
@@ -388,17 +389,25 @@ class NativeLSTM:
                    None, None, 0.0)
         return self.pred[:B]
 
-    def forward_backward(self, x: torch.Tensor, y: torch.Tensor, grad_scale: float,
+    def forward_backward(self, x, y: torch.Tensor, grad_scale: float,
                          zero_grads: bool = True, step: int = 0,
-                         loss_into: torch.Tensor | None = None) -> torch.Tensor:
+                         loss_into: torch.Tensor | None = None, rows: torch.Tensor | None = None) -> torch.Tensor:
         """One training forward + backward on a full batch; grads land in ``self.grads``.
 
         Gradient of ``grad_scale * sum_i loss_i`` (models/base.py contract; use
         1 / global_batch for the mean over all data-parallel ranks). Returns the device
-        scalar sum of per-sample losses of this batch (no host sync).
+        scalar sum of per-sample losses of this batch (no host sync). ``rows`` (int64, device):
+        ``x`` is a resident :class:`~wellflow.data.features.SeriesWindows` and ``y`` its
+        targets; the batch is windows ``rows`` — read in place by the x-pack kernel
+        (``window_indexed``: no per-step gather of the [B][T][F] windows).
         """
         B = self.B
-        assert x.shape == (B, self.T, self.F) and y.shape == (B,)
+        if rows is not None:
+            assert rows.shape == (B,) and x.rows.shape[1] == self.F and x.T == self.T
+            y = y.index_select(0, rows)
+        else:
+            assert x.shape == (B, self.T, self.F)
+        assert y.shape == (B,)
         C = self._C
         lay = self.lay
         W, w_out, b_out = lay.views(self.params)
@@ -410,7 +419,11 @@ class NativeLSTM:
         ls = loss_into if loss_into is not None else self.loss_sum
         if loss_into is None:
             self.loss_sum.zero_()
-        self._pack_x(x.contiguous(), B)
+        if rows is not None:
+            self._C.lstm_pack_x_win(x.rows, x.starts, rows, self.XH, *self._dims(B), not self._xh_const)
+            self._xh_const = True
+        else:
+            self._pack_x(x.contiguous(), B)
         self._forward_steps(B)
         hT = self._hT(B)
         y = y.contiguous().float()

@@ -119,6 +119,12 @@ MAX_SLICED_STEPS = 128
 SMALL_STEPS_PER_LAUNCH = 256
 
 
+def _resident_windows(X, device) -> bool:
+    rows = getattr(X, "rows", None)
+    return (torch.is_tensor(rows) and torch.is_tensor(getattr(X, "starts", None)) and rows.device == device
+            and rows.dtype == torch.float32 and rows.is_contiguous() and rows.dim() == 2)
+
+
 def _input_format(eng, Xd):
     """A resident dataset in the engine's input format (``to_input_format``, else ``input_dtype``)."""
     if not torch.is_tensor(Xd):
@@ -433,6 +439,9 @@ class Trainer:
             idx = self._idx[b] = torch.zeros(b, dtype=torch.long, device=eng.device)
 
         row_indexed = getattr(eng, "row_indexed", False) and torch.is_tensor(Xd)
+        # resident windows (SeriesWindows on the device) that the engine reads in place through
+        # the step's window ids (NativeLSTM: the x-pack kernel gathers them)
+        row_indexed = row_indexed or (getattr(eng, "window_indexed", False) and _resident_windows(Xd, eng.device))
         # groups of n steps as ONE graph replay (StepRunner.run_many): step i of a group reads its
         # rows from slice i of a static order buffer filled by one copy per group; the per-step
         # index copy + replay gap (~8 us of a 165-us MLP step) goes away. Row-indexed engines,

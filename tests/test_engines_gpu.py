@@ -582,3 +582,35 @@ def test_mlp_one_launch_step_matches_two_kernel_step(B, F, indexed):
             assert (a != b).float().mean().item() < 0.01, name
             assert ((a - b).norm() / a.norm()).item() < 1e-3, name
             assert ((a == 0) != (b == 0)).float().mean().item() < 1e-5, name
+
+
+def test_lstm_reads_resident_windows_in_place():
+    """NativeLSTM.forward_backward(windows, y, rows=ids): the x-pack kernel reads the batch's
+    windows straight from the resident row table (data/features.py SeriesWindows) — the same
+    packed input, loss and gradients as the gathered [B][T][F] batch."""
+    from wellflow.data.features import SeriesWindows
+    from wellflow.models.lstm import NativeLSTM, init_lstm_flat
+
+    B, T, F, H = 512, 16, 16, 512
+    g = torch.Generator(device=DEV).manual_seed(3)
+    table = torch.randn(5000, F, device=DEV, generator=g)
+    starts = torch.randint(0, 5000 - T + 1, (3000,), device=DEV, generator=g)
+    win = SeriesWindows(table, starts, T)
+    yall = torch.randn(3000, device=DEV, generator=g)
+    ids = torch.randperm(3000, device=DEV, generator=g)[:B]
+    out = []
+    for inplace in (False, True):
+        eng = NativeLSTM(F, H, T, B, device=DEV)
+        eng.params.copy_(init_lstm_flat(F, H, seed=4).to(DEV))
+        eng.sync_weights()
+        if inplace:
+            ls = eng.forward_backward(win, yall, 1.0 / B, rows=ids)
+        else:
+            ls = eng.forward_backward(win[ids], yall.index_select(0, ids), 1.0 / B)
+        torch.cuda.synchronize()
+        xb = eng.XH.view(T + 1, B, -1)[:T, :, : eng.lay.KX].clone()
+        out.append((ls.item(), eng.grads.clone(), xb))
+    (la, ga, xa), (lb, gb, xbb) = out
+    assert torch.equal(xa, xbb)
+    assert abs(la - lb) <= 1e-6 * abs(lb)
+    assert _rel(gb, ga) < 1e-3
