@@ -252,7 +252,7 @@ static void launch_dw_192(const bf16_t* A, long lda, const bf16_t* B, long ldb, 
 // 256x192, 8 waves of 64x96, 32-deep half steps through an NSLOT-deep ring (gemm_core.h
 // gemm_mainloop_glds_h): the same tile as launch_dw_192 with its DMA issued NSLOT - 1 half
 // steps ahead instead of one 64-deep step
-template <int BM, int BN, int NSLOT, int WM, int WN, int PRIO, int BKD = 32, bool GL = false>
+template <int BM, int BN, int NSLOT, int WM, int WN, int PRIO, int BKD = 32, bool GL = false, int DG = 0>
 __global__ __launch_bounds__(64 * WM * WN) void gemm_dw_h_kernel(const bf16_t* __restrict__ A, long lda,
                                                         const bf16_t* __restrict__ B, long ldb, int N,
                                                         int kchunk, int tiles, float* __restrict__ out,
@@ -266,7 +266,7 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_dw_h_kernel(const bf16_t* _
   const int split = L / tiles, t = L % tiles;
   const int m0 = (t / tiles_n) * BM, n0 = (t % tiles_n) * BN;
   f32x4 acc[C::TM][C::TN];
-  gemm_mainloop_glds_h<C, NSLOT, PRIO, BKD, GL>(A, lda, B, ldb, split * kchunk, kchunk / BKD, m0, n0, smem, acc);
+  gemm_mainloop_glds_h<C, NSLOT, PRIO, BKD, GL, DG>(A, lda, B, ldb, split * kchunk, kchunk / BKD, m0, n0, smem, acc);
   const AccCoord<C> cc(m0, n0);
   if (slab != nullptr) {  // this split's partial tile, plain-stored (dw_slab_reduce_kernel adds the splits)
     float* o = slab + (size_t)split * slab_stride;
@@ -359,7 +359,7 @@ __global__ __launch_bounds__(256) void dw_slab_reduce_kernel(float* __restrict__
 // FLOP per staged byte than 256x192 (the dW loop's LDS-DMA bytes per CU per step, not its
 // MFMAs or the DMA latency, track its time across tiles: 256x128 1.33, 256x192 1.17 ms)
 static void launch_dw_288w(const bf16_t* A, long lda, const bf16_t* B, long ldb, int M, int N, int K,
-                           int ksplit, const GemmEpilogue& e, hipStream_t s, bool gl = false) {
+                           int ksplit, const GemmEpilogue& e, hipStream_t s, bool gl = false, int dg = 0) {
   constexpr int BM = 256, BN = 288;
   const int tiles = (M / BM) * (N / BN);
   // one workgroup per CU: 16 tiles x split-K 16 on 256 CUs (tools/dw_tiles.py, B = 8192:
@@ -381,7 +381,15 @@ static void launch_dw_288w(const bf16_t* A, long lda, const bf16_t* B, long ldb,
   // s_setprio 1 around each MFMA cluster (static priority for waves 4-7 measured slower, r4/lstm_dw_prio;
   // the WELLFLOW_DW288_PRIO knob was removed in round 5)
   constexpr int prio = 1;
-  if (gl)  // tile 8 (A/B): the DMA by global_load_lds; measured slower (1.105 vs 1.050 ms, r6/diag/glds.txt)
+  if (dg == 1)  // tiles 9 / 10: diagnostics (wrong results), gemm_core.h gemm_mainloop_glds_h DG
+    hipLaunchKernelGGL((gemm_dw_h_kernel<BM, BN, 4, 4, 2, 1, 32, false, 1>), dim3(tiles * nsplit), dim3(512), 0, s, A,
+                       lda, B, ldb, N, kchunk, tiles, e.outF, e.ldo, e.alpha, use_slab ? e.slab : nullptr,
+                       use_slab ? mn : 0L);
+  else if (dg == 2)
+    hipLaunchKernelGGL((gemm_dw_h_kernel<BM, BN, 4, 4, 2, 1, 32, false, 2>), dim3(tiles * nsplit), dim3(512), 0, s, A,
+                       lda, B, ldb, N, kchunk, tiles, e.outF, e.ldo, e.alpha, use_slab ? e.slab : nullptr,
+                       use_slab ? mn : 0L);
+  else if (gl)  // tile 8 (A/B): the DMA by global_load_lds; measured slower (1.105 vs 1.050 ms, r6/diag/glds.txt)
     hipLaunchKernelGGL((gemm_dw_h_kernel<BM, BN, 4, 4, 2, 1, 32, true>), dim3(tiles * nsplit), dim3(512), 0, s, A, lda,
                        B, ldb, N, kchunk, tiles, e.outF, e.ldo, e.alpha, use_slab ? e.slab : nullptr,
                        use_slab ? mn : 0L);
@@ -400,9 +408,10 @@ static void launch_dw_288w(const bf16_t* A, long lda, const bf16_t* B, long ldb,
 
 void launch_gemm(const bf16_t* A, long lda, int a_mn, const bf16_t* B, long ldb, int b_mn, int M,
                  int N, int K, int ksplit, const GemmEpilogue& e, hipStream_t s, bool glds_ok) {
-  if (a_mn && b_mn && glds_ok && e.atomic && (e.big_tile == 7 || e.big_tile == 8) && M % 256 == 0 && K % 64 == 0) {
+  if (a_mn && b_mn && glds_ok && e.atomic && (e.big_tile >= 7 && e.big_tile <= 10) && M % 256 == 0 && K % 64 == 0) {
     if (N % 288 == 0) {
-      launch_dw_288w(A, lda, B, ldb, M, N, K, ksplit < 1 ? 1 : ksplit, e, s, e.big_tile == 8);
+      launch_dw_288w(A, lda, B, ldb, M, N, K, ksplit < 1 ? 1 : ksplit, e, s, e.big_tile == 8,
+                     e.big_tile >= 9 ? e.big_tile - 8 : 0);
       return;
     }
     if (N % 192 == 0) {  // e.g. H = 128 (KA = 192): the 256x192 tile

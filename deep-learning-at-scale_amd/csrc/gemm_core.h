@@ -590,7 +590,9 @@ struct GldsOpH {
 
 // BKD = 64 with NSLOT = 2: the plain 2-stage ring of gemm_mainloop_glds2, for tiles whose
 // pieces do not split evenly over the waves (the 288-wide image: 36 pieces per 64-deep step)
-template <class C, int NSLOT, int PRIO = 0, int BKD = 32, bool GL = false>
+// DG (diagnostics, tools/dw_tiles.py tiles 9 / 10; results wrong): 1 = the ring's DMA for every
+// other half step only, 2 = no fragment reads and no MFMAs (the DMA + barrier floor)
+template <class C, int NSLOT, int PRIO = 0, int BKD = 32, bool GL = false, int DG = 0>
 __device__ __forceinline__ void gemm_mainloop_glds_h(const bf16_t* __restrict__ A, long lda,
                                                      const bf16_t* __restrict__ B, long ldb, int kbeg,
                                                      int nh, int m0, int n0, char* smem,
@@ -650,11 +652,12 @@ __device__ __forceinline__ void gemm_mainloop_glds_h(const bf16_t* __restrict__ 
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
     const int tn = tt + NSLOT - 1;
-    if (tn < nh) {
+    if (tn < nh && (DG != 1 || (tn & 1) == 0)) {
       constexpr int sn = (u + NSLOT - 1) % NSLOT;
       oa.issue(tn, smem + sn * STAGE, wid);
       ob.issue(tn, smem + sn * STAGE + OA::BYTES, wid);
     }
+    if constexpr (DG == 2) return;
     // slot origin as an opaque per-step value: with u * STAGE folded into every fragment
     // address (beyond the 16-bit ds offset field) the compiler hoisted one address register
     // per (slot, fragment) out of the loop, and the 288-wide tile spilled them

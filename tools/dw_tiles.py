@@ -5,7 +5,10 @@ rounds, and max |diff| against the default tile (3 = 256x192 64-deep 2-stage).
     python tools/dw_tiles.py [tiles ...]      (default: 1 2 3; 4 / 5 = 256x192 with the 5- / 4-slot
                                               32-deep half-step ring; 7 = the production 256x288,
                                               8 = 256x288 with global_load_lds instead of MUBUF
-                                              LDS-DMA; DW_KS=16,32 picks the split-K depths)
+                                              LDS-DMA; 9 / 10 = diagnostics of 7, results wrong:
+                                              DMA every other half step / DMA + barriers only, no
+                                              fragment reads or MFMAs; DW_KS=16,32 picks the
+                                              split-K depths)
 """
 import sys
 
