@@ -389,6 +389,10 @@ static void launch_dw_288w(const bf16_t* A, long lda, const bf16_t* B, long ldb,
     hipLaunchKernelGGL((gemm_dw_h_kernel<BM, BN, 4, 4, 2, 1, 32, false, 2>), dim3(tiles * nsplit), dim3(512), 0, s, A,
                        lda, B, ldb, N, kchunk, tiles, e.outF, e.ldo, e.alpha, use_slab ? e.slab : nullptr,
                        use_slab ? mn : 0L);
+  else if (dg == 3)  // tile 11: DMA pieces between the MFMAs (gemm_core.h DG 3)
+    hipLaunchKernelGGL((gemm_dw_h_kernel<BM, BN, 4, 4, 2, 1, 32, false, 3>), dim3(tiles * nsplit), dim3(512), 0, s, A,
+                       lda, B, ldb, N, kchunk, tiles, e.outF, e.ldo, e.alpha, use_slab ? e.slab : nullptr,
+                       use_slab ? mn : 0L);
   else if (gl)  // tile 8 (A/B): the DMA by global_load_lds; measured slower (1.105 vs 1.050 ms, r6/diag/glds.txt)
     hipLaunchKernelGGL((gemm_dw_h_kernel<BM, BN, 4, 4, 2, 1, 32, true>), dim3(tiles * nsplit), dim3(512), 0, s, A, lda,
                        B, ldb, N, kchunk, tiles, e.outF, e.ldo, e.alpha, use_slab ? e.slab : nullptr,
@@ -408,7 +412,7 @@ static void launch_dw_288w(const bf16_t* A, long lda, const bf16_t* B, long ldb,
 
 void launch_gemm(const bf16_t* A, long lda, int a_mn, const bf16_t* B, long ldb, int b_mn, int M,
                  int N, int K, int ksplit, const GemmEpilogue& e, hipStream_t s, bool glds_ok) {
-  if (a_mn && b_mn && glds_ok && e.atomic && (e.big_tile >= 7 && e.big_tile <= 10) && M % 256 == 0 && K % 64 == 0) {
+  if (a_mn && b_mn && glds_ok && e.atomic && (e.big_tile >= 7 && e.big_tile <= 11) && M % 256 == 0 && K % 64 == 0) {
     if (N % 288 == 0) {
       launch_dw_288w(A, lda, B, ldb, M, N, K, ksplit < 1 ? 1 : ksplit, e, s, e.big_tile == 8,
                      e.big_tile >= 9 ? e.big_tile - 8 : 0);

@@ -563,6 +563,12 @@ struct GldsOpH {
     base = reinterpret_cast<const char*>(p + (size_t)kbeg * ld + row0);
     kstep_bytes = (int)(BKD * ld * 2);
   }
+  // piece i of this wave alone (DG 3: pieces placed between the MFMAs)
+  __device__ __forceinline__ void issue1(int i, int step, char* lds_tile, int wid) const {
+    if (i + 1 < MAXPW || REM == 0 || wid < REM)  // wave-uniform
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (lds_void*)(lds_tile + (i * NW + wid) * 1024), 16, (int)src[i],
+                                               step * kstep_bytes, 0, 0);
+  }
   __device__ __forceinline__ void issue(int step, char* lds_tile, int wid) const {
     const int so = step * kstep_bytes;
 #pragma unroll
@@ -591,7 +597,10 @@ struct GldsOpH {
 // BKD = 64 with NSLOT = 2: the plain 2-stage ring of gemm_mainloop_glds2, for tiles whose
 // pieces do not split evenly over the waves (the 288-wide image: 36 pieces per 64-deep step)
 // DG (diagnostics, tools/dw_tiles.py tiles 9 / 10; results wrong): 1 = the ring's DMA for every
-// other half step only, 2 = no fragment reads and no MFMAs (the DMA + barrier floor)
+// other half step only, 2 = no fragment reads and no MFMAs (the DMA + barrier floor).
+// DG 3 (tile 11, results exact): the half step's DMA pieces issued AFTER its fragment reads, one
+// between every few MFMAs — a piece costs its wave ~60 issue cycles among bare MFMAs but 100-185
+// in a phase of fragment reads (MI355X_MICROARCH.md, LDS-DMA piece issue cost)
 template <class C, int NSLOT, int PRIO = 0, int BKD = 32, bool GL = false, int DG = 0>
 __device__ __forceinline__ void gemm_mainloop_glds_h(const bf16_t* __restrict__ A, long lda,
                                                      const bf16_t* __restrict__ B, long ldb, int kbeg,
@@ -652,7 +661,7 @@ __device__ __forceinline__ void gemm_mainloop_glds_h(const bf16_t* __restrict__ 
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
     const int tn = tt + NSLOT - 1;
-    if (tn < nh && (DG != 1 || (tn & 1) == 0)) {
+    if (DG != 3 && tn < nh && (DG != 1 || (tn & 1) == 0)) {
       constexpr int sn = (u + NSLOT - 1) % NSLOT;
       oa.issue(tn, smem + sn * STAGE, wid);
       ob.issue(tn, smem + sn * STAGE + OA::BYTES, wid);
@@ -664,6 +673,34 @@ __device__ __forceinline__ void gemm_mainloop_glds_h(const bf16_t* __restrict__ 
     int so = u * STAGE;
     asm volatile("" : "+v"(so));
     const char* sl = smem + so;
+    if constexpr (DG == 3) {
+      static_assert(BKD == 32, "DG 3: one fragment set per half step");
+      constexpr int NP = OA::MAXPW + OB::MAXPW;             // this wave's pieces (the last maybe none)
+      constexpr int NM = C::TM * C::TN, GAP = NM / (NP + 1);  // MFMAs between pieces
+      constexpr int sn = (u + NSLOT - 1) % NSLOT;
+      const bool more = tn < nh;
+      bf16x8 a[C::TM], b[C::TN];
+#pragma unroll
+      for (int i = 0; i < C::TM; ++i) a[i] = fa.template frag<0, 0>(sl, i);
+#pragma unroll
+      for (int j = 0; j < C::TN; ++j) b[j] = fbr.template frag<0, OA::BYTES>(sl, j);
+      if constexpr (PRIO == 1) __builtin_amdgcn_s_setprio(1);
+      static_for<0, NM>([&](auto mc) {
+        constexpr int m = decltype(mc)::value, i = m / C::TN, j = m % C::TN;
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
+        if constexpr ((m + 1) % GAP == 0 && (m + 1) / GAP <= NP) {
+          constexpr int p = (m + 1) / GAP - 1;
+          __builtin_amdgcn_sched_barrier(0);
+          if (more) {
+            if constexpr (p < OA::MAXPW) oa.issue1(p, tn, smem + sn * STAGE, wid);
+            else ob.issue1(p - OA::MAXPW, tn, smem + sn * STAGE + OA::BYTES, wid);
+          }
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      });
+      if constexpr (PRIO == 1) __builtin_amdgcn_s_setprio(0);
+      return;
+    }
     static_for<0, BKD / 32>([&](auto kc) {
       constexpr int KK = decltype(kc)::value;
       bf16x8 a[C::TM], b[C::TN];

@@ -7,7 +7,8 @@ rounds, and max |diff| against the default tile (3 = 256x192 64-deep 2-stage).
                                               8 = 256x288 with global_load_lds instead of MUBUF
                                               LDS-DMA; 9 / 10 = diagnostics of 7, results wrong:
                                               DMA every other half step / DMA + barriers only, no
-                                              fragment reads or MFMAs; DW_KS=16,32 picks the
+                                              fragment reads or MFMAs; 11 = 7 with the DMA pieces
+                                              between the MFMAs; DW_KS=16,32 picks the
                                               split-K depths)
 """
 import sys
