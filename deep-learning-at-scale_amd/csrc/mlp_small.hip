@@ -366,10 +366,6 @@ __global__ __launch_bounds__(256, 1) void mlp_small_kernel(const MlpSmallArgs a)
     stage_x();
     __syncthreads();
     stamp(1);
-    if (k + 1 < K) {
-      prefetch();        // step k + 1 (ids fetched a step ago)
-      fetch_ids(k + 2);  // consumed by the next prefetch
-    }
     stamp(14);
     {
       f32x4 bv[4];
@@ -378,7 +374,8 @@ __global__ __launch_bounds__(256, 1) void mlp_small_kernel(const MlpSmallArgs a)
         bv[q] = f32x4{__uint_as_float(bvu[q][0]), __uint_as_float(bvu[q][1]), __uint_as_float(bvu[q][2]),
                       __uint_as_float(bvu[q][3])};
       // two row tiles per iteration, 8 independent accumulators and the next pair's X fragments
-      // read ahead (one accumulator set per tile serialised MFMA -> convert -> store: 2.9 us)
+      // read ahead (one accumulator set per tile serialised MFMA -> convert -> store: 2.9 us;
+      // four tiles per iteration measured slower, 2.64 vs 2.40 us: the 128-KiB H1 store bounds it)
       auto xfrag = [&](int rt) {
         const int r = 16 * rt + l15;
         return *reinterpret_cast<const bf16x8*>(Xs + r * 64 + ((g ^ ((r >> 2) & 3)) << 4));
@@ -440,6 +437,12 @@ __global__ __launch_bounds__(256, 1) void mlp_small_kernel(const MlpSmallArgs a)
     stamp(3);
     stamp(4);
 
+    // the next batch's gathers: issued here, where the head-partial poll waits anyway (issued
+    // before H1 they cost that critical-path phase ~0.5 us); xv / yv were staged in phase A
+    if (k + 1 < K) {
+      prefetch();        // step k + 1 (ids fetched a step ago)
+      fetch_ids(k + 2);  // consumed by the next prefetch
+    }
     // ---- C: prediction, dy, loss (every worker, every row; fixed summation order)
     {
       float lossv = 0.f, dyv = 0.f;
