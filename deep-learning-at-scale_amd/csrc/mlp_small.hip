@@ -327,6 +327,9 @@ __global__ __launch_bounds__(256, 1) void mlp_small_kernel(const MlpSmallArgs a)
     // the W1 / b1 images (published before barrier 3) requested before the X staging
     bf16x8 w1f[4];
     sb_u32x4 bvu[4];
+    // this step's batch (gathered during the previous step) into LDS first: the stores overlap
+    // the W1 wait (every wave's reads of Xs / ys ended before the previous step's last barrier)
+    stage_x();
     {
       const unsigned tg = tagv(k);
       // light poll first: lanes 0-15 watch the LAST W1 granule of producer `lane` (written after
@@ -363,7 +366,6 @@ __global__ __launch_bounds__(256, 1) void mlp_small_kernel(const MlpSmallArgs a)
         more = poll_again(ok);
       }
     }
-    stage_x();
     __syncthreads();
     stamp(1);
     stamp(14);
