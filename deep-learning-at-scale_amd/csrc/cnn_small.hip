@@ -64,7 +64,7 @@ __global__ __launch_bounds__(CS_NT, 1) void cnn_small_kernel(const CnnSmallArgs 
   // [.][filter][step]: steps fastest, so lanes over consecutive steps hit consecutive banks in
   // every loop below ([.][step][filter] put the dWc loop into 16-way bank conflicts)
   __shared__ __attribute__((aligned(16))) float act[CS_MAXB][CS_FPW][CS_T];  // relu(P) kept (unscaled), then dP
-  __shared__ float dout[CS_MAXB][CS_OP];
+  __shared__ __attribute__((aligned(16))) float dout[CS_MAXB][CS_OP];
   __shared__ __attribute__((aligned(16))) float wc[CS_FPW][CS_KC];
   __shared__ float vc[CS_FPW][CS_KC];
   __shared__ __attribute__((aligned(16))) float wd[CS_OP][CS_FPW][CS_T];
@@ -357,10 +357,14 @@ __global__ __launch_bounds__(CS_NT, 1) void cnn_small_kernel(const CnnSmallArgs 
     for (int i = tid; i < B * CS_FPW * (CS_T / 4); i += CS_NT) {
       const int w = i / (CS_FPW * (CS_T / 4)), fl = (i / (CS_T / 4)) % CS_FPW, t4 = 4 * (i % (CS_T / 4));
       float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+      float dr[CS_OP];  // the window's dOut row in 4 float4 reads (was 12 scalar reads)
+#pragma unroll
+      for (int c = 0; c < CS_OP / 4; ++c)
+        *reinterpret_cast<float4*>(&dr[4 * c]) = *reinterpret_cast<const float4*>(&dout[w][4 * c]);
 #pragma unroll
       for (int j = 0; j < CS_OP; ++j)
         if (j < O) {
-          const float d = dout[w][j];
+          const float d = dr[j];
           const float4 wv = *reinterpret_cast<const float4*>(&wd[j][fl][t4]);
           s.x = fmaf(d, wv.x, s.x);
           s.y = fmaf(d, wv.y, s.y);
@@ -435,11 +439,16 @@ __global__ __launch_bounds__(CS_NT, 1) void cnn_small_kernel(const CnnSmallArgs 
         sgd(wc[fl][kk], vc[fl][kk], gs);
       }
     }
-    if (tid >= 64 && tid < 64 + O) {  // dbd = sum over windows, in order
+    if (tid >= 64 && tid < 64 + O) {  // dbd = sum over windows: 4 partial sums (w mod 4), fixed order
+      // (one chain of B dependent LDS loads was ~0.6 us of this phase)
       const int j = tid - 64;
-      float s = 0.f;
-      for (int w = 0; w < B; ++w) s += dout[w][j];
-      sgd(bd[j], vb[j], s);
+      float s4[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll 4
+      for (int w = 0; w < B; w += 4) {  // B % 4 == 0 (launcher)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) s4[e] += dout[w + e][j];
+      }
+      sgd(bd[j], vb[j], (s4[0] + s4[1]) + (s4[2] + s4[3]));
     }
     __syncthreads();
     stamp(8);
