@@ -402,9 +402,10 @@ def bench_mlp(args, ctx, online: bool):
             cstream, events, staged, launches = torch.cuda.Stream(ctx.device), [None, None], [0, 0], [0]
 
             def stage(j, rows):  # launch j's rows (the next launch's: prefetched behind this one)
+                compute = torch.cuda.current_stream(ctx.device)  # (the copy stream inside the `with`)
                 with torch.cuda.stream(cstream):
                     # buffer j % 2 was last read by launch j - 2, enqueued before this copy
-                    cstream.wait_stream(torch.cuda.current_stream(ctx.device))
+                    cstream.wait_stream(compute)
                     bufs[j % 2][0][:rows].copy_(xh[:rows], non_blocking=True)
                     bufs[j % 2][1][:rows].copy_(yh[:rows], non_blocking=True)
                     events[j % 2] = torch.cuda.Event()

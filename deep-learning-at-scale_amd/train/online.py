@@ -122,9 +122,10 @@ class _ChunkStage:
 
     def copy(self, i: int, off: int, rows: int) -> None:
         xb, yb = self.bufs[i % 2]
+        compute = torch.cuda.current_stream(self.dev)  # (inside the `with` below it is the copy stream)
         with torch.cuda.stream(self.stream):
             # buffer i % 2 was last read by chunk i - 2, enqueued on the compute stream before this
-            self.stream.wait_stream(torch.cuda.current_stream(self.dev))
+            self.stream.wait_stream(compute)
             xb[:rows].copy_(self.Xs[off : off + rows], non_blocking=True)
             yb[:rows].copy_(self.Ys[off : off + rows], non_blocking=True)
             ev = torch.cuda.Event()
