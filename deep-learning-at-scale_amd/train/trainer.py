@@ -121,8 +121,10 @@ SMALL_STEPS_PER_LAUNCH = 256
 
 def _resident_windows(X, device) -> bool:
     rows = getattr(X, "rows", None)
-    return (torch.is_tensor(rows) and torch.is_tensor(getattr(X, "starts", None)) and rows.device == device
-            and rows.dtype == torch.float32 and rows.is_contiguous() and rows.dim() == 2)
+    if not (torch.is_tensor(rows) and torch.is_tensor(getattr(X, "starts", None))):
+        return False
+    same = rows.device.type == device.type and (device.index is None or rows.device.index in (None, device.index))
+    return same and rows.is_cuda and rows.dtype == torch.float32 and rows.is_contiguous() and rows.dim() == 2
 
 
 def _input_format(eng, Xd):
