@@ -21,12 +21,12 @@
 //      may still be in E)
 // Small hand-offs are 8-B {value, tag} granules written by ONE sc1 store and polled by the
 // consumer itself (MI355X_MICROARCH.md R2: no flag, no barrier; the tag names the launch and
-// step). The 128-KiB dZ2 exchange keeps one counter barrier per step (sc1 16-B stores, every
-// storing wave's vmcnt(0), a workgroup barrier, ONE agent-scope add per workgroup; sc1 polls
-// and sc1 loads of every handed-off byte). Buffer reuse needs no more: a worker reaches step
-// k + 1's writes only after every worker's step-k granules of W1 arrived, i.e. after every
-// worker finished its step-k reads. The counter counts up through the launch (barrier k
-// completes at 16 (k + 1)) and the last worker out re-zeroes it, so a launch needs no memset.
+// step). The 128-KiB dZ2 exchange is plain data behind one flag per worker (sc1 16-B stores,
+// every storing wave's vmcnt(0), a workgroup barrier, ONE sc1 flag granule carrying the step's
+// tag; the consumer polls the 16 flags, then sc1 loads of every handed-off byte). Buffer reuse
+// needs no more: a worker reaches step k + 1's writes only after every worker's step-k granules
+// of W1 arrived, i.e. after every worker finished its step-k reads. Tags only grow (launch
+// ordinal x 4096 + step + 1), so no launch needs a memset.
 // A spin bound turns a lost hand-off into a sticky error word (results garbage, the host
 // raises) instead of a hang. Every reduction has a fixed order (no float atomics), so K fused
 // steps equal K single-step launches bit for bit.
@@ -45,7 +45,7 @@ constexpr int SB_G = 16;  // worker workgroups
 
 // scratch (floats): granules {value, tag} of [part 16 x 256][b1 256][b3 (+ pad)][W1 256 x 16 words
 // (bf16 pairs)], then the barrier-guarded blocks [dZ2 bf16 16 x 256 x 16][W2^T bf16 2 x 16 x 256 x 16]
-constexpr int SBO_PART = 0, SBO_B1 = 8192, SBO_B3 = 8704, SBO_W1 = 8768, SBO_DZ2 = 16960, SBO_W2T = 49728;
+constexpr int SBO_PART = 0, SBO_B1 = 8192, SBO_B3 = 8704, SBO_FLAG = 8736, SBO_W1 = 8768, SBO_DZ2 = 16960, SBO_W2T = 49728;
 static_assert(SBO_W2T + 65536 == kMlpSmallScratch, "scratch layout");
 
 // LDS (bytes): X [256][64 B] | H1 [256][512 B] (tile_off) | dZ2 / dZ1 own [256][16] bf16 |
@@ -130,35 +130,7 @@ __global__ __launch_bounds__(256, 1) void mlp_small_kernel(const MlpSmallArgs a)
   sb_g32* const cnt = (sb_g32*)a.sync;
   unsigned nbar = 0;
   if (tid == 0) sflag[0] = 0u;
-  auto arrive = [&]() {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave's sc1 stores landed
-    __syncthreads();
-    if (tid == 0) __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    ++nbar;
-  };
-  auto wait = [&]() {
-    if (wid == 0) {
-      const unsigned target = nbar * SB_G;
-      unsigned failed = sflag[0];
-      unsigned spins = 0;
-      while (failed == 0u) {
-        const unsigned v = __hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if ((int)(v - target) >= 0) break;
-        if (__hip_atomic_load((sb_g32*)(a.sync + 2), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) {
-          failed = 1u;
-          break;
-        }
-        if (++spins > a.spin_limit) {
-          __hip_atomic_store((sb_g32*)(a.sync + 2), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          failed = 1u;
-          break;
-        }
-        __builtin_amdgcn_s_sleep(1);
-      }
-      if (lane == 0) sflag[0] = failed;
-    }
-    __syncthreads();
-  };
+  (void)nbar;
 
   // granule poll bookkeeping: true = keep polling (not all tags seen, no failure, bound not hit)
   unsigned gspins = 0;
@@ -182,6 +154,26 @@ __global__ __launch_bounds__(256, 1) void mlp_small_kernel(const MlpSmallArgs a)
   // never 0 (the zeroed scratch) and never a stale step of this or an earlier launch
   const unsigned lc = __hip_atomic_load((sb_g32*)(a.sync + 3), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   auto tagv = [&](int j) { return (lc << 12) + (unsigned)j + 1u; };
+  // dZ2 hand-off: every storing wave's vmcnt(0), a workgroup barrier, then ONE sc1 flag granule
+  // per worker {tag, tag}; the consumer's wave 0 polls the 16 flags (a flag only advances: a
+  // later step's tag also counts), then sc1 loads of the blocks. (A counter barrier — one
+  // agent-scope atomic add per worker, polled — cost the same hand-off an RMW round trip.)
+  auto arrive = [&](unsigned tg) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave's sc1 stores landed
+    __syncthreads();
+    if (tid == 0) st8(tg, tg, SBO_FLAG + 2 * wk);
+  };
+  auto wait = [&](unsigned tg) {
+    if (wid == 0) {
+      bool more = true;
+      while (more) {
+        bool ok = true;
+        if (lane < SB_G) ok = (int)(ld8(SBO_FLAG + 2 * lane)[0] - tg) >= 0;
+        more = poll_again(ok);
+      }
+    }
+    __syncthreads();
+  };
   int kcur = 0;
   auto stamp = [&](int ph) {  // diagnostics: phase boundaries of the first 64 steps (tools/small_timeline.py)
     if (a.stamps != nullptr && tid == 0 && kcur < 64)
@@ -522,7 +514,7 @@ __global__ __launch_bounds__(256, 1) void mlp_small_kernel(const MlpSmallArgs a)
     for (int piece = tid; piece < 2 * B; piece += 256)
       st16(*reinterpret_cast<const sb_u32x4*>(ZS + piece * 16), SBO_DZ2 + wk * 2048 + piece * 4);
     stamp(6);
-    arrive();  // barrier 2: dZ2 blocks
+    arrive(tagv(k));  // hand-off 2: dZ2 blocks
 
     // dW2[O, :] = dZ2[:, O]^T H1 (own; overlaps the other workers' arrivals): wave w in-tiles
     // 4w .. 4w + 3, K = rows; db2 by the ones operand (wave 0)
@@ -584,7 +576,7 @@ __global__ __launch_bounds__(256, 1) void mlp_small_kernel(const MlpSmallArgs a)
       a2[ks] = __builtin_bit_cast(bf16x8, ld16(SBO_W2T + ((par * SB_G + owner) * 256 + 16 * wk + l15) * 8 + 4 * (g & 1)));
     }
     stamp(7);
-    wait();  // barrier 2 (also: every wave is done reading ZS / H1s for dW2)
+    wait(tagv(k));  // hand-off 2 (and the workgroup barrier: every wave is done reading ZS / H1s for dW2)
     stamp(8);
 
     // ---- E: dH1[:, U] = dZ2 W2[:, U] from L2 fragments (two row tiles in flight); dZ1 =
