@@ -63,7 +63,8 @@ __global__ __launch_bounds__(CS_NT, 1) void cnn_small_kernel(const CnnSmallArgs 
   __shared__ float ysm[CS_MAXB][CS_OP];
   // [.][filter][step]: steps fastest, so lanes over consecutive steps hit consecutive banks in
   // every loop below ([.][step][filter] put the dWc loop into 16-way bank conflicts)
-  __shared__ __attribute__((aligned(16))) float act[CS_MAXB][CS_FPW][CS_T];  // relu(P) kept (unscaled), then dP
+  __shared__ __attribute__((aligned(16))) float act[CS_MAXB][CS_FPW][CS_T];  // relu(P) kept (unscaled)
+  __shared__ __attribute__((aligned(16))) float dp[CS_MAXB][CS_FPW][CS_T];   // dAct -> dP (masked)
   __shared__ __attribute__((aligned(16))) float dout[CS_MAXB][CS_OP];
   __shared__ __attribute__((aligned(16))) float wc[CS_FPW][CS_KC];
   __shared__ float vc[CS_FPW][CS_KC];
@@ -331,7 +332,7 @@ __global__ __launch_bounds__(CS_NT, 1) void cnn_small_kernel(const CnnSmallArgs 
       __syncthreads();
     }
     stamp(4);
-    // ---- dWd (own columns) = ks * dOut^T act, then dAct = ks * dOut Wd masked -> dP (in act)
+    // ---- dWd (own columns) = ks * dOut^T act, and dAct = ks * dOut Wd masked -> dP
     // task (j, fl, 4 steps), tid < CS_OP * CS_FPW * CS_T / 4 = 576: the SGD below updates the
     // same 4 parameters in the same thread
     constexpr int NWD = CS_OP * CS_FPW * (CS_T / 4);
@@ -352,7 +353,7 @@ __global__ __launch_bounds__(CS_NT, 1) void cnn_small_kernel(const CnnSmallArgs 
       }
       gwd = make_float4(ks * s.x, ks * s.y, ks * s.z, ks * s.w);
     }
-    __syncthreads();  // act read by every dWd before it becomes dP
+    // (no barrier: dAct writes dP to its own buffer, so it runs beside dWd's reads of act)
     stamp(5);
     for (int i = tid; i < B * CS_FPW * (CS_T / 4); i += CS_NT) {
       const int w = i / (CS_FPW * (CS_T / 4)), fl = (i / (CS_T / 4)) % CS_FPW, t4 = 4 * (i % (CS_T / 4));
@@ -371,10 +372,10 @@ __global__ __launch_bounds__(CS_NT, 1) void cnn_small_kernel(const CnnSmallArgs 
           s.z = fmaf(d, wv.z, s.z);
           s.w = fmaf(d, wv.w, s.w);
         }
-      float4* ap = reinterpret_cast<float4*>(&act[w][fl][t4]);
-      const float4 av = *ap;
-      *ap = make_float4(av.x > 0.f ? ks * s.x : 0.f, av.y > 0.f ? ks * s.y : 0.f, av.z > 0.f ? ks * s.z : 0.f,
-                        av.w > 0.f ? ks * s.w : 0.f);
+      const float4 av = *reinterpret_cast<const float4*>(&act[w][fl][t4]);
+      *reinterpret_cast<float4*>(&dp[w][fl][t4]) =
+          make_float4(av.x > 0.f ? ks * s.x : 0.f, av.y > 0.f ? ks * s.y : 0.f, av.z > 0.f ? ks * s.z : 0.f,
+                      av.w > 0.f ? ks * s.w : 0.f);
     }
     __syncthreads();
     stamp(6);
@@ -394,7 +395,7 @@ __global__ __launch_bounds__(CS_NT, 1) void cnn_small_kernel(const CnnSmallArgs 
 #pragma unroll
       for (int q = 0; q < 7; ++q) s[q] = 0.f;
       for (int w = wq; w < B; w += 4) {  // B % 4 == 0 (launcher)
-        const float4 av = *reinterpret_cast<const float4*>(&act[w][fl][t4]);
+        const float4 av = *reinterpret_cast<const float4*>(&dp[w][fl][t4]);
         const float d[4] = {av.x, av.y, av.z, av.w};
         float xw[12];  // x[t4 + 4 kh + j]
 #pragma unroll
