@@ -124,6 +124,8 @@ def _timed(ctx, step, steps, warmup, min_s: float = 0.0, many=None, graph_steps:
         # streamed config varies step to step (round 4: 1.1x left 0.079-0.098 s windows)
         steps = max(steps, int(math.ceil(min_s * 1.5 / max(per, 1e-9))))
     n = graph_steps if many is not None and graph_steps > 1 else 1
+    if min_s > 0 and n > 1:  # a secondary's raised window: whole replays / launches only
+        steps = -(-steps // n) * n
     if n > 1:
         many(n)  # capture (untimed) + one n-step replay of warmup
         total += n
@@ -325,7 +327,7 @@ def bench_cnn(args, ctx):
     if ctx.world_size == 1 and not args.no_small and eng.small_steps_reason(B, opt, x) is None:
         # small batches (the reference's 20 windows, one process): the Trainer's path — n complete
         # steps per persistent launch (NativeCNN.fused_steps, csrc/cnn_small.hip)
-        gsteps = max(1, min(args.steps, 256))
+        gsteps = _small_launch_steps(args)
         ridx = torch.arange(B, device=ctx.device).repeat(gsteps)  # the one resident batch, every step
 
         def many(n):  # noqa: F811
@@ -394,7 +396,7 @@ def bench_mlp(args, ctx, online: bool):
             # chunk of n batches crosses PCIe as ONE async copy into a device buffer (two,
             # alternating: the next chunk's copy overlaps this launch) and its batches train as
             # n complete steps per persistent launch (NativeMLP.fused_steps)
-            nmax = max(1, min(args.steps, 256))
+            nmax = _small_launch_steps(args)
             xh, yh = synth_tabular_batch(nmax * B, F, seed=1000 * ctx.rank)
             xh = eng.to_input_format(xh).pin_memory()
             yh = yh.float().pin_memory()
@@ -447,7 +449,7 @@ def bench_mlp(args, ctx, online: bool):
             # (forward, backward, Adam) per persistent launch (NativeMLP.fused_steps); step i of
             # a launch reads batch i % N of the resident set through row ids
             # as the Trainer: up to 256 steps per launch (the timed window is one launch at <= 256 steps)
-            nmax = max(1, min(args.steps, 256))
+            nmax = _small_launch_steps(args)
             ridx = torch.arange(nmax * B, device=ctx.device) % (B * nb)
 
             def many(n):  # noqa: F811 - replaces the graph replay for this path
@@ -470,7 +472,19 @@ def bench_mlp(args, ctx, online: bool):
     return el, k, B, model, run.take_loss() / (B * n), run, eng, extra
 
 
-SECONDARY = ("mlp", "mlp_online", "cnn")
+SECONDARY = ("mlp", "mlp_online", "cnn", "cnn_b20", "mlp_b256", "mlp_online_b256")
+# the submission API's own defaults as secondaries (config.py MODEL_DEFAULTS: CNN 20 windows,
+# cnn.py:128; MLP / online MLP 256 rows): on one GPU the K-steps-per-launch paths
+SMALL_SECONDARY = {"cnn_b20": ("cnn", 20), "mlp_b256": ("mlp", 256), "mlp_online_b256": ("mlp_online", 256)}
+
+
+def _small_launch_steps(args) -> int:
+    """Steps per persistent launch of the small-batch paths: the Trainer's 256; the headline
+    times exactly --steps (<= 256 of them as one launch, as its graph replays), a secondary
+    (min_timed_s > 0, steps raised to fill its window) runs the Trainer's launches."""
+    if getattr(args, "min_timed_s", 0.0) > 0:
+        return 256
+    return max(1, min(args.steps, 256))
 CPU_BATCH = {"lstm": 256, "mlp": 8192, "mlp_online": 8192, "cnn": 1024}
 
 
@@ -494,8 +508,11 @@ def _secondary(args, ctx, models) -> dict:
     out = {}
     for m in models:
         a = argparse.Namespace(**vars(args))
-        a.model = m
-        a.batch = (CPU_BATCH if ctx.device.type == "cpu" else DEFAULT_BATCH)[m]
+        if m in SMALL_SECONDARY:
+            a.model, a.batch = SMALL_SECONDARY[m]
+        else:
+            a.model = m
+            a.batch = (CPU_BATCH if ctx.device.type == "cpu" else DEFAULT_BATCH)[m]
         a.min_timed_s = args.secondary_min_s  # the headline keeps the driver's --steps exactly
         gc.collect()
         if ctx.device.type == "cuda":
@@ -512,7 +529,7 @@ def _secondary(args, ctx, models) -> dict:
                     # the all-reduce runs serially inside the step (after the backward, before the
                     # optimizer): its share of the timed step is the DP efficiency it costs
                     "comm_share": None if comm is None else round(comm / ms, 4)}
-        out[m] = {"metric": f"rows/sec (whole node), {m} regression training", "value": round(B * W * k / el, 1),
+        out[m] = {"metric": f"rows/sec (whole node), {a.model} regression training", "value": round(B * W * k / el, 1),
                   "unit": "rows/s", "ms_per_step": round(1000.0 * el / max(k, 1), 4), "steps": k,
                   "warmup": a.warmup, "untimed_steps": untimed, "timed_s": round(el, 4), "per_gpu_batch": B,
                   "global_batch": B * W,

@@ -141,3 +141,15 @@ def test_gpu_state_sampler_window_math():
     off = GpuStateSampler.__new__(GpuStateSampler)
     off._h, off._thread = None, None
     assert not off.available and off.stop() is None
+
+
+def test_bench_job_default_secondaries():
+    """The submission API's own batches ride in the bench line too (CNN 20 windows, MLP and
+    online MLP 256 rows): the secondary names map to (model, per-GPU batch)."""
+    rec = _run(1, "lstm", ["--batch", "4", "--seq", "6", "--hidden", "16", "--secondary",
+                           "cnn_b20,mlp_b256,mlp_online_b256"])
+    sec = rec["secondary"]
+    assert set(sec) == {"cnn_b20", "mlp_b256", "mlp_online_b256"}
+    assert sec["cnn_b20"]["per_gpu_batch"] == 20 and "cnn" in sec["cnn_b20"]["metric"]
+    assert sec["mlp_b256"]["per_gpu_batch"] == 256 and sec["mlp_online_b256"]["per_gpu_batch"] == 256
+    assert all(v["value"] > 0 for v in sec.values())
