@@ -14,9 +14,11 @@ Secondary configs (BASELINE.json:8-10), same JSON contract:
   --model mlp         static 3-layer MLP (F -> 256 -> 256 -> 1), resident batch
   --model mlp_online  dynamic MLP: every step trains on a NEW mini-batch streamed host -> HBM
   --model cnn         the reference's own 1-D CNN (cnn.py:110-118), SGD-Nesterov, 65,536 windows
-The default invocation times all three AFTER the headline's timed region and reports them in
-a nested "secondary" object of the same JSON line (each with its own steps, ms/step, rows/s,
-timed seconds); the headline "value" is the LSTM alone.
+The default invocation times all three AFTER the headline's timed region, then the same
+models at the submission API's own batches (cnn_b20, mlp_b256, mlp_online_b256: CNN 20
+windows, MLP / online MLP 256 rows; on one GPU the K-steps-per-launch paths), and reports them
+in a nested "secondary" object of the same JSON line (each with its own steps, ms/step,
+rows/s, timed seconds); the headline "value" is the LSTM alone.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B_per_gpu] [--model ...]
 
