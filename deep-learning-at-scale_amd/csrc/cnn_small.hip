@@ -75,6 +75,7 @@ __global__ __launch_bounds__(CS_NT, 1) void cnn_small_kernel(const CnnSmallArgs 
   __shared__ float lred[CS_NT / 64];
   __shared__ __attribute__((aligned(16))) float red2[48][28];  // hop 1 of the output sums: [own output][share]
   __shared__ unsigned sflag;
+  __shared__ __attribute__((aligned(16))) unsigned hw[CS_MAXB * CS_T];  // the step's dropout hash words
 
   const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)a.scr, 0, 0x7FFFFFFF, 0x00020000);
   auto st8 = [&](unsigned val, unsigned tag, int fo) {
@@ -171,6 +172,15 @@ __global__ __launch_bounds__(CS_NT, 1) void cnn_small_kernel(const CnnSmallArgs 
     kcur = k;
     stamp(0);
     stage();
+    // the dropout hash of every (window, step), staged beside x: the fused kernels' mask word
+    // (cnn_fused.hip cnn_mask_word) depends on the filter only through the bit it selects, and
+    // a worker's 4 filters share the word's other inputs (q = f >> 2 & 3 = wk & 3), so one hash
+    // per (window, step) serves all 4 (the conv computed it 4 times per element before)
+    const unsigned rstep = rng0 + (unsigned)k;
+    const unsigned smix = cs_lowbias32(a.seed ^ cs_lowbias32(rstep + 0x9E3779B9u));
+    if (a.drop) {
+      for (int i = tid; i < B * CS_T; i += CS_NT) hw[i] = cs_lowbias32(((unsigned)i * 4u + (unsigned)(wk & 3)) ^ smix);
+    }
     __syncthreads();
     stamp(1);
     if (k + 1 < K) {
@@ -178,8 +188,6 @@ __global__ __launch_bounds__(CS_NT, 1) void cnn_small_kernel(const CnnSmallArgs 
       fetch_ids(k + 2);
     }
     // ---- conv + ReLU + dropout of the own filters, every window and step
-    const unsigned rstep = rng0 + (unsigned)k;
-    const unsigned smix = cs_lowbias32(a.seed ^ cs_lowbias32(rstep + 0x9E3779B9u));
     // (every loop below has compile-time trip counts and is unrolled: the runtime-bounded forms
     // were LDS-latency chains, one load -> wait -> fma per iteration: conv 9.3 us per step)
     // task (window, filter, 4 steps): x[t4 .. t4 + 15] and the filter row in 8 float4 reads
@@ -198,18 +206,14 @@ __global__ __launch_bounds__(CS_NT, 1) void cnn_small_kernel(const CnnSmallArgs 
 #pragma unroll
         for (int kk = 0; kk < CS_TAPS; ++kk) pv[e] = fmaf(wcr[kk], xw[e + kk], pv[e]);
       }
-      float o[4];
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        bool keep = true;
-        if (a.drop) {  // the fused kernels' keep bit (cnn_fused.hip cnn_mask_word)
-          const int f = f0 + fl, q = (f >> 2) & 3, r = f & 3, b = f >> 4;
-          const unsigned m = cs_lowbias32((((unsigned)w * CS_T + (unsigned)(t4 + e)) * 4u + (unsigned)q) ^ smix);
-          keep = ((m >> (2 * b + (r >> 1) + 16 * (r & 1))) & 1u) != 0u;
-        }
-        o[e] = (keep && pv[e] > 0.f) ? pv[e] : 0.f;
-      }
-      *reinterpret_cast<float4*>(&act[w][fl][t4]) = make_float4(o[0], o[1], o[2], o[3]);
+      uint4 mw = make_uint4(~0u, ~0u, ~0u, ~0u);  // the 4 steps' hash words (all-keep without dropout)
+      if (a.drop) mw = *reinterpret_cast<const uint4*>(&hw[w * CS_T + t4]);
+      const int f = f0 + fl, r = f & 3, bsh = 2 * (f >> 4) + (r >> 1) + 16 * (r & 1);
+      const float o0 = ((mw.x >> bsh) & 1u) != 0u && pv[0] > 0.f ? pv[0] : 0.f;
+      const float o1 = ((mw.y >> bsh) & 1u) != 0u && pv[1] > 0.f ? pv[1] : 0.f;
+      const float o2 = ((mw.z >> bsh) & 1u) != 0u && pv[2] > 0.f ? pv[2] : 0.f;
+      const float o3 = ((mw.w >> bsh) & 1u) != 0u && pv[3] > 0.f ? pv[3] : 0.f;
+      *reinterpret_cast<float4*>(&act[w][fl][t4]) = make_float4(o0, o1, o2, o3);
     }
     __syncthreads();
     stamp(2);
