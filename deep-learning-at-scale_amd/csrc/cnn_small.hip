@@ -491,7 +491,7 @@ __global__ __launch_bounds__(CS_NT, 1) void cnn_small_kernel(const CnnSmallArgs 
 }  // namespace
 
 bool launch_cnn_small(const CnnSmallArgs& a, hipStream_t s) {
-  if (a.B < 4 || a.B > CS_MAXB || a.B % 4 != 0 || a.K <= 0 || a.O < 1 || a.O > CS_OP || a.taps != CS_L - CS_T + 1 ||
+  if (a.B < 4 || a.B > CS_MAXB || a.B % 4 != 0 || a.K <= 0 || a.K > 4095 || a.O < 1 || a.O > CS_OP || a.taps != CS_L - CS_T + 1 ||
       a.filters < 1 || a.filters > CS_FP)
     return false;
   const int G = (a.filters + CS_FPW - 1) / CS_FPW;

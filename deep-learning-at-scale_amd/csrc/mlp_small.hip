@@ -704,7 +704,8 @@ __global__ __launch_bounds__(256, 1) void mlp_small_kernel(const MlpSmallArgs a)
 }  // namespace
 
 bool launch_mlp_small(const MlpSmallArgs& a, hipStream_t s) {
-  if (a.B < 32 || a.B > 256 || a.B % 32 != 0 || a.Fp <= 0 || a.Fp > 32 || a.Fp % 8 != 0 || a.K <= 0) return false;
+  if (a.B < 32 || a.B > 256 || a.B % 32 != 0 || a.Fp <= 0 || a.Fp > 32 || a.Fp % 8 != 0 || a.K <= 0 || a.K > 4095)
+    return false;  // (tags: launch ordinal x 4096 + step + 1)
   if (a.scr == nullptr || a.sync == nullptr || a.p == nullptr || a.m == nullptr || a.v == nullptr || a.step == nullptr)
     return false;
   if (a.Fp <= 16)
