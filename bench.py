@@ -16,7 +16,8 @@ Secondary configs (BASELINE.json:8-10), same JSON contract:
   --model cnn         the reference's own 1-D CNN (cnn.py:110-118), SGD-Nesterov, 65,536 windows
 The default invocation times all three AFTER the headline's timed region, then the same
 models at the submission API's own batches (cnn_b20, mlp_b256, mlp_online_b256: CNN 20
-windows, MLP / online MLP 256 rows; on one GPU the K-steps-per-launch paths), and reports them
+windows, MLP / online MLP 256 rows; one-GPU runs only, by default: the K-steps-per-launch
+paths), and reports them
 in a nested "secondary" object of the same JSON line (each with its own steps, ms/step,
 rows/s, timed seconds); the headline "value" is the LSTM alone.
 
@@ -603,6 +604,10 @@ def main() -> int:
         DEFAULT_BATCH["lstm"] if args.device != "cpu" else CPU_BATCH["lstm"], 64, 512, 16)
     if args.secondary == "auto":
         secondary = list(SECONDARY) if default_headline else []
+        if args.gpus > 1 or int(os.environ.get("WORLD_SIZE", "1")) > 1:
+            # the job-default configs show the one-GPU K-steps-per-launch paths; at DP they would
+            # time per-step launches behind a latency-bound all-reduce (pass them explicitly)
+            secondary = [m for m in secondary if m not in SMALL_SECONDARY]
     else:
         secondary = [m for m in args.secondary.split(",") if m and m != "none"]
         bad = [m for m in secondary if m not in SECONDARY]
