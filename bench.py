@@ -481,6 +481,16 @@ SECONDARY = ("mlp", "mlp_online", "cnn", "cnn_b20", "mlp_b256", "mlp_online_b256
 SMALL_SECONDARY = {"cnn_b20": ("cnn", 20), "mlp_b256": ("mlp", 256), "mlp_online_b256": ("mlp_online", 256)}
 
 
+def _auto_secondary(default_headline: bool, world: int) -> list:
+    """The configs a default invocation times after the headline: all of SECONDARY on one GPU;
+    under DP without the job-default ones (they show the one-GPU K-steps-per-launch paths; at
+    DP they would time per-step launches behind a latency-bound all-reduce — pass them
+    explicitly for that)."""
+    if not default_headline:
+        return []
+    return [m for m in SECONDARY if world <= 1 or m not in SMALL_SECONDARY]
+
+
 def _small_launch_steps(args) -> int:
     """Steps per persistent launch of the small-batch paths: the Trainer's 256; the headline
     times exactly --steps (<= 256 of them as one launch, as its graph replays), a secondary
@@ -603,11 +613,7 @@ def main() -> int:
     default_headline = args.model == "lstm" and (args.batch, args.seq, args.hidden, args.features) == (
         DEFAULT_BATCH["lstm"] if args.device != "cpu" else CPU_BATCH["lstm"], 64, 512, 16)
     if args.secondary == "auto":
-        secondary = list(SECONDARY) if default_headline else []
-        if args.gpus > 1 or int(os.environ.get("WORLD_SIZE", "1")) > 1:
-            # the job-default configs show the one-GPU K-steps-per-launch paths; at DP they would
-            # time per-step launches behind a latency-bound all-reduce (pass them explicitly)
-            secondary = [m for m in secondary if m not in SMALL_SECONDARY]
+        secondary = _auto_secondary(default_headline, max(args.gpus, int(os.environ.get("WORLD_SIZE", "1"))))
     else:
         secondary = [m for m in args.secondary.split(",") if m and m != "none"]
         bad = [m for m in secondary if m not in SECONDARY]

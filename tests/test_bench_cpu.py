@@ -153,3 +153,22 @@ def test_bench_job_default_secondaries():
     assert sec["cnn_b20"]["per_gpu_batch"] == 20 and "cnn" in sec["cnn_b20"]["metric"]
     assert sec["mlp_b256"]["per_gpu_batch"] == 256 and sec["mlp_online_b256"]["per_gpu_batch"] == 256
     assert all(v["value"] > 0 for v in sec.values())
+
+
+def test_small_launch_steps_and_dp_secondaries():
+    """The headline times exactly --steps (<= 256 per launch); a secondary's raised window runs
+    the Trainer's 256-step launches. Under a DP world the job-default secondaries are left out
+    of the automatic set (they show one-GPU paths)."""
+    import argparse
+    import importlib.util
+
+    spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(ROOT, "bench.py"))
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    assert bench._small_launch_steps(argparse.Namespace(min_timed_s=0.0, steps=20)) == 20
+    assert bench._small_launch_steps(argparse.Namespace(min_timed_s=0.0, steps=1000)) == 256
+    assert bench._small_launch_steps(argparse.Namespace(min_timed_s=0.1, steps=20)) == 256
+    assert set(bench.SMALL_SECONDARY) <= set(bench.SECONDARY)
+    assert bench._auto_secondary(True, 1) == list(bench.SECONDARY)
+    assert bench._auto_secondary(True, 8) == ["mlp", "mlp_online", "cnn"]
+    assert bench._auto_secondary(False, 1) == []
